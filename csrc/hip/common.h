@@ -1,0 +1,34 @@
+// Shared helpers for the CDNA4 (gfx950) HIP code of ray_memory_management_amd.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#define RMM_HIP_CHECK(expr)                                                                 \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);     \
+  } while (0)
+
+namespace rmm {
+namespace hip {
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+// XCD-aware remap of a linear workgroup id (bijective for any grid size): consecutive
+// logical ids land on the same XCD so neighbouring tiles share an L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
+  const uint32_t kXcd = 8;
+  if (nwg < kXcd) return orig;
+  uint32_t q = nwg / kXcd, r = nwg % kXcd;
+  uint32_t xcd = orig % kXcd;
+  uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / kXcd;
+}
+
+}  // namespace hip
+}  // namespace rmm

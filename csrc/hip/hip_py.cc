@@ -1,0 +1,275 @@
+// pybind11 bindings for the CDNA4 kernels and the HBM GPU object store.
+// Tensors cross the boundary as raw device pointers + the caller's hipStream_t (from
+// torch.cuda.current_stream().cuda_stream); results come back zero-copy as DLPack capsules.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+
+#include "common.h"
+#include "gpu_store.h"
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace rmm::hip;
+
+namespace {
+
+inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <typename T>
+inline T* P(uint64_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+// ---- minimal DLPack ABI (stable C ABI, v0.x "dltensor" capsule)
+struct DLDevice {
+  int32_t device_type;
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code;
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+
+struct Ctx {
+  std::vector<int64_t> shape, strides;
+  std::shared_ptr<GpuStore> store;
+  std::string id;
+  PyObject* callback = nullptr;
+};
+
+void dl_deleter(DLManagedTensor* t) {
+  Ctx* c = static_cast<Ctx*>(t->manager_ctx);
+  if (c->store) c->store->Release(c->id);
+  if (c->callback) {
+    py::gil_scoped_acquire gil;
+    PyObject* r = PyObject_CallObject(c->callback, nullptr);
+    if (!r) PyErr_Clear();
+    Py_XDECREF(r);
+    Py_DECREF(c->callback);
+  }
+  delete c;
+  delete t;
+}
+
+void capsule_destructor(PyObject* cap) {
+  // only delete if never consumed (consumer renames to "used_dltensor")
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (t && t->deleter) t->deleter(t);
+  }
+}
+
+py::object make_dlpack(uint64_t ptr, std::vector<int64_t> shape, int code, int bits, int device,
+                       std::shared_ptr<GpuStore> store, const std::string& id, py::object callback) {
+  auto* t = new DLManagedTensor();
+  auto* c = new Ctx();
+  c->shape = std::move(shape);
+  c->strides.resize(c->shape.size());
+  int64_t st = 1;
+  for (int i = int(c->shape.size()) - 1; i >= 0; i--) {
+    c->strides[size_t(i)] = st;
+    st *= c->shape[size_t(i)];
+  }
+  c->store = std::move(store);
+  c->id = id;
+  if (!callback.is_none()) {
+    c->callback = callback.ptr();
+    Py_INCREF(c->callback);
+  }
+  t->dl_tensor.data = reinterpret_cast<void*>(ptr);
+  t->dl_tensor.device = {kDLROCM, device};
+  t->dl_tensor.ndim = int32_t(c->shape.size());
+  t->dl_tensor.dtype = {uint8_t(code), uint8_t(bits), 1};
+  t->dl_tensor.shape = c->shape.data();
+  t->dl_tensor.strides = c->strides.data();
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = c;
+  t->deleter = dl_deleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(t, "dltensor", capsule_destructor));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "CDNA4 (gfx950) kernels + HBM GPU object store";
+
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return n;
+  });
+  m.def("device_synchronize", [] {
+    py::gil_scoped_release nogil;
+    RMM_HIP_CHECK(hipDeviceSynchronize());
+  });
+  m.def("stream_synchronize", [](uint64_t s) {
+    py::gil_scoped_release nogil;
+    RMM_HIP_CHECK(hipStreamSynchronize(S(s)));
+  });
+  m.def("arch", [](int dev) {
+    hipDeviceProp_t p;
+    RMM_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    return std::string(p.gcnArchName);
+  });
+
+  // ---------------------------------------------------------------- kernels
+  m.def("multi_copy",
+        [](const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>>& segs, uint64_t stream) {
+          std::vector<CopySeg> cs;
+          cs.reserve(segs.size());
+          for (auto& s : segs) cs.push_back({std::get<0>(s), std::get<1>(s), std::get<2>(s)});
+          multi_copy(cs, S(stream));
+        });
+  m.def("gather_rows", [](uint64_t in, uint64_t idx, uint64_t out, int64_t rows, int64_t row_bytes,
+                          uint64_t stream) {
+    gather_rows(P<const void>(in), P<const int64_t>(idx), P<void>(out), rows, row_bytes, S(stream));
+  });
+  m.def("gae", [](uint64_t rew, uint64_t val, uint64_t done, uint64_t last, uint64_t adv, uint64_t ret,
+                  int64_t T, int64_t B, float gamma, float lam, uint64_t stream) {
+    gae(P<const float>(rew), P<const float>(val), P<const float>(done), P<const float>(last), P<float>(adv),
+        P<float>(ret), T, B, gamma, lam, S(stream));
+  });
+  m.def("compress_bound", &compress_bound);
+  m.def("compress_workspace", &compress_workspace);
+  m.def("compress", [](uint64_t src, uint64_t n, int bits, uint64_t dst, uint64_t ws, uint64_t stream) {
+    py::gil_scoped_release nogil;
+    return compress(P<const void>(src), n, bits, P<void>(dst), P<void>(ws), S(stream));
+  });
+  m.def("decompress", [](uint64_t src, uint64_t dst, uint64_t n, int bits, uint64_t ws, uint64_t stream) {
+    decompress(P<const void>(src), P<void>(dst), n, bits, P<void>(ws), S(stream));
+  });
+  m.def("scan_u16", [](uint64_t in, uint64_t out, uint64_t n, uint64_t ws, uint64_t stream) {
+    scan_u16(P<const uint16_t>(in), P<uint64_t>(out), n, P<void>(ws), S(stream));
+  });
+  m.def("ppo_loss", [](uint64_t logp_new, uint64_t logp_old, uint64_t adv, uint64_t v_new, uint64_t v_tgt,
+                       uint64_t ent, uint64_t g_logp, uint64_t g_v, uint64_t g_ent, uint64_t stats, int64_t n,
+                       float clip, float vf_clip, float vf_coeff, float ent_coeff, uint64_t stream) {
+    ppo_loss_fwd(P<const float>(logp_new), P<const float>(logp_old), P<const float>(adv), P<const float>(v_new),
+                 nullptr, P<const float>(v_tgt), P<const float>(ent), P<float>(g_logp), P<float>(g_v),
+                 P<float>(g_ent), P<float>(stats), n, clip, vf_clip, vf_coeff, ent_coeff, S(stream));
+  });
+
+  // ---------------------------------------------------------------- IPC
+  m.def("ipc_open", [](py::bytes handle, int device) {
+    std::string h = handle;
+    if (h.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle size");
+    hipIpcMemHandle_t mh;
+    memcpy(&mh, h.data(), sizeof(mh));
+    RMM_HIP_CHECK(hipSetDevice(device));
+    void* p = nullptr;
+    RMM_HIP_CHECK(hipIpcOpenMemHandle(&p, mh, hipIpcMemLazyEnablePeerAccess));
+    return reinterpret_cast<uint64_t>(p);
+  });
+  m.def("ipc_close", [](uint64_t p) { RMM_HIP_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void*>(p))); });
+  m.def("memcpy_async", [](uint64_t dst, uint64_t src, uint64_t n, uint64_t stream) {
+    RMM_HIP_CHECK(hipMemcpyAsync(P<void>(dst), P<const void>(src), n, hipMemcpyDefault, S(stream)));
+  });
+  m.def("host_register", [](uint64_t p, uint64_t n) {
+    return hipHostRegister(P<void>(p), n, hipHostRegisterDefault) == hipSuccess;
+  });
+  m.def("host_unregister", [](uint64_t p) { return hipHostUnregister(P<void>(p)) == hipSuccess; });
+
+  // DLPack capsule over device memory. dtype code: 0 int, 1 uint, 2 float, 4 bfloat.
+  m.def("dlpack", [](uint64_t ptr, std::vector<int64_t> shape, int code, int bits, int device, py::object cb) {
+    return make_dlpack(ptr, std::move(shape), code, bits, device, nullptr, std::string(), cb);
+  }, py::arg("ptr"), py::arg("shape"), py::arg("code"), py::arg("bits"), py::arg("device"),
+     py::arg("release") = py::none());
+
+  // ---------------------------------------------------------------- GPU object store
+  py::class_<GpuStore, std::shared_ptr<GpuStore>>(m, "GpuStore")
+      .def(py::init<int, uint64_t, uint64_t, const std::string&, bool>(), py::arg("device"),
+           py::arg("capacity"), py::arg("slab_bytes") = 8ull << 30, py::arg("shm_name") = "",
+           py::arg("compress_spill") = true)
+      .def("create", [](GpuStore& s, py::bytes id, uint64_t n, int bits) {
+        return s.Create(std::string(id), n, bits);
+      })
+      .def("seal", [](GpuStore& s, py::bytes id, uint64_t stream) { s.Seal(std::string(id), S(stream)); })
+      .def("put_segments",
+           [](GpuStore& s, py::bytes id, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int bits,
+              uint64_t stream) {
+             std::string sid = id;
+             py::gil_scoped_release nogil;
+             return s.PutSegments(sid, segs, bits, S(stream));
+           })
+      .def("get", [](GpuStore& s, py::bytes id, uint64_t stream) {
+        std::string sid = id;
+        py::gil_scoped_release nogil;
+        return s.Get(sid, S(stream));
+      })
+      .def("release", [](GpuStore& s, py::bytes id) { s.Release(std::string(id)); })
+      .def("delete", [](GpuStore& s, py::bytes id) {
+        std::string sid = id;
+        py::gil_scoped_release nogil;
+        return s.Delete(sid);
+      })
+      .def("contains", [](GpuStore& s, py::bytes id) { return s.Contains(std::string(id)); })
+      .def("is_spilled", [](GpuStore& s, py::bytes id) { return s.IsSpilled(std::string(id)); })
+      .def("locate", [](GpuStore& s, py::bytes id) {
+        int slab;
+        uint64_t off = 0, n = 0;
+        s.Locate(std::string(id), &slab, &off, &n);
+        return py::make_tuple(slab, off, n);
+      })
+      .def("slab_ipc_handle", [](GpuStore& s, int slab) { return py::bytes(s.SlabIpcHandle(slab)); })
+      .def("slab_base", &GpuStore::SlabBase)
+      .def("spill", [](GpuStore& s, uint64_t bytes) {
+        py::gil_scoped_release nogil;
+        return s.Spill(bytes);
+      })
+      .def("spill_object", [](GpuStore& s, py::bytes id) {
+        std::string sid = id;
+        py::gil_scoped_release nogil;
+        return s.SpillObject(sid);
+      })
+      .def_static("host_id", [](py::bytes id) { return py::bytes(GpuStore::HostId(std::string(id))); })
+      .def_property_readonly("device", &GpuStore::device)
+      .def("stats", [](GpuStore& s) {
+        GpuStats st = s.Stats();
+        py::dict d;
+        d["capacity"] = st.capacity;
+        d["slab_bytes_allocated"] = st.slab_bytes_allocated;
+        d["bytes_in_use"] = st.bytes_in_use;
+        d["num_objects"] = st.num_objects;
+        d["spilled_objects"] = st.spilled_objects;
+        d["spilled_bytes_total"] = st.spilled_bytes_total;
+        d["spilled_host_bytes_total"] = st.spilled_host_bytes_total;
+        d["restored_bytes_total"] = st.restored_bytes_total;
+        d["puts"] = st.puts;
+        d["gets"] = st.gets;
+        return d;
+      });
+
+  // Zero-copy DLPack view of a GPU-store object; the pin is released when the tensor dies.
+  m.def("store_dlpack", [](std::shared_ptr<GpuStore> s, py::bytes id, std::vector<int64_t> shape, int code,
+                           int bits, uint64_t stream) {
+    std::string sid = id;
+    uint64_t ptr;
+    {
+      py::gil_scoped_release nogil;
+      ptr = s->Get(sid, S(stream));
+    }
+    if (!ptr) throw std::runtime_error("GPU object not found");
+    return make_dlpack(ptr, std::move(shape), code, bits, s->device(), s, sid, py::none());
+  });
+}

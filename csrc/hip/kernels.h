@@ -1,0 +1,53 @@
+// Host launchers for the CDNA4 kernels (all asynchronous on the given stream unless noted).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace rmm {
+namespace hip {
+
+struct CopySeg {
+  uint64_t src;
+  uint64_t dst;
+  uint64_t nbytes;
+};
+
+// K1/K2: one launch copies many (src,dst,n) segments — tensor pack/unpack for
+// serialization, sample-batch concat. Any alignment; 16 B/lane vector path when possible.
+void multi_copy(const std::vector<CopySeg>& segs, hipStream_t stream);
+
+// K2: out[i,:] = in[idx[i],:] for `rows` rows of `row_bytes` bytes (minibatch gather).
+void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, int64_t row_bytes,
+                 hipStream_t stream);
+
+// K3: GAE over time-major [T,B] fp32 tensors. dones is fp32 0/1 (1 = episode ended after t).
+// adv[t] = delta[t] + gamma*lam*(1-d[t])*adv[t+1];  ret = adv + values.
+void gae(const float* rewards, const float* values, const float* dones, const float* last_values,
+         float* adv, float* ret, int64_t T, int64_t B, float gamma, float lam, hipStream_t stream);
+
+// K4: lossless block compression for the spill path.
+// elem_bits = 16 (bf16/fp16) or 32 (fp32). Returns the upper bound of the compressed stream.
+uint64_t compress_bound(uint64_t n_elems, int elem_bits);
+// Workspace bytes needed by compress/decompress.
+uint64_t compress_workspace(uint64_t n_elems);
+// Compress `n_elems` elements at `src` into `dst` (device, >= compress_bound bytes).
+// Synchronises the stream once to read back the total; returns compressed byte count.
+uint64_t compress(const void* src, uint64_t n_elems, int elem_bits, void* dst, void* workspace,
+                  hipStream_t stream);
+// Inverse of compress(); `src` is the device copy of the compressed stream.
+void decompress(const void* src, void* dst, uint64_t n_elems, int elem_bits, void* workspace,
+                hipStream_t stream);
+
+// Exclusive scan of u16 -> u64 with total written to out[n] (device); helper exposed for tests.
+void scan_u16(const uint16_t* in, uint64_t* out, uint64_t n, void* workspace, hipStream_t stream);
+
+// K5: fused PPO surrogate loss pieces (ratio/clip/value/entropy reductions) — see kernels.hip.
+void ppo_loss_fwd(const float* logp_new, const float* logp_old, const float* adv,
+                  const float* v_new, const float* v_old, const float* v_tgt, const float* ent,
+                  float* grad_logp, float* grad_v, float* grad_ent, float* stats, int64_t n,
+                  float clip, float vf_clip, float vf_coeff, float ent_coeff, hipStream_t stream);
+
+}  // namespace hip
+}  // namespace rmm

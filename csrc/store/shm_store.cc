@@ -1,0 +1,967 @@
+// Shared-memory object store implementation. See shm_store.h for the design notes.
+#include "shm_store.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+namespace rmm {
+
+namespace {
+
+constexpr uint64_t kMagic = 0x524d4d53544f5245ull;  // "RMMSTORE"
+constexpr uint64_t kVersion = 3;
+constexpr uint64_t kFreeBit = 1;
+constexpr uint64_t kSizeMask = ~uint64_t(kAlign - 1);
+
+struct Blk {
+  uint64_t size;       // total block bytes (multiple of 64) | kFreeBit
+  uint64_t prev_phys;  // absolute offset of previous physical block, 0 if first
+  uint64_t next_free;
+  uint64_t prev_free;
+};
+
+inline uint64_t AlignUp(uint64_t v, uint64_t a) { return (v + a - 1) & ~(a - 1); }
+
+inline int64_t NowNs() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return int64_t(ts.tv_sec) * 1000000000ll + ts.tv_nsec;
+}
+
+inline uint64_t HashId(const ObjectId& id) {
+  uint64_t a, b;
+  uint32_t c;
+  memcpy(&a, id.b, 8);
+  memcpy(&b, id.b + 8, 8);
+  memcpy(&c, id.b + 16, 4);
+  uint64_t h = a * 0x9E3779B97F4A7C15ull;
+  h ^= (b + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2));
+  h ^= (uint64_t(c) * 0xC2B2AE3D27D4EB4Full);
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 32;
+  return h;
+}
+
+inline void MappingInsert(uint64_t size, int* fl, int* sl) {
+  int f = 63 - __builtin_clzll(size);
+  *sl = int((size >> (f - kSLBits)) ^ (uint64_t(1) << kSLBits));
+  *fl = f;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- lifecycle
+
+static void InitSync(Header* h) {
+  pthread_mutexattr_t ma;
+  pthread_mutexattr_init(&ma);
+  pthread_mutexattr_setpshared(&ma, PTHREAD_PROCESS_SHARED);
+  pthread_mutexattr_setrobust(&ma, PTHREAD_MUTEX_ROBUST);
+  pthread_mutex_init(&h->mu, &ma);
+  pthread_mutexattr_destroy(&ma);
+  pthread_condattr_t ca;
+  pthread_condattr_init(&ca);
+  pthread_condattr_setpshared(&ca, PTHREAD_PROCESS_SHARED);
+  pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
+  pthread_cond_init(&h->cv, &ca);
+  pthread_condattr_destroy(&ca);
+}
+
+Store* Store::Create(const std::string& name, uint64_t size, const std::string& spill_dir,
+                     double spill_threshold, uint64_t min_spill_size, bool fallback) {
+  if (size < (8ull << 20)) size = 8ull << 20;
+  uint64_t table_cap = 1 << 14;
+  while (table_cap < (size >> 14) && table_cap < (1ull << 21)) table_cap <<= 1;
+  uint64_t off = AlignUp(sizeof(Header), 4096);
+  uint64_t table_off = off;
+  off = AlignUp(off + table_cap * sizeof(Entry), 4096);
+  uint64_t ring_off = off;
+  off = AlignUp(off + kRingCap * sizeof(ObjectId), 4096);
+  uint64_t spill_off = off;
+  off = AlignUp(off + kSpillSlots * sizeof(SpillFileSlot), 4096);
+  uint64_t heap_off = off;
+  uint64_t heap_size = AlignUp(size, 4096);
+  uint64_t total = heap_off + heap_size;
+
+  int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+  if (fd < 0) throw std::runtime_error("shm_open(create) failed for " + name + ": " + strerror(errno));
+  if (ftruncate(fd, off_t(total)) != 0) {
+    close(fd);
+    shm_unlink(name.c_str());
+    throw std::runtime_error("ftruncate failed: " + std::string(strerror(errno)));
+  }
+  void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    shm_unlink(name.c_str());
+    throw std::runtime_error("mmap failed: " + std::string(strerror(errno)));
+  }
+  Store* s = new Store();
+  s->name_ = name;
+  s->base_ = static_cast<uint8_t*>(p);
+  s->size_ = total;
+  s->owner_ = true;
+  Header* h = reinterpret_cast<Header*>(p);
+  memset(h, 0, sizeof(Header));
+  h->total_size = total;
+  h->table_off = table_off;
+  h->table_cap = table_cap;
+  h->ring_off = ring_off;
+  h->spill_off = spill_off;
+  h->heap_off = heap_off;
+  h->heap_size = heap_size;
+  h->lru_head = h->lru_tail = -1;
+  h->next_file_id = 1;
+  h->spill_threshold = spill_threshold;
+  h->min_spill_size = min_spill_size;
+  h->spill_enabled = spill_dir.empty() ? 0 : 1;
+  h->fallback_enabled = (fallback && !spill_dir.empty()) ? 1 : 0;
+  strncpy(h->spill_dir, spill_dir.c_str(), sizeof(h->spill_dir) - 1);
+  InitSync(h);
+  s->hdr_ = h;
+  s->table_ = reinterpret_cast<Entry*>(s->base_ + table_off);
+  s->ring_ = reinterpret_cast<ObjectId*>(s->base_ + ring_off);
+  s->spill_ = reinterpret_cast<SpillFileSlot*>(s->base_ + spill_off);
+  // table pages are zero from ftruncate (kEmpty == 0).
+  // Heap: one big free block followed by a used sentinel header.
+  uint64_t first = heap_off;
+  uint64_t sentinel = heap_off + heap_size - kBlockHdr;
+  Blk* b = reinterpret_cast<Blk*>(s->base_ + first);
+  b->size = (sentinel - first) | kFreeBit;
+  b->prev_phys = 0;
+  Blk* sb = reinterpret_cast<Blk*>(s->base_ + sentinel);
+  sb->size = kBlockHdr;  // used
+  sb->prev_phys = first;
+  s->TlsfInsert(first);
+  __atomic_store_n(&h->version, kVersion, __ATOMIC_RELEASE);
+  __atomic_store_n(&h->magic, kMagic, __ATOMIC_RELEASE);
+  return s;
+}
+
+Store* Store::Attach(const std::string& name) {
+  int fd = shm_open(name.c_str(), O_RDWR, 0600);
+  if (fd < 0) throw std::runtime_error("shm_open(attach) failed for " + name + ": " + strerror(errno));
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    throw std::runtime_error("fstat failed");
+  }
+  void* p = mmap(nullptr, size_t(st.st_size), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error("mmap(attach) failed: " + std::string(strerror(errno)));
+  Header* h = reinterpret_cast<Header*>(p);
+  if (__atomic_load_n(&h->magic, __ATOMIC_ACQUIRE) != kMagic || h->version != kVersion) {
+    munmap(p, size_t(st.st_size));
+    throw std::runtime_error("object store segment " + name + " is not initialised / wrong version");
+  }
+  Store* s = new Store();
+  s->name_ = name;
+  s->base_ = static_cast<uint8_t*>(p);
+  s->size_ = uint64_t(st.st_size);
+  s->hdr_ = h;
+  s->table_ = reinterpret_cast<Entry*>(s->base_ + h->table_off);
+  s->ring_ = reinterpret_cast<ObjectId*>(s->base_ + h->ring_off);
+  s->spill_ = reinterpret_cast<SpillFileSlot*>(s->base_ + h->spill_off);
+  return s;
+}
+
+Store::~Store() {
+  for (auto& m : fb_maps_) munmap(m.ptr, m.size);
+  if (base_) munmap(base_, size_);
+  if (owner_) shm_unlink(name_.c_str());
+}
+
+void Store::Lock() {
+  int rc = pthread_mutex_lock(&hdr_->mu);
+  if (rc == EOWNERDEAD) {
+    // A process died holding the lock. Our state changes are short and mostly
+    // single-word updates, so mark it consistent and carry on.
+    pthread_mutex_consistent(&hdr_->mu);
+  } else if (rc != 0) {
+    throw std::runtime_error("store mutex lock failed");
+  }
+}
+void Store::Unlock() { pthread_mutex_unlock(&hdr_->mu); }
+
+void Store::CondWait(int64_t deadline_ns) {
+  if (deadline_ns < 0) {
+    // Bounded waits even for "forever" so a lost wakeup can never hang a reader.
+    deadline_ns = NowNs() + 200000000ll;
+  }
+  timespec ts;
+  ts.tv_sec = deadline_ns / 1000000000ll;
+  ts.tv_nsec = deadline_ns % 1000000000ll;
+  int rc = pthread_cond_timedwait(&hdr_->cv, &hdr_->mu, &ts);
+  if (rc == EOWNERDEAD) pthread_mutex_consistent(&hdr_->mu);
+}
+
+void Store::Wake() {
+  Lock();
+  Broadcast();
+  Unlock();
+}
+
+// ---------------------------------------------------------------- TLSF allocator
+
+void Store::TlsfInsert(uint64_t blk) {
+  Blk* b = reinterpret_cast<Blk*>(base_ + blk);
+  int fl, sl;
+  MappingInsert(b->size & kSizeMask, &fl, &sl);
+  uint64_t head = hdr_->free_heads[fl][sl];
+  b->next_free = head;
+  b->prev_free = kNil;
+  if (head != kNil) reinterpret_cast<Blk*>(base_ + head)->prev_free = blk;
+  hdr_->free_heads[fl][sl] = blk;
+  hdr_->fl_bitmap |= (1ull << fl);
+  hdr_->sl_bitmap[fl] |= (1u << sl);
+}
+
+void Store::TlsfRemove(uint64_t blk) {
+  Blk* b = reinterpret_cast<Blk*>(base_ + blk);
+  int fl, sl;
+  MappingInsert(b->size & kSizeMask, &fl, &sl);
+  if (b->prev_free != kNil) reinterpret_cast<Blk*>(base_ + b->prev_free)->next_free = b->next_free;
+  if (b->next_free != kNil) reinterpret_cast<Blk*>(base_ + b->next_free)->prev_free = b->prev_free;
+  if (hdr_->free_heads[fl][sl] == blk) {
+    hdr_->free_heads[fl][sl] = b->next_free;
+    if (b->next_free == kNil) {
+      hdr_->sl_bitmap[fl] &= ~(1u << sl);
+      if (hdr_->sl_bitmap[fl] == 0) hdr_->fl_bitmap &= ~(1ull << fl);
+    }
+  }
+  b->next_free = b->prev_free = kNil;
+}
+
+uint64_t Store::TlsfFind(uint64_t size) {
+  // Round up to the next class boundary so any block in the found list fits.
+  int f0 = 63 - __builtin_clzll(size);
+  uint64_t rounded = size + (uint64_t(1) << (f0 - kSLBits)) - 1;
+  int fl, sl;
+  MappingInsert(rounded, &fl, &sl);
+  if (fl >= kFL) return kNil;
+  uint32_t sl_map = hdr_->sl_bitmap[fl] & (~0u << sl);
+  if (sl_map == 0) {
+    uint64_t fl_map = (fl + 1 >= 64) ? 0 : (hdr_->fl_bitmap & (~0ull << (fl + 1)));
+    if (fl_map == 0) return kNil;
+    fl = __builtin_ctzll(fl_map);
+    sl_map = hdr_->sl_bitmap[fl];
+  }
+  sl = __builtin_ctz(sl_map);
+  uint64_t blk = hdr_->free_heads[fl][sl];
+  if (blk != kNil) TlsfRemove(blk);
+  return blk;
+}
+
+uint64_t Store::HeapAlloc(uint64_t n) {
+  uint64_t need = AlignUp(n, kAlign) + kBlockHdr;
+  if (need < kMinBlock) need = kMinBlock;
+  uint64_t blk = TlsfFind(need);
+  if (blk == kNil) return kNil;
+  Blk* b = reinterpret_cast<Blk*>(base_ + blk);
+  uint64_t bsize = b->size & kSizeMask;
+  uint64_t rem = bsize - need;
+  if (rem >= kMinBlock) {
+    uint64_t nb = blk + need;
+    Blk* n2 = reinterpret_cast<Blk*>(base_ + nb);
+    n2->size = rem | kFreeBit;
+    n2->prev_phys = blk;
+    Blk* after = reinterpret_cast<Blk*>(base_ + nb + rem);
+    after->prev_phys = nb;
+    TlsfInsert(nb);
+    bsize = need;
+  }
+  b->size = bsize;  // used
+  hdr_->stats.bytes_in_use += bsize;
+  return blk + kBlockHdr;
+}
+
+void Store::HeapFree(uint64_t payload_off) {
+  uint64_t blk = payload_off - kBlockHdr;
+  Blk* b = reinterpret_cast<Blk*>(base_ + blk);
+  uint64_t bsize = b->size & kSizeMask;
+  hdr_->stats.bytes_in_use -= bsize;
+  // merge with previous
+  if (b->prev_phys != 0) {
+    Blk* p = reinterpret_cast<Blk*>(base_ + b->prev_phys);
+    if (p->size & kFreeBit) {
+      TlsfRemove(b->prev_phys);
+      uint64_t psize = p->size & kSizeMask;
+      blk = b->prev_phys;
+      bsize += psize;
+      b = p;
+    }
+  }
+  // merge with next
+  uint64_t nxt = blk + bsize;
+  Blk* nb = reinterpret_cast<Blk*>(base_ + nxt);
+  if (nb->size & kFreeBit) {
+    TlsfRemove(nxt);
+    bsize += nb->size & kSizeMask;
+  }
+  b->size = bsize | kFreeBit;
+  Blk* after = reinterpret_cast<Blk*>(base_ + blk + bsize);
+  after->prev_phys = blk;
+  TlsfInsert(blk);
+}
+
+uint64_t Store::CheckHeap() {
+  Lock();
+  uint64_t off = hdr_->heap_off, end = hdr_->heap_off + hdr_->heap_size - kBlockHdr;
+  uint64_t prev = 0, free_bytes = 0, used_bytes = 0, nfree = 0;
+  bool ok = true;
+  bool prev_free = false;
+  while (off < end) {
+    Blk* b = reinterpret_cast<Blk*>(base_ + off);
+    uint64_t sz = b->size & kSizeMask;
+    if (sz == 0 || b->prev_phys != prev) { ok = false; break; }
+    bool fr = b->size & kFreeBit;
+    if (fr && prev_free) { ok = false; break; }  // adjacent free blocks must be merged
+    if (fr) { free_bytes += sz; nfree++; } else { used_bytes += sz; }
+    prev_free = fr;
+    prev = off;
+    off += sz;
+  }
+  if (off != end) ok = false;
+  uint64_t listed = 0;
+  for (int f = 0; f < kFL && ok; f++)
+    for (int s = 0; s < kSL; s++)
+      for (uint64_t b = hdr_->free_heads[f][s]; b != kNil;
+           b = reinterpret_cast<Blk*>(base_ + b)->next_free)
+        listed++;
+  if (listed != nfree) ok = false;
+  if (used_bytes != hdr_->stats.bytes_in_use) ok = false;
+  Unlock();
+  if (!ok) throw std::runtime_error("heap check failed");
+  return free_bytes;
+}
+
+// ---------------------------------------------------------------- object table
+
+int64_t Store::Find(const ObjectId& id) {
+  uint64_t mask = hdr_->table_cap - 1;
+  uint64_t i = HashId(id) & mask;
+  for (uint64_t n = 0; n <= mask; n++, i = (i + 1) & mask) {
+    Entry* e = &table_[i];
+    if (e->state == kEmpty) return -1;
+    if (e->state != kTombstone && memcmp(e->id, id.b, kIdSize) == 0) return int64_t(i);
+  }
+  return -1;
+}
+
+int64_t Store::Insert(const ObjectId& id) {
+  uint64_t cap = hdr_->table_cap;
+  if (hdr_->table_used + 1 > cap - cap / 8) {
+    // Too many tombstones: rebuild in place, keeping LRU order.
+    uint64_t live = hdr_->stats.num_objects;
+    if (live + 1 > cap - cap / 4) throw std::runtime_error("object table full");
+    std::vector<Entry> keep;
+    keep.reserve(live);
+    std::vector<int64_t> lru_order;
+    for (int32_t i = hdr_->lru_head; i >= 0; i = table_[i].lru_next) lru_order.push_back(i);
+    std::vector<ObjectId> lru_ids;
+    for (auto i : lru_order) { ObjectId o; memcpy(o.b, table_[i].id, kIdSize); lru_ids.push_back(o); }
+    for (uint64_t i = 0; i < cap; i++)
+      if (table_[i].state != kEmpty && table_[i].state != kTombstone) keep.push_back(table_[i]);
+    memset(table_, 0, cap * sizeof(Entry));
+    hdr_->table_used = 0;
+    hdr_->lru_head = hdr_->lru_tail = -1;
+    for (auto& e : keep) {
+      ObjectId o;
+      memcpy(o.b, e.id, kIdSize);
+      uint64_t mask = cap - 1, j = HashId(o) & mask;
+      while (table_[j].state != kEmpty) j = (j + 1) & mask;
+      table_[j] = e;
+      table_[j].in_lru = 0;
+      table_[j].lru_prev = table_[j].lru_next = -1;
+      hdr_->table_used++;
+    }
+    for (auto& o : lru_ids) LruPush(Find(o));
+  }
+  uint64_t mask = cap - 1;
+  uint64_t i = HashId(id) & mask;
+  int64_t tomb = -1;
+  for (uint64_t n = 0; n <= mask; n++, i = (i + 1) & mask) {
+    Entry* e = &table_[i];
+    if (e->state == kEmpty) break;
+    if (e->state == kTombstone) {
+      if (tomb < 0) tomb = int64_t(i);
+      continue;
+    }
+    if (memcmp(e->id, id.b, kIdSize) == 0) return -2 - int64_t(i);  // exists
+  }
+  int64_t slot = tomb >= 0 ? tomb : int64_t(i);
+  if (tomb < 0) hdr_->table_used++;
+  Entry* e = &table_[slot];
+  memset(e, 0, sizeof(Entry));
+  memcpy(e->id, id.b, kIdSize);
+  e->lru_prev = e->lru_next = -1;
+  hdr_->stats.num_objects++;
+  return slot;
+}
+
+void Store::RemoveEntry(int64_t idx) {
+  Entry* e = E(idx);
+  if (e->in_lru) LruRemove(idx);
+  e->state = kTombstone;
+  hdr_->stats.num_objects--;
+}
+
+void Store::LruPush(int64_t idx) {
+  Entry* e = E(idx);
+  if (e->in_lru) return;
+  e->in_lru = 1;
+  e->lru_next = -1;
+  e->lru_prev = hdr_->lru_tail;
+  if (hdr_->lru_tail >= 0) table_[hdr_->lru_tail].lru_next = int32_t(idx);
+  hdr_->lru_tail = int32_t(idx);
+  if (hdr_->lru_head < 0) hdr_->lru_head = int32_t(idx);
+}
+
+void Store::LruRemove(int64_t idx) {
+  Entry* e = E(idx);
+  if (!e->in_lru) return;
+  if (e->lru_prev >= 0) table_[e->lru_prev].lru_next = e->lru_next;
+  else hdr_->lru_head = e->lru_next;
+  if (e->lru_next >= 0) table_[e->lru_next].lru_prev = e->lru_prev;
+  else hdr_->lru_tail = e->lru_prev;
+  e->lru_prev = e->lru_next = -1;
+  e->in_lru = 0;
+}
+
+// ---------------------------------------------------------------- spill files
+
+std::string Store::SpillPath(uint64_t fid) const {
+  return std::string(hdr_->spill_dir) + "/rmm-spill-" + std::to_string(fid) + ".bin";
+}
+std::string Store::FallbackPath(uint64_t fid) const {
+  return std::string(hdr_->spill_dir) + "/rmm-fallback-" + std::to_string(fid) + ".bin";
+}
+
+int64_t Store::SpillSlot(uint64_t fid, bool create) {
+  uint64_t i = fid & (kSpillSlots - 1);
+  for (uint64_t n = 0; n < kSpillSlots; n++, i = (i + 1) & (kSpillSlots - 1)) {
+    if (spill_[i].file_id == fid) return int64_t(i);
+    if (create && spill_[i].file_id == 0) {
+      spill_[i].file_id = fid;
+      spill_[i].live = 0;
+      return int64_t(i);
+    }
+  }
+  return -1;
+}
+
+void Store::DropSpillRef(uint64_t fid) {
+  int64_t s = SpillSlot(fid, false);
+  if (s < 0) return;
+  if (--spill_[s].live <= 0) {
+    spill_[s].file_id = 0;
+    unlink(SpillPath(fid).c_str());
+  }
+}
+
+uint8_t* Store::FallbackMap(uint64_t fid, uint64_t size, bool create) {
+  pthread_mutex_lock(&fb_mu_);
+  for (auto& m : fb_maps_)
+    if (m.fid == fid) { pthread_mutex_unlock(&fb_mu_); return m.ptr; }
+  std::string path = FallbackPath(fid);
+  int fd = open(path.c_str(), create ? (O_CREAT | O_RDWR) : O_RDWR, 0600);
+  uint8_t* ptr = nullptr;
+  uint64_t msz = size ? size : 1;
+  if (fd >= 0) {
+    if (!create || ftruncate(fd, off_t(msz)) == 0) {
+      void* p = mmap(nullptr, msz, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      if (p != MAP_FAILED) ptr = static_cast<uint8_t*>(p);
+    }
+    close(fd);
+  }
+  if (ptr) fb_maps_.push_back({fid, ptr, msz});
+  pthread_mutex_unlock(&fb_mu_);
+  return ptr;
+}
+
+void Store::FallbackUnlink(uint64_t fid) {
+  pthread_mutex_lock(&fb_mu_);
+  for (size_t i = 0; i < fb_maps_.size(); i++) {
+    if (fb_maps_[i].fid == fid) {
+      munmap(fb_maps_[i].ptr, fb_maps_[i].size);
+      fb_maps_.erase(fb_maps_.begin() + long(i));
+      break;
+    }
+  }
+  pthread_mutex_unlock(&fb_mu_);
+  unlink(FallbackPath(fid).c_str());
+}
+
+void Store::FreeEntryStorage(int64_t idx) {
+  Entry* e = E(idx);
+  if (e->flags & kFlagFallback) {
+    hdr_->stats.fallback_bytes_current -= e->data_size + e->meta_size;
+    FallbackUnlink(e->fallback_id);
+    e->flags &= ~kFlagFallback;
+  } else if (e->state == kSealed || e->state == kCreating || e->state == kSpilling) {
+    HeapFree(e->offset);
+  }
+  if (e->flags & kFlagHasSpillCopy) {
+    DropSpillRef(e->spill_file);
+    if (e->state == kSpilled) {
+      hdr_->stats.spilled_bytes_current -= e->data_size + e->meta_size;
+      hdr_->stats.spilled_objects_current--;
+    }
+    e->flags &= ~kFlagHasSpillCopy;
+  }
+}
+
+// Spill LRU victims with the lock held on entry and exit (released around file IO).
+uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
+  if (!hdr_->spill_enabled) return 0;
+  uint64_t freed = 0;
+  // 1) free objects that already have an up-to-date spill copy (no IO needed)
+  std::vector<ObjectId> batch;
+  uint64_t batch_bytes = 0;
+  uint64_t target = std::max<uint64_t>(bytes, hdr_->min_spill_size);
+  for (int32_t i = hdr_->lru_head; i >= 0 && (freed < bytes || batch_bytes < target);) {
+    Entry* e = &table_[i];
+    int32_t nxt = e->lru_next;
+    if (e->state == kSealed && e->pin_count == 0 && !(e->flags & kFlagFallback)) {
+      if (e->flags & kFlagHasSpillCopy) {
+        LruRemove(i);
+        HeapFree(e->offset);
+        e->state = kSpilled;
+        hdr_->stats.spilled_bytes_current += e->data_size + e->meta_size;
+        hdr_->stats.spilled_objects_current++;
+        freed += AlignUp(e->data_size + e->meta_size, kAlign) + kBlockHdr;
+      } else if (freed + batch_bytes < bytes || batch_bytes < target) {
+        ObjectId o;
+        memcpy(o.b, e->id, kIdSize);
+        batch.push_back(o);
+        batch_bytes += AlignUp(e->data_size + e->meta_size, kAlign) + kBlockHdr;
+        LruRemove(i);
+        e->state = kSpilling;
+        e->pin_count++;
+      }
+    }
+    i = nxt;
+  }
+  if (batch.empty()) return freed;
+  uint64_t fid = hdr_->next_file_id++;
+  struct Item { ObjectId id; uint64_t off, len; uint8_t* src; };
+  std::vector<Item> items;
+  uint64_t foff = 0;
+  for (auto& o : batch) {
+    Entry* e = E(Find(o));
+    uint64_t len = e->data_size + e->meta_size;
+    items.push_back({o, foff, len, base_ + e->offset});
+    foff += AlignUp(len, 4096);
+  }
+  Unlock();
+  bool ok = true;
+  std::string path = SpillPath(fid);
+  int fd = open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0600);
+  if (fd < 0) ok = false;
+  for (auto& it : items) {
+    if (!ok) break;
+    uint64_t done = 0;
+    while (done < it.len) {
+      ssize_t w = pwrite(fd, it.src + done, it.len - done, off_t(it.off + done));
+      if (w <= 0) { ok = false; break; }
+      done += uint64_t(w);
+    }
+  }
+  if (fd >= 0) close(fd);
+  Lock();
+  if (!ok) unlink(path.c_str());
+  int64_t slot = ok ? SpillSlot(fid, true) : -1;
+  for (auto& it : items) {
+    int64_t idx = Find(it.id);
+    if (idx < 0) continue;
+    Entry* e = E(idx);
+    e->pin_count--;
+    if (!ok || slot < 0) {
+      e->state = kSealed;
+      if (e->pin_count == 0) LruPush(idx);
+      continue;
+    }
+    e->flags |= kFlagHasSpillCopy;
+    e->spill_file = fid;
+    e->spill_off = it.off;
+    spill_[slot].live++;
+    hdr_->stats.bytes_spilled_total += it.len;
+    hdr_->stats.objects_spilled_total++;
+    if (e->flags & kFlagDeletePending) {
+      if (e->pin_count == 0) {
+        e->state = kSealed;
+        FreeEntryStorage(idx);
+        RemoveEntry(idx);
+        freed += AlignUp(it.len, kAlign) + kBlockHdr;
+      } else {
+        e->state = kSealed;
+      }
+      continue;
+    }
+    if (e->pin_count == 0) {
+      HeapFree(e->offset);
+      e->state = kSpilled;
+      hdr_->stats.spilled_bytes_current += it.len;
+      hdr_->stats.spilled_objects_current++;
+      freed += AlignUp(it.len, kAlign) + kBlockHdr;
+    } else {
+      e->state = kSealed;  // someone pinned it meanwhile; keep in memory + spill copy
+    }
+  }
+  if (slot >= 0 && spill_[slot].live == 0) {
+    spill_[slot].file_id = 0;
+    unlink(path.c_str());
+  }
+  Broadcast();
+  return freed;
+}
+
+uint64_t Store::SpillBytes(uint64_t bytes) {
+  Lock();
+  uint64_t f = SpillLocked(bytes, nullptr);
+  Unlock();
+  return f;
+}
+
+bool Store::RestoreLocked(int64_t idx) {
+  Entry* e = E(idx);
+  ObjectId id;
+  memcpy(id.b, e->id, kIdSize);
+  uint64_t len = e->data_size + e->meta_size;
+  e->state = kRestoring;
+  e->pin_count++;
+  uint64_t off = HeapAlloc(len);
+  while (off == kNil) {
+    uint64_t f = SpillLocked(len, nullptr);
+    off = HeapAlloc(len);
+    if (off == kNil && f == 0) break;
+  }
+  idx = Find(id);
+  e = E(idx);
+  if (off == kNil) {
+    e->state = kSpilled;
+    e->pin_count--;
+    Broadcast();
+    return false;
+  }
+  uint64_t fid = e->spill_file, foff = e->spill_off;
+  uint8_t* dst = base_ + off;
+  Unlock();
+  bool ok = true;
+  int fd = open(SpillPath(fid).c_str(), O_RDONLY);
+  if (fd < 0) ok = false;
+  uint64_t done = 0;
+  while (ok && done < len) {
+    ssize_t r = pread(fd, dst + done, len - done, off_t(foff + done));
+    if (r <= 0) { ok = false; break; }
+    done += uint64_t(r);
+  }
+  if (fd >= 0) close(fd);
+  Lock();
+  idx = Find(id);
+  e = E(idx);
+  e->pin_count--;
+  if (!ok) {
+    HeapFree(off);
+    e->state = kSpilled;
+    Broadcast();
+    return false;
+  }
+  e->offset = off;
+  e->state = kSealed;
+  hdr_->stats.spilled_bytes_current -= len;
+  hdr_->stats.spilled_objects_current--;
+  hdr_->stats.bytes_restored_total += len;
+  hdr_->stats.objects_restored_total++;
+  Broadcast();
+  return true;
+}
+
+// ---------------------------------------------------------------- public API
+
+uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t meta_size,
+                             uint32_t user_tag, uint32_t flags, bool* exists) {
+  *exists = false;
+  uint64_t len = data_size + meta_size;
+  Lock();
+  int64_t idx = Insert(id);
+  if (idx <= -2) {
+    *exists = true;
+    Unlock();
+    return nullptr;
+  }
+  Entry* e = E(idx);
+  e->state = kCreating;
+  e->flags = flags & kFlagError;
+  e->user_tag = user_tag;
+  e->data_size = data_size;
+  e->meta_size = meta_size;
+  e->pin_count = 1;
+  e->creator_pid = getpid();
+  e->create_ns = uint64_t(NowNs());
+  hdr_->stats.creates_total++;
+  // proactive threshold spilling is driven by the node (SpillBytes); here only on demand.
+  uint64_t off = HeapAlloc(len);
+  while (off == kNil && hdr_->spill_enabled) {
+    uint64_t f = SpillLocked(len, nullptr);
+    off = HeapAlloc(len);
+    if (f == 0) break;
+  }
+  idx = Find(id);
+  e = E(idx);
+  uint8_t* ptr = nullptr;
+  if (off != kNil) {
+    e->offset = off;
+    ptr = base_ + off;
+  } else if (hdr_->fallback_enabled) {
+    uint64_t fid = hdr_->next_file_id++;
+    Unlock();
+    ptr = FallbackMap(fid, len, true);
+    Lock();
+    idx = Find(id);
+    e = E(idx);
+    if (ptr) {
+      e->flags |= kFlagFallback;
+      e->fallback_id = fid;
+      hdr_->stats.fallback_bytes_current += len;
+      hdr_->stats.fallback_allocs_total++;
+    }
+  }
+  if (!ptr) {
+    RemoveEntry(idx);
+    Unlock();
+    throw std::runtime_error("ObjectStoreFullError: cannot allocate " + std::to_string(len) +
+                             " bytes (capacity " + std::to_string(hdr_->heap_size) + ")");
+  }
+  Unlock();
+  return ptr;
+}
+
+void Store::Seal(const ObjectId& id) {
+  Lock();
+  int64_t idx = Find(id);
+  if (idx < 0 || E(idx)->state != kCreating) {
+    Unlock();
+    throw std::runtime_error("Seal: object not in creating state");
+  }
+  Entry* e = E(idx);
+  e->state = kSealed;
+  hdr_->stats.num_sealed++;
+  hdr_->seal_seq++;
+  memcpy(ring_[hdr_->ring_head & (kRingCap - 1)].b, e->id, kIdSize);
+  hdr_->ring_head++;
+  Broadcast();
+  Unlock();
+}
+
+void Store::Abort(const ObjectId& id) {
+  Lock();
+  int64_t idx = Find(id);
+  if (idx >= 0 && E(idx)->state == kCreating) {
+    FreeEntryStorage(idx);
+    RemoveEntry(idx);
+  }
+  Unlock();
+}
+
+int Store::AbortCreator(int pid) {
+  int n = 0;
+  Lock();
+  for (uint64_t i = 0; i < hdr_->table_cap; i++) {
+    Entry* e = &table_[i];
+    if (e->state == kCreating && e->creator_pid == pid) {
+      FreeEntryStorage(int64_t(i));
+      RemoveEntry(int64_t(i));
+      n++;
+    }
+  }
+  Unlock();
+  return n;
+}
+
+bool Store::Get(const ObjectId& id, int64_t timeout_ms, View* out) {
+  int64_t deadline = timeout_ms < 0 ? -1 : NowNs() + timeout_ms * 1000000ll;
+  Lock();
+  for (;;) {
+    int64_t idx = Find(id);
+    if (idx >= 0) {
+      Entry* e = E(idx);
+      if (e->state == kSealed || e->state == kSpilling) {
+        if (e->pin_count == 0 && e->in_lru) LruRemove(idx);
+        e->pin_count++;
+        hdr_->stats.gets_total++;
+        out->data_size = e->data_size;
+        out->meta_size = e->meta_size;
+        out->user_tag = e->user_tag;
+        out->flags = e->flags;
+        if (e->flags & kFlagFallback) {
+          uint64_t fid = e->fallback_id, len = e->data_size + e->meta_size;
+          Unlock();
+          out->data = FallbackMap(fid, len, false);
+          if (!out->data) {
+            Release(id);
+            throw std::runtime_error("failed to map fallback object");
+          }
+          return true;
+        }
+        out->data = base_ + e->offset;
+        Unlock();
+        return true;
+      }
+      if (e->state == kSpilled) {
+        if (!RestoreLocked(idx)) {
+          Unlock();
+          throw std::runtime_error("ObjectStoreFullError: cannot restore spilled object");
+        }
+        continue;
+      }
+    }
+    if (deadline >= 0 && NowNs() >= deadline) {
+      Unlock();
+      return false;
+    }
+    CondWait(deadline);
+  }
+}
+
+int Store::Wait(const std::vector<ObjectId>& ids, int num_required, int64_t timeout_ms,
+                std::vector<uint8_t>* ready) {
+  int64_t deadline = timeout_ms < 0 ? -1 : NowNs() + timeout_ms * 1000000ll;
+  ready->assign(ids.size(), 0);
+  Lock();
+  for (;;) {
+    int n = 0;
+    for (size_t i = 0; i < ids.size(); i++) {
+      if (!(*ready)[i]) {
+        int64_t idx = Find(ids[i]);
+        if (idx >= 0) {
+          uint32_t st = E(idx)->state;
+          if (st == kSealed || st == kSpilling || st == kSpilled || st == kRestoring) (*ready)[i] = 1;
+        }
+      }
+      n += (*ready)[i];
+    }
+    if (n >= num_required || (deadline >= 0 && NowNs() >= deadline)) {
+      Unlock();
+      return n;
+    }
+    CondWait(deadline);
+  }
+}
+
+void Store::Release(const ObjectId& id) {
+  Lock();
+  int64_t idx = Find(id);
+  if (idx < 0) { Unlock(); return; }
+  Entry* e = E(idx);
+  if (e->pin_count > 0) e->pin_count--;
+  if (e->pin_count == 0) {
+    if (e->flags & kFlagDeletePending) {
+      FreeEntryStorage(idx);
+      RemoveEntry(idx);
+    } else if (e->state == kSealed && !(e->flags & kFlagFallback)) {
+      LruPush(idx);
+    }
+  }
+  Unlock();
+}
+
+bool Store::Delete(const ObjectId& id) {
+  Lock();
+  int64_t idx = Find(id);
+  if (idx < 0) { Unlock(); return false; }
+  Entry* e = E(idx);
+  hdr_->stats.deletes_total++;
+  if (e->state == kSealed || e->state == kSpilled) {
+    if (e->pin_count > 0) {
+      e->flags |= kFlagDeletePending;
+    } else {
+      if (e->state == kSealed) hdr_->stats.num_sealed--;
+      FreeEntryStorage(idx);
+      RemoveEntry(idx);
+    }
+  } else {
+    e->flags |= kFlagDeletePending;  // creating / spilling / restoring: finish first
+  }
+  Unlock();
+  return true;
+}
+
+bool Store::Contains(const ObjectId& id) {
+  Lock();
+  int64_t idx = Find(id);
+  bool r = false;
+  if (idx >= 0) {
+    uint32_t st = E(idx)->state;
+    r = st == kSealed || st == kSpilling || st == kSpilled || st == kRestoring;
+  }
+  Unlock();
+  return r;
+}
+
+int Store::State(const ObjectId& id) {
+  Lock();
+  int64_t idx = Find(id);
+  int r = idx >= 0 ? int(E(idx)->state) : -1;
+  Unlock();
+  return r;
+}
+
+uint64_t Store::PollSealed(uint64_t cursor, std::vector<ObjectId>* out, bool* overflow) {
+  Lock();
+  uint64_t head = hdr_->ring_head;
+  *overflow = head - cursor > kRingCap;
+  if (*overflow) cursor = head - kRingCap;
+  out->reserve(head - cursor);
+  for (uint64_t c = cursor; c < head; c++) out->push_back(ring_[c & (kRingCap - 1)]);
+  Unlock();
+  return head;
+}
+
+uint64_t Store::SealSeq() { return __atomic_load_n(&hdr_->seal_seq, __ATOMIC_ACQUIRE); }
+
+uint64_t Store::WaitSealSeq(uint64_t seq, int64_t timeout_ms) {
+  int64_t deadline = timeout_ms < 0 ? -1 : NowNs() + timeout_ms * 1000000ll;
+  Lock();
+  while (hdr_->seal_seq == seq) {
+    if (deadline >= 0 && NowNs() >= deadline) break;
+    CondWait(deadline);
+  }
+  uint64_t s = hdr_->seal_seq;
+  Unlock();
+  return s;
+}
+
+Stats Store::GetStats() {
+  Lock();
+  Stats s = hdr_->stats;
+  Unlock();
+  return s;
+}
+
+std::vector<std::pair<ObjectId, Entry>> Store::ListObjects() {
+  std::vector<std::pair<ObjectId, Entry>> r;
+  Lock();
+  for (uint64_t i = 0; i < hdr_->table_cap; i++) {
+    Entry& e = table_[i];
+    if (e.state != kEmpty && e.state != kTombstone) {
+      ObjectId o;
+      memcpy(o.b, e.id, kIdSize);
+      r.push_back({o, e});
+    }
+  }
+  Unlock();
+  return r;
+}
+
+}  // namespace rmm

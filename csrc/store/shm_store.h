@@ -1,0 +1,223 @@
+// Shared-memory object store ("plasma" equivalent), MI355X-node edition.
+//
+// Parity: reference src/ray/object_manager/plasma/{store.cc,object_lifecycle_manager.cc,
+// eviction_policy.cc,plasma_allocator.cc,create_request_queue.cc} and
+// src/ray/raylet/local_object_manager.cc (spill / restore).
+//
+// Design (not a port): the reference runs plasma as a server inside the raylet and every
+// client talks to it over a Unix socket (fd passing + flatbuffers). Here the WHOLE store —
+// allocator state, object table, LRU list, spill bookkeeping, a process-shared robust mutex
+// and condition variable — lives inside one /dev/shm segment that every process on the node
+// maps. create/seal/get/release are therefore plain function calls (no IPC round trip);
+// a seal broadcasts the in-segment condvar, which is what `get` waiters and the scheduler's
+// dependency watcher block on. The data heap is managed by a TLSF (two-level segregated
+// fit) allocator addressed by offsets, so it is valid in every mapping. The segment can be
+// hipHostRegister'ed by GPU processes so spills of HBM objects DMA straight into it.
+#pragma once
+#include <pthread.h>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace rmm {
+
+constexpr int kIdSize = 20;
+constexpr uint64_t kAlign = 64;
+constexpr uint64_t kBlockHdr = 64;
+constexpr uint64_t kMinBlock = 128;
+constexpr int kFL = 48;      // first-level classes (2^48 = 256 TB max block)
+constexpr int kSLBits = 4;   // 16 second-level classes
+constexpr int kSL = 1 << kSLBits;
+constexpr uint64_t kNil = 0;
+
+enum ObjState : uint32_t {
+  kEmpty = 0,
+  kCreating = 1,
+  kSealed = 2,
+  kSpilling = 3,   // sealed, being written to external storage (still readable)
+  kSpilled = 4,    // only in external storage
+  kRestoring = 5,  // being read back from external storage
+  kTombstone = 6,
+};
+
+enum ObjFlags : uint32_t {
+  kFlagFallback = 1u << 0,      // data lives in a per-object mmap file, not the heap
+  kFlagDeletePending = 1u << 1, // delete requested while pinned
+  kFlagHasSpillCopy = 1u << 2,  // an up-to-date copy exists in external storage
+  kFlagError = 1u << 3,         // payload is a serialized error
+};
+
+struct ObjectId {
+  uint8_t b[kIdSize];
+};
+
+struct Entry {
+  uint8_t id[kIdSize];
+  uint32_t state;
+  uint32_t flags;
+  int32_t pin_count;
+  int32_t creator_pid;
+  int32_t lru_prev;  // intrusive LRU list of evictable (sealed, unpinned) entries
+  int32_t lru_next;
+  uint32_t in_lru;
+  uint32_t user_tag;    // opaque to the store (e.g. serialization format / GPU meta)
+  uint64_t offset;      // heap offset of payload (data followed by metadata)
+  uint64_t data_size;
+  uint64_t meta_size;
+  uint64_t spill_file;  // spill file id (when kFlagHasSpillCopy / kSpilled)
+  uint64_t spill_off;
+  uint64_t fallback_id; // file id for kFlagFallback objects
+  uint64_t create_ns;
+};
+
+struct SpillFileSlot {
+  uint64_t file_id;  // 0 = free
+  int64_t live;      // objects still referencing this fused file
+};
+
+constexpr uint64_t kSpillSlots = 1 << 14;
+constexpr uint64_t kRingCap = 1 << 16;
+
+struct Stats {
+  uint64_t bytes_in_use;
+  uint64_t num_objects;
+  uint64_t num_sealed;
+  uint64_t bytes_spilled_total;
+  uint64_t objects_spilled_total;
+  uint64_t bytes_restored_total;
+  uint64_t objects_restored_total;
+  uint64_t spilled_bytes_current;
+  uint64_t spilled_objects_current;
+  uint64_t fallback_bytes_current;
+  uint64_t fallback_allocs_total;
+  uint64_t creates_total;
+  uint64_t gets_total;
+  uint64_t deletes_total;
+};
+
+struct Header {
+  uint64_t magic;
+  uint64_t version;
+  uint64_t total_size;
+  uint64_t table_off;
+  uint64_t table_cap;  // power of two
+  uint64_t ring_off;
+  uint64_t spill_off;
+  uint64_t heap_off;   // absolute offset of heap start inside the segment
+  uint64_t heap_size;
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  uint64_t seal_seq;
+  uint64_t ring_head;
+  uint64_t next_file_id;
+  uint64_t table_used;  // live + tombstones
+  int32_t lru_head;
+  int32_t lru_tail;
+  // TLSF control (offsets relative to segment base)
+  uint64_t fl_bitmap;
+  uint32_t sl_bitmap[kFL];
+  uint64_t free_heads[kFL][kSL];
+  // config
+  double spill_threshold;       // proactively spill when usage > threshold * heap
+  uint64_t min_spill_size;      // fuse at least this many bytes per spill file
+  int32_t spill_enabled;
+  int32_t fallback_enabled;
+  char spill_dir[512];
+  Stats stats;
+};
+
+class Store {
+ public:
+  // Create a new segment (head process) or attach to an existing one.
+  static Store* Create(const std::string& name, uint64_t size, const std::string& spill_dir,
+                       double spill_threshold, uint64_t min_spill_size, bool fallback);
+  static Store* Attach(const std::string& name);
+  ~Store();
+
+  // Returns payload pointer or nullptr (already exists => *exists=true).
+  // Throws std::runtime_error on out-of-memory when spilling/fallback cannot help.
+  uint8_t* CreateObject(const ObjectId& id, uint64_t data_size, uint64_t meta_size,
+                        uint32_t user_tag, uint32_t flags, bool* exists);
+  void Seal(const ObjectId& id);
+  void Abort(const ObjectId& id);
+  // Pins and returns pointer; waits up to timeout_ms (<0 = forever, 0 = no wait).
+  // Returns nullptr on timeout.
+  struct View {
+    uint8_t* data = nullptr;
+    uint64_t data_size = 0;
+    uint64_t meta_size = 0;
+    uint32_t user_tag = 0;
+    uint32_t flags = 0;
+  };
+  bool Get(const ObjectId& id, int64_t timeout_ms, View* out);
+  // Batched non-pinning readiness check: returns count of ready ids and fills ready mask.
+  int Wait(const std::vector<ObjectId>& ids, int num_required, int64_t timeout_ms,
+           std::vector<uint8_t>* ready);
+  void Release(const ObjectId& id);
+  // Delete (free) an object; deferred if pinned. Returns false if unknown.
+  bool Delete(const ObjectId& id);
+  bool Contains(const ObjectId& id);   // sealed / spilled
+  int State(const ObjectId& id);       // ObjState or -1
+  // Spill LRU unpinned objects until `bytes` have been freed. Returns bytes freed.
+  uint64_t SpillBytes(uint64_t bytes);
+  // Abort all objects still being created by `pid` (crashed creator).
+  int AbortCreator(int pid);
+  // Sealed-notification ring: returns new cursor; sets overflow when the consumer fell behind.
+  uint64_t PollSealed(uint64_t cursor, std::vector<ObjectId>* out, bool* overflow);
+  uint64_t SealSeq();
+  // Block until seal_seq != seq or timeout. Returns current seal_seq.
+  uint64_t WaitSealSeq(uint64_t seq, int64_t timeout_ms);
+  Stats GetStats();
+  uint64_t Capacity() const { return hdr_->heap_size; }
+  uint8_t* Base() const { return base_; }
+  uint64_t MappedSize() const { return size_; }
+  std::vector<std::pair<ObjectId, Entry>> ListObjects();
+  // Allocator self-check (used by tests): verifies heap walk + free lists. Returns free bytes.
+  uint64_t CheckHeap();
+  void Wake();
+
+ private:
+  Store() = default;
+  // All Locked* helpers require hdr_->mu held.
+  void Lock();
+  void Unlock();
+  int64_t Find(const ObjectId& id);
+  int64_t Insert(const ObjectId& id);
+  void RemoveEntry(int64_t idx);
+  Entry* E(int64_t idx) { return &table_[idx]; }
+  uint64_t HeapAlloc(uint64_t n);
+  void HeapFree(uint64_t payload_off);
+  void LruPush(int64_t idx);
+  void LruRemove(int64_t idx);
+  void FreeEntryStorage(int64_t idx);
+  void DropSpillRef(uint64_t file_id);
+  int64_t SpillSlot(uint64_t file_id, bool create);
+  uint64_t SpillLocked(uint64_t bytes, std::vector<int64_t>* pinned_victims);
+  bool RestoreLocked(int64_t idx);
+  uint8_t* FallbackMap(uint64_t fid, uint64_t size, bool create);
+  void FallbackUnlink(uint64_t fid);
+  std::string SpillPath(uint64_t fid) const;
+  std::string FallbackPath(uint64_t fid) const;
+  void Broadcast() { pthread_cond_broadcast(&hdr_->cv); }
+  void CondWait(int64_t deadline_ns);
+  // TLSF
+  void TlsfInsert(uint64_t blk);
+  void TlsfRemove(uint64_t blk);
+  uint64_t TlsfFind(uint64_t size);
+
+  std::string name_;
+  uint8_t* base_ = nullptr;
+  uint64_t size_ = 0;
+  Header* hdr_ = nullptr;
+  Entry* table_ = nullptr;
+  ObjectId* ring_ = nullptr;
+  SpillFileSlot* spill_ = nullptr;
+  bool owner_ = false;
+  // per-process cache of fallback mappings: fid -> (ptr,size)
+  struct FbMap { uint64_t fid; uint8_t* ptr; uint64_t size; };
+  std::vector<FbMap> fb_maps_;
+  pthread_mutex_t fb_mu_ = PTHREAD_MUTEX_INITIALIZER;
+};
+
+}  // namespace rmm

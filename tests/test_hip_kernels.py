@@ -1,0 +1,131 @@
+"""Numerics of the CDNA4 kernels against plain PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu(cuda):
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    assert "gfx950" in h.arch(0)
+    return h
+
+
+def test_multi_copy_any_alignment(cuda):
+    from ray_memory_management_amd import ops
+
+    torch.manual_seed(0)
+    srcs = [torch.randint(0, 255, (n,), dtype=torch.uint8, device=cuda) for n in (1, 15, 16, 1000, 1 << 20, 3 << 20 | 7)]
+    # misaligned views
+    srcs.append(torch.randint(0, 255, (5000,), dtype=torch.uint8, device=cuda)[3:])
+    dsts = [torch.empty(s.numel() + 13, dtype=torch.uint8, device=cuda)[5:5 + s.numel()] for s in srcs]
+    ops.multi_copy(list(zip(srcs, dsts)))
+    torch.cuda.synchronize()
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(s, d)
+
+
+def test_many_segments_split_launches(cuda):
+    from ray_memory_management_amd import ops
+
+    srcs = [torch.full((100 + i,), i % 251, dtype=torch.uint8, device=cuda) for i in range(200)]
+    dsts = [torch.empty_like(s) for s in srcs]
+    ops.multi_copy(list(zip(srcs, dsts)))
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(s, d)
+
+
+def test_pack_unpack_roundtrip(cuda):
+    from ray_memory_management_amd import ops
+
+    ts = [torch.randn(37, 5, device=cuda, dtype=torch.bfloat16), torch.arange(11, device=cuda),
+          torch.randn(3, 4, 5, device=cuda), torch.empty(0, device=cuda)]
+    buf, layout = ops.pack_tensors(ts)
+    outs = ops.unpack_tensors(buf, layout, copy=True)
+    for a, b in zip(ts, outs):
+        assert torch.equal(a, b)
+
+
+def test_concat_matches_torch_cat(cuda):
+    from ray_memory_management_amd import ops
+
+    ts = [torch.randn(n, 84, 84, device=cuda).to(torch.bfloat16) for n in (3, 0, 17, 64)]
+    assert torch.equal(ops.concat(ts), torch.cat(ts))
+
+
+def test_gather_rows(cuda):
+    from ray_memory_management_amd import ops
+
+    x = torch.randn(1000, 4, 84, 84, device=cuda).to(torch.bfloat16)
+    idx = torch.randperm(1000, device=cuda)[:333]
+    assert torch.equal(ops.gather_rows(x, idx), x[idx])
+    y = torch.arange(999 * 3, dtype=torch.uint8, device=cuda).view(999, 3)  # odd row bytes
+    idx2 = torch.randint(0, 999, (77,), device=cuda)
+    assert torch.equal(ops.gather_rows(y, idx2), y[idx2])
+
+
+@pytest.mark.parametrize("T,B", [(1, 1), (7, 3), (128, 64), (200, 1000), (1000, 17)])
+def test_gae_matches_fp32_reference(cuda, T, B):
+    from ray_memory_management_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(T * 1000 + B)
+    r = torch.randn(T, B, generator=g).to(cuda)
+    v = torch.randn(T, B, generator=g).to(cuda)
+    d = (torch.rand(T, B, generator=g) < 0.05).float().to(cuda)
+    lv = torch.randn(B, generator=g).to(cuda)
+    adv, ret = ops.gae(r, v, d, lv, 0.99, 0.95)
+    ra, rr = ops.gae_reference(r.cpu().double(), v.cpu().double(), d.cpu().double(), lv.cpu().double(), 0.99, 0.95)
+    torch.testing.assert_close(adv.cpu().double(), ra, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(ret.cpu().double(), rr, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 100_003, 1 << 20])
+def test_compress_lossless(cuda, dtype, n):
+    from ray_memory_management_amd import ops
+
+    x = (torch.randn(n, device=cuda) * 0.02).to(dtype)
+    x[: n // 3] = 0  # zero blocks
+    c = ops.compress(x)
+    y = ops.decompress(c, n, dtype)
+    assert torch.equal(x.view(torch.int16 if dtype != torch.float32 else torch.int32),
+                       y.view(torch.int16 if dtype != torch.float32 else torch.int32))
+    if n >= 100_000:
+        assert c.numel() < x.numel() * x.element_size() * 0.85
+
+
+def test_compress_special_values(cuda):
+    from ray_memory_management_amd import ops
+
+    x = torch.tensor([float("inf"), -float("inf"), float("nan"), -0.0, 0.0, 1e-40, -3.5] * 100, device=cuda)
+    for dt in (torch.float32, torch.bfloat16):
+        xx = x.to(dt)
+        y = ops.decompress(ops.compress(xx), xx.numel(), dt)
+        assert torch.equal(xx.view(torch.int32 if dt == torch.float32 else torch.int16),
+                           y.view(torch.int32 if dt == torch.float32 else torch.int16))
+
+
+def test_ppo_loss_matches_reference(cuda):
+    from ray_memory_management_amd import ops
+
+    torch.manual_seed(1)
+    n = 4097
+    ln = (torch.randn(n, device=cuda) * 0.3).requires_grad_()
+    lo = torch.randn(n, device=cuda) * 0.3
+    adv = torch.randn(n, device=cuda)
+    vn = torch.randn(n, device=cuda).requires_grad_()
+    vt = torch.randn(n, device=cuda) * 3
+    ent = torch.rand(n, device=cuda).requires_grad_()
+    tot, means = ops.ppo_loss(ln, lo, adv, vn, vt, ent, 0.2, 4.0, 0.5, 0.01)
+    tot.backward()
+    g1 = (ln.grad.clone(), vn.grad.clone(), ent.grad.clone())
+    ln.grad = vn.grad = ent.grad = None
+    rt, rmeans = ops.ppo_loss_reference(ln, lo, adv, vn, vt, ent, 0.2, 4.0, 0.5, 0.01)
+    rt.backward()
+    torch.testing.assert_close(tot, rt, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(means, rmeans, rtol=1e-4, atol=1e-5)
+    for a, b in zip(g1, (ln.grad, vn.grad, ent.grad)):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-7)
