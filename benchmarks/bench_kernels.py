@@ -100,14 +100,15 @@ def main():
             g.delete(oid)
         ids.clear()
         iters = 5
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        dt = 0.0
         for _ in range(iters):
-            put_get()
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / iters
-        for oid in ids:
-            g.delete(oid)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            v = put_get()
+            torch.cuda.synchronize()
+            dt += (time.perf_counter() - t0) / iters
+            del v
+            g.delete(ids.pop())
         out(bench="gpu_put_get", GB=gb, ms=dt * 1e3, GBps=(gb << 30) / dt / 1e9)
         del t
     # spill/restore throughput

@@ -116,6 +116,7 @@ class GpuStore {
   hipStream_t side_ = nullptr;   // spill / restore stream
   hipStream_t side2_ = nullptr;  // D2H copies overlapped with compression
   std::unique_ptr<Store> host_;
+  bool host_registered_ = false;  // whole shm segment pinned for DMA
   // compression scratch (double buffered)
   void* scratch_[2] = {nullptr, nullptr};
   void* work_ = nullptr;

@@ -1,6 +1,7 @@
 // HBM GPU object store implementation. See gpu_store.h.
 #include "gpu_store.h"
 
+#include <stdlib.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -30,7 +31,8 @@ ObjectId ToOid(const std::string& s) {
 struct HostPin {
   void* base = nullptr;
   bool ok = false;
-  HostPin(void* p, uint64_t n) {
+  HostPin(void* p, uint64_t n, bool already) {
+    if (already) return;
     long pg = sysconf(_SC_PAGESIZE);
     uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(pg - 1);
     uintptr_t e = (reinterpret_cast<uintptr_t>(p) + n + pg - 1) & ~uintptr_t(pg - 1);
@@ -58,7 +60,16 @@ GpuStore::GpuStore(int device, uint64_t capacity, uint64_t slab_bytes, const std
   RMM_HIP_CHECK(hipSetDevice(device_));
   RMM_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   RMM_HIP_CHECK(hipStreamCreateWithFlags(&side2_, hipStreamNonBlocking));
-  if (!shm_name.empty()) host_.reset(Store::Attach(shm_name));
+  if (!shm_name.empty()) {
+    host_.reset(Store::Attach(shm_name));
+    // Pin the whole host segment once so every spill/restore is a straight DMA (no per-spill
+    // page pinning). Falls back to per-object pinning if the segment cannot be registered.
+    if (getenv("RMM_GPU_NO_HOST_REGISTER") == nullptr &&
+        hipHostRegister(host_->Base(), host_->MappedSize(), hipHostRegisterDefault) == hipSuccess)
+      host_registered_ = true;
+    else
+      (void)hipGetLastError();
+  }
   st_.capacity = capacity_;
 }
 
@@ -69,10 +80,11 @@ GpuStore::~GpuStore() {
   for (auto& kv : objs_)
     if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
   for (auto& s : slabs_)
-    if (s->base) (void)hipFree(s->base);
+    if (s && s->base) (void)hipFree(s->base);
   for (auto p : scratch_)
     if (p) (void)hipFree(p);
   if (work_) (void)hipFree(work_);
+  if (host_registered_) (void)hipHostUnregister(host_->Base());
   if (side_) (void)hipStreamDestroy(side_);
   if (side2_) (void)hipStreamDestroy(side2_);
 }
@@ -347,6 +359,14 @@ void GpuStore::EnsureScratch() {
 // csize == 0 marks a raw (uncompressed) chunk of min(kSpillChunk, remaining) bytes.
 bool GpuStore::SpillOneLocked(const std::string& id, GpuObject& o) {
   if (!host_) return false;
+  // A reader in another process may hold a zero-copy view through the descriptor: the flag can
+  // only be set while nobody pins the descriptor, and readers that see it take the host path.
+  if (!host_->TrySetFlag(ToOid(id), kFlagGpuSpilled)) return false;
+  bool done = false;
+  struct ClearOnFail {
+    Store* s; ObjectId oid; bool* done;
+    ~ClearOnFail() { if (!*done) s->ClearFlag(oid, kFlagGpuSpilled); }
+  } guard{host_.get(), ToOid(id), &done};
   uint8_t* src = static_cast<uint8_t*>(slabs_[size_t(o.slab)]->base) + o.offset;
   if (o.ready) RMM_HIP_CHECK(hipStreamWaitEvent(side_, o.ready, 0));
   uint64_t nchunks = (o.nbytes + kSpillChunk - 1) / kSpillChunk;
@@ -389,7 +409,7 @@ bool GpuStore::SpillOneLocked(const std::string& id, GpuObject& o) {
   h[3] = nchunks;
   for (uint64_t c = 0; c < nchunks; c++) h[4 + c] = csize[c];
   {
-    HostPin pin(dst + hdr, payload);
+    HostPin pin(dst + hdr, payload, host_registered_);
     uint64_t doff = hdr;
     hipEvent_t done[2] = {nullptr, nullptr};
     RMM_HIP_CHECK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
@@ -433,21 +453,24 @@ bool GpuStore::SpillOneLocked(const std::string& id, GpuObject& o) {
   st_.spilled_objects++;
   st_.spilled_bytes_total += o.nbytes;
   st_.spilled_host_bytes_total += payload;
+  done = true;
   return true;
 }
 
 uint64_t GpuStore::SpillLocked(uint64_t bytes) {
   uint64_t freed = 0;
-  while (freed < bytes && !lru_.empty()) {
-    std::string victim = lru_.front();
-    GpuObject& o = objs_[victim];
+  std::vector<std::string> order(lru_.begin(), lru_.end());
+  for (auto& victim : order) {
+    if (freed >= bytes) break;
+    auto it = objs_.find(victim);
+    if (it == objs_.end()) continue;
+    GpuObject& o = it->second;
     if (o.pins > 0 || o.spilled) {
       LruDrop(o);
       continue;
     }
     uint64_t n = AlignG(o.nbytes);
-    if (!SpillOneLocked(victim, o)) break;
-    freed += n;
+    if (SpillOneLocked(victim, o)) freed += n;
   }
   return freed;
 }
@@ -489,7 +512,7 @@ bool GpuStore::RestoreLocked(const std::string& id, GpuObject& o, hipStream_t st
   }
   uint8_t* dst = static_cast<uint8_t*>(slabs_[size_t(slab)]->base) + off;
   {
-    HostPin pin(v.data + hdr, v.data_size - hdr);
+    HostPin pin(v.data + hdr, v.data_size - hdr, host_registered_);
     uint64_t soff = hdr;
     bool any_c = false;
     for (uint64_t c = 0; c < nchunks; c++) any_c |= h[4 + c] != 0;
@@ -529,6 +552,20 @@ bool GpuStore::RestoreLocked(const std::string& id, GpuObject& o, hipStream_t st
   o.slab = slab;
   o.offset = off;
   o.spilled = false;
+  // publish the new location to cross-process readers, then clear the spilled flag
+  {
+    Slab* sl = slabs_[size_t(slab)].get();
+    ObjectId did = ToOid(id);
+    host_->WithLockedData(did, [&](uint8_t* d, uint32_t) {
+      GpuDesc* g = reinterpret_cast<GpuDesc*>(d);
+      if (g->magic == kGpuDescMagic) {
+        g->slab = slab;
+        g->offset = off;
+        memcpy(g->ipc, &sl->ipc, sizeof(g->ipc));
+      }
+    });
+    host_->ClearFlag(did, kFlagGpuSpilled);
+  }
   st_.restored_bytes_total += o.nbytes;
   (void)stream;
   return true;

@@ -909,6 +909,26 @@ bool Store::Contains(const ObjectId& id) {
   return r;
 }
 
+bool Store::TrySetFlag(const ObjectId& id, uint32_t flag) {
+  Lock();
+  int64_t idx = Find(id);
+  bool ok = true;
+  if (idx >= 0) {
+    Entry* e = E(idx);
+    if (e->pin_count > 0) ok = false;
+    else e->flags |= flag;
+  }
+  Unlock();
+  return ok;
+}
+
+void Store::ClearFlag(const ObjectId& id, uint32_t flag) {
+  Lock();
+  int64_t idx = Find(id);
+  if (idx >= 0) E(idx)->flags &= ~flag;
+  Unlock();
+}
+
 int Store::State(const ObjectId& id) {
   Lock();
   int64_t idx = Find(id);

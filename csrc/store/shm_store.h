@@ -46,7 +46,24 @@ enum ObjFlags : uint32_t {
   kFlagDeletePending = 1u << 1, // delete requested while pinned
   kFlagHasSpillCopy = 1u << 2,  // an up-to-date copy exists in external storage
   kFlagError = 1u << 3,         // payload is a serialized error
+  kFlagGpuSpilled = 1u << 4,    // GPU-object descriptor: HBM copy spilled to the host store
 };
+
+// Binary header of a GPU-object descriptor object (tag kTagGpu). The owning process's GPU
+// store rewrites slab/offset/ipc in place when it restores a spilled object; readers only trust
+// these fields while they hold a pin AND kFlagGpuSpilled is clear (both checked under the lock).
+struct GpuDesc {
+  uint64_t magic;  // kGpuDescMagic
+  uint64_t nbytes;
+  int64_t slab;
+  uint64_t offset;
+  int32_t device;
+  int32_t owner_pid;
+  uint8_t ipc[64];
+  char pci_bus_id[16];
+  uint64_t meta_len;  // pickled (dtype, shape, ...) follows the header
+};
+constexpr uint64_t kGpuDescMagic = 0x4353454455504752ull;  // "RGPUDESC"
 
 struct ObjectId {
   uint8_t b[kIdSize];
@@ -158,6 +175,19 @@ class Store {
   // Delete (free) an object; deferred if pinned. Returns false if unknown.
   bool Delete(const ObjectId& id);
   bool Contains(const ObjectId& id);   // sealed / spilled
+  // Set `flag` only if nobody holds a pin (returns false if pinned; true if absent).
+  bool TrySetFlag(const ObjectId& id, uint32_t flag);
+  void ClearFlag(const ObjectId& id, uint32_t flag);
+  // Run `fn(data)` on a sealed object's payload under the store lock (in-place metadata update).
+  template <typename F>
+  bool WithLockedData(const ObjectId& id, F fn) {
+    Lock();
+    int64_t idx = Find(id);
+    bool ok = idx >= 0 && E(idx)->state == kSealed && !(E(idx)->flags & kFlagFallback);
+    if (ok) fn(base_ + E(idx)->offset, E(idx)->flags);
+    Unlock();
+    return ok;
+  }
   int State(const ObjectId& id);       // ObjState or -1
   // Spill LRU unpinned objects until `bytes` have been freed. Returns bytes freed.
   uint64_t SpillBytes(uint64_t bytes);

@@ -312,7 +312,7 @@ PYBIND11_MODULE(_store, m) {
             pin->size = v.data_size + v.meta_size;
             pin->writable = false;
             return py::make_tuple(py::cast(pin), v.data_size, v.meta_size, v.user_tag,
-                                  bool(v.flags & kFlagError));
+                                  bool(v.flags & kFlagError), v.flags);
           },
           py::arg("oid"), py::arg("timeout_ms") = -1)
       .def(
@@ -387,6 +387,9 @@ PYBIND11_MODULE(_store, m) {
         return out;
       });
 
+  m.attr("FLAG_GPU_SPILLED") = uint32_t(kFlagGpuSpilled);
+  m.attr("GPU_DESC_MAGIC") = kGpuDescMagic;
+  m.attr("GPU_DESC_SIZE") = sizeof(GpuDesc);
   m.def("parallel_memcpy",
         [](py::buffer dst, py::buffer src) {
           auto d = dst.request(true);

@@ -1,0 +1,1237 @@
+"""Head node process: GCS + raylet roles for one machine (plus virtual nodes for tests).
+
+Parity (behaviour, re-designed): reference src/ray/raylet/node_manager.cc (task dispatch, worker
+lifecycle, blocked-worker resource release), src/ray/raylet/worker_pool.cc (process pool keyed by
+runtime env), src/ray/raylet/local_task_manager.cc (dispatch queue), src/ray/gcs/gcs_server/
+{gcs_actor_manager,gcs_placement_group_manager,gcs_kv_manager,gcs_job_manager}.cc,
+src/ray/core_worker/reference_count.cc (we count centrally: every process reports batched
+deltas), src/ray/core_worker/task_manager.cc (retries), src/ray/raylet/local_object_manager.cc
+(threshold spilling), python/ray/_private/memory_monitor.py.
+
+Design: ONE event-loop thread owns all state. Heavy lifting is native: the C++ scheduler
+(`_sched`) decides placement/resources/dependencies; the shared-memory store (`_store`) is the
+data plane — object seals reach this loop through the store's sealed-object ring (a watcher thread
+blocks on the in-segment condvar and pokes the loop through a self-pipe).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import os
+import pickle
+import selectors
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, List, Optional
+
+from ray_memory_management_amd._native import sched_ext, store_ext
+from ray_memory_management_amd._private import protocol as P
+from ray_memory_management_amd._private import serialization as ser
+from ray_memory_management_amd._private.ids import ID_SIZE, object_id_for_return
+from ray_memory_management_amd import exceptions as exc
+
+PENDING, RUNNING, FINISHED, FAILED, CANCELLED = "PENDING", "RUNNING", "FINISHED", "FAILED", "CANCELLED"
+ACTOR_PENDING, ACTOR_ALIVE, ACTOR_RESTARTING, ACTOR_DEAD = (
+    "PENDING_CREATION", "ALIVE", "RESTARTING", "DEAD")
+
+
+def actor_ref_key(actor_id: bytes) -> bytes:
+    """Pseudo object id used to reference-count actor handles."""
+    return b"\xaa" + actor_id[:16] + b"\xaa\xaa\xaa"
+
+
+class Conn:
+    __slots__ = ("sock", "reader", "kind", "worker", "pid", "lock", "job_id", "alive", "wbuf")
+
+    def __init__(self, sock):
+        self.sock = sock
+        self.reader = P.FrameReader()
+        self.kind = None
+        self.worker = None
+        self.pid = None
+        self.lock = threading.Lock()
+        self.job_id = None
+        self.alive = True
+
+    def send(self, msg):
+        if not self.alive:
+            return
+        try:
+            P.send(self.sock, msg, self.lock)
+        except OSError:
+            self.alive = False
+
+
+class WorkerRec:
+    __slots__ = ("worker_id", "pid", "proc", "conn", "node", "env_key", "state", "task", "actor_id",
+                 "fns", "gpu_key", "blocked", "start_time", "tasks_run", "lease", "idle_since", "calls")
+
+    def __init__(self, worker_id, proc, node, env_key, gpu_key):
+        self.worker_id = worker_id
+        self.pid = proc.pid if proc else None
+        self.proc = proc
+        self.conn: Optional[Conn] = None
+        self.node = node
+        self.env_key = env_key
+        self.gpu_key = gpu_key
+        self.state = "STARTING"
+        self.task = None
+        self.actor_id = None
+        self.fns = set()
+        self.blocked = False
+        self.start_time = time.time()
+        self.tasks_run = 0
+        self.lease = None
+        self.idle_since = time.time()
+        self.calls = collections.Counter()
+
+
+class TaskRec:
+    __slots__ = ("spec", "state", "worker", "node", "assign", "retries_left", "attempt", "submit_time",
+                 "start_time", "end_time", "arg_refs", "owner_conn", "cancelled", "error")
+
+    def __init__(self, spec, owner_conn):
+        self.spec = spec
+        self.state = PENDING
+        self.worker = None
+        self.node = None
+        self.assign = None
+        self.retries_left = spec.get("max_retries", 3)
+        self.attempt = 0
+        self.submit_time = time.time()
+        self.start_time = None
+        self.end_time = None
+        self.arg_refs = spec.get("arg_refs", [])
+        self.owner_conn = owner_conn
+        self.cancelled = False
+        self.error = None
+
+
+class ActorRec:
+    def __init__(self, spec, owner_conn):
+        self.spec = spec
+        self.actor_id = spec["actor_id"]
+        self.state = ACTOR_PENDING
+        self.worker: Optional[WorkerRec] = None
+        self.address = None
+        self.name = spec.get("name")
+        self.namespace = spec.get("namespace")
+        self.detached = spec.get("lifetime") == "detached"
+        self.restarts_left = spec.get("max_restarts", 0)
+        self.num_restarts = 0
+        self.node = None
+        self.assign = None
+        self.waiters: List[tuple] = []
+        self.owner_conn = owner_conn
+        self.job_id = spec.get("job_id")
+        self.death_cause = None
+        self.pid = None
+        self.task_key = None
+        self.start_time = time.time()
+
+
+class PGRec:
+    def __init__(self, pg_id, bundles, strategy, name, lifetime, job_id):
+        self.pg_id = pg_id
+        self.bundles = bundles
+        self.strategy = strategy
+        self.name = name
+        self.lifetime = lifetime
+        self.job_id = job_id
+        self.state = "PENDING"
+        self.waiters: List[tuple] = []
+        self.nodes = []
+
+
+class Head:
+    def __init__(self, args):
+        self.args = args
+        self.session_dir = args.session_dir
+        self.sock_path = os.path.join(self.session_dir, "sockets", "head.sock")
+        self.store_name = args.store_name
+        self.config = json.loads(args.config) if args.config else {}
+        spill_dir = self.config.get("spill_dir") or os.path.join(self.session_dir, "spill")
+        os.makedirs(spill_dir, exist_ok=True)
+        cap = int(args.object_store_memory)
+        min_spill = int(self.config.get("min_spilling_size", min(100 << 20, max(1 << 20, cap // 16))))
+        self.spill_threshold = float(self.config.get("object_spilling_threshold", 0.8))
+        self.store = store_ext().ObjectStore.create_segment(
+            self.store_name, cap, spill_dir if self.config.get("automatic_object_spilling_enabled", True) else "",
+            self.spill_threshold, min_spill, True)
+        self.sched = sched_ext().Scheduler()
+        self.sched.set_spread_threshold(float(self.config.get("scheduler_spread_threshold", 0.5)))
+        self.nodes: Dict[int, dict] = {}
+        self.head_node = 1
+        res = json.loads(args.resources)
+        self._add_node(self.head_node, res, head=True)
+        self.sel = selectors.DefaultSelector()
+        self.lsock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.lsock.bind(self.sock_path)
+        self.lsock.listen(512)
+        self.lsock.setblocking(False)
+        self.sel.register(self.lsock, selectors.EVENT_READ, ("listen", None))
+        self.wake_r, self.wake_w = os.pipe()
+        os.set_blocking(self.wake_r, False)
+        self.sel.register(self.wake_r, selectors.EVENT_READ, ("wake", None))
+        self.pending_calls = collections.deque()
+        self.pending_lock = threading.Lock()
+        self.conns: Dict[int, Conn] = {}
+        self.workers: Dict[bytes, WorkerRec] = {}
+        self.idle: Dict[tuple, List[WorkerRec]] = collections.defaultdict(list)
+        self.starting: Dict[tuple, int] = collections.Counter()
+        self.tasks: Dict[bytes, TaskRec] = {}
+        self.finished_tasks = collections.OrderedDict()
+        self.task_keys: Dict[int, bytes] = {}
+        self.key_counter = 0
+        self.dispatch_q: Dict[int, collections.deque] = collections.defaultdict(collections.deque)
+        self.actors: Dict[bytes, ActorRec] = {}
+        self.named_actors: Dict[tuple, bytes] = {}
+        self.pgs: Dict[bytes, PGRec] = {}
+        self.named_pgs: Dict[tuple, bytes] = {}
+        self.kv: Dict[bytes, Dict[bytes, bytes]] = collections.defaultdict(dict)
+        self.fn_table: Dict[bytes, bytes] = {}
+        self.refcounts: Dict[bytes, int] = collections.defaultdict(int)
+        self.contained: Dict[bytes, List[bytes]] = {}
+        self.freed_early: set = set()
+        self.gpu_owner: Dict[bytes, bytes] = {}
+        self.jobs: Dict[bytes, dict] = {}
+        self.events = collections.deque(maxlen=int(self.config.get("timeline_max_events", 200000)))
+        self.seal_cursor = 0
+        self.running = True
+        self.driver_conn = None
+        self.next_node_id = 2
+        self.max_workers = int(self.config.get("max_workers", max(64, 4 * int(res.get("CPU", 1)))))
+        self.prestart = int(self.config.get("prestart_workers", min(2, int(res.get("CPU", 1)))))
+        self.idle_timeout = float(self.config.get("idle_worker_killing_time_threshold_ms", 60000)) / 1000.0
+        self.memory_monitor = None
+        self.last_housekeeping = 0.0
+        self.watcher = threading.Thread(target=self._seal_watcher, daemon=True)
+        self.watcher.start()
+        if self.config.get("memory_monitor_refresh_ms", 250) > 0:
+            from ray_memory_management_amd._private.memory_monitor import MemoryMonitor
+
+            self.memory_monitor = MemoryMonitor(
+                threshold=float(self.config.get("memory_usage_threshold", 0.95)))
+
+    # ------------------------------------------------------------------ nodes
+    def _add_node(self, node_id, resources, head=False):
+        resources = {k: float(v) for k, v in resources.items() if v}
+        resources.setdefault("node:__internal_head__" if head else f"node:{node_id}", 1.0)
+        resources[f"node:{node_id}"] = 1.0
+        self.sched.add_node(node_id, resources)
+        self.nodes[node_id] = {"node_id": node_id, "resources": resources, "alive": True,
+                               "start_time": time.time(), "is_head": head}
+
+    def _remove_node(self, node_id):
+        if node_id not in self.nodes or node_id == self.head_node:
+            return False
+        self.nodes[node_id]["alive"] = False
+        for w in list(self.workers.values()):
+            if w.node == node_id:
+                self._kill_worker(w)
+        self.sched.remove_node(node_id)
+        return True
+
+    # ------------------------------------------------------------------ plumbing
+    def _wake(self):
+        try:
+            os.write(self.wake_w, b"x")
+        except OSError:
+            pass
+
+    def call_soon(self, fn, *a):
+        with self.pending_lock:
+            self.pending_calls.append((fn, a))
+        self._wake()
+
+    def _seal_watcher(self):
+        seq = self.store.seal_seq()
+        while self.running:
+            nseq = self.store.wait_seal_seq(seq, 200)
+            if nseq != seq:
+                seq = nseq
+                self._wake()
+
+    def serve(self):
+        os.makedirs(os.path.dirname(self.sock_path), exist_ok=True)
+        ready_file = os.path.join(self.session_dir, "head.ready")
+        with open(ready_file, "w") as f:
+            f.write(str(os.getpid()))
+        for _ in range(self.prestart):
+            self._start_worker(self.head_node, ("", ""), None)
+        while self.running:
+            try:
+                events = self.sel.select(timeout=0.05)
+            except InterruptedError:
+                continue
+            for key, _ in events:
+                kind, conn = key.data
+                if kind == "listen":
+                    self._accept()
+                elif kind == "wake":
+                    try:
+                        while os.read(self.wake_r, 4096):
+                            pass
+                    except (BlockingIOError, OSError):
+                        pass
+                else:
+                    self._read(conn)
+            self._drain_calls()
+            self._poll_sealed()
+            self._schedule()
+            now = time.time()
+            if now - self.last_housekeeping > 0.1:
+                self.last_housekeeping = now
+                self._housekeeping()
+        self._shutdown()
+
+    def _drain_calls(self):
+        while True:
+            with self.pending_lock:
+                if not self.pending_calls:
+                    return
+                fn, a = self.pending_calls.popleft()
+            try:
+                fn(*a)
+            except Exception:
+                traceback.print_exc()
+
+    def _accept(self):
+        while True:
+            try:
+                s, _ = self.lsock.accept()
+            except (BlockingIOError, OSError):
+                return
+            s.setblocking(True)
+            c = Conn(s)
+            self.conns[s.fileno()] = c
+            s.setblocking(False)
+            self.sel.register(s, selectors.EVENT_READ, ("conn", c))
+
+    def _read(self, c: Conn):
+        try:
+            data = c.sock.recv(1 << 20)
+        except BlockingIOError:
+            return
+        except OSError:
+            data = b""
+        if not data:
+            self._disconnect(c)
+            return
+        try:
+            msgs = c.reader.feed(data)
+        except Exception:
+            traceback.print_exc()
+            self._disconnect(c)
+            return
+        for m in msgs:
+            try:
+                self._handle(c, m)
+            except Exception:
+                traceback.print_exc()
+
+    def _send_nb(self, c: Conn, msg):
+        """Send from the loop thread: sockets are non-blocking for reads; writes block briefly."""
+        if not c.alive:
+            return
+        s = c.sock
+        try:
+            s.setblocking(True)
+            P.send(s, msg, c.lock)
+        except OSError:
+            c.alive = False
+        finally:
+            try:
+                s.setblocking(False)
+            except OSError:
+                pass
+
+    def _reply(self, c, req_id, value):
+        self._send_nb(c, (P.REPLY, req_id, value))
+
+    # ------------------------------------------------------------------ dispatch table
+    def _handle(self, c: Conn, m):
+        t = m[0]
+        if t == P.REF_DELTAS:
+            self._ref_deltas(m[1])
+        elif t == P.SUBMIT_TASK:
+            self._submit_task(c, m[1])
+        elif t == P.TASK_DONE:
+            self._task_done(c, m[1], m[2], m[3], m[4] if len(m) > 4 else None)
+        elif t == P.REGISTER:
+            self._register(c, m[1], m[2])
+        elif t == P.CREATE_ACTOR:
+            self._create_actor(c, m[1], m[2])
+        elif t == P.WAIT_ACTOR:
+            self._wait_actor(c, m[1], m[2])
+        elif t == P.ACTOR_READY:
+            self._actor_ready(c, m[1], m[2])
+        elif t == P.ACTOR_FAILED_INIT:
+            self._actor_failed_init(c, m[1], m[2])
+        elif t == P.CONTAINED:
+            self._add_contained(m[1], m[2])
+        elif t == P.BLOCKED:
+            self._blocked(c, True)
+        elif t == P.UNBLOCKED:
+            self._blocked(c, False)
+        elif t == P.KV_PUT:
+            ns, k, v, overwrite = m[2], m[3], m[4], m[5]
+            existed = k in self.kv[ns]
+            if overwrite or not existed:
+                self.kv[ns][k] = v
+            if m[1] is not None:
+                self._reply(c, m[1], existed)
+        elif t == P.KV_GET:
+            self._reply(c, m[1], self.kv[m[2]].get(m[3]))
+        elif t == P.KV_DEL:
+            ns, k, prefix = m[2], m[3], m[4]
+            if prefix:
+                ks = [x for x in self.kv[ns] if x.startswith(k)]
+            else:
+                ks = [k] if k in self.kv[ns] else []
+            for x in ks:
+                del self.kv[ns][x]
+            if m[1] is not None:
+                self._reply(c, m[1], len(ks))
+        elif t == P.KV_KEYS:
+            self._reply(c, m[1], [x for x in self.kv[m[2]] if x.startswith(m[3])])
+        elif t == P.GET_ACTOR:
+            self._get_actor(c, m[1], m[2], m[3])
+        elif t == P.KILL_ACTOR:
+            self._kill_actor(m[1], m[2], "ray.kill() was called")
+        elif t == P.CANCEL:
+            self._cancel(m[1], m[2], m[3])
+        elif t == P.PG_CREATE:
+            self._pg_create(c, m[1], m[2])
+        elif t == P.PG_REMOVE:
+            self._pg_remove(m[1])
+        elif t == P.PG_WAIT:
+            self._pg_wait(c, m[1], m[2])
+        elif t == P.PG_TABLE:
+            self._reply(c, m[1], self._pg_table(m[2]))
+        elif t == P.STATE:
+            self._reply(c, m[1], self._state(m[2], m[3] if len(m) > 3 else None))
+        elif t == P.EVENTS:
+            self.events.extend(m[1])
+        elif t == P.GPU_OBJECT:
+            self.gpu_owner[m[1]] = c.worker.worker_id if c.worker else b"driver:" + str(c.pid).encode()
+            self.gpu_owner_conn = getattr(self, "gpu_owner_conn", {})
+            self.gpu_owner_conn[m[1]] = c
+        elif t == P.ADD_NODE:
+            nid = self.next_node_id
+            self.next_node_id += 1
+            self._add_node(nid, m[2])
+            self._reply(c, m[1], nid)
+        elif t == P.REMOVE_NODE:
+            self._reply(c, m[1], self._remove_node(m[2]))
+        elif t == P.JOB_INFO:
+            self._reply(c, m[1], {"session_dir": self.session_dir, "store_name": self.store_name,
+                                  "config": self.config})
+        elif t == P.ACTOR_EXITING:
+            a = self.actors.get(m[1])
+            if a is not None:
+                a.restarts_left = 0
+                a.death_cause = "The actor exited via exit_actor()."
+        elif t == P.SHUTDOWN:
+            self.running = False
+        else:
+            print(f"[head] unknown message {t}", file=sys.stderr)
+
+    # ------------------------------------------------------------------ registration / workers
+    def _register(self, c: Conn, kind, info):
+        c.kind = kind
+        c.pid = info.get("pid")
+        if kind == "driver":
+            job_id = info.get("job_id")
+            c.job_id = job_id
+            self.jobs[job_id] = {"job_id": job_id, "pid": c.pid, "start_time": time.time(), "end_time": None,
+                                 "namespace": info.get("namespace"), "alive": True, "conn": c}
+            if self.driver_conn is None:
+                self.driver_conn = c
+            self._reply(c, info["req_id"], {
+                "store_name": self.store_name, "session_dir": self.session_dir, "node_id": self.head_node,
+                "config": self.config, "resources": self.sched.cluster_total()})
+            return
+        wid = info["worker_id"]
+        w = self.workers.get(wid)
+        if w is None:
+            # a worker started by someone else (should not happen) — adopt
+            return
+        w.conn = c
+        c.worker = w
+        w.state = "IDLE"
+        w.idle_since = time.time()
+        self.starting[(w.node, w.env_key, w.gpu_key)] -= 1
+        if w.actor_id is not None:
+            a = self.actors.get(w.actor_id)
+            if a is None or a.state == ACTOR_DEAD:
+                self._kill_worker(w)
+                return
+            w.state = "ACTOR"
+            self._send_nb(c, (P.CREATE_ACTOR_INSTANCE, a.spec, self.fn_table.get(a.spec["class_id"]),
+                              {"gpu_ids": a.assign[2] if a.assign else [], "node_id": a.node,
+                               "restart": a.num_restarts}))
+            return
+        self.idle[(w.node, w.env_key, w.gpu_key)].append(w)
+
+    def _worker_env(self, node, env_key, gpu_ids, runtime_env):
+        env = dict(os.environ)
+        env["RMM_SESSION_DIR"] = self.session_dir
+        env["RMM_STORE_NAME"] = self.store_name
+        env["RMM_NODE_ID"] = str(node)
+        env["RMM_HEAD_SOCKET"] = self.sock_path
+        env["PYTHONUNBUFFERED"] = "1"
+        env["RMM_CONFIG"] = json.dumps(self.config)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+        if gpu_ids is not None:
+            vis = ",".join(str(g) for g in gpu_ids)
+            env["HIP_VISIBLE_DEVICES"] = vis
+            env["CUDA_VISIBLE_DEVICES"] = vis
+            env["RMM_GPU_IDS"] = vis
+        if runtime_env:
+            for k, v in (runtime_env.get("env_vars") or {}).items():
+                env[str(k)] = str(v)
+            if runtime_env.get("working_dir") or runtime_env.get("py_modules"):
+                env["RMM_RUNTIME_ENV"] = json.dumps({k: runtime_env[k] for k in ("working_dir", "py_modules")
+                                                     if runtime_env.get(k)})
+        env.pop("RMM_DRIVER", None)
+        return env
+
+    def _start_worker(self, node, key, gpu_ids, actor_id=None, runtime_env=None):
+        env_key, gpu_key = key
+        wid = os.urandom(16)
+        env = self._worker_env(node, env_key, gpu_ids, runtime_env)
+        env["RMM_WORKER_ID"] = wid.hex()
+        log_dir = os.path.join(self.session_dir, "logs")
+        out = open(os.path.join(log_dir, f"worker-{wid.hex()[:12]}.log"), "ab")
+        cmd = [sys.executable, "-u", "-m", "ray_memory_management_amd._private.worker_main"]
+        proc = subprocess.Popen(cmd, env=env, stdout=out, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                start_new_session=False)
+        out.close()
+        w = WorkerRec(wid, proc, node, env_key, gpu_key)
+        w.actor_id = actor_id
+        self.workers[wid] = w
+        self.starting[(node, env_key, gpu_key)] += 1
+        return w
+
+    def _kill_worker(self, w: WorkerRec, force=True):
+        if w.proc is not None and w.proc.poll() is None:
+            try:
+                if force:
+                    w.proc.kill()
+                else:
+                    w.proc.terminate()
+            except OSError:
+                pass
+        w.state = "DEAD"
+
+    def _disconnect(self, c: Conn):
+        if not c.alive and c.sock.fileno() < 0:
+            return
+        c.alive = False
+        try:
+            self.sel.unregister(c.sock)
+        except Exception:
+            pass
+        self.conns.pop(c.sock.fileno(), None)
+        try:
+            c.sock.close()
+        except OSError:
+            pass
+        if c.kind == "driver":
+            self._driver_exit(c)
+        elif c.worker is not None:
+            self._worker_died(c.worker)
+
+    def _driver_exit(self, c: Conn):
+        job = self.jobs.get(c.job_id)
+        if job:
+            job["alive"] = False
+            job["end_time"] = time.time()
+        # kill non-detached actors of this job
+        for a in list(self.actors.values()):
+            if a.job_id == c.job_id and not a.detached and a.state != ACTOR_DEAD:
+                a.restarts_left = 0
+                self._kill_actor(a.actor_id, True, "The driver exited.")
+        # release the driver's references
+        if c is self.driver_conn and not self.args.persistent:
+            self.running = False
+
+    def _worker_died(self, w: WorkerRec):
+        if w.state == "GONE":
+            return
+        prev_state = w.state
+        w.state = "GONE"
+        self.workers.pop(w.worker_id, None)
+        for lst in self.idle.values():
+            if w in lst:
+                lst.remove(w)
+        if prev_state == "STARTING":
+            self.starting[(w.node, w.env_key, w.gpu_key)] -= 1
+        if w.pid:
+            try:
+                self.store.abort_creator(w.pid)
+            except Exception:
+                pass
+        if w.proc is not None:
+            try:
+                w.proc.wait(timeout=0.05)
+            except Exception:
+                pass
+        if w.task is not None:
+            t = self.tasks.get(w.task)
+            w.task = None
+            if t is not None:
+                self._release_task_resources(t)
+                if t.cancelled:
+                    self._fail_task(t, exc.TaskCancelledError(t.spec["task_id"].hex()), CANCELLED)
+                elif t.retries_left != 0:
+                    if t.retries_left > 0:
+                        t.retries_left -= 1
+                    t.attempt += 1
+                    t.state = PENDING
+                    self._enqueue(t)
+                else:
+                    self._fail_task(t, exc.WorkerCrashedError(), FAILED)
+        if w.actor_id is not None:
+            a = self.actors.get(w.actor_id)
+            if a is not None and a.worker is w:
+                self._actor_died(a)
+
+    def _blocked(self, c: Conn, blocked: bool):
+        w = c.worker
+        if w is None or w.task is None or w.blocked == blocked:
+            return
+        t = self.tasks.get(w.task)
+        if t is None or t.assign is None:
+            return
+        w.blocked = blocked
+        req = t.spec["resources"]
+        cpu_only = {k: v for k, v in req.items() if k == "CPU"}
+        if not cpu_only:
+            return
+        if blocked:
+            self.sched.release(t.node, cpu_only)
+        else:
+            self.sched.acquire(t.node, cpu_only, True)
+
+    # ------------------------------------------------------------------ refcounting
+    def _ref_deltas(self, deltas):
+        rc = self.refcounts
+        for oid, d in deltas:
+            n = rc[oid] + d
+            if n <= 0:
+                del rc[oid]
+                self._free(oid)
+            else:
+                rc[oid] = n
+
+    def _add_contained(self, outer, inners):
+        if not inners:
+            return
+        self.contained.setdefault(outer, []).extend(inners)
+        rc = self.refcounts
+        for i in inners:
+            rc[i] += 1
+
+    def _free(self, oid: bytes):
+        if oid[:1] == b"\xaa" and oid[-3:] == b"\xaa\xaa\xaa":
+            self._actor_out_of_scope(oid[1:17])
+            return
+        deleted = self.store.delete([oid])
+        if not deleted:
+            self.freed_early.add(oid)
+        owner = self.gpu_owner.pop(oid, None)
+        if owner is not None:
+            c = getattr(self, "gpu_owner_conn", {}).pop(oid, None)
+            if c is not None:
+                self._send_nb(c, (P.FREE_GPU, [oid]))
+        inner = self.contained.pop(oid, None)
+        if inner:
+            self._ref_deltas([(i, -1) for i in inner])
+
+    def _poll_sealed(self):
+        cur, oids, overflow = self.store.poll_sealed(self.seal_cursor)
+        self.seal_cursor = cur
+        if not oids:
+            return
+        self.sched.objects_ready(oids)
+        if self.freed_early:
+            dead = [o for o in oids if o in self.freed_early]
+            if dead:
+                for o in dead:
+                    self.freed_early.discard(o)
+                    if o not in self.refcounts:
+                        self.store.delete([o])
+
+    # ------------------------------------------------------------------ tasks
+    def _new_key(self, task_id):
+        self.key_counter += 1
+        self.task_keys[self.key_counter] = task_id
+        return self.key_counter
+
+    def _submit_task(self, c: Conn, spec):
+        fn_blob = spec.pop("fn_blob", None)
+        if fn_blob is not None:
+            self.fn_table[spec["fn_id"]] = fn_blob
+        t = TaskRec(spec, c)
+        self.tasks[spec["task_id"]] = t
+        for r in t.arg_refs:
+            self.refcounts[r] += 1
+        self._enqueue(t)
+
+    def _strategy_args(self, spec):
+        st = spec.get("strategy") or {}
+        kind = st.get("type", "DEFAULT")
+        if kind == "SPREAD":
+            return 1, -1, False, "", -1
+        if kind == "NODE_AFFINITY":
+            return 2, int(st["node_id"]), bool(st.get("soft", False)), "", -1
+        if kind == "PLACEMENT_GROUP":
+            return 3, -1, False, st["pg_id"].hex(), int(st.get("bundle_index", -1))
+        return 0, -1, False, "", -1
+
+    def _enqueue(self, t: TaskRec):
+        spec = t.spec
+        deps = [r for r in t.arg_refs if not self.store.contains(r)]
+        key = self._new_key(spec["task_id"])
+        t.spec["_key"] = key
+        strat, aff, soft, pg, bidx = self._strategy_args(spec)
+        res = spec["resources"]
+        if strat == 3:
+            pgrec = self.pgs.get(bytes.fromhex(pg))
+            if pgrec is None or pgrec.state == "REMOVED":
+                self._fail_task(t, exc.TaskPlacementGroupRemoved("placement group was removed"), FAILED)
+                return
+        self.sched.submit(key, res, strat, aff, soft, pg, bidx, deps)
+
+    def _schedule(self):
+        placed = self.sched.schedule_placement_groups()
+        for pg_hex in placed:
+            self._pg_placed(bytes.fromhex(pg_hex))
+        assigns = self.sched.schedule(1 << 20)
+        for key, node, gpu_ids, amounts in assigns:
+            tid = self.task_keys.pop(key, None)
+            if tid is None:
+                continue
+            if isinstance(tid, tuple):  # actor creation
+                self._actor_placed(tid[1], node, gpu_ids, amounts)
+                continue
+            t = self.tasks.get(tid)
+            if t is None or t.cancelled:
+                self.sched.release(node, t.spec["resources"] if t else {}, gpu_ids, amounts)
+                if t is not None:
+                    self._fail_task(t, exc.TaskCancelledError(tid.hex()), CANCELLED)
+                continue
+            t.node = node
+            t.assign = (node, gpu_ids, amounts)
+            self.dispatch_q[node].append(t)
+        for node, q in self.dispatch_q.items():
+            while q:
+                t = q[0]
+                if not self._dispatch(t):
+                    break
+                q.popleft()
+
+    def _gpu_key(self, gpu_ids):
+        return ",".join(map(str, gpu_ids)) if gpu_ids else ""
+
+    def _dispatch(self, t: TaskRec) -> bool:
+        spec = t.spec
+        node, gpu_ids, amounts = t.assign
+        env_key = spec.get("env_key", "")
+        gkey = self._gpu_key(gpu_ids)
+        key = (node, env_key, gkey)
+        pool = self.idle.get(key)
+        w = None
+        while pool:
+            cand = pool.pop()
+            if cand.state == "IDLE" and cand.conn is not None and cand.conn.alive:
+                w = cand
+                break
+        if w is None:
+            # GPU tasks may reuse a never-GPU worker only by spawning with the right devices
+            n_start = self.starting[key]
+            waiting = sum(1 for x in self.dispatch_q[node] if x.spec.get("env_key", "") == env_key)
+            if n_start < max(1, waiting) and len(self.workers) < self.max_workers + 32:
+                self._start_worker(node, (env_key, gkey), gpu_ids if gpu_ids else None,
+                                   runtime_env=spec.get("runtime_env"))
+            return False
+        fid = spec["fn_id"]
+        blob = None
+        if fid not in w.fns:
+            blob = self.fn_table.get(fid)
+            w.fns.add(fid)
+        w.state = "BUSY"
+        w.task = spec["task_id"]
+        t.worker = w
+        t.state = RUNNING
+        t.start_time = time.time()
+        self._send_nb(w.conn, (P.EXECUTE, spec, blob, {"gpu_ids": gpu_ids, "attempt": t.attempt,
+                                                       "node_id": node}))
+        return True
+
+    def _release_task_resources(self, t: TaskRec):
+        if t.assign is not None:
+            node, gpu_ids, amounts = t.assign
+            req = dict(t.spec["resources"])
+            if t.worker is not None and t.worker.blocked and "CPU" in req:
+                req.pop("CPU")
+                t.worker.blocked = False
+            self.sched.release(node, req, gpu_ids, amounts)
+            t.assign = None
+
+    def _finish(self, t: TaskRec, state):
+        t.state = state
+        t.end_time = time.time()
+        self.tasks.pop(t.spec["task_id"], None)
+        if t.arg_refs:
+            self._ref_deltas([(r, -1) for r in t.arg_refs])
+            t.arg_refs = []
+        self.finished_tasks[t.spec["task_id"]] = t
+        while len(self.finished_tasks) > 10000:
+            self.finished_tasks.popitem(last=False)
+
+    def _task_done(self, c: Conn, task_id, status, contained, info):
+        w = c.worker
+        t = self.tasks.get(task_id)
+        if w is not None and w.task == task_id:
+            w.task = None
+            w.blocked = w.blocked  # released below
+            w.tasks_run += 1
+        if t is None:
+            if w is not None:
+                self._make_idle(w)
+            return
+        self._release_task_resources(t)
+        if contained:
+            for outer, inners in contained.items():
+                self._add_contained(outer, inners)
+        if info and info.get("events"):
+            self.events.extend(info["events"])
+        if status == "retry" and t.retries_left != 0 and not t.cancelled:
+            if t.retries_left > 0:
+                t.retries_left -= 1
+            t.attempt += 1
+            t.state = PENDING
+            if w is not None:
+                self._make_idle(w)
+            self._enqueue(t)
+            return
+        self._finish(t, FINISHED if status == "ok" else FAILED)
+        if w is not None:
+            if info and info.get("exit"):
+                self._kill_worker(w, force=False)
+            else:
+                self._make_idle(w)
+
+    def _make_idle(self, w: WorkerRec):
+        if w.state in ("DEAD", "GONE"):
+            return
+        w.state = "IDLE"
+        w.idle_since = time.time()
+        self.idle[(w.node, w.env_key, w.gpu_key)].append(w)
+
+    def _fail_task(self, t: TaskRec, error: BaseException, state=FAILED):
+        spec = t.spec
+        self._store_error(spec["task_id"], spec.get("num_returns", 1), error)
+        self._finish(t, state)
+
+    def _store_error(self, task_id, num_returns, error):
+        n = num_returns if isinstance(num_returns, int) else 1
+        data, bufs, _ = ser.serialize(error)
+        for i in range(1, max(n, 1) + 1):
+            oid = object_id_for_return(task_id, i)
+            try:
+                if self.store.state(oid) == 1:  # CREATING by a dead process
+                    self.store.abort(oid)
+                self.store.put_serialized(oid, data, bufs, ser.TAG_ERROR, True)
+            except Exception:
+                traceback.print_exc()
+
+    def _cancel(self, task_id, force, recursive):
+        t = self.tasks.get(task_id)
+        if t is None:
+            return
+        t.cancelled = True
+        if t.state == PENDING:
+            key = t.spec.get("_key")
+            if key is not None and self.sched.cancel(key):
+                self.task_keys.pop(key, None)
+            for node, q in self.dispatch_q.items():
+                if t in q:
+                    q.remove(t)
+                    self._release_task_resources(t)
+            self._fail_task(t, exc.TaskCancelledError(task_id.hex()), CANCELLED)
+        elif t.state == RUNNING and t.worker is not None:
+            if force:
+                self._kill_worker(t.worker)
+            elif t.worker.conn is not None:
+                self._send_nb(t.worker.conn, (P.CANCEL_TASK, task_id))
+
+    # ------------------------------------------------------------------ actors
+    def _create_actor(self, c: Conn, req_id, spec):
+        fn_blob = spec.pop("class_blob", None)
+        if fn_blob is not None:
+            self.fn_table[spec["class_id"]] = fn_blob
+        name = spec.get("name")
+        if name:
+            key = (spec.get("namespace"), name)
+            existing = self.named_actors.get(key)
+            if existing is not None and self.actors[existing].state != ACTOR_DEAD:
+                if req_id is not None:
+                    self._reply(c, req_id, ("exists", existing))
+                return
+            self.named_actors[key] = spec["actor_id"]
+        a = ActorRec(spec, c)
+        self.actors[a.actor_id] = a
+        for r in spec.get("arg_refs", []):
+            self.refcounts[r] += 1
+        if req_id is not None:
+            self._reply(c, req_id, ("ok", a.actor_id))
+        self._schedule_actor(a)
+
+    def _schedule_actor(self, a: ActorRec):
+        spec = a.spec
+        key = self._new_key(("actor", a.actor_id))
+        self.task_keys[key] = ("actor", a.actor_id)
+        a.task_key = key
+        strat, aff, soft, pg, bidx = self._strategy_args(spec)
+        deps = [r for r in spec.get("arg_refs", []) if not self.store.contains(r)]
+        self.sched.submit(key, spec["placement_resources"], strat, aff, soft, pg, bidx, deps)
+
+    def _actor_placed(self, actor_id, node, gpu_ids, amounts):
+        a = self.actors.get(actor_id)
+        if a is None or a.state == ACTOR_DEAD:
+            self.sched.release(node, a.spec["placement_resources"] if a else {}, gpu_ids, amounts)
+            return
+        # Keep only the lifetime resources; return the scheduling-only part.
+        pres, lres = a.spec["placement_resources"], a.spec["resources"]
+        extra = {k: v - lres.get(k, 0.0) for k, v in pres.items() if v - lres.get(k, 0.0) > 0}
+        if extra:
+            self.sched.release(node, extra, [], [])
+        if not lres.get("GPU"):
+            gpu_ids, amounts = [], []
+        a.node = node
+        a.assign = (node, gpu_ids, amounts)
+        w = self._start_worker(node, (a.spec.get("env_key", ""), "actor"), gpu_ids if gpu_ids else None,
+                               actor_id=actor_id, runtime_env=a.spec.get("runtime_env"))
+        a.worker = w
+        a.pid = w.pid
+
+    def _actor_ready(self, c: Conn, actor_id, address):
+        a = self.actors.get(actor_id)
+        if a is None:
+            return
+        a.state = ACTOR_ALIVE
+        a.address = address
+        for wc, rid in a.waiters:
+            self._reply(wc, rid, ("alive", address, a.num_restarts))
+        a.waiters.clear()
+
+    def _actor_failed_init(self, c: Conn, actor_id, err_blob):
+        a = self.actors.get(actor_id)
+        if a is None:
+            return
+        a.restarts_left = 0
+        a.death_cause = err_blob
+        self._kill_actor(actor_id, True, err_blob)
+
+    def _wait_actor(self, c: Conn, req_id, actor_id):
+        a = self.actors.get(actor_id)
+        if a is None:
+            self._reply(c, req_id, ("dead", "actor not found", 0))
+        elif a.state == ACTOR_ALIVE:
+            self._reply(c, req_id, ("alive", a.address, a.num_restarts))
+        elif a.state == ACTOR_DEAD:
+            self._reply(c, req_id, ("dead", a.death_cause, a.num_restarts))
+        else:
+            a.waiters.append((c, req_id))
+
+    def _get_actor(self, c: Conn, req_id, name, namespace):
+        aid = self.named_actors.get((namespace, name))
+        if aid is None or self.actors[aid].state == ACTOR_DEAD:
+            self._reply(c, req_id, None)
+        else:
+            self._reply(c, req_id, self.actors[aid].spec)
+
+    def _actor_died(self, a: ActorRec):
+        if a.assign is not None:
+            node, gpu_ids, amounts = a.assign
+            self.sched.release(node, a.spec["resources"], gpu_ids, amounts)
+            a.assign = None
+        a.worker = None
+        a.address = None
+        if a.state != ACTOR_DEAD and a.restarts_left != 0:
+            if a.restarts_left > 0:
+                a.restarts_left -= 1
+            a.num_restarts += 1
+            a.state = ACTOR_RESTARTING
+            self._schedule_actor(a)
+            return
+        self._mark_actor_dead(a, a.death_cause or "The actor process died unexpectedly.")
+
+    def _mark_actor_dead(self, a: ActorRec, cause):
+        a.state = ACTOR_DEAD
+        a.death_cause = cause
+        for wc, rid in a.waiters:
+            self._reply(wc, rid, ("dead", cause, a.num_restarts))
+        a.waiters.clear()
+        if a.name and self.named_actors.get((a.namespace, a.name)) == a.actor_id:
+            del self.named_actors[(a.namespace, a.name)]
+        refs = a.spec.get("arg_refs", [])
+        if refs:
+            a.spec["arg_refs"] = []
+            self._ref_deltas([(r, -1) for r in refs])
+
+    def _kill_actor(self, actor_id, no_restart, cause):
+        a = self.actors.get(actor_id)
+        if a is None or a.state == ACTOR_DEAD:
+            return
+        if no_restart:
+            a.restarts_left = 0
+        if isinstance(cause, str):
+            a.death_cause = a.death_cause or cause
+        if a.task_key is not None and a.state in (ACTOR_PENDING, ACTOR_RESTARTING) and a.worker is None:
+            if self.sched.cancel(a.task_key):
+                self.task_keys.pop(a.task_key, None)
+        w = a.worker
+        if w is not None:
+            self._kill_worker(w)
+            if no_restart:
+                # resources are released when the process exit is observed
+                pass
+        else:
+            if a.restarts_left == 0:
+                self._mark_actor_dead(a, a.death_cause)
+
+    def _actor_out_of_scope(self, actor_id):
+        a = self.actors.get(actor_id)
+        if a is None or a.detached or a.name or a.state == ACTOR_DEAD:
+            return
+        a.restarts_left = 0
+        self._kill_actor(actor_id, True, "All references to the actor were removed.")
+
+    # ------------------------------------------------------------------ placement groups
+    def _pg_create(self, c, req_id, info):
+        pg_id = info["pg_id"]
+        name = info.get("name")
+        if name:
+            key = (info.get("namespace"), name)
+            if key in self.named_pgs:
+                self._reply(c, req_id, ("exists", None))
+                return
+            self.named_pgs[key] = pg_id
+        pg = PGRec(pg_id, info["bundles"], info["strategy"], name, info.get("lifetime"), info.get("job_id"))
+        self.pgs[pg_id] = pg
+        strat = {"PACK": 0, "SPREAD": 1, "STRICT_PACK": 2, "STRICT_SPREAD": 3}[info["strategy"]]
+        self.sched.create_placement_group(pg_id.hex(), info["bundles"], strat)
+        self._reply(c, req_id, ("ok", None))
+
+    def _pg_placed(self, pg_id):
+        pg = self.pgs.get(pg_id)
+        if pg is None:
+            return
+        pg.state = "CREATED"
+        pg.nodes = self.sched.placement_group_nodes(pg_id.hex())
+        for wc, rid in pg.waiters:
+            self._reply(wc, rid, True)
+        pg.waiters.clear()
+
+    def _pg_wait(self, c, req_id, pg_id):
+        pg = self.pgs.get(pg_id)
+        if pg is None or pg.state == "REMOVED":
+            self._reply(c, req_id, False)
+        elif pg.state == "CREATED":
+            self._reply(c, req_id, True)
+        else:
+            pg.waiters.append((c, req_id))
+
+    def _pg_remove(self, pg_id):
+        pg = self.pgs.get(pg_id)
+        if pg is None:
+            return
+        # kill actors / fail tasks using the group
+        for a in list(self.actors.values()):
+            st = a.spec.get("strategy") or {}
+            if st.get("type") == "PLACEMENT_GROUP" and st.get("pg_id") == pg_id and a.state != ACTOR_DEAD:
+                a.restarts_left = 0
+                self._kill_actor(a.actor_id, True, "The placement group was removed.")
+        for t in list(self.tasks.values()):
+            st = t.spec.get("strategy") or {}
+            if st.get("type") == "PLACEMENT_GROUP" and st.get("pg_id") == pg_id:
+                if t.state == PENDING:
+                    t.cancelled = True
+                    key = t.spec.get("_key")
+                    if key is not None and self.sched.cancel(key):
+                        self.task_keys.pop(key, None)
+                    self._fail_task(t, exc.TaskPlacementGroupRemoved("placement group was removed"), FAILED)
+                elif t.worker is not None:
+                    self._kill_worker(t.worker)
+        self.sched.remove_placement_group(pg_id.hex())
+        pg.state = "REMOVED"
+        for wc, rid in pg.waiters:
+            self._reply(wc, rid, False)
+        pg.waiters.clear()
+        if pg.name:
+            self.named_pgs = {k: v for k, v in self.named_pgs.items() if v != pg_id}
+
+    def _pg_table(self, pg_id):
+        def info(pg):
+            return {"placement_group_id": pg.pg_id.hex(), "name": pg.name or "", "bundles": dict(enumerate(pg.bundles)),
+                    "strategy": pg.strategy, "state": pg.state, "bundles_to_node_id": pg.nodes}
+        if pg_id is None:
+            return {pg.pg_id.hex(): info(pg) for pg in self.pgs.values()}
+        if isinstance(pg_id, tuple):  # lookup by name
+            pid = self.named_pgs.get(pg_id)
+            return info(self.pgs[pid]) if pid else None
+        pg = self.pgs.get(pg_id)
+        return info(pg) if pg else None
+
+    # ------------------------------------------------------------------ state API
+    def _state(self, what, arg):
+        if what == "cluster_resources":
+            return self.sched.cluster_total()
+        if what == "available_resources":
+            return self.sched.cluster_available()
+        if what == "nodes":
+            out = []
+            for nid, n in self.nodes.items():
+                out.append({"NodeID": nid, "Alive": n["alive"], "Resources": self.sched.total(nid) if n["alive"] else {},
+                            "Available": self.sched.available(nid) if n["alive"] else {}, "IsHead": n["is_head"],
+                            "NodeManagerAddress": "127.0.0.1", "ObjectStoreSocketName": self.store_name,
+                            "alive": n["alive"]})
+            return out
+        if what == "actors":
+            return [{"actor_id": a.actor_id.hex(), "class_name": a.spec.get("class_name"), "state": a.state,
+                     "name": a.name or "", "namespace": a.namespace, "pid": a.pid, "node_id": a.node,
+                     "num_restarts": a.num_restarts, "death_cause": a.death_cause if isinstance(a.death_cause, str) else None,
+                     "job_id": a.job_id.hex() if a.job_id else None, "lifetime": "detached" if a.detached else "non_detached"}
+                    for a in self.actors.values()]
+        if what == "tasks":
+            out = []
+            for coll in (self.tasks, self.finished_tasks):
+                for tid, t in coll.items():
+                    out.append({"task_id": tid.hex(), "name": t.spec.get("name"), "state": t.state,
+                                "func_or_class_name": t.spec.get("name"), "node_id": t.node, "attempt": t.attempt,
+                                "start_time": t.start_time, "end_time": t.end_time, "required_resources": t.spec["resources"],
+                                "worker_pid": t.worker.pid if t.worker else None})
+            return out
+        if what == "workers":
+            return [{"worker_id": w.worker_id.hex(), "pid": w.pid, "state": w.state, "node_id": w.node,
+                     "actor_id": w.actor_id.hex() if w.actor_id else None, "tasks_run": w.tasks_run}
+                    for w in self.workers.values()]
+        if what == "objects":
+            objs = self.store.list_objects()
+            for o in objs:
+                o["object_id"] = o["object_id"].hex()
+                o["reference_count"] = self.refcounts.get(bytes.fromhex(o["object_id"]), 0)
+            return objs
+        if what == "store_stats":
+            return self.store.stats()
+        if what == "jobs":
+            return [{k: v for k, v in j.items() if k != "conn"} for j in self.jobs.values()]
+        if what == "placement_groups":
+            return self._pg_table(None)
+        if what == "refcounts":
+            return dict(self.refcounts)
+        if what == "timeline":
+            return list(self.events)
+        if what == "summary":
+            return {"pending_tasks": sum(1 for t in self.tasks.values() if t.state == PENDING),
+                    "running_tasks": sum(1 for t in self.tasks.values() if t.state == RUNNING),
+                    "workers": len(self.workers), "actors": len(self.actors),
+                    "infeasible": len(self.sched.infeasible_tasks())}
+        if what == "memory":
+            return self.memory_monitor.snapshot() if self.memory_monitor else {}
+        raise ValueError(f"unknown state query {what}")
+
+    # ------------------------------------------------------------------ housekeeping
+    def _housekeeping(self):
+        now = time.time()
+        # reap dead worker processes that never connected / crashed
+        for w in list(self.workers.values()):
+            if w.proc is not None and w.proc.poll() is not None:
+                if w.conn is None or not w.conn.alive or w.state == "DEAD":
+                    self._worker_died(w)
+        # threshold-driven spilling
+        st = self.store.stats()
+        cap = st["capacity"]
+        if cap and st["bytes_in_use"] > self.spill_threshold * cap:
+            excess = st["bytes_in_use"] - int(self.spill_threshold * cap)
+            threading.Thread(target=self.store.spill, args=(excess,), daemon=True).start()
+        # idle worker reaping (keep prestart pool)
+        idle_total = sum(len(v) for v in self.idle.values())
+        if idle_total > self.prestart:
+            for key, lst in self.idle.items():
+                for w in list(lst):
+                    if idle_total <= self.prestart:
+                        break
+                    if now - w.idle_since > self.idle_timeout and w.state == "IDLE":
+                        lst.remove(w)
+                        self._send_nb(w.conn, (P.EXIT,))
+                        w.state = "DEAD"
+                        idle_total -= 1
+        # memory monitor: kill the newest retriable task worker when the node is nearly OOM
+        if self.memory_monitor is not None:
+            victim = self.memory_monitor.pick_victim(self)
+            if victim is not None:
+                t = self.tasks.get(victim.task) if victim.task else None
+                if t is not None:
+                    t.error = "oom"
+                self._kill_worker(victim)
+
+    def _shutdown(self):
+        for w in list(self.workers.values()):
+            if w.conn is not None and w.conn.alive:
+                try:
+                    self._send_nb(w.conn, (P.EXIT,))
+                except Exception:
+                    pass
+        deadline = time.time() + 1.0
+        for w in list(self.workers.values()):
+            if w.proc is not None:
+                try:
+                    w.proc.wait(timeout=max(0.0, deadline - time.time()))
+                except Exception:
+                    pass
+                if w.proc.poll() is None:
+                    try:
+                        w.proc.kill()
+                    except OSError:
+                        pass
+        try:
+            os.unlink(self.sock_path)
+        except OSError:
+            pass
+        del self.store
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--session-dir", required=True)
+    ap.add_argument("--store-name", required=True)
+    ap.add_argument("--object-store-memory", required=True)
+    ap.add_argument("--resources", required=True)
+    ap.add_argument("--config", default="")
+    ap.add_argument("--persistent", action="store_true")
+    args = ap.parse_args()
+    os.makedirs(os.path.join(args.session_dir, "logs"), exist_ok=True)
+    os.makedirs(os.path.join(args.session_dir, "sockets"), exist_ok=True)
+    signal.signal(signal.SIGTERM, lambda *a: sys.exit(0))
+    h = Head(args)
+    try:
+        h.serve()
+    finally:
+        h.running = False
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+"""Object serialization into the shared-memory store.
+
+Parity: reference python/ray/_private/serialization.py (pickle5 out-of-band buffers, ObjectRef
+tracking, error objects). Values are pickled with protocol 5; large contiguous buffers (numpy
+arrays, CPU torch tensors, bytes-likes) go out-of-band and are copied once into the shm arena
+(parallel memcpy), so ``get`` returns zero-copy, read-only arrays backed by the arena.
+
+CUDA(ROCm) tensors inside a value are moved through host memory by default (like the
+reference); a top-level ``put(cuda_tensor)`` instead goes to the HBM GPU object store
+(``gpu_object_store.py``) and stays on the device.
+"""
+from __future__ import annotations
+
+import io
+import pickle
+import threading
+from typing import Any, List, Tuple
+
+import cloudpickle
+
+TAG_PICKLE = 1
+TAG_ERROR = 2
+TAG_GPU = 3
+TAG_RAW = 4
+
+INLINE_THRESHOLD = 100 * 1024  # args smaller than this are inlined into the task spec
+
+_tls = threading.local()
+
+
+def _contained():
+    c = getattr(_tls, "contained", None)
+    return c
+
+
+class _Pickler(cloudpickle.CloudPickler):
+    def reducer_override(self, obj):
+        t = type(obj)
+        mod = t.__module__
+        if mod == "torch" and t.__name__ in ("Tensor", "Parameter"):
+            try:
+                import torch
+
+                if isinstance(obj, torch.Tensor) and obj.is_cuda:
+                    return _rebuild_cuda_tensor, (obj.detach().cpu(), obj.device.index, obj.requires_grad)
+            except Exception:
+                pass
+        return super().reducer_override(obj)
+
+
+def _rebuild_cuda_tensor(cpu_tensor, device_index, requires_grad):
+    import torch
+
+    if torch.cuda.is_available():
+        idx = device_index if device_index is not None and device_index < torch.cuda.device_count() else 0
+        t = cpu_tensor.to(f"cuda:{idx}")
+    else:
+        t = cpu_tensor
+    if requires_grad:
+        t.requires_grad_(True)
+    return t
+
+
+def serialize(value: Any) -> Tuple[bytes, List[pickle.PickleBuffer], List[bytes]]:
+    """Returns (pickle_bytes, out_of_band_buffers, contained_object_ids)."""
+    prev = getattr(_tls, "contained", None)
+    _tls.contained = []
+    buffers: List[pickle.PickleBuffer] = []
+    try:
+        f = io.BytesIO()
+        p = _Pickler(f, protocol=5, buffer_callback=buffers.append)
+        p.dump(value)
+        data = f.getvalue()
+        contained = _tls.contained
+    finally:
+        _tls.contained = prev
+    # PickleBuffers that are not contiguous must be materialised
+    out = []
+    for b in buffers:
+        try:
+            out.append(b.raw())
+        except BufferError:
+            out.append(memoryview(bytes(b)))
+    return data, out, contained
+
+
+def note_contained(oid: bytes):
+    c = getattr(_tls, "contained", None)
+    if c is not None:
+        c.append(oid)
+
+
+def deserialize(data, buffers) -> Any:
+    return pickle.loads(data, buffers=buffers)
+
+
+def dumps_inline(value: Any) -> Tuple[bytes, List[bytes]]:
+    """In-band pickle for small task args (buffers are inlined)."""
+    prev = getattr(_tls, "contained", None)
+    _tls.contained = []
+    try:
+        f = io.BytesIO()
+        _Pickler(f, protocol=5).dump(value)
+        return f.getvalue(), _tls.contained
+    finally:
+        _tls.contained = prev
+
+
+def loads_inline(data: bytes) -> Any:
+    return pickle.loads(data)

@@ -1,0 +1,863 @@
+"""Core worker (one per process: driver or worker) and the public core API.
+
+Parity: reference python/ray/_private/worker.py (init/get/put/wait/remote/kill/cancel/shutdown,
+get_gpu_ids) and src/ray/core_worker/core_worker.cc (task submission, reference counting,
+direct actor transport, dependency handling for `get`).
+"""
+from __future__ import annotations
+
+import atexit
+import collections
+import ctypes
+import hashlib
+import json
+import logging
+import os
+import queue
+import socket
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+import traceback
+import uuid
+from typing import Any, Dict, List, Optional, Sequence
+
+import cloudpickle
+
+from ray_memory_management_amd import exceptions as exc
+from ray_memory_management_amd._native import store_ext
+from ray_memory_management_amd._private import ids as _ids
+from ray_memory_management_amd._private import protocol as P
+from ray_memory_management_amd._private import serialization as ser
+from ray_memory_management_amd.object_ref import ObjectRef, _set_worker
+
+logger = logging.getLogger("ray_memory_management_amd")
+
+SCRIPT_MODE = 0
+WORKER_MODE = 1
+LOCAL_MODE = 2
+SPILL_WORKER_MODE = 3
+RESTORE_WORKER_MODE = 4
+
+global_worker: Optional["CoreWorker"] = None
+_init_lock = threading.RLock()
+
+
+class _Pending:
+    __slots__ = ("ev", "value")
+
+    def __init__(self):
+        self.ev = threading.Event()
+        self.value = None
+
+
+class ActorConn:
+    """Direct caller→actor connection with in-flight tracking (direct actor transport)."""
+
+    def __init__(self, worker: "CoreWorker", actor_id: bytes, max_task_retries: int):
+        self.worker = worker
+        self.actor_id = actor_id
+        self.max_task_retries = max_task_retries
+        self.lock = threading.Lock()
+        self.sock: Optional[socket.socket] = None
+        self.seq = 0
+        self.inflight: Dict[int, tuple] = {}
+        self.dead_error: Optional[BaseException] = None
+        self.epoch = -1
+        self.connected = threading.Event()
+        self.connecting = False
+
+    def _connect(self):
+        status = self.worker.request(lambda rid: (P.WAIT_ACTOR, rid, self.actor_id))
+        kind, addr, restarts = status
+        if kind == "dead":
+            cause = addr
+            if isinstance(cause, (bytes, bytearray)):
+                try:
+                    cause = ser.loads_inline(cause)
+                except Exception:
+                    cause = None
+            if isinstance(cause, BaseException):
+                self.dead_error = exc.RayActorError(self.actor_id.hex(),
+                                                    f"The actor died because of an error raised in its creation task: {cause}")
+                self.dead_error.__cause__ = cause
+            else:
+                self.dead_error = exc.RayActorError(self.actor_id.hex(), f"The actor is dead: {cause}")
+            return False
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(addr)
+        P.send(s, (P.ACTOR_HELLO, os.getpid()))
+        self.sock = s
+        self.epoch = restarts
+        threading.Thread(target=self._reader, args=(s,), daemon=True).start()
+        return True
+
+    def submit(self, spec, keep_alive):
+        with self.lock:
+            if self.dead_error is not None:
+                self.worker._store_errors(spec["return_ids"], self.dead_error)
+                return
+            if self.sock is None:
+                if not self._connect():
+                    self.worker._store_errors(spec["return_ids"], self.dead_error)
+                    return
+            self.seq += 1
+            spec["seq"] = self.seq
+            self.inflight[self.seq] = (spec, keep_alive, 0)
+            try:
+                P.send(self.sock, (P.ACTOR_TASK, spec))
+            except OSError:
+                pass  # the reader thread observes the failure and handles in-flight tasks
+
+    def _reader(self, s: socket.socket):
+        try:
+            while True:
+                m = P.recv(s)
+                if m[0] == P.REPLY:  # ack batch: list of seq
+                    with self.lock:
+                        for sq in m[2]:
+                            self.inflight.pop(sq, None)
+        except (ConnectionError, OSError, EOFError):
+            pass
+        self._on_disconnect(s)
+
+    def _on_disconnect(self, s):
+        with self.lock:
+            if self.sock is not s:
+                return
+            self.sock = None
+            pending = sorted(self.inflight.items())
+            self.inflight.clear()
+            retry = []
+            for sq, (spec, keep, tries) in pending:
+                if self.max_task_retries != 0 and (self.max_task_retries < 0 or tries < self.max_task_retries):
+                    retry.append((spec, keep, tries + 1))
+                else:
+                    self.worker._store_errors(spec["return_ids"], exc.RayActorError(
+                        self.actor_id.hex(), "The actor died unexpectedly before finishing this task."))
+            if retry:
+                if not self._connect():
+                    for spec, keep, tries in retry:
+                        self.worker._store_errors(spec["return_ids"], self.dead_error)
+                    return
+                for spec, keep, tries in retry:
+                    self.seq += 1
+                    spec["seq"] = self.seq
+                    self.inflight[self.seq] = (spec, keep, tries)
+                    try:
+                        P.send(self.sock, (P.ACTOR_TASK, spec))
+                    except OSError:
+                        break
+
+    def close(self):
+        with self.lock:
+            if self.sock is not None:
+                try:
+                    self.sock.close()
+                except OSError:
+                    pass
+
+
+class CoreWorker:
+    def __init__(self, mode, head_socket, store_name, session_dir, job_id=None, namespace=None,
+                 worker_id=None, node_id=1):
+        self.mode = mode
+        self.session_dir = session_dir
+        self.head_socket = head_socket
+        self.store_name = store_name
+        self.store = store_ext().ObjectStore.attach(store_name)
+        self.worker_id = worker_id or os.urandom(16)
+        self.job_id = job_id or os.urandom(4)
+        self.namespace = namespace
+        self.node_id = node_id
+        self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.sock.connect(head_socket)
+        self.send_lock = threading.Lock()
+        self.req_lock = threading.Lock()
+        self.reqs: Dict[int, _Pending] = {}
+        self.req_counter = 0
+        self.task_queue: "queue.Queue" = queue.Queue()
+        self.ref_lock = threading.Lock()
+        self.local_refs: Dict[bytes, int] = {}
+        self.deltas: Dict[bytes, int] = {}
+        self.exported = set()
+        self.actor_conns: Dict[bytes, ActorConn] = {}
+        self.connected = True
+        self.current_task_id: Optional[bytes] = None
+        self.current_actor_id: Optional[bytes] = None
+        self.current_task_name = None
+        self.gpu_ids: List[int] = [int(x) for x in os.environ.get("RMM_GPU_IDS", "").split(",") if x != ""]
+        self.blocked = False
+        self.events: List[dict] = []
+        self.events_lock = threading.Lock()
+        self.gpu_store = None
+        self.config: Dict[str, Any] = json.loads(os.environ.get("RMM_CONFIG", "{}") or "{}")
+        self.placement_group_capture = None  # (pg, capture_child_tasks)
+        self.actor_handle_for_self = None
+        self._reader_t = threading.Thread(target=self._reader, daemon=True, name="rmm-reader")
+        self._reader_t.start()
+        self._flusher_stop = threading.Event()
+        self._flusher = threading.Thread(target=self._flush_loop, daemon=True, name="rmm-flusher")
+        self._flusher.start()
+
+    # ------------------------------------------------------------------ head connection
+    def _reader(self):
+        try:
+            while True:
+                m = P.recv(self.sock)
+                t = m[0]
+                if t == P.REPLY:
+                    p = self.reqs.pop(m[1], None)
+                    if p is not None:
+                        p.value = m[2]
+                        p.ev.set()
+                elif t == P.CANCEL_TASK:
+                    self._cancel_current(m[1])
+                elif t == P.FREE_GPU:
+                    self._free_gpu(m[1])
+                else:
+                    self.task_queue.put(m)
+        except (ConnectionError, OSError, EOFError):
+            pass
+        self.connected = False
+        for p in list(self.reqs.values()):
+            p.value = exc.LocalRayletDiedError()
+            p.ev.set()
+        self.task_queue.put((P.EXIT,))
+
+    def _flush_loop(self):
+        while not self._flusher_stop.wait(0.01):
+            if self.deltas:
+                try:
+                    self.send(None)
+                except Exception:
+                    pass
+
+    def _take_deltas(self):
+        with self.ref_lock:
+            if not self.deltas:
+                return None
+            d = [(k, v) for k, v in self.deltas.items() if v]
+            self.deltas = {}
+        return d
+
+    def send(self, msg):
+        if not self.connected:
+            if msg is None:
+                return
+            raise exc.LocalRayletDiedError()
+        with self.send_lock:
+            d = self._take_deltas()
+            try:
+                if d:
+                    P.send(self.sock, (P.REF_DELTAS, d))
+                if msg is not None:
+                    P.send(self.sock, msg)
+            except OSError:
+                self.connected = False
+                if msg is not None:
+                    raise exc.LocalRayletDiedError()
+
+    def request(self, build, timeout=None):
+        p = _Pending()
+        with self.req_lock:
+            self.req_counter += 1
+            rid = self.req_counter
+            self.reqs[rid] = p
+        self.send(build(rid))
+        if not p.ev.wait(timeout):
+            self.reqs.pop(rid, None)
+            raise exc.GetTimeoutError("request to the head timed out")
+        if isinstance(p.value, exc.LocalRayletDiedError):
+            raise p.value
+        return p.value
+
+    # ------------------------------------------------------------------ reference counting
+    def add_local_ref(self, oid: bytes):
+        with self.ref_lock:
+            n = self.local_refs.get(oid, 0)
+            self.local_refs[oid] = n + 1
+            if n == 0:
+                self.deltas[oid] = self.deltas.get(oid, 0) + 1
+
+    def remove_local_ref(self, oid: bytes):
+        with self.ref_lock:
+            n = self.local_refs.get(oid, 0) - 1
+            if n <= 0:
+                self.local_refs.pop(oid, None)
+                self.deltas[oid] = self.deltas.get(oid, 0) - 1
+            else:
+                self.local_refs[oid] = n
+
+    # ------------------------------------------------------------------ objects
+    def put_object(self, value, oid: Optional[bytes] = None, _owner=None) -> ObjectRef:
+        if isinstance(value, ObjectRef):
+            raise TypeError("Calling 'put' on an ObjectRef is not allowed. If you really want to do this, "
+                            "you can wrap the ObjectRef in a list and call 'put' on it.")
+        oid = oid or _ids.new_put_id()
+        ref = None
+        if _is_cuda_tensor(value) and self.config.get("gpu_object_store", True):
+            from ray_memory_management_amd._private import gpu_object_store as gos
+
+            ref = ObjectRef(oid)
+            gos.put_tensor(self, oid, value)
+            self.send((P.GPU_OBJECT, oid))
+            return ref
+        data, bufs, contained = ser.serialize(value)
+        ref = ObjectRef(oid)
+        if contained:
+            self.send((P.CONTAINED, oid, contained))
+        try:
+            self.store.put_serialized(oid, data, bufs, ser.TAG_PICKLE, False)
+        except RuntimeError as e:
+            if "ObjectStoreFullError" in str(e):
+                raise exc.ObjectStoreFullError(str(e)) from None
+            raise
+        return ref
+
+    def _store_errors(self, return_ids, error):
+        data, bufs, _ = ser.serialize(error)
+        for oid in return_ids:
+            try:
+                if not self.store.contains(oid):
+                    self.store.put_serialized(oid, data, bufs, ser.TAG_ERROR, True)
+            except Exception:
+                pass
+
+    def _deserialize_entry(self, oid, r):
+        pickled, bufs, tag, is_error, raw = r
+        if tag == ser.TAG_GPU:
+            from ray_memory_management_amd._private import gpu_object_store as gos
+
+            return gos.get_tensor(self, oid, pickled), False
+        value = ser.deserialize(pickled, bufs)
+        return value, is_error
+
+    def _set_blocked(self, blocked: bool):
+        if self.mode == WORKER_MODE and self.current_task_id is not None and self.current_actor_id is None:
+            if self.blocked != blocked:
+                self.blocked = blocked
+                try:
+                    self.send((P.BLOCKED if blocked else P.UNBLOCKED,))
+                except Exception:
+                    pass
+
+    def get(self, refs: Sequence[ObjectRef], timeout: Optional[float] = None):
+        deadline = None if timeout is None else time.time() + timeout
+        out = []
+        blocked = False
+        try:
+            for ref in refs:
+                if not isinstance(ref, ObjectRef):
+                    raise TypeError(f"get() expects ObjectRefs, got {type(ref)}")
+                oid = ref.binary()
+                r = self.store.get_serialized(oid, 0)
+                while r is None:
+                    if not blocked:
+                        blocked = True
+                        self._set_blocked(True)
+                    if not self.connected:
+                        raise exc.LocalRayletDiedError()
+                    if deadline is not None:
+                        rem = deadline - time.time()
+                        if rem <= 0:
+                            raise exc.GetTimeoutError(f"Get timed out: some object(s) not ready: {ref}")
+                        slice_ms = int(min(rem, 1.0) * 1000) or 1
+                    else:
+                        slice_ms = 1000
+                    r = self.store.get_serialized(oid, slice_ms)
+                value, is_error = self._deserialize_entry(oid, r)
+                if is_error:
+                    if isinstance(value, exc.RayTaskError):
+                        raise value.as_instanceof_cause()
+                    if isinstance(value, BaseException):
+                        raise value
+                out.append(value)
+        finally:
+            if blocked:
+                self._set_blocked(False)
+        return out
+
+    def wait(self, refs, num_returns=1, timeout=None, fetch_local=True):
+        if not refs:
+            return [], []
+        oids = [r.binary() for r in refs]
+        blocked = False
+        tm = -1 if timeout is None else int(timeout * 1000)
+        try:
+            ready_mask = self.store.wait(oids, num_returns, 0)
+            if sum(ready_mask) < num_returns and tm != 0:
+                blocked = True
+                self._set_blocked(True)
+                ready_mask = self.store.wait(oids, num_returns, tm)
+        finally:
+            if blocked:
+                self._set_blocked(False)
+        ready, not_ready = [], []
+        for r, ok in zip(refs, ready_mask):
+            if ok and len(ready) < num_returns:
+                ready.append(r)
+            else:
+                not_ready.append(r)
+        return ready, not_ready
+
+    # ------------------------------------------------------------------ submission
+    def export(self, fid: bytes, blob: bytes) -> Optional[bytes]:
+        if fid in self.exported:
+            return None
+        self.exported.add(fid)
+        return blob
+
+    def prepare_args(self, args, kwargs):
+        """Returns (encoded_args, encoded_kwargs, arg_refs, keep_alive)."""
+        arg_refs: List[bytes] = []
+        keep: List[Any] = []
+
+        def enc(v):
+            if isinstance(v, ObjectRef):
+                arg_refs.append(v.binary())
+                keep.append(v)
+                return ("r", v.binary())
+            data, contained = ser.dumps_inline(v)
+            if len(data) > ser.INLINE_THRESHOLD:
+                ref = self.put_object(v)
+                keep.append(ref)
+                arg_refs.append(ref.binary())
+                return ("r", ref.binary())
+            if contained:
+                arg_refs.extend(contained)
+            return ("v", data)
+
+        ea = [enc(a) for a in args]
+        ek = {k: enc(v) for k, v in kwargs.items()}
+        return ea, ek, arg_refs, keep
+
+    def submit_task(self, spec: dict, keep) -> List[ObjectRef]:
+        task_id = _ids.new_task_id()
+        spec["task_id"] = task_id
+        nr = spec.get("num_returns", 1)
+        n = nr if isinstance(nr, int) else 1
+        ret_ids = [_ids.object_id_for_return(task_id, i) for i in range(1, n + 1)]
+        refs = [ObjectRef(o) for o in ret_ids]
+        spec["return_ids"] = ret_ids
+        spec["job_id"] = self.job_id
+        spec["parent_task_id"] = self.current_task_id
+        self.send((P.SUBMIT_TASK, spec))
+        return refs
+
+    def submit_actor_task(self, actor_id: bytes, spec: dict, keep, max_task_retries: int) -> List[ObjectRef]:
+        task_id = _ids.new_task_id()
+        spec["task_id"] = task_id
+        nr = spec.get("num_returns", 1)
+        n = nr if isinstance(nr, int) else 1
+        ret_ids = [_ids.object_id_for_return(task_id, i) for i in range(1, n + 1)]
+        refs = [ObjectRef(o) for o in ret_ids]
+        spec["return_ids"] = ret_ids
+        conn = self.actor_conns.get(actor_id)
+        if conn is None:
+            conn = self.actor_conns.setdefault(actor_id, ActorConn(self, actor_id, max_task_retries))
+        # flush ref deltas first so the actor never sees a ref the head does not know about
+        self.send(None)
+        conn.submit(spec, keep)
+        return refs
+
+    # ------------------------------------------------------------------ cancellation / gpu
+    def _cancel_current(self, task_id):
+        if self.current_task_id == task_id and self.main_thread_id is not None:
+            ctypes.pythonapi.PyThreadState_SetAsyncExc(ctypes.c_ulong(self.main_thread_id),
+                                                       ctypes.py_object(exc.TaskCancelledError))
+
+    main_thread_id = None
+
+    def _free_gpu(self, oids):
+        from ray_memory_management_amd._private import gpu_object_store as gos
+
+        for o in oids:
+            gos.free(self, o)
+
+    def record_event(self, ev: dict):
+        with self.events_lock:
+            self.events.append(ev)
+            if len(self.events) >= 256:
+                evs, self.events = self.events, []
+                try:
+                    self.send((P.EVENTS, evs))
+                except Exception:
+                    pass
+
+    def flush_events(self):
+        with self.events_lock:
+            evs, self.events = self.events, []
+        if evs:
+            try:
+                self.send((P.EVENTS, evs))
+            except Exception:
+                pass
+
+    def shutdown(self):
+        self._flusher_stop.set()
+        try:
+            self.flush_events()
+            self.send(None)
+        except Exception:
+            pass
+        for c in self.actor_conns.values():
+            c.close()
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
+def _is_cuda_tensor(v) -> bool:
+    t = type(v)
+    if t.__module__ != "torch" or t.__name__ not in ("Tensor", "Parameter"):
+        return False
+    try:
+        return v.is_cuda
+    except Exception:
+        return False
+
+
+# ====================================================================== driver bootstrap
+
+_head_proc: Optional[subprocess.Popen] = None
+_session_dir: Optional[str] = None
+_local_mode = False
+
+
+def _detect_gpus() -> int:
+    """Count GPUs from the KFD topology without initialising HIP in this process."""
+    env = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for d in os.listdir(base):
+            try:
+                with open(os.path.join(base, d, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+                if int(props.get("simd_count", "0")) > 0:
+                    n += 1
+            except OSError:
+                continue
+    except OSError:
+        return 0
+    if env is not None and env != "":
+        n = min(n, len([x for x in env.split(",") if x != ""]))
+    return n
+
+
+def _default_store_size() -> int:
+    try:
+        import psutil
+
+        total = psutil.virtual_memory().available
+    except Exception:
+        total = 8 << 30
+    size = int(total * 0.3)
+    try:
+        st = os.statvfs("/dev/shm")
+        shm_free = st.f_bavail * st.f_frsize
+        size = min(size, int(shm_free * 0.9))
+    except OSError:
+        pass
+    return max(64 << 20, min(size, 200 << 30))
+
+
+def is_initialized() -> bool:
+    return global_worker is not None or _local_mode
+
+
+def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_gpus: Optional[int] = None,
+         resources: Optional[Dict[str, float]] = None, object_store_memory: Optional[int] = None,
+         local_mode: bool = False, ignore_reinit_error: bool = False, namespace: Optional[str] = None,
+         runtime_env: Optional[dict] = None, include_dashboard: Optional[bool] = None,
+         logging_level=logging.INFO, log_to_driver: bool = True, _system_config: Optional[dict] = None,
+         _temp_dir: Optional[str] = None, **kwargs):
+    """Start (or connect to) a local cluster. Parity: reference python/ray/_private/worker.py:init."""
+    global global_worker, _head_proc, _session_dir, _local_mode
+    with _init_lock:
+        if is_initialized():
+            if ignore_reinit_error:
+                return RayContext()
+            raise RuntimeError("Maybe you called ray.init twice by accident? This error can be suppressed by "
+                               "passing in 'ignore_reinit_error=True' or by calling 'ray.shutdown()' prior to 'ray.init()'.")
+        if local_mode:
+            from ray_memory_management_amd._private import local_mode as lm
+
+            lm.start(num_cpus=num_cpus, num_gpus=num_gpus, resources=resources)
+            _local_mode = True
+            return RayContext()
+        cfg = dict(_system_config or {})
+        if address in ("auto",) or (address and address.startswith("rmm://")):
+            sess = _find_session(address)
+            head_sock = os.path.join(sess, "sockets", "head.sock")
+            info = json.load(open(os.path.join(sess, "session.json")))
+            store_name = info["store_name"]
+            _session_dir = sess
+        else:
+            base = _temp_dir or os.path.join(tempfile.gettempdir(), "rmm")
+            os.makedirs(base, exist_ok=True)
+            sess = tempfile.mkdtemp(prefix=f"session_{time.strftime('%Y-%m-%d_%H-%M-%S')}_", dir=base)
+            for sub in ("logs", "sockets", "spill"):
+                os.makedirs(os.path.join(sess, sub), exist_ok=True)
+            res = dict(resources or {})
+            res["CPU"] = float(num_cpus if num_cpus is not None else (os.cpu_count() or 1))
+            ng = num_gpus if num_gpus is not None else _detect_gpus()
+            if ng:
+                res["GPU"] = float(ng)
+            osm = int(object_store_memory or _default_store_size())
+            try:
+                import psutil
+
+                res.setdefault("memory", float(int(psutil.virtual_memory().available * 0.7)))
+            except Exception:
+                pass
+            res["object_store_memory"] = float(osm)
+            store_name = f"/rmm-{uuid.uuid4().hex[:12]}"
+            head_sock = os.path.join(sess, "sockets", "head.sock")
+            env = dict(os.environ)
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+            cmd = [sys.executable, "-u", "-m", "ray_memory_management_amd._private.node", "--session-dir", sess,
+                   "--store-name", store_name, "--object-store-memory", str(osm), "--resources", json.dumps(res),
+                   "--config", json.dumps(cfg)]
+            if kwargs.get("_persistent"):
+                cmd.append("--persistent")
+            log = open(os.path.join(sess, "logs", "head.log"), "ab")
+            _head_proc = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL)
+            log.close()
+            ready = os.path.join(sess, "head.ready")
+            t0 = time.time()
+            while not os.path.exists(ready):
+                if _head_proc.poll() is not None:
+                    raise RuntimeError("head process failed to start:\n" +
+                                       open(os.path.join(sess, "logs", "head.log")).read()[-4000:])
+                if time.time() - t0 > 60:
+                    raise RuntimeError("timed out starting the head process")
+                time.sleep(0.005)
+            with open(os.path.join(sess, "session.json"), "w") as f:
+                json.dump({"store_name": store_name, "head_pid": _head_proc.pid}, f)
+            _session_dir = sess
+            with open(os.path.join(base, "latest_session"), "w") as f:
+                f.write(sess)
+        ns = namespace or f"anon-{uuid.uuid4().hex[:8]}"
+        w = CoreWorker(SCRIPT_MODE, head_sock, store_name, sess, namespace=ns)
+        w.main_thread_id = threading.main_thread().ident
+        info = w.request(lambda rid: (P.REGISTER, "driver", {"pid": os.getpid(), "job_id": w.job_id,
+                                                             "namespace": ns, "req_id": rid}))
+        w.config = info.get("config", {})
+        w.job_runtime_env = runtime_env
+        global_worker = w
+        _set_worker(w)
+        atexit.register(shutdown)
+        return RayContext()
+
+
+def _find_session(address):
+    if address and address.startswith("rmm://"):
+        return address[len("rmm://"):]
+    base = os.path.join(tempfile.gettempdir(), "rmm")
+    with open(os.path.join(base, "latest_session")) as f:
+        return f.read().strip()
+
+
+def shutdown(_exiting_interpreter: bool = False):
+    global global_worker, _head_proc, _local_mode
+    with _init_lock:
+        if _local_mode:
+            from ray_memory_management_amd._private import local_mode as lm
+
+            lm.stop()
+            _local_mode = False
+            return
+        w = global_worker
+        if w is None:
+            return
+        from ray_memory_management_amd._private import gpu_object_store as gos
+
+        gos.shutdown_process_store(w)
+        if _head_proc is not None:
+            try:
+                w.send((P.SHUTDOWN,))
+            except Exception:
+                pass
+        w.shutdown()
+        global_worker = None
+        _set_worker(None)
+        if _head_proc is not None:
+            try:
+                _head_proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                _head_proc.kill()
+                _head_proc.wait()
+            _head_proc = None
+
+
+class RayContext(dict):
+    def __init__(self):
+        super().__init__(session_dir=_session_dir, address=f"rmm://{_session_dir}" if _session_dir else None)
+        self.address_info = dict(self)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        shutdown()
+
+
+def _require_worker() -> CoreWorker:
+    if global_worker is None:
+        if _local_mode:
+            raise RuntimeError("local mode worker")
+        # auto-init like the reference
+        init()
+    return global_worker
+
+
+# ====================================================================== public API
+
+def put(value, *, _owner=None) -> ObjectRef:
+    if _local_mode:
+        from ray_memory_management_amd._private import local_mode as lm
+
+        return lm.put(value)
+    return _require_worker().put_object(value)
+
+
+def get(object_refs, *, timeout: Optional[float] = None):
+    if _local_mode:
+        from ray_memory_management_amd._private import local_mode as lm
+
+        return lm.get(object_refs, timeout)
+    w = _require_worker()
+    from ray_memory_management_amd.object_ref import ObjectRefGenerator
+
+    if isinstance(object_refs, ObjectRefGenerator):
+        object_refs = list(object_refs)
+    if isinstance(object_refs, ObjectRef):
+        return w.get([object_refs], timeout)[0]
+    if isinstance(object_refs, (list, tuple)):
+        return w.get(list(object_refs), timeout)
+    raise ValueError("'object_refs' must either be an ObjectRef or a list of ObjectRefs.")
+
+
+def wait(object_refs, *, num_returns: int = 1, timeout: Optional[float] = None, fetch_local: bool = True):
+    if _local_mode:
+        from ray_memory_management_amd._private import local_mode as lm
+
+        return lm.wait(object_refs, num_returns, timeout)
+    if isinstance(object_refs, ObjectRef):
+        raise TypeError("wait() expected a list of ObjectRef, got a single ObjectRef")
+    object_refs = list(object_refs)
+    if len(set(object_refs)) != len(object_refs):
+        raise ValueError("Wait requires a list of unique object refs.")
+    if num_returns <= 0:
+        raise ValueError("Invalid number of objects to return %d." % num_returns)
+    if num_returns > len(object_refs):
+        raise ValueError("num_returns cannot be greater than the number of objects provided.")
+    return _require_worker().wait(object_refs, num_returns, timeout, fetch_local)
+
+
+def kill(actor, *, no_restart: bool = True):
+    from ray_memory_management_amd.actor import ActorHandle
+
+    if not isinstance(actor, ActorHandle):
+        raise ValueError("ray.kill() only supported for actors. Got: {}.".format(type(actor)))
+    if _local_mode:
+        return
+    w = _require_worker()
+    w.send((P.KILL_ACTOR, actor._actor_id, no_restart))
+
+
+def cancel(object_ref: ObjectRef, *, force: bool = False, recursive: bool = True):
+    if not isinstance(object_ref, ObjectRef):
+        raise TypeError("ray.cancel() only supported for non-actor object refs.")
+    if _local_mode:
+        return
+    w = _require_worker()
+    w.send((P.CANCEL, object_ref.binary()[:16], force, recursive))
+
+
+def get_actor(name: str, namespace: Optional[str] = None):
+    from ray_memory_management_amd.actor import ActorHandle
+
+    if not name:
+        raise ValueError("Please supply a non-empty value to get_actor")
+    w = _require_worker()
+    ns = namespace if namespace is not None else w.namespace
+    spec = w.request(lambda rid: (P.GET_ACTOR, rid, name, ns))
+    if spec is None:
+        raise ValueError(f"Failed to look up actor with name '{name}'. This could because 1. You are trying to look "
+                         f"up a named actor you didn't create. 2. The named actor died. 3. You did not use a namespace "
+                         f"matching the namespace of the actor.")
+    return ActorHandle._from_spec(spec)
+
+
+def get_gpu_ids():
+    if _local_mode:
+        return []
+    w = _require_worker()
+    return list(w.gpu_ids)
+
+
+def remote(*args, **kwargs):
+    from ray_memory_management_amd.actor import make_actor_class
+    from ray_memory_management_amd.remote_function import RemoteFunction
+
+    def make(obj, opts):
+        import inspect
+
+        if inspect.isclass(obj):
+            return make_actor_class(obj, opts)
+        if callable(obj):
+            return RemoteFunction(obj, opts)
+        raise TypeError("The @remote decorator must be applied to either a function or a class.")
+
+    if len(args) == 1 and not kwargs and callable(args[0]):
+        return make(args[0], {})
+    if args:
+        raise TypeError("The @remote decorator must be applied either with no arguments and no parentheses, "
+                        "for example '@remote', or it must be applied using some of the arguments like "
+                        "'@remote(num_returns=2, resources={\"CustomResource\": 1})'.")
+    return lambda obj: make(obj, kwargs)
+
+
+def timeline(filename: Optional[str] = None):
+    """Chrome-trace events of task execution. Parity: reference python/ray/_private/state.py:timeline."""
+    w = _require_worker()
+    w.flush_events()
+    time.sleep(0.05)
+    evs = w.request(lambda rid: (P.STATE, rid, "timeline", None))
+    if filename:
+        with open(filename, "w") as f:
+            json.dump(evs, f)
+        return None
+    return evs
+
+
+def _state(what, arg=None):
+    w = _require_worker()
+    return w.request(lambda rid: (P.STATE, rid, what, arg))
+
+
+def cluster_resources():
+    if _local_mode:
+        from ray_memory_management_amd._private import local_mode as lm
+
+        return lm.resources()
+    return _state("cluster_resources")
+
+
+def available_resources():
+    if _local_mode:
+        from ray_memory_management_amd._private import local_mode as lm
+
+        return lm.resources()
+    return _state("available_resources")
+
+
+def nodes():
+    return _state("nodes")

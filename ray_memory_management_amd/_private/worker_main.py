@@ -1,0 +1,430 @@
+"""Worker process: executes normal tasks dispatched by the head, or hosts one actor.
+
+Parity: reference python/ray/_private/workers/default_worker.py + the execution half of
+python/ray/_raylet.pyx (execute_task, store task outputs, actor creation, async/threaded actors,
+concurrency groups) and src/ray/core_worker/transport/direct_actor_transport.cc (actor task
+receiving, in-order execution per caller).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import concurrent.futures
+import inspect
+import json
+import os
+import queue
+import socket
+import sys
+import threading
+import time
+import traceback
+
+import cloudpickle
+
+from ray_memory_management_amd import exceptions as exc
+from ray_memory_management_amd._private import protocol as P
+from ray_memory_management_amd._private import serialization as ser
+from ray_memory_management_amd._private import worker as _w
+from ray_memory_management_amd._private.ids import object_id_for_return
+from ray_memory_management_amd.object_ref import ObjectRef, _set_worker
+
+
+def _apply_runtime_env():
+    spec = os.environ.get("RMM_RUNTIME_ENV")
+    if not spec:
+        return
+    env = json.loads(spec)
+    wd = env.get("working_dir")
+    if wd and os.path.isdir(wd):
+        os.chdir(wd)
+        sys.path.insert(0, wd)
+    for m in env.get("py_modules") or []:
+        if os.path.isdir(m):
+            sys.path.insert(0, os.path.dirname(os.path.abspath(m)))
+            sys.path.insert(0, m)
+
+
+class Executor:
+    def __init__(self, w: _w.CoreWorker):
+        self.w = w
+        self.fns = {}
+        self.call_counts = collections.Counter()
+        self.actor = None
+        self.actor_spec = None
+        self.actor_server = None
+        self.actor_q: "queue.Queue" = queue.Queue()
+        self.pool = None
+        self.group_pools = {}
+        self.loop = None
+        self.exiting = False
+        self.pid = os.getpid()
+
+    # ------------------------------------------------------------------ argument handling
+    def resolve(self, enc):
+        kind, v = enc
+        if kind == "v":
+            return ser.loads_inline(v)
+        return self.w.get([ObjectRef(v)])[0]
+
+    def resolve_all(self, args, kwargs):
+        # fetch all by-ref args in one batched get so errors surface in order
+        return [self.resolve(a) for a in args], {k: self.resolve(v) for k, v in kwargs.items()}
+
+    # ------------------------------------------------------------------ outputs
+    def store_outputs(self, return_ids, num_returns, result, contained_map, holds):
+        if num_returns == 0:
+            return
+        if num_returns == "dynamic":
+            refs = []
+            tid = return_ids[0][:16]
+            for i, v in enumerate(result):
+                oid = object_id_for_return(tid, 1000 + i)
+                self._put_value(oid, v, contained_map, holds)
+                refs.append(ObjectRef(oid))
+            from ray_memory_management_amd.object_ref import ObjectRefGenerator
+
+            self._put_value(return_ids[0], ObjectRefGenerator(refs), contained_map, holds)
+            holds.extend(refs)
+            return
+        if num_returns == 1:
+            values = [result]
+        else:
+            if not isinstance(result, (tuple, list)) or len(result) != num_returns:
+                raise ValueError(f"Task returned {result!r} but num_returns={num_returns}")
+            values = list(result)
+        for oid, v in zip(return_ids, values):
+            self._put_value(oid, v, contained_map, holds)
+
+    def _put_value(self, oid, v, contained_map, holds):
+        if _w._is_cuda_tensor(v) and self.w.config.get("gpu_object_store", True):
+            from ray_memory_management_amd._private import gpu_object_store as gos
+
+            gos.put_tensor(self.w, oid, v)
+            self.w.send((P.GPU_OBJECT, oid))
+            return
+        data, bufs, contained = ser.serialize(v)
+        if contained:
+            contained_map[oid] = contained
+            for c in contained:  # keep inner objects alive until TASK_DONE reached the head
+                holds.append(ObjectRef(c))
+        if not self.w.store.put_serialized(oid, data, bufs, ser.TAG_PICKLE, False):
+            pass  # already exists (retry of a task whose output survived)
+
+    def store_error(self, return_ids, err):
+        data, bufs, _ = ser.serialize(err)
+        for oid in return_ids:
+            try:
+                self.w.store.put_serialized(oid, data, bufs, ser.TAG_ERROR, True)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ normal tasks
+    def execute(self, spec, blob, info):
+        w = self.w
+        fid = spec["fn_id"]
+        fn = self.fns.get(fid)
+        if fn is None:
+            if blob is None:
+                raise RuntimeError("function blob missing")
+            fn = cloudpickle.loads(blob)
+            self.fns[fid] = fn
+        w.current_task_id = spec["task_id"]
+        w.current_task_name = spec.get("name")
+        w.gpu_ids = list(info.get("gpu_ids") or [])
+        if w.gpu_ids:
+            vis = ",".join(map(str, w.gpu_ids))
+            if os.environ.get("HIP_VISIBLE_DEVICES") is None:
+                os.environ["HIP_VISIBLE_DEVICES"] = vis
+                os.environ["CUDA_VISIBLE_DEVICES"] = vis
+        st = spec.get("strategy") or {}
+        w.placement_group_capture = None
+        if st.get("type") == "PLACEMENT_GROUP" and st.get("capture"):
+            from ray_memory_management_amd.util.placement_group import PlacementGroup
+            from ray_memory_management_amd._private.ids import PlacementGroupID
+
+            w.placement_group_capture = PlacementGroup(PlacementGroupID(st["pg_id"]))
+        env_vars = (spec.get("runtime_env") or {}).get("env_vars") or {}
+        saved_env = {k: os.environ.get(k) for k in env_vars}
+        for k, v in env_vars.items():
+            os.environ[str(k)] = str(v)
+        status = "ok"
+        contained_map = {}
+        holds = []
+        t0 = time.time()
+        try:
+            try:
+                args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
+            except exc.RayTaskError as e:
+                # an argument was an error object: propagate it as this task's output
+                self.store_error(spec["return_ids"], e)
+                status = "err"
+                raise _Handled()
+            except exc.RayError as e:
+                self.store_error(spec["return_ids"], e)
+                status = "err"
+                raise _Handled()
+            result = fn(*args, **kwargs)
+            if inspect.isgenerator(result) and spec.get("num_returns") not in ("dynamic",):
+                result = list(result) if spec.get("num_returns", 1) != 1 else list(result)
+            self.store_outputs(spec["return_ids"], spec.get("num_returns", 1), result, contained_map, holds)
+        except _Handled:
+            pass
+        except exc.TaskCancelledError:
+            self.store_error(spec["return_ids"], exc.TaskCancelledError(spec["task_id"].hex()))
+            status = "err"
+        except KeyboardInterrupt:
+            self.store_error(spec["return_ids"], exc.TaskCancelledError(spec["task_id"].hex()))
+            status = "err"
+        except BaseException as e:  # noqa: BLE001
+            if isinstance(e, SystemExit) and not isinstance(e, Exception):
+                self.exiting = True
+            retry_ex = spec.get("retry_exceptions", False)
+            retryable = (retry_ex is True or (isinstance(retry_ex, (list, tuple)) and isinstance(e, tuple(retry_ex))))
+            max_retries = spec.get("max_retries", 0)
+            if retryable and (max_retries < 0 or info.get("attempt", 0) < max_retries):
+                status = "retry"
+            else:
+                err = exc.RayTaskError.from_exception(e, spec.get("name", "task"), pid=self.pid)
+                self.store_error(spec["return_ids"], err)
+                status = "err"
+        finally:
+            for k, v in saved_env.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            w.current_task_id = None
+            w.placement_group_capture = None
+        t1 = time.time()
+        w.record_event({"cat": "task", "name": spec.get("name", "task"), "ph": "X", "pid": f"node{info.get('node_id', 1)}",
+                        "tid": f"worker {self.pid}", "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6,
+                        "args": {"task_id": spec["task_id"].hex(), "status": status}})
+        self.call_counts[fid] += 1
+        mc = spec.get("max_calls", 0)
+        exit_after = bool(mc and self.call_counts[fid] >= mc) or self.exiting
+        w.send((P.TASK_DONE, spec["task_id"], status, contained_map, {"exit": exit_after}))
+        del holds
+        if exit_after:
+            w.flush_events()
+            os._exit(0)
+
+    # ------------------------------------------------------------------ actors
+    def create_actor(self, spec, blob, info):
+        w = self.w
+        self.actor_spec = spec
+        w.current_actor_id = spec["actor_id"]
+        w.gpu_ids = list(info.get("gpu_ids") or [])
+        for k, v in ((spec.get("runtime_env") or {}).get("env_vars") or {}).items():
+            os.environ[str(k)] = str(v)
+        st = spec.get("strategy") or {}
+        if st.get("type") == "PLACEMENT_GROUP" and st.get("capture"):
+            from ray_memory_management_amd.util.placement_group import PlacementGroup
+            from ray_memory_management_amd._private.ids import PlacementGroupID
+
+            w.placement_group_capture = PlacementGroup(PlacementGroupID(st["pg_id"]))
+        try:
+            cls = cloudpickle.loads(blob) if blob is not None else None
+            if cls is None:
+                raise RuntimeError("actor class blob missing")
+            args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
+            from ray_memory_management_amd.actor import ActorHandle
+
+            w.actor_handle_for_self = ActorHandle(spec["actor_id"], spec["class_name"], spec["method_meta"],
+                                                  spec.get("max_task_retries", 0), _count=False)
+            self.actor = cls.__new__(cls)
+            self.actor.__init__(*args, **kwargs)
+        except BaseException as e:  # noqa: BLE001
+            err = exc.RayTaskError.from_exception(e, f"{spec['class_name']}.__init__", pid=self.pid)
+            w.send((P.ACTOR_FAILED_INIT, spec["actor_id"], ser.dumps_inline(err)[0]))
+            time.sleep(0.2)
+            os._exit(1)
+        max_conc = spec.get("max_concurrency", 1)
+        if spec.get("is_async"):
+            self.loop = asyncio.new_event_loop()
+            self.sem = None
+            threading.Thread(target=self._run_loop, args=(max_conc,), daemon=True).start()
+        elif max_conc > 1:
+            self.pool = concurrent.futures.ThreadPoolExecutor(max_conc)
+        for g, n in (spec.get("concurrency_groups") or {}).items():
+            if not spec.get("is_async"):
+                self.group_pools[g] = concurrent.futures.ThreadPoolExecutor(int(n))
+        path = os.path.join(w.session_dir, "sockets", f"actor-{spec['actor_id'].hex()}-{self.pid}.sock")
+        srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        srv.bind(path)
+        srv.listen(256)
+        self.actor_server = srv
+        threading.Thread(target=self._accept_loop, args=(srv,), daemon=True).start()
+        w.send((P.ACTOR_READY, spec["actor_id"], path))
+
+    def _run_loop(self, max_conc):
+        asyncio.set_event_loop(self.loop)
+        self.sem = asyncio.Semaphore(max_conc)
+        self.loop.run_forever()
+
+    def _accept_loop(self, srv):
+        while True:
+            try:
+                s, _ = srv.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._conn_loop, args=(s,), daemon=True).start()
+
+    def _conn_loop(self, s):
+        lock = threading.Lock()
+        try:
+            while True:
+                m = P.recv(s)
+                if m[0] == P.ACTOR_TASK:
+                    self.actor_q.put((s, lock, m[1]))
+        except (ConnectionError, OSError, EOFError):
+            pass
+
+    def _ack(self, s, lock, seq):
+        try:
+            P.send(s, (P.REPLY, 0, [seq]), lock)
+        except OSError:
+            pass
+
+    def run_actor_task(self, s, lock, spec):
+        w = self.w
+        name = spec["method"]
+        ret_ids = spec["return_ids"]
+        t0 = time.time()
+        holds = []
+        contained_map = {}
+        try:
+            if name == "__ray_terminate__":
+                self._ack(s, lock, spec["seq"])
+                self.store_outputs(ret_ids, 1, None, contained_map, holds)
+                w.flush_events()
+                w.send(None)
+                os._exit(0)
+            if name == "__ray_ready__":
+                result = True
+            else:
+                args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
+                m = getattr(self.actor, name)
+                result = m(*args, **kwargs)
+                if inspect.iscoroutine(result):
+                    raise RuntimeError("coroutine returned from a non-async actor path")
+            self.store_outputs(ret_ids, spec.get("num_returns", 1), result, contained_map, holds)
+        except BaseException as e:  # noqa: BLE001
+            from ray_memory_management_amd.actor import _ActorExit
+
+            if isinstance(e, _ActorExit):
+                self.store_outputs(ret_ids, spec.get("num_returns", 1), None, contained_map, holds)
+                self._ack(s, lock, spec["seq"])
+                w.send((P.ACTOR_EXITING, spec.get("actor_id") or w.current_actor_id))
+                w.flush_events()
+                w.send(None)
+                time.sleep(0.05)
+                os._exit(0)
+            if isinstance(e, exc.RayError) and not isinstance(e, exc.RayTaskError) and name != "__init__":
+                self.store_error(ret_ids, e)
+            else:
+                self.store_error(ret_ids, exc.RayTaskError.from_exception(e, spec.get("name", name), pid=self.pid))
+        if contained_map:
+            for outer, inners in contained_map.items():
+                w.send((P.CONTAINED, outer, inners))
+        t1 = time.time()
+        w.record_event({"cat": "actor_task", "name": spec.get("name", name), "ph": "X", "pid": "actors",
+                        "tid": f"actor {self.pid}", "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6})
+        self._ack(s, lock, spec["seq"])
+        del holds
+
+    async def run_async_actor_task(self, s, lock, spec):
+        async with self.sem:
+            name = spec["method"]
+            ret_ids = spec["return_ids"]
+            holds, contained_map = [], {}
+            try:
+                if name == "__ray_ready__":
+                    result = True
+                elif name == "__ray_terminate__":
+                    self.store_outputs(ret_ids, 1, None, contained_map, holds)
+                    self._ack(s, lock, spec["seq"])
+                    os._exit(0)
+                else:
+                    loop = asyncio.get_running_loop()
+                    args, kwargs = await loop.run_in_executor(None, self.resolve_all, spec["args"], spec["kwargs"])
+                    m = getattr(self.actor, name)
+                    result = m(*args, **kwargs)
+                    if inspect.isawaitable(result):
+                        result = await result
+                self.store_outputs(ret_ids, spec.get("num_returns", 1), result, contained_map, holds)
+            except BaseException as e:  # noqa: BLE001
+                from ray_memory_management_amd.actor import _ActorExit
+
+                if isinstance(e, _ActorExit):
+                    self._ack(s, lock, spec["seq"])
+                    self.w.send((P.ACTOR_EXITING, self.w.current_actor_id))
+                    os._exit(0)
+                self.store_error(ret_ids, exc.RayTaskError.from_exception(e, spec.get("name", name), pid=self.pid))
+            if contained_map:
+                for outer, inners in contained_map.items():
+                    self.w.send((P.CONTAINED, outer, inners))
+            self._ack(s, lock, spec["seq"])
+
+    def actor_loop(self):
+        while True:
+            s, lock, spec = self.actor_q.get()
+            if self.loop is not None:
+                asyncio.run_coroutine_threadsafe(self.run_async_actor_task(s, lock, spec), self.loop)
+                continue
+            g = spec.get("concurrency_group")
+            if g and g in self.group_pools:
+                self.group_pools[g].submit(self.run_actor_task, s, lock, spec)
+            elif self.pool is not None:
+                self.pool.submit(self.run_actor_task, s, lock, spec)
+            else:
+                self.run_actor_task(s, lock, spec)
+
+
+class _Handled(Exception):
+    pass
+
+
+def main():
+    _apply_runtime_env()
+    head = os.environ["RMM_HEAD_SOCKET"]
+    store = os.environ["RMM_STORE_NAME"]
+    sess = os.environ["RMM_SESSION_DIR"]
+    wid = bytes.fromhex(os.environ["RMM_WORKER_ID"])
+    node = int(os.environ.get("RMM_NODE_ID", "1"))
+    w = _w.CoreWorker(_w.WORKER_MODE, head, store, sess, worker_id=wid, node_id=node)
+    w.main_thread_id = threading.main_thread().ident
+    _w.global_worker = w
+    _set_worker(w)
+    ex = Executor(w)
+    w.send((P.REGISTER, "worker", {"worker_id": wid, "pid": os.getpid()}))
+    info = None
+    while True:
+        m = w.task_queue.get()
+        t = m[0]
+        if t == P.EXECUTE:
+            try:
+                ex.execute(m[1], m[2], m[3])
+            except KeyboardInterrupt:
+                pass
+        elif t == P.CREATE_ACTOR_INSTANCE:
+            ex.create_actor(m[1], m[2], m[3])
+            threading.Thread(target=_drain_head_queue, args=(w,), daemon=True).start()
+            ex.actor_loop()
+        elif t == P.EXIT:
+            break
+    w.flush_events()
+    w.shutdown()
+    os._exit(0)
+
+
+def _drain_head_queue(w):
+    while True:
+        m = w.task_queue.get()
+        if m[0] == P.EXIT:
+            w.flush_events()
+            os._exit(0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,298 @@
+"""Actors. Parity: reference python/ray/actor.py (ActorClass, ActorHandle, ActorMethod, options,
+named/detached actors, get_if_exists, max_restarts/max_task_retries, concurrency groups)."""
+from __future__ import annotations
+
+import hashlib
+import inspect
+from typing import Any, Dict, Optional
+
+import cloudpickle
+
+from ray_memory_management_amd._private import protocol as P
+from ray_memory_management_amd._private import worker as _w
+from ray_memory_management_amd.remote_function import (env_key_of, resources_from_options,
+                                                       strategy_from_options)
+
+_ACTOR_OPTIONS = {
+    "num_cpus", "num_gpus", "memory", "object_store_memory", "resources", "accelerator_type", "max_restarts",
+    "max_task_retries", "max_concurrency", "name", "namespace", "lifetime", "scheduling_strategy",
+    "placement_group", "placement_group_bundle_index", "placement_group_capture_child_tasks", "runtime_env",
+    "get_if_exists", "concurrency_groups", "max_pending_calls", "_metadata",
+}
+
+
+def method(*args, **kwargs):
+    """Annotate an actor method (num_returns / concurrency_group). Parity: ray.method."""
+    def deco(f):
+        if "num_returns" in kwargs:
+            f.__ray_num_returns__ = kwargs["num_returns"]
+        if "concurrency_group" in kwargs:
+            f.__ray_concurrency_group__ = kwargs["concurrency_group"]
+        return f
+
+    if len(args) == 1 and callable(args[0]) and not kwargs:
+        return args[0]
+    return deco
+
+
+def _actor_ref_key(actor_id: bytes) -> bytes:
+    return b"\xaa" + actor_id[:16] + b"\xaa\xaa\xaa"
+
+
+class ActorMethod:
+    def __init__(self, handle, name, num_returns=1, concurrency_group=None):
+        self._handle = handle
+        self._name = name
+        self._num_returns = num_returns
+        self._concurrency_group = concurrency_group
+
+    def __call__(self, *a, **k):
+        raise TypeError(f"Actor methods cannot be called directly. Instead of running 'object.{self._name}()', "
+                        f"try 'object.{self._name}.remote()'.")
+
+    def remote(self, *args, **kwargs):
+        return self._handle._submit(self._name, args, kwargs, self._num_returns, self._concurrency_group)
+
+    def options(self, **opts):
+        parent = self
+
+        class _Opt:
+            def remote(self_inner, *args, **kwargs):
+                return parent._handle._submit(parent._name, args, kwargs, opts.get("num_returns", parent._num_returns),
+                                              opts.get("concurrency_group", parent._concurrency_group))
+
+            def bind(self_inner, *args, **kwargs):
+                from ray_memory_management_amd.dag import ClassMethodNode
+
+                return ClassMethodNode(parent._handle, parent._name, args, kwargs, opts)
+
+        return _Opt()
+
+    def bind(self, *args, **kwargs):
+        from ray_memory_management_amd.dag import ClassMethodNode
+
+        return ClassMethodNode(self._handle, self._name, args, kwargs, {})
+
+
+class ActorHandle:
+    def __init__(self, actor_id: bytes, class_name: str, method_meta: Dict[str, tuple], max_task_retries: int,
+                 _count: bool = True, spec=None):
+        self._actor_id = actor_id
+        self._class_name = class_name
+        self._method_meta = method_meta
+        self._max_task_retries = max_task_retries
+        self._spec = spec
+        self._counted = False
+        if _count and _w.global_worker is not None:
+            _w.global_worker.add_local_ref(_actor_ref_key(actor_id))
+            self._counted = True
+
+    @classmethod
+    def _from_spec(cls, spec):
+        return cls(spec["actor_id"], spec["class_name"], spec["method_meta"], spec.get("max_task_retries", 0), spec=spec)
+
+    def __getattr__(self, item):
+        if item.startswith("__") and item not in ("__ray_ready__", "__ray_terminate__"):
+            raise AttributeError(item)
+        meta = self._method_meta.get(item)
+        if meta is None:
+            if item in ("__ray_ready__", "__ray_terminate__"):
+                meta = (1, None)
+            else:
+                raise AttributeError(f"'{self._class_name}' object has no attribute '{item}'")
+        return ActorMethod(self, item, meta[0], meta[1])
+
+    def _submit(self, method_name, args, kwargs, num_returns, concurrency_group):
+        if _w._local_mode:
+            from ray_memory_management_amd._private import local_mode as lm
+
+            return lm.submit_actor_method(self, method_name, args, kwargs, num_returns)
+        w = _w._require_worker()
+        ea, ek, arg_refs, keep = w.prepare_args(args, kwargs)
+        spec = {"method": method_name, "args": ea, "kwargs": ek, "num_returns": num_returns,
+                "concurrency_group": concurrency_group, "name": f"{self._class_name}.{method_name}"}
+        refs = w.submit_actor_task(self._actor_id, spec, keep, self._max_task_retries)
+        if num_returns == 0:
+            return None
+        if num_returns == 1 or num_returns == "dynamic":
+            return refs[0]
+        return refs
+
+    def __reduce__(self):
+        from ray_memory_management_amd._private import serialization as ser
+
+        ser.note_contained(_actor_ref_key(self._actor_id))
+        return (_rebuild_handle, (self._actor_id, self._class_name, self._method_meta, self._max_task_retries))
+
+    def __del__(self):
+        if self._counted:
+            w = _w.global_worker
+            if w is not None:
+                try:
+                    w.remove_local_ref(_actor_ref_key(self._actor_id))
+                except Exception:
+                    pass
+
+    def __repr__(self):
+        return f"Actor({self._class_name}, {self._actor_id.hex()})"
+
+    def __hash__(self):
+        return hash(self._actor_id)
+
+    def __eq__(self, o):
+        return isinstance(o, ActorHandle) and o._actor_id == self._actor_id
+
+    @property
+    def _ray_actor_id(self):
+        from ray_memory_management_amd._private.ids import ActorID
+
+        return ActorID(self._actor_id)
+
+
+def _rebuild_handle(actor_id, class_name, method_meta, max_task_retries):
+    return ActorHandle(actor_id, class_name, method_meta, max_task_retries)
+
+
+def _method_meta(cls) -> Dict[str, tuple]:
+    meta = {}
+    for name, fn in inspect.getmembers(cls, predicate=lambda x: inspect.isfunction(x) or inspect.ismethod(x)):
+        meta[name] = (getattr(fn, "__ray_num_returns__", 1), getattr(fn, "__ray_concurrency_group__", None))
+    return meta
+
+
+def _is_async_class(cls) -> bool:
+    return any(inspect.iscoroutinefunction(fn) or inspect.isasyncgenfunction(fn)
+               for _, fn in inspect.getmembers(cls, predicate=inspect.isfunction))
+
+
+class ActorClass:
+    def __init__(self, cls, options: Dict[str, Any]):
+        for k in options:
+            if k not in _ACTOR_OPTIONS:
+                raise ValueError(f"Invalid option keyword {k} for actors. Valid ones are {sorted(_ACTOR_OPTIONS)}.")
+        self._cls = cls
+        self._options = dict(options)
+        self._blob = None
+        self._cid = None
+        self._meta = _method_meta(cls)
+        self._is_async = _is_async_class(cls)
+        self.__name__ = cls.__name__
+        self.__doc__ = cls.__doc__
+
+    def __call__(self, *a, **k):
+        raise TypeError(f"Actors cannot be instantiated directly. Instead of '{self._cls.__name__}()', use "
+                        f"'{self._cls.__name__}.remote()'.")
+
+    def _ensure_pickled(self):
+        if self._blob is None:
+            self._blob = cloudpickle.dumps(self._cls)
+            self._cid = hashlib.sha1(self._blob).digest()
+        return self._cid, self._blob
+
+    def options(self, **opts):
+        for k in opts:
+            if k not in _ACTOR_OPTIONS:
+                raise ValueError(f"Invalid option keyword {k} for actors.")
+        parent = self
+        merged = {**self._options, **opts}
+
+        class _Opt:
+            def remote(self_inner, *args, **kwargs):
+                return parent._remote(args, kwargs, merged)
+
+            def bind(self_inner, *args, **kwargs):
+                from ray_memory_management_amd.dag import ClassNode
+
+                return ClassNode(parent, args, kwargs, merged)
+
+        return _Opt()
+
+    def remote(self, *args, **kwargs):
+        return self._remote(args, kwargs, self._options)
+
+    def bind(self, *args, **kwargs):
+        from ray_memory_management_amd.dag import ClassNode
+
+        return ClassNode(self, args, kwargs, self._options)
+
+    def _remote(self, args, kwargs, opts):
+        if _w._local_mode:
+            from ray_memory_management_amd._private import local_mode as lm
+
+            return lm.create_actor(self, args, kwargs, opts)
+        w = _w._require_worker()
+        name = opts.get("name")
+        namespace = opts.get("namespace", w.namespace)
+        lifetime = opts.get("lifetime")
+        if lifetime not in (None, "detached", "non_detached"):
+            raise ValueError("actor `lifetime` argument must be one of 'detached', 'non_detached' and 'None'.")
+        if name is not None and not isinstance(name, str):
+            raise TypeError(f"name must be None or a string, got: '{type(name)}'.")
+        if name == "":
+            raise ValueError("Actor name cannot be an empty string.")
+        if opts.get("get_if_exists") and name:
+            try:
+                return _w.get_actor(name, namespace=namespace)
+            except ValueError:
+                pass
+        cid, blob = self._ensure_pickled()
+        ea, ek, arg_refs, keep = w.prepare_args(args, kwargs)
+        # Reference semantics (python/ray/actor.py:_remote): with no resources specified the actor
+        # holds nothing for its lifetime but needs 1 CPU to be placed; otherwise everything
+        # specified (CPU defaulting to 1) is held for the lifetime.
+        spec_res = resources_from_options(opts, default_cpus=0.0)
+        if opts.get("num_cpus") is None:
+            spec_res.pop("CPU", None)
+        if not set(spec_res) - {"memory", "object_store_memory"}:
+            lres = dict(spec_res)
+            pres = dict(lres)
+            pres["CPU"] = pres.get("CPU", 0.0) + 1.0
+        else:
+            lres = dict(spec_res)
+            if opts.get("num_cpus") is None:
+                lres["CPU"] = 1.0
+            pres = dict(lres)
+        actor_id = _w._ids.random_id(16)
+        max_conc = opts.get("max_concurrency", 1000 if self._is_async else 1)
+        runtime_env = opts.get("runtime_env") or getattr(w, "job_runtime_env", None)
+        spec = {
+            "actor_id": actor_id, "class_id": cid, "class_name": self._cls.__name__, "args": ea, "kwargs": ek,
+            "arg_refs": arg_refs, "resources": lres, "placement_resources": pres,
+            "max_restarts": opts.get("max_restarts", 0), "max_task_retries": opts.get("max_task_retries", 0),
+            "max_concurrency": max_conc, "name": name, "namespace": namespace, "lifetime": lifetime,
+            "strategy": strategy_from_options(opts, w), "method_meta": self._meta, "is_async": self._is_async,
+            "concurrency_groups": opts.get("concurrency_groups") or {}, "job_id": w.job_id,
+            "runtime_env": runtime_env, "env_key": env_key_of(runtime_env),
+        }
+        b = w.export(cid, blob)
+        if b is not None:
+            spec["class_blob"] = b
+        if name:
+            r = w.request(lambda rid: (P.CREATE_ACTOR, rid, spec))
+            if r[0] == "exists":
+                if opts.get("get_if_exists"):
+                    return _w.get_actor(name, namespace=namespace)
+                raise ValueError(f"The name {name} (namespace={namespace}) is already taken. Please use a different "
+                                 f"name or get the existing actor using ray.get_actor('{name}', namespace='{namespace}')")
+        else:
+            w.send((P.CREATE_ACTOR, None, spec))
+        handle = ActorHandle(actor_id, self._cls.__name__, self._meta, spec["max_task_retries"], spec=spec)
+        return handle
+
+
+def make_actor_class(cls, options):
+    return ActorClass(cls, options)
+
+
+def exit_actor():
+    """Terminate the current actor gracefully after the current task. Parity: ray.actor.exit_actor."""
+    w = _w.global_worker
+    if w is None or w.current_actor_id is None:
+        raise TypeError("exit_actor API is called on a non-actor worker.")
+    from ray_memory_management_amd.exceptions import AsyncioActorExit
+
+    raise _ActorExit()
+
+
+class _ActorExit(SystemExit):
+    pass

@@ -1,0 +1,116 @@
+"""ObjectRef — a future for an object in the store.
+
+Parity: reference python/ray/includes/object_ref.pxi. Each live ObjectRef instance holds one
+process-local reference; the core worker reports 0↔1 transitions of the per-process count to
+the head (batched), which frees the object when the cluster-wide count reaches zero.
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures
+import threading
+
+from ray_memory_management_amd._private import serialization as ser
+
+_worker = None  # set by _private.worker
+
+
+def _set_worker(w):
+    global _worker
+    _worker = w
+
+
+class ObjectRef:
+    __slots__ = ("_id", "_counted", "__weakref__")
+
+    def __init__(self, oid: bytes, _add_ref: bool = True):
+        self._id = oid
+        self._counted = False
+        if _add_ref and _worker is not None:
+            _worker.add_local_ref(oid)
+            self._counted = True
+
+    def binary(self) -> bytes:
+        return self._id
+
+    def hex(self) -> str:
+        return self._id.hex()
+
+    def task_id(self):
+        from ray_memory_management_amd._private.ids import TaskID
+
+        return TaskID(self._id[:16])
+
+    def is_nil(self) -> bool:
+        return self._id == b"\xff" * 20
+
+    @classmethod
+    def nil(cls):
+        return cls(b"\xff" * 20, _add_ref=False)
+
+    @classmethod
+    def from_random(cls):
+        import os
+
+        return cls(os.urandom(20))
+
+    def __hash__(self):
+        return hash(self._id)
+
+    def __eq__(self, other):
+        return isinstance(other, ObjectRef) and other._id == self._id
+
+    def __repr__(self):
+        return f"ObjectRef({self._id.hex()})"
+
+    def __del__(self):
+        if self._counted:
+            w = _worker
+            if w is not None:
+                try:
+                    w.remove_local_ref(self._id)
+                except Exception:
+                    pass
+
+    def __reduce__(self):
+        ser.note_contained(self._id)
+        return (_rebuild_ref, (self._id,))
+
+    # ---- futures / asyncio integration (reference: ObjectRef.future(), __await__)
+    def future(self) -> concurrent.futures.Future:
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+
+        def run():
+            try:
+                fut.set_result(_worker.get([self])[0])
+            except BaseException as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        threading.Thread(target=run, daemon=True).start()
+        return fut
+
+    def as_future(self):
+        return asyncio.wrap_future(self.future())
+
+    def __await__(self):
+        return self.as_future().__await__()
+
+
+def _rebuild_ref(oid: bytes) -> ObjectRef:
+    return ObjectRef(oid)
+
+
+class ObjectRefGenerator:
+    """Iterator over dynamically-returned ObjectRefs (``num_returns="dynamic"``)."""
+
+    def __init__(self, refs):
+        self._refs = list(refs)
+
+    def __iter__(self):
+        return iter(self._refs)
+
+    def __len__(self):
+        return len(self._refs)
+
+    def __getitem__(self, i):
+        return self._refs[i]

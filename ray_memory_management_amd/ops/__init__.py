@@ -120,16 +120,17 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 def gae_reference(rewards, values, dones, last_values, gamma: float, lam: float):
     """Plain fp32 torch GAE over time-major [T, B] tensors (also the CPU path)."""
     T = rewards.shape[0]
-    adv = torch.empty_like(rewards, dtype=torch.float32)
-    a = torch.zeros_like(last_values, dtype=torch.float32)
-    vnext = last_values.float()
+    dt = torch.promote_types(rewards.dtype, torch.float32)
+    adv = torch.empty(rewards.shape, dtype=dt, device=rewards.device)
+    a = torch.zeros(last_values.shape, dtype=dt, device=rewards.device)
+    vnext = last_values.to(dt)
     for t in range(T - 1, -1, -1):
-        nd = 1.0 - dones[t].float()
-        delta = rewards[t].float() + gamma * vnext * nd - values[t].float()
+        nd = 1.0 - dones[t].to(dt)
+        delta = rewards[t].to(dt) + gamma * vnext * nd - values[t].to(dt)
         a = delta + gamma * lam * nd * a
         adv[t] = a
-        vnext = values[t].float()
-    return adv, adv + values.float()
+        vnext = values[t].to(dt)
+    return adv, adv + values.to(dt)
 
 
 def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, last_values: torch.Tensor,

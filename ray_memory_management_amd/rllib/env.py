@@ -1,0 +1,246 @@
+"""Environments and spaces (gym is not installed here; a minimal compatible API is provided).
+
+Parity: reference rllib/env/{base_env,vector_env}.py, rllib/examples/env/* (CartPole is the
+reference's standard smoke env; Atari frames are replaced by synthetic 84x84x4 uint8 frames).
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Optional, Tuple
+
+import numpy as np
+
+
+class Space:
+    shape: Tuple[int, ...] = ()
+    dtype = np.float32
+
+    def sample(self):
+        raise NotImplementedError
+
+    def contains(self, x) -> bool:
+        raise NotImplementedError
+
+
+class Discrete(Space):
+    def __init__(self, n: int):
+        self.n = int(n)
+        self.shape = ()
+        self.dtype = np.int64
+
+    def sample(self):
+        return int(np.random.randint(self.n))
+
+    def contains(self, x):
+        return 0 <= int(x) < self.n
+
+    def __repr__(self):
+        return f"Discrete({self.n})"
+
+
+class Box(Space):
+    def __init__(self, low, high, shape=None, dtype=np.float32):
+        self.dtype = np.dtype(dtype)
+        if shape is None:
+            shape = np.shape(low)
+        self.shape = tuple(shape)
+        self.low = np.broadcast_to(np.asarray(low, dtype=self.dtype), self.shape)
+        self.high = np.broadcast_to(np.asarray(high, dtype=self.dtype), self.shape)
+
+    def sample(self):
+        if np.issubdtype(self.dtype, np.integer):
+            return np.random.randint(self.low, self.high.astype(np.int64) + 1, size=self.shape).astype(self.dtype)
+        lo = np.where(np.isfinite(self.low), self.low, -1.0)
+        hi = np.where(np.isfinite(self.high), self.high, 1.0)
+        return np.random.uniform(lo, hi, size=self.shape).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+    def __repr__(self):
+        return f"Box({self.shape}, {self.dtype})"
+
+
+class Env:
+    observation_space: Space
+    action_space: Space
+
+    def reset(self, *, seed: Optional[int] = None):
+        raise NotImplementedError
+
+    def step(self, action):
+        """Returns (obs, reward, done, info)."""
+        raise NotImplementedError
+
+    def close(self):
+        pass
+
+
+class CartPoleEnv(Env):
+    """Classic cart-pole (same dynamics constants as gym's CartPole-v1)."""
+
+    def __init__(self, config=None):
+        self.gravity, self.masscart, self.masspole, self.length = 9.8, 1.0, 0.1, 0.5
+        self.total_mass = self.masspole + self.masscart
+        self.polemass_length = self.masspole * self.length
+        self.force_mag, self.tau = 10.0, 0.02
+        self.theta_threshold = 12 * 2 * math.pi / 360
+        self.x_threshold = 2.4
+        self.max_steps = (config or {}).get("max_episode_steps", 500)
+        high = np.array([self.x_threshold * 2, np.finfo(np.float32).max, self.theta_threshold * 2,
+                         np.finfo(np.float32).max], dtype=np.float32)
+        self.observation_space = Box(-high, high, dtype=np.float32)
+        self.action_space = Discrete(2)
+        self.rng = np.random.default_rng()
+        self.state = None
+        self.steps = 0
+
+    def reset(self, *, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.state = self.rng.uniform(-0.05, 0.05, size=4)
+        self.steps = 0
+        return self.state.astype(np.float32)
+
+    def step(self, action):
+        x, x_dot, theta, theta_dot = self.state
+        force = self.force_mag if int(action) == 1 else -self.force_mag
+        ct, st = math.cos(theta), math.sin(theta)
+        temp = (force + self.polemass_length * theta_dot ** 2 * st) / self.total_mass
+        thetaacc = (self.gravity * st - ct * temp) / (
+            self.length * (4.0 / 3.0 - self.masspole * ct ** 2 / self.total_mass))
+        xacc = temp - self.polemass_length * thetaacc * ct / self.total_mass
+        x = x + self.tau * x_dot
+        x_dot = x_dot + self.tau * xacc
+        theta = theta + self.tau * theta_dot
+        theta_dot = theta_dot + self.tau * thetaacc
+        self.state = np.array([x, x_dot, theta, theta_dot])
+        self.steps += 1
+        done = bool(x < -self.x_threshold or x > self.x_threshold or theta < -self.theta_threshold
+                    or theta > self.theta_threshold or self.steps >= self.max_steps)
+        return self.state.astype(np.float32), 1.0, done, {}
+
+
+class SyntheticAtariEnv(Env):
+    """84x84x4 uint8 frame-stacked observations with Atari-like dynamics statistics (CPU)."""
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.num_actions = config.get("num_actions", 4)
+        self.episode_len = config.get("episode_len", 1000)
+        self.observation_space = Box(0, 255, shape=(84, 84, 4), dtype=np.uint8)
+        self.action_space = Discrete(self.num_actions)
+        self.rng = np.random.default_rng(config.get("seed"))
+        self._pool = self.rng.integers(0, 256, size=(64, 84, 84), dtype=np.uint8)
+        self.frames = None
+        self.t = 0
+
+    def reset(self, *, seed=None):
+        self.t = 0
+        idx = self.rng.integers(0, 64, size=4)
+        self.frames = np.stack([self._pool[i] for i in idx], axis=-1)
+        return self.frames.copy()
+
+    def step(self, action):
+        self.t += 1
+        nf = np.roll(self._pool[self.rng.integers(0, 64)], int(action) + 1, axis=1)
+        self.frames = np.concatenate([self.frames[..., 1:], nf[..., None]], axis=-1)
+        reward = float(self.rng.random() < 0.05)
+        done = self.t >= self.episode_len
+        return self.frames.copy(), reward, done, {}
+
+
+class VectorEnv:
+    """Batched CPU envs (reference rllib/env/vector_env.py)."""
+
+    def __init__(self, make_env, num_envs: int):
+        self.envs = [make_env(i) for i in range(num_envs)]
+        self.num_envs = num_envs
+        self.observation_space = self.envs[0].observation_space
+        self.action_space = self.envs[0].action_space
+
+    def vector_reset(self):
+        return [e.reset() for e in self.envs]
+
+    def reset_at(self, i):
+        return self.envs[i].reset()
+
+    def vector_step(self, actions):
+        obs, rew, done, info = [], [], [], []
+        for e, a in zip(self.envs, actions):
+            o, r, d, i = e.step(a)
+            obs.append(o)
+            rew.append(r)
+            done.append(d)
+            info.append(i)
+        return obs, rew, done, info
+
+
+class GPUSyntheticAtariVectorEnv:
+    """Device-resident vectorised synthetic Atari env: B envs, frames [B, 4, 84, 84] uint8 on the
+    GPU; a step rolls the frame stack and writes one new frame per env (action-dependent shift of
+    a pooled random frame), rewards are sparse Bernoulli, episodes truncate at `episode_len`.
+    Keeps the whole sample→learn loop on the MI355X (no host round trips)."""
+
+    def __init__(self, num_envs: int, device, num_actions: int = 4, episode_len: int = 1000, seed: int = 0):
+        import torch
+
+        self.num_envs = num_envs
+        self.device = torch.device(device)
+        self.num_actions = num_actions
+        self.episode_len = episode_len
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        self.gen = g
+        self.pool = torch.randint(0, 256, (64, 84, 84), dtype=torch.uint8, device=self.device, generator=g)
+        self.frames = self.pool[torch.randint(0, 64, (num_envs, 4), device=self.device, generator=g)]
+        self.t = torch.zeros(num_envs, dtype=torch.int32, device=self.device)
+        self.observation_space = Box(0, 255, shape=(4, 84, 84), dtype=np.uint8)
+        self.action_space = Discrete(num_actions)
+
+    def reset(self):
+        return self.frames
+
+    def step(self, actions):
+        import torch
+
+        B = self.num_envs
+        idx = torch.randint(0, 64, (B,), device=self.device, generator=self.gen)
+        new = self.pool[idx]
+        # action-dependent horizontal shift (cheap stand-in for game dynamics)
+        shift = (actions.to(torch.int64) % 4) * 3
+        cols = (torch.arange(84, device=self.device)[None, :] - shift[:, None]) % 84
+        new = torch.gather(new, 2, cols[:, None, :].expand(B, 84, 84))
+        self.frames = torch.cat([self.frames[:, 1:], new[:, None]], dim=1)
+        self.t += 1
+        reward = (torch.rand(B, device=self.device, generator=self.gen) < 0.05).float()
+        done = self.t >= self.episode_len
+        if bool(done.any()):
+            self.t = torch.where(done, torch.zeros_like(self.t), self.t)
+        return self.frames, reward, done.float()
+
+
+_REGISTRY = {
+    "CartPole-v1": CartPoleEnv,
+    "CartPole-v0": lambda cfg=None: CartPoleEnv({"max_episode_steps": 200, **(cfg or {})}),
+    "SyntheticAtari-v0": SyntheticAtariEnv,
+    "BreakoutNoFrameskip-v4": SyntheticAtariEnv,
+}
+
+
+def register_env(name: str, creator):
+    """Parity: ray.tune.registry.register_env."""
+    _REGISTRY[name] = creator
+
+
+def make_env(env, config=None):
+    if isinstance(env, str):
+        if env not in _REGISTRY:
+            raise ValueError(f"unknown env {env!r}; register it with register_env()")
+        return _REGISTRY[env](config or {})
+    if isinstance(env, type):
+        return env(config or {})
+    if callable(env):
+        return env(config or {})
+    raise ValueError(f"invalid env {env!r}")

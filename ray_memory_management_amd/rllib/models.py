@@ -1,0 +1,105 @@
+"""Policy/value networks. Parity: reference rllib/models/torch/{fcnet,visionnet}.py and
+rllib/models/utils.py:get_filter_config (84x84 Atari filters [[16,8,4],[32,4,2],[256,11,1]])."""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+import torch.nn as nn
+
+
+def _act(name):
+    return {"relu": nn.ReLU, "tanh": nn.Tanh, "elu": nn.ELU, "swish": nn.SiLU, "silu": nn.SiLU}[name]()
+
+
+class FullyConnectedNetwork(nn.Module):
+    def __init__(self, obs_dim: int, num_outputs: int, hiddens: Sequence[int] = (256, 256), activation="tanh",
+                 vf_share_layers: bool = False):
+        super().__init__()
+        self.vf_share_layers = vf_share_layers
+
+        def mlp():
+            layers, d = [], obs_dim
+            for h in hiddens:
+                layers += [nn.Linear(d, h), _act(activation)]
+                d = h
+            return nn.Sequential(*layers), d
+
+        self.body, d = mlp()
+        self.logits = nn.Linear(d, num_outputs)
+        if vf_share_layers:
+            self.value = nn.Linear(d, 1)
+        else:
+            self.vf_body, dv = mlp()
+            self.value = nn.Linear(dv, 1)
+        nn.init.orthogonal_(self.logits.weight, 0.01)
+        nn.init.zeros_(self.logits.bias)
+
+    def forward(self, obs):
+        obs = obs.float().flatten(1)
+        h = self.body(obs)
+        v = self.value(h if self.vf_share_layers else self.vf_body(obs))
+        return self.logits(h), v.squeeze(-1)
+
+
+class VisionNetwork(nn.Module):
+    """RLlib's default Atari conv stack with a shared value head (vf_share_layers=True).
+
+    Input: uint8 frames [B, 4, 84, 84] (channels-first) or [B, 84, 84, 4]; scaled by 1/255 in the
+    first layer. Uses channels_last memory format so MIOpen picks NHWC kernels on gfx950."""
+
+    def __init__(self, num_outputs: int, in_channels: int = 4,
+                 filters: List[list] = ((16, 8, 4), (32, 4, 2), (256, 11, 1)), in_hw: int = 84):
+        super().__init__()
+        layers = []
+        c = in_channels
+        hw = in_hw
+        for i, (out, k, s) in enumerate(filters):
+            last = i == len(filters) - 1
+            pad = 0 if last else _same_pad(hw, k, s)
+            layers += [nn.Conv2d(c, out, k, s, padding=pad), nn.ReLU()]
+            hw = (hw + 2 * pad - k) // s + 1
+            c = out
+        self.out_hw = hw
+        self.convs = nn.Sequential(*layers)
+        self.logits = nn.Linear(c, num_outputs)
+        self.value = nn.Linear(c, 1)
+        nn.init.orthogonal_(self.logits.weight, 0.01)
+        nn.init.zeros_(self.logits.bias)
+
+    def forward(self, obs):
+        if obs.shape[-1] in (1, 3, 4) and obs.shape[1] not in (1, 3, 4):
+            obs = obs.permute(0, 3, 1, 2)
+        x = obs.to(self.logits.weight.dtype if not torch.is_autocast_enabled() else torch.float32) * (1.0 / 255.0)
+        x = x.contiguous(memory_format=torch.channels_last)
+        h = self.convs(x)
+        if h.shape[-1] != 1 or h.shape[-2] != 1:
+            h = torch.nn.functional.adaptive_avg_pool2d(h, 1)
+        h = h.flatten(1)
+        return self.logits(h), self.value(h).squeeze(-1)
+
+
+def _same_pad(hw, k, s):
+    """Symmetric padding giving TF "same" output size ceil(hw/s) (RLlib SlimConv2d)."""
+    out = -(-hw // s)
+    total = max((out - 1) * s + k - hw, 0)
+    return -(-total // 2)
+
+
+def build_model(obs_space, action_space, model_config=None) -> nn.Module:
+    model_config = model_config or {}
+    n = getattr(action_space, "n", None)
+    if n is None:
+        n = 2 * int(torch.tensor(action_space.shape).prod())  # diag-gaussian mean+logstd
+    shape = tuple(obs_space.shape)
+    if len(shape) == 3:
+        in_ch = shape[0] if shape[0] in (1, 3, 4) and shape[-1] not in (1, 3, 4) else shape[-1]
+        filters = model_config.get("conv_filters") or ((16, 8, 4), (32, 4, 2), (256, 11, 1))
+        filters = [(f[0], f[1] if isinstance(f[1], int) else f[1][0], f[2] if isinstance(f[2], int) else f[2][0])
+                   for f in filters]
+        hw = shape[1] if shape[0] == in_ch else shape[0]
+        return VisionNetwork(n, in_ch, filters, in_hw=hw)
+    obs_dim = int(torch.tensor(shape).prod()) if shape else 1
+    return FullyConnectedNetwork(obs_dim, n, model_config.get("fcnet_hiddens", (256, 256)),
+                                 model_config.get("fcnet_activation", "tanh"),
+                                 model_config.get("vf_share_layers", False))
