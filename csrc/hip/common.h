@@ -1,5 +1,6 @@
 // Shared helpers for the CDNA4 (gfx950) HIP code of ray_memory_management_amd.
 #pragma once
+#include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -145,6 +145,11 @@ PYBIND11_MODULE(_hip, m) {
                           uint64_t stream) {
     gather_rows(P<const void>(in), P<const int64_t>(idx), P<void>(out), rows, row_bytes, S(stream));
   });
+  m.def("frames_to_nhwc_bf16", [](uint64_t src, uint64_t idx, uint64_t dst, int64_t B, int64_t C, int64_t H,
+                                  int64_t W, float scale, uint64_t stream) {
+    frames_to_nhwc_bf16(P<const uint8_t>(src), idx ? P<const int64_t>(idx) : nullptr, P<void>(dst), B, C, H, W,
+                        scale, S(stream));
+  });
   m.def("gae", [](uint64_t rew, uint64_t val, uint64_t done, uint64_t last, uint64_t adv, uint64_t ret,
                   int64_t T, int64_t B, float gamma, float lam, uint64_t stream) {
     gae(P<const float>(rew), P<const float>(val), P<const float>(done), P<const float>(last), P<float>(adv),

@@ -22,6 +22,10 @@ void multi_copy(const std::vector<CopySeg>& segs, hipStream_t stream);
 void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, int64_t row_bytes,
                  hipStream_t stream);
 
+// K2b: uint8 NCHW frames (optionally gathered by idx) -> scaled bf16 NHWC (conv input).
+void frames_to_nhwc_bf16(const uint8_t* src, const int64_t* idx, void* dst, int64_t B, int64_t C, int64_t H,
+                         int64_t W, float scale, hipStream_t stream);
+
 // K3: GAE over time-major [T,B] fp32 tensors. dones is fp32 0/1 (1 = episode ended after t).
 // adv[t] = delta[t] + gamma*lam*(1-d[t])*adv[t+1];  ret = adv + values.
 void gae(const float* rewards, const float* values, const float* dones, const float* last_values,

@@ -158,6 +158,54 @@ void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, in
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+// ============================================================== K2b frames -> NHWC bf16
+
+// dst[b, h, w, c] = bf16(src[idx ? idx[b] : b, c, h, w] * scale). One thread per pixel, C <= 8.
+// Reads are coalesced per channel plane (consecutive w), writes are one 8/16-byte vector per pixel.
+template <int C>
+__global__ __launch_bounds__(256) void k_frames_nhwc(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx,
+                                                    __hip_bfloat16* __restrict__ dst, int64_t B, int64_t HW,
+                                                    float scale) {
+  const int64_t total = B * HW;
+  for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < total;
+       p += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = p / HW, s = p - b * HW;
+    const int64_t sb = idx ? idx[b] : b;
+    const uint8_t* in = src + sb * C * HW + s;
+    unsigned short v[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      __hip_bfloat16 h = __float2bfloat16(float(in[c * HW]) * scale);
+      v[c] = *reinterpret_cast<unsigned short*>(&h);
+    }
+    unsigned short* o = reinterpret_cast<unsigned short*>(dst) + p * C;
+    if constexpr (C == 4) {
+      uint2 w;
+      w.x = uint32_t(v[0]) | (uint32_t(v[1]) << 16);
+      w.y = uint32_t(v[2]) | (uint32_t(v[3]) << 16);
+      *reinterpret_cast<uint2*>(o) = w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; c++) o[c] = v[c];
+    }
+  }
+}
+
+void frames_to_nhwc_bf16(const uint8_t* src, const int64_t* idx, void* dst, int64_t B, int64_t C, int64_t H,
+                         int64_t W, float scale, hipStream_t stream) {
+  int64_t total = B * H * W;
+  if (total <= 0) return;
+  int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 32);
+  auto* d = static_cast<__hip_bfloat16*>(dst);
+  switch (C) {
+    case 1: hipLaunchKernelGGL(k_frames_nhwc<1>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale); break;
+    case 3: hipLaunchKernelGGL(k_frames_nhwc<3>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale); break;
+    case 4: hipLaunchKernelGGL(k_frames_nhwc<4>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale); break;
+    default: throw std::invalid_argument("frames_to_nhwc_bf16: C must be 1, 3 or 4");
+  }
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 // ============================================================== K3 GAE
 
 // Workgroup = 64 envs (one per lane) x C chunks (one wave per chunk), C <= 16.

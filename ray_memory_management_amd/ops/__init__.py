@@ -117,6 +117,25 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def frames_to_nhwc(x: torch.Tensor, idx: torch.Tensor = None, scale: float = 1.0 / 255.0) -> torch.Tensor:
+    """uint8 frames [B, C, H, W] (rows optionally gathered by `idx`) → bf16 scaled, returned as a
+    [B', C, H, W] tensor in channels_last memory (what the NHWC conv kernels consume), one pass."""
+    if x.device.type != "cuda":
+        y = x[idx] if idx is not None else x
+        return (y.float() * scale).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    h = require_hip()
+    x = x.contiguous()
+    B0, C, H, W = x.shape
+    B = idx.numel() if idx is not None else B0
+    out = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=x.device)
+    if idx is not None:
+        idx = idx.to(device=x.device, dtype=torch.int64).contiguous()
+    if B:
+        h.frames_to_nhwc_bf16(x.data_ptr(), idx.data_ptr() if idx is not None else 0, out.data_ptr(), B, C, H, W,
+                              float(scale), _stream(x))
+    return out.permute(0, 3, 1, 2)
+
+
 def gae_reference(rewards, values, dones, last_values, gamma: float, lam: float):
     """Plain fp32 torch GAE over time-major [T, B] tensors (also the CPU path)."""
     T = rewards.shape[0]

@@ -192,10 +192,11 @@ class GPUSyntheticAtariVectorEnv:
         self.episode_len = episode_len
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
-        self.gen = g
         self.pool = torch.randint(0, 256, (64, 84, 84), dtype=torch.uint8, device=self.device, generator=g)
-        self.frames = self.pool[torch.randint(0, 64, (num_envs, 4), device=self.device, generator=g)]
-        self.t = torch.zeros(num_envs, dtype=torch.int32, device=self.device)
+        self.frames = self.pool[torch.randint(0, 64, (num_envs, 4), device=self.device, generator=g)].contiguous()
+        # stagger episode starts so truncations are spread over time
+        self.t = torch.randint(0, episode_len, (num_envs,), dtype=torch.int32, device=self.device, generator=g)
+        self.cols = torch.arange(84, device=self.device)
         self.observation_space = Box(0, 255, shape=(4, 84, 84), dtype=np.uint8)
         self.action_space = Discrete(num_actions)
 
@@ -203,21 +204,22 @@ class GPUSyntheticAtariVectorEnv:
         return self.frames
 
     def step(self, actions):
+        """All state updates are in place and host-sync free, so a step can be captured in a HIP
+        graph (randomness comes from the default, graph-safe generator)."""
         import torch
 
         B = self.num_envs
-        idx = torch.randint(0, 64, (B,), device=self.device, generator=self.gen)
+        idx = torch.randint(0, 64, (B,), device=self.device)
         new = self.pool[idx]
         # action-dependent horizontal shift (cheap stand-in for game dynamics)
         shift = (actions.to(torch.int64) % 4) * 3
-        cols = (torch.arange(84, device=self.device)[None, :] - shift[:, None]) % 84
+        cols = (self.cols[None, :] - shift[:, None]) % 84
         new = torch.gather(new, 2, cols[:, None, :].expand(B, 84, 84))
-        self.frames = torch.cat([self.frames[:, 1:], new[:, None]], dim=1)
-        self.t += 1
-        reward = (torch.rand(B, device=self.device, generator=self.gen) < 0.05).float()
+        self.frames.copy_(torch.cat([self.frames[:, 1:], new[:, None]], dim=1))
+        self.t.add_(1)
+        reward = (torch.rand(B, device=self.device) < 0.05).float()
         done = self.t >= self.episode_len
-        if bool(done.any()):
-            self.t = torch.where(done, torch.zeros_like(self.t), self.t)
+        self.t.masked_fill_(done, 0)
         return self.frames, reward, done.float()
 
 

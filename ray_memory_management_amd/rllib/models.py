@@ -54,11 +54,19 @@ class VisionNetwork(nn.Module):
         layers = []
         c = in_channels
         hw = in_hw
+        self.dense_tail = None
         for i, (out, k, s) in enumerate(filters):
             last = i == len(filters) - 1
             pad = 0 if last else _same_pad(hw, k, s)
-            layers += [nn.Conv2d(c, out, k, s, padding=pad), nn.ReLU()]
-            hw = (hw + 2 * pad - k) // s + 1
+            if last and pad == 0 and k == hw:
+                # A "valid" conv whose kernel covers the whole feature map is a dense layer:
+                # run it as one GEMM on the NHWC-flattened map (hipBLASLt, MFMA) instead of an
+                # implicit-GEMM conv (MIOpen picks a 2 TFLOP/s kernel for its backward on gfx950).
+                self.dense_tail = nn.Linear(c * k * k, out)
+                hw = 1
+            else:
+                layers += [nn.Conv2d(c, out, k, s, padding=pad), nn.ReLU()]
+                hw = (hw + 2 * pad - k) // s + 1
             c = out
         self.out_hw = hw
         self.convs = nn.Sequential(*layers)
@@ -70,12 +78,23 @@ class VisionNetwork(nn.Module):
     def forward(self, obs):
         if obs.shape[-1] in (1, 3, 4) and obs.shape[1] not in (1, 3, 4):
             obs = obs.permute(0, 3, 1, 2)
-        x = obs.to(self.logits.weight.dtype if not torch.is_autocast_enabled() else torch.float32) * (1.0 / 255.0)
-        x = x.contiguous(memory_format=torch.channels_last)
+        bf16_path = obs.is_cuda and obs.dtype == torch.uint8 and obs.is_contiguous() and (
+            torch.is_autocast_enabled() or self.logits.weight.dtype == torch.bfloat16)
+        if bf16_path:
+            from ray_memory_management_amd import ops
+
+            x = ops.frames_to_nhwc(obs)  # fused u8->bf16 scale + NCHW->NHWC (kernel K2b)
+        else:
+            x = obs.to(self.logits.weight.dtype if not torch.is_autocast_enabled() else torch.float32) * (1.0 / 255.0)
+            x = x.contiguous(memory_format=torch.channels_last)
         h = self.convs(x)
-        if h.shape[-1] != 1 or h.shape[-2] != 1:
-            h = torch.nn.functional.adaptive_avg_pool2d(h, 1)
-        h = h.flatten(1)
+        if self.dense_tail is not None:
+            # NHWC memory: permute+reshape is a view, the GEMM reads the map in place
+            h = torch.relu(self.dense_tail(h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)))
+        else:
+            if h.shape[-1] != 1 or h.shape[-2] != 1:
+                h = torch.nn.functional.adaptive_avg_pool2d(h, 1)
+            h = h.flatten(1)
         return self.logits(h), self.value(h).squeeze(-1)
 
 

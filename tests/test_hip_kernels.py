@@ -129,3 +129,17 @@ def test_ppo_loss_matches_reference(cuda):
     torch.testing.assert_close(means, rmeans, rtol=1e-4, atol=1e-5)
     for a, b in zip(g1, (ln.grad, vn.grad, ent.grad)):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("C", [1, 3, 4])
+def test_frames_to_nhwc(cuda, C):
+    from ray_memory_management_amd import ops
+
+    x = torch.randint(0, 256, (37, C, 84, 84), dtype=torch.uint8, device=cuda)
+    ref = (x.float() / 255.0).to(torch.bfloat16)
+    y = ops.frames_to_nhwc(x)
+    assert y.is_contiguous(memory_format=torch.channels_last) or C == 1
+    assert torch.equal(y.contiguous(), ref)
+    idx = torch.randint(0, 37, (11,), device=cuda)
+    y2 = ops.frames_to_nhwc(x, idx)
+    assert torch.equal(y2.contiguous(), ref[idx])
