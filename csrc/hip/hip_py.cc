@@ -175,6 +175,28 @@ PYBIND11_MODULE(_hip, m) {
                  P<float>(g_ent), P<float>(stats), n, clip, vf_clip, vf_coeff, ent_coeff, S(stream));
   });
 
+  m.def("ppo_cat_loss", [](bool fwd, uint64_t logits, bool logits_bf16, uint64_t old_logits, uint64_t actions,
+                           uint64_t old_logp, uint64_t adv, uint64_t values, bool values_bf16, uint64_t vtgt,
+                           uint64_t coef, uint64_t stats, uint64_t gout, uint64_t g_logits, uint64_t g_values,
+                           int64_t N, int A, uint64_t stream) {
+    ppo_cat_loss(fwd, P<const void>(logits), logits_bf16, P<const float>(old_logits), P<const int64_t>(actions),
+                 P<const float>(old_logp), P<const float>(adv), P<const void>(values), values_bf16, P<const float>(vtgt),
+                 P<const float>(coef), P<float>(stats), P<const float>(gout), P<void>(g_logits), P<void>(g_values), N,
+                 A, S(stream));
+  });
+  m.def("adam_flat", [](uint64_t master, uint64_t m1, uint64_t m2, uint64_t grad, bool grad_bf16, uint64_t wbf16,
+                        uint64_t hp, float grad_scale, int64_t n, uint64_t stream) {
+    adam_flat(P<float>(master), P<float>(m1), P<float>(m2), P<const void>(grad), grad_bf16,
+              wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream));
+  });
+  m.def("sample_store", [](uint64_t logits, bool logits_bf16, uint64_t values, bool values_bf16, uint64_t t_ptr,
+                           uint64_t ctr, uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
+                           uint64_t act_now, int64_t B, int A, uint64_t stream) {
+    sample_store(P<const void>(logits), logits_bf16, P<const void>(values), values_bf16, P<const int64_t>(t_ptr),
+                 P<const int64_t>(ctr), seed, P<int64_t>(act), P<float>(logp), P<float>(vf), P<float>(lout),
+                 P<int64_t>(act_now), B, A, S(stream));
+  });
+
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {
     std::string h = handle;

@@ -53,5 +53,20 @@ void ppo_loss_fwd(const float* logp_new, const float* logp_old, const float* adv
                   float* grad_logp, float* grad_v, float* grad_ent, float* stats, int64_t n,
                   float clip, float vf_clip, float vf_coeff, float ent_coeff, hipStream_t stream);
 
+// K5b: whole categorical PPO loss head (fwd: stats; bwd: d/dlogits, d/dvalues scaled by *gout).
+void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* old_logits, const int64_t* actions,
+                  const float* old_logp, const float* adv, const void* values, bool values_bf16, const float* vtgt,
+                  const float* coef, float* stats, const float* gout, void* g_logits, void* g_values, int64_t N,
+                  int A, hipStream_t stream);
+
+// K6: flat Adam/AdamW with fp32 master weights, bf16 or fp32 grads, optional bf16 weight output.
+void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
+               float grad_scale, int64_t n, hipStream_t stream);
+
+// K7: Gumbel-max categorical sampling + rollout buffer writes at device-side row *t_ptr.
+void sample_store(const void* logits, bool logits_bf16, const void* values, bool values_bf16, const int64_t* t_ptr,
+                  const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf, float* lout,
+                  int64_t* act_now, int64_t B, int A, hipStream_t stream);
+
 }  // namespace hip
 }  // namespace rmm

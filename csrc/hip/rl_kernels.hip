@@ -1,0 +1,295 @@
+// Fused RL kernels for the PPO learner on CDNA4 (gfx950).
+//
+//  K5b ppo_cat_fwd / ppo_cat_bwd — the WHOLE categorical PPO loss head in two launches:
+//        log-softmax, log p(a), entropy, KL(old||new), ratio, clipped surrogate, clipped value
+//        loss, stats reduction (fwd) and d/dlogits, d/dvalue scaled by the upstream gradient read
+//        from device memory (bwd). Replaces ~30 PyTorch elementwise/reduction launches per step.
+//        Parity: reference rllib/algorithms/ppo/ppo_torch_policy.py:loss (+ TorchCategorical).
+//  K6  adam_flat — Adam over ONE flat fp32 master buffer with bf16 gradients in, bf16 weights
+//        out (the compute copy the model reads), bias correction from a device step counter:
+//        the whole optimizer step is one launch and graph-capturable.
+//  K7  sample_store — Gumbel-max categorical sampling with a stateless counter-based hash RNG,
+//        writes action / log p(a) / value / logits straight into the rollout buffers at row t
+//        read from device memory (HIP-graph friendly).
+//
+// Small-A categorical heads (A <= 32): one thread per sample, logits held in registers.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace rmm {
+namespace hip {
+
+constexpr int kMaxA = 32;
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, int64_t i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<__hip_bfloat16>(const __hip_bfloat16* p, int64_t i) {
+  return __bfloat162float(p[i]);
+}
+template <typename T>
+__device__ __forceinline__ void stf(T* p, int64_t i, float v);
+template <>
+__device__ __forceinline__ void stf<float>(float* p, int64_t i, float v) { p[i] = v; }
+template <>
+__device__ __forceinline__ void stf<__hip_bfloat16>(__hip_bfloat16* p, int64_t i, float v) {
+  p[i] = __float2bfloat16(v);
+}
+
+// coef layout (device): [clip, vf_clip, vf_coeff, ent_coeff, kl_coeff]
+// stats layout: [sum(-surr), sum(vf_clipped), sum(entropy), sum(kl), sum(clipped), sum(total)]
+template <typename TL, typename TV>
+__global__ __launch_bounds__(256) void k_ppo_cat_fwd(const TL* __restrict__ logits, const float* __restrict__ old_logits,
+                                                    const int64_t* __restrict__ actions,
+                                                    const float* __restrict__ old_logp, const float* __restrict__ adv,
+                                                    const TV* __restrict__ values, const float* __restrict__ vtgt,
+                                                    const float* __restrict__ coef, float* __restrict__ stats,
+                                                    int64_t N, int A) {
+  const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
+  float s[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += int64_t(gridDim.x) * blockDim.x) {
+    float l[kMaxA], lo[kMaxA];
+    float mx = -INFINITY, mxo = -INFINITY;
+    for (int j = 0; j < A; j++) {
+      l[j] = ldf(logits, i * A + j);
+      lo[j] = old_logits[i * A + j];
+      mx = fmaxf(mx, l[j]);
+      mxo = fmaxf(mxo, lo[j]);
+    }
+    float se = 0.f, seo = 0.f;
+    for (int j = 0; j < A; j++) {
+      se += __expf(l[j] - mx);
+      seo += __expf(lo[j] - mxo);
+    }
+    const float lse = mx + __logf(se), lseo = mxo + __logf(seo);
+    float m = 0.f, kl = 0.f;
+    for (int j = 0; j < A; j++) {
+      const float p = __expf(l[j] - lse), po = __expf(lo[j] - lseo);
+      m += p * l[j];
+      kl += po * ((lo[j] - lseo) - (l[j] - lse));
+    }
+    const float ent = lse - m;
+    const int a = int(actions[i]);
+    const float logp = l[a] - lse;
+    const float r = __expf(logp - old_logp[i]);
+    const float ad = adv[i];
+    const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
+    const float surr = fminf(r * ad, rc * ad);
+    const float d = ldf(values, i) - vtgt[i];
+    const float vf = fminf(d * d, vf_clip);
+    s[0] += -surr;
+    s[1] += vf;
+    s[2] += ent;
+    s[3] += kl;
+    s[4] += (fabsf(r - 1.f) > clip) ? 1.f : 0.f;
+    s[5] += -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_xor(s[k], o, 64);
+  __shared__ float red[6][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0)
+    for (int k = 0; k < 6; k++) red[k][w] = s[k];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float t = 0.f;
+    for (int k = 0; k < int(blockDim.x >> 6); k++) t += red[threadIdx.x][k];
+    atomicAdd(&stats[threadIdx.x], t);
+  }
+}
+
+template <typename TL, typename TV>
+__global__ __launch_bounds__(256) void k_ppo_cat_bwd(const TL* __restrict__ logits, const float* __restrict__ old_logits,
+                                                    const int64_t* __restrict__ actions,
+                                                    const float* __restrict__ old_logp, const float* __restrict__ adv,
+                                                    const TV* __restrict__ values, const float* __restrict__ vtgt,
+                                                    const float* __restrict__ coef, const float* __restrict__ gout,
+                                                    TL* __restrict__ g_logits, TV* __restrict__ g_values, int64_t N,
+                                                    int A) {
+  const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
+  const float gs = gout[0] / float(N);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += int64_t(gridDim.x) * blockDim.x) {
+    float l[kMaxA], lo[kMaxA];
+    float mx = -INFINITY, mxo = -INFINITY;
+    for (int j = 0; j < A; j++) {
+      l[j] = ldf(logits, i * A + j);
+      lo[j] = old_logits[i * A + j];
+      mx = fmaxf(mx, l[j]);
+      mxo = fmaxf(mxo, lo[j]);
+    }
+    float se = 0.f, seo = 0.f;
+    for (int j = 0; j < A; j++) {
+      se += __expf(l[j] - mx);
+      seo += __expf(lo[j] - mxo);
+    }
+    const float lse = mx + __logf(se), lseo = mxo + __logf(seo);
+    float m = 0.f;
+    for (int j = 0; j < A; j++) m += __expf(l[j] - lse) * l[j];
+    const int a = int(actions[i]);
+    const float logp = l[a] - lse;
+    const float r = __expf(logp - old_logp[i]);
+    const float ad = adv[i];
+    const bool unclipped = r * ad <= fminf(fmaxf(r, 1.f - clip), 1.f + clip) * ad;
+    const bool inside = (r >= 1.f - clip) && (r <= 1.f + clip);
+    const float spg = (unclipped || inside) ? -(r * ad) : 0.f;  // d(-surr)/d logp
+    for (int j = 0; j < A; j++) {
+      const float p = __expf(l[j] - lse), po = __expf(lo[j] - lseo);
+      const float g = spg * ((j == a ? 1.f : 0.f) - p) + ent_coeff * p * (l[j] - m) + kl_coeff * (p - po);
+      stf(g_logits, i * A + j, g * gs);
+    }
+    const float d = ldf(values, i) - vtgt[i];
+    stf(g_values, i, (d * d < vf_clip) ? vf_coeff * 2.f * d * gs : 0.f);
+  }
+}
+
+void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* old_logits, const int64_t* actions,
+                  const float* old_logp, const float* adv, const void* values, bool values_bf16, const float* vtgt,
+                  const float* coef, float* stats, const float* gout, void* g_logits, void* g_values, int64_t N,
+                  int A, hipStream_t stream) {
+  if (A > kMaxA) throw std::invalid_argument("ppo_cat_loss: at most 32 actions");
+  if (N <= 0) return;
+  int64_t blocks = std::min<int64_t>((N + 255) / 256, 1024);
+  using bf = __hip_bfloat16;
+#define RMM_PPO_LAUNCH(TL, TV)                                                                                    \
+  if (fwd)                                                                                                       \
+    hipLaunchKernelGGL((k_ppo_cat_fwd<TL, TV>), dim3(uint32_t(blocks)), dim3(256), 0, stream,                   \
+                       static_cast<const TL*>(logits), old_logits, actions, old_logp, adv,                       \
+                       static_cast<const TV*>(values), vtgt, coef, stats, N, A);                                 \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_ppo_cat_bwd<TL, TV>), dim3(uint32_t(blocks)), dim3(256), 0, stream,                   \
+                       static_cast<const TL*>(logits), old_logits, actions, old_logp, adv,                       \
+                       static_cast<const TV*>(values), vtgt, coef, gout, static_cast<TL*>(g_logits),             \
+                       static_cast<TV*>(g_values), N, A);
+  if (logits_bf16 && values_bf16) {
+    RMM_PPO_LAUNCH(bf, bf)
+  } else if (logits_bf16) {
+    RMM_PPO_LAUNCH(bf, float)
+  } else if (values_bf16) {
+    RMM_PPO_LAUNCH(float, bf)
+  } else {
+    RMM_PPO_LAUNCH(float, float)
+  }
+#undef RMM_PPO_LAUNCH
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+// ============================================================== K6 flat Adam (fp32 master -> bf16 weights)
+
+// hp layout (device): [lr, beta1, beta2, eps, weight_decay, step]; step is incremented by the caller
+// before the launch (a 1-element add in the same stream / graph).
+template <typename TG>
+__global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, float* __restrict__ m1,
+                                                  float* __restrict__ m2, const TG* __restrict__ grad,
+                                                  __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
+                                                  float grad_scale, int64_t n) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], step = hp[5];
+  const float bc1 = 1.f - __powf(b1, step), bc2 = 1.f - __powf(b2, step);
+  const float step_size = lr / bc1;
+  const float bc2_sqrt = sqrtf(bc2);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    float g = ldf(grad, i) * grad_scale;
+    float w = master[i];
+    if (wd != 0.f) w -= lr * wd * w;  // decoupled (AdamW) decay
+    const float a = b1 * m1[i] + (1.f - b1) * g;
+    const float b = b2 * m2[i] + (1.f - b2) * g * g;
+    m1[i] = a;
+    m2[i] = b;
+    w -= step_size * a / (sqrtf(b) / bc2_sqrt + eps);
+    master[i] = w;
+    if (wbf16) wbf16[i] = __float2bfloat16(w);
+  }
+}
+
+void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
+               float grad_scale, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 8);
+  if (grad_bf16)
+    hipLaunchKernelGGL(k_adam_flat<__hip_bfloat16>, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2,
+                       static_cast<const __hip_bfloat16*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n);
+  else
+    hipLaunchKernelGGL(k_adam_flat<float>, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2,
+                       static_cast<const float*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+// ============================================================== K7 sample + store
+
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  // counter-based mix (murmur3 finaliser over three words)
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+// logits [B, A] (TL), values [B] (TV); writes row t (=*t_ptr) of act [T,B], logp [T,B], vf [T,B],
+// logits_out [T,B,A]; rng: uniform from hash(seed, counter, b*A+j); counter = *ctr (advanced by caller).
+template <typename TL, typename TV>
+__global__ __launch_bounds__(256) void k_sample_store(const TL* __restrict__ logits, const TV* __restrict__ values,
+                                                     const int64_t* __restrict__ t_ptr, const int64_t* __restrict__ ctr,
+                                                     uint32_t seed, int64_t* __restrict__ act, float* __restrict__ logp,
+                                                     float* __restrict__ vf, float* __restrict__ lout,
+                                                     int64_t* __restrict__ act_now, int64_t B, int A) {
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
+  for (int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; b < B; b += int64_t(gridDim.x) * blockDim.x) {
+    float best = -INFINITY, mx = -INFINITY;
+    int arg = 0;
+    float l[kMaxA];
+    for (int j = 0; j < A; j++) {
+      l[j] = ldf(logits, b * A + j);
+      mx = fmaxf(mx, l[j]);
+      const uint32_t h = hash3(seed, c, uint32_t(b * A + j));
+      const float u = (float(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float gmb = l[j] - __logf(-__logf(u));
+      if (gmb > best) {
+        best = gmb;
+        arg = j;
+      }
+    }
+    float se = 0.f;
+    for (int j = 0; j < A; j++) se += __expf(l[j] - mx);
+    const int64_t o = t * B + b;
+    act[o] = arg;
+    act_now[b] = arg;
+    logp[o] = l[arg] - mx - __logf(se);
+    vf[o] = ldf(values, b);
+    for (int j = 0; j < A; j++) lout[o * A + j] = l[j];
+  }
+}
+
+void sample_store(const void* logits, bool logits_bf16, const void* values, bool values_bf16, const int64_t* t_ptr,
+                  const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf, float* lout,
+                  int64_t* act_now, int64_t B, int A, hipStream_t stream) {
+  if (A > kMaxA) throw std::invalid_argument("sample_store: at most 32 actions");
+  int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((B + 255) / 256, 1024));
+  using bf = __hip_bfloat16;
+#define RMM_SS(TL, TV)                                                                                          \
+  hipLaunchKernelGGL((k_sample_store<TL, TV>), dim3(uint32_t(blocks)), dim3(256), 0, stream,                   \
+                     static_cast<const TL*>(logits), static_cast<const TV*>(values), t_ptr, ctr, seed, act, logp, vf, \
+                     lout, act_now, B, A);
+  if (logits_bf16 && values_bf16) {
+    RMM_SS(bf, bf)
+  } else if (logits_bf16) {
+    RMM_SS(bf, float)
+  } else if (values_bf16) {
+    RMM_SS(float, bf)
+  } else {
+    RMM_SS(float, float)
+  }
+#undef RMM_SS
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace rmm

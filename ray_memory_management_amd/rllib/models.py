@@ -75,7 +75,11 @@ class VisionNetwork(nn.Module):
         nn.init.orthogonal_(self.logits.weight, 0.01)
         nn.init.zeros_(self.logits.bias)
 
-    def forward(self, obs):
+    def forward(self, obs, prescaled: bool = False):
+        """obs: uint8 frames [B,C,H,W] / [B,H,W,C], or (prescaled=True) an already scaled bf16/fp32
+        [B,C,H,W] tensor such as ops.frames_to_nhwc() returns."""
+        if prescaled:
+            return self._trunk(obs)
         if obs.shape[-1] in (1, 3, 4) and obs.shape[1] not in (1, 3, 4):
             obs = obs.permute(0, 3, 1, 2)
         bf16_path = obs.is_cuda and obs.dtype == torch.uint8 and obs.is_contiguous() and (
@@ -87,6 +91,9 @@ class VisionNetwork(nn.Module):
         else:
             x = obs.to(self.logits.weight.dtype if not torch.is_autocast_enabled() else torch.float32) * (1.0 / 255.0)
             x = x.contiguous(memory_format=torch.channels_last)
+        return self._trunk(x)
+
+    def _trunk(self, x):
         h = self.convs(x)
         if self.dense_tail is not None:
             # NHWC memory: permute+reshape is a view, the GEMM reads the map in place

@@ -6,15 +6,19 @@ value loss, entropy bonus, KL penalty with adaptive coefficient), rllib/algorith
 rllib/execution/multi_gpu_learner_thread.py + train_ops.multi_gpu_train_one_step (multi-GPU
 learner).
 
-MI355X design:
-  * one learner process per GPU; gradients live in ONE flat fp32 bucket (every ``p.grad`` is a view
-    into it) so the data-parallel sync is a single RCCL all-reduce per minibatch step over xGMI —
-    the Atari net is ~1M params (4 MB), far below where splitting buckets pays on a 7-link ring;
-  * the batch stays in HBM: minibatches are gathered on-device (K2), frames converted to bf16 NHWC by
-    K2b, GAE by K3, the PPO loss + its gradient by the fused K5 kernel, bf16 autocast convolutions;
-  * launch overhead is removed with HIP graphs: one graph per rollout step (policy forward, action
-    sampling, env step, writes into the [T, B] buffers at a device-side step counter) and one per SGD
-    step (zero grads, gather, forward, fused loss, backward, [all-reduce], capturable fused Adam).
+MI355X design (fast path, ``device.type == "cuda"``):
+  * mixed precision with fp32 MASTER weights: the model holds bf16 compute weights (no autocast
+    casts per forward); one flat fp32 master / Adam-moment buffer; the whole optimizer step is one
+    launch of the K6 kernel, which also rewrites the bf16 weights in place;
+  * gradients land in ONE flat bf16 bucket (one multi-segment copy launch, K1) so the data-parallel
+    sync is a single RCCL all-reduce per minibatch step over xGMI — the Atari net is ~1M params;
+  * minibatch gather + uint8→bf16 NHWC conversion in one launch (K2b), the remaining columns packed
+    into one fp32 matrix and gathered in one launch (K2);
+  * the whole categorical PPO loss head (log-softmax, logp, entropy, KL, ratio/clip, value clip, stats)
+    forward and backward are one launch each (K5b);
+  * rollout: Gumbel-max sampling + buffer writes at a device-side step counter in one launch (K7);
+  * every rollout step and every SGD step is one HIP-graph replay.
+The CPU path (rollout workers without GPUs, tests) is plain fp32 PyTorch with the same math.
 """
 from __future__ import annotations
 
@@ -25,22 +29,77 @@ import torch
 import torch.nn as nn
 
 from ray_memory_management_amd import ops
+from ray_memory_management_amd._native import require_hip
 from ray_memory_management_amd.rllib.distributions import Categorical, dist_class_for
 from ray_memory_management_amd.rllib.sample_batch import SampleBatch
 
 DEFAULT_PPO = dict(
     gamma=0.99, lambda_=0.95, kl_coeff=0.5, kl_target=0.01, clip_param=0.1, vf_clip_param=10.0,
     vf_loss_coeff=1.0, entropy_coeff=0.01, lr=5e-5, train_batch_size=5000, sgd_minibatch_size=500,
-    num_sgd_iter=10, grad_clip=None, use_fused_loss=True, bf16=True, standardize_advantages=True,
-    use_graphs=True, allreduce_in_graph=True,
+    num_sgd_iter=10, grad_clip=None, standardize_advantages=True, use_graphs=True, fused=True,
+    allreduce_in_graph=True, adam_betas=(0.9, 0.999), adam_eps=1e-8, weight_decay=0.0,
 )
 
 _LOSS_KEYS = (SampleBatch.OBS, SampleBatch.ACTIONS, SampleBatch.ACTION_LOGP, SampleBatch.ACTION_DIST_INPUTS,
               SampleBatch.ADVANTAGES, SampleBatch.VALUE_TARGETS)
 
 
-def _graphs_enabled(cfg, device) -> bool:
-    return bool(cfg.get("use_graphs")) and device.type == "cuda" and not os.environ.get("RMM_NO_GRAPHS")
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class _CatPPOLoss(torch.autograd.Function):
+    """K5b: the categorical PPO loss head; forward = stats, backward = d/dlogits, d/dvalues."""
+
+    @staticmethod
+    def forward(ctx, logits, values, old_logits, actions, old_logp, adv, vtgt, coef):
+        h = require_hip()
+        N, A = logits.shape
+        stats = torch.zeros(6, dtype=torch.float32, device=logits.device)
+        h.ppo_cat_loss(True, logits.data_ptr(), logits.dtype == torch.bfloat16, old_logits.data_ptr(),
+                       actions.data_ptr(), old_logp.data_ptr(), adv.data_ptr(), values.data_ptr(),
+                       values.dtype == torch.bfloat16, vtgt.data_ptr(), coef.data_ptr(), stats.data_ptr(), 0, 0, 0,
+                       N, A, _stream())
+        ctx.save_for_backward(logits, values, old_logits, actions, old_logp, adv, vtgt, coef)
+        total = stats[5] / N
+        ctx.mark_non_differentiable(stats)
+        return total, stats
+
+    @staticmethod
+    def backward(ctx, g_total, g_stats):
+        h = require_hip()
+        logits, values, old_logits, actions, old_logp, adv, vtgt, coef = ctx.saved_tensors
+        N, A = logits.shape
+        g_logits = torch.empty_like(logits)
+        g_values = torch.empty_like(values)
+        g = g_total.reshape(1).float().contiguous()
+        h.ppo_cat_loss(False, logits.data_ptr(), logits.dtype == torch.bfloat16, old_logits.data_ptr(),
+                       actions.data_ptr(), old_logp.data_ptr(), adv.data_ptr(), values.data_ptr(),
+                       values.dtype == torch.bfloat16, vtgt.data_ptr(), coef.data_ptr(), 0, g.data_ptr(),
+                       g_logits.data_ptr(), g_values.data_ptr(), N, A, _stream())
+        return g_logits, g_values, None, None, None, None, None, None
+
+
+def ppo_categorical_loss(logits, values, old_logits, actions, old_logp, adv, vtgt, coef):
+    """Fused categorical PPO loss. coef = device tensor [clip, vf_clip, vf_coeff, ent_coeff, kl_coeff].
+    Returns (total, stats[6] = sums of -surr, vf, entropy, kl, clipped, total)."""
+    return _CatPPOLoss.apply(logits.contiguous(), values.contiguous(), old_logits.contiguous(), actions.contiguous(),
+                             old_logp.contiguous(), adv.contiguous(), vtgt.contiguous(), coef)
+
+
+def ppo_categorical_loss_reference(logits, values, old_logits, actions, old_logp, adv, vtgt, coef):
+    clip, vf_clip, vf_coeff, ent_coeff, kl_coeff = [float(x) for x in coef.tolist()]
+    d, old = Categorical(logits.float()), Categorical(old_logits.float())
+    logp = d.logp(actions)
+    ent = d.entropy()
+    kl = old.kl(d)
+    ratio = torch.exp(logp - old_logp)
+    surr = torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip))
+    vf = torch.clamp((values.float() - vtgt) ** 2, max=vf_clip)
+    per = -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl
+    stats = torch.stack([(-surr).sum(), vf.sum(), ent.sum(), kl.sum(), ((ratio - 1).abs() > clip).float().sum(),
+                         per.sum()]).detach()
+    return per.mean(), stats
 
 
 class PPOLearner:
@@ -48,123 +107,129 @@ class PPOLearner:
                  action_space=None):
         self.cfg = {**DEFAULT_PPO, **(config or {})}
         self.device = torch.device(device)
-        self.model = model.to(self.device)
-        if self.device.type == "cuda":
-            self.model = self.model.to(memory_format=torch.channels_last)
         self.dist_cls = dist_class_for(action_space) if action_space is not None else Categorical
+        self.fast = (self.device.type == "cuda" and bool(self.cfg["fused"]) and self.dist_cls is Categorical)
         self.pg = process_group
         self.world = 1
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world = torch.distributed.get_world_size(process_group)
-        params = [p for p in self.model.parameters() if p.requires_grad]
-        self.params = params
+        model = model.to(self.device)
+        if self.device.type == "cuda":
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
+        params = [p for p in model.parameters() if p.requires_grad]
         if self.world > 1:  # identical initial weights: broadcast rank 0's
             with torch.no_grad():
-                flat = torch.cat([p.detach().reshape(-1) for p in params])
-                torch.distributed.broadcast(flat, src=torch.distributed.get_global_rank(process_group, 0)
-                                            if process_group is not None else 0, group=process_group)
+                flat = torch.cat([p.detach().float().reshape(-1) for p in params])
+                src = torch.distributed.get_global_rank(process_group, 0) if process_group is not None else 0
+                torch.distributed.broadcast(flat, src=src, group=process_group)
                 off = 0
                 for p in params:
-                    p.copy_(flat[off:off + p.numel()].view_as(p))
+                    p.copy_(flat[off:off + p.numel()].view(p.shape))
                     off += p.numel()
-        # one flat gradient bucket
-        n = sum(p.numel() for p in params)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
-        off = 0
-        for p in params:
-            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        self.graphs = _graphs_enabled(self.cfg, self.device)
-        kw = {"lr": self.cfg["lr"]}
-        if self.device.type == "cuda":
-            kw["fused"] = True
-            if self.graphs:
-                kw["capturable"] = True
-        try:
-            self.opt = torch.optim.Adam(params, **kw)
-        except (TypeError, RuntimeError, ValueError):
-            kw.pop("fused", None)
-            self.opt = torch.optim.Adam(params, **kw)
         self.kl_coeff = float(self.cfg["kl_coeff"])
-        self.kl_coeff_t = torch.tensor(self.kl_coeff, device=self.device)
-        self.acc = torch.zeros(5, device=self.device)
         self.stats: Dict[str, float] = {}
         self._graph = None
         self._static = None
-        self._sidx = None
         self._mbs = None
-
-    # ------------------------------------------------------------------ loss
-    def _forward(self, obs):
-        if self.cfg["bf16"] and self.device.type == "cuda":
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                logits, v = self.model(obs)
-            return logits.float(), v.float()
-        return self.model(obs)
-
-    def loss(self, mb):
-        c = self.cfg
-        logits, v = self._forward(mb[SampleBatch.OBS])
-        dist = self.dist_cls(logits)
-        old = self.dist_cls(mb[SampleBatch.ACTION_DIST_INPUTS])
-        logp = dist.logp(mb[SampleBatch.ACTIONS])
-        ent = dist.entropy()
-        kl = old.kl(dist).mean()
-        if c["use_fused_loss"] and self.device.type == "cuda":
-            total, means = ops.ppo_loss(logp, mb[SampleBatch.ACTION_LOGP], mb[SampleBatch.ADVANTAGES], v,
-                                        mb[SampleBatch.VALUE_TARGETS], ent, c["clip_param"], c["vf_clip_param"],
-                                        c["vf_loss_coeff"], c["entropy_coeff"])
+        if self.fast:
+            self._init_fast(params)
         else:
-            total, means = ops.ppo_loss_reference(logp, mb[SampleBatch.ACTION_LOGP], mb[SampleBatch.ADVANTAGES], v,
-                                                  mb[SampleBatch.VALUE_TARGETS], ent, c["clip_param"],
-                                                  c["vf_clip_param"], c["vf_loss_coeff"], c["entropy_coeff"])
-        total = total + self.kl_coeff_t * kl
-        return total, means, kl
+            self.params = params
+            self.opt = torch.optim.Adam(params, lr=self.cfg["lr"], betas=self.cfg["adam_betas"],
+                                        eps=self.cfg["adam_eps"], weight_decay=self.cfg["weight_decay"])
+        self.graphs = self.fast and bool(self.cfg["use_graphs"]) and not os.environ.get("RMM_NO_GRAPHS")
 
-    # ------------------------------------------------------------------ one SGD step
-    def _allreduce(self):
-        torch.distributed.all_reduce(self.flat_grad, group=self.pg)
-        self.flat_grad.mul_(1.0 / self.world)
+    # ------------------------------------------------------------------ fast-path state
+    def _init_fast(self, params):
+        dev = self.device
+        n = sum(p.numel() for p in params)
+        self.n_params = n
+        # fp32 master + moments (flat), bf16 compute weights (flat; params become views into it)
+        self.master = torch.empty(n, dtype=torch.float32, device=dev)
+        self.w_bf16 = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        off = 0
+        self.params = []
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                # lay the master out in the param's MEMORY order so one flat kernel updates both
+                self.master.as_strided(p.size(), p.stride(), off).copy_(p.detach().float())
+                view = self.w_bf16.as_strided(p.size(), p.stride(), off)
+                view.copy_(p.detach())
+                p.data = view
+                self.params.append(p)
+                off += k
+        self.m1 = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.m2 = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        b1, b2 = self.cfg["adam_betas"]
+        self.hp = torch.tensor([self.cfg["lr"], b1, b2, self.cfg["adam_eps"], self.cfg["weight_decay"], 0.0],
+                               dtype=torch.float32, device=dev)
+        self.coef = torch.tensor([self.cfg["clip_param"], self.cfg["vf_clip_param"], self.cfg["vf_loss_coeff"],
+                                  self.cfg["entropy_coeff"], self.kl_coeff], dtype=torch.float32, device=dev)
+        self.acc = torch.zeros(6, device=dev)
+        self._grad_segs = None
 
-    def _step_body(self, full, idx, with_sync: bool):
-        self.flat_grad.zero_()
-        mb = {k: ops.gather_rows(full[k], idx) for k in _LOSS_KEYS}
-        total, means, kl = self.loss(mb)
-        total.backward()
-        if with_sync:
-            if self.world > 1:
-                self._allreduce()
-            if self.cfg["grad_clip"]:
-                nn.utils.clip_grad_norm_(self.params, self.cfg["grad_clip"])
-            self.opt.step()
-        self.acc += torch.cat([total.detach().reshape(1), means[:3].detach(), kl.detach().reshape(1)])
+    def _opt_step(self):
+        h = require_hip()
+        if self.world > 1:
+            torch.distributed.all_reduce(self.flat_grad, group=self.pg)
+        self.hp[5:6].add_(1.0)
+        h.adam_flat(self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
+                    self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream())
 
-    def _eager_step(self, full, idx):
-        self._step_body(full, idx, True)
+    def _fast_step(self, full, idx, with_opt: bool):
+        h = require_hip()
+        x = ops.frames_to_nhwc(full["obs"], idx)            # K2b: gather + u8→bf16 NHWC
+        cols = ops.gather_rows(full["cols"], idx)            # K2: one gather for all float columns
+        act = ops.gather_rows(full["actions"], idx)
+        A = full["A"]
+        old_logits = cols[:, :A]
+        old_logp, adv, vtgt = cols[:, A], cols[:, A + 1], cols[:, A + 2]
+        logits, v = self.model(x, prescaled=True)
+        total, stats = ppo_categorical_loss(logits, v, old_logits, act, old_logp, adv, vtgt, self.coef)
+        grads = list(torch.autograd.grad(total, self.params))
+        for i, (g, p) in enumerate(zip(grads, self.params)):
+            if g.stride() != p.stride() and g.numel() > 1:  # match the flat bucket's memory order
+                grads[i] = torch.empty_strided(p.size(), p.stride(), dtype=g.dtype, device=g.device).copy_(g)
+        segs = []
+        off = 0
+        for g, p in zip(grads, self.params):
+            nb = g.numel() * 2
+            segs.append((g.data_ptr(), self.flat_grad.data_ptr() + off * 2, nb))
+            off += p.numel()
+        h.multi_copy(segs, _stream())                        # K1: grads → one flat bucket
+        self.acc.add_(stats)
+        if with_opt:
+            self._opt_step()
+
+    def _pack(self, batch):
+        A = batch[SampleBatch.ACTION_DIST_INPUTS].shape[-1]
+        cols = torch.cat([batch[SampleBatch.ACTION_DIST_INPUTS].float(),
+                          batch[SampleBatch.ACTION_LOGP].float().unsqueeze(1),
+                          batch[SampleBatch.ADVANTAGES].float().unsqueeze(1),
+                          batch[SampleBatch.VALUE_TARGETS].float().unsqueeze(1)], dim=1).contiguous()
+        return {"obs": batch[SampleBatch.OBS].contiguous(), "cols": cols,
+                "actions": batch[SampleBatch.ACTIONS].to(torch.int64).contiguous(), "A": A}
 
     def _capture(self, full, mbs):
-        in_graph_sync = self.world == 1 or self.cfg["allreduce_in_graph"]
+        in_graph_opt = self.world == 1 or self.cfg["allreduce_in_graph"]
         self._sidx = torch.arange(mbs, device=self.device, dtype=torch.int64)
+        saved = (self.master.clone(), self.m1.clone(), self.m2.clone(), self.hp.clone(), self.w_bf16.clone())
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        saved = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
-        saved_opt = None
         with torch.cuda.stream(s):
-            for _ in range(3):  # warm up kernels / MIOpen find / allocator before capture
-                self._step_body(full, self._sidx, in_graph_sync)
+            for _ in range(3):  # warm up (MIOpen find, allocator) before capture
+                self._fast_step(full, self._sidx, in_graph_opt)
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._step_body(full, self._sidx, in_graph_sync)
-        # undo the warm-up/capture updates (capture does not execute, warm-up did)
-        with torch.no_grad():
-            self.model.load_state_dict(saved)
-        for st in self.opt.state.values():
-            for k, v in st.items():
-                if torch.is_tensor(v):
-                    v.zero_()
+            self._fast_step(full, self._sidx, in_graph_opt)
+        for dst, src in zip((self.master, self.m1, self.m2, self.hp, self.w_bf16), saved):
+            dst.copy_(src)  # undo warm-up updates
         self._graph = g
-        self._graph_sync = in_graph_sync
+        self._graph_opt = in_graph_opt
         self._mbs = mbs
 
     # ------------------------------------------------------------------ update
@@ -177,70 +242,121 @@ class PPOLearner:
         n = batch.count
         mbs = min(c["sgd_minibatch_size"], n)
         nmb = max(n // mbs, 1)
-        use_graph = self.graphs
-        if use_graph:
-            if self._static is None or self._static[SampleBatch.OBS].shape != batch[SampleBatch.OBS].shape:
-                self._static = {k: batch[k].detach().clone() for k in _LOSS_KEYS}
+        if not self.fast:
+            return self._update_eager(batch, mbs)
+        packed = self._pack(batch)
+        if self.graphs:
+            st = self._static
+            if st is None or st["obs"].shape != packed["obs"].shape or st["cols"].shape != packed["cols"].shape:
+                self._static = st = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in packed.items()}
                 self._graph = None
             else:
-                for k in _LOSS_KEYS:
-                    self._static[k].copy_(batch[k])
+                for k in ("obs", "cols", "actions"):
+                    st[k].copy_(packed[k])
             if self._graph is None or self._mbs != mbs:
                 try:
-                    self._capture(self._static, mbs)
+                    self._capture(st, mbs)
                 except Exception as e:  # pragma: no cover - capture unsupported: stay eager
                     print(f"[PPOLearner] HIP graph capture failed ({e!r}); running eagerly")
-                    self.graphs = use_graph = False
+                    self.graphs = False
                     torch.cuda.synchronize(self.device)
-        full = self._static if use_graph else {k: batch[k] for k in _LOSS_KEYS}
+            full = st if self.graphs else packed
+        else:
+            full = packed
         self.acc.zero_()
-        self.kl_coeff_t.fill_(self.kl_coeff)
+        self.coef[4].fill_(self.kl_coeff)
         steps = 0
         for _ in range(c["num_sgd_iter"]):
             perm = torch.randperm(n, device=self.device)
             for i in range(nmb):
                 idx = perm[i * mbs:(i + 1) * mbs]
-                if use_graph:
+                if self.graphs:
                     self._sidx.copy_(idx)
                     self._graph.replay()
-                    if not self._graph_sync:
-                        if self.world > 1:
-                            self._allreduce()
-                        self.opt.step()
+                    if not self._graph_opt:
+                        self._opt_step()
                 else:
-                    self._eager_step(full, idx)
+                    self._fast_step(full, idx, True)
                 steps += 1
-        acc = (self.acc / max(steps, 1)).tolist()  # one host sync per update
-        kl_mean = acc[4]
+        acc = (self.acc / float(max(steps, 1) * mbs)).tolist()  # one host sync per update
+        return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
+
+    def _finish(self, pol, vf, ent, kl_mean, total, steps):
+        c = self.cfg
         # adaptive KL coefficient (reference ppo.py UpdateKL)
         if kl_mean > 2.0 * c["kl_target"]:
             self.kl_coeff *= 1.5
         elif kl_mean < 0.5 * c["kl_target"]:
             self.kl_coeff *= 0.5
-        self.stats = {"total_loss": acc[0], "policy_loss": acc[1], "vf_loss": acc[2], "entropy": acc[3],
-                      "kl": kl_mean, "cur_kl_coeff": self.kl_coeff, "num_sgd_steps": steps}
+        self.stats = {"total_loss": total, "policy_loss": pol, "vf_loss": vf, "entropy": ent, "kl": kl_mean,
+                      "cur_kl_coeff": self.kl_coeff, "num_sgd_steps": steps}
         return self.stats
 
+    def _update_eager(self, batch, mbs):
+        c = self.cfg
+        coef = torch.tensor([c["clip_param"], c["vf_clip_param"], c["vf_loss_coeff"], c["entropy_coeff"],
+                             self.kl_coeff])
+        acc = torch.zeros(6)
+        steps = 0
+        for _ in range(c["num_sgd_iter"]):
+            for mb in batch.minibatches(mbs, shuffle=True):
+                logits, v = self.model(mb[SampleBatch.OBS])
+                total, stats = ppo_categorical_loss_reference(
+                    logits, v, mb[SampleBatch.ACTION_DIST_INPUTS], mb[SampleBatch.ACTIONS],
+                    mb[SampleBatch.ACTION_LOGP].float(), mb[SampleBatch.ADVANTAGES].float(),
+                    mb[SampleBatch.VALUE_TARGETS].float(), coef)
+                self.opt.zero_grad(set_to_none=True)
+                total.backward()
+                if self.world > 1:
+                    for p in self.params:
+                        torch.distributed.all_reduce(p.grad, group=self.pg)
+                        p.grad.mul_(1.0 / self.world)
+                if c["grad_clip"]:
+                    nn.utils.clip_grad_norm_(self.params, c["grad_clip"])
+                self.opt.step()
+                acc += stats.cpu() / mb.count
+                steps += 1
+        acc = (acc / max(steps, 1)).tolist()
+        return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
+
     def get_weights(self):
+        if self.fast:  # publish the fp32 masters (the bf16 weights are derived)
+            out, off = {}, 0
+            sd = self.model.state_dict()
+            names = {id(p): n for n, p in self.model.named_parameters()}
+            for p in self.params:
+                out[names[id(p)]] = self.master.as_strided(p.size(), p.stride(), off).detach().cpu().clone()
+                off += p.numel()
+            for k, v in sd.items():
+                out.setdefault(k, v.detach().cpu())
+            return out
         return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
 
     def set_weights(self, w):
         with torch.no_grad():
-            self.model.load_state_dict(w)
+            if self.fast:
+                names = {id(p): n for n, p in self.model.named_parameters()}
+                off = 0
+                for p in self.params:
+                    src = w[names[id(p)]].to(self.device).float()
+                    self.master.as_strided(p.size(), p.stride(), off).copy_(src)
+                    p.copy_(src)
+                    off += p.numel()
+            else:
+                self.model.load_state_dict(w)
 
 
 class GPURolloutSampler:
     """Samples `fragment` steps from a device-resident vectorised env with on-GPU inference and
     postprocesses with the GAE kernel. Output: a flat SampleBatch of fragment*num_envs rows in HBM.
-    Each env step (policy forward, Gumbel-max sampling, env step, buffer writes at a device-side
-    step counter) is one HIP-graph replay."""
+    Each env step (policy forward, K7 sampling + buffer writes, env step) is one HIP-graph replay."""
 
-    def __init__(self, env, model: nn.Module, fragment: int, gamma=0.99, lam=0.95, bf16=True, use_graphs=True):
+    def __init__(self, env, model: nn.Module, fragment: int, gamma=0.99, lam=0.95, use_graphs=True, seed=0):
         self.env = env
         self.model = model
         self.T = fragment
         self.B = env.num_envs
-        self.gamma, self.lam, self.bf16 = gamma, lam, bf16
+        self.gamma, self.lam = gamma, lam
         dev = env.device
         self.device = dev
         obs = env.reset()
@@ -252,36 +368,43 @@ class GPURolloutSampler:
         self.buf_vf = torch.empty((T, B), dtype=torch.float32, device=dev)
         self.buf_rew = torch.empty((T, B), dtype=torch.float32, device=dev)
         self.buf_done = torch.empty((T, B), dtype=torch.float32, device=dev)
+        self.act_now = torch.zeros(B, dtype=torch.int64, device=dev)
         with torch.no_grad():
-            logits, _ = self._policy(self.s_obs)
-        self.buf_logits = torch.empty((T, B, logits.shape[-1]), dtype=torch.float32, device=dev)
+            logits, _ = self.model(self.s_obs)
+        self.A = logits.shape[-1]
+        self.buf_logits = torch.empty((T, B, self.A), dtype=torch.float32, device=dev)
         self.t_idx = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.graphs = use_graphs and dev.type == "cuda" and not os.environ.get("RMM_NO_GRAPHS")
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.seed = int(seed) & 0xFFFFFFFF
+        self.fast = dev.type == "cuda"
+        self.graphs = use_graphs and self.fast and not os.environ.get("RMM_NO_GRAPHS")
         self._graph = None
-
-    def _policy(self, obs):
-        if self.bf16 and self.device.type == "cuda":
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                logits, v = self.model(obs)
-            return logits.float(), v.float()
-        return self.model(obs)
 
     @torch.no_grad()
     def _step_body(self):
-        logits, v = self._policy(self.s_obs)
-        d = Categorical(logits)
-        a = d.sample()
+        logits, v = self.model(self.s_obs)
         t = self.t_idx
+        if self.fast:
+            require_hip().sample_store(
+                logits.data_ptr(), logits.dtype == torch.bfloat16, v.data_ptr(), v.dtype == torch.bfloat16,
+                t.data_ptr(), self.ctr.data_ptr(), self.seed, self.buf_act.data_ptr(), self.buf_logp.data_ptr(),
+                self.buf_vf.data_ptr(), self.buf_logits.data_ptr(), self.act_now.data_ptr(), self.B, self.A,
+                _stream())
+            a = self.act_now
+        else:
+            d = Categorical(logits.float())
+            a = d.sample()
+            self.buf_act.index_copy_(0, t, a.unsqueeze(0))
+            self.buf_logp.index_copy_(0, t, d.logp(a).unsqueeze(0))
+            self.buf_vf.index_copy_(0, t, v.float().unsqueeze(0))
+            self.buf_logits.index_copy_(0, t, logits.float().unsqueeze(0))
         self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
-        self.buf_act.index_copy_(0, t, a.unsqueeze(0))
-        self.buf_logp.index_copy_(0, t, d.logp(a).unsqueeze(0))
-        self.buf_vf.index_copy_(0, t, v.unsqueeze(0))
-        self.buf_logits.index_copy_(0, t, logits.unsqueeze(0))
         obs, r, done = self.env.step(a)
         self.s_obs.copy_(obs)
         self.buf_rew.index_copy_(0, t, r.unsqueeze(0))
         self.buf_done.index_copy_(0, t, done.unsqueeze(0))
         self.t_idx.add_(1)
+        self.ctr.add_(1)
 
     def _capture(self):
         s = torch.cuda.Stream(self.device)
@@ -311,8 +434,8 @@ class GPURolloutSampler:
                 self._graph.replay()
             else:
                 self._step_body()
-        _, last_v = self._policy(self.s_obs)
-        adv, ret = ops.gae(self.buf_rew, self.buf_vf, self.buf_done, last_v, self.gamma, self.lam)
+        _, last_v = self.model(self.s_obs)
+        adv, ret = ops.gae(self.buf_rew, self.buf_vf, self.buf_done, last_v.float(), self.gamma, self.lam)
         n = self.T * self.B
         return SampleBatch({
             SampleBatch.OBS: self.buf_obs.view(n, *self.buf_obs.shape[2:]),
@@ -328,14 +451,13 @@ class GPURolloutSampler:
 
 
 def smoke_step(device="cuda:0"):
-    """One tiny PPO iteration (sample → GAE kernel → fused-loss SGD step) on `device`."""
+    """One tiny PPO iteration (K7 sampling → K3 GAE → K2/K2b gathers → K5b loss → K6 Adam)."""
     from ray_memory_management_amd.rllib.env import GPUSyntheticAtariVectorEnv
     from ray_memory_management_amd.rllib.models import VisionNetwork
 
     torch.manual_seed(0)
     env = GPUSyntheticAtariVectorEnv(8, device, num_actions=4)
-    model = VisionNetwork(4).to(device)
-    learner = PPOLearner(model, {"sgd_minibatch_size": 32, "num_sgd_iter": 1}, device=device,
+    learner = PPOLearner(VisionNetwork(4), {"sgd_minibatch_size": 32, "num_sgd_iter": 1}, device=device,
                          action_space=env.action_space)
     sampler = GPURolloutSampler(env, learner.model, fragment=8)
     batch = sampler.sample()

@@ -1,4 +1,5 @@
-"""GPU PPO learner: HIP-graph path must match the eager path; sampler produces sane batches."""
+"""GPU PPO learner: fused-kernel numerics vs PyTorch reference, HIP-graph path == eager path,
+sampler produces sane batches."""
 import pytest
 import torch
 
@@ -18,6 +19,59 @@ def _setup(cuda, graphs, seed=0):
     return env, learner
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fused_cat_loss_matches_reference(cuda, dt):
+    from ray_memory_management_amd.rllib.ppo_learner import (ppo_categorical_loss,
+                                                             ppo_categorical_loss_reference)
+
+    torch.manual_seed(3)
+    N, A = 513, 6
+    logits = (torch.randn(N, A, device=cuda) * 2).to(dt).requires_grad_()
+    values = (torch.randn(N, device=cuda)).to(dt).requires_grad_()
+    old_logits = torch.randn(N, A, device=cuda)
+    act = torch.randint(0, A, (N,), device=cuda)
+    old_logp = torch.log_softmax(old_logits, -1).gather(1, act[:, None]).squeeze(1)
+    adv = torch.randn(N, device=cuda)
+    vt = torch.randn(N, device=cuda) * 3
+    coef = torch.tensor([0.2, 4.0, 0.5, 0.01, 0.3], device=cuda)
+    tot, stats = ppo_categorical_loss(logits, values, old_logits, act, old_logp, adv, vt, coef)
+    (2.0 * tot).backward()
+    g1 = (logits.grad.clone(), values.grad.clone())
+    logits.grad = values.grad = None
+    lf, vf = logits.detach().float().requires_grad_(), values.detach().float().requires_grad_()
+    rt, rstats = ppo_categorical_loss_reference(lf, vf, old_logits, act, old_logp, adv, vt, coef)
+    (2.0 * rt).backward()
+    torch.testing.assert_close(tot.float(), rt, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(stats, rstats, rtol=1e-4, atol=1e-3)
+    tol = dict(rtol=2e-2, atol=1e-5) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(g1[0].float(), lf.grad, **tol)
+    torch.testing.assert_close(g1[1].float(), vf.grad, **tol)
+
+
+def test_adam_flat_matches_torch(cuda):
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    torch.manual_seed(0)
+    n = 10007
+    w = torch.randn(n, device=cuda)
+    p = w.clone().requires_grad_()
+    opt = torch.optim.Adam([p], lr=1e-3)
+    master, m1, m2 = w.clone(), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    wb = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    hp = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0, 0.0], device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(5):
+        g = torch.randn(n, device=cuda)
+        p.grad = g.clone()
+        opt.step()
+        hp[5] += 1
+        h.adam_flat(master.data_ptr(), m1.data_ptr(), m2.data_ptr(), g.data_ptr(), False, wb.data_ptr(),
+                    hp.data_ptr(), 1.0, n, s)
+    torch.testing.assert_close(master, p.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(wb.float(), p.detach(), rtol=1e-2, atol=1e-2)
+
+
 def test_graph_matches_eager(cuda):
     from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler
 
@@ -26,14 +80,13 @@ def test_graph_matches_eager(cuda):
     batch = sampler.sample()
     frozen = {k: v.clone() for k, v in batch.items()}
     _, lg = _setup(cuda, True)
-    lg.model.load_state_dict(le.model.state_dict())
+    lg.set_weights(le.get_weights())
     torch.manual_seed(123)
     s1 = le.update(type(batch)({k: v.clone() for k, v in frozen.items()}))
     torch.manual_seed(123)
     s2 = lg.update(type(batch)({k: v.clone() for k, v in frozen.items()}))
     assert lg.graphs, "graph capture should succeed on MI355X"
-    for a, b in zip(le.model.parameters(), lg.model.parameters()):
-        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(le.master, lg.master, rtol=1e-3, atol=1e-4)
     assert abs(s1["total_loss"] - s2["total_loss"]) < 1e-2 * max(1.0, abs(s1["total_loss"]))
 
 
@@ -42,13 +95,30 @@ def test_graph_sampler_fills_buffers(cuda):
 
     env, lg = _setup(cuda, True)
     sampler = GPURolloutSampler(env, lg.model, fragment=12, use_graphs=True)
-    b1 = sampler.sample()
+    sampler.sample()
     b2 = sampler.sample()
     assert sampler._graph is not None
-    assert b1.count == 12 * 16
+    assert b2.count == 12 * 16
     a = b2["actions"]
     assert int(a.min()) >= 0 and int(a.max()) < 4
-    # observations advance between steps (frame stack shifts)
+    # actions are not constant (the sampler RNG advances per step)
+    assert len(torch.unique(a)) > 1
     obs = b2["obs"].view(12, 16, 4, 84, 84)
-    assert torch.equal(obs[1, :, 0], obs[0, :, 1])
+    assert torch.equal(obs[1, :, 0], obs[0, :, 1])  # frame stack shifts between steps
     assert torch.isfinite(b2["advantages"]).all()
+    lp = torch.log_softmax(b2["action_dist_inputs"], -1).gather(1, a[:, None]).squeeze(1)
+    torch.testing.assert_close(lp, b2["action_logp"], rtol=1e-4, atol=1e-4)
+
+
+def test_learning_reduces_value_loss(cuda):
+    """A few PPO iterations on the synthetic env must reduce the value loss (sanity of training)."""
+    from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler
+
+    env, lg = _setup(cuda, True)
+    lg.cfg["lr"] = 1e-3
+    lg.hp[0] = 1e-3
+    sampler = GPURolloutSampler(env, lg.model, fragment=32)
+    first = lg.update(sampler.sample())["vf_loss"]
+    for _ in range(6):
+        last = lg.update(sampler.sample())["vf_loss"]
+    assert last < first
