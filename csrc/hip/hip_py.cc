@@ -197,6 +197,16 @@ PYBIND11_MODULE(_hip, m) {
                  P<int64_t>(act_now), B, A, S(stream));
   });
 
+  m.def("bias_relu_fwd", [](uint64_t y, uint64_t bias, int64_t M, int C, bool relu, uint64_t stream) {
+    bias_relu_fwd(P<void>(y), P<const void>(bias), M, C, relu, S(stream));
+  });
+  m.def("bias_relu_bwd_partials", &bias_relu_bwd_partials);
+  m.def("bias_relu_bwd", [](uint64_t dy, uint64_t y, uint64_t dpre, uint64_t db, uint64_t partial, int64_t M, int C,
+                            bool relu, uint64_t stream) {
+    bias_relu_bwd(P<const void>(dy), P<const void>(y), P<void>(dpre), P<void>(db), P<float>(partial), M, C, relu,
+                  S(stream));
+  });
+
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {
     std::string h = handle;

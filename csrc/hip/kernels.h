@@ -68,5 +68,12 @@ void sample_store(const void* logits, bool logits_bf16, const void* values, bool
                   const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf, float* lout,
                   int64_t* act_now, int64_t B, int A, hipStream_t stream);
 
+// K8: conv epilogue for NHWC bf16 maps [M, C]: y = relu(y + b) in place; backward dpre = dy*(y>0)
+// and db = column sums of dpre (two-pass, deterministic; `partial` holds bias_relu_bwd_partials(M)*C f32).
+void bias_relu_fwd(void* y, const void* bias, int64_t M, int C, bool relu, hipStream_t stream);
+int64_t bias_relu_bwd_partials(int64_t M);
+void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, float* partial, int64_t M, int C,
+                   bool relu, hipStream_t stream);
+
 }  // namespace hip
 }  // namespace rmm

@@ -291,5 +291,120 @@ void sample_store(const void* logits, bool logits_bf16, const void* values, bool
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+// ============================================================== K8 conv epilogue: bias + ReLU
+
+// y[M, C] (NHWC conv output, bf16) <- relu(y + bias). 8 channels (16 B) per thread.
+__global__ __launch_bounds__(256) void k_bias_relu_fwd(__hip_bfloat16* __restrict__ y, const __hip_bfloat16* __restrict__ bias,
+                                                      int64_t M, int C, int relu) {
+  const int groups = C / 8;
+  const int64_t total = M * groups;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+    const int g = int(e % groups);
+    uint4 v = reinterpret_cast<uint4*>(y)[e];
+    const uint4 bv = reinterpret_cast<const uint4*>(bias)[g];
+    uint32_t* pv = reinterpret_cast<uint32_t*>(&v);
+    const uint32_t* pb = reinterpret_cast<const uint32_t*>(&bv);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      float lo = __uint_as_float(pv[k] << 16) + __uint_as_float(pb[k] << 16);
+      float hi = __uint_as_float(pv[k] & 0xFFFF0000u) + __uint_as_float(pb[k] & 0xFFFF0000u);
+      if (relu) {
+        lo = fmaxf(lo, 0.f);
+        hi = fmaxf(hi, 0.f);
+      }
+      __hip_bfloat16 l = __float2bfloat16(lo), h = __float2bfloat16(hi);
+      pv[k] = uint32_t(*reinterpret_cast<unsigned short*>(&l)) | (uint32_t(*reinterpret_cast<unsigned short*>(&h)) << 16);
+    }
+    reinterpret_cast<uint4*>(y)[e] = v;
+  }
+}
+
+// dpre = dy * (y > 0) (relu) and per-workgroup channel partial sums of dpre (deterministic: no
+// atomics, no cross-workgroup hand-off; k_colsum_partials finishes the reduction).
+constexpr int kBRThreads = 256;
+__global__ __launch_bounds__(kBRThreads) void k_bias_relu_bwd(const __hip_bfloat16* __restrict__ dy,
+                                                             const __hip_bfloat16* __restrict__ y,
+                                                             __hip_bfloat16* __restrict__ dpre, float* __restrict__ partial,
+                                                             int64_t M, int C, int relu, int64_t rows_per_wg) {
+  const int groups = C / 8;                  // channel groups of 8
+  const int rpi = kBRThreads / groups;       // rows per iteration of the workgroup
+  const int g = threadIdx.x % groups;
+  const int r0 = threadIdx.x / groups;
+  const int64_t row_begin = int64_t(blockIdx.x) * rows_per_wg;
+  const int64_t row_end = min(M, row_begin + rows_per_wg);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rpi) {
+    for (int64_t r = row_begin + r0; r < row_end; r += rpi) {
+      const int64_t e = r * groups + g;
+      uint4 d = reinterpret_cast<const uint4*>(dy)[e];
+      uint32_t* pd = reinterpret_cast<uint32_t*>(&d);
+      if (relu) {
+        const uint4 yv = reinterpret_cast<const uint4*>(y)[e];
+        const uint32_t* py = reinterpret_cast<const uint32_t*>(&yv);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t mlo = (py[k] & 0x7FFFu) && !(py[k] & 0x8000u) ? 0x0000FFFFu : 0u;
+          const uint32_t mhi = (py[k] & 0x7FFF0000u) && !(py[k] & 0x80000000u) ? 0xFFFF0000u : 0u;
+          pd[k] &= (mlo | mhi);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        acc[2 * k] += __uint_as_float(pd[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(pd[k] & 0xFFFF0000u);
+      }
+      reinterpret_cast<uint4*>(dpre)[e] = d;
+    }
+  }
+  // reduce threads sharing a channel group through LDS
+  __shared__ float red[kBRThreads][9];
+#pragma unroll
+  for (int k = 0; k < 8; k++) red[threadIdx.x][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < groups * 8) {
+    const int gg = threadIdx.x / 8, k = threadIdx.x % 8;
+    float s = 0.f;
+    for (int t = gg; t < rpi * groups; t += groups) s += red[t][k];
+    partial[int64_t(blockIdx.x) * C + gg * 8 + k] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_colsum_partials(const float* __restrict__ partial, int64_t G, int C,
+                                                        __hip_bfloat16* __restrict__ out_bf16, float* __restrict__ out_f32) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int64_t g = 0; g < G; g++) s += partial[g * C + c];
+    if (out_bf16) out_bf16[c] = __float2bfloat16(s);
+    if (out_f32) out_f32[c] = s;
+  }
+}
+
+void bias_relu_fwd(void* y, const void* bias, int64_t M, int C, bool relu, hipStream_t stream) {
+  if (C % 8) throw std::invalid_argument("bias_relu_fwd: C must be a multiple of 8");
+  int64_t total = M * (C / 8);
+  if (total <= 0) return;
+  int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(k_bias_relu_fwd, dim3(uint32_t(blocks)), dim3(256), 0, stream, static_cast<__hip_bfloat16*>(y),
+                     static_cast<const __hip_bfloat16*>(bias), M, C, relu ? 1 : 0);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+int64_t bias_relu_bwd_partials(int64_t M) {
+  return std::max<int64_t>(1, std::min<int64_t>(1024, (M + 1023) / 1024));
+}
+
+void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, float* partial, int64_t M, int C,
+                   bool relu, hipStream_t stream) {
+  if (C % 8 || C > 8 * kBRThreads) throw std::invalid_argument("bias_relu_bwd: bad C");
+  const int64_t G = bias_relu_bwd_partials(M);
+  const int64_t rows_per_wg = (M + G - 1) / G;
+  hipLaunchKernelGGL(k_bias_relu_bwd, dim3(uint32_t(G)), dim3(kBRThreads), 0, stream,
+                     static_cast<const __hip_bfloat16*>(dy), static_cast<const __hip_bfloat16*>(y),
+                     static_cast<__hip_bfloat16*>(dpre), partial, M, C, relu ? 1 : 0, rows_per_wg);
+  hipLaunchKernelGGL(k_colsum_partials, dim3(1), dim3(256), 0, stream, partial, G, C,
+                     static_cast<__hip_bfloat16*>(dbias_bf16), static_cast<float*>(nullptr));
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace hip
 }  // namespace rmm

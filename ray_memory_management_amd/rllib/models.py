@@ -8,6 +8,57 @@ import torch
 import torch.nn as nn
 
 
+class _ConvBiasReLUFn(torch.autograd.Function):
+    """MIOpen conv (no bias) + fused bias/ReLU epilogue (K8); backward: fused ReLU mask + bias grad
+    (deterministic two-pass reduction, K8) then MIOpen data/weight grads."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        y = torch.convolution(x, w, None, stride, padding, (1, 1), False, (0, 0), 1)
+        if not y.is_contiguous(memory_format=torch.channels_last):
+            y = y.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = y.shape
+        h.bias_relu_fwd(y.data_ptr(), b.data_ptr(), N * H * W, C, True, torch.cuda.current_stream().cuda_stream)
+        ctx.save_for_backward(x, w, y)
+        ctx.conf = (stride, padding)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        x, w, y = ctx.saved_tensors
+        stride, padding = ctx.conf
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = y.shape
+        M = N * H * W
+        dpre = torch.empty_like(dy)
+        db = torch.empty(C, dtype=y.dtype, device=y.device)
+        partial = torch.empty(h.bias_relu_bwd_partials(M) * C, dtype=torch.float32, device=y.device)
+        h.bias_relu_bwd(dy.data_ptr(), y.data_ptr(), dpre.data_ptr(), db.data_ptr(), partial.data_ptr(), M, C, True,
+                        torch.cuda.current_stream().cuda_stream)
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            dpre, x, w, None, stride, padding, (1, 1), False, (0, 0), 1,
+            (ctx.needs_input_grad[0], ctx.needs_input_grad[1], False))
+        return dx, dw, db, None, None
+
+
+class ConvReLU(nn.Conv2d):
+    """Conv2d followed by ReLU. On MI355X (bf16 NHWC) the bias add + ReLU and its backward run as
+    fused HIP kernels around the MIOpen convolution."""
+
+    def forward(self, x):
+        if (x.is_cuda and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16 and self.bias is not None
+                and self.out_channels % 8 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+                and not torch.is_autocast_enabled()):
+            return _ConvBiasReLUFn.apply(x, self.weight, self.bias, self.stride, self.padding)
+        return torch.relu(super().forward(x))
+
+
 def _act(name):
     return {"relu": nn.ReLU, "tanh": nn.Tanh, "elu": nn.ELU, "swish": nn.SiLU, "silu": nn.SiLU}[name]()
 
@@ -65,7 +116,7 @@ class VisionNetwork(nn.Module):
                 self.dense_tail = nn.Linear(c * k * k, out)
                 hw = 1
             else:
-                layers += [nn.Conv2d(c, out, k, s, padding=pad), nn.ReLU()]
+                layers.append(ConvReLU(c, out, k, s, padding=pad))
                 hw = (hw + 2 * pad - k) // s + 1
             c = out
         self.out_hw = hw

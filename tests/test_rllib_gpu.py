@@ -110,6 +110,47 @@ def test_graph_sampler_fills_buffers(cuda):
     torch.testing.assert_close(lp, b2["action_logp"], rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("C,k,s", [(16, 8, 4), (32, 4, 2)])
+def test_conv_bias_relu_fused_matches_torch(cuda, C, k, s):
+    from ray_memory_management_amd.rllib.models import ConvReLU
+
+    torch.manual_seed(0)
+    cin = 4 if C == 16 else 16
+    hw = 84 if C == 16 else 21
+    m = ConvReLU(cin, C, k, s, padding=2).to(cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(37, cin, hw, hw, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = m(x)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().float().requires_grad_(True)
+    br = m.bias.detach().float().requires_grad_(True)
+    yr = torch.relu(torch.nn.functional.conv2d(xr, wr, br, s, 2))
+    (yr * gy.float()).sum().backward()
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(m.bias.grad.float(), br.grad, rtol=3e-2, atol=3e-1)
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=3e-2, atol=3e-1)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+
+
+def test_many_graph_replays_stay_finite(cuda):
+    """Regression: 1000+ back-to-back SGD-step replays at bench scale must stay finite."""
+    from ray_memory_management_amd.rllib.env import GPUSyntheticAtariVectorEnv
+    from ray_memory_management_amd.rllib.models import VisionNetwork
+    from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler, PPOLearner
+
+    torch.manual_seed(1234)
+    env = GPUSyntheticAtariVectorEnv(50, cuda, num_actions=4)
+    L = PPOLearner(VisionNetwork(4), {"sgd_minibatch_size": 500, "num_sgd_iter": 10}, device=cuda,
+                   action_space=env.action_space)
+    S = GPURolloutSampler(env, L.model, fragment=100)
+    for _ in range(12):
+        st = L.update(S.sample())
+        assert all(v == v for v in st.values()), st  # no NaN
+    assert torch.isfinite(L.master).all()
+
+
 def test_learning_reduces_value_loss(cuda):
     """A few PPO iterations on the synthetic env must reduce the value loss (sanity of training)."""
     from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler
