@@ -203,6 +203,18 @@ int64_t Scheduler::PickNode(const Task& t, bool require_available) {
 void Scheduler::AcquireOn(Node* n, const ResourceRequest& r, Assignment* out) {
   for (auto& it : r.items) {
     n->avail[size_t(it.first)] -= it.second;
+    if (out && it.second > 0) {
+      auto gg = group_gpu_ids_.find(it.first);
+      if (gg != group_gpu_ids_.end()) {
+        // a task inside a placement-group bundle sees the bundle's GPU instances (amount 0:
+        // the instances stay reserved by the bundle, not by the task)
+        for (int g : gg->second)
+          if (std::find(out->gpu_ids.begin(), out->gpu_ids.end(), g) == out->gpu_ids.end()) {
+            out->gpu_ids.push_back(g);
+            out->gpu_amounts.push_back(0);
+          }
+      }
+    }
     if (it.first == gpu_id_ && out) {
       if (it.second >= kUnit) {
         int need = int(it.second / kUnit);
@@ -429,8 +441,14 @@ void Scheduler::CommitBundle(PlacementGroup* pg, size_t i, int64_t node) {
   Node* n = GetNode(node);
   ResourceRequest r;
   r.items = pg->bundles[i];
-  Assignment dummy;
-  AcquireOn(n, r, nullptr);
+  Assignment inst;
+  AcquireOn(n, r, &inst);  // reserves concrete GPU instances for the bundle
+  if (pg->bundle_gpu_ids.size() < pg->bundles.size()) {
+    pg->bundle_gpu_ids.resize(pg->bundles.size());
+    pg->bundle_gpu_amt.resize(pg->bundles.size());
+  }
+  pg->bundle_gpu_ids[i] = inst.gpu_ids;
+  pg->bundle_gpu_amt[i] = inst.gpu_amounts;
   std::map<std::string, double> derived;
   for (auto& it : pg->bundles[i]) {
     const std::string nm = names_[size_t(it.first)];
@@ -445,6 +463,11 @@ void Scheduler::CommitBundle(PlacementGroup* pg, size_t i, int64_t node) {
     Grow(n);
     n->total[size_t(rid)] += ToFixed(kv.second);
     n->avail[size_t(rid)] += ToFixed(kv.second);
+    if (!inst.gpu_ids.empty() && kv.first.rfind("GPU_group_", 0) == 0) {
+      auto& v = group_gpu_ids_[rid];
+      for (int g : inst.gpu_ids)
+        if (std::find(v.begin(), v.end(), g) == v.end()) v.push_back(g);
+    }
   }
   pg->placement[i] = node;
 }
@@ -466,10 +489,19 @@ void Scheduler::ReturnBundle(PlacementGroup* pg, size_t i) {
     n->total[size_t(rid)] -= ToFixed(kv.second);
     n->avail[size_t(rid)] -= ToFixed(kv.second);
     if (n->total[size_t(rid)] < 0) n->total[size_t(rid)] = 0;
+    group_gpu_ids_.erase(rid);
   }
   ResourceRequest r;
   r.items = pg->bundles[i];
   for (auto& it : r.items) n->avail[size_t(it.first)] += it.second;
+  if (i < pg->bundle_gpu_ids.size()) {
+    for (size_t k = 0; k < pg->bundle_gpu_ids[i].size(); k++) {
+      size_t g = size_t(pg->bundle_gpu_ids[i][k]);
+      if (g < n->gpu_free.size()) n->gpu_free[g] = std::min(kUnit, n->gpu_free[g] + pg->bundle_gpu_amt[i][k]);
+    }
+    pg->bundle_gpu_ids[i].clear();
+    pg->bundle_gpu_amt[i].clear();
+  }
   pg->placement[i] = -1;
 }
 

@@ -68,6 +68,8 @@ struct PlacementGroup {
   PgStrategy strategy;
   std::vector<std::vector<std::pair<int, Fixed>>> bundles;
   std::vector<int64_t> placement;  // node per bundle (-1 = unplaced)
+  std::vector<std::vector<int>> bundle_gpu_ids;    // GPU instances reserved by each bundle
+  std::vector<std::vector<Fixed>> bundle_gpu_amt;
   bool placed = false;
   bool removed = false;
 };
@@ -149,6 +151,8 @@ class Scheduler {
   std::vector<std::string> class_order_;
   std::map<std::string, PlacementGroup> pgs_;
   std::vector<std::string> pending_pgs_;
+  // derived "GPU_group_*" resource id -> GPU instance ids reserved by the bundle(s)
+  std::unordered_map<int, std::vector<int>> group_gpu_ids_;
   std::unordered_set<std::string> ready_objects_;  // small recent cache (bounded)
   std::deque<std::string> ready_objects_fifo_;
 };

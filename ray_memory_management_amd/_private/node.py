@@ -46,6 +46,26 @@ def actor_ref_key(actor_id: bytes) -> bytes:
     return b"\xaa" + actor_id[:16] + b"\xaa\xaa\xaa"
 
 
+def _is_actor_key(oid: bytes) -> bool:
+    return oid[:1] == b"\xaa" and oid[-3:] == b"\xaa\xaa\xaa"
+
+
+def pg_rewrite(res: dict, pg_hex: str, bidx: int) -> dict:
+    """Resources of a task placed in a bundle: the derived per-bundle names the native scheduler
+    commits when the group is placed (reference naming, bundle_spec.cc)."""
+    out = {}
+    for k, v in res.items():
+        if v <= 0:
+            continue
+        out[f"{k}_group_{bidx}_{pg_hex}" if bidx >= 0 else f"{k}_group_{pg_hex}"] = v
+    out[f"bundle_group_{bidx}_{pg_hex}" if bidx >= 0 else f"bundle_group_{pg_hex}"] = 0.001
+    return out
+
+
+def _cpu_part(res: dict) -> dict:
+    return {k: v for k, v in res.items() if k == "CPU" or k.startswith("CPU_group_")}
+
+
 class Conn:
     __slots__ = ("sock", "reader", "kind", "worker", "pid", "lock", "job_id", "alive", "wbuf")
 
@@ -475,7 +495,7 @@ class Head:
                 return
             w.state = "ACTOR"
             self._send_nb(c, (P.CREATE_ACTOR_INSTANCE, a.spec, self.fn_table.get(a.spec["class_id"]),
-                              {"gpu_ids": a.assign[2] if a.assign else [], "node_id": a.node,
+                              {"gpu_ids": a.assign[1] if a.assign else [], "node_id": a.node,
                                "restart": a.num_restarts}))
             return
         self.idle[(w.node, w.env_key, w.gpu_key)].append(w)
@@ -513,7 +533,7 @@ class Head:
         out = open(os.path.join(log_dir, f"worker-{wid.hex()[:12]}.log"), "ab")
         cmd = [sys.executable, "-u", "-m", "ray_memory_management_amd._private.worker_main"]
         proc = subprocess.Popen(cmd, env=env, stdout=out, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
-                                start_new_session=False)
+                                start_new_session=True)
         out.close()
         w = WorkerRec(wid, proc, node, env_key, gpu_key)
         w.actor_id = actor_id
@@ -613,8 +633,7 @@ class Head:
         if t is None or t.assign is None:
             return
         w.blocked = blocked
-        req = t.spec["resources"]
-        cpu_only = {k: v for k, v in req.items() if k == "CPU"}
+        cpu_only = _cpu_part(t.spec["_res"])
         if not cpu_only:
             return
         if blocked:
@@ -700,17 +719,20 @@ class Head:
 
     def _enqueue(self, t: TaskRec):
         spec = t.spec
-        deps = [r for r in t.arg_refs if not self.store.contains(r)]
+        deps = [r for r in t.arg_refs if not _is_actor_key(r) and not self.store.contains(r)]
         key = self._new_key(spec["task_id"])
         t.spec["_key"] = key
         strat, aff, soft, pg, bidx = self._strategy_args(spec)
-        res = spec["resources"]
         if strat == 3:
             pgrec = self.pgs.get(bytes.fromhex(pg))
             if pgrec is None or pgrec.state == "REMOVED":
                 self._fail_task(t, exc.TaskPlacementGroupRemoved("placement group was removed"), FAILED)
                 return
-        self.sched.submit(key, res, strat, aff, soft, pg, bidx, deps)
+            spec["_res"] = pg_rewrite(spec["resources"], pg, bidx)
+            strat, pg, bidx = 0, "", -1
+        else:
+            spec["_res"] = spec["resources"]
+        self.sched.submit(key, spec["_res"], strat, aff, soft, pg, bidx, deps)
 
     def _schedule(self):
         placed = self.sched.schedule_placement_groups()
@@ -726,7 +748,7 @@ class Head:
                 continue
             t = self.tasks.get(tid)
             if t is None or t.cancelled:
-                self.sched.release(node, t.spec["resources"] if t else {}, gpu_ids, amounts)
+                self.sched.release(node, t.spec.get("_res", {}) if t else {}, gpu_ids, amounts)
                 if t is not None:
                     self._fail_task(t, exc.TaskCancelledError(tid.hex()), CANCELLED)
                 continue
@@ -781,9 +803,10 @@ class Head:
     def _release_task_resources(self, t: TaskRec):
         if t.assign is not None:
             node, gpu_ids, amounts = t.assign
-            req = dict(t.spec["resources"])
-            if t.worker is not None and t.worker.blocked and "CPU" in req:
-                req.pop("CPU")
+            req = dict(t.spec.get("_res", t.spec["resources"]))
+            if t.worker is not None and t.worker.blocked:
+                for k in _cpu_part(req):
+                    req.pop(k)
                 t.worker.blocked = False
             self.sched.release(node, req, gpu_ids, amounts)
             t.assign = None
@@ -904,20 +927,26 @@ class Head:
         self.task_keys[key] = ("actor", a.actor_id)
         a.task_key = key
         strat, aff, soft, pg, bidx = self._strategy_args(spec)
-        deps = [r for r in spec.get("arg_refs", []) if not self.store.contains(r)]
-        self.sched.submit(key, spec["placement_resources"], strat, aff, soft, pg, bidx, deps)
+        deps = [r for r in spec.get("arg_refs", []) if not _is_actor_key(r) and not self.store.contains(r)]
+        if strat == 3:
+            spec["_pres"] = pg_rewrite(spec["placement_resources"], pg, bidx)
+            spec["_lres"] = pg_rewrite(spec["resources"], pg, bidx)
+            strat, pg, bidx = 0, "", -1
+        else:
+            spec["_pres"], spec["_lres"] = spec["placement_resources"], spec["resources"]
+        self.sched.submit(key, spec["_pres"], strat, aff, soft, pg, bidx, deps)
 
     def _actor_placed(self, actor_id, node, gpu_ids, amounts):
         a = self.actors.get(actor_id)
         if a is None or a.state == ACTOR_DEAD:
-            self.sched.release(node, a.spec["placement_resources"] if a else {}, gpu_ids, amounts)
+            self.sched.release(node, a.spec.get("_pres", {}) if a else {}, gpu_ids, amounts)
             return
         # Keep only the lifetime resources; return the scheduling-only part.
-        pres, lres = a.spec["placement_resources"], a.spec["resources"]
+        pres, lres = a.spec["_pres"], a.spec["_lres"]
         extra = {k: v - lres.get(k, 0.0) for k, v in pres.items() if v - lres.get(k, 0.0) > 0}
         if extra:
             self.sched.release(node, extra, [], [])
-        if not lres.get("GPU"):
+        if not any(k == "GPU" or k.startswith("GPU_group_") for k in lres):
             gpu_ids, amounts = [], []
         a.node = node
         a.assign = (node, gpu_ids, amounts)
@@ -965,7 +994,7 @@ class Head:
     def _actor_died(self, a: ActorRec):
         if a.assign is not None:
             node, gpu_ids, amounts = a.assign
-            self.sched.release(node, a.spec["resources"], gpu_ids, amounts)
+            self.sched.release(node, a.spec.get("_lres", a.spec["resources"]), gpu_ids, amounts)
             a.assign = None
         a.worker = None
         a.address = None

@@ -70,7 +70,20 @@ class ActorConn:
         self.connecting = False
 
     def _connect(self):
-        status = self.worker.request(lambda rid: (P.WAIT_ACTOR, rid, self.actor_id))
+        # The head may briefly still advertise the address of a process that just died; retry
+        # until it reports the restarted address or the death.
+        for attempt in range(200):
+            status = self.worker.request(lambda rid: (P.WAIT_ACTOR, rid, self.actor_id))
+            if status[0] != "alive" or status[2] != self.epoch or self.epoch < 0:
+                try:
+                    return self._connect_once(status)
+                except (ConnectionRefusedError, FileNotFoundError):
+                    pass
+            time.sleep(0.05)
+        self.dead_error = exc.RayActorError(self.actor_id.hex(), "could not connect to the actor")
+        return False
+
+    def _connect_once(self, status):
         kind, addr, restarts = status
         if kind == "dead":
             cause = addr
@@ -627,7 +640,8 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             if kwargs.get("_persistent"):
                 cmd.append("--persistent")
             log = open(os.path.join(sess, "logs", "head.log"), "ab")
-            _head_proc = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL)
+            _head_proc = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                          start_new_session=True)
             log.close()
             ready = os.path.join(sess, "head.ready")
             t0 = time.time()

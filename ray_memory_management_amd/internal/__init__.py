@@ -1,0 +1,76 @@
+"""Internal APIs. Parity: reference python/ray/_private/internal_api.py (memory_summary, free,
+global_gc) and python/ray/experimental/internal_kv.py."""
+from __future__ import annotations
+
+from typing import List, Optional
+
+from ray_memory_management_amd._private import protocol as P
+from ray_memory_management_amd._private import worker as _w
+
+
+def free(object_refs: list, local_only: bool = False):
+    """Eagerly delete objects from the store (reference ray.internal.free)."""
+    w = _w._require_worker()
+    w.store.delete([r.binary() for r in object_refs])
+
+
+def memory_summary(address=None, stats_only: bool = False, units: str = "MB", num_entries: int = 50) -> str:
+    """`ray memory` equivalent: object store usage, spilling stats and the largest objects."""
+    div = {"B": 1, "KB": 1 << 10, "MB": 1 << 20, "GB": 1 << 30}[units]
+    st = _w._state("store_stats")
+    lines = ["======== Object store statistics ========",
+             f"Object store: {st['bytes_in_use'] / div:.2f} / {st['capacity'] / div:.2f} {units} used, "
+             f"{st['num_objects']} objects",
+             f"Spilled: {st['bytes_spilled_total'] / div:.2f} {units} in {st['objects_spilled_total']} objects "
+             f"(currently {st['spilled_objects_current']} spilled, {st['spilled_bytes_current'] / div:.2f} {units})",
+             f"Restored: {st['bytes_restored_total'] / div:.2f} {units} in {st['objects_restored_total']} objects",
+             f"Fallback allocations: {st['fallback_allocs_total']} ({st['fallback_bytes_current'] / div:.2f} {units} live)"]
+    if not stats_only:
+        objs = sorted(_w._state("objects"), key=lambda o: -o["size"])[:num_entries]
+        lines.append("======== Objects (largest first) ========")
+        lines.append(f"{'object_id':42s} {'size':>12s} {'state':>10s} {'pins':>5s} {'refs':>5s}")
+        for o in objs:
+            lines.append(f"{o['object_id']:42s} {o['size'] / div:12.3f} {o['state']:>10s} {o['pin_count']:5d} "
+                         f"{o['reference_count']:5d}")
+    return "\n".join(lines)
+
+
+def global_gc():
+    import gc
+
+    gc.collect()
+
+
+# ---- internal KV (reference python/ray/experimental/internal_kv.py)
+def _internal_kv_initialized() -> bool:
+    return _w.global_worker is not None
+
+
+def _internal_kv_put(key, value, overwrite: bool = True, namespace: Optional[str] = None) -> bool:
+    w = _w._require_worker()
+    k = key.encode() if isinstance(key, str) else key
+    v = value.encode() if isinstance(value, str) else value
+    ns = (namespace or "").encode()
+    return w.request(lambda rid: (P.KV_PUT, rid, ns, k, v, overwrite))
+
+
+def _internal_kv_get(key, namespace: Optional[str] = None):
+    w = _w._require_worker()
+    k = key.encode() if isinstance(key, str) else key
+    return w.request(lambda rid: (P.KV_GET, rid, (namespace or "").encode(), k))
+
+
+def _internal_kv_exists(key, namespace: Optional[str] = None) -> bool:
+    return _internal_kv_get(key, namespace) is not None
+
+
+def _internal_kv_del(key, del_by_prefix: bool = False, namespace: Optional[str] = None) -> int:
+    w = _w._require_worker()
+    k = key.encode() if isinstance(key, str) else key
+    return w.request(lambda rid: (P.KV_DEL, rid, (namespace or "").encode(), k, del_by_prefix))
+
+
+def _internal_kv_list(prefix, namespace: Optional[str] = None) -> List[bytes]:
+    w = _w._require_worker()
+    p = prefix.encode() if isinstance(prefix, str) else prefix
+    return w.request(lambda rid: (P.KV_KEYS, rid, (namespace or "").encode(), p))

@@ -1,0 +1,266 @@
+"""Actors. Mirrors reference python/ray/tests/test_actor*.py, test_actor_failures.py, test_asyncio.py,
+test_threaded_actor.py, test_concurrency_group.py, test_namespace.py."""
+import asyncio
+import os
+import threading
+import time
+
+import pytest
+
+import ray_memory_management_amd as ray
+
+
+@ray.remote
+class Counter:
+    def __init__(self, start=0):
+        self.n = start
+
+    def inc(self, k=1):
+        self.n += k
+        return self.n
+
+    def get(self):
+        return self.n
+
+    def pid(self):
+        return os.getpid()
+
+    def fail(self):
+        raise KeyError("actor method failed")
+
+    def die(self):
+        os._exit(1)
+
+    @ray.method(num_returns=2)
+    def two(self):
+        return 1, 2
+
+
+def test_actor_basic_and_ordering(ray_start):
+    c = Counter.remote(5)
+    refs = [c.inc.remote() for _ in range(100)]
+    assert ray.get(refs) == list(range(6, 106))
+    a, b = c.two.remote()
+    assert ray.get([a, b]) == [1, 2]
+
+
+def test_actor_method_error_does_not_kill(ray_start):
+    c = Counter.remote()
+    with pytest.raises(KeyError):
+        ray.get(c.fail.remote())
+    assert ray.get(c.inc.remote()) == 1
+
+
+def test_actor_handle_passing(ray_start):
+    c = Counter.remote()
+
+    @ray.remote
+    def use(h):
+        return ray.get(h.inc.remote(10))
+
+    assert ray.get(use.remote(c)) == 10
+    assert ray.get(c.get.remote()) == 10
+
+
+def test_actor_death_raises_actor_error(ray_start):
+    c = Counter.remote()
+    ray.get(c.inc.remote())
+    with pytest.raises(ray.exceptions.RayActorError):
+        ray.get(c.die.remote())
+    with pytest.raises(ray.exceptions.RayActorError):
+        ray.get(c.inc.remote(), timeout=10)
+
+
+def test_actor_restart(ray_start):
+    c = Counter.options(max_restarts=1).remote()
+    p1 = ray.get(c.pid.remote())
+    ray.get(c.inc.remote())
+    try:
+        ray.get(c.die.remote())
+    except ray.exceptions.RayActorError:
+        pass
+    # restarted: fresh state, new process
+    p2 = ray.get(c.pid.remote(), timeout=20)
+    assert p2 != p1
+    assert ray.get(c.get.remote()) == 0
+
+
+def test_kill_actor(ray_start):
+    c = Counter.remote()
+    ray.get(c.inc.remote())
+    ray.kill(c)
+    with pytest.raises(ray.exceptions.RayActorError):
+        ray.get(c.inc.remote(), timeout=10)
+
+
+def test_named_actor_and_namespace(ray_start):
+    c = Counter.options(name="ctr").remote(3)
+    assert ray.get(ray.get_actor("ctr").inc.remote()) == 4
+    with pytest.raises(ValueError):
+        Counter.options(name="ctr").remote()
+    same = Counter.options(name="ctr", get_if_exists=True).remote()
+    assert ray.get(same.get.remote()) == 4
+    with pytest.raises(ValueError):
+        ray.get_actor("nope")
+    d = Counter.options(name="dd", namespace="other").remote()
+    ray.get(d.inc.remote())
+    with pytest.raises(ValueError):
+        ray.get_actor("dd")
+    assert ray.get(ray.get_actor("dd", namespace="other").get.remote()) == 1
+
+
+def test_actor_creation_error(ray_start):
+    @ray.remote
+    class Bad:
+        def __init__(self):
+            raise RuntimeError("ctor failed")
+
+        def f(self):
+            return 1
+
+    b = Bad.remote()
+    with pytest.raises(ray.exceptions.RayActorError):
+        ray.get(b.f.remote(), timeout=20)
+
+
+def test_async_actor_concurrency(ray_start):
+    @ray.remote
+    class AsyncA:
+        def __init__(self):
+            self.active = 0
+            self.peak = 0
+
+        async def work(self):
+            self.active += 1
+            self.peak = max(self.peak, self.active)
+            await asyncio.sleep(0.2)
+            self.active -= 1
+            return 1
+
+        async def peak_(self):
+            return self.peak
+
+    a = AsyncA.remote()
+    t0 = time.time()
+    assert sum(ray.get([a.work.remote() for _ in range(10)])) == 10
+    assert time.time() - t0 < 1.5
+    assert ray.get(a.peak_.remote()) > 1
+
+
+def test_threaded_actor(ray_start):
+    @ray.remote(max_concurrency=4)
+    class T:
+        def __init__(self):
+            self.lock = threading.Lock()
+            self.active = 0
+            self.peak = 0
+
+        def work(self):
+            with self.lock:
+                self.active += 1
+                self.peak = max(self.peak, self.active)
+            time.sleep(0.2)
+            with self.lock:
+                self.active -= 1
+            return self.peak
+
+    t = T.remote()
+    peaks = ray.get([t.work.remote() for _ in range(8)])
+    assert max(peaks) > 1
+
+
+def test_concurrency_groups(ray_start):
+    @ray.remote(concurrency_groups={"io": 2})
+    class G:
+        @ray.method(concurrency_group="io")
+        def slow(self):
+            time.sleep(0.3)
+            return "io"
+
+        def fast(self):
+            return "fast"
+
+    g = G.remote()
+    r = [g.slow.remote() for _ in range(2)]
+    assert ray.get(g.fast.remote()) == "fast"
+    assert ray.get(r) == ["io", "io"]
+
+
+def test_exit_actor(ray_start):
+    @ray.remote
+    class E:
+        def bye(self):
+            ray.actor.exit_actor()
+
+        def ping(self):
+            return 1
+
+    e = E.remote()
+    assert ray.get(e.ping.remote()) == 1
+    ray.get(e.bye.remote())
+    with pytest.raises(ray.exceptions.RayActorError):
+        ray.get(e.ping.remote(), timeout=10)
+
+
+def test_actor_out_of_scope_is_killed(ray_start):
+    c = Counter.remote()
+    pid = ray.get(c.pid.remote())
+    del c
+    deadline = time.time() + 10
+    alive = True
+    while time.time() < deadline:
+        try:
+            os.kill(pid, 0)
+        except OSError:
+            alive = False
+            break
+        time.sleep(0.1)
+    assert not alive
+
+
+def test_detached_actor_listed(ray_start):
+    c = Counter.options(name="det", lifetime="detached").remote()
+    ray.get(c.inc.remote())
+    from ray_memory_management_amd.util import state
+
+    actors = state.list_actors()
+    assert any(a["name"] == "det" and a["state"] == "ALIVE" for a in actors)
+
+
+def test_terminate(ray_start):
+    c = Counter.remote()
+    ray.get(c.inc.remote())
+    c.__ray_terminate__.remote()
+    with pytest.raises(ray.exceptions.RayActorError):
+        for _ in range(50):
+            ray.get(c.inc.remote(), timeout=10)
+            time.sleep(0.05)
+
+
+def test_many_actors(ray_start):
+    actors = [Counter.remote(i) for i in range(12)]
+    assert ray.get([a.inc.remote() for a in actors]) == [i + 1 for i in range(12)]
+
+
+def test_actor_gpu_assignment():
+    ray.init(num_cpus=2, num_gpus=2, object_store_memory=128 << 20)
+    try:
+        @ray.remote(num_gpus=1)
+        class G:
+            def ids(self):
+                return ray.get_gpu_ids(), os.environ.get("HIP_VISIBLE_DEVICES")
+
+        a, b = G.remote(), G.remote()
+        (ia, ea), (ib, eb) = ray.get([a.ids.remote(), b.ids.remote()])
+        assert sorted(ia + ib) == [0, 1]
+        assert ea == str(ia[0]) and eb == str(ib[0])
+
+        @ray.remote(num_gpus=0.5)
+        def frac():
+            return ray.get_gpu_ids()
+
+        ray.kill(a)
+        time.sleep(0.5)
+        assert len(ray.get(frac.remote(), timeout=20)) == 1
+    finally:
+        ray.shutdown()

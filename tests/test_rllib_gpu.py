@@ -123,15 +123,23 @@ def test_conv_bias_relu_fused_matches_torch(cuda, C, k, s):
     y = m(x)
     gy = torch.randn_like(y)
     (y.float() * gy.float()).sum().backward()
-    xr = x.detach().float().requires_grad_(True)
-    wr = m.weight.detach().float().requires_grad_(True)
-    br = m.bias.detach().float().requires_grad_(True)
-    yr = torch.relu(torch.nn.functional.conv2d(xr, wr, br, s, 2))
-    (yr * gy.float()).sum().backward()
+    xr = x.detach().float()
+    wr = m.weight.detach().float()
+    yr = torch.relu(torch.nn.functional.conv2d(xr, wr, m.bias.detach().float(), s, 2))
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
-    torch.testing.assert_close(m.bias.grad.float(), br.grad, rtol=3e-2, atol=3e-1)
-    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=3e-2, atol=3e-1)
-    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+    # fp32 reference backward through the SAME activation mask (bf16 vs fp32 forward differ in the
+    # sign of near-zero pre-activations, which is not what this test is about)
+    dpre = gy.float() * (y.float() > 0).float()
+    db_ref = dpre.sum((0, 2, 3))
+    dw_ref = torch.nn.grad.conv2d_weight(xr, wr.shape, dpre, s, 2)
+    dx_ref = torch.nn.grad.conv2d_input(xr.shape, wr, dpre, s, 2)
+
+    def rel(a, b):
+        return float((a.float() - b).norm() / b.norm().clamp_min(1e-6))
+
+    assert rel(m.bias.grad, db_ref) < 2e-2
+    assert rel(m.weight.grad, dw_ref) < 2e-2
+    assert rel(x.grad, dx_ref) < 2e-2
 
 
 def test_many_graph_replays_stay_finite(cuda):
