@@ -784,6 +784,11 @@ def kill(actor, *, no_restart: bool = True):
         return
     w = _require_worker()
     w.send((P.KILL_ACTOR, actor._actor_id, no_restart))
+    if no_restart:
+        # calls submitted by this process after kill() fail deterministically
+        conn = w.actor_conns.setdefault(actor._actor_id, ActorConn(w, actor._actor_id, 0))
+        with conn.lock:
+            conn.dead_error = exc.RayActorError(actor._actor_id.hex(), "The actor was killed by ray.kill().")
 
 
 def cancel(object_ref: ObjectRef, *, force: bool = False, recursive: bool = True):
