@@ -634,6 +634,8 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             env = dict(os.environ)
             root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+            # workers can import the driver's modules (reference: job code search path)
+            env["RMM_DRIVER_SYS_PATH"] = json.dumps([p for p in sys.path if p and os.path.isdir(p)])
             cmd = [sys.executable, "-u", "-m", "ray_memory_management_amd._private.node", "--session-dir", sess,
                    "--store-name", store_name, "--object-store-memory", str(osm), "--resources", json.dumps(res),
                    "--config", json.dumps(cfg)]

@@ -386,6 +386,9 @@ class _Handled(Exception):
 
 
 def main():
+    for p in json.loads(os.environ.get("RMM_DRIVER_SYS_PATH", "[]")):
+        if p not in sys.path:
+            sys.path.append(p)
     _apply_runtime_env()
     head = os.environ["RMM_HEAD_SOCKET"]
     store = os.environ["RMM_STORE_NAME"]

@@ -1,0 +1,17 @@
+"""Distributed training. Parity: reference python/ray/train/ (Trainer API of Ray AIR)."""
+from ray_memory_management_amd.air.checkpoint import Checkpoint  # noqa: F401
+from ray_memory_management_amd.air.config import (CheckpointConfig, FailureConfig, RunConfig,  # noqa: F401
+                                                  ScalingConfig)
+from ray_memory_management_amd.air.result import Result  # noqa: F401
+from ray_memory_management_amd.air import session  # noqa: F401
+from ray_memory_management_amd.train.base_trainer import BaseTrainer, DataParallelTrainer  # noqa: F401
+
+
+def __getattr__(name):
+    import importlib
+
+    if name in ("torch",):
+        return importlib.import_module("ray_memory_management_amd.train.torch")
+    if name == "TorchTrainer":
+        return importlib.import_module("ray_memory_management_amd.train.torch").TorchTrainer
+    raise AttributeError(name)

@@ -1,0 +1,97 @@
+"""Train: TorchTrainer DDP (gloo on CPU; RCCL on the GPU box). Mirrors reference
+python/ray/train/tests/test_torch_trainer.py / test_data_parallel_trainer.py."""
+import os
+
+import pytest
+import torch
+
+import ray_memory_management_amd as ray
+from ray_memory_management_amd.air import Checkpoint, CheckpointConfig, FailureConfig, RunConfig, ScalingConfig, session
+from ray_memory_management_amd.train.torch import TorchTrainer, prepare_model
+
+
+def _loop(config):
+    import torch.distributed as dist
+
+    torch.manual_seed(0)
+    model = prepare_model(torch.nn.Linear(4, 1))
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    start = 0
+    ck = session.get_checkpoint()
+    if ck is not None:
+        start = ck.to_dict()["epoch"] + 1
+    w = torch.tensor([1.0, -2.0, 3.0, 0.5])
+    for epoch in range(start, config["epochs"]):
+        g = torch.Generator().manual_seed(epoch * 100 + session.get_world_rank())
+        x = torch.randn(64, 4, generator=g)
+        y = (x @ w).unsqueeze(1)
+        loss = torch.nn.functional.mse_loss(model(x.to(next(model.parameters()).device)),
+                                            y.to(next(model.parameters()).device))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        # DDP keeps replicas identical
+        p = torch.cat([q.detach().reshape(-1).cpu() for q in model.parameters()])
+        ps = [torch.zeros_like(p) for _ in range(dist.get_world_size())]
+        dist.all_gather(ps, p)
+        same = all(torch.allclose(ps[0], q) for q in ps)
+        session.report({"loss": float(loss), "epoch": epoch, "replicas_equal": same, "world": session.get_world_size()},
+                       checkpoint=Checkpoint.from_dict({"epoch": epoch}))
+
+
+def test_torch_trainer_ddp_gloo(ray_start, tmp_path):
+    trainer = TorchTrainer(_loop, train_loop_config={"epochs": 5},
+                           scaling_config=ScalingConfig(num_workers=2, use_gpu=False),
+                           run_config=RunConfig(name="t1", local_dir=str(tmp_path),
+                                                checkpoint_config=CheckpointConfig(num_to_keep=2)))
+    res = trainer.fit()
+    assert res.error is None, res.error
+    assert res.metrics["world"] == 2 and res.metrics["replicas_equal"]
+    assert res.metrics_history[-1]["loss"] < res.metrics_history[0]["loss"]
+    assert res.checkpoint.to_dict()["epoch"] == 4
+    assert len(res.best_checkpoints) == 2
+    assert len(res.metrics_dataframe) == 5
+
+
+def test_resume_from_checkpoint(ray_start, tmp_path):
+    trainer = TorchTrainer(_loop, train_loop_config={"epochs": 4},
+                           scaling_config=ScalingConfig(num_workers=2),
+                           run_config=RunConfig(name="t2", local_dir=str(tmp_path)),
+                           resume_from_checkpoint=Checkpoint.from_dict({"epoch": 1}))
+    res = trainer.fit()
+    assert [m["epoch"] for m in res.metrics_history] == [2, 3]
+
+
+def test_training_error_reported(ray_start, tmp_path):
+    def bad(config):
+        raise ValueError("bad loop")
+
+    res = TorchTrainer(bad, scaling_config=ScalingConfig(num_workers=2),
+                       run_config=RunConfig(name="t3", local_dir=str(tmp_path))).fit()
+    assert res.error is not None and "bad loop" in str(res.error)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    c = Checkpoint.from_dict({"a": 1, "t": torch.ones(2)})
+    p = c.to_directory(str(tmp_path / "ck"))
+    c2 = Checkpoint.from_directory(p)
+    d = c2.to_dict()
+    assert d["a"] == 1 and torch.equal(d["t"], torch.ones(2))
+    with c2.as_directory() as dd:
+        assert os.path.isdir(dd)
+
+
+@pytest.mark.gpu
+def test_torch_trainer_rccl_gpu(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ray.init(num_cpus=4, num_gpus=1, object_store_memory=256 << 20)
+    try:
+        res = TorchTrainer(_loop, train_loop_config={"epochs": 3},
+                           scaling_config=ScalingConfig(num_workers=2, use_gpu=True,
+                                                        resources_per_worker={"CPU": 1, "GPU": 0.5}),
+                           run_config=RunConfig(name="g", local_dir=str(tmp_path))).fit()
+        assert res.error is None, res.error
+        assert res.metrics["replicas_equal"]
+    finally:
+        ray.shutdown()
