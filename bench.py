@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--sgd-iters", type=int, default=10)
     ap.add_argument("--no-putget", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
+    ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal only)")
     args = ap.parse_args()
 
     import torch
@@ -74,10 +76,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:  # rehearsal of the multi-rank path on a 1-GPU box (use --dist-backend gloo)
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device(f"cuda:{local_rank}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from ray_memory_management_amd._native import require_hip
     from ray_memory_management_amd.rllib.env import GPUSyntheticAtariVectorEnv

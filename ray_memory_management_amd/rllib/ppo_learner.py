@@ -37,7 +37,7 @@ DEFAULT_PPO = dict(
     gamma=0.99, lambda_=0.95, kl_coeff=0.5, kl_target=0.01, clip_param=0.1, vf_clip_param=10.0,
     vf_loss_coeff=1.0, entropy_coeff=0.01, lr=5e-5, train_batch_size=5000, sgd_minibatch_size=500,
     num_sgd_iter=10, grad_clip=None, standardize_advantages=True, use_graphs=True, fused=True,
-    allreduce_in_graph=True, adam_betas=(0.9, 0.999), adam_eps=1e-8, weight_decay=0.0,
+    allreduce_in_graph=False, adam_betas=(0.9, 0.999), adam_eps=1e-8, weight_decay=0.0,
 )
 
 _LOSS_KEYS = (SampleBatch.OBS, SampleBatch.ACTIONS, SampleBatch.ACTION_LOGP, SampleBatch.ACTION_DIST_INPUTS,
@@ -278,6 +278,9 @@ class PPOLearner:
                 else:
                     self._fast_step(full, idx, True)
                 steps += 1
+        if self.world > 1:  # KL adaptation and stats from the global batch, identical on every rank
+            torch.distributed.all_reduce(self.acc, group=self.pg)
+            self.acc.mul_(1.0 / self.world)
         acc = (self.acc / float(max(steps, 1) * mbs)).tolist()  # one host sync per update
         return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
 
@@ -316,6 +319,10 @@ class PPOLearner:
                 self.opt.step()
                 acc += stats.cpu() / mb.count
                 steps += 1
+        if self.world > 1:
+            acc_d = acc.to(self.device)
+            torch.distributed.all_reduce(acc_d, group=self.pg)
+            acc = acc_d.cpu() / self.world
         acc = (acc / max(steps, 1)).tolist()
         return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
 
