@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--no-putget", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
+    ap.add_argument("--breakdown", action="store_true", help="time sampling and SGD phases separately")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal only)")
     args = ap.parse_args()
 
@@ -100,7 +101,20 @@ def main():
                          device=dev, action_space=env.action_space)
     sampler = GPURolloutSampler(env, learner.model, fragment=args.fragment)
 
+    phase = {"sample_s": 0.0, "update_s": 0.0}
+
     def step():
+        if args.breakdown:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            batch = sampler.sample()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            st = learner.update(batch)
+            torch.cuda.synchronize()
+            phase["sample_s"] += t1 - t0
+            phase["update_s"] += time.perf_counter() - t1
+            return st
         batch = sampler.sample()
         return learner.update(batch)
 
@@ -150,6 +164,9 @@ def main():
             "put_get_vs_baseline": None if put_gbps is None else round(put_gbps / BASE_PUT_GBPS, 2),
             "last_stats": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in stats.items()},
         }
+        if args.breakdown:
+            n = args.steps + args.warmup
+            out["breakdown_ms"] = {k: round(v / n * 1e3, 3) for k, v in phase.items()}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

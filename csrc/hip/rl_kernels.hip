@@ -369,13 +369,22 @@ __global__ __launch_bounds__(kBRThreads) void k_bias_relu_bwd(const __hip_bfloat
   }
 }
 
+// Column sums of partial[G, C]: blockIdx.x owns channels [c0, c0 + 64); 4 waves stride over G with
+// coalesced row reads (lane = channel), then a 4-way LDS combine. Fixed order => deterministic.
 __global__ __launch_bounds__(256) void k_colsum_partials(const float* __restrict__ partial, int64_t G, int C,
                                                         __hip_bfloat16* __restrict__ out_bf16, float* __restrict__ out_f32) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = 0.f;
-    for (int64_t g = 0; g < G; g++) s += partial[g * C + c];
-    if (out_bf16) out_bf16[c] = __float2bfloat16(s);
-    if (out_f32) out_f32[c] = s;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (c < C)
+    for (int64_t g = w; g < G; g += 4) s += partial[g * C + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (out_bf16) out_bf16[c] = __float2bfloat16(t);
+    if (out_f32) out_f32[c] = t;
   }
 }
 
@@ -390,7 +399,8 @@ void bias_relu_fwd(void* y, const void* bias, int64_t M, int C, bool relu, hipSt
 }
 
 int64_t bias_relu_bwd_partials(int64_t M) {
-  return std::max<int64_t>(1, std::min<int64_t>(1024, (M + 1023) / 1024));
+  // >= 2 workgroups per CU when M allows (256 CUs); each workgroup streams >= 256 rows
+  return std::max<int64_t>(1, std::min<int64_t>(1024, (M + 255) / 256));
 }
 
 void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, float* partial, int64_t M, int C,
@@ -401,7 +411,7 @@ void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, 
   hipLaunchKernelGGL(k_bias_relu_bwd, dim3(uint32_t(G)), dim3(kBRThreads), 0, stream,
                      static_cast<const __hip_bfloat16*>(dy), static_cast<const __hip_bfloat16*>(y),
                      static_cast<__hip_bfloat16*>(dpre), partial, M, C, relu ? 1 : 0, rows_per_wg);
-  hipLaunchKernelGGL(k_colsum_partials, dim3(1), dim3(256), 0, stream, partial, G, C,
+  hipLaunchKernelGGL(k_colsum_partials, dim3(uint32_t((C + 63) / 64)), dim3(256), 0, stream, partial, G, C,
                      static_cast<__hip_bfloat16*>(dbias_bf16), static_cast<float*>(nullptr));
   RMM_HIP_CHECK(hipGetLastError());
 }

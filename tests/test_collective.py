@@ -7,8 +7,7 @@ import ray_memory_management_amd as ray
 from ray_memory_management_amd.util import collective as col
 
 
-@ray.remote(num_cpus=0)
-class Worker:
+class _WorkerBase:
     def __init__(self, device="cpu"):
         self.device = device
 
@@ -48,6 +47,9 @@ class Worker:
         return out
 
 
+Worker = ray.remote(num_cpus=0)(_WorkerBase)
+
+
 def _check(outs, n):
     s = sum(range(1, n + 1))
     for r, o in enumerate(outs):
@@ -68,19 +70,21 @@ def test_gloo_collectives_between_actors(ray_start, n):
 
 
 @pytest.mark.gpu
-def test_rccl_collectives_single_gpu_pair():
-    """Two actors sharing the one GPU of the box (RCCL allows it for correctness checks)."""
+@pytest.mark.parametrize("backend", ["nccl", "gloo"])
+def test_gpu_tensor_collectives(backend):
+    """GPU tensors between actors: RCCL needs one GPU per rank (skipped on a 1-GPU box);
+    gloo over GPU tensors runs two ranks on one GPU."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    ray.init(num_cpus=2, num_gpus=1, object_store_memory=256 << 20)
+    ngpu = torch.cuda.device_count()
+    if backend == "nccl" and ngpu < 2:
+        pytest.skip("RCCL rejects two ranks on one GPU; needs >= 2 GPUs")
+    ray.init(num_cpus=2, num_gpus=ngpu, object_store_memory=256 << 20)
     try:
-        @ray.remote(num_gpus=0.5, num_cpus=0)
-        class G(Worker):
-            pass
-
+        G = ray.remote(num_gpus=1 if backend == "nccl" else 0.5, num_cpus=0)(_WorkerBase)
         ws = [G.remote("cuda") for _ in range(2)]
-        col.create_collective_group(ws, 2, [0, 1], backend="nccl", group_name="rccl")
-        outs = ray.get([w.run.remote("rccl") for w in ws], timeout=180)
+        col.create_collective_group(ws, 2, [0, 1], backend=backend, group_name="gpu")
+        outs = ray.get([w.run.remote("gpu") for w in ws], timeout=180)
         _check(outs, 2)
     finally:
         ray.shutdown()

@@ -85,13 +85,23 @@ def test_checkpoint_roundtrip(tmp_path):
 def test_torch_trainer_rccl_gpu(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    ray.init(num_cpus=4, num_gpus=1, object_store_memory=256 << 20)
+    from ray_memory_management_amd.train.torch import TorchConfig
+
+    ngpu = torch.cuda.device_count()
+    ray.init(num_cpus=4, num_gpus=ngpu, object_store_memory=256 << 20)
     try:
+        # one worker per GPU over RCCL (world = #GPUs on the box)
         res = TorchTrainer(_loop, train_loop_config={"epochs": 3},
-                           scaling_config=ScalingConfig(num_workers=2, use_gpu=True,
-                                                        resources_per_worker={"CPU": 1, "GPU": 0.5}),
+                           scaling_config=ScalingConfig(num_workers=ngpu, use_gpu=True),
                            run_config=RunConfig(name="g", local_dir=str(tmp_path))).fit()
         assert res.error is None, res.error
         assert res.metrics["replicas_equal"]
+        # two GPU workers sharing one GPU over gloo (exercises the multi-worker GPU path)
+        res = TorchTrainer(_loop, train_loop_config={"epochs": 2}, torch_config=TorchConfig(backend="gloo"),
+                           scaling_config=ScalingConfig(num_workers=2, use_gpu=True,
+                                                        resources_per_worker={"CPU": 1, "GPU": 0.5}),
+                           run_config=RunConfig(name="g2", local_dir=str(tmp_path))).fit()
+        assert res.error is None, res.error
+        assert res.metrics["replicas_equal"] and res.metrics["world"] == 2
     finally:
         ray.shutdown()
