@@ -197,6 +197,13 @@ PYBIND11_MODULE(_hip, m) {
                  P<int64_t>(act_now), B, A, S(stream));
   });
 
+  m.def("synth_env_step", [](uint64_t frames, uint64_t pool, uint64_t actions, uint64_t tenv, uint64_t ctr_t,
+                             uint64_t buf_obs, uint64_t buf_rew, uint64_t buf_done, uint32_t seed, int episode_len,
+                             int64_t B, uint64_t stream) {
+    synth_env_step(P<uint8_t>(frames), P<const uint8_t>(pool), P<const int64_t>(actions), P<int32_t>(tenv),
+                   P<const int64_t>(ctr_t), buf_obs ? P<uint8_t>(buf_obs) : nullptr, P<float>(buf_rew),
+                   P<float>(buf_done), seed, episode_len, B, S(stream));
+  });
   m.def("bias_relu_fwd", [](uint64_t y, uint64_t bias, int64_t M, int C, bool relu, uint64_t stream) {
     bias_relu_fwd(P<void>(y), P<const void>(bias), M, C, relu, S(stream));
   });

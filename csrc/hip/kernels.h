@@ -68,6 +68,12 @@ void sample_store(const void* logits, bool logits_bf16, const void* values, bool
                   const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf, float* lout,
                   int64_t* act_now, int64_t B, int A, hipStream_t stream);
 
+// K9: synthetic 84x84x4 Atari vector-env step fused with the rollout-buffer writes.
+// ctr_t = device int64[2] {rng counter, rollout row}.
+void synth_env_step(uint8_t* frames, const uint8_t* pool, const int64_t* actions, int32_t* tenv, const int64_t* ctr_t,
+                    uint8_t* buf_obs, float* buf_rew, float* buf_done, uint32_t seed, int episode_len, int64_t B,
+                    hipStream_t stream);
+
 // K8: conv epilogue for NHWC bf16 maps [M, C]: y = relu(y + b) in place; backward dpre = dy*(y>0)
 // and db = column sums of dpre (two-pass, deterministic; `partial` holds bias_relu_bwd_partials(M)*C f32).
 void bias_relu_fwd(void* y, const void* bias, int64_t M, int C, bool relu, hipStream_t stream);

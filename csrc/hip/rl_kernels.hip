@@ -291,6 +291,66 @@ void sample_store(const void* logits, bool logits_bf16, const void* values, bool
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+// ============================================================== K9 synthetic Atari env step
+
+// One thread per (env, pixel): stores the CURRENT observation into the rollout buffer row *t_ptr,
+// shifts the 4-frame stack in place and writes the new frame (pooled frame chosen by a counter
+// hash, shifted by 3*(action%4) columns); the (0,0) thread of each env also writes the reward
+// (Bernoulli 0.05), advances the episode clock and writes done. Replaces ~12 PyTorch launches and
+// the observation index_copy of a rollout step.
+__global__ __launch_bounds__(256) void k_synth_env_step(uint8_t* __restrict__ frames, const uint8_t* __restrict__ pool,
+                                                       const int64_t* __restrict__ actions, int32_t* __restrict__ tenv,
+                                                       const int64_t* __restrict__ ctr_t, uint8_t* __restrict__ buf_obs,
+                                                       float* __restrict__ buf_rew, float* __restrict__ buf_done,
+                                                       uint32_t seed, int episode_len, int64_t B) {
+  constexpr int H = 84, W = 84, HW = H * W, C = 4;
+  const uint32_t ctr = uint32_t(ctr_t[0]);
+  const int64_t trow = ctr_t[1];
+  const int64_t total = B * HW;
+  for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < total; p += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = p / HW;
+    const int s = int(p - b * HW);
+    const int h = s / W, w = s - h * W;
+    uint8_t* f = frames + b * C * HW + s;
+    const uint8_t f0 = f[0], f1 = f[HW], f2 = f[2 * HW], f3 = f[3 * HW];
+    if (buf_obs) {
+      uint8_t* o = buf_obs + (trow * B + b) * C * HW + s;
+      o[0] = f0;
+      o[HW] = f1;
+      o[2 * HW] = f2;
+      o[3 * HW] = f3;
+    }
+    const uint32_t pidx = hash3(seed, ctr, uint32_t(b) * 2u) & 63u;
+    const int shift = int(actions[b] & 3) * 3;
+    int src_w = w - shift;
+    if (src_w < 0) src_w += W;
+    const uint8_t nf = pool[pidx * HW + h * W + src_w];
+    f[0] = f1;
+    f[HW] = f2;
+    f[2 * HW] = f3;
+    f[3 * HW] = nf;
+    if (s == 0) {
+      const uint32_t hr = hash3(seed, ctr, uint32_t(b) * 2u + 1u);
+      const float u = float(hr >> 8) * (1.0f / 16777216.0f);
+      int32_t t = tenv[b] + 1;
+      const bool done = t >= episode_len;
+      tenv[b] = done ? 0 : t;
+      buf_rew[trow * B + b] = u < 0.05f ? 1.f : 0.f;
+      buf_done[trow * B + b] = done ? 1.f : 0.f;
+    }
+  }
+}
+
+void synth_env_step(uint8_t* frames, const uint8_t* pool, const int64_t* actions, int32_t* tenv, const int64_t* ctr_t,
+                    uint8_t* buf_obs, float* buf_rew, float* buf_done, uint32_t seed, int episode_len, int64_t B,
+                    hipStream_t stream) {
+  int64_t total = B * 84 * 84;
+  int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(k_synth_env_step, dim3(uint32_t(blocks)), dim3(256), 0, stream, frames, pool, actions, tenv,
+                     ctr_t, buf_obs, buf_rew, buf_done, seed, episode_len, B);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 // ============================================================== K8 conv epilogue: bias + ReLU
 
 // y[M, C] (NHWC conv output, bf16) <- relu(y + bias). 8 channels (16 B) per thread.

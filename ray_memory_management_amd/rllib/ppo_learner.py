@@ -380,10 +380,15 @@ class GPURolloutSampler:
             logits, _ = self.model(self.s_obs)
         self.A = logits.shape[-1]
         self.buf_logits = torch.empty((T, B, self.A), dtype=torch.float32, device=dev)
-        self.t_idx = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        # device-side {rng counter, rollout row}; both advance by one per step (one add launch)
+        self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.ctr = self.ctr_t[0:1]
+        self.t_idx = self.ctr_t[1:2]
         self.seed = int(seed) & 0xFFFFFFFF
         self.fast = dev.type == "cuda"
+        self.fused_env = self.fast and hasattr(env, "fused_step")
+        if self.fused_env:
+            self.s_obs = env.frames  # the env's frame stack IS the observation buffer
         self.graphs = use_graphs and self.fast and not os.environ.get("RMM_NO_GRAPHS")
         self._graph = None
 
@@ -405,13 +410,15 @@ class GPURolloutSampler:
             self.buf_logp.index_copy_(0, t, d.logp(a).unsqueeze(0))
             self.buf_vf.index_copy_(0, t, v.float().unsqueeze(0))
             self.buf_logits.index_copy_(0, t, logits.float().unsqueeze(0))
-        self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
-        obs, r, done = self.env.step(a)
-        self.s_obs.copy_(obs)
-        self.buf_rew.index_copy_(0, t, r.unsqueeze(0))
-        self.buf_done.index_copy_(0, t, done.unsqueeze(0))
-        self.t_idx.add_(1)
-        self.ctr.add_(1)
+        if self.fused_env:  # K9: obs row write + frame-stack step + reward/done in one launch
+            self.env.fused_step(a, self.ctr_t, self.buf_obs, self.buf_rew, self.buf_done, self.seed)
+        else:
+            self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
+            obs, r, done = self.env.step(a)
+            self.s_obs.copy_(obs)
+            self.buf_rew.index_copy_(0, t, r.unsqueeze(0))
+            self.buf_done.index_copy_(0, t, done.unsqueeze(0))
+        self.ctr_t.add_(1)
 
     def _capture(self):
         s = torch.cuda.Stream(self.device)

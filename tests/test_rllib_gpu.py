@@ -159,6 +159,33 @@ def test_many_graph_replays_stay_finite(cuda):
     assert torch.isfinite(L.master).all()
 
 
+def test_fused_env_step_semantics(cuda):
+    from ray_memory_management_amd.rllib.env import GPUSyntheticAtariVectorEnv
+
+    env = GPUSyntheticAtariVectorEnv(7, cuda, num_actions=4, episode_len=3, seed=1)
+    env.t.zero_()
+    T, B = 5, 7
+    buf_obs = torch.zeros((T, B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    rew = torch.full((T, B), -1.0, device=cuda)
+    done = torch.full((T, B), -1.0, device=cuda)
+    ctr_t = torch.zeros(2, dtype=torch.int64, device=cuda)
+    for t in range(T):
+        before = env.frames.clone()
+        a = torch.randint(0, 4, (B,), device=cuda)
+        env.fused_step(a, ctr_t, buf_obs, rew, done, seed=9)
+        ctr_t += 1
+        assert torch.equal(buf_obs[t], before)                      # current obs stored at row t
+        assert torch.equal(env.frames[:, :3], before[:, 1:])        # stack shifted
+        # new frame = some pool frame shifted right by 3*(a%4) columns
+        nf = env.frames[:, 3]
+        for b in range(B):
+            sh = int(a[b] % 4) * 3
+            unshift = torch.roll(nf[b], -sh, dims=1)
+            assert any(torch.equal(unshift, env.pool[k]) for k in range(64))
+    assert set(rew.unique().tolist()) <= {0.0, 1.0}
+    assert done[2].eq(1).all() and done[0].eq(0).all()              # episode_len = 3
+
+
 def test_learning_reduces_value_loss(cuda):
     """A few PPO iterations on the synthetic env must reduce the value loss (sanity of training)."""
     from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler

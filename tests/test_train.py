@@ -31,7 +31,7 @@ def _loop(config):
         loss.backward()
         opt.step()
         # DDP keeps replicas identical
-        p = torch.cat([q.detach().reshape(-1).cpu() for q in model.parameters()])
+        p = torch.cat([q.detach().reshape(-1) for q in model.parameters()])  # on the PG's device
         ps = [torch.zeros_like(p) for _ in range(dist.get_world_size())]
         dist.all_gather(ps, p)
         same = all(torch.allclose(ps[0], q) for q in ps)
