@@ -142,14 +142,17 @@ PYBIND11_MODULE(_hip, m) {
           multi_copy(cs, S(stream));
         });
   m.def("gather_rows", [](uint64_t in, uint64_t idx, uint64_t out, int64_t rows, int64_t row_bytes,
-                          uint64_t stream) {
-    gather_rows(P<const void>(in), P<const int64_t>(idx), P<void>(out), rows, row_bytes, S(stream));
-  });
+                          uint64_t stream, uint64_t ctr, int64_t period) {
+    gather_rows(P<const void>(in), P<const int64_t>(idx), P<void>(out), rows, row_bytes, S(stream),
+                ctr ? P<const int64_t>(ctr) : nullptr, period);
+  }, py::arg("in"), py::arg("idx"), py::arg("out"), py::arg("rows"), py::arg("row_bytes"), py::arg("stream"),
+     py::arg("ctr") = 0, py::arg("period") = 1);
   m.def("frames_to_nhwc_bf16", [](uint64_t src, uint64_t idx, uint64_t dst, int64_t B, int64_t C, int64_t H,
-                                  int64_t W, float scale, uint64_t stream) {
+                                  int64_t W, float scale, uint64_t stream, uint64_t ctr, int64_t period) {
     frames_to_nhwc_bf16(P<const uint8_t>(src), idx ? P<const int64_t>(idx) : nullptr, P<void>(dst), B, C, H, W,
-                        scale, S(stream));
-  });
+                        scale, S(stream), ctr ? P<const int64_t>(ctr) : nullptr, period);
+  }, py::arg("src"), py::arg("idx"), py::arg("dst"), py::arg("B"), py::arg("C"), py::arg("H"), py::arg("W"),
+     py::arg("scale"), py::arg("stream"), py::arg("ctr") = 0, py::arg("period") = 1);
   m.def("gae", [](uint64_t rew, uint64_t val, uint64_t done, uint64_t last, uint64_t adv, uint64_t ret,
                   int64_t T, int64_t B, float gamma, float lam, uint64_t stream) {
     gae(P<const float>(rew), P<const float>(val), P<const float>(done), P<const float>(last), P<float>(adv),
@@ -185,17 +188,26 @@ PYBIND11_MODULE(_hip, m) {
                  A, S(stream));
   });
   m.def("adam_flat", [](uint64_t master, uint64_t m1, uint64_t m2, uint64_t grad, bool grad_bf16, uint64_t wbf16,
-                        uint64_t hp, float grad_scale, int64_t n, uint64_t stream) {
+                        uint64_t hp, float grad_scale, int64_t n, uint64_t stream, uint64_t step_ctr) {
     adam_flat(P<float>(master), P<float>(m1), P<float>(m2), P<const void>(grad), grad_bf16,
-              wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream));
+              wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream),
+              step_ctr ? P<const int64_t>(step_ctr) : nullptr);
+  }, py::arg("master"), py::arg("m1"), py::arg("m2"), py::arg("grad"), py::arg("grad_bf16"), py::arg("wbf16"),
+     py::arg("hp"), py::arg("grad_scale"), py::arg("n"), py::arg("stream"), py::arg("step_ctr") = 0);
+  m.def("ppo_heads_loss", [](bool bwd, uint64_t heads, uint64_t cols, uint64_t coef, uint64_t acc, uint64_t gout,
+                             uint64_t g_heads, int64_t N, int A, uint64_t stream) {
+    ppo_heads_loss(bwd, P<const void>(heads), P<const float>(cols), P<const float>(coef), P<float>(acc),
+                   P<const float>(gout), P<void>(g_heads), N, A, S(stream));
   });
   m.def("sample_store", [](uint64_t logits, bool logits_bf16, uint64_t values, bool values_bf16, uint64_t t_ptr,
                            uint64_t ctr, uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
-                           uint64_t act_now, int64_t B, int A, uint64_t stream) {
+                           uint64_t act_now, int64_t B, int A, uint64_t stream, int64_t ldl, int64_t ldv) {
     sample_store(P<const void>(logits), logits_bf16, P<const void>(values), values_bf16, P<const int64_t>(t_ptr),
                  P<const int64_t>(ctr), seed, P<int64_t>(act), P<float>(logp), P<float>(vf), P<float>(lout),
-                 P<int64_t>(act_now), B, A, S(stream));
-  });
+                 P<int64_t>(act_now), B, A, S(stream), ldl, ldv);
+  }, py::arg("logits"), py::arg("logits_bf16"), py::arg("values"), py::arg("values_bf16"), py::arg("t_ptr"),
+     py::arg("ctr"), py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"), py::arg("lout"),
+     py::arg("act_now"), py::arg("B"), py::arg("A"), py::arg("stream"), py::arg("ldl") = 0, py::arg("ldv") = 0);
 
   m.def("synth_env_step", [](uint64_t frames, uint64_t pool, uint64_t actions, uint64_t tenv, uint64_t ctr_t,
                              uint64_t buf_obs, uint64_t buf_rew, uint64_t buf_done, uint32_t seed, int episode_len,

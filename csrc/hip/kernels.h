@@ -20,11 +20,12 @@ void multi_copy(const std::vector<CopySeg>& segs, hipStream_t stream);
 
 // K2: out[i,:] = in[idx[i],:] for `rows` rows of `row_bytes` bytes (minibatch gather).
 void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, int64_t row_bytes,
-                 hipStream_t stream);
+                 hipStream_t stream, const int64_t* ctr = nullptr, int64_t period = 1);
 
 // K2b: uint8 NCHW frames (optionally gathered by idx) -> scaled bf16 NHWC (conv input).
 void frames_to_nhwc_bf16(const uint8_t* src, const int64_t* idx, void* dst, int64_t B, int64_t C, int64_t H,
-                         int64_t W, float scale, hipStream_t stream);
+                         int64_t W, float scale, hipStream_t stream, const int64_t* ctr = nullptr,
+                         int64_t period = 1);
 
 // K3: GAE over time-major [T,B] fp32 tensors. dones is fp32 0/1 (1 = episode ended after t).
 // adv[t] = delta[t] + gamma*lam*(1-d[t])*adv[t+1];  ret = adv + values.
@@ -61,12 +62,16 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
 
 // K6: flat Adam/AdamW with fp32 master weights, bf16 or fp32 grads, optional bf16 weight output.
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
-               float grad_scale, int64_t n, hipStream_t stream);
+               float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr = nullptr);
+
+// K5c: merged policy/value head PPO loss reading packed columns (see rl_kernels.hip).
+void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float* coef, float* acc, const float* gout,
+                    void* g_heads, int64_t N, int A, hipStream_t stream);
 
 // K7: Gumbel-max categorical sampling + rollout buffer writes at device-side row *t_ptr.
 void sample_store(const void* logits, bool logits_bf16, const void* values, bool values_bf16, const int64_t* t_ptr,
                   const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf, float* lout,
-                  int64_t* act_now, int64_t B, int A, hipStream_t stream);
+                  int64_t* act_now, int64_t B, int A, hipStream_t stream, int64_t ldl = 0, int64_t ldv = 0);
 
 // K9: synthetic 84x84x4 Atari vector-env step fused with the rollout-buffer writes.
 // ctr_t = device int64[2] {rng counter, rollout row}.

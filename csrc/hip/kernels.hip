@@ -118,10 +118,19 @@ void multi_copy(const std::vector<CopySeg>& segs, hipStream_t stream) {
 
 // ============================================================== K2 gather_rows
 
+// idx may be offset by a device counter: rows are taken from idx + (ctr[0] % period) * rows, so a
+// HIP graph can walk a whole epoch's permutation without any host-side copies between replays.
+__device__ __forceinline__ const int64_t* offset_idx(const int64_t* idx, const int64_t* ctr, int64_t period,
+                                                     int64_t rows) {
+  return (ctr && idx) ? idx + (ctr[0] % period) * rows : idx;
+}
+
 __global__ __launch_bounds__(256) void k_gather_rows16(const uint4* __restrict__ in,
-                                                      const int64_t* __restrict__ idx,
+                                                      const int64_t* __restrict__ idx0,
                                                       uint4* __restrict__ out, int64_t rows,
-                                                      int64_t row_vec) {
+                                                      int64_t row_vec, const int64_t* __restrict__ ctr,
+                                                      int64_t period) {
+  const int64_t* idx = offset_idx(idx0, ctr, period, rows);
   const int64_t total = rows * row_vec;
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
        e += int64_t(gridDim.x) * blockDim.x) {
@@ -131,9 +140,11 @@ __global__ __launch_bounds__(256) void k_gather_rows16(const uint4* __restrict__
 }
 
 __global__ __launch_bounds__(256) void k_gather_rows1(const uint8_t* __restrict__ in,
-                                                     const int64_t* __restrict__ idx,
+                                                     const int64_t* __restrict__ idx0,
                                                      uint8_t* __restrict__ out, int64_t rows,
-                                                     int64_t row_bytes) {
+                                                     int64_t row_bytes, const int64_t* __restrict__ ctr,
+                                                     int64_t period) {
+  const int64_t* idx = offset_idx(idx0, ctr, period, rows);
   const int64_t total = rows * row_bytes;
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
        e += int64_t(gridDim.x) * blockDim.x) {
@@ -143,18 +154,20 @@ __global__ __launch_bounds__(256) void k_gather_rows1(const uint8_t* __restrict_
 }
 
 void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, int64_t row_bytes,
-                 hipStream_t stream) {
+                 hipStream_t stream, const int64_t* ctr, int64_t period) {
   if (rows <= 0 || row_bytes <= 0) return;
   bool vec = (row_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(in) % 16 == 0) &&
              (reinterpret_cast<uintptr_t>(out) % 16 == 0);
   int64_t units = vec ? rows * (row_bytes / 16) : rows * row_bytes;
   int64_t blocks = std::min<int64_t>((units + 255) / 256, 256 * 16);
+  if (period <= 0) period = 1;
   if (vec)
     hipLaunchKernelGGL(k_gather_rows16, dim3(uint32_t(blocks)), dim3(256), 0, stream,
-                       static_cast<const uint4*>(in), idx, static_cast<uint4*>(out), rows, row_bytes / 16);
+                       static_cast<const uint4*>(in), idx, static_cast<uint4*>(out), rows, row_bytes / 16, ctr,
+                       period);
   else
     hipLaunchKernelGGL(k_gather_rows1, dim3(uint32_t(blocks)), dim3(256), 0, stream,
-                       static_cast<const uint8_t*>(in), idx, static_cast<uint8_t*>(out), rows, row_bytes);
+                       static_cast<const uint8_t*>(in), idx, static_cast<uint8_t*>(out), rows, row_bytes, ctr, period);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -163,9 +176,10 @@ void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, in
 // dst[b, h, w, c] = bf16(src[idx ? idx[b] : b, c, h, w] * scale). One thread per pixel, C <= 8.
 // Reads are coalesced per channel plane (consecutive w), writes are one 8/16-byte vector per pixel.
 template <int C>
-__global__ __launch_bounds__(256) void k_frames_nhwc(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx,
+__global__ __launch_bounds__(256) void k_frames_nhwc(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx0,
                                                     __hip_bfloat16* __restrict__ dst, int64_t B, int64_t HW,
-                                                    float scale) {
+                                                    float scale, const int64_t* __restrict__ ctr, int64_t period) {
+  const int64_t* idx = offset_idx(idx0, ctr, period, B);
   const int64_t total = B * HW;
   for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < total;
        p += int64_t(gridDim.x) * blockDim.x) {
@@ -192,15 +206,16 @@ __global__ __launch_bounds__(256) void k_frames_nhwc(const uint8_t* __restrict__
 }
 
 void frames_to_nhwc_bf16(const uint8_t* src, const int64_t* idx, void* dst, int64_t B, int64_t C, int64_t H,
-                         int64_t W, float scale, hipStream_t stream) {
+                         int64_t W, float scale, hipStream_t stream, const int64_t* ctr, int64_t period) {
   int64_t total = B * H * W;
   if (total <= 0) return;
+  if (period <= 0) period = 1;
   int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 32);
   auto* d = static_cast<__hip_bfloat16*>(dst);
   switch (C) {
-    case 1: hipLaunchKernelGGL(k_frames_nhwc<1>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale); break;
-    case 3: hipLaunchKernelGGL(k_frames_nhwc<3>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale); break;
-    case 4: hipLaunchKernelGGL(k_frames_nhwc<4>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale); break;
+    case 1: hipLaunchKernelGGL(k_frames_nhwc<1>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale, ctr, period); break;
+    case 3: hipLaunchKernelGGL(k_frames_nhwc<3>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale, ctr, period); break;
+    case 4: hipLaunchKernelGGL(k_frames_nhwc<4>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, d, B, H * W, scale, ctr, period); break;
     default: throw std::invalid_argument("frames_to_nhwc_bf16: C must be 1, 3 or 4");
   }
   RMM_HIP_CHECK(hipGetLastError());

@@ -179,6 +179,106 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+// ============================================================== K5c merged-head PPO loss
+
+// heads[N, A+1] (bf16): logits in columns [0, A), value in column A (one Linear for both heads).
+// cols[N, A+4] (f32): old logits [0, A), old logp A, advantage A+1, value target A+2, action A+3.
+// fwd: atomically accumulates the 6 stats sums into acc[0..5] (zeroed by the caller per update).
+// bwd: g_heads[N, A+1] = d(total)/d(heads) * (*gout) / N.
+template <bool kBwd>
+__global__ __launch_bounds__(256) void k_ppo_heads(const __hip_bfloat16* __restrict__ heads,
+                                                  const float* __restrict__ cols, const float* __restrict__ coef,
+                                                  float* __restrict__ acc, const float* __restrict__ gout,
+                                                  __hip_bfloat16* __restrict__ g_heads, int64_t N, int A) {
+  const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
+  const int lh = A + 1, lc = A + 4;
+  float s[6] = {0, 0, 0, 0, 0, 0};
+  const float gs = kBwd ? gout[0] / float(N) : 0.f;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += int64_t(gridDim.x) * blockDim.x) {
+    const __hip_bfloat16* hrow = heads + i * lh;
+    const float* crow = cols + i * lc;
+    float l[kMaxA], lo[kMaxA];
+    float mx = -INFINITY, mxo = -INFINITY;
+    for (int j = 0; j < A; j++) {
+      l[j] = __bfloat162float(hrow[j]);
+      lo[j] = crow[j];
+      mx = fmaxf(mx, l[j]);
+      mxo = fmaxf(mxo, lo[j]);
+    }
+    float se = 0.f, seo = 0.f;
+    for (int j = 0; j < A; j++) {
+      se += __expf(l[j] - mx);
+      seo += __expf(lo[j] - mxo);
+    }
+    const float lse = mx + __logf(se), lseo = mxo + __logf(seo);
+    float m = 0.f, kl = 0.f;
+    for (int j = 0; j < A; j++) {
+      const float p = __expf(l[j] - lse), po = __expf(lo[j] - lseo);
+      m += p * l[j];
+      kl += po * ((lo[j] - lseo) - (l[j] - lse));
+    }
+    const int a = min(max(int(crow[A + 3]), 0), A - 1);
+    const float logp = l[a] - lse;
+    const float r = __expf(logp - crow[A]);
+    const float ad = crow[A + 1];
+    const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
+    const float d = __bfloat162float(hrow[A]) - crow[A + 2];
+    if constexpr (!kBwd) {
+      const float ent = lse - m;
+      const float surr = fminf(r * ad, rc * ad);
+      const float vf = fminf(d * d, vf_clip);
+      s[0] += -surr;
+      s[1] += vf;
+      s[2] += ent;
+      s[3] += kl;
+      s[4] += (fabsf(r - 1.f) > clip) ? 1.f : 0.f;
+      s[5] += -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl;
+    } else {
+      const bool unclipped = r * ad <= rc * ad;
+      const bool inside = (r >= 1.f - clip) && (r <= 1.f + clip);
+      const float spg = (unclipped || inside) ? -(r * ad) : 0.f;
+      __hip_bfloat16* grow = g_heads + i * lh;
+      for (int j = 0; j < A; j++) {
+        const float p = __expf(l[j] - lse), po = __expf(lo[j] - lseo);
+        const float g = spg * ((j == a ? 1.f : 0.f) - p) + ent_coeff * p * (l[j] - m) + kl_coeff * (p - po);
+        grow[j] = __float2bfloat16(g * gs);
+      }
+      grow[A] = __float2bfloat16((d * d < vf_clip) ? vf_coeff * 2.f * d * gs : 0.f);
+    }
+  }
+  if constexpr (!kBwd) {
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_xor(s[k], o, 64);
+    __shared__ float red[6][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0)
+      for (int k = 0; k < 6; k++) red[k][w] = s[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      float t = 0.f;
+      for (int k = 0; k < int(blockDim.x >> 6); k++) t += red[threadIdx.x][k];
+      atomicAdd(&acc[threadIdx.x], t);
+    }
+  }
+}
+
+void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float* coef, float* acc, const float* gout,
+                    void* g_heads, int64_t N, int A, hipStream_t stream) {
+  if (A > kMaxA) throw std::invalid_argument("ppo_heads_loss: at most 32 actions");
+  if (N <= 0) return;
+  int64_t blocks = std::min<int64_t>((N + 255) / 256, 1024);
+  auto* h = static_cast<const __hip_bfloat16*>(heads);
+  if (bwd)
+    hipLaunchKernelGGL(k_ppo_heads<true>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
+                       static_cast<__hip_bfloat16*>(g_heads), N, A);
+  else
+    hipLaunchKernelGGL(k_ppo_heads<false>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
+                       static_cast<__hip_bfloat16*>(nullptr), N, A);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 // ============================================================== K6 flat Adam (fp32 master -> bf16 weights)
 
 // hp layout (device): [lr, beta1, beta2, eps, weight_decay, step]; step is incremented by the caller
@@ -187,8 +287,10 @@ template <typename TG>
 __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, float* __restrict__ m1,
                                                   float* __restrict__ m2, const TG* __restrict__ grad,
                                                   __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
-                                                  float grad_scale, int64_t n) {
-  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], step = hp[5];
+                                                  float grad_scale, int64_t n, const int64_t* __restrict__ step_ctr) {
+  // step: hp[5], or (device step counter + 1) when the counter is given (graph-friendly)
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+  const float step = step_ctr ? float(step_ctr[0] + 1) : hp[5];
   const float bc1 = 1.f - __powf(b1, step), bc2 = 1.f - __powf(b2, step);
   const float step_size = lr / bc1;
   const float bc2_sqrt = sqrtf(bc2);
@@ -207,15 +309,17 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
 }
 
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
-               float grad_scale, int64_t n, hipStream_t stream) {
+               float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr) {
   if (n <= 0) return;
   int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 8);
   if (grad_bf16)
     hipLaunchKernelGGL(k_adam_flat<__hip_bfloat16>, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2,
-                       static_cast<const __hip_bfloat16*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n);
+                       static_cast<const __hip_bfloat16*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n,
+                       step_ctr);
   else
     hipLaunchKernelGGL(k_adam_flat<float>, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2,
-                       static_cast<const float*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n);
+                       static_cast<const float*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n,
+                       step_ctr);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -232,14 +336,16 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
-// logits [B, A] (TL), values [B] (TV); writes row t (=*t_ptr) of act [T,B], logp [T,B], vf [T,B],
+// logits [B, A] (TL, row stride ldl), values [B] (TV, stride ldv — both may view one merged
+// [B, A+1] head output); writes row t (=*t_ptr) of act [T,B], logp [T,B], vf [T,B],
 // logits_out [T,B,A]; rng: uniform from hash(seed, counter, b*A+j); counter = *ctr (advanced by caller).
 template <typename TL, typename TV>
 __global__ __launch_bounds__(256) void k_sample_store(const TL* __restrict__ logits, const TV* __restrict__ values,
                                                      const int64_t* __restrict__ t_ptr, const int64_t* __restrict__ ctr,
                                                      uint32_t seed, int64_t* __restrict__ act, float* __restrict__ logp,
                                                      float* __restrict__ vf, float* __restrict__ lout,
-                                                     int64_t* __restrict__ act_now, int64_t B, int A) {
+                                                     int64_t* __restrict__ act_now, int64_t B, int A, int64_t ldl,
+                                                     int64_t ldv) {
   const int64_t t = *t_ptr;
   const uint32_t c = uint32_t(*ctr);
   for (int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; b < B; b += int64_t(gridDim.x) * blockDim.x) {
@@ -247,7 +353,7 @@ __global__ __launch_bounds__(256) void k_sample_store(const TL* __restrict__ log
     int arg = 0;
     float l[kMaxA];
     for (int j = 0; j < A; j++) {
-      l[j] = ldf(logits, b * A + j);
+      l[j] = ldf(logits, b * ldl + j);
       mx = fmaxf(mx, l[j]);
       const uint32_t h = hash3(seed, c, uint32_t(b * A + j));
       const float u = (float(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
@@ -263,21 +369,23 @@ __global__ __launch_bounds__(256) void k_sample_store(const TL* __restrict__ log
     act[o] = arg;
     act_now[b] = arg;
     logp[o] = l[arg] - mx - __logf(se);
-    vf[o] = ldf(values, b);
+    vf[o] = ldf(values, b * ldv);
     for (int j = 0; j < A; j++) lout[o * A + j] = l[j];
   }
 }
 
 void sample_store(const void* logits, bool logits_bf16, const void* values, bool values_bf16, const int64_t* t_ptr,
                   const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf, float* lout,
-                  int64_t* act_now, int64_t B, int A, hipStream_t stream) {
+                  int64_t* act_now, int64_t B, int A, hipStream_t stream, int64_t ldl, int64_t ldv) {
   if (A > kMaxA) throw std::invalid_argument("sample_store: at most 32 actions");
+  if (ldl <= 0) ldl = A;
+  if (ldv <= 0) ldv = 1;
   int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((B + 255) / 256, 1024));
   using bf = __hip_bfloat16;
 #define RMM_SS(TL, TV)                                                                                          \
   hipLaunchKernelGGL((k_sample_store<TL, TV>), dim3(uint32_t(blocks)), dim3(256), 0, stream,                   \
                      static_cast<const TL*>(logits), static_cast<const TV*>(values), t_ptr, ctr, seed, act, logp, vf, \
-                     lout, act_now, B, A);
+                     lout, act_now, B, A, ldl, ldv);
   if (logits_bf16 && values_bf16) {
     RMM_SS(bf, bf)
   } else if (logits_bf16) {

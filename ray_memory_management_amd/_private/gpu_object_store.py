@@ -197,14 +197,14 @@ def free(worker, oid: bytes):
     stores = getattr(worker, "_gpu_stores", None)
     if not stores:
         return
-    for g in stores.values():
+    for g in list(stores.values()):  # called from the reader thread while the owner may add stores
         if g.contains(oid):
             g.delete(oid)
 
 
 def stats(worker) -> dict:
     stores = getattr(worker, "_gpu_stores", None) or {}
-    return {dev: g.stats() for dev, g in stores.items()}
+    return {dev: g.stats() for dev, g in list(stores.items())}
 
 
 def shutdown_process_store(worker):

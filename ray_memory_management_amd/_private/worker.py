@@ -226,10 +226,14 @@ class CoreWorker:
                     if p is not None:
                         p.value = m[2]
                         p.ev.set()
-                elif t == P.CANCEL_TASK:
-                    self._cancel_current(m[1])
-                elif t == P.FREE_GPU:
-                    self._free_gpu(m[1])
+                elif t in (P.CANCEL_TASK, P.FREE_GPU):
+                    try:  # a failing side-channel handler must never take the reader thread down
+                        if t == P.CANCEL_TASK:
+                            self._cancel_current(m[1])
+                        else:
+                            self._free_gpu(m[1])
+                    except Exception as e:  # pragma: no cover
+                        logger.warning("handler for message %s failed: %r", t, e)
                 else:
                     self.task_queue.put(m)
         except (ConnectionError, OSError, EOFError):

@@ -103,36 +103,62 @@ def concat(tensors: Sequence[torch.Tensor], dim: int = 0) -> torch.Tensor:
     return out
 
 
-def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-    """out[i] = x[idx[i]] over dim 0 (minibatch gather)."""
+def _counter_window(idx, rows, ctr, period):
+    """CPU semantics of the device-counter gathers: the rows-long window of idx at ctr[0] % period."""
+    k = int(ctr.reshape(-1)[0]) % max(int(period), 1)
+    return idx.reshape(-1)[k * rows:(k + 1) * rows]
+
+
+def gather_rows(x: torch.Tensor, idx: torch.Tensor, rows: int = None, ctr: torch.Tensor = None,
+                period: int = 1) -> torch.Tensor:
+    """out[i] = x[idx[i]] over dim 0 (minibatch gather).
+
+    With a device counter `ctr` (int64 tensor, element 0 is read by the kernel) the indices are
+    idx[(ctr[0] % period) * rows : ... + rows] — a HIP graph walks a whole epoch's index table
+    without host-side copies between replays."""
+    if ctr is not None and rows is None:
+        raise ValueError("gather_rows: rows is required with ctr")
     if x.device.type != "cuda":
-        return x[idx]
+        return x[_counter_window(idx, rows, ctr, period) if ctr is not None else idx]
     h = require_hip()
     x = x.contiguous()
     idx = idx.to(device=x.device, dtype=torch.int64).contiguous()
-    out = torch.empty((idx.numel(), *x.shape[1:]), dtype=x.dtype, device=x.device)
+    n = idx.numel() if rows is None else int(rows)
+    if ctr is not None:
+        assert ctr.dtype == torch.int64 and ctr.device == x.device and idx.numel() >= n * period
+    out = torch.empty((n, *x.shape[1:]), dtype=x.dtype, device=x.device)
     row_bytes = x[0].numel() * x.element_size() if x.shape[0] else 0
-    if idx.numel() and row_bytes:
-        h.gather_rows(x.data_ptr(), idx.data_ptr(), out.data_ptr(), idx.numel(), row_bytes, _stream(x))
+    if n and row_bytes:
+        h.gather_rows(x.data_ptr(), idx.data_ptr(), out.data_ptr(), n, row_bytes, _stream(x),
+                      ctr=ctr.data_ptr() if ctr is not None else 0, period=int(period))
     return out
 
 
-def frames_to_nhwc(x: torch.Tensor, idx: torch.Tensor = None, scale: float = 1.0 / 255.0) -> torch.Tensor:
-    """uint8 frames [B, C, H, W] (rows optionally gathered by `idx`) → bf16 scaled, returned as a
-    [B', C, H, W] tensor in channels_last memory (what the NHWC conv kernels consume), one pass."""
+def frames_to_nhwc(x: torch.Tensor, idx: torch.Tensor = None, scale: float = 1.0 / 255.0, rows: int = None,
+                   ctr: torch.Tensor = None, period: int = 1) -> torch.Tensor:
+    """uint8 frames [B, C, H, W] (rows optionally gathered by `idx`, or by the device-counter
+    window of idx as in gather_rows) → bf16 scaled, returned as a [B', C, H, W] tensor in
+    channels_last memory (what the NHWC conv kernels consume), one pass."""
+    if ctr is not None and (rows is None or idx is None):
+        raise ValueError("frames_to_nhwc: idx and rows are required with ctr")
     if x.device.type != "cuda":
+        if ctr is not None:
+            idx = _counter_window(idx, rows, ctr, period)
         y = x[idx] if idx is not None else x
         return (y.float() * scale).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     h = require_hip()
     x = x.contiguous()
     B0, C, H, W = x.shape
-    B = idx.numel() if idx is not None else B0
+    B = int(rows) if rows is not None else (idx.numel() if idx is not None else B0)
     out = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=x.device)
     if idx is not None:
         idx = idx.to(device=x.device, dtype=torch.int64).contiguous()
+    if ctr is not None:
+        assert ctr.dtype == torch.int64 and ctr.device == x.device and idx.numel() >= B * period
     if B:
         h.frames_to_nhwc_bf16(x.data_ptr(), idx.data_ptr() if idx is not None else 0, out.data_ptr(), B, C, H, W,
-                              float(scale), _stream(x))
+                              float(scale), _stream(x), ctr=ctr.data_ptr() if ctr is not None else 0,
+                              period=int(period))
     return out.permute(0, 3, 1, 2)
 
 

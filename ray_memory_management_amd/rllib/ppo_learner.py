@@ -14,8 +14,12 @@ MI355X design (fast path, ``device.type == "cuda"``):
     sync is a single RCCL all-reduce per minibatch step over xGMI — the Atari net is ~1M params;
   * minibatch gather + uint8→bf16 NHWC conversion in one launch (K2b), the remaining columns packed
     into one fp32 matrix and gathered in one launch (K2);
-  * the whole categorical PPO loss head (log-softmax, logp, entropy, KL, ratio/clip, value clip, stats)
-    forward and backward are one launch each (K5b);
+  * policy logits + value are ONE [N, A+1] Linear; the whole categorical PPO loss (log-softmax, logp,
+    entropy, KL, ratio/clip, value clip, stats accumulated in place) forward and backward are one
+    launch each (K5c), reading all per-sample columns from one packed fp32 matrix;
+  * the update's minibatch index table is built once (one rand + one sort); the SGD-step graph
+    reads its window through a device step counter that also drives Adam's bias correction, so
+    replays need no host→device copies;
   * rollout: Gumbel-max sampling + buffer writes at a device-side step counter in one launch (K7);
   * every rollout step and every SGD step is one HIP-graph replay.
 The CPU path (rollout workers without GPUs, tests) is plain fp32 PyTorch with the same math.
@@ -78,6 +82,39 @@ class _CatPPOLoss(torch.autograd.Function):
                        values.dtype == torch.bfloat16, vtgt.data_ptr(), coef.data_ptr(), 0, g.data_ptr(),
                        g_logits.data_ptr(), g_values.data_ptr(), N, A, _stream())
         return g_logits, g_values, None, None, None, None, None, None
+
+
+class _HeadsPPOLoss(torch.autograd.Function):
+    """K5c: PPO loss on the merged [N, A+1] head output with all per-sample columns packed in one
+    fp32 matrix [N, A+4] (old logits, old logp, advantage, value target, action). The forward adds
+    the 6 stat sums into `acc` in place and returns an (unwritten) scalar handle; the backward
+    reads the upstream gradient from device memory, so the whole step is allocation/copy free."""
+
+    @staticmethod
+    def forward(ctx, heads, cols, coef, acc):
+        N, A1 = heads.shape
+        require_hip().ppo_heads_loss(False, heads.data_ptr(), cols.data_ptr(), coef.data_ptr(), acc.data_ptr(), 0, 0,
+                                     N, A1 - 1, _stream())
+        ctx.save_for_backward(heads, cols, coef)
+        return torch.empty((), dtype=torch.float32, device=heads.device)
+
+    @staticmethod
+    def backward(ctx, g):
+        heads, cols, coef = ctx.saved_tensors
+        N, A1 = heads.shape
+        g_heads = torch.empty_like(heads)
+        g = g.float().contiguous()
+        require_hip().ppo_heads_loss(True, heads.data_ptr(), cols.data_ptr(), coef.data_ptr(), 0, g.data_ptr(),
+                                     g_heads.data_ptr(), N, A1 - 1, _stream())
+        return g_heads, None, None, None
+
+
+def ppo_heads_loss(heads, cols, coef, acc):
+    """Fused PPO loss on a merged head output (see _HeadsPPOLoss). Differentiate the returned
+    handle with grad_outputs=<device scalar 1.0>; the loss VALUE is only available through acc[5]/N."""
+    assert heads.dtype == torch.bfloat16 and heads.is_contiguous() and cols.dtype == torch.float32
+    assert cols.shape == (heads.shape[0], heads.shape[1] + 3) and cols.is_contiguous()
+    return _HeadsPPOLoss.apply(heads, cols, coef, acc)
 
 
 def ppo_categorical_loss(logits, values, old_logits, actions, old_logp, adv, vtgt, coef):
@@ -169,27 +206,41 @@ class PPOLearner:
         self.coef = torch.tensor([self.cfg["clip_param"], self.cfg["vf_clip_param"], self.cfg["vf_loss_coeff"],
                                   self.cfg["entropy_coeff"], self.kl_coeff], dtype=torch.float32, device=dev)
         self.acc = torch.zeros(6, device=dev)
-        self._grad_segs = None
+        # device counters {minibatch step within the update, Adam step}: the SGD-step graph reads
+        # its minibatch indices at idx_all[ctr[0]] and the Adam bias correction from ctr[1]; one
+        # add per step advances both, so no host→device copy happens between graph replays.
+        self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._one = torch.ones((), dtype=torch.float32, device=dev)
+        self.heads_ok = hasattr(self.model, "forward_heads")
 
     def _opt_step(self):
         h = require_hip()
         if self.world > 1:
             torch.distributed.all_reduce(self.flat_grad, group=self.pg)
-        self.hp[5:6].add_(1.0)
         h.adam_flat(self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
-                    self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream())
+                    self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream(),
+                    step_ctr=self.ctr.data_ptr() + 8)
+        self.ctr.add_(1)
 
-    def _fast_step(self, full, idx, with_opt: bool):
+    def _fast_step(self, full, with_opt: bool):
         h = require_hip()
-        x = ops.frames_to_nhwc(full["obs"], idx)            # K2b: gather + u8→bf16 NHWC
-        cols = ops.gather_rows(full["cols"], idx)            # K2: one gather for all float columns
-        act = ops.gather_rows(full["actions"], idx)
-        A = full["A"]
-        old_logits = cols[:, :A]
-        old_logp, adv, vtgt = cols[:, A], cols[:, A + 1], cols[:, A + 2]
-        logits, v = self.model(x, prescaled=True)
-        total, stats = ppo_categorical_loss(logits, v, old_logits, act, old_logp, adv, vtgt, self.coef)
-        grads = list(torch.autograd.grad(total, self.params))
+        mbs, period = full["mbs"], full["period"]
+        ctr = self.ctr
+        # K2b: minibatch gather + u8→bf16 NHWC; K2: ONE gather for every per-sample column —
+        # both index idx_all at the device step counter
+        x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
+        cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
+        if self.heads_ok:
+            heads = self.model.forward_heads(x, prescaled=True)
+            total = ppo_heads_loss(heads, cols, self.coef, self.acc)     # K5c
+            grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
+        else:
+            A = full["A"]
+            logits, v = self.model(x, prescaled=True)
+            total, stats = ppo_categorical_loss(logits, v, cols[:, :A], cols[:, A + 3].long(), cols[:, A],
+                                                cols[:, A + 1], cols[:, A + 2], self.coef)
+            grads = list(torch.autograd.grad(total, self.params))
+            self.acc.add_(stats)
         for i, (g, p) in enumerate(zip(grads, self.params)):
             if g.stride() != p.stride() and g.numel() > 1:  # match the flat bucket's memory order
                 grads[i] = torch.empty_strided(p.size(), p.stride(), dtype=g.dtype, device=g.device).copy_(g)
@@ -200,37 +251,41 @@ class PPOLearner:
             segs.append((g.data_ptr(), self.flat_grad.data_ptr() + off * 2, nb))
             off += p.numel()
         h.multi_copy(segs, _stream())                        # K1: grads → one flat bucket
-        self.acc.add_(stats)
-        if with_opt:
+        if with_opt:  # otherwise the caller runs _opt_step (all-reduce + Adam + counters) eagerly
             self._opt_step()
 
-    def _pack(self, batch):
+    def _pack(self, batch, mbs, nmb):
+        """One fp32 column matrix [n, A+4] (old logits, old logp, adv, value target, action) and the
+        whole update's minibatch index table [iters * nmb * mbs] (one rand + one sort launch)."""
         A = batch[SampleBatch.ACTION_DIST_INPUTS].shape[-1]
+        n = batch.count
         cols = torch.cat([batch[SampleBatch.ACTION_DIST_INPUTS].float(),
                           batch[SampleBatch.ACTION_LOGP].float().unsqueeze(1),
                           batch[SampleBatch.ADVANTAGES].float().unsqueeze(1),
-                          batch[SampleBatch.VALUE_TARGETS].float().unsqueeze(1)], dim=1).contiguous()
-        return {"obs": batch[SampleBatch.OBS].contiguous(), "cols": cols,
-                "actions": batch[SampleBatch.ACTIONS].to(torch.int64).contiguous(), "A": A}
+                          batch[SampleBatch.VALUE_TARGETS].float().unsqueeze(1),
+                          batch[SampleBatch.ACTIONS].float().reshape(n, 1)], dim=1).contiguous()
+        iters = self.cfg["num_sgd_iter"]
+        idx = torch.rand(iters, n, device=self.device).argsort(dim=1)[:, :nmb * mbs].reshape(-1).contiguous()
+        return {"obs": batch[SampleBatch.OBS].contiguous(), "cols": cols, "idx": idx, "A": A, "mbs": mbs,
+                "period": iters * nmb}
 
-    def _capture(self, full, mbs):
+    def _capture(self, full):
         in_graph_opt = self.world == 1 or self.cfg["allreduce_in_graph"]
-        self._sidx = torch.arange(mbs, device=self.device, dtype=torch.int64)
-        saved = (self.master.clone(), self.m1.clone(), self.m2.clone(), self.hp.clone(), self.w_bf16.clone())
+        saved = (self.master.clone(), self.m1.clone(), self.m2.clone(), self.w_bf16.clone(), self.ctr.clone(),
+                 self.acc.clone())
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(3):  # warm up (MIOpen find, allocator) before capture
-                self._fast_step(full, self._sidx, in_graph_opt)
+                self._fast_step(full, in_graph_opt)
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._fast_step(full, self._sidx, in_graph_opt)
-        for dst, src in zip((self.master, self.m1, self.m2, self.hp, self.w_bf16), saved):
+            self._fast_step(full, in_graph_opt)
+        for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc), saved):
             dst.copy_(src)  # undo warm-up updates
         self._graph = g
         self._graph_opt = in_graph_opt
-        self._mbs = mbs
 
     # ------------------------------------------------------------------ update
     def update(self, batch: SampleBatch) -> Dict[str, float]:
@@ -244,18 +299,21 @@ class PPOLearner:
         nmb = max(n // mbs, 1)
         if not self.fast:
             return self._update_eager(batch, mbs)
-        packed = self._pack(batch)
+        packed = self._pack(batch, mbs, nmb)
+        self.acc.zero_()
+        self.coef[4].fill_(self.kl_coeff)
         if self.graphs:
             st = self._static
-            if st is None or st["obs"].shape != packed["obs"].shape or st["cols"].shape != packed["cols"].shape:
+            if st is None or any(st[k].shape != packed[k].shape for k in ("obs", "cols", "idx")) \
+                    or st["mbs"] != mbs:
                 self._static = st = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in packed.items()}
                 self._graph = None
             else:
-                for k in ("obs", "cols", "actions"):
+                for k in ("obs", "cols", "idx"):
                     st[k].copy_(packed[k])
-            if self._graph is None or self._mbs != mbs:
+            if self._graph is None:
                 try:
-                    self._capture(st, mbs)
+                    self._capture(st)
                 except Exception as e:  # pragma: no cover - capture unsupported: stay eager
                     print(f"[PPOLearner] HIP graph capture failed ({e!r}); running eagerly")
                     self.graphs = False
@@ -263,21 +321,16 @@ class PPOLearner:
             full = st if self.graphs else packed
         else:
             full = packed
-        self.acc.zero_()
-        self.coef[4].fill_(self.kl_coeff)
+        self.ctr[0:1].zero_()
         steps = 0
-        for _ in range(c["num_sgd_iter"]):
-            perm = torch.randperm(n, device=self.device)
-            for i in range(nmb):
-                idx = perm[i * mbs:(i + 1) * mbs]
-                if self.graphs:
-                    self._sidx.copy_(idx)
-                    self._graph.replay()
-                    if not self._graph_opt:
-                        self._opt_step()
-                else:
-                    self._fast_step(full, idx, True)
-                steps += 1
+        for _ in range(c["num_sgd_iter"] * nmb):
+            if self.graphs:
+                self._graph.replay()
+                if not self._graph_opt:
+                    self._opt_step()
+            else:
+                self._fast_step(full, True)
+            steps += 1
         if self.world > 1:  # KL adaptation and stats from the global batch, identical on every rank
             torch.distributed.all_reduce(self.acc, group=self.pg)
             self.acc.mul_(1.0 / self.world)
@@ -394,16 +447,25 @@ class GPURolloutSampler:
 
     @torch.no_grad()
     def _step_body(self):
-        logits, v = self.model(self.s_obs)
         t = self.t_idx
         if self.fast:
+            if hasattr(self.model, "forward_heads"):  # merged [B, A+1] head read in place (strided)
+                hd = self.model.forward_heads(self.s_obs)
+                lp, vp, ld = hd.data_ptr(), hd.data_ptr() + self.A * hd.element_size(), hd.stride(0)
+                lbf = vbf = hd.dtype == torch.bfloat16
+                lds = (ld, ld)
+            else:
+                logits, v = self.model(self.s_obs)
+                logits, v = logits.contiguous(), v.contiguous()
+                lp, vp, lbf, vbf, lds = (logits.data_ptr(), v.data_ptr(), logits.dtype == torch.bfloat16,
+                                         v.dtype == torch.bfloat16, (self.A, 1))
             require_hip().sample_store(
-                logits.data_ptr(), logits.dtype == torch.bfloat16, v.data_ptr(), v.dtype == torch.bfloat16,
-                t.data_ptr(), self.ctr.data_ptr(), self.seed, self.buf_act.data_ptr(), self.buf_logp.data_ptr(),
-                self.buf_vf.data_ptr(), self.buf_logits.data_ptr(), self.act_now.data_ptr(), self.B, self.A,
-                _stream())
+                lp, lbf, vp, vbf, t.data_ptr(), self.ctr.data_ptr(), self.seed, self.buf_act.data_ptr(),
+                self.buf_logp.data_ptr(), self.buf_vf.data_ptr(), self.buf_logits.data_ptr(),
+                self.act_now.data_ptr(), self.B, self.A, _stream(), ldl=lds[0], ldv=lds[1])
             a = self.act_now
         else:
+            logits, v = self.model(self.s_obs)
             d = Categorical(logits.float())
             a = d.sample()
             self.buf_act.index_copy_(0, t, a.unsqueeze(0))

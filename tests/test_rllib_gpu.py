@@ -198,3 +198,65 @@ def test_learning_reduces_value_loss(cuda):
     for _ in range(6):
         last = lg.update(sampler.sample())["vf_loss"]
     assert last < first
+
+
+def test_fused_heads_loss_matches_reference(cuda):
+    """K5c (merged [N, A+1] head, packed columns, stats accumulated in place) vs fp32 torch."""
+    from ray_memory_management_amd.rllib.ppo_learner import ppo_categorical_loss_reference, ppo_heads_loss
+
+    torch.manual_seed(5)
+    N, A = 777, 6
+    heads = (torch.randn(N, A + 1, device=cuda) * 2).to(torch.bfloat16).requires_grad_()
+    old_logits = torch.randn(N, A, device=cuda)
+    act = torch.randint(0, A, (N,), device=cuda)
+    old_logp = torch.log_softmax(old_logits, -1).gather(1, act[:, None]).squeeze(1)
+    adv, vt = torch.randn(N, device=cuda), torch.randn(N, device=cuda) * 3
+    cols = torch.cat([old_logits, old_logp[:, None], adv[:, None], vt[:, None], act[:, None].float()], 1).contiguous()
+    coef = torch.tensor([0.2, 4.0, 0.5, 0.01, 0.3], device=cuda)
+    acc = torch.full((6,), 1.0, device=cuda)  # accumulates on top of what is there
+    h = ppo_heads_loss(heads, cols, coef, acc)
+    (g,) = torch.autograd.grad(h, heads, grad_outputs=torch.tensor(2.0, device=cuda))
+    hf = heads.detach().float().requires_grad_()
+    rt, rstats = ppo_categorical_loss_reference(hf[:, :A], hf[:, A], old_logits, act, old_logp, adv, vt, coef)
+    (2.0 * rt).backward()
+    torch.testing.assert_close(acc - 1.0, rstats, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(g.float(), hf.grad, rtol=2e-2, atol=1e-5)
+
+
+def test_counter_gathers_walk_index_table(cuda):
+    from ray_memory_management_amd import ops
+
+    torch.manual_seed(0)
+    n, rows, period = 300, 40, 5
+    frames = torch.randint(0, 255, (n, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    cols = torch.randn(n, 10, device=cuda)
+    idx = torch.randperm(n, device=cuda)[:rows * period].contiguous()
+    ctr = torch.zeros(2, dtype=torch.int64, device=cuda)
+    for k in range(period + 2):  # wraps modulo period
+        sel = idx[(k % period) * rows:(k % period + 1) * rows]
+        torch.testing.assert_close(ops.gather_rows(cols, idx, rows=rows, ctr=ctr, period=period), cols[sel])
+        x = ops.frames_to_nhwc(frames, idx, rows=rows, ctr=ctr, period=period)
+        torch.testing.assert_close(x.float(), (frames[sel].float() / 255.0).to(torch.bfloat16).float())
+        ctr.add_(1)
+
+
+def test_adam_step_counter_matches_host_step(cuda):
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    torch.manual_seed(0)
+    n = 4099
+    s = torch.cuda.current_stream().cuda_stream
+    st = [torch.randn(n, device=cuda) for _ in range(1)] * 2
+    ma, mb = st[0].clone(), st[1].clone()
+    z = [torch.zeros(n, device=cuda) for _ in range(4)]
+    hp = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0, 0.0], device=cuda)
+    ctr = torch.zeros(2, dtype=torch.int64, device=cuda)
+    for _ in range(4):
+        g = torch.randn(n, device=cuda)
+        hp[5] += 1
+        h.adam_flat(ma.data_ptr(), z[0].data_ptr(), z[1].data_ptr(), g.data_ptr(), False, 0, hp.data_ptr(), 1.0, n, s)
+        h.adam_flat(mb.data_ptr(), z[2].data_ptr(), z[3].data_ptr(), g.data_ptr(), False, 0, hp.data_ptr(), 1.0, n, s,
+                    step_ctr=ctr.data_ptr() + 8)
+        ctr.add_(1)
+    torch.testing.assert_close(ma, mb, rtol=0, atol=0)
