@@ -537,20 +537,35 @@ __global__ __launch_bounds__(kBRThreads) void k_bias_relu_bwd(const __hip_bfloat
   }
 }
 
-// Column sums of partial[G, C]: blockIdx.x owns channels [c0, c0 + 64); 4 waves stride over G with
-// coalesced row reads (lane = channel), then a 4-way LDS combine. Fixed order => deterministic.
+// Column sums of partial[G, C]: blockIdx.x owns channels [c0, c0 + cb) with cb = min(C, 64);
+// the 256 threads form (256 / cb) row slots x cb channels, each slot sums a strided subset of the
+// G rows (independent loads in flight), then slots combine through LDS in a fixed order =>
+// deterministic. (One slot per wave was latency bound: ~30 us for G ~ 900 on gfx950.)
 __global__ __launch_bounds__(256) void k_colsum_partials(const float* __restrict__ partial, int64_t G, int C,
                                                         __hip_bfloat16* __restrict__ out_bf16, float* __restrict__ out_f32) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  __shared__ float red[256];
+  const int cb = C < 64 ? C : 64;
+  const int nslots = 256 / cb;
+  const int slot = threadIdx.x / cb, lc = threadIdx.x % cb;
+  const int c = blockIdx.x * 64 + lc;
   float s = 0.f;
-  if (c < C)
-    for (int64_t g = w; g < G; g += 4) s += partial[g * C + c];
-  red[w][lane] = s;
+  if (slot < nslots && c < C) {
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t g = slot;
+    for (; g + 3 * nslots < G; g += 4 * nslots) {
+      s += partial[g * C + c];
+      s1 += partial[(g + nslots) * C + c];
+      s2 += partial[(g + 2 * nslots) * C + c];
+      s3 += partial[(g + 3 * nslots) * C + c];
+    }
+    for (; g < G; g += nslots) s += partial[g * C + c];
+    s = (s + s1) + (s2 + s3);
+  }
+  red[threadIdx.x] = s;
   __syncthreads();
-  if (w == 0 && c < C) {
-    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (threadIdx.x < cb && c < C) {
+    float t = 0.f;
+    for (int k = 0; k < nslots; k++) t += red[k * cb + threadIdx.x];
     if (out_bf16) out_bf16[c] = __float2bfloat16(t);
     if (out_f32) out_f32[c] = t;
   }
@@ -567,8 +582,9 @@ void bias_relu_fwd(void* y, const void* bias, int64_t M, int C, bool relu, hipSt
 }
 
 int64_t bias_relu_bwd_partials(int64_t M) {
-  // >= 2 workgroups per CU when M allows (256 CUs); each workgroup streams >= 256 rows
-  return std::max<int64_t>(1, std::min<int64_t>(1024, (M + 255) / 256));
+  // one workgroup per CU at most (256 CUs), each streaming >= 512 rows: enough bytes in flight
+  // for HBM while keeping the second-pass column sum short
+  return std::max<int64_t>(1, std::min<int64_t>(256, (M + 511) / 512));
 }
 
 void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, float* partial, int64_t M, int C,
