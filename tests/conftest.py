@@ -31,3 +31,13 @@ def ray_start():
     ray.init(num_cpus=4, object_store_memory=256 << 20, ignore_reinit_error=True)
     yield ray
     ray.shutdown()
+
+
+@pytest.fixture(scope="module")
+def ray_shared():
+    """One cluster shared by every test of a module (for tests that do not disturb cluster state)."""
+    import ray_memory_management_amd as ray
+
+    ray.init(num_cpus=4, object_store_memory=256 << 20, ignore_reinit_error=True)
+    yield ray
+    ray.shutdown()
