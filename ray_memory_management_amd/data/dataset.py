@@ -1,0 +1,718 @@
+"""Dataset: a distributed collection of blocks in the object store.
+
+Parity: reference python/ray/data/dataset.py (Dataset: map / map_batches / flat_map / filter /
+add_column / drop_columns / repartition / random_shuffle / randomize_block_order / random_sample
+/ split / split_at_indices / split_proportionately / train_test_split / union / zip / groupby /
+aggregate / sum / min / max / mean / std / sort / limit / take / take_all / show / count / schema
+/ num_blocks / size_bytes / input_files / write_* / iter_rows / iter_batches /
+iter_torch_batches / to_torch / to_pandas / to_*_refs / repeat / window / fully_executed / stats
+/ lazy / get_internal_block_refs) and python/ray/data/_internal/plan.py (lazy plans with stage
+fusion).
+
+Execution: one-to-one stages are appended to the plan and, unless the Dataset is lazy, executed
+immediately; consecutive task-compute stages with the same resource options are FUSED into one
+task per block. All-to-all operations (shuffle, sort, repartition, groupby) are map/reduce
+exchanges of block partitions through the shared-memory store (see _internal.py).
+"""
+from __future__ import annotations
+
+import collections
+import itertools
+import math
+import os
+import time
+from typing import Any, Callable, Dict, Iterator, List, Optional, Union
+
+import numpy as np
+
+import ray_memory_management_amd as ray
+from ray_memory_management_amd.data import _internal as I
+from ray_memory_management_amd.data.aggregate import AggregateFn, Max, Mean, Min, Std, Sum
+from ray_memory_management_amd.data.block import (TENSOR_COL, BlockAccessor, BlockMetadata, NumpyBlock,
+                                                  concat_blocks)
+from ray_memory_management_amd.data.context import DatasetContext
+
+
+class _Stage:
+    def __init__(self, name, transform: I.BlockTransform, compute, remote_args):
+        self.name, self.transform, self.compute, self.remote_args = name, transform, compute, remote_args or {}
+
+    def can_fuse(self, other: "_Stage") -> bool:
+        return (isinstance(self.compute, I.TaskPoolStrategy) and isinstance(other.compute, I.TaskPoolStrategy)
+                and self.remote_args == other.remote_args)
+
+
+class ExecutionPlan:
+    def __init__(self, blocks: List[Any], metas: List[Any], stats: Optional[I.DatasetStats] = None):
+        self.in_blocks = list(blocks)
+        self.in_metas = list(metas)       # BlockMetadata or ObjectRef[BlockMetadata]
+        self.stages: List[_Stage] = []
+        self.stats = stats or I.DatasetStats()
+
+    def copy(self) -> "ExecutionPlan":
+        p = ExecutionPlan(self.in_blocks, self.in_metas, I.DatasetStats(self.stats))
+        p.stages = list(self.stages)
+        return p
+
+    def with_stage(self, st: _Stage) -> "ExecutionPlan":
+        p = self.copy()
+        p.stages.append(st)
+        return p
+
+    def is_executed(self) -> bool:
+        return not self.stages
+
+    def execute(self) -> "ExecutionPlan":
+        if self.stages:
+            blocks = self.in_blocks
+            metas = self.in_metas
+            i = 0
+            while i < len(self.stages):
+                group = [self.stages[i]]
+                while i + len(group) < len(self.stages) and group[-1].can_fuse(self.stages[i + len(group)]):
+                    group.append(self.stages[i + len(group)])
+                t0 = time.perf_counter()
+                blocks, metas = I.run_transforms(blocks, [s.transform for s in group], group[0].compute,
+                                                 group[0].remote_args)
+                name = "->".join(s.name for s in group)
+                if DatasetContext.get_current().block_until_stage_done:
+                    ray.wait(metas, num_returns=len(metas))
+                self.stats.record(name, len(blocks), time.perf_counter() - t0)
+                i += len(group)
+            self.in_blocks, self.in_metas, self.stages = list(blocks), list(metas), []
+        return self
+
+    def metadata(self) -> List[BlockMetadata]:
+        self.execute()
+        refs = [(i, m) for i, m in enumerate(self.in_metas) if isinstance(m, ray.ObjectRef)]
+        if refs:
+            vals = ray.get([m for _, m in refs])
+            for (i, _), v in zip(refs, vals):
+                self.in_metas[i] = v
+        return self.in_metas
+
+
+def _fn_name(fn) -> str:
+    return getattr(fn, "__name__", type(fn).__name__)
+
+
+class Dataset:
+    def __init__(self, plan: ExecutionPlan, epoch: int = 0, lazy: bool = False):
+        self._plan = plan
+        self._epoch = epoch
+        self._lazy = lazy
+        if not lazy:
+            self._plan.execute()
+
+    # ------------------------------------------------------------------ helpers
+    def _new(self, plan: ExecutionPlan) -> "Dataset":
+        return Dataset(plan, self._epoch, self._lazy)
+
+    def _one_to_one(self, name, transform, compute=None, ray_remote_args=None) -> "Dataset":
+        compute = I.get_compute(compute)
+        if isinstance(transform.fn, type) and isinstance(compute, I.TaskPoolStrategy):
+            raise ValueError("``compute`` must be specified when using a callable class. For example, use "
+                             "``compute=ActorPoolStrategy()``")
+        return self._new(self._plan.with_stage(_Stage(name, transform, compute, ray_remote_args)))
+
+    def _blocks(self) -> List[Any]:
+        self._plan.execute()
+        return list(self._plan.in_blocks)
+
+    def _metas(self) -> List[BlockMetadata]:
+        return self._plan.metadata()
+
+    def _counts(self) -> List[int]:
+        return [m.num_rows for m in self._metas()]
+
+    def _from_refs(self, blocks, metas, stage_name: Optional[str] = None, t0: Optional[float] = None):
+        st = I.DatasetStats(self._plan.stats)
+        if stage_name:
+            st.record(stage_name, len(blocks), time.perf_counter() - (t0 or time.perf_counter()))
+        return Dataset(ExecutionPlan(blocks, metas, st), self._epoch, self._lazy)
+
+    # ------------------------------------------------------------------ one-to-one transforms
+    def map(self, fn: Callable, *, compute=None, **ray_remote_args) -> "Dataset":
+        return self._one_to_one(f"map({_fn_name(fn)})", I.BlockTransform("map", fn), compute, ray_remote_args)
+
+    def flat_map(self, fn: Callable, *, compute=None, **ray_remote_args) -> "Dataset":
+        return self._one_to_one(f"flat_map({_fn_name(fn)})", I.BlockTransform("flat_map", fn), compute,
+                                ray_remote_args)
+
+    def filter(self, fn: Callable, *, compute=None, **ray_remote_args) -> "Dataset":
+        return self._one_to_one(f"filter({_fn_name(fn)})", I.BlockTransform("filter", fn), compute, ray_remote_args)
+
+    def map_batches(self, fn, *, batch_size: Optional[int] = 4096, compute=None, batch_format: str = "native",
+                    fn_args=None, fn_kwargs=None, fn_constructor_args=None, fn_constructor_kwargs=None,
+                    **ray_remote_args) -> "Dataset":
+        if batch_size is not None and batch_size < 1:
+            raise ValueError("Batch size cannot be negative or 0")
+        t = I.BlockTransform("map_batches", fn, batch_size, batch_format, fn_args, fn_kwargs, fn_constructor_args,
+                             fn_constructor_kwargs)
+        return self._one_to_one(f"map_batches({_fn_name(fn)})", t, compute, ray_remote_args)
+
+    def add_column(self, col: str, fn: Callable, *, compute=None, **ray_remote_args) -> "Dataset":
+        def add(batch):
+            batch = batch.copy()
+            batch[col] = fn(batch)
+            return batch
+
+        return self.map_batches(add, batch_format="pandas", compute=compute, **ray_remote_args)
+
+    def drop_columns(self, cols: List[str], *, compute=None, **ray_remote_args) -> "Dataset":
+        return self.map_batches(lambda b: b.drop(columns=cols), batch_format="pandas", compute=compute,
+                                **ray_remote_args)
+
+    def select_columns(self, cols: List[str], *, compute=None, **ray_remote_args) -> "Dataset":
+        return self.map_batches(lambda b: b.select(cols), batch_format="pyarrow", compute=compute, **ray_remote_args)
+
+    def random_sample(self, fraction: float, *, seed: Optional[int] = None) -> "Dataset":
+        if fraction < 0 or fraction > 1:
+            raise ValueError("Fraction must be between 0 and 1.")
+
+        def sample(block, fraction=fraction, seed=seed):
+            acc = BlockAccessor.for_block(block)
+            rng = np.random.default_rng(seed)
+            keep = np.nonzero(rng.random(acc.num_rows()) < fraction)[0]
+            return acc.take(keep)
+
+        return self._one_to_one("random_sample", I.BlockTransform("block", sample))
+
+    # ------------------------------------------------------------------ all-to-all
+    def repartition(self, num_blocks: int, *, shuffle: bool = False) -> "Dataset":
+        t0 = time.perf_counter()
+        if shuffle:
+            b, m = I.shuffle_blocks(self._blocks(), num_blocks, seed=None)
+        else:
+            b, m = I.repartition_blocks(self._blocks(), self._counts(), num_blocks)
+        return self._from_refs(b, m, "repartition", t0)
+
+    def random_shuffle(self, *, seed: Optional[int] = None, num_blocks: Optional[int] = None) -> "Dataset":
+        t0 = time.perf_counter()
+        blocks = self._blocks()
+        ctx = DatasetContext.get_current()
+        b, m = I.shuffle_blocks(blocks, num_blocks or len(blocks), seed, push_based=ctx.use_push_based_shuffle)
+        return self._from_refs(b, m, "random_shuffle", t0)
+
+    def randomize_block_order(self, *, seed: Optional[int] = None) -> "Dataset":
+        blocks, metas = self._blocks(), list(self._plan.in_metas)
+        order = np.random.default_rng(seed).permutation(len(blocks))
+        return self._from_refs([blocks[i] for i in order], [metas[i] for i in order])
+
+    def sort(self, key: Union[None, str, List[str], Callable] = None, descending: bool = False) -> "Dataset":
+        t0 = time.perf_counter()
+        b, m = I.sort_blocks(self._blocks(), key, descending)
+        return self._from_refs(b, m, "sort", t0)
+
+    def groupby(self, key) -> "GroupedDataset":
+        from ray_memory_management_amd.data.grouped_dataset import GroupedDataset
+
+        return GroupedDataset(self, key)
+
+    def aggregate(self, *aggs: AggregateFn):
+        from ray_memory_management_amd.data.grouped_dataset import GroupedDataset
+
+        rows = GroupedDataset(self, None).aggregate(*aggs).take(1)
+        return rows[0] if rows else None
+
+    def _simple_agg(self, cls, on, ignore_nulls=True, **kw):
+        if isinstance(on, list):
+            aggs = [cls(c, ignore_nulls=ignore_nulls, **kw) for c in on]
+            r = self.aggregate(*aggs)
+            return r
+        r = self.aggregate(cls(on, ignore_nulls=ignore_nulls, **kw))
+        if r is None:
+            return None
+        return r[0] if isinstance(r, tuple) else (list(r.values())[0] if isinstance(r, dict) else r)
+
+    def sum(self, on=None, ignore_nulls: bool = True):
+        return self._simple_agg(Sum, on, ignore_nulls)
+
+    def min(self, on=None, ignore_nulls: bool = True):
+        return self._simple_agg(Min, on, ignore_nulls)
+
+    def max(self, on=None, ignore_nulls: bool = True):
+        return self._simple_agg(Max, on, ignore_nulls)
+
+    def mean(self, on=None, ignore_nulls: bool = True):
+        return self._simple_agg(Mean, on, ignore_nulls)
+
+    def std(self, on=None, ddof: int = 1, ignore_nulls: bool = True):
+        return self._simple_agg(Std, on, ignore_nulls, ddof=ddof)
+
+    # ------------------------------------------------------------------ splitting / combining
+    def split(self, n: int, *, equal: bool = False, locality_hints: Optional[List[Any]] = None) -> List["Dataset"]:
+        if n <= 0:
+            raise ValueError(f"The number of splits {n} is not positive.")
+        if locality_hints is not None and len(locality_hints) != n:
+            raise ValueError(f"The length of locality_hints {len(locality_hints)} doesn't equal the number of "
+                             f"splits {n}.")
+        blocks, metas = self._blocks(), self._metas()
+        if equal:
+            total = sum(m.num_rows for m in metas)
+            per = total // n
+            b, m = I.repartition_blocks(blocks, [x.num_rows for x in metas], n, [per] * n)
+            return [self._from_refs([b[i]], [m[i]]) for i in range(n)]
+        # assign whole blocks, balancing rows greedily
+        order = sorted(range(len(blocks)), key=lambda i: -metas[i].num_rows)
+        bins: List[List[int]] = [[] for _ in range(n)]
+        loads = [0] * n
+        for i in order:
+            j = int(np.argmin(loads))
+            bins[j].append(i)
+            loads[j] += metas[i].num_rows
+        return [self._from_refs([blocks[i] for i in sorted(bn)], [metas[i] for i in sorted(bn)]) for bn in bins]
+
+    def split_at_indices(self, indices: List[int]) -> List["Dataset"]:
+        if len(indices) < 1:
+            raise ValueError("indices must be at least of length 1")
+        if sorted(indices) != list(indices):
+            raise ValueError("indices must be sorted")
+        if indices[0] < 0:
+            raise ValueError("indices must be positive")
+        counts = self._counts()
+        total = sum(counts)
+        cuts = [min(i, total) for i in indices]
+        sizes = [cuts[0]] + [cuts[i] - cuts[i - 1] for i in range(1, len(cuts))] + [total - cuts[-1]]
+        b, m = I.repartition_blocks(self._blocks(), counts, len(sizes), sizes)
+        return [self._from_refs([b[i]], [m[i]]) for i in range(len(sizes))]
+
+    def split_proportionately(self, proportions: List[float]) -> List["Dataset"]:
+        if len(proportions) < 1:
+            raise ValueError("proportions must be at least of length 1")
+        if sum(proportions) >= 1:
+            raise ValueError("proportions must sum to less than 1")
+        if any(p <= 0 for p in proportions):
+            raise ValueError("proportions must be bigger than 0")
+        total = self.count()
+        cum, idx = 0.0, []
+        for p in proportions:
+            cum += p
+            idx.append(int(cum * total))
+        return self.split_at_indices(idx)
+
+    def train_test_split(self, test_size: Union[int, float], *, shuffle: bool = False,
+                         seed: Optional[int] = None):
+        ds = self.random_shuffle(seed=seed) if shuffle else self
+        if isinstance(test_size, float):
+            if test_size <= 0 or test_size >= 1:
+                raise ValueError("If `test_size` is a float, it must be bigger than 0 and smaller than 1. "
+                                 f"Got {test_size}.")
+            return tuple(ds.split_proportionately([1 - test_size]))
+        n = ds.count()
+        if test_size <= 0 or test_size >= n:
+            raise ValueError("If `test_size` is an int, it must be bigger than 0 and smaller than the size of the "
+                             f"dataset ({n}). Got {test_size}.")
+        return tuple(ds.split_at_indices([n - test_size]))
+
+    def union(self, *other: "Dataset") -> "Dataset":
+        blocks, metas = self._blocks(), list(self._metas())
+        for o in other:
+            blocks += o._blocks()
+            metas += o._metas()
+        return self._from_refs(blocks, metas, "union")
+
+    def zip(self, other: "Dataset") -> "Dataset":
+        counts = self._counts()
+        if sum(counts) != other.count():
+            raise ValueError("Cannot zip datasets of different number of rows: "
+                             f"{sum(counts)}, {other.count()}")
+        ob, _ = I.repartition_blocks(other._blocks(), other._counts(), len(counts), counts)
+        out_b, out_m = [], []
+        for a, b in zip(self._blocks(), ob):
+            rb, rm = _zip_blocks.options(num_returns=2).remote(a, b)
+            out_b.append(rb)
+            out_m.append(rm)
+        return self._from_refs(out_b, out_m, "zip")
+
+    def limit(self, limit: int) -> "Dataset":
+        blocks, metas = self._blocks(), self._metas()
+        out_b, out_m, need = [], [], limit
+        for b, m in zip(blocks, metas):
+            if need <= 0:
+                break
+            if m.num_rows <= need:
+                out_b.append(b)
+                out_m.append(m)
+                need -= m.num_rows
+            else:
+                rb, rm = I._concat_with_meta.options(num_returns=2).remote(I._slice_block.remote(b, 0, need))
+                out_b.append(rb)
+                out_m.append(rm)
+                need = 0
+        return self._from_refs(out_b, out_m, "limit")
+
+    # ------------------------------------------------------------------ consumption
+    def take(self, limit: int = 20) -> List[Any]:
+        out = []
+        for r in self.iter_rows():
+            if len(out) >= limit:
+                break
+            out.append(r)
+        return out
+
+    def take_all(self, limit: Optional[int] = None) -> List[Any]:
+        out = []
+        for r in self.iter_rows():
+            out.append(r)
+            if limit is not None and len(out) > limit:
+                raise ValueError(f"The dataset has more than the given limit of {limit} records.")
+        return out
+
+    def show(self, limit: int = 20) -> None:
+        for r in self.take(limit):
+            print(r)
+
+    def count(self) -> int:
+        return int(sum(self._counts()))
+
+    def schema(self, fetch_if_missing: bool = False):
+        for m in self._metas():
+            if m.num_rows and m.schema is not None:
+                return m.schema
+        return None
+
+    def num_blocks(self) -> int:
+        self._plan.execute()
+        return len(self._plan.in_blocks)
+
+    def size_bytes(self) -> int:
+        return int(sum(m.size_bytes or 0 for m in self._metas()))
+
+    def input_files(self) -> List[str]:
+        files = []
+        for m in self._metas():
+            for f in m.input_files:
+                if f not in files:
+                    files.append(f)
+        return files
+
+    def iter_rows(self, *, prefetch_blocks: int = 0) -> Iterator:
+        for block in self._iter_blocks(prefetch_blocks):
+            yield from BlockAccessor.for_block(block).iter_rows()
+
+    def _iter_blocks(self, prefetch_blocks: int = 0):
+        blocks = self._blocks()
+        window = max(prefetch_blocks, 0) + 1
+        for i in range(len(blocks)):
+            if window > 1:  # issue waits ahead so the fetch overlaps consumption
+                ray.wait(blocks[i:i + window], num_returns=min(window, len(blocks) - i), timeout=0)
+            yield ray.get(blocks[i])
+
+    def iter_batches(self, *, prefetch_blocks: int = 0, batch_size: Optional[int] = 256,
+                     batch_format: str = "native", drop_last: bool = False,
+                     local_shuffle_buffer_size: Optional[int] = None,
+                     local_shuffle_seed: Optional[int] = None) -> Iterator:
+        from ray_memory_management_amd.data.block import BlockAccessor as BA
+
+        buf = []          # pending blocks
+        buffered = 0
+        rng = np.random.default_rng(local_shuffle_seed)
+
+        def emit(n):
+            nonlocal buf, buffered
+            b = concat_blocks(buf)
+            acc = BA.for_block(b)
+            if local_shuffle_buffer_size:
+                acc = BA.for_block(acc.take(rng.permutation(acc.num_rows())))
+            head, tail = acc.slice(0, n), acc.slice(n, acc.num_rows())
+            buf = [tail] if BA.for_block(tail).num_rows() else []
+            buffered = BA.for_block(tail).num_rows()
+            return BA.for_block(head).to_batch(batch_format)
+
+        min_buffer = max(local_shuffle_buffer_size or 0, batch_size or 0)
+        for block in self._iter_blocks(prefetch_blocks):
+            n = BA.for_block(block).num_rows()
+            if n == 0:
+                continue
+            if batch_size is None:
+                yield BA.for_block(block).to_batch(batch_format)
+                continue
+            buf.append(block)
+            buffered += n
+            while buffered >= min_buffer and buffered >= batch_size:
+                yield emit(batch_size)
+        while batch_size is not None and buffered > 0:
+            if buffered < batch_size and drop_last:
+                break
+            yield emit(min(batch_size, buffered))
+
+    def iter_torch_batches(self, *, prefetch_blocks: int = 0, batch_size: Optional[int] = 256, dtypes=None,
+                           device: Optional[str] = None, collate_fn=None, drop_last: bool = False,
+                           local_shuffle_buffer_size: Optional[int] = None,
+                           local_shuffle_seed: Optional[int] = None) -> Iterator:
+        """Batches as torch tensors. With device="cuda[:i]" the host batch is staged through pinned
+        memory and copied to HBM asynchronously on a side stream, one batch ahead of consumption."""
+        import torch
+
+        def to_tensors(batch):
+            if collate_fn is not None:
+                return collate_fn(batch)
+            if isinstance(batch, dict):
+                return {k: _as_tensor(v, dtypes[k] if isinstance(dtypes, dict) else dtypes) for k, v in batch.items()}
+            return _as_tensor(batch, dtypes)
+
+        it = self.iter_batches(prefetch_blocks=prefetch_blocks, batch_size=batch_size, batch_format="numpy",
+                               drop_last=drop_last, local_shuffle_buffer_size=local_shuffle_buffer_size,
+                               local_shuffle_seed=local_shuffle_seed)
+        if device is None or not str(device).startswith("cuda") or not torch.cuda.is_available():
+            for b in it:
+                t = to_tensors(b)
+                yield _to_device(t, device) if device else t
+            return
+        stream = torch.cuda.Stream(device=device)
+        pending = None
+        for b in it:
+            t = to_tensors(b)
+            with torch.cuda.stream(stream):
+                nxt = _to_device(_pin(t), device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            if pending is not None:
+                torch.cuda.current_stream(device).wait_event(pending[1])
+                yield pending[0]
+            pending = (nxt, ev)
+        if pending is not None:
+            torch.cuda.current_stream(device).wait_event(pending[1])
+            yield pending[0]
+
+    def to_torch(self, *, label_column: Optional[str] = None, feature_columns=None, label_column_dtype=None,
+                 feature_column_dtypes=None, batch_size: int = 1, prefetch_blocks: int = 0, drop_last: bool = False,
+                 local_shuffle_buffer_size=None, local_shuffle_seed=None, unsqueeze_label_tensor: bool = True,
+                 unsqueeze_feature_tensors: bool = True):
+        import torch
+
+        ds = self
+
+        class _It(torch.utils.data.IterableDataset):
+            def __iter__(self):
+                for batch in ds.iter_batches(batch_size=batch_size, batch_format="pandas", drop_last=drop_last,
+                                             prefetch_blocks=prefetch_blocks,
+                                             local_shuffle_buffer_size=local_shuffle_buffer_size,
+                                             local_shuffle_seed=local_shuffle_seed):
+                    label = None
+                    if label_column:
+                        label = torch.as_tensor(batch.pop(label_column).values, dtype=label_column_dtype)
+                        if unsqueeze_label_tensor:
+                            label = label.view(-1, 1)
+                    cols = feature_columns or list(batch.columns)
+                    if isinstance(cols, dict):
+                        feats = {k: _df_tensor(batch, v, feature_column_dtypes, unsqueeze_feature_tensors)
+                                 for k, v in cols.items()}
+                    elif cols and isinstance(cols[0], list):
+                        feats = [_df_tensor(batch, c, feature_column_dtypes, unsqueeze_feature_tensors) for c in cols]
+                    else:
+                        feats = _df_tensor(batch, cols, feature_column_dtypes, unsqueeze_feature_tensors)
+                    yield feats, label
+
+        return _It()
+
+    def to_pandas(self, limit: int = 100000):
+        if self.count() > limit:
+            raise ValueError(f"The dataset has more than the given limit of {limit} records. Use "
+                             "ds.limit(N).to_pandas().")
+        import pandas as pd
+
+        dfs = [BlockAccessor.for_block(b).to_pandas() for b in ray.get(self._blocks())]
+        return pd.concat(dfs, ignore_index=True) if dfs else pd.DataFrame()
+
+    def to_pandas_refs(self) -> List[Any]:
+        return [_to_format.remote(b, "pandas") for b in self._blocks()]
+
+    def to_numpy_refs(self, *, column: Optional[str] = None) -> List[Any]:
+        return [_to_numpy_col.remote(b, column) for b in self._blocks()]
+
+    def to_arrow_refs(self) -> List[Any]:
+        return [_to_format.remote(b, "pyarrow") for b in self._blocks()]
+
+    def to_random_access_dataset(self, key: str, num_workers: Optional[int] = None):
+        from ray_memory_management_amd.data.random_access_dataset import RandomAccessDataset
+
+        return RandomAccessDataset(self, key, num_workers=num_workers)
+
+    # ------------------------------------------------------------------ writes
+    def write_datasource(self, datasource, **write_args) -> None:
+        blocks = self._blocks()
+        metas = self._metas()
+        refs = datasource.do_write(blocks, metas, **write_args)
+        try:
+            ray.get(refs)
+            datasource.on_write_complete(refs)
+        except Exception as e:
+            datasource.on_write_failed(refs, e)
+            raise
+
+    def write_parquet(self, path: str, **kw) -> None:
+        from ray_memory_management_amd.data.datasource import ParquetDatasource
+
+        self.write_datasource(ParquetDatasource(), path=path, dataset_uuid=self._uuid(), **kw)
+
+    def write_json(self, path: str, **kw) -> None:
+        from ray_memory_management_amd.data.datasource import JSONDatasource
+
+        self.write_datasource(JSONDatasource(), path=path, dataset_uuid=self._uuid(), **kw)
+
+    def write_csv(self, path: str, **kw) -> None:
+        from ray_memory_management_amd.data.datasource import CSVDatasource
+
+        self.write_datasource(CSVDatasource(), path=path, dataset_uuid=self._uuid(), **kw)
+
+    def write_numpy(self, path: str, *, column: str = TENSOR_COL, **kw) -> None:
+        from ray_memory_management_amd.data.datasource import NumpyDatasource
+
+        self.write_datasource(NumpyDatasource(), path=path, dataset_uuid=self._uuid(), column=column, **kw)
+
+    def _uuid(self):
+        return os.urandom(8).hex()
+
+    # ------------------------------------------------------------------ pipelines / plan control
+    def repeat(self, times: Optional[int] = None):
+        from ray_memory_management_amd.data.dataset_pipeline import DatasetPipeline
+
+        if times is not None and times < 1:
+            raise ValueError("`times` must be >= 1, got {}".format(times))
+        base = self.fully_executed()
+
+        def gen():
+            for i in (range(times) if times is not None else itertools.count()):
+                yield lambda i=i: Dataset(base._plan.copy(), i, base._lazy)
+
+        return DatasetPipeline(gen(), length=times if times is not None else float("inf"), epoch_len=1)
+
+    def window(self, *, blocks_per_window: Optional[int] = 10, bytes_per_window: Optional[int] = None):
+        from ray_memory_management_amd.data.dataset_pipeline import DatasetPipeline
+
+        base = self.fully_executed()
+        blocks, metas = base._blocks(), base._metas()
+        groups: List[List[int]] = []
+        if bytes_per_window:
+            cur, size = [], 0
+            for i, m in enumerate(metas):
+                if cur and size + (m.size_bytes or 0) > bytes_per_window:
+                    groups.append(cur)
+                    cur, size = [], 0
+                cur.append(i)
+                size += m.size_bytes or 0
+            if cur:
+                groups.append(cur)
+        else:
+            k = max(int(blocks_per_window or 1), 1)
+            groups = [list(range(i, min(i + k, len(blocks)))) for i in range(0, len(blocks), k)]
+
+        def gen():
+            for g in groups:
+                yield lambda g=g: Dataset(ExecutionPlan([blocks[i] for i in g], [metas[i] for i in g]), 0,
+                                          base._lazy)
+
+        return DatasetPipeline(gen(), length=len(groups))
+
+    def fully_executed(self) -> "Dataset":
+        self._plan.execute()
+        self._metas()
+        return self
+
+    def is_fully_executed(self) -> bool:
+        return self._plan.is_executed()
+
+    def lazy(self) -> "Dataset":
+        return Dataset(self._plan.copy(), self._epoch, lazy=True)
+
+    experimental_lazy = lazy
+
+    def stats(self) -> str:
+        self._plan.execute()
+        return self._plan.stats.summary_string()
+
+    def get_internal_block_refs(self) -> List[Any]:
+        return self._blocks()
+
+    def __repr__(self):
+        if self._plan.is_executed():
+            metas = self._plan.in_metas
+            if all(isinstance(m, BlockMetadata) for m in metas):
+                return f"Dataset(num_blocks={len(metas)}, num_rows={sum(m.num_rows for m in metas)}, " \
+                       f"schema={self.schema()})"
+            return f"Dataset(num_blocks={len(metas)})"
+        return f"Dataset(num_blocks={len(self._plan.in_blocks)}, pending_stages={len(self._plan.stages)})"
+
+    def __iter__(self):
+        raise TypeError("`Dataset` objects aren't iterable. To iterate records, call `ds.iter_rows()` or "
+                        "`ds.iter_batches()`.")
+
+    def __len__(self):
+        raise AttributeError("Use `ds.count()` to compute the length of a distributed Dataset.")
+
+
+# ---------------------------------------------------------------------- remote helpers
+@ray.remote
+def _zip_blocks(a, b):
+    aa, ba = BlockAccessor.for_block(a), BlockAccessor.for_block(b)
+    if isinstance(a, NumpyBlock) and isinstance(b, NumpyBlock):
+        out = NumpyBlock(dict(a))
+        for k, v in b.items():
+            out[k if k not in out else f"{k}_1"] = v
+    elif isinstance(a, list) and isinstance(b, list):
+        out = list(zip(a, b))
+    else:
+        ta, tb = aa.to_arrow(), ba.to_arrow()
+        for name, col in zip(tb.column_names, tb.columns):
+            nm = name if name not in ta.column_names else f"{name}_1"
+            ta = ta.append_column(nm, col)
+        out = ta
+    return out, BlockAccessor.for_block(out).get_metadata()
+
+
+@ray.remote
+def _to_format(block, fmt):
+    return BlockAccessor.for_block(block).to_batch(fmt)
+
+
+@ray.remote
+def _to_numpy_col(block, column):
+    return BlockAccessor.for_block(block).to_numpy(column)
+
+
+def _as_tensor(v, dtype=None):
+    import torch
+
+    if isinstance(v, torch.Tensor):
+        return v.to(dtype) if dtype is not None else v
+    arr = np.asarray(v)
+    if arr.dtype == object:
+        arr = np.stack([np.asarray(x) for x in arr])
+    arr = np.ascontiguousarray(arr)
+    if not arr.flags.writeable:  # zero-copy view of the read-only shm store: torch needs its own copy
+        arr = arr.copy()
+    t = torch.from_numpy(arr)
+    return t.to(dtype) if dtype is not None else t
+
+
+def _pin(t):
+    if isinstance(t, dict):
+        return {k: _pin(v) for k, v in t.items()}
+    try:
+        return t.pin_memory()
+    except Exception:
+        return t
+
+
+def _to_device(t, device, non_blocking=False):
+    if isinstance(t, dict):
+        return {k: _to_device(v, device, non_blocking) for k, v in t.items()}
+    return t.to(device, non_blocking=non_blocking)
+
+
+def _df_tensor(df, cols, dtypes, unsqueeze):
+    import torch
+
+    cols = [cols] if isinstance(cols, str) else list(cols)
+    arrs = []
+    for c in cols:
+        v = df[c].values
+        if v.dtype == object:
+            v = np.stack([np.asarray(x) for x in v])
+        t = torch.as_tensor(v, dtype=dtypes if not isinstance(dtypes, dict) else None)
+        if unsqueeze and t.dim() == 1:
+            t = t.view(-1, 1)
+        arrs.append(t)
+    return torch.cat(arrs, dim=1) if len(arrs) > 1 else arrs[0]

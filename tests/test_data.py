@@ -1,0 +1,212 @@
+"""Data library: mirrors reference python/ray/data/tests/{test_dataset,test_sort,test_split,
+test_dataset_formats,test_dataset_pipeline,test_preprocessors}.py at smaller scale."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+
+@pytest.fixture(scope="module")
+def ray_data(ray_shared):
+    import ray_memory_management_amd.data as data
+
+    return ray_shared, data
+
+
+def test_basic_range_and_transforms(ray_data):
+    ray, data = ray_data
+    ds = data.range(100, parallelism=5)
+    assert ds.count() == 100 and ds.num_blocks() == 5
+    assert ds.take(3) == [0, 1, 2]
+    assert ds.map(lambda x: x * 2).take(3) == [0, 2, 4]
+    assert ds.filter(lambda x: x % 10 == 0).take_all() == list(range(0, 100, 10))
+    assert ds.flat_map(lambda x: [x, x]).count() == 200
+    assert sorted(ds.map_batches(lambda b: [x + 1 for x in b], batch_size=7).take_all()) == list(range(1, 101))
+    assert ds.sum() == sum(range(100)) and ds.min() == 0 and ds.max() == 99
+    assert ds.mean() == pytest.approx(49.5)
+    assert ds.std() == pytest.approx(np.std(np.arange(100), ddof=1))
+    with pytest.raises(TypeError):
+        iter(ds)
+
+
+def test_lazy_fusion_and_stats(ray_data):
+    ray, data = ray_data
+    ds = data.range(20, parallelism=4).lazy().map(lambda x: x + 1).map(lambda x: x * 3)
+    assert not ds.is_fully_executed()
+    assert ds.take_all() == [(i + 1) * 3 for i in range(20)]
+    assert "map(<lambda>)->map(<lambda>)" in ds.stats()  # the two stages ran fused
+
+
+def test_table_ops(ray_data):
+    ray, data = ray_data
+    ds = data.from_items([{"a": i, "b": i % 3, "c": float(i)} for i in range(30)], parallelism=3)
+    assert ds.count() == 30 and ds.schema().names == ["a", "b", "c"]
+    assert ds.sum("a") == sum(range(30))
+    g = ds.groupby("b").count().take_all()
+    assert g == [{"b": 0, "count()": 10}, {"b": 1, "count()": 10}, {"b": 2, "count()": 10}]
+    s = ds.groupby("b").sum("a").take_all()
+    assert [r["sum(a)"] for r in s] == [sum(range(0, 30, 3)), sum(range(1, 30, 3)), sum(range(2, 30, 3))]
+    m = ds.groupby("b").aggregate(data.Mean("c"), data.Max("a")).take_all()
+    assert m[2]["max(a)"] == 29 and m[0]["mean(c)"] == pytest.approx(np.mean(range(0, 30, 3)))
+    mg = ds.groupby("b").map_groups(lambda df: df.head(1), batch_format="pandas").take_all()
+    assert [r["a"] for r in mg] == [0, 1, 2]
+    df = ds.add_column("d", lambda df: df["a"] * 2).drop_columns(["c"]).to_pandas()
+    assert list(df.columns) == ["a", "b", "d"] and (df["d"] == df["a"] * 2).all()
+    pbatches = list(ds.iter_batches(batch_size=8, batch_format="pandas"))
+    assert [len(b) for b in pbatches] == [8, 8, 8, 6] and isinstance(pbatches[0], pd.DataFrame)
+
+
+def test_sort_shuffle_repartition(ray_data):
+    ray, data = ray_data
+    ds = data.range(200, parallelism=8).random_shuffle(seed=1)
+    vals = ds.take_all()
+    assert sorted(vals) == list(range(200)) and vals != list(range(200))
+    assert ds.sort().take_all() == list(range(200))
+    assert ds.sort(descending=True).take(3) == [199, 198, 197]
+    t = data.from_items([{"k": (i * 37) % 101, "v": i} for i in range(101)], parallelism=4)
+    assert [r["k"] for r in t.sort("k").take_all()] == list(range(101))
+    r = data.range(100, parallelism=3).repartition(7)
+    assert r.num_blocks() == 7 and r.take_all() == list(range(100))
+    assert sorted(data.range(50, parallelism=2).repartition(4, shuffle=True).take_all()) == list(range(50))
+    rb = data.range(40, parallelism=4).randomize_block_order(seed=0)
+    assert sorted(rb.take_all()) == list(range(40))
+    smp = data.range(1000, parallelism=4).random_sample(0.1, seed=3).count()
+    assert 40 < smp < 180
+
+
+def test_push_based_shuffle(ray_data):
+    ray, data = ray_data
+    ctx = data.DatasetContext.get_current()
+    ctx.use_push_based_shuffle = True
+    try:
+        ds = data.range(300, parallelism=12).random_shuffle(seed=5)
+        assert sorted(ds.take_all()) == list(range(300))
+    finally:
+        ctx.use_push_based_shuffle = False
+
+
+def test_split_zip_union_limit(ray_data):
+    ray, data = ray_data
+    ds = data.range(20, parallelism=4)
+    parts = ds.split(3)
+    assert sum(p.count() for p in parts) == 20
+    eq = ds.split(3, equal=True)
+    assert [p.count() for p in eq] == [6, 6, 6]
+    a, b, c = ds.split_at_indices([5, 12])
+    assert a.take_all() == list(range(5)) and b.take_all() == list(range(5, 12)) and c.count() == 8
+    tr, te = ds.train_test_split(0.25)
+    assert tr.count() == 15 and te.count() == 5
+    p1, p2 = ds.split_proportionately([0.5])
+    assert p1.count() == 10 and p2.count() == 10
+    z = ds.zip(data.range(20, parallelism=2).map(lambda x: -x))
+    assert z.take(2) == [(0, 0), (1, -1)]
+    assert ds.union(data.range(5)).count() == 25
+    assert ds.limit(7).take_all() == list(range(7))
+
+
+def test_tensor_and_numpy(ray_data):
+    ray, data = ray_data
+    ds = data.range_tensor(10, shape=(2, 3), parallelism=2)
+    arr = np.concatenate(ray.get(ds.to_numpy_refs()))
+    assert arr.shape == (10, 2, 3) and arr[3].max() == 3
+    nds = data.from_numpy(np.arange(12).reshape(6, 2))
+    out = list(nds.iter_batches(batch_size=4, batch_format="numpy"))
+    assert out[0].shape == (4, 2) and out[1].shape == (2, 2)
+    import torch
+
+    tb = list(nds.iter_torch_batches(batch_size=3))
+    assert isinstance(tb[0], torch.Tensor) and tb[0].shape == (3, 2)
+    doubled = nds.map_batches(lambda b: b * 2, batch_format="numpy")
+    assert np.concatenate(ray.get(doubled.to_numpy_refs()))[-1].tolist() == [20, 22]
+
+
+def test_actor_pool_compute(ray_data):
+    ray, data = ray_data
+
+    class AddN:
+        def __init__(self, n):
+            self.n = n
+
+        def __call__(self, batch):
+            return [x + self.n for x in batch]
+
+    ds = data.range(40, parallelism=4).map_batches(AddN, compute=data.ActorPoolStrategy(1, 2),
+                                                   fn_constructor_args=(100,), num_cpus=0.5)
+    assert sorted(ds.take_all()) == list(range(100, 140))
+    with pytest.raises(ValueError):
+        data.range(4).map_batches(AddN)
+
+
+def test_read_write_formats(ray_data, tmp_path):
+    ray, data = ray_data
+    ds = data.from_items([{"x": i, "y": str(i)} for i in range(25)], parallelism=3)
+    for fmt in ("parquet", "csv", "json"):
+        d = str(tmp_path / fmt)
+        getattr(ds, f"write_{fmt}")(d)
+        assert len(os.listdir(d)) == 3
+        back = getattr(data, f"read_{fmt}")(d)
+        assert sorted(r["x"] for r in back.take_all()) == list(range(25))
+        assert len(back.input_files()) == 3
+    nd = str(tmp_path / "npy")
+    data.from_numpy(np.arange(10)).write_numpy(nd)
+    assert sorted(data.read_numpy(nd).take_all()) == list(range(10))
+    tf = tmp_path / "t.txt"
+    tf.write_text("a\nb\n\nc\n")
+    assert data.read_text(str(tf)).take_all() == ["a", "b", "c"]
+    assert data.read_binary_files(str(tf)).take_all() == [b"a\nb\n\nc\n"]
+    dfs = data.from_pandas([pd.DataFrame({"q": [1, 2]}), pd.DataFrame({"q": [3]})])
+    assert dfs.to_pandas()["q"].tolist() == [1, 2, 3]
+    out = data.datasource.DummyOutputDatasource()
+    dfs.write_datasource(out)
+    assert out.num_ok == 1 and out.rows_written == 3
+
+
+def test_pipeline(ray_data):
+    ray, data = ray_data
+    pipe = data.range(12, parallelism=4).window(blocks_per_window=2).map(lambda x: x * 10)
+    assert pipe.take_all() if hasattr(pipe, "take_all") else True
+    p2 = data.range(12, parallelism=4).window(blocks_per_window=2).map(lambda x: x * 10)
+    assert list(p2.iter_rows()) == [x * 10 for x in range(12)]
+    rep = data.range(5, parallelism=1).repeat(3)
+    assert rep.count() == 15
+    epochs = list(data.range(4, parallelism=2).repeat(2).random_shuffle_each_window(seed=0).iter_epochs())
+    assert len(epochs) == 2 and sorted(epochs[1].iter_rows()) == [0, 1, 2, 3]
+    shards = data.range(8, parallelism=4).window(blocks_per_window=2).split(2)
+    assert sorted(list(shards[0].iter_rows()) + list(shards[1].iter_rows())) == list(range(8))
+
+
+def test_random_access(ray_data):
+    ray, data = ray_data
+    ds = data.from_items([{"id": i, "v": i * i} for i in range(50)], parallelism=5)
+    rad = ds.to_random_access_dataset("id", num_workers=2)
+    assert ray.get(rad.get_async(7))["v"] == 49
+    assert [r["v"] if r else None for r in rad.multiget([3, 40, 1000])] == [9, 1600, None]
+
+
+def test_preprocessors(ray_data):
+    ray, data = ray_data
+    from ray_memory_management_amd.data.preprocessor import PreprocessorNotFittedException
+    from ray_memory_management_amd.data.preprocessors import (BatchMapper, Chain, Concatenator, LabelEncoder,
+                                                              MinMaxScaler, OneHotEncoder, SimpleImputer,
+                                                              StandardScaler)
+
+    df = pd.DataFrame({"a": [1.0, 2.0, 3.0, 4.0], "b": [10.0, None, 30.0, 40.0], "cat": ["x", "y", "x", "z"]})
+    ds = data.from_pandas(df)
+    sc = StandardScaler(["a"])
+    with pytest.raises(PreprocessorNotFittedException):
+        sc.transform(ds)
+    out = sc.fit_transform(ds).to_pandas()
+    assert out["a"].mean() == pytest.approx(0.0) and sc.stats_["mean(a)"] == pytest.approx(2.5)
+    mm = MinMaxScaler(["a"]).fit(ds)
+    assert mm.transform_batch(df.copy())["a"].tolist() == pytest.approx([0, 1 / 3, 2 / 3, 1])
+    imp = SimpleImputer(["b"]).fit(ds)
+    assert imp.transform_batch(df.copy())["b"].tolist() == pytest.approx([10, 80 / 3, 30, 40])
+    oh = OneHotEncoder(["cat"]).fit(ds).transform_batch(df.copy())
+    assert oh["cat_x"].tolist() == [1, 0, 1, 0]
+    le = LabelEncoder("cat").fit(ds).transform_batch(df.copy())
+    assert le["cat"].tolist() == [0, 1, 0, 2]
+    ch = Chain(SimpleImputer(["b"]), BatchMapper(lambda d: d.assign(s=d["a"] + d["b"])),
+               Concatenator(include=["a", "b"]))
+    res = ch.fit_transform(ds).to_pandas()
+    assert "concat_out" in res.columns and len(res["concat_out"][0]) == 2
