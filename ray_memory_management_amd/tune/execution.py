@@ -1,0 +1,417 @@
+"""Trial execution. Parity: reference python/ray/tune/execution/{trial_runner.py (event loop:
+start trials while resources allow, process results, apply stoppers / scheduler decisions,
+checkpoint, retry failures), ray_trial_executor.py (one actor per trial, pause = save + stop,
+resume = new actor + restore)} and tune/experiment/trial.py (Trial state).
+
+Every trial is an actor hosting a Trainable; the driver keeps ONE `train()` call in flight per
+running trial and harvests them with `wait`, so a slow trial never blocks the others.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+import traceback
+import uuid
+from typing import Any, Callable, Dict, List, Optional
+
+import ray_memory_management_amd as ray
+from ray_memory_management_amd.air.checkpoint import Checkpoint
+from ray_memory_management_amd.tune.schedulers import FIFOScheduler, TrialScheduler
+from ray_memory_management_amd.tune.stopper import DictStopper, FunctionStopper, NoopStopper, Stopper
+from ray_memory_management_amd.tune.trainable import RESULT_DUPLICATE, PlacementGroupFactory, resources_to_pgf
+
+
+class Trial:
+    PENDING, RUNNING, PAUSED, TERMINATED, ERROR = "PENDING", "RUNNING", "PAUSED", "TERMINATED", "ERROR"
+
+    def __init__(self, trainable_name: str, config: Dict, trial_id: str, local_dir: str,
+                 resources: PlacementGroupFactory, max_failures: int = 0, experiment_tag: str = ""):
+        self.trainable_name = trainable_name
+        self.config = config
+        self.trial_id = trial_id
+        self.status = Trial.PENDING
+        self.resources = resources
+        self.placement_group_factory = resources
+        self.max_failures = max_failures
+        self.num_failures = 0
+        self.last_result: Dict[str, Any] = {}
+        self.metric_analysis: Dict[str, Dict[str, float]] = {}
+        self.results: List[Dict[str, Any]] = []
+        self.error_msg: Optional[str] = None
+        self.error: Optional[BaseException] = None
+        self.checkpoint: Optional[Checkpoint] = None      # latest (in-memory) checkpoint
+        self.saved_checkpoints: List[tuple] = []         # (path, metrics) persisted
+        self.experiment_tag = experiment_tag
+        self.logdir = os.path.join(local_dir, f"{trainable_name}_{trial_id}")
+        self.runner = None
+        self._pending = None
+        self._unpaused = False
+        self.start_time = None
+
+    def __repr__(self):
+        return f"{self.trainable_name}_{self.trial_id}"
+
+    def __str__(self):
+        return self.__repr__()
+
+    @property
+    def local_path(self):
+        return self.logdir
+
+    def update_last_result(self, result: Dict):
+        self.last_result = result
+        self.results.append(result)
+        for k, v in result.items():
+            if isinstance(v, (int, float)) and not isinstance(v, bool):
+                a = self.metric_analysis.setdefault(k, {"max": v, "min": v, "avg": v, "last": v, "_n": 0, "_s": 0.0})
+                a["max"], a["min"], a["last"] = max(a["max"], v), min(a["min"], v), v
+                a["_n"] += 1
+                a["_s"] += v
+                a["avg"] = a["_s"] / a["_n"]
+
+    @property
+    def is_finished(self):
+        return self.status in (Trial.TERMINATED, Trial.ERROR)
+
+
+class _TrialActor:
+    def __init__(self, trainable_cls, config, trial_info, checkpoint=None):
+        os.makedirs(trial_info["logdir"], exist_ok=True)
+        self._info = trial_info
+        t = trainable_cls.__new__(trainable_cls)
+        t._trial_info = trial_info  # visible to setup() (trial_id / trial_name / session)
+        trainable_cls.__init__(t, config)
+        self.t = t
+        if checkpoint is not None:
+            self.t.restore(checkpoint)
+
+    def train(self):
+        return self.t.train()
+
+    def save(self):
+        return self.t.save()
+
+    def restore(self, ckpt):
+        self.t.restore(ckpt)
+        return True
+
+    def reset_config(self, cfg):
+        ok = self.t.reset_config(cfg)
+        if ok:
+            self.t.config = cfg
+        return ok
+
+    def stop(self):
+        self.t.stop()
+        return True
+
+
+class TrialRunner:
+    def __init__(self, trainable_cls, search_alg, scheduler: Optional[TrialScheduler], local_dir: str,
+                 stopper=None, metric: Optional[str] = None, mode: Optional[str] = None,
+                 max_concurrent_trials: Optional[int] = None, time_budget_s: Optional[float] = None,
+                 checkpoint_freq: int = 0, checkpoint_at_end: bool = False, max_failures: int = 0,
+                 fail_fast: bool = False, callbacks=None, resources=None, num_to_keep: Optional[int] = None,
+                 verbose: int = 0, reuse_actors: bool = False):
+        self.trainable_cls = trainable_cls
+        self.trainable_name = getattr(trainable_cls, "__name__", "trainable")
+        self.search_alg = search_alg
+        self.scheduler = scheduler or FIFOScheduler()
+        self.local_dir = local_dir
+        self.stopper = _make_stopper(stopper)
+        self.metric, self.mode = metric, mode
+        self.max_concurrent = max_concurrent_trials
+        self.time_budget_s = time_budget_s
+        self.checkpoint_freq, self.checkpoint_at_end = checkpoint_freq, checkpoint_at_end
+        self.max_failures, self.fail_fast = max_failures, fail_fast
+        self.callbacks = list(callbacks or [])
+        self.pgf = resources_to_pgf(resources if resources is not None else getattr(trainable_cls, "_resources",
+                                                                                   None))
+        self.num_to_keep = num_to_keep
+        self.verbose = verbose
+        self._trials: List[Trial] = []
+        self._search_done = False
+        self._start = time.time()
+        self._actor_cls = ray.remote(_TrialActor)
+        self._stop_all = False
+        os.makedirs(local_dir, exist_ok=True)
+
+    # ------------------------------------------------------------------ public
+    def get_trials(self) -> List[Trial]:
+        return self._trials
+
+    def add_trial(self, trial: Trial):
+        self._trials.append(trial)
+        self.scheduler.on_trial_add(self, trial)
+        self._cb("on_trial_add", trial=trial)
+
+    def has_resources_for_trial(self, trial: Trial) -> bool:
+        running = [t for t in self._trials if t.status == Trial.RUNNING]
+        if self.max_concurrent and len(running) >= self.max_concurrent:
+            return False
+        total = ray.cluster_resources()
+        used: Dict[str, float] = {}
+        for t in running:
+            for k, v in t.resources.required_resources().items():
+                used[k] = used.get(k, 0) + v
+        for k, v in trial.resources.required_resources().items():
+            if used.get(k, 0) + v > total.get(k, 0) + 1e-9:
+                return False
+        return True
+
+    def run(self):
+        self._create_trials()
+        while not self.is_finished():
+            self.step()
+        for t in self._trials:
+            if t.status == Trial.RUNNING:
+                self._stop(t, Trial.TERMINATED)
+        self._cb("on_experiment_end", trials=self._trials)
+        return self._trials
+
+    def is_finished(self) -> bool:
+        if self._stop_all:
+            return not any(t.status == Trial.RUNNING for t in self._trials)
+        return self._search_done and all(t.is_finished for t in self._trials)
+
+    # ------------------------------------------------------------------ loop
+    def _create_trials(self):
+        from ray_memory_management_amd.tune.search.variant_generator import Searcher
+
+        while not self._search_done:
+            tid = uuid.uuid4().hex[:8]
+            cfg = self.search_alg.suggest(tid)
+            if cfg == Searcher.FINISHED:
+                self._search_done = True
+                break
+            if cfg is None:
+                break
+            pgf = self.pgf
+            res = getattr(self.trainable_cls, "_resources", None)
+            if callable(res) and not isinstance(res, (dict, PlacementGroupFactory)):
+                pgf = resources_to_pgf(res(cfg))
+            self.add_trial(Trial(self.trainable_name, cfg, tid, self.local_dir, pgf, self.max_failures,
+                                 experiment_tag=f"{len(self._trials)}"))
+
+    def step(self):
+        if self.time_budget_s and time.time() - self._start > self.time_budget_s:
+            self._stop_all = True
+        if self.stopper.stop_all():
+            self._stop_all = True
+        if not self._stop_all:
+            self._create_trials()
+            while True:
+                t = self.scheduler.choose_trial_to_run(self)
+                if t is None:
+                    break
+                self._start_trial(t)
+        running = [t for t in self._trials if t.status == Trial.RUNNING and t._pending is not None]
+        if not running:
+            if not self._stop_all and not self._search_done:
+                time.sleep(0.01)
+            elif self._stop_all:
+                for t in self._trials:
+                    if t.status in (Trial.PENDING, Trial.PAUSED):
+                        t.status = Trial.TERMINATED
+            elif not any(t.status == Trial.RUNNING for t in self._trials) and \
+                    any(t.status in (Trial.PENDING, Trial.PAUSED) for t in self._trials):
+                # nothing can run: resources too small for any pending trial, or paused forever
+                stuck = [t for t in self._trials if t.status in (Trial.PENDING, Trial.PAUSED)]
+                if all(t.status == Trial.PAUSED and not t._unpaused for t in stuck):
+                    for t in stuck:  # scheduler will never resume them: finish them
+                        t._unpaused = True
+                elif not any(self.has_resources_for_trial(t) for t in stuck):
+                    raise RuntimeError(f"Insufficient cluster resources to launch trial {stuck[0]} "
+                                       f"(requires {stuck[0].resources.required_resources()}, cluster has "
+                                       f"{ray.cluster_resources()})")
+            return
+        ready, _ = ray.wait([t._pending for t in running], num_returns=1, timeout=1.0)
+        for ref in ready:
+            t = next(x for x in running if x._pending is ref)
+            t._pending = None
+            try:
+                result = ray.get(ref)
+            except Exception as e:  # trial error
+                self._on_error(t, e)
+                continue
+            self._on_result(t, result)
+
+    def _start_trial(self, t: Trial, checkpoint: Optional[Checkpoint] = None):
+        ck = checkpoint if checkpoint is not None else (t.checkpoint if t.status == Trial.PAUSED or t.num_failures
+                                                        else None)
+        head = t.resources.head_bundle
+        opts = {"num_cpus": head.get("CPU", 0), "num_gpus": head.get("GPU", 0),
+                "resources": {k: v for k, v in head.items() if k not in ("CPU", "GPU")}}
+        if not opts["resources"]:
+            opts.pop("resources")
+        info = {"trial_id": t.trial_id, "trial_name": str(t), "logdir": t.logdir,
+                "resources": t.resources.required_resources()}
+        t.runner = self._actor_cls.options(**opts).remote(self.trainable_cls, t.config, info, ck)
+        t.status = Trial.RUNNING
+        t._unpaused = False
+        t.start_time = t.start_time or time.time()
+        os.makedirs(t.logdir, exist_ok=True)
+        with open(os.path.join(t.logdir, "params.json"), "w") as f:
+            json.dump(t.config, f, default=str)
+        t._pending = t.runner.train.remote()
+        self._cb("on_trial_start", trial=t)
+
+    def _on_result(self, t: Trial, result: Dict):
+        dup = result.pop(RESULT_DUPLICATE, False)
+        if not dup or not t.last_result:
+            result.setdefault("trial_id", t.trial_id)
+            result["config"] = t.config
+            result.setdefault("experiment_tag", t.experiment_tag)
+            t.update_last_result(result)
+            with open(os.path.join(t.logdir, "result.json"), "a") as f:
+                f.write(json.dumps(_jsonable(result)) + "\n")
+            self.search_alg.on_trial_result(t.trial_id, result)
+            self._cb("on_trial_result", trial=t, result=result)
+        done = result.get("done", False) or (not dup and self.stopper(t.trial_id, result))
+        if self.checkpoint_freq and not dup and result.get("training_iteration", 0) % self.checkpoint_freq == 0:
+            self._checkpoint(t)
+        if done:
+            self._complete(t)
+            return
+        decision = self.scheduler.on_trial_result(self, t, result) if not dup else TrialScheduler.CONTINUE
+        if t.status != Trial.RUNNING:  # the scheduler acted on the trial itself (e.g. PBT exploit)
+            return
+        if decision == TrialScheduler.STOP:
+            self._complete(t)
+        elif decision == TrialScheduler.PAUSE:
+            self._pause(t)
+        elif t._pending is None and t.status == Trial.RUNNING:
+            t._pending = t.runner.train.remote()
+
+    def _complete(self, t: Trial):
+        if self.checkpoint_at_end:
+            self._checkpoint(t)
+        self._stop(t, Trial.TERMINATED)
+        self.scheduler.on_trial_complete(self, t, t.last_result)
+        self.search_alg.on_trial_complete(t.trial_id, t.last_result)
+        self._cb("on_trial_complete", trial=t)
+
+    def _on_error(self, t: Trial, e: BaseException):
+        t.num_failures += 1
+        t.error = e
+        t.error_msg = "".join(traceback.format_exception_only(type(e), e))
+        os.makedirs(t.logdir, exist_ok=True)
+        with open(os.path.join(t.logdir, "error.txt"), "w") as f:
+            f.write(str(e))
+        self._stop(t, Trial.ERROR, kill=True)
+        if t.num_failures <= max(t.max_failures, 0) or t.max_failures < 0:
+            t.status = Trial.PENDING  # retried from its latest checkpoint
+            return
+        self.scheduler.on_trial_error(self, t)
+        self.search_alg.on_trial_complete(t.trial_id, None, error=True)
+        self._cb("on_trial_error", trial=t)
+        if self.fail_fast:
+            self._stop_all = True
+
+    def _stop(self, t: Trial, status: str, kill: bool = False):
+        if t.runner is not None:
+            if not kill:
+                try:
+                    ray.get(t.runner.stop.remote(), timeout=10)
+                except Exception:
+                    pass
+            try:
+                ray.kill(t.runner)
+            except Exception:
+                pass
+        t.runner = None
+        t._pending = None
+        t.status = status
+
+    # scheduler hooks --------------------------------------------------
+    def checkpoint_trial(self, t: Trial) -> Optional[Checkpoint]:
+        if t.status == Trial.RUNNING and t.runner is not None:
+            if t._pending is not None:  # let the in-flight iteration finish first
+                try:
+                    r = ray.get(t._pending)
+                    t._pending = None
+                    self._record_only(t, r)
+                except Exception:
+                    return t.checkpoint
+            t.checkpoint = ray.get(t.runner.save.remote())
+        return t.checkpoint
+
+    def _record_only(self, t, result):
+        if not result.pop(RESULT_DUPLICATE, False):
+            result["config"] = t.config
+            t.update_last_result(result)
+        if result.get("done"):
+            t._done_pending = True
+        elif t.status == Trial.RUNNING and t.runner is not None:
+            t._pending = t.runner.train.remote()
+
+    def _checkpoint(self, t: Trial):
+        ck = self.checkpoint_trial(t)
+        if ck is None:
+            return
+        path = os.path.join(t.logdir, f"checkpoint_{t.last_result.get('training_iteration', 0):06d}")
+        ck.to_directory(path)
+        t.saved_checkpoints.append((path, dict(t.last_result)))
+        if self.num_to_keep and len(t.saved_checkpoints) > self.num_to_keep:
+            import shutil
+
+            old, _ = t.saved_checkpoints.pop(0)
+            shutil.rmtree(old, ignore_errors=True)
+
+    def _pause(self, t: Trial):
+        t.checkpoint = ray.get(t.runner.save.remote()) if t.runner is not None else t.checkpoint
+        self._stop(t, Trial.PAUSED)
+
+    def stop_trial(self, t: Trial):
+        if t.status in (Trial.RUNNING, Trial.PAUSED, Trial.PENDING):
+            self._stop(t, Trial.TERMINATED)
+            self.search_alg.on_trial_complete(t.trial_id, t.last_result)
+            self._cb("on_trial_complete", trial=t)
+
+    def unpause_trial(self, t: Trial):
+        t._unpaused = True
+
+    def exploit_trial(self, t: Trial, new_config: Dict, checkpoint: Checkpoint, donor: Trial):
+        """PBT: restart `t` from `donor`'s checkpoint with `new_config`."""
+        self._stop(t, Trial.PAUSED)
+        t.config = new_config
+        t.checkpoint = checkpoint
+        self._start_trial(t, checkpoint)
+
+    def _cb(self, hook, **kw):
+        for cb in self.callbacks:
+            fn = getattr(cb, hook, None)
+            if fn is not None:
+                try:
+                    fn(iteration=0, trials=self._trials, **kw)
+                except TypeError:
+                    fn(**kw)
+
+
+def _make_stopper(stop) -> Stopper:
+    if stop is None:
+        return NoopStopper()
+    if isinstance(stop, Stopper):
+        return stop
+    if isinstance(stop, dict):
+        return DictStopper(stop)
+    if callable(stop):
+        return FunctionStopper(stop)
+    raise ValueError(f"Invalid stop criteria {stop!r}")
+
+
+def _jsonable(d):
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, (int, float, str, bool)) or v is None:
+            out[k] = v
+        elif isinstance(v, dict):
+            out[k] = _jsonable(v)
+        else:
+            try:
+                json.dumps(v)
+                out[k] = v
+            except TypeError:
+                out[k] = repr(v)
+    return out

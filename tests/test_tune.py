@@ -1,0 +1,251 @@
+"""Tune: mirrors reference python/ray/tune/tests/{test_api,test_sample,test_trial_scheduler,
+test_tuner,test_stopper}.py at small scale."""
+import os
+import random
+
+import pytest
+
+
+def test_search_space_sampling():
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.search.variant_generator import count_variants, generate_variants
+
+    rng = random.Random(0)
+    for _ in range(50):
+        assert 1 <= tune.uniform(1, 2).sample(random_state=rng) <= 2
+        assert 1e-4 <= tune.loguniform(1e-4, 1e-1).sample(random_state=rng) <= 1e-1
+        assert tune.randint(0, 3).sample(random_state=rng) in (0, 1, 2)
+        assert tune.quniform(0, 1, 0.25).sample(random_state=rng) in (0, 0.25, 0.5, 0.75, 1.0)
+        assert tune.choice(["a", "b"]).sample(random_state=rng) in ("a", "b")
+        assert tune.qrandint(0, 10, 5).sample(random_state=rng) in (0, 5, 10)
+    space = {"a": tune.grid_search([1, 2, 3]), "b": {"c": tune.grid_search(["x", "y"])},
+             "d": tune.uniform(0, 1), "e": tune.sample_from(lambda spec: spec.config.a * 10)}
+    assert count_variants(space) == 6
+    vs = list(generate_variants(space, random.Random(1)))
+    assert len(vs) == 6 and {(v["a"], v["b"]["c"]) for v in vs} == {(a, c) for a in (1, 2, 3) for c in "xy"}
+    assert all(v["e"] == v["a"] * 10 for v in vs)
+
+
+def _objective(config):
+    from ray_memory_management_amd.air import session
+
+    for i in range(config.get("iters", 5)):
+        session.report({"score": config["x"] * (i + 1), "neg": -config["x"]})
+
+
+def test_tuner_grid_and_best(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.air.config import RunConfig
+
+    tuner = tune.Tuner(_objective, param_space={"x": tune.grid_search([1, 2, 3])},
+                       tune_config=tune.TuneConfig(metric="score", mode="max"),
+                       run_config=RunConfig(name="grid", local_dir=str(tmp_path)))
+    grid = tuner.fit()
+    assert len(grid) == 3 and grid.num_errors == 0
+    best = grid.get_best_result()
+    assert best.config["x"] == 3 and best.metrics["score"] == 15 and best.metrics["training_iteration"] == 5
+    assert grid.get_best_result("neg", "max").config["x"] == 1
+    df = grid.get_dataframe()
+    assert set(df["config/x"]) == {1, 2, 3}
+    assert os.path.exists(os.path.join(best.log_dir, "result.json"))
+    assert len(best.metrics_dataframe) == 5
+
+
+def test_tune_run_legacy_api_and_stop(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+
+    def train(config, checkpoint_dir=None):
+        for i in range(100):
+            tune.report(mean_loss=1.0 / (i + 1) / config["lr"])
+
+    analysis = tune.run(train, config={"lr": tune.grid_search([0.1, 1.0])}, stop={"training_iteration": 7},
+                        metric="mean_loss", mode="min", local_dir=str(tmp_path))
+    assert all(t.last_result["training_iteration"] == 7 for t in analysis.trials)
+    assert analysis.best_config["lr"] == 1.0
+    assert analysis.results_df.shape[0] == 2
+
+
+class _Counter:
+    pass
+
+
+def test_class_trainable_checkpoint_and_resources(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+
+    class MyTrainable(tune.Trainable):
+        def setup(self, config):
+            self.v = config["start"]
+
+        def step(self):
+            self.v += 1
+            return {"v": self.v, "done": self.v >= self.config["start"] + 4}
+
+        def save_checkpoint(self, d):
+            return {"v": self.v}
+
+        def load_checkpoint(self, ck):
+            self.v = ck["v"]
+
+    analysis = tune.run(MyTrainable, config={"start": tune.grid_search([0, 10])}, checkpoint_freq=2,
+                        checkpoint_at_end=True, resources_per_trial={"cpu": 1}, local_dir=str(tmp_path),
+                        metric="v", mode="max")
+    t = analysis.best_trial
+    assert t.last_result["v"] == 14 and t.saved_checkpoints
+    assert analysis.get_best_checkpoint(t).to_dict()["__data__"]["v"] == 14
+
+
+def test_trial_error_and_retry(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.air.config import FailureConfig, RunConfig
+
+    marker = tmp_path / "failed_once"
+
+    def flaky(config):
+        from ray_memory_management_amd.air import session
+
+        if config["x"] == 1 and not marker.exists():
+            marker.write_text("x")
+            raise RuntimeError("boom")
+        if config["x"] == 2:
+            raise ValueError("always")
+        session.report({"ok": 1})
+
+    grid = tune.Tuner(flaky, param_space={"x": tune.grid_search([1, 2])},
+                      run_config=RunConfig(local_dir=str(tmp_path), failure_config=FailureConfig(max_failures=1))
+                      ).fit()
+    assert grid.num_errors == 1
+    ok = [r for r in grid if r.error is None]
+    assert len(ok) == 1 and ok[0].metrics["ok"] == 1
+    with pytest.raises(tune.TuneError):
+        tune.run(flaky, config={"x": 2}, local_dir=str(tmp_path))
+
+
+def _curve(config):
+    from ray_memory_management_amd.air import session
+
+    for i in range(1, 21):
+        session.report({"acc": config["q"] * i})
+
+
+def test_asha_stops_bad_trials(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.schedulers import ASHAScheduler
+
+    sched = ASHAScheduler(max_t=20, grace_period=2, reduction_factor=2)
+    grid = tune.Tuner(_curve, param_space={"q": tune.grid_search([8, 7, 6, 5, 4, 3, 2, 1])},
+                      tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=sched,
+                                                  max_concurrent_trials=8)).fit()
+    iters = sorted(r.metrics["training_iteration"] for r in grid)
+    assert iters[-1] == 20 and iters[0] < 20  # some trials early-stopped, the best one ran to max_t
+    assert grid.get_best_result().config["q"] == 8
+
+
+def test_median_stopping_and_hyperband(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.schedulers import HyperBandScheduler, MedianStoppingRule
+
+    med = MedianStoppingRule(time_attr="training_iteration", grace_period=2, min_samples_required=2)
+    grid = tune.Tuner(_curve, param_space={"q": tune.grid_search([1, 2, 3, 4])},
+                      tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=med,
+                                                  max_concurrent_trials=4)).fit()
+    assert min(r.metrics["training_iteration"] for r in grid) < 20
+    hb = HyperBandScheduler(max_t=9, reduction_factor=3)
+    grid = tune.Tuner(_curve, param_space={"q": tune.grid_search(list(range(1, 7)))},
+                      tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=hb,
+                                                  max_concurrent_trials=3)).fit()
+    assert grid.num_errors == 0 and grid.get_best_result().config["q"] == 6
+
+
+def test_pbt_exploits(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.schedulers import PopulationBasedTraining
+
+    class PBTTrainable(tune.Trainable):
+        def setup(self, config):
+            self.total = 0.0
+
+        def step(self):
+            self.total += self.config["lr"]
+            return {"total": self.total, "lr": self.config["lr"]}
+
+        def save_checkpoint(self, d):
+            return {"total": self.total}
+
+        def load_checkpoint(self, ck):
+            self.total = ck["total"]
+
+        def reset_config(self, c):
+            self.config = c
+            return True
+
+    pbt = PopulationBasedTraining(time_attr="training_iteration", perturbation_interval=2,
+                                  hyperparam_mutations={"lr": [0.01, 0.1, 1.0, 10.0]}, quantile_fraction=0.5, seed=0)
+    analysis = tune.run(PBTTrainable, config={"lr": tune.grid_search([0.01, 10.0])}, scheduler=pbt,
+                        metric="total", mode="max", stop={"training_iteration": 8}, local_dir=str(tmp_path))
+    assert pbt._num_perturbations >= 1
+    # the weak trial cloned the strong one's state: both end far above 8 * 0.01
+    assert min(t.last_result["total"] for t in analysis.trials) > 1.0
+
+
+def test_stoppers_and_callbacks(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.air.config import RunConfig
+    from ray_memory_management_amd.tune.stopper import (CombinedStopper, MaximumIterationStopper,
+                                                        TrialPlateauStopper)
+
+    seen = []
+
+    class CB(tune.Callback):
+        def on_trial_result(self, iteration, trials, trial, result, **info):
+            seen.append(result["training_iteration"])
+
+    def const(config):
+        from ray_memory_management_amd.air import session
+
+        for _ in range(50):
+            session.report({"m": 1.0})
+
+    grid = tune.Tuner(const, run_config=RunConfig(
+        local_dir=str(tmp_path), callbacks=[CB()],
+        stop=CombinedStopper(MaximumIterationStopper(30), TrialPlateauStopper("m", num_results=3, grace_period=3)))
+    ).fit()
+    assert grid[0].metrics["training_iteration"] == 3 and seen[-1] == 3
+
+
+def test_with_parameters_and_repeater(ray_shared, tmp_path):
+    import numpy as np
+
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.search import BasicVariantGenerator, ConcurrencyLimiter
+
+    big = np.arange(1000)
+
+    def f(config, data=None):
+        from ray_memory_management_amd.air import session
+
+        session.report({"s": int(data.sum()) + config["k"]})
+
+    grid = tune.Tuner(tune.with_parameters(f, data=big), param_space={"k": tune.randint(0, 5)},
+                      tune_config=tune.TuneConfig(num_samples=4, metric="s", mode="max",
+                                                  search_alg=ConcurrencyLimiter(BasicVariantGenerator(), 2))).fit()
+    assert len(grid) == 4 and all(r.metrics["s"] >= 499500 for r in grid)
+
+
+def _train_loop(config):
+    from ray_memory_management_amd.air import session
+
+    for i in range(3):
+        session.report({"loss": config["lr"] * (3 - i), "rank": session.get_world_rank()})
+
+
+def test_tuner_over_trainer(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.air.config import RunConfig, ScalingConfig
+    from ray_memory_management_amd.train.torch import TorchTrainer
+
+    trainer = TorchTrainer(_train_loop, scaling_config=ScalingConfig(num_workers=2),
+                           run_config=RunConfig(local_dir=str(tmp_path)))
+    grid = tune.Tuner(trainer, param_space={"train_loop_config": {"lr": tune.grid_search([0.1, 0.3])}},
+                      tune_config=tune.TuneConfig(metric="loss", mode="min")).fit()
+    assert grid.num_errors == 0, grid.errors
+    assert grid.get_best_result().config["train_loop_config"]["lr"] == 0.1
