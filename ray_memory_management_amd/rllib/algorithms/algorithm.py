@@ -1,0 +1,149 @@
+"""Algorithm base: a Tune Trainable driving rollout workers + a learner.
+Parity: reference rllib/algorithms/algorithm.py (setup: WorkerSet + policy; step ->
+training_step + metrics; evaluate; compute_single_action; save/restore checkpoints; get_policy;
+stop) and rllib/evaluation/metrics.py (episode_reward_mean/min/max, episode_len_mean, ...).
+"""
+from __future__ import annotations
+
+import collections
+import time
+from typing import Any, Dict, Optional
+
+import numpy as np
+
+from ray_memory_management_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_memory_management_amd.rllib.env import make_env
+from ray_memory_management_amd.rllib.evaluation.rollout_worker import RolloutWorker
+from ray_memory_management_amd.rllib.evaluation.worker_set import WorkerSet
+from ray_memory_management_amd.tune.trainable import Trainable
+
+
+class Algorithm(Trainable):
+    _config_class = AlgorithmConfig
+
+    @classmethod
+    def get_default_config(cls) -> AlgorithmConfig:
+        return cls._config_class(algo_class=cls)
+
+    def __init__(self, config=None, env=None, logger_creator=None, **kw):
+        if isinstance(config, dict) or config is None:
+            cfg = self.get_default_config().update_from_dict(dict(config or {}))
+        else:
+            cfg = config.copy()
+        if env is not None:
+            cfg.env = env
+        self.algo_config = cfg
+        super().__init__(cfg.to_dict())
+
+    def setup(self, config: Dict):
+        import ray_memory_management_amd as ray
+
+        if not ray.is_initialized():
+            ray.init()
+        c = self.algo_config
+        self.validate_config(c)
+        env_creator = c.env if callable(c.env) and not isinstance(c.env, str) else None
+        cfg = c.to_dict()
+        self.workers = WorkerSet(env_creator, cfg, num_workers=c.num_workers)
+        self._episode_history = collections.deque(maxlen=c.metrics_num_episodes_for_smoothing)
+        self._episodes_total = 0
+        self._timesteps_total = 0
+        self._counters = collections.Counter()
+        self._env_creator = env_creator
+        self.callbacks = c.callbacks_class() if c.callbacks_class else None
+        self._setup_learner()
+
+    def validate_config(self, config: AlgorithmConfig):
+        if config.env is None:
+            raise ValueError("No env specified: use config.environment(env=...)")
+
+    def _setup_learner(self):
+        pass
+
+    # ------------------------------------------------------------------ Trainable
+    def step(self) -> Dict:
+        t0 = time.time()
+        c = self.algo_config
+        results: Dict[str, Any] = {}
+        while True:
+            results = self.training_step()
+            if not c.min_time_s_per_iteration or time.time() - t0 >= c.min_time_s_per_iteration:
+                break
+        episodes = self.workers.collect_metrics()
+        for r, ln in episodes:
+            self._episode_history.append((r, ln))
+        self._episodes_total += len(episodes)
+        hist = list(self._episode_history)
+        out = {
+            "episode_reward_mean": float(np.mean([h[0] for h in hist])) if hist else float("nan"),
+            "episode_reward_min": float(np.min([h[0] for h in hist])) if hist else float("nan"),
+            "episode_reward_max": float(np.max([h[0] for h in hist])) if hist else float("nan"),
+            "episode_len_mean": float(np.mean([h[1] for h in hist])) if hist else float("nan"),
+            "episodes_this_iter": len(episodes),
+            "episodes_total": self._episodes_total,
+            "timesteps_total": self._timesteps_total,
+            "num_env_steps_sampled": self._counters["num_env_steps_sampled"],
+            "num_env_steps_trained": self._counters["num_env_steps_trained"],
+            "info": {"learner": {"default_policy": {"learner_stats": results}}, **dict(self._counters)},
+        }
+        if c.evaluation_interval and (self.iteration + 1) % c.evaluation_interval == 0:
+            out["evaluation"] = self.evaluate()
+        if self.callbacks is not None and hasattr(self.callbacks, "on_train_result"):
+            self.callbacks.on_train_result(algorithm=self, result=out)
+        return out
+
+    def training_step(self) -> Dict:
+        raise NotImplementedError
+
+    def evaluate(self) -> Dict:
+        c = self.algo_config
+        rewards, lens = RolloutWorker.evaluate_episodes(self.get_policy(), self._env_creator, c.env, c.env_config,
+                                                        int(c.evaluation_duration))
+        return {"episode_reward_mean": float(np.mean(rewards)), "episode_reward_max": float(np.max(rewards)),
+                "episode_reward_min": float(np.min(rewards)), "episode_len_mean": float(np.mean(lens)),
+                "episodes_this_iter": len(rewards)}
+
+    def get_policy(self, policy_id: str = "default_policy"):
+        return self.workers.local_worker().policy
+
+    def compute_single_action(self, observation, *, explore: Optional[bool] = None, policy_id="default_policy"):
+        return self.get_policy().compute_single_action(observation, explore=bool(explore))
+
+    def get_weights(self):
+        return self.get_policy().get_weights()
+
+    def set_weights(self, weights):
+        self.get_policy().set_weights(weights)
+        self.workers.sync_weights(weights)
+
+    def save_checkpoint(self, checkpoint_dir: str):
+        return {"weights": self.get_weights(), "counters": dict(self._counters),
+                "timesteps_total": self._timesteps_total, "episodes_total": self._episodes_total,
+                "extra": self._extra_state()}
+
+    def load_checkpoint(self, ck):
+        self.set_weights(ck["weights"])
+        self._counters = collections.Counter(ck.get("counters", {}))
+        self._timesteps_total = ck.get("timesteps_total", 0)
+        self._episodes_total = ck.get("episodes_total", 0)
+        self._load_extra_state(ck.get("extra") or {})
+
+    def _extra_state(self):
+        return {}
+
+    def _load_extra_state(self, s):
+        pass
+
+    def cleanup(self):
+        self.workers.stop()
+
+    @classmethod
+    def default_resource_request(cls, config):
+        from ray_memory_management_amd.tune.trainable import PlacementGroupFactory
+
+        cfg = config if isinstance(config, dict) else config.to_dict()
+        head = {"CPU": cfg.get("num_cpus_for_local_worker", 1), "GPU": cfg.get("num_gpus", 0)}
+        workers = [{"CPU": cfg.get("num_cpus_per_worker", 1), "GPU": cfg.get("num_gpus_per_worker", 0)}
+                   for _ in range(cfg.get("num_workers", 0))]
+        return PlacementGroupFactory([{k: v for k, v in head.items() if v}] +
+                                     [{k: v for k, v in w.items() if v} for w in workers])

@@ -1,0 +1,91 @@
+"""WorkerSet: one local RolloutWorker + N remote RolloutWorker actors.
+Parity: reference rllib/evaluation/worker_set.py (local_worker, remote_workers, sync_weights,
+foreach_worker, add_workers, recreate failed workers) and
+rllib/execution/rollout_ops.py:synchronous_parallel_sample.
+Weights are broadcast with ONE ray.put per sync (every worker reads the same shm object)."""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import ray_memory_management_amd as ray
+from ray_memory_management_amd.rllib.evaluation.rollout_worker import RolloutWorker
+from ray_memory_management_amd.rllib.sample_batch import SampleBatch, concat_samples
+
+
+class WorkerSet:
+    def __init__(self, env_creator=None, config: Optional[dict] = None, num_workers: int = 0,
+                 local_worker: bool = True):
+        self._config = dict(config or {})
+        self._env_creator = env_creator
+        self._local = RolloutWorker(env_creator, self._config, 0, num_workers) if local_worker else None
+        self._remote_cls = ray.remote(RolloutWorker).options(
+            num_cpus=self._config.get("num_cpus_per_worker", 1), num_gpus=self._config.get("num_gpus_per_worker", 0))
+        self._remote: List = []
+        self.add_workers(num_workers)
+
+    def add_workers(self, n: int):
+        start = len(self._remote)
+        self._remote += [self._remote_cls.remote(self._env_creator, self._config, start + i + 1, start + n)
+                         for i in range(n)]
+
+    def local_worker(self) -> RolloutWorker:
+        return self._local
+
+    def remote_workers(self) -> List:
+        return list(self._remote)
+
+    def num_remote_workers(self) -> int:
+        return len(self._remote)
+
+    def sync_weights(self, weights=None, from_worker=None):
+        if weights is None:
+            weights = (from_worker or self._local).get_weights()
+        if self._remote:
+            ref = ray.put(weights)
+            ray.get([w.set_weights.remote(ref) for w in self._remote])
+        if self._local is not None and from_worker is not None and from_worker is not self._local:
+            self._local.set_weights(weights)
+
+    def foreach_worker(self, fn: Callable, local_worker: bool = True):
+        out = [fn(self._local)] if local_worker and self._local is not None else []
+        if self._remote:
+            out += ray.get([w.apply.remote(fn) for w in self._remote])
+        return out
+
+    def synchronous_parallel_sample(self, max_env_steps: int) -> SampleBatch:
+        """Sample until >= max_env_steps were collected (reference rollout_ops.py)."""
+        batches, steps = [], 0
+        while steps < max_env_steps:
+            if self._remote:
+                new = ray.get([w.sample.remote() for w in self._remote])
+            else:
+                new = [self._local.sample()]
+            for b in new:
+                steps += b.count
+            batches += new
+        return concat_samples(batches)
+
+    def collect_metrics(self) -> List[tuple]:
+        out = list(self._local.get_metrics()) if self._local is not None else []
+        if self._remote:
+            for m in ray.get([w.get_metrics.remote() for w in self._remote]):
+                out += m
+        return out
+
+    def recreate_failed_workers(self):
+        alive = []
+        for i, w in enumerate(self._remote):
+            try:
+                ray.get(w.get_metrics.remote(), timeout=30)
+                alive.append(w)
+            except Exception:
+                alive.append(self._remote_cls.remote(self._env_creator, self._config, i + 1, len(self._remote)))
+        self._remote = alive
+
+    def stop(self):
+        for w in self._remote:
+            try:
+                ray.kill(w)
+            except Exception:
+                pass
+        self._remote = []

@@ -87,7 +87,7 @@ class FullyConnectedNetwork(nn.Module):
         nn.init.zeros_(self.logits.bias)
 
     def forward(self, obs):
-        obs = obs.float().flatten(1)
+        obs = obs.to(self.logits.weight.dtype).flatten(1)  # fp32 on CPU, bf16 on the GPU fast path
         h = self.body(obs)
         v = self.value(h if self.vf_share_layers else self.vf_body(obs))
         return self.logits(h), v.squeeze(-1)

@@ -228,15 +228,19 @@ class PPOLearner:
         ctr = self.ctr
         # K2b: minibatch gather + u8→bf16 NHWC; K2: ONE gather for every per-sample column —
         # both index idx_all at the device step counter
-        x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
+        frames = full["obs"].dtype == torch.uint8 and full["obs"].dim() == 4
+        if frames:
+            x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
+        else:  # vector observations (e.g. CartPole): plain row gather
+            x = ops.gather_rows(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
-        if self.heads_ok:
+        if self.heads_ok and frames:
             heads = self.model.forward_heads(x, prescaled=True)
             total = ppo_heads_loss(heads, cols, self.coef, self.acc)     # K5c
             grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
         else:
             A = full["A"]
-            logits, v = self.model(x, prescaled=True)
+            logits, v = self.model(x, prescaled=True) if frames else self.model(x)
             total, stats = ppo_categorical_loss(logits, v, cols[:, :A], cols[:, A + 3].long(), cols[:, A],
                                                 cols[:, A + 1], cols[:, A + 2], self.coef)
             grads = list(torch.autograd.grad(total, self.params))
