@@ -1,0 +1,155 @@
+"""Workflows + DAG API: mirrors reference python/ray/workflow/tests/{test_basic_workflows,
+test_recovery,test_cancellation,test_events}.py and python/ray/dag/tests at small scale."""
+import os
+import time
+
+import pytest
+
+
+@pytest.fixture
+def wf(ray_shared, tmp_path):
+    from ray_memory_management_amd import workflow
+
+    workflow.init(str(tmp_path / "wf"))
+    return ray_shared, workflow
+
+
+def test_dag_execute(ray_shared):
+    ray = ray_shared
+    from ray_memory_management_amd.dag import InputNode, MultiOutputNode
+
+    @ray.remote
+    def add(a, b):
+        return a + b
+
+    @ray.remote
+    class Acc:
+        def __init__(self, s):
+            self.s = s
+
+        def inc(self, x):
+            self.s += x
+            return self.s
+
+    with InputNode() as inp:
+        x = add.bind(inp[0], inp[1])
+        y = add.bind(x, 10)
+        a = Acc.bind(100)
+        z = a.inc.bind(y)
+        dag = MultiOutputNode([x, y, z])
+    assert ray.get(dag.execute(1, 2)) == [3, 13, 113]
+
+
+def test_workflow_run_and_outputs(wf):
+    ray, workflow = wf
+
+    @ray.remote
+    def book(x):
+        return f"booked {x}"
+
+    @ray.remote
+    def finalize(items):
+        return sorted(items)
+
+    dag = finalize.bind([book.bind("a"), book.bind("b"), book.options(
+        **workflow.options(task_id="special")).bind("c")])
+    out = workflow.run(dag, workflow_id="trip")
+    assert out == ["booked a", "booked b", "booked c"]
+    assert workflow.get_status("trip") == workflow.WorkflowStatus.SUCCESSFUL
+    assert workflow.get_output("trip") == out
+    assert workflow.get_output("trip", task_id="special") == "booked c"
+    assert ("trip", workflow.WorkflowStatus.SUCCESSFUL) in workflow.list_all()
+    meta = workflow.get_metadata("trip")
+    assert meta["stats"]["end_time"] >= meta["stats"]["start_time"]
+    assert workflow.run(dag, workflow_id="trip") == out  # finished workflows return the stored output
+    workflow.delete("trip")
+    with pytest.raises(workflow.WorkflowNotFoundError):
+        workflow.get_status("trip")
+
+
+def test_workflow_recovery_skips_finished_tasks(wf, tmp_path):
+    ray, workflow = wf
+    marker = tmp_path / "fail_once"
+    marker.write_text("1")
+    counter = tmp_path / "count"
+
+    @ray.remote
+    def step1():
+        with open(counter, "a") as f:
+            f.write("x")
+        return 1
+
+    @ray.remote(max_retries=0)
+    def step2(x):
+        if os.path.exists(marker):
+            raise RuntimeError("transient")
+        return x + 1
+
+    dag = step2.options(**workflow.options(max_retries=0)).bind(step1.bind())
+    with pytest.raises(Exception):
+        workflow.run(dag, workflow_id="rec")
+    assert workflow.get_status("rec") == workflow.WorkflowStatus.FAILED
+    os.remove(marker)
+    assert workflow.resume("rec") == 2
+    assert counter.read_text() == "x"  # step1 ran once: its checkpoint was reused
+
+
+def test_workflow_continuation_and_catch(wf):
+    ray, workflow = wf
+
+    @ray.remote
+    def fact(n, acc=1):
+        if n <= 1:
+            return acc
+        return workflow.continuation(fact.bind(n - 1, acc * n))
+
+    assert workflow.run(fact.bind(5), workflow_id="fact") == 120
+
+    @ray.remote
+    def bad():
+        raise ValueError("nope")
+
+    res, err = workflow.run(bad.options(**workflow.options(catch_exceptions=True)).bind(), workflow_id="catch")
+    assert res is None and isinstance(err, ValueError)
+
+
+def test_workflow_cancel_and_sleep(wf):
+    ray, workflow = wf
+
+    @ray.remote
+    def after(ev):
+        return "done"
+
+    t0 = time.time()
+    assert workflow.run(after.bind(workflow.sleep(0.5)), workflow_id="sleepy") == "done"
+    assert time.time() - t0 >= 0.5
+
+    @ray.remote
+    def slow():
+        time.sleep(30)
+        return 1
+
+    @ray.remote
+    def then(x):
+        return x
+
+    ref = workflow.run_async(then.bind(slow.bind()), workflow_id="cancel_me")
+    time.sleep(0.5)
+    workflow.cancel("cancel_me")
+    assert workflow.get_status("cancel_me") == workflow.WorkflowStatus.CANCELED
+    with pytest.raises(Exception):
+        ray.get(ref)
+
+
+def test_workflow_events(wf):
+    ray, workflow = wf
+
+    class Ready(workflow.EventListener):
+        def poll_for_event(self, value):
+            return value * 2
+
+    @ray.remote
+    def use(ev):
+        return ev + 1
+
+    assert workflow.run(use.bind(workflow.wait_for_event(Ready, 20)), workflow_id="ev") == 41
