@@ -81,7 +81,9 @@ Store* Store::Create(const std::string& name, uint64_t size, const std::string& 
                      double spill_threshold, uint64_t min_spill_size, bool fallback) {
   if (size < (8ull << 20)) size = 8ull << 20;
   uint64_t table_cap = 1 << 14;
-  while (table_cap < (size >> 14) && table_cap < (1ull << 21)) table_cap <<= 1;
+  // one slot per 4 KiB of arena (112 B each, ~2.7% overhead): small-object heavy workloads
+  // (millions of tiny puts) must not run out of slots before they run out of bytes
+  while (table_cap < (size >> 12) && table_cap < (1ull << 22)) table_cap <<= 1;
   uint64_t off = AlignUp(sizeof(Header), 4096);
   uint64_t table_off = off;
   off = AlignUp(off + table_cap * sizeof(Entry), 4096);
@@ -360,10 +362,13 @@ int64_t Store::Find(const ObjectId& id) {
 
 int64_t Store::Insert(const ObjectId& id) {
   uint64_t cap = hdr_->table_cap;
-  if (hdr_->table_used + 1 > cap - cap / 8) {
+  uint64_t live_now = hdr_->stats.num_objects;
+  // truly full (keeps >= 1/16 of the slots empty or tombstoned so probes terminate quickly);
+  // the caller unlocks and reports -- never throw while holding the store mutex
+  if (live_now + 1 > cap - cap / 16) return -1;
+  if (hdr_->table_used + 1 > cap - cap / 8 && live_now + 1 <= cap - cap / 4) {
     // Too many tombstones: rebuild in place, keeping LRU order.
-    uint64_t live = hdr_->stats.num_objects;
-    if (live + 1 > cap - cap / 4) throw std::runtime_error("object table full");
+    uint64_t live = live_now;
     std::vector<Entry> keep;
     keep.reserve(live);
     std::vector<int64_t> lru_order;
@@ -695,6 +700,12 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   uint64_t len = data_size + meta_size;
   Lock();
   int64_t idx = Insert(id);
+  if (idx == -1) {
+    uint64_t live = hdr_->stats.num_objects;
+    Unlock();
+    throw std::runtime_error("ObjectStoreFullError: object table full (" + std::to_string(live) +
+                             " live objects)");
+  }
   if (idx <= -2) {
     *exists = true;
     Unlock();

@@ -608,6 +608,8 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             _local_mode = True
             return RayContext()
         cfg = dict(_system_config or {})
+        if address is None:  # jobs started by the job manager / `rmm start` users connect this way
+            address = os.environ.get("RMM_ADDRESS") or None
         if address in ("auto",) or (address and address.startswith("rmm://")):
             sess = _find_session(address)
             head_sock = os.path.join(sess, "sockets", "head.sock")

@@ -386,6 +386,11 @@ class _Handled(Exception):
 
 
 def main():
+    import faulthandler
+    import signal as _signal
+
+    # `rmm stack` / debugging: SIGUSR1 dumps every thread's stack into this worker's log
+    faulthandler.register(_signal.SIGUSR1, all_threads=True)
     for p in json.loads(os.environ.get("RMM_DRIVER_SYS_PATH", "[]")):
         if p not in sys.path:
             sys.path.append(p)

@@ -163,3 +163,28 @@ def test_memory_monitor_reads_usage():
     assert 0 < used <= total
     m = MemoryMonitor(threshold=1.0)
     assert m.snapshot()["total"] == total
+
+
+def test_object_table_full_does_not_wedge_the_store():
+    """Regression: a full object table used to throw while holding the store mutex, hanging every
+    process that touched the store afterwards."""
+    import os
+
+    from ray_memory_management_amd import _native
+
+    st = _native.store_ext().ObjectStore.create_segment(f"/rmm-tfull-{os.getpid()}", 16 << 20)
+    ids = [i.to_bytes(20, "little") for i in range(1, 16000)]  # table: 16384 slots
+    made = []
+    with pytest.raises(RuntimeError, match="object table full"):
+        for oid in ids:
+            p = st.create(oid, 8)
+            st.seal(oid)
+            p.release()
+            made.append(oid)
+    assert len(made) >= 14000
+    # the lock was released: deletes and new creates still work
+    assert st.delete(made[:100]) == 100
+    p = st.create(ids[-1], 8)
+    st.seal(ids[-1])
+    p.release()
+    assert st.contains(ids[-1])
