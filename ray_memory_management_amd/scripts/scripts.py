@@ -1,0 +1,282 @@
+"""Command line interface: `python -m ray_memory_management_amd.scripts <command>` (or `bin/rmm`).
+
+Parity: reference python/ray/scripts/scripts.py (start --head / stop / status / memory /
+timeline / stack / microbenchmark / submit), experimental/state/state_cli.py (list / summary)
+and dashboard/modules/job/cli.py (job submit / status / logs / stop / list / delete).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import sys
+import tempfile
+import time
+
+
+def _connect(address=None):
+    import ray_memory_management_amd as ray
+
+    if not ray.is_initialized():
+        ray.init(address=address or os.environ.get("RMM_ADDRESS") or "auto")
+    return ray
+
+
+def _session(address=None):
+    from ray_memory_management_amd._private.worker import _find_session
+
+    return _find_session(address or os.environ.get("RMM_ADDRESS") or "auto")
+
+
+def cmd_start(a):
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd._private import worker as _w
+
+    if not a.head:
+        print("only `--head` is supported: every node of this runtime is started by the head (cluster_utils)")
+        return 1
+    res = json.loads(a.resources) if a.resources else None
+    ctx = ray.init(num_cpus=a.num_cpus, num_gpus=a.num_gpus, resources=res,
+                   object_store_memory=a.object_store_memory, _persistent=True)
+    sess = ctx["session_dir"]
+    _w._head_proc = None  # detach: the head keeps running after this process exits
+    ray.shutdown()
+    print(f"Started head. Address: rmm://{sess}\n  connect with ray.init(address='auto') or "
+          f"RMM_ADDRESS=rmm://{sess}\n  stop with `rmm stop`")
+    return 0
+
+
+def cmd_stop(a):
+    try:
+        sess = _session(a.address)
+        info = json.load(open(os.path.join(sess, "session.json")))
+    except (OSError, ValueError):
+        print("no running cluster found")
+        return 0
+    pid = info.get("head_pid")
+    try:
+        os.kill(pid, signal.SIGKILL if a.force else signal.SIGTERM)
+    except ProcessLookupError:
+        pass
+    t0 = time.time()
+    while time.time() - t0 < a.grace_period:
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.1)
+    print(f"Stopped head (pid {pid})")
+    return 0
+
+
+def cmd_status(a):
+    ray = _connect(a.address)
+    tot, avail = ray.cluster_resources(), ray.available_resources()
+    nodes = ray.nodes()
+    print("======== Cluster status ========")
+    print(f"Nodes: {len([n for n in nodes if n.get('Alive', True)])} alive")
+    print("Resources:")
+    for k in sorted(tot):
+        if k.startswith("node:") or "_group_" in k:
+            continue
+        used = tot[k] - avail.get(k, 0)
+        unit = ""
+        if k in ("memory", "object_store_memory"):
+            print(f"  {used / 2**30:.2f}/{tot[k] / 2**30:.2f} GiB {k}")
+        else:
+            print(f"  {used:g}/{tot[k]:g} {k}{unit}")
+    return 0
+
+
+def cmd_memory(a):
+    _connect(a.address)
+    from ray_memory_management_amd import internal
+
+    print(internal.memory_summary(stats_only=a.stats_only, units=a.units, num_entries=a.num_entries))
+    return 0
+
+
+def cmd_timeline(a):
+    ray = _connect(a.address)
+    path = a.output or os.path.join(tempfile.gettempdir(), f"rmm-timeline-{time.strftime('%Y-%m-%d_%H-%M-%S')}.json")
+    ray.timeline(filename=path)
+    print(f"Trace file written to {path} (open in chrome://tracing or ui.perfetto.dev)")
+    return 0
+
+
+def cmd_list(a):
+    _connect(a.address)
+    from ray_memory_management_amd.util import state
+
+    fn = {"actors": state.list_actors, "tasks": state.list_tasks, "objects": state.list_objects,
+          "nodes": state.list_nodes, "workers": state.list_workers, "jobs": state.list_jobs,
+          "placement-groups": state.list_placement_groups}[a.resource]
+    filters = []
+    for f in a.filter or []:
+        for op in ("!=", "="):
+            if op in f:
+                k, v = f.split(op, 1)
+                filters.append((k.strip(), op, v.strip()))
+                break
+    rows = fn(filters=filters, limit=a.limit)
+    if a.format == "json":
+        print(json.dumps(rows, indent=1, default=str))
+    else:
+        for r in rows:
+            print(json.dumps(r, default=str))
+    return 0
+
+
+def cmd_summary(a):
+    _connect(a.address)
+    from ray_memory_management_amd.util import state
+
+    fn = {"tasks": state.summarize_tasks, "actors": getattr(state, "summarize_actors", state.summarize_tasks),
+          "objects": getattr(state, "summarize_objects", state.summarize_tasks)}[a.resource]
+    print(json.dumps(fn(), indent=1, default=str))
+    return 0
+
+
+def cmd_stack(a):
+    """SIGUSR1 every worker of the local session: each dumps all thread stacks into its log."""
+    sess = _session(a.address)
+    info = json.load(open(os.path.join(sess, "session.json")))
+    import psutil
+
+    head = psutil.Process(info["head_pid"])
+    n = 0
+    for c in head.children(recursive=False):
+        try:
+            c.send_signal(signal.SIGUSR1)
+            n += 1
+        except psutil.Error:
+            pass
+    time.sleep(0.5)
+    print(f"Dumped stacks of {n} worker processes into {os.path.join(sess, 'logs')}/worker-*.log")
+    return 0
+
+
+def cmd_microbenchmark(a):
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd._private import ray_perf
+
+    ray.init(num_cpus=a.num_cpus, object_store_memory=a.object_store_memory)
+    ray_perf.run(duration=a.duration, filter_pattern=a.filter)
+    ray.shutdown()
+    return 0
+
+
+def cmd_job(a):
+    from ray_memory_management_amd.job_submission import JobSubmissionClient
+
+    c = JobSubmissionClient(a.address)
+    if a.job_cmd == "submit":
+        rt = json.loads(a.runtime_env_json) if a.runtime_env_json else {}
+        if a.working_dir:
+            rt["working_dir"] = a.working_dir
+        sid = c.submit_job(entrypoint=" ".join(a.entrypoint), submission_id=a.submission_id, runtime_env=rt)
+        print(f"Job '{sid}' submitted successfully")
+        if not a.no_wait:
+            for chunk in c.tail_job_logs(sid):
+                print(chunk, end="")
+            st = c.get_job_status(sid)
+            print(f"\nJob '{sid}' {st.value}")
+            return 0 if st.value == "SUCCEEDED" else 1
+    elif a.job_cmd == "status":
+        info = c.get_job_info(a.job_id)
+        print(f"Status for job '{a.job_id}': {info.status.value}\nStatus message: {info.message}")
+    elif a.job_cmd == "logs":
+        if a.follow:
+            for chunk in c.tail_job_logs(a.job_id):
+                print(chunk, end="")
+        else:
+            print(c.get_job_logs(a.job_id), end="")
+    elif a.job_cmd == "stop":
+        c.stop_job(a.job_id)
+        print(f"Job '{a.job_id}' stopped")
+    elif a.job_cmd == "list":
+        for j in c.list_jobs():
+            print(json.dumps({"submission_id": j.submission_id, "status": j.status.value,
+                              "entrypoint": j.entrypoint, "message": j.message}))
+    elif a.job_cmd == "delete":
+        c.delete_job(a.job_id)
+        print(f"Job '{a.job_id}' deleted")
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="rmm", description="ray_memory_management_amd cluster CLI")
+    sub = p.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("start", help="start a persistent head node")
+    s.add_argument("--head", action="store_true")
+    s.add_argument("--num-cpus", type=int, default=None)
+    s.add_argument("--num-gpus", type=int, default=None)
+    s.add_argument("--resources", default=None, help="JSON dict of custom resources")
+    s.add_argument("--object-store-memory", type=int, default=None)
+    s.set_defaults(fn=cmd_start)
+    s = sub.add_parser("stop", help="stop the head started by `rmm start`")
+    s.add_argument("--address", default=None)
+    s.add_argument("-f", "--force", action="store_true")
+    s.add_argument("-g", "--grace-period", type=float, default=10)
+    s.set_defaults(fn=cmd_stop)
+    for name, fn in (("status", cmd_status), ("timeline", cmd_timeline), ("stack", cmd_stack)):
+        s = sub.add_parser(name)
+        s.add_argument("--address", default=None)
+        if name == "timeline":
+            s.add_argument("--output", default=None)
+        s.set_defaults(fn=fn)
+    s = sub.add_parser("memory", help="object store usage and objects")
+    s.add_argument("--address", default=None)
+    s.add_argument("--stats-only", action="store_true")
+    s.add_argument("--units", default="MB", choices=["B", "KB", "MB", "GB"])
+    s.add_argument("--num-entries", type=int, default=50)
+    s.set_defaults(fn=cmd_memory)
+    s = sub.add_parser("list", help="state API listing")
+    s.add_argument("resource", choices=["actors", "tasks", "objects", "nodes", "workers", "jobs",
+                                        "placement-groups"])
+    s.add_argument("--address", default=None)
+    s.add_argument("-f", "--filter", action="append")
+    s.add_argument("--limit", type=int, default=100)
+    s.add_argument("--format", default="table", choices=["table", "json"])
+    s.set_defaults(fn=cmd_list)
+    s = sub.add_parser("summary")
+    s.add_argument("resource", choices=["tasks", "actors", "objects"])
+    s.add_argument("--address", default=None)
+    s.set_defaults(fn=cmd_summary)
+    s = sub.add_parser("microbenchmark", help="core microbenchmarks (ray_perf)")
+    s.add_argument("--duration", type=float, default=2.0)
+    s.add_argument("--filter", default="")
+    s.add_argument("--num-cpus", type=int, default=None)
+    s.add_argument("--object-store-memory", type=int, default=None)
+    s.set_defaults(fn=cmd_microbenchmark)
+    j = sub.add_parser("job", help="job submission")
+    jsub = j.add_subparsers(dest="job_cmd", required=True)
+    x = jsub.add_parser("submit")
+    x.add_argument("--address", default=None)
+    x.add_argument("--submission-id", default=None)
+    x.add_argument("--working-dir", default=None)
+    x.add_argument("--runtime-env-json", default=None)
+    x.add_argument("--no-wait", action="store_true")
+    x.add_argument("entrypoint", nargs=argparse.REMAINDER)
+    for name in ("status", "logs", "stop", "delete"):
+        x = jsub.add_parser(name)
+        x.add_argument("job_id")
+        x.add_argument("--address", default=None)
+        if name == "logs":
+            x.add_argument("-f", "--follow", action="store_true")
+    x = jsub.add_parser("list")
+    x.add_argument("--address", default=None)
+    j.set_defaults(fn=cmd_job)
+    return p
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    if getattr(a, "entrypoint", None) and a.entrypoint[:1] == ["--"]:
+        a.entrypoint = a.entrypoint[1:]
+    return int(a.fn(a) or 0)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,80 @@
+"""CLI (start/status/memory/list/timeline/stop) and job submission, mirroring reference
+python/ray/tests/test_cli.py and dashboard/modules/job/tests/test_job_manager.py at small scale.
+Runs the CLI as subprocesses against a persistent head it starts and stops itself."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cli(*args, env=None, timeout=120):
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    e.update(env or {})
+    return subprocess.run([sys.executable, "-m", "ray_memory_management_amd.scripts", *args], capture_output=True,
+                          text=True, env=e, timeout=timeout)
+
+
+@pytest.fixture(scope="module")
+def head():
+    r = _cli("start", "--head", "--num-cpus", "2", "--object-store-memory", str(128 << 20))
+    assert r.returncode == 0, r.stderr + r.stdout
+    addr = [w for w in r.stdout.split() if w.startswith("rmm://")][0]
+    yield addr
+    r = _cli("stop", "--address", addr)
+    assert r.returncode == 0, r.stderr
+
+
+def test_cli_status_memory_list_timeline(head, tmp_path):
+    r = _cli("status", "--address", head)
+    assert r.returncode == 0 and "CPU" in r.stdout, r.stderr
+    r = _cli("memory", "--address", head, "--stats-only")
+    assert r.returncode == 0 and "Object store" in r.stdout, r.stderr
+    r = _cli("list", "nodes", "--address", head, "--format", "json")
+    assert r.returncode == 0 and len(json.loads(r.stdout)) >= 1, r.stderr
+    out = tmp_path / "tl.json"
+    r = _cli("timeline", "--address", head, "--output", str(out))
+    assert r.returncode == 0 and out.exists(), r.stderr
+
+
+def test_job_submission_lifecycle(head, tmp_path):
+    script = tmp_path / "job.py"
+    script.write_text(
+        "import ray_memory_management_amd as ray\n"
+        "ray.init()\n"
+        "@ray.remote\n"
+        "def f(x):\n    return x * 2\n"
+        "print('result', sum(ray.get([f.remote(i) for i in range(10)])))\n")
+    r = _cli("job", "submit", "--address", head, "--", sys.executable, str(script),
+             env={"PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "result 90" in r.stdout and "SUCCEEDED" in r.stdout
+    # python API: failing job, stop of a long job, listing
+    from ray_memory_management_amd.job_submission import JobStatus, JobSubmissionClient
+
+    import ray_memory_management_amd as ray
+
+    ray.init(address=head)
+    try:
+        c = JobSubmissionClient(head)
+        bad = c.submit_job(entrypoint="exit 3")
+        long = c.submit_job(entrypoint="sleep 60", submission_id="long_job")
+        deadline = time.time() + 30
+        while not c.get_job_status(bad).is_terminal() and time.time() < deadline:
+            time.sleep(0.1)
+        assert c.get_job_status(bad) == JobStatus.FAILED and c.get_job_info(bad).driver_exit_code == 3
+        while c.get_job_status(long) != JobStatus.RUNNING and time.time() < deadline:
+            time.sleep(0.1)
+        assert c.stop_job(long)
+        assert c.get_job_status(long) == JobStatus.STOPPED
+        ids = {j.submission_id for j in c.list_jobs()}
+        assert {bad, "long_job"} <= ids
+        c.delete_job(bad)
+        assert bad not in {j.submission_id for j in c.list_jobs()}
+    finally:
+        ray.shutdown()
