@@ -256,7 +256,9 @@ class CoreWorker:
         with self.ref_lock:
             if not self.deltas:
                 return None
-            d = [(k, v) for k, v in self.deltas.items() if v]
+            # A ref created and dropped between two flushes nets to 0 but must still reach the head:
+            # (oid, 0) with no local ref left lets the head free an object nobody else references.
+            d = [(k, v) for k, v in self.deltas.items() if v or k not in self.local_refs]
             self.deltas = {}
         return d
 
