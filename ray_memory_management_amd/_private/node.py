@@ -220,6 +220,9 @@ class Head:
         self.contained: Dict[bytes, List[bytes]] = {}
         self.freed_early: set = set()
         self.gpu_owner: Dict[bytes, bytes] = {}
+        from ray_memory_management_amd._private.object_recovery import ObjectRecoveryManager
+
+        self.recovery = ObjectRecoveryManager(self, int(self.config.get("max_lineage_entries", 200_000)))
         self.jobs: Dict[bytes, dict] = {}
         self.events = collections.deque(maxlen=int(self.config.get("timeline_max_events", 200000)))
         self.seal_cursor = 0
@@ -252,10 +255,21 @@ class Head:
         if node_id not in self.nodes or node_id == self.head_node:
             return False
         self.nodes[node_id]["alive"] = False
+        # returns a running task already sealed on the node die with it (its TaskDone may still be
+        # in flight); the task itself is retried when its worker's death is processed
+        for t in list(self.tasks.values()):
+            if t.node == node_id and t.state == RUNNING:
+                for oid in self.recovery.returns_of(t.spec):
+                    try:
+                        self.store.delete([oid])
+                    except Exception:
+                        pass
         for w in list(self.workers.values()):
             if w.node == node_id:
                 self._kill_worker(w)
         self.sched.remove_node(node_id)
+        # the node's primary object copies are gone with it: recover them through lineage
+        self.recovery.node_removed(node_id)
         return True
 
     # ------------------------------------------------------------------ plumbing
@@ -624,6 +638,14 @@ class Head:
             a = self.actors.get(w.actor_id)
             if a is not None and a.worker is w:
                 self._actor_died(a)
+        # GPU objects live in the dead process's HBM arena: they are lost
+        lost = [o for o, owner in self.gpu_owner.items() if owner == w.worker_id]
+        if lost:
+            conns = getattr(self, "gpu_owner_conn", {})
+            for o in lost:
+                self.gpu_owner.pop(o, None)
+                conns.pop(o, None)
+            self.recovery.objects_lost(lost, f"the worker process {w.pid} owning them died", owner_died=True)
 
     def _blocked(self, c: Conn, blocked: bool):
         w = c.worker
@@ -664,6 +686,7 @@ class Head:
         if oid[:1] == b"\xaa" and oid[-3:] == b"\xaa\xaa\xaa":
             self._actor_out_of_scope(oid[1:17])
             return
+        self.recovery.object_freed(oid)
         deleted = self.store.delete([oid])
         if not deleted:
             self.freed_early.add(oid)
@@ -705,6 +728,16 @@ class Head:
         for r in t.arg_refs:
             self.refcounts[r] += 1
         self._enqueue(t)
+
+    def _resubmit(self, spec):
+        """Re-run a finished task to recompute its lost returns (lineage reconstruction)."""
+        t = TaskRec(spec, None)
+        t.attempt = 1
+        self.tasks[spec["task_id"]] = t
+        for r in t.arg_refs:
+            self.refcounts[r] += 1
+        self._enqueue(t)
+        self._wake()
 
     def _strategy_args(self, spec):
         st = spec.get("strategy") or {}
@@ -815,6 +848,8 @@ class Head:
         t.state = state
         t.end_time = time.time()
         self.tasks.pop(t.spec["task_id"], None)
+        if state == FINISHED:
+            self.recovery.task_finished(t.spec, t.node)
         if t.arg_refs:
             self._ref_deltas([(r, -1) for r in t.arg_refs])
             t.arg_refs = []
@@ -849,6 +884,9 @@ class Head:
             self._enqueue(t)
             return
         self._finish(t, FINISHED if status == "ok" else FAILED)
+        if status == "ok" and t.node is not None and not self.nodes.get(t.node, {}).get("alive", True):
+            # finished on a node removed meanwhile: its outputs went down with the node
+            self.recovery.objects_lost(self.recovery.returns_of(t.spec), f"node {t.node} was removed")
         if w is not None:
             if info and info.get("exit"):
                 self._kill_worker(w, force=False)
@@ -1171,6 +1209,8 @@ class Head:
             return self._pg_table(None)
         if what == "refcounts":
             return dict(self.refcounts)
+        if what == "recovery":
+            return self.recovery.stats()
         if what == "timeline":
             return list(self.events)
         if what == "summary":

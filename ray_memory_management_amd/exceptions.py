@@ -125,12 +125,13 @@ class GetTimeoutError(RayError, TimeoutError):
 
 
 class ObjectLostError(RayError):
-    def __init__(self, object_ref_hex="", owner_address="", call_site=""):
+    def __init__(self, object_ref_hex="", owner_address="", call_site="", message=None):
         self.object_ref_hex = object_ref_hex
-        super().__init__(f"Object {object_ref_hex} is lost.")
+        self.message = message
+        super().__init__(message or f"Object {object_ref_hex} is lost.")
 
     def __reduce__(self):
-        return (type(self), (self.object_ref_hex,))
+        return (type(self), (self.object_ref_hex, "", "", self.message))
 
 
 class ObjectFetchTimedOutError(ObjectLostError):
