@@ -84,5 +84,7 @@ PYBIND11_MODULE(_sched, m) {
       .def("nodes", &Scheduler::Nodes)
       .def("num_pending", &Scheduler::NumPending)
       .def("infeasible_tasks", &Scheduler::InfeasibleTasks)
-      .def("waiting_tasks", &Scheduler::WaitingTasks);
+      .def("waiting_tasks", &Scheduler::WaitingTasks)
+      .def("resource_demands", &Scheduler::ResourceDemands)
+      .def("pending_placement_groups", &Scheduler::PendingPlacementGroups);
 }

@@ -420,6 +420,40 @@ std::vector<int64_t> Scheduler::WaitingTasks() const {
   return r;
 }
 
+std::vector<std::map<std::string, double>> Scheduler::ResourceDemands() const {
+  std::vector<std::map<std::string, double>> r;
+  for (auto& kv : tasks_) {
+    const Task& t = kv.second;
+    if (t.cancelled || !t.missing.empty()) continue;
+    std::map<std::string, double> m;
+    bool bundle = false;
+    for (auto& it : t.req.items) {
+      const std::string& n = names_[size_t(it.first)];
+      if (n.find("_group_") != std::string::npos) bundle = true;
+      m[n] = FromFixed(it.second);
+    }
+    if (!bundle) r.push_back(std::move(m));
+  }
+  return r;
+}
+
+std::vector<std::pair<int, std::vector<std::map<std::string, double>>>>
+Scheduler::PendingPlacementGroups() const {
+  std::vector<std::pair<int, std::vector<std::map<std::string, double>>>> r;
+  for (auto& id : pending_pgs_) {
+    auto it = pgs_.find(id);
+    if (it == pgs_.end() || it->second.placed || it->second.removed) continue;
+    std::vector<std::map<std::string, double>> bs;
+    for (auto& b : it->second.bundles) {
+      std::map<std::string, double> m;
+      for (auto& x : b) m[names_[size_t(x.first)]] = FromFixed(x.second);
+      bs.push_back(std::move(m));
+    }
+    r.emplace_back(int(it->second.strategy), std::move(bs));
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------- placement groups
 
 void Scheduler::CreatePlacementGroup(const std::string& id,

@@ -118,6 +118,11 @@ class Scheduler {
   size_t NumPending() const { return tasks_.size(); }
   std::vector<int64_t> InfeasibleTasks();
   std::vector<int64_t> WaitingTasks() const;
+  // Autoscaler views (reference autoscaler/_private/load_metrics.py resource demand vector):
+  // requests of tasks whose deps are ready but that are not placed yet (bundle-targeted
+  // requests excluded: bundles are the demand), and bundles of placement groups not placed yet.
+  std::vector<std::map<std::string, double>> ResourceDemands() const;
+  std::vector<std::pair<int, std::vector<std::map<std::string, double>>>> PendingPlacementGroups() const;
 
  private:
   Node* GetNode(int64_t id);

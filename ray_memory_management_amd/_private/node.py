@@ -233,6 +233,11 @@ class Head:
         self.prestart = int(self.config.get("prestart_workers", min(2, int(res.get("CPU", 1)))))
         self.idle_timeout = float(self.config.get("idle_worker_killing_time_threshold_ms", 60000)) / 1000.0
         self.memory_monitor = None
+        self.autoscaler = None
+        if self.config.get("autoscaler"):
+            from ray_memory_management_amd.autoscaler._private.monitor import Monitor
+
+            self.autoscaler = Monitor(self, self.config["autoscaler"])
         self.last_housekeeping = 0.0
         self.watcher = threading.Thread(target=self._seal_watcher, daemon=True)
         self.watcher.start()
@@ -1248,6 +1253,8 @@ class Head:
                         self._send_nb(w.conn, (P.EXIT,))
                         w.state = "DEAD"
                         idle_total -= 1
+        if self.autoscaler is not None:
+            self.autoscaler.tick()
         # memory monitor: kill the newest retriable task worker when the node is nearly OOM
         if self.memory_monitor is not None:
             victim = self.memory_monitor.pick_victim(self)

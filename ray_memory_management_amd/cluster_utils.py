@@ -70,3 +70,34 @@ class Cluster:
         ray.shutdown()
         self.head = None
         self.worker_nodes = []
+
+
+class AutoscalingCluster:
+    """A local cluster whose worker nodes are added and removed by the autoscaler.
+
+    Parity: reference python/ray/cluster_utils.py:AutoscalingCluster (fake multi-node provider).
+    ``worker_node_types``: {name: {"resources": {...}, "min_workers": m, "max_workers": M}}."""
+
+    def __init__(self, head_resources: dict, worker_node_types: dict, idle_timeout_minutes: float = 0.05,
+                 upscaling_speed: float = 1.0, update_interval_s: float = 0.2, max_workers: Optional[int] = None):
+        self.head_resources = dict(head_resources)
+        types = {k: dict(v) for k, v in worker_node_types.items()}
+        for v in types.values():
+            v.setdefault("min_workers", 0)
+            v.setdefault("max_workers", 1)
+        self.config = {"head_node_type": "head", "available_node_types": types,
+                       "idle_timeout_minutes": idle_timeout_minutes, "upscaling_speed": upscaling_speed,
+                       "update_interval_s": update_interval_s, "provider": {"type": "virtual"}}
+        if max_workers is not None:
+            self.config["max_workers"] = max_workers
+
+    def start(self, _system_config: Optional[dict] = None, **init_kwargs):
+        res = dict(self.head_resources)
+        cpus = res.pop("CPU", 0)
+        gpus = res.pop("GPU", 0)
+        cfg = dict(_system_config or {})
+        cfg["autoscaler"] = self.config
+        ray.init(num_cpus=cpus, num_gpus=gpus, resources=res or None, _system_config=cfg, **init_kwargs)
+
+    def shutdown(self):
+        ray.shutdown()

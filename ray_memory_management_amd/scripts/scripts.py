@@ -86,6 +86,20 @@ def cmd_status(a):
             print(f"  {used / 2**30:.2f}/{tot[k] / 2**30:.2f} GiB {k}")
         else:
             print(f"  {used:g}/{tot[k]:g} {k}{unit}")
+    from ray_memory_management_amd.autoscaler import sdk
+
+    st = sdk.get_status()
+    if st:
+        print("======== Autoscaler ========")
+        for t, n in sorted(st.get("active_nodes", {}).items()):
+            print(f"  {n} {t}")
+        print(f"  launches: {st.get('num_launches', 0)}  terminations: {st.get('num_terminations', 0)}")
+        for d in st.get("demands", [])[:10]:
+            print(f"  pending demand: {d}")
+        for d in st.get("infeasible", [])[:10]:
+            print(f"  infeasible: {d}")
+        for e in st.get("events", [])[-5:]:
+            print(f"  {e}")
     return 0
 
 
