@@ -101,6 +101,15 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True, parallel_
     if parallel_strategy and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         kw = {"bucket_cap_mb": 256, "gradient_as_bucket_view": True}
         kw.update(parallel_strategy_kwargs or {})
+        if parallel_strategy == "bucketed":
+            # our own overlapped bucketed all-reduce (ray_memory_management_amd.parallel)
+            from ray_memory_management_amd.parallel import BucketedAllReduce
+
+            for t in list(model.parameters()) + list(model.buffers()):
+                dist.broadcast(t.data, 0)
+            model._rmm_grad_sync = BucketedAllReduce(model.parameters(),
+                                                     bucket_cap_mb=(parallel_strategy_kwargs or {}).get("bucket_cap_mb"))
+            return model
         if parallel_strategy == "fsdp":
             from torch.distributed.fsdp import FullyShardedDataParallel
 

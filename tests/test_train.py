@@ -14,7 +14,7 @@ def _loop(config):
     import torch.distributed as dist
 
     torch.manual_seed(0)
-    model = prepare_model(torch.nn.Linear(4, 1))
+    model = prepare_model(torch.nn.Linear(4, 1), parallel_strategy=config.get("strategy", "ddp"))
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     start = 0
     ck = session.get_checkpoint()
@@ -51,6 +51,27 @@ def test_torch_trainer_ddp_gloo(ray_start, tmp_path):
     assert res.checkpoint.to_dict()["epoch"] == 4
     assert len(res.best_checkpoints) == 2
     assert len(res.metrics_dataframe) == 5
+
+
+def test_torch_trainer_bucketed_allreduce(ray_start, tmp_path):
+    trainer = TorchTrainer(_loop, train_loop_config={"epochs": 4, "strategy": "bucketed"},
+                           scaling_config=ScalingConfig(num_workers=2, use_gpu=False),
+                           run_config=RunConfig(name="tb", local_dir=str(tmp_path)))
+    res = trainer.fit()
+    assert res.error is None, res.error
+    assert res.metrics["replicas_equal"]
+    assert res.metrics_history[-1]["loss"] < res.metrics_history[0]["loss"]
+
+
+def test_resnet_shapes_and_zero_init():
+    from ray_memory_management_amd.models import resnet18, resnet50
+
+    m = resnet50(num_classes=10)
+    assert sum(p.numel() for p in m.parameters()) == 23528522  # ResNet-50 trunk + 10-way head
+    m = resnet18(num_classes=7).to(memory_format=torch.channels_last)
+    out = m(torch.randn(2, 3, 64, 64).to(memory_format=torch.channels_last))
+    assert out.shape == (2, 7)
+    assert float(m.layer1[0].bn2.weight.abs().sum()) == 0.0
 
 
 def test_resume_from_checkpoint(ray_start, tmp_path):
