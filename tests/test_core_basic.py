@@ -304,3 +304,29 @@ def test_init_twice_and_reinit(ray_start):
     with pytest.raises(RuntimeError):
         ray.init()
     ray.init(ignore_reinit_error=True)
+
+
+def test_dynamic_generator_returns(ray_start):
+    @ray.remote(num_returns="dynamic")
+    def gen(n):
+        for i in range(n):
+            yield np.full(10, i)
+
+    g = ray.get(gen.remote(4))
+    refs = list(g)
+    assert len(refs) == 4
+    assert [int(ray.get(r)[0]) for r in refs] == [0, 1, 2, 3]
+
+
+def test_runtime_env_working_dir(ray_start, tmp_path):
+    (tmp_path / "helper_mod_rmm.py").write_text("VALUE = 41\n")
+    (tmp_path / "data.txt").write_text("hello")
+
+    @ray.remote(runtime_env={"working_dir": str(tmp_path)})
+    def f():
+        import helper_mod_rmm
+
+        with open("data.txt") as fh:
+            return helper_mod_rmm.VALUE + 1, fh.read()
+
+    assert ray.get(f.remote()) == (42, "hello")
