@@ -30,7 +30,15 @@ def train_loop(config):
     from ray_memory_management_amd.train.torch import get_device, prepare_model
 
     dev = get_device()
-    torch.backends.cudnn.benchmark = True
+    # MIOpen immediate mode (heuristic kernel choice): exhaustive find-mode tuning of every ResNet
+    # conv costs minutes on a fresh box
+    torch.backends.cudnn.benchmark = bool(config.get("tune", False))
+    log = open(config["log"], "a") if config.get("log") else None
+
+    def progress(msg):
+        if log:
+            log.write(f"[rank {session.get_world_rank()}] {time.strftime('%H:%M:%S')} {msg}\n")
+            log.flush()
     torch.manual_seed(0)
     model = resnet50(num_classes=1000).to(dev, memory_format=torch.channels_last)
     model = prepare_model(model, parallel_strategy=config["strategy"] if session.get_world_size() > 1 else None)
@@ -40,6 +48,7 @@ def train_loop(config):
     x = torch.randn(b, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (b,), device=dev, generator=g)
     crit = torch.nn.CrossEntropyLoss()
+    progress("model and data ready")
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -49,8 +58,10 @@ def train_loop(config):
         opt.step()
         return loss
 
-    for _ in range(config["warmup"]):
+    for i in range(config["warmup"]):
         step()
+        torch.cuda.synchronize()
+        progress(f"warmup step {i} done")
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
@@ -61,6 +72,7 @@ def train_loop(config):
     if dist.is_initialized():
         dist.barrier()
     el = time.perf_counter() - t0
+    progress(f"timed {config['steps']} steps in {el:.3f}s")
     if dist.is_initialized():
         e = torch.tensor([el], device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -75,17 +87,31 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--strategy", default="ddp", choices=["ddp", "bucketed"])
+    ap.add_argument("--tune", action="store_true", help="MIOpen find mode (cudnn.benchmark)")
+    ap.add_argument("--log", default=os.path.join(ROOT, "gpurun_out", "resnet50_progress.log"))
     a = ap.parse_args()
 
+    os.makedirs(os.path.dirname(a.log), exist_ok=True)
     import ray_memory_management_amd as ray
     from ray_memory_management_amd.air import RunConfig, ScalingConfig
     from ray_memory_management_amd.train.torch import TorchTrainer
 
     ray.init(num_cpus=max(2, a.workers + 1), num_gpus=a.workers,
              _system_config={"memory_monitor_refresh_ms": 0})
+    import threading
+
+    stop = threading.Event()
+
+    def heartbeat():  # keep the run visibly alive while the workers warm up
+        t0 = time.time()
+        while not stop.wait(20):
+            print(f"[train_resnet50] running {time.time() - t0:.0f}s", flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     try:
         tr = TorchTrainer(train_loop, train_loop_config={"batch": a.batch, "steps": a.steps, "warmup": a.warmup,
-                                                         "strategy": a.strategy},
+                                                         "strategy": a.strategy, "tune": a.tune,
+                                                         "log": a.log},
                           scaling_config=ScalingConfig(num_workers=a.workers, use_gpu=True),
                           run_config=RunConfig(name="resnet50_bench"))
         res = tr.fit()
@@ -99,6 +125,7 @@ def main():
                           "dtype": "bf16 autocast", "strategy": a.strategy, "loss": round(m["loss"], 4),
                           "data": "synthetic 224x224 on-device, random init"}), flush=True)
     finally:
+        stop.set()
         ray.shutdown()
 
 
