@@ -1,0 +1,442 @@
+// K10 — fused Nature-CNN trunk (RLlib's default 84x84 Atari vision net) on MFMA.
+//
+// Geometry (rllib/models/utils.py:get_filter_config for 84x84, SAME padding as RLlib SlimConv2d):
+//   frames u8 [B,4,84,84] --conv1 8x8/4 pad 2, 4->16, +b, ReLU--> h1 [B,21,21,16]
+//                          --conv2 4x4/2 pad 2, 16->32, +b, ReLU--> h2 [B,11,11,32] (= NHWC flatten 3872)
+// The 11x11 "valid" third conv is a dense GEMM and stays in hipBLASLt.
+//
+// Why fused: per SGD minibatch (500 frames) these two layers are ~3.6+2.0 MFLOP/frame — nothing
+// for MFMA — but MIOpen runs them as 10+ launches (gather/convert, implicit-GEMM fwd, bias/ReLU,
+// bwd-data, two weight-grad kernels with zero-fills, bias-grad reductions) of 5-35 us each. Here
+// one workgroup owns one frame at a time entirely in LDS:
+//   fwd:  gather u8 frame by minibatch index (device counter window, HIP-graph friendly) → LDS,
+//         conv1 as im2col-on-the-fly GEMM  M=441 pos x N=16 x K=256 (v_mfma_f32_16x16x32_bf16),
+//         bias+ReLU epilogue into an LDS NHWC tile (and h1 out for backward), conv2 the same way
+//         M=121 x N=32 x K=256 from LDS, bias+ReLU → h2.  1 launch.
+//   bwd:  dpre2 = dh2·[h2>0] (+db2), dW2 += dpre2ᵀ·im2col(h1) (K = positions), dh1 = conv2ᵀ by
+//         stride-parity class (each class is a dense K=4 taps x 32 GEMM), dpre1 = dh1·[h1>0]
+//         (+db1), dW1 += dpre1ᵀ·im2col(frame). Weight-grad accumulators stay in registers across
+//         the frames a workgroup owns; one deterministic reduce launch sums the per-workgroup
+//         partials and writes bf16 grads in the parameters' memory order.  2 launches.
+// The 1/255 frame scale is applied to the fp32 conv1 accumulator (exact integer pixels in bf16).
+//
+// MFMA 16x16x32 bf16 fragment maps (gfx950): lane l holds A[row l&15][k 8(l>>4)+j],
+// B[k 8(l>>4)+j][col l&15], j = 0..7; C/D: col l&15, row 4(l>>4)+i, i = 0..3.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace rmm {
+namespace hip {
+namespace trunk {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int C0 = 4, H0 = 84, P0 = 88;            // frame, padded by 2 each side
+constexpr int H1 = 21, C1 = 16, NP1 = 441, NP1P = 448;
+constexpr int P1 = 25;                              // h1 padded by 2 each side
+constexpr int H2 = 11, C2 = 32, NP2 = 121, NP2P = 128;
+constexpr int FRAME_BYTES = C0 * P0 * P0;          // 30976
+constexpr int H1P_ELEMS = P1 * P1 * C1;            // 10000 bf16
+
+__device__ __forceinline__ unsigned short f2bf(float f) {  // round-to-nearest-even
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<unsigned short>(u >> 16);
+}
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(uint32_t(h) << 16); }
+__device__ __forceinline__ unsigned short u8bf(uint32_t b) { return static_cast<unsigned short>(__float_as_uint(float(b)) >> 16); }
+
+__device__ __forceinline__ bf16x8 as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ const int64_t* window(const int64_t* idx, const int64_t* ctr, int64_t period, int64_t rows) {
+  return (ctr && idx) ? idx + (ctr[0] % period) * rows : idx;
+}
+
+// Copy one u8 frame [4][84][84] into the padded LDS image (pixel (y,x) at byte (y+2)*88 + x+2).
+__device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint8_t* frame) {
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+  for (int w = threadIdx.x; w < C0 * H0 * 21; w += blockDim.x) {
+    const int row = w / 21, col = w - row * 21;  // row = ci*84 + y
+    const int ci = row / H0, y = row - ci * H0;
+    const uint32_t v = s32[w];
+    unsigned short* d = reinterpret_cast<unsigned short*>(frame + ci * P0 * P0 + (y + 2) * P0 + 2 + 4 * col);
+    d[0] = static_cast<unsigned short>(v & 0xffffu);
+    d[1] = static_cast<unsigned short>(v >> 16);
+  }
+}
+
+__device__ __forceinline__ void zero_lds(void* p, int bytes) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) q[i] = make_uint4(0, 0, 0, 0);
+}
+
+// 8 consecutive u8 pixels (4-byte aligned start) → bf16x8
+__device__ __forceinline__ bf16x8 frame8(const uint8_t* frame, int off) {
+  const uint32_t a = *reinterpret_cast<const uint32_t*>(frame + off);
+  const uint32_t b = *reinterpret_cast<const uint32_t*>(frame + off + 4);
+  u16x8 v;
+  v[0] = u8bf(a & 0xff); v[1] = u8bf((a >> 8) & 0xff); v[2] = u8bf((a >> 16) & 0xff); v[3] = u8bf(a >> 24);
+  v[4] = u8bf(b & 0xff); v[5] = u8bf((b >> 8) & 0xff); v[6] = u8bf((b >> 16) & 0xff); v[7] = u8bf(b >> 24);
+  return as_bf(v);
+}
+
+struct WStrides { int64_t s0, s1, s2, s3; };  // [co][ci][ky][kx] element strides
+
+// ================================================================ forward
+// grid = B workgroups (one frame each), 256 threads = 4 waves.
+__global__ __launch_bounds__(256) void k_trunk_fwd(
+    const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
+    int64_t B, const unsigned short* __restrict__ W1, WStrides w1, const unsigned short* __restrict__ b1,
+    const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ b2,
+    unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out) {
+  __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t b = blockIdx.x;
+  const int64_t* idx = window(idx0, ctr, period, B);
+  const int64_t src = idx ? idx[b] : b;
+
+  zero_lds(frame, FRAME_BYTES);
+  zero_lds(h1p, H1P_ELEMS * 2);
+  __syncthreads();
+  load_frame(obs + src * (C0 * H0 * H0), frame);
+
+  // conv1 weight fragments: k = 32s + 8g + j → ci = s>>1, ky = 4(s&1) + g, kx = j; col = co = r
+  bf16x8 wf1[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    u16x8 v;
+    const int ci = s >> 1, ky = 4 * (s & 1) + g;
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = W1[r * w1.s0 + ci * w1.s1 + ky * w1.s2 + j * w1.s3];
+    wf1[s] = as_bf(v);
+  }
+  const float bias1 = bf2f(b1[r]);
+  __syncthreads();
+
+  // ---- conv1: 28 M-tiles of 16 positions over 4 waves
+  for (int mt = wave; mt < NP1P / 16; mt += 4) {
+    const int p = min(mt * 16 + r, NP1 - 1);
+    const int oy = p / H1, ox = p - oy * H1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const int ci = s >> 1, ky = 4 * (s & 1) + g;
+      acc = mfma(frame8(frame, ci * P0 * P0 + (4 * oy + ky) * P0 + 4 * ox), wf1[s], acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int q = mt * 16 + 4 * g + i;
+      if (q < NP1) {
+        const float v = fmaxf(acc[i] * (1.0f / 255.0f) + bias1, 0.f);
+        const unsigned short hb = f2bf(v);
+        const int y = q / H1, x = q - y * H1;
+        h1p[((y + 2) * P1 + (x + 2)) * C1 + r] = hb;
+        if (h1_out) h1_out[(b * NP1 + q) * C1 + r] = hb;
+      }
+    }
+  }
+  // conv2 weight fragments (two 16-wide N tiles): k = 32s + 8g + j → pixel pp = 2s + (g>>1)
+  // (ky = pp>>2, kx = pp&3), ci = 8(g&1) + j
+  bf16x8 wf2[2][8];
+#pragma unroll
+  for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      u16x8 v;
+      const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3, co = nt * 16 + r;
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = W2[co * w2.s0 + (8 * (g & 1) + j) * w2.s1 + ky * w2.s2 + kx * w2.s3];
+      wf2[nt][s] = as_bf(v);
+    }
+  const float bias2[2] = {bf2f(b2[r]), bf2f(b2[16 + r])};
+  __syncthreads();
+
+  // ---- conv2: 8 M-tiles (wave w: w, w+4) x 2 N-tiles
+  for (int mt = wave; mt < NP2P / 16; mt += 4) {
+    const int q = min(mt * 16 + r, NP2 - 1);
+    const int oy = q / H2, ox = q - oy * H2;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
+      const u16x8 av = *reinterpret_cast<const u16x8*>(&h1p[((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1)]);
+      const bf16x8 a = as_bf(av);
+      acc0 = mfma(a, wf2[0][s], acc0);
+      acc1 = mfma(a, wf2[1][s], acc1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int qq = mt * 16 + 4 * g + i;
+      if (qq < NP2) {
+        h2_out[(b * NP2 + qq) * C2 + r] = f2bf(fmaxf(acc0[i] + bias2[0], 0.f));
+        h2_out[(b * NP2 + qq) * C2 + 16 + r] = f2bf(fmaxf(acc1[i] + bias2[1], 0.f));
+      }
+    }
+  }
+}
+
+// ================================================================ backward
+constexpr int PART = C1 * 256 + C2 * 256 + C1 + C2;  // per-workgroup fp32 partial: dW1, dW2, db1, db2
+
+// grid = G workgroups, each loops over frames b = blockIdx.x, +G, ...
+__global__ __launch_bounds__(256) void k_trunk_bwd(
+    const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
+    int64_t B, const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ h1,
+    const unsigned short* __restrict__ h2, const unsigned short* __restrict__ dh2, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short dp2[NP2P * C2];    // [q][co2]
+  __shared__ __attribute__((aligned(16))) unsigned short dp2t[C2 * NP2P];   // [co2][q]
+  __shared__ __attribute__((aligned(16))) unsigned short dp1t[C1 * NP1P];   // [ci][p]
+  __shared__ float red[4 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t* idx = window(idx0, ctr, period, B);
+
+  zero_lds(frame, FRAME_BYTES);
+  zero_lds(h1p, H1P_ELEMS * 2);
+  zero_lds(dp2, NP2P * C2 * 2);
+  zero_lds(dp2t, C2 * NP2P * 2);
+  zero_lds(dp1t, C1 * NP1P * 2);
+
+  // dh1 = conv2ᵀ(dpre2): wave w owns stride-parity class (py, px) = (w>>1, w&1). In a class,
+  // input pixel (y, x) = (2a+py, 2c+px) receives taps ky ∈ {py, py+2}, kx ∈ {px, px+2} from
+  // output pixel (a+1-ty, c+1-tx); k = tap*32 + co2, tap = 2ty+tx → one k-step per tap.
+  const int py = wave >> 1, px = wave & 1;
+  const int nrow = py ? 10 : 11, ncol = px ? 10 : 11, ncls = nrow * ncol;
+  bf16x8 wt[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = W2[(8 * g + j) * w2.s0 + r * w2.s1 + ky * w2.s2 + kx * w2.s3];
+    wt[t] = as_bf(v);
+  }
+  f32x4 aw2[2][4], aw1[4];  // dW2 tiles (mt 0/1 x nt w+4i), dW1 tiles (nt w+4i)
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    aw1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    aw2[0][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    aw2[1][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float db1 = 0.f;                       // this lane's ci = r
+  float db2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // co2 = 8(tid&3) + j
+  __syncthreads();
+
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    const int64_t src = idx ? idx[b] : b;
+    // ---- P0: stage frame, h1, dpre2
+    load_frame(obs + src * (C0 * H0 * H0), frame);
+    for (int v = threadIdx.x; v < NP1 * 2; v += blockDim.x) {
+      const int p = v >> 1, half = v & 1;
+      const int y = p / H1, x = p - y * H1;
+      *reinterpret_cast<uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * half]) =
+          *reinterpret_cast<const uint4*>(&h1[(b * NP1 + p) * C1 + 8 * half]);
+    }
+    for (int v = threadIdx.x; v < NP2 * 4; v += blockDim.x) {
+      const int q = v >> 2, c0 = 8 * (v & 3);
+      const u16x8 hv = *reinterpret_cast<const u16x8*>(&h2[(b * NP2 + q) * C2 + c0]);
+      const u16x8 gv = *reinterpret_cast<const u16x8*>(&dh2[(b * NP2 + q) * C2 + c0]);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const unsigned short d = (hv[j] != 0 && !(hv[j] & 0x8000)) ? gv[j] : static_cast<unsigned short>(0);
+        o[j] = d;
+        db2[j] += bf2f(d);
+        dp2t[(c0 + j) * NP2P + q] = d;
+      }
+      *reinterpret_cast<u16x8*>(&dp2[q * C2 + c0]) = o;
+    }
+    __syncthreads();
+
+    // ---- P1a: dW2[co2][k=(ky,kx,ci)] += Σ_q dpre2[q][co2] · h1p[2oy+ky][2ox+kx][ci]
+#pragma unroll
+    for (int s = 0; s < NP2P / 32; s++) {
+      const bf16x8 a0 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[r * NP2P + 32 * s + 8 * g]));
+      const bf16x8 a1 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[(16 + r) * NP2P + 32 * s + 8 * g]));
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int k = (wave + 4 * i) * 16 + r;
+        const int ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+        u16x8 bv;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int q = min(32 * s + 8 * g + j, NP2 - 1);
+          const int oy = q / H2, ox = q - oy * H2;
+          bv[j] = h1p[((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + ci];
+        }
+        const bf16x8 bb = as_bf(bv);
+        aw2[0][i] = mfma(a0, bb, aw2[0][i]);
+        aw2[1][i] = mfma(a1, bb, aw2[1][i]);
+      }
+    }
+    // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 → dp1t, db1
+    for (int mt = 0; mt * 16 < ncls; mt++) {
+      const int m = mt * 16 + r;
+      const int a = m / ncol, c = m - a * ncol;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
+        u16x8 av = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (m < ncls && oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
+          av = *reinterpret_cast<const u16x8*>(&dp2[(oy * H2 + ox) * C2 + 8 * g]);
+        acc = mfma(as_bf(av), wt[t], acc);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int mm = mt * 16 + 4 * g + i;
+        if (mm < ncls) {
+          const int aa = mm / ncol, cc = mm - aa * ncol;
+          const int y = 2 * aa + py, x = 2 * cc + px;
+          const unsigned short hv = h1p[((y + 2) * P1 + (x + 2)) * C1 + r];
+          const float d = (hv != 0 && !(hv & 0x8000)) ? acc[i] : 0.f;
+          const unsigned short db = f2bf(d);
+          db1 += bf2f(db);
+          dp1t[r * NP1P + y * H1 + x] = db;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- P2: dW1[co][k=(ci,ky,kx)] += Σ_p dpre1[p][co] · frame[ci][4oy+ky][4ox+kx] / 255
+#pragma unroll 2
+    for (int s = 0; s < NP1P / 32; s++) {
+      const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(&dp1t[r * NP1P + 32 * s + 8 * g]));
+      int pys[8], pxs[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int p = min(32 * s + 8 * g + j, NP1 - 1);
+        pys[j] = p / H1;
+        pxs[j] = p - pys[j] * H1;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int k = (wave + 4 * i) * 16 + r;
+        const int ci = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+        const uint8_t* base = frame + ci * P0 * P0 + ky * P0 + kx;
+        u16x8 bv;
+#pragma unroll
+        for (int j = 0; j < 8; j++) bv[j] = u8bf(base[4 * pys[j] * P0 + 4 * pxs[j]]);
+        aw1[i] = mfma(a, as_bf(bv), aw1[i]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- write this workgroup's partials (fp32): [dW1 16x256][dW2 32x256][db1 16][db2 32]
+  float* out = partial + int64_t(blockIdx.x) * PART;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int col = (wave + 4 * i) * 16 + r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int row = 4 * g + e;
+      out[row * 256 + col] = aw1[i][e] * (1.0f / 255.0f);
+      out[C1 * 256 + row * 256 + col] = aw2[0][i][e];
+      out[C1 * 256 + (16 + row) * 256 + col] = aw2[1][i][e];
+    }
+  }
+  // db1: lanes r, r+16, r+32, r+48 of every wave share ci = r
+  db1 += __shfl_xor(db1, 16);
+  db1 += __shfl_xor(db1, 32);
+  if (lane < 16) red[wave * 16 + lane] = db1;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int t = threadIdx.x;
+    out[C1 * 256 + C2 * 256 + t] = red[t] + red[16 + t] + red[32 + t] + red[48 + t];
+  }
+  __syncthreads();
+  // db2: thread t holds co2 = 8(t&3)+j; 64 threads share each (t&3)
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    float v = db2[j];
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 4) red[wave * 64 + lane * 8 + j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int co = threadIdx.x;  // = 8*(lane&3) + j
+    const int q4 = co >> 3, j = co & 7;
+    float s = 0.f;
+    for (int w = 0; w < 4; w++) s += red[w * 64 + q4 * 8 + j];
+    out[C1 * 256 + C2 * 256 + C1 + co] = s;
+  }
+}
+
+// Sum the G partials in a fixed order and write bf16 grads in each parameter's memory order.
+__global__ __launch_bounds__(256) void k_trunk_reduce(const float* __restrict__ partial, int G,
+                                                      unsigned short* __restrict__ dW1, WStrides w1,
+                                                      unsigned short* __restrict__ db1,
+                                                      unsigned short* __restrict__ dW2, WStrides w2,
+                                                      unsigned short* __restrict__ db2) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= PART) return;
+  float s = 0.f;
+  for (int gi = 0; gi < G; gi++) s += partial[int64_t(gi) * PART + e];
+  const unsigned short v = f2bf(s);
+  if (e < C1 * 256) {  // k = (ci, ky, kx)
+    const int co = e >> 8, k = e & 255, ci = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+    dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3] = v;
+  } else if (e < C1 * 256 + C2 * 256) {  // k = (ky, kx, ci)
+    const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+    dW2[co * w2.s0 + ci * w2.s1 + ky * w2.s2 + kx * w2.s3] = v;
+  } else if (e < C1 * 256 + C2 * 256 + C1) {
+    db1[e - C1 * 256 - C2 * 256] = v;
+  } else {
+    db2[e - C1 * 256 - C2 * 256 - C1] = v;
+  }
+}
+
+}  // namespace trunk
+
+static trunk::WStrides ws(const int64_t* s) { return trunk::WStrides{s[0], s[1], s[2], s[3]}; }
+
+void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
+                      const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
+                      const void* b2, void* h1, void* h2, hipStream_t stream) {
+  if (B <= 0) return;
+  if (period <= 0) period = 1;
+  hipLaunchKernelGGL(trunk::k_trunk_fwd, dim3(uint32_t(B)), dim3(256), 0, stream, obs, idx, ctr, period, B,
+                     static_cast<const unsigned short*>(W1), ws(w1s), static_cast<const unsigned short*>(b1),
+                     static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(b2),
+                     static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2));
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+int nature_trunk_bwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 256))); }
+int64_t nature_trunk_partial_floats(int64_t B) { return int64_t(nature_trunk_bwd_groups(B)) * trunk::PART; }
+
+void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
+                      const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
+                      float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
+                      hipStream_t stream) {
+  if (B <= 0) return;
+  if (period <= 0) period = 1;
+  const int G = nature_trunk_bwd_groups(B);
+  hipLaunchKernelGGL(trunk::k_trunk_bwd, dim3(uint32_t(G)), dim3(256), 0, stream, obs, idx, ctr, period, B,
+                     static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(h1),
+                     static_cast<const unsigned short*>(h2), static_cast<const unsigned short*>(dh2), partial);
+  RMM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3((trunk::PART + 255) / 256), dim3(256), 0, stream, partial, G,
+                     static_cast<unsigned short*>(dW1), ws(w1s), static_cast<unsigned short*>(db1),
+                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2));
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace rmm

@@ -86,5 +86,20 @@ int64_t bias_relu_bwd_partials(int64_t M);
 void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, float* partial, int64_t M, int C,
                    bool relu, hipStream_t stream);
 
+// K10: fused Nature-CNN trunk (conv 8x8/4 4->16 + conv 4x4/2 16->32, bias+ReLU) on MFMA, one
+// workgroup per frame in LDS. Frames u8 [.,4,84,84] gathered by idx (device-counter window like
+// gather_rows); weights bf16 with element strides w*s = [co, ci, ky, kx]. h1 [B,441,16] (may be
+// null: inference) and h2 [B,121,32] bf16 outputs. Backward writes bf16 dW1/db1/dW2/db2 (param
+// memory order) through `partial` (nature_trunk_partial_floats(B) fp32).
+void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
+                      const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
+                      const void* b2, void* h1, void* h2, hipStream_t stream);
+int nature_trunk_bwd_groups(int64_t B);
+int64_t nature_trunk_partial_floats(int64_t B);
+void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
+                      const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
+                      float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
+                      hipStream_t stream);
+
 }  // namespace hip
 }  // namespace rmm

@@ -2,6 +2,7 @@
 rllib/models/utils.py:get_filter_config (84x84 Atari filters [[16,8,4],[32,4,2],[256,11,1]])."""
 from __future__ import annotations
 
+import os
 from typing import List, Sequence
 
 import torch
@@ -45,6 +46,76 @@ class _ConvBiasReLUFn(torch.autograd.Function):
             dpre, x, w, None, stride, padding, (1, 1), False, (0, 0), 1,
             (ctx.needs_input_grad[0], ctx.needs_input_grad[1], False))
         return dx, dw, db, None, None
+
+
+class _NatureTrunkFn(torch.autograd.Function):
+    """K10: both Nature-CNN convs (+bias/ReLU, + the u8 frame gather/scale) as ONE MFMA kernel
+    forward and one kernel (+ a deterministic partial-sum reduce) backward — see
+    csrc/hip/conv_kernels.hip. Input: u8 frames [N,4,84,84] and optional minibatch indices (with a
+    device step counter window, as ops.gather_rows). Output: h2 [rows, 11*11*32] bf16 (NHWC flatten)."""
+
+    @staticmethod
+    def forward(ctx, obs, idx, ctr, period, rows, w1, b1, w2, b2):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        dev = obs.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        train = any(ctx.needs_input_grad[5:9])  # grad mode is off inside forward(): ask ctx
+        h2 = torch.empty((rows, 11 * 11 * 32), dtype=torch.bfloat16, device=dev)
+        h1 = torch.empty((rows, 441, 16), dtype=torch.bfloat16, device=dev) if train else None
+        h.nature_trunk_fwd(obs.data_ptr(), idx.data_ptr() if idx is not None else 0,
+                           ctr.data_ptr() if ctr is not None else 0, int(period), int(rows), w1.data_ptr(),
+                           list(w1.stride()), b1.data_ptr(), w2.data_ptr(), list(w2.stride()), b2.data_ptr(),
+                           h1.data_ptr() if h1 is not None else 0, h2.data_ptr(), stream)
+        if train:
+            ctx.save_for_backward(obs, idx, ctr, w1, w2, h1, h2)
+            ctx.conf = (int(period), int(rows))
+        return h2
+
+    @staticmethod
+    def backward(ctx, dh2):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        obs, idx, ctr, w1, w2, h1, h2 = ctx.saved_tensors
+        period, rows = ctx.conf
+        dh2 = dh2.contiguous()
+        dev = obs.device
+        part = torch.empty(h.nature_trunk_partial_floats(rows), dtype=torch.float32, device=dev)
+        dw1 = torch.empty_strided(w1.size(), w1.stride(), dtype=w1.dtype, device=dev)
+        dw2 = torch.empty_strided(w2.size(), w2.stride(), dtype=w2.dtype, device=dev)
+        db1 = torch.empty(16, dtype=w1.dtype, device=dev)
+        db2 = torch.empty(32, dtype=w2.dtype, device=dev)
+        h.nature_trunk_bwd(obs.data_ptr(), idx.data_ptr() if idx is not None else 0,
+                           ctr.data_ptr() if ctr is not None else 0, period, rows, w2.data_ptr(), list(w2.stride()),
+                           h1.data_ptr(), h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(),
+                           list(w1.stride()), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(),
+                           torch.cuda.current_stream(dev).cuda_stream)
+        return None, None, None, None, None, dw1, db1, dw2, db2
+
+
+def nature_trunk(obs, w1, b1, w2, b2, idx=None, ctr=None, period: int = 1, rows: int = None):
+    """Fused Nature-CNN trunk on u8 frames (see _NatureTrunkFn). Checks shapes on the host before
+    launching the hand-written kernel."""
+    if obs.dtype != torch.uint8 or obs.dim() != 4 or tuple(obs.shape[1:]) != (4, 84, 84) or not obs.is_contiguous():
+        raise ValueError(f"nature_trunk: need contiguous u8 frames [N,4,84,84], got {tuple(obs.shape)} {obs.dtype}")
+    if tuple(w1.shape) != (16, 4, 8, 8) or tuple(w2.shape) != (32, 16, 4, 4) or b1.numel() != 16 or b2.numel() != 32:
+        raise ValueError("nature_trunk: weights must be conv 4->16 8x8 and 16->32 4x4")
+    if any(t.dtype != torch.bfloat16 for t in (w1, b1, w2, b2)):
+        raise ValueError("nature_trunk: bf16 weights required")
+    if idx is None:
+        rows = obs.shape[0] if rows is None else rows
+        if rows > obs.shape[0]:
+            raise ValueError("nature_trunk: rows > frames")
+    else:
+        if idx.dtype != torch.int64 or not idx.is_contiguous() or rows is None:
+            raise ValueError("nature_trunk: idx must be contiguous int64 and rows given")
+        if idx.numel() < rows * (period if ctr is not None else 1):
+            raise ValueError("nature_trunk: index table shorter than rows * period")
+        if ctr is not None and (ctr.dtype != torch.int64 or ctr.device != obs.device):
+            raise ValueError("nature_trunk: ctr must be an int64 device tensor")
+    return _NatureTrunkFn.apply(obs, idx, ctr, period, rows, w1, b1.contiguous(), w2, b2.contiguous())
 
 
 class ConvReLU(nn.Conv2d):
@@ -121,6 +192,10 @@ class VisionNetwork(nn.Module):
             c = out
         self.out_hw = hw
         self.convs = nn.Sequential(*layers)
+        # the exact RLlib 84x84 Atari stack runs as the fused K10 kernel on the GPU bf16 path
+        self.nature = (in_hw == 84 and in_channels == 4 and len(layers) == 2 and self.dense_tail is not None
+                       and [(l.in_channels, l.out_channels, l.kernel_size, l.stride, l.padding) for l in layers]
+                       == [(4, 16, (8, 8), (4, 4), (2, 2)), (16, 32, (4, 4), (2, 2), (2, 2))])
         self.num_outputs = num_outputs
         # policy logits and the (shared-trunk) value head are ONE Linear of width A+1: one GEMM
         # forward/backward, and the fused loss (K5c) / sampler (K7) read both columns in place.
@@ -145,6 +220,8 @@ class VisionNetwork(nn.Module):
             obs = obs.permute(0, 3, 1, 2)
         bf16_path = obs.is_cuda and obs.dtype == torch.uint8 and obs.is_contiguous() and (
             torch.is_autocast_enabled() or self.heads.weight.dtype == torch.bfloat16)
+        if bf16_path and self.fused_trunk_ok(obs):
+            return self.forward_frames(obs)
         if bf16_path:
             from ray_memory_management_amd import ops
 
@@ -153,6 +230,19 @@ class VisionNetwork(nn.Module):
             x = obs.to(self.heads.weight.dtype if not torch.is_autocast_enabled() else torch.float32) * (1.0 / 255.0)
             x = x.contiguous(memory_format=torch.channels_last)
         return self._trunk(x)
+
+    def fused_trunk_ok(self, obs) -> bool:
+        return (self.nature and obs.is_cuda and obs.dtype == torch.uint8 and obs.dim() == 4
+                and tuple(obs.shape[1:]) == (4, 84, 84) and obs.is_contiguous()
+                and self.heads.weight.dtype == torch.bfloat16 and not torch.is_autocast_enabled()
+                and not os.environ.get("RMM_NO_FUSED_TRUNK"))
+
+    def forward_frames(self, obs, idx=None, ctr=None, period: int = 1, rows: int = None):
+        """u8 frames (optionally gathered by a minibatch index window) → heads [rows, A+1], with both
+        convs in the fused K10 kernel."""
+        c1, c2 = self.convs[0], self.convs[1]
+        h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
+        return self.heads(torch.relu(self.dense_tail(h)))
 
     def _trunk(self, x):
         h = self.convs(x)

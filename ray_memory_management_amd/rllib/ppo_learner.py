@@ -229,12 +229,20 @@ class PPOLearner:
         # K2b: minibatch gather + u8→bf16 NHWC; K2: ONE gather for every per-sample column —
         # both index idx_all at the device step counter
         frames = full["obs"].dtype == torch.uint8 and full["obs"].dim() == 4
-        if frames:
+        fused = frames and self.heads_ok and getattr(self.model, "fused_trunk_ok", None) is not None \
+            and self.model.fused_trunk_ok(full["obs"])
+        if fused:  # K10: gather + both convs inside one MFMA kernel
+            x = None
+        elif frames:
             x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         else:  # vector observations (e.g. CartPole): plain row gather
             x = ops.gather_rows(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
-        if self.heads_ok and frames:
+        if fused:
+            heads = self.model.forward_frames(full["obs"], idx=full["idx"], ctr=ctr, period=period, rows=mbs)
+            total = ppo_heads_loss(heads, cols, self.coef, self.acc)     # K5c
+            grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
+        elif self.heads_ok and frames:
             heads = self.model.forward_heads(x, prescaled=True)
             total = ppo_heads_loss(heads, cols, self.coef, self.acc)     # K5c
             grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
