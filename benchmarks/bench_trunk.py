@@ -1,0 +1,59 @@
+"""Microbenchmark of the K10 fused Nature-CNN trunk kernels (csrc/hip/conv_kernels.hip) with the
+profiling phase masks: prints µs per launch for fwd (B=500 SGD minibatch, B=50 rollout step) and
+bwd (B=500), each phase skipped in turn to attribute time. Usage: python benchmarks/bench_trunk.py"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from ray_memory_management_amd._native import require_hip  # noqa: E402
+
+
+def timeit(fn, iters=200):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    h = require_hip()
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    obs = torch.randint(0, 256, (5000, 4, 84, 84), dtype=torch.uint8, device=dev)
+    w1 = (torch.randn(16, 4, 8, 8, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w2 = (torch.randn(32, 16, 4, 4, device=dev) * 0.1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b1 = torch.zeros(16, dtype=torch.bfloat16, device=dev)
+    b2 = torch.zeros(32, dtype=torch.bfloat16, device=dev)
+    out = {}
+    for B in (500, 50):
+        idx = torch.randperm(5000, device=dev)[:B].contiguous()
+        h1 = torch.empty(B, 441, 16, dtype=torch.bfloat16, device=dev)
+        h2 = torch.empty(B, 3872, dtype=torch.bfloat16, device=dev)
+        for dbg in (0, 1, 2, 3, 4, 7):
+            out[f"fwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_fwd(
+                obs.data_ptr(), idx.data_ptr(), 0, 1, B, w1.data_ptr(), list(w1.stride()), b1.data_ptr(),
+                w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), st, dbg=dbg)), 1)
+        if B == 500:
+            dh2 = torch.randn(B, 3872, device=dev).to(torch.bfloat16)
+            part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
+            dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
+            db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
+            for dbg in (0, 1, 2, 4, 7, 8, 15):
+                out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
+                    obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
+                    h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
+                    dw2.data_ptr(), db2.data_ptr(), st, dbg=dbg)), 1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -10,7 +10,7 @@
 // bwd-data, two weight-grad kernels with zero-fills, bias-grad reductions) of 5-35 us each. Here
 // one workgroup owns one frame at a time entirely in LDS:
 //   fwd:  gather u8 frame by minibatch index (device counter window, HIP-graph friendly) → LDS,
-//         conv1 as im2col-on-the-fly GEMM  M=441 pos x N=16 x K=256 (v_mfma_f32_16x16x32_bf16),
+//         conv1 as im2col-on-the-fly GEMM  M=441 pos x N=16 x K=256 (k = ky,kx,ci over an HWC LDS frame) (v_mfma_f32_16x16x32_bf16),
 //         bias+ReLU epilogue into an LDS NHWC tile (and h1 out for backward), conv2 the same way
 //         M=121 x N=32 x K=256 from LDS, bias+ReLU → h2.  1 launch.
 //   bwd:  dpre2 = dh2·[h2>0] (+db2), dW2 += dpre2ᵀ·im2col(h1) (K = positions), dh1 = conv2ᵀ by
@@ -60,16 +60,37 @@ __device__ __forceinline__ const int64_t* window(const int64_t* idx, const int64
   return (ctr && idx) ? idx + (ctr[0] % period) * rows : idx;
 }
 
-// Copy one u8 frame [4][84][84] into the padded LDS image (pixel (y,x) at byte (y+2)*88 + x+2).
+// Copy one u8 frame [4][84][84] (NCHW) into the padded HWC LDS image: pixel (y, x) channel c at
+// byte ((y+2)*88 + x+2)*4 + c. A thread takes the same 4-pixel word from the 4 channel planes
+// (4 coalesced u32 loads), transposes the 4x4 bytes in registers and writes 16 B of HWC pixels.
+// All of a thread's loads are issued before any LDS write (28 in flight): a load→store per
+// iteration would serialise ~28 HBM round trips per frame. Needs blockDim 256.
 __device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint8_t* frame) {
+  constexpr int NW = H0 * H0 / 4, PER = (NW + 255) / 256;  // 1764 words per plane
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
-  for (int w = threadIdx.x; w < C0 * H0 * 21; w += blockDim.x) {
-    const int row = w / 21, col = w - row * 21;  // row = ci*84 + y
-    const int ci = row / H0, y = row - ci * H0;
-    const uint32_t v = s32[w];
-    unsigned short* d = reinterpret_cast<unsigned short*>(frame + ci * P0 * P0 + (y + 2) * P0 + 2 + 4 * col);
-    d[0] = static_cast<unsigned short>(v & 0xffffu);
-    d[1] = static_cast<unsigned short>(v >> 16);
+  uint32_t v[PER][C0];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + 256 * k;
+    if (o < NW) {
+#pragma unroll
+      for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + 256 * k;
+    if (o < NW) {
+      const int y = o / 21, x = 4 * (o - y * 21);
+      uint32_t px[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)  // pixel q: bytes (c0, c1, c2, c3) = byte q of each plane word
+        px[q] = ((v[k][0] >> (8 * q)) & 0xffu) | (((v[k][1] >> (8 * q)) & 0xffu) << 8) |
+                (((v[k][2] >> (8 * q)) & 0xffu) << 16) | (((v[k][3] >> (8 * q)) & 0xffu) << 24);
+      uint2* d = reinterpret_cast<uint2*>(frame + ((y + 2) * P0 + x + 2) * 4);  // 8-B aligned
+      d[0] = make_uint2(px[0], px[1]);
+      d[1] = make_uint2(px[2], px[3]);
+    }
   }
 }
 
@@ -78,10 +99,10 @@ __device__ __forceinline__ void zero_lds(void* p, int bytes) {
   for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) q[i] = make_uint4(0, 0, 0, 0);
 }
 
-// 8 consecutive u8 pixels (4-byte aligned start) → bf16x8
+// 8 consecutive bytes of the HWC frame (8-byte aligned: 2 pixels x 4 channels) → bf16x8
 __device__ __forceinline__ bf16x8 frame8(const uint8_t* frame, int off) {
-  const uint32_t a = *reinterpret_cast<const uint32_t*>(frame + off);
-  const uint32_t b = *reinterpret_cast<const uint32_t*>(frame + off + 4);
+  const uint2 w = *reinterpret_cast<const uint2*>(frame + off);
+  const uint32_t a = w.x, b = w.y;
   u16x8 v;
   v[0] = u8bf(a & 0xff); v[1] = u8bf((a >> 8) & 0xff); v[2] = u8bf((a >> 16) & 0xff); v[3] = u8bf(a >> 24);
   v[4] = u8bf(b & 0xff); v[5] = u8bf((b >> 8) & 0xff); v[6] = u8bf((b >> 16) & 0xff); v[7] = u8bf(b >> 24);
@@ -96,7 +117,7 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, const unsigned short* __restrict__ W1, WStrides w1, const unsigned short* __restrict__ b1,
     const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ b2,
-    unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out) {
+    unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -108,17 +129,22 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
   zero_lds(frame, FRAME_BYTES);
   zero_lds(h1p, H1P_ELEMS * 2);
   __syncthreads();
-  load_frame(obs + src * (C0 * H0 * H0), frame);
+  if (!(dbg & 4)) load_frame(obs + src * (C0 * H0 * H0), frame);
 
-  // conv1 weight fragments: k = 32s + 8g + j → ci = s>>1, ky = 4(s&1) + g, kx = j; col = co = r
+  // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
+  // j → (kx = 2g + (j>>2), ci = j&3); col = co = r. Channels-last weights: one 16-B load.
   bf16x8 wf1[8];
+  const bool w1_cl = (w1.s1 == 1 && w1.s3 == 4);
 #pragma unroll
   for (int s = 0; s < 8; s++) {
-    u16x8 v;
-    const int ci = s >> 1, ky = 4 * (s & 1) + g;
+    if (w1_cl) {
+      wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&W1[r * w1.s0 + s * w1.s2 + 2 * g * 4]));
+    } else {
+      u16x8 v;
 #pragma unroll
-    for (int j = 0; j < 8; j++) v[j] = W1[r * w1.s0 + ci * w1.s1 + ky * w1.s2 + j * w1.s3];
-    wf1[s] = as_bf(v);
+      for (int j = 0; j < 8; j++) v[j] = W1[r * w1.s0 + (j & 3) * w1.s1 + s * w1.s2 + (2 * g + (j >> 2)) * w1.s3];
+      wf1[s] = as_bf(v);
+    }
   }
   const float bias1 = bf2f(b1[r]);
   __syncthreads();
@@ -128,61 +154,79 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
     const int p = min(mt * 16 + r, NP1 - 1);
     const int oy = p / H1, ox = p - oy * H1;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (!(dbg & 1)) {
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-      const int ci = s >> 1, ky = 4 * (s & 1) + g;
-      acc = mfma(frame8(frame, ci * P0 * P0 + (4 * oy + ky) * P0 + 4 * ox), wf1[s], acc);
+      for (int s = 0; s < 8; s++)
+        acc = mfma(frame8(frame, ((4 * oy + s) * P0 + 4 * ox + 2 * g) * 4), wf1[s], acc);
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int q = mt * 16 + 4 * g + i;
       if (q < NP1) {
         const float v = fmaxf(acc[i] * (1.0f / 255.0f) + bias1, 0.f);
-        const unsigned short hb = f2bf(v);
         const int y = q / H1, x = q - y * H1;
-        h1p[((y + 2) * P1 + (x + 2)) * C1 + r] = hb;
-        if (h1_out) h1_out[(b * NP1 + q) * C1 + r] = hb;
+        h1p[((y + 2) * P1 + (x + 2)) * C1 + r] = f2bf(v);
       }
     }
   }
   // conv2 weight fragments (two 16-wide N tiles): k = 32s + 8g + j → pixel pp = 2s + (g>>1)
   // (ky = pp>>2, kx = pp&3), ci = 8(g&1) + j
   bf16x8 wf2[2][8];
+  const bool w2_cl = (w2.s1 == 1);
 #pragma unroll
   for (int nt = 0; nt < 2; nt++)
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-      u16x8 v;
       const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3, co = nt * 16 + r;
+      if (w2_cl) {
+        wf2[nt][s] = as_bf(*reinterpret_cast<const u16x8*>(&W2[co * w2.s0 + ky * w2.s2 + kx * w2.s3 + 8 * (g & 1)]));
+      } else {
+        u16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = W2[co * w2.s0 + (8 * (g & 1) + j) * w2.s1 + ky * w2.s2 + kx * w2.s3];
-      wf2[nt][s] = as_bf(v);
+        for (int j = 0; j < 8; j++) v[j] = W2[co * w2.s0 + (8 * (g & 1) + j) * w2.s1 + ky * w2.s2 + kx * w2.s3];
+        wf2[nt][s] = as_bf(v);
+      }
     }
   const float bias2[2] = {bf2f(b2[r]), bf2f(b2[16 + r])};
   __syncthreads();
+  // h1 out for backward: coalesced 16-B rows from the LDS tile
+  if (h1_out) {
+    for (int v = threadIdx.x; v < NP1 * 2; v += 256) {
+      const int p = v >> 1, y = p / H1, x = p - y * H1;
+      *reinterpret_cast<uint4*>(&h1_out[(b * NP1 + p) * C1 + 8 * (v & 1)]) =
+          *reinterpret_cast<const uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1)]);
+    }
+  }
+  unsigned short* h2s = reinterpret_cast<unsigned short*>(frame);  // frame is dead after conv1
 
   // ---- conv2: 8 M-tiles (wave w: w, w+4) x 2 N-tiles
   for (int mt = wave; mt < NP2P / 16; mt += 4) {
     const int q = min(mt * 16 + r, NP2 - 1);
     const int oy = q / H2, ox = q - oy * H2;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    if (!(dbg & 2)) {
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-      const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
-      const u16x8 av = *reinterpret_cast<const u16x8*>(&h1p[((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1)]);
-      const bf16x8 a = as_bf(av);
-      acc0 = mfma(a, wf2[0][s], acc0);
-      acc1 = mfma(a, wf2[1][s], acc1);
+      for (int s = 0; s < 8; s++) {
+        const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
+        const u16x8 av =
+            *reinterpret_cast<const u16x8*>(&h1p[((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1)]);
+        const bf16x8 a = as_bf(av);
+        acc0 = mfma(a, wf2[0][s], acc0);
+        acc1 = mfma(a, wf2[1][s], acc1);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int qq = mt * 16 + 4 * g + i;
       if (qq < NP2) {
-        h2_out[(b * NP2 + qq) * C2 + r] = f2bf(fmaxf(acc0[i] + bias2[0], 0.f));
-        h2_out[(b * NP2 + qq) * C2 + 16 + r] = f2bf(fmaxf(acc1[i] + bias2[1], 0.f));
+        h2s[qq * C2 + r] = f2bf(fmaxf(acc0[i] + bias2[0], 0.f));
+        h2s[qq * C2 + 16 + r] = f2bf(fmaxf(acc1[i] + bias2[1], 0.f));
       }
     }
   }
+  __syncthreads();
+  for (int v = threadIdx.x; v < NP2 * C2 / 8; v += 256)
+    *reinterpret_cast<uint4*>(&h2_out[b * NP2 * C2 + 8 * v]) = *reinterpret_cast<const uint4*>(&h2s[8 * v]);
 }
 
 // ================================================================ backward
@@ -192,7 +236,8 @@ constexpr int PART = C1 * 256 + C2 * 256 + C1 + C2;  // per-workgroup fp32 parti
 __global__ __launch_bounds__(256) void k_trunk_bwd(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ h1,
-    const unsigned short* __restrict__ h2, const unsigned short* __restrict__ dh2, float* __restrict__ partial) {
+    const unsigned short* __restrict__ h2, const unsigned short* __restrict__ dh2, float* __restrict__ partial,
+    int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short dp2[NP2P * C2];    // [q][co2]
@@ -237,32 +282,56 @@ __global__ __launch_bounds__(256) void k_trunk_bwd(
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
     const int64_t src = idx ? idx[b] : b;
     // ---- P0: stage frame, h1, dpre2
-    load_frame(obs + src * (C0 * H0 * H0), frame);
-    for (int v = threadIdx.x; v < NP1 * 2; v += blockDim.x) {
-      const int p = v >> 1, half = v & 1;
-      const int y = p / H1, x = p - y * H1;
-      *reinterpret_cast<uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * half]) =
-          *reinterpret_cast<const uint4*>(&h1[(b * NP1 + p) * C1 + 8 * half]);
-    }
-    for (int v = threadIdx.x; v < NP2 * 4; v += blockDim.x) {
-      const int q = v >> 2, c0 = 8 * (v & 3);
-      const u16x8 hv = *reinterpret_cast<const u16x8*>(&h2[(b * NP2 + q) * C2 + c0]);
-      const u16x8 gv = *reinterpret_cast<const u16x8*>(&dh2[(b * NP2 + q) * C2 + c0]);
-      u16x8 o;
+    if (!(dbg & 8)) load_frame(obs + src * (C0 * H0 * H0), frame);
+    if (!(dbg & 8)) {  // h1 [441][16] → padded LDS tile; h2, dh2 → dpre2 (both layouts) + db2. Loads first.
+      constexpr int NH1 = NP1 * 2, PH1 = (NH1 + 255) / 256;  // 882 x 16 B
+      constexpr int NH2 = NP2 * 4, PH2 = (NH2 + 255) / 256;  // 484 x 16 B
+      uint4 hv1[PH1];
+      u16x8 hv2[PH2], gv2[PH2];
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const unsigned short d = (hv[j] != 0 && !(hv[j] & 0x8000)) ? gv[j] : static_cast<unsigned short>(0);
-        o[j] = d;
-        db2[j] += bf2f(d);
-        dp2t[(c0 + j) * NP2P + q] = d;
+      for (int k = 0; k < PH1; k++) {
+        const int v = threadIdx.x + 256 * k;
+        if (v < NH1) hv1[k] = *reinterpret_cast<const uint4*>(&h1[(b * NP1 + (v >> 1)) * C1 + 8 * (v & 1)]);
       }
-      *reinterpret_cast<u16x8*>(&dp2[q * C2 + c0]) = o;
+#pragma unroll
+      for (int k = 0; k < PH2; k++) {
+        const int v = threadIdx.x + 256 * k;
+        if (v < NH2) {
+          hv2[k] = *reinterpret_cast<const u16x8*>(&h2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
+          gv2[k] = *reinterpret_cast<const u16x8*>(&dh2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PH1; k++) {
+        const int v = threadIdx.x + 256 * k;
+        if (v < NH1) {
+          const int p = v >> 1, y = p / H1, x = p - y * H1;
+          *reinterpret_cast<uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1)]) = hv1[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PH2; k++) {
+        const int v = threadIdx.x + 256 * k;
+        if (v < NH2) {
+          const int q = v >> 2, c0 = 8 * (v & 3);
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const unsigned short hj = hv2[k][j];
+            const unsigned short d = (hj != 0 && !(hj & 0x8000)) ? gv2[k][j] : static_cast<unsigned short>(0);
+            o[j] = d;
+            db2[j] += bf2f(d);
+            dp2t[(c0 + j) * NP2P + q] = d;
+          }
+          *reinterpret_cast<u16x8*>(&dp2[q * C2 + c0]) = o;
+        }
+      }
     }
     __syncthreads();
 
     // ---- P1a: dW2[co2][k=(ky,kx,ci)] += Σ_q dpre2[q][co2] · h1p[2oy+ky][2ox+kx][ci]
 #pragma unroll
-    for (int s = 0; s < NP2P / 32; s++) {
+    for (int s = 0; s < ((dbg & 1) ? 0 : NP2P / 32); s++) {
       const bf16x8 a0 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[r * NP2P + 32 * s + 8 * g]));
       const bf16x8 a1 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[(16 + r) * NP2P + 32 * s + 8 * g]));
 #pragma unroll
@@ -282,7 +351,7 @@ __global__ __launch_bounds__(256) void k_trunk_bwd(
       }
     }
     // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 → dp1t, db1
-    for (int mt = 0; mt * 16 < ncls; mt++) {
+    for (int mt = 0; mt * 16 < ((dbg & 2) ? 0 : ncls); mt++) {
       const int m = mt * 16 + r;
       const int a = m / ncol, c = m - a * ncol;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -310,9 +379,9 @@ __global__ __launch_bounds__(256) void k_trunk_bwd(
     }
     __syncthreads();
 
-    // ---- P2: dW1[co][k=(ci,ky,kx)] += Σ_p dpre1[p][co] · frame[ci][4oy+ky][4ox+kx] / 255
+    // ---- P2: dW1[co][k=(ky,kx,ci)] += Σ_p dpre1[p][co] · frame[4oy+ky][4ox+kx][ci] / 255
 #pragma unroll 2
-    for (int s = 0; s < NP1P / 32; s++) {
+    for (int s = 0; s < ((dbg & 4) ? 0 : NP1P / 32); s++) {
       const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(&dp1t[r * NP1P + 32 * s + 8 * g]));
       int pys[8], pxs[8];
 #pragma unroll
@@ -324,11 +393,11 @@ __global__ __launch_bounds__(256) void k_trunk_bwd(
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int k = (wave + 4 * i) * 16 + r;
-        const int ci = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
-        const uint8_t* base = frame + ci * P0 * P0 + ky * P0 + kx;
+        const int ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
+        const uint8_t* base = frame + (ky * P0 + kx) * 4 + ci;
         u16x8 bv;
 #pragma unroll
-        for (int j = 0; j < 8; j++) bv[j] = u8bf(base[4 * pys[j] * P0 + 4 * pxs[j]]);
+        for (int j = 0; j < 8; j++) bv[j] = u8bf(base[(4 * pys[j] * P0 + 4 * pxs[j]) * 4]);
         aw1[i] = mfma(a, as_bf(bv), aw1[i]);
       }
     }
@@ -379,18 +448,38 @@ __global__ __launch_bounds__(256) void k_trunk_bwd(
 }
 
 // Sum the G partials in a fixed order and write bf16 grads in each parameter's memory order.
-__global__ __launch_bounds__(256) void k_trunk_reduce(const float* __restrict__ partial, int G,
+// Workgroup = 64 consecutive outputs x 8 slices of G (coalesced 256-B rows, 8 loads in flight per
+// lane), slices combined in LDS in a fixed order → deterministic.
+constexpr int RED_SLICES = 8;
+__global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ partial, int G,
                                                       unsigned short* __restrict__ dW1, WStrides w1,
                                                       unsigned short* __restrict__ db1,
                                                       unsigned short* __restrict__ dW2, WStrides w2,
                                                       unsigned short* __restrict__ db2) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= PART) return;
+  __shared__ float red[RED_SLICES][64];
+  const int c = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int gi = 0; gi < G; gi++) s += partial[int64_t(gi) * PART + e];
-  const unsigned short v = f2bf(s);
-  if (e < C1 * 256) {  // k = (ci, ky, kx)
-    const int co = e >> 8, k = e & 255, ci = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+  if (e < PART) {
+    int gi = slice;
+    for (; gi + 3 * RED_SLICES < G; gi += 4 * RED_SLICES) {
+      const float a0 = partial[int64_t(gi) * PART + e];
+      const float a1 = partial[int64_t(gi + RED_SLICES) * PART + e];
+      const float a2 = partial[int64_t(gi + 2 * RED_SLICES) * PART + e];
+      const float a3 = partial[int64_t(gi + 3 * RED_SLICES) * PART + e];
+      s += (a0 + a1) + (a2 + a3);
+    }
+    for (; gi < G; gi += RED_SLICES) s += partial[int64_t(gi) * PART + e];
+  }
+  red[slice][c] = s;
+  __syncthreads();
+  if (slice != 0 || e >= PART) return;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
+  const unsigned short v = f2bf(t);
+  if (e < C1 * 256) {  // k = (ky, kx, ci)
+    const int co = e >> 8, k = e & 255, ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
     dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3] = v;
   } else if (e < C1 * 256 + C2 * 256) {  // k = (ky, kx, ci)
     const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
@@ -408,13 +497,13 @@ static trunk::WStrides ws(const int64_t* s) { return trunk::WStrides{s[0], s[1],
 
 void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
-                      const void* b2, void* h1, void* h2, hipStream_t stream) {
+                      const void* b2, void* h1, void* h2, hipStream_t stream, int dbg) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
   hipLaunchKernelGGL(trunk::k_trunk_fwd, dim3(uint32_t(B)), dim3(256), 0, stream, obs, idx, ctr, period, B,
                      static_cast<const unsigned short*>(W1), ws(w1s), static_cast<const unsigned short*>(b1),
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(b2),
-                     static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2));
+                     static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2), dbg);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -424,15 +513,16 @@ int64_t nature_trunk_partial_floats(int64_t B) { return int64_t(nature_trunk_bwd
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream) {
+                      hipStream_t stream, int dbg) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
   const int G = nature_trunk_bwd_groups(B);
   hipLaunchKernelGGL(trunk::k_trunk_bwd, dim3(uint32_t(G)), dim3(256), 0, stream, obs, idx, ctr, period, B,
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(h1),
-                     static_cast<const unsigned short*>(h2), static_cast<const unsigned short*>(dh2), partial);
+                     static_cast<const unsigned short*>(h2), static_cast<const unsigned short*>(dh2), partial, dbg);
   RMM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3((trunk::PART + 255) / 256), dim3(256), 0, stream, partial, G,
+  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3((trunk::PART + 63) / 64), dim3(64 * trunk::RED_SLICES), 0, stream,
+                     partial, G,
                      static_cast<unsigned short*>(dW1), ws(w1s), static_cast<unsigned short*>(db1),
                      static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2));
   RMM_HIP_CHECK(hipGetLastError());

@@ -228,24 +228,28 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("nature_trunk_fwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W1,
                                std::vector<int64_t> w1s, uint64_t b1, uint64_t W2, std::vector<int64_t> w2s,
-                               uint64_t b2, uint64_t h1, uint64_t h2, uint64_t stream) {
+                               uint64_t b2, uint64_t h1, uint64_t h2, uint64_t stream, int dbg) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("nature_trunk_fwd: 4 strides per weight");
     nature_trunk_fwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr,
                      ctr ? P<const int64_t>(ctr) : nullptr, period, B, P<const void>(W1), w1s.data(),
                      P<const void>(b1), P<const void>(W2), w2s.data(), P<const void>(b2), h1 ? P<void>(h1) : nullptr,
-                     P<void>(h2), S(stream));
-  });
+                     P<void>(h2), S(stream), dbg);
+  }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W1"), py::arg("w1s"),
+     py::arg("b1"), py::arg("W2"), py::arg("w2s"), py::arg("b2"), py::arg("h1"), py::arg("h2"), py::arg("stream"),
+     py::arg("dbg") = 0);
   m.def("nature_trunk_partial_floats", &nature_trunk_partial_floats);
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,
                                uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
-                               uint64_t stream) {
+                               uint64_t stream, int dbg) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("nature_trunk_bwd: 4 strides per weight");
     nature_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr,
                      ctr ? P<const int64_t>(ctr) : nullptr, period, B, P<const void>(W2), w2s.data(),
                      P<const void>(h1), P<const void>(h2), P<const void>(dh2), P<float>(partial), P<void>(dW1),
-                     w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream));
-  });
+                     w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream), dbg);
+  }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W2"), py::arg("w2s"),
+     py::arg("h1"), py::arg("h2"), py::arg("dh2"), py::arg("partial"), py::arg("dW1"), py::arg("w1s"), py::arg("db1"),
+     py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0);
 
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {

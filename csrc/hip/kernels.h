@@ -93,13 +93,15 @@ void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, 
 // memory order) through `partial` (nature_trunk_partial_floats(B) fp32).
 void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
-                      const void* b2, void* h1, void* h2, hipStream_t stream);
+                      const void* b2, void* h1, void* h2, hipStream_t stream, int dbg = 0);
 int nature_trunk_bwd_groups(int64_t B);
 int64_t nature_trunk_partial_floats(int64_t B);
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream);
+                      hipStream_t stream, int dbg = 0);
+// dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
+// load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 skip the staging loads.
 
 }  // namespace hip
 }  // namespace rmm
