@@ -220,6 +220,11 @@ PYBIND11_MODULE(_hip, m) {
     bias_relu_fwd(P<void>(y), P<const void>(bias), M, C, relu, S(stream));
   });
   m.def("bias_relu_bwd_partials", &bias_relu_bwd_partials);
+  m.def("mask_colsum", [](uint64_t dy, uint64_t y, uint64_t dpre, uint64_t db, int64_t M, int C, bool relu,
+                          uint64_t stream) {
+    mask_colsum(P<const void>(dy), y ? P<const void>(y) : nullptr, dpre ? P<void>(dpre) : nullptr, P<void>(db), M, C,
+                relu, S(stream));
+  });
   m.def("bias_relu_bwd", [](uint64_t dy, uint64_t y, uint64_t dpre, uint64_t db, uint64_t partial, int64_t M, int C,
                             bool relu, uint64_t stream) {
     bias_relu_bwd(P<const void>(dy), P<const void>(y), P<void>(dpre), P<void>(db), P<float>(partial), M, C, relu,

@@ -86,6 +86,11 @@ int64_t bias_relu_bwd_partials(int64_t M);
 void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, float* partial, int64_t M, int C,
                    bool relu, hipStream_t stream);
 
+// K8b: dpre = dy*[y>0] (relu) or dy, and bf16 column sums db, one launch (dense layers, small M).
+// dpre may be null (bias grad only). y is read only when relu.
+void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M, int C, bool relu,
+                 hipStream_t stream);
+
 // K10: fused Nature-CNN trunk (conv 8x8/4 4->16 + conv 4x4/2 16->32, bias+ReLU) on MFMA, one
 // workgroup per frame in LDS. Frames u8 [.,4,84,84] gathered by idx (device-counter window like
 // gather_rows); weights bf16 with element strides w*s = [co, ci, ky, kx]. h1 [B,441,16] (may be

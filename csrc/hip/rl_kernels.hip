@@ -600,5 +600,75 @@ void bias_relu_bwd(const void* dy, const void* y, void* dpre, void* dbias_bf16, 
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+// K8b: dense-layer epilogue backward for small M (a PPO minibatch): dpre = dy * [y > 0] (or dy)
+// and db = column sums, ONE launch, deterministic. Workgroup = V adjacent columns x all rows
+// (256 threads stride the rows, fixed-order LDS tree for the sum).
+template <int V>
+__global__ __launch_bounds__(256) void k_mask_colsum(const unsigned short* __restrict__ dy,
+                                                     const unsigned short* __restrict__ y,
+                                                     unsigned short* __restrict__ dpre,
+                                                     unsigned short* __restrict__ db, int64_t M, int C, int relu) {
+  __shared__ float red[V][256];
+  const int col0 = blockIdx.x * V;
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; v++) acc[v] = 0.f;
+  for (int64_t m = threadIdx.x; m < M; m += 256) {
+    unsigned short g[V], h[V];
+    if constexpr (V == 8) {
+      *reinterpret_cast<uint4*>(g) = *reinterpret_cast<const uint4*>(&dy[m * C + col0]);
+      if (relu) *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(&y[m * C + col0]);
+    } else {
+#pragma unroll
+      for (int v = 0; v < V; v++) {
+        g[v] = dy[m * C + col0 + v];
+        h[v] = relu ? y[m * C + col0 + v] : static_cast<unsigned short>(0);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      if (relu && (h[v] == 0 || (h[v] & 0x8000))) g[v] = 0;
+      acc[v] += __uint_as_float(uint32_t(g[v]) << 16);
+    }
+    if (dpre) {
+      if constexpr (V == 8) {
+        *reinterpret_cast<uint4*>(&dpre[m * C + col0]) = *reinterpret_cast<const uint4*>(g);
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; v++) dpre[m * C + col0 + v] = g[v];
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; v++) red[v][threadIdx.x] = acc[v];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+#pragma unroll
+      for (int v = 0; v < V; v++) red[v][threadIdx.x] += red[v][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < V) {
+    uint32_t u = __float_as_uint(red[threadIdx.x][0]);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    db[col0 + threadIdx.x] = static_cast<unsigned short>(u >> 16);
+  }
+}
+
+void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M, int C, bool relu,
+                 hipStream_t stream) {
+  if (M <= 0 || C <= 0) return;
+  auto* g = static_cast<const unsigned short*>(dy);
+  auto* h = static_cast<const unsigned short*>(y);
+  auto* d = static_cast<unsigned short*>(dpre);
+  auto* b = static_cast<unsigned short*>(db);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(k_mask_colsum<8>, dim3(uint32_t(C / 8)), dim3(256), 0, stream, g, h, d, b, M, C, relu ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_mask_colsum<1>, dim3(uint32_t(C)), dim3(256), 0, stream, g, h, d, b, M, C, relu ? 1 : 0);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace hip
 }  // namespace rmm

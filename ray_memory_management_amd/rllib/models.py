@@ -71,6 +71,7 @@ class _NatureTrunkFn(torch.autograd.Function):
         if train:
             ctx.save_for_backward(obs, idx, ctr, w1, w2, h1, h2)
             ctx.conf = (int(period), int(rows))
+            ctx.gout = tuple(_grad_out(t) for t in (w1, b1, w2, b2))
         return h2
 
     @staticmethod
@@ -83,16 +84,71 @@ class _NatureTrunkFn(torch.autograd.Function):
         dh2 = dh2.contiguous()
         dev = obs.device
         part = torch.empty(h.nature_trunk_partial_floats(rows), dtype=torch.float32, device=dev)
-        dw1 = torch.empty_strided(w1.size(), w1.stride(), dtype=w1.dtype, device=dev)
-        dw2 = torch.empty_strided(w2.size(), w2.stride(), dtype=w2.dtype, device=dev)
-        db1 = torch.empty(16, dtype=w1.dtype, device=dev)
-        db2 = torch.empty(32, dtype=w2.dtype, device=dev)
+        g1, gb1, g2, gb2 = ctx.gout
+        dw1 = g1 if g1 is not None else torch.empty_strided(w1.size(), w1.stride(), dtype=w1.dtype, device=dev)
+        dw2 = g2 if g2 is not None else torch.empty_strided(w2.size(), w2.stride(), dtype=w2.dtype, device=dev)
+        db1 = gb1 if gb1 is not None else torch.empty(16, dtype=w1.dtype, device=dev)
+        db2 = gb2 if gb2 is not None else torch.empty(32, dtype=w2.dtype, device=dev)
+        assert dw1.stride() == w1.stride() and dw2.stride() == w2.stride()
         h.nature_trunk_bwd(obs.data_ptr(), idx.data_ptr() if idx is not None else 0,
                            ctr.data_ptr() if ctr is not None else 0, period, rows, w2.data_ptr(), list(w2.stride()),
                            h1.data_ptr(), h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(),
                            list(w1.stride()), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(),
                            torch.cuda.current_stream(dev).cuda_stream)
         return None, None, None, None, None, dw1, db1, dw2, db2
+
+
+def _grad_out(p):
+    """Optional preallocated gradient buffer of a parameter (e.g. its view into the PPO learner's
+    flat gradient bucket): backward kernels write the gradient there directly, no copy."""
+    return getattr(p, "_rmm_grad_out", None)
+
+
+class _DenseFn(torch.autograd.Function):
+    """y = act(x Wᵀ + b) for the PPO dense layers on the bf16 GPU path. Forward: one hipBLASLt GEMM
+    with the bias(+ReLU) epilogue. Backward: K8b mask + bias column-sum in one launch, dW GEMM
+    written straight into the parameter's gradient buffer when it has one, dX GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        y = torch._addmm_activation(b, x, w.t()) if relu else torch.addmm(b, x, w.t())
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.relu = relu
+        ctx.gout = (_grad_out(w), _grad_out(b))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        x, w, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        M, C = dy.shape
+        gw, gb = ctx.gout
+        db = gb if gb is not None else torch.empty(C, dtype=dy.dtype, device=dy.device)
+        stream = torch.cuda.current_stream(dy.device).cuda_stream
+        if ctx.relu:
+            dpre = torch.empty_like(dy)
+            h.mask_colsum(dy.data_ptr(), y.data_ptr(), dpre.data_ptr(), db.data_ptr(), M, C, True, stream)
+        else:
+            dpre = dy
+            h.mask_colsum(dy.data_ptr(), 0, 0, db.data_ptr(), M, C, False, stream)
+        if gw is not None:
+            torch.mm(dpre.t(), x, out=gw)
+            dw = gw
+        else:
+            dw = dpre.t() @ x
+        dx = dpre @ w if ctx.needs_input_grad[0] else None
+        return dx, dw, db, None
+
+
+def dense(x, layer: nn.Linear, relu: bool):
+    if (x.is_cuda and x.dtype == torch.bfloat16 and layer.weight.dtype == torch.bfloat16 and x.dim() == 2
+            and layer.bias is not None):
+        return _DenseFn.apply(x.contiguous(), layer.weight, layer.bias, relu)
+    y = layer(x)
+    return torch.relu(y) if relu else y
 
 
 def nature_trunk(obs, w1, b1, w2, b2, idx=None, ctr=None, period: int = 1, rows: int = None):
@@ -242,7 +298,7 @@ class VisionNetwork(nn.Module):
         convs in the fused K10 kernel."""
         c1, c2 = self.convs[0], self.convs[1]
         h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
-        return self.heads(torch.relu(self.dense_tail(h)))
+        return dense(dense(h, self.dense_tail, True), self.heads, False)
 
     def _trunk(self, x):
         h = self.convs(x)

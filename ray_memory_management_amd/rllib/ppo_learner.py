@@ -200,6 +200,12 @@ class PPOLearner:
         self.m1 = torch.zeros(n, dtype=torch.float32, device=dev)
         self.m2 = torch.zeros(n, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        # each param's slice of the flat bucket: fused backward kernels (K10 trunk, K8b dense) write
+        # their gradients there directly and the bucket copy skips them
+        off = 0
+        for p in self.params:
+            p._rmm_grad_out = self.flat_grad.as_strided(p.size(), p.stride(), off)
+            off += p.numel()
         b1, b2 = self.cfg["adam_betas"]
         self.hp = torch.tensor([self.cfg["lr"], b1, b2, self.cfg["adam_eps"], self.cfg["weight_decay"], 0.0],
                                dtype=torch.float32, device=dev)
@@ -260,9 +266,12 @@ class PPOLearner:
         off = 0
         for g, p in zip(grads, self.params):
             nb = g.numel() * 2
-            segs.append((g.data_ptr(), self.flat_grad.data_ptr() + off * 2, nb))
+            dst = self.flat_grad.data_ptr() + off * 2
+            if g.data_ptr() != dst:  # fused backward kernels already wrote into the bucket
+                segs.append((g.data_ptr(), dst, nb))
             off += p.numel()
-        h.multi_copy(segs, _stream())                        # K1: grads → one flat bucket
+        if segs:
+            h.multi_copy(segs, _stream())                    # K1: remaining grads → one flat bucket
         if with_opt:  # otherwise the caller runs _opt_step (all-reduce + Adam + counters) eagerly
             self._opt_step()
 
