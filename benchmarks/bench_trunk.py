@@ -25,6 +25,14 @@ def timeit(fn, iters=200):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="'bwd' or 'fwd': time one kernel config (for PMC runs)")
+    ap.add_argument("--B", type=int, default=500)
+    ap.add_argument("--dbg", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
     h = require_hip()
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -34,6 +42,27 @@ def main():
     b1 = torch.zeros(16, dtype=torch.bfloat16, device=dev)
     b2 = torch.zeros(32, dtype=torch.bfloat16, device=dev)
     out = {}
+    if a.only:
+        B = a.B
+        idx = torch.randperm(5000, device=dev)[:B].contiguous()
+        h1 = torch.zeros(B, 441, 16, dtype=torch.bfloat16, device=dev)
+        h2 = torch.zeros(B, 3872, dtype=torch.bfloat16, device=dev)
+        if a.only == "fwd":
+            t = timeit(lambda: h.nature_trunk_fwd(
+                obs.data_ptr(), idx.data_ptr(), 0, 1, B, w1.data_ptr(), list(w1.stride()), b1.data_ptr(),
+                w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), st, dbg=a.dbg), a.iters)
+        else:
+            dh2 = torch.randn(B, 3872, device=dev).to(torch.bfloat16)
+            part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
+            dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
+            db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
+            t = timeit(lambda: h.nature_trunk_bwd(
+                obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
+                h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
+                dw2.data_ptr(), db2.data_ptr(), st, dbg=a.dbg), a.iters)
+        print(json.dumps({f"{a.only}_B{B}_dbg{a.dbg}": round(t, 1),
+                          "cus": torch.cuda.get_device_properties(0).multi_processor_count}))
+        return
     for B in (500, 50):
         idx = torch.randperm(5000, device=dev)[:B].contiguous()
         h1 = torch.empty(B, 441, 16, dtype=torch.bfloat16, device=dev)
@@ -47,11 +76,25 @@ def main():
             part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
             dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
             db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
-            for dbg in (0, 1, 2, 4, 7, 8, 15):
+            for dbg in (0, 1, 2, 4, 7, 8, 15, 31):
                 out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                     obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                     h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
                     dw2.data_ptr(), db2.data_ptr(), st, dbg=dbg)), 1)
+    # latency vs throughput: backward at growing B (G = min(B, 256) workgroups)
+    for B in (1, 16, 64, 256):
+        idx = torch.randperm(5000, device=dev)[:B].contiguous()
+        h1 = torch.zeros(B, 441, 16, dtype=torch.bfloat16, device=dev)
+        h2 = torch.zeros(B, 3872, dtype=torch.bfloat16, device=dev)
+        dh2 = torch.randn(B, 3872, device=dev).to(torch.bfloat16)
+        part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
+        dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
+        db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
+        for dbg in (0, 15, 31):
+            out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
+                obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
+                h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
+                dw2.data_ptr(), db2.data_ptr(), st, dbg=dbg)), 1)
     print(json.dumps(out))
 
 

@@ -56,6 +56,8 @@ __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+struct WStrides { int64_t s0, s1, s2, s3; };  // [co][ci][ky][kx] element strides
+
 __device__ __forceinline__ const int64_t* window(const int64_t* idx, const int64_t* ctr, int64_t period, int64_t rows) {
   return (ctr && idx) ? idx + (ctr[0] % period) * rows : idx;
 }
@@ -95,6 +97,62 @@ __device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint
   }
 }
 
+// Backward variant: the same transpose, stored as bf16 (exact for 0..255) so the weight-grad
+// gathers need no per-use conversion: pixel (y, x) channel c at element ((y+2)*88 + x+2)*4 + c.
+template <int NT>
+__device__ __forceinline__ void load_frame_bf16(const uint8_t* __restrict__ src, unsigned short* frame) {
+  constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+  uint32_t v[PER][C0];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + NT * k;
+    if (o < NW) {
+#pragma unroll
+      for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + NT * k;
+    if (o < NW) {
+      const int y = o / 21, x = 4 * (o - y * 21);
+      uint32_t w[8];  // 4 pixels x 4 channels of bf16, two per word
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        w[2 * q] = uint32_t(u8bf((v[k][0] >> (8 * q)) & 0xffu)) | (uint32_t(u8bf((v[k][1] >> (8 * q)) & 0xffu)) << 16);
+        w[2 * q + 1] = uint32_t(u8bf((v[k][2] >> (8 * q)) & 0xffu)) | (uint32_t(u8bf((v[k][3] >> (8 * q)) & 0xffu)) << 16);
+      }
+      uint4* d = reinterpret_cast<uint4*>(frame + ((y + 2) * P0 + x + 2) * 4);  // 16-B aligned
+      d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+  }
+}
+
+// Stage a conv weight into LDS as canonical [co][ky][kx][ci] rows of `pitch` elements (row = co).
+// Every workgroup needs the whole (tiny) weight: per-lane fragment loads straight from global make
+// all workgroups hammer the same few L2 lines (measured: skeleton cost grew 7→20-30 µs from 1 to
+// 256 workgroups). Here each element is read once per workgroup, 16 B at a time when the weight
+// is channels-last contiguous ([co][ky][kx][ci] in memory).
+template <int NT, int CO, int CI, int KH>
+__device__ __forceinline__ void stage_weight(const unsigned short* __restrict__ W, WStrides ws_, unsigned short* dst,
+                                             int pitch) {
+  constexpr int ROW = KH * KH * CI;  // elements per output channel
+  if (ws_.s1 == 1 && ws_.s3 == CI && ws_.s2 == KH * CI && ws_.s0 == ROW) {
+    for (int v = threadIdx.x; v < CO * ROW / 8; v += NT) {
+      const int co = (8 * v) / ROW, e = 8 * v - co * ROW;
+      *reinterpret_cast<uint4*>(&dst[co * pitch + e]) = *reinterpret_cast<const uint4*>(&W[8 * v]);
+    }
+  } else {
+    for (int v = threadIdx.x; v < CO * ROW; v += NT) {
+      const int co = v / ROW, e = v - co * ROW, ky = e / (KH * CI), kx = (e / CI) % KH, ci = e % CI;
+      dst[co * pitch + e] = W[co * ws_.s0 + ci * ws_.s1 + ky * ws_.s2 + kx * ws_.s3];
+    }
+  }
+}
+constexpr int W1_PITCH = 256 + 8, W2_PITCH = 256 + 8;  // +16 B: 16 lanes x 16-B reads hit distinct banks
+
 __device__ __forceinline__ void zero_lds(void* p, int bytes) {
   uint4* q = reinterpret_cast<uint4*>(p);
   for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) q[i] = make_uint4(0, 0, 0, 0);
@@ -110,7 +168,12 @@ __device__ __forceinline__ bf16x8 frame8(const uint8_t* frame, int off) {
   return as_bf(v);
 }
 
-struct WStrides { int64_t s0, s1, s2, s3; };  // [co][ci][ky][kx] element strides
+
+// Weight-grad GEMMs reduce over positions (MFMA K). Lane group g's 8 K values are taken as
+// positions 32s + g + 4j (j = 0..7) so the four lane groups gather NEIGHBOURING pixels (distinct
+// LDS banks; with 8g + j they sit 8 positions apart, on the same bank: 4-way conflicts). The
+// transposed dpre tiles are stored in that permuted order so the A operand stays one 16-B read.
+__device__ __forceinline__ int kperm(int p) { return (p & ~31) + 8 * (p & 3) + ((p & 31) >> 2); }
 
 // ================================================================ forward
 // grid = B workgroups (one frame each), 256 threads = 4 waves.
@@ -121,6 +184,8 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
     unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short w1s[C1 * W1_PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short w2s[C2 * W2_PITCH];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int64_t b = blockIdx.x;
@@ -129,24 +194,16 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
 
   zero_lds(frame, FRAME_BYTES);
   zero_lds(h1p, H1P_ELEMS * 2);
+  stage_weight<256, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
+  stage_weight<256, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   __syncthreads();
   if (!(dbg & 4)) load_frame<256>(obs + src * (C0 * H0 * H0), frame);
 
   // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
-  // j → (kx = 2g + (j>>2), ci = j&3); col = co = r. Channels-last weights: one 16-B load.
+  // j → (kx = 2g + (j>>2), ci = j&3); col = co = r: one 16-B LDS read each.
   bf16x8 wf1[8];
-  const bool w1_cl = (w1.s1 == 1 && w1.s3 == 4);
 #pragma unroll
-  for (int s = 0; s < 8; s++) {
-    if (w1_cl) {
-      wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&W1[r * w1.s0 + s * w1.s2 + 2 * g * 4]));
-    } else {
-      u16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = W1[r * w1.s0 + (j & 3) * w1.s1 + s * w1.s2 + (2 * g + (j >> 2)) * w1.s3];
-      wf1[s] = as_bf(v);
-    }
-  }
+  for (int s = 0; s < 8; s++) wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&w1s[r * W1_PITCH + (s * 8 + 2 * g) * 4]));
   const float bias1 = bf2f(b1[r]);
   __syncthreads();
 
@@ -173,20 +230,12 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
   // conv2 weight fragments (two 16-wide N tiles): k = 32s + 8g + j → pixel pp = 2s + (g>>1)
   // (ky = pp>>2, kx = pp&3), ci = 8(g&1) + j
   bf16x8 wf2[2][8];
-  const bool w2_cl = (w2.s1 == 1);
 #pragma unroll
   for (int nt = 0; nt < 2; nt++)
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-      const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3, co = nt * 16 + r;
-      if (w2_cl) {
-        wf2[nt][s] = as_bf(*reinterpret_cast<const u16x8*>(&W2[co * w2.s0 + ky * w2.s2 + kx * w2.s3 + 8 * (g & 1)]));
-      } else {
-        u16x8 v;
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = W2[co * w2.s0 + (8 * (g & 1) + j) * w2.s1 + ky * w2.s2 + kx * w2.s3];
-        wf2[nt][s] = as_bf(v);
-      }
+    for (int s = 0; s < 8; s++) {  // pixel pp = (ky, kx) → canonical offset pp*16 + ci
+      const int pp = 2 * s + (g >> 1), co = nt * 16 + r;
+      wf2[nt][s] = as_bf(*reinterpret_cast<const u16x8*>(&w2s[co * W2_PITCH + pp * 16 + 8 * (g & 1)]));
     }
   const float bias2[2] = {bf2f(b2[r]), bf2f(b2[16 + r])};
   __syncthreads();
@@ -232,6 +281,9 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
 
 // ================================================================ backward
 constexpr int PART = C1 * 256 + C2 * 256 + C1 + C2;  // per-workgroup fp32 partial: dW1, dW2, db1, db2
+// row pitches of the transposed dpre tiles: +8 elements so the 16 rows written by one lane
+// group land 4 dwords apart (2-way instead of 16-way bank conflicts) while keeping 16-B reads
+constexpr int DP2_PITCH = NP2P + 8, DP1_PITCH = NP1P + 8;
 
 // grid = G workgroups of 8 waves (2 per SIMD hide the LDS/MFMA latency chains of one frame),
 // each loops over frames b = blockIdx.x, +G, ...
@@ -241,21 +293,24 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     int64_t B, const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ h1,
     const unsigned short* __restrict__ h2, const unsigned short* __restrict__ dh2, float* __restrict__ partial,
     int dbg) {
-  __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned short frame[FRAME_BYTES];  // bf16 HWC
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short dp2[NP2P * C2];    // [q][co2]
-  __shared__ __attribute__((aligned(16))) unsigned short dp2t[C2 * NP2P];   // [co2][q]
-  __shared__ __attribute__((aligned(16))) unsigned short dp1t[C1 * NP1P];   // [ci][p]
+  __shared__ __attribute__((aligned(16))) unsigned short dp2t[C2 * DP2_PITCH];   // [co2][kperm(q)]
+  __shared__ __attribute__((aligned(16))) unsigned short dp1t[C1 * DP1_PITCH];   // [ci][kperm(p)]
   __shared__ float red[8 * 64];
+  __shared__ __attribute__((aligned(16))) unsigned short w2s[C2 * W2_PITCH];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int64_t* idx = window(idx0, ctr, period, B);
+  if (dbg & 64) return;
 
-  zero_lds(frame, FRAME_BYTES);
+  if (!(dbg & 32)) zero_lds(frame, FRAME_BYTES * 2);
+  stage_weight<NTB, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   zero_lds(h1p, H1P_ELEMS * 2);
   zero_lds(dp2, NP2P * C2 * 2);
-  zero_lds(dp2t, C2 * NP2P * 2);
-  zero_lds(dp1t, C1 * NP1P * 2);
+  zero_lds(dp2t, C2 * DP2_PITCH * 2);
+  zero_lds(dp1t, C1 * DP1_PITCH * 2);
 
   // dh1 = conv2ᵀ(dpre2): waves 2c, 2c+1 own stride-parity class c = (py, px). In a class,
   // input pixel (y, x) = (2a+py, 2c+px) receives taps ky ∈ {py, py+2}, kx ∈ {px, px+2} from
@@ -263,13 +318,14 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   const int cls = wave >> 1, half = wave & 1;
   const int py = cls >> 1, px = cls & 1;
   const int nrow = py ? 10 : 11, ncol = px ? 10 : 11, ncls = nrow * ncol;
+  __syncthreads();  // w2s staged
   bf16x8 wt[4];
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
     u16x8 v;
 #pragma unroll
-    for (int j = 0; j < 8; j++) v[j] = W2[(8 * g + j) * w2.s0 + r * w2.s1 + ky * w2.s2 + kx * w2.s3];
+    for (int j = 0; j < 8; j++) v[j] = w2s[(8 * g + j) * W2_PITCH + (ky * 4 + kx) * 16 + r];
     wt[t] = as_bf(v);
   }
   f32x4 aw2[2][2], aw1[2];  // dW2 tiles (mt 0/1 x nt w+8i), dW1 tiles (nt w+8i)
@@ -286,7 +342,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
     const int64_t src = idx ? idx[b] : b;
     // ---- P0: stage frame, h1, dpre2
-    if (!(dbg & 8)) load_frame<NTB>(obs + src * (C0 * H0 * H0), frame);
+    if (!(dbg & 8)) load_frame_bf16<NTB>(obs + src * (C0 * H0 * H0), frame);
     if (!(dbg & 8)) {  // h1 [441][16] → padded LDS tile; h2, dh2 → dpre2 (both layouts) + db2. Loads first.
       constexpr int NH1 = NP1 * 2, PH1 = (NH1 + NTB - 1) / NTB;  // 882 x 16 B
       constexpr int NH2 = NP2 * 4, PH2 = (NH2 + NTB - 1) / NTB;  // 484 x 16 B
@@ -325,7 +381,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
             const unsigned short d = (hj != 0 && !(hj & 0x8000)) ? gv2[k][j] : static_cast<unsigned short>(0);
             o[j] = d;
             db2[j] += bf2f(d);
-            dp2t[(c0 + j) * NP2P + q] = d;
+            dp2t[(c0 + j) * DP2_PITCH + kperm(q)] = d;
           }
           *reinterpret_cast<u16x8*>(&dp2[q * C2 + c0]) = o;
         }
@@ -336,19 +392,27 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     // ---- P1a: dW2[co2][k=(ky,kx,ci)] += Σ_q dpre2[q][co2] · h1p[2oy+ky][2ox+kx][ci]
 #pragma unroll
     for (int s = 0; s < ((dbg & 1) ? 0 : NP2P / 32); s++) {
-      const bf16x8 a0 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[r * NP2P + 32 * s + 8 * g]));
-      const bf16x8 a1 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[(16 + r) * NP2P + 32 * s + 8 * g]));
+      const bf16x8 a0 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[r * DP2_PITCH + 32 * s + 8 * g]));
+      const bf16x8 a1 = as_bf(*reinterpret_cast<const u16x8*>(&dp2t[(16 + r) * DP2_PITCH + 32 * s + 8 * g]));
+      int qoff[8];  // positions q = 32s + g + 4j → element offset of (2oy, 2ox) in h1p
+      {
+        const int q0 = 32 * s + g;
+        int oy = q0 / H2, ox = q0 - oy * H2;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          qoff[j] = (q0 + 4 * j < NP2) ? (oy * 2 * P1 + ox * 2) * C1 : 0;  // dpre2 is 0 there
+          ox += 4;
+          if (ox >= H2) { ox -= H2; oy++; }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 2; i++) {
         const int k = (wave + 8 * i) * 16 + r;
         const int ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+        const unsigned short* base = h1p + (ky * P1 + kx) * C1 + ci;
         u16x8 bv;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int q = min(32 * s + 8 * g + j, NP2 - 1);
-          const int oy = q / H2, ox = q - oy * H2;
-          bv[j] = h1p[((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + ci];
-        }
+        for (int j = 0; j < 8; j++) bv[j] = base[qoff[j]];
         const bf16x8 bb = as_bf(bv);
         aw2[0][i] = mfma(a0, bb, aw2[0][i]);
         aw2[1][i] = mfma(a1, bb, aw2[1][i]);
@@ -377,7 +441,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
           const float d = (hv != 0 && !(hv & 0x8000)) ? acc[i] : 0.f;
           const unsigned short db = f2bf(d);
           db1 += bf2f(db);
-          dp1t[r * NP1P + y * H1 + x] = db;
+          dp1t[r * DP1_PITCH + kperm(y * H1 + x)] = db;
         }
       }
     }
@@ -386,22 +450,26 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     // ---- P2: dW1[co][k=(ky,kx,ci)] += Σ_p dpre1[p][co] · frame[4oy+ky][4ox+kx][ci] / 255
 #pragma unroll 2
     for (int s = 0; s < ((dbg & 4) ? 0 : NP1P / 32); s++) {
-      const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(&dp1t[r * NP1P + 32 * s + 8 * g]));
-      int pys[8], pxs[8];
+      const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(&dp1t[r * DP1_PITCH + 32 * s + 8 * g]));
+      int poff[8];  // positions p = 32s + g + 4j → byte offset of (4oy, 4ox) in the HWC frame
+      {
+        const int p0 = 32 * s + g;
+        int oy = p0 / H1, ox = p0 - oy * H1;
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int p = min(32 * s + 8 * g + j, NP1 - 1);
-        pys[j] = p / H1;
-        pxs[j] = p - pys[j] * H1;
+        for (int j = 0; j < 8; j++) {
+          poff[j] = (p0 + 4 * j < NP1) ? (oy * 4 * P0 + ox * 4) * 4 : 0;  // elements; dpre1 is 0 there
+          ox += 4;
+          if (ox >= H1) { ox -= H1; oy++; }
+        }
       }
 #pragma unroll
       for (int i = 0; i < 2; i++) {
         const int k = (wave + 8 * i) * 16 + r;
         const int ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
-        const uint8_t* base = frame + (ky * P0 + kx) * 4 + ci;
+        const unsigned short* base = frame + (ky * P0 + kx) * 4 + ci;
         u16x8 bv;
 #pragma unroll
-        for (int j = 0; j < 8; j++) bv[j] = u8bf(base[(4 * pys[j] * P0 + 4 * pxs[j]) * 4]);
+        for (int j = 0; j < 8; j++) bv[j] = base[poff[j]];
         aw1[i] = mfma(a, as_bf(bv), aw1[i]);
       }
     }
@@ -413,7 +481,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   // stores here, 54 vs 65 us per backward at B=500)
   float* out = partial + int64_t(blockIdx.x) * PART;
 #pragma unroll
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < ((dbg & 16) ? 0 : 2); i++) {
     const int col = (wave + 8 * i) * 16 + r;
 #pragma unroll
     for (int e = 0; e < 4; e++) {

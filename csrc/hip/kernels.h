@@ -106,7 +106,7 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
                       hipStream_t stream, int dbg = 0);
 // dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
-// load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 skip the staging loads.
+// load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores.
 
 }  // namespace hip
 }  // namespace rmm
