@@ -72,13 +72,13 @@ __device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint
   constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;  // 1764 words per plane
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
   uint32_t v[PER][C0];
+  // unconditional loads at a clamped index: a guarded load inside an unrolled batch makes hipcc
+  // branch around each one and wait vmcnt(0) per load (an HBM round trip each)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
+    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
 #pragma unroll
-      for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
-    }
+    for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
   }
 #pragma unroll
   for (int k = 0; k < PER; k++) {
@@ -104,13 +104,13 @@ __device__ __forceinline__ void load_frame_bf16(const uint8_t* __restrict__ src,
   constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
   uint32_t v[PER][C0];
+  // unconditional loads at a clamped index: a guarded load inside an unrolled batch makes hipcc
+  // branch around each one and wait vmcnt(0) per load (an HBM round trip each)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
+    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
 #pragma unroll
-      for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
-    }
+    for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
   }
 #pragma unroll
   for (int k = 0; k < PER; k++) {
@@ -349,17 +349,15 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
       uint4 hv1[PH1];
       u16x8 hv2[PH2], gv2[PH2];
 #pragma unroll
-      for (int k = 0; k < PH1; k++) {
-        const int v = threadIdx.x + NTB * k;
-        if (v < NH1) hv1[k] = *reinterpret_cast<const uint4*>(&h1[(b * NP1 + (v >> 1)) * C1 + 8 * (v & 1)]);
+      for (int k = 0; k < PH1; k++) {  // clamped, unconditional (see load_frame)
+        const int v = min(int(threadIdx.x) + NTB * k, NH1 - 1);
+        hv1[k] = *reinterpret_cast<const uint4*>(&h1[(b * NP1 + (v >> 1)) * C1 + 8 * (v & 1)]);
       }
 #pragma unroll
       for (int k = 0; k < PH2; k++) {
-        const int v = threadIdx.x + NTB * k;
-        if (v < NH2) {
-          hv2[k] = *reinterpret_cast<const u16x8*>(&h2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
-          gv2[k] = *reinterpret_cast<const u16x8*>(&dh2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
-        }
+        const int v = min(int(threadIdx.x) + NTB * k, NH2 - 1);
+        hv2[k] = *reinterpret_cast<const u16x8*>(&h2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
+        gv2[k] = *reinterpret_cast<const u16x8*>(&dh2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
       }
 #pragma unroll
       for (int k = 0; k < PH1; k++) {
