@@ -188,12 +188,16 @@ PYBIND11_MODULE(_hip, m) {
                  A, S(stream));
   });
   m.def("adam_flat", [](uint64_t master, uint64_t m1, uint64_t m2, uint64_t grad, bool grad_bf16, uint64_t wbf16,
-                        uint64_t hp, float grad_scale, int64_t n, uint64_t stream, uint64_t step_ctr) {
+                        uint64_t hp, float grad_scale, int64_t n, uint64_t stream, uint64_t step_ctr, uint64_t bump,
+                        int nbump, uint64_t done) {
     adam_flat(P<float>(master), P<float>(m1), P<float>(m2), P<const void>(grad), grad_bf16,
               wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream),
-              step_ctr ? P<const int64_t>(step_ctr) : nullptr);
+              step_ctr ? P<const int64_t>(step_ctr) : nullptr, bump ? P<int64_t>(bump) : nullptr, nbump,
+              done ? P<uint32_t>(done) : nullptr);
   }, py::arg("master"), py::arg("m1"), py::arg("m2"), py::arg("grad"), py::arg("grad_bf16"), py::arg("wbf16"),
-     py::arg("hp"), py::arg("grad_scale"), py::arg("n"), py::arg("stream"), py::arg("step_ctr") = 0);
+     py::arg("hp"), py::arg("grad_scale"), py::arg("n"), py::arg("stream"), py::arg("step_ctr") = 0,
+     py::arg("bump") = 0, py::arg("nbump") = 0, py::arg("done") = 0);
+  m.def("bump_done_words", &bump_done_words);
   m.def("ppo_heads_loss", [](bool bwd, uint64_t heads, uint64_t cols, uint64_t coef, uint64_t acc, uint64_t gout,
                              uint64_t g_heads, int64_t N, int A, uint64_t stream) {
     ppo_heads_loss(bwd, P<const void>(heads), P<const float>(cols), P<const float>(coef), P<float>(acc),
@@ -211,11 +215,14 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("synth_env_step", [](uint64_t frames, uint64_t pool, uint64_t actions, uint64_t tenv, uint64_t ctr_t,
                              uint64_t buf_obs, uint64_t buf_rew, uint64_t buf_done, uint32_t seed, int episode_len,
-                             int64_t B, uint64_t stream) {
+                             int64_t B, uint64_t stream, uint64_t bump, uint64_t done) {
     synth_env_step(P<uint8_t>(frames), P<const uint8_t>(pool), P<const int64_t>(actions), P<int32_t>(tenv),
                    P<const int64_t>(ctr_t), buf_obs ? P<uint8_t>(buf_obs) : nullptr, P<float>(buf_rew),
-                   P<float>(buf_done), seed, episode_len, B, S(stream));
-  });
+                   P<float>(buf_done), seed, episode_len, B, S(stream), bump ? P<int64_t>(bump) : nullptr,
+                   done ? P<uint32_t>(done) : nullptr);
+  }, py::arg("frames"), py::arg("pool"), py::arg("actions"), py::arg("tenv"), py::arg("ctr_t"), py::arg("buf_obs"),
+     py::arg("buf_rew"), py::arg("buf_done"), py::arg("seed"), py::arg("episode_len"), py::arg("B"), py::arg("stream"),
+     py::arg("bump") = 0, py::arg("done") = 0);
   m.def("bias_relu_fwd", [](uint64_t y, uint64_t bias, int64_t M, int C, bool relu, uint64_t stream) {
     bias_relu_fwd(P<void>(y), P<const void>(bias), M, C, relu, S(stream));
   });

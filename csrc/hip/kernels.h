@@ -62,7 +62,8 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
 
 // K6: flat Adam/AdamW with fp32 master weights, bf16 or fp32 grads, optional bf16 weight output.
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
-               float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr = nullptr);
+               float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr = nullptr,
+               int64_t* bump = nullptr, int nbump = 0, uint32_t* done = nullptr);
 
 // K5c: merged policy/value head PPO loss reading packed columns (see rl_kernels.hip).
 void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float* coef, float* acc, const float* gout,
@@ -77,7 +78,11 @@ void sample_store(const void* logits, bool logits_bf16, const void* values, bool
 // ctr_t = device int64[2] {rng counter, rollout row}.
 void synth_env_step(uint8_t* frames, const uint8_t* pool, const int64_t* actions, int32_t* tenv, const int64_t* ctr_t,
                     uint8_t* buf_obs, float* buf_rew, float* buf_done, uint32_t seed, int episode_len, int64_t B,
-                    hipStream_t stream);
+                    hipStream_t stream, int64_t* bump = nullptr, uint32_t* done = nullptr);
+// bump/done (optional, K6 and K9): the kernel's last workgroup adds 1 to bump[0..n) after every
+// workgroup has read its counters (replaces a separate counter-increment launch per step).
+// done: a zero-initialised device buffer of bump_done_words() u32 per call site.
+int bump_done_words();
 
 // K8: conv epilogue for NHWC bf16 maps [M, C]: y = relu(y + b) in place; backward dpre = dy*(y>0)
 // and db = column sums of dpre (two-pass, deterministic; `partial` holds bias_relu_bwd_partials(M)*C f32).

@@ -185,7 +185,7 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
 // cols[N, A+4] (f32): old logits [0, A), old logp A, advantage A+1, value target A+2, action A+3.
 // fwd: atomically accumulates the 6 stats sums into acc[0..5] (zeroed by the caller per update).
 // bwd: g_heads[N, A+1] = d(total)/d(heads) * (*gout) / N.
-template <bool kBwd>
+template <int kMode>  // 0: stats (fwd), 1: grads (bwd), 2: both in one pass
 __global__ __launch_bounds__(256) void k_ppo_heads(const __hip_bfloat16* __restrict__ heads,
                                                   const float* __restrict__ cols, const float* __restrict__ coef,
                                                   float* __restrict__ acc, const float* __restrict__ gout,
@@ -193,7 +193,8 @@ __global__ __launch_bounds__(256) void k_ppo_heads(const __hip_bfloat16* __restr
   const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
   const int lh = A + 1, lc = A + 4;
   float s[6] = {0, 0, 0, 0, 0, 0};
-  const float gs = kBwd ? gout[0] / float(N) : 0.f;
+  constexpr bool kStats = kMode != 1, kGrads = kMode != 0;
+  const float gs = kGrads ? gout[0] / float(N) : 0.f;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += int64_t(gridDim.x) * blockDim.x) {
     const __hip_bfloat16* hrow = heads + i * lh;
     const float* crow = cols + i * lc;
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(256) void k_ppo_heads(const __hip_bfloat16* __restr
     const float ad = crow[A + 1];
     const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
     const float d = __bfloat162float(hrow[A]) - crow[A + 2];
-    if constexpr (!kBwd) {
+    if constexpr (kStats) {
       const float ent = lse - m;
       const float surr = fminf(r * ad, rc * ad);
       const float vf = fminf(d * d, vf_clip);
@@ -233,7 +234,8 @@ __global__ __launch_bounds__(256) void k_ppo_heads(const __hip_bfloat16* __restr
       s[3] += kl;
       s[4] += (fabsf(r - 1.f) > clip) ? 1.f : 0.f;
       s[5] += -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl;
-    } else {
+    }
+    if constexpr (kGrads) {
       const bool unclipped = r * ad <= rc * ad;
       const bool inside = (r >= 1.f - clip) && (r <= 1.f + clip);
       const float spg = (unclipped || inside) ? -(r * ad) : 0.f;
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(256) void k_ppo_heads(const __hip_bfloat16* __restr
       grow[A] = __float2bfloat16((d * d < vf_clip) ? vf_coeff * 2.f * d * gs : 0.f);
     }
   }
-  if constexpr (!kBwd) {
+  if constexpr (kStats) {
 #pragma unroll
     for (int k = 0; k < 6; k++)
 #pragma unroll
@@ -270,13 +272,44 @@ void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float*
   if (N <= 0) return;
   int64_t blocks = std::min<int64_t>((N + 255) / 256, 1024);
   auto* h = static_cast<const __hip_bfloat16*>(heads);
-  if (bwd)
-    hipLaunchKernelGGL(k_ppo_heads<true>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
+  if (bwd && acc)  // stats + grads in one pass (the upstream gradient is known at forward time)
+    hipLaunchKernelGGL(k_ppo_heads<2>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
+                       static_cast<__hip_bfloat16*>(g_heads), N, A);
+  else if (bwd)
+    hipLaunchKernelGGL(k_ppo_heads<1>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
                        static_cast<__hip_bfloat16*>(g_heads), N, A);
   else
-    hipLaunchKernelGGL(k_ppo_heads<false>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
+    hipLaunchKernelGGL(k_ppo_heads<0>, dim3(uint32_t(blocks)), dim3(256), 0, stream, h, cols, coef, acc, gout,
                        static_cast<__hip_bfloat16*>(nullptr), N, A);
   RMM_HIP_CHECK(hipGetLastError());
+}
+
+// Device step counters advanced by the LAST workgroup of the kernel that reads them, instead of a
+// separate 1-element add launch per step (~4 µs each in a HIP graph). Every workgroup reads the
+// counters at its start, so once all of them have drawn a ticket nobody reads them any more;
+// the kernel boundary publishes the new values to the next launch. Tickets are relaxed (nothing
+// is published between workgroups; an acq_rel agent-scope atomic costs an L2 writeback per
+// workgroup) and two-level: 16 sub-counters on separate 128-B lines, then one top counter, so
+// ~2000 workgroups do not serialise on a single address (one address cost ~2 µs/1000 WGs).
+// `done` = kBumpWords zero-initialised u32 owned by the call site; counters reset themselves.
+constexpr int kBumpSubs = 16, kBumpStride = 32, kBumpWords = (kBumpSubs + 1) * kBumpStride;
+__device__ __forceinline__ void last_block_bump(int64_t* bump, int nbump, uint32_t* done) {
+  if (!bump) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t G = gridDim.x, sub = blockIdx.x % kBumpSubs;
+    const uint32_t members = (G - sub + kBumpSubs - 1) / kBumpSubs;
+    uint32_t* sc = done + sub * kBumpStride;
+    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t* top = done + kBumpSubs * kBumpStride;
+      const uint32_t nsubs = G < uint32_t(kBumpSubs) ? G : uint32_t(kBumpSubs);
+      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsubs - 1) {
+        for (int k = 0; k < nbump; k++) bump[k] += 1;
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // ============================================================== K6 flat Adam (fp32 master -> bf16 weights)
@@ -287,7 +320,8 @@ template <typename TG>
 __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, float* __restrict__ m1,
                                                   float* __restrict__ m2, const TG* __restrict__ grad,
                                                   __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
-                                                  float grad_scale, int64_t n, const int64_t* __restrict__ step_ctr) {
+                                                  float grad_scale, int64_t n, const int64_t* __restrict__ step_ctr,
+                                                  int64_t* bump, int nbump, uint32_t* done) {
   // step: hp[5], or (device step counter + 1) when the counter is given (graph-friendly)
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
   const float step = step_ctr ? float(step_ctr[0] + 1) : hp[5];
@@ -306,20 +340,24 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
     master[i] = w;
     if (wbf16) wbf16[i] = __float2bfloat16(w);
   }
+  last_block_bump(bump, nbump, done);
 }
 
+int bump_done_words() { return kBumpWords; }
+
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
-               float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr) {
+               float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr, int64_t* bump, int nbump,
+               uint32_t* done) {
   if (n <= 0) return;
   int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 8);
   if (grad_bf16)
     hipLaunchKernelGGL(k_adam_flat<__hip_bfloat16>, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2,
                        static_cast<const __hip_bfloat16*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n,
-                       step_ctr);
+                       step_ctr, bump, nbump, done);
   else
     hipLaunchKernelGGL(k_adam_flat<float>, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2,
                        static_cast<const float*>(grad), static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n,
-                       step_ctr);
+                       step_ctr, bump, nbump, done);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -410,7 +448,8 @@ __global__ __launch_bounds__(256) void k_synth_env_step(uint8_t* __restrict__ fr
                                                        const int64_t* __restrict__ actions, int32_t* __restrict__ tenv,
                                                        const int64_t* __restrict__ ctr_t, uint8_t* __restrict__ buf_obs,
                                                        float* __restrict__ buf_rew, float* __restrict__ buf_done,
-                                                       uint32_t seed, int episode_len, int64_t B) {
+                                                       uint32_t seed, int episode_len, int64_t B,
+                                                       int64_t* bump, uint32_t* done_ctr) {
   constexpr int H = 84, W = 84, HW = H * W, C = 4;
   const uint32_t ctr = uint32_t(ctr_t[0]);
   const int64_t trow = ctr_t[1];
@@ -441,21 +480,22 @@ __global__ __launch_bounds__(256) void k_synth_env_step(uint8_t* __restrict__ fr
       const uint32_t hr = hash3(seed, ctr, uint32_t(b) * 2u + 1u);
       const float u = float(hr >> 8) * (1.0f / 16777216.0f);
       int32_t t = tenv[b] + 1;
-      const bool done = t >= episode_len;
-      tenv[b] = done ? 0 : t;
+      const bool ended = t >= episode_len;
+      tenv[b] = ended ? 0 : t;
       buf_rew[trow * B + b] = u < 0.05f ? 1.f : 0.f;
-      buf_done[trow * B + b] = done ? 1.f : 0.f;
+      buf_done[trow * B + b] = ended ? 1.f : 0.f;
     }
   }
+  last_block_bump(bump, 2, done_ctr);
 }
 
 void synth_env_step(uint8_t* frames, const uint8_t* pool, const int64_t* actions, int32_t* tenv, const int64_t* ctr_t,
                     uint8_t* buf_obs, float* buf_rew, float* buf_done, uint32_t seed, int episode_len, int64_t B,
-                    hipStream_t stream) {
+                    hipStream_t stream, int64_t* bump, uint32_t* done) {
   int64_t total = B * 84 * 84;
   int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(k_synth_env_step, dim3(uint32_t(blocks)), dim3(256), 0, stream, frames, pool, actions, tenv,
-                     ctr_t, buf_obs, buf_rew, buf_done, seed, episode_len, B);
+                     ctr_t, buf_obs, buf_rew, buf_done, seed, episode_len, B, bump, done);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

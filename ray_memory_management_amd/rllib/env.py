@@ -203,18 +203,26 @@ class GPUSyntheticAtariVectorEnv:
     def reset(self):
         return self.frames
 
-    def fused_step(self, actions, ctr_t, buf_obs, buf_rew, buf_done, seed: int = 0):
+    def fused_step(self, actions, ctr_t, buf_obs, buf_rew, buf_done, seed: int = 0, advance: bool = False):
         """One-launch step (HIP kernel K9): writes the current observation into buf_obs[row],
         advances the frame stack in place, writes reward/done into buf_rew/buf_done[row].
-        ctr_t is a device int64[2] = {rng counter, rollout row}."""
+        ctr_t is a device int64[2] = {rng counter, rollout row}; with advance=True the kernel's last
+        workgroup also increments both (no separate counter launch)."""
         from ray_memory_management_amd._native import require_hip
         import torch
 
+        done = 0
+        if advance:
+            if getattr(self, "_bump_done", None) is None:
+                self._bump_done = torch.zeros(require_hip().bump_done_words(), dtype=torch.int32,
+                                               device=self.frames.device)
+            done = self._bump_done.data_ptr()
         require_hip().synth_env_step(self.frames.data_ptr(), self.pool.data_ptr(), actions.data_ptr(),
                                      self.t.data_ptr(), ctr_t.data_ptr(),
                                      buf_obs.data_ptr() if buf_obs is not None else 0, buf_rew.data_ptr(),
                                      buf_done.data_ptr(), int(seed) & 0xFFFFFFFF, int(self.episode_len),
-                                     self.num_envs, torch.cuda.current_stream().cuda_stream)
+                                     self.num_envs, torch.cuda.current_stream().cuda_stream,
+                                     bump=ctr_t.data_ptr() if advance else 0, done=done)
 
     def step(self, actions):
         """All state updates are in place and host-sync free, so a step can be captured in a HIP

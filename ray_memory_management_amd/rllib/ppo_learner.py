@@ -91,30 +91,40 @@ class _HeadsPPOLoss(torch.autograd.Function):
     reads the upstream gradient from device memory, so the whole step is allocation/copy free."""
 
     @staticmethod
-    def forward(ctx, heads, cols, coef, acc):
+    def forward(ctx, heads, cols, coef, acc, gout):
         N, A1 = heads.shape
-        require_hip().ppo_heads_loss(False, heads.data_ptr(), cols.data_ptr(), coef.data_ptr(), acc.data_ptr(), 0, 0,
-                                     N, A1 - 1, _stream())
+        ctx.g_heads = None
+        if gout is not None:  # upstream gradient known now: stats AND d/dheads in one launch
+            ctx.g_heads = torch.empty_like(heads)
+            ctx.gout_ptr = gout.data_ptr()
+            require_hip().ppo_heads_loss(True, heads.data_ptr(), cols.data_ptr(), coef.data_ptr(), acc.data_ptr(),
+                                         gout.data_ptr(), ctx.g_heads.data_ptr(), N, A1 - 1, _stream())
+        else:
+            require_hip().ppo_heads_loss(False, heads.data_ptr(), cols.data_ptr(), coef.data_ptr(), acc.data_ptr(),
+                                         0, 0, N, A1 - 1, _stream())
         ctx.save_for_backward(heads, cols, coef)
         return torch.empty((), dtype=torch.float32, device=heads.device)
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.g_heads is not None and g.data_ptr() == ctx.gout_ptr:
+            return ctx.g_heads, None, None, None, None
         heads, cols, coef = ctx.saved_tensors
         N, A1 = heads.shape
         g_heads = torch.empty_like(heads)
         g = g.float().contiguous()
         require_hip().ppo_heads_loss(True, heads.data_ptr(), cols.data_ptr(), coef.data_ptr(), 0, g.data_ptr(),
                                      g_heads.data_ptr(), N, A1 - 1, _stream())
-        return g_heads, None, None, None
+        return g_heads, None, None, None, None
 
 
-def ppo_heads_loss(heads, cols, coef, acc):
+def ppo_heads_loss(heads, cols, coef, acc, gout=None):
     """Fused PPO loss on a merged head output (see _HeadsPPOLoss). Differentiate the returned
-    handle with grad_outputs=<device scalar 1.0>; the loss VALUE is only available through acc[5]/N."""
+    handle with grad_outputs=<device scalar 1.0>; the loss VALUE is only available through acc[5]/N.
+    Passing that same device scalar as `gout` computes the gradient in the forward launch."""
     assert heads.dtype == torch.bfloat16 and heads.is_contiguous() and cols.dtype == torch.float32
     assert cols.shape == (heads.shape[0], heads.shape[1] + 3) and cols.is_contiguous()
-    return _HeadsPPOLoss.apply(heads, cols, coef, acc)
+    return _HeadsPPOLoss.apply(heads, cols, coef, acc, gout)
 
 
 def ppo_categorical_loss(logits, values, old_logits, actions, old_logp, adv, vtgt, coef):
@@ -216,6 +226,7 @@ class PPOLearner:
         # its minibatch indices at idx_all[ctr[0]] and the Adam bias correction from ctr[1]; one
         # add per step advances both, so no host→device copy happens between graph replays.
         self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._bump_done = torch.zeros(require_hip().bump_done_words(), dtype=torch.int32, device=dev)
         self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.heads_ok = hasattr(self.model, "forward_heads")
 
@@ -223,10 +234,11 @@ class PPOLearner:
         h = require_hip()
         if self.world > 1:
             torch.distributed.all_reduce(self.flat_grad, group=self.pg)
+        # K6 also advances both device counters {minibatch step, Adam step} from its last workgroup
         h.adam_flat(self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
                     self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream(),
-                    step_ctr=self.ctr.data_ptr() + 8)
-        self.ctr.add_(1)
+                    step_ctr=self.ctr.data_ptr() + 8, bump=self.ctr.data_ptr(), nbump=2,
+                    done=self._bump_done.data_ptr())
 
     def _fast_step(self, full, with_opt: bool):
         h = require_hip()
@@ -246,7 +258,7 @@ class PPOLearner:
         cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
         if fused:
             heads = self.model.forward_frames(full["obs"], idx=full["idx"], ctr=ctr, period=period, rows=mbs)
-            total = ppo_heads_loss(heads, cols, self.coef, self.acc)     # K5c
+            total = ppo_heads_loss(heads, cols, self.coef, self.acc, gout=self._one)  # K5c, fwd+bwd
             grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
         elif self.heads_ok and frames:
             heads = self.model.forward_heads(x, prescaled=True)
@@ -493,8 +505,9 @@ class GPURolloutSampler:
             self.buf_logp.index_copy_(0, t, d.logp(a).unsqueeze(0))
             self.buf_vf.index_copy_(0, t, v.float().unsqueeze(0))
             self.buf_logits.index_copy_(0, t, logits.float().unsqueeze(0))
-        if self.fused_env:  # K9: obs row write + frame-stack step + reward/done in one launch
-            self.env.fused_step(a, self.ctr_t, self.buf_obs, self.buf_rew, self.buf_done, self.seed)
+        if self.fused_env:  # K9: obs row write + frame-stack step + reward/done + counters in one launch
+            self.env.fused_step(a, self.ctr_t, self.buf_obs, self.buf_rew, self.buf_done, self.seed, advance=True)
+            return
         else:
             self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
             obs, r, done = self.env.step(a)
