@@ -143,6 +143,57 @@ class _DenseFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _DenseHeadsFn(torch.autograd.Function):
+    """hidden = ReLU(x Wᵀ + b); heads = hidden Whᵀ + bh. Forward: two hipBLASLt GEMMs with fused
+    epilogues. Backward: ONE K12 launch (csrc/hip/dense_kernels.hip) for dx, dW, db, dWh, dbh,
+    writing parameter gradients straight into their gradient buffers when they have one."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wh, bh):
+        hidden = torch._addmm_activation(b, x, w.t())
+        heads = torch.addmm(bh, hidden, wh.t())
+        ctx.save_for_backward(x, w, wh, hidden)
+        ctx.gout = tuple(_grad_out(t) for t in (w, b, wh, bh))
+        return heads
+
+    @staticmethod
+    def backward(ctx, dheads):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        x, w, wh, hidden = ctx.saved_tensors
+        dheads = dheads.contiguous()
+        M, K = x.shape
+        A1 = wh.shape[0]
+        dev = x.device
+
+        def out(g, like):
+            return g if g is not None else torch.empty_like(like, memory_format=torch.contiguous_format)
+
+        gw, gb, gwh, gbh = ctx.gout
+        dw = out(gw, w)
+        db = gb if gb is not None else torch.empty(w.shape[0], dtype=w.dtype, device=dev)
+        dwh = out(gwh, wh)
+        dbh = gbh if gbh is not None else torch.empty(A1, dtype=wh.dtype, device=dev)
+        assert dw.is_contiguous() and dwh.is_contiguous()
+        dx = torch.empty_like(x)
+        h.dense_heads_bwd(dheads.data_ptr(), A1, wh.data_ptr(), hidden.data_ptr(), x.data_ptr(), w.data_ptr(), M, K,
+                          dx.data_ptr(), dw.data_ptr(), db.data_ptr(), dwh.data_ptr(), dbh.data_ptr(),
+                          torch.cuda.current_stream(dev).cuda_stream)
+        return dx, dw, db, dwh, dbh
+
+
+def dense_heads(x, layer: nn.Linear, heads: nn.Linear):
+    """heads(ReLU(layer(x))) with the fused K12 backward on the bf16 GPU path."""
+    ok = (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and layer.weight.dtype == torch.bfloat16
+          and heads.weight.dtype == torch.bfloat16 and layer.out_features == 256 and layer.in_features % 32 == 0
+          and heads.out_features <= 16 and x.shape[0] <= 640 and layer.bias is not None and heads.bias is not None
+          and layer.weight.is_contiguous() and heads.weight.is_contiguous() and not os.environ.get("RMM_NO_K12"))
+    if not ok:
+        return dense(dense(x, layer, True), heads, False)
+    return _DenseHeadsFn.apply(x.contiguous(), layer.weight, layer.bias, heads.weight, heads.bias)
+
+
 def dense(x, layer: nn.Linear, relu: bool):
     if (x.is_cuda and x.dtype == torch.bfloat16 and layer.weight.dtype == torch.bfloat16 and x.dim() == 2
             and layer.bias is not None):
@@ -298,7 +349,7 @@ class VisionNetwork(nn.Module):
         convs in the fused K10 kernel."""
         c1, c2 = self.convs[0], self.convs[1]
         h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
-        return dense(dense(h, self.dense_tail, True), self.heads, False)
+        return dense_heads(h, self.dense_tail, self.heads)
 
     def _trunk(self, x):
         h = self.convs(x)

@@ -242,3 +242,26 @@ def test_dense_fn_matches_linear(cuda):
     assert gw.data_ptr() == gout.data_ptr()  # written in place into the bucket view (learner path)
     for a, b in ((gw, ref_lin.weight.grad), (gb, ref_lin.bias.grad), (gx, xr.grad)):
         assert float((a.float() - b).abs().max() / b.abs().max()) < 2e-2
+
+
+@pytest.mark.parametrize("M,K,A1", [(500, 3872, 5), (37, 96, 7), (64, 64, 1)])
+def test_dense_heads_bwd_matches_fp32(cuda, M, K, A1):
+    """K12 fused dense+heads backward vs fp32 autograd of ReLU(x Wᵀ+b) Whᵀ+bh (same bf16 inputs)."""
+    from ray_memory_management_amd.rllib.models import dense_heads
+
+    torch.manual_seed(0)
+    layer = torch.nn.Linear(K, 256).to(cuda).to(torch.bfloat16)
+    heads = torch.nn.Linear(256, A1).to(cuda).to(torch.bfloat16)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    out = dense_heads(x, layer, heads)
+    g = torch.randn(M, A1, device=cuda).to(torch.bfloat16)
+    got = torch.autograd.grad(out, (x, layer.weight, layer.bias, heads.weight, heads.bias), g)
+    xr = x.detach().float().requires_grad_(True)
+    ps = [t.detach().float().requires_grad_(True) for t in (layer.weight, layer.bias, heads.weight, heads.bias)]
+    hidden = torch.relu(xr @ ps[0].t() + ps[1])
+    ref_out = hidden @ ps[2].t() + ps[3]
+    assert float((out.float() - ref_out).abs().max() / ref_out.abs().max()) < 2e-2
+    ref = torch.autograd.grad(ref_out, [xr] + ps, g.float())
+    errs = {n: float((a.float() - b).abs().max() / b.abs().max().clamp_min(1e-6))
+            for n, a, b in zip(("dx", "dW", "db", "dWh", "dbh"), got, ref)}
+    assert max(errs.values()) < 2e-2, errs
