@@ -54,13 +54,62 @@ __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// dpre = (dheads · Wh) ⊙ [hidden > 0], computed ONCE for the batch (32 rows per workgroup) and
+// read by every column-block workgroup of k_dense_heads_bwd. Recomputing it inside each of those
+// 121 workgroups made that kernel VALU-bound (PMC: ~5.3k VALU instructions per wave, 40 µs).
+template <int A1>
+__global__ __launch_bounds__(NT) void k_dense_dpre(const unsigned short* __restrict__ dz,
+                                                   const unsigned short* __restrict__ wh,
+                                                   const unsigned short* __restrict__ y, int64_t M,
+                                                   unsigned short* __restrict__ dpre) {
+  __shared__ __attribute__((aligned(16))) unsigned short whs[A1 * H];
+  const int tid = threadIdx.x;
+  const int pm = tid & (MC - 1), hb = (tid / MC) * 16;
+  const int64_t row = int64_t(blockIdx.x) * MC + pm, rc = row < M ? row : M - 1;
+  const uint4 y0 = *reinterpret_cast<const uint4*>(&y[rc * H + hb]);
+  const uint4 y1 = *reinterpret_cast<const uint4*>(&y[rc * H + hb + 8]);
+  unsigned short rdz[A1];
+#pragma unroll
+  for (int a = 0; a < A1; a++) rdz[a] = dz[rc * A1 + a];
+  for (int e = tid; e < A1 * H; e += NT) whs[e] = wh[e];
+  __syncthreads();
+  if (row >= M) return;
+  float dyv[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) dyv[i] = 0.f;
+#pragma unroll
+  for (int a = 0; a < A1; a++) {
+    const float za = bf2f(rdz[a]);
+    const u16x8 w0 = *reinterpret_cast<const u16x8*>(&whs[a * H + hb]);
+    const u16x8 w1 = *reinterpret_cast<const u16x8*>(&whs[a * H + hb + 8]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      dyv[i] += za * bf2f(w0[i]);
+      dyv[8 + i] += za * bf2f(w1[i]);
+    }
+  }
+  unsigned short yv[16];
+  *reinterpret_cast<uint4*>(&yv[0]) = y0;
+  *reinterpret_cast<uint4*>(&yv[8]) = y1;
+  u16x8 o0, o1;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const unsigned short yi = yv[i];
+    const unsigned short dp = (yi != 0 && !(yi & 0x8000)) ? f2bf(dyv[i]) : static_cast<unsigned short>(0);
+    if (i < 8) o0[i] = dp; else o1[i - 8] = dp;
+  }
+  *reinterpret_cast<u16x8*>(&dpre[row * H + hb]) = o0;
+  *reinterpret_cast<u16x8*>(&dpre[row * H + hb + 8]) = o1;
+}
+
 // A1 is a template parameter: a runtime `if (a < A1)` around the per-element Wh reads made hipcc
 // branch around each LDS load and wait for it (measured 128 µs per call; see the dispatch below).
 template <int A1>
 __global__ __launch_bounds__(NT) void k_dense_heads_bwd(
     const unsigned short* __restrict__ dz, const unsigned short* __restrict__ wh,
     const unsigned short* __restrict__ y, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
-    int64_t M, int64_t K, unsigned short* __restrict__ dx, unsigned short* __restrict__ dw,
+    const unsigned short* __restrict__ dpre, int64_t M, int64_t K, unsigned short* __restrict__ dx,
+    unsigned short* __restrict__ dw,
     unsigned short* __restrict__ db, unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh) {
   __shared__ __attribute__((aligned(16))) unsigned short wt[JB * HP];   // W[:, J]ᵀ  [j][h]
   __shared__ __attribute__((aligned(16))) unsigned short whs[AMAX * H]; // Wh [a][h]
@@ -133,12 +182,16 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd(
   // transposed dpre/hidden stores ([h][m]) are conflict-free and Wh reads broadcast.
   const int pm = tid & (MC - 1), hb = (tid / MC) * 16;
   const int xm = tid >> 4, xj = (tid & 15) * 2;  // (b): row xm (0..31), cols xj, xj+1 (512 threads)
-  uint4 ry0, ry1;
+  uint4 rp0, rp1, ry0 = make_uint4(0, 0, 0, 0), ry1 = make_uint4(0, 0, 0, 0);
   uint32_t rx;
   auto stage = [&](int64_t m0) {  // unconditional clamped loads (see load_frame in K10)
     const int64_t row = m0 + pm, rc = row < M ? row : M - 1;
-    ry0 = *reinterpret_cast<const uint4*>(&y[rc * H + hb]);
-    ry1 = *reinterpret_cast<const uint4*>(&y[rc * H + hb + 8]);
+    rp0 = *reinterpret_cast<const uint4*>(&dpre[rc * H + hb]);
+    rp1 = *reinterpret_cast<const uint4*>(&dpre[rc * H + hb + 8]);
+    if (head_wg) {
+      ry0 = *reinterpret_cast<const uint4*>(&y[rc * H + hb]);
+      ry1 = *reinterpret_cast<const uint4*>(&y[rc * H + hb + 8]);
+    }
     const int64_t xr = m0 + xm, xc = xr < M ? xr : M - 1;
     rx = *reinterpret_cast<const uint32_t*>(&x[xc * K + J0 + xj]);
   };
@@ -149,42 +202,25 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd(
     // ---- (a) dpre chunk from the staged registers (and wg 0: hidden / dheads transposed)
     {
       const bool valid = m0 + pm < M;
-      const int zrow = int(valid ? m0 + pm : 0) * A1;
-      unsigned short rdz[A1];
-#pragma unroll
-      for (int a = 0; a < A1; a++) rdz[a] = dzs[zrow + a];
-      float dyv[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) dyv[i] = 0.f;
-#pragma unroll
-      for (int a = 0; a < A1; a++) {  // dY = dheads · Wh for this thread's 16 columns
-        const float za = valid ? bf2f(rdz[a]) : 0.f;
-        const u16x8 w0 = *reinterpret_cast<const u16x8*>(&whs[a * H + hb]);
-        const u16x8 w1 = *reinterpret_cast<const u16x8*>(&whs[a * H + hb + 8]);
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          dyv[i] += za * bf2f(w0[i]);
-          dyv[8 + i] += za * bf2f(w1[i]);
-        }
+      u16x8 o0 = __builtin_bit_cast(u16x8, rp0), o1 = __builtin_bit_cast(u16x8, rp1);
+      if (!valid) {
+        o0 = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        o1 = o0;
       }
-      unsigned short yv[16];
-      *reinterpret_cast<uint4*>(&yv[0]) = ry0;
-      *reinterpret_cast<uint4*>(&yv[8]) = ry1;
-      u16x8 o0, o1;
 #pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const float d = dyv[i];
-        const unsigned short yi = yv[i];
-        const unsigned short dp = (valid && yi != 0 && !(yi & 0x8000)) ? f2bf(d) : static_cast<unsigned short>(0);
-        if (i < 8) o0[i] = dp; else o1[i - 8] = dp;
-        dt[(hb + i) * MP + pm] = dp;
-        if (head_wg) yt[(hb + i) * MP + pm] = valid ? yi : static_cast<unsigned short>(0);
-      }
+      for (int i = 0; i < 16; i++) dt[(hb + i) * MP + pm] = i < 8 ? o0[i] : o1[i - 8];
       *reinterpret_cast<u16x8*>(&dm[pm * HP + hb]) = o0;
       *reinterpret_cast<u16x8*>(&dm[pm * HP + hb + 8]) = o1;
-      if (head_wg && hb == 0) {
+      if (head_wg) {
+        u16x8 h0 = __builtin_bit_cast(u16x8, ry0), h1 = __builtin_bit_cast(u16x8, ry1);
 #pragma unroll
-        for (int a = 0; a < A1; a++) dzt[a * MP + pm] = valid ? rdz[a] : static_cast<unsigned short>(0);
+        for (int i = 0; i < 16; i++)
+          yt[(hb + i) * MP + pm] = valid ? (i < 8 ? h0[i] : h1[i - 8]) : static_cast<unsigned short>(0);
+        if (hb == 0) {
+          const int zrow = int(valid ? m0 + pm : 0) * A1;
+#pragma unroll
+          for (int a = 0; a < A1; a++) dzt[a * MP + pm] = valid ? dzs[zrow + a] : static_cast<unsigned short>(0);
+        }
       }
       // ---- (b) x[chunk, J]ᵀ
       {  // MC * JB / 2 == NT pairs: every thread writes one
@@ -293,7 +329,8 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd(
 }  // namespace dense
 
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
-                     int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, hipStream_t stream) {
+                     int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
+                     hipStream_t stream) {
   if (M <= 0) return;
   if (K % dense::JB != 0) throw std::invalid_argument("dense_heads_bwd: K must be a multiple of 32");
   if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_bwd: 1 <= A+1 <= 16");
@@ -301,10 +338,13 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
   auto V = [](void* p) { return static_cast<unsigned short*>(p); };
   const dim3 grid(uint32_t(K / dense::JB)), block(dense::NT);
-#define RMM_K12(N)                                                                                              \
-  case N:                                                                                                       \
-    hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w), M, K, \
-                       V(dx), V(dw), V(db), V(dwh), V(dbh));                                                    \
+  const dim3 pgrid(uint32_t((M + dense::MC - 1) / dense::MC));
+  auto* dp = V(dpre_scratch);
+#define RMM_K12(N)                                                                                               \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);              \
+    hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w), dp,  \
+                       M, K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                               \
     break;
   switch (A1) {
     RMM_K12(1) RMM_K12(2) RMM_K12(3) RMM_K12(4) RMM_K12(5) RMM_K12(6) RMM_K12(7) RMM_K12(8)

@@ -252,9 +252,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("nature_trunk_partial_floats", &nature_trunk_partial_floats);
   m.def("dense_heads_bwd", [](uint64_t dz, int A1, uint64_t wh, uint64_t y, uint64_t x, uint64_t w, int64_t M,
                               int64_t K, uint64_t dx, uint64_t dw, uint64_t db, uint64_t dwh, uint64_t dbh,
-                              uint64_t stream) {
+                              uint64_t scratch, uint64_t stream) {
     dense_heads_bwd(P<const void>(dz), A1, P<const void>(wh), P<const void>(y), P<const void>(x), P<const void>(w), M,
-                    K, P<void>(dx), P<void>(dw), P<void>(db), P<void>(dwh), P<void>(dbh), S(stream));
+                    K, P<void>(dx), P<void>(dw), P<void>(db), P<void>(dwh), P<void>(dbh), P<void>(scratch),
+                    S(stream));
   });
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,

@@ -100,7 +100,8 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
 // dheads: dx [M,K], dW [256,K], db [256], dWh [A1,256], dbh [A1] (all bf16, row-major), one launch.
 // K % 32 == 0, A1 <= 16, M <= 640 (a PPO minibatch; larger batches take the hipBLASLt path).
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
-                     int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, hipStream_t stream);
+                     int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
+                     hipStream_t stream);  // dpre_scratch: M*256 bf16
 
 // K10: fused Nature-CNN trunk (conv 8x8/4 4->16 + conv 4x4/2 16->32, bias+ReLU) on MFMA, one
 // workgroup per frame in LDS. Frames u8 [.,4,84,84] gathered by idx (device-counter window like

@@ -177,8 +177,9 @@ class _DenseHeadsFn(torch.autograd.Function):
         dbh = gbh if gbh is not None else torch.empty(A1, dtype=wh.dtype, device=dev)
         assert dw.is_contiguous() and dwh.is_contiguous()
         dx = torch.empty_like(x)
+        dpre = torch.empty_like(hidden)  # scratch: (dheads Wh) ⊙ [hidden > 0]
         h.dense_heads_bwd(dheads.data_ptr(), A1, wh.data_ptr(), hidden.data_ptr(), x.data_ptr(), w.data_ptr(), M, K,
-                          dx.data_ptr(), dw.data_ptr(), db.data_ptr(), dwh.data_ptr(), dbh.data_ptr(),
+                          dx.data_ptr(), dw.data_ptr(), db.data_ptr(), dwh.data_ptr(), dbh.data_ptr(), dpre.data_ptr(),
                           torch.cuda.current_stream(dev).cuda_stream)
         return dx, dw, db, dwh, dbh
 
