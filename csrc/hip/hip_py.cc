@@ -250,6 +250,16 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("b1"), py::arg("W2"), py::arg("w2s"), py::arg("b2"), py::arg("h1"), py::arg("h2"), py::arg("stream"),
      py::arg("dbg") = 0);
   m.def("nature_trunk_partial_floats", &nature_trunk_partial_floats);
+  m.def("partition_groups", &partition_groups);
+  m.def("partition_hist", [](uint64_t keys, int64_t n, int R, int mode, uint64_t counts, uint64_t stream) {
+    partition_hist(P<const int64_t>(keys), n, R, mode, P<int64_t>(counts), S(stream));
+  });
+  m.def("partition_scatter", [](uint64_t keys, uint64_t vals, int64_t n, int64_t row_bytes, int R, int mode,
+                                uint64_t offsets, uint64_t out_keys, uint64_t out_vals, uint64_t stream) {
+    partition_scatter(P<const int64_t>(keys), vals ? P<const void>(vals) : nullptr, n, row_bytes, R, mode,
+                      P<const int64_t>(offsets), P<int64_t>(out_keys), out_vals ? P<void>(out_vals) : nullptr,
+                      S(stream));
+  });
   m.def("dense_heads_bwd", [](uint64_t dz, int A1, uint64_t wh, uint64_t y, uint64_t x, uint64_t w, int64_t M,
                               int64_t K, uint64_t dx, uint64_t dw, uint64_t db, uint64_t dwh, uint64_t dbh,
                               uint64_t scratch, uint64_t stream) {

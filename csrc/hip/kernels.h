@@ -103,6 +103,15 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
                      hipStream_t stream);  // dpre_scratch: M*256 bf16
 
+// K11: shuffle partitioning. dest = splitmix64(key) % R (mode 0) or key mod R (mode 1), R <= 1024.
+// partition_hist writes counts[G][R] (G = partition_groups(n)); the caller turns them into
+// exclusive offsets (destination-major: all of destination 0's rows first) and partition_scatter
+// moves keys + row_bytes payloads to out_keys / out_vals.
+int64_t partition_groups(int64_t n);
+void partition_hist(const int64_t* keys, int64_t n, int R, int mode, int64_t* counts, hipStream_t stream);
+void partition_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int R, int mode,
+                       const int64_t* offsets, int64_t* out_keys, void* out_vals, hipStream_t stream);
+
 // K10: fused Nature-CNN trunk (conv 8x8/4 4->16 + conv 4x4/2 16->32, bias+ReLU) on MFMA, one
 // workgroup per frame in LDS. Frames u8 [.,4,84,84] gathered by idx (device-counter window like
 // gather_rows); weights bf16 with element strides w*s = [co, ci, ky, kx]. h1 [B,441,16] (may be

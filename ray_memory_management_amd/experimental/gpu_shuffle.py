@@ -1,0 +1,196 @@
+"""GPU-resident all-to-all shuffle of keyed tensor blocks (the Exoshuffle data path on MI355X).
+
+Parity: the reference shuffles through the object store only (python/ray/experimental/shuffle.py,
+python/ray/data/_internal/push_based_shuffle.py): map tasks partition host blocks, reduce tasks
+fetch partitions through plasma. On a node of MI355X GPUs the blocks already live in HBM and the
+GPUs are directly connected by xGMI, so here a shuffle round is:
+
+  1. partition on the GPU (K11, ``csrc/hip/shuffle_kernels.hip``): histogram + scatter so every
+     destination's rows are contiguous (two launches, no host round trip except the [R] counts);
+  2. exchange the per-destination row counts with one tiny all-to-all;
+  3. ONE ``all_to_all`` of keys and ONE of payload bytes over RCCL (xGMI point-to-point links:
+     each pair of GPUs exchanges its block directly, no host staging);
+  4. optionally ``ray.put`` the received block: the HBM object store keeps it resident and spills
+     it to host memory (compressed, K4) under HBM pressure.
+
+CPU tensors take the same path with torch ops and a gloo group (tests, rehearsal).
+
+Entry points: :func:`partition` (local), :func:`shuffle` (collective, inside a process group),
+:class:`ShuffleWorker` + :func:`run_gpu_shuffle` (driver API: one actor per GPU, a collective
+group between them, synthetic blocks, throughput + an order-independent checksum).
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+MODES = {"hash": 0, "mod": 1}
+
+
+def _splitmix64(keys: torch.Tensor) -> np.ndarray:
+    """The K11 hash on the host (numpy uint64 arithmetic wraps like the device's)."""
+    x = keys.detach().cpu().numpy().astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xbf58476d1ce4e5b9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94d049bb133111eb)
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def destinations(keys: torch.Tensor, num_partitions: int, mode: str = "hash") -> torch.Tensor:
+    """dest(key) exactly as K11 computes it (CPU reference / CPU path)."""
+    k = keys.detach().cpu().to(torch.int64)
+    if mode == "mod":
+        return torch.remainder(k, num_partitions)
+    return torch.from_numpy((_splitmix64(k) % np.uint64(num_partitions)).astype(np.int64))
+
+
+def partition(keys: torch.Tensor, values: Optional[torch.Tensor], num_partitions: int,
+              mode: str = "hash") -> Tuple[torch.Tensor, Optional[torch.Tensor], torch.Tensor]:
+    """Reorder rows so destination 0's rows come first, then destination 1's, ...
+
+    keys: int64 [n]; values: any dtype [n, ...] (rows travel as raw bytes) or None.
+    Returns (keys_out, values_out, counts[num_partitions] int64 on the keys' device)."""
+    if keys.dtype != torch.int64 or keys.dim() != 1:
+        raise ValueError("partition: keys must be a 1-D int64 tensor")
+    n = keys.shape[0]
+    if values is not None and values.shape[0] != n:
+        raise ValueError("partition: values must have one row per key")
+    if not 1 <= num_partitions <= 1024:
+        raise ValueError("partition: 1 <= num_partitions <= 1024")
+    if keys.is_cuda:
+        return _partition_hip(keys.contiguous(), None if values is None else values.contiguous(), num_partitions,
+                              MODES[mode])
+    dest = destinations(keys, num_partitions, mode)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=num_partitions).to(torch.int64)
+    return keys[order], (None if values is None else values[order]), counts
+
+
+def _partition_hip(keys, values, R, mode):
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    dev = keys.device
+    n = keys.shape[0]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    G = h.partition_groups(n)
+    counts_wg = torch.zeros((G, R), dtype=torch.int64, device=dev)
+    h.partition_hist(keys.data_ptr(), n, R, mode, counts_wg.data_ptr(), stream)
+    counts = counts_wg.sum(0)
+    # destination-major exclusive offsets: base[r] + rows of destination r in earlier workgroups
+    base = torch.cumsum(counts, 0) - counts
+    offsets = (torch.cumsum(counts_wg, 0) - counts_wg + base.unsqueeze(0)).contiguous()
+    out_keys = torch.empty_like(keys)
+    out_vals = None
+    row_bytes = 0
+    if values is not None:
+        out_vals = torch.empty_like(values)
+        row_bytes = values[0].numel() * values.element_size() if n else 0
+    h.partition_scatter(keys.data_ptr(), values.data_ptr() if values is not None else 0, n, row_bytes, R, mode,
+                        offsets.data_ptr(), out_keys.data_ptr(), out_vals.data_ptr() if out_vals is not None else 0,
+                        stream)
+    return out_keys, out_vals, counts
+
+
+def _alltoall(pg, out, inp, out_splits, in_splits):
+    if pg is None:
+        dist.all_to_all_single(out, inp, out_splits, in_splits)
+    else:
+        pg.alltoall_base(out, inp, out_splits, in_splits, dist.AllToAllOptions()).wait()
+
+
+def shuffle(keys: torch.Tensor, values: Optional[torch.Tensor] = None, group=None, mode: str = "hash",
+            world_size: Optional[int] = None, rank: Optional[int] = None):
+    """Collective: every rank calls it with its block; returns the rows whose dest == this rank.
+
+    group: a ``torch.distributed`` ProcessGroup object (e.g. from util.collective) or None for the
+    default group. Keys and payload bytes each go in ONE all_to_all with split sizes."""
+    world = world_size if world_size is not None else (group.size() if group is not None else dist.get_world_size())
+    k, v, counts = partition(keys, values, world, mode)
+    send_counts = counts.to(keys.device)
+    recv_counts = torch.empty_like(send_counts)
+    _alltoall(group, recv_counts, send_counts, [1] * world, [1] * world)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    out_k = torch.empty(sum(rc), dtype=torch.int64, device=keys.device)
+    _alltoall(group, out_k, k, rc, sc)
+    out_v = None
+    if v is not None:
+        row = values.element_size()
+        for d in values.shape[1:]:
+            row *= int(d)
+        vb = v.contiguous().view(torch.uint8).reshape(-1) if v.numel() else \
+            torch.empty(0, dtype=torch.uint8, device=keys.device)
+        out_b = torch.empty(sum(rc) * row, dtype=torch.uint8, device=keys.device)
+        _alltoall(group, out_b, vb.contiguous(), [c * row for c in rc], [c * row for c in sc])
+        out_v = out_b.view(values.dtype).reshape(sum(rc), *values.shape[1:])
+    return out_k, out_v
+
+
+class ShuffleWorker:
+    """Actor body (wrap with ray.remote): owns one device and one block of synthetic rows."""
+
+    def __init__(self, rank: int, world: int, device: str = "cuda"):
+        self.rank, self.world = rank, world
+        self.device = torch.device(device if device != "cuda" else f"cuda:{torch.cuda.current_device()}") \
+            if device.startswith("cuda") else torch.device("cpu")
+        self.group_name = None
+
+    def _collective_init(self, world_size, rank, backend, group_name):
+        from ray_memory_management_amd.util import collective as col
+
+        col.init_collective_group(world_size, rank, backend, group_name)
+        self.group_name = group_name
+        return True
+
+    def generate(self, rows: int, row_bytes: int, seed: int = 0):
+        g = torch.Generator(device="cpu").manual_seed(1000 + self.rank + seed)
+        self.keys = torch.randint(0, 2 ** 62, (rows,), generator=g, dtype=torch.int64).to(self.device)
+        self.vals = torch.randint(0, 256, (rows, row_bytes), generator=g, dtype=torch.uint8).to(self.device)
+        return int(self.keys.sum().item() % (1 << 61))
+
+    def shuffle(self, mode: str = "hash"):
+        from ray_memory_management_amd.util.collective.collective import get_group_handle
+
+        pg = get_group_handle(self.group_name).pg
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        k, v = shuffle(self.keys, self.vals, group=pg, mode=mode, world_size=self.world, rank=self.rank)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - t0
+        dest = destinations(k, self.world, mode)
+        ok = bool((dest == self.rank).all().item())
+        bytes_moved = self.keys.numel() * 8 + self.vals.numel()
+        return {"rows_in": int(self.keys.numel()), "rows_out": int(k.numel()), "seconds": dt, "ok": ok,
+                "bytes": bytes_moved, "key_sum": int(k.sum().item() % (1 << 61)) if k.numel() else 0}
+
+
+def run_gpu_shuffle(num_workers: int = 2, rows_per_worker: int = 1 << 20, row_bytes: int = 256,
+                    backend: str = "nccl", mode: str = "hash") -> dict:
+    """Driver API: one ShuffleWorker actor per GPU (or CPU worker with backend='gloo'), one
+    collective group, one shuffle round. Returns throughput and correctness checks."""
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd.util import collective as col
+
+    gpu = backend == "nccl"
+    Actor = ray.remote(num_gpus=1 if gpu else 0, num_cpus=1)(ShuffleWorker)
+    workers = [Actor.remote(r, num_workers, "cuda" if gpu else "cpu") for r in range(num_workers)]
+    name = f"shuffle-{time.time_ns()}"
+    col.create_collective_group(workers, num_workers, list(range(num_workers)), backend=backend, group_name=name)
+    sums_in = ray.get([w.generate.remote(rows_per_worker, row_bytes) for w in workers])
+    res = ray.get([w.shuffle.remote(mode) for w in workers])
+    total_bytes = sum(r["bytes"] for r in res)
+    secs = max(r["seconds"] for r in res)
+    for w in workers:
+        ray.kill(w)
+    return {"ok": all(r["ok"] for r in res) and sum(r["rows_out"] for r in res) == rows_per_worker * num_workers
+            and sum(sums_in) % (1 << 61) == sum(r["key_sum"] for r in res) % (1 << 61),
+            "GBps": total_bytes / secs / 1e9, "seconds": secs, "bytes": total_bytes, "workers": num_workers}

@@ -250,3 +250,15 @@ def recv(tensor, src_rank: int, group_name: str = "default", tag: int = 0):
         raise RuntimeError("The source rank is the current rank.")
     _pg_for(g, tensor).recv([tensor], src_rank, tag).wait()
     return tensor
+
+
+def alltoall(output, input, output_split_sizes=None, input_split_sizes=None, group_name: str = "default"):
+    """All-to-all along dim 0 (split sizes in rows; None = equal splits). RCCL on GPU groups: every
+    pair of ranks exchanges its slice directly over xGMI. Parity: extends the reference's
+    util.collective API (torch.distributed.all_to_all_single semantics)."""
+    g = get_group_handle(group_name)
+    pg = _pg_for(g, input)
+    outs = list(output_split_sizes) if output_split_sizes is not None else []
+    ins = list(input_split_sizes) if input_split_sizes is not None else []
+    pg.alltoall_base(output, input, outs, ins, dist.AllToAllOptions()).wait()
+    return output
