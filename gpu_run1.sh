@@ -1,3 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_shuffle.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_shuffle.log 2>&1; rc=$?; echo "shuffle rc=$rc"; tail -12 gpurun_out/pytest_shuffle.log
+timeout -k 10 200 python benchmarks/gpu_shuffle.py --rows-per-gpu 8000000 --row-bytes 256 > gpurun_out/gpu_shuffle.log 2>&1; echo "rc=$?"; tail -2 gpurun_out/gpu_shuffle.log
