@@ -1,3 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 200 python benchmarks/gpu_shuffle.py --rows-per-gpu 8000000 --row-bytes 256 > gpurun_out/gpu_shuffle.log 2>&1; echo "rc=$?"; tail -2 gpurun_out/gpu_shuffle.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_all.log 2>&1; rc=$?; echo "gpu tests rc=$rc"; tail -4 gpurun_out/pytest_gpu_all.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -2 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; echo "bench rc=$?"; tail -1 gpurun_out/bench.log | cut -c1-400
