@@ -250,6 +250,10 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("b1"), py::arg("W2"), py::arg("w2s"), py::arg("b2"), py::arg("h1"), py::arg("h2"), py::arg("stream"),
      py::arg("dbg") = 0);
   m.def("nature_trunk_partial_floats", &nature_trunk_partial_floats);
+  m.def("dense_relu_fwd", [](uint64_t x, uint64_t w, uint64_t b, int64_t M, int64_t K, int N, uint64_t y,
+                             uint64_t stream) {
+    dense_relu_fwd(P<const void>(x), P<const void>(w), P<const void>(b), M, K, N, P<void>(y), S(stream));
+  });
   m.def("partition_groups", &partition_groups);
   m.def("partition_hist", [](uint64_t keys, int64_t n, int R, int mode, uint64_t counts, uint64_t stream) {
     partition_hist(P<const int64_t>(keys), n, R, mode, P<int64_t>(counts), S(stream));

@@ -112,6 +112,10 @@ void partition_hist(const int64_t* keys, int64_t n, int R, int mode, int64_t* co
 void partition_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int R, int mode,
                        const int64_t* offsets, int64_t* out_keys, void* out_vals, hipStream_t stream);
 
+// K13: y = ReLU(x Wᵀ + b), x [M,K], W [N,K] row-major bf16, K % 32 == 0, N % 16 == 0 (small-M GEMM).
+void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int64_t K, int N, void* y,
+                    hipStream_t stream);
+
 // K10: fused Nature-CNN trunk (conv 8x8/4 4->16 + conv 4x4/2 16->32, bias+ReLU) on MFMA, one
 // workgroup per frame in LDS. Frames u8 [.,4,84,84] gathered by idx (device-counter window like
 // gather_rows); weights bf16 with element strides w*s = [co, ci, ky, kx]. h1 [B,441,16] (may be

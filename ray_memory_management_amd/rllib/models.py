@@ -144,13 +144,18 @@ class _DenseFn(torch.autograd.Function):
 
 
 class _DenseHeadsFn(torch.autograd.Function):
-    """hidden = ReLU(x Wᵀ + b); heads = hidden Whᵀ + bh. Forward: two hipBLASLt GEMMs with fused
-    epilogues. Backward: ONE K12 launch (csrc/hip/dense_kernels.hip) for dx, dW, db, dWh, dbh,
+    """hidden = ReLU(x Wᵀ + b); heads = hidden Whᵀ + bh. Forward: K13 (small-M MFMA GEMM with the
+    bias+ReLU epilogue) and one hipBLASLt GEMM for the 5-wide head. Backward: ONE K12 launch (csrc/hip/dense_kernels.hip) for dx, dW, db, dWh, dbh,
     writing parameter gradients straight into their gradient buffers when they have one."""
 
     @staticmethod
     def forward(ctx, x, w, b, wh, bh):
-        hidden = torch._addmm_activation(b, x, w.t())
+        from ray_memory_management_amd._native import require_hip
+
+        M, K = x.shape
+        hidden = torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device)
+        require_hip().dense_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), M, K, w.shape[0], hidden.data_ptr(),
+                                     torch.cuda.current_stream(x.device).cuda_stream)  # K13
         heads = torch.addmm(bh, hidden, wh.t())
         ctx.save_for_backward(x, w, wh, hidden)
         ctx.gout = tuple(_grad_out(t) for t in (w, b, wh, bh))
