@@ -176,8 +176,9 @@ __device__ __forceinline__ bf16x8 frame8(const uint8_t* frame, int off) {
 __device__ __forceinline__ int kperm(int p) { return (p & ~31) + 8 * (p & 3) + ((p & 31) >> 2); }
 
 // ================================================================ forward
-// grid = B workgroups (one frame each), 256 threads = 4 waves.
-__global__ __launch_bounds__(256) void k_trunk_fwd(
+// grid = B workgroups (one frame each), NTF threads.
+constexpr int NTF = 512;  // forward: 8 waves per frame halve each wave's serial MFMA/LDS chain
+__global__ __launch_bounds__(NTF) void k_trunk_fwd(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, const unsigned short* __restrict__ W1, WStrides w1, const unsigned short* __restrict__ b1,
     const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ b2,
@@ -194,10 +195,10 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
 
   zero_lds(frame, FRAME_BYTES);
   zero_lds(h1p, H1P_ELEMS * 2);
-  stage_weight<256, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
-  stage_weight<256, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
+  stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
+  stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   __syncthreads();
-  if (!(dbg & 4)) load_frame<256>(obs + src * (C0 * H0 * H0), frame);
+  if (!(dbg & 4)) load_frame<NTF>(obs + src * (C0 * H0 * H0), frame);
 
   // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
   // j → (kx = 2g + (j>>2), ci = j&3); col = co = r: one 16-B LDS read each.
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
   __syncthreads();
 
   // ---- conv1: 28 M-tiles of 16 positions over 4 waves
-  for (int mt = wave; mt < NP1P / 16; mt += 4) {
+  for (int mt = wave; mt < NP1P / 16; mt += NTF / 64) {
     const int p = min(mt * 16 + r, NP1 - 1);
     const int oy = p / H1, ox = p - oy * H1;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
   __syncthreads();
   // h1 out for backward: coalesced 16-B rows from the LDS tile
   if (h1_out) {
-    for (int v = threadIdx.x; v < NP1 * 2; v += 256) {
+    for (int v = threadIdx.x; v < NP1 * 2; v += NTF) {
       const int p = v >> 1, y = p / H1, x = p - y * H1;
       *reinterpret_cast<uint4*>(&h1_out[(b * NP1 + p) * C1 + 8 * (v & 1)]) =
           *reinterpret_cast<const uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1)]);
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
   unsigned short* h2s = reinterpret_cast<unsigned short*>(frame);  // frame is dead after conv1
 
   // ---- conv2: 8 M-tiles (wave w: w, w+4) x 2 N-tiles
-  for (int mt = wave; mt < NP2P / 16; mt += 4) {
+  for (int mt = wave; mt < NP2P / 16; mt += NTF / 64) {
     const int q = min(mt * 16 + r, NP2 - 1);
     const int oy = q / H2, ox = q - oy * H2;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(256) void k_trunk_fwd(
     }
   }
   __syncthreads();
-  for (int v = threadIdx.x; v < NP2 * C2 / 8; v += 256)
+  for (int v = threadIdx.x; v < NP2 * C2 / 8; v += NTF)
     *reinterpret_cast<uint4*>(&h2_out[b * NP2 * C2 + 8 * v]) = *reinterpret_cast<const uint4*>(&h2s[8 * v]);
 }
 
@@ -574,7 +575,7 @@ void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                       const void* b2, void* h1, void* h2, hipStream_t stream, int dbg) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
-  hipLaunchKernelGGL(trunk::k_trunk_fwd, dim3(uint32_t(B)), dim3(256), 0, stream, obs, idx, ctr, period, B,
+  hipLaunchKernelGGL(trunk::k_trunk_fwd, dim3(uint32_t(B)), dim3(trunk::NTF), 0, stream, obs, idx, ctr, period, B,
                      static_cast<const unsigned short*>(W1), ws(w1s), static_cast<const unsigned short*>(b1),
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(b2),
                      static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2), dbg);
