@@ -15,7 +15,8 @@
 //         M=121 x N=32 x K=256 from LDS, bias+ReLU → h2.  1 launch.
 //   bwd:  dpre2 = dh2·[h2>0] (+db2), dW2 += dpre2ᵀ·im2col(h1) (K = positions), dh1 = conv2ᵀ by
 //         stride-parity class (each class is a dense K=4 taps x 32 GEMM), dpre1 = dh1·[h1>0]
-//         (+db1), dW1 += dpre1ᵀ·im2col(frame). Weight-grad accumulators stay in registers across
+//         (+db1), dW1 += dpre1ᵀ·im2col(frame) computed in space-to-depth form (a 2x2 stride-1
+//         correlation over a 64-channel 22x22 grid: contiguous operands). Weight-grad accumulators stay in registers across
 //         the frames a workgroup owns; one deterministic reduce launch sums the per-workgroup
 //         partials and writes bf16 grads in the parameters' memory order.  2 launches.
 // The 1/255 frame scale is applied to the fp32 conv1 accumulator (exact integer pixels in bf16).
@@ -97,10 +98,17 @@ __device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint
   }
 }
 
-// Backward variant: the same transpose, stored as bf16 (exact for 0..255) so the weight-grad
-// gathers need no per-use conversion: pixel (y, x) channel c at element ((y+2)*88 + x+2)*4 + c.
+// Backward variant: the padded frame in space-to-depth form, transposed, bf16 (exact for 0..255):
+// padded pixel (yp, xp) = (y+2, x+2) = (4Y+ry, 4X+rx), channel ci → st[c][Y*ST_W + X] with
+// c = 16ry + 4rx + ci. conv1 (8x8/4) is then a 2x2 stride-1 correlation over a 64-channel 22x22
+// grid: ky = 4a+ry, kx = 4b+rx, input (Y, X) = (oy+a, ox+b). Its weight gradient reduces over
+// grid positions, which are CONTIGUOUS per channel here (one 16-B LDS read per MFMA operand
+// instead of 8 strided 2-B gathers). Row pitch ST_W = 24 (3 chunks of 8), 23 rows (row 22 and
+// columns 22, 23 stay zero: K padding), channel pitch 552 el = 276 dwords (8 lanes reading 8
+// channels hit distinct 4-bank groups).
+constexpr int ST_W = 24, ST_CP = 23 * ST_W, ST_C = 64;
 template <int NT>
-__device__ __forceinline__ void load_frame_bf16(const uint8_t* __restrict__ src, unsigned short* frame) {
+__device__ __forceinline__ void load_frame_s2d(const uint8_t* __restrict__ src, unsigned short* st) {
   constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
   uint32_t v[PER][C0];
@@ -116,16 +124,15 @@ __device__ __forceinline__ void load_frame_bf16(const uint8_t* __restrict__ src,
   for (int k = 0; k < PER; k++) {
     const int o = threadIdx.x + NT * k;
     if (o < NW) {
-      const int y = o / 21, x = 4 * (o - y * 21);
-      uint32_t w[8];  // 4 pixels x 4 channels of bf16, two per word
+      const int y = o / 21, xw = o - y * 21;  // pixels x = 4xw .. 4xw+3 → xp = 4xw+2 .. 4xw+5
+      const int yp = y + 2;
+      unsigned short* row = st + (16 * (yp & 3)) * ST_CP + (yp >> 2) * ST_W + xw;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        w[2 * q] = uint32_t(u8bf((v[k][0] >> (8 * q)) & 0xffu)) | (uint32_t(u8bf((v[k][1] >> (8 * q)) & 0xffu)) << 16);
-        w[2 * q + 1] = uint32_t(u8bf((v[k][2] >> (8 * q)) & 0xffu)) | (uint32_t(u8bf((v[k][3] >> (8 * q)) & 0xffu)) << 16);
+        const int rx = (q + 2) & 3, dX = (q + 2) >> 2;  // compile-time after unrolling
+#pragma unroll
+        for (int c = 0; c < C0; c++) row[(4 * rx + c) * ST_CP + dX] = u8bf((v[k][c] >> (8 * q)) & 0xffu);
       }
-      uint4* d = reinterpret_cast<uint4*>(frame + ((y + 2) * P0 + x + 2) * 4);  // 16-B aligned
-      d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-      d[1] = make_uint4(w[4], w[5], w[6], w[7]);
     }
   }
 }
@@ -284,7 +291,16 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
 constexpr int PART = C1 * 256 + C2 * 256 + C1 + C2;  // per-workgroup fp32 partial: dW1, dW2, db1, db2
 // row pitches of the transposed dpre tiles: +8 elements so the 16 rows written by one lane
 // group land 4 dwords apart (2-way instead of 16-way bank conflicts) while keeping 16-B reads
-constexpr int DP2_PITCH = NP2P + 8, DP1_PITCH = NP1P + 8;
+constexpr int DP2_PITCH = NP2P + 8;
+// dpre2 in a 12x12 grid (row/column 11 zero) so the dh1 taps read it without bounds branches
+constexpr int D2W = 12;
+// dpre1 for the dW1 GEMM: two copies (b = 0, 1) [co][Yrow*24 + X] = dpre1[Yrow-1][X-b], zero
+// elsewhere, so input-grid position t = Y*24+X pairs with copy b at t + (1-a)*24 (a, b = the
+// space-to-depth tap offsets). 24 rows; co pitch 584 el = 292 dwords (conflict-free 16-B reads).
+constexpr int DB_CP = 24 * ST_W + 8, DB_B = 16 * DB_CP;
+constexpr int KSTEPS1 = (22 * ST_W + 31) / 32;  // 17 K-steps of 32 grid positions
+static_assert(KSTEPS1 * 32 + 8 <= ST_CP, "st K padding");
+static_assert(KSTEPS1 * 32 + ST_W <= 24 * ST_W, "dpre1 copy K padding");
 
 // grid = G workgroups of 8 waves (2 per SIMD hide the LDS/MFMA latency chains of one frame),
 // each loops over frames b = blockIdx.x, +G, ...
@@ -294,24 +310,24 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     int64_t B, const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ h1,
     const unsigned short* __restrict__ h2, const unsigned short* __restrict__ dh2, float* __restrict__ partial,
     int dbg) {
-  __shared__ __attribute__((aligned(16))) unsigned short frame[FRAME_BYTES];  // bf16 HWC
+  __shared__ __attribute__((aligned(16))) unsigned short st[ST_C * ST_CP];  // space-to-depth frame
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
-  __shared__ __attribute__((aligned(16))) unsigned short dp2[NP2P * C2];    // [q][co2]
+  __shared__ __attribute__((aligned(16))) unsigned short dp2[D2W * D2W * C2];  // [oy*12+ox][co2]
   __shared__ __attribute__((aligned(16))) unsigned short dp2t[C2 * DP2_PITCH];   // [co2][kperm(q)]
-  __shared__ __attribute__((aligned(16))) unsigned short dp1t[C1 * DP1_PITCH];   // [ci][kperm(p)]
+  __shared__ __attribute__((aligned(16))) unsigned short dp1s[2 * DB_B];       // dpre1 copies b = 0, 1
   __shared__ float red[8 * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short w2s[C2 * W2_PITCH];
+  static_assert(C2 * W2_PITCH <= 2 * DB_B, "w2s aliases the dpre1 copies");
+  unsigned short* w2s = dp1s;  // only read before the frame loop (into wt registers)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int64_t* idx = window(idx0, ctr, period, B);
   if (dbg & 64) return;
 
-  if (!(dbg & 32)) zero_lds(frame, FRAME_BYTES * 2);
+  if (!(dbg & 32)) zero_lds(st, ST_C * ST_CP * 2);
   stage_weight<NTB, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   zero_lds(h1p, H1P_ELEMS * 2);
-  zero_lds(dp2, NP2P * C2 * 2);
+  zero_lds(dp2, D2W * D2W * C2 * 2);
   zero_lds(dp2t, C2 * DP2_PITCH * 2);
-  zero_lds(dp1t, C1 * DP1_PITCH * 2);
 
   // dh1 = conv2ᵀ(dpre2): waves 2c, 2c+1 own stride-parity class c = (py, px). In a class,
   // input pixel (y, x) = (2a+py, 2c+px) receives taps ky ∈ {py, py+2}, kx ∈ {px, px+2} from
@@ -319,6 +335,9 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   const int cls = wave >> 1, half = wave & 1;
   const int py = cls >> 1, px = cls & 1;
   const int nrow = py ? 10 : 11, ncol = px ? 10 : 11, ncls = nrow * ncol;
+  // m / ncol for m < 200 as a multiply-shift (ncol is wave-uniform but not compile-time: a real
+  // division is ~30 VALU ops, and the dh1 loop does five per tile)
+  const uint32_t cdiv = px ? 6554u : 5958u;
   __syncthreads();  // w2s staged
   bf16x8 wt[4];
 #pragma unroll
@@ -329,7 +348,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     for (int j = 0; j < 8; j++) v[j] = w2s[(8 * g + j) * W2_PITCH + (ky * 4 + kx) * 16 + r];
     wt[t] = as_bf(v);
   }
-  f32x4 aw2[2][2], aw1[2];  // dW2 tiles (mt 0/1 x nt w+8i), dW1 tiles (nt w+8i)
+  f32x4 aw2[2][2], aw1[2];  // dW2 tiles (mt 0/1 x nt w+8i), dW1 tiles (b = 0, 1; see P2)
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     aw1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -338,12 +357,14 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   }
   float db1 = 0.f;                       // this lane's ci = r
   float db2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // co2 = 8(tid&3) + j
+  __syncthreads();  // wt read from w2s
+  zero_lds(dp1s, 2 * DB_B * 2);
   __syncthreads();
 
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
     const int64_t src = idx ? idx[b] : b;
     // ---- P0: stage frame, h1, dpre2
-    if (!(dbg & 8)) load_frame_bf16<NTB>(obs + src * (C0 * H0 * H0), frame);
+    if (!(dbg & 8)) load_frame_s2d<NTB>(obs + src * (C0 * H0 * H0), st);
     if (!(dbg & 8)) {  // h1 [441][16] → padded LDS tile; h2, dh2 → dpre2 (both layouts) + db2. Loads first.
       constexpr int NH1 = NP1 * 2, PH1 = (NH1 + NTB - 1) / NTB;  // 882 x 16 B
       constexpr int NH2 = NP2 * 4, PH2 = (NH2 + NTB - 1) / NTB;  // 484 x 16 B
@@ -372,7 +393,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
       for (int k = 0; k < PH2; k++) {
         const int v = threadIdx.x + NTB * k;
         if (v < NH2) {
-          const int q = v >> 2, c0 = 8 * (v & 3);
+          const int q = v >> 2, c0 = 8 * (v & 3), oy = q / H2, ox = q - oy * H2;
           u16x8 o;
 #pragma unroll
           for (int j = 0; j < 8; j++) {
@@ -382,7 +403,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
             db2[j] += bf2f(d);
             dp2t[(c0 + j) * DP2_PITCH + kperm(q)] = d;
           }
-          *reinterpret_cast<u16x8*>(&dp2[q * C2 + c0]) = o;
+          *reinterpret_cast<u16x8*>(&dp2[(oy * D2W + ox) * C2 + c0]) = o;
         }
       }
     }
@@ -419,57 +440,46 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     }
     // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 → dp1t, db1
     for (int mt = half; mt * 16 < ((dbg & 2) ? 0 : ncls); mt += 2) {
-      const int m = mt * 16 + r;
-      const int a = m / ncol, c = m - a * ncol;
+      const int m = min(mt * 16 + r, ncls - 1);  // rows >= ncls are computed but not stored
+      const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < 4; t++) {
+      for (int t = 0; t < 4; t++) {  // oy = a+1-ty, ox = c+1-tx ∈ [0, 11]; row/col 11 of dp2 is zero
         const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
-        u16x8 av = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (m < ncls && oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
-          av = *reinterpret_cast<const u16x8*>(&dp2[(oy * H2 + ox) * C2 + 8 * g]);
+        const u16x8 av = *reinterpret_cast<const u16x8*>(&dp2[(oy * D2W + ox) * C2 + 8 * g]);
         acc = mfma(as_bf(av), wt[t], acc);
       }
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int mm = mt * 16 + 4 * g + i;
         if (mm < ncls) {
-          const int aa = mm / ncol, cc = mm - aa * ncol;
+          const int aa = int((uint32_t(mm) * cdiv) >> 16), cc = mm - aa * ncol;
           const int y = 2 * aa + py, x = 2 * cc + px;
           const unsigned short hv = h1p[((y + 2) * P1 + (x + 2)) * C1 + r];
           const float d = (hv != 0 && !(hv & 0x8000)) ? acc[i] : 0.f;
           const unsigned short db = f2bf(d);
           db1 += bf2f(db);
-          dp1t[r * DP1_PITCH + kperm(y * H1 + x)] = db;
+          dp1s[r * DB_CP + (y + 1) * ST_W + x] = db;
+          dp1s[DB_B + r * DB_CP + (y + 1) * ST_W + x + 1] = db;
         }
       }
     }
     __syncthreads();
 
-    // ---- P2: dW1[co][k=(ky,kx,ci)] += Σ_p dpre1[p][co] · frame[4oy+ky][4ox+kx][ci] / 255
-#pragma unroll 2
-    for (int s = 0; s < ((dbg & 4) ? 0 : NP1P / 32); s++) {
-      const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(&dp1t[r * DP1_PITCH + 32 * s + 8 * g]));
-      int poff[8];  // positions p = 32s + g + 4j → byte offset of (4oy, 4ox) in the HWC frame
-      {
-        const int p0 = 32 * s + g;
-        int oy = p0 / H1, ox = p0 - oy * H1;
+    // ---- P2: dW1 in space-to-depth form: D[(a, b, c)][co] = Σ_t st[c][t] · dpre1_b[co][t + (1-a)*24]
+    // over grid positions t (K). Wave w: channel block cb = w&3 (16 channels), a = w>>2, b = 0, 1
+    // share the st operand.
+    {
+      const int cb = wave & 3, a = wave >> 2;
+      const unsigned short* sa = st + (16 * cb + r) * ST_CP + 8 * g;
+      const unsigned short* d0 = dp1s + r * DB_CP + (1 - a) * ST_W + 8 * g;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-          poff[j] = (p0 + 4 * j < NP1) ? (oy * 4 * P0 + ox * 4) * 4 : 0;  // elements; dpre1 is 0 there
-          ox += 4;
-          if (ox >= H1) { ox -= H1; oy++; }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; i++) {
-        const int k = (wave + 8 * i) * 16 + r;
-        const int ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
-        const unsigned short* base = frame + (ky * P0 + kx) * 4 + ci;
-        u16x8 bv;
-#pragma unroll
-        for (int j = 0; j < 8; j++) bv[j] = base[poff[j]];
-        aw1[i] = mfma(a, as_bf(bv), aw1[i]);
+      for (int s = 0; s < ((dbg & 4) ? 0 : KSTEPS1); s++) {
+        const bf16x8 av = as_bf(*reinterpret_cast<const u16x8*>(sa + 32 * s));
+        const bf16x8 b0 = as_bf(*reinterpret_cast<const u16x8*>(d0 + 32 * s));
+        const bf16x8 b1 = as_bf(*reinterpret_cast<const u16x8*>(d0 + DB_B + 32 * s));
+        aw1[0] = mfma(av, b0, aw1[0]);
+        aw1[1] = mfma(av, b1, aw1[1]);
       }
     }
     __syncthreads();
@@ -485,10 +495,17 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       const int row = 4 * g + e;
-      out[row * 256 + col] = aw1[i][e] * (1.0f / 255.0f);
       out[C1 * 256 + row * 256 + col] = aw2[0][i][e];
       out[C1 * 256 + (16 + row) * 256 + col] = aw2[1][i][e];
     }
+  }
+  // dW1: tile b holds D[m = 4g+e][co = r], channel c = 16cb + m → ry = cb, rx = g, ci = e;
+  // ky = 4a + ry, kx = 4b + rx, k = 32ky + 4kx + ci
+#pragma unroll
+  for (int bb = 0; bb < ((dbg & 16) ? 0 : 2); bb++) {
+    const int ky = 4 * (wave >> 2) + (wave & 3), kx = 4 * bb + g;
+#pragma unroll
+    for (int e = 0; e < 4; e++) out[r * 256 + ky * 32 + kx * 4 + e] = aw1[bb][e] * (1.0f / 255.0f);
   }
   // db1: lanes r, r+16, r+32, r+48 of every wave share ci = r
   db1 += __shfl_xor(db1, 16);

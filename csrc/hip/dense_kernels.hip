@@ -326,6 +326,279 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd(
   }
 }
 
+// ---------------------------------------------------------------- K12 (transposed-read form)
+// Same outputs as above, restructured after PMC + phase timing showed the per-chunk critical
+// path (u16 scatter transposes into LDS, two barriers per 32-row chunk, and workgroup 0 carrying
+// the head gradients on top of its column block) set the time: ~1.8 µs per chunk.
+//  * Operands that must be reduced over rows (dpreᵀ, xᵀ, dzᵀ, hiddenᵀ) are read from ROW-MAJOR LDS
+//    images with gfx950's ds_read_b64_tr_b16 (a 4-row x 16-column block per 16-lane group,
+//    delivered column-wise): staging is plain coalesced 16-B loads + ds_write_b128, no VALU
+//    transposes. The k order inside a step is permuted (lane group g takes rows 4g..4g+3 and
+//    16+4g..16+4g+3) identically for both operands: a 32-lane half then reads 8 consecutive rows,
+//    conflict-free at row pitch 272 (136 dwords ≡ 8 mod 64).
+//  * 64-row chunks, double-buffered LDS, ONE barrier per chunk; next-next chunk's loads in flight.
+//  * dx is computed as dxᵀ tiles (A = Wᵀ fragments kept in registers for the whole launch), so a
+//    lane's 4 outputs are 4 consecutive columns: one 8-byte LDS store.
+//  * The head gradients (dWh, db, dbh) run in their own extra workgroup (index K/32).
+constexpr int MC2 = 64;       // rows per chunk
+constexpr int DMP = H + 16;   // dpre / hidden image row pitch (b128 row reads P=2 slots, tr reads conflict-free)
+constexpr int DXP = JB + 8;   // dx block pitch (8-byte stores: 2-way at most, 16-B aligned rows)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 tr4(const unsigned short* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+// A/B fragment from two transposed reads: elements 0-3 from block p0, 4-7 from block p1
+__device__ __forceinline__ bf16x8 tr8(const unsigned short* p0, const unsigned short* p1) {
+  const s16x4 a = tr4(p0), b = tr4(p1);
+  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// ok ? v : 0 per component (a ternary on the uint4 struct is lowered through a stack copy: scratch)
+__device__ __forceinline__ uint4 keep_if(bool ok, uint4 v) {
+  return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
+}
+
+constexpr int K12_LDS_DM = 2 * MC2 * DMP;                 // elements, both roles
+constexpr int K12_WS = 2 * H * 16, K12_XS = 2 * 2 * MC2 * 16, K12_DXS = MMAX * DXP;
+constexpr int K12_YS = 2 * MC2 * DMP, K12_DZS = MMAX * 16;
+constexpr int K12_RB = (K12_WS + K12_XS + K12_DXS) > (K12_YS + K12_DZS) ? (K12_WS + K12_XS + K12_DXS)
+                                                                       : (K12_YS + K12_DZS);
+static_assert((K12_LDS_DM + K12_RB) * 2 <= 160 * 1024, "K12 LDS");
+
+// column-block role: dx[:, J] and dW[:, J] for J = [J0, J0+32)
+__device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
+                                         const unsigned short* __restrict__ dpre, int64_t M, int64_t K, int64_t J0,
+                                         unsigned short* __restrict__ dx, unsigned short* __restrict__ dw,
+                                         unsigned short* dm, unsigned short* rb) {
+  unsigned short* ws = rb;                    // [jt][h][16]  W[:, J] (setup only)
+  unsigned short* xs = rb + K12_WS;           // [buf][jt][m][16]
+  unsigned short* dxs = rb + K12_WS + K12_XS; // [m][DXP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int q = r >> 2, p = r & 3;
+  const int NC = int((M + MC2 - 1) / MC2);
+
+  uint4 sd[4], sx;
+  auto load = [&](int c) {  // unconditional clamped loads (rows >= M are zeroed at the LDS store)
+    const int64_t m0 = int64_t(c) * MC2;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const int64_t rr = min(m0 + row, M - 1);
+      sd[k] = *reinterpret_cast<const uint4*>(&dpre[rr * H + 8 * pc]);
+    }
+    const int row = (tid >> 2) & (MC2 - 1), pc = tid & 3;  // threads 256.. duplicate 0..255 (not stored)
+    sx = *reinterpret_cast<const uint4*>(&x[min(m0 + row, M - 1) * K + J0 + 8 * pc]);
+  };
+  auto store = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC2;
+    unsigned short* d = dm + (c & 1) * MC2 * DMP;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      *reinterpret_cast<uint4*>(&d[row * DMP + 8 * pc]) = keep_if(m0 + row < M, sd[k]);
+    }
+    if (tid < MC2 * 4) {
+      const int row = tid >> 2, pc = tid & 3;
+      *reinterpret_cast<uint4*>(&xs[(((c & 1) * 2 + (pc >> 1)) * MC2 + row) * 16 + 8 * (pc & 1)]) =
+          keep_if(m0 + row < M, sx);
+    }
+  };
+
+  {  // W[:, J] → ws (two 16-column halves, row-major over h)
+    uint4 wv[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int v = tid + NT * k, h = v >> 2, pc = v & 3;
+      wv[k] = *reinterpret_cast<const uint4*>(&w[int64_t(h) * K + J0 + 8 * pc]);
+    }
+    load(0);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int v = tid + NT * k, h = v >> 2, pc = v & 3;
+      *reinterpret_cast<uint4*>(&ws[((pc >> 1) * H + h) * 16 + 8 * (pc & 1)]) = wv[k];
+    }
+  }
+  store(0);
+  if (NC > 1) load(1);
+  lds_barrier();
+
+  // Wᵀ fragments for this wave's column tile nt: A[row j = 16nt + r][k = h = 32s + 8g + e]
+  const int mt = wave >> 1, nt = wave & 1;
+  bf16x8 wf[H / 32];
+#pragma unroll
+  for (int s = 0; s < H / 32; s++) {
+    const unsigned short* p0 = &ws[(nt * H + 32 * s + 8 * g + q) * 16 + 4 * p];
+    wf[s] = tr8(p0, p0 + 4 * 16);
+  }
+  f32x4 adw[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) adw[i][0] = adw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c = 0; c < NC; c++) {
+    const unsigned short* d = dm + (c & 1) * MC2 * DMP;
+    const unsigned short* xb = xs + (c & 1) * 2 * MC2 * 16;
+    {  // dxᵀ tile: D[j][m] = Σ_h Wᵀ[j][h] · dpre[m][h]  (B = dpre row reads)
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      const unsigned short* drow = d + (16 * mt + r) * DMP + 8 * g;
+#pragma unroll
+      for (int s = 0; s < H / 32; s += 2) {
+        a0 = mfma(wf[s], as_bf(*reinterpret_cast<const u16x8*>(drow + 32 * s)), a0);
+        a1 = mfma(wf[s + 1], as_bf(*reinterpret_cast<const u16x8*>(drow + 32 * s + 32)), a1);
+      }
+      const f32x4 t = a0 + a1;
+      const uint2 o = make_uint2(uint32_t(f2bf(t[0])) | (uint32_t(f2bf(t[1])) << 16),
+                                 uint32_t(f2bf(t[2])) | (uint32_t(f2bf(t[3])) << 16));
+      *reinterpret_cast<uint2*>(&dxs[(c * MC2 + 16 * mt + r) * DXP + 16 * nt + 4 * g]) = o;
+    }
+    // dW[h][j] += Σ_m dpre[m][h] x[m][j]: both operands by transposed reads (permuted k order)
+#pragma unroll
+    for (int ks = 0; ks < MC2 / 32; ks++) {
+      bf16x8 bx[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; jt++) {
+        const unsigned short* p0 = &xb[(jt * MC2 + 32 * ks + 4 * g + q) * 16 + 4 * p];
+        bx[jt] = tr8(p0, p0 + 16 * 16);
+      }
+#pragma unroll
+      for (int hi = 0; hi < 2; hi++) {
+        const unsigned short* p0 = &d[(32 * ks + 4 * g + q) * DMP + 16 * (wave + 8 * hi) + 4 * p];
+        const bf16x8 ad = tr8(p0, p0 + 16 * DMP);
+        adw[hi][0] = mfma(ad, bx[0], adw[hi][0]);
+        adw[hi][1] = mfma(ad, bx[1], adw[hi][1]);
+      }
+    }
+    if (c + 1 < NC) store(c + 1);  // loaded one chunk ago
+    if (c + 2 < NC) load(c + 2);   // in flight across the barrier and the next chunk's MFMAs
+    lds_barrier();
+  }
+
+  for (int v = tid; v < int(M) * (JB / 8); v += NT) {
+    const int row = v >> 2, pc = v & 3;
+    *reinterpret_cast<uint4*>(&dx[int64_t(row) * K + J0 + 8 * pc]) = *reinterpret_cast<const uint4*>(&dxs[row * DXP + 8 * pc]);
+  }
+#pragma unroll
+  for (int hi = 0; hi < 2; hi++)
+#pragma unroll
+    for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + J0 + 16 * jt + r] = f2bf(adw[hi][jt][i]);
+}
+
+// head role: dWh = dheadsᵀ hidden [A1, 256], db = Σ_m dpre, dbh = Σ_m dheads
+template <int A1>
+__device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, const unsigned short* __restrict__ y,
+                                         const unsigned short* __restrict__ dpre, int64_t M,
+                                         unsigned short* __restrict__ db, unsigned short* __restrict__ dwh,
+                                         unsigned short* __restrict__ dbh, unsigned short* dm, unsigned short* rb) {
+  unsigned short* ys = rb;            // [buf][m][DMP]
+  unsigned short* dzs = rb + K12_YS;  // [m][16] (a >= A1 and rows >= M zero)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int q = r >> 2, p = r & 3;
+  const int NC = int((M + MC2 - 1) / MC2);
+
+  uint4 sd[4], sy[4];
+  auto load = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC2;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const int64_t rr = min(m0 + row, M - 1);
+      sd[k] = *reinterpret_cast<const uint4*>(&dpre[rr * H + 8 * pc]);
+      sy[k] = *reinterpret_cast<const uint4*>(&y[rr * H + 8 * pc]);
+    }
+  };
+  auto store = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC2;
+    const int o = (c & 1) * MC2 * DMP;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const bool ok = m0 + row < M;
+      *reinterpret_cast<uint4*>(&dm[o + row * DMP + 8 * pc]) = keep_if(ok, sd[k]);
+      *reinterpret_cast<uint4*>(&ys[o + row * DMP + 8 * pc]) = keep_if(ok, sy[k]);
+    }
+  };
+  {
+    constexpr int PZ = MMAX * 16 / NT;  // 20
+    unsigned short zv[PZ];
+#pragma unroll
+    for (int k = 0; k < PZ; k++) {
+      const int e = tid + NT * k, m = e >> 4, a = e & 15;
+      zv[k] = dz[int64_t(min(int64_t(m), M - 1)) * A1 + min(a, A1 - 1)];
+    }
+    load(0);
+#pragma unroll
+    for (int k = 0; k < PZ; k++) {
+      const int e = tid + NT * k, m = e >> 4, a = e & 15;
+      dzs[e] = (m < M && a < A1) ? zv[k] : static_cast<unsigned short>(0);
+    }
+  }
+  store(0);
+  if (NC > 1) load(1);
+  lds_barrier();
+
+  u16x8 onev;
+#pragma unroll
+  for (int j = 0; j < 8; j++) onev[j] = (r == 0) ? static_cast<unsigned short>(0x3f80) : static_cast<unsigned short>(0);
+  const bf16x8 ones = as_bf(onev);  // as A: row 0 all ones; as B: column 0 all ones
+  f32x4 awh[2], adb[2], abh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 2; i++) awh[i] = adb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c = 0; c < NC; c++) {
+    const int o = (c & 1) * MC2 * DMP;
+#pragma unroll
+    for (int ks = 0; ks < MC2 / 32; ks++) {
+      const unsigned short* pz = &dzs[(c * MC2 + 32 * ks + 4 * g + q) * 16 + 4 * p];
+      const bf16x8 az = tr8(pz, pz + 16 * 16);  // A[row a = r][k = m]
+#pragma unroll
+      for (int hi = 0; hi < 2; hi++) {
+        const int off = o + (32 * ks + 4 * g + q) * DMP + 16 * (wave + 8 * hi) + 4 * p;
+        const bf16x8 by = tr8(&ys[off], &ys[off + 16 * DMP]);
+        const bf16x8 bd = tr8(&dm[off], &dm[off + 16 * DMP]);
+        awh[hi] = mfma(az, by, awh[hi]);
+        adb[hi] = mfma(ones, bd, adb[hi]);
+      }
+      if (wave == 0) abh = mfma(az, ones, abh);
+    }
+    if (c + 1 < NC) store(c + 1);
+    if (c + 2 < NC) load(c + 2);
+    lds_barrier();
+  }
+#pragma unroll
+  for (int hi = 0; hi < 2; hi++) {
+    const int h = 16 * (wave + 8 * hi) + r;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * g + i < A1) dwh[(4 * g + i) * H + h] = f2bf(awh[hi][i]);
+    if (g == 0) db[h] = f2bf(adb[hi][0]);
+  }
+  if (wave == 0 && r == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * g + i < A1) dbh[4 * g + i] = f2bf(abh[i]);
+  }
+}
+
+template <int A1>
+__global__ __launch_bounds__(NT) void k_dense_heads_bwd2(
+    const unsigned short* __restrict__ dz, const unsigned short* __restrict__ y, const unsigned short* __restrict__ x,
+    const unsigned short* __restrict__ w, const unsigned short* __restrict__ dpre, int64_t M, int64_t K,
+    unsigned short* __restrict__ dx, unsigned short* __restrict__ dw, unsigned short* __restrict__ db,
+    unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh) {
+  __shared__ __attribute__((aligned(16))) unsigned short dm[K12_LDS_DM];
+  __shared__ __attribute__((aligned(16))) unsigned short rb[K12_RB];
+  if (int64_t(blockIdx.x) * JB == K)
+    k12_head<A1>(dz, y, dpre, M, db, dwh, dbh, dm, rb);
+  else
+    k12_cols(x, w, dpre, M, K, int64_t(blockIdx.x) * JB, dx, dw, dm, rb);
+}
+
 // K13: hidden = ReLU(x Wᵀ + b) for small M (PPO minibatch / rollout batch). One 4-wave workgroup
 // per 16x16 output tile, K split over the waves and streamed straight from L2 with 4 independent
 // accumulator chains and 8 x 16-B loads in flight per lane. A (16 rows of x) and B (16 rows of W) fragments are both contiguous
@@ -398,14 +671,22 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   if (M > dense::MMAX) throw std::invalid_argument("dense_heads_bwd: at most 640 rows per call");
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
   auto V = [](void* p) { return static_cast<unsigned short*>(p); };
-  const dim3 grid(uint32_t(K / dense::JB)), block(dense::NT);
+  const dim3 grid(uint32_t(K / dense::JB)), grid2(uint32_t(K / dense::JB + 1)), block(dense::NT);
+  static const bool v2 = [] {  // RMM_K12_V1=1 selects the first (LDS-transpose) version, for A/B timing
+    const char* e = std::getenv("RMM_K12_V1");
+    return !(e && e[0] == '1');
+  }();
   const dim3 pgrid(uint32_t((M + dense::MC - 1) / dense::MC));
   auto* dp = V(dpre_scratch);
 #define RMM_K12(N)                                                                                               \
   case N:                                                                                                        \
     hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);              \
-    hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w), dp,  \
-                       M, K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                               \
+    if (v2)                                                                                                      \
+      hipLaunchKernelGGL(dense::k_dense_heads_bwd2<N>, grid2, block, 0, stream, U(dz), U(y), U(x), U(w), dp, M, \
+                         K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                                \
+    else                                                                                                         \
+      hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w),   \
+                         dp, M, K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                         \
     break;
   switch (A1) {
     RMM_K12(1) RMM_K12(2) RMM_K12(3) RMM_K12(4) RMM_K12(5) RMM_K12(6) RMM_K12(7) RMM_K12(8)

@@ -244,7 +244,7 @@ def test_dense_fn_matches_linear(cuda):
         assert float((a.float() - b).abs().max() / b.abs().max()) < 2e-2
 
 
-@pytest.mark.parametrize("M,K,A1", [(500, 3872, 5), (37, 96, 7), (64, 64, 1)])
+@pytest.mark.parametrize("M,K,A1", [(500, 3872, 5), (37, 96, 7), (64, 64, 1), (130, 64, 16), (640, 96, 3)])
 def test_dense_heads_bwd_matches_fp32(cuda, M, K, A1):
     """K12 fused dense+heads backward vs fp32 autograd of ReLU(x Wᵀ+b) Whᵀ+bh (same bf16 inputs)."""
     from ray_memory_management_amd.rllib.models import dense_heads
