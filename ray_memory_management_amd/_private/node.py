@@ -264,7 +264,21 @@ class Head:
         # in flight); the task itself is retried when its worker's death is processed
         for t in list(self.tasks.values()):
             if t.node == node_id and t.state == RUNNING:
-                for oid in self.recovery.returns_of(t.spec):
+                rets = self.recovery.returns_of(t.spec)
+                try:
+                    sealed = bool(rets) and all(self.store.contains(o) for o in rets)
+                except Exception:
+                    sealed = False
+                if sealed and t.spec.get("actor_id") is None and not t.spec.get("actor_creation"):
+                    # the task sealed its returns but its TaskDone is still in flight: it finished on
+                    # this node, so record it (lineage) and let node_removed below treat its
+                    # returns as lost with the node
+                    if t.worker is not None and t.worker.task == t.spec["task_id"]:
+                        t.worker.task = None
+                    self._release_task_resources(t)
+                    self._finish(t, FINISHED)
+                    continue
+                for oid in rets:
                     try:
                         self.store.delete([oid])
                     except Exception:

@@ -28,6 +28,16 @@ def _node(cluster, tag):
     return cluster.add_node(num_cpus=2, resources={tag: 2})
 
 
+def _settle(timeout=10.0):
+    """Wait until the head has processed every TaskDone: an object is readable as soon as it is
+    sealed, slightly before the head learns that its task ended (and records its lineage)."""
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if all(t["state"] not in ("PENDING", "RUNNING") for t in _state("tasks")):
+            return
+        time.sleep(0.01)
+
+
 def test_basic_reconstruction(cluster, tmp_path):
     n = _node(cluster, "worker")
     counter = tmp_path / "count"
@@ -40,6 +50,7 @@ def test_basic_reconstruction(cluster, tmp_path):
 
     ref = big.remote(str(counter))
     assert int(ray.get(ref)[5]) == 7
+    _settle()
     cluster.remove_node(n)
     _node(cluster, "worker")
     out = ray.get(ref, timeout=60)
@@ -61,6 +72,7 @@ def test_reconstruction_chain(cluster):
     assert float(ray.get(c)[0]) == 3.0
     del a, b  # intermediate refs go out of scope: lineage is still pinned by c
     time.sleep(0.3)
+    _settle()
     cluster.remove_node(n)
     _node(cluster, "worker")
     assert float(ray.get(c, timeout=60)[0]) == 3.0
@@ -78,6 +90,7 @@ def test_multiple_returns_reconstructed_once(cluster, tmp_path):
 
     x, y = two.remote(str(counter))
     ray.get([x, y])
+    _settle()
     cluster.remove_node(n)
     _node(cluster, "worker")
     assert float(ray.get(y, timeout=60)[0]) == 2.0 and float(ray.get(x, timeout=60)[0]) == 1.0
@@ -93,6 +106,7 @@ def test_no_retries_raises_object_lost(cluster):
 
     ref = f.remote()
     ray.get(ref)
+    _settle()
     cluster.remove_node(n)
     with pytest.raises(exc.ObjectLostError):
         ray.get(ref, timeout=30)
@@ -107,9 +121,11 @@ def test_retry_budget_exhausted(cluster):
 
     ref = f.remote()
     ray.get(ref)
+    _settle()
     cluster.remove_node(n)
     n2 = _node(cluster, "worker")
     assert int(ray.get(ref, timeout=60)[3]) == 3
+    _settle()
     cluster.remove_node(n2)
     _node(cluster, "worker")
     with pytest.raises(exc.ObjectLostError):
@@ -125,6 +141,7 @@ def test_lineage_released_when_out_of_scope(cluster):
 
     refs = [f.remote(i) for i in range(20)]
     ray.get(refs)
+    _settle()
     before = _state("recovery")["lineage_entries"]
     assert before >= 20
     del refs
@@ -147,6 +164,7 @@ def test_objects_on_surviving_nodes_untouched(cluster, tmp_path):
 
     ref = kept.remote(str(counter))
     ray.get(ref)
+    _settle()
     cluster.remove_node(gone)
     time.sleep(0.2)
     ray.get(ref)
