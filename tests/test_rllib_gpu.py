@@ -72,6 +72,35 @@ def test_adam_flat_matches_torch(cuda):
     torch.testing.assert_close(wb.float(), p.detach(), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("offset", [0, 1])
+def test_adam_flat_bf16_grad_vector_and_scalar_paths(cuda, offset):
+    """bf16 gradients; offset 0 takes the 4-wide vector path (plus a 3-element tail), offset 1
+    misaligns every pointer and takes the scalar path. Reference: fp32 torch.optim.Adam."""
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    torch.manual_seed(1)
+    n = 4099
+    w = torch.randn(n + offset, device=cuda)[offset:]
+    p = w.clone().requires_grad_()
+    opt = torch.optim.Adam([p], lr=1e-3)
+    master = w.clone() if offset == 0 else torch.cat([w.new_zeros(1), w])[1:]
+    m1 = torch.zeros(n + offset, device=cuda)[offset:]
+    m2 = torch.zeros(n + offset, device=cuda)[offset:]
+    wb = torch.empty(n + offset, dtype=torch.bfloat16, device=cuda)[offset:]
+    hp = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0, 0.0], device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(4):
+        gb = torch.randn(n + offset, device=cuda).to(torch.bfloat16)[offset:]
+        p.grad = gb.float()
+        opt.step()
+        hp[5] += 1
+        h.adam_flat(master.data_ptr(), m1.data_ptr(), m2.data_ptr(), gb.data_ptr(), True, wb.data_ptr(),
+                    hp.data_ptr(), 1.0, n, s)
+    torch.testing.assert_close(master, p.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(wb.float(), p.detach(), rtol=1e-2, atol=1e-2)
+
+
 def test_graph_matches_eager(cuda):
     from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler
 
