@@ -650,7 +650,66 @@ __global__ __launch_bounds__(256) void k_dense_fwd(const unsigned short* __restr
   }
 }
 
+
+// K14 — the A1-wide head GEMM heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16 in/out, fp32 accumulate).
+// Too narrow for MFMA or hipBLASLt to pay (a 16x256 macro tile for 5 useful columns, ~5-6 µs): one
+// wave per row, each lane a 4-element slice of the row (8-B load) dotted against all A1 head rows
+// (Wh, bias staged once per workgroup in LDS), then A1 butterfly reductions across the wave.
+template <int A1>
+__global__ __launch_bounds__(256) void k_heads_fwd(const unsigned short* __restrict__ hid,
+                                                   const unsigned short* __restrict__ wh,
+                                                   const unsigned short* __restrict__ bh, int64_t M,
+                                                   unsigned short* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= M) return;  // whole wave exits together (row is wave-uniform)
+  const uint2 v = *reinterpret_cast<const uint2*>(&hid[row * H + 4 * lane]);
+  const float h0 = __uint_as_float(v.x << 16), h1 = __uint_as_float(v.x & 0xffff0000u);
+  const float h2 = __uint_as_float(v.y << 16), h3 = __uint_as_float(v.y & 0xffff0000u);
+  float acc[A1];
+#pragma unroll
+  for (int a = 0; a < A1; a++) {
+    const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+    acc[a] = h0 * w.x + h1 * w.y + h2 * w.z + h3 * w.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < A1; a++) acc[a] += __shfl_xor(acc[a], o, 64);
+  if (lane < A1) {
+    float r = acc[0];
+#pragma unroll
+    for (int a = 1; a < A1; a++)
+      if (lane == a) r = acc[a];
+    out[row * A1 + lane] = f2bf(r + bhs[lane]);
+  }
+}
+
 }  // namespace dense
+
+void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
+                     hipStream_t stream) {
+  if (M <= 0) return;
+  if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_fwd: 1 <= A+1 <= 16");
+  const dim3 grid(uint32_t((M + 3) / 4)), block(256);
+  auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
+  auto* o = static_cast<unsigned short*>(heads);
+#define RMM_K14(N)                                                                                   \
+  case N:                                                                                            \
+    hipLaunchKernelGGL(dense::k_heads_fwd<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), M, o); \
+    break;
+  switch (A1) {
+    RMM_K14(1) RMM_K14(2) RMM_K14(3) RMM_K14(4) RMM_K14(5) RMM_K14(6) RMM_K14(7) RMM_K14(8)
+    RMM_K14(9) RMM_K14(10) RMM_K14(11) RMM_K14(12) RMM_K14(13) RMM_K14(14) RMM_K14(15) RMM_K14(16)
+  }
+#undef RMM_K14
+  RMM_HIP_CHECK(hipGetLastError());
+}
 
 void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int64_t K, int N, void* y,
                     hipStream_t stream) {

@@ -254,6 +254,10 @@ PYBIND11_MODULE(_hip, m) {
                              uint64_t stream) {
     dense_relu_fwd(P<const void>(x), P<const void>(w), P<const void>(b), M, K, N, P<void>(y), S(stream));
   });
+  m.def("dense_heads_fwd", [](uint64_t hidden, uint64_t wh, uint64_t bh, int64_t M, int A1, uint64_t heads,
+                              uint64_t stream) {
+    dense_heads_fwd(P<const void>(hidden), P<const void>(wh), P<const void>(bh), M, A1, P<void>(heads), S(stream));
+  });
   m.def("partition_groups", &partition_groups);
   m.def("partition_hist", [](uint64_t keys, int64_t n, int R, int mode, uint64_t counts, uint64_t stream) {
     partition_hist(P<const int64_t>(keys), n, R, mode, P<int64_t>(counts), S(stream));

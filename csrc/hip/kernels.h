@@ -113,6 +113,9 @@ void partition_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t
                        const int64_t* offsets, int64_t* out_keys, void* out_vals, hipStream_t stream);
 
 // K13: y = ReLU(x Wᵀ + b), x [M,K], W [N,K] row-major bf16, K % 32 == 0, N % 16 == 0 (small-M GEMM).
+// K14: heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16), one wave per row
+void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
+                     hipStream_t stream);
 void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int64_t K, int N, void* y,
                     hipStream_t stream);
 

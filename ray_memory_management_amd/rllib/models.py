@@ -145,7 +145,7 @@ class _DenseFn(torch.autograd.Function):
 
 class _DenseHeadsFn(torch.autograd.Function):
     """hidden = ReLU(x Wᵀ + b); heads = hidden Whᵀ + bh. Forward: K13 (small-M MFMA GEMM with the
-    bias+ReLU epilogue) and one hipBLASLt GEMM for the 5-wide head. Backward: ONE K12 launch (csrc/hip/dense_kernels.hip) for dx, dW, db, dWh, dbh,
+    bias+ReLU epilogue) and K14 (one wave per row) for the 5-wide head. Backward: ONE K12 launch (csrc/hip/dense_kernels.hip) for dx, dW, db, dWh, dbh,
     writing parameter gradients straight into their gradient buffers when they have one."""
 
     @staticmethod
@@ -156,7 +156,9 @@ class _DenseHeadsFn(torch.autograd.Function):
         hidden = torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device)
         require_hip().dense_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), M, K, w.shape[0], hidden.data_ptr(),
                                      torch.cuda.current_stream(x.device).cuda_stream)  # K13
-        heads = torch.addmm(bh, hidden, wh.t())
+        heads = torch.empty((M, wh.shape[0]), dtype=x.dtype, device=x.device)
+        require_hip().dense_heads_fwd(hidden.data_ptr(), wh.data_ptr(), bh.data_ptr(), M, wh.shape[0],
+                                      heads.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)  # K14
         ctx.save_for_backward(x, w, wh, hidden)
         ctx.gout = tuple(_grad_out(t) for t in (w, b, wh, bh))
         return heads
