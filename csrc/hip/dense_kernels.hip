@@ -690,6 +690,133 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const unsigned short* __restr
   }
 }
 
+
+// K15 — the SGD step's head layer + PPO loss in ONE launch (replaces K14 + K5c + the K12 dpre
+// pre-kernel). One wave per row as in K14; after the butterfly every lane holds the full head row,
+// so every lane evaluates the (A ≤ 15 wide) categorical PPO loss of its row redundantly (no
+// broadcast), lanes < A1 store d(loss)/d(heads) (bf16, scaled by *gout / M), and each lane turns
+// its 4 hidden elements into dpre = (dheads Wh) ⊙ [hidden > 0] — exactly what K12 needs, while the
+// row is still in registers. Loss statistics: lane 0 per row → workgroup sum → 6 atomics.
+// cols[M, A+4] (f32): old logits [0, A), old logp A, advantage A+1, value target A+2, action A+3.
+// coef: [clip, vf_clip, vf_coeff, entropy_coeff, kl_coeff]; acc[6] as K5c (zeroed per update).
+template <int A1>
+__global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restrict__ hid,
+                                                   const unsigned short* __restrict__ wh,
+                                                   const unsigned short* __restrict__ bh,
+                                                   const float* __restrict__ cols, const float* __restrict__ coef,
+                                                   float* __restrict__ acc, const float* __restrict__ gout, int64_t M,
+                                                   unsigned short* __restrict__ dz,
+                                                   unsigned short* __restrict__ dpre) {
+  constexpr int A = A1 - 1;
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  __shared__ float red[6][4];
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) + wave;
+  const bool valid = row < M;  // wave-uniform
+  const int64_t rr = valid ? row : M - 1;
+  const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
+  const float gs = gout[0] / float(M);
+  const uint2 v = *reinterpret_cast<const uint2*>(&hid[rr * H + 4 * lane]);
+  const float hv[4] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                       __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+  float hd[A1];
+#pragma unroll
+  for (int a = 0; a < A1; a++) {
+    const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+    hd[a] = hv[0] * w.x + hv[1] * w.y + hv[2] * w.z + hv[3] * w.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
+#pragma unroll
+  for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));  // the bf16 head output
+  const float* crow = cols + rr * (A + 4);
+  float mx = -INFINITY, mxo = -INFINITY, lo[A > 0 ? A : 1];
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    lo[j] = crow[j];
+    mx = fmaxf(mx, hd[j]);
+    mxo = fmaxf(mxo, lo[j]);
+  }
+  float se = 0.f, seo = 0.f;
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    se += __expf(hd[j] - mx);
+    seo += __expf(lo[j] - mxo);
+  }
+  const float lse = mx + __logf(se), lseo = mxo + __logf(seo);
+  float m = 0.f, kl = 0.f, p[A > 0 ? A : 1], po[A > 0 ? A : 1];
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    p[j] = __expf(hd[j] - lse);
+    po[j] = __expf(lo[j] - lseo);
+    m += p[j] * hd[j];
+    kl += po[j] * ((lo[j] - lseo) - (hd[j] - lse));
+  }
+  const int act = min(max(int(crow[A + 3]), 0), A - 1);
+  float la = hd[0];
+#pragma unroll
+  for (int j = 1; j < A; j++)
+    if (j == act) la = hd[j];
+  const float r = __expf((la - lse) - crow[A]);
+  const float ad = crow[A + 1];
+  const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
+  const float d = hd[A] - crow[A + 2];
+  // statistics (lane 0 of each valid row)
+  float s[6] = {0, 0, 0, 0, 0, 0};
+  if (valid && lane == 0) {
+    const float ent = lse - m, surr = fminf(r * ad, rc * ad), vf = fminf(d * d, vf_clip);
+    s[0] = -surr;
+    s[1] = vf;
+    s[2] = ent;
+    s[3] = kl;
+    s[4] = (fabsf(r - 1.f) > clip) ? 1.f : 0.f;
+    s[5] = -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl;
+  }
+  // d(loss)/d(heads), rounded to bf16 (what K12 reads)
+  const bool unclipped = r * ad <= rc * ad;
+  const bool inside = (r >= 1.f - clip) && (r <= 1.f + clip);
+  const float spg = (unclipped || inside) ? -(r * ad) : 0.f;
+  float g[A1];
+#pragma unroll
+  for (int j = 0; j < A; j++)
+    g[j] = bf2f(f2bf((spg * ((j == act ? 1.f : 0.f) - p[j]) + ent_coeff * p[j] * (hd[j] - m) +
+                      kl_coeff * (p[j] - po[j])) * gs));
+  g[A] = bf2f(f2bf((d * d < vf_clip) ? vf_coeff * 2.f * d * gs : 0.f));
+  if (valid) {
+    if (lane < A1) {
+      float gl = g[0];
+#pragma unroll
+      for (int j = 1; j < A1; j++)
+        if (lane == j) gl = g[j];
+      dz[row * A1 + lane] = f2bf(gl);
+    }
+    float dp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < A1; a++) {
+      const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+      dp[0] += g[a] * w.x, dp[1] += g[a] * w.y, dp[2] += g[a] * w.z, dp[3] += g[a] * w.w;
+    }
+    unsigned short o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) o[k] = hv[k] > 0.f ? f2bf(dp[k]) : static_cast<unsigned short>(0);
+    *reinterpret_cast<uint2*>(&dpre[row * H + 4 * lane]) =
+        make_uint2(uint32_t(o[0]) | (uint32_t(o[1]) << 16), uint32_t(o[2]) | (uint32_t(o[3]) << 16));
+  }
+  if (lane == 0)
+    for (int k = 0; k < 6; k++) red[k][wave] = s[k];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float t = 0.f;
+    for (int k = 0; k < int(blockDim.x >> 6); k++) t += red[threadIdx.x][k];
+    atomicAdd(&acc[threadIdx.x], t);
+  }
+}
 }  // namespace dense
 
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
@@ -711,6 +838,26 @@ void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
+                     float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream) {
+  if (M <= 0) return;
+  if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_ppo: 2 <= A <= 15 actions");
+  const dim3 grid(uint32_t((M + 3) / 4)), block(256);
+  auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
+  auto V = [](void* p) { return static_cast<unsigned short*>(p); };
+#define RMM_K15(N)                                                                                        \
+  case N:                                                                                                 \
+    hipLaunchKernelGGL(dense::k_heads_ppo<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), cols, coef, \
+                       acc, gout, M, V(dz), V(dpre));                                                     \
+    break;
+  switch (A1) {
+    RMM_K15(3) RMM_K15(4) RMM_K15(5) RMM_K15(6) RMM_K15(7) RMM_K15(8) RMM_K15(9)
+    RMM_K15(10) RMM_K15(11) RMM_K15(12) RMM_K15(13) RMM_K15(14) RMM_K15(15) RMM_K15(16)
+  }
+#undef RMM_K15
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int64_t K, int N, void* y,
                     hipStream_t stream) {
   if (M <= 0) return;
@@ -723,7 +870,7 @@ void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int6
 
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
-                     hipStream_t stream) {
+                     hipStream_t stream, bool dpre_ready) {
   if (M <= 0) return;
   if (K % dense::JB != 0) throw std::invalid_argument("dense_heads_bwd: K must be a multiple of 32");
   if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_bwd: 1 <= A+1 <= 16");
@@ -739,7 +886,8 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   auto* dp = V(dpre_scratch);
 #define RMM_K12(N)                                                                                               \
   case N:                                                                                                        \
-    hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);              \
+    if (!dpre_ready || !v2)                                                                                      \
+      hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);            \
     if (v2)                                                                                                      \
       hipLaunchKernelGGL(dense::k_dense_heads_bwd2<N>, grid2, block, 0, stream, U(dz), U(y), U(x), U(w), dp, M, \
                          K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                                \

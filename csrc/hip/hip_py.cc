@@ -270,9 +270,17 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("dense_heads_bwd", [](uint64_t dz, int A1, uint64_t wh, uint64_t y, uint64_t x, uint64_t w, int64_t M,
                               int64_t K, uint64_t dx, uint64_t dw, uint64_t db, uint64_t dwh, uint64_t dbh,
-                              uint64_t scratch, uint64_t stream) {
+                              uint64_t scratch, uint64_t stream, bool dpre_ready) {
     dense_heads_bwd(P<const void>(dz), A1, P<const void>(wh), P<const void>(y), P<const void>(x), P<const void>(w), M,
                     K, P<void>(dx), P<void>(dw), P<void>(db), P<void>(dwh), P<void>(dbh), P<void>(scratch),
+                    S(stream), dpre_ready);
+  }, py::arg("dz"), py::arg("A1"), py::arg("wh"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("M"), py::arg("K"),
+     py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("dwh"), py::arg("dbh"), py::arg("scratch"), py::arg("stream"),
+     py::arg("dpre_ready") = false);
+  m.def("dense_heads_ppo", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t cols, uint64_t coef, uint64_t acc,
+                              uint64_t gout, int64_t M, int A1, uint64_t dz, uint64_t dpre, uint64_t stream) {
+    dense_heads_ppo(P<const void>(hidden), P<const void>(wh), P<const void>(bh), P<const float>(cols),
+                    P<const float>(coef), P<float>(acc), P<const float>(gout), M, A1, P<void>(dz), P<void>(dpre),
                     S(stream));
   });
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,

@@ -101,7 +101,7 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
 // K % 32 == 0, A1 <= 16, M <= 640 (a PPO minibatch; larger batches take the hipBLASLt path).
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
-                     hipStream_t stream);  // dpre_scratch: M*256 bf16
+                     hipStream_t stream, bool dpre_ready = false);  // dpre_scratch: M*256 bf16
 
 // K11: shuffle partitioning. dest = splitmix64(key) % R (mode 0) or key mod R (mode 1), R <= 1024.
 // partition_hist writes counts[G][R] (G = partition_groups(n)); the caller turns them into
@@ -113,6 +113,9 @@ void partition_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t
                        const int64_t* offsets, int64_t* out_keys, void* out_vals, hipStream_t stream);
 
 // K13: y = ReLU(x Wᵀ + b), x [M,K], W [N,K] row-major bf16, K % 32 == 0, N % 16 == 0 (small-M GEMM).
+// K15: K14 + fused PPO loss stats + dheads + dpre (for dense_heads_bwd(dpre_ready=true))
+void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
+                     float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream);
 // K14: heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16), one wave per row
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
                      hipStream_t stream);

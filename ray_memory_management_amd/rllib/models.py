@@ -191,6 +191,69 @@ class _DenseHeadsFn(torch.autograd.Function):
         return dx, dw, db, dwh, dbh
 
 
+class _DenseHeadsPPOFn(torch.autograd.Function):
+    """PPO loss of heads(ReLU(layer(x))) for the fused learner step. Forward: K13 dense + ONE K15
+    launch (head GEMM, loss statistics into `acc`, d/dheads and dpre for the backward, with the
+    upstream gradient `gout` — a device scalar — known up front). Backward: K12 without its dpre
+    pre-kernel. Returns an (unwritten) scalar handle; differentiate it with grad_outputs=gout."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wh, bh, cols, coef, acc, gout):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        M, K = x.shape
+        A1 = wh.shape[0]
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        hidden = torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device)
+        h.dense_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), M, K, w.shape[0], hidden.data_ptr(), stream)  # K13
+        dz = torch.empty((M, A1), dtype=x.dtype, device=x.device)
+        dpre = torch.empty_like(hidden)
+        h.dense_heads_ppo(hidden.data_ptr(), wh.data_ptr(), bh.data_ptr(), cols.data_ptr(), coef.data_ptr(),
+                          acc.data_ptr(), gout.data_ptr(), M, A1, dz.data_ptr(), dpre.data_ptr(), stream)  # K15
+        ctx.save_for_backward(x, w, wh, hidden, dz, dpre)
+        ctx.gout = tuple(_grad_out(t) for t in (w, b, wh, bh))
+        ctx.gout_ptr = gout.data_ptr()
+        return torch.empty((), dtype=torch.float32, device=x.device)
+
+    @staticmethod
+    def backward(ctx, g):
+        from ray_memory_management_amd._native import require_hip
+
+        if g.data_ptr() != ctx.gout_ptr:
+            raise RuntimeError("dense_heads_ppo: differentiate with grad_outputs=<the gout scalar of the forward>")
+        h = require_hip()
+        x, w, wh, hidden, dz, dpre = ctx.saved_tensors
+        M, K = x.shape
+        A1 = wh.shape[0]
+        dev = x.device
+        gw, gb, gwh, gbh = ctx.gout
+        dw = gw if gw is not None else torch.empty_like(w, memory_format=torch.contiguous_format)
+        db = gb if gb is not None else torch.empty(w.shape[0], dtype=w.dtype, device=dev)
+        dwh = gwh if gwh is not None else torch.empty_like(wh, memory_format=torch.contiguous_format)
+        dbh = gbh if gbh is not None else torch.empty(A1, dtype=wh.dtype, device=dev)
+        dx = torch.empty_like(x)
+        h.dense_heads_bwd(dz.data_ptr(), A1, wh.data_ptr(), hidden.data_ptr(), x.data_ptr(), w.data_ptr(), M, K,
+                          dx.data_ptr(), dw.data_ptr(), db.data_ptr(), dwh.data_ptr(), dbh.data_ptr(), dpre.data_ptr(),
+                          torch.cuda.current_stream(dev).cuda_stream, dpre_ready=True)
+        return dx, dw, db, dwh, dbh, None, None, None, None
+
+
+def dense_heads_ppo_ok(x, layer: nn.Linear, heads: nn.Linear) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and layer.weight.dtype == torch.bfloat16
+            and heads.weight.dtype == torch.bfloat16 and layer.out_features == 256 and layer.in_features % 32 == 0
+            and 3 <= heads.out_features <= 16 and x.shape[0] <= 640 and layer.bias is not None
+            and heads.bias is not None and layer.weight.is_contiguous() and heads.weight.is_contiguous()
+            and not os.environ.get("RMM_NO_K12") and not os.environ.get("RMM_NO_K15"))
+
+
+def dense_heads_ppo(x, layer: nn.Linear, heads: nn.Linear, cols, coef, acc, gout):
+    """Fused PPO loss handle over heads(ReLU(layer(x))) (see _DenseHeadsPPOFn)."""
+    assert cols.dtype == torch.float32 and cols.is_contiguous() and cols.shape == (x.shape[0], heads.out_features + 3)
+    return _DenseHeadsPPOFn.apply(x.contiguous(), layer.weight, layer.bias, heads.weight, heads.bias, cols, coef, acc,
+                                  gout)
+
+
 def dense_heads(x, layer: nn.Linear, heads: nn.Linear):
     """heads(ReLU(layer(x))) with the fused K12 backward on the bf16 GPU path."""
     ok = (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and layer.weight.dtype == torch.bfloat16
@@ -358,6 +421,16 @@ class VisionNetwork(nn.Module):
         c1, c2 = self.convs[0], self.convs[1]
         h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
         return dense_heads(h, self.dense_tail, self.heads)
+
+    def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,
+                           rows: int = None):
+        """forward_frames fused with the PPO loss (K10 trunk → K13 → K15); returns the loss handle,
+        or None when the K15 path does not apply (caller falls back to forward_frames + K5c)."""
+        c1, c2 = self.convs[0], self.convs[1]
+        h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
+        if not dense_heads_ppo_ok(h, self.dense_tail, self.heads):
+            return None, h
+        return dense_heads_ppo(h, self.dense_tail, self.heads, cols, coef, acc, gout), h
 
     def _trunk(self, x):
         h = self.convs(x)

@@ -256,9 +256,14 @@ class PPOLearner:
         else:  # vector observations (e.g. CartPole): plain row gather
             x = ops.gather_rows(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
-        if fused:
-            heads = self.model.forward_frames(full["obs"], idx=full["idx"], ctr=ctr, period=period, rows=mbs)
-            total = ppo_heads_loss(heads, cols, self.coef, self.acc, gout=self._one)  # K5c, fwd+bwd
+        if fused:  # K10 trunk → K13 → K15 (heads + PPO loss + dheads + dpre) ; bwd K12 → K10
+            total, h = self.model.forward_frames_ppo(full["obs"], cols, self.coef, self.acc, self._one,
+                                                     idx=full["idx"], ctr=ctr, period=period, rows=mbs)
+            if total is None:
+                from ray_memory_management_amd.rllib.models import dense_heads
+
+                heads = dense_heads(h, self.model.dense_tail, self.model.heads)
+                total = ppo_heads_loss(heads, cols, self.coef, self.acc, gout=self._one)  # K5c, fwd+bwd
             grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
         elif self.heads_ok and frames:
             heads = self.model.forward_heads(x, prescaled=True)

@@ -289,3 +289,51 @@ def test_adam_step_counter_matches_host_step(cuda):
                     step_ctr=ctr.data_ptr() + 8)
         ctr.add_(1)
     torch.testing.assert_close(ma, mb, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,A", [(500, 4), (37, 6), (130, 15)])
+def test_dense_heads_ppo_matches_unfused(cuda, M, A):
+    """K15 (heads GEMM + PPO loss stats + dheads + dpre in one launch, K12 without its dpre
+    pre-kernel) vs the unfused K14 + K5c + K12 path, and the loss statistics vs fp32."""
+    from ray_memory_management_amd.rllib.models import dense_heads, dense_heads_ppo
+    from ray_memory_management_amd.rllib.ppo_learner import ppo_heads_loss
+
+    torch.manual_seed(0)
+    K = 96
+    layer = torch.nn.Linear(K, 256).to(cuda).to(torch.bfloat16)
+    heads = torch.nn.Linear(256, A + 1).to(cuda).to(torch.bfloat16)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    cols = torch.zeros(M, A + 4, device=cuda)
+    cols[:, :A] = torch.randn(M, A, device=cuda) * 0.1
+    cols[:, A] = torch.log_softmax(cols[:, :A], -1)[:, 0] + 0.05 * torch.randn(M, device=cuda)
+    cols[:, A + 1] = torch.randn(M, device=cuda)
+    cols[:, A + 2] = torch.randn(M, device=cuda)
+    cols[:, A + 3] = torch.randint(0, A, (M,), device=cuda).float()
+    coef = torch.tensor([0.2, 10.0, 0.5, 0.01, 0.2], device=cuda)
+    one = torch.ones((), device=cuda)
+    ps = [x, layer.weight, layer.bias, heads.weight, heads.bias]
+
+    acc1 = torch.zeros(6, device=cuda)
+    t1 = dense_heads_ppo(x, layer, heads, cols, coef, acc1, one)
+    g1 = torch.autograd.grad(t1, ps, grad_outputs=one)
+    acc2 = torch.zeros(6, device=cuda)
+    h2 = dense_heads(x, layer, heads)
+    t2 = ppo_heads_loss(h2, cols, coef, acc2, gout=one)
+    g2 = torch.autograd.grad(t2, ps, grad_outputs=one)
+    torch.testing.assert_close(acc1, acc2, rtol=1e-3, atol=1e-3)
+    for n, a, b in zip(("dx", "dW", "db", "dWh", "dbh"), g1, g2):
+        err = float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6))
+        assert err < 2e-2, (n, err)
+    # statistics vs an fp32 evaluation of the same loss on the same (bf16) head outputs
+    hf = h2.float()
+    lp = torch.log_softmax(hf[:, :A], -1)
+    lpo = torch.log_softmax(cols[:, :A], -1)
+    act = cols[:, A + 3].long()
+    r = torch.exp(lp.gather(1, act[:, None])[:, 0] - cols[:, A])
+    adv = cols[:, A + 1]
+    surr = torch.minimum(r * adv, r.clamp(0.8, 1.2) * adv)
+    vf = torch.clamp((hf[:, A] - cols[:, A + 2]) ** 2, max=10.0)
+    ent = -(lp.exp() * lp).sum(-1)
+    kl = (lpo.exp() * (lpo - lp)).sum(-1)
+    ref = torch.stack([-surr.sum(), vf.sum(), ent.sum(), kl.sum()])
+    torch.testing.assert_close(acc1[:4], ref, rtol=2e-3, atol=2e-3)
