@@ -33,3 +33,20 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
 
 }  // namespace hip
 }  // namespace rmm
+
+#if defined(__HIPCC__)
+namespace rmm {
+namespace hip {
+// counter-based mix (murmur3 finaliser over three words); shared by the samplers and the synthetic env
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+}  // namespace hip
+}  // namespace rmm
+#endif

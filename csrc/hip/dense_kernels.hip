@@ -817,6 +817,80 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
     atomicAdd(&acc[threadIdx.x], t);
   }
 }
+
+// K16 — the rollout step's head layer + action sampling in ONE launch (replaces K14 + K7). One wave
+// per env row as in K14; after the butterfly every lane holds the bf16-rounded head row; lane 0
+// draws the Gumbel-max action (same counter hash and stream as K7, so the two paths sample
+// identically) and writes act/logp/vf of rollout row t = *t_ptr, lanes < A write the logits row.
+template <int A1>
+__global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __restrict__ hid,
+                                                      const unsigned short* __restrict__ wh,
+                                                      const unsigned short* __restrict__ bh,
+                                                      const int64_t* __restrict__ t_ptr,
+                                                      const int64_t* __restrict__ ctr, uint32_t seed,
+                                                      int64_t* __restrict__ act, float* __restrict__ logp,
+                                                      float* __restrict__ vf, float* __restrict__ lout,
+                                                      int64_t* __restrict__ act_now, int64_t B) {
+  constexpr int A = A1 - 1;
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= B) return;  // wave-uniform
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
+  const uint2 v = *reinterpret_cast<const uint2*>(&hid[b * H + 4 * lane]);
+  const float h0 = __uint_as_float(v.x << 16), h1 = __uint_as_float(v.x & 0xffff0000u);
+  const float h2 = __uint_as_float(v.y << 16), h3 = __uint_as_float(v.y & 0xffff0000u);
+  float hd[A1];
+#pragma unroll
+  for (int a = 0; a < A1; a++) {
+    const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+    hd[a] = h0 * w.x + h1 * w.y + h2 * w.z + h3 * w.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
+#pragma unroll
+  for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));
+  const int64_t o = t * B + b;
+  if (lane < A) {
+    float l = hd[0];
+#pragma unroll
+    for (int j = 1; j < A; j++)
+      if (lane == j) l = hd[j];
+    lout[o * A + lane] = l;
+  }
+  if (lane == 0) {
+    float best = -INFINITY, mx = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int j = 0; j < A; j++) {
+      mx = fmaxf(mx, hd[j]);
+      const uint32_t hh = hash3(seed, c, uint32_t(b * A + j));
+      const float u = (float(hh >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float gmb = hd[j] - __logf(-__logf(u));
+      if (gmb > best) {
+        best = gmb;
+        arg = j;
+      }
+    }
+    float se = 0.f, la = hd[0];
+#pragma unroll
+    for (int j = 0; j < A; j++) {
+      se += __expf(hd[j] - mx);
+      if (j == arg) la = hd[j];
+    }
+    act[o] = arg;
+    act_now[b] = arg;
+    logp[o] = la - mx - __logf(se);
+    vf[o] = hd[A];
+  }
+}
 }  // namespace dense
 
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
@@ -855,6 +929,26 @@ void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const f
     RMM_K15(10) RMM_K15(11) RMM_K15(12) RMM_K15(13) RMM_K15(14) RMM_K15(15) RMM_K15(16)
   }
 #undef RMM_K15
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void dense_heads_sample(const void* hidden, const void* wh, const void* bh, const int64_t* t_ptr, const int64_t* ctr,
+                        uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B,
+                        int A1, hipStream_t stream) {
+  if (B <= 0) return;
+  if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_sample: 2 <= A <= 15 actions");
+  const dim3 grid(uint32_t((B + 3) / 4)), block(256);
+  auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
+#define RMM_K16(N)                                                                                          \
+  case N:                                                                                                   \
+    hipLaunchKernelGGL(dense::k_heads_sample<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), t_ptr, ctr, \
+                       seed, act, logp, vf, lout, act_now, B);                                              \
+    break;
+  switch (A1) {
+    RMM_K16(3) RMM_K16(4) RMM_K16(5) RMM_K16(6) RMM_K16(7) RMM_K16(8) RMM_K16(9)
+    RMM_K16(10) RMM_K16(11) RMM_K16(12) RMM_K16(13) RMM_K16(14) RMM_K16(15) RMM_K16(16)
+  }
+#undef RMM_K16
   RMM_HIP_CHECK(hipGetLastError());
 }
 

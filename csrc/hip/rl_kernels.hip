@@ -416,16 +416,6 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
 
 // ============================================================== K7 sample + store
 
-__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
-  // counter-based mix (murmur3 finaliser over three words)
-  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return h;
-}
 
 // logits [B, A] (TL, row stride ldl), values [B] (TV, stride ldv — both may view one merged
 // [B, A+1] head output); writes row t (=*t_ptr) of act [T,B], logp [T,B], vf [T,B],

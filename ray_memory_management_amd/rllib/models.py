@@ -422,6 +422,33 @@ class VisionNetwork(nn.Module):
         h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
         return dense_heads(h, self.dense_tail, self.heads)
 
+    @torch.no_grad()
+    def forward_sample(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now) -> bool:
+        """Rollout step: K10 trunk → K13 → K16 (head GEMM + Gumbel-max sampling + rollout-row stores,
+        same sampling stream as sample_store). Returns False (nothing launched) when not applicable."""
+        if not self.fused_trunk_ok(obs):
+            return False
+        B = obs.shape[0]
+        layer, heads = self.dense_tail, self.heads
+        if not (heads.out_features >= 3 and heads.out_features <= 16 and layer is not None
+                and layer.out_features == 256 and layer.in_features % 32 == 0 and layer.bias is not None
+                and heads.bias is not None and layer.weight.is_contiguous() and heads.weight.is_contiguous()
+                and not os.environ.get("RMM_NO_K16")):
+            return False
+        from ray_memory_management_amd._native import require_hip
+
+        c1, c2 = self.convs[0], self.convs[1]
+        h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias)
+        hip = require_hip()
+        stream = torch.cuda.current_stream(obs.device).cuda_stream
+        hidden = torch.empty((B, 256), dtype=h.dtype, device=h.device)
+        hip.dense_relu_fwd(h.data_ptr(), layer.weight.data_ptr(), layer.bias.data_ptr(), B, h.shape[1], 256,
+                           hidden.data_ptr(), stream)  # K13
+        hip.dense_heads_sample(hidden.data_ptr(), heads.weight.data_ptr(), heads.bias.data_ptr(), t_ptr.data_ptr(),
+                               ctr.data_ptr(), seed, act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
+                               act_now.data_ptr(), B, heads.out_features, stream)  # K16
+        return True
+
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,
                            rows: int = None):
         """forward_frames fused with the PPO loss (K10 trunk → K13 → K15); returns the loss handle,

@@ -486,7 +486,12 @@ class GPURolloutSampler:
     @torch.no_grad()
     def _step_body(self):
         t = self.t_idx
-        if self.fast:
+        if self.fast and hasattr(self.model, "forward_sample") and getattr(
+                getattr(self.model, "heads", None), "out_features", -1) == self.A + 1 and self.model.forward_sample(
+                self.s_obs, t, self.ctr, self.seed, self.buf_act, self.buf_logp, self.buf_vf, self.buf_logits,
+                self.act_now):  # K10 → K13 → K16: heads + sampling + row stores in one launch
+            a = self.act_now
+        elif self.fast:
             if hasattr(self.model, "forward_heads"):  # merged [B, A+1] head read in place (strided)
                 hd = self.model.forward_heads(self.s_obs)
                 lp, vp, ld = hd.data_ptr(), hd.data_ptr() + self.A * hd.element_size(), hd.stride(0)

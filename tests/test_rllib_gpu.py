@@ -337,3 +337,43 @@ def test_dense_heads_ppo_matches_unfused(cuda, M, A):
     kl = (lpo.exp() * (lpo - lp)).sum(-1)
     ref = torch.stack([-surr.sum(), vf.sum(), ent.sum(), kl.sum()])
     torch.testing.assert_close(acc1[:4], ref, rtol=2e-3, atol=2e-3)
+
+
+def test_heads_sample_matches_unfused(cuda):
+    """K16 (heads + Gumbel-max sampling + row stores) vs K14 heads + K7 sample_store: same hash
+    stream, so actions match exactly; logp / vf / logits to bf16 rounding."""
+    from ray_memory_management_amd._native import require_hip
+    from ray_memory_management_amd.rllib.models import dense_heads
+
+    h = require_hip()
+    torch.manual_seed(0)
+    B, A, T, K = 37, 6, 3, 96
+    layer = torch.nn.Linear(K, 256).to(cuda).to(torch.bfloat16)
+    heads = torch.nn.Linear(256, A + 1).to(cuda).to(torch.bfloat16)
+    heads.weight.data *= 8  # spread the logits so sampling is not uniform
+    x = torch.randn(B, K, device=cuda).to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+    hidden = torch.empty(B, 256, dtype=torch.bfloat16, device=cuda)
+    h.dense_relu_fwd(x.data_ptr(), layer.weight.data_ptr(), layer.bias.data_ptr(), B, K, 256, hidden.data_ptr(), s)
+    t = torch.tensor([1], device=cuda)
+    ctr = torch.tensor([12345], device=cuda)
+    outs = []
+    for fused in (True, False):
+        act = torch.zeros(T, B, dtype=torch.int64, device=cuda)
+        logp, vf = torch.zeros(T, B, device=cuda), torch.zeros(T, B, device=cuda)
+        lout, now = torch.zeros(T, B, A, device=cuda), torch.zeros(B, dtype=torch.int64, device=cuda)
+        if fused:
+            h.dense_heads_sample(hidden.data_ptr(), heads.weight.data_ptr(), heads.bias.data_ptr(), t.data_ptr(),
+                                 ctr.data_ptr(), 7, act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
+                                 now.data_ptr(), B, A + 1, s)
+        else:
+            hd = dense_heads(x, layer, heads).contiguous()
+            h.sample_store(hd.data_ptr(), True, hd.data_ptr() + 2 * A, True, t.data_ptr(), ctr.data_ptr(), 7,
+                           act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(), now.data_ptr(), B, A, s,
+                           ldl=A + 1, ldv=A + 1)
+        outs.append((act, logp, vf, lout, now))
+    (a1, l1, v1, o1, n1), (a2, l2, v2, o2, n2) = outs
+    assert torch.equal(n1, n2) and torch.equal(a1, a2) and int(a1[0].abs().sum()) == 0
+    for u, w in ((l1, l2), (v1, v2), (o1, o2)):
+        torch.testing.assert_close(u, w, rtol=2e-2, atol=2e-2)
+    assert len(set(n1.tolist())) > 1
