@@ -706,7 +706,9 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
                                                    const float* __restrict__ cols, const float* __restrict__ coef,
                                                    float* __restrict__ acc, const float* __restrict__ gout, int64_t M,
                                                    unsigned short* __restrict__ dz,
-                                                   unsigned short* __restrict__ dpre) {
+                                                   unsigned short* __restrict__ dpre,
+                                                   const int64_t* __restrict__ cidx,
+                                                   const int64_t* __restrict__ ctr, int64_t period) {
   constexpr int A = A1 - 1;
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
@@ -735,7 +737,9 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
     for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
 #pragma unroll
   for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));  // the bf16 head output
-  const float* crow = cols + rr * (A + 4);
+  // cols row: gathered in place through the minibatch index window (as K2) when cidx is given
+  const int64_t crr = cidx ? (ctr ? cidx[(ctr[0] % period) * M + rr] : cidx[rr]) : rr;
+  const float* crow = cols + crr * (A + 4);
   float mx = -INFINITY, mxo = -INFINITY, lo[A > 0 ? A : 1];
 #pragma unroll
   for (int j = 0; j < A; j++) {
@@ -913,8 +917,10 @@ void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t
 }
 
 void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
-                     float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream) {
+                     float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream,
+                     const int64_t* cidx, const int64_t* ctr, int64_t period) {
   if (M <= 0) return;
+  if (period < 1) period = 1;
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_ppo: 2 <= A <= 15 actions");
   const dim3 grid(uint32_t((M + 3) / 4)), block(256);
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
@@ -922,7 +928,7 @@ void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const f
 #define RMM_K15(N)                                                                                        \
   case N:                                                                                                 \
     hipLaunchKernelGGL(dense::k_heads_ppo<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), cols, coef, \
-                       acc, gout, M, V(dz), V(dpre));                                                     \
+                       acc, gout, M, V(dz), V(dpre), cidx, ctr, period);                                  \
     break;
   switch (A1) {
     RMM_K15(3) RMM_K15(4) RMM_K15(5) RMM_K15(6) RMM_K15(7) RMM_K15(8) RMM_K15(9)

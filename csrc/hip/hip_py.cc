@@ -285,11 +285,14 @@ PYBIND11_MODULE(_hip, m) {
                        P<int64_t>(act_now), B, A1, S(stream));
   });
   m.def("dense_heads_ppo", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t cols, uint64_t coef, uint64_t acc,
-                              uint64_t gout, int64_t M, int A1, uint64_t dz, uint64_t dpre, uint64_t stream) {
+                              uint64_t gout, int64_t M, int A1, uint64_t dz, uint64_t dpre, uint64_t stream,
+                              uint64_t cidx, uint64_t ctr, int64_t period) {
     dense_heads_ppo(P<const void>(hidden), P<const void>(wh), P<const void>(bh), P<const float>(cols),
                     P<const float>(coef), P<float>(acc), P<const float>(gout), M, A1, P<void>(dz), P<void>(dpre),
-                    S(stream));
-  });
+                    S(stream), P<const int64_t>(cidx), P<const int64_t>(ctr), period);
+  }, py::arg("hidden"), py::arg("wh"), py::arg("bh"), py::arg("cols"), py::arg("coef"), py::arg("acc"),
+     py::arg("gout"), py::arg("M"), py::arg("A1"), py::arg("dz"), py::arg("dpre"), py::arg("stream"),
+     py::arg("cidx") = 0, py::arg("ctr") = 0, py::arg("period") = 1);
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,
                                uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,

@@ -119,7 +119,8 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
                         int A1, hipStream_t stream);
 // K15: K14 + fused PPO loss stats + dheads + dpre (for dense_heads_bwd(dpre_ready=true))
 void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
-                     float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream);
+                     float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream,
+                     const int64_t* cidx = nullptr, const int64_t* ctr = nullptr, int64_t period = 1);
 // K14: heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16), one wave per row
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
                      hipStream_t stream);

@@ -198,7 +198,7 @@ class _DenseHeadsPPOFn(torch.autograd.Function):
     pre-kernel. Returns an (unwritten) scalar handle; differentiate it with grad_outputs=gout."""
 
     @staticmethod
-    def forward(ctx, x, w, b, wh, bh, cols, coef, acc, gout):
+    def forward(ctx, x, w, b, wh, bh, cols, coef, acc, gout, cidx=None, ctr=None, period=1):
         from ray_memory_management_amd._native import require_hip
 
         h = require_hip()
@@ -210,7 +210,9 @@ class _DenseHeadsPPOFn(torch.autograd.Function):
         dz = torch.empty((M, A1), dtype=x.dtype, device=x.device)
         dpre = torch.empty_like(hidden)
         h.dense_heads_ppo(hidden.data_ptr(), wh.data_ptr(), bh.data_ptr(), cols.data_ptr(), coef.data_ptr(),
-                          acc.data_ptr(), gout.data_ptr(), M, A1, dz.data_ptr(), dpre.data_ptr(), stream)  # K15
+                          acc.data_ptr(), gout.data_ptr(), M, A1, dz.data_ptr(), dpre.data_ptr(), stream,
+                          cidx=cidx.data_ptr() if cidx is not None else 0,
+                          ctr=ctr.data_ptr() if ctr is not None else 0, period=int(period))  # K15
         ctx.save_for_backward(x, w, wh, hidden, dz, dpre)
         ctx.gout = tuple(_grad_out(t) for t in (w, b, wh, bh))
         ctx.gout_ptr = gout.data_ptr()
@@ -236,7 +238,7 @@ class _DenseHeadsPPOFn(torch.autograd.Function):
         h.dense_heads_bwd(dz.data_ptr(), A1, wh.data_ptr(), hidden.data_ptr(), x.data_ptr(), w.data_ptr(), M, K,
                           dx.data_ptr(), dw.data_ptr(), db.data_ptr(), dwh.data_ptr(), dbh.data_ptr(), dpre.data_ptr(),
                           torch.cuda.current_stream(dev).cuda_stream, dpre_ready=True)
-        return dx, dw, db, dwh, dbh, None, None, None, None
+        return dx, dw, db, dwh, dbh, None, None, None, None, None, None, None
 
 
 def dense_heads_ppo_ok(x, layer: nn.Linear, heads: nn.Linear) -> bool:
@@ -247,11 +249,20 @@ def dense_heads_ppo_ok(x, layer: nn.Linear, heads: nn.Linear) -> bool:
             and not os.environ.get("RMM_NO_K12") and not os.environ.get("RMM_NO_K15"))
 
 
-def dense_heads_ppo(x, layer: nn.Linear, heads: nn.Linear, cols, coef, acc, gout):
-    """Fused PPO loss handle over heads(ReLU(layer(x))) (see _DenseHeadsPPOFn)."""
-    assert cols.dtype == torch.float32 and cols.is_contiguous() and cols.shape == (x.shape[0], heads.out_features + 3)
+def dense_heads_ppo(x, layer: nn.Linear, heads: nn.Linear, cols, coef, acc, gout, idx=None, ctr=None,
+                    period: int = 1):
+    """Fused PPO loss handle over heads(ReLU(layer(x))) (see _DenseHeadsPPOFn). With `idx` the loss
+    columns are read in place as cols[idx[...]] (the device-counter window of ops.gather_rows)."""
+    M = x.shape[0]
+    assert cols.dtype == torch.float32 and cols.is_contiguous() and cols.dim() == 2
+    assert cols.shape[1] == heads.out_features + 3
+    if idx is None:
+        assert cols.shape[0] == M
+    else:
+        assert idx.dtype == torch.int64 and idx.is_contiguous() and idx.numel() >= M * (period if ctr is not None else 1)
+        assert ctr is None or (ctr.dtype == torch.int64 and ctr.device == x.device)
     return _DenseHeadsPPOFn.apply(x.contiguous(), layer.weight, layer.bias, heads.weight, heads.bias, cols, coef, acc,
-                                  gout)
+                                  gout, idx, ctr, period)
 
 
 def dense_heads(x, layer: nn.Linear, heads: nn.Linear):
@@ -451,13 +462,15 @@ class VisionNetwork(nn.Module):
 
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,
                            rows: int = None):
-        """forward_frames fused with the PPO loss (K10 trunk → K13 → K15); returns the loss handle,
-        or None when the K15 path does not apply (caller falls back to forward_frames + K5c)."""
+        """forward_frames fused with the PPO loss (K10 trunk → K13 → K15); `cols` is the FULL loss-column
+        table, read through the same index window as the frames. Returns (loss handle, trunk output),
+        handle None when the K15 path does not apply (caller falls back to dense_heads + K5c)."""
         c1, c2 = self.convs[0], self.convs[1]
         h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias, idx=idx, ctr=ctr, period=period, rows=rows)
         if not dense_heads_ppo_ok(h, self.dense_tail, self.heads):
             return None, h
-        return dense_heads_ppo(h, self.dense_tail, self.heads, cols, coef, acc, gout), h
+        return dense_heads_ppo(h, self.dense_tail, self.heads, cols, coef, acc, gout, idx=idx, ctr=ctr,
+                               period=period), h
 
     def _trunk(self, x):
         h = self.convs(x)

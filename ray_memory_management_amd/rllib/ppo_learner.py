@@ -255,11 +255,12 @@ class PPOLearner:
             x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         else:  # vector observations (e.g. CartPole): plain row gather
             x = ops.gather_rows(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
-        cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
-        if fused:  # K10 trunk → K13 → K15 (heads + PPO loss + dheads + dpre) ; bwd K12 → K10
-            total, h = self.model.forward_frames_ppo(full["obs"], cols, self.coef, self.acc, self._one,
+        cols = None if fused else ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
+        if fused:  # K10 trunk → K13 → K15 (heads + PPO loss + dheads + dpre, cols gathered in place); bwd K12 → K10
+            total, h = self.model.forward_frames_ppo(full["obs"], full["cols"], self.coef, self.acc, self._one,
                                                      idx=full["idx"], ctr=ctr, period=period, rows=mbs)
             if total is None:
+                cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
                 from ray_memory_management_amd.rllib.models import dense_heads
 
                 heads = dense_heads(h, self.model.dense_tail, self.model.heads)

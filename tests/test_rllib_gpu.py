@@ -377,3 +377,34 @@ def test_heads_sample_matches_unfused(cuda):
     for u, w in ((l1, l2), (v1, v2), (o1, o2)):
         torch.testing.assert_close(u, w, rtol=2e-2, atol=2e-2)
     assert len(set(n1.tolist())) > 1
+
+
+def test_dense_heads_ppo_gathers_cols_through_index_window(cuda):
+    """K15 reading cols[idx[(ctr % period) * M + row]] in place == K15 on pre-gathered cols."""
+    from ray_memory_management_amd.rllib.models import dense_heads_ppo
+
+    torch.manual_seed(2)
+    M, A, K, period = 50, 4, 64, 3
+    layer = torch.nn.Linear(K, 256).to(cuda).to(torch.bfloat16)
+    heads = torch.nn.Linear(256, A + 1).to(cuda).to(torch.bfloat16)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    full = torch.randn(M * period, A + 4, device=cuda)
+    full[:, A + 3] = torch.randint(0, A, (M * period,), device=cuda).float()
+    full[:, A] = -1.5
+    idx = torch.randperm(M * period, device=cuda)
+    ctr = torch.tensor([4], device=cuda)  # window 4 % 3 = 1
+    coef = torch.tensor([0.2, 10.0, 0.5, 0.01, 0.2], device=cuda)
+    one = torch.ones((), device=cuda)
+    res = []
+    for gathered in (False, True):
+        xx = x.clone().requires_grad_(True)
+        acc = torch.zeros(6, device=cuda)
+        if gathered:
+            t = dense_heads_ppo(xx, layer, heads, full[idx[M:2 * M]].contiguous(), coef, acc, one)
+        else:
+            t = dense_heads_ppo(xx, layer, heads, full, coef, acc, one, idx=idx, ctr=ctr, period=period)
+        g = torch.autograd.grad(t, [xx, layer.weight, heads.weight], grad_outputs=one)
+        res.append((acc, g))
+    torch.testing.assert_close(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
