@@ -165,6 +165,9 @@ def test_pbt_exploits(ray_shared, tmp_path):
             self.total = 0.0
 
         def step(self):
+            import time
+
+            time.sleep(0.05)  # keep the two trials interleaved even on a loaded host
             self.total += self.config["lr"]
             return {"total": self.total, "lr": self.config["lr"]}
 
@@ -181,7 +184,7 @@ def test_pbt_exploits(ray_shared, tmp_path):
     pbt = PopulationBasedTraining(time_attr="training_iteration", perturbation_interval=2,
                                   hyperparam_mutations={"lr": [0.01, 0.1, 1.0, 10.0]}, quantile_fraction=0.5, seed=0)
     analysis = tune.run(PBTTrainable, config={"lr": tune.grid_search([0.01, 10.0])}, scheduler=pbt,
-                        metric="total", mode="max", stop={"training_iteration": 8}, local_dir=str(tmp_path))
+                        metric="total", mode="max", stop={"training_iteration": 12}, local_dir=str(tmp_path))
     assert pbt._num_perturbations >= 1
     # the weak trial cloned the strong one's state: both end far above 8 * 0.01
     assert min(t.last_result["total"] for t in analysis.trials) > 1.0
