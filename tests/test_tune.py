@@ -121,9 +121,12 @@ def test_trial_error_and_retry(ray_shared, tmp_path):
 
 
 def _curve(config):
+    import time
+
     from ray_memory_management_amd.air import session
 
     for i in range(1, 21):
+        time.sleep(0.02)  # let the scheduler act between reports even on a loaded host
         session.report({"acc": config["q"] * i})
 
 
