@@ -65,7 +65,7 @@ def extensions():
     if tl:
         hip_ld = [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"] + hip_ld
     exts.append(
-        _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/hip_py.cc",
+        _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/ingest_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/hip_py.cc",
               "csrc/store/shm_store.cc"], HIPCC,
              common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"],
              hip_ld, ["csrc/hip/kernels.h", "csrc/hip/gpu_store.h", "csrc/hip/common.h", "csrc/store/shm_store.h"]))
@@ -84,6 +84,25 @@ def _stale(e) -> bool:
     return any(os.path.getmtime(s) > t for s in e["sources"] + e["headers"] if os.path.exists(s))
 
 
+def _compile_obj(e, src, verbose):
+    """Compile one source of a multi-source extension to build/obj (cached by mtime)."""
+    od = os.path.join(ROOT, "build", "obj", e["name"])
+    os.makedirs(od, exist_ok=True)
+    obj = os.path.join(od, os.path.basename(src) + ".o")
+    deps = [src] + e["headers"]
+    if os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in deps if os.path.exists(d)):
+        return obj
+    flags = [f for f in e["flags"] if f != "-shared"]
+    cmd = [e["compiler"]] + flags + ["-c", src, "-o", obj + ".tmp"]
+    if verbose:
+        print("[build_native]", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compiling {src} failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
 def build_one(e, force=False, verbose=True):
     if not force and not _stale(e):
         return e["name"], "up-to-date"
@@ -92,12 +111,20 @@ def build_one(e, force=False, verbose=True):
         return e["name"], f"skipped (missing {missing})"
     out = _out(e["name"])
     tmp = out + ".tmp"
-    cmd = [e["compiler"]] + e["flags"] + e["sources"] + ["-o", tmp] + e["ldflags"]
+    if force:
+        import shutil
+
+        shutil.rmtree(os.path.join(ROOT, "build", "obj", e["name"]), ignore_errors=True)
+    # per-source objects in parallel (hipcc is single-threaded per file), then one link
+    with ThreadPoolExecutor(max_workers=min(8, len(e["sources"]))) as ex:
+        objs = list(ex.map(lambda s: _compile_obj(e, s, verbose), e["sources"]))
+    link = [f for f in e["flags"] if f.startswith("--offload-arch") or f in ("-shared", "-fPIC")]
+    cmd = [e["compiler"]] + link + objs + ["-o", tmp] + e["ldflags"]
     if verbose:
         print("[build_native]", " ".join(cmd), flush=True)
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"building {e['name']} failed:\n{r.stdout}\n{r.stderr}")
+        raise RuntimeError(f"linking {e['name']} failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, out)
     return e["name"], "built"
 

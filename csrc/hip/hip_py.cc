@@ -189,14 +189,34 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("adam_flat", [](uint64_t master, uint64_t m1, uint64_t m2, uint64_t grad, bool grad_bf16, uint64_t wbf16,
                         uint64_t hp, float grad_scale, int64_t n, uint64_t stream, uint64_t step_ctr, uint64_t bump,
-                        int nbump, uint64_t done) {
+                        int nbump, uint64_t done, uint64_t scale_ptr) {
     adam_flat(P<float>(master), P<float>(m1), P<float>(m2), P<const void>(grad), grad_bf16,
               wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream),
               step_ctr ? P<const int64_t>(step_ctr) : nullptr, bump ? P<int64_t>(bump) : nullptr, nbump,
-              done ? P<uint32_t>(done) : nullptr);
+              done ? P<uint32_t>(done) : nullptr, scale_ptr ? P<const float>(scale_ptr) : nullptr);
   }, py::arg("master"), py::arg("m1"), py::arg("m2"), py::arg("grad"), py::arg("grad_bf16"), py::arg("wbf16"),
      py::arg("hp"), py::arg("grad_scale"), py::arg("n"), py::arg("stream"), py::arg("step_ctr") = 0,
-     py::arg("bump") = 0, py::arg("nbump") = 0, py::arg("done") = 0);
+     py::arg("bump") = 0, py::arg("nbump") = 0, py::arg("done") = 0, py::arg("scale_ptr") = 0);
+  m.def("grad_clip_workspace_floats", &grad_clip_workspace_floats);
+  m.def("ingest_gae", [](uint64_t raw, uint64_t boot, uint64_t blocks, int nblocks, int A, float gamma, float lam,
+                         uint64_t cols, uint64_t stats, uint64_t stream) {
+    ingest_gae(P<const float>(raw), P<const float>(boot), P<const IngestBlock>(blocks), nblocks, A, gamma, lam,
+               P<float>(cols), P<double>(stats), S(stream));
+  });
+  m.def("ingest_block_bytes", [] { return int(sizeof(IngestBlock)); });
+  m.def("standardize_col", [](uint64_t cols, int64_t N, int C, int col, uint64_t stats, uint64_t stream) {
+    standardize_col(P<float>(cols), N, C, col, P<const double>(stats), S(stream));
+  });
+  m.def("host_register_segment", [](uint64_t base, uint64_t size) { host_register_segment(base, size); });
+  m.def("h2d_from_segment", [](uint64_t dst, uint64_t src, uint64_t n, uint64_t stream) {
+    py::gil_scoped_release nogil;
+    return h2d_from_segment(P<void>(dst), P<const void>(src), n, S(stream));
+  });
+  m.def("host_unregister_all", [] { host_unregister_all(); });
+  m.def("grad_clip_coef", [](uint64_t grad, bool grad_bf16, int64_t n, float grad_scale, float max_norm,
+                             uint64_t ws, uint64_t out, uint64_t stream) {
+    grad_clip_coef(P<const void>(grad), grad_bf16, n, grad_scale, max_norm, P<float>(ws), P<float>(out), S(stream));
+  });
   m.def("bump_done_words", &bump_done_words);
   m.def("ppo_heads_loss", [](bool bwd, uint64_t heads, uint64_t cols, uint64_t coef, uint64_t acc, uint64_t gout,
                              uint64_t g_heads, int64_t N, int A, uint64_t stream) {

@@ -63,7 +63,12 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
 // K6: flat Adam/AdamW with fp32 master weights, bf16 or fp32 grads, optional bf16 weight output.
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr = nullptr,
-               int64_t* bump = nullptr, int nbump = 0, uint32_t* done = nullptr);
+               int64_t* bump = nullptr, int nbump = 0, uint32_t* done = nullptr, const float* scale_ptr = nullptr);
+// K6b: out[0] = min(1, max_norm / ||grad*grad_scale||), out[1] = the norm (device; feeds K6 scale_ptr).
+// workspace: grad_clip_workspace_floats() floats, zero-initialised once (its ticket resets itself).
+int64_t grad_clip_workspace_floats();
+void grad_clip_coef(const void* grad, bool grad_bf16, int64_t n, float grad_scale, float max_norm, float* workspace,
+                    float* out, hipStream_t stream);
 
 // K5c: merged policy/value head PPO loss reading packed columns (see rl_kernels.hip).
 void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float* coef, float* acc, const float* gout,
@@ -143,6 +148,27 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                       hipStream_t stream, int dbg = 0);
 // dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
 // load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores.
+
+// K17: learner-side sample-batch ingest (see ingest_kernels.hip). raw [rows, A+5] fp32 =
+// [logits(A) | logp | vf | reward | done | action], blocks = one entry per rollout fragment
+// (time-major rows t*n+env starting at row0; bootstrap values at boot[boot0 .. boot0+n)).
+// cols [rows, A+4] = [logits | logp | adv | value target | action]; stats (2 doubles, zeroed by
+// the caller) accumulate sum(adv), sum(adv^2) for standardize_col (K17b).
+struct IngestBlock {
+  int64_t row0;
+  int32_t T;
+  int32_t n;
+  int32_t boot0;
+  int32_t pad;
+};
+void ingest_gae(const float* raw, const float* boot, const IngestBlock* blocks_dev, int nblocks, int A, float gamma,
+                float lam, float* cols, double* stats, hipStream_t stream);
+void standardize_col(float* cols, int64_t N, int C, int col, const double* stats, hipStream_t stream);
+// Page-locked DMA out of a shared-memory object-store segment: chunks of the registered segment
+// are hipHostRegister'ed on first use. Returns the bytes newly registered by this call.
+void host_register_segment(uintptr_t base, uint64_t size);
+uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream);
+void host_unregister_all();
 
 }  // namespace hip
 }  // namespace rmm

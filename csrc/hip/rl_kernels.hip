@@ -349,8 +349,11 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
                                                   float* __restrict__ m2, const TG* __restrict__ grad,
                                                   __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
                                                   float grad_scale, int64_t n, const int64_t* __restrict__ step_ctr,
-                                                  int64_t* bump, int nbump, uint32_t* done) {
+                                                  int64_t* bump, int nbump, uint32_t* done,
+                                                  const float* __restrict__ scale_ptr) {
   // step: hp[5], or (device step counter + 1) when the counter is given (graph-friendly)
+  // scale_ptr (optional): a device-side factor, e.g. the global-norm clip coefficient of K6b
+  if (scale_ptr) grad_scale *= scale_ptr[0];
   AdamCoef c;
   c.lr = hp[0], c.b1 = hp[1], c.b2 = hp[2], c.eps = hp[3], c.wd = hp[4];
   const float step = step_ctr ? float(step_ctr[0] + 1) : hp[5];
@@ -394,7 +397,7 @@ int bump_done_words() { return kBumpWords; }
 
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr, int64_t* bump, int nbump,
-               uint32_t* done) {
+               uint32_t* done, const float* scale_ptr) {
   if (n <= 0) return;
   auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
   const bool vec = al(master, 16) && al(m1, 16) && al(m2, 16) && al(grad, grad_bf16 ? 8 : 16) &&
@@ -403,7 +406,8 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 256 * 8));
   auto go = [&](auto kern, const auto* g) {
     hipLaunchKernelGGL(kern, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2, g,
-                       static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n, step_ctr, bump, nbump, done);
+                       static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n, step_ctr, bump, nbump, done,
+                       scale_ptr);
   };
   const auto* gb = static_cast<const __hip_bfloat16*>(grad);
   const auto* gf = static_cast<const float*>(grad);
@@ -411,6 +415,59 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
     vec ? go(k_adam_flat<__hip_bfloat16, true>, gb) : go(k_adam_flat<__hip_bfloat16, false>, gb);
   else
     vec ? go(k_adam_flat<float, true>, gf) : go(k_adam_flat<float, false>, gf);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+// ============================================================== K6b global-norm clip coefficient
+
+// out[0] = min(1, max_norm / (||grad * grad_scale||_2 + 1e-6)) (torch.nn.utils.clip_grad_norm_
+// semantics), computed on the device so it can feed K6's scale_ptr inside a HIP graph. Per-block
+// fp32 partial sums of squares, the last block (ticket) reduces them in fixed order: deterministic.
+constexpr int kNormBlocks = 256;
+template <typename TG>
+__global__ __launch_bounds__(256) void k_grad_clip_coef(const TG* __restrict__ g, int64_t n, float grad_scale,
+                                                       float max_norm, float* __restrict__ partial,
+                                                       uint32_t* __restrict__ ticket, float* __restrict__ out) {
+  __shared__ float red[256 / kWave];
+  float s = 0.f;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const float v = ldf(g, i);
+    s += v * v;
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = 0.f;
+    for (int w = 0; w < int(blockDim.x / kWave); w++) b += red[w];
+    partial[blockIdx.x] = b;
+    __threadfence();
+    if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __threadfence();
+      double tot = 0.0;
+      for (uint32_t k = 0; k < gridDim.x; k++) tot += double(__hip_atomic_load(partial + k, __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT));
+      const float norm = float(sqrt(tot)) * fabsf(grad_scale);
+      out[0] = fminf(1.f, max_norm / (norm + 1e-6f));
+      out[1] = norm;
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int64_t grad_clip_workspace_floats() { return kNormBlocks + 1; }
+
+void grad_clip_coef(const void* grad, bool grad_bf16, int64_t n, float grad_scale, float max_norm, float* workspace,
+                    float* out, hipStream_t stream) {
+  // workspace: kNormBlocks partial floats followed by one zero-initialised u32 ticket
+  const int blocks = int(std::max<int64_t>(1, std::min<int64_t>(kNormBlocks, (n + 255) / 256)));
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(workspace + kNormBlocks);
+  if (grad_bf16)
+    hipLaunchKernelGGL(k_grad_clip_coef<__hip_bfloat16>, dim3(blocks), dim3(256), 0, stream,
+                       static_cast<const __hip_bfloat16*>(grad), n, grad_scale, max_norm, workspace, ticket, out);
+  else
+    hipLaunchKernelGGL(k_grad_clip_coef<float>, dim3(blocks), dim3(256), 0, stream, static_cast<const float*>(grad),
+                       n, grad_scale, max_norm, workspace, ticket, out);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

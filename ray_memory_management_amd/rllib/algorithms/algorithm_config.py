@@ -52,6 +52,13 @@ class AlgorithmConfig:
         self.recreate_failed_workers = False
         # MI355X fast path: on-device vectorised env + fused learner
         self.gpu_rollouts = False
+        # learner actors: one data-parallel learner per GPU, gradients all-reduced over RCCL
+        # (0 = one learner in the driver process, the reference's default)
+        self.num_learner_workers = 0
+        self.num_gpus_per_learner_worker = 1
+        self.num_cpus_per_learner_worker = 1
+        # rollout workers ship raw fragments; GAE + advantage standardisation run on the learner GPU
+        self.postprocess_on_learner = False
 
     # ---- builder methods (each returns self)
     def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None,
@@ -74,7 +81,9 @@ class AlgorithmConfig:
         return self
 
     def rollouts(self, *, num_rollout_workers=None, num_envs_per_worker=None, rollout_fragment_length=None,
-                 batch_mode=None, gpu_rollouts=None, **kw) -> "AlgorithmConfig":
+                 batch_mode=None, gpu_rollouts=None, postprocess_on_learner=None, **kw) -> "AlgorithmConfig":
+        if postprocess_on_learner is not None:
+            self.postprocess_on_learner = bool(postprocess_on_learner)
         if num_rollout_workers is not None:
             self.num_workers = num_rollout_workers
         if num_envs_per_worker is not None:
@@ -105,7 +114,14 @@ class AlgorithmConfig:
         return self
 
     def resources(self, *, num_gpus=None, num_cpus_per_worker=None, num_gpus_per_worker=None,
-                  num_cpus_for_local_worker=None, **kw) -> "AlgorithmConfig":
+                  num_cpus_for_local_worker=None, num_learner_workers=None, num_gpus_per_learner_worker=None,
+                  num_cpus_per_learner_worker=None, **kw) -> "AlgorithmConfig":
+        if num_learner_workers is not None:
+            self.num_learner_workers = int(num_learner_workers)
+        if num_gpus_per_learner_worker is not None:
+            self.num_gpus_per_learner_worker = num_gpus_per_learner_worker
+        if num_cpus_per_learner_worker is not None:
+            self.num_cpus_per_learner_worker = num_cpus_per_learner_worker
         if num_gpus is not None:
             self.num_gpus = num_gpus
         if num_cpus_per_worker is not None:

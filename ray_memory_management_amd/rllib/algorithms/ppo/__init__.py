@@ -2,6 +2,10 @@
 PPO.training_step: synchronous_parallel_sample -> standardize advantages ->
 multi_gpu_train_one_step (num_sgd_iter x minibatches) -> sync weights -> UpdateKL).
 
+With ``num_learner_workers=N`` the learner is N GPU learner actors (rllib/execution/learner_group.py)
+averaging gradients over RCCL; with ``postprocess_on_learner=True`` rollout workers ship raw
+fragments and GAE + advantage standardisation run on the learner GPUs (K17).
+
 On MI355X the learner is the fused PPOLearner (bf16 weights / fp32 master, HIP-graph SGD steps,
 K5 loss, K6 Adam); with `gpu_rollouts=True` and a GPU-vectorisable env the sampler is the
 on-device GPURolloutSampler too (the bench.py configuration).
@@ -12,6 +16,7 @@ from typing import Dict
 
 import torch
 
+import ray_memory_management_amd as ray
 from ray_memory_management_amd.rllib.algorithms.algorithm import Algorithm
 from ray_memory_management_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_memory_management_amd.rllib.sample_batch import SampleBatch
@@ -66,21 +71,49 @@ class PPO(Algorithm):
                              f"({c.train_batch_size}).")
         if c.entropy_coeff < 0:
             raise ValueError("`entropy_coeff` must be >= 0.0")
+        if c.num_learner_workers and c.num_learner_workers > 1:
+            if c.train_batch_size % c.num_learner_workers or c.sgd_minibatch_size % c.num_learner_workers:
+                raise ValueError("train_batch_size and sgd_minibatch_size are totals across learner workers: "
+                                 "they must be divisible by num_learner_workers")
+            if c.num_workers % c.num_learner_workers:
+                raise ValueError("num_workers (rollout workers) must be a multiple of num_learner_workers so "
+                                 "every learner trains on the same number of fragments")
+
+    def _learner_cfg(self, n_learners: int = 1) -> dict:
+        c = self.algo_config
+        return dict(gamma=c.gamma, lambda_=c.lambda_, kl_coeff=c.kl_coeff, kl_target=c.kl_target,
+                    clip_param=c.clip_param, vf_clip_param=c.vf_clip_param, vf_loss_coeff=c.vf_loss_coeff,
+                    entropy_coeff=c.entropy_coeff, lr=c.lr, train_batch_size=c.train_batch_size // n_learners,
+                    sgd_minibatch_size=c.sgd_minibatch_size // n_learners, num_sgd_iter=c.num_sgd_iter,
+                    grad_clip=c.grad_clip, lr_schedule=c.lr_schedule,
+                    entropy_coeff_schedule=c.entropy_coeff_schedule)
 
     def _setup_learner(self):
         from ray_memory_management_amd.rllib.ppo_learner import PPOLearner
 
         c = self.algo_config
-        dev = "cuda" if c.num_gpus and torch.cuda.is_available() else "cpu"
         local = self.workers.local_worker()
+        self.learner = None
+        self.learner_group = None
+        self._weights_ref = None
+        if c.num_learner_workers and c.num_learner_workers > 0:
+            from ray_memory_management_amd.rllib.execution.learner_group import LearnerGroup
+
+            n = int(c.num_learner_workers)
+            self.learner_group = LearnerGroup(
+                n, local.env.observation_space, local.env.action_space, c.model, self._learner_cfg(n),
+                num_gpus_per_learner=c.num_gpus_per_learner_worker,
+                num_cpus_per_learner=c.num_cpus_per_learner_worker, seed=int(c.seed or 0))
+            self._device = "learner_actors"
+            self._weights_ref = self.learner_group.weights_ref()
+            local.set_weights(ray.get(self._weights_ref))
+            self.workers.sync_weights(ref=self._weights_ref)
+            return
         import copy
 
+        dev = "cuda" if c.num_gpus and torch.cuda.is_available() else "cpu"
         model = copy.deepcopy(local.policy.model)
-        lcfg = dict(gamma=c.gamma, lambda_=c.lambda_, kl_coeff=c.kl_coeff, kl_target=c.kl_target,
-                    clip_param=c.clip_param, vf_clip_param=c.vf_clip_param, vf_loss_coeff=c.vf_loss_coeff,
-                    entropy_coeff=c.entropy_coeff, lr=c.lr, train_batch_size=c.train_batch_size,
-                    sgd_minibatch_size=c.sgd_minibatch_size, num_sgd_iter=c.num_sgd_iter, grad_clip=c.grad_clip)
-        self.learner = PPOLearner(model, lcfg, device=dev, action_space=local.env.action_space)
+        self.learner = PPOLearner(model, self._learner_cfg(), device=dev, action_space=local.env.action_space)
         self._device = dev
         self._sync_from_learner()
 
@@ -90,33 +123,107 @@ class PPO(Algorithm):
         self.workers.sync_weights(w)
 
     def training_step(self) -> Dict:
+        if self.learner_group is not None:
+            return self._training_step_learner_actors()
         c = self.algo_config
-        batch = self.workers.synchronous_parallel_sample(c.train_batch_size)
-        n = batch.count
+        batch = self.workers.synchronous_parallel_sample(c.train_batch_size, concat=not c.postprocess_on_learner)
+        n = sum(b.count for b in batch) if isinstance(batch, list) else batch.count
         self._counters["num_env_steps_sampled"] += n
         self._timesteps_total += n
-        batch = SampleBatch({k: torch.as_tensor(v) for k, v in batch.items()})
-        if self._device != "cpu":
-            batch = batch.to_device(self._device)
-        stats = self.learner.update(batch)
+        if c.postprocess_on_learner:
+            st = self.learner.update_fragments(batch)
+        else:
+            batch = SampleBatch({k: torch.as_tensor(v) for k, v in batch.items()})
+            if self._device != "cpu":
+                batch = batch.to_device(self._device)
+            st = self.learner.update(batch)
         self._counters["num_env_steps_trained"] += n
         self._counters["num_agent_steps_trained"] += n
         self._sync_from_learner()
-        return dict(stats)
+        return dict(st)
+
+    def _training_step_learner_actors(self) -> Dict:
+        """synchronous_parallel_sample over the rollout actors (each first loads the weights the
+        learners published last iteration — same actor queue, so no extra round trip) → every
+        learner actor trains on its shard of fragments straight from the object store → learner 0
+        publishes the new weights as an object ref for the next round. The driver only sees refs
+        and the small stats dicts."""
+        from ray_memory_management_amd.rllib.execution.sample_ingest import split_for_learners
+
+        c = self.algo_config
+        remote = self.workers.remote_workers()
+        if not remote:
+            raise ValueError("learner actors need remote rollout workers (num_workers > 0)")
+        n_l = self.learner_group.n
+        refs, steps = [], 0
+        per_round = c.num_workers * c.rollout_fragment_length * c.num_envs_per_worker
+        rounds = max(1, -(-c.train_batch_size // max(per_round, 1)))
+        for r in range(rounds):
+            for w in remote:
+                if r == 0 and self._weights_ref is not None:
+                    w.set_weights.remote(self._weights_ref)
+                refs.append(w.sample.remote())
+            steps += per_round
+        if c.postprocess_on_learner:
+            stats = self.learner_group.update(split_for_learners(refs, n_l))
+        else:
+            from ray_memory_management_amd.rllib.sample_batch import concat_samples
+
+            shards = split_for_learners(refs, n_l)
+            stats = ray.get([l.update_batch.remote(concat_samples(ray.get(s)))
+                             for l, s in zip(self.learner_group.learners, shards)])
+        self._weights_ref = self.learner_group.weights_ref()
+        self._counters["num_env_steps_sampled"] += steps
+        self._counters["num_env_steps_trained"] += steps
+        self._counters["num_agent_steps_trained"] += steps
+        self._timesteps_total += steps
+        st = dict(stats[0])
+        st["num_learners"] = n_l
+        st["learner_update_s_max"] = max(s.get("learner_update_s", 0.0) for s in stats)
+        return st
 
     def _extra_state(self):
-        return {"kl_coeff": self.learner.kl_coeff}
+        if self.learner_group is not None:
+            s = self.learner_group.get_state()
+            return {"kl_coeff": s["kl_coeff"], "learner_timesteps": s["timesteps"]}
+        return {"kl_coeff": self.learner.kl_coeff, "learner_timesteps": self.learner.timesteps}
 
     def _load_extra_state(self, s):
+        if self.learner_group is not None:
+            st = self.learner_group.get_state()
+            st.update({"kl_coeff": s.get("kl_coeff", st["kl_coeff"]),
+                       "timesteps": s.get("learner_timesteps", st["timesteps"])})
+            self.learner_group.set_state(st)
+            return
         if "kl_coeff" in s:
             self.learner.kl_coeff = s["kl_coeff"]
+        if "learner_timesteps" in s:
+            self.learner.timesteps = s["learner_timesteps"]
 
     def get_weights(self):
+        if self.learner_group is not None:
+            return self.learner_group.get_weights()
         return self.learner.get_weights()
 
     def set_weights(self, weights):
+        if self.learner_group is not None:
+            self.learner_group.set_weights(weights)
+            self._weights_ref = self.learner_group.weights_ref()
+            self.workers.local_worker().set_weights(weights)
+            self.workers.sync_weights(ref=self._weights_ref)
+            return
         self.learner.set_weights(weights)
         self._sync_from_learner()
+
+    def get_policy(self, policy_id: str = "default_policy"):
+        if self.learner_group is not None and self._weights_ref is not None:
+            self.workers.local_worker().set_weights(ray.get(self._weights_ref))
+        return super().get_policy(policy_id)
+
+    def cleanup(self):
+        if getattr(self, "learner_group", None) is not None:
+            self.learner_group.stop()
+        super().cleanup()
 
 
 DEFAULT_CONFIG = PPOConfig().to_dict()

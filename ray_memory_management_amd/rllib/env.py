@@ -177,6 +177,46 @@ class VectorEnv:
         return obs, rew, done, info
 
 
+class CPUSyntheticAtariVectorEnv:
+    """numpy-vectorised synthetic Atari env for CPU rollout workers: `num_envs` envs stepped in
+    lock-step, frame stacks [n, 4, 84, 84] uint8 (channels-first, the layout the learner's fused
+    trunk reads, so ingest is a straight DMA). A step shifts in one pooled random frame per env,
+    column-rolled by an action-dependent amount (a cheap stand-in for game dynamics); rewards are
+    sparse Bernoulli(0.05); episodes truncate at `episode_len` (staggered starts). Same statistics
+    as SyntheticAtariEnv / GPUSyntheticAtariVectorEnv. Reference role: the vector env a RolloutWorker
+    steps (rllib/env/vector_env.py) with the Atari frame-stack wrapper (rllib/env/wrappers/atari_wrappers.py)."""
+
+    is_native_vector_env = True
+
+    def __init__(self, num_envs: int, config=None):
+        config = dict(config or {})
+        self.num_envs = int(num_envs)
+        self.num_actions = int(config.get("num_actions", 4))
+        self.episode_len = int(config.get("episode_len", 1000))
+        self.rng = np.random.default_rng(config.get("seed"))
+        pool = self.rng.integers(0, 256, size=(64, 84, 84), dtype=np.uint8)
+        # one pre-rolled copy of the pool per action: a step is a single fancy-index gather
+        self._pools = np.stack([np.roll(pool, 3 * (a % 4) + 1, axis=2) for a in range(self.num_actions)])
+        self.frames = np.ascontiguousarray(pool[self.rng.integers(0, 64, size=(self.num_envs, 4))])
+        self.t = self.rng.integers(0, self.episode_len, size=self.num_envs)
+        self.observation_space = Box(0, 255, shape=(4, 84, 84), dtype=np.uint8)
+        self.action_space = Discrete(self.num_actions)
+
+    def vector_reset(self):
+        return self.frames
+
+    def vector_step(self, actions):
+        a = np.asarray(actions, dtype=np.int64) % self.num_actions
+        k = self.rng.integers(0, 64, size=self.num_envs)
+        self.frames[:, :3] = self.frames[:, 1:].copy()
+        self.frames[:, 3] = self._pools[a, k]
+        self.t += 1
+        rew = (self.rng.random(self.num_envs) < 0.05).astype(np.float32)
+        done = self.t >= self.episode_len
+        self.t[done] = 0
+        return self.frames, rew, done.astype(np.float32)
+
+
 class GPUSyntheticAtariVectorEnv:
     """Device-resident vectorised synthetic Atari env: B envs, frames [B, 4, 84, 84] uint8 on the
     GPU; a step rolls the frame stack and writes one new frame per env (action-dependent shift of
@@ -250,6 +290,26 @@ _REGISTRY = {
     "SyntheticAtari-v0": SyntheticAtariEnv,
     "BreakoutNoFrameskip-v4": SyntheticAtariEnv,
 }
+
+
+_VECTOR_REGISTRY = {
+    "SyntheticAtariVec-v0": CPUSyntheticAtariVectorEnv,
+}
+
+
+def register_vector_env(name: str, cls):
+    """Register a natively vectorised env class ``cls(num_envs, env_config)`` (vector_reset /
+    vector_step on whole batches)."""
+    _VECTOR_REGISTRY[name] = cls
+
+
+def make_vector_env(env, num_envs: int, config=None):
+    """A native vector env for `env` if one is registered (or `env` is such a class), else None."""
+    if isinstance(env, str) and env in _VECTOR_REGISTRY:
+        return _VECTOR_REGISTRY[env](num_envs, config or {})
+    if isinstance(env, type) and getattr(env, "is_native_vector_env", False):
+        return env(num_envs, config or {})
+    return None
 
 
 def register_env(name: str, creator):

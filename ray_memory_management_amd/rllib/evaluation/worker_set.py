@@ -37,7 +37,13 @@ class WorkerSet:
     def num_remote_workers(self) -> int:
         return len(self._remote)
 
-    def sync_weights(self, weights=None, from_worker=None):
+    def sync_weights(self, weights=None, from_worker=None, ref=None):
+        """Broadcast weights to the remote workers through ONE store object (`ref` if the caller
+        already has one, e.g. the learner actor's returned weights)."""
+        if ref is not None:
+            if self._remote:
+                ray.get([w.set_weights.remote(ref) for w in self._remote])
+            return
         if weights is None:
             weights = (from_worker or self._local).get_weights()
         if self._remote:
@@ -52,8 +58,9 @@ class WorkerSet:
             out += ray.get([w.apply.remote(fn) for w in self._remote])
         return out
 
-    def synchronous_parallel_sample(self, max_env_steps: int) -> SampleBatch:
-        """Sample until >= max_env_steps were collected (reference rollout_ops.py)."""
+    def synchronous_parallel_sample(self, max_env_steps: int, concat: bool = True):
+        """Sample until >= max_env_steps were collected (reference rollout_ops.py). concat=False
+        returns the list of per-worker batches (fragments keep their layout for learner ingest)."""
         batches, steps = [], 0
         while steps < max_env_steps:
             if self._remote:
@@ -63,7 +70,7 @@ class WorkerSet:
             for b in new:
                 steps += b.count
             batches += new
-        return concat_samples(batches)
+        return concat_samples(batches) if concat else batches
 
     def collect_metrics(self) -> List[tuple]:
         out = list(self._local.get_metrics()) if self._local is not None else []

@@ -42,6 +42,7 @@ DEFAULT_PPO = dict(
     vf_loss_coeff=1.0, entropy_coeff=0.01, lr=5e-5, train_batch_size=5000, sgd_minibatch_size=500,
     num_sgd_iter=10, grad_clip=None, standardize_advantages=True, use_graphs=True, fused=True,
     allreduce_in_graph=False, adam_betas=(0.9, 0.999), adam_eps=1e-8, weight_decay=0.0,
+    lr_schedule=None, entropy_coeff_schedule=None, manual_step=True,
 )
 
 _LOSS_KEYS = (SampleBatch.OBS, SampleBatch.ACTIONS, SampleBatch.ACTION_LOGP, SampleBatch.ACTION_DIST_INPUTS,
@@ -150,35 +151,44 @@ def ppo_categorical_loss_reference(logits, values, old_logits, actions, old_logp
 
 
 class PPOLearner:
+    """Data-parallel PPO learner on one device (see module docstring). `comm` selects the
+    process group that averages gradients: None → torch.distributed's default group when it is
+    initialised (torchrun ranks), a util.collective group name (learner actors), or a Comm."""
+
     def __init__(self, model: nn.Module, config: Optional[dict] = None, device="cuda", process_group=None,
-                 action_space=None):
+                 action_space=None, comm=None):
+        from ray_memory_management_amd.parallel.comm import as_comm
+        from ray_memory_management_amd.rllib.utils.schedules import make_schedule
+
         self.cfg = {**DEFAULT_PPO, **(config or {})}
         self.device = torch.device(device)
         self.dist_cls = dist_class_for(action_space) if action_space is not None else Categorical
         self.fast = (self.device.type == "cuda" and bool(self.cfg["fused"]) and self.dist_cls is Categorical)
-        self.pg = process_group
-        self.world = 1
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            self.world = torch.distributed.get_world_size(process_group)
+        self.comm = as_comm(comm if comm is not None else process_group)
+        self.world = self.comm.world
         model = model.to(self.device)
         if self.device.type == "cuda":
             model = model.to(memory_format=torch.channels_last)
         self.model = model
         params = [p for p in model.parameters() if p.requires_grad]
-        if self.world > 1:  # identical initial weights: broadcast rank 0's
+        if self.world > 1:  # identical initial weights: broadcast rank 0's (one flat collective)
             with torch.no_grad():
                 flat = torch.cat([p.detach().float().reshape(-1) for p in params])
-                src = torch.distributed.get_global_rank(process_group, 0) if process_group is not None else 0
-                torch.distributed.broadcast(flat, src=src, group=process_group)
+                self.comm.broadcast(flat, 0)
                 off = 0
                 for p in params:
                     p.copy_(flat[off:off + p.numel()].view(p.shape))
                     off += p.numel()
         self.kl_coeff = float(self.cfg["kl_coeff"])
+        self.lr_sched = make_schedule(self.cfg.get("lr_schedule"), self.cfg["lr"])
+        self.ent_sched = make_schedule(self.cfg.get("entropy_coeff_schedule"), self.cfg["entropy_coeff"])
+        self.timesteps = 0  # global env steps trained (drives the schedules)
         self.stats: Dict[str, float] = {}
         self._graph = None
+        self._graphs_split = None
         self._static = None
         self._mbs = None
+        self._ingest = None
         if self.fast:
             self._init_fast(params)
         else:
@@ -229,16 +239,108 @@ class PPOLearner:
         self._bump_done = torch.zeros(require_hip().bump_done_words(), dtype=torch.int32, device=dev)
         self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.heads_ok = hasattr(self.model, "forward_heads")
+        # global-norm gradient clipping on the device (K6b → K6 scale pointer), graph-capturable
+        self.clip_ws = self.clip_out = None
+        if self.cfg["grad_clip"]:
+            self.clip_ws = torch.zeros(require_hip().grad_clip_workspace_floats(), dtype=torch.float32, device=dev)
+            self.clip_out = torch.ones(2, dtype=torch.float32, device=dev)
+        self._manual = self._manual_layout()
 
-    def _opt_step(self):
+    def _manual_layout(self):
+        """The flagship Nature-CNN model runs its SGD step as explicit kernel launches (no autograd):
+        K10 fwd → K13 → K15 → K12 → K10 bwd, which lets a multi-rank step all-reduce the dense+heads
+        bucket (≈99% of the gradient, ready after K12) WHILE the trunk backward runs. Returns the
+        trunk/dense split of the flat bucket, or None when the model does not have that layout."""
+        from ray_memory_management_amd.rllib.models import VisionNetwork
+
+        m = self.model
+        if not (self.cfg.get("manual_step", True) and isinstance(m, VisionNetwork) and m.nature
+                and m.dense_tail is not None and not os.environ.get("RMM_NO_MANUAL_STEP")):
+            return None
+        c1, c2 = m.convs[0], m.convs[1]
+        order = [c1.weight, c1.bias, c2.weight, c2.bias, m.dense_tail.weight, m.dense_tail.bias, m.heads.weight,
+                 m.heads.bias]
+        if len(order) != len(self.params) or any(a is not b for a, b in zip(order, self.params)):
+            return None
+        if not (m.dense_tail.out_features == 256 and m.dense_tail.in_features % 32 == 0
+                and 3 <= m.heads.out_features <= 16 and m.dense_tail.weight.is_contiguous()
+                and m.heads.weight.is_contiguous()):
+            return None
+        return sum(p.numel() for p in order[:4])
+
+    def _manual_ok(self, full) -> bool:
+        return (self._manual is not None and full["obs"].dtype == torch.uint8 and full["mbs"] <= 640
+                and self.model.fused_trunk_ok(full["obs"]) and not os.environ.get("RMM_NO_K12")
+                and not os.environ.get("RMM_NO_K15"))
+
+    def _manual_ws(self, mbs):
+        ws = getattr(self, "_mws", None)
+        if ws is not None and ws["mbs"] == mbs:
+            return ws
+        dev, bf = self.device, torch.bfloat16
+        A1 = self.model.heads.out_features
+        K = self.model.dense_tail.in_features
+        ws = {"mbs": mbs, "h1": torch.empty((mbs, 441, 16), dtype=bf, device=dev),
+              "h2": torch.empty((mbs, K), dtype=bf, device=dev), "hidden": torch.empty((mbs, 256), dtype=bf, device=dev),
+              "dz": torch.empty((mbs, A1), dtype=bf, device=dev), "dpre": torch.empty((mbs, 256), dtype=bf, device=dev),
+              "dx": torch.empty((mbs, K), dtype=bf, device=dev),
+              "part": torch.empty(require_hip().nature_trunk_partial_floats(mbs), dtype=torch.float32, device=dev)}
+        self._mws = ws
+        return ws
+
+    def _manual_fwd_dense_bwd(self, full):
+        """K10 fwd → K13 → K15 (loss stats + dheads + dpre) → K12: dense+heads grads into the bucket."""
         h = require_hip()
-        if self.world > 1:
-            torch.distributed.all_reduce(self.flat_grad, group=self.pg)
-        # K6 also advances both device counters {minibatch step, Adam step} from its last workgroup
+        m = self.model
+        c1, c2, dl, hd = m.convs[0], m.convs[1], m.dense_tail, m.heads
+        mbs, period, idx, ctr = full["mbs"], full["period"], full["idx"], self.ctr
+        ws = self._manual_ws(mbs)
+        st = _stream()
+        K, A1 = dl.in_features, hd.out_features
+        h.nature_trunk_fwd(full["obs"].data_ptr(), idx.data_ptr(), ctr.data_ptr(), int(period), int(mbs),
+                           c1.weight.data_ptr(), list(c1.weight.stride()), c1.bias.data_ptr(), c2.weight.data_ptr(),
+                           list(c2.weight.stride()), c2.bias.data_ptr(), ws["h1"].data_ptr(), ws["h2"].data_ptr(), st)
+        h.dense_relu_fwd(ws["h2"].data_ptr(), dl.weight.data_ptr(), dl.bias.data_ptr(), mbs, K, 256,
+                         ws["hidden"].data_ptr(), st)
+        h.dense_heads_ppo(ws["hidden"].data_ptr(), hd.weight.data_ptr(), hd.bias.data_ptr(), full["cols"].data_ptr(),
+                          self.coef.data_ptr(), self.acc.data_ptr(), self._one.data_ptr(), mbs, A1,
+                          ws["dz"].data_ptr(), ws["dpre"].data_ptr(), st, cidx=idx.data_ptr(), ctr=ctr.data_ptr(),
+                          period=int(period))
+        g = [p._rmm_grad_out for p in self.params]
+        h.dense_heads_bwd(ws["dz"].data_ptr(), A1, hd.weight.data_ptr(), ws["hidden"].data_ptr(), ws["h2"].data_ptr(),
+                          dl.weight.data_ptr(), mbs, K, ws["dx"].data_ptr(), g[4].data_ptr(), g[5].data_ptr(),
+                          g[6].data_ptr(), g[7].data_ptr(), ws["dpre"].data_ptr(), st, dpre_ready=True)
+
+    def _manual_trunk_bwd(self, full):
+        """K10 backward: trunk grads (conv1/conv2 weights + biases) into the bucket."""
+        h = require_hip()
+        c1, c2 = self.model.convs[0], self.model.convs[1]
+        ws = self._manual_ws(full["mbs"])
+        g = [p._rmm_grad_out for p in self.params]
+        h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), self.ctr.data_ptr(), int(full["period"]),
+                           int(full["mbs"]), c2.weight.data_ptr(), list(c2.weight.stride()), ws["h1"].data_ptr(),
+                           ws["h2"].data_ptr(), ws["dx"].data_ptr(), ws["part"].data_ptr(), g[0].data_ptr(),
+                           list(c1.weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream())
+
+    def _opt_launch(self):
+        """[K6b global-norm clip coefficient →] K6 Adam; K6 also advances both device counters
+        {minibatch step, Adam step} from its last workgroup. Graph-capturable."""
+        h = require_hip()
+        scale_ptr = 0
+        if self.clip_out is not None:
+            h.grad_clip_coef(self.flat_grad.data_ptr(), True, self.n_params, 1.0 / self.world,
+                             float(self.cfg["grad_clip"]), self.clip_ws.data_ptr(), self.clip_out.data_ptr(),
+                             _stream())
+            scale_ptr = self.clip_out.data_ptr()
         h.adam_flat(self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
                     self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream(),
                     step_ctr=self.ctr.data_ptr() + 8, bump=self.ctr.data_ptr(), nbump=2,
-                    done=self._bump_done.data_ptr())
+                    done=self._bump_done.data_ptr(), scale_ptr=scale_ptr)
+
+    def _opt_step(self):
+        if self.world > 1:
+            self.comm.allreduce(self.flat_grad)
+        self._opt_launch()
 
     def _fast_step(self, full, with_opt: bool):
         h = require_hip()
@@ -257,13 +359,13 @@ class PPOLearner:
             x = ops.gather_rows(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         cols = None if fused else ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
         if fused:  # K10 trunk → K13 → K15 (heads + PPO loss + dheads + dpre, cols gathered in place); bwd K12 → K10
-            total, h = self.model.forward_frames_ppo(full["obs"], full["cols"], self.coef, self.acc, self._one,
-                                                     idx=full["idx"], ctr=ctr, period=period, rows=mbs)
+            total, trunk = self.model.forward_frames_ppo(full["obs"], full["cols"], self.coef, self.acc, self._one,
+                                                         idx=full["idx"], ctr=ctr, period=period, rows=mbs)
             if total is None:
                 cols = ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
                 from ray_memory_management_amd.rllib.models import dense_heads
 
-                heads = dense_heads(h, self.model.dense_tail, self.model.heads)
+                heads = dense_heads(trunk, self.model.dense_tail, self.model.heads)
                 total = ppo_heads_loss(heads, cols, self.coef, self.acc, gout=self._one)  # K5c, fwd+bwd
             grads = list(torch.autograd.grad(total, self.params, grad_outputs=self._one))
         elif self.heads_ok and frames:
@@ -293,52 +395,150 @@ class PPOLearner:
         if with_opt:  # otherwise the caller runs _opt_step (all-reduce + Adam + counters) eagerly
             self._opt_step()
 
-    def _pack(self, batch, mbs, nmb):
-        """One fp32 column matrix [n, A+4] (old logits, old logp, adv, value target, action) and the
-        whole update's minibatch index table [iters * nmb * mbs] (one rand + one sort launch)."""
-        A = batch[SampleBatch.ACTION_DIST_INPUTS].shape[-1]
+    # ------------------------------------------------------------------ one SGD step (any mode)
+    def _step_eager(self, full):
+        """One minibatch step without graphs: manual kernels (overlapped all-reduce) or autograd."""
+        if self._manual_ok(full):
+            self._manual_fwd_dense_bwd(full)
+            if self.world > 1:
+                work = self.comm.allreduce_async(self.flat_grad[self._manual:])   # dense+heads bucket
+                self._manual_trunk_bwd(full)                                        # overlaps the RCCL op
+                work2 = self.comm.allreduce_async(self.flat_grad[:self._manual])  # trunk bucket
+                work.wait()
+                work2.wait()
+            else:
+                self._manual_trunk_bwd(full)
+            self._opt_launch()
+        else:
+            self._fast_step(full, True)
+
+    def _make_cols(self, batch):
+        """One fp32 column matrix [n, A+4] (old logits, old logp, adv, value target, action)."""
         n = batch.count
-        cols = torch.cat([batch[SampleBatch.ACTION_DIST_INPUTS].float(),
+        return torch.cat([batch[SampleBatch.ACTION_DIST_INPUTS].float(),
                           batch[SampleBatch.ACTION_LOGP].float().unsqueeze(1),
                           batch[SampleBatch.ADVANTAGES].float().unsqueeze(1),
                           batch[SampleBatch.VALUE_TARGETS].float().unsqueeze(1),
                           batch[SampleBatch.ACTIONS].float().reshape(n, 1)], dim=1).contiguous()
+
+    def _pack(self, obs, cols, A, mbs, nmb):
+        """The whole update's minibatch index table [iters * nmb * mbs] (one rand + one sort)."""
+        n = obs.shape[0]
         iters = self.cfg["num_sgd_iter"]
         idx = torch.rand(iters, n, device=self.device).argsort(dim=1)[:, :nmb * mbs].reshape(-1).contiguous()
-        return {"obs": batch[SampleBatch.OBS].contiguous(), "cols": cols, "idx": idx, "A": A, "mbs": mbs,
-                "period": iters * nmb}
+        return {"obs": obs.contiguous(), "cols": cols, "idx": idx, "A": A, "mbs": mbs, "period": iters * nmb}
 
     def _capture(self, full):
-        in_graph_opt = self.world == 1 or self.cfg["allreduce_in_graph"]
         saved = (self.master.clone(), self.m1.clone(), self.m2.clone(), self.w_bf16.clone(), self.ctr.clone(),
                  self.acc.clone())
+        manual = self._manual_ok(full)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(3):  # warm up (MIOpen find, allocator) before capture
-                self._fast_step(full, in_graph_opt)
+            for _ in range(3):  # warm up (MIOpen find, allocator, RCCL communicator) before capture
+                self._step_eager(full)
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._fast_step(full, in_graph_opt)
+        self._graph = self._graphs_split = None
+        if self.world == 1 or self.cfg["allreduce_in_graph"]:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                if manual:
+                    self._manual_fwd_dense_bwd(full)
+                    if self.world > 1:
+                        self.comm.allreduce(self.flat_grad[self._manual:])
+                    self._manual_trunk_bwd(full)
+                    if self.world > 1:
+                        self.comm.allreduce(self.flat_grad[:self._manual])
+                    self._opt_launch()
+                else:
+                    self._fast_step(full, True)
+            self._graph = g
+        elif manual:
+            # multi-rank: three graphs with the two bucket all-reduces between them, so the
+            # dense+heads all-reduce (issued after graph A) runs on RCCL's stream during graph B
+            ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self._manual_fwd_dense_bwd(full)
+            with torch.cuda.graph(gb):
+                self._manual_trunk_bwd(full)
+            with torch.cuda.graph(gc):
+                self._opt_launch()
+            self._graphs_split = (ga, gb, gc)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._fast_step(full, False)
+            self._graph = g
         for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc), saved):
             dst.copy_(src)  # undo warm-up updates
-        self._graph = g
-        self._graph_opt = in_graph_opt
+
+    def _replay(self):
+        if self._graphs_split is not None:
+            ga, gb, gc = self._graphs_split
+            ga.replay()
+            work = self.comm.allreduce_async(self.flat_grad[self._manual:])
+            gb.replay()
+            work2 = self.comm.allreduce_async(self.flat_grad[:self._manual])
+            work.wait()
+            work2.wait()
+            gc.replay()
+        elif self.world > 1 and not self.cfg["allreduce_in_graph"]:
+            self._graph.replay()
+            self._opt_step()
+        else:
+            self._graph.replay()
+
+    def _apply_schedules(self):
+        lr = float(self.lr_sched(self.timesteps))
+        ent = float(self.ent_sched(self.timesteps))
+        if self.fast:
+            self.hp[0].fill_(lr)
+            self.coef[3].fill_(ent)
+        else:
+            for g in self.opt.param_groups:
+                g["lr"] = lr
+        self.cur_lr, self.cur_entropy_coeff = lr, ent
 
     # ------------------------------------------------------------------ update
     def update(self, batch: SampleBatch) -> Dict[str, float]:
-        """num_sgd_iter epochs of shuffled minibatch SGD over a device-resident batch."""
+        """num_sgd_iter epochs of shuffled minibatch SGD over a (device-resident) batch."""
         c = self.cfg
         if c["standardize_advantages"]:
             a = batch[SampleBatch.ADVANTAGES].float()
-            batch[SampleBatch.ADVANTAGES] = (a - a.mean()) / a.std().clamp_min(1e-4)
-        n = batch.count
+            batch[SampleBatch.ADVANTAGES] = (a - a.mean()) / a.std(unbiased=False).clamp_min(1e-4)
+        if not self.fast:
+            self._apply_schedules()
+            return self._update_eager(batch, min(c["sgd_minibatch_size"], batch.count))
+        A = batch[SampleBatch.ACTION_DIST_INPUTS].shape[-1]
+        return self._update_tables(batch[SampleBatch.OBS], self._make_cols(batch), A)
+
+    def update_fragments(self, frags) -> Dict[str, float]:
+        """Train on rollout fragments straight from the object store (postprocess_on_learner):
+        K17 ingest (DMA + GAE + advantage standardisation on the GPU), then the SGD epochs."""
+        from ray_memory_management_amd.rllib.execution.sample_ingest import (SampleIngest, fragment_dims,
+                                                                              fragments_to_batch_cpu)
+
+        c = self.cfg
+        A = fragment_dims(frags[0])[2]
+        if not self.fast:
+            obs, cols = fragments_to_batch_cpu(frags, c["gamma"], c["lambda_"], c["standardize_advantages"])
+            batch = SampleBatch({SampleBatch.OBS: obs, SampleBatch.ACTION_DIST_INPUTS: cols[:, :A],
+                                 SampleBatch.ACTION_LOGP: cols[:, A], SampleBatch.ADVANTAGES: cols[:, A + 1],
+                                 SampleBatch.VALUE_TARGETS: cols[:, A + 2], SampleBatch.ACTIONS: cols[:, A + 3].long()})
+            self._apply_schedules()
+            return self._update_eager(batch, min(c["sgd_minibatch_size"], batch.count))
+        if self._ingest is None:
+            self._ingest = SampleIngest(self.device, c["gamma"], c["lambda_"])
+        obs, cols = self._ingest.ingest(frags, standardize=c["standardize_advantages"])
+        return self._update_tables(obs, cols, A)
+
+    def _update_tables(self, obs, cols, A):
+        c = self.cfg
+        n = obs.shape[0]
         mbs = min(c["sgd_minibatch_size"], n)
         nmb = max(n // mbs, 1)
-        if not self.fast:
-            return self._update_eager(batch, mbs)
-        packed = self._pack(batch, mbs, nmb)
+        self._apply_schedules()
+        packed = self._pack(obs, cols, A, mbs, nmb)
         self.acc.zero_()
         self.coef[4].fill_(self.kl_coeff)
         if self.graphs:
@@ -346,11 +546,12 @@ class PPOLearner:
             if st is None or any(st[k].shape != packed[k].shape for k in ("obs", "cols", "idx")) \
                     or st["mbs"] != mbs:
                 self._static = st = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in packed.items()}
-                self._graph = None
+                self._graph = self._graphs_split = None
             else:
                 for k in ("obs", "cols", "idx"):
-                    st[k].copy_(packed[k])
-            if self._graph is None:
+                    if st[k].data_ptr() != packed[k].data_ptr():
+                        st[k].copy_(packed[k])
+            if self._graph is None and self._graphs_split is None:
                 try:
                     self._capture(st)
                 except Exception as e:  # pragma: no cover - capture unsupported: stay eager
@@ -364,17 +565,19 @@ class PPOLearner:
         steps = 0
         for _ in range(c["num_sgd_iter"] * nmb):
             if self.graphs:
-                self._graph.replay()
-                if not self._graph_opt:
-                    self._opt_step()
+                self._replay()
             else:
-                self._fast_step(full, True)
+                self._step_eager(full)
             steps += 1
         if self.world > 1:  # KL adaptation and stats from the global batch, identical on every rank
-            torch.distributed.all_reduce(self.acc, group=self.pg)
+            self.comm.allreduce(self.acc)
             self.acc.mul_(1.0 / self.world)
         acc = (self.acc / float(max(steps, 1) * mbs)).tolist()  # one host sync per update
-        return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
+        self.timesteps += n * self.world
+        st = self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
+        if self.clip_out is not None:
+            st["grad_gnorm"] = float(self.clip_out[1])
+        return st
 
     def _finish(self, pol, vf, ent, kl_mean, total, steps):
         c = self.cfg
@@ -384,12 +587,13 @@ class PPOLearner:
         elif kl_mean < 0.5 * c["kl_target"]:
             self.kl_coeff *= 0.5
         self.stats = {"total_loss": total, "policy_loss": pol, "vf_loss": vf, "entropy": ent, "kl": kl_mean,
-                      "cur_kl_coeff": self.kl_coeff, "num_sgd_steps": steps}
+                      "cur_kl_coeff": self.kl_coeff, "num_sgd_steps": steps, "cur_lr": self.cur_lr,
+                      "entropy_coeff": self.cur_entropy_coeff}
         return self.stats
 
     def _update_eager(self, batch, mbs):
         c = self.cfg
-        coef = torch.tensor([c["clip_param"], c["vf_clip_param"], c["vf_loss_coeff"], c["entropy_coeff"],
+        coef = torch.tensor([c["clip_param"], c["vf_clip_param"], c["vf_loss_coeff"], self.cur_entropy_coeff,
                              self.kl_coeff])
         acc = torch.zeros(6)
         steps = 0
@@ -400,12 +604,19 @@ class PPOLearner:
                     logits, v, mb[SampleBatch.ACTION_DIST_INPUTS], mb[SampleBatch.ACTIONS],
                     mb[SampleBatch.ACTION_LOGP].float(), mb[SampleBatch.ADVANTAGES].float(),
                     mb[SampleBatch.VALUE_TARGETS].float(), coef)
-                self.opt.zero_grad(set_to_none=True)
+                self.opt.zero_grad(set_to_none=False)
                 total.backward()
-                if self.world > 1:
+                if self.world > 1:  # one flat collective per step
                     for p in self.params:
-                        torch.distributed.all_reduce(p.grad, group=self.pg)
-                        p.grad.mul_(1.0 / self.world)
+                        if p.grad is None:
+                            p.grad = torch.zeros_like(p)
+                    flat = torch.cat([p.grad.reshape(-1) for p in self.params])
+                    self.comm.allreduce(flat)
+                    flat.mul_(1.0 / self.world)
+                    off = 0
+                    for p in self.params:
+                        p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+                        off += p.numel()
                 if c["grad_clip"]:
                     nn.utils.clip_grad_norm_(self.params, c["grad_clip"])
                 self.opt.step()
@@ -413,26 +624,34 @@ class PPOLearner:
                 steps += 1
         if self.world > 1:
             acc_d = acc.to(self.device)
-            torch.distributed.all_reduce(acc_d, group=self.pg)
+            self.comm.allreduce(acc_d)
             acc = acc_d.cpu() / self.world
         acc = (acc / max(steps, 1)).tolist()
+        self.timesteps += batch.count * self.world
         return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
 
-    def get_weights(self):
+    def get_weights(self, numpy: bool = False):
+        """fp32 weights keyed like the model's state_dict (ONE device→host copy of the flat masters
+        on the fast path). numpy=True returns contiguous ndarrays (zero-copy through the store)."""
+        sd = self.model.state_dict()
+        out = {}
         if self.fast:  # publish the fp32 masters (the bf16 weights are derived)
-            out, off = {}, 0
-            sd = self.model.state_dict()
+            flat = self.master.detach().cpu()
             names = {id(p): n for n, p in self.model.named_parameters()}
+            off = 0
             for p in self.params:
-                out[names[id(p)]] = self.master.as_strided(p.size(), p.stride(), off).detach().cpu().clone()
+                out[names[id(p)]] = flat.as_strided(p.size(), p.stride(), off).contiguous()
                 off += p.numel()
-            for k, v in sd.items():
-                out.setdefault(k, v.detach().cpu())
-            return out
-        return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        for k, v in sd.items():
+            if k not in out:
+                out[k] = v.detach().float().cpu().contiguous() if v.is_floating_point() else v.detach().cpu()
+        if numpy:
+            return {k: v.numpy() for k, v in out.items()}
+        return out
 
     def set_weights(self, w):
         with torch.no_grad():
+            w = {k: torch.as_tensor(v) for k, v in w.items()}
             if self.fast:
                 names = {id(p): n for n, p in self.model.named_parameters()}
                 off = 0

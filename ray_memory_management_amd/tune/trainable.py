@@ -94,8 +94,17 @@ class Trainable:
         result.setdefault("pid", os.getpid())
         return result
 
-    def save(self) -> Checkpoint:
-        """Checkpoint (as a dict-backed Checkpoint, transportable through the object store)."""
+    def save(self, checkpoint_dir: Optional[str] = None):
+        """Checkpoint (as a dict-backed Checkpoint, transportable through the object store). With
+        `checkpoint_dir` (reference Trainable.save(checkpoint_dir)) it is also written there and
+        the directory path is returned; restore() accepts either form."""
+        ck = self._save_checkpoint_obj()
+        if checkpoint_dir is None:
+            return ck
+        os.makedirs(checkpoint_dir, exist_ok=True)
+        return ck.to_directory(checkpoint_dir)
+
+    def _save_checkpoint_obj(self) -> Checkpoint:
         d = tempfile.mkdtemp(prefix="rmm_ckpt_")
         try:
             out = self.save_checkpoint(d)
@@ -110,7 +119,9 @@ class Trainable:
         finally:
             shutil.rmtree(d, ignore_errors=True)
 
-    def restore(self, checkpoint: Checkpoint):
+    def restore(self, checkpoint):
+        if isinstance(checkpoint, str):
+            checkpoint = Checkpoint.from_directory(checkpoint)
         data = checkpoint.to_dict()
         self._iteration = data.pop("_iteration", self._iteration)
         self._time_total = data.pop("_time_total", self._time_total)

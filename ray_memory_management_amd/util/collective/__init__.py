@@ -8,7 +8,7 @@ directly on a rendezvous store — no global default group, so an actor can be i
 store is a FileStore in the session directory (node-local); ranks find it by group name.
 """
 from ray_memory_management_amd.util.collective.collective import (  # noqa: F401
-    Backend, ReduceOp, allgather, alltoall, allgather_multigpu, allreduce, allreduce_multigpu, barrier, broadcast,
+    Backend, ReduceOp, allgather, alltoall, allreduce_async, allgather_multigpu, allreduce, allreduce_multigpu, barrier, broadcast,
     broadcast_multigpu, create_collective_group, destroy_collective_group, get_collective_group_size,
     get_group_handle, get_rank, init_collective_group, is_group_initialized, nccl_available, gloo_available,
     recv, reduce, reducescatter, send)

@@ -174,6 +174,14 @@ def allreduce(tensor, group_name: str = "default", op=ReduceOp.SUM):
     return tensor
 
 
+def allreduce_async(tensor, group_name: str = "default", op=ReduceOp.SUM):
+    """Non-blocking all-reduce: returns the work handle (``.wait()``). On an RCCL group the
+    collective runs on RCCL's stream after the caller's current stream; work issued before
+    ``wait()`` overlaps it (used by the learners to hide gradient buckets behind backward)."""
+    g = get_group_handle(group_name)
+    return _pg_for(g, tensor).allreduce([tensor], _opts(dist.AllreduceOptions, reduceOp=_TORCH_OP[op]))
+
+
 def allreduce_multigpu(tensor_list, group_name: str = "default", op=ReduceOp.SUM):
     for t in tensor_list:
         allreduce(t, group_name, op)
