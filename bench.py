@@ -112,6 +112,8 @@ def _fused_loop(args, world, rank, local_rank, dist_backend):
     from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler, PPOLearner
 
     require_hip()
+    if args.same_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device(f"cuda:{local_rank}")
     if world > 1 and not dist.is_initialized():
@@ -153,7 +155,8 @@ def _runtime(args, n_gpus):
     else:
         w_per, envs = 1, TRAIN_BATCH // args.fragment
         n_cpus = max(budget, 2 * n_gpus + 1)
-    ray.init(num_cpus=n_cpus, num_gpus=n_gpus, object_store_memory=args.store_gb << 30,
+    phys = 1 if args.same_device else n_gpus
+    ray.init(num_cpus=n_cpus, num_gpus=phys, object_store_memory=args.store_gb << 30,
              _system_config={"prestart_workers": 0})
     try:
         cfg = (PPOConfig()
@@ -165,8 +168,9 @@ def _runtime(args, n_gpus):
                .training(train_batch_size=TRAIN_BATCH * n_gpus, sgd_minibatch_size=args.minibatch * n_gpus,
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
                          vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99)
-               .resources(num_learner_workers=n_gpus, num_gpus_per_learner_worker=1,
-                          num_gpus_per_worker=0.5 if args.rollout == "gpu" else 0)
+               .resources(num_learner_workers=n_gpus, num_gpus_per_learner_worker=phys / n_gpus,
+                          num_gpus_per_worker=0.5 if args.rollout == "gpu" else 0,
+                          learner_collective_backend="gloo" if args.same_device else args.dist_backend)
                .debugging(seed=0))
         algo = cfg.build()
         info = {"rollout_workers": w_per * n_gpus, "envs_per_worker": envs, "learner_actors": n_gpus,
@@ -193,7 +197,9 @@ def main():
     ap.add_argument("--store-gb", type=int, default=8)
     ap.add_argument("--no-putget", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused-loop reference number (N=1)")
-    ap.add_argument("--dist-backend", default="nccl", help="fused mode: nccl (=RCCL) or gloo (rehearsal)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every learner on GPU 0 (use --dist-backend gloo)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -57,6 +57,7 @@ class AlgorithmConfig:
         self.num_learner_workers = 0
         self.num_gpus_per_learner_worker = 1
         self.num_cpus_per_learner_worker = 1
+        self.learner_collective_backend = "auto"  # nccl (=RCCL) for GPU learners, gloo on CPU
         # rollout workers ship raw fragments; GAE + advantage standardisation run on the learner GPU
         self.postprocess_on_learner = False
 
@@ -115,7 +116,9 @@ class AlgorithmConfig:
 
     def resources(self, *, num_gpus=None, num_cpus_per_worker=None, num_gpus_per_worker=None,
                   num_cpus_for_local_worker=None, num_learner_workers=None, num_gpus_per_learner_worker=None,
-                  num_cpus_per_learner_worker=None, **kw) -> "AlgorithmConfig":
+                  num_cpus_per_learner_worker=None, learner_collective_backend=None, **kw) -> "AlgorithmConfig":
+        if learner_collective_backend is not None:
+            self.learner_collective_backend = learner_collective_backend
         if num_learner_workers is not None:
             self.num_learner_workers = int(num_learner_workers)
         if num_gpus_per_learner_worker is not None:

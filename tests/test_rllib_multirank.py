@@ -80,7 +80,7 @@ def test_bench_two_ranks_same_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--no-putget", "--dist-backend", "gloo", "--same-device",
-           "--num-envs", "8", "--fragment", "16", "--minibatch", "32", "--sgd-iters", "2"]
+           "--mode", "fused", "--fragment", "100", "--minibatch", "500", "--sgd-iters", "2"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     import json
@@ -89,3 +89,24 @@ def test_bench_two_ranks_same_gpu():
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0
     assert all(v == v for v in out["last_stats"].values() if isinstance(v, float))
+
+
+@pytest.mark.gpu
+def test_bench_runtime_two_learner_actors_same_gpu():
+    """bench.py's runtime mode under torchrun: rank 0 drives 2 learner ACTORS (rehearsal: both on
+    GPU 0 over gloo, the 8-GPU node uses RCCL), rank 1 only joins the timing barriers."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--no-putget", "--same-device", "--workers-per-learner", "2",
+           "--sgd-iters", "2", "--store-gb", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["mode"] == "runtime"
+    assert out["config"]["learner_actors"] == 2 and len(out["config"]["learners"]) == 2
