@@ -214,7 +214,7 @@ def main():
         import torch.distributed as dist
 
         if world > 1:
-            e = torch.tensor([elapsed], device=f"cuda:{local_rank}")
+            e = torch.tensor([elapsed], device=f"cuda:{0 if args.same_device else local_rank}")
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             elapsed = float(e.item())
         sps = TRAIN_BATCH * args.steps * world / elapsed
