@@ -213,6 +213,7 @@ PYBIND11_MODULE(_hip, m) {
     return h2d_from_segment(P<void>(dst), P<const void>(src), n, S(stream));
   });
   m.def("host_unregister_all", [] { host_unregister_all(); });
+  m.def("h2d_stats", [] { return h2d_stats(); });
   m.def("grad_clip_coef", [](uint64_t grad, bool grad_bf16, int64_t n, float grad_scale, float max_norm,
                              uint64_t ws, uint64_t out, uint64_t stream) {
     grad_clip_coef(P<const void>(grad), grad_bf16, n, grad_scale, max_norm, P<float>(ws), P<float>(out), S(stream));

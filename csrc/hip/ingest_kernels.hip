@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -169,10 +170,49 @@ void host_register_segment(uintptr_t base, uint64_t size) {
   Registry().segs[base] = {base, size};
 }
 
+namespace {
+struct H2DStats {
+  uint64_t direct = 0, staged = 0, chunks_ok = 0, chunks_failed = 0;
+} g_h2d;
+
+// Page-locked bounce buffers for ranges the registry could not pin (e.g. pages another process on
+// the same GPU already registered): host memcpy into buffer k while buffer k^1 is in flight.
+struct Staging {
+  void* buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  static constexpr uint64_t kBytes = 32ull << 20;
+};
+Staging& Stage() {
+  static Staging s;
+  if (!s.buf[0]) {
+    for (int k = 0; k < 2; k++) {
+      RMM_HIP_CHECK(hipHostMalloc(&s.buf[k], Staging::kBytes, hipHostMallocDefault));
+      RMM_HIP_CHECK(hipEventCreateWithFlags(&s.ev[k], hipEventDisableTiming));
+    }
+  }
+  return s;
+}
+
+void staged_copy(void* dst, const void* src, uint64_t n, hipStream_t stream) {
+  Staging& st = Stage();
+  const uint8_t* s8 = static_cast<const uint8_t*>(src);
+  uint8_t* d8 = static_cast<uint8_t*>(dst);
+  int k = 0;
+  for (uint64_t off = 0; off < n; off += Staging::kBytes, k ^= 1) {
+    const uint64_t len = std::min<uint64_t>(Staging::kBytes, n - off);
+    RMM_HIP_CHECK(hipEventSynchronize(st.ev[k]));  // the DMA that last read buffer k is done
+    memcpy(st.buf[k], s8 + off, len);
+    RMM_HIP_CHECK(hipMemcpyAsync(d8 + off, st.buf[k], len, hipMemcpyHostToDevice, stream));
+    RMM_HIP_CHECK(hipEventRecord(st.ev[k], stream));
+  }
+}
+}  // namespace
+
 uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream) {
   auto& R = Registry();
   const uintptr_t s = reinterpret_cast<uintptr_t>(src);
   uint64_t newly = 0;
+  bool all_ok = false;
   {
     std::lock_guard<std::mutex> g(R.mu);
     auto it = R.segs.upper_bound(s);
@@ -180,20 +220,39 @@ uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t st
       --it;
       const uintptr_t base = it->second.first, end = base + it->second.second;
       if (s >= base && s + n <= end) {
+        all_ok = true;
         for (uintptr_t c = base + ((s - base) / kRegChunk) * kRegChunk; c < s + n; c += kRegChunk) {
-          if (R.chunks.count(c)) continue;
-          const uint64_t len = std::min<uint64_t>(kRegChunk, end - c);
-          const bool ok = hipHostRegister(reinterpret_cast<void*>(c), len, hipHostRegisterDefault) == hipSuccess;
-          if (!ok) (void)hipGetLastError();  // unpinnable: the copy below stages through the runtime
-          R.chunks[c] = ok;
-          if (ok) newly += len;
+          auto ck = R.chunks.find(c);
+          if (ck == R.chunks.end()) {
+            const uint64_t len = std::min<uint64_t>(kRegChunk, end - c);
+            const bool ok = hipHostRegister(reinterpret_cast<void*>(c), len, hipHostRegisterDefault) == hipSuccess;
+            if (!ok) (void)hipGetLastError();
+            ck = R.chunks.emplace(c, ok).first;
+            if (ok) {
+              newly += len;
+              g_h2d.chunks_ok++;
+            } else {
+              g_h2d.chunks_failed++;
+            }
+          }
+          all_ok &= ck->second;
         }
       }
     }
   }
-  RMM_HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, stream));
+  if (all_ok) {
+    if (hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, stream) == hipSuccess) {
+      g_h2d.direct += n;
+      return newly;
+    }
+    (void)hipGetLastError();  // the runtime refused the range: take the staged path
+  }
+  staged_copy(dst, src, n, stream);
+  g_h2d.staged += n;
   return newly;
 }
+
+std::vector<uint64_t> h2d_stats() { return {g_h2d.direct, g_h2d.staged, g_h2d.chunks_ok, g_h2d.chunks_failed}; }
 
 void host_unregister_all() {
   auto& R = Registry();

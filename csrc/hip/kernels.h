@@ -168,6 +168,9 @@ void standardize_col(float* cols, int64_t N, int C, int col, const double* stats
 // are hipHostRegister'ed on first use. Returns the bytes newly registered by this call.
 void host_register_segment(uintptr_t base, uint64_t size);
 uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream);
+// {bytes DMA'd straight from registered chunks, bytes staged via bounce buffers, chunks pinned,
+//  chunks that could not be pinned}
+std::vector<uint64_t> h2d_stats();
 void host_unregister_all();
 
 }  // namespace hip

@@ -69,6 +69,12 @@ class LearnerActor:
         st["rank"] = self.rank
         if self.learner._ingest is not None:
             st["ingest_bytes"] = self.learner._ingest.bytes_ingested
+            if self.device != "cpu":
+                from ray_memory_management_amd._native import require_hip
+
+                d, sg, ok, bad = require_hip().h2d_stats()
+                st.update(ingest_direct_bytes=d, ingest_staged_bytes=sg, ingest_chunks_pinned=ok,
+                          ingest_chunks_unpinnable=bad)
         return st
 
     def update_batch(self, batch) -> Dict:
