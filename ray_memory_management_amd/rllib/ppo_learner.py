@@ -200,6 +200,7 @@ class PPOLearner:
     # ------------------------------------------------------------------ fast-path state
     def _init_fast(self, params):
         dev = self.device
+        params = self._bucket_order(params)
         n = sum(p.numel() for p in params)
         self.n_params = n
         # fp32 master + moments (flat), bf16 compute weights (flat; params become views into it)
@@ -245,6 +246,21 @@ class PPOLearner:
             self.clip_ws = torch.zeros(require_hip().grad_clip_workspace_floats(), dtype=torch.float32, device=dev)
             self.clip_out = torch.ones(2, dtype=torch.float32, device=dev)
         self._manual = self._manual_layout()
+
+    def _bucket_order(self, params):
+        """Flat-bucket order: for the Nature-CNN layout the trunk (conv) parameters first, then
+        dense + heads, so the gradient that K12 produces before the trunk backward is ONE contiguous
+        tail slice of the bucket (all-reduced while K10 backward runs)."""
+        from ray_memory_management_amd.rllib.models import VisionNetwork
+
+        m = self.model
+        if isinstance(m, VisionNetwork) and m.nature and m.dense_tail is not None:
+            c1, c2 = m.convs[0], m.convs[1]
+            order = [c1.weight, c1.bias, c2.weight, c2.bias, m.dense_tail.weight, m.dense_tail.bias,
+                     m.heads.weight, m.heads.bias]
+            if len(order) == len(params) and {id(p) for p in order} == {id(p) for p in params}:
+                return order
+        return list(params)
 
     def _manual_layout(self):
         """The flagship Nature-CNN model runs its SGD step as explicit kernel launches (no autograd):
