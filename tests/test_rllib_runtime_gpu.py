@@ -70,8 +70,9 @@ def test_manual_step_matches_autograd_step(cuda, graphs):
         st = L._update_tables(obs, cols, 4)
         outs.append((L.master.clone(), st))
     (m1, s1), (m2, s2) = outs
-    assert torch.equal(m1, m2)  # same kernels, same order: bit-identical
-    assert s1["total_loss"] == s2["total_loss"]
+    assert torch.equal(m1, m2)  # same kernels, same order: bit-identical weights
+    # loss statistics are accumulated with device atomics (order-dependent in the last ulp)
+    assert abs(s1["total_loss"] - s2["total_loss"]) < 1e-5 * max(1.0, abs(s1["total_loss"]))
 
 
 def test_grad_clip_coef_matches_torch(cuda):
