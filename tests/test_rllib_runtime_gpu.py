@@ -103,7 +103,8 @@ def test_fused_update_with_clip_matches_fp32_reference(cuda):
     obs, cols = _tables(cuda, N=200)
     torch.manual_seed(9)
     st = L._update_tables(obs, cols, 4)  # one minibatch holding all 200 rows (the mean is order-free)
-    g_fused = torch.cat([p._rmm_grad_out.float().reshape(-1) for p in L.params])
+    fused_by_name = {n: p._rmm_grad_out.float().reshape(-1) for n, p in L.model.named_parameters()}
+    g_fused = torch.cat([fused_by_name[n] for n, _ in ref.named_parameters()])
     logits, v = ref(obs)
     coef = torch.tensor([0.1, 10.0, 1.0, 0.01, 0.2])
     total, _ = ppo_categorical_loss_reference(logits, v, cols[:, :4], cols[:, 7].long(), cols[:, 4], cols[:, 5],
