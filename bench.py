@@ -168,7 +168,8 @@ def _runtime(args, n_gpus):
                .training(train_batch_size=TRAIN_BATCH * n_gpus, sgd_minibatch_size=args.minibatch * n_gpus,
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
                          vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99)
-               .resources(num_learner_workers=n_gpus, num_gpus_per_learner_worker=phys / n_gpus,
+               .resources(num_learner_workers=n_gpus,
+                          num_gpus_per_learner_worker=0.5 if args.rollout == "gpu" else phys / n_gpus,
                           num_gpus_per_worker=0.5 if args.rollout == "gpu" else 0,
                           learner_collective_backend="gloo" if args.same_device else args.dist_backend)
                .debugging(seed=0))

@@ -2,9 +2,11 @@
 #include "gpu_store.h"
 
 #include <stdlib.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 
@@ -18,6 +20,7 @@ namespace {
 constexpr uint64_t kAlignG = 256;
 constexpr uint64_t kSpillChunk = 64ull << 20;  // input bytes per compression chunk
 constexpr uint64_t kSpillMagic = 0x4c4c495053555047ull;  // "GPUSPILL"
+constexpr uint32_t kTagGpuSpill = 0x47505553u;           // "GPUS"
 inline uint64_t AlignG(uint64_t v) { return (v + kAlignG - 1) & ~(kAlignG - 1); }
 
 ObjectId ToOid(const std::string& s) {
@@ -27,23 +30,32 @@ ObjectId ToOid(const std::string& s) {
   return o;
 }
 
-// Page-aligned hipHostRegister of [p, p+n) so DMA goes straight to/from the shm segment.
-struct HostPin {
-  void* base = nullptr;
-  bool ok = false;
-  HostPin(void* p, uint64_t n, bool already) {
-    if (already) return;
-    long pg = sysconf(_SC_PAGESIZE);
-    uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(pg - 1);
-    uintptr_t e = (reinterpret_cast<uintptr_t>(p) + n + pg - 1) & ~uintptr_t(pg - 1);
-    base = reinterpret_cast<void*>(a);
-    ok = hipHostRegister(base, e - a, hipHostRegisterDefault) == hipSuccess;
-    if (!ok) (void)hipGetLastError();
-  }
-  ~HostPin() {
-    if (ok) (void)hipHostUnregister(base);
-  }
+int64_t NowNs() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return int64_t(ts.tv_sec) * 1000000000ll + ts.tv_nsec;
+}
+
+// Host callback of SealDescriptorAsync: runs on a HIP runtime thread once the put's copy is
+// done; touches only the shared-memory store (no HIP calls allowed here).
+struct SealCtx {
+  Store* host;
+  ObjectId id;
 };
+void SealCallback(void* p) {
+  SealCtx* c = static_cast<SealCtx*>(p);
+  try {
+    c->host->Seal(c->id);
+  } catch (...) {
+    // aborted meanwhile (creator died / deleted before sealing): nothing to publish
+  }
+  c->host->Release(c->id);
+  delete c;
+}
+
+// Host spill object layout: [magic][nbytes][elem_bits][nchunks][csize * nchunks] then chunks.
+// csize == 0 marks a raw (uncompressed) chunk of min(kSpillChunk, remaining) bytes.
+inline uint64_t SpillHdrBytes(uint64_t nchunks) { return ((4 + nchunks) * 8 + 63) & ~uint64_t(63); }
 }  // namespace
 
 std::string GpuStore::HostId(const std::string& id) {
@@ -55,25 +67,30 @@ std::string GpuStore::HostId(const std::string& id) {
 }
 
 GpuStore::GpuStore(int device, uint64_t capacity, uint64_t slab_bytes, const std::string& shm_name,
-                   bool compress_spill)
-    : device_(device), capacity_(capacity), slab_bytes_(AlignG(slab_bytes)), compress_(compress_spill) {
+                   bool compress_spill, double spill_threshold)
+    : device_(device), capacity_(capacity), slab_bytes_(AlignG(slab_bytes)), compress_(compress_spill),
+      spill_threshold_(spill_threshold) {
   RMM_HIP_CHECK(hipSetDevice(device_));
   RMM_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   RMM_HIP_CHECK(hipStreamCreateWithFlags(&side2_, hipStreamNonBlocking));
+  for (auto& e : ev_) RMM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (!shm_name.empty()) {
     host_.reset(Store::Attach(shm_name));
-    // Pin the whole host segment once so every spill/restore is a straight DMA (no per-spill
-    // page pinning). Falls back to per-object pinning if the segment cannot be registered.
-    if (getenv("RMM_GPU_NO_HOST_REGISTER") == nullptr &&
-        hipHostRegister(host_->Base(), host_->MappedSize(), hipHostRegisterDefault) == hipSuccess)
-      host_registered_ = true;
-    else
-      (void)hipGetLastError();
+    // spill / restore DMA pins 64 MB chunks of the host segment on first use (ingest_kernels.hip)
+    host_register_segment(reinterpret_cast<uintptr_t>(host_->Base()), host_->MappedSize());
   }
   st_.capacity = capacity_;
+  bg_ = std::thread([this] { BackgroundSpiller(); });
 }
 
 GpuStore::~GpuStore() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  bg_cv_.notify_all();
+  if (bg_.joinable()) bg_.join();
+  std::lock_guard<std::mutex> x(xfer_mu_);
   std::lock_guard<std::mutex> g(mu_);
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
@@ -84,7 +101,8 @@ GpuStore::~GpuStore() {
   for (auto p : scratch_)
     if (p) (void)hipFree(p);
   if (work_) (void)hipFree(work_);
-  if (host_registered_) (void)hipHostUnregister(host_->Base());
+  for (auto e : ev_)
+    if (e) (void)hipEventDestroy(e);
   if (side_) (void)hipStreamDestroy(side_);
   if (side2_) (void)hipStreamDestroy(side2_);
 }
@@ -114,7 +132,6 @@ bool GpuStore::NewSlabLocked(uint64_t min_bytes) {
   else (void)hipGetLastError();
   allocated_ += sz;
   st_.slab_bytes_allocated = allocated_;
-  // reuse an empty slot if any
   for (size_t i = 0; i < slabs_.size(); i++)
     if (!slabs_[i]) {
       slabs_[i] = std::move(s);
@@ -124,9 +141,9 @@ bool GpuStore::NewSlabLocked(uint64_t min_bytes) {
   return true;
 }
 
-uint64_t GpuStore::AllocLocked(uint64_t nbytes, int* slab_out) {
+uint64_t GpuStore::AllocLocked(Lock& lk, uint64_t nbytes, int* slab_out) {
   uint64_t need = AlignG(std::max<uint64_t>(nbytes, 1));
-  for (int attempt = 0; attempt < 3; attempt++) {
+  for (;;) {
     // best fit across slabs
     int best = -1;
     uint64_t best_size = UINT64_MAX, best_off = 0;
@@ -170,13 +187,13 @@ uint64_t GpuStore::AllocLocked(uint64_t nbytes, int* slab_out) {
       }
     st_.slab_bytes_allocated = allocated_;
     if (freed_slab) continue;
-    if (SpillLocked(need) == 0) break;
-    attempt = 0;  // progress was made; keep trying
-    if (lru_.empty() && !NewSlabLocked(need)) {
-      // nothing more to spill
+    if (SpillLocked(lk, need) > 0) continue;
+    if (spills_in_flight_ > 0) {  // another thread is freeing memory right now: wait for it
+      cv_.wait(lk);
+      continue;
     }
+    throw std::runtime_error("GPU object store full: cannot allocate " + std::to_string(nbytes) + " bytes");
   }
-  throw std::runtime_error("GPU object store full: cannot allocate " + std::to_string(nbytes) + " bytes");
 }
 
 void GpuStore::FreeLocked(int slab, uint64_t off, uint64_t nbytes) {
@@ -209,6 +226,7 @@ void GpuStore::FreeLocked(int slab, uint64_t off, uint64_t nbytes) {
   }
   s->free_by_off[off] = sz;
   s->free_by_size.insert({sz, off});
+  cv_.notify_all();
 }
 
 void GpuStore::LruTouch(const std::string& id, GpuObject& o) {
@@ -225,11 +243,15 @@ void GpuStore::LruDrop(GpuObject& o) {
 }
 
 uint64_t GpuStore::Create(const std::string& id, uint64_t nbytes, int elem_bits) {
-  std::lock_guard<std::mutex> g(mu_);
+  Lock lk(mu_);
   RMM_HIP_CHECK(hipSetDevice(device_));
   if (objs_.count(id)) throw std::runtime_error("GPU object already exists");
   int slab;
-  uint64_t off = AllocLocked(nbytes, &slab);
+  uint64_t off = AllocLocked(lk, nbytes, &slab);
+  if (objs_.count(id)) {  // the lock was released while spilling: re-check
+    FreeLocked(slab, off, nbytes);
+    throw std::runtime_error("GPU object already exists");
+  }
   GpuObject& o = objs_[id];
   o.slab = slab;
   o.offset = off;
@@ -238,7 +260,9 @@ uint64_t GpuStore::Create(const std::string& id, uint64_t nbytes, int elem_bits)
   o.pins = 1;
   st_.num_objects++;
   st_.puts++;
-  return reinterpret_cast<uint64_t>(slabs_[size_t(slab)]->base) + off;
+  uint64_t ptr = reinterpret_cast<uint64_t>(slabs_[size_t(slab)]->base) + off;
+  if (spill_threshold_ > 0 && double(st_.bytes_in_use) > spill_threshold_ * double(capacity_)) bg_cv_.notify_all();
+  return ptr;
 }
 
 void GpuStore::Seal(const std::string& id, hipStream_t stream) {
@@ -249,7 +273,10 @@ void GpuStore::Seal(const std::string& id, hipStream_t stream) {
   if (!o.ready) RMM_HIP_CHECK(hipEventCreateWithFlags(&o.ready, hipEventDisableTiming));
   RMM_HIP_CHECK(hipEventRecord(o.ready, stream));
   o.sealed = true;
-  if (--o.pins == 0) LruTouch(id, o);
+  if (--o.pins == 0) {
+    if (o.delete_pending) DeleteLocked(id);
+    else LruTouch(id, o);
+  }
 }
 
 uint64_t GpuStore::PutSegments(const std::string& id, const std::vector<std::pair<uint64_t, uint64_t>>& segs,
@@ -269,19 +296,42 @@ uint64_t GpuStore::PutSegments(const std::string& id, const std::vector<std::pai
   return dst;
 }
 
-uint64_t GpuStore::Get(const std::string& id, hipStream_t stream) {
-  std::lock_guard<std::mutex> g(mu_);
-  RMM_HIP_CHECK(hipSetDevice(device_));
-  auto it = objs_.find(id);
-  if (it == objs_.end()) return 0;
-  GpuObject& o = it->second;
-  if (o.spilled) {
-    if (!RestoreLocked(id, o, stream)) throw std::runtime_error("failed to restore spilled GPU object");
+void GpuStore::SealDescriptorAsync(const std::string& desc_id, hipStream_t stream) {
+  if (!host_) throw std::runtime_error("SealDescriptorAsync: no host store attached");
+  auto* c = new SealCtx{host_.get(), ToOid(desc_id)};
+  hipError_t e = hipLaunchHostFunc(stream, SealCallback, c);
+  if (e != hipSuccess) {  // fall back to a synchronous seal
+    (void)hipGetLastError();
+    RMM_HIP_CHECK(hipStreamSynchronize(stream));
+    SealCallback(c);
   }
-  if (o.ready) RMM_HIP_CHECK(hipStreamWaitEvent(stream, o.ready, 0));
-  if (o.pins++ == 0) LruDrop(o);
-  st_.gets++;
-  return reinterpret_cast<uint64_t>(slabs_[size_t(o.slab)]->base) + o.offset;
+}
+
+void GpuStore::WaitIdleLocked(Lock& lk, const std::string& id) {
+  for (;;) {
+    auto it = objs_.find(id);
+    if (it == objs_.end() || (!it->second.spilling && !it->second.restoring)) return;
+    cv_.wait(lk);
+  }
+}
+
+uint64_t GpuStore::Get(const std::string& id, hipStream_t stream) {
+  Lock lk(mu_);
+  RMM_HIP_CHECK(hipSetDevice(device_));
+  for (;;) {
+    WaitIdleLocked(lk, id);
+    auto it = objs_.find(id);
+    if (it == objs_.end() || it->second.delete_pending) return 0;
+    GpuObject& o = it->second;
+    if (o.spilled) {
+      if (!RestoreOne(lk, id, &o)) throw std::runtime_error("failed to restore spilled GPU object");
+      continue;  // re-validate after the lock was released
+    }
+    if (o.ready) RMM_HIP_CHECK(hipStreamWaitEvent(stream, o.ready, 0));
+    if (o.pins++ == 0) LruDrop(o);
+    st_.gets++;
+    return reinterpret_cast<uint64_t>(slabs_[size_t(o.slab)]->base) + o.offset;
+  }
 }
 
 void GpuStore::Release(const std::string& id) {
@@ -289,13 +339,15 @@ void GpuStore::Release(const std::string& id) {
   auto it = objs_.find(id);
   if (it == objs_.end()) return;
   GpuObject& o = it->second;
-  if (o.pins > 0 && --o.pins == 0 && o.sealed && !o.spilled) LruTouch(id, o);
+  if (o.pins > 0 && --o.pins == 0) {
+    if (o.delete_pending) DeleteLocked(id);
+    else if (o.sealed && !o.spilled) LruTouch(id, o);
+  }
 }
 
-bool GpuStore::Delete(const std::string& id) {
-  std::lock_guard<std::mutex> g(mu_);
+void GpuStore::DeleteLocked(const std::string& id) {
   auto it = objs_.find(id);
-  if (it == objs_.end()) return false;
+  if (it == objs_.end()) return;
   GpuObject& o = it->second;
   LruDrop(o);
   if (!o.spilled) {
@@ -308,12 +360,29 @@ bool GpuStore::Delete(const std::string& id) {
   if (o.ready) (void)hipEventDestroy(o.ready);
   objs_.erase(it);
   st_.num_objects--;
+}
+
+bool GpuStore::Delete(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = objs_.find(id);
+  if (it == objs_.end()) return false;
+  GpuObject& o = it->second;
+  if (o.pins > 0 || o.spilling || o.restoring) {
+    // a zero-copy view (or a transfer) still uses the memory: free on the last Release /
+    // when the transfer finishes
+    if (!o.delete_pending) st_.deferred_deletes++;
+    o.delete_pending = true;
+    LruDrop(o);
+    return true;
+  }
+  DeleteLocked(id);
   return true;
 }
 
 bool GpuStore::Contains(const std::string& id) {
   std::lock_guard<std::mutex> g(mu_);
-  return objs_.count(id) > 0;
+  auto it = objs_.find(id);
+  return it != objs_.end() && !it->second.delete_pending;
 }
 
 bool GpuStore::IsSpilled(const std::string& id) {
@@ -326,8 +395,7 @@ void GpuStore::Locate(const std::string& id, int* slab, uint64_t* offset, uint64
   std::lock_guard<std::mutex> g(mu_);
   auto it = objs_.find(id);
   *slab = -1;
-  if (it == objs_.end() || it->second.spilled) return;
-  if (it->second.ready) (void)hipEventSynchronize(it->second.ready);
+  if (it == objs_.end() || it->second.spilled || it->second.spilling) return;
   *slab = it->second.slab;
   *offset = it->second.offset;
   *nbytes = it->second.nbytes;
@@ -355,46 +423,19 @@ void GpuStore::EnsureScratch() {
   RMM_HIP_CHECK(hipMalloc(&work_, 2 * work_bytes_));
 }
 
-// Host spill object layout: [magic][nbytes][elem_bits][nchunks][csize * nchunks] then chunks.
-// csize == 0 marks a raw (uncompressed) chunk of min(kSpillChunk, remaining) bytes.
-bool GpuStore::SpillOneLocked(const std::string& id, GpuObject& o) {
-  if (!host_) return false;
-  // A reader in another process may hold a zero-copy view through the descriptor: the flag can
-  // only be set while nobody pins the descriptor, and readers that see it take the host path.
-  if (!host_->TrySetFlag(ToOid(id), kFlagGpuSpilled)) return false;
-  bool done = false;
-  struct ClearOnFail {
-    Store* s; ObjectId oid; bool* done;
-    ~ClearOnFail() { if (!*done) s->ClearFlag(oid, kFlagGpuSpilled); }
-  } guard{host_.get(), ToOid(id), &done};
-  uint8_t* src = static_cast<uint8_t*>(slabs_[size_t(o.slab)]->base) + o.offset;
-  if (o.ready) RMM_HIP_CHECK(hipStreamWaitEvent(side_, o.ready, 0));
-  uint64_t nchunks = (o.nbytes + kSpillChunk - 1) / kSpillChunk;
-  if (nchunks == 0) nchunks = 1;
-  std::vector<uint64_t> csize(nchunks, 0);
-  bool use_c = compress_ && (o.elem_bits == 16 || o.elem_bits == 32) && o.nbytes >= (1u << 20);
-  uint64_t payload = 0;
-  if (use_c) {
-    EnsureScratch();
-    uint64_t eb = uint64_t(o.elem_bits / 8);
-    for (uint64_t c = 0; c < nchunks; c++) {
-      uint64_t len = std::min(kSpillChunk, o.nbytes - c * kSpillChunk);
-      uint64_t n = len / eb;
-      uint64_t cs = (len % eb == 0) ? compress(src + c * kSpillChunk, n, o.elem_bits, scratch_[0], work_, side_) : 0;
-      // keep the chunk compressed only if it saves >= 6 %
-      csize[c] = (cs && cs < len - len / 16) ? cs : 0;
-      payload += csize[c] ? csize[c] : len;
-    }
-  } else {
-    payload = o.nbytes;
-  }
-  uint64_t hdr = (4 + nchunks) * 8;
-  hdr = (hdr + 63) & ~uint64_t(63);
-  ObjectId hid = ToOid(HostId(id));
+// ---------------------------------------------------------------- spill
+
+bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t nbytes, int elem_bits,
+                             hipEvent_t ready, uint64_t* host_bytes, bool* compressed) {
+  RMM_HIP_CHECK(hipSetDevice(device_));
+  uint64_t nchunks = std::max<uint64_t>(1, (nbytes + kSpillChunk - 1) / kSpillChunk);
+  const bool use_c = compress_ && (elem_bits == 16 || elem_bits == 32) && nbytes >= (1u << 20);
+  const uint64_t hdr = SpillHdrBytes(nchunks);
+  const ObjectId hid = ToOid(HostId(id));
   bool exists = false;
   uint8_t* dst = nullptr;
   try {
-    dst = host_->CreateObject(hid, hdr + payload, 0, 0x47505553u /*GPUS*/, 0, &exists);
+    dst = host_->CreateObject(hid, hdr + nbytes, 0, kTagGpuSpill, 0, &exists);  // worst case: all raw
   } catch (const std::exception&) {
     return false;
   }
@@ -402,62 +443,115 @@ bool GpuStore::SpillOneLocked(const std::string& id, GpuObject& o) {
     host_->Delete(hid);
     return false;
   }
-  uint64_t* h = reinterpret_cast<uint64_t*>(dst);
-  h[0] = kSpillMagic;
-  h[1] = o.nbytes;
-  h[2] = uint64_t(o.elem_bits);
-  h[3] = nchunks;
-  for (uint64_t c = 0; c < nchunks; c++) h[4 + c] = csize[c];
-  {
-    HostPin pin(dst + hdr, payload, host_registered_);
-    uint64_t doff = hdr;
-    hipEvent_t done[2] = {nullptr, nullptr};
-    RMM_HIP_CHECK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
-    RMM_HIP_CHECK(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
-    for (uint64_t c = 0; c < nchunks; c++) {
-      uint64_t len = std::min(kSpillChunk, o.nbytes - c * kSpillChunk);
-      if (csize[c]) {
-        int b = int(c & 1);
-        // scratch[b] may still be read by the D2H of chunk c-2
-        if (c >= 2) RMM_HIP_CHECK(hipStreamWaitEvent(side_, done[b], 0));
-        uint64_t eb = uint64_t(o.elem_bits / 8);
-        uint64_t cs = compress(src + c * kSpillChunk, len / eb, o.elem_bits, scratch_[b],
-                               static_cast<uint8_t*>(work_) + uint64_t(b) * work_bytes_, side_);
-        if (cs != csize[c]) throw std::runtime_error("spill compression is not deterministic");
-        RMM_HIP_CHECK(hipMemcpyAsync(dst + doff, scratch_[b], cs, hipMemcpyDeviceToHost, side2_));
-        RMM_HIP_CHECK(hipEventRecord(done[b], side2_));
-        doff += cs;
-      } else {
-        hipEvent_t prod;
-        RMM_HIP_CHECK(hipEventCreateWithFlags(&prod, hipEventDisableTiming));
-        RMM_HIP_CHECK(hipEventRecord(prod, side_));
-        RMM_HIP_CHECK(hipStreamWaitEvent(side2_, prod, 0));
-        RMM_HIP_CHECK(hipMemcpyAsync(dst + doff, src + c * kSpillChunk, len, hipMemcpyDeviceToHost, side2_));
-        RMM_HIP_CHECK(hipEventDestroy(prod));
-        doff += len;
-      }
+  const bool pinned = host_pin_range(dst, hdr + nbytes);
+  if (use_c) EnsureScratch();
+  if (ready) RMM_HIP_CHECK(hipStreamWaitEvent(side_, ready, 0));
+  std::vector<uint64_t> csize(nchunks, 0);
+  uint64_t doff = hdr;
+  hipEvent_t* done = ev_;  // done[b]: the D2H that last read scratch[b]
+  const uint64_t eb = use_c ? uint64_t(elem_bits / 8) : 1;
+  for (uint64_t c = 0; c < nchunks; c++) {
+    const uint64_t len = std::min(kSpillChunk, nbytes - c * kSpillChunk);
+    const uint8_t* s = src + c * kSpillChunk;
+    uint64_t cs = 0;
+    const int b = int(c & 1);
+    if (use_c && len % eb == 0) {
+      if (c >= 2) RMM_HIP_CHECK(hipStreamWaitEvent(side_, done[b], 0));
+      // ONE compression pass; compress() reads the total back (stream sync on side_)
+      cs = compress(s, len / eb, elem_bits, scratch_[b], static_cast<uint8_t*>(work_) + uint64_t(b) * work_bytes_,
+                    side_);
+      if (cs >= len - len / 16) cs = 0;  // keep compressed only if it saves >= 6 %
     }
-    RMM_HIP_CHECK(hipStreamSynchronize(side2_));
-    RMM_HIP_CHECK(hipStreamSynchronize(side_));
-    (void)hipEventDestroy(done[0]);
-    (void)hipEventDestroy(done[1]);
+    if (cs) {
+      RMM_HIP_CHECK(hipEventRecord(ev_[2], side_));
+      RMM_HIP_CHECK(hipStreamWaitEvent(side2_, ev_[2], 0));
+      RMM_HIP_CHECK(hipMemcpyAsync(dst + doff, scratch_[b], cs, hipMemcpyDeviceToHost, side2_));
+      RMM_HIP_CHECK(hipEventRecord(done[b], side2_));
+      doff += cs;
+    } else {
+      RMM_HIP_CHECK(hipEventRecord(ev_[2], side_));  // orders after `ready`
+      RMM_HIP_CHECK(hipStreamWaitEvent(side2_, ev_[2], 0));
+      RMM_HIP_CHECK(hipMemcpyAsync(dst + doff, s, len, hipMemcpyDeviceToHost, side2_));
+      doff += len;
+    }
+    csize[c] = cs;
+    if (!pinned) RMM_HIP_CHECK(hipStreamSynchronize(side2_));
   }
+  RMM_HIP_CHECK(hipStreamSynchronize(side2_));
+  RMM_HIP_CHECK(hipStreamSynchronize(side_));
+  // header last: a reader never sees a complete header over incomplete chunks
+  uint64_t* h = reinterpret_cast<uint64_t*>(dst);
+  for (uint64_t c = 0; c < nchunks; c++) h[4 + c] = csize[c];
+  h[1] = nbytes;
+  h[2] = uint64_t(elem_bits);
+  h[3] = nchunks;
+  h[0] = kSpillMagic;
+  host_->ShrinkCreating(hid, doff);
   host_->Seal(hid);
   host_->Release(hid);
-  FreeLocked(o.slab, o.offset, o.nbytes);
-  LruDrop(o);
-  o.spilled = true;
-  o.spill_bytes = hdr + payload;
-  o.spill_compressed = use_c;
-  o.slab = -1;
-  st_.spilled_objects++;
-  st_.spilled_bytes_total += o.nbytes;
-  st_.spilled_host_bytes_total += payload;
-  done = true;
+  *host_bytes = doff;
+  *compressed = use_c;
   return true;
 }
 
-uint64_t GpuStore::SpillLocked(uint64_t bytes) {
+bool GpuStore::SpillOne(Lock& lk, const std::string& id) {
+  if (!host_) return false;
+  auto it = objs_.find(id);
+  if (it == objs_.end()) return false;
+  GpuObject& o = it->second;
+  if (o.pins > 0 || o.spilled || o.spilling || o.restoring || !o.sealed || o.delete_pending) return false;
+  // A reader in another process may hold a zero-copy view through the descriptor: the flag can
+  // only be set while nobody pins the descriptor, and readers that see it take the host path.
+  if (!host_->TrySetFlag(ToOid(id), kFlagGpuSpilled)) return false;
+  o.spilling = true;
+  LruDrop(o);
+  spills_in_flight_++;
+  const uint8_t* src = static_cast<uint8_t*>(slabs_[size_t(o.slab)]->base) + o.offset;
+  const uint64_t nbytes = o.nbytes;
+  const int bits = o.elem_bits;
+  hipEvent_t ready = o.ready;
+  lk.unlock();
+  uint64_t host_bytes = 0;
+  bool compressed = false, ok = false;
+  const int64_t t0 = NowNs();
+  try {
+    std::lock_guard<std::mutex> x(xfer_mu_);
+    ok = SpillTransfer(id, src, nbytes, bits, ready, &host_bytes, &compressed);
+  } catch (...) {
+    ok = false;
+  }
+  const int64_t t1 = NowNs();
+  lk.lock();
+  spills_in_flight_--;
+  auto jt = objs_.find(id);
+  if (jt == objs_.end()) {  // cannot happen (Delete defers while spilling); be safe
+    cv_.notify_all();
+    return ok;
+  }
+  GpuObject& p = jt->second;
+  p.spilling = false;
+  if (!ok) {
+    host_->ClearFlag(ToOid(id), kFlagGpuSpilled);
+    if (p.delete_pending && p.pins == 0) DeleteLocked(id);
+    else if (p.pins == 0) LruTouch(id, p);
+    cv_.notify_all();
+    return false;
+  }
+  FreeLocked(p.slab, p.offset, p.nbytes);
+  p.spilled = true;
+  p.spill_bytes = host_bytes;
+  p.spill_compressed = compressed;
+  p.slab = -1;
+  st_.spilled_objects++;
+  st_.spilled_bytes_total += nbytes;
+  st_.spilled_host_bytes_total += host_bytes;
+  st_.spill_ns_total += uint64_t(t1 - t0);
+  if (p.delete_pending && p.pins == 0) DeleteLocked(id);
+  cv_.notify_all();
+  return true;
+}
+
+uint64_t GpuStore::SpillLocked(Lock& lk, uint64_t bytes) {
   uint64_t freed = 0;
   std::vector<std::string> order(lru_.begin(), lru_.end());
   for (auto& victim : order) {
@@ -470,88 +564,136 @@ uint64_t GpuStore::SpillLocked(uint64_t bytes) {
       continue;
     }
     uint64_t n = AlignG(o.nbytes);
-    if (SpillOneLocked(victim, o)) freed += n;
+    if (SpillOne(lk, victim)) freed += n;
   }
   return freed;
 }
 
 uint64_t GpuStore::Spill(uint64_t bytes) {
-  std::lock_guard<std::mutex> g(mu_);
+  Lock lk(mu_);
   RMM_HIP_CHECK(hipSetDevice(device_));
-  return SpillLocked(bytes);
+  return SpillLocked(lk, bytes);
 }
 
 uint64_t GpuStore::SpillObject(const std::string& id) {
-  std::lock_guard<std::mutex> g(mu_);
+  Lock lk(mu_);
   RMM_HIP_CHECK(hipSetDevice(device_));
   auto it = objs_.find(id);
   if (it == objs_.end() || it->second.spilled || it->second.pins > 0) return 0;
   uint64_t n = it->second.nbytes;
-  return SpillOneLocked(id, it->second) ? n : 0;
+  return SpillOne(lk, id) ? n : 0;
 }
 
-bool GpuStore::RestoreLocked(const std::string& id, GpuObject& o, hipStream_t stream) {
-  if (!host_) return false;
-  ObjectId hid = ToOid(HostId(id));
+void GpuStore::SetSpillThreshold(double t) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    spill_threshold_ = t;
+  }
+  bg_cv_.notify_all();
+}
+
+void GpuStore::BackgroundSpiller() {
+  (void)hipSetDevice(device_);
+  Lock lk(mu_);
+  while (!stop_) {
+    bg_cv_.wait_for(lk, std::chrono::milliseconds(50));
+    if (stop_) break;
+    if (spill_threshold_ <= 0 || !host_) continue;
+    const double hi = spill_threshold_ * double(capacity_);
+    if (double(st_.bytes_in_use) <= hi) continue;
+    // spill down to a low watermark 5 % of the capacity below the threshold
+    const double lo = std::max(0.0, spill_threshold_ - 0.05) * double(capacity_);
+    const uint64_t excess = uint64_t(double(st_.bytes_in_use) - lo);
+    const uint64_t before = st_.spilled_objects;
+    SpillLocked(lk, excess);
+    st_.proactive_spills += st_.spilled_objects - before;
+  }
+}
+
+// ---------------------------------------------------------------- restore
+
+uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uint64_t nbytes, bool delete_host) {
+  RMM_HIP_CHECK(hipSetDevice(device_));
+  const ObjectId hid = ToOid(host_id);
   Store::View v;
-  if (!host_->Get(hid, 0, &v)) return false;
+  if (!host_->Get(hid, 0, &v)) return 0;
   const uint64_t* h = reinterpret_cast<const uint64_t*>(v.data);
-  if (h[0] != kSpillMagic || h[1] != o.nbytes) {
+  if (h[0] != kSpillMagic || h[1] != nbytes) {
     host_->Release(hid);
+    return 0;
+  }
+  const int bits = int(h[2]);
+  const uint64_t nchunks = h[3];
+  const uint64_t hdr = SpillHdrBytes(nchunks);
+  const bool pinned = host_pin_range(v.data, v.data_size);
+  bool any_c = false;
+  for (uint64_t c = 0; c < nchunks; c++) any_c |= h[4 + c] != 0;
+  if (any_c) EnsureScratch();
+  uint64_t soff = hdr;
+  hipEvent_t* done = ev_;  // done[b]: the decompression that last read scratch[b]
+  for (uint64_t c = 0; c < nchunks; c++) {
+    const uint64_t len = std::min(kSpillChunk, nbytes - c * kSpillChunk);
+    const uint64_t cs = h[4 + c];
+    if (cs) {
+      const int b = int(c & 1);
+      if (c >= 2) RMM_HIP_CHECK(hipStreamWaitEvent(side2_, done[b], 0));
+      RMM_HIP_CHECK(hipMemcpyAsync(scratch_[b], v.data + soff, cs, hipMemcpyHostToDevice, side2_));
+      RMM_HIP_CHECK(hipEventRecord(ev_[2 + b], side2_));
+      RMM_HIP_CHECK(hipStreamWaitEvent(side_, ev_[2 + b], 0));
+      const uint64_t eb = uint64_t(bits / 8);
+      decompress(scratch_[b], dst + c * kSpillChunk, len / eb, bits,
+                 static_cast<uint8_t*>(work_) + uint64_t(b) * work_bytes_, side_);
+      RMM_HIP_CHECK(hipEventRecord(done[b], side_));
+      soff += cs;
+    } else {
+      RMM_HIP_CHECK(hipMemcpyAsync(dst + c * kSpillChunk, v.data + soff, len, hipMemcpyHostToDevice, side2_));
+      soff += len;
+    }
+    if (!pinned) RMM_HIP_CHECK(hipStreamSynchronize(side2_));
+  }
+  RMM_HIP_CHECK(hipStreamSynchronize(side2_));
+  RMM_HIP_CHECK(hipStreamSynchronize(side_));
+  host_->Release(hid);
+  if (delete_host) host_->Delete(hid);
+  return nbytes;
+}
+
+bool GpuStore::RestoreOne(Lock& lk, const std::string& id, GpuObject* o) {
+  if (!host_) return false;
+  int slab;
+  const uint64_t want = o->nbytes;  // `o` may dangle once the lock is released below
+  const uint64_t off = AllocLocked(lk, want, &slab);  // may spill others (lock released)
+  auto it = objs_.find(id);
+  if (it == objs_.end() || !it->second.spilled || it->second.restoring) {  // raced: give the memory back
+    FreeLocked(slab, off, want);
+    return true;
+  }
+  GpuObject& p = it->second;
+  p.restoring = true;
+  const uint64_t nbytes = p.nbytes;
+  uint8_t* dst = static_cast<uint8_t*>(slabs_[size_t(slab)]->base) + off;
+  lk.unlock();
+  uint64_t got = 0;
+  const int64_t t0 = NowNs();
+  try {
+    std::lock_guard<std::mutex> x(xfer_mu_);
+    got = RestoreTransfer(HostId(id), dst, nbytes, true);
+  } catch (...) {
+    got = 0;
+  }
+  const int64_t t1 = NowNs();
+  lk.lock();
+  auto jt = objs_.find(id);
+  GpuObject& q = jt->second;
+  q.restoring = false;
+  if (got != nbytes) {
+    FreeLocked(slab, off, nbytes);
+    cv_.notify_all();
     return false;
   }
-  uint64_t nchunks = h[3];
-  uint64_t hdr = ((4 + nchunks) * 8 + 63) & ~uint64_t(63);
-  int slab;
-  uint64_t off;
-  try {
-    off = AllocLocked(o.nbytes, &slab);
-  } catch (...) {
-    host_->Release(hid);
-    throw;
-  }
-  uint8_t* dst = static_cast<uint8_t*>(slabs_[size_t(slab)]->base) + off;
-  {
-    HostPin pin(v.data + hdr, v.data_size - hdr, host_registered_);
-    uint64_t soff = hdr;
-    bool any_c = false;
-    for (uint64_t c = 0; c < nchunks; c++) any_c |= h[4 + c] != 0;
-    if (any_c) EnsureScratch();
-    hipEvent_t done[2] = {nullptr, nullptr};
-    RMM_HIP_CHECK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
-    RMM_HIP_CHECK(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
-    for (uint64_t c = 0; c < nchunks; c++) {
-      uint64_t len = std::min(kSpillChunk, o.nbytes - c * kSpillChunk);
-      uint64_t cs = h[4 + c];
-      if (cs) {
-        int b = int(c & 1);
-        if (c >= 2) RMM_HIP_CHECK(hipStreamWaitEvent(side2_, done[b], 0));
-        RMM_HIP_CHECK(hipMemcpyAsync(scratch_[b], v.data + soff, cs, hipMemcpyHostToDevice, side2_));
-        hipEvent_t copied;
-        RMM_HIP_CHECK(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
-        RMM_HIP_CHECK(hipEventRecord(copied, side2_));
-        RMM_HIP_CHECK(hipStreamWaitEvent(side_, copied, 0));
-        uint64_t eb = uint64_t(o.elem_bits / 8);
-        decompress(scratch_[b], dst + c * kSpillChunk, len / eb, o.elem_bits,
-                   static_cast<uint8_t*>(work_) + uint64_t(b) * work_bytes_, side_);
-        RMM_HIP_CHECK(hipEventRecord(done[b], side_));
-        RMM_HIP_CHECK(hipEventDestroy(copied));
-        soff += cs;
-      } else {
-        RMM_HIP_CHECK(hipMemcpyAsync(dst + c * kSpillChunk, v.data + soff, len, hipMemcpyHostToDevice, side2_));
-        soff += len;
-      }
-    }
-    RMM_HIP_CHECK(hipStreamSynchronize(side2_));
-    RMM_HIP_CHECK(hipStreamSynchronize(side_));
-    (void)hipEventDestroy(done[0]);
-    (void)hipEventDestroy(done[1]);
-  }
-  host_->Release(hid);
-  host_->Delete(hid);
-  o.slab = slab;
-  o.offset = off;
-  o.spilled = false;
+  q.slab = slab;
+  q.offset = off;
+  q.spilled = false;  // the data is in place: the transfer synchronised its streams
   // publish the new location to cross-process readers, then clear the spilled flag
   {
     Slab* sl = slabs_[size_t(slab)].get();
@@ -566,9 +708,23 @@ bool GpuStore::RestoreLocked(const std::string& id, GpuObject& o, hipStream_t st
     });
     host_->ClearFlag(did, kFlagGpuSpilled);
   }
-  st_.restored_bytes_total += o.nbytes;
-  (void)stream;
+  st_.restored_bytes_total += nbytes;
+  st_.restore_ns_total += uint64_t(t1 - t0);
+  if (q.delete_pending && q.pins == 0) DeleteLocked(id);
+  else if (q.pins == 0) LruTouch(id, q);
+  cv_.notify_all();
   return true;
+}
+
+uint64_t GpuStore::RestoreForeign(const std::string& host_id, uint64_t dst, uint64_t nbytes) {
+  if (!host_) throw std::runtime_error("RestoreForeign: no host store attached");
+  std::lock_guard<std::mutex> x(xfer_mu_);
+  const int64_t t0 = NowNs();
+  uint64_t n = RestoreTransfer(host_id, reinterpret_cast<uint8_t*>(dst), nbytes, false);
+  std::lock_guard<std::mutex> g(mu_);
+  st_.restored_bytes_total += n;
+  st_.restore_ns_total += uint64_t(NowNs() - t0);
+  return n;
 }
 
 GpuStats GpuStore::Stats() {

@@ -339,6 +339,23 @@ PYBIND11_MODULE(_hip, m) {
     return reinterpret_cast<uint64_t>(p);
   });
   m.def("ipc_close", [](uint64_t p) { RMM_HIP_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void*>(p))); });
+  // Canonical PCI address "dddd:bb:dd.f" of a visible device: identifies a physical GPU across
+  // processes whose HIP_VISIBLE_DEVICES differ (a local device index does not).
+  m.def("pci_bus_id", [](int device) {
+    char buf[64] = {0};
+    RMM_HIP_CHECK(hipDeviceGetPCIBusId(buf, int(sizeof(buf)), device));
+    std::string s(buf);
+    for (auto& ch : s) ch = char(tolower(ch));
+    return s;
+  });
+  m.def("can_access_peer", [](int dev, int peer) {
+    int ok = 0;
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return ok != 0;
+  });
   m.def("memcpy_async", [](uint64_t dst, uint64_t src, uint64_t n, uint64_t stream) {
     RMM_HIP_CHECK(hipMemcpyAsync(P<void>(dst), P<const void>(src), n, hipMemcpyDefault, S(stream)));
   });
@@ -355,9 +372,18 @@ PYBIND11_MODULE(_hip, m) {
 
   // ---------------------------------------------------------------- GPU object store
   py::class_<GpuStore, std::shared_ptr<GpuStore>>(m, "GpuStore")
-      .def(py::init<int, uint64_t, uint64_t, const std::string&, bool>(), py::arg("device"),
+      .def(py::init<int, uint64_t, uint64_t, const std::string&, bool, double>(), py::arg("device"),
            py::arg("capacity"), py::arg("slab_bytes") = 8ull << 30, py::arg("shm_name") = "",
-           py::arg("compress_spill") = true)
+           py::arg("compress_spill") = true, py::arg("spill_threshold") = 0.0)
+      .def("seal_descriptor_async", [](GpuStore& s, py::bytes desc_id, uint64_t stream) {
+        s.SealDescriptorAsync(std::string(desc_id), S(stream));
+      })
+      .def("restore_foreign", [](GpuStore& s, py::bytes host_id, uint64_t dst, uint64_t nbytes) {
+        std::string hid = host_id;
+        py::gil_scoped_release nogil;
+        return s.RestoreForeign(hid, dst, nbytes);
+      })
+      .def("set_spill_threshold", &GpuStore::SetSpillThreshold)
       .def("create", [](GpuStore& s, py::bytes id, uint64_t n, int bits) {
         return s.Create(std::string(id), n, bits);
       })
@@ -414,6 +440,10 @@ PYBIND11_MODULE(_hip, m) {
         d["restored_bytes_total"] = st.restored_bytes_total;
         d["puts"] = st.puts;
         d["gets"] = st.gets;
+        d["spill_s_total"] = double(st.spill_ns_total) * 1e-9;
+        d["restore_s_total"] = double(st.restore_ns_total) * 1e-9;
+        d["proactive_spills"] = st.proactive_spills;
+        d["deferred_deletes"] = st.deferred_deletes;
         return d;
       });
 

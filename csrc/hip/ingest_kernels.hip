@@ -208,7 +208,7 @@ void staged_copy(void* dst, const void* src, uint64_t n, hipStream_t stream) {
 }
 }  // namespace
 
-uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream) {
+bool host_pin_range(const void* src, uint64_t n, uint64_t* newly_out) {
   auto& R = Registry();
   const uintptr_t s = reinterpret_cast<uintptr_t>(src);
   uint64_t newly = 0;
@@ -240,7 +240,13 @@ uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t st
       }
     }
   }
-  if (all_ok) {
+  if (newly_out) *newly_out += newly;
+  return all_ok;
+}
+
+uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream) {
+  uint64_t newly = 0;
+  if (host_pin_range(src, n, &newly)) {
     if (hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, stream) == hipSuccess) {
       g_h2d.direct += n;
       return newly;

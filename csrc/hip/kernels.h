@@ -167,6 +167,9 @@ void standardize_col(float* cols, int64_t N, int C, int col, const double* stats
 // Page-locked DMA out of a shared-memory object-store segment: chunks of the registered segment
 // are hipHostRegister'ed on first use. Returns the bytes newly registered by this call.
 void host_register_segment(uintptr_t base, uint64_t size);
+// Page-lock the registered-segment chunks covering [p, p+n); true if all of them are pinned
+// (then DMA straight from/to the range is safe). newly (optional) accumulates bytes pinned now.
+bool host_pin_range(const void* p, uint64_t n, uint64_t* newly = nullptr);
 uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream);
 // {bytes DMA'd straight from registered chunks, bytes staged via bounce buffers, chunks pinned,
 //  chunks that could not be pinned}

@@ -316,6 +316,44 @@ void Store::HeapFree(uint64_t payload_off) {
   TlsfInsert(blk);
 }
 
+void Store::HeapShrink(uint64_t payload_off, uint64_t n) {
+  uint64_t blk = payload_off - kBlockHdr;
+  Blk* b = reinterpret_cast<Blk*>(base_ + blk);
+  uint64_t bsize = b->size & kSizeMask;
+  uint64_t need = AlignUp(n, kAlign) + kBlockHdr;
+  if (need < kMinBlock) need = kMinBlock;
+  if (bsize < need || bsize - need < kMinBlock) return;
+  uint64_t rem = bsize - need;
+  uint64_t nb = blk + need;
+  Blk* tail = reinterpret_cast<Blk*>(base_ + nb);
+  tail->prev_phys = blk;
+  // coalesce the freed tail with a free physical successor
+  uint64_t nxt = blk + bsize;
+  Blk* nx = reinterpret_cast<Blk*>(base_ + nxt);
+  if (nx->size & kFreeBit) {
+    TlsfRemove(nxt);
+    rem += nx->size & kSizeMask;
+  }
+  tail->size = rem | kFreeBit;
+  reinterpret_cast<Blk*>(base_ + nb + rem)->prev_phys = nb;
+  TlsfInsert(nb);
+  b->size = need;
+  hdr_->stats.bytes_in_use -= bsize - need;
+}
+
+bool Store::ShrinkCreating(const ObjectId& id, uint64_t data_size) {
+  Lock();
+  int64_t idx = Find(id);
+  bool ok = idx >= 0 && E(idx)->state == kCreating && !(E(idx)->flags & kFlagFallback) &&
+            E(idx)->meta_size == 0 && data_size <= E(idx)->data_size;
+  if (ok) {
+    HeapShrink(E(idx)->offset, data_size);
+    E(idx)->data_size = data_size;
+  }
+  Unlock();
+  return ok;
+}
+
 uint64_t Store::CheckHeap() {
   Lock();
   uint64_t off = hdr_->heap_off, end = hdr_->heap_off + hdr_->heap_size - kBlockHdr;

@@ -158,6 +158,10 @@ class Store {
                         uint32_t user_tag, uint32_t flags, bool* exists);
   void Seal(const ObjectId& id);
   void Abort(const ObjectId& id);
+  // Shrink an object still being created (no metadata) to `data_size` bytes, returning the tail
+  // of its heap block to the allocator. Used by writers that allocate a worst case first (the
+  // GPU spill path writes a compressed stream whose size is known only at the end).
+  bool ShrinkCreating(const ObjectId& id, uint64_t data_size);
   // Pins and returns pointer; waits up to timeout_ms (<0 = forever, 0 = no wait).
   // Returns nullptr on timeout.
   struct View {
@@ -218,6 +222,7 @@ class Store {
   Entry* E(int64_t idx) { return &table_[idx]; }
   uint64_t HeapAlloc(uint64_t n);
   void HeapFree(uint64_t payload_off);
+  void HeapShrink(uint64_t payload_off, uint64_t n);
   void LruPush(int64_t idx);
   void LruRemove(int64_t idx);
   void FreeEntryStorage(int64_t idx);

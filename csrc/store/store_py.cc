@@ -172,7 +172,10 @@ PYBIND11_MODULE(_store, m) {
           p.released = true;
           p.store->Release(p.id);
         }
-      });
+      })
+      // hand the pin over to native code that releases it later (e.g. a HIP host callback that
+      // seals a GPU-object descriptor once the device copy has completed)
+      .def("disown", [](Pinned& p) { p.released = true; });
 
   py::class_<PyStore>(m, "ObjectStore")
       .def_static(

@@ -103,7 +103,8 @@ class Executor:
             gos.put_tensor(self.w, oid, v)
             self.w.send((P.GPU_OBJECT, oid))
             return
-        data, bufs, contained = ser.serialize(v)
+        with self.w.gpu_sink():
+            data, bufs, contained = ser.serialize(v)
         if contained:
             contained_map[oid] = contained
             for c in contained:  # keep inner objects alive until TASK_DONE reached the head

@@ -44,7 +44,9 @@ class Algorithm(Trainable):
         self.validate_config(c)
         env_creator = c.env if callable(c.env) and not isinstance(c.env, str) else None
         cfg = c.to_dict()
-        self.workers = WorkerSet(env_creator, cfg, num_workers=c.num_workers)
+        self._placement_group = None
+        strategy = self._rollout_worker_strategy(c)
+        self.workers = WorkerSet(env_creator, cfg, num_workers=c.num_workers, worker_strategy=strategy)
         self._episode_history = collections.deque(maxlen=c.metrics_num_episodes_for_smoothing)
         self._episodes_total = 0
         self._timesteps_total = 0
@@ -52,6 +54,33 @@ class Algorithm(Trainable):
         self._env_creator = env_creator
         self.callbacks = c.callbacks_class() if c.callbacks_class else None
         self._setup_learner()
+
+    def _rollout_worker_strategy(self, c):
+        """GPU rollout workers next to GPU learner actors: one placement-group bundle per learner
+        GPU {GPU: 1}; learner k and its rollout workers share bundle k (fractional GPUs), so a
+        fragment never leaves the GPU that trains on it."""
+        if not (getattr(c, "gpu_rollouts", False) and getattr(c, "num_learner_workers", 0)):
+            return None
+        import ray_memory_management_amd as ray
+        from ray_memory_management_amd.util.placement_group import placement_group
+        from ray_memory_management_amd.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+        n = int(c.num_learner_workers)
+        per = max(1, c.num_workers // n)
+        cpus = c.num_cpus_per_learner_worker + per * c.num_cpus_per_worker
+        pg = placement_group([{"GPU": 1.0, "CPU": float(cpus)} for _ in range(n)], strategy="PACK")
+        ray.get(pg.ready())
+        self._placement_group = pg
+        # worker i feeds learner i % n (split_for_learners is round-robin): same bundle, same GPU
+        return lambda i: PlacementGroupSchedulingStrategy(pg, placement_group_bundle_index=i % n)
+
+    def learner_strategy(self):
+        if getattr(self, "_placement_group", None) is None:
+            return None
+        from ray_memory_management_amd.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+        pg = self._placement_group
+        return lambda r: PlacementGroupSchedulingStrategy(pg, placement_group_bundle_index=r)
 
     def validate_config(self, config: AlgorithmConfig):
         if config.env is None:
@@ -136,6 +165,14 @@ class Algorithm(Trainable):
 
     def cleanup(self):
         self.workers.stop()
+        if getattr(self, "_placement_group", None) is not None:
+            from ray_memory_management_amd.util.placement_group import remove_placement_group
+
+            try:
+                remove_placement_group(self._placement_group)
+            except Exception:
+                pass
+            self._placement_group = None
 
     @classmethod
     def default_resource_request(cls, config):

@@ -104,7 +104,7 @@ class PPO(Algorithm):
                 n, local.env.observation_space, local.env.action_space, c.model, self._learner_cfg(n),
                 num_gpus_per_learner=c.num_gpus_per_learner_worker,
                 num_cpus_per_learner=c.num_cpus_per_learner_worker, backend=c.learner_collective_backend,
-                seed=int(c.seed or 0))
+                seed=int(c.seed or 0), strategy=self.learner_strategy())
             self._device = "learner_actors"
             self._weights_ref = self.learner_group.weights_ref()
             local.set_weights(ray.get(self._weights_ref))

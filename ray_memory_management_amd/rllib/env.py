@@ -294,6 +294,9 @@ _REGISTRY = {
 
 _VECTOR_REGISTRY = {
     "SyntheticAtariVec-v0": CPUSyntheticAtariVectorEnv,
+    # GPU rollout workers step the device env (GPUSyntheticAtariVectorEnv, K9); a driver-side local
+    # worker of the same config gets the CPU twin (same spaces and statistics)
+    "GPUSyntheticAtari-v0": CPUSyntheticAtariVectorEnv,
 }
 
 

@@ -128,7 +128,8 @@ class LearnerGroup:
 
     def __init__(self, num_learners: int, obs_space, action_space, model_config: dict, learner_cfg: dict,
                  num_gpus_per_learner: float = 1.0, num_cpus_per_learner: float = 1.0, backend: str = "auto",
-                 seed: int = 0):
+                 seed: int = 0, strategy=None):
+        """`strategy(rank)` (optional): the learner's scheduling strategy (e.g. its GPU's bundle)."""
         self.n = int(num_learners)
         use_gpu = num_gpus_per_learner > 0
         if backend == "auto":
@@ -137,8 +138,9 @@ class LearnerGroup:
         self.group_name = f"learners-{uuid.uuid4().hex[:8]}" if self.n > 1 else None
         cls = ray.remote(LearnerActor).options(num_gpus=num_gpus_per_learner, num_cpus=num_cpus_per_learner)
         # all ranks must be alive together: their constructors rendezvous in the collective group
-        self.learners = [cls.remote(obs_space, action_space, model_config, learner_cfg, r, self.n, self.group_name,
-                                    backend, seed, use_gpu) for r in range(self.n)]
+        self.learners = [(cls.options(scheduling_strategy=strategy(r)) if strategy is not None else cls).remote(
+            obs_space, action_space, model_config, learner_cfg, r, self.n, self.group_name, backend, seed, use_gpu)
+            for r in range(self.n)]
         ray.get([l.__ray_ready__.remote() for l in self.learners])
 
     def update(self, shards: List[List]) -> List[Dict]:

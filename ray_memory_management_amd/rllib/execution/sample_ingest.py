@@ -57,6 +57,19 @@ def fragment_dims(b) -> Tuple[int, int, int]:
     return rows // n, n, int(b["_raw"].shape[1]) - RAW_EXTRA
 
 
+def pack_fragment_device(obs, logits, logp, vf, rew, done, actions, boot):
+    """GPU rollout worker side: time-major device buffers → a fragment of CUDA tensors (the raw
+    table is built on the GPU; returned as task output the tensors go to the HBM object store)."""
+    from ray_memory_management_amd.rllib.sample_batch import SampleBatch
+
+    T, n = rew.shape
+    A = logits.shape[-1]
+    raw = torch.cat([logits.reshape(T * n, A).float(), logp.reshape(-1, 1).float(), vf.reshape(-1, 1).float(),
+                     rew.reshape(-1, 1).float(), done.reshape(-1, 1).float(), actions.reshape(-1, 1).float()], 1)
+    return SampleBatch({"obs": obs.reshape((T * n,) + tuple(obs.shape[2:])), "_raw": raw.contiguous(),
+                        "_boot": boot.reshape(n).float().contiguous()})
+
+
 def fragments_to_batch_cpu(frags: Sequence, gamma: float, lam: float, standardize: bool = True):
     """Reference (fp32 torch) ingest: fragments → (obs, cols[N, A+4]) on the CPU. Used by the CPU
     learner path and as the numerics oracle of the GPU kernels."""
@@ -123,10 +136,11 @@ class SampleIngest:
         A = dims[0][2]
         if any(d[2] != A for d in dims):
             raise ValueError("ingest: fragments disagree on the action dimension")
-        obs0 = np.asarray(frags[0]["obs"])
+        on_dev = torch.is_tensor(frags[0]["obs"])
+        obs_shape = tuple(frags[0]["obs"].shape[1:])
         N = sum(T * n for T, n, _ in dims)
         nb = sum(n for _, n, _ in dims)
-        obs = self._buf("_obs", (N,) + obs0.shape[1:], torch.uint8)
+        obs = self._buf("_obs", (N,) + obs_shape, torch.uint8)
         raw = self._buf("_raw", (N, A + RAW_EXTRA), torch.float32)
         boot = self._buf("_boot", (nb,), torch.float32)
         cols = self._buf("_cols", (N, A + 4), torch.float32)
@@ -134,25 +148,40 @@ class SampleIngest:
         table = np.zeros((len(frags), 3), dtype=np.int64)  # IngestBlock: row0 | (T, n) | (boot0, pad)
         row = bo = 0
         orow = obs.stride(0)
+        segs = []
         for i, (b, (T, n, _)) in enumerate(zip(frags, dims)):
-            o = np.asarray(b["obs"])
-            r = np.asarray(b["_raw"])
-            bt = np.asarray(b["_boot"])
-            if o.dtype != np.uint8 or o.shape[1:] != obs0.shape[1:] or not o.flags.c_contiguous:
-                raise ValueError("ingest: fragments must carry contiguous uint8 frames of one shape")
-            if r.dtype != np.float32 or not r.flags.c_contiguous or bt.dtype != np.float32:
-                raise ValueError("ingest: _raw/_boot must be contiguous float32")
             rows = T * n
-            self.bytes_registered += h.h2d_from_segment(obs.data_ptr() + row * orow, o.ctypes.data, o.nbytes, stream)
-            self.bytes_registered += h.h2d_from_segment(raw.data_ptr() + row * raw.stride(0) * 4, r.ctypes.data,
-                                                        r.nbytes, stream)
-            h.memcpy_async(boot.data_ptr() + bo * 4, bt.ctypes.data, bt.nbytes, stream)
+            if on_dev:  # GPU rollout fragments: zero-copy IPC views of the producer's HBM objects
+                o, r, bt = b["obs"], b["_raw"], b["_boot"]
+                if o.dtype != torch.uint8 or tuple(o.shape[1:]) != obs_shape or not o.is_contiguous():
+                    raise ValueError("ingest: fragments must carry contiguous uint8 frames of one shape")
+                if r.dtype != torch.float32 or bt.dtype != torch.float32:
+                    raise ValueError("ingest: _raw/_boot must be float32")
+                segs += [(o.data_ptr(), obs.data_ptr() + row * orow, o.numel()),
+                         (r.contiguous().data_ptr(), raw.data_ptr() + row * raw.stride(0) * 4, r.numel() * 4),
+                         (bt.contiguous().data_ptr(), boot.data_ptr() + bo * 4, bt.numel() * 4)]
+                self.bytes_ingested += o.numel() + r.numel() * 4
+            else:
+                o = np.asarray(b["obs"])
+                r = np.asarray(b["_raw"])
+                bt = np.asarray(b["_boot"])
+                if o.dtype != np.uint8 or tuple(o.shape[1:]) != obs_shape or not o.flags.c_contiguous:
+                    raise ValueError("ingest: fragments must carry contiguous uint8 frames of one shape")
+                if r.dtype != np.float32 or not r.flags.c_contiguous or bt.dtype != np.float32:
+                    raise ValueError("ingest: _raw/_boot must be contiguous float32")
+                self.bytes_registered += h.h2d_from_segment(obs.data_ptr() + row * orow, o.ctypes.data, o.nbytes,
+                                                            stream)
+                self.bytes_registered += h.h2d_from_segment(raw.data_ptr() + row * raw.stride(0) * 4, r.ctypes.data,
+                                                            r.nbytes, stream)
+                h.memcpy_async(boot.data_ptr() + bo * 4, bt.ctypes.data, bt.nbytes, stream)
+                self.bytes_ingested += o.nbytes + r.nbytes
             table[i, 0] = row
             table[i, 1] = (T & 0xFFFFFFFF) | (n << 32)
             table[i, 2] = bo
-            self.bytes_ingested += o.nbytes + r.nbytes
             row += rows
             bo += n
+        if segs:  # K1: every device-side fragment column into the learner tables, one launch
+            h.multi_copy(segs, stream)
         blocks = torch.from_numpy(table.view(np.uint8).reshape(-1)).to(self.device, non_blocking=False)
         self._stats.zero_()
         h.ingest_gae(raw.data_ptr(), boot.data_ptr(), blocks.data_ptr(), len(frags), A, self.gamma, self.lam,

@@ -776,7 +776,8 @@ class GPURolloutSampler:
         self._graph = g
 
     @torch.no_grad()
-    def sample(self) -> SampleBatch:
+    def run_fragment(self):
+        """Step the env `fragment` times into the rollout buffers (one graph replay per step)."""
         if self.graphs and self._graph is None:
             try:
                 self._capture()
@@ -790,6 +791,10 @@ class GPURolloutSampler:
                 self._graph.replay()
             else:
                 self._step_body()
+
+    @torch.no_grad()
+    def sample(self) -> SampleBatch:
+        self.run_fragment()
         _, last_v = self.model(self.s_obs)
         adv, ret = ops.gae(self.buf_rew, self.buf_vf, self.buf_done, last_v.float(), self.gamma, self.lam)
         n = self.T * self.B

@@ -107,3 +107,92 @@ def test_gpu_object_reconstructed_when_owner_dies(gpu_ray, tmp_path):
     again = ray.get(t_ref, timeout=60)
     assert float(again.sum()) == 5.0 * (1 << 16)
     assert counter.read_text() == "xx"
+
+
+def test_freed_object_not_recycled_while_reader_holds_view(gpu_ray):
+    """The owner must not recycle HBM whose descriptor a reader in another process still pins
+    (a temporary ref dropped right after get): the free is deferred until the view dies."""
+    import torch
+
+    @ray.remote(num_gpus=1)
+    class Owner:
+        def make(self, v, n):
+            return torch.full((n,), float(v), device="cuda")
+
+        def gpu_objects(self):
+            from ray_memory_management_amd._private import gpu_object_store as gos
+            from ray_memory_management_amd._private.worker import global_worker
+
+            return sum(s["num_objects"] for s in gos.stats(global_worker).values())
+
+    o = Owner.remote()
+    x = ray.get(o.make.remote(1.0, 1 << 20))  # the ref is a temporary: refcount drops to 0 now
+    time.sleep(0.5)  # FREE_GPU reaches the owner, which must defer (the view pins the descriptor)
+    ys = [ray.get(o.make.remote(2.0 + i, 1 << 20)) for i in range(4)]  # would reuse the region
+    torch.cuda.synchronize()
+    assert float(x.min()) == 1.0 and float(x.max()) == 1.0
+    for i, y in enumerate(ys):
+        assert float(y.min()) == 2.0 + i
+    del x, ys
+    deadline = time.time() + 20
+    while time.time() < deadline and ray.get(o.gpu_objects.remote()) > 0:
+        time.sleep(0.1)
+    assert ray.get(o.gpu_objects.remote()) == 0  # deferred frees completed once the views died
+
+
+def test_nested_cuda_tensors_stay_in_hbm(gpu_ray):
+    import torch
+
+    @ray.remote(num_gpus=1)
+    def make():
+        return {"a": torch.arange(1000, device="cuda", dtype=torch.float32),
+                "b": [torch.ones(7, device="cuda", dtype=torch.bfloat16), 3]}
+
+    d = ray.get(make.remote())
+    assert d["a"].is_cuda and d["b"][0].is_cuda and d["b"][1] == 3
+    assert float(d["a"].sum()) == sum(range(1000)) and float(d["b"][0].sum()) == 7.0
+    # and a dict put from the driver round-trips through a task on the same GPU
+    r = ray.put({"x": torch.full((64,), 4.0, device="cuda")})
+
+    @ray.remote(num_gpus=1)
+    def total(dd):
+        return float(dd["x"].sum())
+
+    assert ray.get(total.remote(r)) == 256.0
+
+
+def test_cross_gpu_pull_path_with_quota(gpu_ray):
+    """Forced peer path (RMM_TEST_FORCE_PEER_COPY): the consumer imports the owner's slab and DMAs
+    the object into its own memory under the pull quota instead of aliasing it."""
+    import torch
+
+    t = torch.arange(1 << 20, device="cuda", dtype=torch.float32)
+    ref = ray.put(t)
+
+    @ray.remote(num_gpus=1, runtime_env={"env_vars": {"RMM_TEST_FORCE_PEER_COPY": "1"}})
+    def consume(x):
+        from ray_memory_management_amd._private import gpu_object_store as gos
+
+        x.add_(1.0)  # a private replica: mutating it must not touch the owner's object
+        return float(x.double().sum()), gos.pull_stats()
+
+    s, st = ray.get(consume.remote(ref))
+    assert s == float(t.double().sum()) + (1 << 20)
+    assert st["pulls"] == 1 and st["bytes_pulled"] == t.numel() * 4
+    assert torch.equal(ray.get(ref), t)
+
+
+def test_async_put_then_cross_process_read(gpu_ray):
+    """put() returns before the device copy finishes; a reader in another process waits for the
+    descriptor seal (host callback after the copy) and sees complete data."""
+    import torch
+
+    big = torch.randn(64 << 20, device="cuda", dtype=torch.bfloat16)  # 128 MiB copy
+    refs = [ray.put(big) for _ in range(3)]
+
+    @ray.remote(num_gpus=1)
+    def checksum(x):
+        return float(x.float().sum())
+
+    want = float(big.float().sum())
+    assert all(abs(v - want) <= 1e-3 * abs(want) + 1e-3 for v in ray.get([checksum.remote(r) for r in refs]))
