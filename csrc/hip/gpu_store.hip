@@ -103,6 +103,7 @@ GpuStore::~GpuStore() {
   if (work_) (void)hipFree(work_);
   for (auto e : ev_)
     if (e) (void)hipEventDestroy(e);
+  if (host_) host_unregister_segment(reinterpret_cast<uintptr_t>(host_->Base()));
   if (side_) (void)hipStreamDestroy(side_);
   if (side2_) (void)hipStreamDestroy(side2_);
 }

@@ -213,6 +213,7 @@ PYBIND11_MODULE(_hip, m) {
     return h2d_from_segment(P<void>(dst), P<const void>(src), n, S(stream));
   });
   m.def("host_unregister_all", [] { host_unregister_all(); });
+  m.def("host_unregister_segment", [](uint64_t base) { host_unregister_segment(base); });
   m.def("h2d_stats", [] { return h2d_stats(); });
   m.def("grad_clip_coef", [](uint64_t grad, bool grad_bf16, int64_t n, float grad_scale, float max_norm,
                              uint64_t ws, uint64_t out, uint64_t stream) {

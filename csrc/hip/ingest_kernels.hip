@@ -260,6 +260,19 @@ uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t st
 
 std::vector<uint64_t> h2d_stats() { return {g_h2d.direct, g_h2d.staged, g_h2d.chunks_ok, g_h2d.chunks_failed}; }
 
+void host_unregister_segment(uintptr_t base) {
+  auto& R = Registry();
+  std::lock_guard<std::mutex> g(R.mu);
+  auto it = R.segs.find(base);
+  if (it == R.segs.end()) return;
+  const uintptr_t end = base + it->second.second;
+  for (auto c = R.chunks.lower_bound(base); c != R.chunks.end() && c->first < end;) {
+    if (c->second) (void)hipHostUnregister(reinterpret_cast<void*>(c->first));
+    c = R.chunks.erase(c);
+  }
+  R.segs.erase(it);
+}
+
 void host_unregister_all() {
   auto& R = Registry();
   std::lock_guard<std::mutex> g(R.mu);

@@ -175,6 +175,9 @@ uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t st
 //  chunks that could not be pinned}
 std::vector<uint64_t> h2d_stats();
 void host_unregister_all();
+// Unpin every chunk of a segment and forget it: MUST run before the segment is unmapped (a stale
+// registration would alias whatever is mapped at that address next).
+void host_unregister_segment(uintptr_t base);
 
 }  // namespace hip
 }  // namespace rmm

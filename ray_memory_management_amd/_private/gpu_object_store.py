@@ -430,3 +430,17 @@ def shutdown_process_store(worker):
         stores.clear()
     if getattr(worker, "_gpu_meta", None):
         worker._gpu_meta.clear()
+    unpin_store_segment(worker)
+
+
+def unpin_store_segment(worker):
+    """Drop every host-registration chunk of this worker's shm segment (ingest / spill DMA) before
+    the segment is unmapped at shutdown."""
+    import sys
+
+    if "ray_memory_management_amd._hip" not in sys.modules or getattr(worker, "store", None) is None:
+        return
+    try:
+        require_hip().host_unregister_segment(worker.store.base_address())
+    except Exception:
+        pass
