@@ -78,7 +78,9 @@ static void InitSync(Header* h) {
 }
 
 Store* Store::Create(const std::string& name, uint64_t size, const std::string& spill_dir,
-                     double spill_threshold, uint64_t min_spill_size, bool fallback) {
+                     double spill_threshold, uint64_t min_spill_size, bool fallback, double oom_grace_s) {
+  if (spill_dir.size() >= sizeof(Header::spill_dir))
+    throw std::runtime_error("spill directory list too long");
   if (size < (8ull << 20)) size = 8ull << 20;
   uint64_t table_cap = 1 << 14;
   // one slot per 4 KiB of arena (112 B each, ~2.7% overhead): small-object heavy workloads
@@ -129,6 +131,7 @@ Store* Store::Create(const std::string& name, uint64_t size, const std::string& 
   h->spill_enabled = spill_dir.empty() ? 0 : 1;
   h->fallback_enabled = (fallback && !spill_dir.empty()) ? 1 : 0;
   strncpy(h->spill_dir, spill_dir.c_str(), sizeof(h->spill_dir) - 1);
+  h->oom_grace_ns = int64_t(oom_grace_s * 1e9);
   InitSync(h);
   s->hdr_ = h;
   s->table_ = reinterpret_cast<Entry*>(s->base_ + table_off);
@@ -483,11 +486,56 @@ void Store::LruRemove(int64_t idx) {
 
 // ---------------------------------------------------------------- spill files
 
+std::vector<std::string> Store::SpillDirs() const {
+  std::vector<std::string> out;
+  std::string all(hdr_->spill_dir);
+  size_t b = 0;
+  while (b <= all.size()) {
+    size_t e = all.find(':', b);
+    if (e == std::string::npos) e = all.size();
+    if (e > b) out.push_back(all.substr(b, e - b));
+    b = e + 1;
+  }
+  return out;
+}
+
+// Spill / fallback files are spread round-robin over the configured directories (reference:
+// python/ray/_private/external_storage.py FileSystemStorage with several directory_path entries).
+std::string Store::DirFor(uint64_t fid) const {
+  const char* all = hdr_->spill_dir;
+  int n = 1;
+  for (const char* c = all; *c; c++) n += (*c == ':');
+  int k = int(fid % uint64_t(n)), i = 0;
+  const char* b = all;
+  for (const char* c = all;; c++) {
+    if (*c == ':' || *c == 0) {
+      if (i == k) return std::string(b, size_t(c - b));
+      if (*c == 0) break;
+      i++;
+      b = c + 1;
+    }
+  }
+  return std::string(all);
+}
+
 std::string Store::SpillPath(uint64_t fid) const {
-  return std::string(hdr_->spill_dir) + "/rmm-spill-" + std::to_string(fid) + ".bin";
+  return DirFor(fid) + "/rmm-spill-" + std::to_string(fid) + ".bin";
 }
 std::string Store::FallbackPath(uint64_t fid) const {
-  return std::string(hdr_->spill_dir) + "/rmm-fallback-" + std::to_string(fid) + ".bin";
+  return DirFor(fid) + "/rmm-fallback-" + std::to_string(fid) + ".bin";
+}
+
+void Store::SetDiskFull(bool full) {
+  Lock();
+  hdr_->disk_full = full ? 1 : 0;
+  Broadcast();
+  Unlock();
+}
+
+void Store::SetOomGrace(double seconds) {
+  Lock();
+  hdr_->oom_grace_ns = int64_t(seconds * 1e9);
+  Unlock();
 }
 
 int64_t Store::SpillSlot(uint64_t fid, bool create) {
@@ -566,7 +614,7 @@ void Store::FreeEntryStorage(int64_t idx) {
 
 // Spill LRU victims with the lock held on entry and exit (released around file IO).
 uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
-  if (!hdr_->spill_enabled) return 0;
+  if (!hdr_->spill_enabled || hdr_->disk_full) return 0;
   uint64_t freed = 0;
   // 1) free objects that already have an up-to-date spill copy (no IO needed)
   std::vector<ObjectId> batch;
@@ -760,11 +808,30 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   e->create_ns = uint64_t(NowNs());
   hdr_->stats.creates_total++;
   // proactive threshold spilling is driven by the node (SpillBytes); here only on demand.
+  // Create-request queue semantics (reference plasma/create_request_queue.cc:88): when neither
+  // the heap nor spilling can satisfy the request, wait — bumping gc_requests so the node
+  // broadcasts a global GC, and letting in-flight spills / releases free memory — for up to
+  // oom_grace_ns, then fall back to a file-backed allocation (if enabled) or fail.
   uint64_t off = HeapAlloc(len);
-  while (off == kNil && hdr_->spill_enabled) {
-    uint64_t f = SpillLocked(len, nullptr);
+  int64_t wait_deadline = -1;
+  bool waited = false;
+  for (;;) {
+    while (off == kNil && hdr_->spill_enabled && !hdr_->disk_full) {
+      uint64_t f = SpillLocked(len, nullptr);
+      off = HeapAlloc(len);
+      if (f == 0) break;
+    }
+    if (off != kNil || hdr_->oom_grace_ns <= 0 || len > hdr_->heap_size) break;
+    const int64_t now = NowNs();
+    if (wait_deadline < 0) {
+      wait_deadline = now + hdr_->oom_grace_ns;
+      __atomic_add_fetch(&hdr_->gc_requests, 1, __ATOMIC_RELEASE);
+      if (!waited) hdr_->oom_waits_total++;
+      waited = true;
+    }
+    if (now >= wait_deadline) break;
+    CondWait(std::min<int64_t>(wait_deadline, now + 20000000ll));  // re-check every 20 ms (or on a broadcast)
     off = HeapAlloc(len);
-    if (f == 0) break;
   }
   idx = Find(id);
   e = E(idx);
@@ -772,7 +839,7 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   if (off != kNil) {
     e->offset = off;
     ptr = base_ + off;
-  } else if (hdr_->fallback_enabled) {
+  } else if (hdr_->fallback_enabled && !hdr_->disk_full) {
     uint64_t fid = hdr_->next_file_id++;
     Unlock();
     ptr = FallbackMap(fid, len, true);
@@ -788,7 +855,12 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   }
   if (!ptr) {
     RemoveEntry(idx);
+    hdr_->oom_errors_total++;
+    const bool disk = hdr_->disk_full != 0;
     Unlock();
+    if (disk)
+      throw std::runtime_error("OutOfDiskError: local disk is full: cannot spill or fall back to allocate " +
+                               std::to_string(len) + " bytes (capacity " + std::to_string(hdr_->heap_size) + ")");
     throw std::runtime_error("ObjectStoreFullError: cannot allocate " + std::to_string(len) +
                              " bytes (capacity " + std::to_string(hdr_->heap_size) + ")");
   }
@@ -976,6 +1048,17 @@ void Store::ClearFlag(const ObjectId& id, uint32_t flag) {
   int64_t idx = Find(id);
   if (idx >= 0) E(idx)->flags &= ~flag;
   Unlock();
+}
+
+std::vector<int64_t> Store::Sizes(const std::vector<ObjectId>& ids) {
+  std::vector<int64_t> out(ids.size(), -1);
+  Lock();
+  for (size_t i = 0; i < ids.size(); i++) {
+    int64_t idx = Find(ids[i]);
+    if (idx >= 0 && E(idx)->state != kCreating) out[i] = int64_t(E(idx)->data_size + E(idx)->meta_size);
+  }
+  Unlock();
+  return out;
 }
 
 int Store::State(const ObjectId& id) {

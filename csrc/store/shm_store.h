@@ -140,7 +140,14 @@ struct Header {
   uint64_t min_spill_size;      // fuse at least this many bytes per spill file
   int32_t spill_enabled;
   int32_t fallback_enabled;
-  char spill_dir[512];
+  char spill_dir[2048];        // one or more directories separated by ':' (round-robin per file)
+  // memory-pressure machinery (reference: plasma create_request_queue.cc, file_system_monitor.cc)
+  int64_t oom_grace_ns;        // a create that cannot be satisfied waits this long (GC + spill) first
+  int32_t disk_full;           // set by the node's disk monitor: no spilling / fallback files
+  int32_t pad0;
+  uint64_t gc_requests;        // bumped by a starved create: the node broadcasts a global GC
+  uint64_t oom_waits_total;    // creates that had to wait for memory
+  uint64_t oom_errors_total;   // creates that failed after the grace period
   Stats stats;
 };
 
@@ -148,7 +155,16 @@ class Store {
  public:
   // Create a new segment (head process) or attach to an existing one.
   static Store* Create(const std::string& name, uint64_t size, const std::string& spill_dir,
-                       double spill_threshold, uint64_t min_spill_size, bool fallback);
+                       double spill_threshold, uint64_t min_spill_size, bool fallback,
+                       double oom_grace_s = 2.0);
+  // Memory-pressure controls / counters (see Header).
+  void SetDiskFull(bool full);
+  bool DiskFull() const { return hdr_->disk_full != 0; }
+  uint64_t GcRequests() const { return __atomic_load_n(&hdr_->gc_requests, __ATOMIC_ACQUIRE); }
+  uint64_t OomWaits() const { return hdr_->oom_waits_total; }
+  uint64_t OomErrors() const { return hdr_->oom_errors_total; }
+  void SetOomGrace(double seconds);
+  std::vector<std::string> SpillDirs() const;
   static Store* Attach(const std::string& name);
   ~Store();
 
@@ -193,6 +209,8 @@ class Store {
     return ok;
   }
   int State(const ObjectId& id);       // ObjState or -1
+  // data + metadata bytes of each object (-1 if absent), one lock acquisition for the batch
+  std::vector<int64_t> Sizes(const std::vector<ObjectId>& ids);
   // Spill LRU unpinned objects until `bytes` have been freed. Returns bytes freed.
   uint64_t SpillBytes(uint64_t bytes);
   // Abort all objects still being created by `pid` (crashed creator).
@@ -233,6 +251,7 @@ class Store {
   uint8_t* FallbackMap(uint64_t fid, uint64_t size, bool create);
   void FallbackUnlink(uint64_t fid);
   std::string SpillPath(uint64_t fid) const;
+  std::string DirFor(uint64_t fid) const;
   std::string FallbackPath(uint64_t fid) const;
   void Broadcast() { pthread_cond_broadcast(&hdr_->cv); }
   void CondWait(int64_t deadline_ns);

@@ -181,14 +181,15 @@ PYBIND11_MODULE(_store, m) {
       .def_static(
           "create_segment",
           [](const std::string& name, uint64_t size, const std::string& spill_dir,
-             double spill_threshold, uint64_t min_spill_size, bool fallback) {
+             double spill_threshold, uint64_t min_spill_size, bool fallback, double oom_grace_s) {
             PyStore ps;
-            ps.s.reset(Store::Create(name, size, spill_dir, spill_threshold, min_spill_size, fallback));
+            ps.s.reset(Store::Create(name, size, spill_dir, spill_threshold, min_spill_size, fallback,
+                                     oom_grace_s));
             return ps;
           },
           py::arg("name"), py::arg("size"), py::arg("spill_dir") = "",
           py::arg("spill_threshold") = 0.8, py::arg("min_spill_size") = 100ull << 20,
-          py::arg("fallback") = true)
+          py::arg("fallback") = true, py::arg("oom_grace_s") = 2.0)
       .def_static("attach",
                   [](const std::string& name) {
                     PyStore ps;
@@ -345,6 +346,12 @@ PYBIND11_MODULE(_store, m) {
            })
       .def("contains", [](PyStore& self, py::bytes oid) { return self.s->Contains(ToId(oid)); })
       .def("state", [](PyStore& self, py::bytes oid) { return self.s->State(ToId(oid)); })
+      .def("sizes", [](PyStore& self, const std::vector<py::bytes>& oids) {
+        std::vector<ObjectId> ids;
+        ids.reserve(oids.size());
+        for (auto& o : oids) ids.push_back(ToId(o));
+        return self.s->Sizes(ids);
+      })
       .def("spill",
            [](PyStore& self, uint64_t bytes) {
              py::gil_scoped_release nogil;
@@ -369,6 +376,19 @@ PYBIND11_MODULE(_store, m) {
       .def("wake", [](PyStore& self) { self.s->Wake(); })
       .def("stats", [](PyStore& self) { return StatsDict(self.s->GetStats(), self.s->Capacity()); })
       .def("capacity", [](PyStore& self) { return self.s->Capacity(); })
+      .def("set_disk_full", [](PyStore& self, bool full) { self.s->SetDiskFull(full); })
+      .def("disk_full", [](PyStore& self) { return self.s->DiskFull(); })
+      .def("gc_requests", [](PyStore& self) { return self.s->GcRequests(); })
+      .def("set_oom_grace", [](PyStore& self, double s) { self.s->SetOomGrace(s); })
+      .def("spill_dirs", [](PyStore& self) { return self.s->SpillDirs(); })
+      .def("oom_stats", [](PyStore& self) {
+        py::dict d;
+        d["oom_waits_total"] = self.s->OomWaits();
+        d["oom_errors_total"] = self.s->OomErrors();
+        d["gc_requests"] = self.s->GcRequests();
+        d["disk_full"] = self.s->DiskFull();
+        return d;
+      })
       .def("base_address", [](PyStore& self) { return reinterpret_cast<uintptr_t>(self.s->Base()); })
       .def("mapped_size", [](PyStore& self) { return self.s->MappedSize(); })
       .def("check_heap", [](PyStore& self) { return self.s->CheckHeap(); })

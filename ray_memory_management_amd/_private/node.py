@@ -114,7 +114,7 @@ class WorkerRec:
 
 class TaskRec:
     __slots__ = ("spec", "state", "worker", "node", "assign", "retries_left", "attempt", "submit_time",
-                 "start_time", "end_time", "arg_refs", "owner_conn", "cancelled", "error")
+                 "start_time", "end_time", "arg_refs", "owner_conn", "cancelled", "error", "pinned_bytes")
 
     def __init__(self, spec, owner_conn):
         self.spec = spec
@@ -131,6 +131,7 @@ class TaskRec:
         self.owner_conn = owner_conn
         self.cancelled = False
         self.error = None
+        self.pinned_bytes = None
 
 
 class ActorRec:
@@ -176,14 +177,39 @@ class Head:
         self.sock_path = os.path.join(self.session_dir, "sockets", "head.sock")
         self.store_name = args.store_name
         self.config = json.loads(args.config) if args.config else {}
-        spill_dir = self.config.get("spill_dir") or os.path.join(self.session_dir, "spill")
-        os.makedirs(spill_dir, exist_ok=True)
+        self.spill_dirs = self._spill_dirs()
+        for d in self.spill_dirs:
+            os.makedirs(d, exist_ok=True)
         cap = int(args.object_store_memory)
         min_spill = int(self.config.get("min_spilling_size", min(100 << 20, max(1 << 20, cap // 16))))
         self.spill_threshold = float(self.config.get("object_spilling_threshold", 0.8))
         self.store = store_ext().ObjectStore.create_segment(
-            self.store_name, cap, spill_dir if self.config.get("automatic_object_spilling_enabled", True) else "",
-            self.spill_threshold, min_spill, True)
+            self.store_name, cap,
+            ":".join(self.spill_dirs) if self.config.get("automatic_object_spilling_enabled", True) else "",
+            self.spill_threshold, min_spill, bool(self.config.get("object_store_fallback_allocation", True)),
+            float(self.config.get("oom_grace_period_s", 2.0)))
+        # memory-pressure machinery (reference: local_object_manager.cc IO-worker spilling,
+        # local_task_manager.cc:615 PinTaskArgsIfMemoryAvailable, node_manager.cc:2799
+        # TriggerGlobalGC, file_system_monitor.cc)
+        import concurrent.futures
+
+        self.max_io_workers = int(self.config.get("max_io_workers", 4))
+        self.io_pool = concurrent.futures.ThreadPoolExecutor(self.max_io_workers, thread_name_prefix="rmm-io")
+        self.spills_in_flight = 0
+        self.spill_lock = threading.Lock()
+        self.max_spill_bytes_per_job = int(self.config.get("max_spill_bytes_per_io_worker", 1 << 30))
+        self.task_args_fraction = float(self.config.get("max_task_args_memory_fraction", 0.7))
+        self.pinned_arg_bytes = 0
+        self.pinned_arg_tasks = 0
+        self.disk_threshold = float(self.config.get("local_fs_capacity_threshold", 0.95))
+        self.disk_check_interval = float(self.config.get("local_fs_monitor_interval_ms", 1000)) / 1000.0
+        self.last_disk_check = 0.0
+        self.gc_seen = 0
+        self.last_global_gc = 0.0
+        self.gc_min_interval = float(self.config.get("global_gc_min_interval_s", 1.0))
+        self.gc_high_usage = float(self.config.get("high_plasma_storage_usage", 0.7))
+        self.gc_auto_interval = float(self.config.get("automatic_gc_min_interval_s", 30.0))
+        self.mem_stats = collections.Counter()
         self.sched = sched_ext().Scheduler()
         self.sched.set_spread_threshold(float(self.config.get("scheduler_spread_threshold", 0.5)))
         self.nodes: Dict[int, dict] = {}
@@ -246,6 +272,21 @@ class Head:
 
             self.memory_monitor = MemoryMonitor(
                 threshold=float(self.config.get("memory_usage_threshold", 0.95)))
+
+    def _spill_dirs(self):
+        """Spill directories: `spill_dir` (str or list) or the reference's object_spilling_config
+        JSON ({"type": "filesystem", "params": {"directory_path": str | [str, ...]}})."""
+        c = self.config
+        dirs = c.get("spill_dir")
+        if not dirs and c.get("object_spilling_config"):
+            sc = c["object_spilling_config"]
+            sc = json.loads(sc) if isinstance(sc, str) else sc
+            dirs = (sc.get("params") or {}).get("directory_path")
+        if not dirs:
+            dirs = [os.path.join(self.session_dir, "spill")]
+        if isinstance(dirs, str):
+            dirs = [dirs]
+        return [os.path.abspath(d) for d in dirs]
 
     # ------------------------------------------------------------------ nodes
     def _add_node(self, node_id, resources, head=False):
@@ -491,6 +532,8 @@ class Head:
             if a is not None:
                 a.restarts_left = 0
                 a.death_cause = "The actor exited via exit_actor()."
+        elif t == P.GLOBAL_GC:
+            self._global_gc("requested")
         elif t == P.SHUTDOWN:
             self.running = False
         else:
@@ -817,6 +860,34 @@ class Head:
     def _gpu_key(self, gpu_ids):
         return ",".join(map(str, gpu_ids)) if gpu_ids else ""
 
+    def _pin_task_args(self, t: TaskRec) -> bool:
+        """Reference local_task_manager.cc:615 PinTaskArgsIfMemoryAvailable: a task's by-ref
+        arguments stay pinned in the store while it runs; a new task is held back when pinning its
+        args would push the pinned total over max_task_args_memory_fraction of the store (unless
+        nothing is pinned, so one oversized task can still make progress)."""
+        if getattr(t, "pinned_bytes", None) is not None:
+            return True
+        refs = [r for r in t.arg_refs if not _is_actor_key(r)]
+        n = 0
+        if refs:
+            n = sum(max(0, x) for x in self.store.sizes(refs))
+        cap = self.store.capacity()
+        if n and self.pinned_arg_tasks > 0 and self.pinned_arg_bytes + n > self.task_args_fraction * cap:
+            self.mem_stats["task_args_backpressure"] += 1
+            return False
+        t.pinned_bytes = n
+        if n:
+            self.pinned_arg_bytes += n
+            self.pinned_arg_tasks += 1
+        return True
+
+    def _unpin_task_args(self, t: TaskRec):
+        n = getattr(t, "pinned_bytes", None)
+        if n:
+            self.pinned_arg_bytes -= n
+            self.pinned_arg_tasks -= 1
+        t.pinned_bytes = None
+
     def _dispatch(self, t: TaskRec) -> bool:
         spec = t.spec
         node, gpu_ids, amounts = t.assign
@@ -838,6 +909,10 @@ class Head:
                 self._start_worker(node, (env_key, gkey), gpu_ids if gpu_ids else None,
                                    runtime_env=spec.get("runtime_env"))
             return False
+        if not self._pin_task_args(t):
+            pool = self.idle.setdefault(key, [])
+            pool.append(w)
+            return False
         fid = spec["fn_id"]
         blob = None
         if fid not in w.fns:
@@ -853,6 +928,7 @@ class Head:
         return True
 
     def _release_task_resources(self, t: TaskRec):
+        self._unpin_task_args(t)
         if t.assign is not None:
             node, gpu_ids, amounts = t.assign
             req = dict(t.spec.get("_res", t.spec["resources"]))
@@ -1239,6 +1315,10 @@ class Head:
                     "infeasible": len(self.sched.infeasible_tasks())}
         if what == "memory":
             return self.memory_monitor.snapshot() if self.memory_monitor else {}
+        if what == "memory_pressure":
+            return {**dict(self.mem_stats), "pinned_arg_bytes": self.pinned_arg_bytes,
+                    "pinned_arg_tasks": self.pinned_arg_tasks, "spills_in_flight": self.spills_in_flight,
+                    "spill_dirs": self.spill_dirs, **self.store.oom_stats()}
         raise ValueError(f"unknown state query {what}")
 
     # ------------------------------------------------------------------ housekeeping
@@ -1249,12 +1329,23 @@ class Head:
             if w.proc is not None and w.proc.poll() is not None:
                 if w.conn is None or not w.conn.alive or w.state == "DEAD":
                     self._worker_died(w)
-        # threshold-driven spilling
+        # threshold-driven spilling by a capped pool of IO workers (local_object_manager.cc:149,172)
         st = self.store.stats()
         cap = st["capacity"]
         if cap and st["bytes_in_use"] > self.spill_threshold * cap:
             excess = st["bytes_in_use"] - int(self.spill_threshold * cap)
-            threading.Thread(target=self.store.spill, args=(excess,), daemon=True).start()
+            with self.spill_lock:
+                free_slots = self.max_io_workers - self.spills_in_flight
+            for _ in range(max(0, free_slots)):
+                if excess <= 0:
+                    break
+                job = min(excess, self.max_spill_bytes_per_job)
+                excess -= job
+                with self.spill_lock:
+                    self.spills_in_flight += 1
+                self.io_pool.submit(self._io_spill, job)
+        self._disk_monitor(now)
+        self._maybe_global_gc(now, st)
         # idle worker reaping (keep prestart pool)
         idle_total = sum(len(v) for v in self.idle.values())
         if idle_total > self.prestart:
@@ -1278,7 +1369,61 @@ class Head:
                     t.error = "oom"
                 self._kill_worker(victim)
 
+    def _io_spill(self, nbytes):
+        try:
+            freed = self.store.spill(nbytes)
+            self.mem_stats["io_spill_jobs"] += 1
+            self.mem_stats["io_spilled_bytes"] += freed
+        except Exception:
+            traceback.print_exc()
+        finally:
+            with self.spill_lock:
+                self.spills_in_flight -= 1
+
+    def _disk_monitor(self, now):
+        """Reference src/ray/common/file_system_monitor.cc: spilling (and fallback files) stop when
+        a spill directory's filesystem is over local_fs_capacity_threshold; a put that then cannot
+        be satisfied raises OutOfDiskError."""
+        if now - self.last_disk_check < self.disk_check_interval:
+            return
+        self.last_disk_check = now
+        full = False
+        for d in self.spill_dirs:
+            try:
+                v = os.statvfs(d)
+            except OSError:
+                continue
+            total = v.f_blocks * v.f_frsize
+            if total and 1.0 - (v.f_bavail * v.f_frsize) / total > self.disk_threshold:
+                full = True
+        if full != self.store.disk_full():
+            self.store.set_disk_full(full)
+            self.mem_stats["disk_full_transitions"] += 1
+
+    def _maybe_global_gc(self, now, st):
+        """A create starved past its first retry bumps the store's gc_requests; the head then
+        broadcasts a GC to every worker and driver (node_manager.cc:2799 TriggerGlobalGC). Also
+        triggered periodically while the store is above high_plasma_storage_usage."""
+        req = self.store.gc_requests()
+        cap = st.get("capacity") or 0
+        if req != self.gc_seen and now - self.last_global_gc >= self.gc_min_interval:
+            self.gc_seen = req
+            self._global_gc("store pressure")
+        elif cap and st["bytes_in_use"] > self.gc_high_usage * cap and now - self.last_global_gc >= self.gc_auto_interval:
+            self._global_gc("high usage")
+
+    def _global_gc(self, reason):
+        self.last_global_gc = time.time()
+        self.mem_stats["global_gc"] += 1
+        for c in list(self.conns.values()):
+            if c.alive and (c.kind == "driver" or c.worker is not None):
+                self._send_nb(c, (P.TRIGGER_GC, reason))
+
     def _shutdown(self):
+        try:
+            self.io_pool.shutdown(wait=False)
+        except Exception:
+            pass
         for w in list(self.workers.values()):
             if w.conn is not None and w.conn.alive:
                 try:

@@ -47,6 +47,7 @@ ADD_NODE = 28
 REMOVE_NODE = 29
 ACTOR_EXITING = 30
 GPU_OBJECT = 31
+GLOBAL_GC = 32
 
 # ---- head -> worker
 EXECUTE = 101
@@ -55,6 +56,7 @@ EXIT = 103
 CANCEL_TASK = 104
 REPLY = 105
 FREE_GPU = 106
+TRIGGER_GC = 107
 
 # ---- caller -> actor (direct transport)
 ACTOR_TASK = 201

@@ -226,6 +226,8 @@ class CoreWorker:
                     if p is not None:
                         p.value = m[2]
                         p.ev.set()
+                elif t == P.TRIGGER_GC:
+                    threading.Thread(target=_collect_garbage, daemon=True).start()
                 elif t in (P.CANCEL_TASK, P.FREE_GPU):
                     try:  # a failing side-channel handler must never take the reader thread down
                         if t == P.CANCEL_TASK:
@@ -339,6 +341,8 @@ class CoreWorker:
         try:
             self.store.put_serialized(oid, data, bufs, ser.TAG_PICKLE, False)
         except RuntimeError as e:
+            if "OutOfDiskError" in str(e):
+                raise exc.OutOfDiskError(str(e)) from None
             if "ObjectStoreFullError" in str(e):
                 raise exc.ObjectStoreFullError(str(e)) from None
             raise
@@ -558,6 +562,19 @@ class CoreWorker:
             self.sock.close()
         except OSError:
             pass
+
+
+_gc_count = 0
+
+
+def _collect_garbage():
+    """Head-triggered global GC: drop unreachable ObjectRefs (reference cycles) so their objects
+    can be freed under memory pressure (reference: CoreWorker::HandleLocalGC)."""
+    global _gc_count
+    import gc
+
+    gc.collect()
+    _gc_count += 1
 
 
 def _is_cuda_tensor(v) -> bool:

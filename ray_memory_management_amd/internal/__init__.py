@@ -36,9 +36,20 @@ def memory_summary(address=None, stats_only: bool = False, units: str = "MB", nu
 
 
 def global_gc():
+    """Trigger a garbage collection in every worker and driver of the cluster (reference
+    python/ray/_private/internal_api.py global_gc → raylet TriggerGlobalGC)."""
     import gc
 
     gc.collect()
+    w = _w.global_worker
+    if w is not None:
+        w.send((P.GLOBAL_GC,))
+
+
+def memory_pressure_stats() -> dict:
+    """Counters of the node's memory-pressure machinery (task-arg backpressure, IO-worker spills,
+    global GCs, create-request waits / failures, disk-full state)."""
+    return _w._state("memory_pressure")
 
 
 # ---- internal KV (reference python/ray/experimental/internal_kv.py)
