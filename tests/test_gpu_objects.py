@@ -133,7 +133,7 @@ def test_freed_object_not_recycled_while_reader_holds_view(gpu_ray):
     assert float(x.min()) == 1.0 and float(x.max()) == 1.0
     for i, y in enumerate(ys):
         assert float(y.min()) == 2.0 + i
-    del x, ys
+    del x, ys, y  # (y: the loop variable still references the last view)
     deadline = time.time() + 20
     while time.time() < deadline and ray.get(o.gpu_objects.remote()) > 0:
         time.sleep(0.1)
