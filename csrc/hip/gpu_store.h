@@ -111,6 +111,7 @@ class GpuStore {
   uint64_t RestoreForeign(const std::string& host_id, uint64_t dst, uint64_t nbytes);
   void SetSpillThreshold(double t);
   GpuStats Stats();
+  std::string LastError();  // message of the last failed spill / restore transfer
   int device() const { return device_; }
 
   // Spill-object id in the host store for a GPU object id.
@@ -162,6 +163,11 @@ class GpuStore {
   bool stop_ = false;
   std::condition_variable bg_cv_;
   std::thread bg_;
+  std::mutex err_mu_;
+  std::string last_error_;
+  std::string last_stale_;
+  uint64_t stale_errors_ = 0;
+  void ClearStaleError(const char* where);
 };
 
 }  // namespace hip

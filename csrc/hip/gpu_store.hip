@@ -426,9 +426,21 @@ void GpuStore::EnsureScratch() {
 
 // ---------------------------------------------------------------- spill
 
+void GpuStore::ClearStaleError(const char* where) {
+  // HIP's last-error is sticky per thread: an unchecked failure of an unrelated earlier call
+  // (another library on this thread) must not be reported by our kernels' launch checks
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::lock_guard<std::mutex> g(err_mu_);
+    stale_errors_++;
+    last_stale_ = std::string(where) + ": " + hipGetErrorString(e);
+  }
+}
+
 bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t nbytes, int elem_bits,
                              hipEvent_t ready, uint64_t* host_bytes, bool* compressed) {
   RMM_HIP_CHECK(hipSetDevice(device_));
+  ClearStaleError("spill");
   uint64_t nchunks = std::max<uint64_t>(1, (nbytes + kSpillChunk - 1) / kSpillChunk);
   const bool use_c = compress_ && (elem_bits == 16 || elem_bits == 32) && nbytes >= (1u << 20);
   const uint64_t hdr = SpillHdrBytes(nchunks);
@@ -444,7 +456,15 @@ bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t
     host_->Delete(hid);
     return false;
   }
-  const bool pinned = host_pin_range(dst, hdr + nbytes);
+  struct AbortGuard {  // a failed transfer must not leave a half-written CREATING object behind
+    Store* s;
+    ObjectId id;
+    bool done = false;
+    ~AbortGuard() {
+      if (!done) s->Abort(id);
+    }
+  } guard{host_.get(), hid};
+  host_pin_range(dst, hdr + nbytes);
   if (use_c) EnsureScratch();
   if (ready) RMM_HIP_CHECK(hipStreamWaitEvent(side_, ready, 0));
   std::vector<uint64_t> csize(nchunks, 0);
@@ -466,17 +486,16 @@ bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t
     if (cs) {
       RMM_HIP_CHECK(hipEventRecord(ev_[2], side_));
       RMM_HIP_CHECK(hipStreamWaitEvent(side2_, ev_[2], 0));
-      RMM_HIP_CHECK(hipMemcpyAsync(dst + doff, scratch_[b], cs, hipMemcpyDeviceToHost, side2_));
+      dma_host_segment(dst + doff, scratch_[b], cs, false, side2_);
       RMM_HIP_CHECK(hipEventRecord(done[b], side2_));
       doff += cs;
     } else {
       RMM_HIP_CHECK(hipEventRecord(ev_[2], side_));  // orders after `ready`
       RMM_HIP_CHECK(hipStreamWaitEvent(side2_, ev_[2], 0));
-      RMM_HIP_CHECK(hipMemcpyAsync(dst + doff, s, len, hipMemcpyDeviceToHost, side2_));
+      dma_host_segment(dst + doff, const_cast<uint8_t*>(s), len, false, side2_);
       doff += len;
     }
     csize[c] = cs;
-    if (!pinned) RMM_HIP_CHECK(hipStreamSynchronize(side2_));
   }
   RMM_HIP_CHECK(hipStreamSynchronize(side2_));
   RMM_HIP_CHECK(hipStreamSynchronize(side_));
@@ -490,6 +509,7 @@ bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t
   host_->ShrinkCreating(hid, doff);
   host_->Seal(hid);
   host_->Release(hid);
+  guard.done = true;
   *host_bytes = doff;
   *compressed = use_c;
   return true;
@@ -518,6 +538,10 @@ bool GpuStore::SpillOne(Lock& lk, const std::string& id) {
   try {
     std::lock_guard<std::mutex> x(xfer_mu_);
     ok = SpillTransfer(id, src, nbytes, bits, ready, &host_bytes, &compressed);
+  } catch (const std::exception& e) {
+    ok = false;
+    std::lock_guard<std::mutex> g(err_mu_);
+    last_error_ = e.what();
   } catch (...) {
     ok = false;
   }
@@ -615,6 +639,7 @@ void GpuStore::BackgroundSpiller() {
 
 uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uint64_t nbytes, bool delete_host) {
   RMM_HIP_CHECK(hipSetDevice(device_));
+  ClearStaleError("restore");
   const ObjectId hid = ToOid(host_id);
   Store::View v;
   if (!host_->Get(hid, 0, &v)) return 0;
@@ -626,7 +651,7 @@ uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uin
   const int bits = int(h[2]);
   const uint64_t nchunks = h[3];
   const uint64_t hdr = SpillHdrBytes(nchunks);
-  const bool pinned = host_pin_range(v.data, v.data_size);
+  host_pin_range(v.data, v.data_size);
   bool any_c = false;
   for (uint64_t c = 0; c < nchunks; c++) any_c |= h[4 + c] != 0;
   if (any_c) EnsureScratch();
@@ -638,7 +663,7 @@ uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uin
     if (cs) {
       const int b = int(c & 1);
       if (c >= 2) RMM_HIP_CHECK(hipStreamWaitEvent(side2_, done[b], 0));
-      RMM_HIP_CHECK(hipMemcpyAsync(scratch_[b], v.data + soff, cs, hipMemcpyHostToDevice, side2_));
+      dma_host_segment(const_cast<uint8_t*>(v.data) + soff, scratch_[b], cs, true, side2_);
       RMM_HIP_CHECK(hipEventRecord(ev_[2 + b], side2_));
       RMM_HIP_CHECK(hipStreamWaitEvent(side_, ev_[2 + b], 0));
       const uint64_t eb = uint64_t(bits / 8);
@@ -647,10 +672,9 @@ uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uin
       RMM_HIP_CHECK(hipEventRecord(done[b], side_));
       soff += cs;
     } else {
-      RMM_HIP_CHECK(hipMemcpyAsync(dst + c * kSpillChunk, v.data + soff, len, hipMemcpyHostToDevice, side2_));
+      dma_host_segment(const_cast<uint8_t*>(v.data) + soff, dst + c * kSpillChunk, len, true, side2_);
       soff += len;
     }
-    if (!pinned) RMM_HIP_CHECK(hipStreamSynchronize(side2_));
   }
   RMM_HIP_CHECK(hipStreamSynchronize(side2_));
   RMM_HIP_CHECK(hipStreamSynchronize(side_));
@@ -679,6 +703,10 @@ bool GpuStore::RestoreOne(Lock& lk, const std::string& id, GpuObject* o) {
   try {
     std::lock_guard<std::mutex> x(xfer_mu_);
     got = RestoreTransfer(HostId(id), dst, nbytes, true);
+  } catch (const std::exception& e) {
+    got = 0;
+    std::lock_guard<std::mutex> g(err_mu_);
+    last_error_ = e.what();
   } catch (...) {
     got = 0;
   }
@@ -726,6 +754,13 @@ uint64_t GpuStore::RestoreForeign(const std::string& host_id, uint64_t dst, uint
   st_.restored_bytes_total += n;
   st_.restore_ns_total += uint64_t(NowNs() - t0);
   return n;
+}
+
+std::string GpuStore::LastError() {
+  std::lock_guard<std::mutex> g(err_mu_);
+  if (stale_errors_) return last_error_ + " [stale errors cleared: " + std::to_string(stale_errors_) + ", last: " +
+                            last_stale_ + "]";
+  return last_error_;
 }
 
 GpuStats GpuStore::Stats() {

@@ -215,6 +215,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("host_unregister_all", [] { host_unregister_all(); });
   m.def("host_unregister_segment", [](uint64_t base) { host_unregister_segment(base); });
   m.def("h2d_stats", [] { return h2d_stats(); });
+  m.def("host_register_last_error", [] { return host_register_last_error(); });
   m.def("grad_clip_coef", [](uint64_t grad, bool grad_bf16, int64_t n, float grad_scale, float max_norm,
                              uint64_t ws, uint64_t out, uint64_t stream) {
     grad_clip_coef(P<const void>(grad), grad_bf16, n, grad_scale, max_norm, P<float>(ws), P<float>(out), S(stream));
@@ -385,6 +386,7 @@ PYBIND11_MODULE(_hip, m) {
         return s.RestoreForeign(hid, dst, nbytes);
       })
       .def("set_spill_threshold", &GpuStore::SetSpillThreshold)
+      .def("last_error", &GpuStore::LastError)
       .def("create", [](GpuStore& s, py::bytes id, uint64_t n, int bits) {
         return s.Create(std::string(id), n, bits);
       })

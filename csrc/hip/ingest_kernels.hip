@@ -171,6 +171,7 @@ void host_register_segment(uintptr_t base, uint64_t size) {
 }
 
 namespace {
+std::string g_reg_error;
 struct H2DStats {
   uint64_t direct = 0, staged = 0, chunks_ok = 0, chunks_failed = 0;
 } g_h2d;
@@ -225,8 +226,13 @@ bool host_pin_range(const void* src, uint64_t n, uint64_t* newly_out) {
           auto ck = R.chunks.find(c);
           if (ck == R.chunks.end()) {
             const uint64_t len = std::min<uint64_t>(kRegChunk, end - c);
-            const bool ok = hipHostRegister(reinterpret_cast<void*>(c), len, hipHostRegisterDefault) == hipSuccess;
-            if (!ok) (void)hipGetLastError();
+            const hipError_t re = hipHostRegister(reinterpret_cast<void*>(c), len, hipHostRegisterDefault);
+            const bool ok = re == hipSuccess;
+            if (!ok) {
+              (void)hipGetLastError();
+              g_reg_error = std::string(hipGetErrorString(re)) + " registering " + std::to_string(len) + " B at +" +
+                            std::to_string(c - base);
+            }
             ck = R.chunks.emplace(c, ok).first;
             if (ok) {
               newly += len;
@@ -244,17 +250,73 @@ bool host_pin_range(const void* src, uint64_t n, uint64_t* newly_out) {
   return all_ok;
 }
 
+namespace {
+// D2H through the bounce buffers (host side is not page-locked).
+void staged_copy_d2h(void* dst, const void* src, uint64_t n, hipStream_t stream) {
+  Staging& st = Stage();
+  const uint8_t* s8 = static_cast<const uint8_t*>(src);
+  uint8_t* d8 = static_cast<uint8_t*>(dst);
+  for (uint64_t off = 0; off < n; off += Staging::kBytes) {
+    const uint64_t len = std::min<uint64_t>(Staging::kBytes, n - off);
+    RMM_HIP_CHECK(hipEventSynchronize(st.ev[0]));
+    RMM_HIP_CHECK(hipMemcpyAsync(st.buf[0], s8 + off, len, hipMemcpyDeviceToHost, stream));
+    RMM_HIP_CHECK(hipStreamSynchronize(stream));
+    memcpy(d8 + off, st.buf[0], len);
+  }
+}
+}  // namespace
+
+void dma_host_segment(void* host, void* dev, uint64_t n, bool to_device, hipStream_t stream) {
+  auto& R = Registry();
+  const uintptr_t h = reinterpret_cast<uintptr_t>(host);
+  uintptr_t base = 0, end = 0;
+  {
+    std::lock_guard<std::mutex> g(R.mu);
+    auto it = R.segs.upper_bound(h);
+    if (it != R.segs.begin()) {
+      --it;
+      if (h >= it->second.first && h + n <= it->second.first + it->second.second) {
+        base = it->second.first;
+        end = base + it->second.second;
+      }
+    }
+  }
+  auto piece = [&](uintptr_t p, uint64_t len, bool pinned) {
+    void* hp = reinterpret_cast<void*>(p);
+    uint8_t* dp = static_cast<uint8_t*>(dev) + (p - h);
+    if (pinned) {
+      if (to_device) RMM_HIP_CHECK(hipMemcpyAsync(dp, hp, len, hipMemcpyHostToDevice, stream));
+      else RMM_HIP_CHECK(hipMemcpyAsync(hp, dp, len, hipMemcpyDeviceToHost, stream));
+      g_h2d.direct += len;
+    } else {
+      if (to_device) staged_copy(dp, hp, len, stream);
+      else staged_copy_d2h(hp, dp, len, stream);
+      g_h2d.staged += len;
+    }
+  };
+  if (!base) {  // not inside a registered segment
+    piece(h, n, false);
+    return;
+  }
+  // never let one copy straddle a pinned and an unpinned chunk: split at chunk boundaries
+  for (uintptr_t p = h; p < h + n;) {
+    const uintptr_t c = base + ((p - base) / kRegChunk) * kRegChunk;
+    const uintptr_t cend = std::min<uintptr_t>(std::min<uintptr_t>(c + kRegChunk, end), h + n);
+    const bool ok = host_pin_range(reinterpret_cast<const void*>(p), cend - p, nullptr);
+    piece(p, cend - p, ok);
+    p = cend;
+  }
+}
+
+std::string host_register_last_error() {
+  std::lock_guard<std::mutex> g(Registry().mu);
+  return g_reg_error;
+}
+
 uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream) {
   uint64_t newly = 0;
-  if (host_pin_range(src, n, &newly)) {
-    if (hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, stream) == hipSuccess) {
-      g_h2d.direct += n;
-      return newly;
-    }
-    (void)hipGetLastError();  // the runtime refused the range: take the staged path
-  }
-  staged_copy(dst, src, n, stream);
-  g_h2d.staged += n;
+  host_pin_range(src, n, &newly);
+  dma_host_segment(const_cast<void*>(src), dst, n, true, stream);
   return newly;
 }
 

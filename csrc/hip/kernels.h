@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 namespace rmm {
@@ -171,6 +172,11 @@ void host_register_segment(uintptr_t base, uint64_t size);
 // (then DMA straight from/to the range is safe). newly (optional) accumulates bytes pinned now.
 bool host_pin_range(const void* p, uint64_t n, uint64_t* newly = nullptr);
 uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t stream);
+// Host<->device copy of a range of a registered segment, split at registration-chunk boundaries:
+// page-locked chunks are async DMA on `stream`, chunks that could not be pinned go through the
+// bounce buffers (synchronously). One copy never straddles pinned and pageable memory.
+void dma_host_segment(void* host, void* dev, uint64_t n, bool to_device, hipStream_t stream);
+std::string host_register_last_error();
 // {bytes DMA'd straight from registered chunks, bytes staged via bounce buffers, chunks pinned,
 //  chunks that could not be pinned}
 std::vector<uint64_t> h2d_stats();
