@@ -71,14 +71,19 @@ def _rollout_layout(n_gpus: int, budget: int, fragment: int):
     return 1, total_envs
 
 
-def _put_get_bench(dev_index: int, gb: float = 4.0, iters: int = 5) -> float:
-    """Same-process ray.put(cuda bf16 tensor) + owner-side ray.get (zero-copy view); GB/s."""
+def _put_get_bench(dev_index: int, gb: float = 4.0, iters: int = 5):
+    """GPU object store numbers (BASELINE config #2). Returns (put_get_GBps, details):
+    put_get_GBps = same-process ray.put (HBM copy) + owner zero-copy get of one 4 GiB bf16 tensor;
+    details = benchmarks/gpu_object_store_bench.py: put GB/s at 1 and 16 GiB, cross-process get
+    (hipIPC, zero-copy) + full read, native spill / restore GB/s and bf16 compression ratio."""
     import torch
 
     import ray_memory_management_amd as ray
+    from benchmarks import gpu_object_store_bench as gb_bench
 
-    ray.init(num_cpus=1, num_gpus=0, object_store_memory=512 << 20,
-             _system_config={"prestart_workers": 0, "memory_monitor_refresh_ms": 0})
+    ray.init(num_cpus=2, num_gpus=1, object_store_memory=4 << 30,
+             _system_config={"prestart_workers": 0, "memory_monitor_refresh_ms": 0,
+                             "gpu_object_store_memory": 40 << 30})
     try:
         nel = int(gb * (1 << 30)) // 2
         t = torch.randn(nel, device=f"cuda:{dev_index}", dtype=torch.bfloat16)
@@ -96,7 +101,17 @@ def _put_get_bench(dev_index: int, gb: float = 4.0, iters: int = 5) -> float:
             torch.cuda.synchronize()
             total += time.perf_counter() - t0
             del v, r
-        return nel * 2 * iters / total / 1e9
+        del t
+        details = {}
+        try:
+            details.update(gb_bench.bench_put_get([1.0, 16.0], 3))
+            details.update(gb_bench.bench_xproc(1.0, 3))
+            from ray_memory_management_amd._private.worker import global_worker
+
+            details.update(gb_bench.bench_spill(1.0, global_worker.store_name))
+        except Exception as ex:  # noqa: BLE001
+            details["error"] = repr(ex)
+        return nel * 2 * iters / total / 1e9, details
     finally:
         ray.shutdown()
 
@@ -283,10 +298,10 @@ def main():
                 extra["fused_loop_samples_per_s"] = round(TRAIN_BATCH * a2.steps / fe, 1)
             except Exception as ex:  # noqa: BLE001
                 print(f"[bench] fused loop failed: {ex!r}", file=sys.stderr)
-        put_gbps = None
+        put_gbps, store_details = None, None
         if not args.no_putget and world == 1:
             try:
-                put_gbps = _put_get_bench(0)
+                put_gbps, store_details = _put_get_bench(0)
             except Exception as ex:  # noqa: BLE001
                 print(f"[bench] put/get failed: {ex!r}", file=sys.stderr)
         out = {
@@ -301,6 +316,7 @@ def main():
             **extra,
             "put_get_GBps": None if put_gbps is None else round(put_gbps, 2),
             "put_get_note": "same-process put (HBM copy) + owner zero-copy get of one 4 GiB bf16 tensor",
+            "gpu_object_store": store_details,
             "baseline_note": "vs_baseline divides by 1250 samples/s: RLlib 0.8.7 PPO Breakout, real emulator, "
                              "one V100 learner on a shared node (weak anchor, not like-for-like)",
             "last_stats": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in stats.items()
