@@ -120,6 +120,14 @@ def bench_spill(gb, shm_name):
     g = h.GpuStore(0, int(3 * gb * (1 << 30)), 8 << 30, shm_name, True)
     s = torch.cuda.current_stream().cuda_stream
     out = {}
+    # warm-up: the first spill into fresh host pages pays their first touch + page-locking
+    w = torch.randn(n, device="cuda", dtype=torch.bfloat16)
+    wid = os.urandom(20)
+    g.put_segments(wid, [(w.data_ptr(), n * 2)], 16, s)
+    _sync()
+    g.spill_object(wid)
+    g.delete(wid)
+    del w
     for name, x in (("randn", torch.randn(n, device="cuda", dtype=torch.bfloat16)),
                     ("smooth", torch.linspace(-1, 1, n, device="cuda").to(torch.bfloat16))):
         oid = os.urandom(20)

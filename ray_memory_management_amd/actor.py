@@ -200,6 +200,9 @@ class ActorClass:
             def remote(self_inner, *args, **kwargs):
                 return parent._remote(args, kwargs, merged)
 
+            def options(self_inner, **more):  # chained .options(...).options(...)
+                return parent.options(**{**opts, **more})
+
             def bind(self_inner, *args, **kwargs):
                 from ray_memory_management_amd.dag import ClassNode
 
