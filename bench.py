@@ -23,9 +23,11 @@ One timed step = one ``algo.train()`` iteration: sample 5000·N env steps, inges
 500-sample minibatch SGD on every learner, publish weights. Weak scaling (per-GPU batch fixed).
 ``value`` = whole-job env samples trained per second.
 
-``--rollout gpu`` swaps the CPU rollout workers for one GPU rollout actor per learner (device env +
-on-GPU inference, fragments through the HBM object store); ``--mode fused`` times the
-single-process fused loop of round 1 (env, sampler and learner in one process, torchrun for N>1).
+After the timed CPU-rollout run the bench also reports (separately labelled, same K/W):
+``runtime_gpu_rollout_samples_per_s`` — the same runtime path with one GPU rollout actor per learner
+(device env + on-GPU inference, fragments through the HBM object store via hipIPC, same GPU), and at
+N=1 ``fused_loop_samples_per_s`` — round 1's single-process fused loop (no runtime). ``--rollout gpu``
+makes the GPU-rollout mode the timed one; ``--mode fused`` times the fused loop (torchrun for N>1).
 """
 from __future__ import annotations
 
@@ -44,8 +46,9 @@ METRIC = "GPU ray.put/get GB/s + RLlib PPO samples/sec at 1/2/4/8 MI355X"
 TRAIN_BATCH = 5000     # atari-ppo.yaml, per learner
 
 
-def _cpu_budget() -> int:
-    """CPUs this job may use: cgroup quota if any, else the affinity mask."""
+def _cpu_budget(n_gpus: int = 1) -> int:
+    """CPUs this job may use: cgroup quota if any, else the affinity mask (and, where the GPU pool
+    exports OMP_NUM_THREADS as the CPU share of ONE GPU, that share times the GPUs in use)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
@@ -55,8 +58,8 @@ def _cpu_budget() -> int:
     except (OSError, ValueError):
         pass
     omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0 and n > 4 * int(omp):
-        n = min(n, int(omp))  # the GPU pool exports OMP_NUM_THREADS = the job's CPU share per GPU
+    if omp and omp.isdigit() and int(omp) > 0 and n > 4 * int(omp) * max(1, n_gpus):
+        n = min(n, int(omp) * max(1, n_gpus))
     return max(1, n)
 
 
@@ -160,7 +163,7 @@ def _runtime(args, n_gpus):
     import ray_memory_management_amd as ray
     from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
 
-    budget = _cpu_budget()
+    budget = _cpu_budget(n_gpus)
     if args.rollout == "cpu":
         w_per, envs = _rollout_layout(n_gpus, budget, args.fragment)
         if args.workers_per_learner:
@@ -213,6 +216,8 @@ def main():
     ap.add_argument("--store-gb", type=int, default=8)
     ap.add_argument("--no-putget", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused-loop reference number (N=1)")
+    ap.add_argument("--no-gpu-rollout", action="store_true",
+                    help="skip the extra runtime measurement with GPU rollout actors")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every learner on GPU 0 (use --dist-backend gloo)")
@@ -288,6 +293,34 @@ def main():
 
     if rank == 0:
         extra = {}
+        if args.mode == "runtime" and args.rollout == "cpu" and not args.no_gpu_rollout and not args.same_device:
+            # second, clearly separate runtime measurement: GPU rollout actors (device env + on-GPU
+            # inference) next to each learner, fragments through the HBM object store (hipIPC)
+            import copy
+
+            import ray_memory_management_amd as ray
+
+            a2 = copy.copy(args)
+            a2.rollout = "gpu"
+            algo2 = None
+            try:
+                algo2, info2 = _runtime(a2, n_gpus)
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    algo2.train()
+                e2 = time.perf_counter() - t0
+                extra["runtime_gpu_rollout_samples_per_s"] = round(TRAIN_BATCH * n_gpus * args.steps / e2, 1)
+                extra["runtime_gpu_rollout_ms_per_step"] = round(e2 / args.steps * 1e3, 3)
+            except Exception as ex:  # noqa: BLE001
+                print(f"[bench] gpu-rollout runtime mode failed: {ex!r}", file=sys.stderr)
+                extra["runtime_gpu_rollout_error"] = repr(ex)[:300]
+            finally:
+                if algo2 is not None:
+                    try:
+                        algo2.stop()
+                    except Exception:
+                        pass
+                ray.shutdown()
         if args.mode == "runtime" and n_gpus == 1 and world == 1 and not args.no_fused:
             try:
                 import copy
