@@ -5,6 +5,8 @@ from ray_memory_management_amd.air.config import (CheckpointConfig, FailureConfi
 from ray_memory_management_amd.air.result import Result  # noqa: F401
 from ray_memory_management_amd.air import session  # noqa: F401
 from ray_memory_management_amd.train.base_trainer import BaseTrainer, DataParallelTrainer  # noqa: F401
+from ray_memory_management_amd.train.batch_predictor import BatchPredictor  # noqa: F401
+from ray_memory_management_amd.train.predictor import Predictor  # noqa: F401
 
 
 def __getattr__(name):
@@ -14,4 +16,6 @@ def __getattr__(name):
         return importlib.import_module("ray_memory_management_amd.train.torch")
     if name == "TorchTrainer":
         return importlib.import_module("ray_memory_management_amd.train.torch").TorchTrainer
+    if name == "TorchPredictor":
+        return importlib.import_module("ray_memory_management_amd.train.predictor").TorchPredictor
     raise AttributeError(name)

@@ -180,3 +180,6 @@ class TorchCheckpoint(Checkpoint):
             model.load_state_dict(m)
             return model
         return m
+
+
+from ray_memory_management_amd.train.predictor import TorchPredictor  # noqa: E402,F401

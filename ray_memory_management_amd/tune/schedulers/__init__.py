@@ -384,3 +384,7 @@ def _resample(spec, rng):
 
 __all__ = ["TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
            "MedianStoppingRule", "PopulationBasedTraining"]
+
+
+from ray_memory_management_amd.tune.schedulers.resource_changing_scheduler import (  # noqa: E402,F401
+    DistributeResources, DistributeResourcesToTopJob, ResourceChangingScheduler)

@@ -74,6 +74,11 @@ class Trainable:
     def trial_name(self):
         return (self._trial_info or {}).get("trial_name", "default")
 
+    @property
+    def trial_resources(self) -> Dict:
+        """The resources this trial currently holds (changes under ResourceChangingScheduler)."""
+        return dict((self._trial_info or {}).get("resources") or {})
+
     def get_config(self):
         return self.config
 

@@ -126,3 +126,27 @@ def test_torch_trainer_rccl_gpu(tmp_path):
         assert res.metrics["replicas_equal"] and res.metrics["world"] == 2
     finally:
         ray.shutdown()
+
+
+def test_batch_predictor_torch(ray_start):
+    import numpy as np
+    import pandas as pd
+    import torch
+
+    from ray_memory_management_amd import data as rdata
+    from ray_memory_management_amd.train import BatchPredictor
+    from ray_memory_management_amd.train.torch import TorchCheckpoint, TorchPredictor
+
+    model = torch.nn.Linear(3, 1, bias=False)
+    with torch.no_grad():
+        model.weight.copy_(torch.tensor([[1.0, 2.0, 3.0]]))
+    ckpt = TorchCheckpoint.from_model(model)
+    df = pd.DataFrame({"a": np.arange(10.0), "b": np.ones(10), "c": np.zeros(10), "id": np.arange(10)})
+    ds = rdata.from_pandas(df)
+    bp = BatchPredictor.from_checkpoint(ckpt, TorchPredictor, model=torch.nn.Linear(3, 1, bias=False))
+    out = bp.predict(ds, feature_columns=["a", "b", "c"], keep_columns=["id"], batch_size=4,
+                     min_scoring_workers=2).to_pandas().sort_values("id")
+    preds = np.array([float(np.asarray(p).reshape(-1)[0]) for p in out["predictions"]])
+    np.testing.assert_allclose(preds, np.arange(10.0) + 2.0)
+    pipe = bp.predict_pipelined(ds, blocks_per_window=1, feature_columns=["a", "b", "c"])
+    assert pipe.count() == 10

@@ -255,3 +255,33 @@ def test_tuner_over_trainer(ray_shared, tmp_path):
                       tune_config=tune.TuneConfig(metric="loss", mode="min")).fit()
     assert grid.num_errors == 0, grid.errors
     assert grid.get_best_result().config["train_loop_config"]["lr"] == 0.1
+
+
+def test_resource_changing_scheduler_grows_lone_trial(ray_shared, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.schedulers import DistributeResources, ResourceChangingScheduler
+
+    class Grow(tune.Trainable):
+        def setup(self, config):
+            self.n = 0
+
+        def step(self):
+            import time
+
+            time.sleep(0.05)
+            self.n += 1
+            return {"score": self.n, "cpus": self.trial_resources.get("CPU", 0)}
+
+        def save_checkpoint(self, d):
+            return {"n": self.n}
+
+        def load_checkpoint(self, ck):
+            self.n = ck["n"]
+
+    sched = ResourceChangingScheduler(resources_allocation_function=DistributeResources(reserve_resources={"CPU": 1}))
+    analysis = tune.run(Grow, config={}, scheduler=sched, metric="score", mode="max",
+                        stop={"training_iteration": 6}, local_dir=str(tmp_path))
+    t = analysis.trials[0]
+    assert sched.num_reallocations >= 1
+    # the only trial grew to the cluster's free CPUs (4 - 1 reserved) and kept its progress
+    assert t.last_result["cpus"] == 3.0 and t.last_result["score"] >= 6
