@@ -11,6 +11,8 @@ def __getattr__(name):
 
     if name in ("PPO", "PPOConfig"):
         return getattr(importlib.import_module("ray_memory_management_amd.rllib.ppo"), name)
+    if name in ("DQN", "DQNConfig"):
+        return getattr(importlib.import_module("ray_memory_management_amd.rllib.algorithms.dqn"), name)
     if name in ("RolloutWorker", "WorkerSet"):
         return getattr(importlib.import_module("ray_memory_management_amd.rllib.rollout_worker"), name)
     raise AttributeError(name)

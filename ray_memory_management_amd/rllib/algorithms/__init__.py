@@ -1,11 +1,19 @@
 """Parity: reference rllib/algorithms/registry.py (get_algorithm_class)."""
+import importlib
+
 from ray_memory_management_amd.rllib.algorithms.algorithm import Algorithm  # noqa: F401
 from ray_memory_management_amd.rllib.algorithms.algorithm_config import AlgorithmConfig  # noqa: F401
 
+ALGORITHMS = {
+    "PPO": ("ppo", "PPO"),
+    "DQN": ("dqn", "DQN"),
+    "IMPALA": ("impala", "Impala"),
+    "APPO": ("appo", "APPO"),
+}
+
 
 def get_algorithm_class(name: str):
-    if name == "PPO":
-        from ray_memory_management_amd.rllib.algorithms.ppo import PPO
-
-        return PPO
-    raise ValueError(f"Unknown algorithm {name!r}")
+    if name not in ALGORITHMS:
+        raise ValueError(f"Unknown algorithm {name!r}")
+    mod, cls = ALGORITHMS[name]
+    return getattr(importlib.import_module(f"ray_memory_management_amd.rllib.algorithms.{mod}"), cls)

@@ -94,9 +94,12 @@ class Algorithm(Trainable):
         t0 = time.time()
         c = self.algo_config
         results: Dict[str, Any] = {}
+        ts0 = self._counters["num_env_steps_sampled"]
         while True:
             results = self.training_step()
-            if not c.min_time_s_per_iteration or time.time() - t0 >= c.min_time_s_per_iteration:
+            time_ok = not c.min_time_s_per_iteration or time.time() - t0 >= c.min_time_s_per_iteration
+            steps_ok = self._counters["num_env_steps_sampled"] - ts0 >= (c.min_sample_timesteps_per_iteration or 0)
+            if time_ok and steps_ok:
                 break
         episodes = self.workers.collect_metrics()
         for r, ln in episodes:

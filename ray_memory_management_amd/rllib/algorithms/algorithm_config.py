@@ -60,6 +60,8 @@ class AlgorithmConfig:
         self.learner_collective_backend = "auto"  # nccl (=RCCL) for GPU learners, gloo on CPU
         # rollout workers ship raw fragments; GAE + advantage standardisation run on the learner GPU
         self.postprocess_on_learner = False
+        # rollout-side policy class (class or dotted import path); None = the PG TorchPolicy
+        self.policy_class = None
 
     # ---- builder methods (each returns self)
     def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None,
@@ -187,7 +189,8 @@ class AlgorithmConfig:
         d = {k: copy.deepcopy(v) for k, v in self.__dict__.items() if k != "algo_class"}
         d["framework"] = d.pop("framework_str")
         d["callbacks"] = d.pop("callbacks_class")
-        d["lambda"] = d.get("lambda_", d.get("lambda"))
+        if d.get("lambda_", d.get("lambda")) is not None:
+            d["lambda"] = d.get("lambda_", d.get("lambda"))
         return d
 
     def update_from_dict(self, d: Dict[str, Any]) -> "AlgorithmConfig":

@@ -46,7 +46,13 @@ class RolloutWorker:
             vcfg.setdefault("seed", int(base_seed) * 1000 + worker_index)
         self.vec_env = None if env_creator is not None else make_vector_env(env, n_envs, vcfg)
         self.env = self.vec_env if self.vec_env is not None else VectorEnv(mk, n_envs)
-        self.policy = TorchPolicy(self.env.observation_space, self.env.action_space, self.config, device="cpu")
+        pcls = self.config.get("policy_class") or TorchPolicy
+        if isinstance(pcls, str):
+            import importlib
+
+            mod, _, name = pcls.rpartition(".")
+            pcls = getattr(importlib.import_module(mod), name)
+        self.policy = pcls(self.env.observation_space, self.env.action_space, self.config, device="cpu")
         if base_seed is not None:
             torch.manual_seed(int(base_seed) + worker_index)
         self._obs = self.env.vector_reset()
@@ -63,11 +69,13 @@ class RolloutWorker:
         T = int(self.config.get("rollout_fragment_length", 200))
         n = self.env.num_envs
         obs_buf, act_buf, logp_buf, vf_buf, logits_buf, rew_buf, done_buf = [], [], [], [], [], [], []
+        nobs_buf = []
         eps_ids = []
         for _ in range(T):
             obs = np.stack([np.asarray(o) for o in self._obs])
             a, _, extra = self.policy.compute_actions(obs, explore=self.config.get("explore", True))
             nobs, rew, done, _info = self.env.vector_step(list(a))
+            nobs_buf.append(np.stack([np.asarray(o) for o in nobs]))  # before resets: terminal obs kept
             obs_buf.append(obs)
             act_buf.append(a)
             logp_buf.append(extra[SampleBatch.ACTION_LOGP])
@@ -99,7 +107,8 @@ class RolloutWorker:
             SampleBatch.OBS: flat(obs_buf), SampleBatch.ACTIONS: flat(act_buf),
             SampleBatch.ACTION_LOGP: flat(logp_buf).astype(np.float32), SampleBatch.VF_PREDS: flat(vf),
             SampleBatch.ACTION_DIST_INPUTS: flat(logits_buf).astype(np.float32), SampleBatch.REWARDS: flat(rew),
-            SampleBatch.DONES: flat(dn), SampleBatch.ADVANTAGES: flat(adv).astype(np.float32),
+            SampleBatch.DONES: flat(dn), SampleBatch.NEXT_OBS: flat(nobs_buf),
+            SampleBatch.ADVANTAGES: flat(adv).astype(np.float32),
             SampleBatch.VALUE_TARGETS: flat(ret).astype(np.float32),
         })
         self._sample_time += time.perf_counter() - t0
