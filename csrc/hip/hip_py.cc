@@ -203,7 +203,14 @@ PYBIND11_MODULE(_hip, m) {
     ingest_gae(P<const float>(raw), P<const float>(boot), P<const IngestBlock>(blocks), nblocks, A, gamma, lam,
                P<float>(cols), P<double>(stats), S(stream));
   });
-  m.def("ingest_block_bytes", [] { return int(sizeof(IngestBlock)); });
+  m.def("vtrace", [](uint64_t blogp, uint64_t tlogp, uint64_t rew, uint64_t val, uint64_t done, uint64_t boot,
+                     int64_t T, int64_t B, float gamma, float clip_rho, float clip_pg_rho, float lam, uint64_t vs,
+                     uint64_t pg, uint64_t stream) {
+    vtrace(P<const float>(blogp), P<const float>(tlogp), P<const float>(rew), P<const float>(val),
+           P<const float>(done), P<const float>(boot), T, B, gamma, clip_rho, clip_pg_rho, lam, P<float>(vs),
+           P<float>(pg), S(stream));
+  });
+  m.def("ingest_block_bytes",[] { return int(sizeof(IngestBlock)); });
   m.def("standardize_col", [](uint64_t cols, int64_t N, int C, int col, uint64_t stats, uint64_t stream) {
     standardize_col(P<float>(cols), N, C, col, P<const double>(stats), S(stream));
   });

@@ -165,6 +165,11 @@ struct IngestBlock {
 void ingest_gae(const float* raw, const float* boot, const IngestBlock* blocks_dev, int nblocks, int A, float gamma,
                 float lam, float* cols, double* stats, hipStream_t stream);
 void standardize_col(float* cols, int64_t N, int C, int col, const double* stats, hipStream_t stream);
+// K18: V-trace targets over time-major [T, B] columns (vtrace_kernels.hip). clip_rho /
+// clip_pg_rho = +inf disables the clip.
+void vtrace(const float* blogp, const float* tlogp, const float* rew, const float* val, const float* done,
+            const float* boot, int64_t T, int64_t B, float gamma, float clip_rho, float clip_pg_rho, float lam,
+            float* vs, float* pg, hipStream_t stream);
 // Page-locked DMA out of a shared-memory object-store segment: chunks of the registered segment
 // are hipHostRegister'ed on first use. Returns the bytes newly registered by this call.
 void host_register_segment(uintptr_t base, uint64_t size);

@@ -13,7 +13,7 @@ import torch
 from ray_memory_management_amd._native import hip_ext, require_hip
 
 __all__ = [
-    "multi_copy", "pack_tensors", "unpack_tensors", "concat", "gather_rows", "gae",
+    "multi_copy", "pack_tensors", "unpack_tensors", "concat", "gather_rows", "gae", "vtrace",
     "compress", "decompress", "ppo_loss", "hip_available",
 ]
 
@@ -195,6 +195,54 @@ def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, last_v
     h.gae(r.data_ptr(), v.data_ptr(), d.data_ptr(), lv.data_ptr(), adv.data_ptr(), ret.data_ptr(),
           T, B, float(gamma), float(lam), _stream(r))
     return adv, ret
+
+
+def vtrace_reference(behaviour_logp, target_logp, rewards, values, dones, bootstrap, gamma: float,
+                     clip_rho: float = 1.0, clip_pg_rho: float = 1.0, lam: float = 1.0):
+    """Plain fp32 torch V-trace over time-major [T, B] tensors (also the CPU path). Parity:
+    reference rllib/algorithms/impala/vtrace_torch.py:from_importance_weights."""
+    f = lambda t: t.to(torch.float32)  # noqa: E731
+    rho = torch.exp(f(target_logp) - f(behaviour_logp))
+    disc = gamma * (1.0 - f(dones))
+    v = f(values)
+    boot = f(bootstrap).reshape(-1)
+    v_tp1 = torch.cat([v[1:], boot.unsqueeze(0)], 0)
+    crho = torch.clamp(rho, max=clip_rho) if clip_rho is not None else rho
+    deltas = crho * (f(rewards) + disc * v_tp1 - v)
+    cs = lam * torch.clamp(rho, max=1.0)
+    acc = torch.zeros_like(boot)
+    out = torch.empty_like(v)
+    for t in range(v.shape[0] - 1, -1, -1):
+        acc = deltas[t] + disc[t] * cs[t] * acc
+        out[t] = acc
+    vs = out + v
+    vs_tp1 = torch.cat([vs[1:], boot.unsqueeze(0)], 0)
+    prho = torch.clamp(rho, max=clip_pg_rho) if clip_pg_rho is not None else rho
+    return vs, prho * (f(rewards) + disc * vs_tp1 - v)
+
+
+def vtrace(behaviour_logp, target_logp, rewards, values, dones, bootstrap, gamma: float = 0.99,
+           clip_rho: float = 1.0, clip_pg_rho: float = 1.0, lam: float = 1.0):
+    """V-trace targets (vs, pg_advantages) over time-major [T, B] tensors; no gradient flows
+    through them. CUDA tensors run the K18 kernel (one launch for the whole recursion)."""
+    if rewards.device.type != "cuda":
+        return vtrace_reference(behaviour_logp, target_logp, rewards, values, dones, bootstrap, gamma, clip_rho,
+                                clip_pg_rho, lam)
+    h = require_hip()
+    T, B = rewards.shape
+    f = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
+    bl, tl, r, v, d, bt = (f(behaviour_logp), f(target_logp), f(rewards), f(values), f(dones),
+                           f(bootstrap).reshape(B))
+    for x in (bl, tl, v, d):
+        if tuple(x.shape) != (T, B) or x.device != r.device:
+            raise ValueError("vtrace: all [T, B] inputs must match rewards' shape and device")
+    vs = torch.empty((T, B), dtype=torch.float32, device=r.device)
+    pg = torch.empty_like(vs)
+    inf = float("inf")
+    h.vtrace(bl.data_ptr(), tl.data_ptr(), r.data_ptr(), v.data_ptr(), d.data_ptr(), bt.data_ptr(), T, B,
+             float(gamma), inf if clip_rho is None else float(clip_rho),
+             inf if clip_pg_rho is None else float(clip_pg_rho), float(lam), vs.data_ptr(), pg.data_ptr(), _stream(r))
+    return vs, pg
 
 
 _BITS = {torch.bfloat16: 16, torch.float16: 16, torch.float32: 32, torch.int16: 16, torch.int32: 32}

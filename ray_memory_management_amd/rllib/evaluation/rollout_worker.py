@@ -189,6 +189,62 @@ class RolloutWorker:
         self._sample_time += time.perf_counter() - t0
         return out
 
+    def sample_time_major(self) -> Dict[str, Any]:
+        """One unroll for an off-policy (V-trace) learner: time-major [T, n] columns + each env's
+        observation after the last step (the learner bootstraps from its own value of it).
+        Parity: reference rllib/algorithms/impala (rollout_fragment_length unrolls, make_time_major).
+        Returns {"T", "n", "obs", "actions", "action_logp", "action_dist_inputs", "rewards",
+        "dones", "last_obs"}; no GAE, no value head on the worker."""
+        import torch
+
+        t0 = time.perf_counter()
+        T = int(self.config.get("rollout_fragment_length", 50))
+        n = self.env.num_envs
+        explore = self.config.get("explore", True)
+        obs0 = np.asarray(self._obs) if self.vec_env is not None else np.stack([np.asarray(o) for o in self._obs])
+        A = getattr(self.env.action_space, "n", 1)
+        out = {"obs": np.empty((T, n) + obs0.shape[1:], dtype=obs0.dtype), "actions": np.empty((T, n), np.int64),
+               "action_logp": np.empty((T, n), np.float32), "action_dist_inputs": np.empty((T, n, A), np.float32),
+               "rewards": np.empty((T, n), np.float32), "dones": np.empty((T, n), np.float32)}
+        model = self.policy.model
+        obs = obs0
+        with torch.inference_mode():
+            for t in range(T):
+                out["obs"][t] = obs
+                logits, _ = model(torch.from_numpy(np.ascontiguousarray(obs)))
+                logits = logits.float()
+                if explore:  # Gumbel-max sampling of the categorical policy
+                    g = -torch.log(-torch.log(torch.rand_like(logits).clamp_(1e-10, 1.0)))
+                    a = torch.argmax(logits + g, dim=-1)
+                else:
+                    a = torch.argmax(logits, dim=-1)
+                out["action_dist_inputs"][t] = logits.numpy()
+                out["action_logp"][t] = torch.log_softmax(logits, -1).gather(1, a.unsqueeze(1)).squeeze(1).numpy()
+                an = a.numpy()
+                out["actions"][t] = an
+                if self.vec_env is not None:
+                    obs, rew, done = self.env.vector_step(an)
+                    rew, done = np.asarray(rew, np.float32), np.asarray(done, bool)
+                else:
+                    nobs, rew, done, _ = self.env.vector_step(list(an))
+                    rew, done = np.asarray(rew, np.float32), np.asarray(done, bool)
+                    for i in np.nonzero(done)[0]:
+                        nobs[i] = self.env.reset_at(i)
+                    obs = np.stack([np.asarray(o) for o in nobs])
+                out["rewards"][t] = rew
+                out["dones"][t] = done
+                self._ep_reward += rew
+                self._ep_len += 1
+                for i in np.nonzero(done)[0]:
+                    self._completed.append((float(self._ep_reward[i]), int(self._ep_len[i])))
+                    self._ep_reward[i] = 0.0
+                    self._ep_len[i] = 0
+        self._obs = obs if self.vec_env is not None else list(obs)
+        self.policy.global_timestep += T * n
+        out.update(T=T, n=n, last_obs=np.array(obs, copy=True))
+        self._sample_time += time.perf_counter() - t0
+        return out
+
     def sample_with_count(self):
         b = self.sample()
         return b, b.count
