@@ -41,8 +41,7 @@ class ReplayBuffer:
         if self.device and self.device != "cpu":
             import torch
 
-            dt = torch.as_tensor(np.asarray(v[:1])).dtype if not hasattr(v, "dtype") or not hasattr(v, "device") \
-                else v.dtype
+            dt = v.dtype if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v[:1])).dtype
             return torch.empty(shape, dtype=dt, device=self.device)
         return np.empty(shape, dtype=np.asarray(v[:1]).dtype)
 
@@ -50,8 +49,8 @@ class ReplayBuffer:
         if self.device and self.device != "cpu":
             import torch
 
-            dst[start:start + len(v)] = torch.as_tensor(np.asarray(v) if not hasattr(v, "device") else v).to(
-                self.device, non_blocking=True)
+            src = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            dst[start:start + len(v)] = src.to(self.device, non_blocking=True)
         else:
             dst[start:start + len(v)] = np.asarray(v)
 
