@@ -1472,10 +1472,20 @@ def main():
     os.makedirs(os.path.join(args.session_dir, "sockets"), exist_ok=True)
     signal.signal(signal.SIGTERM, lambda *a: sys.exit(0))
     h = Head(args)
+    prof_path = os.environ.get("RMM_HEAD_PROFILE")  # control-plane profiling: cProfile of the loop
+    prof = None
+    if prof_path:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     try:
         h.serve()
     finally:
         h.running = False
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(prof_path)
 
 
 if __name__ == "__main__":

@@ -724,7 +724,49 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
         global_worker = w
         _set_worker(w)
         atexit.register(shutdown)
+        if include_dashboard and _head_proc is not None:
+            _start_dashboard(sess, kwargs.get("dashboard_host", "127.0.0.1"), int(kwargs.get("dashboard_port", 8265)))
         return RayContext()
+
+
+_dashboard_proc = None
+_dashboard_url = None
+
+
+def _start_dashboard(sess: str, host: str, port: int):
+    """Launch the dashboard process (dashboard/head.py) next to the head; it connects as a client
+    driver. Parity: reference ray.init(include_dashboard=True, dashboard_host, dashboard_port)."""
+    global _dashboard_proc, _dashboard_url
+    ready = os.path.join(sess, "dashboard.json")
+    env = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    log = open(os.path.join(sess, "logs", "dashboard.log"), "ab")
+    _dashboard_proc = subprocess.Popen(
+        [sys.executable, "-u", "-m", "ray_memory_management_amd.dashboard", "--address", f"rmm://{sess}",
+         "--host", host, "--port", str(port), "--ready-file", ready],
+        env=env, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, start_new_session=True)
+    log.close()
+    t0 = time.time()
+    while not os.path.exists(ready):
+        if _dashboard_proc.poll() is not None or time.time() - t0 > 60:
+            logger.warning("dashboard failed to start; see %s", os.path.join(sess, "logs", "dashboard.log"))
+            _dashboard_proc = None
+            return
+        time.sleep(0.01)
+    _dashboard_url = json.load(open(ready))["url"]
+
+
+def _stop_dashboard():
+    global _dashboard_proc, _dashboard_url
+    p, _dashboard_proc, _dashboard_url = _dashboard_proc, None, None
+    if p is not None and p.poll() is None:
+        p.terminate()
+        try:
+            p.wait(timeout=5)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
 
 
 def _find_session(address):
@@ -750,6 +792,7 @@ def shutdown(_exiting_interpreter: bool = False):
         from ray_memory_management_amd._private import gpu_object_store as gos
 
         gos.shutdown_process_store(w)
+        _stop_dashboard()
         if _head_proc is not None:
             try:
                 w.send((P.SHUTDOWN,))
@@ -769,8 +812,10 @@ def shutdown(_exiting_interpreter: bool = False):
 
 class RayContext(dict):
     def __init__(self):
-        super().__init__(session_dir=_session_dir, address=f"rmm://{_session_dir}" if _session_dir else None)
+        super().__init__(session_dir=_session_dir, address=f"rmm://{_session_dir}" if _session_dir else None,
+                         dashboard_url=_dashboard_url)
         self.address_info = dict(self)
+        self.dashboard_url = _dashboard_url
 
     def __enter__(self):
         return self

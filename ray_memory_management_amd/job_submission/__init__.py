@@ -164,8 +164,63 @@ def _to_info(sid, d) -> JobInfo:
                    metadata=d.get("metadata"), runtime_env=d.get("runtime_env"), driver_exit_code=d.get("exit"))
 
 
+class _HttpJobClient:
+    """REST client for the dashboard's job module (reference dashboard/modules/job/sdk.py talks
+    HTTP to /api/jobs/)."""
+
+    def __init__(self, url: str):
+        self.url = url.rstrip("/")
+
+    def _call(self, method, path, body=None):
+        import json
+        import urllib.error
+        import urllib.request
+
+        data = json.dumps(body).encode() if body is not None else None
+        req = urllib.request.Request(self.url + path, data=data, method=method,
+                                     headers={"Content-Type": "application/json"})
+        try:
+            with urllib.request.urlopen(req, timeout=60) as r:
+                return json.loads(r.read())
+        except urllib.error.HTTPError as e:
+            msg = e.read().decode(errors="replace")
+            raise RuntimeError(f"{method} {path} -> {e.code}: {msg}") from None
+
+    def submit(self, entrypoint, sid, runtime_env, metadata):
+        return self._call("POST", "/api/jobs/", {"entrypoint": entrypoint, "submission_id": sid,
+                                                  "runtime_env": runtime_env, "metadata": metadata})["submission_id"]
+
+    def stop(self, sid):
+        return self._call("POST", f"/api/jobs/{sid}/stop")["stopped"]
+
+    def delete(self, sid):
+        return self._call("DELETE", f"/api/jobs/{sid}")["deleted"]
+
+    def info(self, sid):
+        try:
+            d = self._call("GET", f"/api/jobs/{sid}")
+        except RuntimeError:
+            return None
+        d["exit"] = d.pop("driver_exit_code", None)
+        return d
+
+    def list(self):
+        out = {}
+        for d in self._call("GET", "/api/jobs/"):
+            d["exit"] = d.pop("driver_exit_code", None)
+            out[d["submission_id"]] = d
+        return out
+
+    def logs(self, sid, offset=0):
+        return self._call("GET", f"/api/jobs/{sid}/logs?offset={int(offset)}")["logs"]
+
+
 class JobSubmissionClient:
     def __init__(self, address: Optional[str] = None, create_cluster_if_needed: bool = False, **kw):
+        if address and address.startswith(("http://", "https://")):
+            self._http = _HttpJobClient(address)
+            return
+        self._http = None
         if not ray.is_initialized():
             ray.init(address=address or "auto") if not create_cluster_if_needed else ray.init(address=address)
         from ray_memory_management_amd._private import worker as _w
@@ -176,41 +231,46 @@ class JobSubmissionClient:
             self._m = ray.remote(_JobManager).options(name=_MANAGER, namespace=_NS, lifetime="detached", num_cpus=0,
                                                       max_concurrency=64, get_if_exists=True).remote(_w._session_dir)
 
+    def _do(self, name, *args):
+        if self._http is not None:
+            return getattr(self._http, name)(*args)
+        return ray.get(getattr(self._m, name).remote(*args))
+
     def submit_job(self, *, entrypoint: str, job_id: Optional[str] = None, submission_id: Optional[str] = None,
                    runtime_env: Optional[Dict[str, Any]] = None, metadata: Optional[Dict[str, str]] = None,
                    **kw) -> str:
-        return ray.get(self._m.submit.remote(entrypoint, submission_id or job_id, runtime_env, metadata))
+        return self._do("submit", entrypoint, submission_id or job_id, runtime_env, metadata)
 
     def stop_job(self, job_id: str) -> bool:
-        return ray.get(self._m.stop.remote(job_id))
+        return self._do("stop", job_id)
 
     def delete_job(self, job_id: str) -> bool:
-        return ray.get(self._m.delete.remote(job_id))
+        return self._do("delete", job_id)
 
     def get_job_info(self, job_id: str) -> JobInfo:
-        d = ray.get(self._m.info.remote(job_id))
+        d = self._do("info", job_id)
         if d is None:
             raise RuntimeError(f"Job {job_id} does not exist")
         return _to_info(job_id, d)
 
     def list_jobs(self) -> List[JobInfo]:
-        return [_to_info(s, d) for s, d in ray.get(self._m.list.remote()).items()]
+        return [_to_info(s, d) for s, d in self._do("list").items()]
 
     def get_job_status(self, job_id: str) -> JobStatus:
         return self.get_job_info(job_id).status
 
-    def get_job_logs(self, job_id: str) -> str:
-        return ray.get(self._m.logs.remote(job_id))
+    def get_job_logs(self, job_id: str, offset: int = 0) -> str:
+        return self._do("logs", job_id, offset)
 
     def tail_job_logs(self, job_id: str, poll_s: float = 0.2) -> Iterator[str]:
         off = 0
         while True:
-            chunk = ray.get(self._m.logs.remote(job_id, off))
+            chunk = self._do("logs", job_id, off)
             if chunk:
                 off += len(chunk.encode())
                 yield chunk
             if self.get_job_status(job_id).is_terminal():
-                rest = ray.get(self._m.logs.remote(job_id, off))
+                rest = self._do("logs", job_id, off)
                 if rest:
                     yield rest
                 return

@@ -38,12 +38,17 @@ def cmd_start(a):
         return 1
     res = json.loads(a.resources) if a.resources else None
     ctx = ray.init(num_cpus=a.num_cpus, num_gpus=a.num_gpus, resources=res,
-                   object_store_memory=a.object_store_memory, _persistent=True)
+                   object_store_memory=a.object_store_memory, _persistent=True,
+                   include_dashboard=a.include_dashboard, dashboard_host=a.dashboard_host,
+                   dashboard_port=a.dashboard_port)
     sess = ctx["session_dir"]
     _w._head_proc = None  # detach: the head keeps running after this process exits
+    _w._dashboard_proc = None  # the dashboard exits with the head
     ray.shutdown()
     print(f"Started head. Address: rmm://{sess}\n  connect with ray.init(address='auto') or "
           f"RMM_ADDRESS=rmm://{sess}\n  stop with `rmm stop`")
+    if ctx.dashboard_url:
+        print(f"  dashboard: {ctx.dashboard_url}")
     return 0
 
 
@@ -226,6 +231,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--head", action="store_true")
     s.add_argument("--num-cpus", type=int, default=None)
     s.add_argument("--num-gpus", type=int, default=None)
+    s.add_argument("--include-dashboard", action="store_true")
+    s.add_argument("--dashboard-host", default="127.0.0.1")
+    s.add_argument("--dashboard-port", type=int, default=8265)
     s.add_argument("--resources", default=None, help="JSON dict of custom resources")
     s.add_argument("--object-store-memory", type=int, default=None)
     s.set_defaults(fn=cmd_start)

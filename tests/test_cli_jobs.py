@@ -22,9 +22,11 @@ def _cli(*args, env=None, timeout=120):
 
 @pytest.fixture(scope="module")
 def head():
-    r = _cli("start", "--head", "--num-cpus", "2", "--object-store-memory", str(128 << 20))
+    r = _cli("start", "--head", "--num-cpus", "2", "--object-store-memory", str(128 << 20), "--include-dashboard",
+             "--dashboard-port", "0")
     assert r.returncode == 0, r.stderr + r.stdout
     addr = [w for w in r.stdout.split() if w.startswith("rmm://")][0]
+    assert any(w.startswith("http://") for w in r.stdout.split()), r.stdout
     yield addr
     r = _cli("stop", "--address", addr)
     assert r.returncode == 0, r.stderr
@@ -78,3 +80,25 @@ def test_job_submission_lifecycle(head, tmp_path):
         assert bad not in {j.submission_id for j in c.list_jobs()}
     finally:
         ray.shutdown()
+
+
+def test_persistent_head_dashboard_and_http_job_cli(head, tmp_path):
+    """`rmm start --include-dashboard` leaves a dashboard serving; `rmm job submit --address http://`
+    goes through its REST job module (reference: `ray job submit --address http://...:8265`)."""
+    import urllib.request
+
+    url = _dashboard_url(head)
+    with urllib.request.urlopen(url + "/api/gcs_healthz", timeout=30) as resp:
+        assert json.loads(resp.read()) == "success"
+    script = tmp_path / "hjob.py"
+    script.write_text("print('over http', 6 * 7)\n")
+    r = _cli("job", "submit", "--address", url, "--", sys.executable, str(script))
+    assert r.returncode == 0 and "over http 42" in r.stdout and "SUCCEEDED" in r.stdout, r.stdout + r.stderr
+    r = _cli("job", "list", "--address", url)
+    assert r.returncode == 0 and "SUCCEEDED" in r.stdout
+
+
+def _dashboard_url(addr):
+    sess = addr[len("rmm://"):]
+    with open(os.path.join(sess, "dashboard.json")) as f:
+        return json.load(f)["url"]

