@@ -90,7 +90,8 @@ class Conn:
 
 class WorkerRec:
     __slots__ = ("worker_id", "pid", "proc", "conn", "node", "env_key", "state", "task", "actor_id",
-                 "fns", "gpu_key", "blocked", "start_time", "tasks_run", "lease", "idle_since", "calls")
+                 "fns", "gpu_key", "blocked", "start_time", "tasks_run", "lease", "idle_since", "calls",
+                 "direct_addr")
 
     def __init__(self, worker_id, proc, node, env_key, gpu_key):
         self.worker_id = worker_id
@@ -110,6 +111,7 @@ class WorkerRec:
         self.lease = None
         self.idle_since = time.time()
         self.calls = collections.Counter()
+        self.direct_addr = None  # the worker's direct-task socket (leased task submission)
 
 
 class TaskRec:
@@ -233,6 +235,8 @@ class Head:
         self.starting: Dict[tuple, int] = collections.Counter()
         self.tasks: Dict[bytes, TaskRec] = {}
         self.finished_tasks = collections.OrderedDict()
+        self.direct_tasks = collections.deque(maxlen=10000)  # rows of directly submitted tasks
+        self.lease_stats = collections.Counter()
         self.task_keys: Dict[int, bytes] = {}
         self.key_counter = 0
         self.dispatch_q: Dict[int, collections.deque] = collections.defaultdict(collections.deque)
@@ -297,6 +301,18 @@ class Head:
         self.sched.add_node(node_id, resources)
         self.nodes[node_id] = {"node_id": node_id, "resources": resources, "alive": True,
                                "start_time": time.time(), "is_head": head}
+        if not head:
+            self._broadcast_nodes()
+
+    def _multi_node(self) -> bool:
+        return sum(1 for n in self.nodes.values() if n["alive"]) > 1
+
+    def _broadcast_nodes(self):
+        """Owners submit tasks directly over leases only on a single-node cluster (no object can be
+        lost with a node, so the head need not hold every task's lineage up front)."""
+        for c in list(self.conns.values()):
+            if c.kind is not None:
+                self._send_nb(c, (P.NODES_CHANGED, self._multi_node()))
 
     def _remove_node(self, node_id):
         if node_id not in self.nodes or node_id == self.head_node:
@@ -457,6 +473,14 @@ class Head:
             self._ref_deltas(m[1])
         elif t == P.SUBMIT_TASK:
             self._submit_task(c, m[1])
+        elif t == P.DIRECT_DONE:
+            self._direct_done(m[1])
+        elif t == P.LEASE_REQUEST:
+            self._lease_request(c, m[1], m[2])
+        elif t == P.LEASE_RETURN:
+            self._lease_return(m[1], m[2])
+        elif t == P.FN_EXPORT:
+            self.fn_table[m[1]] = m[2]
         elif t == P.TASK_DONE:
             self._task_done(c, m[1], m[2], m[3], m[4] if len(m) > 4 else None)
         elif t == P.REGISTER:
@@ -549,6 +573,8 @@ class Head:
     def _register(self, c: Conn, kind, info):
         c.kind = kind
         c.pid = info.get("pid")
+        if self._multi_node():
+            self._send_nb(c, (P.NODES_CHANGED, True))
         if kind == "driver":
             job_id = info.get("job_id")
             c.job_id = job_id
@@ -567,6 +593,7 @@ class Head:
             return
         w.conn = c
         c.worker = w
+        w.direct_addr = info.get("direct_addr")
         w.state = "IDLE"
         w.idle_since = time.time()
         self.starting[(w.node, w.env_key, w.gpu_key)] -= 1
@@ -647,6 +674,7 @@ class Head:
             c.sock.close()
         except OSError:
             pass
+        self._release_owner_leases(c)
         if c.kind == "driver":
             self._driver_exit(c)
         elif c.worker is not None:
@@ -690,6 +718,10 @@ class Head:
         if w.task is not None:
             t = self.tasks.get(w.task)
             w.task = None
+            if t is not None and t.spec.get("_lease") is not None:
+                self.tasks.pop(t.spec["task_id"], None)
+                self._release_task_resources(t)
+                t = None
             if t is not None:
                 self._release_task_resources(t)
                 if t.cancelled:
@@ -800,6 +832,55 @@ class Head:
         for r in t.arg_refs:
             self.refcounts[r] += 1
         self._enqueue(t)
+
+    # ------------------------------------------------------------------ worker leases
+    def _lease_request(self, c: Conn, req_id, ls):
+        """Reference node_manager.cc HandleRequestWorkerLease: the lease is scheduled like a task
+        (resources, worker pool keyed by runtime env / GPUs) and, once placed, the owner gets the
+        worker's direct address instead of the worker getting an EXECUTE."""
+        spec = {"task_id": ls["lease_id"], "name": "lease", "resources": ls["resources"], "strategy": None,
+                "env_key": ls.get("env_key", ""), "runtime_env": ls.get("runtime_env"), "fn_id": None,
+                "arg_refs": [], "max_retries": 0, "num_returns": 0, "_lease": req_id}
+        t = TaskRec(spec, c)
+        self.tasks[spec["task_id"]] = t
+        self.lease_stats["requested"] += 1
+        self._enqueue(t)
+
+    def _lease_return(self, lease_id, kill: bool):
+        t = self.tasks.pop(lease_id, None)
+        if t is None or t.spec.get("_lease") is None:
+            return
+        self.lease_stats["returned"] += 1
+        if t.state == PENDING:
+            key = t.spec.get("_key")
+            if key is not None and self.sched.cancel(key):
+                self.task_keys.pop(key, None)
+            for q in self.dispatch_q.values():
+                if t in q:
+                    q.remove(t)
+                    self._release_task_resources(t)
+            return
+        self._release_task_resources(t)
+        w = t.worker
+        if w is not None and w.task == lease_id:
+            w.task = None
+            w.tasks_run += 1
+            if kill:
+                self._kill_worker(w)
+            else:
+                self._make_idle(w)
+
+    def _release_owner_leases(self, c: Conn):
+        for lid in [tid for tid, t in self.tasks.items() if t.owner_conn is c and t.spec.get("_lease") is not None]:
+            self._lease_return(lid, False)
+
+    def _direct_done(self, items):
+        """Completion records of directly submitted tasks: lineage for reconstruction + the state
+        API / timeline row (reference: owner-side task events reported to GCS)."""
+        for lineage, rec in items:
+            if lineage is not None:
+                self.recovery.task_finished(lineage, rec[3])
+        self.direct_tasks.extend(rec for _, rec in items)
 
     def _resubmit(self, spec):
         """Re-run a finished task to recompute its lost returns (lineage reconstruction)."""
@@ -919,6 +1000,17 @@ class Head:
                 self._start_worker(node, (env_key, gkey), gpu_ids if gpu_ids else None,
                                    runtime_env=spec.get("runtime_env"))
             return False
+        if spec.get("_lease") is not None:  # a worker lease: hand the worker to the owner
+            w.state = "BUSY"
+            w.task = spec["task_id"]
+            t.worker = w
+            t.state = RUNNING
+            t.start_time = time.time()
+            self.lease_stats["granted"] += 1
+            multi = self._multi_node()
+            self._reply(t.owner_conn, spec["_lease"], ("granted", spec["task_id"], w.direct_addr, w.worker_id,
+                                                      gpu_ids, node, multi))
+            return True
         if not self._pin_task_args(t):
             pool = self.idle.setdefault(key, [])
             pool.append(w)
@@ -1291,11 +1383,20 @@ class Head:
             out = []
             for coll in (self.tasks, self.finished_tasks):
                 for tid, t in coll.items():
+                    if t.spec.get("_lease") is not None:
+                        continue
                     out.append({"task_id": tid.hex(), "name": t.spec.get("name"), "state": t.state,
                                 "func_or_class_name": t.spec.get("name"), "node_id": t.node, "attempt": t.attempt,
                                 "start_time": t.start_time, "end_time": t.end_time, "required_resources": t.spec["resources"],
                                 "worker_pid": t.worker.pid if t.worker else None})
+            for tid, name, ok, node, attempt, t0, t1, res in self.direct_tasks:
+                out.append({"task_id": tid.hex(), "name": name, "state": FINISHED if ok else FAILED,
+                            "func_or_class_name": name, "node_id": node, "attempt": attempt, "start_time": t0,
+                            "end_time": t1, "required_resources": res, "worker_pid": None})
             return out
+        if what == "leases":
+            return {**dict(self.lease_stats), "held": sum(1 for t in self.tasks.values()
+                                                          if t.spec.get("_lease") is not None and t.state == RUNNING)}
         if what == "workers":
             return [{"worker_id": w.worker_id.hex(), "pid": w.pid, "state": w.state, "node_id": w.node,
                      "actor_id": w.actor_id.hex() if w.actor_id else None, "tasks_run": w.tasks_run}
@@ -1319,8 +1420,9 @@ class Head:
         if what == "timeline":
             return list(self.events)
         if what == "summary":
-            return {"pending_tasks": sum(1 for t in self.tasks.values() if t.state == PENDING),
-                    "running_tasks": sum(1 for t in self.tasks.values() if t.state == RUNNING),
+            real = [t for t in self.tasks.values() if t.spec.get("_lease") is None]
+            return {"pending_tasks": sum(1 for t in real if t.state == PENDING),
+                    "running_tasks": sum(1 for t in real if t.state == RUNNING),
                     "workers": len(self.workers), "actors": len(self.actors),
                     "infeasible": len(self.sched.infeasible_tasks())}
         if what == "memory":

@@ -48,6 +48,10 @@ REMOVE_NODE = 29
 ACTOR_EXITING = 30
 GPU_OBJECT = 31
 GLOBAL_GC = 32
+LEASE_REQUEST = 33   # owner asks for a worker lease (direct task submission)
+LEASE_RETURN = 34    # owner hands a lease back (optionally: kill the worker)
+DIRECT_DONE = 35     # batched completion records of directly submitted tasks (lineage + state)
+FN_EXPORT = 36       # function blob for the head's table (first direct submission of a function)
 
 # ---- head -> worker
 EXECUTE = 101
@@ -57,10 +61,12 @@ CANCEL_TASK = 104
 REPLY = 105
 FREE_GPU = 106
 TRIGGER_GC = 107
+NODES_CHANGED = 108  # (NODES_CHANGED, multi_node: bool)
 
 # ---- caller -> actor (direct transport)
 ACTOR_TASK = 201
 ACTOR_HELLO = 202
+DIRECT_TASK = 203    # owner -> leased worker: (DIRECT_TASK, spec, fn_blob, info)
 
 
 def dumps(obj) -> bytes:

@@ -91,8 +91,19 @@ def _rebuild_cuda_tensor(cpu_tensor, device_index, requires_grad):
     return t
 
 
+_PRIMITIVES = (int, float, bool, str, type(None))
+
+
+def _is_primitive(v) -> bool:
+    """Values the C pickler handles exactly like cloudpickle (no refs, no buffers, no code)."""
+    t = type(v)
+    return t in _PRIMITIVES or (t is bytes and len(v) <= 4096)
+
+
 def serialize(value: Any) -> Tuple[bytes, List[pickle.PickleBuffer], List[bytes]]:
     """Returns (pickle_bytes, out_of_band_buffers, contained_object_ids)."""
+    if _is_primitive(value):
+        return pickle.dumps(value, protocol=5), [], []
     prev = getattr(_tls, "contained", None)
     _tls.contained = []
     buffers: List[pickle.PickleBuffer] = []
@@ -126,6 +137,8 @@ def deserialize(data, buffers) -> Any:
 
 def dumps_inline(value: Any) -> Tuple[bytes, List[bytes]]:
     """In-band pickle for small task args (buffers are inlined)."""
+    if _is_primitive(value):
+        return pickle.dumps(value, protocol=5), []
     prev = getattr(_tls, "contained", None)
     _tls.contained = []
     try:

@@ -46,11 +46,12 @@ _init_lock = threading.RLock()
 
 
 class _Pending:
-    __slots__ = ("ev", "value")
+    __slots__ = ("ev", "value", "cb")
 
-    def __init__(self):
+    def __init__(self, cb=None):
         self.ev = threading.Event()
         self.value = None
+        self.cb = cb
 
 
 class ActorConn:
@@ -209,6 +210,8 @@ class CoreWorker:
         self.config: Dict[str, Any] = json.loads(os.environ.get("RMM_CONFIG", "{}") or "{}")
         self.placement_group_capture = None  # (pg, capture_child_tasks)
         self.actor_handle_for_self = None
+        self.direct = None  # DirectTaskSubmitter (worker leases), created on first eligible task
+        self.multi_node = False  # head-pushed: direct submission only on single-node clusters
         self._reader_t = threading.Thread(target=self._reader, daemon=True, name="rmm-reader")
         self._reader_t.start()
         self._flusher_stop = threading.Event()
@@ -224,8 +227,16 @@ class CoreWorker:
                 if t == P.REPLY:
                     p = self.reqs.pop(m[1], None)
                     if p is not None:
+                        if p.cb is not None:
+                            try:
+                                p.cb(m[2])
+                            except Exception as e:  # pragma: no cover
+                                logger.warning("async reply handler failed: %r", e)
+                            continue
                         p.value = m[2]
                         p.ev.set()
+                elif t == P.NODES_CHANGED:
+                    self.multi_node = bool(m[1])
                 elif t == P.TRIGGER_GC:
                     threading.Thread(target=_collect_garbage, daemon=True).start()
                 elif t in (P.CANCEL_TASK, P.FREE_GPU):
@@ -244,10 +255,17 @@ class CoreWorker:
         for p in list(self.reqs.values()):
             p.value = exc.LocalRayletDiedError()
             p.ev.set()
+            if p.cb is not None:
+                try:
+                    p.cb(p.value)
+                except Exception:
+                    pass
         self.task_queue.put((P.EXIT,))
 
     def _flush_loop(self):
         while not self._flusher_stop.wait(0.01):
+            if self.direct is not None and self.direct.done_buf:
+                self.direct.flush()
             if getattr(self, "_gpu_deferred_free", None):
                 try:  # GPU objects whose descriptors were still pinned by readers at FREE time
                     from ray_memory_management_amd._private import gpu_object_store as gos
@@ -287,6 +305,15 @@ class CoreWorker:
                 self.connected = False
                 if msg is not None:
                     raise exc.LocalRayletDiedError()
+
+    def request_async(self, build, cb):
+        """Send a request; `cb(reply)` runs on the reader thread when the head answers."""
+        p = _Pending(cb)
+        with self.req_lock:
+            self.req_counter += 1
+            rid = self.req_counter
+            self.reqs[rid] = p
+        self.send(build(rid))
 
     def request(self, build, timeout=None):
         p = _Pending()
@@ -387,8 +414,15 @@ class CoreWorker:
         value = ser.deserialize(pickled, bufs)
         return value, is_error
 
+    on_block = None  # worker processes: bounce queued direct tasks when the running one blocks
+
     def _set_blocked(self, blocked: bool):
         if self.mode == WORKER_MODE and self.current_task_id is not None and self.current_actor_id is None:
+            if blocked and self.on_block is not None:
+                try:
+                    self.on_block()
+                except Exception as e:  # pragma: no cover
+                    logger.warning("bouncing queued direct tasks failed: %r", e)
             if self.blocked != blocked:
                 self.blocked = blocked
                 try:
@@ -487,7 +521,7 @@ class CoreWorker:
         ek = {k: enc(v) for k, v in kwargs.items()}
         return ea, ek, arg_refs, keep
 
-    def submit_task(self, spec: dict, keep) -> List[ObjectRef]:
+    def submit_task(self, spec: dict, keep, blob: Optional[bytes] = None) -> List[ObjectRef]:
         task_id = _ids.new_task_id()
         spec["task_id"] = task_id
         nr = spec.get("num_returns", 1)
@@ -497,6 +531,20 @@ class CoreWorker:
         spec["return_ids"] = ret_ids
         spec["job_id"] = self.job_id
         spec["parent_task_id"] = self.current_task_id
+        if self.config.get("direct_task_submission", True):
+            d = self.direct
+            if d is None:
+                from ray_memory_management_amd._private.direct_task import DirectTaskSubmitter
+
+                d = self.direct = DirectTaskSubmitter(self)
+            if d.eligible(spec):
+                fn_blob = spec.pop("fn_blob", None)
+                if fn_blob is not None:  # the head still needs it (head-path tasks, lineage resubmits)
+                    self.send((P.FN_EXPORT, spec["fn_id"], fn_blob))
+                if spec.get("arg_refs"):  # the head must know the args' refs before the worker drops its own
+                    self.send(None)
+                d.submit(spec, keep, fn_blob if fn_blob is not None else blob)
+                return refs
         self.send((P.SUBMIT_TASK, spec))
         return refs
 
@@ -552,10 +600,14 @@ class CoreWorker:
     def shutdown(self):
         self._flusher_stop.set()
         try:
+            if self.direct is not None:
+                self.direct.flush()
             self.flush_events()
             self.send(None)
         except Exception:
             pass
+        if self.direct is not None:
+            self.direct.close()
         for c in self.actor_conns.values():
             c.close()
         try:
@@ -899,6 +951,8 @@ def cancel(object_ref: ObjectRef, *, force: bool = False, recursive: bool = True
     if _local_mode:
         return
     w = _require_worker()
+    if w.direct is not None and w.direct.cancel(object_ref.binary()[:16], force):
+        return
     w.send((P.CANCEL, object_ref.binary()[:16], force, recursive))
 
 

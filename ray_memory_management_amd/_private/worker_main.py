@@ -59,6 +59,82 @@ class Executor:
         self.loop = None
         self.exiting = False
         self.pid = os.getpid()
+        self.cancelled_direct = set()
+        self.pending_blobs = {}
+        self.pending_acks = {}  # direct conn -> [lock, [ack, ...]]
+        self.acks_since = 0.0
+
+    # ------------------------------------------------------------------ direct task socket
+    def start_direct_server(self) -> str:
+        """Listening socket owners push leased tasks to (reference: the worker's gRPC
+        CoreWorkerService PushTask endpoint)."""
+        path = os.path.join(self.w.session_dir, "sockets", f"w-{self.w.worker_id.hex()[:20]}.sock")
+        srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        srv.bind(path)
+        srv.listen(64)
+        threading.Thread(target=self._direct_accept, args=(srv,), daemon=True, name="rmm-direct-accept").start()
+        return path
+
+    def flush_acks(self):
+        self.acks_since = 0.0
+        for s, (lock, acks) in list(self.pending_acks.items()):
+            if acks:
+                batch = list(acks)
+                acks.clear()
+                try:
+                    P.send(s, (P.REPLY, 0, batch), lock)
+                except OSError:
+                    pass
+
+    def bounce_direct(self):
+        """The running task blocked in get(): hand every queued, unstarted direct task back to its
+        owner (status "requeue") so it runs elsewhere instead of waiting behind the blocked one."""
+        self.flush_acks()
+        q = self.w.task_queue
+        with q.mutex:
+            bounce = [m for m in q.queue if m[0] == P.DIRECT_TASK]
+            if not bounce:
+                return
+            rest = [m for m in q.queue if m[0] != P.DIRECT_TASK]
+            q.queue.clear()
+            q.queue.extend(rest)
+        for _, s, lock, spec, blob, info in bounce:
+            if blob is not None:
+                self.pending_blobs[spec["fn_id"]] = blob  # the owner will not resend it on this conn
+            try:
+                P.send(s, (P.REPLY, 0, [(spec["task_id"], "requeue", 0.0, 0.0)]), lock)
+            except OSError:
+                pass
+
+    def _direct_accept(self, srv):
+        while True:
+            try:
+                s, _ = srv.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._direct_conn, args=(s,), daemon=True, name="rmm-direct").start()
+
+    def _direct_conn(self, s):
+        lock = threading.Lock()
+        rd = P.FrameReader()
+        try:
+            while True:
+                data = s.recv(1 << 16)
+                if not data:
+                    return
+                for m in rd.feed(data):
+                    if m[0] == P.DIRECT_TASK:
+                        info = m[2]
+                        for spec, blob, attempt in m[1]:
+                            self.w.task_queue.put((P.DIRECT_TASK, s, lock, spec, blob,
+                                                   {**info, "attempt": attempt}))
+                    elif m[0] == P.CANCEL_TASK:
+                        if self.w.current_task_id == m[1]:
+                            self.w._cancel_current(m[1])
+                        else:
+                            self.cancelled_direct.add(m[1])
+        except (OSError, EOFError):
+            pass
 
     # ------------------------------------------------------------------ argument handling
     def resolve(self, enc):
@@ -122,10 +198,49 @@ class Executor:
 
     # ------------------------------------------------------------------ normal tasks
     def execute(self, spec, blob, info):
+        status, contained_map, holds, t0, t1, exit_after = self._run(spec, blob, info)
+        self.w.send((P.TASK_DONE, spec["task_id"], status, contained_map, {"exit": exit_after}))
+        del holds
+        if exit_after:
+            self.w.flush_events()
+            os._exit(0)
+
+    def execute_direct(self, s, lock, spec, blob, info):
+        """A task pushed by its owner over a lease (direct task transport): outputs go to the store
+        as usual, nested-ref bookkeeping to the head, and the completion ack to the owner."""
+        tid = spec["task_id"]
+        if tid in self.cancelled_direct:
+            self.cancelled_direct.discard(tid)
+            self.store_error(spec["return_ids"], exc.TaskCancelledError(tid.hex()))
+            t = time.time()
+            status, contained_map, holds, t0, t1, exit_after = "err", {}, [], t, t, False
+        else:
+            if self.acks_since and time.time() - self.acks_since > 0.001:
+                self.flush_acks()  # never hold finished acks across a task that may run long
+            status, contained_map, holds, t0, t1, exit_after = self._run(spec, blob, info)
+        for outer, inners in contained_map.items():
+            self.w.send((P.CONTAINED, outer, inners))
+        if contained_map:
+            self.w.send(None)
+        # acks are coalesced while more direct work is queued (one frame per burst)
+        acks = self.pending_acks.setdefault(s, [lock, []])
+        acks[1].append((tid, status, t0, t1))
+        if not self.acks_since:
+            self.acks_since = time.time()
+        if len(acks[1]) >= 16 or self.w.task_queue.empty():
+            self.flush_acks()
+        del holds
+        if exit_after:
+            self.w.flush_events()
+            os._exit(0)
+
+    def _run(self, spec, blob, info):
         w = self.w
         fid = spec["fn_id"]
         fn = self.fns.get(fid)
         if fn is None:
+            if blob is None:
+                blob = self.pending_blobs.pop(fid, None)
             if blob is None:
                 raise RuntimeError("function blob missing")
             fn = cloudpickle.loads(blob)
@@ -204,11 +319,7 @@ class Executor:
         self.call_counts[fid] += 1
         mc = spec.get("max_calls", 0)
         exit_after = bool(mc and self.call_counts[fid] >= mc) or self.exiting
-        w.send((P.TASK_DONE, spec["task_id"], status, contained_map, {"exit": exit_after}))
-        del holds
-        if exit_after:
-            w.flush_events()
-            os._exit(0)
+        return status, contained_map, holds, t0, t1, exit_after
 
     # ------------------------------------------------------------------ actors
     def create_actor(self, spec, blob, info):
@@ -406,8 +517,17 @@ def main():
     _w.global_worker = w
     _set_worker(w)
     ex = Executor(w)
-    w.send((P.REGISTER, "worker", {"worker_id": wid, "pid": os.getpid()}))
+    direct_addr = ex.start_direct_server()
+    w.on_block = ex.bounce_direct
+    w.send((P.REGISTER, "worker", {"worker_id": wid, "pid": os.getpid(), "direct_addr": direct_addr}))
     info = None
+    prof_dir = os.environ.get("RMM_WORKER_PROFILE_DIR")  # control-plane profiling: cProfile per worker
+    prof = None
+    if prof_dir:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     while True:
         m = w.task_queue.get()
         t = m[0]
@@ -416,12 +536,20 @@ def main():
                 ex.execute(m[1], m[2], m[3])
             except KeyboardInterrupt:
                 pass
+        elif t == P.DIRECT_TASK:
+            try:
+                ex.execute_direct(m[1], m[2], m[3], m[4], m[5])
+            except KeyboardInterrupt:
+                pass
         elif t == P.CREATE_ACTOR_INSTANCE:
             ex.create_actor(m[1], m[2], m[3])
             threading.Thread(target=_drain_head_queue, args=(w,), daemon=True).start()
             ex.actor_loop()
         elif t == P.EXIT:
             break
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.path.join(prof_dir, f"worker-{os.getpid()}.prof"))
     w.flush_events()
     w.shutdown()
     os._exit(0)

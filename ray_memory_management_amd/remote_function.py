@@ -161,7 +161,7 @@ class RemoteFunction:
         b = w.export(fid, blob)
         if b is not None:
             spec["fn_blob"] = b
-        refs = w.submit_task(spec, keep)
+        refs = w.submit_task(spec, keep, blob)
         if nr == "dynamic":
             return refs[0]
         if nr == 0:
