@@ -48,6 +48,12 @@ def timeit(name: str, fn: Callable[[], None], multiplier: float = 1, duration: f
 
 
 @ray.remote
+def _do_put():
+    for _ in range(10):
+        ray.put(np.zeros(10 * 1024 * 1024, dtype=np.int64))
+
+
+@ray.remote
 def _small_value():
     return b"ok"
 
@@ -135,8 +141,8 @@ def run(duration: float = 2.0, filter_pattern: str = "") -> List[dict]:
         1000 * len(clients))
     arr = np.zeros(100 * 1024 * 1024, dtype=np.int64)  # 800 MB per put (reference: 8 x 0.1 GB)
     add("single client put gigabytes", lambda: ray.put(arr), 8 * 0.1)
-    add("multi client put gigabytes",
-        lambda: ray.get([c.put_large.remote(2, 100 * 1024 * 1024 // 8) for c in clients]), 2 * 0.1 * len(clients))
+    # reference ray_perf.py:139-146: 10 tasks x 10 puts of a fresh 80 MB np.zeros each
+    add("multi client put gigabytes", lambda: ray.get([_do_put.remote() for _ in range(10)]), 10 * 8 * 0.1)
     add("single client tasks and get batch", lambda: ray.get([_small_value.remote() for _ in range(1000)]))
     add("single client tasks sync", lambda: ray.get(_small_value.remote()))
     add("single client tasks async", lambda: ray.get([_small_value.remote() for _ in range(1000)]), 1000)

@@ -502,6 +502,8 @@ class CoreWorker:
         keep: List[Any] = []
 
         def enc(v):
+            if type(v) in ser._PRIMITIVES:  # hot path: small scalars pickle directly
+                return ("v", ser.pickle.dumps(v, protocol=5))
             if isinstance(v, ObjectRef):
                 arg_refs.append(v.binary())
                 keep.append(v)

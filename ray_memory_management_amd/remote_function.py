@@ -58,6 +58,8 @@ def strategy_from_options(opts, worker=None):
 
     st = opts.get("scheduling_strategy")
     pg = opts.get("placement_group")
+    if st is None and pg is None and (worker is None or worker.placement_group_capture is None):
+        return None  # hot path: default strategy, no captured placement group
     if pg is not None and pg != "default" and st is None:
         st = PlacementGroupSchedulingStrategy(pg, opts.get("placement_group_bundle_index", -1),
                                               opts.get("placement_group_capture_child_tasks"))
@@ -99,6 +101,7 @@ class RemoteFunction:
         self._module = getattr(function, "__module__", "")
         self._blob = None
         self._fid = None
+        self._res_cache = None  # (opts dict, resources, runtime_env key) for the default options
         self._is_generator = inspect.isgeneratorfunction(function)
         self.__doc__ = function.__doc__
         self.__name__ = getattr(function, "__name__", "remote_function")
@@ -150,13 +153,20 @@ class RemoteFunction:
         if self._is_generator and nr == 1 and "num_returns" not in opts:
             nr = 1
         runtime_env = opts.get("runtime_env") or getattr(w, "job_runtime_env", None)
+        rc = self._res_cache
+        if rc is not None and rc[0] is opts and rc[3] is runtime_env:
+            res, env_key = dict(rc[1]), rc[2]
+        else:
+            res, env_key = resources_from_options(opts), env_key_of(runtime_env)
+            if opts is self._options:
+                self._res_cache = (opts, dict(res), env_key, runtime_env)
         spec = {
             "fn_id": fid, "name": self._name, "args": ea, "kwargs": ek, "arg_refs": arg_refs,
-            "num_returns": nr, "resources": resources_from_options(opts),
+            "num_returns": nr, "resources": res,
             "max_retries": opts.get("max_retries", 3 if w.config.get("task_max_retries") is None
                                     else w.config.get("task_max_retries")),
             "retry_exceptions": opts.get("retry_exceptions", False), "strategy": strategy_from_options(opts, w),
-            "runtime_env": runtime_env, "env_key": env_key_of(runtime_env), "max_calls": opts.get("max_calls", 0),
+            "runtime_env": runtime_env, "env_key": env_key, "max_calls": opts.get("max_calls", 0),
         }
         b = w.export(fid, blob)
         if b is not None:
