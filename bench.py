@@ -11,11 +11,13 @@ synthetic 84x84 frames, sample-batch GPU ingest + GAE HIP scan"):
 
 * ``PPO`` with ``num_learner_workers=N``: N learner ACTORS, one per GPU, each running the fused
   bf16 learner (HIP graphs, MFMA kernels) and all-reducing gradients over RCCL (xGMI);
-* CPU rollout-worker ACTORS (numpy-vectorised synthetic Atari env, CPU policy inference): per
-  learner 10 workers x 5 envs x 100 steps = 5000 samples per iteration (the reference
-  rllib/tuned_examples/ppo/atari-ppo.yaml: num_workers 10, num_envs_per_worker 5,
-  rollout_fragment_length 100, train_batch_size 5000, sgd_minibatch_size 500, num_sgd_iter 10);
-  fewer workers with more envs each when the host has fewer CPUs (same 5000 samples);
+* CPU rollout-worker ACTORS stepping the numpy-vectorised synthetic Atari env on their CPU, with the
+  policy on the worker's slice of the learner GPU (RLlib ``num_gpus_per_worker > 0``; default
+  ``--rollout hybrid``): every env step is one HIP-graph replay (pinned H2D obs copy → K10 trunk →
+  K13 dense → K16 heads + Gumbel sampling → D2H actions), 2 workers x 25 envs x 100 steps = 5000
+  samples per learner per iteration (atari-ppo.yaml: train_batch_size 5000, rollout_fragment_length
+  100, sgd_minibatch_size 500, num_sgd_iter 10; its 10 workers x 5 envs layout is what
+  ``--rollout cpu`` runs, with the policy on the worker CPUs as num_gpus_per_worker: 0 does);
 * fragments travel rollout worker → shared-memory object store → learner, where they are DMA'd
   onto the GPU and GAE + advantage standardisation run as one kernel (K17).
 
@@ -23,11 +25,12 @@ One timed step = one ``algo.train()`` iteration: sample 5000·N env steps, inges
 500-sample minibatch SGD on every learner, publish weights. Weak scaling (per-GPU batch fixed).
 ``value`` = whole-job env samples trained per second.
 
-After the timed CPU-rollout run the bench also reports (separately labelled, same K/W):
-``runtime_gpu_rollout_samples_per_s`` — the same runtime path with one GPU rollout actor per learner
-(device env + on-GPU inference, fragments through the HBM object store via hipIPC, same GPU), and at
-N=1 ``fused_loop_samples_per_s`` — round 1's single-process fused loop (no runtime). ``--rollout gpu``
-makes the GPU-rollout mode the timed one; ``--mode fused`` times the fused loop (torchrun for N>1).
+At N=1 the bench also reports (separately labelled, same K/W): ``runtime_cpu_rollout_*`` — the
+same path with the policy on the rollout workers' CPUs (10 x 5 envs, the yaml's layout);
+``runtime_gpu_rollout_*`` — one GPU rollout actor per learner (device env + on-GPU inference,
+fragments through the HBM object store via hipIPC); ``fused_loop_samples_per_s`` — the
+single-process fused loop (no runtime). ``--rollout {cpu,gpu}`` times those modes instead;
+``--mode fused`` times the fused loop (torchrun for N>1).
 """
 from __future__ import annotations
 
@@ -164,8 +167,12 @@ def _runtime(args, n_gpus):
     from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
 
     budget = _cpu_budget(n_gpus)
-    if args.rollout == "cpu":
+    if args.rollout in ("cpu", "hybrid"):
         w_per, envs = _rollout_layout(n_gpus, budget, args.fragment)
+        if args.rollout == "hybrid" and not args.workers_per_learner:
+            # GPU policy: 2 workers x 25 envs per learner GPU measured best on MI355X
+            # (profiles/bench_r2_hybrid_sweep.txt): bigger inference batches, fewer GPU contexts
+            w_per, envs = 2, TRAIN_BATCH // (args.fragment * 2)
         if args.workers_per_learner:
             w_per = args.workers_per_learner
             envs = max(1, TRAIN_BATCH // (args.fragment * w_per))
@@ -178,7 +185,7 @@ def _runtime(args, n_gpus):
              _system_config={"prestart_workers": 0})
     try:
         cfg = (PPOConfig()
-               .environment("SyntheticAtariVec-v0" if args.rollout == "cpu" else "GPUSyntheticAtari-v0",
+               .environment("GPUSyntheticAtari-v0" if args.rollout == "gpu" else "SyntheticAtariVec-v0",
                             env_config={"num_actions": 4, "episode_len": 1000})
                .rollouts(num_rollout_workers=w_per * n_gpus, num_envs_per_worker=envs,
                          rollout_fragment_length=args.fragment, postprocess_on_learner=True,
@@ -187,8 +194,9 @@ def _runtime(args, n_gpus):
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
                          vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99)
                .resources(num_learner_workers=n_gpus,
-                          num_gpus_per_learner_worker=0.5 if args.rollout == "gpu" else phys / n_gpus,
-                          num_gpus_per_worker=0.5 if args.rollout == "gpu" else 0,
+                          num_gpus_per_learner_worker=(0.5 if args.rollout != "cpu" else 1.0) * phys / n_gpus,
+                          # hybrid: CPU env, policy on the worker's slice of the learner's GPU
+                          num_gpus_per_worker={"gpu": 0.5, "hybrid": 0.5 / w_per}.get(args.rollout, 0) * phys / n_gpus,
                           learner_collective_backend="gloo" if args.same_device else args.dist_backend)
                .debugging(seed=0))
         algo = cfg.build()
@@ -208,7 +216,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", choices=("runtime", "fused"), default="runtime")
-    ap.add_argument("--rollout", choices=("cpu", "gpu"), default="cpu")
+    ap.add_argument("--rollout", choices=("cpu", "gpu", "hybrid"), default="hybrid",
+                    help="cpu: CPU env + CPU policy (atari-ppo.yaml); hybrid: CPU env + policy on the rollout "
+                         "worker's GPU slice (num_gpus_per_worker > 0); gpu: device env + GPU policy")
     ap.add_argument("--workers-per-learner", type=int, default=0)
     ap.add_argument("--fragment", type=int, default=100)
     ap.add_argument("--minibatch", type=int, default=500)
@@ -287,40 +297,45 @@ def main():
                 dist.destroy_process_group()
             raise err
         sps = TRAIN_BATCH * n_gpus * args.steps / elapsed
-        mode_info = {"mode": "runtime", "rollout": args.rollout, **(info or {})}
+        mode_info = {"mode": "runtime", "rollout": args.rollout,
+                     "rollout_env": "gpu" if args.rollout == "gpu" else "cpu",
+                     "rollout_policy_device": "cpu" if args.rollout == "cpu" else "gpu", **(info or {})}
         if world > 1:
             dist.destroy_process_group()
 
     if rank == 0:
         extra = {}
-        if args.mode == "runtime" and args.rollout == "cpu" and not args.no_gpu_rollout and not args.same_device:
-            # second, clearly separate runtime measurement: GPU rollout actors (device env + on-GPU
-            # inference) next to each learner, fragments through the HBM object store (hipIPC)
+        if args.mode == "runtime" and n_gpus == 1 and not args.no_gpu_rollout and not args.same_device:
+            # extra, clearly separate runtime measurements on the same config: (1) cpu — the CPU envs
+            # with the policy on the rollout workers' CPUs (atari-ppo.yaml num_gpus_per_worker: 0);
+            # (2) gpu — GPU rollout actors (device env + on-GPU inference), fragments through the
+            # HBM object store (hipIPC)
             import copy
 
             import ray_memory_management_amd as ray
 
-            a2 = copy.copy(args)
-            a2.rollout = "gpu"
-            algo2 = None
-            try:
-                algo2, info2 = _runtime(a2, n_gpus)
-                t0 = time.perf_counter()
-                for _ in range(args.steps):
-                    algo2.train()
-                e2 = time.perf_counter() - t0
-                extra["runtime_gpu_rollout_samples_per_s"] = round(TRAIN_BATCH * n_gpus * args.steps / e2, 1)
-                extra["runtime_gpu_rollout_ms_per_step"] = round(e2 / args.steps * 1e3, 3)
-            except Exception as ex:  # noqa: BLE001
-                print(f"[bench] gpu-rollout runtime mode failed: {ex!r}", file=sys.stderr)
-                extra["runtime_gpu_rollout_error"] = repr(ex)[:300]
-            finally:
-                if algo2 is not None:
-                    try:
-                        algo2.stop()
-                    except Exception:
-                        pass
-                ray.shutdown()
+            for mode in [m for m in ("cpu", "hybrid", "gpu") if m != args.rollout]:
+                a2 = copy.copy(args)
+                a2.rollout = mode
+                algo2 = None
+                try:
+                    algo2, info2 = _runtime(a2, n_gpus)
+                    t0 = time.perf_counter()
+                    for _ in range(args.steps):
+                        algo2.train()
+                    e2 = time.perf_counter() - t0
+                    extra[f"runtime_{mode}_rollout_samples_per_s"] = round(TRAIN_BATCH * n_gpus * args.steps / e2, 1)
+                    extra[f"runtime_{mode}_rollout_ms_per_step"] = round(e2 / args.steps * 1e3, 3)
+                except Exception as ex:  # noqa: BLE001
+                    print(f"[bench] {mode}-rollout runtime mode failed: {ex!r}", file=sys.stderr)
+                    extra[f"runtime_{mode}_rollout_error"] = repr(ex)[:300]
+                finally:
+                    if algo2 is not None:
+                        try:
+                            algo2.stop()
+                        except Exception:
+                            pass
+                    ray.shutdown()
         if args.mode == "runtime" and n_gpus == 1 and world == 1 and not args.no_fused:
             try:
                 import copy

@@ -59,7 +59,8 @@ class Algorithm(Trainable):
         """GPU rollout workers next to GPU learner actors: one placement-group bundle per learner
         GPU {GPU: 1}; learner k and its rollout workers share bundle k (fractional GPUs), so a
         fragment never leaves the GPU that trains on it."""
-        if not (getattr(c, "gpu_rollouts", False) and getattr(c, "num_learner_workers", 0)):
+        gpu_workers = getattr(c, "gpu_rollouts", False) or (c.num_gpus_per_worker or 0) > 0
+        if not (gpu_workers and getattr(c, "num_learner_workers", 0)):
             return None
         import ray_memory_management_amd as ray
         from ray_memory_management_amd.util.placement_group import placement_group
@@ -68,7 +69,8 @@ class Algorithm(Trainable):
         n = int(c.num_learner_workers)
         per = max(1, c.num_workers // n)
         cpus = c.num_cpus_per_learner_worker + per * c.num_cpus_per_worker
-        pg = placement_group([{"GPU": 1.0, "CPU": float(cpus)} for _ in range(n)], strategy="PACK")
+        gpus = min(1.0, float(c.num_gpus_per_learner_worker) + per * float(c.num_gpus_per_worker or 0))
+        pg = placement_group([{"GPU": gpus, "CPU": float(cpus)} for _ in range(n)], strategy="PACK")
         ray.get(pg.ready())
         self._placement_group = pg
         # worker i feeds learner i % n (split_for_learners is round-robin): same bundle, same GPU

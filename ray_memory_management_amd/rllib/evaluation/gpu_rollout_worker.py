@@ -89,3 +89,167 @@ class GPURolloutWorker:
 
     def stop(self):
         pass
+
+
+class HybridRolloutWorker(GPURolloutWorker):
+    """CPU rollout worker whose env steps on the CPU and whose policy runs on its (fractional) GPU.
+
+    Role parity: reference rllib/evaluation/rollout_worker.py with ``num_gpus_per_worker > 0`` and
+    a CPU env (the policy is placed on the worker's GPU). MI355X design: each env step is ONE
+    HIP-graph replay — pinned-host → HBM observation copy, K10 trunk → K13 dense → K16 heads +
+    Gumbel sampling + rollout-row stores, action copy back to pinned host — then a single stream
+    sync and the CPU vector-env step. The fragment goes out exactly like a CPU worker's
+    (``pack_fragment``: frames + packed fp32 rows through the shm object store, GAE on the learner).
+    """
+
+    def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
+                 num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
+        import torch
+
+        from ray_memory_management_amd._native import require_hip
+        from ray_memory_management_amd.rllib.env import make_vector_env
+        from ray_memory_management_amd.rllib.models import build_model
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("HybridRolloutWorker needs a GPU (num_gpus_per_worker > 0)")
+        require_hip()
+        self.config = dict(config or {})
+        self.worker_index = worker_index
+        ec = dict(self.config.get("env_config") or {})
+        base_seed = seed if seed is not None else self.config.get("seed")
+        s = (int(base_seed or 0) * 1000 + worker_index) & 0x7FFFFFFF
+        ec.setdefault("seed", s)
+        n = int(self.config.get("num_envs_per_worker", 1))
+        self.env = make_vector_env(self.config.get("env"), n, ec)
+        if self.env is None:
+            raise ValueError("HybridRolloutWorker needs a native CPU vector env")
+        torch.set_num_threads(1)
+        self.device = torch.device("cuda:0")
+        torch.cuda.set_device(0)
+        torch.manual_seed(s)
+        model = build_model(self.env.observation_space, self.env.action_space, self.config.get("model") or {})
+        self.model = model.to(self.device).to(torch.bfloat16).to(memory_format=torch.channels_last)
+        self.T = int(self.config.get("rollout_fragment_length", 200))
+        self.n = n
+        self.seed = s
+        obs = np.asarray(self.env.vector_reset())
+        T, dev = self.T, self.device
+        self.h_obs = torch.empty(obs.shape, dtype=torch.uint8).pin_memory()
+        self.h_obs.numpy()[:] = obs
+        self.h_act = torch.empty(n, dtype=torch.int64).pin_memory()
+        self.s_obs = torch.empty(obs.shape, dtype=torch.uint8, device=dev)
+        self.s_obs.copy_(self.h_obs)
+        with torch.no_grad():
+            logits, _ = self.model(self.s_obs)
+        self.A = int(logits.shape[-1])
+        self.buf_act = torch.empty((T, n), dtype=torch.int64, device=dev)
+        self.buf_logp = torch.empty((T, n), dtype=torch.float32, device=dev)
+        self.buf_vf = torch.empty((T, n), dtype=torch.float32, device=dev)
+        self.buf_logits = torch.empty((T, n, self.A), dtype=torch.float32, device=dev)
+        self.act_now = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)  # {rng counter, rollout row}
+        self.h_frames = np.empty((T,) + obs.shape, dtype=np.uint8)
+        self.h_rew = np.empty((T, n), dtype=np.float32)
+        self.h_done = np.empty((T, n), dtype=np.float32)
+        self.stream = torch.cuda.Stream(dev)
+        self.fused = hasattr(self.model, "forward_sample") and getattr(
+            getattr(self.model, "heads", None), "out_features", -1) == self.A + 1
+        self._graph = None
+        self._ep_len = np.zeros(n, dtype=np.int64)
+        self._ep_rew = np.zeros(n, dtype=np.float64)
+        self._completed: List[tuple] = []
+        self._sample_time = 0.0
+
+    def _policy_step(self):
+        """H2D obs → fused policy step (row t of the device buffers) → D2H actions; graph body."""
+        import torch
+
+        from ray_memory_management_amd._native import require_hip
+
+        self.s_obs.copy_(self.h_obs, non_blocking=True)
+        t, ctr = self.ctr_t[1:2], self.ctr_t[0:1]
+        if not (self.fused and self.model.forward_sample(self.s_obs, t, ctr, self.seed, self.buf_act, self.buf_logp,
+                                                          self.buf_vf, self.buf_logits, self.act_now)):
+            hd = self.model.forward_heads(self.s_obs)
+            lp, vp, ld = hd.data_ptr(), hd.data_ptr() + self.A * hd.element_size(), hd.stride(0)
+            bf = hd.dtype == torch.bfloat16
+            require_hip().sample_store(lp, bf, vp, bf, t.data_ptr(), ctr.data_ptr(), self.seed,
+                                       self.buf_act.data_ptr(), self.buf_logp.data_ptr(), self.buf_vf.data_ptr(),
+                                       self.buf_logits.data_ptr(), self.act_now.data_ptr(), self.n, self.A,
+                                       torch.cuda.current_stream().cuda_stream, ldl=ld, ldv=ld)
+        self.h_act.copy_(self.act_now, non_blocking=True)
+        self.ctr_t.add_(1)
+
+    def _capture(self):
+        import torch
+
+        with torch.cuda.stream(self.stream):
+            for _ in range(2):
+                self._policy_step()
+            self.ctr_t[1].zero_()
+        self.stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream):
+            self._policy_step()
+        self._graph = g
+
+    def sample(self):
+        import time
+
+        import torch
+
+        from ray_memory_management_amd.rllib.execution.sample_ingest import pack_fragment
+
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            if self._graph is None:
+                try:
+                    self._capture()
+                except Exception as e:  # pragma: no cover
+                    print(f"[HybridRolloutWorker] HIP graph capture failed ({e!r}); running eagerly")
+                    self._graph = False
+            with torch.cuda.stream(self.stream):
+                self.ctr_t[1].zero_()
+            obs_np = self.h_obs.numpy()
+            act_np = self.h_act.numpy()
+            for t in range(self.T):
+                self.h_frames[t] = obs_np
+                if self._graph:
+                    self._graph.replay()
+                else:
+                    with torch.cuda.stream(self.stream):
+                        self._policy_step()
+                self.stream.synchronize()
+                obs, rew, done = self.env.vector_step(act_np.copy())
+                obs_np[:] = obs
+                self.h_rew[t] = rew
+                self.h_done[t] = done
+                self._ep_rew += rew
+                self._ep_len += 1
+                if done.any():
+                    for i in np.nonzero(done)[0]:
+                        self._completed.append((float(self._ep_rew[i]), int(self._ep_len[i])))
+                        self._ep_rew[i] = 0.0
+                        self._ep_len[i] = 0
+            with torch.cuda.stream(self.stream):
+                self.s_obs.copy_(self.h_obs, non_blocking=True)
+                _, last_v = self.model(self.s_obs)
+                dev_rows = torch.cat([self.buf_logits.reshape(self.T * self.n, self.A),
+                                      torch.stack([self.buf_logp, self.buf_vf, self.buf_act.float()], -1)
+                                      .reshape(self.T * self.n, 3)], 1).cpu()
+                boot = last_v.float().cpu().numpy()
+            rows = dev_rows.numpy()
+            A = self.A
+            frag = pack_fragment(self.h_frames, rows[:, :A].reshape(self.T, self.n, A),
+                                 rows[:, A].reshape(self.T, self.n), rows[:, A + 1].reshape(self.T, self.n),
+                                 self.h_rew, self.h_done, rows[:, A + 2].astype(np.int64).reshape(self.T, self.n),
+                                 boot)
+        self._sample_time += time.perf_counter() - t0
+        return frag
+
+    def set_weights(self, weights, global_vars=None):
+        import torch
+
+        self.stream.synchronize()
+        super().set_weights(weights, global_vars)
+        torch.cuda.synchronize(self.device)

@@ -25,6 +25,15 @@ class WorkerSet:
             from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import GPURolloutWorker
 
             cls = GPURolloutWorker
+        elif self._config.get("num_gpus_per_worker", 0) and env_creator is None:
+            from ray_memory_management_amd.rllib.env import _VECTOR_REGISTRY
+
+            env = self._config.get("env")
+            if isinstance(env, str) and env in _VECTOR_REGISTRY:
+                # CPU vector env + policy on the worker's GPU (RLlib num_gpus_per_worker > 0)
+                from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+                cls = HybridRolloutWorker
         self._remote_cls = ray.remote(cls).options(
             num_cpus=self._config.get("num_cpus_per_worker", 1), num_gpus=self._config.get("num_gpus_per_worker", 0))
         self._strategy = worker_strategy

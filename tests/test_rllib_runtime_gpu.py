@@ -178,3 +178,56 @@ def test_ppo_gpu_learner_actor_cpu_rollouts(cuda):
         algo.stop()
     finally:
         ray.shutdown()
+
+
+def test_hybrid_worker_fragment_consistent(cuda):
+    """CPU env + GPU policy worker: one graph replay per step; the fragment's logp must equal
+    log_softmax(logits)[action] and rows must be time-major like a CPU worker's."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+    from ray_memory_management_amd.rllib.execution.sample_ingest import fragment_dims
+
+    w = HybridRolloutWorker(config={"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 30},
+                                    "num_envs_per_worker": 4, "rollout_fragment_length": 16, "seed": 3})
+    for _ in range(2):
+        f = w.sample()
+        T, n, A = fragment_dims(f)
+        assert (T, n) == (16, 4) and f["obs"].shape == (64, 4, 84, 84) and f["obs"].dtype == np.uint8
+        raw = f["_raw"]
+        lsm = torch.log_softmax(torch.as_tensor(raw[:, :A]), -1).numpy()
+        act = raw[:, A + 4].astype(np.int64)
+        assert act.min() >= 0 and act.max() < A
+        np.testing.assert_allclose(lsm[np.arange(len(act)), act], raw[:, A], atol=2e-3)
+        assert np.isfinite(f["_boot"]).all() and f["_boot"].shape == (4,)
+    # weights from a learner land in the graph-captured bf16 parameters in place
+    wts = {k: np.zeros(v.shape, np.float32) for k, v in w.get_weights().items()}
+    w.set_weights(wts)
+    f = w.sample()
+    np.testing.assert_allclose(f["_raw"][:, :A], 0.0, atol=1e-6)  # zero weights -> zero logits
+    assert len(w.get_metrics()) > 0  # episode_len 30 < 3 x 16 steps
+
+
+def test_ppo_hybrid_rollouts(cuda):
+    """PPO with CPU-env / GPU-policy rollout workers co-located with the learner actor."""
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
+
+    ray.init(num_cpus=4, num_gpus=1, object_store_memory=1 << 30)
+    try:
+        cfg = (PPOConfig().environment("SyntheticAtariVec-v0", env_config={"episode_len": 50})
+               .rollouts(num_rollout_workers=2, num_envs_per_worker=5, rollout_fragment_length=20,
+                         postprocess_on_learner=True)
+               .training(train_batch_size=200, sgd_minibatch_size=50, num_sgd_iter=2)
+               .resources(num_learner_workers=1, num_gpus_per_learner_worker=0.5, num_gpus_per_worker=0.25)
+               .debugging(seed=0))
+        algo = cfg.build()
+        names = ray.get([w.apply.remote(lambda x: type(x).__name__) for w in algo.workers.remote_workers()])
+        assert names == ["HybridRolloutWorker"] * 2
+        for _ in range(2):
+            r = algo.train()
+        st = r["info"]["learner"]["default_policy"]["learner_stats"]
+        assert np.isfinite(st["total_loss"]) and st["num_sgd_steps"] == 8
+        algo.stop()
+    finally:
+        ray.shutdown()
