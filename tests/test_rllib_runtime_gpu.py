@@ -193,18 +193,22 @@ def test_hybrid_worker_fragment_consistent(cuda):
     for _ in range(2):
         f = w.sample()
         T, n, A = fragment_dims(f)
-        assert (T, n) == (16, 4) and f["obs"].shape == (64, 4, 84, 84) and f["obs"].dtype == np.uint8
-        raw = f["_raw"]
+        assert (T, n) == (16, 4) and tuple(f["obs"].shape) == (64, 4, 84, 84) and f["obs"].dtype == torch.uint8
+        assert f["obs"].is_cuda and f["_raw"].is_cuda  # frames stay in HBM
+        raw = f["_raw"].cpu().numpy()
         lsm = torch.log_softmax(torch.as_tensor(raw[:, :A]), -1).numpy()
         act = raw[:, A + 4].astype(np.int64)
         assert act.min() >= 0 and act.max() < A
         np.testing.assert_allclose(lsm[np.arange(len(act)), act], raw[:, A], atol=2e-3)
-        assert np.isfinite(f["_boot"]).all() and f["_boot"].shape == (4,)
+        boot = f["_boot"].cpu().numpy()
+        assert np.isfinite(boot).all() and boot.shape == (4,)
+        # row t*n+e of obs is the frame env e saw at step t: first rows match the reset frames
+        assert int(f["obs"][:4].float().sum()) > 0
     # weights from a learner land in the graph-captured bf16 parameters in place
     wts = {k: np.zeros(v.shape, np.float32) for k, v in w.get_weights().items()}
     w.set_weights(wts)
     f = w.sample()
-    np.testing.assert_allclose(f["_raw"][:, :A], 0.0, atol=1e-6)  # zero weights -> zero logits
+    np.testing.assert_allclose(f["_raw"][:, :A].cpu().numpy(), 0.0, atol=1e-6)  # zero weights -> zero logits
     assert len(w.get_metrics()) > 0  # episode_len 30 < 3 x 16 steps
 
 
