@@ -91,79 +91,37 @@ class GPURolloutWorker:
         pass
 
 
-class HybridRolloutWorker(GPURolloutWorker):
-    """CPU rollout worker whose env steps on the CPU and whose policy runs on its (fractional) GPU.
+class _EnvGroup:
+    """One double-buffered slice of a hybrid worker's envs: its own CPU vector env, pinned
+    observation / action staging, device rollout buffers, RNG/row counters and HIP graph."""
 
-    Role parity: reference rllib/evaluation/rollout_worker.py with ``num_gpus_per_worker > 0`` and
-    a CPU env (the policy is placed on the worker's GPU). MI355X design: each env step is ONE
-    HIP-graph replay — pinned-host → HBM observation copy, K10 trunk → K13 dense → K16 heads +
-    Gumbel sampling + rollout-row stores (the frame row included), action copy back to pinned
-    host — then a single stream sync and the CPU vector-env step. The frames each step uploads for
-    inference stay in HBM as the fragment's observation rows, so the fragment is returned as CUDA
-    tensors (``pack_fragment_device``): it lands in this process's HBM object store and the learner
-    on the same GPU reads it zero-copy via hipIPC — no 28 KB/frame host round trip at the learner.
-    """
-
-    def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
-                 num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
+    def __init__(self, env, model, T: int, A: int, dev, seed: int):
         import torch
 
-        from ray_memory_management_amd._native import require_hip
-        from ray_memory_management_amd.rllib.env import make_vector_env
-        from ray_memory_management_amd.rllib.models import build_model
-
-        if not torch.cuda.is_available():
-            raise RuntimeError("HybridRolloutWorker needs a GPU (num_gpus_per_worker > 0)")
-        require_hip()
-        self.config = dict(config or {})
-        self.worker_index = worker_index
-        ec = dict(self.config.get("env_config") or {})
-        base_seed = seed if seed is not None else self.config.get("seed")
-        s = (int(base_seed or 0) * 1000 + worker_index) & 0x7FFFFFFF
-        ec.setdefault("seed", s)
-        n = int(self.config.get("num_envs_per_worker", 1))
-        self.env = make_vector_env(self.config.get("env"), n, ec)
-        if self.env is None:
-            raise ValueError("HybridRolloutWorker needs a native CPU vector env")
-        torch.set_num_threads(1)
-        self.device = torch.device("cuda:0")
-        torch.cuda.set_device(0)
-        torch.manual_seed(s)
-        model = build_model(self.env.observation_space, self.env.action_space, self.config.get("model") or {})
-        self.model = model.to(self.device).to(torch.bfloat16).to(memory_format=torch.channels_last)
-        self.T = int(self.config.get("rollout_fragment_length", 200))
-        self.n = n
-        self.seed = s
-        obs = np.asarray(self.env.vector_reset())
-        T, dev = self.T, self.device
+        self.env, self.model, self.T, self.A, self.dev, self.seed = env, model, T, A, dev, seed
+        obs = np.asarray(env.vector_reset())
+        n = self.n = obs.shape[0]
         self.h_obs = torch.empty(obs.shape, dtype=torch.uint8).pin_memory()
         self.h_obs.numpy()[:] = obs
         self.h_act = torch.empty(n, dtype=torch.int64).pin_memory()
+        self.h_rew = torch.empty((T, n), dtype=torch.float32).pin_memory()
+        self.h_done = torch.empty((T, n), dtype=torch.float32).pin_memory()
         self.s_obs = torch.empty(obs.shape, dtype=torch.uint8, device=dev)
-        self.s_obs.copy_(self.h_obs)
-        with torch.no_grad():
-            logits, _ = self.model(self.s_obs)
-        self.A = int(logits.shape[-1])
+        self.buf_obs = torch.empty((T,) + obs.shape, dtype=torch.uint8, device=dev)
         self.buf_act = torch.empty((T, n), dtype=torch.int64, device=dev)
         self.buf_logp = torch.empty((T, n), dtype=torch.float32, device=dev)
         self.buf_vf = torch.empty((T, n), dtype=torch.float32, device=dev)
-        self.buf_logits = torch.empty((T, n, self.A), dtype=torch.float32, device=dev)
+        self.buf_logits = torch.empty((T, n, A), dtype=torch.float32, device=dev)
         self.act_now = torch.zeros(n, dtype=torch.int64, device=dev)
         self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)  # {rng counter, rollout row}
-        self.buf_obs = torch.empty((T,) + obs.shape, dtype=torch.uint8, device=dev)
-        self.h_rew = torch.empty((T, n), dtype=torch.float32).pin_memory()
-        self.h_done = torch.empty((T, n), dtype=torch.float32).pin_memory()
-        self.stream = torch.cuda.Stream(dev)
-        self.fused = hasattr(self.model, "forward_sample") and getattr(
-            getattr(self.model, "heads", None), "out_features", -1) == self.A + 1
-        self._graph = None
-        self._ep_len = np.zeros(n, dtype=np.int64)
-        self._ep_rew = np.zeros(n, dtype=np.float64)
-        self._completed: List[tuple] = []
-        self._sample_time = 0.0
+        self.fused = hasattr(model, "forward_sample") and getattr(
+            getattr(model, "heads", None), "out_features", -1) == A + 1
+        self.graph = None
+        self.ep_len = np.zeros(n, dtype=np.int64)
+        self.ep_rew = np.zeros(n, dtype=np.float64)
 
-    def _policy_step(self):
-        """H2D obs → fused policy step (row t of the device buffers) → D2H actions; graph body."""
+    def policy_step(self):
+        """H2D obs → frame row t → fused policy step (row t of the device buffers) → D2H actions."""
         import torch
 
         from ray_memory_management_amd._native import require_hip
@@ -183,18 +141,102 @@ class HybridRolloutWorker(GPURolloutWorker):
         self.h_act.copy_(self.act_now, non_blocking=True)
         self.ctr_t.add_(1)
 
-    def _capture(self):
+    def capture(self, stream):
         import torch
 
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(stream):
             for _ in range(2):
-                self._policy_step()
+                self.policy_step()
             self.ctr_t[1].zero_()
-        self.stream.synchronize()
+        stream.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=self.stream):
-            self._policy_step()
-        self._graph = g
+        with torch.cuda.graph(g, stream=stream):
+            self.policy_step()
+        self.graph = g
+
+    def launch(self, stream):
+        """Enqueue one policy step on `stream` (graph replay launches on the current stream) and
+        return an event that completes with the action copy."""
+        import torch
+
+        with torch.cuda.stream(stream):
+            if self.graph:
+                self.graph.replay()
+            else:
+                self.policy_step()
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return ev
+
+    def env_step(self, t: int, completed: list):
+        obs, rew, done = self.env.vector_step(self.h_act.numpy().copy())
+        self.h_obs.numpy()[:] = obs
+        self.h_rew.numpy()[t] = rew
+        self.h_done.numpy()[t] = done
+        self.ep_rew += rew
+        self.ep_len += 1
+        if done.any():
+            for i in np.nonzero(done)[0]:
+                completed.append((float(self.ep_rew[i]), int(self.ep_len[i])))
+                self.ep_rew[i] = 0.0
+                self.ep_len[i] = 0
+
+
+class HybridRolloutWorker(GPURolloutWorker):
+    """CPU rollout worker whose env steps on the CPU and whose policy runs on its (fractional) GPU.
+
+    Role parity: reference rllib/evaluation/rollout_worker.py with ``num_gpus_per_worker > 0`` and
+    a CPU env (the policy is placed on the worker's GPU). MI355X design: each env step is ONE
+    HIP-graph replay — pinned-host → HBM observation copy, frame row store, K10 trunk → K13 dense →
+    K16 heads + Gumbel sampling + rollout-row stores, action copy back to pinned host. The envs
+    are split into two groups that are double-buffered: while the GPU runs group A's policy step
+    the CPU steps group B's envs and vice versa, so env time and inference latency overlap. The
+    frames each step uploads stay in HBM as the fragment's observation rows, so the fragment is
+    returned as CUDA tensors (``pack_fragment_device``): it lands in this process's HBM object store
+    and the learner on the same GPU reads it zero-copy via hipIPC.
+    """
+
+    def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
+                 num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
+        import torch
+
+        from ray_memory_management_amd._native import require_hip
+        from ray_memory_management_amd.rllib.env import make_vector_env
+        from ray_memory_management_amd.rllib.models import build_model
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("HybridRolloutWorker needs a GPU (num_gpus_per_worker > 0)")
+        require_hip()
+        self.config = dict(config or {})
+        self.worker_index = worker_index
+        ec = dict(self.config.get("env_config") or {})
+        base_seed = seed if seed is not None else self.config.get("seed")
+        s = (int(base_seed or 0) * 1000 + worker_index) & 0x7FFFFFFF
+        n = int(self.config.get("num_envs_per_worker", 1))
+        groups = 2 if n >= 2 and self.config.get("rollout_double_buffer", True) else 1
+        sizes = [n // groups + (1 if g < n % groups else 0) for g in range(groups)]
+        envs = [make_vector_env(self.config.get("env"), k, {**ec, "seed": s * 7 + g}) for g, k in enumerate(sizes)]
+        if any(e is None for e in envs):
+            raise ValueError("HybridRolloutWorker needs a native CPU vector env")
+        self.env = envs[0]
+        torch.set_num_threads(1)
+        self.device = torch.device("cuda:0")
+        torch.cuda.set_device(0)
+        torch.manual_seed(s)
+        model = build_model(self.env.observation_space, self.env.action_space, self.config.get("model") or {})
+        self.model = model.to(self.device).to(torch.bfloat16).to(memory_format=torch.channels_last)
+        self.T = int(self.config.get("rollout_fragment_length", 200))
+        self.n = n
+        probe = torch.zeros((1,) + tuple(np.asarray(self.env.vector_reset()).shape[1:]), dtype=torch.uint8,
+                            device=self.device)
+        with torch.no_grad():
+            self.A = int(self.model(probe)[0].shape[-1])
+        self.groups = [_EnvGroup(e, self.model, self.T, self.A, self.device, (s * 131 + g) & 0x7FFFFFFF)
+                       for g, e in enumerate(envs)]
+        self.stream = torch.cuda.Stream(self.device)
+        self._captured = False
+        self._completed: List[tuple] = []
+        self._sample_time = 0.0
 
     def sample(self):
         import time
@@ -204,47 +246,43 @@ class HybridRolloutWorker(GPURolloutWorker):
         from ray_memory_management_amd.rllib.execution.sample_ingest import pack_fragment_device
 
         t0 = time.perf_counter()
+        G, T, st = self.groups, self.T, self.stream
         with torch.no_grad():
-            if self._graph is None:
-                try:
-                    self._capture()
-                except Exception as e:  # pragma: no cover
-                    print(f"[HybridRolloutWorker] HIP graph capture failed ({e!r}); running eagerly")
-                    self._graph = False
-            # the previous fragment's frames (views of buf_obs) were copied into the HBM object store
-            # on the default stream at task return: finish that before overwriting the buffers
-            self.stream.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self.stream):
-                self.ctr_t[1].zero_()
-            obs_np = self.h_obs.numpy()
-            act_np = self.h_act.numpy()
-            rew_np, done_np = self.h_rew.numpy(), self.h_done.numpy()
-            for t in range(self.T):
-                if self._graph:
-                    self._graph.replay()
-                else:
-                    with torch.cuda.stream(self.stream):
-                        self._policy_step()
-                self.stream.synchronize()
-                obs, rew, done = self.env.vector_step(act_np.copy())
-                obs_np[:] = obs
-                rew_np[t] = rew
-                done_np[t] = done
-                self._ep_rew += rew
-                self._ep_len += 1
-                if done.any():
-                    for i in np.nonzero(done)[0]:
-                        self._completed.append((float(self._ep_rew[i]), int(self._ep_len[i])))
-                        self._ep_rew[i] = 0.0
-                        self._ep_len[i] = 0
-            with torch.cuda.stream(self.stream):
-                self.s_obs.copy_(self.h_obs, non_blocking=True)
-                _, last_v = self.model(self.s_obs)
-                rew_d = self.h_rew.to(self.device, non_blocking=True)
-                done_d = self.h_done.to(self.device, non_blocking=True)
-                frag = pack_fragment_device(self.buf_obs, self.buf_logits, self.buf_logp, self.buf_vf, rew_d, done_d,
-                                            self.buf_act, last_v)
-            self.stream.synchronize()
+            if not self._captured:
+                self._captured = True
+                for g in G:
+                    try:
+                        g.capture(st)
+                    except Exception as e:  # pragma: no cover
+                        print(f"[HybridRolloutWorker] HIP graph capture failed ({e!r}); running eagerly")
+                        g.graph = False
+            # the previous fragment's frames (views of the group buffers) were copied into the HBM
+            # object store on the default stream at task return: finish that before overwriting
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                for g in G:
+                    g.ctr_t[1].zero_()
+            evs = [g.launch(st) for g in G]
+            for t in range(T):
+                for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
+                    evs[i].synchronize()
+                    g.env_step(t, self._completed)
+                    if t + 1 < T:
+                        evs[i] = g.launch(st)
+            with torch.cuda.stream(st):
+                parts = []
+                for g in G:
+                    g.s_obs.copy_(g.h_obs, non_blocking=True)
+                    _, last_v = self.model(g.s_obs)
+                    parts.append((g.buf_obs, g.buf_logits, g.buf_logp, g.buf_vf,
+                                  g.h_rew.to(self.device, non_blocking=True),
+                                  g.h_done.to(self.device, non_blocking=True), g.buf_act, last_v.reshape(-1)))
+                if len(parts) == 1:
+                    frag = pack_fragment_device(*parts[0])
+                else:  # time-major [T, n]: the groups' env columns side by side
+                    cat = [torch.cat(xs, dim=0 if k == 7 else 1) for k, xs in enumerate(zip(*parts))]
+                    frag = pack_fragment_device(*cat)
+            st.synchronize()
         self._sample_time += time.perf_counter() - t0
         return frag
 
