@@ -9,6 +9,8 @@ ALGORITHMS = {
     "DQN": ("dqn", "DQN"),
     "IMPALA": ("impala", "Impala"),
     "APPO": ("appo", "APPO"),
+    "PG": ("pg", "PG"),
+    "A2C": ("a2c", "A2C"),
 }
 
 

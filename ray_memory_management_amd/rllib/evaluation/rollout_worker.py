@@ -96,6 +96,9 @@ class RolloutWorker:
         rew = np.stack(rew_buf)
         vf = np.stack(vf_buf)
         dn = np.stack(done_buf)
+        if not self.config.get("use_critic", True):  # PG: advantages = discounted returns, no baseline
+            vf = np.zeros_like(vf)
+            last_v = np.zeros_like(np.asarray(last_v))
         adv, ret = compute_gae_for_trajectories(rew, vf, dn, last_v, self.config.get("gamma", 0.99),
                                                 self.config.get("lambda", self.config.get("lambda_", 1.0)))
 
@@ -172,7 +175,10 @@ class RolloutWorker:
             out = pack_fragment(bufs["obs"], bufs["logits"], bufs["logp"], bufs["vf"], bufs["rew"], bufs["done"],
                                 bufs["act"], last_v)
         else:
-            adv, ret = compute_gae_for_trajectories(bufs["rew"], bufs["vf"], bufs["done"], last_v,
+            vfb = bufs["vf"] if self.config.get("use_critic", True) else np.zeros_like(bufs["vf"])
+            if not self.config.get("use_critic", True):
+                last_v = np.zeros_like(last_v)
+            adv, ret = compute_gae_for_trajectories(bufs["rew"], vfb, bufs["done"], last_v,
                                                     self.config.get("gamma", 0.99),
                                                     self.config.get("lambda", self.config.get("lambda_", 1.0)))
             rows = T * n  # time-major rows (row = t*n + env)
