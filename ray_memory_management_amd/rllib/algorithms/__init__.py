@@ -11,6 +11,8 @@ ALGORITHMS = {
     "APPO": ("appo", "APPO"),
     "PG": ("pg", "PG"),
     "A2C": ("a2c", "A2C"),
+    "MARWIL": ("marwil", "MARWIL"),
+    "BC": ("bc", "BC"),
 }
 
 

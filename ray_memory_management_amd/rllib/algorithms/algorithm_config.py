@@ -62,6 +62,13 @@ class AlgorithmConfig:
         self.postprocess_on_learner = False
         # rollout-side policy class (class or dotted import path); None = the PG TorchPolicy
         self.policy_class = None
+        # offline data (reference AlgorithmConfig.offline_data)
+        self.input_ = "sampler"
+        self.shuffle_buffer_size = 0
+        self.output = None
+        self.output_compress_columns = ["obs", "new_obs"]
+        self.output_max_file_size = 64 * 1024 * 1024
+        self.off_policy_estimation_methods = {}
 
     # ---- builder methods (each returns self)
     def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None,
@@ -179,6 +186,22 @@ class AlgorithmConfig:
             self.exploration_config = dict(exploration_config)
         return self
 
+    def offline_data(self, *, input_=None, shuffle_buffer_size=None, output=None, output_compress_columns=None,
+                     output_max_file_size=None, off_policy_estimation_methods=None, **kw) -> "AlgorithmConfig":
+        if input_ is not None:
+            self.input_ = input_
+        if shuffle_buffer_size is not None:
+            self.shuffle_buffer_size = shuffle_buffer_size
+        if output is not None:
+            self.output = output
+        if output_compress_columns is not None:
+            self.output_compress_columns = list(output_compress_columns)
+        if output_max_file_size is not None:
+            self.output_max_file_size = output_max_file_size
+        if off_policy_estimation_methods is not None:
+            self.off_policy_estimation_methods = dict(off_policy_estimation_methods)
+        return self
+
     def fault_tolerance(self, *, recreate_failed_workers=None, **kw) -> "AlgorithmConfig":
         if recreate_failed_workers is not None:
             self.recreate_failed_workers = recreate_failed_workers
@@ -189,6 +212,7 @@ class AlgorithmConfig:
         d = {k: copy.deepcopy(v) for k, v in self.__dict__.items() if k != "algo_class"}
         d["framework"] = d.pop("framework_str")
         d["callbacks"] = d.pop("callbacks_class")
+        d["input"] = d.pop("input_", "sampler")
         if d.get("lambda_", d.get("lambda")) is not None:
             d["lambda"] = d.get("lambda_", d.get("lambda"))
         return d
@@ -201,6 +225,8 @@ class AlgorithmConfig:
                 self.callbacks_class = v
             elif k == "lambda":
                 self.lambda_ = v
+            elif k == "input":
+                self.input_ = v
             elif k == "model":
                 self.model = {**self.model, **v}
             else:

@@ -60,19 +60,45 @@ class RolloutWorker:
         self._ep_len = np.zeros(n_envs, dtype=np.int64)
         self._completed: List[tuple] = []
         self._sample_time = 0.0
+        # offline IO (reference rllib/offline + rollout_worker input_creator / output_creator)
+        self.output_writer = None
+        out = self.config.get("output")
+        if out:
+            from ray_memory_management_amd.rllib.offline import JsonWriter
+
+            self.output_writer = JsonWriter(out, self.config.get("output_max_file_size", 64 << 20),
+                                            self.config.get("output_compress_columns", ("obs", "new_obs")),
+                                            worker_index)
+        self.input_reader = None
+        inp = self.config.get("input", "sampler")
+        if inp and inp != "sampler":
+            from ray_memory_management_amd.rllib.offline import JsonReader, ShuffledInput
+
+            self.input_reader = ShuffledInput(JsonReader(inp, seed=base_seed),
+                                              int(self.config.get("shuffle_buffer_size", 0) or 0), seed=base_seed)
 
     # ------------------------------------------------------------------ sampling
     def sample(self) -> SampleBatch:
-        if self.vec_env is not None:
-            return self._sample_vector()
+        if self.input_reader is not None:  # offline data replaces the env sampler
+            return self.input_reader.next()
+        batch = self._sample_vector() if self.vec_env is not None else self._sample_env()
+        if self.output_writer is not None and "_raw" not in batch:
+            self.output_writer.write(batch)
+        return batch
+
+    def _sample_env(self) -> SampleBatch:
         t0 = time.perf_counter()
         T = int(self.config.get("rollout_fragment_length", 200))
         n = self.env.num_envs
         obs_buf, act_buf, logp_buf, vf_buf, logits_buf, rew_buf, done_buf = [], [], [], [], [], [], []
         nobs_buf = []
-        eps_ids = []
+        eps_buf = []
+        if getattr(self, "_eps", None) is None:  # per-env episode ids, unique across workers
+            self._eps = np.arange(n, dtype=np.int64) + self.worker_index * (1 << 40)
+            self._next_eps = int(self._eps[-1]) + 1
         for _ in range(T):
             obs = np.stack([np.asarray(o) for o in self._obs])
+            eps_buf.append(self._eps.copy())
             a, _, extra = self.policy.compute_actions(obs, explore=self.config.get("explore", True))
             nobs, rew, done, _info = self.env.vector_step(list(a))
             nobs_buf.append(np.stack([np.asarray(o) for o in nobs]))  # before resets: terminal obs kept
@@ -91,6 +117,8 @@ class RolloutWorker:
                     self._ep_reward[i] = 0.0
                     self._ep_len[i] = 0
                     nobs[i] = self.env.reset_at(i)
+                    self._eps[i] = self._next_eps
+                    self._next_eps += 1
             self._obs = nobs
         last_v = self.policy.value(np.stack([np.asarray(o) for o in self._obs]))
         rew = np.stack(rew_buf)
@@ -110,7 +138,7 @@ class RolloutWorker:
             SampleBatch.OBS: flat(obs_buf), SampleBatch.ACTIONS: flat(act_buf),
             SampleBatch.ACTION_LOGP: flat(logp_buf).astype(np.float32), SampleBatch.VF_PREDS: flat(vf),
             SampleBatch.ACTION_DIST_INPUTS: flat(logits_buf).astype(np.float32), SampleBatch.REWARDS: flat(rew),
-            SampleBatch.DONES: flat(dn), SampleBatch.NEXT_OBS: flat(nobs_buf),
+            SampleBatch.DONES: flat(dn), SampleBatch.NEXT_OBS: flat(nobs_buf), SampleBatch.EPS_ID: flat(eps_buf),
             SampleBatch.ADVANTAGES: flat(adv).astype(np.float32),
             SampleBatch.VALUE_TARGETS: flat(ret).astype(np.float32),
         })
@@ -286,7 +314,8 @@ class RolloutWorker:
         return self._sample_time
 
     def stop(self):
-        pass
+        if self.output_writer is not None:
+            self.output_writer.close()
 
     @staticmethod
     def evaluate_episodes(policy, env_creator, env, env_config, num_episodes: int, max_steps: int = 100000):

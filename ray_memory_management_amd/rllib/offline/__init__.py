@@ -1,0 +1,219 @@
+"""Offline experience IO. Parity: reference rllib/offline/{json_writer.py (JsonWriter: one JSON
+object per line, rolled over at ``max_file_size``, ``compress_columns`` for obs/new_obs),
+json_reader.py (JsonReader over a path / glob / list of files, ``next()`` cycles through the data
+in shuffled file order), input_reader.py, output_writer.py, shuffled_input.py (ShuffledInput),
+is_estimator.py / wis_estimator.py (importance-sampling off-policy estimates)}.
+
+Encoding: every numpy column is written as {"__nd__": [dtype, shape], "b64": raw bytes base64}
+(exact round trip, ~1.33x the raw size); ``compress_columns`` additionally zlib-compress those
+columns (frames compress 10-50x) — the reference uses lz4 for the same columns.
+"""
+from __future__ import annotations
+
+import base64
+import glob as _glob
+import json
+import os
+import random
+import time
+import zlib
+from typing import Any, Dict, Iterable, List, Optional, Union
+
+import numpy as np
+
+from ray_memory_management_amd.rllib.sample_batch import SampleBatch
+
+
+def _enc(v, compress: bool):
+    if hasattr(v, "detach"):  # torch tensor
+        v = v.detach().cpu().numpy()
+    if isinstance(v, np.ndarray) and v.dtype != object:
+        raw = np.ascontiguousarray(v).tobytes()
+        out = {"__nd__": [v.dtype.str, list(v.shape)]}
+        if compress:
+            out["z"] = base64.b64encode(zlib.compress(raw, 1)).decode()
+        else:
+            out["b64"] = base64.b64encode(raw).decode()
+        return out
+    if isinstance(v, np.generic):
+        return v.item()
+    if isinstance(v, list):
+        return v
+    return v
+
+
+def _dec(v):
+    if isinstance(v, dict) and "__nd__" in v:
+        dt, shape = v["__nd__"]
+        raw = zlib.decompress(base64.b64decode(v["z"])) if "z" in v else base64.b64decode(v["b64"])
+        return np.frombuffer(raw, dtype=np.dtype(dt)).reshape(shape).copy()
+    if isinstance(v, list):
+        return np.asarray(v)
+    return v
+
+
+def to_json(batch: SampleBatch, compress_columns: Iterable[str] = ("obs", "new_obs")) -> str:
+    cc = set(compress_columns or ())
+    return json.dumps({"type": "SampleBatch", "count": int(batch.count),
+                       **{k: _enc(v, k in cc) for k, v in batch.items()}})
+
+
+def from_json(line: str) -> SampleBatch:
+    d = json.loads(line)
+    d.pop("type", None)
+    count = d.pop("count", None)
+    b = SampleBatch({k: _dec(v) for k, v in d.items()})
+    if count is not None:
+        b.count = int(count)
+    return b
+
+
+class OutputWriter:
+    def write(self, batch: SampleBatch):
+        raise NotImplementedError
+
+
+class NoopOutput(OutputWriter):
+    def write(self, batch: SampleBatch):
+        pass
+
+
+class JsonWriter(OutputWriter):
+    """Append sample batches as JSON lines under ``path`` (a directory), one file per writer,
+    rolled over when it exceeds ``max_file_size`` bytes."""
+
+    def __init__(self, path: str, max_file_size: int = 64 << 20, compress_columns=("obs", "new_obs"),
+                 worker_index: int = 0):
+        self.path = os.path.abspath(os.path.expanduser(path))
+        os.makedirs(self.path, exist_ok=True)
+        self.max_file_size = int(max_file_size)
+        self.compress_columns = tuple(compress_columns or ())
+        self.worker_index = worker_index
+        self.file_index = 0
+        self.cur = None
+        self.bytes_written = 0
+
+    def _open(self):
+        ts = time.strftime("%Y-%m-%d_%H-%M-%S")
+        name = f"output-{ts}_worker-{self.worker_index}_{os.getpid()}_{self.file_index}.json"
+        self.file_index += 1
+        self.cur = open(os.path.join(self.path, name), "w")
+        self.bytes_written = 0
+
+    def write(self, batch: SampleBatch):
+        if self.cur is None or self.bytes_written > self.max_file_size:
+            if self.cur is not None:
+                self.cur.close()
+            self._open()
+        line = to_json(batch, self.compress_columns) + "\n"
+        self.cur.write(line)
+        self.cur.flush()
+        self.bytes_written += len(line)
+
+    def close(self):
+        if self.cur is not None:
+            self.cur.close()
+            self.cur = None
+
+
+class InputReader:
+    def next(self) -> SampleBatch:
+        raise NotImplementedError
+
+
+class JsonReader(InputReader):
+    """Cycle through JSON sample-batch files (directory, glob or list) in shuffled file order."""
+
+    def __init__(self, inputs: Union[str, List[str]], seed: Optional[int] = None):
+        if isinstance(inputs, str):
+            p = os.path.abspath(os.path.expanduser(inputs))
+            if os.path.isdir(p):
+                files = sorted(_glob.glob(os.path.join(p, "*.json")))
+            elif any(ch in p for ch in "*?["):
+                files = sorted(_glob.glob(p))
+            else:
+                files = [p]
+        else:
+            files = [os.path.abspath(os.path.expanduser(f)) for f in inputs]
+        if not files:
+            raise ValueError(f"no offline input files found for {inputs!r}")
+        self.files = files
+        self.rng = random.Random(seed)
+        self._lines: List[str] = []
+
+    def _refill(self):
+        order = list(self.files)
+        self.rng.shuffle(order)
+        for f in order:
+            with open(f) as fh:
+                self._lines.extend(ln for ln in fh.read().splitlines() if ln.strip())
+        if not self._lines:
+            raise ValueError("offline input files are empty")
+        self._lines.reverse()  # pop() from the end keeps file order
+
+    def next(self) -> SampleBatch:
+        if not self._lines:
+            self._refill()
+        return from_json(self._lines.pop())
+
+    def read_all(self) -> List[SampleBatch]:
+        out = []
+        for f in self.files:
+            with open(f) as fh:
+                out += [from_json(ln) for ln in fh.read().splitlines() if ln.strip()]
+        return out
+
+
+class ShuffledInput(InputReader):
+    """Row-shuffles over a buffer of ``n`` batches (reference shuffled_input.py)."""
+
+    def __init__(self, child: InputReader, n: int = 0, seed: Optional[int] = None):
+        self.child, self.n = child, n
+        self.buf: List[SampleBatch] = []
+        self.rng = random.Random(seed)
+
+    def next(self) -> SampleBatch:
+        if self.n <= 1:
+            return self.child.next()
+        while len(self.buf) < self.n:
+            self.buf.append(self.child.next())
+        i = self.rng.randrange(len(self.buf))
+        b, self.buf[i] = self.buf[i], self.child.next()
+        return b
+
+
+def importance_sampling_estimate(batch: SampleBatch, new_logp: np.ndarray, gamma: float, weighted: bool = False):
+    """Per-episode (weighted) importance-sampling estimate of the target policy's return from
+    behaviour data (reference is_estimator.py / wis_estimator.py). Returns
+    {"v_behavior", "v_target", "v_gain"} averaged over the episodes in ``batch``."""
+    rew = np.asarray(batch[SampleBatch.REWARDS], np.float64)
+    dones = np.asarray(batch[SampleBatch.DONES]).astype(bool)
+    ratio = np.exp(np.asarray(new_logp, np.float64) - np.asarray(batch[SampleBatch.ACTION_LOGP], np.float64))
+    eps, start = [], 0
+    for i in range(len(rew)):
+        if dones[i] or i == len(rew) - 1:
+            eps.append((start, i + 1))
+            start = i + 1
+    vb, vt_terms = [], []
+    for s, e in eps:
+        disc = gamma ** np.arange(e - s)
+        p = np.cumprod(ratio[s:e])
+        vb.append(float((disc * rew[s:e]).sum()))
+        vt_terms.append((disc, p, rew[s:e]))
+    if weighted:
+        L = max(len(d) for d, _, _ in vt_terms)
+        w = np.zeros(L)
+        cnt = np.zeros(L)
+        for d, p, r in vt_terms:
+            w[:len(p)] += p
+            cnt[:len(p)] += 1
+        w = np.where(cnt > 0, w / np.maximum(cnt, 1), 1.0)
+        vt = [float((d * p / w[:len(p)] * r).sum()) for d, p, r in vt_terms]
+    else:
+        vt = [float((d * p * r).sum()) for d, p, r in vt_terms]
+    v_b, v_t = float(np.mean(vb)), float(np.mean(vt))
+    return {"v_behavior": v_b, "v_target": v_t, "v_gain": v_t / v_b if v_b else float("nan")}
+
+
+__all__ = ["JsonWriter", "JsonReader", "ShuffledInput", "InputReader", "OutputWriter", "NoopOutput", "to_json",
+           "from_json", "importance_sampling_estimate"]
