@@ -113,7 +113,7 @@ class TrialRunner:
                  max_concurrent_trials: Optional[int] = None, time_budget_s: Optional[float] = None,
                  checkpoint_freq: int = 0, checkpoint_at_end: bool = False, max_failures: int = 0,
                  fail_fast: bool = False, callbacks=None, resources=None, num_to_keep: Optional[int] = None,
-                 verbose: int = 0, reuse_actors: bool = False):
+                 verbose: int = 0, reuse_actors: bool = False, progress_reporter=None, sync_config=None):
         self.trainable_cls = trainable_cls
         self.trainable_name = getattr(trainable_cls, "__name__", "trainable")
         self.search_alg = search_alg
@@ -130,6 +130,18 @@ class TrialRunner:
                                                                                    None))
         self.num_to_keep = num_to_keep
         self.verbose = verbose
+        self.syncer = None
+        if sync_config is not None and getattr(sync_config, "upload_dir", None):
+            from ray_memory_management_amd.tune.syncer import Syncer
+
+            self.syncer = Syncer(sync_config, local_dir)
+        self.reporter = progress_reporter
+        if self.reporter is None and verbose >= 2:
+            from ray_memory_management_amd.tune.progress_reporter import CLIReporter
+
+            self.reporter = CLIReporter(metric=metric, mode=mode)
+        if self.reporter is not None:
+            self.reporter.setup(start_time=time.time(), metric=metric, mode=mode)
         self._trials: List[Trial] = []
         self._search_done = False
         self._start = time.time()
@@ -164,9 +176,18 @@ class TrialRunner:
         self._create_trials()
         while not self.is_finished():
             self.step()
+            if self.reporter is not None and self.reporter.should_report(self._trials, done=False):
+                self.reporter.report(self._trials, False)
+            if self.syncer is not None:
+                self.syncer.sync_up()
         for t in self._trials:
             if t.status == Trial.RUNNING:
                 self._stop(t, Trial.TERMINATED)
+        if self.reporter is not None:
+            self.reporter.should_report(self._trials, done=True)
+            self.reporter.report(self._trials, True)
+        if self.syncer is not None:
+            self.syncer.sync_up(force=True)
         self._cb("on_experiment_end", trials=self._trials)
         return self._trials
 
