@@ -280,3 +280,39 @@ def test_annotations_and_timer():
         time.sleep(0.01)
     t.push_units_processed(10)
     assert t.count == 1 and t.mean > 0.005 and t.mean_throughput > 0
+
+
+def test_joblib_ray_backend(ray_shared):
+    """Reference util/joblib tests: Parallel over the ray backend returns in order."""
+    import joblib
+
+    from ray_memory_management_amd.util.joblib import register_ray
+
+    register_ray()
+    with joblib.parallel_backend("ray"):
+        out = joblib.Parallel(n_jobs=2)(joblib.delayed(pow)(i, 2) for i in range(20))
+    assert out == [i * i for i in range(20)]
+
+
+def test_actor_group(ray_shared):
+    """Reference util/tests/test_actor_group.py: group method calls, execute, execute_single."""
+    from ray_memory_management_amd.util.actor_group import ActorGroup
+
+    class Counter:
+        def __init__(self, start):
+            self.v = start
+
+        def inc(self, k=1):
+            self.v += k
+            return self.v
+
+    g = ActorGroup(Counter, num_actors=3, num_cpus_per_actor=0.1, init_args=(10,))
+    assert len(g) == 3
+    assert ray_shared.get(g.inc.remote(5)) == [15, 15, 15]
+    assert g.execute(lambda a, m: a.v * m, 2) == [30, 30, 30]
+    assert g.execute_single(1, lambda a: a.inc()) == 16
+    assert ray_shared.get(g[1].inc.remote()) == 17
+    with pytest.raises(AttributeError):
+        g.nope
+    g.shutdown()
+    assert len(g) == 0
