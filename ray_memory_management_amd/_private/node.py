@@ -270,6 +270,14 @@ class Head:
 
             self.autoscaler = Monitor(self, self.config["autoscaler"])
         self.last_housekeeping = 0.0
+        # GCS persistence (reference gcs_server/gcs_table_storage + redis_store_client: with external
+        # storage the GCS tables survive a head restart): internal KV, function/class table entries of
+        # detached actors, detached actor specs, job history — snapshotted to `gcs_storage_path`
+        self.gcs_path = self.config.get("gcs_storage_path")
+        self.gcs_dirty = False
+        self.gcs_last_flush = 0.0
+        self.gcs_flush_s = float(self.config.get("gcs_storage_flush_interval_ms", 100)) / 1000.0
+        self.gcs_restored = {"kv_namespaces": 0, "actors": 0, "jobs": 0}
         self.watcher = threading.Thread(target=self._seal_watcher, daemon=True)
         self.watcher.start()
         if self.config.get("memory_monitor_refresh_ms", 250) > 0:
@@ -369,7 +377,54 @@ class Head:
                 seq = nseq
                 self._wake()
 
+    # ------------------------------------------------------------------ GCS persistence
+    def _gcs_snapshot(self) -> dict:
+        det = []
+        for a in self.actors.values():
+            if a.detached and a.state != ACTOR_DEAD and not a.spec.get("arg_refs"):
+                spec = {k: v for k, v in a.spec.items() if not k.startswith("_")}
+                det.append((spec, self.fn_table.get(spec["class_id"])))
+        jobs = [{k: v for k, v in j.items() if k != "conn"} for j in self.jobs.values()]
+        return {"version": 1, "kv": {ns: dict(d) for ns, d in self.kv.items()}, "detached_actors": det,
+                "jobs": jobs, "time": time.time()}
+
+    def _gcs_flush(self, force=False):
+        if not self.gcs_path or not (self.gcs_dirty or force):
+            return
+        os.makedirs(self.gcs_path, exist_ok=True)
+        dst = os.path.join(self.gcs_path, "gcs_snapshot.pkl")
+        tmp = dst + f".tmp{os.getpid()}"
+        with open(tmp, "wb") as f:
+            pickle.dump(self._gcs_snapshot(), f, protocol=5)
+        os.replace(tmp, dst)  # atomic: a crash mid-write keeps the previous snapshot
+        self.gcs_dirty = False
+        self.gcs_last_flush = time.time()
+
+    def _gcs_restore(self):
+        """Head restart with the same storage: reload KV and job history, recreate detached actors
+        (fresh state, like a restart after their node died)."""
+        path = os.path.join(self.gcs_path, "gcs_snapshot.pkl") if self.gcs_path else None
+        if not path or not os.path.exists(path):
+            return
+        with open(path, "rb") as f:
+            snap = pickle.load(f)  # written by this head process type only (trusted local file)
+        for ns, d in snap.get("kv", {}).items():
+            self.kv[ns].update(d)
+        self.gcs_restored["kv_namespaces"] = len(snap.get("kv", {}))
+        for j in snap.get("jobs", []):
+            j = dict(j)
+            j["alive"] = False
+            j.setdefault("end_time", j.get("end_time") or snap.get("time"))
+            self.jobs.setdefault(j["job_id"], j)
+        self.gcs_restored["jobs"] = len(snap.get("jobs", []))
+        for spec, blob in snap.get("detached_actors", []):
+            if blob is not None:
+                spec = dict(spec, class_blob=blob)
+            self._create_actor(None, None, spec)
+            self.gcs_restored["actors"] += 1
+
     def serve(self):
+        self._gcs_restore()
         os.makedirs(os.path.dirname(self.sock_path), exist_ok=True)
         ready_file = os.path.join(self.session_dir, "head.ready")
         with open(ready_file, "w") as f:
@@ -400,6 +455,9 @@ class Head:
             if now - self.last_housekeeping > 0.1:
                 self.last_housekeeping = now
                 self._housekeeping()
+                if self.gcs_dirty and now - self.gcs_last_flush >= self.gcs_flush_s:
+                    self._gcs_flush()
+        self._gcs_flush(force=bool(self.gcs_path))
         self._shutdown()
 
     def _drain_calls(self):
@@ -504,6 +562,7 @@ class Head:
             existed = k in self.kv[ns]
             if overwrite or not existed:
                 self.kv[ns][k] = v
+                self.gcs_dirty = True
             if m[1] is not None:
                 self._reply(c, m[1], existed)
         elif t == P.KV_GET:
@@ -516,6 +575,7 @@ class Head:
                 ks = [k] if k in self.kv[ns] else []
             for x in ks:
                 del self.kv[ns][x]
+            self.gcs_dirty = self.gcs_dirty or bool(ks)
             if m[1] is not None:
                 self._reply(c, m[1], len(ks))
         elif t == P.KV_KEYS:
@@ -578,6 +638,7 @@ class Head:
         if kind == "driver":
             job_id = info.get("job_id")
             c.job_id = job_id
+            self.gcs_dirty = True
             self.jobs[job_id] = {"job_id": job_id, "pid": c.pid, "start_time": time.time(), "end_time": None,
                                  "namespace": info.get("namespace"), "alive": True, "conn": c}
             if self.driver_conn is None:
@@ -685,6 +746,7 @@ class Head:
         if job:
             job["alive"] = False
             job["end_time"] = time.time()
+            self.gcs_dirty = True
         # kill non-detached actors of this job
         for a in list(self.actors.values()):
             if a.job_id == c.job_id and not a.detached and a.state != ACTOR_DEAD:
@@ -1150,6 +1212,8 @@ class Head:
             self.named_actors[key] = spec["actor_id"]
         a = ActorRec(spec, c)
         self.actors[a.actor_id] = a
+        if a.detached:
+            self.gcs_dirty = True
         for r in spec.get("arg_refs", []):
             self.refcounts[r] += 1
         if req_id is not None:
@@ -1244,6 +1308,7 @@ class Head:
 
     def _mark_actor_dead(self, a: ActorRec, cause):
         a.state = ACTOR_DEAD
+        self.gcs_dirty = self.gcs_dirty or a.detached
         a.death_cause = cause
         for wc, rid in a.waiters:
             self._reply(wc, rid, ("dead", cause, a.num_restarts))
@@ -1394,6 +1459,9 @@ class Head:
                             "func_or_class_name": name, "node_id": node, "attempt": attempt, "start_time": t0,
                             "end_time": t1, "required_resources": res, "worker_pid": None})
             return out
+        if what == "gcs":
+            return {"storage_path": self.gcs_path, "restored": dict(self.gcs_restored), "dirty": self.gcs_dirty,
+                    "last_flush": self.gcs_last_flush}
         if what == "leases":
             return {**dict(self.lease_stats), "held": sum(1 for t in self.tasks.values()
                                                           if t.spec.get("_lease") is not None and t.state == RUNNING)}

@@ -37,8 +37,9 @@ def cmd_start(a):
         print("only `--head` is supported: every node of this runtime is started by the head (cluster_utils)")
         return 1
     res = json.loads(a.resources) if a.resources else None
+    sc = {"gcs_storage_path": os.path.abspath(a.gcs_storage_path)} if a.gcs_storage_path else None
     ctx = ray.init(num_cpus=a.num_cpus, num_gpus=a.num_gpus, resources=res,
-                   object_store_memory=a.object_store_memory, _persistent=True,
+                   object_store_memory=a.object_store_memory, _persistent=True, _system_config=sc,
                    include_dashboard=a.include_dashboard, dashboard_host=a.dashboard_host,
                    dashboard_port=a.dashboard_port)
     sess = ctx["session_dir"]
@@ -232,6 +233,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--num-cpus", type=int, default=None)
     s.add_argument("--num-gpus", type=int, default=None)
     s.add_argument("--include-dashboard", action="store_true")
+    s.add_argument("--gcs-storage-path", default=None,
+                   help="persist KV / detached actors / job history here; a head restarted with the same "
+                        "path restores them")
     s.add_argument("--dashboard-host", default="127.0.0.1")
     s.add_argument("--dashboard-port", type=int, default=8265)
     s.add_argument("--resources", default=None, help="JSON dict of custom resources")
