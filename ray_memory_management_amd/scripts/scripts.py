@@ -46,6 +46,21 @@ def cmd_start(a):
     _w._head_proc = None  # detach: the head keeps running after this process exits
     _w._dashboard_proc = None  # the dashboard exits with the head
     ray.shutdown()
+    if a.ray_client_server_port is not None:
+        import subprocess
+        import sys
+
+        ready = os.path.join(sess, "client_server.json")
+        log = open(os.path.join(sess, "logs", "ray_client_server.log"), "ab")
+        subprocess.Popen([sys.executable, "-u", "-m", "ray_memory_management_amd.util.client.server", "--address",
+                          f"rmm://{sess}", "--port", str(a.ray_client_server_port), "--ready-file", ready],
+                         stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, start_new_session=True)
+        t0 = time.time()
+        while not os.path.exists(ready) and time.time() - t0 < 60:
+            time.sleep(0.05)
+        if os.path.exists(ready):
+            port = json.load(open(ready))["port"]
+            print(f"  Ray Client server: ray://127.0.0.1:{port}")
     print(f"Started head. Address: rmm://{sess}\n  connect with ray.init(address='auto') or "
           f"RMM_ADDRESS=rmm://{sess}\n  stop with `rmm stop`")
     if ctx.dashboard_url:
@@ -233,6 +248,8 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--num-cpus", type=int, default=None)
     s.add_argument("--num-gpus", type=int, default=None)
     s.add_argument("--include-dashboard", action="store_true")
+    s.add_argument("--ray-client-server-port", type=int, default=None,
+                   help="also start a Ray Client server (ray.init('ray://127.0.0.1:PORT'))")
     s.add_argument("--gcs-storage-path", default=None,
                    help="persist KV / detached actors / job history here; a head restarted with the same "
                         "path restores them")

@@ -1,0 +1,181 @@
+"""Ray Client server: a driver inside the cluster that executes API calls for remote clients.
+
+Parity: reference python/ray/util/client/server/{server.py (RayletServicer: put / get / wait /
+schedule task / actor creation / actor method calls / terminate / cluster info, one session per
+client connection, refs held for the client until it releases them), proxier.py (the
+`ray start --ray-client-server-port` entry)}. Transport: TCP with cloudpickle frames (the
+reference uses gRPC)."""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import socket
+import threading
+import traceback
+
+import cloudpickle
+
+import ray_memory_management_amd as ray
+from ray_memory_management_amd.util.client import common as C
+
+
+class _Table:
+    def __init__(self):
+        self.refs = {}
+        self.actors = {}
+        self.fns = {}
+
+
+class _Session(threading.Thread):
+    def __init__(self, sock: socket.socket, server: "ClientServer"):
+        super().__init__(daemon=True, name="rmm-client-session")
+        self.sock, self.server = sock, server
+        self.lock = threading.Lock()
+        self.table = _Table()
+        self.namespace = None
+
+    def run(self):
+        C._tls.table = self.table
+        try:
+            while True:
+                raw = C.recv(self.sock)
+                rid, op, payload = cloudpickle.loads(raw)  # resolves ids against this session's table
+                try:
+                    out = ("ok", self.handle(op, payload))
+                except BaseException as e:  # noqa: BLE001 - shipped to the client
+                    out = ("err", e)
+                try:
+                    data = C.server_dumps((rid, out), self.table)
+                except Exception as e:  # unpicklable result / error
+                    data = C.server_dumps((rid, ("err", RuntimeError(f"{type(e).__name__}: {e}\n"
+                                                                      f"{traceback.format_exc()}"))), self.table)
+                C.send_raw(self.sock, data, self.lock)
+        except (ConnectionError, OSError, EOFError):
+            pass
+        finally:
+            self.table.refs.clear()  # drop every ref this client held
+            self.table.actors.clear()
+            try:
+                self.sock.close()
+            except OSError:
+                pass
+
+    def _fn(self, blob: bytes, is_class: bool):
+        key = hashlib.sha1(blob).digest()
+        f = self.table.fns.get(key)
+        if f is None:
+            obj = cloudpickle.loads(blob)
+            f = self.table.fns[key] = obj
+        return f
+
+    def handle(self, op, p):
+        if op == "init":
+            self.namespace = p.get("namespace")
+            return {"cluster_resources": ray.cluster_resources(), "namespace": self.namespace}
+        if op == "put":
+            ref = ray.put(p)
+            self.table.refs[ref.binary()] = ref
+            return ref
+        if op == "get":
+            refs, timeout = p
+            return ray.get(refs, timeout=timeout)
+        if op == "wait":
+            refs, num_returns, timeout = p
+            return ray.wait(refs, num_returns=num_returns, timeout=timeout)
+        if op == "task":
+            blob, args, kwargs, opts = p
+            fn = self._fn(blob, False)
+            rf = ray.remote(**opts)(fn) if opts else ray.remote(fn)
+            return rf.remote(*args, **kwargs)
+        if op == "actor":
+            blob, args, kwargs, opts = p
+            if self.namespace and opts.get("name") and "namespace" not in opts:
+                opts = dict(opts, namespace=self.namespace)  # named actors live in the client's namespace
+            cls = self._fn(blob, True)
+            ac = ray.remote(**opts)(cls) if opts else ray.remote(cls)
+            h = ac.remote(*args, **kwargs)
+            self.table.actors[h._actor_id] = h
+            return h
+        if op == "call":
+            aid, name, args, kwargs, opts = p
+            m = getattr(self.table.actors[aid], name)
+            return (m.options(**opts) if opts else m).remote(*args, **kwargs)
+        if op == "release":
+            for oid in p:
+                self.table.refs.pop(oid, None)
+            return None
+        if op == "kill":
+            aid, no_restart = p
+            ray.kill(self.table.actors[aid], no_restart=no_restart)
+            return None
+        if op == "cancel":
+            ref, force = p
+            ray.cancel(ref, force=force)
+            return None
+        if op == "get_actor":
+            name, ns = p
+            h = ray.get_actor(name, namespace=ns if ns is not None else self.namespace)
+            self.table.actors[h._actor_id] = h
+            return h
+        if op == "cluster_resources":
+            return ray.cluster_resources()
+        if op == "available_resources":
+            return ray.available_resources()
+        if op == "nodes":
+            return ray.nodes()
+        raise ValueError(f"unknown client op {op!r}")
+
+
+class ClientServer:
+    def __init__(self, host: str = "127.0.0.1", port: int = 10001):
+        self.srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self.srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.srv.bind((host, port))
+        self.srv.listen(64)
+        self.port = self.srv.getsockname()[1]
+        self.sessions = []
+
+    def serve_forever(self):
+        while True:
+            try:
+                s, _ = self.srv.accept()
+            except OSError:
+                return
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            sess = _Session(s, self)
+            self.sessions.append(sess)
+            sess.start()
+
+    def start(self):
+        threading.Thread(target=self.serve_forever, daemon=True, name="rmm-client-server").start()
+        return self.port
+
+    def stop(self):
+        try:
+            self.srv.close()
+        except OSError:
+            pass
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--address", default="auto")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=10001)
+    ap.add_argument("--ready-file", default=None)
+    a = ap.parse_args(argv)
+    ray.init(address=a.address, namespace="_rmm_client_server")
+    srv = ClientServer(a.host, a.port)
+    if a.ready_file:
+        import json
+        import os
+
+        tmp = a.ready_file + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"port": srv.port, "pid": os.getpid()}, f)
+        os.replace(tmp, a.ready_file)
+    srv.serve_forever()
+
+
+if __name__ == "__main__":
+    main()
