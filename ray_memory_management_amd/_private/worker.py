@@ -194,6 +194,9 @@ class CoreWorker:
         self.req_counter = 0
         self.task_queue: "queue.Queue" = queue.Queue()
         self.ref_lock = threading.Lock()
+        # removals from __del__ (GC can run them inside a ref_lock critical section of the same
+        # thread): queued lock-free, applied by whoever next holds ref_lock
+        self._deferred_removes: "collections.deque" = collections.deque()
         self.local_refs: Dict[bytes, int] = {}
         self.deltas: Dict[bytes, int] = {}
         self.exported = set()
@@ -281,6 +284,7 @@ class CoreWorker:
 
     def _take_deltas(self):
         with self.ref_lock:
+            self._drain_removes()
             if not self.deltas:
                 return None
             # A ref created and dropped between two flushes nets to 0 but must still reach the head:
@@ -332,13 +336,26 @@ class CoreWorker:
     # ------------------------------------------------------------------ reference counting
     def add_local_ref(self, oid: bytes):
         with self.ref_lock:
+            self._drain_removes()
             n = self.local_refs.get(oid, 0)
             self.local_refs[oid] = n + 1
             if n == 0:
                 self.deltas[oid] = self.deltas.get(oid, 0) + 1
 
     def remove_local_ref(self, oid: bytes):
-        with self.ref_lock:
+        """Called from ObjectRef/ActorHandle __del__, i.e. possibly from a GC pass that runs while
+        this very thread holds ref_lock: never block on it."""
+        self._deferred_removes.append(oid)
+        if self.ref_lock.acquire(blocking=False):
+            try:
+                self._drain_removes()
+            finally:
+                self.ref_lock.release()
+
+    def _drain_removes(self):  # caller holds ref_lock
+        q = self._deferred_removes
+        while q:
+            oid = q.popleft()
             n = self.local_refs.get(oid, 0) - 1
             if n <= 0:
                 self.local_refs.pop(oid, None)
