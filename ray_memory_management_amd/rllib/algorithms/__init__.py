@@ -13,6 +13,12 @@ ALGORITHMS = {
     "A2C": ("a2c", "A2C"),
     "MARWIL": ("marwil", "MARWIL"),
     "BC": ("bc", "BC"),
+    "DDPG": ("ddpg", "DDPG"),
+    "TD3": ("td3", "TD3"),
+    "SAC": ("sac", "SAC"),
+    "SimpleQ": ("simple_q", "SimpleQ"),
+    "APEX": ("apex_dqn", "ApexDQN"),
+    "APEX_DDPG": ("apex_ddpg", "ApexDDPG"),
 }
 
 

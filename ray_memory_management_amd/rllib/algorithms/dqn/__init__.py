@@ -44,8 +44,15 @@ class DQNPolicy(TorchPolicy):
     def __init__(self, observation_space, action_space, config: Dict, device="cpu"):
         super().__init__(observation_space, action_space, config, device)
         ec = dict(config.get("exploration_config") or {})
-        self.eps = PiecewiseSchedule([[0, ec.get("initial_epsilon", 1.0)],
-                                      [ec.get("epsilon_timesteps", 10000), ec.get("final_epsilon", 0.02)]])
+        if ec.get("type") == "PerWorkerEpsilonGreedy":
+            # Ape-X: worker i of N explores with the constant eps 0.4^(1 + 7 (i-1)/(N-1)); the local
+            # (driver) worker acts greedily (reference exploration/per_worker_epsilon_greedy.py)
+            i, n = int(config.get("worker_index", 0)), int(config.get("num_workers", 0))
+            e = 0.0 if i == 0 else 0.4 ** (1 + 7.0 * (i - 1) / max(1, n - 1))
+            self.eps = PiecewiseSchedule([[0, e], [1, e]])
+        else:
+            self.eps = PiecewiseSchedule([[0, ec.get("initial_epsilon", 1.0)],
+                                          [ec.get("epsilon_timesteps", 10000), ec.get("final_epsilon", 0.02)]])
         self.dueling = bool(config.get("dueling", True))
         self._rng = np.random.default_rng(config.get("seed"))
 

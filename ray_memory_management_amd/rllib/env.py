@@ -122,6 +122,74 @@ class CartPoleEnv(Env):
         return self.state.astype(np.float32), 1.0, done, {}
 
 
+class PendulumEnv(Env):
+    """Inverted pendulum swing-up (gym Pendulum-v1 dynamics): obs [cos th, sin th, thdot], one
+    torque action in [-2, 2], cost th^2 + 0.1 thdot^2 + 0.001 u^2, 200-step episodes. The
+    reference's continuous-control smoke env (rllib/tuned_examples/{sac,ddpg,td3}/pendulum-*.yaml)."""
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.max_speed, self.max_torque, self.dt, self.g = 8.0, 2.0, 0.05, float(config.get("g", 10.0))
+        self.max_steps = int(config.get("max_episode_steps", 200))
+        high = np.array([1.0, 1.0, self.max_speed], dtype=np.float32)
+        self.observation_space = Box(-high, high, dtype=np.float32)
+        self.action_space = Box(-self.max_torque, self.max_torque, shape=(1,), dtype=np.float32)
+        self.rng = np.random.default_rng(config.get("seed"))
+        self.th = self.thdot = 0.0
+        self.steps = 0
+
+    def _obs(self):
+        return np.array([math.cos(self.th), math.sin(self.th), self.thdot], dtype=np.float32)
+
+    def reset(self, *, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.th = float(self.rng.uniform(-math.pi, math.pi))
+        self.thdot = float(self.rng.uniform(-1.0, 1.0))
+        self.steps = 0
+        return self._obs()
+
+    def step(self, action):
+        u = float(np.clip(np.asarray(action, dtype=np.float64).reshape(-1)[0], -self.max_torque, self.max_torque))
+        th_n = ((self.th + math.pi) % (2 * math.pi)) - math.pi
+        cost = th_n ** 2 + 0.1 * self.thdot ** 2 + 0.001 * u ** 2
+        thdot = self.thdot + (3.0 * self.g / 2.0 * math.sin(self.th) + 3.0 * u) * self.dt
+        self.thdot = float(np.clip(thdot, -self.max_speed, self.max_speed))
+        self.th = self.th + self.thdot * self.dt
+        self.steps += 1
+        return self._obs(), -cost, self.steps >= self.max_steps, {}
+
+
+class ContinuousTargetEnv(Env):
+    """Tiny continuous-control task for fast learning tests: observe a target in [-1, 1]^d, emit an
+    action in [-1, 1]^d, reward -(||a - target||^2); `episode_len` steps per episode (a fresh target
+    every step). Optimal return 0, a random policy scores about -2d/3 per step."""
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.d = int(config.get("dim", 1))
+        self.episode_len = int(config.get("episode_len", 10))
+        self.observation_space = Box(-1.0, 1.0, shape=(self.d,), dtype=np.float32)
+        self.action_space = Box(-1.0, 1.0, shape=(self.d,), dtype=np.float32)
+        self.rng = np.random.default_rng(config.get("seed"))
+        self.t = 0
+        self.target = np.zeros(self.d, np.float32)
+
+    def reset(self, *, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.t = 0
+        self.target = self.rng.uniform(-1, 1, self.d).astype(np.float32)
+        return self.target.copy()
+
+    def step(self, action):
+        a = np.clip(np.asarray(action, dtype=np.float32).reshape(self.d), -1.0, 1.0)
+        r = -float(np.sum((a - self.target) ** 2))
+        self.t += 1
+        self.target = self.rng.uniform(-1, 1, self.d).astype(np.float32)
+        return self.target.copy(), r, self.t >= self.episode_len, {}
+
+
 class SyntheticAtariEnv(Env):
     """84x84x4 uint8 frame-stacked observations with Atari-like dynamics statistics (CPU)."""
 
@@ -289,6 +357,8 @@ _REGISTRY = {
     "CartPole-v0": lambda cfg=None: CartPoleEnv({"max_episode_steps": 200, **(cfg or {})}),
     "SyntheticAtari-v0": SyntheticAtariEnv,
     "BreakoutNoFrameskip-v4": SyntheticAtariEnv,
+    "Pendulum-v1": PendulumEnv,
+    "ContinuousTarget-v0": ContinuousTargetEnv,
 }
 
 

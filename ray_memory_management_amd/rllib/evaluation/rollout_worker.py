@@ -21,6 +21,8 @@ class RolloutWorker:
     def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
                  num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
         self.config = dict(config or {})
+        # policies see their worker's slot (per-worker exploration, e.g. Ape-X epsilons)
+        self.config["worker_index"], self.config["num_workers"] = worker_index, num_workers
         self.worker_index = worker_index
         self.num_workers = num_workers
         env = self.config.get("env")
