@@ -385,6 +385,22 @@ def free(worker, oid: bytes):
             _meta_cache(worker).pop(oid, None)
 
 
+def free_unescaped(worker, oid: bytes) -> bool:
+    """Owner-side immediate free of a GPU object whose ref never left this process (no other
+    process can have mapped it). Only once its descriptor is sealed, i.e. the put's copy has
+    finished; otherwise the head's FREE_GPU path frees it later. Owner-local views still pin the
+    HBM natively (GpuStore::Delete defers while pinned)."""
+    for g in list((getattr(worker, "_gpu_stores", None) or {}).values()):
+        if g.contains(oid):
+            if worker.store.state(oid) != 2:  # kSealed
+                return False
+            worker.store.delete([oid])
+            g.delete(oid)
+            _meta_cache(worker).pop(oid, None)
+            return True
+    return False
+
+
 def _deferred(worker) -> set:
     d = getattr(worker, "_gpu_deferred_free", None)
     if d is None:

@@ -197,6 +197,11 @@ class CoreWorker:
         # removals from __del__ (GC can run them inside a ref_lock critical section of the same
         # thread): queued lock-free, applied by whoever next holds ref_lock
         self._deferred_removes: "collections.deque" = collections.deque()
+        # GPU objects put by this process whose ref never left it (never pickled, never a task
+        # arg): the owner frees their HBM as soon as its last local ref dies, without the head
+        # round trip (the reference's owner-side free when no borrower exists)
+        self._gpu_unescaped: set = set()
+        self._eager_gpu_free: List[bytes] = []
         self.local_refs: Dict[bytes, int] = {}
         self.deltas: Dict[bytes, int] = {}
         self.exported = set()
@@ -269,6 +274,8 @@ class CoreWorker:
         while not self._flusher_stop.wait(0.01):
             if self.direct is not None and self.direct.done_buf:
                 self.direct.flush()
+            if self._eager_gpu_free:
+                self._run_eager_frees()
             if getattr(self, "_gpu_deferred_free", None):
                 try:  # GPU objects whose descriptors were still pinned by readers at FREE time
                     from ray_memory_management_amd._private import gpu_object_store as gos
@@ -351,6 +358,25 @@ class CoreWorker:
                 self._drain_removes()
             finally:
                 self.ref_lock.release()
+            if self._eager_gpu_free:
+                self._run_eager_frees()
+
+    def note_escaped(self, oid: bytes):
+        """The ref is being serialized or handed to a task: another process may now borrow it."""
+        self._gpu_unescaped.discard(oid)
+
+    def _run_eager_frees(self):
+        from ray_memory_management_amd._private import gpu_object_store as gos
+
+        while self._eager_gpu_free:
+            try:
+                oid = self._eager_gpu_free.pop()
+            except IndexError:
+                return
+            try:
+                gos.free_unescaped(self, oid)
+            except Exception:
+                pass  # the head's FREE_GPU still frees it
 
     def _drain_removes(self):  # caller holds ref_lock
         q = self._deferred_removes
@@ -360,6 +386,9 @@ class CoreWorker:
             if n <= 0:
                 self.local_refs.pop(oid, None)
                 self.deltas[oid] = self.deltas.get(oid, 0) - 1
+                if oid in self._gpu_unescaped:
+                    self._gpu_unescaped.discard(oid)
+                    self._eager_gpu_free.append(oid)
             else:
                 self.local_refs[oid] = n
 
@@ -376,6 +405,8 @@ class CoreWorker:
             ref = ObjectRef(oid)
             gos.put_tensor(self, oid, value)
             self.send((P.GPU_OBJECT, oid))
+            if _owner is None:
+                self._gpu_unescaped.add(oid)
             return ref
         with self.gpu_sink():
             data, bufs, contained = ser.serialize(value)
@@ -522,6 +553,7 @@ class CoreWorker:
             if type(v) in ser._PRIMITIVES:  # hot path: small scalars pickle directly
                 return ("v", ser.pickle.dumps(v, protocol=5))
             if isinstance(v, ObjectRef):
+                self.note_escaped(v._id)
                 arg_refs.append(v.binary())
                 keep.append(v)
                 return ("r", v.binary())

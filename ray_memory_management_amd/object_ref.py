@@ -74,6 +74,9 @@ class ObjectRef:
 
     def __reduce__(self):
         ser.note_contained(self._id)
+        w = _worker
+        if w is not None:
+            w.note_escaped(self._id)
         return (_rebuild_ref, (self._id,))
 
     # ---- futures / asyncio integration (reference: ObjectRef.future(), __await__)

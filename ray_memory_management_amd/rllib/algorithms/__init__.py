@@ -19,6 +19,12 @@ ALGORITHMS = {
     "SimpleQ": ("simple_q", "SimpleQ"),
     "APEX": ("apex_dqn", "ApexDQN"),
     "APEX_DDPG": ("apex_ddpg", "ApexDDPG"),
+    "A3C": ("a3c", "A3C"),
+    "DDPPO": ("ddppo", "DDPPO"),
+    "ES": ("es", "ES"),
+    "ARS": ("ars", "ARS"),
+    "BanditLinUCB": ("bandit", "BanditLinUCB"),
+    "BanditLinTS": ("bandit", "BanditLinTS"),
 }
 
 

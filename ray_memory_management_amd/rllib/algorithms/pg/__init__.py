@@ -79,6 +79,33 @@ class OnPolicyLearner:
         stats["cur_lr"] = self.opt.param_groups[0]["lr"]
         return stats
 
+    def compute_gradients(self, batch: SampleBatch):
+        """Loss gradients for `batch` without stepping (A3C workers): ([np.ndarray per parameter], stats)."""
+        obs, act, adv, vt = self._tensors(batch)
+        self.model.zero_grad(set_to_none=True)
+        logits, values = self.model(obs)
+        total, stats = self.loss(logits.float(), values.float(), act, adv, vt)
+        total.backward()
+        grads = [(p.grad.detach().cpu().numpy().copy() if p.grad is not None else np.zeros(tuple(p.shape), np.float32))
+                 for p in self.model.parameters()]
+        self.num_steps_trained += len(act)
+        return grads, stats
+
+    def apply_gradients(self, grads) -> Dict:
+        """One optimizer step on externally computed gradients (A3C driver)."""
+        c = self.cfg
+        for g in self.opt.param_groups:
+            g["lr"] = self.lr_sched(self.num_steps_trained)
+        for p, g in zip(self.model.parameters(), grads):
+            p.grad = torch.as_tensor(np.asarray(g), device=self.device, dtype=p.dtype)
+        stats = {}
+        if c.get("grad_clip"):
+            stats["grad_gnorm"] = float(nn.utils.clip_grad_norm_(self.model.parameters(), c["grad_clip"]))
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        stats["cur_lr"] = self.opt.param_groups[0]["lr"]
+        return stats
+
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
 

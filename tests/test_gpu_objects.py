@@ -196,3 +196,46 @@ def test_async_put_then_cross_process_read(gpu_ray):
 
     want = float(big.float().sum())
     assert all(abs(v - want) <= 1e-3 * abs(want) + 1e-3 for v in ray.get([checksum.remote(r) for r in refs]))
+
+
+def test_owner_frees_unescaped_object_immediately(gpu_ray):
+    """A put whose ref never left the owner is freed by the owner the moment the last ref dies
+    (no head round trip); a ref handed to a task is not, and the owner-local view keeps its HBM."""
+    import torch
+
+    from ray_memory_management_amd._private import gpu_object_store as gos
+    from ray_memory_management_amd._private.worker import global_worker
+
+    def n_objs():
+        return sum(s["num_objects"] for s in gos.stats(global_worker).values())
+
+    base = n_objs()
+    t = torch.ones(1 << 20, device="cuda")
+    r = ray.put(t)
+    torch.cuda.synchronize()
+    deadline = time.time() + 5
+    while global_worker.store.state(r.binary()) != 2 and time.time() < deadline:
+        time.sleep(0.001)  # async put: descriptor sealed by the HIP host callback
+    assert n_objs() == base + 1
+    del r
+    assert n_objs() == base  # freed synchronously inside `del`
+    # a view obtained by get pins the HBM until the tensor dies
+    r = ray.put(t * 3)
+    torch.cuda.synchronize()
+    while global_worker.store.state(r.binary()) != 2 and time.time() < deadline:
+        time.sleep(0.001)
+    v = ray.get(r)
+    del r
+    r2 = ray.put(t * 5)  # must not reuse v's region
+    torch.cuda.synchronize()
+    assert float(v.min()) == 3.0 and float(v.max()) == 3.0
+    del v, r2
+
+    @ray.remote(num_gpus=1)
+    def total(x):
+        return float(x.sum())
+
+    r = ray.put(t)
+    out = total.remote(r)
+    assert r.binary() not in global_worker._gpu_unescaped  # escaped into a task
+    assert ray.get(out) == float(1 << 20)
