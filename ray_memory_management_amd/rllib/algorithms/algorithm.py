@@ -53,7 +53,14 @@ class Algorithm(Trainable):
         self._counters = collections.Counter()
         self._env_creator = env_creator
         self.callbacks = c.callbacks_class() if c.callbacks_class else None
-        self._setup_learner()
+        self._multi_agent = c.is_multi_agent()
+        if self._multi_agent:
+            if not hasattr(self, "_ma_learner"):
+                raise ValueError(f"{type(self).__name__} does not support multi-agent configs "
+                                 "(multi-agent PG / A2C / PPO are supported)")
+            self._setup_multi_agent()
+        else:
+            self._setup_learner()
 
     def _rollout_worker_strategy(self, c):
         """GPU rollout workers next to GPU learner actors: one placement-group bundle per learner
@@ -118,7 +125,9 @@ class Algorithm(Trainable):
             "timesteps_total": self._timesteps_total,
             "num_env_steps_sampled": self._counters["num_env_steps_sampled"],
             "num_env_steps_trained": self._counters["num_env_steps_trained"],
-            "info": {"learner": {"default_policy": {"learner_stats": results}}, **dict(self._counters)},
+            "info": {"learner": ({pid: {"learner_stats": st} for pid, st in results.items()}
+                                 if getattr(self, "_multi_agent", False) else
+                                 {"default_policy": {"learner_stats": results}}), **dict(self._counters)},
         }
         if c.evaluation_interval and (self.iteration + 1) % c.evaluation_interval == 0:
             out["evaluation"] = self.evaluate()
@@ -129,6 +138,48 @@ class Algorithm(Trainable):
     def training_step(self) -> Dict:
         raise NotImplementedError
 
+    # ------------------------------------------------------------------ multi-agent
+    def _setup_multi_agent(self):
+        """One learner per trainable policy (reference: policy_map + policies_to_train)."""
+        local = self.workers.local_worker()
+        self.ma_learners = {pid: self._ma_learner(pid, local.policy_map[pid]) for pid in local.policies_to_train}
+        self._ma_sync()
+
+    def _ma_sync(self):
+        w = {pid: ln.get_weights() for pid, ln in self.ma_learners.items()}
+        self.workers.local_worker().set_weights(w)
+        self.workers.sync_weights(w)
+
+    def _ma_training_step(self) -> Dict:
+        import ray_memory_management_amd as ray
+        from ray_memory_management_amd.rllib.sample_batch import concat_samples
+
+        c = self.algo_config
+        parts, steps = {}, 0
+        while steps < c.train_batch_size:
+            if self.workers.remote_workers():
+                new = ray.get([w.sample.remote() for w in self.workers.remote_workers()])
+            else:
+                new = [self.workers.local_worker().sample()]
+            for mb in new:
+                steps += mb.count
+                for pid, b in mb.policy_batches.items():
+                    parts.setdefault(pid, []).append(b)
+        self._counters["num_env_steps_sampled"] += steps
+        self._timesteps_total += steps
+        stats = {}
+        for pid, ln in self.ma_learners.items():
+            if pid in parts:
+                b = concat_samples(parts[pid])
+                stats[pid] = self._ma_update(ln, b)
+                self._counters["num_agent_steps_trained"] += b.count
+        self._counters["num_env_steps_trained"] += steps
+        self._ma_sync()
+        return stats
+
+    def _ma_update(self, learner, batch) -> Dict:
+        return learner.update(batch)
+
     def evaluate(self) -> Dict:
         c = self.algo_config
         rewards, lens = RolloutWorker.evaluate_episodes(self.get_policy(), self._env_creator, c.env, c.env_config,
@@ -138,10 +189,12 @@ class Algorithm(Trainable):
                 "episodes_this_iter": len(rewards)}
 
     def get_policy(self, policy_id: str = "default_policy"):
+        if getattr(self, "_multi_agent", False):
+            return self.workers.local_worker().get_policy(policy_id)
         return self.workers.local_worker().policy
 
     def compute_single_action(self, observation, *, explore: Optional[bool] = None, policy_id="default_policy"):
-        return self.get_policy().compute_single_action(observation, explore=bool(explore))
+        return self.get_policy(policy_id).compute_single_action(observation, explore=bool(explore))
 
     def get_weights(self):
         return self.get_policy().get_weights()

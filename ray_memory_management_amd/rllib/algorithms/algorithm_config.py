@@ -69,6 +69,8 @@ class AlgorithmConfig:
         self.output_compress_columns = ["obs", "new_obs"]
         self.output_max_file_size = 64 * 1024 * 1024
         self.off_policy_estimation_methods = {}
+        # multi-agent (reference AlgorithmConfig.multi_agent): policies {id: PolicySpec | tuple | None}
+        self.multiagent: Dict[str, Any] = {"policies": {}, "policy_mapping_fn": None, "policies_to_train": None}
 
     # ---- builder methods (each returns self)
     def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None,
@@ -201,6 +203,19 @@ class AlgorithmConfig:
         if off_policy_estimation_methods is not None:
             self.off_policy_estimation_methods = dict(off_policy_estimation_methods)
         return self
+
+    def multi_agent(self, *, policies=None, policy_mapping_fn=None, policies_to_train=None,
+                    **kw) -> "AlgorithmConfig":
+        if policies is not None:
+            self.multiagent["policies"] = policies
+        if policy_mapping_fn is not None:
+            self.multiagent["policy_mapping_fn"] = policy_mapping_fn
+        if policies_to_train is not None:
+            self.multiagent["policies_to_train"] = list(policies_to_train)
+        return self
+
+    def is_multi_agent(self) -> bool:
+        return bool(self.multiagent.get("policies"))
 
     def fault_tolerance(self, *, recreate_failed_workers=None, **kw) -> "AlgorithmConfig":
         if recreate_failed_workers is not None:

@@ -141,7 +141,14 @@ class PG(Algorithm):
         self.workers.local_worker().set_weights(w)
         self.workers.sync_weights(w)
 
+    def _ma_learner(self, pid, policy):
+        dev = "cuda" if self.algo_config.num_gpus and torch.cuda.is_available() else "cpu"
+        cfg = {k: v for k, v in self._learner_cfg().items() if v is not None}
+        return self._learner_class(copy.deepcopy(policy.model), cfg, device=dev)
+
     def training_step(self) -> Dict:
+        if self._multi_agent:
+            return self._ma_training_step()
         c = self.algo_config
         batch = self.workers.synchronous_parallel_sample(c.train_batch_size)
         self._counters["num_env_steps_sampled"] += batch.count

@@ -400,3 +400,53 @@ def make_env(env, config=None):
     if callable(env):
         return env(config or {})
     raise ValueError(f"invalid env {env!r}")
+
+
+class MultiAgentEnv(Env):
+    """Multi-agent env API (reference rllib/env/multi_agent_env.py): ``reset() -> {agent_id: obs}``;
+    ``step({agent_id: action}) -> (obs, rewards, dones, infos)`` as dicts keyed by the agents that
+    act next, ``dones["__all__"]`` ends the episode. `observation_space` / `action_space` are the
+    (shared) per-agent spaces."""
+
+    def get_agent_ids(self):
+        return set(getattr(self, "_agent_ids", set()))
+
+
+def make_multi_agent(env_name_or_creator):
+    """A MultiAgentEnv class running ``num_agents`` independent copies of a single-agent env
+    (reference multi_agent_env.make_multi_agent); agent i's episode ends with its own copy and the
+    whole episode when every copy is done."""
+
+    class _MultiEnv(MultiAgentEnv):
+        def __init__(self, config=None):
+            config = dict(config or {})
+            n = int(config.pop("num_agents", 1))
+            mk = (lambda c: make_env(env_name_or_creator, c)) if isinstance(env_name_or_creator, str) \
+                else env_name_or_creator
+            self.agents = [mk(config) for _ in range(n)]
+            self._agent_ids = set(range(n))
+            self.observation_space = self.agents[0].observation_space
+            self.action_space = self.agents[0].action_space
+            self.dones = set()
+
+        def reset(self, *, seed=None):
+            self.dones = set()
+            out = {}
+            for i, a in enumerate(self.agents):
+                out[i] = a.reset(seed=None if seed is None else seed + i) if seed is not None else a.reset()
+            return out
+
+        def step(self, action_dict):
+            obs, rew, done, info = {}, {}, {}, {}
+            for i, act in action_dict.items():
+                obs[i], rew[i], done[i], info[i] = self.agents[i].step(act)
+                if done[i]:
+                    self.dones.add(i)
+            done["__all__"] = len(self.dones) == len(self.agents)
+            return obs, rew, done, info
+
+    return _MultiEnv
+
+
+MultiAgentCartPole = make_multi_agent("CartPole-v1")
+_REGISTRY["MultiAgentCartPole-v0"] = MultiAgentCartPole

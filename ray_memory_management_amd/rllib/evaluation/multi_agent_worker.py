@@ -1,0 +1,186 @@
+"""Multi-agent rollout worker.
+
+Parity: reference rllib/evaluation/rollout_worker.py with a MultiAgentEnv (policy_map,
+policy_mapping_fn(agent_id, episode, worker), policies_to_train), rllib/evaluation/collectors/
+simple_list_collector.py (per-agent trajectory buffers postprocessed per policy, bootstrapped with
+the policy's value on truncation) and rllib/policy/policy_map.py. `sample()` returns a
+MultiAgentBatch {policy_id: SampleBatch} covering `rollout_fragment_length` env steps.
+"""
+from __future__ import annotations
+
+import importlib
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ray_memory_management_amd.rllib.env import make_env
+from ray_memory_management_amd.rllib.policy import TorchPolicy, compute_gae_for_trajectories
+from ray_memory_management_amd.rllib.sample_batch import MultiAgentBatch, SampleBatch, concat_samples
+
+
+def _resolve_cls(c):
+    if c is None:
+        return TorchPolicy
+    if isinstance(c, str):
+        mod, _, name = c.rpartition(".")
+        return getattr(importlib.import_module(mod), name)
+    return c
+
+
+def policy_specs(config: Dict, env) -> Dict[str, tuple]:
+    """{pid: (policy_cls, obs_space, act_space, config_overrides)} from config["multiagent"]["policies"]
+    (a set/list of ids, or a dict of PolicySpec / tuples with None entries inferred from the env)."""
+    pols = (config.get("multiagent") or {}).get("policies") or {}
+    out = {}
+    items = pols.items() if isinstance(pols, dict) else [(p, None) for p in pols]
+    for pid, spec in items:
+        cls = obs = act = None
+        over: Dict = {}
+        if spec is not None:
+            if hasattr(spec, "policy_class"):
+                cls, obs, act, over = spec.policy_class, spec.observation_space, spec.action_space, spec.config or {}
+            else:
+                cls, obs, act, over = (list(spec) + [None] * 4)[:4]
+                over = over or {}
+        out[pid] = (_resolve_cls(cls or config.get("policy_class")), obs or env.observation_space,
+                    act or env.action_space, over)
+    return out
+
+
+class MultiAgentRolloutWorker:
+    def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
+                 num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
+        import torch
+
+        self.config = dict(config or {})
+        self.config["worker_index"], self.config["num_workers"] = worker_index, num_workers
+        self.worker_index = worker_index
+        env_config = dict(self.config.get("env_config") or {})
+        self.env = env_creator(env_config) if env_creator is not None else make_env(self.config.get("env"), env_config)
+        base_seed = seed if seed is not None else self.config.get("seed")
+        if base_seed is not None:
+            torch.manual_seed(int(base_seed) + worker_index)
+        torch.set_num_threads(max(1, int(self.config.get("num_cpus_per_worker", 1) or 1)))
+        ma = self.config.get("multiagent") or {}
+        self.policy_mapping_fn = ma.get("policy_mapping_fn") or (lambda agent_id, episode=None, worker=None, **kw:
+                                                                 "default_policy")
+        self.policy_map = {}
+        for pid, (cls, obs, act, over) in policy_specs(self.config, self.env).items():
+            self.policy_map[pid] = cls(obs, act, {**self.config, **over}, device="cpu")
+        self.policies_to_train = list(ma.get("policies_to_train") or self.policy_map)
+        self._obs = self.env.reset(seed=None if base_seed is None else int(base_seed) * 1000 + worker_index)
+        self._episode = 0
+        self._agent_pid: Dict = {}
+        self._ep_reward = 0.0
+        self._ep_len = 0
+        self._completed: List[tuple] = []
+        self._traj: Dict = {}
+
+    @property
+    def policy(self):  # single-policy accessors used by Algorithm helpers
+        return next(iter(self.policy_map.values()))
+
+    def _pid(self, agent_id):
+        pid = self._agent_pid.get(agent_id)
+        if pid is None:
+            pid = self._agent_pid[agent_id] = self.policy_mapping_fn(agent_id, self._episode, self)
+        return pid
+
+    def _flush(self, agent_id, last_obs, done: bool, out: Dict[str, List[SampleBatch]]):
+        tr = self._traj.pop(agent_id, None)
+        if not tr or not tr["obs"]:
+            return
+        pid = self._pid(agent_id)
+        pol = self.policy_map[pid]
+        rew = np.asarray(tr["rew"], np.float32)[:, None]
+        vf = np.asarray(tr["vf"], np.float32)[:, None]
+        dn = np.zeros_like(rew)
+        dn[-1, 0] = 1.0 if done else 0.0
+        last_v = np.zeros(1, np.float32) if done else np.asarray(pol.value(np.asarray(last_obs)[None]), np.float32)
+        if not self.config.get("use_critic", True):
+            vf, last_v = np.zeros_like(vf), np.zeros_like(last_v)
+        adv, ret = compute_gae_for_trajectories(rew, vf, dn, last_v, self.config.get("gamma", 0.99),
+                                                self.config.get("lambda", self.config.get("lambda_", 1.0)))
+        b = SampleBatch({SampleBatch.OBS: np.stack(tr["obs"]), SampleBatch.ACTIONS: np.asarray(tr["act"]),
+                         SampleBatch.REWARDS: rew[:, 0], SampleBatch.DONES: dn[:, 0],
+                         SampleBatch.NEXT_OBS: np.stack(tr["nobs"]),
+                         SampleBatch.ACTION_LOGP: np.asarray(tr["logp"], np.float32),
+                         SampleBatch.VF_PREDS: vf[:, 0],
+                         SampleBatch.ACTION_DIST_INPUTS: np.stack(tr["logits"]).astype(np.float32),
+                         SampleBatch.ADVANTAGES: adv[:, 0].astype(np.float32),
+                         SampleBatch.VALUE_TARGETS: ret[:, 0].astype(np.float32),
+                         SampleBatch.EPS_ID: np.full(len(rew), self._episode, np.int64),
+                         SampleBatch.AGENT_INDEX: np.full(len(rew), hash(agent_id) & 0x7FFFFFFF, np.int64)})
+        out.setdefault(pid, []).append(b)
+
+    def sample(self) -> MultiAgentBatch:
+        T = int(self.config.get("rollout_fragment_length", 200))
+        explore = self.config.get("explore", True)
+        out: Dict[str, List[SampleBatch]] = {}
+        for _ in range(T):
+            by_pid: Dict[str, list] = {}
+            for aid, o in self._obs.items():
+                by_pid.setdefault(self._pid(aid), []).append(aid)
+            actions = {}
+            for pid, aids in by_pid.items():
+                obs = np.stack([np.asarray(self._obs[a]) for a in aids])
+                a, _, extra = self.policy_map[pid].compute_actions(obs, explore=explore)
+                for j, aid in enumerate(aids):
+                    actions[aid] = a[j]
+                    tr = self._traj.setdefault(aid, {k: [] for k in ("obs", "act", "rew", "nobs", "logp", "vf",
+                                                                    "logits")})
+                    tr["obs"].append(obs[j])
+                    tr["act"].append(a[j])
+                    tr["logp"].append(extra[SampleBatch.ACTION_LOGP][j])
+                    tr["vf"].append(extra[SampleBatch.VF_PREDS][j])
+                    tr["logits"].append(extra[SampleBatch.ACTION_DIST_INPUTS][j])
+            nobs, rew, done, _ = self.env.step({k: (int(v) if np.ndim(v) == 0 else v) for k, v in actions.items()})
+            for aid in actions:
+                tr = self._traj[aid]
+                tr["rew"].append(float(rew.get(aid, 0.0)))
+                tr["nobs"].append(np.asarray(nobs.get(aid, self._obs[aid])))
+                self._ep_reward += float(rew.get(aid, 0.0))
+                if done.get(aid, False):
+                    self._flush(aid, nobs.get(aid, self._obs[aid]), True, out)
+            self._ep_len += 1
+            if done.get("__all__", False):
+                for aid in list(self._traj):
+                    self._flush(aid, nobs.get(aid, self._obs.get(aid)), True, out)
+                self._completed.append((self._ep_reward, self._ep_len))
+                self._ep_reward, self._ep_len = 0.0, 0
+                self._episode += 1
+                self._agent_pid = {}
+                self._obs = self.env.reset()
+            else:
+                self._obs = {k: v for k, v in nobs.items() if not done.get(k, False)}
+        for aid in list(self._traj):  # fragment boundary: bootstrap unfinished trajectories
+            self._flush(aid, self._obs.get(aid), False, out)
+        return MultiAgentBatch({pid: concat_samples(bs) for pid, bs in out.items()}, T)
+
+    # -- weights / metrics (weights are {policy_id: state_dict})
+    def get_weights(self, policies=None):
+        return {pid: p.get_weights() for pid, p in self.policy_map.items() if policies is None or pid in policies}
+
+    def set_weights(self, weights, global_vars=None):
+        import torch
+
+        for pid, w in weights.items():
+            if pid in self.policy_map:
+                self.policy_map[pid].set_weights({k: (v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v)))
+                                                  for k, v in w.items()})
+
+    def get_policy(self, policy_id: str = "default_policy"):
+        return self.policy_map.get(policy_id)
+
+    def foreach_policy(self, fn):
+        return [fn(p, pid) for pid, p in self.policy_map.items()]
+
+    def get_metrics(self):
+        out, self._completed = self._completed, []
+        return out
+
+    def apply(self, fn, *args):
+        return fn(self, *args)
+
+    def stop(self):
+        pass

@@ -23,6 +23,7 @@ class SampleBatch(dict):
     DONES = "dones"
     INFOS = "infos"
     EPS_ID = "eps_id"
+    AGENT_INDEX = "agent_index"
     T = "t"
     ACTION_LOGP = "action_logp"
     ACTION_DIST_INPUTS = "action_dist_inputs"
