@@ -88,3 +88,81 @@ def test_gpu_tensor_collectives(backend):
         _check(outs, 2)
     finally:
         ray.shutdown()
+
+
+@ray.remote(num_cpus=0)
+class _Ops(_WorkerBase):
+    def ops(self, group):
+        r = col.get_rank(group)
+        n = col.get_collective_group_size(group)
+        out = {}
+        t = torch.full((3,), float(r + 2))
+        col.reduce(t, 1, group)  # only the destination holds the sum
+        out["reduce"] = t.tolist()
+        t = torch.full((2,), float(r + 2))
+        col.allreduce(t, group, op=col.ReduceOp.PRODUCT)
+        out["prod"] = t.tolist()
+        t = torch.full((2,), float(r + 2))
+        col.allreduce(t, group, op=col.ReduceOp.MIN)
+        out["min"] = t.tolist()
+        work = col.allreduce_async(torch.ones(5) * (r + 1), group)
+        work.wait()
+        inp = torch.arange(n * 2, dtype=torch.float32) + 100 * r
+        o = torch.empty(n * 2)
+        col.alltoall(o, inp, group_name=group)
+        out["alltoall"] = o.tolist()
+        # uneven splits: rank r sends (i + 1) rows to rank i
+        ins = [i + 1 for i in range(n)]
+        inp = torch.cat([torch.full((i + 1,), float(10 * r + i)) for i in range(n)])
+        o = torch.empty((r + 1) * n)
+        col.alltoall(o, inp, [r + 1] * n, ins, group_name=group)
+        out["alltoall_v"] = o.tolist()
+        try:
+            col.send(torch.zeros(1), r, group)
+        except RuntimeError as e:
+            out["self_send"] = str(e)
+        col.destroy_collective_group(group)
+        out["after_destroy"] = (col.is_group_initialized(group), col.get_rank(group))
+        return out
+
+    def reinit(self, world, rank, group):
+        col.init_collective_group(world, rank, "gloo", group)
+        try:
+            col.init_collective_group(world, rank, "gloo", group)
+        except RuntimeError as e:
+            dup = str(e)
+        t = torch.tensor([float(rank)])
+        col.allreduce(t, group)
+        col.destroy_collective_group(group)
+        return dup, float(t[0])
+
+
+def test_gloo_reduce_product_min_alltoall_and_errors(ray_start):
+    n = 3
+    ws = [_Ops.remote() for _ in range(n)]
+    col.create_collective_group(ws, n, list(range(n)), backend="gloo", group_name="ops")
+    outs = ray.get([w.ops.remote("ops") for w in ws])
+    assert outs[1]["reduce"] == [2.0 + 3.0 + 4.0] * 3
+    for r, o in enumerate(outs):
+        assert o["prod"] == [24.0, 24.0] and o["min"] == [2.0, 2.0]
+        # alltoall: rank r receives slice r (2 rows) of every rank's input
+        assert o["alltoall"] == [float(100 * s + 2 * r + j) for s in range(n) for j in range(2)]
+        assert o["alltoall_v"] == [float(10 * s + r) for s in range(n) for _ in range(r + 1)]
+        assert "current rank" in o["self_send"]
+        assert o["after_destroy"] == (False, -1)
+
+
+def test_group_join_inside_tasks_and_double_init_rejected(ray_start):
+    ws = [_Ops.remote() for _ in range(2)]
+    outs = ray.get([w.reinit.remote(2, i, "joined") for i, w in enumerate(ws)])
+    for dup, s in outs:
+        assert "twice" in dup and s == 1.0
+
+
+def test_invalid_rank_and_uninitialized_group():
+    with pytest.raises(ValueError):
+        col.init_collective_group(2, 5, "gloo", "bad")
+    with pytest.raises(RuntimeError, match="not initialized"):
+        col.allreduce(torch.zeros(1), "missing")
+    with pytest.raises(ValueError, match="_collective_init"):
+        col.create_collective_group([object()], 1, [0], backend="gloo", group_name="x")

@@ -210,3 +210,79 @@ def test_preprocessors(ray_data):
                Concatenator(include=["a", "b"]))
     res = ch.fit_transform(ds).to_pandas()
     assert "concat_out" in res.columns and len(res["concat_out"][0]) == 2
+
+
+def test_sampling_and_splits(ray_data):
+    ray, data = ray_data
+    ds = data.range(1000, parallelism=8)
+    s = ds.random_sample(0.1, seed=0).take_all()
+    assert 50 < len(s) < 150 and set(s) <= set(range(1000))
+    with pytest.raises(ValueError):
+        ds.random_sample(1.5)
+    parts = ds.split_at_indices([100, 350])
+    assert [p.count() for p in parts] == [100, 250, 650]
+    assert parts[1].take(2) == [100, 101]
+    a, b = ds.split_proportionately([0.25])
+    assert a.count() == 250 and b.count() == 750
+    with pytest.raises(ValueError):
+        ds.split_proportionately([0.6, 0.5])
+    tr, te = ds.train_test_split(0.2)
+    assert tr.count() == 800 and te.count() == 200 and te.take(1) == [800]
+    tr, te = ds.train_test_split(100, shuffle=True, seed=1)
+    assert te.count() == 100 and sorted(tr.take_all() + te.take_all()) == list(range(1000))
+    r = ds.randomize_block_order(seed=3)
+    assert sorted(r.take_all()) == list(range(1000)) and r.num_blocks() == 8
+    eq = ds.split(3, equal=True)
+    assert len({p.count() for p in eq}) == 1
+
+
+def test_from_sources_and_column_selection(ray_data):
+    ray, data = ray_data
+    import pyarrow as pa
+
+    df = pd.DataFrame({"x": np.arange(10), "y": np.arange(10) * 2.0, "z": list("abcdefghij")})
+    ds = data.from_pandas([df.iloc[:5], df.iloc[5:]])
+    assert ds.num_blocks() == 2 and ds.count() == 10
+    sel = ds.select_columns(["x", "z"]).to_pandas()
+    assert list(sel.columns) == ["x", "z"] and sel["z"].tolist() == list("abcdefghij")
+    t = pa.table({"k": [3, 1, 2]})
+    assert sorted(r["k"] for r in data.from_arrow(t).take_all()) == [1, 2, 3]
+    arr = np.arange(24, dtype=np.float32).reshape(6, 4)
+    nd = data.from_numpy([arr[:3], arr[3:]])
+    assert nd.count() == 6
+    got = np.concatenate([ray.get(r) for r in nd.to_numpy_refs()])
+    np.testing.assert_array_equal(got.reshape(6, 4), arr)
+    assert sum(ray.get(r).num_rows for r in ds.to_arrow_refs()) == 10
+    assert ds.size_bytes() > 0
+    desc = ds.sort("y", descending=True).take(2)
+    assert [r["x"] for r in desc] == [9, 8]
+
+
+def test_torch_iteration(ray_data):
+    ray, data = ray_data
+    import torch
+
+    ds = data.from_items([{"f1": float(i), "f2": float(2 * i), "label": i % 2} for i in range(20)], parallelism=3)
+    batches = list(ds.iter_torch_batches(batch_size=6))
+    assert [len(b["f1"]) for b in batches] == [6, 6, 6, 2]
+    assert isinstance(batches[0]["f1"], torch.Tensor) and batches[0]["f2"][1].item() == 2.0
+    dropped = list(ds.iter_torch_batches(batch_size=6, drop_last=True))
+    assert len(dropped) == 3
+    shuf = torch.cat([b["f1"] for b in ds.iter_torch_batches(batch_size=5, local_shuffle_buffer_size=10,
+                                                             local_shuffle_seed=0)])
+    assert sorted(shuf.tolist()) == [float(i) for i in range(20)] and shuf.tolist() != sorted(shuf.tolist())
+    tds = ds.to_torch(label_column="label", batch_size=4)
+    feats, labels = next(iter(tds))
+    assert feats.shape == (4, 2) and labels.shape == (4, 1)
+
+
+def test_pipeline_repeat_and_window(ray_data):
+    ray, data = ray_data
+    ds = data.range(12, parallelism=4)
+    pipe = ds.repeat(3)
+    assert sum(1 for _ in pipe.iter_rows()) == 36
+    w = ds.window(blocks_per_window=2).map(lambda x: x + 1)
+    seen = [sorted(wd.take_all()) for wd in w.iter_datasets()]
+    assert len(seen) == 2 and seen[0] == list(range(1, 7)) and seen[1] == list(range(7, 13))
+    with pytest.raises(ValueError):
+        ds.repeat(0)
