@@ -243,6 +243,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ctr"), py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"), py::arg("lout"),
      py::arg("act_now"), py::arg("B"), py::arg("A"), py::arg("stream"), py::arg("ldl") = 0, py::arg("ldv") = 0);
 
+  m.def("frame_push", [](uint64_t stack, uint64_t new_frames, uint64_t buf_obs, uint64_t t_ptr, int64_t B, int64_t hw,
+                         uint64_t stream) {
+    frame_push(P<uint8_t>(stack), P<const uint8_t>(new_frames), buf_obs ? P<uint8_t>(buf_obs) : nullptr,
+               t_ptr ? P<const int64_t>(t_ptr) : nullptr, B, hw, S(stream));
+  }, py::arg("stack"), py::arg("new_frames"), py::arg("buf_obs"), py::arg("t_ptr"), py::arg("B"), py::arg("hw"),
+     py::arg("stream"));
   m.def("synth_env_step", [](uint64_t frames, uint64_t pool, uint64_t actions, uint64_t tenv, uint64_t ctr_t,
                              uint64_t buf_obs, uint64_t buf_rew, uint64_t buf_done, uint32_t seed, int episode_len,
                              int64_t B, uint64_t stream, uint64_t bump, uint64_t done) {

@@ -812,3 +812,49 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
 
 }  // namespace hip
 }  // namespace rmm
+
+// ---------------------------------------------------------------------------------------------
+// K19: device-resident frame stacks for hybrid rollout workers. The CPU env uploads only the
+// newest frame per env ([B, HW] u8, pinned H2D); this kernel shifts the HBM stack [B, 4, HW] one
+// frame, appends the new frame and stores the resulting observation as rollout row t of buf_obs
+// ([T, B, 4, HW]; row index read on the device so the step can live in a HIP graph). One thread
+// owns a 16-byte pixel chunk of one env across all 4 channels, so the in-place shift is race free.
+// Replaces: full-stack numpy shift on the CPU + 4x larger H2D copy + a separate row-store launch.
+__global__ void __launch_bounds__(256) k_frame_push(uint8_t* __restrict__ stack, const uint8_t* __restrict__ nf,
+                                                    uint8_t* __restrict__ buf_obs, const int64_t* __restrict__ t_ptr,
+                                                    int64_t B, int64_t chunks) {
+  const int64_t total = B * chunks;
+  const int64_t trow = buf_obs ? *t_ptr : 0;
+  const int64_t HW = chunks * 16;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = i / chunks, c = i - b * chunks;
+    uint4* s = reinterpret_cast<uint4*>(stack + b * 4 * HW) + c;
+    const int64_t cs = chunks;  // channel stride in uint4
+    const uint4 f1 = s[cs], f2 = s[2 * cs], f3 = s[3 * cs];
+    const uint4 n = reinterpret_cast<const uint4*>(nf + b * HW)[c];
+    s[0] = f1;
+    s[cs] = f2;
+    s[2 * cs] = f3;
+    s[3 * cs] = n;
+    if (buf_obs) {
+      uint4* o = reinterpret_cast<uint4*>(buf_obs + (trow * B + b) * 4 * HW) + c;
+      o[0] = f1;
+      o[cs] = f2;
+      o[2 * cs] = f3;
+      o[3 * cs] = n;
+    }
+  }
+}
+
+void frame_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* buf_obs, const int64_t* t_ptr, int64_t B,
+                int64_t hw, hipStream_t stream) {
+  if (hw % 16 != 0) throw std::runtime_error("frame_push: frame bytes must be a multiple of 16");
+  if ((reinterpret_cast<uintptr_t>(stack) | reinterpret_cast<uintptr_t>(new_frames) |
+       reinterpret_cast<uintptr_t>(buf_obs)) & 15)
+    throw std::runtime_error("frame_push: buffers must be 16-byte aligned");
+  const int64_t chunks = hw / 16, total = B * chunks;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_frame_push, dim3(uint32_t(blocks)), dim3(256), 0, stream, stack, new_frames, buf_obs, t_ptr,
+                     B, chunks);
+  RMM_HIP_CHECK(hipGetLastError());
+}

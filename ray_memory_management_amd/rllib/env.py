@@ -284,6 +284,27 @@ class CPUSyntheticAtariVectorEnv:
         self.t[done] = 0
         return self.frames, rew, done.astype(np.float32)
 
+    # frames never reset at episode boundaries (truncation only): a consumer may keep the stacks
+    frame_stack_continuous = True
+
+    def vector_step_frames(self, actions, out: np.ndarray):
+        """Same transition and RNG stream as `vector_step`, but only the NEWEST frame of every env is
+        produced, written straight into `out` ([n, 84, 84] u8, e.g. pinned staging memory); the
+        consumer keeps the frame stacks (hybrid workers: in HBM, K19). `self.frames` is not
+        maintained in this mode. Returns (rewards, dones)."""
+        a = np.asarray(actions, dtype=np.int64) % self.num_actions
+        k = self.rng.integers(0, 64, size=self.num_envs)
+        np.take(self._pools_flat, a * 64 + k, axis=0, out=out)
+        self.t += 1
+        rew = (self.rng.random(self.num_envs) < 0.05).astype(np.float32)
+        done = self.t >= self.episode_len
+        self.t[done] = 0
+        return rew, done.astype(np.float32)
+
+    @property
+    def _pools_flat(self):
+        return self._pools.reshape(-1, 84, 84)
+
 
 class GPUSyntheticAtariVectorEnv:
     """Device-resident vectorised synthetic Atari env: B envs, frames [B, 4, 84, 84] uint8 on the

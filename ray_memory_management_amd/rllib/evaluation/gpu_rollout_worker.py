@@ -116,6 +116,17 @@ class _EnvGroup:
         self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)  # {rng counter, rollout row}
         self.fused = hasattr(model, "forward_sample") and getattr(
             getattr(model, "heads", None), "out_features", -1) == A + 1
+        # device frame stacks (K19): upload only each env's newest frame, shift the stack in HBM
+        self.device_stack = (bool(getattr(env, "frame_stack_continuous", False)) and hasattr(env, "vector_step_frames")
+                             and obs.ndim == 4 and obs.shape[1] == 4 and (obs.shape[2] * obs.shape[3]) % 16 == 0)
+        if self.device_stack:
+            self.hw = obs.shape[2] * obs.shape[3]
+            self.h_new = torch.empty((n,) + obs.shape[2:], dtype=torch.uint8).pin_memory()
+            self.s_new = torch.empty((n,) + obs.shape[2:], dtype=torch.uint8, device=dev)
+            # stack state such that the first push yields the reset observation
+            init = torch.from_numpy(np.ascontiguousarray(obs))
+            self.s_obs[:, 1:].copy_(init[:, :3].to(dev))
+            self.h_new.copy_(init[:, 3])
         self.graph = None
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.ep_rew = np.zeros(n, dtype=np.float64)
@@ -126,9 +137,14 @@ class _EnvGroup:
 
         from ray_memory_management_amd._native import require_hip
 
-        self.s_obs.copy_(self.h_obs, non_blocking=True)
         t, ctr = self.ctr_t[1:2], self.ctr_t[0:1]
-        self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
+        if self.device_stack:
+            self.s_new.copy_(self.h_new, non_blocking=True)
+            require_hip().frame_push(self.s_obs.data_ptr(), self.s_new.data_ptr(), self.buf_obs.data_ptr(),
+                                     t.data_ptr(), self.n, self.hw, torch.cuda.current_stream().cuda_stream)
+        else:
+            self.s_obs.copy_(self.h_obs, non_blocking=True)
+            self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
         if not (self.fused and self.model.forward_sample(self.s_obs, t, ctr, self.seed, self.buf_act, self.buf_logp,
                                                           self.buf_vf, self.buf_logits, self.act_now)):
             hd = self.model.forward_heads(self.s_obs)
@@ -145,9 +161,12 @@ class _EnvGroup:
         import torch
 
         with torch.cuda.stream(stream):
+            saved = self.s_obs.clone() if self.device_stack else None
             for _ in range(2):
                 self.policy_step()
             self.ctr_t[1].zero_()
+            if saved is not None:  # warm-up pushes must not advance the frame stacks
+                self.s_obs.copy_(saved)
         stream.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream):
@@ -169,8 +188,11 @@ class _EnvGroup:
         return ev
 
     def env_step(self, t: int, completed: list):
-        obs, rew, done = self.env.vector_step(self.h_act.numpy().copy())
-        self.h_obs.numpy()[:] = obs
+        if self.device_stack:
+            rew, done = self.env.vector_step_frames(self.h_act.numpy().copy(), self.h_new.numpy())
+        else:
+            obs, rew, done = self.env.vector_step(self.h_act.numpy().copy())
+            self.h_obs.numpy()[:] = obs
         self.h_rew.numpy()[t] = rew
         self.h_done.numpy()[t] = done
         self.ep_rew += rew
@@ -272,8 +294,12 @@ class HybridRolloutWorker(GPURolloutWorker):
             with torch.cuda.stream(st):
                 parts = []
                 for g in G:
-                    g.s_obs.copy_(g.h_obs, non_blocking=True)
-                    _, last_v = self.model(g.s_obs)
+                    if g.device_stack:  # observation after the last env step (pushed next fragment)
+                        g.s_new.copy_(g.h_new, non_blocking=True)
+                        _, last_v = self.model(torch.cat([g.s_obs[:, 1:], g.s_new.unsqueeze(1)], dim=1))
+                    else:
+                        g.s_obs.copy_(g.h_obs, non_blocking=True)
+                        _, last_v = self.model(g.s_obs)
                     parts.append((g.buf_obs, g.buf_logits, g.buf_logp, g.buf_vf,
                                   g.h_rew.to(self.device, non_blocking=True),
                                   g.h_done.to(self.device, non_blocking=True), g.buf_act, last_v.reshape(-1)))

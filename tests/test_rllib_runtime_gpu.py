@@ -212,6 +212,44 @@ def test_hybrid_worker_fragment_consistent(cuda):
     assert len(w.get_metrics()) > 0  # episode_len 30 < 3 x 16 steps
 
 
+def test_k19_frame_push_matches_torch(cuda):
+    import torch
+
+    from ray_memory_management_amd._native import require_hip
+
+    B, T, hw = 5, 3, 84 * 84
+    g = torch.Generator(device="cuda").manual_seed(0)
+    stack = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda", generator=g)
+    new = torch.randint(0, 256, (B, 84, 84), dtype=torch.uint8, device="cuda", generator=g)
+    buf = torch.zeros((T, B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    t = torch.tensor([2], dtype=torch.int64, device="cuda")
+    want = torch.cat([stack[:, 1:], new.unsqueeze(1)], dim=1)
+    require_hip().frame_push(stack.data_ptr(), new.data_ptr(), buf.data_ptr(), t.data_ptr(), B, hw,
+                             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(stack, want) and torch.equal(buf[2], want) and int(buf[:2].sum()) == 0
+
+
+def test_hybrid_device_frame_stacks_match_host_stacks(cuda):
+    """K19 path (newest frame uploaded, stacks kept in HBM) yields the same fragments, bit for bit,
+    as uploading the CPU env's full frame stacks every step."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 20}, "num_envs_per_worker": 6,
+           "rollout_fragment_length": 12, "seed": 5}
+    a = HybridRolloutWorker(config=cfg)
+    b = HybridRolloutWorker(config=cfg)
+    assert all(g.device_stack for g in a.groups)
+    for g in b.groups:
+        g.device_stack = False  # h_obs still holds the reset stacks: full-stack upload path
+    for _ in range(3):
+        fa, fb = a.sample(), b.sample()
+        assert torch.equal(fa["obs"], fb["obs"])
+        assert torch.equal(fa["_raw"], fb["_raw"]) and torch.equal(fa["_boot"], fb["_boot"])
+
+
 def test_ppo_hybrid_rollouts(cuda):
     """PPO with CPU-env / GPU-policy rollout workers co-located with the learner actor."""
     import ray_memory_management_amd as ray
