@@ -20,6 +20,8 @@ ALGORITHMS = {
     "APEX": ("apex_dqn", "ApexDQN"),
     "APEX_DDPG": ("apex_ddpg", "ApexDDPG"),
     "A3C": ("a3c", "A3C"),
+    "CQL": ("cql", "CQL"),
+    "CRR": ("crr", "CRR"),
     "DDPPO": ("ddppo", "DDPPO"),
     "ES": ("es", "ES"),
     "ARS": ("ars", "ARS"),

@@ -91,6 +91,16 @@ class ContinuousActorCritic(nn.Module):
         logp = logp - torch.log(1.0 - t.pow(2) + 1e-6).sum(-1) - torch.log(self.a_half).sum()
         return self.scale(t), logp
 
+    def logp_of(self, obs, act):
+        """log π(a|s) of given (dataset) actions under the tanh-squashed Gaussian (CQL's BC phase,
+        CRR's weighted regression): invert the squash, Gaussian log-density plus the Jacobian."""
+        h = self.actor(obs.flatten(1).float())
+        mean, log_std = h[:, :self.act_dim], h[:, self.act_dim:].clamp(-20.0, 2.0)
+        t = self.unscale(act.float()).clamp(-1 + 1e-6, 1 - 1e-6)
+        u = torch.atanh(t)
+        logp = (-0.5 * ((u - mean) / log_std.exp()) ** 2 - log_std - 0.5 * np.log(2 * np.pi)).sum(-1)
+        return logp - torch.log(1.0 - t.pow(2) + 1e-6).sum(-1) - torch.log(self.a_half).sum()
+
     def q(self, obs, act):
         x = torch.cat([obs.flatten(1).float(), act.float()], dim=-1)
         return self.q1(x).squeeze(-1), (self.q2(x).squeeze(-1) if self.q2 is not None else None)
