@@ -810,8 +810,6 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
   RMM_HIP_CHECK(hipGetLastError());
 }
 
-}  // namespace hip
-}  // namespace rmm
 
 // ---------------------------------------------------------------------------------------------
 // K19: device-resident frame stacks for hybrid rollout workers. The CPU env uploads only the
@@ -858,3 +856,6 @@ void frame_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* buf_obs, con
                      B, chunks);
   RMM_HIP_CHECK(hipGetLastError());
 }
+
+}  // namespace hip
+}  // namespace rmm
