@@ -36,9 +36,22 @@ def _contained():
     return c
 
 
+# user-registered (serializer, deserializer) per class (util.register_serializer); the registry is
+# process-local, as in the reference, so the driver registers before it ships such objects
+_custom_serializers: dict = {}
+
+
+def _rebuild_custom(deserializer, payload):
+    return deserializer(payload)
+
+
 class _Pickler(cloudpickle.CloudPickler):
     def reducer_override(self, obj):
         t = type(obj)
+        if _custom_serializers:
+            ent = _custom_serializers.get(t)
+            if ent is not None:
+                return _rebuild_custom, (ent[1], ent[0](obj))
         mod = t.__module__
         if mod == "torch" and t.__name__ in ("Tensor", "Parameter"):
             try:

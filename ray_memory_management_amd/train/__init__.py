@@ -18,4 +18,6 @@ def __getattr__(name):
         return importlib.import_module("ray_memory_management_amd.train.torch").TorchTrainer
     if name == "TorchPredictor":
         return importlib.import_module("ray_memory_management_amd.train.predictor").TorchPredictor
+    if name in ("sklearn", "rl"):
+        return importlib.import_module(f"ray_memory_management_amd.train.{name}")
     raise AttributeError(name)

@@ -1,0 +1,113 @@
+"""RLlib through the Train API. Parity: reference python/ray/train/rl/{rl_trainer,rl_checkpoint,
+rl_predictor}.py: RLTrainer(algorithm, config, run_config.stop) trains an RLlib Algorithm until a
+stop criterion and returns a Result with the final metrics and a checkpoint; RLPredictor loads the
+policy from that checkpoint and maps observation batches to actions."""
+from __future__ import annotations
+
+import os
+import pickle
+import time
+from typing import Any, Dict, Optional, Union
+
+import numpy as np
+
+from ray_memory_management_amd.air.checkpoint import Checkpoint
+from ray_memory_management_amd.air.config import RunConfig, ScalingConfig
+from ray_memory_management_amd.air.result import Result
+from ray_memory_management_amd.train.base_trainer import BaseTrainer
+from ray_memory_management_amd.train.predictor import Predictor
+
+
+def _algo_class(algorithm):
+    if isinstance(algorithm, str):
+        from ray_memory_management_amd.rllib.algorithms import get_algorithm_class
+
+        return get_algorithm_class(algorithm)
+    return algorithm
+
+
+class RLTrainer(BaseTrainer):
+    def __init__(self, algorithm: Union[str, type], config: Optional[Dict[str, Any]] = None,
+                 scaling_config: Optional[ScalingConfig] = None, run_config: Optional[RunConfig] = None,
+                 resume_from_checkpoint: Optional[Checkpoint] = None, **kw):
+        super().__init__(scaling_config=scaling_config, run_config=run_config,
+                         resume_from_checkpoint=resume_from_checkpoint)
+        self.algorithm = algorithm
+        self.config = dict(config or {})
+        if self.scaling_config and self.scaling_config.num_workers and self.scaling_config.num_workers > 1:
+            self.config.setdefault("num_workers", self.scaling_config.num_workers - 1)
+
+    def _with_config(self, config):
+        import copy
+
+        t = copy.copy(self)
+        t.config = {**self.config, **(config or {})}
+        return t
+
+    def _stop(self, metrics) -> bool:
+        stop = self.run_config.stop
+        if callable(stop):
+            return bool(stop("rl", metrics))
+        if isinstance(stop, dict):
+            return any(metrics.get(k) is not None and metrics[k] >= v for k, v in stop.items())
+        return metrics.get("training_iteration", 0) >= 1
+
+    def fit(self) -> Result:
+        import ray_memory_management_amd as ray
+
+        if not ray.is_initialized():
+            ray.init()
+        cls = _algo_class(self.algorithm)
+        algo = cls(config=self.config)
+        run_dir = self.run_config.resolved_dir(f"RLTrainer_{time.strftime('%Y-%m-%d_%H-%M-%S')}")
+        os.makedirs(run_dir, exist_ok=True)
+        history = []
+        try:
+            if self.resume_from_checkpoint is not None:
+                algo.load_checkpoint(self.resume_from_checkpoint.to_dict()["algorithm_state"])
+            while True:
+                m = algo.train()
+                history.append({k: v for k, v in m.items() if isinstance(v, (int, float, str, bool))})
+                if self._stop(m):
+                    break
+            state = algo.save_checkpoint(run_dir)
+            env = self.config.get("env")
+            ck = Checkpoint.from_dict({"algorithm_state": state, "algorithm": cls.__name__,
+                                       "config": {k: v for k, v in self.config.items() if k != "callbacks"},
+                                       "algo_class": cls, "env": env})
+            path = os.path.join(run_dir, "checkpoint_000000")
+            ck.to_directory(path)
+            return Result(metrics=history[-1], checkpoint=Checkpoint.from_directory(path), error=None,
+                          log_dir=run_dir, metrics_history=history)
+        except Exception as e:  # noqa: BLE001
+            return Result(metrics=history[-1] if history else None, checkpoint=None, error=e, log_dir=run_dir,
+                          metrics_history=history)
+        finally:
+            algo.stop()
+
+
+class RLPredictor(Predictor):
+    """Computes greedy actions with the checkpointed policy (no env, no workers)."""
+
+    def __init__(self, policy, preprocessor=None):
+        super().__init__(preprocessor)
+        self.policy = policy
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint: Checkpoint, env=None, **kw) -> "RLPredictor":
+        d = checkpoint.to_dict()
+        algo_cls = d["algo_class"]
+        cfg = dict(d["config"])
+        cfg["num_workers"] = 0
+        if env is not None:
+            cfg["env"] = env
+        algo = algo_cls(config=cfg)
+        algo.load_checkpoint(d["algorithm_state"])
+        policy = algo.get_policy()
+        algo.workers.stop()
+        return cls(policy)
+
+    def _predict_numpy(self, data, **kwargs):
+        obs = np.asarray(data if not isinstance(data, dict) else next(iter(data.values())), dtype=np.float32)
+        a, _, _ = self.policy.compute_actions(obs, explore=False)
+        return np.asarray(a)

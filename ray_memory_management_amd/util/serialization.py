@@ -1,0 +1,18 @@
+"""Custom serializers. Parity: reference python/ray/util/serialization.py (register_serializer /
+deregister_serializer): objects of `cls` are serialized as ``serializer(obj)`` and rebuilt with
+``deserializer(payload)`` wherever the runtime pickles them (task args, returns, ray.put)."""
+from __future__ import annotations
+
+from typing import Any, Callable
+
+from ray_memory_management_amd._private import serialization as _ser
+
+
+def register_serializer(cls: type, *, serializer: Callable[[Any], Any], deserializer: Callable[[Any], Any]) -> None:
+    if not isinstance(cls, type):
+        raise TypeError("register_serializer expects a class")
+    _ser._custom_serializers[cls] = (serializer, deserializer)
+
+
+def deregister_serializer(cls: type) -> None:
+    _ser._custom_serializers.pop(cls, None)
