@@ -20,6 +20,7 @@ ALGORITHMS = {
     "APEX": ("apex_dqn", "ApexDQN"),
     "APEX_DDPG": ("apex_ddpg", "ApexDDPG"),
     "A3C": ("a3c", "A3C"),
+    "R2D2": ("r2d2", "R2D2"),
     "CQL": ("cql", "CQL"),
     "CRR": ("crr", "CRR"),
     "DDPPO": ("ddppo", "DDPPO"),
