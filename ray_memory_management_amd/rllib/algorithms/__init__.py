@@ -21,6 +21,7 @@ ALGORITHMS = {
     "APEX_DDPG": ("apex_ddpg", "ApexDDPG"),
     "A3C": ("a3c", "A3C"),
     "R2D2": ("r2d2", "R2D2"),
+    "DT": ("dt", "DT"),
     "QMIX": ("qmix", "QMix"),
     "MADDPG": ("maddpg", "MADDPG"),
     "CQL": ("cql", "CQL"),

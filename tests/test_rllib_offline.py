@@ -117,3 +117,29 @@ def test_offline_algorithms_learn_from_expert(ray_shared, tmp_path, algo):
     ev = a.evaluate()
     assert ev["episode_reward_mean"] > 100, ev
     a.stop()
+
+
+def test_decision_transformer_from_expert_episodes(ray_shared, tmp_path):
+    """DT conditioned on a high return imitates the recorded expert (reference dt tests)."""
+    from ray_memory_management_amd.rllib.algorithms import get_algorithm_class
+    from ray_memory_management_amd.rllib.algorithms.dt import episodes_from_batches
+    from ray_memory_management_amd.rllib.offline import JsonReader
+
+    out, _ = _record_expert(tmp_path, ray_shared)
+    eps = episodes_from_batches(JsonReader(str(out)).read_all())
+    assert eps and all(e["dones"][-1] == 1 for e in eps)
+    e0 = eps[0]
+    np.testing.assert_allclose(e0["rtg"][0], e0["rewards"].sum(), rtol=1e-6)
+    cls = get_algorithm_class("DT")
+    cfg = (cls.get_default_config().environment("CartPole-v1").offline_data(input_=str(out))
+           .training(lr=1e-3, train_batch_size=64, target_return=500.0, embed_dim=32, max_seq_len=4)
+           .debugging(seed=0))
+    a = cfg.build()
+    losses = []
+    for _ in range(300):
+        r = a.train()
+        losses.append(r["info"]["learner"]["default_policy"]["learner_stats"]["loss"])
+    assert np.mean(losses[-20:]) < 0.5 * np.mean(losses[:5]), (losses[:5], losses[-20:])
+    ev = a.evaluate(episodes=3)
+    assert ev["episode_reward_mean"] > 150, ev
+    a.stop()
