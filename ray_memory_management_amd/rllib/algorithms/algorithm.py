@@ -183,7 +183,7 @@ class Algorithm(Trainable):
     def evaluate(self) -> Dict:
         c = self.algo_config
         rewards, lens = RolloutWorker.evaluate_episodes(self.get_policy(), self._env_creator, c.env, c.env_config,
-                                                        int(c.evaluation_duration))
+                                                        int(c.evaluation_duration), seed=c.seed)
         return {"episode_reward_mean": float(np.mean(rewards)), "episode_reward_max": float(np.max(rewards)),
                 "episode_reward_min": float(np.min(rewards)), "episode_len_mean": float(np.mean(lens)),
                 "episodes_this_iter": len(rewards)}

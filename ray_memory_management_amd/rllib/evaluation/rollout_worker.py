@@ -320,11 +320,19 @@ class RolloutWorker:
             self.output_writer.close()
 
     @staticmethod
-    def evaluate_episodes(policy, env_creator, env, env_config, num_episodes: int, max_steps: int = 100000):
+    def evaluate_episodes(policy, env_creator, env, env_config, num_episodes: int, max_steps: int = 100000,
+                          seed: Optional[int] = None):
+        """Greedy evaluation episodes; with `seed` the episode starts are reproducible."""
         e = env_creator(env_config) if env_creator is not None else make_env(env, env_config)
         rewards, lens = [], []
-        for _ in range(num_episodes):
-            o = e.reset()
+        for k in range(num_episodes):
+            if seed is not None:
+                try:
+                    o = e.reset(seed=int(seed) * 7919 + 100003 + k)
+                except TypeError:
+                    o = e.reset()
+            else:
+                o = e.reset()
             total, steps, done = 0.0, 0, False
             while not done and steps < max_steps:
                 a = policy.compute_single_action(np.asarray(o), explore=False)
