@@ -22,6 +22,8 @@ ALGORITHMS = {
     "A3C": ("a3c", "A3C"),
     "R2D2": ("r2d2", "R2D2"),
     "DT": ("dt", "DT"),
+    "AlphaZero": ("alpha_zero", "AlphaZero"),
+    "SlateQ": ("slateq", "SlateQ"),
     "QMIX": ("qmix", "QMix"),
     "MADDPG": ("maddpg", "MADDPG"),
     "CQL": ("cql", "CQL"),

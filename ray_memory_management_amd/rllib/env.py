@@ -411,8 +411,22 @@ def register_env(name: str, creator):
     _REGISTRY[name] = creator
 
 
+# envs defined next to the algorithm that uses them: registered on first use in any process
+_LAZY_ENV_MODULES = {
+    "CartPoleSparseRewards-v1": "ray_memory_management_amd.rllib.algorithms.alpha_zero",
+    "TwoStepGame": "ray_memory_management_amd.rllib.algorithms.qmix",
+    "CoopTarget-v0": "ray_memory_management_amd.rllib.algorithms.maddpg",
+    "SlateRecEnv-v0": "ray_memory_management_amd.rllib.algorithms.slateq",
+    "LinearDiscreteEnv": "ray_memory_management_amd.rllib.algorithms.bandit",
+}
+
+
 def make_env(env, config=None):
     if isinstance(env, str):
+        if env not in _REGISTRY and env in _LAZY_ENV_MODULES:
+            import importlib
+
+            importlib.import_module(_LAZY_ENV_MODULES[env])
         if env not in _REGISTRY:
             raise ValueError(f"unknown env {env!r}; register it with register_env()")
         return _REGISTRY[env](config or {})
