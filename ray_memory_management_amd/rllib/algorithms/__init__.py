@@ -24,6 +24,7 @@ ALGORITHMS = {
     "DT": ("dt", "DT"),
     "AlphaZero": ("alpha_zero", "AlphaZero"),
     "SlateQ": ("slateq", "SlateQ"),
+    "MAML": ("maml", "MAML"),
     "QMIX": ("qmix", "QMix"),
     "MADDPG": ("maddpg", "MADDPG"),
     "CQL": ("cql", "CQL"),

@@ -418,6 +418,7 @@ _LAZY_ENV_MODULES = {
     "CoopTarget-v0": "ray_memory_management_amd.rllib.algorithms.maddpg",
     "SlateRecEnv-v0": "ray_memory_management_amd.rllib.algorithms.slateq",
     "LinearDiscreteEnv": "ray_memory_management_amd.rllib.algorithms.bandit",
+    "GoalBandit-v0": "ray_memory_management_amd.rllib.algorithms.maml",
 }
 
 
