@@ -58,3 +58,46 @@ def test_no_storage_no_snapshot(tmp_path):
         assert W._state("gcs")["storage_path"] is None
     finally:
         ray.shutdown()
+
+
+def test_killed_detached_actor_and_deleted_kv_stay_gone(tmp_path):
+    cfg = {"gcs_storage_path": str(tmp_path / "gcs"), "gcs_storage_flush_interval_ms": 10}
+    ray.init(num_cpus=2, namespace="ft2", _system_config=cfg)
+    try:
+        internal._internal_kv_put(b"a", b"1")
+        internal._internal_kv_put(b"b", b"2")
+        internal._internal_kv_del(b"a")
+        k = Keeper.options(name="gone", lifetime="detached").remote("g")
+        ray.get(k.bump.remote())
+        ray.kill(k)
+        keep = Keeper.options(name="kept", lifetime="detached").remote("k")
+        ray.get(keep.bump.remote())
+        time.sleep(0.2)
+    finally:
+        ray.shutdown()
+    ray.init(num_cpus=2, namespace="ft2", _system_config=cfg)
+    try:
+        assert internal._internal_kv_get(b"a") is None and internal._internal_kv_get(b"b") == b"2"
+        try:
+            ray.get_actor("gone")
+            raise AssertionError("a killed detached actor must not come back")
+        except ValueError:
+            pass
+        h = ray.get_actor("kept")
+        assert ray.get(h.bump.remote(), timeout=60) == ("k", 1)
+        ray.kill(h)
+    finally:
+        ray.shutdown()
+
+
+def test_corrupt_snapshot_is_ignored(tmp_path):
+    d = tmp_path / "gcs"
+    d.mkdir()
+    for name in ("gcs_snapshot.json", "snapshot.json", "gcs.json"):
+        (d / name).write_text("{not json")
+    ray.init(num_cpus=1, _system_config={"gcs_storage_path": str(d)})
+    try:
+        assert ray.get(ray.put(3)) == 3  # the head starts with empty tables
+        assert W._state("gcs")["storage_path"] == str(d)
+    finally:
+        ray.shutdown()
