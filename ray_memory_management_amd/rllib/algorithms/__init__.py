@@ -25,6 +25,7 @@ ALGORITHMS = {
     "AlphaZero": ("alpha_zero", "AlphaZero"),
     "SlateQ": ("slateq", "SlateQ"),
     "MAML": ("maml", "MAML"),
+    "Dreamer": ("dreamer", "Dreamer"),
     "QMIX": ("qmix", "QMix"),
     "MADDPG": ("maddpg", "MADDPG"),
     "CQL": ("cql", "CQL"),

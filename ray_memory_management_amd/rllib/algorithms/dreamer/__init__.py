@@ -1,0 +1,270 @@
+"""Dreamer (v1): learn a recurrent state-space world model, then train actor and critic purely in
+imagined latent rollouts.
+
+Parity: reference rllib/algorithms/dreamer/dreamer.py (DreamerConfig: td_model_lr 6e-4,
+actor_lr / critic_lr 8e-5, grad_clip 100, lambda 0.95, dreamer_train_iters, batch_size 50,
+batch_length 50, imagine_horizon 15, free_nats 3.0, kl_coeff 1.0, prefill_timesteps,
+explore_noise 0.3, action_repeat; EpisodicBuffer of whole episodes sampled as fixed-length chunks),
+dreamer_model.py (RSSM: GRU deterministic state + diagonal-Gaussian stochastic state with prior
+p(z|h) and posterior q(z|h, e); observation decoder, reward head, value head, tanh-Gaussian actor)
+and dreamer_torch_policy.py (model loss = recon + reward NLL + max(free_nats, KL(q‖p)); actor
+maximises λ-returns back-propagated through the imagined dynamics; critic regresses them).
+Vector observations here (the reference's conv encoder/decoder target pixels; the RSSM, the
+imagination and the losses are the same).
+"""
+from __future__ import annotations
+
+import collections
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ray_memory_management_amd.rllib.algorithms.algorithm import Algorithm
+from ray_memory_management_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_memory_management_amd.rllib.env import make_env
+
+
+def _mlp(i, o, h, n=2, act=nn.ELU):
+    layers, d = [], i
+    for _ in range(n):
+        layers += [nn.Linear(d, h), act()]
+        d = h
+    layers.append(nn.Linear(d, o))
+    return nn.Sequential(*layers)
+
+
+class RSSM(nn.Module):
+    def __init__(self, obs_dim, act_dim, deter=64, stoch=16, hidden=128):
+        super().__init__()
+        self.deter, self.stoch = deter, stoch
+        self.encoder = _mlp(obs_dim, hidden, hidden, 1)
+        self.img_in = nn.Sequential(nn.Linear(stoch + act_dim, hidden), nn.ELU())
+        self.gru = nn.GRUCell(hidden, deter)
+        self.prior = _mlp(deter, 2 * stoch, hidden, 1)
+        self.post = _mlp(deter + hidden, 2 * stoch, hidden, 1)
+        self.decoder = _mlp(deter + stoch, obs_dim, hidden)
+        self.reward = _mlp(deter + stoch, 1, hidden)
+
+    @staticmethod
+    def _dist(x):
+        mean, std = x.chunk(2, -1)
+        return mean, F.softplus(std) + 0.1
+
+    def initial(self, n, device):
+        return torch.zeros(n, self.deter, device=device), torch.zeros(n, self.stoch, device=device)
+
+    def img_step(self, h, z, a):
+        h = self.gru(self.img_in(torch.cat([z, a], -1)), h)
+        m, s = self._dist(self.prior(h))
+        return h, m + s * torch.randn_like(m), (m, s)
+
+    def obs_step(self, h, z, a, e):
+        h, _, prior = self.img_step(h, z, a)
+        m, s = self._dist(self.post(torch.cat([h, e], -1)))
+        return h, m + s * torch.randn_like(m), prior, (m, s)
+
+    def feat(self, h, z):
+        return torch.cat([h, z], -1)
+
+
+class ActorNet(nn.Module):
+    def __init__(self, feat, act_dim, hidden=128):
+        super().__init__()
+        self.net = _mlp(feat, 2 * act_dim, hidden)
+
+    def forward(self, f, deterministic=False):
+        m, s = self.net(f).chunk(2, -1)
+        s = F.softplus(s) + 1e-4
+        u = m if deterministic else m + s * torch.randn_like(m)
+        return torch.tanh(u)
+
+
+class DreamerConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class=algo_class or Dreamer)
+        self.td_model_lr = 6e-4
+        self.actor_lr = 8e-5
+        self.critic_lr = 8e-5
+        self.grad_clip = 100.0
+        self.lambda_ = 0.95
+        self.dreamer_train_iters = 100
+        self.batch_size = 50
+        self.batch_length = 50
+        self.imagine_horizon = 15
+        self.free_nats = 3.0
+        self.kl_coeff = 1.0
+        self.prefill_timesteps = 5000
+        self.explore_noise = 0.3
+        self.action_repeat = 1
+        self.episodes_per_iteration = 1
+        self.num_workers = 0
+        self.dreamer_model = {"deter_size": 64, "stoch_size": 16, "hidden_size": 128}
+
+
+class Dreamer(Algorithm):
+    _config_class = DreamerConfig
+
+    def _setup_learner(self):
+        c = self.algo_config
+        self.env = make_env(c.env, c.env_config)
+        if not hasattr(self.env.action_space, "low"):
+            raise ValueError("Dreamer needs a continuous (Box) action space")
+        self.low = np.asarray(self.env.action_space.low, np.float32)
+        self.high = np.asarray(self.env.action_space.high, np.float32)
+        od, ad = int(np.prod(self.env.observation_space.shape)), int(np.prod(self.env.action_space.shape))
+        dm = c.dreamer_model
+        if c.seed is not None:
+            torch.manual_seed(int(c.seed))
+        self.device = torch.device("cuda" if c.num_gpus and torch.cuda.is_available() else "cpu")
+        self.model = RSSM(od, ad, dm["deter_size"], dm["stoch_size"], dm["hidden_size"]).to(self.device)
+        feat = dm["deter_size"] + dm["stoch_size"]
+        self.actor = ActorNet(feat, ad, dm["hidden_size"]).to(self.device)
+        self.critic = _mlp(feat, 1, dm["hidden_size"]).to(self.device)
+        self.m_opt = torch.optim.Adam(self.model.parameters(), lr=c.td_model_lr)
+        self.a_opt = torch.optim.Adam(self.actor.parameters(), lr=c.actor_lr)
+        self.c_opt = torch.optim.Adam(self.critic.parameters(), lr=c.critic_lr)
+        self.episodes: List[Dict[str, np.ndarray]] = []
+        self.rng = np.random.default_rng(c.seed)
+        self.ad = ad
+        self._collect(int(c.prefill_timesteps), random=True)
+
+    def _scale(self, a):
+        return self.low + (a + 1.0) * 0.5 * (self.high - self.low)
+
+    @torch.no_grad()
+    def _collect(self, min_steps: int, random: bool = False):
+        c, dev = self.algo_config, self.device
+        steps = 0
+        while steps < max(1, min_steps):
+            o, done = self.env.reset(), False
+            h, z = self.model.initial(1, dev)
+            a_prev = torch.zeros(1, self.ad, device=dev)
+            obs, acts, rews, ret = [np.asarray(o, np.float32)], [], [], 0.0
+            while not done:
+                e = self.model.encoder(torch.as_tensor(obs[-1], device=dev)[None])
+                h, z, _, _ = self.model.obs_step(h, z, a_prev, e)
+                if random:
+                    a = torch.as_tensor(self.rng.uniform(-1, 1, (1, self.ad)).astype(np.float32), device=dev)
+                else:
+                    a = self.actor(self.model.feat(h, z), deterministic=True)
+                    a = (a + c.explore_noise * torch.randn_like(a)).clamp(-1, 1)
+                r = 0.0
+                for _ in range(int(c.action_repeat)):
+                    o, ri, done, _ = self.env.step(self._scale(a[0].cpu().numpy()))
+                    r += ri
+                    if done:
+                        break
+                obs.append(np.asarray(o, np.float32))
+                acts.append(a[0].cpu().numpy())
+                rews.append(r)
+                ret += r
+                a_prev = a
+                steps += 1
+            self.episodes.append({"obs": np.stack(obs), "act": np.stack(acts).astype(np.float32),
+                                  "rew": np.asarray(rews, np.float32)})
+            self._episode_history.append((ret, len(rews)))
+            self._episodes_total += 1
+        self._counters["num_env_steps_sampled"] += steps
+        self._timesteps_total += steps
+        return steps
+
+    def _chunks(self):
+        c = self.algo_config
+        L = int(c.batch_length)
+        O, A, R = [], [], []
+        eps = [e for e in self.episodes if len(e["rew"]) >= L]
+        for _ in range(int(c.batch_size)):
+            e = eps[int(self.rng.integers(len(eps)))]
+            s = int(self.rng.integers(0, len(e["rew"]) - L + 1))
+            # step t pairs obs_t with the action that led into it (a_{t-1}) and the reward r_{t-1}
+            O.append(e["obs"][s + 1:s + L + 1])
+            A.append(e["act"][s:s + L])
+            R.append(e["rew"][s:s + L])
+        t = lambda x: torch.as_tensor(np.stack(x), device=self.device)  # noqa: E731
+        return t(O), t(A), t(R)
+
+    def _train_once(self) -> Dict:
+        c = self.algo_config
+        obs, act, rew = self._chunks()
+        B, L = act.shape[:2]
+        h, z = self.model.initial(B, self.device)
+        emb = self.model.encoder(obs)
+        hs, zs, kls = [], [], []
+        for t in range(L):
+            h, z, (pm, ps), (qm, qs) = self.model.obs_step(h, z, act[:, t], emb[:, t])
+            kl = (torch.log(ps / qs) + (qs ** 2 + (qm - pm) ** 2) / (2 * ps ** 2) - 0.5).sum(-1)
+            hs.append(h)
+            zs.append(z)
+            kls.append(kl)
+        H, Z = torch.stack(hs, 1), torch.stack(zs, 1)
+        feat = self.model.feat(H, Z)
+        recon = ((self.model.decoder(feat) - obs) ** 2).sum(-1).mean()
+        rew_loss = ((self.model.reward(feat).squeeze(-1) - rew) ** 2).mean()
+        kl = torch.stack(kls, 1).mean()
+        model_loss = recon + rew_loss + c.kl_coeff * torch.clamp(kl, min=c.free_nats)
+        self.m_opt.zero_grad(set_to_none=True)
+        model_loss.backward()
+        nn.utils.clip_grad_norm_(self.model.parameters(), c.grad_clip)
+        self.m_opt.step()
+        # imagination from every posterior state (detached), actor gradients through the dynamics
+        for p in self.model.parameters():
+            p.requires_grad_(False)
+        h, z = H.detach().reshape(B * L, -1), Z.detach().reshape(B * L, -1)
+        feats = []
+        for _ in range(int(c.imagine_horizon)):
+            a = self.actor(self.model.feat(h, z))
+            h, z, _ = self.model.img_step(h, z, a)
+            feats.append(self.model.feat(h, z))
+        F_ = torch.stack(feats, 0)  # [T, N, feat]
+        r_im = self.model.reward(F_).squeeze(-1)
+        v_im = self.critic(F_).squeeze(-1)
+        gamma, lam = c.gamma, c.lambda_
+        ret = [None] * len(feats)
+        nxt = v_im[-1]
+        for t in reversed(range(len(feats))):
+            nxt = r_im[t] + gamma * ((1 - lam) * v_im[t] + lam * nxt) if t < len(feats) - 1 else \
+                r_im[t] + gamma * v_im[t]
+            ret[t] = nxt
+        returns = torch.stack(ret, 0)
+        disc = torch.cumprod(torch.cat([torch.ones(1, device=self.device), torch.full((len(feats) - 1,), gamma,
+                                                                                     device=self.device)]), 0)
+        actor_loss = -(disc.unsqueeze(1) * returns).mean()
+        self.a_opt.zero_grad(set_to_none=True)
+        actor_loss.backward()
+        nn.utils.clip_grad_norm_(self.actor.parameters(), c.grad_clip)
+        self.a_opt.step()
+        for p in self.model.parameters():
+            p.requires_grad_(True)
+        critic_loss = ((self.critic(F_.detach()).squeeze(-1) - returns.detach()) ** 2 * disc.unsqueeze(1)).mean()
+        self.c_opt.zero_grad(set_to_none=True)
+        critic_loss.backward()
+        nn.utils.clip_grad_norm_(self.critic.parameters(), c.grad_clip)
+        self.c_opt.step()
+        return {"model_loss": float(model_loss.detach()), "recon_loss": float(recon.detach()),
+                "reward_loss": float(rew_loss.detach()), "kl": float(kl.detach()),
+                "actor_loss": float(actor_loss.detach()), "critic_loss": float(critic_loss.detach())}
+
+    def training_step(self) -> Dict:
+        c = self.algo_config
+        st: Dict = {}
+        for _ in range(int(c.dreamer_train_iters)):
+            st = self._train_once()
+        self._counters["num_env_steps_trained"] += int(c.dreamer_train_iters) * c.batch_size * c.batch_length
+        self._collect(1)  # at least one new episode with the current actor
+        return st
+
+    def get_weights(self):
+        return {"model": {k: v.cpu() for k, v in self.model.state_dict().items()},
+                "actor": {k: v.cpu() for k, v in self.actor.state_dict().items()},
+                "critic": {k: v.cpu() for k, v in self.critic.state_dict().items()}}
+
+    def set_weights(self, w):
+        self.model.load_state_dict(w["model"])
+        self.actor.load_state_dict(w["actor"])
+        self.critic.load_state_dict(w["critic"])
+
+
+DEFAULT_CONFIG = DreamerConfig().to_dict()
