@@ -26,6 +26,7 @@ ALGORITHMS = {
     "SlateQ": ("slateq", "SlateQ"),
     "MAML": ("maml", "MAML"),
     "Dreamer": ("dreamer", "Dreamer"),
+    "MBMPO": ("mbmpo", "MBMPO"),
     "QMIX": ("qmix", "QMix"),
     "MADDPG": ("maddpg", "MADDPG"),
     "CQL": ("cql", "CQL"),

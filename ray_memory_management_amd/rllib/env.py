@@ -419,6 +419,7 @@ _LAZY_ENV_MODULES = {
     "SlateRecEnv-v0": "ray_memory_management_amd.rllib.algorithms.slateq",
     "LinearDiscreteEnv": "ray_memory_management_amd.rllib.algorithms.bandit",
     "GoalBandit-v0": "ray_memory_management_amd.rllib.algorithms.maml",
+    "PointMass-v0": "ray_memory_management_amd.rllib.algorithms.mbmpo",
 }
 
 
