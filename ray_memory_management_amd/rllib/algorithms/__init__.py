@@ -27,6 +27,7 @@ ALGORITHMS = {
     "MAML": ("maml", "MAML"),
     "Dreamer": ("dreamer", "Dreamer"),
     "MBMPO": ("mbmpo", "MBMPO"),
+    "AlphaStar": ("alpha_star", "AlphaStar"),
     "QMIX": ("qmix", "QMix"),
     "MADDPG": ("maddpg", "MADDPG"),
     "CQL": ("cql", "CQL"),

@@ -420,6 +420,7 @@ _LAZY_ENV_MODULES = {
     "LinearDiscreteEnv": "ray_memory_management_amd.rllib.algorithms.bandit",
     "GoalBandit-v0": "ray_memory_management_amd.rllib.algorithms.maml",
     "PointMass-v0": "ray_memory_management_amd.rllib.algorithms.mbmpo",
+    "RockPaperScissors-v0": "ray_memory_management_amd.rllib.algorithms.alpha_star",
 }
 
 

@@ -138,6 +138,9 @@ class MultiAgentRolloutWorker:
             for aid in actions:
                 tr = self._traj[aid]
                 tr["rew"].append(float(rew.get(aid, 0.0)))
+                pr = self.__dict__.setdefault("_pid_ret", {})
+                pid_ = self._pid(aid)
+                pr[pid_] = pr.get(pid_, 0.0) + float(rew.get(aid, 0.0))
                 tr["nobs"].append(np.asarray(nobs.get(aid, self._obs[aid])))
                 self._ep_reward += float(rew.get(aid, 0.0))
                 if done.get(aid, False):
@@ -147,6 +150,8 @@ class MultiAgentRolloutWorker:
                 for aid in list(self._traj):
                     self._flush(aid, nobs.get(aid, self._obs.get(aid)), True, out)
                 self._completed.append((self._ep_reward, self._ep_len))
+                self.__dict__.setdefault("_matches", []).append((self._episode, dict(self.__dict__.get("_pid_ret", {}))))
+                self._pid_ret = {}
                 self._ep_reward, self._ep_len = 0.0, 0
                 self._episode += 1
                 self._agent_pid = {}
@@ -156,6 +161,29 @@ class MultiAgentRolloutWorker:
         for aid in list(self._traj):  # fragment boundary: bootstrap unfinished trajectories
             self._flush(aid, self._obs.get(aid), False, out)
         return MultiAgentBatch({pid: concat_samples(bs) for pid, bs in out.items()}, T)
+
+    def add_policy(self, policy_id, policy_cls=None, observation_space=None, action_space=None, config=None,
+                   weights=None):
+        """Add a policy at run time (reference RolloutWorker.add_policy; league training)."""
+        cls = _resolve_cls(policy_cls or self.config.get("policy_class"))
+        pol = cls(observation_space or self.env.observation_space, action_space or self.env.action_space,
+                  {**self.config, **(config or {})}, device="cpu")
+        if weights is not None:
+            import torch
+
+            pol.set_weights({k: (v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v)))
+                             for k, v in weights.items()})
+        self.policy_map[policy_id] = pol
+        return policy_id
+
+    def set_policy_mapping_fn(self, fn):
+        self.policy_mapping_fn = fn
+        self._agent_pid = {}
+
+    def take_match_results(self):
+        """[(episode, {policy_id: return})] of episodes finished since the last call."""
+        out, self._matches = getattr(self, "_matches", []), []
+        return out
 
     # -- weights / metrics (weights are {policy_id: state_dict})
     def get_weights(self, policies=None):
