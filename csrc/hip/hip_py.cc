@@ -243,6 +243,17 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ctr"), py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"), py::arg("lout"),
      py::arg("act_now"), py::arg("B"), py::arg("A"), py::arg("stream"), py::arg("ldl") = 0, py::arg("ldv") = 0);
 
+  // device-visible address of pinned (hipHostMalloc / registered) host memory; throws if unmapped,
+  // so a kernel is never handed a host pointer the GPU cannot reach
+  m.def("host_device_pointer", [](uint64_t host_ptr) {
+    void* d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, P<void>(host_ptr), 0);
+    if (e != hipSuccess || d == nullptr) {
+      (void)hipGetLastError();
+      throw std::runtime_error(std::string("host_device_pointer: not mapped pinned memory: ") + hipGetErrorString(e));
+    }
+    return reinterpret_cast<uint64_t>(d);
+  }, py::arg("host_ptr"));
   m.def("frame_push", [](uint64_t stack, uint64_t new_frames, uint64_t buf_obs, uint64_t t_ptr, int64_t B, int64_t hw,
                          uint64_t stream) {
     frame_push(P<uint8_t>(stack), P<const uint8_t>(new_frames), buf_obs ? P<uint8_t>(buf_obs) : nullptr,

@@ -127,6 +127,15 @@ class _EnvGroup:
             init = torch.from_numpy(np.ascontiguousarray(obs))
             self.s_obs[:, 1:].copy_(init[:, :3].to(dev))
             self.h_new.copy_(init[:, 3])
+            # K19 reads the newest frames straight from pinned host memory (zero-copy over the host
+            # link) when the pinned buffer is device-mapped: no separate H2D blit per step
+            self.h_new_dev = 0
+            try:
+                from ray_memory_management_amd._native import require_hip
+
+                self.h_new_dev = int(require_hip().host_device_pointer(self.h_new.data_ptr()))
+            except Exception:
+                self.h_new_dev = 0
         self.graph = None
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.ep_rew = np.zeros(n, dtype=np.float64)
@@ -139,8 +148,11 @@ class _EnvGroup:
 
         t, ctr = self.ctr_t[1:2], self.ctr_t[0:1]
         if self.device_stack:
-            self.s_new.copy_(self.h_new, non_blocking=True)
-            require_hip().frame_push(self.s_obs.data_ptr(), self.s_new.data_ptr(), self.buf_obs.data_ptr(),
+            src = self.h_new_dev
+            if not src:
+                self.s_new.copy_(self.h_new, non_blocking=True)
+                src = self.s_new.data_ptr()
+            require_hip().frame_push(self.s_obs.data_ptr(), src, self.buf_obs.data_ptr(),
                                      t.data_ptr(), self.n, self.hw, torch.cuda.current_stream().cuda_stream)
         else:
             self.s_obs.copy_(self.h_obs, non_blocking=True)
