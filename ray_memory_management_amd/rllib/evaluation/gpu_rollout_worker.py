@@ -136,6 +136,16 @@ class _EnvGroup:
                 self.h_new_dev = int(require_hip().host_device_pointer(self.h_new.data_ptr()))
             except Exception:
                 self.h_new_dev = 0
+        # K16 can store the sampled actions straight into the pinned action buffer (device-mapped):
+        # the CPU env reads them after the step's event, no D2H blit
+        self.h_act_dev = 0
+        if self.fused:
+            try:
+                from ray_memory_management_amd._native import require_hip
+
+                self.h_act_dev = int(require_hip().host_device_pointer(self.h_act.data_ptr()))
+            except Exception:
+                self.h_act_dev = 0
         self.graph = None
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.ep_rew = np.zeros(n, dtype=np.float64)
@@ -157,8 +167,11 @@ class _EnvGroup:
         else:
             self.s_obs.copy_(self.h_obs, non_blocking=True)
             self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
+        direct = bool(self.fused and self.h_act_dev)
         if not (self.fused and self.model.forward_sample(self.s_obs, t, ctr, self.seed, self.buf_act, self.buf_logp,
-                                                          self.buf_vf, self.buf_logits, self.act_now)):
+                                                          self.buf_vf, self.buf_logits,
+                                                          self.h_act_dev if direct else self.act_now)):
+            direct = False
             hd = self.model.forward_heads(self.s_obs)
             lp, vp, ld = hd.data_ptr(), hd.data_ptr() + self.A * hd.element_size(), hd.stride(0)
             bf = hd.dtype == torch.bfloat16
@@ -166,7 +179,8 @@ class _EnvGroup:
                                        self.buf_act.data_ptr(), self.buf_logp.data_ptr(), self.buf_vf.data_ptr(),
                                        self.buf_logits.data_ptr(), self.act_now.data_ptr(), self.n, self.A,
                                        torch.cuda.current_stream().cuda_stream, ldl=ld, ldv=ld)
-        self.h_act.copy_(self.act_now, non_blocking=True)
+        if not direct:
+            self.h_act.copy_(self.act_now, non_blocking=True)
         self.ctr_t.add_(1)
 
     def capture(self, stream):

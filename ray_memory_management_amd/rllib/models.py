@@ -457,7 +457,8 @@ class VisionNetwork(nn.Module):
                            hidden.data_ptr(), stream)  # K13
         hip.dense_heads_sample(hidden.data_ptr(), heads.weight.data_ptr(), heads.bias.data_ptr(), t_ptr.data_ptr(),
                                ctr.data_ptr(), seed, act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
-                               act_now.data_ptr(), B, heads.out_features, stream)  # K16
+                               act_now.data_ptr() if hasattr(act_now, "data_ptr") else int(act_now), B,
+                               heads.out_features, stream)  # K16 (act_now may be a device-mapped host address)
         return True
 
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,

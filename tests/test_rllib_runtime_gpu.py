@@ -242,8 +242,10 @@ def test_hybrid_device_frame_stacks_match_host_stacks(cuda):
     a = HybridRolloutWorker(config=cfg)
     b = HybridRolloutWorker(config=cfg)
     assert all(g.device_stack for g in a.groups)
+    assert all(g.h_new_dev and g.h_act_dev for g in a.groups)  # zero-copy frames in, actions out
     for g in b.groups:
         g.device_stack = False  # h_obs still holds the reset stacks: full-stack upload path
+        g.h_act_dev = 0  # staged D2H action copies (env transitions depend on the actions)
     for _ in range(3):
         fa, fb = a.sample(), b.sample()
         assert torch.equal(fa["obs"], fb["obs"])
