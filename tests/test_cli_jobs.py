@@ -102,3 +102,61 @@ def _dashboard_url(addr):
     sess = addr[len("rmm://"):]
     with open(os.path.join(sess, "dashboard.json")) as f:
         return json.load(f)["url"]
+
+
+def test_cli_list_summary_stack_with_live_actor(head, tmp_path):
+    """A driver keeps an actor alive while the CLI lists / summarises state and dumps stacks."""
+    script = tmp_path / "driver.py"
+    flag = tmp_path / "done"
+    script.write_text(
+        "import os, time\n"
+        "import ray_memory_management_amd as ray\n"
+        f"ray.init(address={head!r})\n"
+        "@ray.remote\n"
+        "class Holder:\n"
+        "    def ping(self):\n        return 1\n"
+        "h = Holder.options(name='cli_holder').remote()\n"
+        "ray.get(h.ping.remote())\n"
+        "refs = [ray.put(b'x' * 1000) for _ in range(3)]\n"
+        "print('READY', flush=True)\n"
+        f"while not os.path.exists({str(flag)!r}):\n    time.sleep(0.1)\n")
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    p = subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, text=True, env=e)
+    try:
+        assert p.stdout.readline().strip() == "READY"
+        r = _cli("list", "actors", "--address", head, "--format", "json", "-f", "state=ALIVE")
+        assert r.returncode == 0, r.stderr
+        rows = json.loads(r.stdout)
+        assert any(a.get("name") == "cli_holder" for a in rows), rows
+        r = _cli("list", "objects", "--address", head, "--format", "json")
+        assert r.returncode == 0 and len(json.loads(r.stdout)) >= 3, r.stderr
+        r = _cli("summary", "actors", "--address", head)
+        assert r.returncode == 0 and "Holder" in r.stdout, r.stdout + r.stderr
+        r = _cli("summary", "tasks", "--address", head)
+        assert r.returncode == 0, r.stderr
+        r = _cli("stack", "--address", head)
+        assert r.returncode == 0, r.stderr
+        r = _cli("list", "workers", "--address", head, "--format", "table")
+        assert r.returncode == 0 and r.stdout.strip(), r.stderr
+    finally:
+        flag.write_text("x")
+        p.wait(timeout=60)
+
+
+def test_cli_job_status_logs_delete(head, tmp_path):
+    script = tmp_path / "echo_job.py"
+    script.write_text("print('hello from the job')\n")
+    r = _cli("job", "submit", "--address", head, "--submission-id", "cli-echo-1", "--", sys.executable, str(script),
+             env={"PYTHONPATH": ROOT})
+    assert r.returncode == 0 and "SUCCEEDED" in r.stdout, r.stdout + r.stderr
+    r = _cli("job", "status", "cli-echo-1", "--address", head)
+    assert r.returncode == 0 and "SUCCEEDED" in r.stdout
+    r = _cli("job", "logs", "cli-echo-1", "--address", head)
+    assert r.returncode == 0 and "hello from the job" in r.stdout
+    r = _cli("job", "list", "--address", head)
+    assert r.returncode == 0 and "cli-echo-1" in r.stdout
+    r = _cli("job", "delete", "cli-echo-1", "--address", head)
+    assert r.returncode == 0
+    r = _cli("job", "list", "--address", head)
+    assert "cli-echo-1" not in r.stdout
