@@ -53,6 +53,8 @@ class Algorithm(Trainable):
         self._counters = collections.Counter()
         self._env_creator = env_creator
         self.callbacks = c.callbacks_class() if c.callbacks_class else None
+        if self.callbacks is not None and hasattr(self.callbacks, "on_algorithm_init"):
+            self._init_cb_pending = True
         self._multi_agent = c.is_multi_agent()
         if self._multi_agent:
             if not hasattr(self, "_ma_learner"):
@@ -61,6 +63,8 @@ class Algorithm(Trainable):
             self._setup_multi_agent()
         else:
             self._setup_learner()
+        if getattr(self, "_init_cb_pending", False):
+            self.callbacks.on_algorithm_init(algorithm=self)
 
     def _rollout_worker_strategy(self, c):
         """GPU rollout workers next to GPU learner actors: one placement-group bundle per learner
@@ -111,6 +115,7 @@ class Algorithm(Trainable):
             if time_ok and steps_ok:
                 break
         episodes = self.workers.collect_metrics()
+        custom = self.workers.collect_custom_metrics() if hasattr(self.workers, "collect_custom_metrics") else {}
         for r, ln in episodes:
             self._episode_history.append((r, ln))
         self._episodes_total += len(episodes)
@@ -125,6 +130,8 @@ class Algorithm(Trainable):
             "timesteps_total": self._timesteps_total,
             "num_env_steps_sampled": self._counters["num_env_steps_sampled"],
             "num_env_steps_trained": self._counters["num_env_steps_trained"],
+            "custom_metrics": __import__("ray_memory_management_amd.rllib.algorithms.callbacks",
+                                         fromlist=["x"]).summarize_custom_metrics(custom),
             "info": {"learner": ({pid: {"learner_stats": st} for pid, st in results.items()}
                                  if getattr(self, "_multi_agent", False) else
                                  {"default_policy": {"learner_stats": results}}), **dict(self._counters)},

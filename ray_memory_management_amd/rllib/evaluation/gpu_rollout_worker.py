@@ -48,6 +48,9 @@ class GPURolloutWorker:
         self._completed: List[tuple] = []
         self._sample_time = 0.0
 
+    def get_custom_metrics(self):
+        return {}
+
     def sample(self):
         import time
 

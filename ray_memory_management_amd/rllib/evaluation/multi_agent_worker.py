@@ -203,6 +203,9 @@ class MultiAgentRolloutWorker:
     def foreach_policy(self, fn):
         return [fn(p, pid) for pid, p in self.policy_map.items()]
 
+    def get_custom_metrics(self):
+        return {}
+
     def get_metrics(self):
         out, self._completed = self._completed, []
         return out

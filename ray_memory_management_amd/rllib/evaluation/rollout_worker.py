@@ -62,6 +62,10 @@ class RolloutWorker:
         self._ep_len = np.zeros(n_envs, dtype=np.int64)
         self._completed: List[tuple] = []
         self._sample_time = 0.0
+        cb = self.config.get("callbacks")
+        self.callbacks = cb() if cb is not None else None
+        self._episodes: Dict[int, Any] = {}
+        self._custom_metrics: Dict[str, List[float]] = {}
         # offline IO (reference rllib/offline + rollout_worker input_creator / output_creator)
         self.output_writer = None
         out = self.config.get("output")
@@ -88,6 +92,30 @@ class RolloutWorker:
             self.output_writer.write(batch)
         return batch
 
+    def _episode(self, i: int):
+        """The callbacks' Episode object of env slot i (created on first use = episode start)."""
+        ep = self._episodes.get(i)
+        if ep is None:
+            from ray_memory_management_amd.rllib.algorithms.callbacks import Episode
+
+            ep = self._episodes[i] = Episode(int(self._eps[i]) if getattr(self, "_eps", None) is not None else i, i)
+            self.callbacks.on_episode_start(worker=self, base_env=self.env, policies={"default_policy": self.policy},
+                                            episode=ep, env_index=i)
+        return ep
+
+    def _end_episode(self, i: int):
+        ep = self._episodes.pop(i, None)
+        if ep is None:
+            return
+        self.callbacks.on_episode_end(worker=self, base_env=self.env, policies={"default_policy": self.policy},
+                                      episode=ep, env_index=i)
+        for k, v in ep.custom_metrics.items():
+            self._custom_metrics.setdefault(k, []).append(float(v))
+
+    def get_custom_metrics(self) -> Dict[str, List[float]]:
+        out, self._custom_metrics = self._custom_metrics, {}
+        return out
+
     def _sample_env(self) -> SampleBatch:
         t0 = time.perf_counter()
         T = int(self.config.get("rollout_fragment_length", 200))
@@ -113,6 +141,16 @@ class RolloutWorker:
             done_buf.append(np.asarray(done, dtype=np.float32))
             self._ep_reward += np.asarray(rew, dtype=np.float64)
             self._ep_len += 1
+            if self.callbacks is not None:
+                for i in range(n):
+                    ep = self._episode(i)
+                    ep.length += 1
+                    ep.total_reward += float(rew[i])
+                    ep._last_obs, ep._last_action, ep._last_reward = nobs[i], a[i], float(rew[i])
+                    self.callbacks.on_episode_step(worker=self, base_env=self.env,
+                                                   policies={"default_policy": self.policy}, episode=ep, env_index=i)
+                    if done[i]:
+                        self._end_episode(i)
             for i in range(n):
                 if done[i]:
                     self._completed.append((float(self._ep_reward[i]), int(self._ep_len[i])))
@@ -144,6 +182,8 @@ class RolloutWorker:
             SampleBatch.ADVANTAGES: flat(adv).astype(np.float32),
             SampleBatch.VALUE_TARGETS: flat(ret).astype(np.float32),
         })
+        if self.callbacks is not None:
+            self.callbacks.on_sample_end(worker=self, samples=batch)
         self._sample_time += time.perf_counter() - t0
         return batch
 

@@ -112,6 +112,19 @@ class WorkerSet:
                 out += m
         return out
 
+    def collect_custom_metrics(self):
+        """Per-metric value lists recorded by episode callbacks since the last call."""
+        out = {}
+        parts = []
+        if self._local is not None and hasattr(self._local, "get_custom_metrics"):
+            parts.append(self._local.get_custom_metrics())
+        if self._remote and self._config.get("callbacks") is not None:
+            parts += ray.get([w.get_custom_metrics.remote() for w in self._remote])
+        for p in parts:
+            for k, v in (p or {}).items():
+                out.setdefault(k, []).extend(v)
+        return out
+
     def recreate_failed_workers(self):
         alive = []
         for i, w in enumerate(self._remote):
