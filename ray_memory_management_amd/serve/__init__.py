@@ -10,3 +10,15 @@ from ray_memory_management_amd.serve.handle import RayServeHandle, RayServeSyncH
 __all__ = ["batch", "deployment", "delete", "get_deployment", "get_replica_context", "ingress", "list_deployments",
            "run", "shutdown", "start", "status", "Deployment", "Application", "RayServeHandle", "RayServeSyncHandle",
            "AutoscalingConfig", "DeploymentConfig", "HTTPOptions", "http_port", "get_deployment_handle"]
+
+
+def __getattr__(name):
+    import importlib
+
+    if name in ("drivers", "http_adapters", "air_integrations"):
+        return importlib.import_module(f"ray_memory_management_amd.serve.{name}")
+    if name == "DAGDriver":
+        return importlib.import_module("ray_memory_management_amd.serve.drivers").DAGDriver
+    if name == "PredictorDeployment":
+        return importlib.import_module("ray_memory_management_amd.serve.air_integrations").PredictorDeployment
+    raise AttributeError(name)

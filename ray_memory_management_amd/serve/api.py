@@ -96,9 +96,18 @@ class Application:
         self.deployment, self.args, self.kwargs = deployment, args, kwargs
 
     def _collect(self, out: Dict[str, "Application"]):
-        for a in list(self.args) + list(self.kwargs.values()):
+        def walk(a):  # bound deployments may be nested in lists / tuples / dicts (DAGDriver routes)
             if isinstance(a, Application):
                 a._collect(out)
+            elif isinstance(a, (list, tuple)):
+                for x in a:
+                    walk(x)
+            elif isinstance(a, dict):
+                for x in a.values():
+                    walk(x)
+
+        for a in list(self.args) + list(self.kwargs.values()):
+            walk(a)
         out[self.deployment.name] = self
         return out
 

@@ -275,3 +275,58 @@ def test_handle_method_options_and_async_methods(serve_inst):
     assert ray.get([hp.remote(i) for i in range(8)]) == [i * 2 for i in range(8)]
     assert ray.get(h.count.remote()) == 8
     assert serve.get_deployment("Model").name == "Model"
+
+
+def test_dag_driver_routes_and_adapters(serve_inst):
+    ray, serve = serve_inst
+    from ray_memory_management_amd.serve.drivers import DAGDriver
+    from ray_memory_management_amd.serve.http_adapters import json_request, json_to_ndarray
+
+    @serve.deployment(ray_actor_options={"num_cpus": 0})
+    class Scale:
+        def __init__(self, k):
+            self.k = k
+
+        def __call__(self, x):
+            import numpy as np
+
+            return (np.asarray(x) * self.k).tolist()
+
+    app = DAGDriver.options(ray_actor_options={"num_cpus": 0}).bind(
+        {"/double": Scale.options(name="S2").bind(2), "/triple": Scale.options(name="S3").bind(3)},
+        http_adapter=json_request)
+    h = serve.run(app, route_prefix="/dag")
+    port = serve.http_port()
+    r = requests.post(f"http://127.0.0.1:{port}/dag/double", json=[1, 2], timeout=30)
+    assert r.status_code == 200 and r.json() == [2, 4]
+    r = requests.post(f"http://127.0.0.1:{port}/dag/triple", json=[1], timeout=30)
+    assert r.json() == [3]
+    assert ray.get(h.predict_with_route.remote("/triple", [2])) == [6]
+    serve.delete("DAGDriver")
+    app2 = DAGDriver.options(name="D2", ray_actor_options={"num_cpus": 0}).bind(Scale.options(name="S4").bind(4),
+                                                                                http_adapter=json_to_ndarray)
+    serve.run(app2, route_prefix="/nd")
+    r = requests.post(f"http://127.0.0.1:{port}/nd", json={"array": [1, 2, 3, 4], "shape": [2, 2]}, timeout=30)
+    assert r.json() == [[4, 8], [12, 16]]
+
+
+def test_predictor_deployment_serves_a_checkpoint(serve_inst):
+    ray, serve = serve_inst
+    import numpy as np
+    import torch
+
+    from ray_memory_management_amd.air.checkpoint import Checkpoint
+    from ray_memory_management_amd.serve.air_integrations import PredictorDeployment
+    from ray_memory_management_amd.train.predictor import TorchPredictor
+
+    m = torch.nn.Linear(2, 1, bias=False)
+    with torch.no_grad():
+        m.weight.copy_(torch.tensor([[1.0, 2.0]]))
+    ck = Checkpoint.from_dict({"model": m})
+    app = PredictorDeployment.options(name="Lin", ray_actor_options={"num_cpus": 0}).bind(
+        TorchPredictor, ck, batching_params={"max_batch_size": 4, "batch_wait_timeout_s": 0.05})
+    serve.run(app, route_prefix="/lin")
+    port = serve.http_port()
+    r = requests.post(f"http://127.0.0.1:{port}/lin", json={"array": [[1.0, 1.0], [2.0, 0.5]]}, timeout=30)
+    assert r.status_code == 200, r.text
+    assert np.allclose(np.asarray(r.json()).reshape(-1), [3.0, 3.0])
