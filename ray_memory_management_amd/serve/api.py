@@ -44,17 +44,20 @@ def start(detached: bool = False, http_options: Optional[Union[dict, HTTPOptions
         http_options = {"host": http_options.host, "port": http_options.port, "root_path": http_options.root_path}
     c = _get_controller(True, http_options, detached)
     if http_options is not None and http_options.get("port") is not None and http_options.get("location") != "NoServer":
-        _start_proxy(http_options.get("host", "127.0.0.1"), http_options.get("port", 8000))
+        _start_proxy(http_options.get("host", "127.0.0.1"), http_options.get("port", 8000), detached)
     return c
 
 
-def _start_proxy(host: str, port: int):
+def _start_proxy(host: str, port: int, detached: bool = False):
     from ray_memory_management_amd.serve.http_proxy import HTTPProxyActor
 
     if _state["proxy"] is not None:
         return _state["port"]
-    p = ray.remote(HTTPProxyActor).options(name="SERVE_PROXY_ACTOR", namespace=SERVE_NAMESPACE, num_cpus=0,
-                                           max_concurrency=64, get_if_exists=True).remote(host, port)
+    opts = dict(name="SERVE_PROXY_ACTOR", namespace=SERVE_NAMESPACE, num_cpus=0, max_concurrency=64,
+                get_if_exists=True)
+    if detached:  # `serve deploy` from a CLI: the proxy outlives the deploying driver
+        opts["lifetime"] = "detached"
+    p = ray.remote(HTTPProxyActor).options(**opts).remote(host, port)
     _state["port"] = ray.get(p.ready.remote())
     _state["proxy"] = p
     return _state["port"]
