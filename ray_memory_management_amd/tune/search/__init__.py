@@ -4,4 +4,6 @@ from ray_memory_management_amd.tune.search.sample import (  # noqa: F401
 from ray_memory_management_amd.tune.search.variant_generator import (  # noqa: F401
     BasicVariantGenerator, ConcurrencyLimiter, Repeater, Searcher, generate_variants)
 
-__all__ = ["BasicVariantGenerator", "ConcurrencyLimiter", "Repeater", "Searcher", "generate_variants"]
+from ray_memory_management_amd.tune.search.bayesopt import BayesOptSearch  # noqa: F401
+
+__all__ = ["BayesOptSearch", "BasicVariantGenerator", "ConcurrencyLimiter", "Repeater", "Searcher", "generate_variants"]

@@ -47,7 +47,10 @@ def _search(search_alg, metric, mode, space, num_samples) -> Searcher:
         if isinstance(inner, BasicVariantGenerator):
             inner.set_search_properties(metric, mode, space, num_samples=num_samples)
         else:
-            search_alg.set_search_properties(metric, mode, space)
+            try:  # model-based searchers stop after num_samples suggestions themselves
+                search_alg.set_search_properties(metric, mode, space, num_samples=num_samples)
+            except TypeError:
+                search_alg.set_search_properties(metric, mode, space)
     return search_alg
 
 

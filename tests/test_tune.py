@@ -314,3 +314,35 @@ def test_cli_reporter_and_sync_config(ray_shared, tmp_path):
     with pytest.raises(ValueError):
         tune.run(trainable, config={"x": 1.0}, local_dir=str(tmp_path / "e2"),
                  sync_config=tune.SyncConfig(upload_dir="s3://bucket/x"))
+
+
+def test_bayesopt_search_finds_optimum(ray_start):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.search import BayesOptSearch, ConcurrencyLimiter
+
+    def objective(config):
+        import math
+
+        tune.report(score=-(config["x"] - 0.3) ** 2 - (math.log10(config["opt"]["lr"]) + 2.0) ** 2 / 4.0)
+
+    space = {"x": tune.uniform(0.0, 1.0), "opt": {"lr": tune.loguniform(1e-4, 1.0)}, "fixed": 7}
+    bo = BayesOptSearch(metric="score", mode="max", random_search_steps=6, random_state=0)
+    analysis = tune.run(objective, config=space, search_alg=ConcurrencyLimiter(bo, max_concurrent=2),
+                        num_samples=22, metric="score", mode="max", verbose=0)
+    assert len(analysis.trials) == 22
+    best = analysis.get_best_config(metric="score", mode="max")
+    assert best["fixed"] == 7 and 1e-4 <= best["opt"]["lr"] <= 1.0
+    score = max(t.last_result["score"] for t in analysis.trials)
+    assert score > -0.03, score
+    cfg, val = bo.best()
+    assert abs(val - score) < 1e-9
+
+
+def test_bayesopt_rejects_categorical():
+    import pytest
+
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.search import BayesOptSearch
+
+    with pytest.raises(ValueError):
+        BayesOptSearch(space={"a": tune.choice([1, 2])}, metric="m", mode="max")
