@@ -181,9 +181,9 @@ def _runtime(args, n_gpus):
         w_per, envs = 1, TRAIN_BATCH // args.fragment
         n_cpus = max(budget, 2 * n_gpus + 1)
     phys = 1 if args.same_device else n_gpus
-    # the runtime's processes (head, learner / rollout actors) must not inherit the launcher's
-    # torchrun rendezvous variables: they run their own groups (util.collective), and torchrun's
-    # MASTER_* / RANK / TORCHELASTIC_* settings measurably slowed their gloo transport
+    # the runtime's processes (head, learner / rollout actors) do not inherit the launcher's torchrun
+    # rendezvous variables: they form their own groups (util.collective), and a stray RANK /
+    # WORLD_SIZE / MASTER_* must never be mistaken for theirs
     saved = {k: os.environ.pop(k) for k in list(os.environ)
              if k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
                       "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
