@@ -11,6 +11,7 @@ from ray_memory_management_amd.data.preprocessor import Preprocessor  # noqa: F4
 from ray_memory_management_amd.data.read_api import (  # noqa: F401
     from_arrow, from_arrow_refs, from_huggingface, from_items, from_numpy, from_numpy_refs, from_pandas,
     from_pandas_refs, range, range_arrow, range_table, range_tensor, read_binary_files, read_csv, read_datasource,
+    read_images,
     read_json, read_numpy, read_parquet, read_parquet_bulk, read_text)
 
 
@@ -21,7 +22,7 @@ def set_progress_bars(enabled: bool) -> bool:
 __all__ = [
     "ActorPoolStrategy", "Dataset", "DatasetPipeline", "Datasource", "ReadTask", "from_items", "from_arrow",
     "from_arrow_refs", "from_numpy", "from_numpy_refs", "from_pandas", "from_pandas_refs", "from_huggingface",
-    "range", "range_table", "range_arrow", "range_tensor", "read_text", "read_binary_files", "read_csv",
+    "range", "range_table", "range_arrow", "range_tensor", "read_text", "read_binary_files", "read_csv", "read_images",
     "read_datasource", "read_json", "read_numpy", "read_parquet", "read_parquet_bulk", "set_progress_bars",
     "Preprocessor", "DatasetContext", "GroupedDataset", "AggregateFn", "Count", "Sum", "Min", "Max", "Mean", "Std",
 ]

@@ -244,3 +244,39 @@ class BinaryDatasource(FileBasedDatasource):
         with open(path, "rb") as f:
             data = f.read()
         return [(path, data)] if include_paths else [data]
+
+
+class ImageFolderDatasource(FileBasedDatasource):
+    """``root/<label>/<image>`` trees (reference data/datasource/image_folder_datasource.py):
+    one row per image with an ``image`` array (H, W, C uint8; optionally resized / mode-converted
+    with PIL) and its ``label`` (the sub-directory name)."""
+
+    _FILE_EXTENSIONS = [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".tif", ".tiff"]
+
+    def prepare_read(self, parallelism: int, paths, filesystem=None, partition_filter=None, meta_provider=None,
+                     **reader_args):
+        roots = [paths] if isinstance(paths, str) else list(paths)
+        for r in roots:
+            if not os.path.isdir(r):
+                raise ValueError(f"ImageFolderDatasource expects directories of class folders, got {r!r}")
+        return super().prepare_read(parallelism, roots, filesystem, partition_filter, meta_provider, **reader_args)
+
+    def _read_file(self, path, size=None, mode=None, include_paths=False, **kw):
+        from PIL import Image
+
+        with Image.open(path) as im:
+            if mode is not None:
+                im = im.convert(mode)
+            if size is not None:
+                im = im.resize((int(size[1]), int(size[0])))
+            arr = np.asarray(im)
+        label = os.path.basename(os.path.dirname(path))
+        if size is None:  # shapes may differ: simple rows
+            row = {"image": arr, "label": label}
+            if include_paths:
+                row["path"] = path
+            return [row]
+        cols = {"image": arr[None], "label": np.asarray([label])}
+        if include_paths:
+            cols["path"] = np.asarray([path])
+        return NumpyBlock(cols)  # fixed shape: columnar tensor block

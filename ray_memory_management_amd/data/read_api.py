@@ -209,3 +209,11 @@ def read_binary_files(paths, *, include_paths: bool = False, parallelism: int = 
                       ray_remote_args=None) -> Dataset:
     return read_datasource(D.BinaryDatasource(), parallelism=parallelism, paths=paths, include_paths=include_paths,
                            ray_remote_args=ray_remote_args)
+
+
+def read_images(paths, *, size=None, mode: Optional[str] = None, include_paths: bool = False, parallelism: int = -1,
+                ray_remote_args=None) -> Dataset:
+    """Image-folder dataset (reference ImageFolderDatasource via read_datasource): rows of
+    {"image": HxWxC uint8 array, "label": class-directory name}."""
+    return read_datasource(D.ImageFolderDatasource(), parallelism=parallelism, paths=paths, size=size, mode=mode,
+                           include_paths=include_paths, ray_remote_args=ray_remote_args)

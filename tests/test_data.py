@@ -286,3 +286,31 @@ def test_pipeline_repeat_and_window(ray_data):
     assert len(seen) == 2 and seen[0] == list(range(1, 7)) and seen[1] == list(range(7, 13))
     with pytest.raises(ValueError):
         ds.repeat(0)
+
+
+def test_read_images_folder(ray_data, tmp_path):
+    ray, data = ray_data
+    from PIL import Image
+
+    for label, color in (("cat", (255, 0, 0)), ("dog", (0, 0, 255))):
+        d = tmp_path / label
+        d.mkdir()
+        for i in range(3):
+            Image.new("RGB", (8 + i, 6), color).save(d / f"{i}.png")
+    ds = data.read_images(str(tmp_path), size=(4, 5), mode="RGB")
+    rows = ds.take_all()
+    assert len(rows) == 6 and sorted({r["label"] for r in rows}) == ["cat", "dog"]
+    for r in rows:
+        assert r["image"].shape == (4, 5, 3) and r["image"].dtype == np.uint8
+        assert r["image"][0, 0, 0] == (255 if r["label"] == "cat" else 0)
+
+
+def test_read_images_mixed_sizes_as_rows(ray_data, tmp_path):
+    ray, data = ray_data
+    from PIL import Image
+
+    (tmp_path / "a").mkdir()
+    Image.new("L", (3, 2)).save(tmp_path / "a" / "x.png")
+    Image.new("L", (5, 4)).save(tmp_path / "a" / "y.png")
+    rows = data.read_images(str(tmp_path), include_paths=True).take_all()
+    assert sorted(r["image"].shape for r in rows) == [(2, 3), (4, 5)] and all(r["path"].endswith(".png") for r in rows)
