@@ -202,28 +202,41 @@ class _EnvGroup:
             self.policy_step()
         self.graph = g
 
-    def launch(self, stream):
+    def launch(self, stream, current: bool = False):
         """Enqueue one policy step on `stream` (graph replay launches on the current stream) and
-        return an event that completes with the action copy."""
+        return an event that completes with the action store. With ``current=True`` the caller has
+        already made `stream` current (the rollout loop does, once per fragment). The group reuses
+        ONE event: the previous step's event has been waited on before the next launch."""
         import torch
 
+        ev = getattr(self, "_ev", None)
+        if ev is None:
+            ev = self._ev = torch.cuda.Event()
+        if current:
+            self.graph.replay() if self.graph else self.policy_step()
+            ev.record(stream)
+            return ev
         with torch.cuda.stream(stream):
             if self.graph:
                 self.graph.replay()
             else:
                 self.policy_step()
-            ev = torch.cuda.Event()
             ev.record(stream)
         return ev
 
     def env_step(self, t: int, completed: list):
+        v = getattr(self, "_np", None)
+        if v is None:  # numpy views of the pinned staging buffers, made once
+            v = self._np = {"act": self.h_act.numpy(), "rew": self.h_rew.numpy(), "done": self.h_done.numpy(),
+                            "obs": self.h_obs.numpy(),
+                            "new": self.h_new.numpy() if self.device_stack else None}
         if self.device_stack:
-            rew, done = self.env.vector_step_frames(self.h_act.numpy().copy(), self.h_new.numpy())
+            rew, done = self.env.vector_step_frames(v["act"].copy(), v["new"])
         else:
-            obs, rew, done = self.env.vector_step(self.h_act.numpy().copy())
-            self.h_obs.numpy()[:] = obs
-        self.h_rew.numpy()[t] = rew
-        self.h_done.numpy()[t] = done
+            obs, rew, done = self.env.vector_step(v["act"].copy())
+            v["obs"][:] = obs
+        v["rew"][t] = rew
+        v["done"][t] = done
         self.ep_rew += rew
         self.ep_len += 1
         if done.any():
@@ -313,13 +326,14 @@ class HybridRolloutWorker(GPURolloutWorker):
             with torch.cuda.stream(st):
                 for g in G:
                     g.ctr_t[1].zero_()
-            evs = [g.launch(st) for g in G]
-            for t in range(T):
-                for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
-                    evs[i].synchronize()
-                    g.env_step(t, self._completed)
-                    if t + 1 < T:
-                        evs[i] = g.launch(st)
+            with torch.cuda.stream(st):  # one stream switch per fragment, not per env step
+                evs = [g.launch(st, current=True) for g in G]
+                for t in range(T):
+                    for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
+                        evs[i].synchronize()
+                        g.env_step(t, self._completed)
+                        if t + 1 < T:
+                            evs[i] = g.launch(st, current=True)
             with torch.cuda.stream(st):
                 parts = []
                 for g in G:
