@@ -1,0 +1,139 @@
+"""HuggingFace Transformers on the runtime. Parity: reference
+python/ray/train/huggingface/{huggingface_trainer,huggingface_checkpoint,huggingface_predictor}.py:
+HuggingFaceTrainer(trainer_init_per_worker(train_dataset, eval_dataset, **config) ->
+transformers.Trainer, datasets={"train", "evaluation"}, scaling_config) runs one
+transformers.Trainer per worker of a TorchTrainer worker group (the process group — RCCL on GPUs,
+gloo on CPUs — is set up by the Torch backend, so transformers' DDP path picks it up), reports
+each log / evaluation to the AIR session and checkpoints the final model; HuggingFacePredictor
+restores it for batch inference.
+
+Datasets may be `data.Dataset`s (each worker receives its shard as a torch map-style dataset of
+row dicts) or any torch dataset.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+from typing import Any, Callable, Dict, Optional
+
+import numpy as np
+
+from ray_memory_management_amd.air import session
+from ray_memory_management_amd.air.checkpoint import Checkpoint
+from ray_memory_management_amd.train.predictor import Predictor
+from ray_memory_management_amd.train.torch import TorchConfig, TorchTrainer
+
+
+class _RowsDataset:
+    """Map-style torch dataset over a list of row dicts (values become tensors in the collator)."""
+
+    def __init__(self, rows):
+        self.rows = rows
+
+    def __len__(self):
+        return len(self.rows)
+
+    def __getitem__(self, i):
+        return self.rows[i]
+
+
+def _to_torch_dataset(ds, rank: int, world: int):
+    if ds is None:
+        return None
+    if hasattr(ds, "take_all") and hasattr(ds, "split"):
+        shard = ds.split(world, equal=True)[rank] if world > 1 else ds
+        rows = []
+        for r in shard.iter_rows():
+            rows.append({k: (np.asarray(v) if isinstance(v, (list, np.ndarray)) else v) for k, v in dict(r).items()})
+        return _RowsDataset(rows)
+    return ds
+
+
+def _hf_train_loop(config: Dict[str, Any]):
+    import torch.distributed as dist
+    import transformers
+
+    init = config.pop("_trainer_init_per_worker")
+    datasets = config.pop("_datasets") or {}
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    # accelerate's state probes the env rendezvous variables even when the process group already
+    # exists (it was created by the Torch backend through a file store): give it consistent ones
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
+    train_ds = _to_torch_dataset(datasets.get("train"), rank, world)
+    eval_ds = _to_torch_dataset(datasets.get("evaluation"), rank, world)
+    trainer = init(train_ds, eval_ds, **config)
+    if not isinstance(trainer, transformers.Trainer):
+        raise TypeError("trainer_init_per_worker must return a transformers.Trainer")
+
+    class _Report(transformers.TrainerCallback):
+        def on_log(self, args, state, control, logs=None, **kw):
+            if logs:
+                session.report({**{k: v for k, v in logs.items() if isinstance(v, (int, float))},
+                                "step": state.global_step, "epoch": state.epoch or 0.0})
+
+    trainer.add_callback(_Report())
+    out = trainer.train()
+    metrics = {"train_loss": float(out.training_loss), "step": int(out.global_step)}
+    if eval_ds is not None:
+        ev = trainer.evaluate()
+        metrics.update({k: float(v) for k, v in ev.items() if isinstance(v, (int, float))})
+    ck = None
+    if rank == 0:
+        d = tempfile.mkdtemp(prefix="hf_ckpt_")
+        trainer.save_model(d)
+        tok = getattr(trainer, "tokenizer", None) or getattr(trainer, "processing_class", None)
+        if tok is not None and hasattr(tok, "save_pretrained"):
+            tok.save_pretrained(d)
+        ck = Checkpoint.from_directory(d)
+    session.report(metrics, checkpoint=ck)
+
+
+class HuggingFaceTrainer(TorchTrainer):
+    def __init__(self, trainer_init_per_worker: Callable, *, trainer_init_config: Optional[Dict] = None,
+                 torch_config: Optional[TorchConfig] = None, scaling_config=None, run_config=None,
+                 datasets: Optional[Dict[str, Any]] = None, preprocessor=None, resume_from_checkpoint=None):
+        if datasets and "train" not in datasets:
+            raise KeyError("HuggingFaceTrainer needs a 'train' dataset")
+        cfg = dict(trainer_init_config or {})
+        cfg["_trainer_init_per_worker"] = trainer_init_per_worker
+        cfg["_datasets"] = dict(datasets or {})
+        super().__init__(_hf_train_loop, train_loop_config=cfg, torch_config=torch_config,
+                         scaling_config=scaling_config, run_config=run_config, datasets=None,
+                         preprocessor=preprocessor, resume_from_checkpoint=resume_from_checkpoint)
+
+
+class HuggingFacePredictor(Predictor):
+    """Runs a restored transformers model (or pipeline) on batches of feature arrays / frames."""
+
+    def __init__(self, model, preprocessor=None, use_gpu: bool = False):
+        super().__init__(preprocessor)
+        self.model = model.eval()
+        self.device = "cuda" if use_gpu else "cpu"
+        self.model.to(self.device)
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint: Checkpoint, model_cls=None, use_gpu: bool = False, **kw):
+        import transformers
+
+        d = tempfile.mkdtemp(prefix="hf_restore_")
+        # a directory checkpoint that travelled through the session arrives as {relative path: bytes}
+        for rel, blob in checkpoint.to_dict().items():
+            if isinstance(blob, (bytes, bytearray)):
+                dst = os.path.join(d, rel)
+                os.makedirs(os.path.dirname(dst), exist_ok=True)
+                with open(dst, "wb") as f:
+                    f.write(blob)
+        model_cls = model_cls or transformers.AutoModel
+        return cls(model_cls.from_pretrained(d), use_gpu=use_gpu)
+
+    def _predict_numpy(self, data, **kw):
+        import torch
+
+        feeds = data if isinstance(data, dict) else {"input_ids": data}
+        with torch.no_grad():
+            out = self.model(**{k: torch.as_tensor(np.asarray(v), device=self.device) for k, v in feeds.items()})
+        logits = out.logits if hasattr(out, "logits") else out[0]
+        return logits.float().cpu().numpy()
