@@ -151,8 +151,66 @@ class DatasetPipeline:
                 shards[i].append(lambda p=part: p)
         return [DatasetPipeline(s, length=len(s)) for s in shards]
 
+    def split_at_indices(self, indices: List[int]) -> List["DatasetPipeline"]:
+        """len(indices)+1 pipelines over the index-split shards of every window."""
+        shards: List[List[Callable]] = [[] for _ in range(len(indices) + 1)]
+        for ds in self.iter_datasets():
+            for i, part in enumerate(ds.split_at_indices(indices)):
+                shards[i].append(lambda p=part: p)
+        return [DatasetPipeline(s, length=len(s)) for s in shards]
+
+    @staticmethod
+    def from_iterable(iterable) -> "DatasetPipeline":
+        """A pipeline over zero-arg callables that each produce one window's Dataset."""
+        items = list(iterable)
+        return DatasetPipeline(items, length=len(items))
+
     def take(self, limit: int = 20) -> List[Any]:
         return list(itertools.islice(self.iter_rows(), limit))
+
+    def take_all(self, limit: Optional[int] = None) -> List[Any]:
+        if self._length == float("inf"):
+            raise ValueError("Cannot take_all of a pipeline of infinite length.")
+        out = list(self.iter_rows())
+        if limit is not None and len(out) > limit:
+            raise ValueError(f"The pipeline has more than the given limit of {limit} records.")
+        return out
+
+    def show_windows(self, limit_per_dataset: int = 10) -> None:
+        for i, ds in enumerate(self.iter_datasets()):
+            print(f"=== Window {i} ===")
+            for r in ds.take(limit_per_dataset):
+                print(r)
+
+    def to_torch(self, **kw):
+        """An iterable over the torch batches of every window (reference DatasetPipeline.to_torch)."""
+        pipe = self
+
+        class _It:
+            def __iter__(self_inner):
+                for ds in pipe.iter_datasets():
+                    yield from ds.to_torch(**kw)
+
+        return _It()
+
+    def _write_each(self, method: str, path: str, **kw):
+        import os
+
+        for i, ds in enumerate(self.iter_datasets()):
+            getattr(ds, method)(os.path.join(path, f"window_{i:06d}"), **kw)
+
+    def write_json(self, path: str, **kw):
+        self._write_each("write_json", path, **kw)
+
+    def write_csv(self, path: str, **kw):
+        self._write_each("write_csv", path, **kw)
+
+    def write_parquet(self, path: str, **kw):
+        self._write_each("write_parquet", path, **kw)
+
+    def write_datasource(self, datasource, **kw):
+        for ds in self.iter_datasets():
+            ds.write_datasource(datasource, **kw)
 
     def show(self, limit: int = 20) -> None:
         for r in self.take(limit):

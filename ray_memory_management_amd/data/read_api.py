@@ -81,7 +81,9 @@ def read_datasource(datasource: D.Datasource, *, parallelism: int = -1, ray_remo
         out_m.append(rm)
     if not out_b:
         return _from_blocks([[]])
-    return Dataset(ExecutionPlan(out_b, out_m))
+    plan = ExecutionPlan(out_b, out_m)
+    plan.source = (datasource, parallelism, ray_remote_args, dict(read_args))
+    return Dataset(plan)
 
 
 def range(n: int, *, parallelism: int = -1) -> Dataset:  # noqa: A001 - reference API name

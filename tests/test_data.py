@@ -314,3 +314,36 @@ def test_read_images_mixed_sizes_as_rows(ray_data, tmp_path):
     Image.new("L", (5, 4)).save(tmp_path / "a" / "y.png")
     rows = data.read_images(str(tmp_path), include_paths=True).take_all()
     assert sorted(r["image"].shape for r in rows) == [(2, 3), (4, 5)] and all(r["path"].endswith(".png") for r in rows)
+
+
+def test_pipeline_outputs_and_splits(ray_data, tmp_path):
+    ray, data = ray_data
+    from ray_memory_management_amd.data.dataset_pipeline import DatasetPipeline
+
+    pipe = data.range(20, parallelism=4).window(blocks_per_window=2)
+    a, b = pipe.split_at_indices([3])
+    assert sorted(a.take_all() + b.take_all()) == list(range(20))
+    p2 = DatasetPipeline.from_iterable([lambda: data.range(3), lambda: data.range(2)])
+    assert p2.take_all() == [0, 1, 2, 0, 1]
+    p3 = data.from_items([{"x": i} for i in range(6)], parallelism=2).window(blocks_per_window=1)
+    p3.write_json(str(tmp_path / "out"))
+    assert sorted(os.listdir(tmp_path / "out")) == ["window_000000", "window_000001"]
+    back = data.read_json(str(tmp_path / "out" / "window_000000")).take_all()
+    assert sorted(r["x"] for r in back) == [0, 1, 2]
+    p4 = data.from_items([{"f": float(i), "y": i % 2} for i in range(8)]).repeat(2)
+    n = sum(len(lbl) for _, lbl in p4.to_torch(label_column="y", batch_size=4))
+    assert n == 16
+
+
+def test_lineage_serialization(ray_data, tmp_path):
+    ray, data = ray_data
+    ds = data.range(10, parallelism=2).map(lambda x: x * 3).filter(lambda x: x % 2 == 0)
+    assert ds.has_serializable_lineage()
+    blob = ds.serialize_lineage()
+    again = data.Dataset.deserialize_lineage(blob)
+    assert sorted(again.take_all()) == sorted(ds.take_all()) == [0, 6, 12, 18, 24]
+    assert not data.from_items([1, 2]).has_serializable_lineage()
+    import pytest
+
+    with pytest.raises(ValueError):
+        data.from_items([1, 2]).serialize_lineage()
