@@ -16,6 +16,17 @@ from ray_memory_management_amd.tune.trainable import (  # noqa: F401
     PlacementGroupFactory, Trainable, checkpoint_dir, report, with_parameters, with_resources)
 from ray_memory_management_amd.tune.tune_config import TuneConfig  # noqa: F401
 from ray_memory_management_amd.tune.tuner import Tuner, run, run_experiments  # noqa: F401
+from ray_memory_management_amd.tune.experiment import (  # noqa: F401
+    Experiment, convert_to_experiment_list, create_scheduler, create_searcher)
+from ray_memory_management_amd.air.session import (  # noqa: F401
+    get_trial_dir, get_trial_id, get_trial_name, get_trial_resources)
+
+
+def is_session_enabled() -> bool:
+    """True inside a Tune trial / Train worker (reference tune.is_session_enabled)."""
+    from ray_memory_management_amd.air import session as _s
+
+    return _s._get_session() is not None
 
 __all__ = ["SyncConfig", "CLIReporter", "JupyterNotebookReporter", "ProgressReporter", "Trainable", "TuneError", "Tuner", "TuneConfig", "ResultGrid", "ExperimentAnalysis", "run",
            "run_experiments", "report", "checkpoint_dir", "with_parameters", "with_resources", "Callback", "Stopper",
