@@ -822,30 +822,14 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
   }
 }
 
-// K16 — the rollout step's head layer + action sampling in ONE launch (replaces K14 + K7). One wave
-// per env row as in K14; after the butterfly every lane holds the bf16-rounded head row; lane 0
-// draws the Gumbel-max action (same counter hash and stream as K7, so the two paths sample
-// identically) and writes act/logp/vf of rollout row t = *t_ptr, lanes < A write the logits row.
+// one env row of K16 (one wave): head GEMV + bias, bf16 rounding, Gumbel-max draw, row stores
 template <int A1>
-__global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __restrict__ hid,
-                                                      const unsigned short* __restrict__ wh,
-                                                      const unsigned short* __restrict__ bh,
-                                                      const int64_t* __restrict__ t_ptr,
-                                                      const int64_t* __restrict__ ctr, uint32_t seed,
-                                                      int64_t* __restrict__ act, float* __restrict__ logp,
-                                                      float* __restrict__ vf, float* __restrict__ lout,
-                                                      int64_t* __restrict__ act_now, int64_t B) {
+__device__ __forceinline__ void heads_sample_row(const unsigned short* __restrict__ hid, const float* whs,
+                                                 const float* bhs, const int64_t t, const uint32_t c, uint32_t seed,
+                                                 int64_t* __restrict__ act, float* __restrict__ logp,
+                                                 float* __restrict__ vf, float* __restrict__ lout,
+                                                 int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane) {
   constexpr int A = A1 - 1;
-  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
-  __shared__ float bhs[A1];
-  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
-  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (b >= B) return;  // wave-uniform
-  const int64_t t = *t_ptr;
-  const uint32_t c = uint32_t(*ctr);
   const uint2 v = *reinterpret_cast<const uint2*>(&hid[b * H + 4 * lane]);
   const float h0 = __uint_as_float(v.x << 16), h1 = __uint_as_float(v.x & 0xffff0000u);
   const float h2 = __uint_as_float(v.y << 16), h3 = __uint_as_float(v.y & 0xffff0000u);
@@ -895,6 +879,49 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
     vf[o] = hd[A];
   }
 }
+
+// K16 — the rollout step's head layer + action sampling in ONE launch (replaces K14 + K7). One wave
+// per env row as in K14; after the butterfly every lane holds the bf16-rounded head row; lane 0
+// draws the Gumbel-max action (same counter hash and stream as K7, so the two paths sample
+// identically) and writes act/logp/vf of rollout row t = *t_ptr, lanes < A write the logits row.
+// With `done` set the launch also ADVANCES the step: the last workgroup to finish (device-scope
+// completion counter) bumps *t_ptr and *ctr and re-arms the counter, so a rollout step needs no
+// separate counter-increment kernel after it. Every block has consumed t / ctr before it arrives.
+template <int A1>
+__global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __restrict__ hid,
+                                                      const unsigned short* __restrict__ wh,
+                                                      const unsigned short* __restrict__ bh,
+                                                      const int64_t* t_ptr, const int64_t* ctr, uint32_t seed,
+                                                      int64_t* __restrict__ act, float* __restrict__ logp,
+                                                      float* __restrict__ vf, float* __restrict__ lout,
+                                                      int64_t* __restrict__ act_now, int64_t B,
+                                                      unsigned int* __restrict__ done) {
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b < B) heads_sample_row<A1>(hid, whs, bhs, *t_ptr, uint32_t(*ctr), seed, act, logp, vf, lout, act_now, B, b,
+                                  lane);  // wave-uniform
+  if (done) {
+    __shared__ unsigned int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+      int64_t* tw = const_cast<int64_t*>(t_ptr);
+      int64_t* cw = const_cast<int64_t*>(ctr);
+      *tw += 1;
+      if (cw != tw) *cw += 1;
+      atomicExch(done, 0u);
+    }
+  }
+}
 }  // namespace dense
 
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
@@ -940,7 +967,7 @@ void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const f
 
 void dense_heads_sample(const void* hidden, const void* wh, const void* bh, const int64_t* t_ptr, const int64_t* ctr,
                         uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B,
-                        int A1, hipStream_t stream) {
+                        int A1, hipStream_t stream, unsigned int* done) {
   if (B <= 0) return;
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_sample: 2 <= A <= 15 actions");
   const dim3 grid(uint32_t((B + 3) / 4)), block(256);
@@ -948,7 +975,7 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
 #define RMM_K16(N)                                                                                          \
   case N:                                                                                                   \
     hipLaunchKernelGGL(dense::k_heads_sample<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), t_ptr, ctr, \
-                       seed, act, logp, vf, lout, act_now, B);                                              \
+                       seed, act, logp, vf, lout, act_now, B, done);                                        \
     break;
   switch (A1) {
     RMM_K16(3) RMM_K16(4) RMM_K16(5) RMM_K16(6) RMM_K16(7) RMM_K16(8) RMM_K16(9)

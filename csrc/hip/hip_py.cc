@@ -326,11 +326,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("dpre_ready") = false);
   m.def("dense_heads_sample", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t t_ptr, uint64_t ctr,
                                  uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
-                                 uint64_t act_now, int64_t B, int A1, uint64_t stream) {
+                                 uint64_t act_now, int64_t B, int A1, uint64_t stream, uint64_t done) {
     dense_heads_sample(P<const void>(hidden), P<const void>(wh), P<const void>(bh), P<const int64_t>(t_ptr),
                        P<const int64_t>(ctr), seed, P<int64_t>(act), P<float>(logp), P<float>(vf), P<float>(lout),
-                       P<int64_t>(act_now), B, A1, S(stream));
-  });
+                       P<int64_t>(act_now), B, A1, S(stream), P<unsigned int>(done));
+  }, py::arg("hidden"), py::arg("wh"), py::arg("bh"), py::arg("t_ptr"), py::arg("ctr"), py::arg("seed"), py::arg("act"),
+     py::arg("logp"), py::arg("vf"), py::arg("lout"), py::arg("act_now"), py::arg("B"), py::arg("A1"),
+     py::arg("stream"), py::arg("done") = 0);
   m.def("dense_heads_ppo", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t cols, uint64_t coef, uint64_t acc,
                               uint64_t gout, int64_t M, int A1, uint64_t dz, uint64_t dpre, uint64_t stream,
                               uint64_t cidx, uint64_t ctr, int64_t period) {

@@ -10,6 +10,7 @@ on the same GPU reads them zero-copy through hipIPC (GAE runs on the learner, K1
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -117,6 +118,9 @@ class _EnvGroup:
         self.buf_logits = torch.empty((T, n, A), dtype=torch.float32, device=dev)
         self.act_now = torch.zeros(n, dtype=torch.int64, device=dev)
         self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)  # {rng counter, rollout row}
+        # K16's completion counter (K16 advances the step counters itself); RMM_NO_K16_ADVANCE=1 → add kernel
+        self.k16_done = (None if os.environ.get("RMM_NO_K16_ADVANCE")
+                         else torch.zeros(1, dtype=torch.int32, device=dev))
         self.fused = hasattr(model, "forward_sample") and getattr(
             getattr(model, "heads", None), "out_features", -1) == A + 1
         # device frame stacks (K19): upload only each env's newest frame, shift the stack in HBM
@@ -171,9 +175,11 @@ class _EnvGroup:
             self.s_obs.copy_(self.h_obs, non_blocking=True)
             self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
         direct = bool(self.fused and self.h_act_dev)
-        if not (self.fused and self.model.forward_sample(self.s_obs, t, ctr, self.seed, self.buf_act, self.buf_logp,
-                                                          self.buf_vf, self.buf_logits,
-                                                          self.h_act_dev if direct else self.act_now)):
+        advanced = bool(self.fused and self.model.forward_sample(self.s_obs, t, ctr, self.seed, self.buf_act,
+                                                                 self.buf_logp, self.buf_vf, self.buf_logits,
+                                                                 self.h_act_dev if direct else self.act_now,
+                                                                 done=self.k16_done))
+        if not advanced:
             direct = False
             hd = self.model.forward_heads(self.s_obs)
             lp, vp, ld = hd.data_ptr(), hd.data_ptr() + self.A * hd.element_size(), hd.stride(0)
@@ -184,7 +190,8 @@ class _EnvGroup:
                                        torch.cuda.current_stream().cuda_stream, ldl=ld, ldv=ld)
         if not direct:
             self.h_act.copy_(self.act_now, non_blocking=True)
-        self.ctr_t.add_(1)
+        if not (advanced and self.k16_done is not None):  # else K16 advanced the counters itself
+            self.ctr_t.add_(1)
 
     def capture(self, stream):
         import torch

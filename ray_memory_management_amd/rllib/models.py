@@ -434,9 +434,10 @@ class VisionNetwork(nn.Module):
         return dense_heads(h, self.dense_tail, self.heads)
 
     @torch.no_grad()
-    def forward_sample(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now) -> bool:
+    def forward_sample(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now, done=None) -> bool:
         """Rollout step: K10 trunk → K13 → K16 (head GEMM + Gumbel-max sampling + rollout-row stores,
-        same sampling stream as sample_store). Returns False (nothing launched) when not applicable."""
+        same sampling stream as sample_store). Returns False (nothing launched) when not applicable.
+        With `done` (a zeroed int32 device counter) K16 also advances *t_ptr and *ctr by one."""
         if not self.fused_trunk_ok(obs):
             return False
         B = obs.shape[0]
@@ -458,7 +459,8 @@ class VisionNetwork(nn.Module):
         hip.dense_heads_sample(hidden.data_ptr(), heads.weight.data_ptr(), heads.bias.data_ptr(), t_ptr.data_ptr(),
                                ctr.data_ptr(), seed, act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
                                act_now.data_ptr() if hasattr(act_now, "data_ptr") else int(act_now), B,
-                               heads.out_features, stream)  # K16 (act_now may be a device-mapped host address)
+                               heads.out_features, stream,
+                               done.data_ptr() if done is not None else 0)  # K16 (act_now: maybe device-mapped host)
         return True
 
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,

@@ -408,3 +408,35 @@ def test_dense_heads_ppo_gathers_cols_through_index_window(cuda):
     torch.testing.assert_close(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+def test_heads_sample_advances_step_counters(cuda):
+    """K16 with a completion counter: same outputs as without, and the last workgroup bumps the
+    row / RNG counters by one and re-arms the counter (many workgroups, repeated launches)."""
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    torch.manual_seed(1)
+    B, A, T = 203, 6, 4
+    hidden = torch.randn(B, 256, device=cuda).to(torch.bfloat16)
+    heads = torch.nn.Linear(256, A + 1).to(cuda).to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+    res = []
+    for adv in (False, True):
+        ctr_t = torch.tensor([777, 0], dtype=torch.int64, device=cuda)
+        done = torch.zeros(1, dtype=torch.int32, device=cuda)
+        act = torch.zeros(T, B, dtype=torch.int64, device=cuda)
+        logp, vf = torch.zeros(T, B, device=cuda), torch.zeros(T, B, device=cuda)
+        lout, now = torch.zeros(T, B, A, device=cuda), torch.zeros(B, dtype=torch.int64, device=cuda)
+        for _ in range(T):
+            h.dense_heads_sample(hidden.data_ptr(), heads.weight.data_ptr(), heads.bias.data_ptr(),
+                                 ctr_t[1:2].data_ptr(), ctr_t[0:1].data_ptr(), 3, act.data_ptr(), logp.data_ptr(),
+                                 vf.data_ptr(), lout.data_ptr(), now.data_ptr(), B, A + 1, s,
+                                 done.data_ptr() if adv else 0)
+            if not adv:
+                ctr_t.add_(1)
+        torch.cuda.synchronize()
+        assert ctr_t.tolist() == [777 + T, T] and int(done) == 0
+        res.append((act, logp, vf, lout))
+    for u, w in zip(*res):
+        assert torch.equal(u, w)
