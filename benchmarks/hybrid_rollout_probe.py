@@ -1,5 +1,6 @@
 """Per-step timing of one HybridRolloutWorker (CPU env + GPU policy) in isolation: total per env
-step, time blocked on the GPU (event waits) and time in the CPU env step, for 1 vs 2 env groups."""
+step, time blocked on the GPU (event waits) and time in the CPU env step, for 1 vs 2 env groups
+and one shared vs one-per-group streams."""
 import sys
 import time
 
@@ -12,7 +13,16 @@ from ray_memory_management_amd.rllib.evaluation import gpu_rollout_worker as G  
 
 
 def main():
-    waits = {"sync": 0.0, "env": 0.0}
+    waits = {"sync": 0.0, "env": 0.0, "launch": 0.0}
+    orig_launch = G._EnvGroup.launch
+
+    def launch(self, stream, current=False):
+        t0 = time.perf_counter()
+        ev = orig_launch(self, stream, current)
+        waits["launch"] += time.perf_counter() - t0
+        return ev
+
+    G._EnvGroup.launch = launch
     orig_step = G._EnvGroup.env_step
 
     def env_step(self, t, completed):
@@ -29,19 +39,22 @@ def main():
         waits["sync"] += time.perf_counter() - t0
 
     torch.cuda.Event.synchronize = sync
-    for n, dbl in ((25, False), (25, True), (50, True)):
+    for n, dbl, gs, graphs in ((25, False, False, True), (25, False, False, False), (25, True, False, True),
+                               (25, True, False, False), (25, True, True, True), (50, True, False, True)):
         w = G.HybridRolloutWorker(config={"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 1000},
                                           "num_envs_per_worker": n, "rollout_fragment_length": 100, "seed": 1,
-                                          "rollout_double_buffer": dbl})
+                                          "rollout_double_buffer": dbl, "rollout_group_streams": gs,
+                                          "rollout_graphs": graphs})
         w.sample()
-        waits["sync"] = waits["env"] = 0.0
+        waits["sync"] = waits["env"] = waits["launch"] = 0.0
         k = 5
         t0 = time.perf_counter()
         for _ in range(k):
             w.sample()
         el = (time.perf_counter() - t0) / k
-        print(f"n={n} double_buffer={dbl}: {el * 1e3:.2f} ms/fragment = {el / 100 * 1e6:.1f} us/step; "
-              f"gpu-wait {waits['sync'] / k / 100 * 1e6:.1f} us/step, env {waits['env'] / k / 100 * 1e6:.1f} us/step",
+        print(f"n={n} double_buffer={dbl} group_streams={gs} graphs={graphs}: {el * 1e3:.2f} ms/fragment = {el / 100 * 1e6:.1f} us/step; "
+              f"gpu-wait {waits['sync'] / k / 100 * 1e6:.1f} us/step, env {waits['env'] / k / 100 * 1e6:.1f} us/step, "
+              f"launch {waits['launch'] / k / 100 * 1e6:.1f} us/step",
               flush=True)
 
 

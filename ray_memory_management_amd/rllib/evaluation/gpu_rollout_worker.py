@@ -305,7 +305,16 @@ class HybridRolloutWorker(GPURolloutWorker):
         self.groups = [_EnvGroup(e, self.model, self.T, self.A, self.device, (s * 131 + g) & 0x7FFFFFFF)
                        for g, e in enumerate(envs)]
         self.stream = torch.cuda.Stream(self.device)
-        self._captured = False
+        # optional stream per env group (group A's policy step may run concurrently with group B's).
+        # Off by default: measured no gain in the worker probe (profiles/hybrid_group_streams.txt)
+        gs = self.config.get("rollout_group_streams", os.environ.get("RMM_GROUP_STREAMS", "0") != "0")
+        self.group_streams = ([torch.cuda.Stream(self.device) for _ in self.groups] if gs and len(self.groups) > 1
+                              else [self.stream] * len(self.groups))
+        # HIP-graph replay per policy step (default) or eager launches (rollout_graphs=False)
+        self._captured = not self.config.get("rollout_graphs", os.environ.get("RMM_NO_ROLLOUT_GRAPH") is None)
+        if self._captured:
+            for g in self.groups:
+                g.graph = False
         self._completed: List[tuple] = []
         self._sample_time = 0.0
 
@@ -319,29 +328,44 @@ class HybridRolloutWorker(GPURolloutWorker):
         t0 = time.perf_counter()
         G, T, st = self.groups, self.T, self.stream
         with torch.no_grad():
+            S = self.group_streams
             if not self._captured:
                 self._captured = True
-                for g in G:
+                for g, gs in zip(G, S):
                     try:
-                        g.capture(st)
+                        g.capture(gs)
                     except Exception as e:  # pragma: no cover
                         print(f"[HybridRolloutWorker] HIP graph capture failed ({e!r}); running eagerly")
                         g.graph = False
             # the previous fragment's frames (views of the group buffers) were copied into the HBM
             # object store on the default stream at task return: finish that before overwriting
-            st.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(st):
-                for g in G:
+            cur = torch.cuda.current_stream(self.device)
+            for gs in dict.fromkeys(S):
+                gs.wait_stream(cur)
+            for g, gs in zip(G, S):
+                with torch.cuda.stream(gs):
                     g.ctr_t[1].zero_()
-            with torch.cuda.stream(st):  # one stream switch per fragment, not per env step
-                evs = [g.launch(st, current=True) for g in G]
-                for t in range(T):
-                    for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
-                        evs[i].synchronize()
-                        g.env_step(t, self._completed)
-                        if t + 1 < T:
-                            evs[i] = g.launch(st, current=True)
+            shared = all(gs is st for gs in S)
+            with torch.cuda.stream(st):  # one stream switch per fragment (per launch with group streams)
+                try:
+                    evs = []
+                    for g, gs in zip(G, S):
+                        torch.cuda.set_stream(gs)
+                        evs.append(g.launch(gs, current=True))
+                    for t in range(T):
+                        for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
+                            evs[i].synchronize()
+                            g.env_step(t, self._completed)
+                            if t + 1 < T:
+                                if not shared:
+                                    torch.cuda.set_stream(S[i])
+                                evs[i] = g.launch(S[i], current=True)
+                finally:
+                    torch.cuda.set_stream(st)
             with torch.cuda.stream(st):
+                for gs in dict.fromkeys(S):
+                    if gs is not st:
+                        st.wait_stream(gs)
                 parts = []
                 for g in G:
                     if g.device_stack:  # observation after the last env step (pushed next fragment)

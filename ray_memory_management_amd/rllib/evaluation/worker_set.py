@@ -5,6 +5,7 @@ rllib/execution/rollout_ops.py:synchronous_parallel_sample.
 Weights are broadcast with ONE ray.put per sync (every worker reads the same shm object)."""
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional
 
 import ray_memory_management_amd as ray
@@ -45,7 +46,7 @@ class WorkerSet:
         if cls.__name__ in ("HybridRolloutWorker", "GPURolloutWorker"):
             # rollout workers drive one stream: one hardware queue each keeps many co-located worker
             # processes from oversubscribing the GPU's queue slots (the learner keeps the default)
-            q = self._config.get("rollout_worker_hw_queues", 1)
+            q = self._config.get("rollout_worker_hw_queues", int(os.environ.get("RMM_ROLLOUT_HW_QUEUES", "1")))
             if q:
                 opts["runtime_env"] = {"env_vars": {"GPU_MAX_HW_QUEUES": str(int(q))}}
         self._remote_cls = ray.remote(cls).options(**opts)
