@@ -126,3 +126,7 @@ class FunctionID(BaseID):
 
 class UniqueID(BaseID):
     SIZE = 20
+
+
+class ActorClassID(BaseID):
+    SIZE = 20

@@ -736,6 +736,7 @@ def _default_store_size() -> int:
 
 
 _client = None  # util.client.ClientWorker when connected with ray.init("ray://host:port")
+_system_config_used: dict = {}  # the _system_config this driver started its cluster with (ray._config)
 
 
 def is_initialized() -> bool:
@@ -773,6 +774,8 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             _local_mode = True
             return RayContext()
         cfg = dict(_system_config or {})
+        global _system_config_used
+        _system_config_used = dict(cfg)
         if address is None:  # jobs started by the job manager / `rmm start` users connect this way
             address = os.environ.get("RMM_ADDRESS") or None
         if address in ("auto",) or (address and address.startswith("rmm://")):

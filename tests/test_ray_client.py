@@ -90,3 +90,13 @@ def test_client_end_to_end(client_address):
     finally:
         ray.shutdown()
     assert not ray.is_initialized()
+
+
+def test_client_builder_connect(client_address):
+    """ray.client(address).namespace(...).connect() (reference client_builder.py) as a context manager."""
+    import ray_memory_management_amd as ray
+
+    with ray.client(client_address).namespace("builder").connect() as ctx:
+        assert ray.is_initialized() and ctx.ray_version == ray.__version__
+        assert ray.get(ray.put(41)) + 1 == 42
+    assert not ray.is_initialized()
