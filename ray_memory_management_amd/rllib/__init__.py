@@ -13,6 +13,12 @@ def __getattr__(name):
         return getattr(importlib.import_module("ray_memory_management_amd.rllib.ppo"), name)
     if name in ("DQN", "DQNConfig"):
         return getattr(importlib.import_module("ray_memory_management_amd.rllib.algorithms.dqn"), name)
+    if name in ("Policy", "TorchPolicy", "TFPolicy"):
+        return getattr(importlib.import_module("ray_memory_management_amd.rllib.policy"), name)
+    if name in ("BaseEnv", "ExternalEnv", "convert_to_base_env"):
+        return getattr(importlib.import_module("ray_memory_management_amd.rllib.base_env"), name)
+    if name == "MultiAgentEnv":
+        return importlib.import_module("ray_memory_management_amd.rllib.env").MultiAgentEnv
     if name in ("RolloutWorker", "WorkerSet"):
         return getattr(importlib.import_module("ray_memory_management_amd.rllib.rollout_worker"), name)
     raise AttributeError(name)

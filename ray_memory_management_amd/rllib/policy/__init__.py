@@ -13,7 +13,46 @@ from ray_memory_management_amd.rllib.models import build_model
 from ray_memory_management_amd.rllib.sample_batch import SampleBatch
 
 
-class TorchPolicy:
+class Policy:
+    """Policy interface (reference rllib/policy/policy.py): map observations to actions and hold
+    weights; learning lives in the algorithm's learner. Subclasses implement compute_actions."""
+
+    def __init__(self, observation_space, action_space, config: Dict):
+        self.observation_space, self.action_space, self.config = observation_space, action_space, config
+        self.global_timestep = 0
+
+    def compute_actions(self, obs_batch, explore: bool = True):
+        raise NotImplementedError
+
+    def compute_single_action(self, obs, explore: bool = False):
+        a, _, _ = self.compute_actions([obs], explore=explore)
+        return a[0]
+
+    def postprocess_trajectory(self, sample_batch, other_agent_batches=None, episode=None):
+        return sample_batch
+
+    def get_weights(self):
+        return {}
+
+    def set_weights(self, weights) -> None:
+        pass
+
+    def get_state(self) -> Dict:
+        return {"weights": self.get_weights(), "global_timestep": self.global_timestep}
+
+    def set_state(self, state: Dict) -> None:
+        self.set_weights(state["weights"])
+        self.global_timestep = state.get("global_timestep", 0)
+
+
+class TFPolicy(Policy):
+    """Reference TFPolicy: TensorFlow is not part of the MI355X stack (PyTorch-ROCm only)."""
+
+    def __init__(self, *a, **kw):
+        raise ImportError("TFPolicy needs TensorFlow, which this framework does not use; use TorchPolicy")
+
+
+class TorchPolicy(Policy):
     """Model + action distribution on a device (CPU for rollout workers, cuda for the learner)."""
 
     def __init__(self, observation_space, action_space, config: Dict, device="cpu"):

@@ -21,4 +21,50 @@ def __getattr__(name):
         return importlib.import_module("ray_memory_management_amd.util.debug").log_once
     if name == "pdb":
         return importlib.import_module("ray_memory_management_amd.util.rpdb")
+    if name in ("disable_log_once_globally", "enable_periodic_logging"):
+        return getattr(importlib.import_module("ray_memory_management_amd.util.debug"), name)
+    if name in ("connect", "disconnect"):
+        return globals()["_client_" + name]
     raise AttributeError(name)
+
+
+def get_node_ip_address(address: str = "127.0.0.1:80") -> str:
+    """IP of this node as other nodes see it (reference ray.util.get_node_ip_address): the source
+    address the kernel picks toward `address` (no packet is sent); loopback on a single node."""
+    import socket
+
+    host, _, port = address.rpartition(":")
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        s.connect((host or "127.0.0.1", int(port or 80)))
+        return s.getsockname()[0]
+    except OSError:
+        return "127.0.0.1"
+    finally:
+        s.close()
+
+
+def list_named_actors(all_namespaces: bool = False):
+    """Names of live named actors: in the current namespace, or every namespace as
+    {"name", "namespace"} dicts (reference ray.util.list_named_actors)."""
+    from ray_memory_management_amd.runtime_context import get_runtime_context
+    from ray_memory_management_amd.util import state
+
+    live = [a for a in state.list_actors() if a.get("name") and a.get("state") != "DEAD"]
+    if all_namespaces:
+        return [{"name": a["name"], "namespace": a["namespace"]} for a in live]
+    ns = get_runtime_context().namespace
+    return [a["name"] for a in live if a["namespace"] == ns]
+
+
+def _client_connect(conn_str: str, namespace=None, **_kw):
+    """ray.util.connect (legacy Ray Client entry): same as ray.init("ray://...")."""
+    from ray_memory_management_amd._private import worker
+
+    return worker.init(conn_str if conn_str.startswith("ray://") else "ray://" + conn_str, namespace=namespace)
+
+
+def _client_disconnect():
+    from ray_memory_management_amd._private import worker
+
+    worker.shutdown()

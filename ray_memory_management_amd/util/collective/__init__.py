@@ -11,4 +11,4 @@ from ray_memory_management_amd.util.collective.collective import (  # noqa: F401
     Backend, ReduceOp, allgather, alltoall, allreduce_async, allgather_multigpu, allreduce, allreduce_multigpu, barrier, broadcast,
     broadcast_multigpu, create_collective_group, destroy_collective_group, get_collective_group_size,
     get_group_handle, get_rank, init_collective_group, is_group_initialized, nccl_available, gloo_available,
-    recv, reduce, reducescatter, send)
+    recv, recv_multigpu, reduce, reduce_multigpu, reducescatter, reducescatter_multigpu, send, send_multigpu)

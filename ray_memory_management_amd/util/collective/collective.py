@@ -283,3 +283,34 @@ def alltoall(output, input, output_split_sizes=None, input_split_sizes=None, gro
     ins = list(input_split_sizes) if input_split_sizes is not None else []
     pg.alltoall_base(output, input, outs, ins, dist.AllToAllOptions()).wait()
     return output
+
+
+# *_multigpu: the reference drives several GPUs from ONE process (NCCL group calls); here every GPU
+# has its own process, so a rank holds one tensor per call and the list variants apply the
+# single-tensor collective to each entry (one process per GPU is the supported layout).
+def reduce_multigpu(tensor_list, dst_rank: int = 0, dst_tensor: int = 0, group_name: str = "default",
+                    op=ReduceOp.SUM):
+    for t in tensor_list:
+        reduce(t, dst_rank, group_name, op)
+    return tensor_list
+
+
+def reducescatter_multigpu(output_tensor_list, input_tensor_lists, group_name: str = "default", op=ReduceOp.SUM):
+    for out, ins in zip(output_tensor_list, input_tensor_lists):
+        reducescatter(out, ins, group_name, op)
+    return output_tensor_list
+
+
+def send_multigpu(tensor, dst_rank: int, dst_gpu_index: int = 0, group_name: str = "default", n_elements: int = 0):
+    send(tensor.reshape(-1)[:n_elements] if n_elements else tensor, dst_rank, group_name)
+
+
+def recv_multigpu(tensor, src_rank: int, src_gpu_index: int = 0, group_name: str = "default", n_elements: int = 0):
+    if n_elements:
+        buf = tensor.reshape(-1)[:n_elements].contiguous()
+        recv(buf, src_rank, group_name)
+        tensor.reshape(-1)[:n_elements].copy_(buf)
+    else:
+        recv(tensor, src_rank, group_name)
+    return tensor
+
