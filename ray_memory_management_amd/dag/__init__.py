@@ -185,5 +185,50 @@ class MultiOutputNode(DAGNode):
         return list(args)
 
 
-__all__ = ["DAGNode", "InputNode", "InputAttributeNode", "FunctionNode", "ClassNode", "ClassMethodNode",
+# reference dag/constants.py keys (used when DAG nodes are serialized / introspected)
+PARENT_CLASS_NODE_KEY = "parent_class_node"
+PREV_CLASS_METHOD_CALL_KEY = "prev_class_method_call"
+DAGNODE_TYPE_KEY = "__dag_node_type__"
+
+DAGInputData = _DAGInput  # reference input_node.py DAGInputData: the (args, kwargs) an InputNode resolves to
+
+
+def _label(node: DAGNode) -> str:
+    for attr in ("_remote_fn", "_cls", "_method_name"):
+        v = getattr(node, attr, None)
+        if v is not None:
+            name = getattr(v, "__name__", None) or getattr(getattr(v, "_function", None), "__name__", None) or str(v)
+            return f"{type(node).__name__}\\n{name}"
+    return type(node).__name__
+
+
+def plot(dag: DAGNode, to_file: str = None) -> str:
+    """Graphviz DOT text of the DAG (reference dag/vis_utils.py plot, which renders through pydot —
+    not installed here — so the DOT source is returned and written to `to_file` when given)."""
+    ids, lines, stack, seen = {}, ["digraph G {", "  rankdir=LR;"], [dag], set()
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        ids.setdefault(id(n), f"n{len(ids)}")
+        lines.append(f'  {ids[id(n)]} [label="{_label(n)}"];')
+        children = list(n._children())
+        parent = getattr(n, "_parent", None)
+        if isinstance(parent, DAGNode):
+            children.append(parent)
+        for c in children:
+            ids.setdefault(id(c), f"n{len(ids)}")
+            lines.append(f"  {ids[id(c)]} -> {ids[id(n)]};")
+            stack.append(c)
+    lines.append("}")
+    dot = "\n".join(lines)
+    if to_file:
+        with open(to_file if to_file.endswith(".dot") else to_file + ".dot", "w") as f:
+            f.write(dot)
+    return dot
+
+
+__all__ = ["DAGInputData", "PARENT_CLASS_NODE_KEY", "PREV_CLASS_METHOD_CALL_KEY", "DAGNODE_TYPE_KEY", "plot",
+           "DAGNode", "InputNode", "InputAttributeNode", "FunctionNode", "ClassNode", "ClassMethodNode",
            "MultiOutputNode"]

@@ -219,3 +219,42 @@ def read_images(paths, *, size=None, mode: Optional[str] = None, include_paths: 
     {"image": HxWxC uint8 array, "label": class-directory name}."""
     return read_datasource(D.ImageFolderDatasource(), parallelism=parallelism, paths=paths, size=size, mode=mode,
                            include_paths=include_paths, ray_remote_args=ray_remote_args)
+
+
+# --- integrations with other dataframe engines (reference read_api.py from_dask / from_modin /
+# from_mars / from_spark): each converts the engine's partitions to pandas blocks. The engines are
+# not installed in this image, so the import gate is what runs here; with the package present the
+# partitions become one block each.
+def _require(module: str, fn: str):
+    import importlib
+
+    try:
+        return importlib.import_module(module)
+    except ImportError as e:
+        raise ImportError(f"{fn} needs the `{module}` package, which is not installed") from e
+
+
+def from_dask(df) -> Dataset:
+    _require("dask", "from_dask")
+    return from_pandas([p.compute() for p in df.to_delayed()])
+
+
+def from_modin(df) -> Dataset:
+    _require("modin", "from_modin")
+    from modin.distributed.dataframe.pandas.partitions import unwrap_partitions
+
+    return from_pandas([ray.get(p) if isinstance(p, ray.ObjectRef) else p
+                        for p in unwrap_partitions(df, axis=0)])
+
+
+def from_mars(df) -> Dataset:
+    _require("mars", "from_mars")
+    return from_pandas(df.to_pandas())
+
+
+def from_spark(df, *, parallelism: Optional[int] = None) -> Dataset:
+    _require("pyspark", "from_spark")
+    pdf = df.toPandas()
+    n = parallelism or _default_parallelism(len(pdf))
+    step = max(1, -(-len(pdf) // n))
+    return from_pandas([pdf.iloc[i:i + step] for i in builtins.range(0, len(pdf), step)])

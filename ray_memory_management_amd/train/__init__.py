@@ -7,6 +7,9 @@ from ray_memory_management_amd.air import session  # noqa: F401
 from ray_memory_management_amd.train.base_trainer import BaseTrainer, DataParallelTrainer  # noqa: F401
 from ray_memory_management_amd.train.batch_predictor import BatchPredictor  # noqa: F401
 from ray_memory_management_amd.train.predictor import Predictor  # noqa: F401
+from ray_memory_management_amd.train.trainer import (  # noqa: F401  (v1 API)
+    TRAIN_DATASET_KEY, BackendConfig, CheckpointStrategy, Trainer, TrainingCallback, TrainingIterator,
+    get_dataset_shard, load_checkpoint, local_rank, report, save_checkpoint, world_rank, world_size)
 
 
 def __getattr__(name):

@@ -98,6 +98,8 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True, parallel_
     dev = get_device()
     if move_to_device:
         model = model.to(dev)
+    if _ACCEL["amp"]:
+        model = _AutocastForward(model)
     if parallel_strategy and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         kw = {"bucket_cap_mb": 256, "gradient_as_bucket_view": True}
         kw.update(parallel_strategy_kwargs or {})
@@ -160,6 +162,106 @@ def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_devi
 
 def backward(tensor):
     tensor.backward()
+
+
+# --- accelerate / reproducibility / profiling (reference train/torch/train_loop_utils.py) ---------
+_ACCEL = {"amp": False}
+
+
+def accelerate(amp: bool = False) -> None:
+    """Enable mixed precision for models / optimizers prepared after this call. On MI355X AMP means
+    bf16 autocast (MFMA-native, same exponent range as fp32, so no loss scaler is needed)."""
+    _ACCEL["amp"] = bool(amp)
+
+
+class _AutocastForward(torch.nn.Module):
+    def __init__(self, module: torch.nn.Module):
+        super().__init__()
+        self.module = module
+
+    def forward(self, *a, **kw):
+        dev = get_device().type
+        with torch.autocast(device_type=dev, dtype=torch.bfloat16):
+            out = self.module(*a, **kw)
+        return _to_float(out)
+
+
+def _to_float(x):
+    if torch.is_tensor(x) and x.is_floating_point():
+        return x.float()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_float(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_float(v) for k, v in x.items()}
+    return x
+
+
+class _AMPOptimizer:
+    """Optimizer wrapper handed out by prepare_optimizer under accelerate(amp=True): bf16 needs no
+    loss scaling, so step / zero_grad pass through; state_dict round-trips the inner optimizer."""
+
+    def __init__(self, optimizer):
+        self.optimizer = optimizer
+
+    def __getattr__(self, name):
+        return getattr(self.optimizer, name)
+
+    def step(self, closure=None):
+        return self.optimizer.step(closure)
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.optimizer.zero_grad(set_to_none=set_to_none)
+
+
+def prepare_optimizer(optimizer):
+    return _AMPOptimizer(optimizer) if _ACCEL["amp"] else optimizer
+
+
+def enable_reproducibility(seed: int = 0) -> None:
+    """Seed every RNG and switch torch to deterministic algorithms (reference
+    train.torch.enable_reproducibility); call at the top of the training function."""
+    import os
+    import random
+
+    import numpy as np
+
+    torch.manual_seed(seed)
+    random.seed(seed)
+    np.random.seed(seed)
+    os.environ.setdefault("CUBLAS_WORKSPACE_CONFIG", ":4096:8")
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.deterministic = True
+
+
+class TorchWorkerProfiler:
+    """torch.profiler inside a training worker (reference train/torch/train_loop_utils.py
+    TorchWorkerProfiler): use `trace_handler` as the profiler's on_trace_ready and report
+    `get_and_clear_profile_traces()` through the session; the driver-side callback writes them."""
+
+    def __init__(self, trace_dir: Optional[str] = None):
+        import tempfile
+
+        self.trace_dir = trace_dir or tempfile.mkdtemp(prefix="rmm_torch_prof_")
+        self.profiler_trace_filenames = []
+
+    def trace_handler(self, p) -> None:
+        import os
+
+        from ray_memory_management_amd.air import session
+
+        rank = session.get_world_rank() if session._get_session(warn=False) else 0
+        name = os.path.join(self.trace_dir, f"worker_{rank}_epoch_{len(self.profiler_trace_filenames)}.pt.trace.json")
+        p.export_chrome_trace(name)
+        self.profiler_trace_filenames.append(name)
+
+    def get_and_clear_profile_traces(self) -> Dict[str, Any]:
+        out = {}
+        for fn in self.profiler_trace_filenames:
+            with open(fn) as f:
+                out[fn.rsplit("/", 1)[-1]] = f.read()
+        self.profiler_trace_filenames = []
+        return {"_train_torch_profiler_traces": out}
 
 
 class TorchCheckpoint(Checkpoint):

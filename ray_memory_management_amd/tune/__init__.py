@@ -26,7 +26,7 @@ def is_session_enabled() -> bool:
     """True inside a Tune trial / Train worker (reference tune.is_session_enabled)."""
     from ray_memory_management_amd.air import session as _s
 
-    return _s._get_session() is not None
+    return _s._get_session(warn=False) is not None
 
 __all__ = ["SyncConfig", "CLIReporter", "JupyterNotebookReporter", "ProgressReporter", "Trainable", "TuneError", "Tuner", "TuneConfig", "ResultGrid", "ExperimentAnalysis", "run",
            "run_experiments", "report", "checkpoint_dir", "with_parameters", "with_resources", "Callback", "Stopper",

@@ -300,9 +300,25 @@ class PopulationBasedTraining(TrialScheduler):
         self._last_score: Dict[str, float] = {}
         self._rng = random.Random(seed)
         self._num_perturbations = 0
+        self._log_config = log_config
+        self._last_t: Dict[str, float] = {}
 
     def on_trial_add(self, runner, trial):
         self._last_perturb[trial.trial_id] = 0.0
+
+    def _log_policy(self, trial, donor, t, new_cfg):
+        """Append the exploit/explore step to `pbt_policy_<trial_id>.txt` next to the trial dirs
+        (reference pbt.py _log_config_on_step): [trial, donor, trial step, donor step, old, new]
+        JSON lines — the input of PopulationBasedTrainingReplay."""
+        import json
+        import os
+
+        d = os.path.dirname(getattr(trial, "logdir", "") or "") or "."
+        os.makedirs(d, exist_ok=True)
+        donor_t = donor.last_result.get(self._time_attr, t) if getattr(donor, "last_result", None) else t
+        line = [trial.trial_id, donor.trial_id, t, donor_t, _jsonable(trial.config), _jsonable(new_cfg)]
+        with open(os.path.join(d, f"pbt_policy_{trial.trial_id}.txt"), "a") as f:
+            f.write(json.dumps(line) + "\n")
 
     def on_trial_result(self, runner, trial, result):
         if self._time_attr not in result or self._metric not in result:
@@ -320,6 +336,8 @@ class PopulationBasedTraining(TrialScheduler):
                 return TrialScheduler.CONTINUE
             new_cfg = self._explore(copy.deepcopy(donor.config))
             self._num_perturbations += 1
+            if self._log_config:
+                self._log_policy(trial, donor, t, new_cfg)
             runner.exploit_trial(trial, new_cfg, ckpt, donor)
             return TrialScheduler.NOOP
         return TrialScheduler.CONTINUE
@@ -370,6 +388,72 @@ class PopulationBasedTraining(TrialScheduler):
         return f"PopulationBasedTraining: {self._num_perturbations} perturbs"
 
 
+def _jsonable(cfg):
+    import json
+
+    return {k: v for k, v in cfg.items() if _try_json(json, v)}
+
+
+def _try_json(json, v) -> bool:
+    try:
+        json.dumps(v)
+        return True
+    except TypeError:
+        return False
+
+
+class PopulationBasedTrainingReplay(TrialScheduler):
+    """Replay the config schedule one PBT trial followed (reference pbt.py
+    PopulationBasedTrainingReplay): read `pbt_policy_<trial_id>.txt`, start the (single) trial with
+    the first logged config and switch to each logged new config when the trial reaches that
+    step, continuing from its own checkpoint."""
+
+    def __init__(self, policy_file: str):
+        import json
+
+        with open(policy_file) as f:
+            steps = [json.loads(line) for line in f if line.strip()]
+        if not steps:
+            raise ValueError(f"{policy_file}: empty PBT policy log")
+        self.config = dict(steps[0][4])
+        self._policy = [(float(s[2]), dict(s[5])) for s in steps]
+        self._i = 0
+        self._trial = None
+        self._time_attr = "training_iteration"
+        self._num_perturbations = 0
+
+    def set_search_properties(self, metric, mode, **spec) -> bool:
+        return True
+
+    def on_trial_add(self, runner, trial):
+        if self._trial is not None and self._trial is not trial:
+            raise ValueError("PopulationBasedTrainingReplay replays exactly one trial")
+        self._trial = trial
+        trial.config = {**trial.config, **self.config}
+
+    def on_trial_result(self, runner, trial, result):
+        if self._i >= len(self._policy):
+            return TrialScheduler.CONTINUE
+        at, new_cfg = self._policy[self._i]
+        step = result.get(self._time_attr, 0)
+        if step < at:
+            return TrialScheduler.CONTINUE
+        ckpt = runner.checkpoint_trial(trial)
+        self._i += 1
+        self._num_perturbations += 1
+        runner.exploit_trial(trial, {**trial.config, **new_cfg}, ckpt, trial)
+        return TrialScheduler.NOOP
+
+    def debug_string(self):
+        return f"PopulationBasedTraining replay: {self._num_perturbations} of {len(self._policy)} changes applied"
+
+
+class HyperBandForBOHB(HyperBandScheduler):
+    """HyperBand variant the reference pairs with TuneBOHB (its model-based searcher needs the
+    hpbandster / ConfigSpace packages, not installed here): the same brackets and successive
+    halving, usable with any Searcher (e.g. BayesOptSearch for a model-based flavour)."""
+
+
 def _resample(spec, rng):
     from ray_memory_management_amd.tune.search.sample import Domain
 
@@ -383,7 +467,7 @@ def _resample(spec, rng):
 
 
 __all__ = ["TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
-           "MedianStoppingRule", "PopulationBasedTraining"]
+           "MedianStoppingRule", "PopulationBasedTraining", "PopulationBasedTrainingReplay", "HyperBandForBOHB"]
 
 
 from ray_memory_management_amd.tune.schedulers.resource_changing_scheduler import (  # noqa: E402,F401

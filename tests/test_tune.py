@@ -191,6 +191,21 @@ def test_pbt_exploits(ray_shared, tmp_path):
     assert pbt._num_perturbations >= 1
     # the weak trial cloned the strong one's state: both end far above 8 * 0.01
     assert min(t.last_result["total"] for t in analysis.trials) > 1.0
+    # the exploit steps were logged; replaying one trial's log re-applies its config schedule
+    import glob
+    import json
+
+    from ray_memory_management_amd.tune.schedulers import PopulationBasedTrainingReplay
+
+    logs = glob.glob(str(tmp_path / "**" / "pbt_policy_*.txt"), recursive=True)
+    assert logs
+    steps = [json.loads(x) for x in open(logs[0])]
+    replay = PopulationBasedTrainingReplay(logs[0])
+    assert replay.config["lr"] == steps[0][4]["lr"]
+    an = tune.run(PBTTrainable, config={"lr": 0.5}, scheduler=replay, stop={"training_iteration": 12},
+                  local_dir=str(tmp_path / "replay"))
+    assert replay._num_perturbations == len(steps)
+    assert an.trials[0].last_result["lr"] == steps[-1][5]["lr"]
 
 
 def test_stoppers_and_callbacks(ray_shared, tmp_path):
