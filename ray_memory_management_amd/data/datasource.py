@@ -168,7 +168,12 @@ class FileBasedDatasource(Datasource):
 
         @ray.remote
         def write(block, i):
-            fname = os.path.join(path, f"{dataset_uuid}_{i:06}.{ds._WRITE_EXT}")
+            if block_path_provider is not None:
+                fname = block_path_provider(path, dataset_uuid=dataset_uuid, block=block, block_index=i,
+                                            file_format=ds._WRITE_EXT)
+                os.makedirs(os.path.dirname(fname) or ".", exist_ok=True)
+            else:
+                fname = os.path.join(path, f"{dataset_uuid}_{i:06}.{ds._WRITE_EXT}")
             ds._write_block_path(fname, block, **writer_args)
             return fname
 
@@ -280,3 +285,71 @@ class ImageFolderDatasource(FileBasedDatasource):
         if include_paths:
             cols["path"] = np.asarray([path])
         return NumpyBlock(cols)  # fixed shape: columnar tensor block
+
+
+# --- remaining reference datasource names -------------------------------------------------------
+class RandomIntRowDatasource(Datasource):
+    """n rows x num_columns of random int64 (reference datasource.py RandomIntRowDatasource)."""
+
+    def prepare_read(self, parallelism: int, n: int, num_columns: int):
+        import numpy as np
+
+        from ray_memory_management_amd.data.block import BlockMetadata
+
+        tasks, k = [], max(1, min(parallelism, n))
+        per = -(-n // k)
+        for i in range(0, n, per):
+            cnt = min(per, n - i)
+
+            def make(cnt=cnt, seed=i):
+                import pandas as pd
+
+                rng = np.random.default_rng(seed)
+                return [pd.DataFrame({f"c_{j}": rng.integers(0, 2 ** 62, cnt) for j in range(num_columns)})]
+
+            tasks.append(ReadTask(make, BlockMetadata(cnt, 8 * cnt * num_columns, None)))
+        return tasks
+
+
+class SimpleTorchDatasource(Datasource):
+    """Rows of a map-style torch Dataset (reference simple_torch_datasource.py); the factory is
+    called inside each read task."""
+
+    def prepare_read(self, parallelism: int, dataset_factory):
+        from ray_memory_management_amd.data.block import BlockMetadata
+
+        ds = dataset_factory()
+        n = len(ds)
+        k = max(1, min(parallelism, n))
+        per = -(-n // k)
+        tasks = []
+        for lo in range(0, n, per):
+            hi = min(n, lo + per)
+
+            def make(lo=lo, hi=hi):
+                d = dataset_factory()
+                return [[d[i] for i in range(lo, hi)]]
+
+            tasks.append(ReadTask(make, BlockMetadata(hi - lo, None, None)))
+        return tasks
+
+
+class Reader:
+    """Reference datasource.Reader (lazy read planning): here prepare_read returns the tasks directly."""
+
+    def estimate_inmemory_data_size(self):
+        return None
+
+    def get_read_tasks(self, parallelism: int):
+        raise NotImplementedError
+
+
+WriteResult = Any  # what do_write's tasks return (reference datasource.py WriteResult)
+ParquetBaseDatasource = ParquetDatasource
+
+from ray_memory_management_amd.data.partitioning import (  # noqa: E402,F401
+    BaseFileMetadataProvider, BlockWritePathProvider, DefaultBlockWritePathProvider, DefaultFileMetadataProvider,
+    DefaultParquetMetadataProvider, FastFileMetadataProvider, FileExtensionFilter, FileMetadataProvider,
+    ParquetMetadataProvider, Partitioning, PartitionStyle, PathPartitionEncoder, PathPartitionFilter,
+    PathPartitionParser)
+

@@ -137,3 +137,30 @@ class HuggingFacePredictor(Predictor):
             out = self.model(**{k: torch.as_tensor(np.asarray(v), device=self.device) for k, v in feeds.items()})
         logits = out.logits if hasattr(out, "logits") else out[0]
         return logits.float().cpu().numpy()
+
+
+class HuggingFaceCheckpoint(Checkpoint):
+    """Directory checkpoint of a transformers model (+ tokenizer) written with save_pretrained
+    (reference train/huggingface/huggingface_checkpoint.py)."""
+
+    @classmethod
+    def from_model(cls, model, tokenizer=None, *, path: Optional[str] = None) -> "HuggingFaceCheckpoint":
+        import tempfile
+
+        path = path or tempfile.mkdtemp(prefix="rmm_hf_ckpt_")
+        model.save_pretrained(path)
+        if tokenizer is not None:
+            tokenizer.save_pretrained(path)
+        return cls.from_directory(path)
+
+    def get_model(self, model_cls, **kwargs):
+        import tempfile
+
+        d = self.to_directory(tempfile.mkdtemp(prefix="rmm_hf_load_"))
+        return model_cls.from_pretrained(d, **kwargs)
+
+    def get_tokenizer(self, tokenizer_cls, **kwargs):
+        import tempfile
+
+        d = self.to_directory(tempfile.mkdtemp(prefix="rmm_hf_load_"))
+        return tokenizer_cls.from_pretrained(d, **kwargs)

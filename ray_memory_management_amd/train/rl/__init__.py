@@ -111,3 +111,14 @@ class RLPredictor(Predictor):
         obs = np.asarray(data if not isinstance(data, dict) else next(iter(data.values())), dtype=np.float32)
         a, _, _ = self.policy.compute_actions(obs, explore=False)
         return np.asarray(a)
+
+
+class RLCheckpoint(Checkpoint):
+    """Checkpoint of an RLlib algorithm (reference train/rl/rl_checkpoint.py): get_policy() rebuilds
+    the default policy with the saved weights for serving / batch inference."""
+
+    def get_algorithm_state(self) -> Dict[str, Any]:
+        return self.to_dict()
+
+    def get_policy(self, env=None):
+        return RLPredictor.from_checkpoint(self, env=env).policy

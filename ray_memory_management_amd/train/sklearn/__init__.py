@@ -158,3 +158,21 @@ class SklearnPredictor(Predictor):
         if feature_columns:
             X = X[:, feature_columns]
         return self.estimator.predict(X)
+
+
+class SklearnCheckpoint(Checkpoint):
+    """Checkpoint holding a fitted estimator (+ optional preprocessor) (reference
+    train/sklearn/sklearn_checkpoint.py); readable by SklearnPredictor.from_checkpoint."""
+
+    @classmethod
+    def from_estimator(cls, estimator, *, preprocessor=None) -> "SklearnCheckpoint":
+        d = {MODEL_KEY: pickle.dumps(estimator)}  # same layout SklearnTrainer writes
+        if preprocessor is not None:
+            d["preprocessor"] = preprocessor
+        return cls.from_dict(d)
+
+    def get_estimator(self):
+        return load_estimator(self)[0]
+
+    def get_preprocessor(self):
+        return self.to_dict().get("preprocessor")
