@@ -217,3 +217,125 @@ def importance_sampling_estimate(batch: SampleBatch, new_logp: np.ndarray, gamma
 
 __all__ = ["JsonWriter", "JsonReader", "ShuffledInput", "InputReader", "OutputWriter", "NoopOutput", "to_json",
            "from_json", "importance_sampling_estimate"]
+
+
+# --- IOContext, Dataset-backed IO, mixed input, estimator classes --------------------------------
+# Parity: reference rllib/offline/{io_context.py, dataset_reader.py, dataset_writer.py,
+# mixed_input.py, is_estimator.py, wis_estimator.py, off_policy_estimator.py}.
+class IOContext:
+    """What an input / output creator sees: log dir, algorithm config, worker index."""
+
+    def __init__(self, log_dir: Optional[str] = None, config: Optional[dict] = None, worker_index: int = 0,
+                 worker=None):
+        self.log_dir = log_dir or os.getcwd()
+        self.config = dict(config or {})
+        self.worker_index = worker_index
+        self.worker = worker
+
+    def default_sampler_input(self):
+        return getattr(self.worker, "sampler", None)
+
+
+class DatasetWriter(OutputWriter):
+    """Buffer batches as rows and write them through the Data library (JSON files) on flush/close."""
+
+    def __init__(self, ioctx: Optional[IOContext] = None, compress_columns=("obs", "new_obs"),
+                 path: Optional[str] = None, max_num_samples_per_file: int = 100000):
+        ctx = ioctx or IOContext()
+        out = dict(ctx.config.get("output_config") or {})
+        self.path = os.path.abspath(path or out.get("path") or os.path.join(ctx.log_dir, "dataset_out"))
+        self.max = int(out.get("max_num_samples_per_file", max_num_samples_per_file))
+        self.compress_columns = tuple(compress_columns or ())
+        self.rows: List[dict] = []
+
+    def write(self, batch: SampleBatch):
+        self.rows.append({"batch": to_json(batch, self.compress_columns)})
+        if len(self.rows) >= self.max:
+            self.flush()
+
+    def flush(self):
+        import ray_memory_management_amd as ray
+
+        if self.rows:
+            ray.data.from_items(self.rows).write_json(self.path)
+            self.rows = []
+
+    def close(self):
+        self.flush()
+
+
+class DatasetReader(InputReader):
+    """Serve sample batches from a Dataset (rows written by DatasetWriter, or rows of SampleBatch
+    columns), cycling in order; `batch_size` rows per returned batch for column rows."""
+
+    def __init__(self, ds, ioctx: Optional[IOContext] = None, batch_size: Optional[int] = None):
+        ctx = ioctx or IOContext()
+        self.batch_size = int(batch_size or ctx.config.get("train_batch_size", 1) or 1)
+        self._rows = ds.take_all()
+        if not self._rows:
+            raise ValueError("DatasetReader: empty dataset")
+        self._i = 0
+
+    def next(self) -> SampleBatch:
+        r = self._rows[self._i % len(self._rows)]
+        if isinstance(r, dict) and "batch" in r:
+            self._i += 1
+            return from_json(r["batch"])
+        rows = [self._rows[(self._i + k) % len(self._rows)] for k in range(self.batch_size)]
+        self._i += self.batch_size
+        return SampleBatch({k: np.asarray([row[k] for row in rows]) for k in rows[0]})
+
+
+class MixedInput(InputReader):
+    """Sample from several inputs with given probabilities, e.g. {"sampler": 0.4, reader: 0.6}."""
+
+    def __init__(self, dist: dict, ioctx: Optional[IOContext] = None, seed: Optional[int] = None):
+        if abs(sum(dist.values()) - 1.0) > 1e-6:
+            raise ValueError(f"MixedInput probabilities must sum to 1, got {dist}")
+        ctx = ioctx or IOContext()
+        self.choices, self.p = [], []
+        for k, v in dist.items():
+            if k == "sampler":
+                src = ctx.default_sampler_input()
+                if src is None:
+                    raise ValueError("MixedInput: 'sampler' needs a worker with a sampler in the IOContext")
+            elif isinstance(k, str):
+                src = JsonReader(k, seed=seed)
+            else:
+                src = k
+            self.choices.append(src)
+            self.p.append(v)
+        self.rng = np.random.default_rng(seed)
+
+    def next(self) -> SampleBatch:
+        return self.choices[int(self.rng.choice(len(self.choices), p=self.p))].next()
+
+
+class OffPolicyEstimator:
+    """Base: estimate(batch) → {"v_behavior", "v_target", "v_gain"} for the policy's actions."""
+
+    def __init__(self, policy, gamma: float):
+        self.policy, self.gamma = policy, gamma
+
+    def _new_logp(self, batch: SampleBatch) -> np.ndarray:
+        import torch
+
+        obs = torch.as_tensor(np.asarray(batch[SampleBatch.OBS]), device=self.policy.device)
+        with torch.no_grad():
+            logits, _ = self.policy.model(obs)
+            d = self.policy.dist_class(logits.float())
+            a = torch.as_tensor(np.asarray(batch[SampleBatch.ACTIONS]), device=self.policy.device)
+            return d.logp(a).cpu().numpy()
+
+    def estimate(self, batch: SampleBatch) -> dict:
+        raise NotImplementedError
+
+
+class ImportanceSampling(OffPolicyEstimator):
+    def estimate(self, batch):
+        return importance_sampling_estimate(batch, self._new_logp(batch), self.gamma, weighted=False)
+
+
+class WeightedImportanceSampling(OffPolicyEstimator):
+    def estimate(self, batch):
+        return importance_sampling_estimate(batch, self._new_logp(batch), self.gamma, weighted=True)

@@ -143,3 +143,39 @@ def test_decision_transformer_from_expert_episodes(ray_shared, tmp_path):
     ev = a.evaluate(episodes=3)
     assert ev["episode_reward_mean"] > 150, ev
     a.stop()
+
+
+def test_dataset_io_mixed_input_and_estimators(ray_start, tmp_path):
+    import numpy as np
+
+    from ray_memory_management_amd import data as rdata
+    from ray_memory_management_amd.rllib.env import CartPoleEnv
+    from ray_memory_management_amd.rllib.offline import (DatasetReader, DatasetWriter, ImportanceSampling, IOContext,
+                                                          JsonWriter, MixedInput, WeightedImportanceSampling)
+    from ray_memory_management_amd.rllib.policy import TorchPolicy
+    from ray_memory_management_amd.rllib.sample_batch import SampleBatch
+
+    env = CartPoleEnv()
+    pol = TorchPolicy(env.observation_space, env.action_space, {})
+    obs = np.stack([env.reset() for _ in range(6)]).astype(np.float32)
+    a, _, extra = pol.compute_actions(obs)
+    b = SampleBatch({SampleBatch.OBS: obs, SampleBatch.ACTIONS: a, SampleBatch.REWARDS: np.ones(6, np.float32),
+                     SampleBatch.DONES: np.array([0, 0, 1, 0, 0, 1], bool),
+                     SampleBatch.ACTION_LOGP: extra[SampleBatch.ACTION_LOGP]})
+    ctx = IOContext(str(tmp_path), {"output_config": {"path": str(tmp_path / "ds")}})
+    w = DatasetWriter(ctx)
+    w.write(b)
+    w.write(b)
+    w.close()
+    r = DatasetReader(rdata.read_json(str(tmp_path / "ds")), ctx)
+    got = r.next()
+    assert np.allclose(got[SampleBatch.OBS], obs) and r.next().count == 6
+    jw = JsonWriter(str(tmp_path / "js"))
+    jw.write(b)
+    jw.close()
+    mix = MixedInput({str(tmp_path / "js"): 0.5, r: 0.5}, seed=0)
+    assert all(mix.next().count == 6 for _ in range(4))
+    # the behaviour policy IS the target policy: ratios are 1 → target value == behaviour value
+    for est in (ImportanceSampling(pol, 0.99), WeightedImportanceSampling(pol, 0.99)):
+        res = est.estimate(b)
+        assert abs(res["v_target"] - res["v_behavior"]) < 1e-3
