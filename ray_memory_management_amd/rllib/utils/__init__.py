@@ -1,1 +1,258 @@
-"""RLlib utilities: schedules, replay buffers."""
+"""RLlib utilities. Parity: reference rllib/utils/__init__.py (annotations, dict / list helpers,
+numpy NN helpers, schedules, filters, framework import helpers, numeric constants, test
+checks)."""
+from __future__ import annotations
+
+import copy
+import warnings
+from typing import Any, Dict, List
+
+import numpy as np
+
+from ray_memory_management_amd.rllib.utils.schedules import (  # noqa: F401
+    ConstantSchedule, ExponentialSchedule, LinearSchedule, PiecewiseSchedule, PolynomialSchedule, Schedule)
+
+LARGE_INTEGER = 100000000
+SMALL_NUMBER = 1e-6
+MIN_LOG_NN_OUTPUT = -5
+MAX_LOG_NN_OUTPUT = 2
+
+
+def override(cls):
+    """Marks a method as overriding `cls` (checked at definition time)."""
+    def check(method):
+        if method.__name__ not in dir(cls):
+            raise NameError(f"{method} does not override any method of {cls}")
+        return method
+
+    return check
+
+
+def PublicAPI(obj):  # noqa: N802 - reference decorator names
+    return obj
+
+
+def DeveloperAPI(obj):  # noqa: N802
+    return obj
+
+
+def deprecation_warning(old: str, new: str = None, *, help: str = None, error: bool = False) -> None:
+    msg = f"`{old}` has been deprecated." + (f" Use `{new}` instead." if new else "") + (f" {help}" if help else "")
+    if error:
+        raise DeprecationWarning(msg)
+    warnings.warn(msg, DeprecationWarning, stacklevel=2)
+
+
+def add_mixins(base, mixins, reversed: bool = False):
+    mixins = list(mixins or [])
+    bases = tuple(mixins) + (base,) if not reversed else (base,) + tuple(mixins)
+    return type(base.__name__, bases, {}) if mixins else base
+
+
+def force_list(x) -> List:
+    return [] if x is None else list(x) if isinstance(x, (list, tuple, set)) else [x]
+
+
+def force_tuple(x) -> tuple:
+    return () if x is None else tuple(x) if isinstance(x, (list, tuple)) else (x,)
+
+
+def deep_update(original: Dict, new: Dict, new_keys_allowed: bool = True, allow_new_subkey_list=None,
+                override_all_if_type_changes=None) -> Dict:
+    for k, v in new.items():
+        if k not in original and not new_keys_allowed:
+            raise KeyError(f"Unknown config parameter `{k}`")
+        if isinstance(original.get(k), dict) and isinstance(v, dict):
+            deep_update(original[k], v, True if k in (allow_new_subkey_list or []) else new_keys_allowed)
+        else:
+            original[k] = v
+    return original
+
+
+def merge_dicts(d1: Dict, d2: Dict) -> Dict:
+    return deep_update(copy.deepcopy(d1), d2, True)
+
+
+# numpy NN helpers (reference utils/numpy.py)
+def sigmoid(x, derivative: bool = False):
+    s = 1.0 / (1.0 + np.exp(-np.asarray(x, dtype=np.float64)))
+    return s * (1 - s) if derivative else s
+
+
+def softmax(x, axis: int = -1, epsilon=None):
+    x = np.asarray(x, dtype=np.float64)
+    e = np.exp(x - x.max(axis=axis, keepdims=True))
+    out = e / e.sum(axis=axis, keepdims=True)
+    return np.maximum(out, epsilon) if epsilon else out
+
+
+def relu(x, alpha: float = 0.0):
+    x = np.asarray(x)
+    return np.maximum(x, x * alpha)
+
+
+def one_hot(x, depth: int = 0, on_value: float = 1.0, off_value: float = 0.0):
+    x = np.asarray(x, dtype=np.int64)
+    depth = depth or int(x.max()) + 1
+    out = np.full(x.shape + (depth,), off_value, dtype=np.float32)
+    np.put_along_axis(out, x[..., None], on_value, axis=-1)
+    return out
+
+
+def fc(x, weights, biases=None, framework=None):
+    y = np.matmul(np.asarray(x), np.asarray(weights))
+    return y + biases if biases is not None else y
+
+
+def lstm(x, weights, biases=None, initial_internal_states=None, time_major: bool = False, forget_bias: float = 1.0):
+    """Numpy LSTM over [B, T, in] (or [T, B, in]); weights [in + units, 4 * units] in i, c, f, o order."""
+    x = np.asarray(x, dtype=np.float64)
+    if not time_major:
+        x = x.transpose(1, 0, 2)
+    T, B, _ = x.shape
+    units = weights.shape[1] // 4
+    c = np.zeros((B, units)) if initial_internal_states is None else initial_internal_states[0]
+    h = np.zeros((B, units)) if initial_internal_states is None else initial_internal_states[1]
+    out = np.zeros((T, B, units))
+    for t in range(T):
+        z = np.concatenate([x[t], h], axis=1) @ weights + (0 if biases is None else biases)
+        i, g, f, o = np.split(z, 4, axis=1)
+        c = c * sigmoid(f + forget_bias) + sigmoid(i) * np.tanh(g)
+        h = sigmoid(o) * np.tanh(c)
+        out[t] = h
+    return (out if time_major else out.transpose(1, 0, 2)), (c, h)
+
+
+# framework helpers: torch is THE framework here
+def try_import_torch(error: bool = False):
+    import torch
+    import torch.nn as nn
+
+    return torch, nn
+
+
+def try_import_tf(error: bool = False):
+    if error:
+        raise ImportError("TensorFlow is not part of this framework (PyTorch-ROCm only)")
+    return None, None, None
+
+
+def try_import_tfp(error: bool = False):
+    if error:
+        raise ImportError("TensorFlow Probability is not part of this framework")
+    return None
+
+
+def framework_iterator(config=None, frameworks=("torch",), session: bool = False, **kw):
+    """Yield each framework to test with; only "torch" exists here."""
+    for fw in frameworks:
+        if fw == "torch":
+            if config is not None and hasattr(config, "framework"):
+                config.framework("torch")
+            elif isinstance(config, dict):
+                config["framework"] = "torch"
+            yield "torch"
+
+
+# filters (reference utils/filter.py + filter_manager.py)
+class Filter:
+    def __call__(self, x, update: bool = True):
+        raise NotImplementedError
+
+    def apply_changes(self, other, with_buffer: bool = False):
+        pass
+
+    def copy(self):
+        return copy.deepcopy(self)
+
+    def sync(self, other):
+        self.__dict__.update(copy.deepcopy(other.__dict__))
+
+    def clear_buffer(self):
+        pass
+
+    def as_serializable(self):
+        return self.copy()
+
+
+class NoFilter(Filter):
+    def __call__(self, x, update: bool = True):
+        return np.asarray(x)
+
+
+class FilterManager:
+    @staticmethod
+    def synchronize(local_filters: Dict[str, Filter], workers, update_remote: bool = True, **kw):
+        """Merge every remote worker's filter deltas into the local filters, then push the merged
+        filters back (reference FilterManager.synchronize)."""
+        import ray_memory_management_amd as ray
+
+        remote = ray.get([w.get_filters.remote(flush_after=True) for w in workers])
+        for rf in remote:
+            for k, f in rf.items():
+                local_filters[k].apply_changes(f, with_buffer=False)
+        if update_remote:
+            copies = {k: v.as_serializable() for k, v in local_filters.items()}
+            ray.get([w.sync_filters.remote(copies) for w in workers])
+
+
+# test helpers (reference utils/test_utils.py)
+def check(x, y, decimals: int = 5, atol=None, rtol=None, false: bool = False) -> None:
+    if isinstance(x, dict):
+        assert isinstance(y, dict) and set(x) == set(y), (x, y)
+        for k in x:
+            check(x[k], y[k], decimals, atol, rtol, false)
+        return
+    if isinstance(x, (list, tuple)) and not isinstance(x, np.ndarray):
+        assert len(x) == len(y)
+        for a, b in zip(x, y):
+            check(a, b, decimals, atol, rtol, false)
+        return
+    xa, ya = np.asarray(x, dtype=np.float64), np.asarray(y, dtype=np.float64)
+    close = np.allclose(xa, ya, atol=atol if atol is not None else 0.5 * 10 ** -decimals,
+                        rtol=rtol if rtol is not None else 0.0)
+    assert close != false, f"check failed: {x} vs {y}"
+
+
+def check_env(env) -> None:
+    """Reset / step / spaces sanity check of a (single- or multi-agent) env."""
+    from ray_memory_management_amd.rllib.env import MultiAgentEnv
+
+    if not hasattr(env, "reset") or not hasattr(env, "step"):
+        raise ValueError(f"{env} is not an env (needs reset / step)")
+    obs = env.reset()
+    if isinstance(env, MultiAgentEnv):
+        acts = {a: env.action_space.sample() for a in obs}
+        o, r, d, i = env.step(acts)
+        if "__all__" not in d:
+            raise ValueError("multi-agent dones must contain '__all__'")
+        return
+    if not env.observation_space.contains(np.asarray(obs)):
+        raise ValueError(f"reset() observation {obs!r} is outside the observation space")
+    o, r, d, i = env.step(env.action_space.sample())
+    if not isinstance(d, (bool, np.bool_)):
+        raise ValueError("step() must return a bool done")
+
+
+def check_compute_single_action(algorithm, include_state: bool = False, include_prev_action_reward: bool = False):
+    pol = algorithm.get_policy()
+    obs = pol.observation_space.sample()
+    a = algorithm.compute_single_action(obs) if hasattr(algorithm, "compute_single_action") else \
+        pol.compute_single_action(obs)
+    if not pol.action_space.contains(np.asarray(a)):
+        raise ValueError(f"action {a!r} outside the action space")
+
+
+def check_train_results(train_results: Dict[str, Any]) -> Dict[str, Any]:
+    for key in ("episode_reward_mean", "timesteps_total", "training_iteration"):
+        if key not in train_results:
+            raise KeyError(f"`{key}` missing from train results")
+    return train_results
+
+
+__all__ = ["add_mixins", "check", "check_env", "check_compute_single_action", "check_train_results",
+           "deep_update", "deprecation_warning", "fc", "force_list", "force_tuple", "framework_iterator", "lstm",
+           "merge_dicts", "one_hot", "override", "relu", "sigmoid", "softmax", "try_import_tf", "try_import_tfp",
+           "try_import_torch", "ConstantSchedule", "DeveloperAPI", "ExponentialSchedule", "Filter", "FilterManager",
+           "LARGE_INTEGER", "LinearSchedule", "MAX_LOG_NN_OUTPUT", "MIN_LOG_NN_OUTPUT", "PiecewiseSchedule",
+           "PolynomialSchedule", "PublicAPI", "SMALL_NUMBER"]

@@ -63,6 +63,18 @@ class ExponentialSchedule(Schedule):
         return self.initial * self.decay ** (float(t) / self.T)
 
 
+class PolynomialSchedule(Schedule):
+    """initial → final over `schedule_timesteps` along (1 - t/T)^power, then final."""
+
+    def __init__(self, schedule_timesteps: int, final_p: float, initial_p: float = 1.0, power: float = 2.0):
+        self.T, self.final, self.initial, self.power = float(schedule_timesteps), float(final_p), float(initial_p), \
+            float(power)
+
+    def value(self, t):
+        frac = min(float(t), self.T) / self.T if self.T > 0 else 1.0
+        return self.final + (self.initial - self.final) * (1.0 - frac) ** self.power
+
+
 def make_schedule(spec, default: float) -> Schedule:
     """``None`` → constant default; list of [t, v] → piecewise; a Schedule passes through."""
     if spec is None:
