@@ -190,6 +190,10 @@ def _runtime(args, n_gpus):
              or k.startswith("TORCHELASTIC_")}
     if saved:
         print(f"[bench] runtime processes start without the launcher's {sorted(saved)}", file=sys.stderr)
+    if args.same_device and args.dist_backend == "nccl":
+        # 1-GPU rehearsal of the RCCL learner group: every learner claims its own host id so RCCL
+        # accepts several ranks on one device (socket transport over loopback; functional only)
+        os.environ["RMM_RCCL_SAME_DEVICE"] = "1"
     ray.init(num_cpus=n_cpus, num_gpus=phys, object_store_memory=args.store_gb << 30,
              _system_config={"prestart_workers": 0})
     try:
@@ -206,7 +210,7 @@ def _runtime(args, n_gpus):
                           num_gpus_per_learner_worker=(0.5 if args.rollout != "cpu" else 1.0) * phys / n_gpus,
                           # hybrid: CPU env, policy on the worker's slice of the learner's GPU
                           num_gpus_per_worker={"gpu": 0.5, "hybrid": 0.5 / w_per}.get(args.rollout, 0) * phys / n_gpus,
-                          learner_collective_backend="gloo" if args.same_device else args.dist_backend)
+                          learner_collective_backend=args.dist_backend)
                .debugging(seed=0))
         algo = cfg.build()
         info = {"rollout_workers": w_per * n_gpus, "envs_per_worker": envs, "learner_actors": n_gpus,
@@ -239,7 +243,8 @@ def main():
                     help="skip the extra runtime measurement with GPU rollout actors")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
-                    help="rehearsal on a 1-GPU box: every learner on GPU 0 (use --dist-backend gloo)")
+                    help="rehearsal on a 1-GPU box: every learner on GPU 0 (RCCL ranks get distinct host ids "
+                         "and use the socket transport; or --dist-backend gloo)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

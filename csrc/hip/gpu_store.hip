@@ -717,6 +717,9 @@ bool GpuStore::RestoreOne(Lock& lk, const std::string& id, GpuObject* o) {
   q.restoring = false;
   if (got != nbytes) {
     FreeLocked(slab, off, nbytes);
+    // a Delete() during the transfer only marked the object: it is still spilled, so this frees
+    // its host copy and the entry (nothing else would: no pins, so no Release follows)
+    if (q.delete_pending && q.pins == 0) DeleteLocked(id);
     cv_.notify_all();
     return false;
   }

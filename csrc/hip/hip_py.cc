@@ -10,6 +10,7 @@
 #include "common.h"
 #include "gpu_store.h"
 #include "kernels.h"
+#include "rccl_comm.h"
 
 namespace py = pybind11;
 using namespace rmm::hip;
@@ -488,4 +489,35 @@ PYBIND11_MODULE(_hip, m) {
     if (!ptr) throw std::runtime_error("GPU object not found");
     return make_dlpack(ptr, std::move(shape), code, bits, s->device(), s, sid, py::none());
   });
+
+  // ---------------------------------------------------------------- RCCL (framework-owned communicator)
+  m.def("rccl_load", &rccl_load, py::arg("path"));
+  m.def("rccl_unique_id", [] { return py::bytes(rccl_unique_id()); });
+  m.attr("NCCL_FLOAT32") = int(ncclFloat32);
+  m.attr("NCCL_BFLOAT16") = int(ncclBfloat16);
+  m.attr("NCCL_FLOAT16") = int(ncclFloat16);
+  m.attr("NCCL_INT32") = int(ncclInt32);
+  m.attr("NCCL_INT64") = int(ncclInt64);
+  m.attr("NCCL_UINT8") = int(ncclUint8);
+  m.attr("NCCL_FLOAT64") = int(ncclFloat64);
+  m.attr("NCCL_SUM") = int(ncclSum);
+  m.attr("NCCL_PROD") = int(ncclProd);
+  m.attr("NCCL_MAX") = int(ncclMax);
+  m.attr("NCCL_MIN") = int(ncclMin);
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;  // blocks until every rank has joined
+             return std::make_shared<RcclComm>(u, nranks, rank, device);
+           }),
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device"))
+      .def("all_reduce", &RcclComm::AllReduce, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
+           py::arg("op"), py::arg("stream"))
+      .def("broadcast", &RcclComm::Broadcast, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
+           py::arg("root"), py::arg("stream"))
+      .def("async_error", &RcclComm::AsyncError)
+      .def("abort", &RcclComm::Abort)
+      .def("destroy", &RcclComm::Destroy)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("rank", &RcclComm::rank);
 }

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -172,30 +173,35 @@ void host_register_segment(uintptr_t base, uint64_t size) {
 
 namespace {
 std::string g_reg_error;
-struct H2DStats {
-  uint64_t direct = 0, staged = 0, chunks_ok = 0, chunks_failed = 0;
+struct H2DStats {  // updated from several threads (learner ingest, spill / restore of each GpuStore)
+  std::atomic<uint64_t> direct{0}, staged{0}, chunks_ok{0}, chunks_failed{0};
 } g_h2d;
 
 // Page-locked bounce buffers for ranges the registry could not pin (e.g. pages another process on
 // the same GPU already registered): host memcpy into buffer k while buffer k^1 is in flight.
+// Shared by every thread of the process: `mu` is held for a whole staged transfer, and each buffer's
+// event orders its reuse after the DMA that last read / wrote it (whatever stream that was on).
 struct Staging {
   void* buf[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
+  std::mutex mu;
   static constexpr uint64_t kBytes = 32ull << 20;
 };
 Staging& Stage() {
   static Staging s;
-  if (!s.buf[0]) {
+  static std::once_flag once;
+  std::call_once(once, [] {
     for (int k = 0; k < 2; k++) {
       RMM_HIP_CHECK(hipHostMalloc(&s.buf[k], Staging::kBytes, hipHostMallocDefault));
       RMM_HIP_CHECK(hipEventCreateWithFlags(&s.ev[k], hipEventDisableTiming));
     }
-  }
+  });
   return s;
 }
 
 void staged_copy(void* dst, const void* src, uint64_t n, hipStream_t stream) {
   Staging& st = Stage();
+  std::lock_guard<std::mutex> g(st.mu);
   const uint8_t* s8 = static_cast<const uint8_t*>(src);
   uint8_t* d8 = static_cast<uint8_t*>(dst);
   int k = 0;
@@ -254,6 +260,7 @@ namespace {
 // D2H through the bounce buffers (host side is not page-locked).
 void staged_copy_d2h(void* dst, const void* src, uint64_t n, hipStream_t stream) {
   Staging& st = Stage();
+  std::lock_guard<std::mutex> g(st.mu);
   const uint8_t* s8 = static_cast<const uint8_t*>(src);
   uint8_t* d8 = static_cast<uint8_t*>(dst);
   for (uint64_t off = 0; off < n; off += Staging::kBytes) {
@@ -320,7 +327,9 @@ uint64_t h2d_from_segment(void* dst, const void* src, uint64_t n, hipStream_t st
   return newly;
 }
 
-std::vector<uint64_t> h2d_stats() { return {g_h2d.direct, g_h2d.staged, g_h2d.chunks_ok, g_h2d.chunks_failed}; }
+std::vector<uint64_t> h2d_stats() {
+  return {g_h2d.direct.load(), g_h2d.staged.load(), g_h2d.chunks_ok.load(), g_h2d.chunks_failed.load()};
+}
 
 void host_unregister_segment(uintptr_t base) {
   auto& R = Registry();

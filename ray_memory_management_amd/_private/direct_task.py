@@ -298,7 +298,12 @@ class DirectTaskSubmitter:
             with self.lock:
                 ks = self.keys[sk]
                 ks.pending -= 1
-                self._fail_queue(ks, exc.RaySystemError(f"worker lease failed: {reply!r}"))
+                if ks.leases or ks.pending > 0:
+                    # other leases of this key are live or still on their way: they run the queue
+                    # (pipelined), as the head path would keep the tasks waiting
+                    self._fill(ks, self.depth)
+                else:
+                    self._fail_queue(ks, exc.RaySystemError(f"worker lease failed: {reply!r}"))
             return
         _, lease_id, addr, wid, gpu_ids, node, need_lineage = reply
         with self.lock:

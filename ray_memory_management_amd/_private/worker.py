@@ -283,7 +283,9 @@ class CoreWorker:
                     gos.retry_deferred(self)
                 except Exception:
                     pass
-            if self.deltas:
+            # queued removals count too: a __del__ that lost the try-lock race (or ran inside a
+            # ref_lock critical section) is drained here, under ref_lock, by _take_deltas
+            if self.deltas or self._deferred_removes:
                 try:
                     self.send(None)
                 except Exception:
@@ -410,6 +412,10 @@ class CoreWorker:
             return ref
         with self.gpu_sink():
             data, bufs, contained = ser.serialize(value)
+        return self._put_serialized(oid, data, bufs, contained)
+
+    def _put_serialized(self, oid: bytes, data, bufs, contained) -> ObjectRef:
+        """Store an already-serialized value (`ser.serialize` output) under `oid`."""
         ref = ObjectRef(oid)
         if contained:
             self.send((P.CONTAINED, oid, contained))
@@ -557,15 +563,20 @@ class CoreWorker:
                 arg_refs.append(v.binary())
                 keep.append(v)
                 return ("r", v.binary())
+            # serialize ONCE (nested CUDA tensors become GPU objects here): a second pass for the
+            # by-ref case would create a second, unreferenced set of GPU objects
             with self.gpu_sink():
-                data, contained = ser.dumps_inline(v)
-            if len(data) > ser.INLINE_THRESHOLD:
-                ref = self.put_object(v)
+                data, bufs, contained = ser.serialize(v)
+            size = len(data) + sum(memoryview(b).nbytes for b in bufs)
+            if size > ser.INLINE_THRESHOLD:
+                ref = self._put_serialized(_ids.new_put_id(), data, bufs, contained)
                 keep.append(ref)
                 arg_refs.append(ref.binary())
                 return ("r", ref.binary())
             if contained:
                 arg_refs.extend(contained)
+            if bufs:  # small out-of-band buffers travel with the spec (writable on the worker)
+                return ("b", (data, [bytearray(b) for b in bufs]))
             return ("v", data)
 
         ea = [enc(a) for a in args]

@@ -141,6 +141,8 @@ class Executor:
         kind, v = enc
         if kind == "v":
             return ser.loads_inline(v)
+        if kind == "b":
+            return ser.deserialize(v[0], v[1])
         return self.w.get([ObjectRef(v)])[0]
 
     def resolve_all(self, args, kwargs):

@@ -14,6 +14,7 @@ the dense-bucket all-reduce behind the trunk backward).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -113,6 +114,112 @@ class GroupComm(Comm):
         from ray_memory_management_amd.util.collective import collective as col
 
         col.barrier(self.name)
+
+
+_RCCL_DT = None
+
+
+def _rccl_dtypes(h):
+    global _RCCL_DT
+    if _RCCL_DT is None:
+        _RCCL_DT = {torch.float32: h.NCCL_FLOAT32, torch.bfloat16: h.NCCL_BFLOAT16, torch.float16: h.NCCL_FLOAT16,
+                    torch.int32: h.NCCL_INT32, torch.int64: h.NCCL_INT64, torch.uint8: h.NCCL_UINT8,
+                    torch.float64: h.NCCL_FLOAT64}
+    return _RCCL_DT
+
+
+def rehearsal_host_id(tag: str, rank: int) -> None:
+    """1-GPU rehearsal of a multi-GPU RCCL group (``RMM_RCCL_SAME_DEVICE=1``): RCCL refuses two
+    ranks on one device of one host, so each rank claims its own host id and the ranks talk over
+    the socket transport on loopback. Functional only (the xGMI path needs one GPU per rank).
+    Must run before the process's first RCCL call."""
+    if os.environ.get("RMM_RCCL_SAME_DEVICE") == "1":
+        os.environ["NCCL_HOSTID"] = f"rmm-{tag}-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+
+class _StreamJoin:
+    def __init__(self, cs):
+        self.cs = cs
+
+    def wait(self):
+        torch.cuda.current_stream(self.cs.device).wait_stream(self.cs)
+        return True
+
+
+class RcclComm(Comm):
+    """A communicator the framework owns (csrc/hip/rccl_comm.cc), not torch.distributed's:
+
+    * collectives are enqueued on the stream the caller names, so they can be CAPTURED in a HIP
+      graph (``graph_capturable``) — the PPO learner forks its bucket all-reduces onto
+      ``self.stream`` inside the per-minibatch graph, next to the trunk backward;
+    * rendezvous: rank 0 makes the 128-byte unique id and publishes it in `store` (any
+      torch.distributed Store, e.g. the util.collective FileStore in the session directory).
+
+    Reference parity: the role of rllib/execution/multi_gpu_learner_thread.py's tower averaging and
+    util/collective/collective_group/nccl_collective_group.py's communicator cache."""
+
+    graph_capturable = True
+
+    def __init__(self, store, rank: int, world: int, key: str = "rmm-rccl-uid", device=None):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        h.rccl_load(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+        rehearsal_host_id(key, rank)
+        if rank == 0:
+            uid = h.rccl_unique_id()
+            store.set(key, uid)
+        else:
+            uid = store.get(key)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self._h = h
+        self._c = h.RcclComm(bytes(uid), int(world), int(rank), self.device.index)
+        self.world, self.rank = int(world), int(rank)
+        self.stream = torch.cuda.Stream(self.device)  # comm stream (forked to inside graphs)
+        self._ops = {"sum": h.NCCL_SUM, "max": h.NCCL_MAX, "min": h.NCCL_MIN, "prod": h.NCCL_PROD}
+
+    def _args(self, t):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("RcclComm collectives need contiguous device tensors")
+        return t.data_ptr(), t.numel(), _rccl_dtypes(self._h)[t.dtype]
+
+    def allreduce_on(self, t, stream, op="sum"):
+        p, n, dt = self._args(t)
+        self._c.all_reduce(p, p, n, dt, self._ops[op], stream.cuda_stream)
+
+    def allreduce(self, t, op="sum"):
+        self.allreduce_on(t, torch.cuda.current_stream(self.device), op)
+
+    def allreduce_async(self, t, op="sum"):
+        """Fork onto the comm stream; wait() joins the caller's current stream back."""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        self.allreduce_on(t, self.stream, op)
+        t.record_stream(self.stream)
+        return _StreamJoin(self.stream)
+
+    def broadcast(self, t, src=0):
+        p, n, dt = self._args(t)
+        self._c.broadcast(p, p, n, dt, int(src), torch.cuda.current_stream(self.device).cuda_stream)
+
+    def barrier(self):
+        x = torch.zeros(1, device=self.device)
+        self.allreduce(x)
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def check(self):
+        """Raise if the communicator hit an asynchronous error (e.g. a peer died)."""
+        e = self._c.async_error()
+        if e:
+            raise RuntimeError(f"RCCL communicator error: {e}")
+
+    def close(self):
+        try:
+            self._c.destroy()
+        except Exception:
+            self._c.abort()
 
 
 def default_comm(process_group=None) -> Comm:

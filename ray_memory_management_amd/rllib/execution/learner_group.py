@@ -45,7 +45,17 @@ class LearnerActor:
 
             require_hip()  # the fused learner needs the HIP kernels: fail loudly if they are missing
             torch.cuda.set_device(0)
-        if world > 1:
+        if world > 1 and backend == "nccl" and self.device != "cpu" and not os.environ.get("RMM_TORCH_PG_COMM"):
+            # framework-owned RCCL communicator: its all-reduces are captured INSIDE the SGD-step
+            # graph (torch's ProcessGroupNCCL aborts on captured collectives on ROCm)
+            import torch.distributed as dist
+
+            from ray_memory_management_amd.parallel.comm import RcclComm
+            from ray_memory_management_amd.util.collective.collective import _store_path
+
+            store = dist.FileStore(_store_path(group_name), world)
+            comm = RcclComm(store, rank, world, key=f"{group_name}-rccl")
+        elif world > 1:
             from ray_memory_management_amd.util.collective import collective as col
 
             col.init_collective_group(world, rank, backend, group_name)
@@ -113,11 +123,18 @@ class LearnerActor:
             h.update(v.tobytes())
         return h.hexdigest()
 
+    def comm_info(self):
+        """Which communicator carries the gradients and whether the SGD-step graph contains them."""
+        L = self.learner
+        return {"comm": type(L.comm).__name__, "graph_has_comm": bool(L._graph_has_comm),
+                "split_graphs": L._graphs_split is not None, "graphs": bool(L.graphs)}
+
     def device_info(self):
         import torch
 
         info = {"rank": self.rank, "device": self.device, "pid": os.getpid(),
-                "HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES")}
+                "HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
+                "comm": type(self.learner.comm).__name__}
         if self.device != "cpu":
             info["pci_bus_id"] = getattr(torch.cuda.get_device_properties(0), "pci_bus_id", None)
         return info
