@@ -458,10 +458,14 @@ class PPOLearner:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._graph = self._graphs_split = None
         self._graph_has_comm = False
-        if self.world > 1 and manual and getattr(self.comm, "graph_capturable", False):
+        if self.world > 1 and manual and getattr(self.comm, "graph_capturable", False) \
+                and os.environ.get("RMM_RCCL_IN_GRAPH") == "1":
             # ONE graph per SGD step with the all-reduces inside it: after K12 the graph forks onto
             # the comm stream (dense+heads bucket, ≈99% of the bytes) while K10 backward runs on
-            # the compute stream, then reduces the small trunk bucket and joins before K6 Adam
+            # the compute stream, then reduces the small trunk bucket and joins before K6 Adam.
+            # Opt-in: a captured RCCL op over the socket transport (the 1-GPU rehearsal) crashes
+            # hipGraph capture on torch's RCCL 2.26 (profiles/rccl_native_r3.txt), so the default
+            # multi-rank step is the split-graph one below with the same fork/join done eagerly
             cs = self.comm.stream
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):

@@ -3,9 +3,8 @@
 GPU tests run 2 ranks on ONE MI355X: with RMM_RCCL_SAME_DEVICE=1 each rank claims its own RCCL host
 id, so RCCL accepts both ranks on one device and connects them over its socket transport (the
 8-GPU node uses xGMI; the code path above the transport is the same). Checked: all-reduce / broadcast
-values, all-reduces captured inside a HIP graph on a forked comm stream (what the PPO learner does
-per SGD step), and 2 PPO learner actors whose in-graph gradient all-reduces keep the replicas
-bit-identical. Reference parity: util/collective/tests/single_node_gpu_tests/test_allreduce.py and
+values, all-reduces forked onto the comm stream between graph replays (the PPO learner's multi-rank
+SGD step), and 2 PPO learner actors whose gradient all-reduces keep the replicas bit-identical. Reference parity: util/collective/tests/single_node_gpu_tests/test_allreduce.py and
 rllib/execution/tests/test_multi_gpu_learner_thread.py."""
 import os
 import subprocess
@@ -37,45 +36,62 @@ c.broadcast(b, 1)
 torch.cuda.synchronize()
 ok = float(x.float().min()) == world * (world + 1) / 2 and float(y[0]) == world - 1
 ok = ok and torch.equal(b.cpu(), torch.arange(5, dtype=torch.float32) * 2)
-# fork / join inside a captured graph: compute on the capture stream, all-reduce on the comm stream
+# eager fork / join around graph replays (the learner's split-graph step): compute graph, the
+# all-reduce forked onto the comm stream, more compute overlapping it, join, finishing graph
 a = torch.zeros(4096, device=dev)
 z = torch.zeros(16, device=dev)
+g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
 s = torch.cuda.Stream(dev)
 s.wait_stream(torch.cuda.current_stream())
 with torch.cuda.stream(s):
-    h = c.allreduce_async(a); h.wait()
+    a.add_(0.0); z.add_(0.0); a.mul_(1.0)
 torch.cuda.current_stream().wait_stream(s)
 torch.cuda.synchronize()
-g = torch.cuda.CUDAGraph()
-with torch.cuda.graph(g):
-    cap = torch.cuda.current_stream()
+with torch.cuda.graph(g1):
     a.add_(float(rank + 1))
-    c.stream.wait_stream(cap)
-    c.allreduce_on(a, c.stream)
-    z.add_(1.0)  # overlaps the collective
-    cap.wait_stream(c.stream)
+with torch.cuda.graph(g2):
+    z.add_(1.0)
+with torch.cuda.graph(g3):
     a.mul_(0.5)
 a.zero_()
 for _ in range(3):
-    g.replay()
+    g1.replay()
+    h = c.allreduce_async(a)
+    g2.replay()  # overlaps the collective
+    h.wait()
+    g3.replay()
 torch.cuda.synchronize()
-# replay k: a = (a_prev + sum(rank+1 over ranks)) / 2 ... with a reset to 0 before the first replay
 want = 0.0
 for _ in range(3):
     want = (want * world + world * (world + 1) / 2) * 0.5
 ok = ok and abs(float(a[0]) - want) < 1e-3 and float(z[0]) == 3.0
+if os.environ.get("RMM_RCCL_IN_GRAPH") == "1":  # the collective captured inside one graph
+    gg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gg, capture_error_mode=os.environ.get("RMM_CAPTURE_MODE", "thread_local")):
+        cap = torch.cuda.current_stream()
+        a.add_(1.0)
+        if os.environ.get("RMM_RCCL_FORK", "1") == "1":
+            c.stream.wait_stream(cap)
+            c.allreduce_on(a, c.stream)
+            cap.wait_stream(c.stream)
+        else:
+            c.allreduce_on(a, cap)
+    a.zero_()
+    gg.replay()
+    torch.cuda.synchronize()
+    ok = ok and float(a[0]) == world
 c.check()
 c.close()
 print("RESULT", rank, ok, float(a[0]), want, flush=True)
 """
 
 
-def _spawn(world=2, timeout=240):
+def _spawn(world=2, timeout=240, env=None):
     d = tempfile.mkdtemp(prefix="rccl_t_")
     script = os.path.join(d, "child.py")
     with open(script, "w") as f:
         f.write(_CHILD.format(root=ROOT))
-    env = dict(os.environ, RMM_RCCL_SAME_DEVICE="1")
+    env = dict(os.environ, RMM_RCCL_SAME_DEVICE="1", **(env or {}))
     ps = [subprocess.Popen([sys.executable, script, str(r), str(world), os.path.join(d, "store")], env=env,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
@@ -115,7 +131,7 @@ def test_rccl_binding_loads_and_makes_unique_ids():
 
 
 @pytest.mark.gpu
-def test_rccl_comm_two_ranks_one_gpu_in_graph():
+def test_rccl_comm_two_ranks_one_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     outs = _spawn(2)
@@ -126,9 +142,9 @@ def test_rccl_comm_two_ranks_one_gpu_in_graph():
 
 
 @pytest.mark.gpu
-def test_ppo_learner_actors_rccl_allreduce_in_graph(ray_start):
-    """2 fused PPO learner actors on one GPU over the native RCCL communicator: the gradient
-    all-reduces are captured in the SGD-step graph and the replicas stay bit-identical."""
+def test_ppo_learner_actors_rccl_identical(ray_start):
+    """2 fused PPO learner actors on one GPU over the native RCCL communicator (bucket all-reduces
+    forked onto the comm stream between the SGD step's graphs): the replicas stay bit-identical."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import ray_memory_management_amd as ray
@@ -151,7 +167,7 @@ def test_ppo_learner_actors_rccl_allreduce_in_graph(ray_start):
             st = r["info"]["learner"]["default_policy"]["learner_stats"]
             assert np.isfinite(st["total_loss"]) and st["num_learners"] == 2
             info = ray.get([a.comm_info.remote() for a in algo.learner_group.learners])
-            assert all(i["comm"] == "RcclComm" and i["graph_has_comm"] for i in info), info
+            assert all(i["comm"] == "RcclComm" and (i["graph_has_comm"] or i["split_graphs"]) for i in info), info
             d = algo.learner_group.weights_digests()
             assert d[0] == d[1]
         finally:
