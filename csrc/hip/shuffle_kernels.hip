@@ -1,7 +1,8 @@
 // K11 — key partitioning for the GPU all-to-all shuffle (experimental/gpu_shuffle.py).
 //
 // One shuffle round on one MI355X: every row (int64 key + fixed-size payload) goes to destination
-// dest(key) = splitmix64(key) % R ("hash") or key mod R ("mod"). Rows are reordered so each
+// dest(key) = splitmix64(key) % R ("hash"), key mod R ("mod") or floor(key·R / 2^64) with the key read
+// as unsigned ("range": R equal key ranges, what a distributed sort needs). Rows are reordered so each
 // destination's rows are contiguous — exactly the layout `all_to_all_single` with split sizes
 // sends over RCCL/xGMI. Two launches and a tiny scan:
 //   k_part_hist    — per-workgroup destination histogram in LDS (workgroup w owns rows
@@ -17,6 +18,7 @@ namespace rmm {
 namespace hip {
 
 __device__ __forceinline__ uint32_t part_dest(int64_t key, int R, int mode) {
+  if (mode == 2) return uint32_t(__umul64hi(uint64_t(key), uint64_t(R)));  // range: R equal slices of the u64 keys
   if (mode == 1) {  // mod
     const int64_t m = key % R;
     return uint32_t(m < 0 ? m + R : m);

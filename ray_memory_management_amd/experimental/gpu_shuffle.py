@@ -28,7 +28,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-MODES = {"hash": 0, "mod": 1}
+MODES = {"hash": 0, "mod": 1, "range": 2}
 
 
 def _splitmix64(keys: torch.Tensor) -> np.ndarray:
@@ -48,6 +48,11 @@ def destinations(keys: torch.Tensor, num_partitions: int, mode: str = "hash") ->
     k = keys.detach().cpu().to(torch.int64)
     if mode == "mod":
         return torch.remainder(k, num_partitions)
+    if mode == "range":  # floor(u64(key) * R / 2^64) without 128-bit arithmetic (R <= 1024)
+        u = k.numpy().view(np.uint64)
+        hi, lo = u >> np.uint64(32), u & np.uint64(0xFFFFFFFF)
+        R = np.uint64(num_partitions)
+        return torch.from_numpy(((hi * R + ((lo * R) >> np.uint64(32))) >> np.uint64(32)).astype(np.int64))
     return torch.from_numpy((_splitmix64(k) % np.uint64(num_partitions)).astype(np.int64))
 
 
