@@ -98,6 +98,64 @@ __device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint
   }
 }
 
+// load_frame split in two so the HBM frame loads can be issued before the weight staging and the
+// LDS zeroing (they are independent): frame_issue starts the loads, frame_store transposes and writes
+// the interior; only the 2-pixel border needs zeros (zero_frame_border), so no barrier separates
+// zeroing from the interior stores.
+template <int NT>
+struct FrameRegs {
+  static constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
+  uint32_t v[PER][C0];
+};
+template <int NT>
+__device__ __forceinline__ void frame_issue(const uint8_t* __restrict__ src, FrameRegs<NT>& f) {
+  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
+#pragma unroll
+    for (int c = 0; c < C0; c++) f.v[k][c] = s32[c * NW + o];
+  }
+}
+template <int NT>
+__device__ __forceinline__ void frame_store(const FrameRegs<NT>& f, uint8_t* frame) {
+  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + NT * k;
+    if (o < NW) {
+      const int y = o / 21, x = 4 * (o - y * 21);
+      uint32_t px[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        px[q] = ((f.v[k][0] >> (8 * q)) & 0xffu) | (((f.v[k][1] >> (8 * q)) & 0xffu) << 8) |
+                (((f.v[k][2] >> (8 * q)) & 0xffu) << 16) | (((f.v[k][3] >> (8 * q)) & 0xffu) << 24);
+      uint2* d = reinterpret_cast<uint2*>(frame + ((y + 2) * P0 + x + 2) * 4);
+      d[0] = make_uint2(px[0], px[1]);
+      d[1] = make_uint2(px[2], px[3]);
+    }
+  }
+}
+// zero rows 0, 1, 86, 87 and columns 0, 1, 86, 87 of the padded HWC frame (one u32 = one pixel)
+__device__ __forceinline__ void zero_frame_border(uint8_t* frame) {
+  uint32_t* f32 = reinterpret_cast<uint32_t*>(frame);
+  constexpr int NROW = 4 * P0, NCOL = (P0 - 4) * 4;
+  for (int i = threadIdx.x; i < NROW + NCOL; i += blockDim.x) {
+    int y, x;
+    if (i < NROW) {
+      const int r = i / P0;
+      y = r < 2 ? r : r + (P0 - 4);
+      x = i - r * P0;
+    } else {
+      const int j = i - NROW, c = j & 3;
+      y = 2 + (j >> 2);
+      x = c < 2 ? c : c + (P0 - 4);
+    }
+    f32[y * P0 + x] = 0u;
+  }
+}
+
 // Backward variant: the padded frame in space-to-depth form, transposed, bf16 (exact for 0..255):
 // padded pixel (yp, xp) = (y+2, x+2) = (4Y+ry, 4X+rx), channel ci → st[c][Y*ST_W + X] with
 // c = 16ry + 4rx + ci. conv1 (8x8/4) is then a 2x2 stride-1 correlation over a 64-channel 22x22
@@ -107,6 +165,25 @@ __device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint
 // columns 22, 23 stay zero: K padding), channel pitch 552 el = 276 dwords (8 lanes reading 8
 // channels hit distinct 4-bank groups).
 constexpr int ST_W = 24, ST_CP = 23 * ST_W, ST_C = 64;
+template <int NT>
+__device__ __forceinline__ void frame_store_s2d(const FrameRegs<NT>& f, unsigned short* st) {
+  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + NT * k;
+    if (o < NW) {
+      const int y = o / 21, xw = o - y * 21;  // pixels x = 4xw .. 4xw+3 → xp = 4xw+2 .. 4xw+5
+      const int yp = y + 2;
+      unsigned short* row = st + (16 * (yp & 3)) * ST_CP + (yp >> 2) * ST_W + xw;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int rx = (q + 2) & 3, dX = (q + 2) >> 2;
+#pragma unroll
+        for (int c = 0; c < C0; c++) row[(4 * rx + c) * ST_CP + dX] = u8bf((f.v[k][c] >> (8 * q)) & 0xffu);
+      }
+    }
+  }
+}
 template <int NT>
 __device__ __forceinline__ void load_frame_s2d(const uint8_t* __restrict__ src, unsigned short* st) {
   constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
@@ -200,12 +277,16 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
   const int64_t* idx = window(idx0, ctr, period, B);
   const int64_t src = idx ? idx[b] : b;
 
-  zero_lds(frame, FRAME_BYTES);
+  // the frame's HBM loads go out first and stay in flight through the weight staging (L2) and the
+  // LDS zeroing; one barrier then covers weights, zeros and the frame interior
+  FrameRegs<NTF> fr;
+  frame_issue<NTF>(obs + src * (C0 * H0 * H0), fr);
+  zero_frame_border(frame);
   zero_lds(h1p, H1P_ELEMS * 2);
   stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
   stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
+  frame_store<NTF>(fr, frame);
   __syncthreads();
-  if (!(dbg & 4)) load_frame<NTF>(obs + src * (C0 * H0 * H0), frame);
 
   // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
   // j → (kx = 2g + (j>>2), ci = j&3); col = co = r: one 16-B LDS read each.
@@ -213,7 +294,6 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
 #pragma unroll
   for (int s = 0; s < 8; s++) wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&w1s[r * W1_PITCH + (s * 8 + 2 * g) * 4]));
   const float bias1 = bf2f(b1[r]);
-  __syncthreads();
 
   // ---- conv1: 28 M-tiles of 16 positions over 4 waves
   for (int mt = wave; mt < NP1P / 16; mt += NTF / 64) {
@@ -305,6 +385,22 @@ static_assert(KSTEPS1 * 32 + ST_W <= 24 * ST_W, "dpre1 copy K padding");
 // grid = G workgroups of 8 waves (2 per SIMD hide the LDS/MFMA latency chains of one frame),
 // each loops over frames b = blockIdx.x, +G, ...
 constexpr int NTB = 512;
+constexpr int BWD_NH1 = NP1 * 2, BWD_PH1 = (BWD_NH1 + NTB - 1) / NTB;  // 882 x 16 B
+constexpr int BWD_NH2 = NP2 * 4, BWD_PH2 = (BWD_NH2 + NTB - 1) / NTB;  // 484 x 16 B
+// P0 global loads of frame bb (clamped and unconditional, see load_frame)
+__device__ __forceinline__ void bwd_issue(int64_t bb, const int64_t* __restrict__ idx, const uint8_t* __restrict__ obs,
+                                          const unsigned short* __restrict__ h1, const unsigned short* __restrict__ h2,
+                                          const unsigned short* __restrict__ dh2, FrameRegs<NTB>& fr,
+                                          uint4 (&hv1)[BWD_PH1], u16x8 (&hv2)[BWD_PH2], u16x8 (&gv2)[BWD_PH2]) {
+  const int64_t src = idx ? idx[bb] : bb;
+  frame_issue<NTB>(obs + src * (C0 * H0 * H0), fr);
+#pragma unroll
+  for (int k = 0; k < BWD_PH2; k++) {
+    const int v = min(int(threadIdx.x) + NTB * k, BWD_NH2 - 1);
+    hv2[k] = *reinterpret_cast<const u16x8*>(&h2[(bb * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
+    gv2[k] = *reinterpret_cast<const u16x8*>(&dh2[(bb * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
+  }
+}
 __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ h1,
@@ -361,26 +457,23 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   zero_lds(dp1s, 2 * DB_B * 2);
   __syncthreads();
 
+  // P0 is software-pipelined across this workgroup's frames: the global loads of frame b + G are
+  // issued right after frame b's LDS tiles are written and stay in flight (registers) through
+  // frame b's P1 / P2 MFMA phases, so only the first frame pays the HBM latency in the open.
+  constexpr int NH1 = BWD_NH1, PH1 = BWD_PH1, NH2 = BWD_NH2, PH2 = BWD_PH2;
+  FrameRegs<NTB> fr;
+  uint4 hv1[PH1];
+  u16x8 hv2[PH2], gv2[PH2];
+  if (!(dbg & 8) && int64_t(blockIdx.x) < B) bwd_issue(blockIdx.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
-    const int64_t src = idx ? idx[b] : b;
-    // ---- P0: stage frame, h1, dpre2
-    if (!(dbg & 8)) load_frame_s2d<NTB>(obs + src * (C0 * H0 * H0), st);
-    if (!(dbg & 8)) {  // h1 [441][16] → padded LDS tile; h2, dh2 → dpre2 (both layouts) + db2. Loads first.
-      constexpr int NH1 = NP1 * 2, PH1 = (NH1 + NTB - 1) / NTB;  // 882 x 16 B
-      constexpr int NH2 = NP2 * 4, PH2 = (NH2 + NTB - 1) / NTB;  // 484 x 16 B
-      uint4 hv1[PH1];
-      u16x8 hv2[PH2], gv2[PH2];
+    // ---- P0: frame (space-to-depth), h1 → padded tile, h2 / dh2 → dpre2 (both layouts) + db2
+    if (!(dbg & 8)) {
 #pragma unroll
-      for (int k = 0; k < PH1; k++) {  // clamped, unconditional (see load_frame)
+      for (int k = 0; k < PH1; k++) {  // h1 of this frame: loaded here (prefetching it too spills)
         const int v = min(int(threadIdx.x) + NTB * k, NH1 - 1);
         hv1[k] = *reinterpret_cast<const uint4*>(&h1[(b * NP1 + (v >> 1)) * C1 + 8 * (v & 1)]);
       }
-#pragma unroll
-      for (int k = 0; k < PH2; k++) {
-        const int v = min(int(threadIdx.x) + NTB * k, NH2 - 1);
-        hv2[k] = *reinterpret_cast<const u16x8*>(&h2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
-        gv2[k] = *reinterpret_cast<const u16x8*>(&dh2[(b * NP2 + (v >> 2)) * C2 + 8 * (v & 3)]);
-      }
+      frame_store_s2d<NTB>(fr, st);
 #pragma unroll
       for (int k = 0; k < PH1; k++) {
         const int v = threadIdx.x + NTB * k;
@@ -408,6 +501,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
       }
     }
     __syncthreads();
+    if (!(dbg & 8) && b + gridDim.x < B) bwd_issue(b + gridDim.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);  // next frame: in flight through P1 / P2
 
     // ---- P1a: dW2[co2][k=(ky,kx,ci)] += Σ_q dpre2[q][co2] · h1p[2oy+ky][2ox+kx][ci]
 #pragma unroll

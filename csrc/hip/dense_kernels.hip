@@ -608,12 +608,20 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd2(
 __global__ __launch_bounds__(256) void k_dense_fwd(const unsigned short* __restrict__ x,
                                                    const unsigned short* __restrict__ w,
                                                    const unsigned short* __restrict__ b, int64_t M, int64_t K, int N,
-                                                   unsigned short* __restrict__ y) {
+                                                   unsigned short* __restrict__ y, int xcd_remap) {
   // 4 waves split K (wave w takes k-steps s ≡ w mod 4), 4 accumulator chains each, partial tiles
   // combined through LDS in a fixed order: the serial L2-latency chain per wave is K/128 deep.
   __shared__ f32x4 part[3][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const int64_t m0 = int64_t(blockIdx.x) * 16, n0 = int64_t(blockIdx.y) * 16;
+  // 1-D grid of (M/16) x (N/16) tiles. XCD-aware order (guide §5.5 T1): blocks id, id+8, ... share
+  // an XCD (and its 4 MB L2), so give each XCD a CONTIGUOUS run of tiles = a few 16-row x slices
+  // against all of W. Its L2 then holds ~2.5 MB (W + its x rows) instead of the whole 6 MB
+  // working set every XCD touches in raster order (which streams from the Infinity Cache).
+  const int nn = N / 16;
+  const int64_t total = gridDim.x;
+  int64_t id = blockIdx.x;
+  if (xcd_remap && (total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+  const int64_t m0 = (id / nn) * 16, n0 = (id % nn) * 16;
   const int64_t xr = min(m0 + r, M - 1);
   const unsigned short* xa = x + xr * K + 8 * g;
   const unsigned short* wb = w + (n0 + r) * K + 8 * g;
@@ -989,9 +997,13 @@ void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int6
                     hipStream_t stream) {
   if (M <= 0) return;
   if (K % 32 != 0 || N % 16 != 0) throw std::invalid_argument("dense_relu_fwd: K % 32 == 0 and N % 16 == 0");
-  hipLaunchKernelGGL(dense::k_dense_fwd, dim3(uint32_t((M + 15) / 16), uint32_t(N / 16)), dim3(256), 0, stream,
+  static const int remap = [] {  // RMM_K13_NOREMAP=1: raster tile order (A/B timing)
+    const char* e = std::getenv("RMM_K13_NOREMAP");
+    return (e && e[0] == '1') ? 0 : 1;
+  }();
+  hipLaunchKernelGGL(dense::k_dense_fwd, dim3(uint32_t(((M + 15) / 16) * (N / 16))), dim3(256), 0, stream,
                      static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(w),
-                     static_cast<const unsigned short*>(b), M, K, N, static_cast<unsigned short*>(y));
+                     static_cast<const unsigned short*>(b), M, K, N, static_cast<unsigned short*>(y), remap);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

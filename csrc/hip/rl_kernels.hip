@@ -397,13 +397,14 @@ int bump_done_words() { return kBumpWords; }
 
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr, int64_t* bump, int nbump,
-               uint32_t* done, const float* scale_ptr) {
+               uint32_t* done, const float* scale_ptr, int max_blocks) {
   if (n <= 0) return;
   auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
   const bool vec = al(master, 16) && al(m1, 16) && al(m2, 16) && al(grad, grad_bf16 ? 8 : 16) &&
                    (wbf16 == nullptr || al(wbf16, 8));
   const int64_t work = vec ? (n + 3) / 4 : n;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 256 * 8));
+  // max_blocks > 0 caps the grid (an Adam that runs BESIDE another kernel takes few wave slots)
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, max_blocks > 0 ? max_blocks : 256 * 8));
   auto go = [&](auto kern, const auto* g) {
     hipLaunchKernelGGL(kern, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2, g,
                        static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n, step_ctr, bump, nbump, done,

@@ -355,6 +355,46 @@ class PPOLearner:
                     step_ctr=self.ctr.data_ptr() + 8, bump=self.ctr.data_ptr(), nbump=2,
                     done=self._bump_done.data_ptr(), scale_ptr=scale_ptr)
 
+    def _adam_range(self, lo: int, hi: int, stream: int, bump: bool, max_blocks: int = 0):
+        """K6 over params [lo, hi) of the flat buckets on `stream`; `bump` advances the device
+        counters (exactly one launch per SGD step may)."""
+        h = require_hip()
+        f4, b2 = 4 * lo, 2 * lo
+        h.adam_flat(self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
+                    self.flat_grad.data_ptr() + b2, True, self.w_bf16.data_ptr() + b2, self.hp.data_ptr(),
+                    1.0 / self.world, hi - lo, stream, step_ctr=self.ctr.data_ptr() + 8,
+                    bump=self.ctr.data_ptr() if bump else 0, nbump=2 if bump else 0,
+                    done=self._bump_done.data_ptr() if bump else 0, max_blocks=max_blocks)
+
+    def _split_adam_ok(self) -> bool:
+        """The dense+heads Adam can run beside the trunk backward: their buffers are disjoint and
+        only a global-norm clip (needs every gradient first) couples them. Bucket offsets must keep
+        K6's 16-B vector alignment. Opt-in (RMM_SPLIT_ADAM_BLOCKS=<grid cap>): with the full
+        977-block grid beside K10 backward the SGD step got 16 µs SLOWER on MI355X (the Adam
+        waves delay the LDS-bound trunk workgroups), profiles/split_adam_r3.txt."""
+        return (self._manual is not None and self.clip_out is None and self._manual % 4 == 0
+                and int(os.environ.get("RMM_SPLIT_ADAM_BLOCKS", "0")) > 0)
+
+    def _overlapped_tail(self, full):
+        """World of one: after K12 the dense+heads gradients are final, so their Adam (≈99% of the
+        parameters, ~8 µs of memory traffic) runs on a side stream WHILE the trunk backward (256
+        LDS-bound workgroups, one per CU, leaving most wave slots free) runs on the capture stream;
+        the trunk Adam then joins and advances the step counters."""
+        cap = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        side.wait_stream(cap)
+        self._adam_range(self._manual, self.n_params, side.cuda_stream, bump=False,
+                         max_blocks=int(os.environ.get("RMM_SPLIT_ADAM_BLOCKS", "0")))
+        self._manual_trunk_bwd(full)
+        cap.wait_stream(side)
+        self._adam_range(0, self._manual, cap.cuda_stream, bump=True)
+
+    def _side_stream(self):
+        s = getattr(self, "_side", None)
+        if s is None:
+            s = self._side = torch.cuda.Stream(self.device)
+        return s
+
     def _opt_step(self):
         if self.world > 1:
             self.comm.allreduce(self.flat_grad)
@@ -424,6 +464,9 @@ class PPOLearner:
                 work2 = self.comm.allreduce_async(self.flat_grad[:self._manual])  # trunk bucket
                 work.wait()
                 work2.wait()
+            elif self._split_adam_ok():
+                self._overlapped_tail(full)
+                return
             else:
                 self._manual_trunk_bwd(full)
             self._opt_launch()
@@ -480,6 +523,12 @@ class PPOLearner:
                 self._opt_launch()
             self._graph = g
             self._graph_has_comm = True
+        elif self.world == 1 and manual and self._split_adam_ok():
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._manual_fwd_dense_bwd(full)
+                self._overlapped_tail(full)
+            self._graph = g
         elif self.world == 1 or self.cfg["allreduce_in_graph"]:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
