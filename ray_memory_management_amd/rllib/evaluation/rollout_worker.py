@@ -77,7 +77,11 @@ class RolloutWorker:
                                             worker_index)
         self.input_reader = None
         inp = self.config.get("input", "sampler")
-        if inp and inp != "sampler":
+        if callable(inp):  # input creator(ioctx) -> InputReader (e.g. PolicyServerInput)
+            from ray_memory_management_amd.rllib.offline import IOContext
+
+            self.input_reader = inp(IOContext(config=self.config, worker_index=worker_index, worker=self))
+        elif inp and inp != "sampler":
             from ray_memory_management_amd.rllib.offline import JsonReader, ShuffledInput
 
             self.input_reader = ShuffledInput(JsonReader(inp, seed=base_seed),
@@ -338,6 +342,23 @@ class RolloutWorker:
             warnings.simplefilter("ignore", UserWarning)
             self.policy.set_weights({k: (v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v)))
                                      for k, v in weights.items()})
+
+    # ------------------------------------------------------------------ learning (policy templates)
+    def learn_on_batch(self, samples) -> Dict:
+        return {"default_policy": self.policy.learn_on_batch(samples)}
+
+    def compute_gradients(self, samples):
+        return self.policy.compute_gradients(samples)
+
+    def apply_gradients(self, grads) -> None:
+        self.policy.apply_gradients(grads)
+
+    def get_global_vars(self) -> Dict:
+        return {"timestep": getattr(self.policy, "global_timestep", 0)}
+
+    def set_global_vars(self, global_vars: Dict) -> None:
+        if "timestep" in (global_vars or {}):
+            self.policy.global_timestep = global_vars["timestep"]
 
     def get_metrics(self) -> List[tuple]:
         out, self._completed = self._completed, []

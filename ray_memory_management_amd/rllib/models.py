@@ -496,6 +496,10 @@ def _same_pad(hw, k, s):
 
 def build_model(obs_space, action_space, model_config=None) -> nn.Module:
     model_config = model_config or {}
+    if model_config.get("custom_model"):  # a registered ModelV2 (ModelCatalog), behind (logits, value)
+        from ray_memory_management_amd.rllib.modelv2 import build_custom_model
+
+        return build_custom_model(obs_space, action_space, model_config)
     n = getattr(action_space, "n", None)
     if n is None:
         n = 2 * int(torch.tensor(action_space.shape).prod())  # diag-gaussian mean+logstd
@@ -511,3 +515,9 @@ def build_model(obs_space, action_space, model_config=None) -> nn.Module:
     return FullyConnectedNetwork(obs_dim, n, model_config.get("fcnet_hiddens", (256, 256)),
                                  model_config.get("fcnet_activation", "tanh"),
                                  model_config.get("vf_share_layers", False))
+
+
+# ModelV2 API surface (reference rllib/models/__init__.py)
+from ray_memory_management_amd.rllib.modelv2 import (  # noqa: E402,F401
+    MODEL_DEFAULTS, ActionDistribution, ModelCatalog, ModelV2, Preprocessor, TorchCategorical, TorchDiagGaussian,
+    TorchModelV2, get_preprocessor)

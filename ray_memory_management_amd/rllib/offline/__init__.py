@@ -339,3 +339,46 @@ class ImportanceSampling(OffPolicyEstimator):
 class WeightedImportanceSampling(OffPolicyEstimator):
     def estimate(self, batch):
         return importance_sampling_estimate(batch, self._new_logp(batch), self.gamma, weighted=True)
+
+
+# ---------------------------------------------------------------------------- dataset input helpers
+def get_dataset_and_shards(config: dict, num_workers: int = 0, local_worker: bool = False):
+    """reference rllib/offline/dataset_reader.py:get_dataset_and_shards: for ``input="dataset"``
+    read ``input_config = {"format": "json" | "parquet", "path" | "paths": ...}`` (or take a
+    ready ``input_config["dataset"]``) and split it into one shard per rollout worker (plus the
+    local worker's empty shard, as in the reference)."""
+    if (config or {}).get("input") != "dataset":
+        return None, []
+    ic = dict(config.get("input_config") or {})
+    ds = ic.get("dataset")
+    if ds is None:
+        import ray_memory_management_amd.data as rd
+
+        fmt = ic.get("format")
+        paths = ic.get("paths") or ic.get("path")
+        if not fmt or not paths:
+            raise ValueError("input_config needs 'format' and 'path'/'paths' (or a 'dataset')")
+        readers = {"json": rd.read_json, "parquet": rd.read_parquet, "csv": rd.read_csv}
+        if fmt not in readers:
+            raise ValueError(f"unsupported input format {fmt!r}: use json / parquet / csv")
+        ds = readers[fmt](paths)
+    n = max(1, int(num_workers))
+    shards = ds.repartition(n).split(n, equal=True) if n > 1 else [ds]
+    return ds, ([None] + shards if num_workers > 0 else [ds])
+
+
+def get_offline_io_resource_bundles(config: dict):
+    """Resource bundles the dataset read tasks need (reference offline/resource.py)."""
+    if (config or {}).get("input") != "dataset":
+        return []
+    ic = dict(config.get("input_config") or {})
+    n = int(ic.get("parallelism", config.get("num_workers", 1) or 1))
+    cpus = float(ic.get("num_cpus_per_read_task", 0.5))
+    return [{"CPU": cpus} for _ in range(max(1, n))]
+
+
+class D4RLReader(InputReader):
+    """reference rllib/offline/d4rl_reader.py: needs the `d4rl` package (not installed)."""
+
+    def __init__(self, inputs: str, ioctx=None):
+        raise ImportError("D4RLReader needs the `d4rl` package, which is not installed in this environment")

@@ -89,6 +89,70 @@ class TorchPolicy(Policy):
     def set_weights(self, weights):
         self.model.load_state_dict({k: v.to(self.device) for k, v in weights.items()})
 
+    # ------------------------------------------------------------------ learning (policy templates)
+    # reference rllib/policy/torch_policy.py: loss → compute_gradients / apply_gradients /
+    # learn_on_batch. The built-in algorithms train in their own (fused) learners; these are the
+    # generic path used by policies built with build_policy_class and the execution-plan operators.
+    def loss(self, model, dist_class, train_batch: SampleBatch):
+        raise NotImplementedError(f"{type(self).__name__} defines no loss (build it with build_torch_policy)")
+
+    def optimizer(self) -> torch.optim.Optimizer:
+        opt = getattr(self, "_optimizer", None)
+        if opt is None:
+            opt = self._optimizer = torch.optim.Adam(self.model.parameters(), lr=float(self.config.get("lr", 5e-5)))
+        return opt
+
+    def stats_fn(self, train_batch: SampleBatch) -> Dict:
+        return {}
+
+    def extra_grad_info(self, train_batch: SampleBatch) -> Dict:
+        return {}
+
+    def _lazy_tensor_dict(self, batch) -> SampleBatch:
+        out = SampleBatch({})
+        for k, v in batch.items():
+            if isinstance(v, torch.Tensor):
+                out[k] = v.to(self.device)
+            else:
+                a = np.asarray(v)
+                out[k] = torch.as_tensor(a, device=self.device) if a.dtype != object else v
+        return out
+
+    def _loss_value(self, train) -> torch.Tensor:
+        out = self.loss(self.model, self.dist_class, train)
+        if isinstance(out, (list, tuple)):
+            out = sum(out)
+        return out
+
+    def compute_gradients(self, postprocessed_batch):
+        """(list of numpy gradients in parameter order, info)."""
+        train = self._lazy_tensor_dict(postprocessed_batch)
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        self.model.zero_grad(set_to_none=True)
+        loss = self._loss_value(train)
+        loss.backward()
+        gc = self.config.get("grad_clip")
+        info = {}
+        if gc:
+            info["grad_gnorm"] = float(torch.nn.utils.clip_grad_norm_(params, gc))
+        grads = [(p.grad.detach().cpu().numpy() if p.grad is not None else np.zeros(tuple(p.shape), np.float32))
+                 for p in params]
+        info.update(self.extra_grad_info(train))
+        info["learner_stats"] = {**self.stats_fn(train), "total_loss": float(loss.detach())}
+        return grads, info
+
+    def apply_gradients(self, gradients) -> None:
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        for p, g in zip(params, gradients):
+            p.grad = torch.as_tensor(np.asarray(g), dtype=p.dtype, device=p.device)
+        self.optimizer().step()
+
+    def learn_on_batch(self, samples) -> Dict:
+        grads, info = self.compute_gradients(samples)
+        self.apply_gradients(grads)
+        self.global_timestep += len(next(iter(samples.values()))) if len(samples) else 0
+        return info
+
 
 def compute_gae_for_trajectories(rewards, vf_preds, dones, last_values, gamma, lam):
     """Time-major [T, B] numpy arrays → (advantages, value_targets) via the GAE op (HIP kernel
@@ -96,3 +160,7 @@ def compute_gae_for_trajectories(rewards, vf_preds, dones, last_values, gamma, l
     t = lambda x: torch.as_tensor(np.asarray(x, dtype=np.float32))  # noqa: E731
     adv, ret = ops.gae(t(rewards), t(vf_preds), t(dones), t(last_values), gamma, lam)
     return adv.numpy(), ret.numpy()
+
+
+from ray_memory_management_amd.rllib.policy.policy_template import (  # noqa: E402,F401
+    build_policy_class, build_tf_policy, build_torch_policy)

@@ -193,5 +193,21 @@ class MultiAgentBatch:
     def agent_steps(self):
         return sum(b.count for b in self.policy_batches.values())
 
+    @staticmethod
+    def concat_samples(samples: List["MultiAgentBatch"]) -> "MultiAgentBatch":
+        """Concatenate per policy (reference MultiAgentBatch.concat_samples)."""
+        per: Dict[str, List[SampleBatch]] = {}
+        steps = 0
+        for s in samples:
+            if isinstance(s, SampleBatch):
+                s = MultiAgentBatch({DEFAULT_POLICY_ID: s}, s.count)
+            steps += s.count
+            for pid, b in s.policy_batches.items():
+                per.setdefault(pid, []).append(b)
+        return MultiAgentBatch({pid: concat_samples(bs) for pid, bs in per.items()}, steps)
+
+    def __len__(self):
+        return self.count
+
 
 DEFAULT_POLICY_ID = "default_policy"
