@@ -53,6 +53,12 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def _comm_overlap() -> bool:
+    """Multi-rank step with the dense-bucket all-reduce forked onto a comm stream beside the trunk
+    backward (opt-in: the fork / join costs more than it hides on MI355X)."""
+    return os.environ.get("RMM_COMM_OVERLAP") == "1"
+
+
 class _CatPPOLoss(torch.autograd.Function):
     """K5b: the categorical PPO loss head; forward = stats, backward = d/dlogits, d/dvalues."""
 
@@ -458,12 +464,15 @@ class PPOLearner:
         """One minibatch step without graphs: manual kernels (overlapped all-reduce) or autograd."""
         if self._manual_ok(full):
             self._manual_fwd_dense_bwd(full)
-            if self.world > 1:
+            if self.world > 1 and _comm_overlap():
                 work = self.comm.allreduce_async(self.flat_grad[self._manual:])   # dense+heads bucket
                 self._manual_trunk_bwd(full)                                        # overlaps the RCCL op
                 work2 = self.comm.allreduce_async(self.flat_grad[:self._manual])  # trunk bucket
                 work.wait()
                 work2.wait()
+            elif self.world > 1:
+                self._manual_trunk_bwd(full)
+                self.comm.allreduce(self.flat_grad)  # one collective, same stream: no fork / join
             elif self._split_adam_ok():
                 self._overlapped_tail(full)
                 return
@@ -543,9 +552,9 @@ class PPOLearner:
                 else:
                     self._fast_step(full, True)
             self._graph = g
-        elif manual:
-            # multi-rank: three graphs with the two bucket all-reduces between them, so the
-            # dense+heads all-reduce (issued after graph A) runs on RCCL's stream during graph B
+        elif manual and _comm_overlap():
+            # multi-rank, RMM_COMM_OVERLAP=1: three graphs with the two bucket all-reduces between
+            # them, the dense+heads all-reduce forked onto the comm stream during graph B
             ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
                 self._manual_fwd_dense_bwd(full)
@@ -554,6 +563,19 @@ class PPOLearner:
             with torch.cuda.graph(gc):
                 self._opt_launch()
             self._graphs_split = (ga, gb, gc)
+        elif manual:
+            # multi-rank default: forward + both backwards in one graph, ONE all-reduce of the whole
+            # flat bucket on the same stream, Adam graph. A fork onto a comm stream and the join
+            # back cost ~16 us inside a graph and ~35 us eagerly on MI355X
+            # (benchmarks/stream_fork_cost.py, profiles/stream_fork_r3.txt) — more than the 24 us
+            # trunk backward it would hide the dense-bucket all-reduce behind
+            ga, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self._manual_fwd_dense_bwd(full)
+                self._manual_trunk_bwd(full)
+            with torch.cuda.graph(gc):
+                self._opt_launch()
+            self._graphs_split = (ga, None, gc)
         else:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -563,7 +585,12 @@ class PPOLearner:
             dst.copy_(src)  # undo warm-up updates
 
     def _replay(self):
-        if self._graphs_split is not None:
+        if self._graphs_split is not None and self._graphs_split[1] is None:
+            ga, _, gc = self._graphs_split
+            ga.replay()
+            self.comm.allreduce(self.flat_grad)
+            gc.replay()
+        elif self._graphs_split is not None:
             ga, gb, gc = self._graphs_split
             ga.replay()
             work = self.comm.allreduce_async(self.flat_grad[self._manual:])
