@@ -179,10 +179,11 @@ class PPO(Algorithm):
         refs, steps = [], 0
         per_round = c.num_workers * c.rollout_fragment_length * c.num_envs_per_worker
         rounds = max(1, -(-c.train_batch_size // max(per_round, 1)))
+        dev = self._device_weights_ok()
         for r in range(rounds):
-            for w in remote:
+            for i, w in enumerate(remote):
                 if r == 0 and self._weights_ref is not None:
-                    w.set_weights.remote(self._weights_ref)
+                    w.set_weights.remote(self._dev_refs[i % n_l] if dev and self._dev_refs else self._weights_ref)
                 refs.append(w.sample.remote())
             steps += per_round
         if c.postprocess_on_learner:
@@ -193,7 +194,10 @@ class PPO(Algorithm):
             shards = split_for_learners(refs, n_l)
             stats = ray.get([l.update_batch.remote(concat_samples(ray.get(s)))
                              for l, s in zip(self.learner_group.learners, shards)])
-        self._weights_ref = self.learner_group.weights_ref()
+        if dev:  # GPU rollout workers read the learners' bf16 weights from HBM (hipIPC)
+            self._dev_refs = self.learner_group.device_weights_refs()
+        else:
+            self._weights_ref = self.learner_group.weights_ref()
         self._counters["num_env_steps_sampled"] += steps
         self._counters["num_env_steps_trained"] += steps
         self._counters["num_agent_steps_trained"] += steps
@@ -202,6 +206,19 @@ class PPO(Algorithm):
         st["num_learners"] = n_l
         st["learner_update_s_max"] = max(s.get("learner_update_s", 0.0) for s in stats)
         return st
+
+    _dev_refs = None
+
+    def _device_weights_ok(self) -> bool:
+        """Weights go learner → rollout workers through HBM when both sides are GPU processes:
+        learners with GPUs and rollout workers with a GPU slice (hybrid / GPU rollouts)."""
+        c = self.algo_config
+        if getattr(self, "_dev_w", None) is None:
+            import os
+
+            self._dev_w = bool(c.num_gpus_per_learner_worker and (c.num_gpus_per_worker or c.gpu_rollouts)
+                               and not os.environ.get("RMM_HOST_WEIGHTS"))
+        return self._dev_w
 
     def _extra_state(self):
         if self._multi_agent:
@@ -242,6 +259,8 @@ class PPO(Algorithm):
 
     def get_policy(self, policy_id: str = "default_policy"):
         if self.learner_group is not None and self._weights_ref is not None:
+            if self._dev_refs is not None:  # the host ref is only refreshed on demand on this path
+                self._weights_ref = self.learner_group.weights_ref()
             self.workers.local_worker().set_weights(ray.get(self._weights_ref))
         return super().get_policy(policy_id)
 

@@ -72,6 +72,16 @@ class GPURolloutWorker:
     def set_weights(self, weights, global_vars=None):
         import torch
 
+        if isinstance(weights, dict) and "__rmm_flat_bf16__" in weights:  # learner's HBM weights object
+            flat = weights["__rmm_flat_bf16__"]
+            if flat.device != self.device:
+                flat = flat.to(self.device)
+            with torch.no_grad():
+                sd = self.model.state_dict()
+                for name, off, shape, stride in weights["__rmm_layout__"]:
+                    if name in sd:
+                        sd[name].copy_(flat.as_strided(shape, stride, off))
+            return
         with torch.no_grad():
             sd = self.model.state_dict()
             for k, v in weights.items():
@@ -387,8 +397,16 @@ class HybridRolloutWorker(GPURolloutWorker):
         return frag
 
     def set_weights(self, weights, global_vars=None):
+        import time
+
         import torch
 
+        t0 = time.perf_counter()
         self.stream.synchronize()
         super().set_weights(weights, global_vars)
         torch.cuda.synchronize(self.device)
+        self._set_weights_time = getattr(self, "_set_weights_time", 0.0) + time.perf_counter() - t0
+
+    def timing(self):
+        """Accumulated seconds in sample() and set_weights() (phase breakdown probes)."""
+        return {"sample_s": self._sample_time, "set_weights_s": getattr(self, "_set_weights_time", 0.0)}

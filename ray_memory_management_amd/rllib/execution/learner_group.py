@@ -13,9 +13,10 @@ Data path per training iteration (see PPO.training_step):
 * rollout-worker actors return fragments → shared-memory object store (zero-copy pickle5 buffers);
 * ``LearnerActor.update(*fragment_refs)`` receives its shard (refs resolved from the store as
   zero-copy numpy views), DMAs it onto its GPU and runs GAE + standardisation there (K17), then the
-  fused SGD epochs with the dense-bucket all-reduce overlapping the trunk backward;
-* learner 0 publishes the new fp32 weights with one ``ray.put``-backed return value that every
-  rollout worker reads in place.
+  fused SGD epochs with one all-reduce of the whole gradient bucket per minibatch step;
+* each learner publishes its bf16 weights as ONE flat HBM object (``get_weights_device``) that the
+  GPU rollout workers of its bundle map zero-copy (hipIPC); CPU rollout workers read learner 0's
+  fp32 weights (``get_weights``) from the shared-memory store in place.
 """
 from __future__ import annotations
 
@@ -46,8 +47,9 @@ class LearnerActor:
             require_hip()  # the fused learner needs the HIP kernels: fail loudly if they are missing
             torch.cuda.set_device(0)
         if world > 1 and backend == "nccl" and self.device != "cpu" and not os.environ.get("RMM_TORCH_PG_COMM"):
-            # framework-owned RCCL communicator: its all-reduces are captured INSIDE the SGD-step
-            # graph (torch's ProcessGroupNCCL aborts on captured collectives on ROCm)
+            # framework-owned RCCL communicator (parallel/comm.py:RcclComm): collectives enqueued on
+            # the learner's own stream, capturable in graphs (torch's ProcessGroupNCCL watchdog
+            # aborts on captured collectives on ROCm)
             import torch.distributed as dist
 
             from ray_memory_management_amd.parallel.comm import RcclComm
@@ -100,6 +102,21 @@ class LearnerActor:
 
     def get_weights(self):
         return self.learner.get_weights(numpy=True)
+
+    def get_weights_device(self):
+        """The bf16 compute weights as ONE flat HBM tensor (+ per-parameter layout). Returned
+        through the HBM object store: a GPU rollout worker on the same device maps it zero-copy
+        (hipIPC) and copies each parameter device-to-device — no D2H / pickle / H2D round trip of
+        the fp32 masters per iteration."""
+        L = self.learner
+        if self.device == "cpu" or not getattr(L, "fast", False):
+            return self.get_weights()
+        names = {id(p): n for n, p in L.model.named_parameters()}
+        layout, off = [], 0
+        for p in L.params:
+            layout.append((names[id(p)], off, tuple(p.shape), tuple(p.stride())))
+            off += p.numel()
+        return {"__rmm_flat_bf16__": L.w_bf16.detach().clone(), "__rmm_layout__": layout}
 
     def set_weights(self, w):
         self.learner.set_weights(w)
@@ -175,6 +192,11 @@ class LearnerGroup:
 
     def get_weights(self):
         return ray.get(self.weights_ref())
+
+    def device_weights_refs(self) -> List:
+        """One device-weights object per learner (identical replicas): rollout worker i reads
+        learner i % n's, which sits on its own GPU (same placement-group bundle)."""
+        return [l.get_weights_device.remote() for l in self.learners]
 
     def set_weights(self, w):
         ray.get([l.set_weights.remote(w) for l in self.learners])

@@ -124,8 +124,52 @@ class ResultGrid:
         return f"ResultGrid<{len(self)} results>"
 
 
+class _LoadedTrial:
+    """A finished trial read back from its directory (params.json + result.json)."""
+
+    def __init__(self, logdir: str):
+        import json
+
+        self.logdir = logdir
+        self.trial_id = os.path.basename(logdir.rstrip("/")).rsplit("_", 1)[-1]
+        self.experiment_tag = os.path.basename(logdir.rstrip("/"))
+        with open(os.path.join(logdir, "params.json")) as f:
+            self.config = json.load(f)
+        self.results = []
+        rp = os.path.join(logdir, "result.json")
+        if os.path.exists(rp):
+            with open(rp) as f:
+                self.results = [json.loads(line) for line in f if line.strip()]
+        self.last_result = dict(self.results[-1]) if self.results else {}
+        self.metric_analysis = {}
+        self.saved_checkpoints = sorted(
+            [(os.path.join(logdir, d), {}) for d in os.listdir(logdir)
+             if d.startswith("checkpoint_") and os.path.isdir(os.path.join(logdir, d))])
+        self.checkpoint = None
+        self.status = self.last_result.get("trial_status", "TERMINATED")
+        self.error = None
+
+
+def load_trials(experiment_dir: str) -> List[_LoadedTrial]:
+    """Every trial directory (one with a params.json) under an experiment directory."""
+    out = []
+    for d in sorted(os.listdir(experiment_dir)):
+        full = os.path.join(experiment_dir, d)
+        if os.path.isdir(full) and os.path.exists(os.path.join(full, "params.json")):
+            out.append(_LoadedTrial(full))
+    return out
+
+
 class ExperimentAnalysis:
+    """Analysis of a Tune experiment: from the trials of a run, or (reference
+    tune/analysis/experiment_analysis.py) from an experiment directory on disk."""
+
     def __init__(self, trials, default_metric=None, default_mode=None, experiment_dir=None):
+        if isinstance(trials, (str, os.PathLike)):
+            experiment_dir = os.fspath(trials)
+            if os.path.isfile(experiment_dir):  # an experiment_state file: its directory
+                experiment_dir = os.path.dirname(experiment_dir)
+            trials = load_trials(experiment_dir)
         self.trials = list(trials)
         self.default_metric, self.default_mode = default_metric, default_mode
         self._experiment_dir = experiment_dir

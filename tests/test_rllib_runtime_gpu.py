@@ -272,6 +272,15 @@ def test_ppo_hybrid_rollouts(cuda):
             r = algo.train()
         st = r["info"]["learner"]["default_policy"]["learner_stats"]
         assert np.isfinite(st["total_loss"]) and st["num_sgd_steps"] == 8
+        # weights travel learner -> workers as ONE flat bf16 HBM object (hipIPC), not host numpy
+        assert algo._device_weights_ok() and algo._dev_refs is not None
+        w0 = algo.workers.remote_workers()[0]
+        ray.get(w0.set_weights.remote(algo.learner_group.device_weights_refs()[0]))
+        got = ray.get(w0.get_weights.remote())
+        master = algo.learner_group.get_weights()
+        for k, v in master.items():
+            want = torch.from_numpy(np.ascontiguousarray(v)).to(torch.bfloat16).float().numpy()
+            np.testing.assert_array_equal(got[k], want)
         algo.stop()
     finally:
         ray.shutdown()

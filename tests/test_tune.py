@@ -385,3 +385,27 @@ def test_experiment_objects_factories_and_session_helpers(ray_start):
 
     with pytest.raises(ValueError):
         tune.create_searcher("hyperopt")
+
+
+def test_experiment_analysis_from_disk_and_cli(ray_start, tmp_path):
+    from ray_memory_management_amd import tune
+    from ray_memory_management_amd.tune.analysis import ExperimentAnalysis
+    from ray_memory_management_amd.tune.cli import list_experiments, list_trials
+
+    def f(config):
+        for i in range(3):
+            tune.report(score=config["x"] * i)
+
+    tune.run(f, config={"x": tune.grid_search([1, 2, 3])}, local_dir=str(tmp_path), name="exp", metric="score",
+             mode="max")
+    a = ExperimentAnalysis(str(tmp_path / "exp"), default_metric="score", default_mode="max")
+    assert len(a.trials) == 3 and a.best_config == {"x": 3} and a.best_result["score"] == 6
+    assert len(a.trial_dataframes) == 3
+    table = list_trials(str(tmp_path / "exp"), sort=["config/x"], desc=True, limit=2)
+    assert table.index("3") < table.index("2") and "1 " not in table.split("\n")[-2]
+    out = tmp_path / "t.csv"
+    list_trials(str(tmp_path / "exp"), output=str(out), filter_op="config/x >= 2")
+    import pandas as pd
+
+    assert sorted(pd.read_csv(out)["config/x"].tolist()) == [2, 3]
+    assert "exp" in list_experiments(str(tmp_path))
