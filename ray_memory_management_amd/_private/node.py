@@ -1495,6 +1495,16 @@ class Head:
                     "infeasible": len(self.sched.infeasible_tasks())}
         if what == "memory":
             return self.memory_monitor.snapshot() if self.memory_monitor else {}
+        if what == "session_dir":
+            return self.session_dir
+        if what == "runtime_envs":
+            envs = {}
+            for rec in list(self.actors.values()) + list(self.tasks.values()) + list(self.finished_tasks.values()):
+                re_ = (rec.spec or {}).get("runtime_env") if hasattr(rec, "spec") else None
+                if re_:
+                    key = json.dumps(re_, sort_keys=True, default=str)
+                    envs.setdefault(key, {"runtime_env": re_, "ref_cnt": 0})["ref_cnt"] += 1
+            return list(envs.values())
         if what == "memory_pressure":
             return {**dict(self.mem_stats), "pinned_arg_bytes": self.pinned_arg_bytes,
                     "pinned_arg_tasks": self.pinned_arg_tasks, "spills_in_flight": self.spills_in_flight,

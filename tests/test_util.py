@@ -316,3 +316,37 @@ def test_actor_group(ray_shared):
         g.nope
     g.shutdown()
     assert len(g) == 0
+
+
+def test_state_get_by_id_logs_and_runtime_envs(ray_start):
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd.util import state
+
+    @ray.remote
+    class A:
+        def hello(self):
+            print("hello-from-actor", flush=True)
+            return 1
+
+    a = A.options(runtime_env={"env_vars": {"X": "1"}}).remote()
+    assert ray.get(a.hello.remote()) == 1
+    aid = a._actor_id.hex()
+    assert state.get_actor(aid)["actor_id"] == aid
+    nodes = state.list_nodes()
+    assert state.get_node(nodes[0]["NodeID"]) is not None
+    w = [x for x in state.list_workers() if x["actor_id"] == aid][0]
+    assert state.get_worker(w["worker_id"])["pid"] == w["pid"]
+    logs = state.list_logs()
+    assert any(f.startswith("worker-") for fs in logs.values() for f in fs)
+    import time
+
+    deadline = time.time() + 10
+    found = False
+    while time.time() < deadline and not found:
+        found = any("hello-from-actor" in line for line in state.get_log(actor_id=aid))
+        time.sleep(0.1)
+    assert found
+    envs = state.list_runtime_envs()
+    assert any(e["runtime_env"].get("env_vars") == {"X": "1"} for e in envs)
+    with state.warnings_on_slow_request(address="", endpoint="x", timeout=10, explain=True):
+        pass
