@@ -593,6 +593,9 @@ class CoreWorker:
         spec["return_ids"] = ret_ids
         spec["job_id"] = self.job_id
         spec["parent_task_id"] = self.current_task_id
+        tr = sys.modules.get(_TRACING_MOD)
+        if tr is not None and tr._exporter is not None:
+            tr.inject(spec, spec.get("name", "task"), {"ray.task_id": task_id.hex()})
         if self.config.get("direct_task_submission", True):
             d = self.direct
             if d is None:
@@ -618,6 +621,10 @@ class CoreWorker:
         ret_ids = [_ids.object_id_for_return(task_id, i) for i in range(1, n + 1)]
         refs = [ObjectRef(o) for o in ret_ids]
         spec["return_ids"] = ret_ids
+        tr = sys.modules.get(_TRACING_MOD)
+        if tr is not None and tr._exporter is not None:
+            tr.inject(spec, spec.get("name", spec.get("method", "actor_task")),
+                      {"ray.task_id": task_id.hex(), "ray.actor_id": actor_id.hex()})
         conn = self.actor_conns.get(actor_id)
         if conn is None:
             conn = self.actor_conns.setdefault(actor_id, ActorConn(self, actor_id, max_task_retries))
@@ -747,6 +754,7 @@ def _default_store_size() -> int:
 
 
 _client = None  # util.client.ClientWorker when connected with ray.init("ray://host:port")
+_TRACING_MOD = "ray_memory_management_amd.util.tracing.tracing_helper"  # loaded only when a hook is set
 _system_config_used: dict = {}  # the _system_config this driver started its cluster with (ray._config)
 
 
@@ -785,6 +793,8 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             _local_mode = True
             return RayContext()
         cfg = dict(_system_config or {})
+        if kwargs.get("_tracing_startup_hook"):  # every worker of the job runs it too (RMM_CONFIG)
+            cfg["_tracing_startup_hook"] = kwargs["_tracing_startup_hook"]
         global _system_config_used
         _system_config_used = dict(cfg)
         if address is None:  # jobs started by the job manager / `rmm start` users connect this way
@@ -851,6 +861,11 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
                                                              "namespace": ns, "req_id": rid}))
         w.config = info.get("config", {})
         w.job_runtime_env = runtime_env
+        hook = kwargs.get("_tracing_startup_hook") or w.config.get("_tracing_startup_hook")
+        if hook:
+            from ray_memory_management_amd.util.tracing.tracing_helper import _setup_tracing
+
+            _setup_tracing(hook)
         global_worker = w
         _set_worker(w)
         atexit.register(shutdown)
@@ -909,6 +924,10 @@ def _find_session(address):
 
 def shutdown(_exiting_interpreter: bool = False):
     global global_worker, _head_proc, _local_mode, _client
+    tr = sys.modules.get(_TRACING_MOD)
+    if tr is not None:  # the hook was this job's: the next init() installs its own
+        tr.set_exporter(None)
+        tr._setup_tracing._done = None
     with _init_lock:
         if _client is not None:
             _client.close()

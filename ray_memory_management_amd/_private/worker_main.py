@@ -282,7 +282,13 @@ class Executor:
                 self.store_error(spec["return_ids"], e)
                 status = "err"
                 raise _Handled()
-            result = fn(*args, **kwargs)
+            if "_trace_ctx" in spec:
+                from ray_memory_management_amd.util.tracing.tracing_helper import execution_span
+
+                with execution_span(spec, spec.get("name", "task"), {"ray.task_id": spec["task_id"].hex()}):
+                    result = fn(*args, **kwargs)
+            else:
+                result = fn(*args, **kwargs)
             if inspect.isgenerator(result) and spec.get("num_returns") not in ("dynamic",):
                 result = list(result) if spec.get("num_returns", 1) != 1 else list(result)
             self.store_outputs(spec["return_ids"], spec.get("num_returns", 1), result, contained_map, holds)
@@ -419,7 +425,13 @@ class Executor:
             else:
                 args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
                 m = getattr(self.actor, name)
-                result = m(*args, **kwargs)
+                if "_trace_ctx" in spec:
+                    from ray_memory_management_amd.util.tracing.tracing_helper import execution_span
+
+                    with execution_span(spec, spec.get("name", name), {"ray.task_id": spec["task_id"].hex()}):
+                        result = m(*args, **kwargs)
+                else:
+                    result = m(*args, **kwargs)
                 if inspect.iscoroutine(result):
                     raise RuntimeError("coroutine returned from a non-async actor path")
             self.store_outputs(ret_ids, spec.get("num_returns", 1), result, contained_map, holds)
@@ -518,6 +530,14 @@ def main():
     w.main_thread_id = threading.main_thread().ident
     _w.global_worker = w
     _set_worker(w)
+    hook = w.config.get("_tracing_startup_hook")
+    if hook:  # the job's tracing setup (reference: _tracing_startup_hook run in every worker)
+        try:
+            from ray_memory_management_amd.util.tracing.tracing_helper import _setup_tracing
+
+            _setup_tracing(hook)
+        except Exception as e:  # noqa: BLE001
+            print(f"tracing startup hook {hook!r} failed: {e!r}", file=sys.stderr)
     ex = Executor(w)
     direct_addr = ex.start_direct_server()
     w.on_block = ex.bounce_direct
