@@ -685,6 +685,10 @@ class Head:
             env["HIP_VISIBLE_DEVICES"] = vis
             env["CUDA_VISIBLE_DEVICES"] = vis
             env["RMM_GPU_IDS"] = vis
+            # every GPU of the node, for collective groups that widen their visibility
+            # (_private/gpu_visibility.py: RCCL peers should see each other's devices)
+            n_gpu = int(float((self.nodes.get(node) or {}).get("resources", {}).get("GPU", 0)))
+            env["RMM_NODE_GPU_IDS"] = ",".join(str(g) for g in range(n_gpu))
         if runtime_env:
             for k, v in (runtime_env.get("env_vars") or {}).items():
                 env[str(k)] = str(v)

@@ -40,12 +40,17 @@ class LearnerActor:
         from ray_memory_management_amd.rllib.ppo_learner import PPOLearner
 
         self.rank, self.world = rank, world
-        self.device = "cuda:0" if use_gpu and torch.cuda.is_available() else "cpu"
+        idx = 0
+        if use_gpu and world > 1 and backend == "nccl":
+            from ray_memory_management_amd._private.gpu_visibility import share_node_devices
+
+            idx = share_node_devices()  # RCCL peers on this node see each other's GPUs
+        self.device = f"cuda:{idx}" if use_gpu and torch.cuda.is_available() else "cpu"
         if self.device != "cpu":
             from ray_memory_management_amd._native import require_hip
 
             require_hip()  # the fused learner needs the HIP kernels: fail loudly if they are missing
-            torch.cuda.set_device(0)
+            torch.cuda.set_device(idx)
         if world > 1 and backend == "nccl" and self.device != "cpu" and not os.environ.get("RMM_TORCH_PG_COMM"):
             # framework-owned RCCL communicator (parallel/comm.py:RcclComm): collectives enqueued on
             # the learner's own stream, capturable in graphs (torch's ProcessGroupNCCL watchdog
@@ -153,7 +158,8 @@ class LearnerActor:
                 "HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
                 "comm": type(self.learner.comm).__name__}
         if self.device != "cpu":
-            info["pci_bus_id"] = getattr(torch.cuda.get_device_properties(0), "pci_bus_id", None)
+            info["pci_bus_id"] = getattr(torch.cuda.get_device_properties(self.device), "pci_bus_id", None)
+            info["visible_devices"] = torch.cuda.device_count()
         return info
 
 

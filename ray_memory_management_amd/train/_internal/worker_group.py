@@ -44,6 +44,12 @@ class TrainWorker:
             try:
                 import inspect
 
+                dev = os.environ.get("RMM_TRAIN_DEVICE_INDEX")
+                if dev is not None:  # the CUDA current device is per thread: select this worker's GPU
+                    import torch
+
+                    torch.cuda.set_device(int(dev))
+
                 nparams = len(inspect.signature(train_fn).parameters)
                 out = train_fn(config) if nparams >= 1 else train_fn()
                 s.results.put(("done", out, None))

@@ -32,8 +32,15 @@ class TorchConfig:
 def _init_pg(rank, world, backend, path, timeout_s, device_index):
     import torch.distributed as dist
 
+    if backend == "nccl" and world > 1:
+        # every worker of the node sees the node's GPUs and selects its own (reference
+        # backend_executor._share_cuda_visible_devices): RCCL peers get direct xGMI peer access
+        from ray_memory_management_amd._private.gpu_visibility import share_node_devices
+
+        device_index = share_node_devices()
     if torch.cuda.is_available() and backend == "nccl":
         torch.cuda.set_device(device_index)
+        os.environ["RMM_TRAIN_DEVICE_INDEX"] = str(device_index)
     os.environ["RANK"] = str(rank)
     os.environ["WORLD_SIZE"] = str(world)
     os.environ["LOCAL_RANK"] = str(session.get_local_rank() if session._session else 0)

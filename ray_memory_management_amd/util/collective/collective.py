@@ -105,6 +105,9 @@ def init_collective_group(world_size: int, rank: int, backend=Backend.NCCL, grou
     store = dist.FileStore(path, world_size)
     if backend == Backend.NCCL and torch.cuda.is_available():
         torch.cuda.set_device(torch.cuda.current_device())
+        from ray_memory_management_amd.parallel.comm import rehearsal_host_id
+
+        rehearsal_host_id(group_name, rank)  # no-op unless RMM_RCCL_SAME_DEVICE=1 (1-GPU rehearsal)
     pg = _make_pg(backend, store, rank, world_size, timeout_s)
     with _lock:
         _groups[group_name] = _Group(group_name, world_size, rank, backend, pg, store)

@@ -71,17 +71,19 @@ def test_gloo_collectives_between_actors(ray_start, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("backend", ["nccl", "gloo"])
-def test_gpu_tensor_collectives(backend):
-    """GPU tensors between actors: RCCL needs one GPU per rank (skipped on a 1-GPU box);
-    gloo over GPU tensors runs two ranks on one GPU."""
+def test_gpu_tensor_collectives(backend, monkeypatch):
+    """GPU tensors between actors over RCCL and gloo. With one GPU, the two RCCL ranks share it:
+    RMM_RCCL_SAME_DEVICE=1 gives each rank its own RCCL host id (socket transport on loopback),
+    so the full RCCL group path (init, all ops of `_WorkerBase.run`) still executes."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ngpu = torch.cuda.device_count()
-    if backend == "nccl" and ngpu < 2:
-        pytest.skip("RCCL rejects two ranks on one GPU; needs >= 2 GPUs")
+    same = backend == "nccl" and ngpu < 2
+    if same:
+        monkeypatch.setenv("RMM_RCCL_SAME_DEVICE", "1")  # inherited by the actors
     ray.init(num_cpus=2, num_gpus=ngpu, object_store_memory=256 << 20)
     try:
-        G = ray.remote(num_gpus=1 if backend == "nccl" else 0.5, num_cpus=0)(_WorkerBase)
+        G = ray.remote(num_gpus=1 if backend == "nccl" and not same else 0.5, num_cpus=0)(_WorkerBase)
         ws = [G.remote("cuda") for _ in range(2)]
         col.create_collective_group(ws, 2, [0, 1], backend=backend, group_name="gpu")
         outs = ray.get([w.run.remote("gpu") for w in ws], timeout=180)

@@ -264,3 +264,31 @@ def test_large_arg_with_nested_cuda_tensor_does_not_leak(gpu_ray):
     while time.time() < deadline and n_objs() > base:
         time.sleep(0.1)
     assert n_objs() == base
+
+
+def test_share_node_devices_plan(monkeypatch):
+    """Visible-device sharing for collective groups (reference backend_executor
+    _share_cuda_visible_devices): own GPU 3 of an 8-GPU node -> sees 0..7, selects local index 3."""
+    from ray_memory_management_amd._private import gpu_visibility as gv
+
+    assert gv.plan("3", "0,1,2,3,4,5,6,7") == ("0,1,2,3,4,5,6,7", 3)
+    assert gv.plan("0", "0") is None            # single-GPU node: nothing to share
+    assert gv.plan("", "0,1") is None           # no GPU of its own
+    assert gv.plan("9", "0,1") is None          # inconsistent: stay isolated
+    monkeypatch.setenv("RMM_GPU_IDS", "5")
+    monkeypatch.setenv("RMM_NODE_GPU_IDS", "0,1,2,3,4,5,6,7")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    monkeypatch.delenv("RMM_SHARED_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setattr(gv, "_hip_initialized", lambda: False)
+    assert gv.share_node_devices() == 5
+    import os
+
+    assert os.environ["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7"
+    assert gv.current_own_index() == 5
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    monkeypatch.delenv("RMM_SHARED_VISIBLE_DEVICES")
+    monkeypatch.setattr(gv, "_hip_initialized", lambda: True)  # too late: stays isolated
+    assert gv.share_node_devices() == 0 and os.environ["HIP_VISIBLE_DEVICES"] == "5"
+    monkeypatch.setattr(gv, "_hip_initialized", lambda: False)
+    monkeypatch.setenv("RMM_SHARE_VISIBLE_DEVICES", "0")
+    assert gv.share_node_devices() == 0 and os.environ["HIP_VISIBLE_DEVICES"] == "5"
