@@ -659,6 +659,128 @@ __global__ __launch_bounds__(256) void k_dense_fwd(const unsigned short* __restr
 }
 
 
+// K13s — split-K form of K13 for the fused paths: the K10 → K13 → K15/K16 chain already has a
+// kernel boundary between the dense layer and its consumer, so the cross-workgroup reduction of a
+// split-K GEMM can happen in the CONSUMER's prologue (load_hidden4) instead of in-kernel (an
+// agent-scope release/acquire = L2 write-back across XCDs, 4x slower, round 2) or in an extra
+// reduce launch (+1 boundary, round 2). Output: fp32 partials part[S][M][N], no bias / ReLU.
+// Workgroup = WM x WN waves side by side, each owning FM x FN 16x16 fragments (register blocking:
+// FM + FN fragment loads feed FM*FN MFMAs — K13 issues 2 loads per MFMA, and at M = 500 the CU's
+// vector-load path, hits included, is what bounds it), the remaining KW = 4 / (WM WN) waves split
+// the slice's k-steps and combine through LDS; S contiguous K slices are separate workgroups.
+// Block order: slice slowest, then row tiles, then column tiles, XCD-aware (blocks id, id+8, ... on
+// one XCD get a contiguous run: same K slice, neighbouring tiles → shared x rows / W rows in its L2).
+template <int FM, int FN, int WM, int WN>
+__global__ __launch_bounds__(256) void k_dense_fwd_part(const unsigned short* __restrict__ x,
+                                                        const unsigned short* __restrict__ w, int64_t M, int64_t K,
+                                                        int N, int S, float* __restrict__ part) {
+  constexpr int KW = 4 / (WM * WN);
+  static_assert(WM * WN * KW == 4, "4 waves per workgroup");
+  __shared__ f32x4 red[KW > 1 ? KW - 1 : 1][KW > 1 ? FM * FN : 1][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int nt = N / (16 * FN * WN);
+  const int64_t mt = (M + 16 * FM * WM - 1) / (16 * FM * WM);
+  const int64_t tiles = mt * nt, total = gridDim.x;
+  int64_t id = blockIdx.x;
+  if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+  const int64_t sl = id / tiles, rem = id % tiles, tm = rem / nt, tn = rem % nt;
+  const int sub = wave / KW, kw = wave % KW;
+  const int64_t m0 = tm * 16 * FM * WM + (sub / WN) * 16 * FM, n0 = tn * 16 * FN * WN + (sub % WN) * 16 * FN;
+  const int64_t steps = K / 32, lo = steps * sl / S, hi = steps * (sl + 1) / S;
+  const unsigned short* xa[FM];
+  const unsigned short* wb[FN];
+#pragma unroll
+  for (int i = 0; i < FM; i++) xa[i] = x + min(m0 + 16 * i + r, M - 1) * K + 8 * g;
+#pragma unroll
+  for (int j = 0; j < FN; j++) wb[j] = w + (n0 + 16 * j + r) * K + 8 * g;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; i++)
+#pragma unroll
+    for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int64_t k = lo + kw;
+  for (; k + KW < hi; k += 2 * KW) {  // two of this wave's k-steps per batch: 2 (FM + FN) loads in flight
+    u16x8 av[2][FM], bv[2][FN];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+#pragma unroll
+      for (int i = 0; i < FM; i++) av[c][i] = *reinterpret_cast<const u16x8*>(xa[i] + (k + KW * c) * 32);
+#pragma unroll
+      for (int j = 0; j < FN; j++) bv[c][j] = *reinterpret_cast<const u16x8*>(wb[j] + (k + KW * c) * 32);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+      for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = mfma(as_bf(av[c][i]), as_bf(bv[c][j]), acc[i][j]);
+  }
+  if (k < hi) {
+    u16x8 av[FM], bv[FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++) av[i] = *reinterpret_cast<const u16x8*>(xa[i] + k * 32);
+#pragma unroll
+    for (int j = 0; j < FN; j++) bv[j] = *reinterpret_cast<const u16x8*>(wb[j] + k * 32);
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+      for (int j = 0; j < FN; j++) acc[i][j] = mfma(as_bf(av[i]), as_bf(bv[j]), acc[i][j]);
+  }
+  if constexpr (KW > 1) {
+    if (kw > 0) {
+#pragma unroll
+      for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) red[kw - 1][i * FN + j][lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (kw != 0) return;
+#pragma unroll
+    for (int q = 0; q < KW - 1; q++)
+#pragma unroll
+      for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] += red[q][i * FN + j][lane];
+  }
+  float* out = part + (sl * M) * N + n0 + r;
+#pragma unroll
+  for (int i = 0; i < FM; i++)
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t row = m0 + 16 * i + 4 * g + e;
+      if (row < M)
+#pragma unroll
+        for (int j = 0; j < FN; j++) out[row * N + 16 * j] = acc[i][j][e];
+    }
+}
+
+// Consumer prologue of K13s: a lane's 4 hidden values of row rr = bf16(ReLU(Σ_s part[s] + b)),
+// summed in slice order (deterministic), rounded exactly like K13's epilogue. Without partials
+// (hpart == nullptr) the bf16 hidden row is read as before.
+__device__ __forceinline__ void load_hidden4(const unsigned short* __restrict__ hid, const float* __restrict__ hpart,
+                                             int S, const unsigned short* __restrict__ hb, int64_t M, int64_t rr,
+                                             int lane, float hv[4], uint2& bits) {
+  if (hpart == nullptr) {
+    bits = *reinterpret_cast<const uint2*>(&hid[rr * H + 4 * lane]);
+  } else {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* p = hpart + rr * H + 4 * lane;
+    for (int s = 0; s < S; s++) {
+      const float4 v = *reinterpret_cast<const float4*>(p + int64_t(s) * M * H);
+      a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
+    }
+    const uint2 bb = *reinterpret_cast<const uint2*>(&hb[4 * lane]);
+    const unsigned short o0 = f2bf(fmaxf(a.x + __uint_as_float(bb.x << 16), 0.f));
+    const unsigned short o1 = f2bf(fmaxf(a.y + __uint_as_float(bb.x & 0xffff0000u), 0.f));
+    const unsigned short o2 = f2bf(fmaxf(a.z + __uint_as_float(bb.y << 16), 0.f));
+    const unsigned short o3 = f2bf(fmaxf(a.w + __uint_as_float(bb.y & 0xffff0000u), 0.f));
+    bits = make_uint2(uint32_t(o0) | (uint32_t(o1) << 16), uint32_t(o2) | (uint32_t(o3) << 16));
+  }
+  hv[0] = __uint_as_float(bits.x << 16), hv[1] = __uint_as_float(bits.x & 0xffff0000u);
+  hv[2] = __uint_as_float(bits.y << 16), hv[3] = __uint_as_float(bits.y & 0xffff0000u);
+}
+
+
 // K14 — the A1-wide head GEMM heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16 in/out, fp32 accumulate).
 // Too narrow for MFMA or hipBLASLt to pay (a 16x256 macro tile for 5 useful columns, ~5-6 µs): one
 // wave per row, each lane a 4-element slice of the row (8-B load) dotted against all A1 head rows
@@ -716,7 +838,10 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
                                                    unsigned short* __restrict__ dz,
                                                    unsigned short* __restrict__ dpre,
                                                    const int64_t* __restrict__ cidx,
-                                                   const int64_t* __restrict__ ctr, int64_t period) {
+                                                   const int64_t* __restrict__ ctr, int64_t period,
+                                                   const float* __restrict__ hpart, int S,
+                                                   const unsigned short* __restrict__ hb,
+                                                   unsigned short* __restrict__ hid_out) {
   constexpr int A = A1 - 1;
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
@@ -730,9 +855,10 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
   const int64_t rr = valid ? row : M - 1;
   const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
   const float gs = gout[0] / float(M);
-  const uint2 v = *reinterpret_cast<const uint2*>(&hid[rr * H + 4 * lane]);
-  const float hv[4] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
-                       __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+  float hv[4];
+  uint2 hbits;
+  load_hidden4(hid, hpart, S, hb, M, rr, lane, hv, hbits);
+  if (hid_out != nullptr && valid) *reinterpret_cast<uint2*>(&hid_out[row * H + 4 * lane]) = hbits;  // for K12
   float hd[A1];
 #pragma unroll
   for (int a = 0; a < A1; a++) {
@@ -836,11 +962,14 @@ __device__ __forceinline__ void heads_sample_row(const unsigned short* __restric
                                                  const float* bhs, const int64_t t, const uint32_t c, uint32_t seed,
                                                  int64_t* __restrict__ act, float* __restrict__ logp,
                                                  float* __restrict__ vf, float* __restrict__ lout,
-                                                 int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane) {
+                                                 int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane,
+                                                 const float* __restrict__ hpart, int S,
+                                                 const unsigned short* __restrict__ hb) {
   constexpr int A = A1 - 1;
-  const uint2 v = *reinterpret_cast<const uint2*>(&hid[b * H + 4 * lane]);
-  const float h0 = __uint_as_float(v.x << 16), h1 = __uint_as_float(v.x & 0xffff0000u);
-  const float h2 = __uint_as_float(v.y << 16), h3 = __uint_as_float(v.y & 0xffff0000u);
+  float hv[4];
+  uint2 hbits;
+  load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
+  const float h0 = hv[0], h1 = hv[1], h2 = hv[2], h3 = hv[3];
   float hd[A1];
 #pragma unroll
   for (int a = 0; a < A1; a++) {
@@ -903,7 +1032,9 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
                                                       int64_t* __restrict__ act, float* __restrict__ logp,
                                                       float* __restrict__ vf, float* __restrict__ lout,
                                                       int64_t* __restrict__ act_now, int64_t B,
-                                                      unsigned int* __restrict__ done) {
+                                                      unsigned int* __restrict__ done,
+                                                      const float* __restrict__ hpart, int S,
+                                                      const unsigned short* __restrict__ hb) {
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
   for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
@@ -912,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
   const int lane = threadIdx.x & 63;
   const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (b < B) heads_sample_row<A1>(hid, whs, bhs, *t_ptr, uint32_t(*ctr), seed, act, logp, vf, lout, act_now, B, b,
-                                  lane);  // wave-uniform
+                                  lane, hpart, S, hb);  // wave-uniform
   if (done) {
     __shared__ unsigned int last;
     __syncthreads();
@@ -953,7 +1084,9 @@ void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t
 
 void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
                      float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream,
-                     const int64_t* cidx, const int64_t* ctr, int64_t period) {
+                     const int64_t* cidx, const int64_t* ctr, int64_t period, const float* hpart, int S,
+                     const void* hb, void* hid_out) {
+  if (hpart != nullptr && (S < 1 || hb == nullptr)) throw std::invalid_argument("dense_heads_ppo: partials need S >= 1 and the dense bias");
   if (M <= 0) return;
   if (period < 1) period = 1;
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_ppo: 2 <= A <= 15 actions");
@@ -963,7 +1096,7 @@ void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const f
 #define RMM_K15(N)                                                                                        \
   case N:                                                                                                 \
     hipLaunchKernelGGL(dense::k_heads_ppo<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), cols, coef, \
-                       acc, gout, M, V(dz), V(dpre), cidx, ctr, period);                                  \
+                       acc, gout, M, V(dz), V(dpre), cidx, ctr, period, hpart, S, U(hb), V(hid_out));     \
     break;
   switch (A1) {
     RMM_K15(3) RMM_K15(4) RMM_K15(5) RMM_K15(6) RMM_K15(7) RMM_K15(8) RMM_K15(9)
@@ -975,15 +1108,16 @@ void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const f
 
 void dense_heads_sample(const void* hidden, const void* wh, const void* bh, const int64_t* t_ptr, const int64_t* ctr,
                         uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B,
-                        int A1, hipStream_t stream, unsigned int* done) {
+                        int A1, hipStream_t stream, unsigned int* done, const float* hpart, int S, const void* hb) {
   if (B <= 0) return;
+  if (hpart != nullptr && (S < 1 || hb == nullptr)) throw std::invalid_argument("dense_heads_sample: partials need S >= 1 and the dense bias");
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_sample: 2 <= A <= 15 actions");
   const dim3 grid(uint32_t((B + 3) / 4)), block(256);
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
 #define RMM_K16(N)                                                                                          \
   case N:                                                                                                   \
     hipLaunchKernelGGL(dense::k_heads_sample<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), t_ptr, ctr, \
-                       seed, act, logp, vf, lout, act_now, B, done);                                        \
+                       seed, act, logp, vf, lout, act_now, B, done, hpart, S, U(hb));                       \
     break;
   switch (A1) {
     RMM_K16(3) RMM_K16(4) RMM_K16(5) RMM_K16(6) RMM_K16(7) RMM_K16(8) RMM_K16(9)
@@ -1004,6 +1138,68 @@ void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int6
   hipLaunchKernelGGL(dense::k_dense_fwd, dim3(uint32_t(((M + 15) / 16) * (N / 16))), dim3(256), 0, stream,
                      static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(w),
                      static_cast<const unsigned short*>(b), M, K, N, static_cast<unsigned short*>(y), remap);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+// K13s configurations (FM, FN, WM, WN): 0 = 16x16 tile, 4 waves split K (small M);
+// 1 = 32x32 tile of 4 16x16 waves; 2 = 32x32 per wave, 4 waves split K; 3 = 64x32 per wave, 4 waves
+// split K; 4 = 64x64 tile of 4 32x32 waves; 5 = 64x64 per wave, 6 = 32x64 per wave (4 waves split K).
+struct PartCfg {
+  int fm, fn, wm, wn;
+};
+static constexpr PartCfg kPartCfgs[] = {{1, 1, 1, 1}, {1, 1, 2, 2}, {2, 2, 1, 1}, {4, 2, 1, 1},
+                                        {2, 2, 2, 2}, {4, 4, 1, 1}, {2, 4, 1, 1}};
+
+static void dense_part_cfg(int64_t M, int64_t K, int N, int* cfg, int* S) {
+  // default: by M; slices for ~512-1024 workgroups with >= 4 k-steps each, at most 16 (the
+  // consumer sums S partial rows per lane). RMM_K13S_CFG / RMM_K13S_S override (tuning).
+  static const int force_c = [] {
+    const char* e = std::getenv("RMM_K13S_CFG");
+    return e ? std::atoi(e) : -1;
+  }();
+  static const int force_s = [] {
+    const char* e = std::getenv("RMM_K13S_S");
+    return e ? std::atoi(e) : 0;
+  }();
+  int c = M <= 64 ? 0 : 6;
+  if (force_c >= 0 && force_c < 7) c = force_c;
+  const PartCfg& p = kPartCfgs[c];
+  const int64_t tiles = ((M + 16 * p.fm * p.wm - 1) / (16 * p.fm * p.wm)) * (N / (16 * p.fn * p.wn));
+  const int64_t steps = K / 32;
+  int64_t s = M <= 64 ? 8 : (256 + tiles - 1) / tiles;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, steps / 4));
+  s = std::max<int64_t>(1, std::min<int64_t>(s, 16));
+  if (force_s > 0) s = std::min<int64_t>(force_s, steps);
+  *cfg = c;
+  *S = int(s);
+}
+
+int dense_fwd_part_slices(int64_t M, int64_t K, int N) {
+  int c, S;
+  dense_part_cfg(M, K, N, &c, &S);
+  return S;
+}
+
+void dense_fwd_part(const void* x, const void* w, int64_t M, int64_t K, int N, float* part, int S,
+                    hipStream_t stream) {
+  if (M <= 0) return;
+  if (K % 32 != 0 || N % 64 != 0) throw std::invalid_argument("dense_fwd_part: K % 32 == 0 and N % 64 == 0");
+  int c, s_cfg;
+  dense_part_cfg(M, K, N, &c, &s_cfg);
+  if (S != s_cfg) throw std::invalid_argument("dense_fwd_part: S must be dense_fwd_part_slices(M, K, N)");
+  const PartCfg& p = kPartCfgs[c];
+  const int64_t tiles = ((M + 16 * p.fm * p.wm - 1) / (16 * p.fm * p.wm)) * (N / (16 * p.fn * p.wn));
+  const dim3 grid(uint32_t(tiles * S)), block(256);
+  auto U = [](const void* q) { return static_cast<const unsigned short*>(q); };
+  switch (c) {
+    case 0: hipLaunchKernelGGL((dense::k_dense_fwd_part<1, 1, 1, 1>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+    case 1: hipLaunchKernelGGL((dense::k_dense_fwd_part<1, 1, 2, 2>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+    case 2: hipLaunchKernelGGL((dense::k_dense_fwd_part<2, 2, 1, 1>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+    case 3: hipLaunchKernelGGL((dense::k_dense_fwd_part<4, 2, 1, 1>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+    case 4: hipLaunchKernelGGL((dense::k_dense_fwd_part<2, 2, 2, 2>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+    case 5: hipLaunchKernelGGL((dense::k_dense_fwd_part<4, 4, 1, 1>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+    default: hipLaunchKernelGGL((dense::k_dense_fwd_part<2, 4, 1, 1>), grid, block, 0, stream, U(x), U(w), M, K, N, S, part); break;
+  }
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -328,22 +328,32 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("dpre_ready") = false);
   m.def("dense_heads_sample", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t t_ptr, uint64_t ctr,
                                  uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
-                                 uint64_t act_now, int64_t B, int A1, uint64_t stream, uint64_t done) {
+                                 uint64_t act_now, int64_t B, int A1, uint64_t stream, uint64_t done, uint64_t hpart,
+                                 int nslices, uint64_t hb) {
     dense_heads_sample(P<const void>(hidden), P<const void>(wh), P<const void>(bh), P<const int64_t>(t_ptr),
                        P<const int64_t>(ctr), seed, P<int64_t>(act), P<float>(logp), P<float>(vf), P<float>(lout),
-                       P<int64_t>(act_now), B, A1, S(stream), P<unsigned int>(done));
+                       P<int64_t>(act_now), B, A1, S(stream), P<unsigned int>(done), P<const float>(hpart), nslices,
+                       P<const void>(hb));
   }, py::arg("hidden"), py::arg("wh"), py::arg("bh"), py::arg("t_ptr"), py::arg("ctr"), py::arg("seed"), py::arg("act"),
      py::arg("logp"), py::arg("vf"), py::arg("lout"), py::arg("act_now"), py::arg("B"), py::arg("A1"),
-     py::arg("stream"), py::arg("done") = 0);
+     py::arg("stream"), py::arg("done") = 0, py::arg("hpart") = 0, py::arg("S") = 0, py::arg("hb") = 0);
+  m.def("dense_fwd_part_slices", &dense_fwd_part_slices);
+  m.def("dense_fwd_part", [](uint64_t x, uint64_t w, int64_t M, int64_t K, int N, uint64_t part, int nslices,
+                             uint64_t stream) {
+    dense_fwd_part(P<const void>(x), P<const void>(w), M, K, N, P<float>(part), nslices, S(stream));
+  });
   m.def("dense_heads_ppo", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t cols, uint64_t coef, uint64_t acc,
                               uint64_t gout, int64_t M, int A1, uint64_t dz, uint64_t dpre, uint64_t stream,
-                              uint64_t cidx, uint64_t ctr, int64_t period) {
+                              uint64_t cidx, uint64_t ctr, int64_t period, uint64_t hpart, int nslices, uint64_t hb,
+                              uint64_t hid_out) {
     dense_heads_ppo(P<const void>(hidden), P<const void>(wh), P<const void>(bh), P<const float>(cols),
                     P<const float>(coef), P<float>(acc), P<const float>(gout), M, A1, P<void>(dz), P<void>(dpre),
-                    S(stream), P<const int64_t>(cidx), P<const int64_t>(ctr), period);
+                    S(stream), P<const int64_t>(cidx), P<const int64_t>(ctr), period, P<const float>(hpart), nslices,
+                    P<const void>(hb), P<void>(hid_out));
   }, py::arg("hidden"), py::arg("wh"), py::arg("bh"), py::arg("cols"), py::arg("coef"), py::arg("acc"),
      py::arg("gout"), py::arg("M"), py::arg("A1"), py::arg("dz"), py::arg("dpre"), py::arg("stream"),
-     py::arg("cidx") = 0, py::arg("ctr") = 0, py::arg("period") = 1);
+     py::arg("cidx") = 0, py::arg("ctr") = 0, py::arg("period") = 1, py::arg("hpart") = 0, py::arg("S") = 0,
+     py::arg("hb") = 0, py::arg("hid_out") = 0);
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,
                                uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,

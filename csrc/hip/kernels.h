@@ -123,13 +123,20 @@ void partition_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t
 
 // K13: y = ReLU(x Wᵀ + b), x [M,K], W [N,K] row-major bf16, K % 32 == 0, N % 16 == 0 (small-M GEMM).
 // K16: K14 + Gumbel-max sampling and rollout-row stores (as sample_store)
+// hpart/S/hb: read hidden as bf16(ReLU(Σ_s hpart[s] + hb)) from K13s partials instead of `hidden`
 void dense_heads_sample(const void* hidden, const void* wh, const void* bh, const int64_t* t_ptr, const int64_t* ctr,
                         uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B,
-                        int A1, hipStream_t stream, unsigned int* done = nullptr);
+                        int A1, hipStream_t stream, unsigned int* done = nullptr, const float* hpart = nullptr,
+                        int S = 0, const void* hb = nullptr);
 // K15: K14 + fused PPO loss stats + dheads + dpre (for dense_heads_bwd(dpre_ready=true))
 void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
                      float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream,
-                     const int64_t* cidx = nullptr, const int64_t* ctr = nullptr, int64_t period = 1);
+                     const int64_t* cidx = nullptr, const int64_t* ctr = nullptr, int64_t period = 1,
+                     const float* hpart = nullptr, int S = 0, const void* hb = nullptr, void* hid_out = nullptr);
+// K13s: split-K dense layer, fp32 partials part[S][M][N] (no bias / ReLU: K15 / K16 finish them)
+int dense_fwd_part_slices(int64_t M, int64_t K, int N);
+void dense_fwd_part(const void* x, const void* w, int64_t M, int64_t K, int N, float* part, int S,
+                    hipStream_t stream);
 // K14: heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16), one wave per row
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
                      hipStream_t stream);

@@ -435,7 +435,8 @@ class VisionNetwork(nn.Module):
 
     @torch.no_grad()
     def forward_sample(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now, done=None) -> bool:
-        """Rollout step: K10 trunk → K13 → K16 (head GEMM + Gumbel-max sampling + rollout-row stores,
+        """Rollout step: K10 trunk → K13s (split-K partials) → K16 (partial sum + bias + ReLU, head GEMM +
+        Gumbel-max sampling + rollout-row stores,
         same sampling stream as sample_store). Returns False (nothing launched) when not applicable.
         With `done` (a zeroed int32 device counter) K16 also advances *t_ptr and *ctr by one."""
         if not self.fused_trunk_ok(obs):
@@ -453,14 +454,21 @@ class VisionNetwork(nn.Module):
         h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias)
         hip = require_hip()
         stream = torch.cuda.current_stream(obs.device).cuda_stream
-        hidden = torch.empty((B, 256), dtype=h.dtype, device=h.device)
-        hip.dense_relu_fwd(h.data_ptr(), layer.weight.data_ptr(), layer.bias.data_ptr(), B, h.shape[1], 256,
-                           hidden.data_ptr(), stream)  # K13
-        hip.dense_heads_sample(hidden.data_ptr(), heads.weight.data_ptr(), heads.bias.data_ptr(), t_ptr.data_ptr(),
+        if os.environ.get("RMM_NO_K13S") is None:  # K13s: split-K partials, summed in K16's prologue
+            S = hip.dense_fwd_part_slices(B, h.shape[1], 256)
+            hpart = torch.empty(S * B * 256, dtype=torch.float32, device=h.device)
+            hip.dense_fwd_part(h.data_ptr(), layer.weight.data_ptr(), B, h.shape[1], 256, hpart.data_ptr(), S, stream)
+            hidden_ptr, part = 0, dict(hpart=hpart.data_ptr(), S=S, hb=layer.bias.data_ptr())
+        else:
+            hidden = torch.empty((B, 256), dtype=h.dtype, device=h.device)
+            hip.dense_relu_fwd(h.data_ptr(), layer.weight.data_ptr(), layer.bias.data_ptr(), B, h.shape[1], 256,
+                               hidden.data_ptr(), stream)  # K13
+            hidden_ptr, part = hidden.data_ptr(), {}
+        hip.dense_heads_sample(hidden_ptr, heads.weight.data_ptr(), heads.bias.data_ptr(), t_ptr.data_ptr(),
                                ctr.data_ptr(), seed, act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
                                act_now.data_ptr() if hasattr(act_now, "data_ptr") else int(act_now), B,
                                heads.out_features, stream,
-                               done.data_ptr() if done is not None else 0)  # K16 (act_now: maybe device-mapped host)
+                               done.data_ptr() if done is not None else 0, **part)  # K16 (act_now: maybe device-mapped host)
         return True
 
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,

@@ -49,6 +49,12 @@ _LOSS_KEYS = (SampleBatch.OBS, SampleBatch.ACTIONS, SampleBatch.ACTION_LOGP, Sam
               SampleBatch.ADVANTAGES, SampleBatch.VALUE_TARGETS)
 
 
+def _k13s() -> bool:
+    """K13s split-K dense layer with the reduction in its consumer (K15 / K16); RMM_NO_K13S=1 keeps
+    K13 (bf16 hidden written by the dense kernel itself), for A/B timing."""
+    return os.environ.get("RMM_NO_K13S") is None
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -309,6 +315,9 @@ class PPOLearner:
               "dz": torch.empty((mbs, A1), dtype=bf, device=dev), "dpre": torch.empty((mbs, 256), dtype=bf, device=dev),
               "dx": torch.empty((mbs, K), dtype=bf, device=dev),
               "part": torch.empty(require_hip().nature_trunk_partial_floats(mbs), dtype=torch.float32, device=dev)}
+        if _k13s():  # K13s: split-K dense layer, K15 sums its fp32 partials (and writes `hidden` for K12)
+            ws["S"] = require_hip().dense_fwd_part_slices(mbs, K, 256)
+            ws["hpart"] = torch.empty(ws["S"] * mbs * 256, dtype=torch.float32, device=dev)
         self._mws = ws
         return ws
 
@@ -324,12 +333,18 @@ class PPOLearner:
         h.nature_trunk_fwd(full["obs"].data_ptr(), idx.data_ptr(), ctr.data_ptr(), int(period), int(mbs),
                            c1.weight.data_ptr(), list(c1.weight.stride()), c1.bias.data_ptr(), c2.weight.data_ptr(),
                            list(c2.weight.stride()), c2.bias.data_ptr(), ws["h1"].data_ptr(), ws["h2"].data_ptr(), st)
-        h.dense_relu_fwd(ws["h2"].data_ptr(), dl.weight.data_ptr(), dl.bias.data_ptr(), mbs, K, 256,
-                         ws["hidden"].data_ptr(), st)
+        if "hpart" in ws:
+            h.dense_fwd_part(ws["h2"].data_ptr(), dl.weight.data_ptr(), mbs, K, 256, ws["hpart"].data_ptr(), ws["S"],
+                             st)
+            part = dict(hpart=ws["hpart"].data_ptr(), S=ws["S"], hb=dl.bias.data_ptr(), hid_out=ws["hidden"].data_ptr())
+        else:
+            h.dense_relu_fwd(ws["h2"].data_ptr(), dl.weight.data_ptr(), dl.bias.data_ptr(), mbs, K, 256,
+                             ws["hidden"].data_ptr(), st)
+            part = {}
         h.dense_heads_ppo(ws["hidden"].data_ptr(), hd.weight.data_ptr(), hd.bias.data_ptr(), full["cols"].data_ptr(),
                           self.coef.data_ptr(), self.acc.data_ptr(), self._one.data_ptr(), mbs, A1,
                           ws["dz"].data_ptr(), ws["dpre"].data_ptr(), st, cidx=idx.data_ptr(), ctr=ctr.data_ptr(),
-                          period=int(period))
+                          period=int(period), **part)
         g = [p._rmm_grad_out for p in self.params]
         h.dense_heads_bwd(ws["dz"].data_ptr(), A1, hd.weight.data_ptr(), ws["hidden"].data_ptr(), ws["h2"].data_ptr(),
                           dl.weight.data_ptr(), mbs, K, ws["dx"].data_ptr(), g[4].data_ptr(), g[5].data_ptr(),

@@ -440,3 +440,67 @@ def test_heads_sample_advances_step_counters(cuda):
         res.append((act, logp, vf, lout))
     for u, w in zip(*res):
         assert torch.equal(u, w)
+
+
+@pytest.mark.parametrize("M", [12, 25, 500])
+def test_dense_split_k_partials_feed_k15_k16(cuda, M):
+    """K13s (split-K dense layer → fp32 partials) with the reduction in the consumer: the hidden
+    K15 rebuilds (Σ partials + b, ReLU, bf16) matches the fp32 reference and K13's bf16 hidden to
+    rounding, and K15 / K16 fed from partials match K15 / K16 fed from K13's hidden."""
+    from ray_memory_management_amd._native import require_hip
+
+    h = require_hip()
+    torch.manual_seed(M)
+    K, N, A = 3872, 256, 4
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.02).to(torch.bfloat16)
+    b = (torch.randn(N, device=cuda) * 0.1).to(torch.bfloat16)
+    wh = (torch.randn(A + 1, N, device=cuda) * 0.1).to(torch.bfloat16)
+    bh = (torch.randn(A + 1, device=cuda) * 0.1).to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+    S = h.dense_fwd_part_slices(M, K, N)
+    assert 1 <= S <= 16
+    part = torch.full((S * M * N,), float("nan"), device=cuda)
+    h.dense_fwd_part(x.data_ptr(), w.data_ptr(), M, K, N, part.data_ptr(), S, s)
+    ref = torch.relu(x.float() @ w.float().t() + b.float())
+    pre = part.view(S, M, N).sum(0)
+    torch.testing.assert_close(pre + b.float(), x.float() @ w.float().t() + b.float(), rtol=1e-4, atol=1e-4)
+    hid = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    h.dense_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), M, K, N, hid.data_ptr(), s)
+    # K15 both ways
+    cols = torch.randn(M, A + 4, device=cuda)
+    cols[:, A + 3] = torch.randint(0, A, (M,), device=cuda).float()
+    coef = torch.tensor([0.2, 10.0, 1.0, 0.01, 0.2], device=cuda)
+    one = torch.ones(1, device=cuda)
+    res = []
+    for use_part in (False, True):
+        acc = torch.zeros(6, device=cuda)
+        dz = torch.empty(M, A + 1, dtype=torch.bfloat16, device=cuda)
+        dpre = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        hid_out = torch.zeros(M, N, dtype=torch.bfloat16, device=cuda)
+        kw = dict(hpart=part.data_ptr(), S=S, hb=b.data_ptr(), hid_out=hid_out.data_ptr()) if use_part else {}
+        h.dense_heads_ppo(0 if use_part else hid.data_ptr(), wh.data_ptr(), bh.data_ptr(), cols.data_ptr(),
+                          coef.data_ptr(), acc.data_ptr(), one.data_ptr(), M, A + 1, dz.data_ptr(), dpre.data_ptr(), s,
+                          **kw)
+        res.append((acc, dz, dpre, hid_out))
+    (a0, z0, p0, _), (a1, z1, p1, ho) = res
+    torch.testing.assert_close(ho.float(), ref, rtol=1e-2, atol=1e-2)
+    assert (ho.float() - hid.float()).abs().max() <= 2 ** -6 * max(1.0, float(hid.float().abs().max()))
+    torch.testing.assert_close(a1, a0, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(z1.float(), z0.float(), rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(p1.float(), p0.float(), rtol=2e-2, atol=2e-3)
+    # K16 both ways: actions agree (same hash stream; hidden differs at most by bf16 rounding)
+    t = torch.tensor([0], device=cuda)
+    ctr = torch.tensor([99], device=cuda)
+    acts = []
+    for use_part in (False, True):
+        act = torch.zeros(1, M, dtype=torch.int64, device=cuda)
+        logp, vf = torch.zeros(1, M, device=cuda), torch.zeros(1, M, device=cuda)
+        lout, now = torch.zeros(1, M, A, device=cuda), torch.zeros(M, dtype=torch.int64, device=cuda)
+        kw = dict(hpart=part.data_ptr(), S=S, hb=b.data_ptr()) if use_part else {}
+        h.dense_heads_sample(0 if use_part else hid.data_ptr(), wh.data_ptr(), bh.data_ptr(), t.data_ptr(),
+                             ctr.data_ptr(), 7, act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
+                             now.data_ptr(), M, A + 1, s, **kw)
+        acts.append((act, lout))
+    assert float((acts[0][0] == acts[1][0]).float().mean()) >= 0.95
+    torch.testing.assert_close(acts[1][1], acts[0][1], rtol=2e-2, atol=2e-2)
