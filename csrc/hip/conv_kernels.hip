@@ -137,6 +137,43 @@ __device__ __forceinline__ void frame_store(const FrameRegs<NT>& f, uint8_t* fra
     }
   }
 }
+// Rollout push mode (K19 folded into the trunk): the frame to run is the env's device stack
+// shifted by one with the newest frame appended. The thread that loads word o of planes 1..3 of
+// the stack and of the new frame also writes word o of the 4 shifted planes back (stack, in place:
+// no other thread touches word o of this env) and into rollout row t — so the rollout step needs
+// no separate frame-push launch. `nf` may be device-mapped pinned host memory (zero-copy upload).
+template <int NT>
+__device__ __forceinline__ void frame_issue_push(const uint8_t* stack, const uint8_t* __restrict__ nf,
+                                                 FrameRegs<NT>& f) {
+  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stack);
+  const uint32_t* n32 = reinterpret_cast<const uint32_t*>(nf);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
+#pragma unroll
+    for (int c = 0; c < C0 - 1; c++) f.v[k][c] = s32[(c + 1) * NW + o];
+    f.v[k][C0 - 1] = n32[o];
+  }
+}
+template <int NT>
+__device__ __forceinline__ void frame_push_store(const FrameRegs<NT>& f, uint8_t* stack, uint8_t* row) {
+  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
+  uint32_t* s32 = reinterpret_cast<uint32_t*>(stack);
+  uint32_t* r32 = reinterpret_cast<uint32_t*>(row);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + NT * k;
+    if (o < NW) {
+#pragma unroll
+      for (int c = 0; c < C0; c++) {
+        s32[c * NW + o] = f.v[k][c];
+        if (row) r32[c * NW + o] = f.v[k][c];
+      }
+    }
+  }
+}
+
 // zero rows 0, 1, 86, 87 and columns 0, 1, 86, 87 of the padded HWC frame (one u32 = one pixel)
 __device__ __forceinline__ void zero_frame_border(uint8_t* frame) {
   uint32_t* f32 = reinterpret_cast<uint32_t*>(frame);
@@ -266,7 +303,8 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, const unsigned short* __restrict__ W1, WStrides w1, const unsigned short* __restrict__ b1,
     const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ b2,
-    unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out, int dbg) {
+    unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out, int dbg, uint8_t* push_stack,
+    const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t) {
   __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short w1s[C1 * W1_PITCH];
@@ -280,12 +318,17 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
   // the frame's HBM loads go out first and stay in flight through the weight staging (L2) and the
   // LDS zeroing; one barrier then covers weights, zeros and the frame interior
   FrameRegs<NTF> fr;
-  frame_issue<NTF>(obs + src * (C0 * H0 * H0), fr);
+  constexpr int64_t FB = C0 * H0 * H0;
+  if (push_stack)
+    frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
+  else
+    frame_issue<NTF>(obs + src * FB, fr);
   zero_frame_border(frame);
   zero_lds(h1p, H1P_ELEMS * 2);
   stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
   stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   frame_store<NTF>(fr, frame);
+  if (push_stack) frame_push_store<NTF>(fr, push_stack + b * FB, push_rows ? push_rows + (push_t[0] * B + b) * FB : nullptr);
   __syncthreads();
 
   // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
@@ -689,7 +732,25 @@ void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
   hipLaunchKernelGGL(trunk::k_trunk_fwd, dim3(uint32_t(B)), dim3(trunk::NTF), 0, stream, obs, idx, ctr, period, B,
                      static_cast<const unsigned short*>(W1), ws(w1s), static_cast<const unsigned short*>(b1),
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(b2),
-                     static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2), dbg);
+                     static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2), dbg, nullptr, nullptr,
+                     nullptr, nullptr);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void nature_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
+                           const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
+                           const void* b2, void* h2, hipStream_t stream) {
+  if (B <= 0) return;
+  if (stack == nullptr || new_frames == nullptr) throw std::invalid_argument("nature_trunk_fwd_push: stack and new frames");
+  if (rows != nullptr && t_ptr == nullptr) throw std::invalid_argument("nature_trunk_fwd_push: rows need the row counter");
+  if ((reinterpret_cast<uintptr_t>(stack) | reinterpret_cast<uintptr_t>(new_frames) |
+       reinterpret_cast<uintptr_t>(rows)) & 3)
+    throw std::invalid_argument("nature_trunk_fwd_push: buffers must be 4-byte aligned");
+  hipLaunchKernelGGL(trunk::k_trunk_fwd, dim3(uint32_t(B)), dim3(trunk::NTF), 0, stream, nullptr, nullptr, nullptr,
+                     int64_t(1), B, static_cast<const unsigned short*>(W1), ws(w1s),
+                     static_cast<const unsigned short*>(b1), static_cast<const unsigned short*>(W2), ws(w2s),
+                     static_cast<const unsigned short*>(b2), nullptr, static_cast<unsigned short*>(h2), 0, stack,
+                     new_frames, rows, t_ptr);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

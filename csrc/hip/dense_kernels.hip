@@ -1061,6 +1061,35 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
     }
   }
 }
+
+// K16 for a small rollout batch with the step advance (B <= 32): ONE workgroup of 16 waves loops
+// the rows, then thread 0 bumps *t_ptr / *ctr after a workgroup barrier — no device-scope fence
+// and completion atomic (an L2 write-back across XCDs) as the multi-workgroup K16 needs.
+template <int A1>
+__global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __restrict__ hid,
+                                                        const unsigned short* __restrict__ wh,
+                                                        const unsigned short* __restrict__ bh, int64_t* t_ptr,
+                                                        int64_t* ctr, uint32_t seed, int64_t* __restrict__ act,
+                                                        float* __restrict__ logp, float* __restrict__ vf,
+                                                        float* __restrict__ lout, int64_t* __restrict__ act_now,
+                                                        int64_t B, const float* __restrict__ hpart, int S,
+                                                        const unsigned short* __restrict__ hb) {
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int64_t b = threadIdx.x >> 6; b < B; b += blockDim.x >> 6)  // wave-uniform
+    heads_sample_row<A1>(hid, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane, hpart, S, hb);
+  __syncthreads();  // every wave has read t / ctr
+  if (threadIdx.x == 0) {
+    *t_ptr = t + 1;
+    if (ctr != t_ptr) *ctr = int64_t(c) + 1;
+  }
+}
 }  // namespace dense
 
 void dense_heads_fwd(const void* hidden, const void* wh, const void* bh, int64_t M, int A1, void* heads,
@@ -1112,8 +1141,28 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
   if (B <= 0) return;
   if (hpart != nullptr && (S < 1 || hb == nullptr)) throw std::invalid_argument("dense_heads_sample: partials need S >= 1 and the dense bias");
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_sample: 2 <= A <= 15 actions");
-  const dim3 grid(uint32_t((B + 3) / 4)), block(256);
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
+  static const bool one_wg = [] {  // RMM_K16_MULTI=1: multi-workgroup K16 + completion counter (A/B)
+    const char* e = std::getenv("RMM_K16_MULTI");
+    return !(e && e[0] == '1');
+  }();
+  if (done != nullptr && B <= 32 && one_wg) {
+    auto* tw = const_cast<int64_t*>(t_ptr);
+    auto* cw = const_cast<int64_t*>(ctr);
+#define RMM_K16S(N)                                                                                            \
+  case N:                                                                                                      \
+    hipLaunchKernelGGL(dense::k_heads_sample1<N>, dim3(1), dim3(1024), 0, stream, U(hidden), U(wh), U(bh), tw, cw, \
+                       seed, act, logp, vf, lout, act_now, B, hpart, S, U(hb));                                \
+    break;
+    switch (A1) {
+      RMM_K16S(3) RMM_K16S(4) RMM_K16S(5) RMM_K16S(6) RMM_K16S(7) RMM_K16S(8) RMM_K16S(9)
+      RMM_K16S(10) RMM_K16S(11) RMM_K16S(12) RMM_K16S(13) RMM_K16S(14) RMM_K16S(15) RMM_K16S(16)
+    }
+#undef RMM_K16S
+    RMM_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const dim3 grid(uint32_t((B + 3) / 4)), block(256);
 #define RMM_K16(N)                                                                                          \
   case N:                                                                                                   \
     hipLaunchKernelGGL(dense::k_heads_sample<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), t_ptr, ctr, \

@@ -151,6 +151,12 @@ void dense_relu_fwd(const void* x, const void* w, const void* b, int64_t M, int6
 void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
                       const void* b2, void* h1, void* h2, hipStream_t stream, int dbg = 0);
+// K10 forward in rollout push mode (K19 folded in): frames = stack[b] shifted by one + new_frames[b]
+// (may be device-mapped pinned host memory); writes the shifted stack back and, with rows, rollout
+// row *t_ptr ([T, B, 4, 84, 84] u8). h2 as nature_trunk_fwd.
+void nature_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
+                           const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
+                           const void* b2, void* h2, hipStream_t stream);
 int nature_trunk_bwd_groups(int64_t B);
 int64_t nature_trunk_partial_floats(int64_t B);
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,

@@ -163,6 +163,8 @@ class _EnvGroup:
                 self.h_act_dev = int(require_hip().host_device_pointer(self.h_act.data_ptr()))
             except Exception:
                 self.h_act_dev = 0
+        # K19 folded into the K10 trunk launch (push mode); RMM_NO_FOLD_PUSH=1 keeps the separate kernel
+        self.fold_push = os.environ.get("RMM_NO_FOLD_PUSH") is None
         self.graph = None
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.ep_rew = np.zeros(n, dtype=np.float64)
@@ -174,13 +176,17 @@ class _EnvGroup:
         from ray_memory_management_amd._native import require_hip
 
         t, ctr = self.ctr_t[1:2], self.ctr_t[0:1]
+        push = None
         if self.device_stack:
             src = self.h_new_dev
             if not src:
                 self.s_new.copy_(self.h_new, non_blocking=True)
                 src = self.s_new.data_ptr()
-            require_hip().frame_push(self.s_obs.data_ptr(), src, self.buf_obs.data_ptr(),
-                                     t.data_ptr(), self.n, self.hw, torch.cuda.current_stream().cuda_stream)
+            if self.fused and self.fold_push and self.model.fused_trunk_ok(self.s_obs):
+                push = (src, self.buf_obs)  # K10 shifts the stack and stores row t itself
+            else:
+                require_hip().frame_push(self.s_obs.data_ptr(), src, self.buf_obs.data_ptr(),
+                                         t.data_ptr(), self.n, self.hw, torch.cuda.current_stream().cuda_stream)
         else:
             self.s_obs.copy_(self.h_obs, non_blocking=True)
             self.buf_obs.index_copy_(0, t, self.s_obs.unsqueeze(0))
@@ -188,7 +194,7 @@ class _EnvGroup:
         advanced = bool(self.fused and self.model.forward_sample(self.s_obs, t, ctr, self.seed, self.buf_act,
                                                                  self.buf_logp, self.buf_vf, self.buf_logits,
                                                                  self.h_act_dev if direct else self.act_now,
-                                                                 done=self.k16_done))
+                                                                 done=self.k16_done, push=push))
         if not advanced:
             direct = False
             hd = self.model.forward_heads(self.s_obs)

@@ -434,26 +434,42 @@ class VisionNetwork(nn.Module):
         return dense_heads(h, self.dense_tail, self.heads)
 
     @torch.no_grad()
-    def forward_sample(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now, done=None) -> bool:
+    def forward_sample(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now, done=None, push=None) -> bool:
         """Rollout step: K10 trunk → K13s (split-K partials) → K16 (partial sum + bias + ReLU, head GEMM +
         Gumbel-max sampling + rollout-row stores,
         same sampling stream as sample_store). Returns False (nothing launched) when not applicable.
-        With `done` (a zeroed int32 device counter) K16 also advances *t_ptr and *ctr by one."""
-        if not self.fused_trunk_ok(obs):
-            return False
-        B = obs.shape[0]
-        layer, heads = self.dense_tail, self.heads
-        if not (heads.out_features >= 3 and heads.out_features <= 16 and layer is not None
-                and layer.out_features == 256 and layer.in_features % 32 == 0 and layer.bias is not None
-                and heads.bias is not None and layer.weight.is_contiguous() and heads.weight.is_contiguous()
-                and not os.environ.get("RMM_NO_K16")):
-            return False
+        With `done` (a zeroed int32 device counter) K16 also advances *t_ptr and *ctr by one.
+        With `push` = (new-frame pointer [B,84,84] u8, rollout rows [T,B,4,84,84] u8 or None), `obs`
+        is the env's device frame stack: K10 shifts it by one, appends the new frames and stores row
+        *t_ptr itself (K19 folded into the trunk launch) — also when the fused step does not apply
+        (then only the push runs and False is returned)."""
         from ray_memory_management_amd._native import require_hip
 
+        B = obs.shape[0]
+        layer, heads = self.dense_tail, self.heads
+        if not (self.fused_trunk_ok(obs) and heads.out_features >= 3 and heads.out_features <= 16
+                and layer is not None and layer.out_features == 256 and layer.in_features % 32 == 0
+                and layer.bias is not None and heads.bias is not None and layer.weight.is_contiguous()
+                and heads.weight.is_contiguous() and not os.environ.get("RMM_NO_K16")):
+            if push is not None:
+                nf, rows = push
+                require_hip().frame_push(obs.data_ptr(), int(nf), rows.data_ptr() if rows is not None else 0,
+                                         t_ptr.data_ptr(), B, obs.shape[2] * obs.shape[3],
+                                         torch.cuda.current_stream(obs.device).cuda_stream)
+            return False
+
         c1, c2 = self.convs[0], self.convs[1]
-        h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias)
         hip = require_hip()
         stream = torch.cuda.current_stream(obs.device).cuda_stream
+        if push is not None:
+            nf, rows = push
+            h = torch.empty((B, 11 * 11 * 32), dtype=torch.bfloat16, device=obs.device)
+            hip.nature_trunk_fwd_push(obs.data_ptr(), int(nf), rows.data_ptr() if rows is not None else 0,
+                                      t_ptr.data_ptr(), B, c1.weight.data_ptr(), list(c1.weight.stride()),
+                                      c1.bias.data_ptr(), c2.weight.data_ptr(), list(c2.weight.stride()),
+                                      c2.bias.data_ptr(), h.data_ptr(), stream)
+        else:
+            h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias)
         if os.environ.get("RMM_NO_K13S") is None:  # K13s: split-K partials, summed in K16's prologue
             S = hip.dense_fwd_part_slices(B, h.shape[1], 256)
             hpart = torch.empty(S * B * 256, dtype=torch.float32, device=h.device)

@@ -1,5 +1,8 @@
 """GPU PPO learner: fused-kernel numerics vs PyTorch reference, HIP-graph path == eager path,
 sampler produces sane batches."""
+import json
+import os
+
 import pytest
 import torch
 
@@ -504,3 +507,73 @@ def test_dense_split_k_partials_feed_k15_k16(cuda, M):
         acts.append((act, lout))
     assert float((acts[0][0] == acts[1][0]).float().mean()) >= 0.95
     torch.testing.assert_close(acts[1][1], acts[0][1], rtol=2e-2, atol=2e-2)
+
+
+def test_trunk_push_mode_matches_frame_push_then_trunk(cuda):
+    """K10 push mode (K19 folded in): shifting the device frame stack, appending the new frames and
+    storing rollout row t inside the trunk launch gives the same stack, row and h2 as K19 followed
+    by the plain K10 forward."""
+    from ray_memory_management_amd._native import require_hip
+    from ray_memory_management_amd.rllib.models import nature_trunk
+
+    h = require_hip()
+    torch.manual_seed(3)
+    B, T = 13, 4
+    c1 = torch.nn.Conv2d(4, 16, 8, 4, padding=2).to(cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    c2 = torch.nn.Conv2d(16, 32, 4, 2, padding=2).to(cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    stack0 = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    nf = torch.randint(0, 256, (B, 84, 84), dtype=torch.uint8, device=cuda)
+    t = torch.tensor([2], device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    # reference: K19 then K10
+    st_a, rows_a = stack0.clone(), torch.zeros((T, B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    h.frame_push(st_a.data_ptr(), nf.data_ptr(), rows_a.data_ptr(), t.data_ptr(), B, 84 * 84, s)
+    h2_a = nature_trunk(st_a, c1.weight, c1.bias, c2.weight, c2.bias)
+    # push mode
+    st_b, rows_b = stack0.clone(), torch.zeros_like(rows_a)
+    h2_b = torch.empty_like(h2_a)
+    h.nature_trunk_fwd_push(st_b.data_ptr(), nf.data_ptr(), rows_b.data_ptr(), t.data_ptr(), B, c1.weight.data_ptr(),
+                            list(c1.weight.stride()), c1.bias.data_ptr(), c2.weight.data_ptr(),
+                            list(c2.weight.stride()), c2.bias.data_ptr(), h2_b.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(st_a, st_b) and torch.equal(rows_a, rows_b)
+    assert torch.equal(st_b[:, :3], stack0[:, 1:]) and torch.equal(st_b[:, 3], nf)
+    assert torch.equal(h2_a, h2_b)
+
+
+@pytest.mark.parametrize("B", [12, 25])
+def test_heads_sample_single_workgroup_advance(cuda, B):
+    """K16 with the step advance for small batches runs as ONE workgroup (no device-scope fence):
+    same rows as the multi-workgroup launch and the counters advance by exactly one."""
+    import subprocess
+    import sys
+
+    code = f"""
+import torch, json
+from ray_memory_management_amd._native import require_hip
+h = require_hip(); torch.manual_seed(1); B, A = {B}, 6
+wh = (torch.randn(A + 1, 256, device='cuda') * 0.3).to(torch.bfloat16)
+bh = torch.zeros(A + 1, device='cuda', dtype=torch.bfloat16)
+hid = torch.relu(torch.randn(B, 256, device='cuda')).to(torch.bfloat16)
+ct = torch.tensor([5, 1], device='cuda'); done = torch.zeros(1, dtype=torch.int32, device='cuda')
+act = torch.zeros(3, B, dtype=torch.int64, device='cuda'); logp = torch.zeros(3, B, device='cuda')
+vf = torch.zeros(3, B, device='cuda'); lout = torch.zeros(3, B, A, device='cuda'); now = torch.zeros(B, dtype=torch.int64, device='cuda')
+for _ in range(2):
+    h.dense_heads_sample(hid.data_ptr(), wh.data_ptr(), bh.data_ptr(), ct[1:].data_ptr(), ct[:1].data_ptr(), 7,
+                         act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(), now.data_ptr(), B, A + 1,
+                         torch.cuda.current_stream().cuda_stream, done.data_ptr())
+torch.cuda.synchronize()
+print(json.dumps({{"ct": ct.tolist(), "act": act.tolist(), "logp": logp.tolist(), "done": int(done)}}))
+"""
+    outs = []
+    for multi in ("0", "1"):
+        env = dict(os.environ, RMM_K16_MULTI=multi)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    a, b = outs
+    assert a["ct"] == [7, 3] and b["ct"] == [7, 3]  # two launches: rng counter 5 -> 7, row 1 -> 3
+    assert a["act"] == b["act"] and a["logp"] == b["logp"]
+    assert a["act"][0] == [0] * B and any(a["act"][1]) and any(a["act"][2])
+    assert a["done"] == 0 and b["done"] == 0
