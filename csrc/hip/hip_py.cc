@@ -256,6 +256,9 @@ PYBIND11_MODULE(_hip, m) {
     }
     return reinterpret_cast<uint64_t>(d);
   }, py::arg("host_ptr"));
+  m.def("step_gate", [](uint64_t host_release, uint64_t dev_seq, int64_t max_polls, uint64_t err, uint64_t stream) {
+    step_gate(P<const int64_t>(host_release), P<int64_t>(dev_seq), max_polls, P<int>(err), S(stream));
+  });
   m.def("frame_push", [](uint64_t stack, uint64_t new_frames, uint64_t buf_obs, uint64_t t_ptr, int64_t B, int64_t hw,
                          uint64_t stream) {
     frame_push(P<uint8_t>(stack), P<const uint8_t>(new_frames), buf_obs ? P<uint8_t>(buf_obs) : nullptr,

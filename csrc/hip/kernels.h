@@ -83,6 +83,8 @@ void sample_store(const void* logits, bool logits_bf16, const void* values, bool
 // K9: synthetic 84x84x4 Atari vector-env step fused with the rollout-buffer writes.
 // ctr_t = device int64[2] {rng counter, rollout row}.
 // K19: shift a device frame stack [B,4,hw] by one frame, append new_frames [B,hw], store row *t_ptr of buf_obs
+// rollout step gate: wait (bounded) until *host_release >= *dev_seq + 1, then *dev_seq += 1
+void step_gate(const int64_t* host_release, int64_t* dev_seq, int64_t max_polls, int* err, hipStream_t stream);
 void frame_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* buf_obs, const int64_t* t_ptr, int64_t B,
                 int64_t hw, hipStream_t stream);
 void synth_env_step(uint8_t* frames, const uint8_t* pool, const int64_t* actions, int32_t* tenv, const int64_t* ctr_t,

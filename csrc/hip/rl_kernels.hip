@@ -845,6 +845,34 @@ __global__ void __launch_bounds__(256) k_frame_push(uint8_t* __restrict__ stack,
   }
 }
 
+// Rollout step gate: lets the host enqueue step t+1 (a HIP-graph replay) BEFORE its CPU env step
+// has produced the frames, so the launch latency overlaps the env step. The first node of the step
+// waits until the host's release counter (device-mapped pinned memory, bumped by the CPU after
+// writing the frames) reaches this step's sequence number, then publishes it in *dev_seq. Bounded:
+// after `max_polls` polls (~s_sleep-paced) it gives up, flags *err and lets the step run, so a host
+// that dies mid-fragment can never leave a wave spinning.
+__global__ void __launch_bounds__(64) k_step_gate(const int64_t* host_release, int64_t* __restrict__ dev_seq,
+                                                  int64_t max_polls, int* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  const int64_t want = dev_seq[0] + 1;
+  int64_t n = 0;
+  while (__hip_atomic_load(host_release, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+    if (++n >= max_polls) {
+      err[0] = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  dev_seq[0] = want;
+}
+
+void step_gate(const int64_t* host_release, int64_t* dev_seq, int64_t max_polls, int* err, hipStream_t stream) {
+  if (host_release == nullptr || dev_seq == nullptr || err == nullptr) throw std::invalid_argument("step_gate: null pointer");
+  if (max_polls < 1) max_polls = 1;
+  hipLaunchKernelGGL(k_step_gate, dim3(1), dim3(64), 0, stream, host_release, dev_seq, max_polls, err);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 void frame_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* buf_obs, const int64_t* t_ptr, int64_t B,
                 int64_t hw, hipStream_t stream) {
   if (hw % 16 != 0) throw std::runtime_error("frame_push: frame bytes must be a multiple of 16");

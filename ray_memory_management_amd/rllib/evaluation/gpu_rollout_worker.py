@@ -165,6 +165,23 @@ class _EnvGroup:
                 self.h_act_dev = 0
         # K19 folded into the K10 trunk launch (push mode); RMM_NO_FOLD_PUSH=1 keeps the separate kernel
         self.fold_push = os.environ.get("RMM_NO_FOLD_PUSH") is None
+        # step gate (graphs only, opt-in RMM_ROLLOUT_GATE=1): step t+1 is enqueued before step t's CPU
+        # env step and held by a device-side gate until the host releases it, so the graph launch
+        # overlaps the env step. Measured SLOWER on MI355X (runtime PPO 17.4 -> 18.5 ms/iter,
+        # profiles/rollout_push_r3.txt): the gate node + host-memory polling cost more than the
+        # launch latency it hides.
+        self.gate = False
+        self.h_release = torch.zeros(1, dtype=torch.int64).pin_memory()
+        self._rel = self.h_release.numpy()
+        self.h_release_dev = 0
+        try:
+            from ray_memory_management_amd._native import require_hip
+
+            self.h_release_dev = int(require_hip().host_device_pointer(self.h_release.data_ptr()))
+        except Exception:
+            self.h_release_dev = 0
+        self.dev_seq = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.gate_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.ep_rew = np.zeros(n, dtype=np.float64)
@@ -176,6 +193,9 @@ class _EnvGroup:
         from ray_memory_management_amd._native import require_hip
 
         t, ctr = self.ctr_t[1:2], self.ctr_t[0:1]
+        if self.gate:
+            require_hip().step_gate(self.h_release_dev, self.dev_seq.data_ptr(), 200000, self.gate_err.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
         push = None
         if self.device_stack:
             src = self.h_new_dev
@@ -209,12 +229,28 @@ class _EnvGroup:
         if not (advanced and self.k16_done is not None):  # else K16 advanced the counters itself
             self.ctr_t.add_(1)
 
+    def release(self):
+        """Open the device-side gate of the next enqueued step (its frames are written)."""
+        self._rel[0] += 1
+
+    def resync(self, stream):
+        """Align the host release counter with the device gate sequence (fragment start: a gated
+        step abandoned by an exception has consumed a sequence number on its bounded timeout)."""
+        if self.gate:
+            stream.synchronize()
+            self._rel[0] = int(self.dev_seq.item())
+            if int(self.gate_err.item()):
+                self.gate_err.zero_()
+                raise RuntimeError("rollout step gate timed out (a policy step ran without its frames)")
+
     def capture(self, stream):
         import torch
 
+        self.gate = bool(self.h_release_dev) and os.environ.get("RMM_ROLLOUT_GATE", "0") != "0"
         with torch.cuda.stream(stream):
             saved = self.s_obs.clone() if self.device_stack else None
             for _ in range(2):
+                self.release()
                 self.policy_step()
             self.ctr_t[1].zero_()
             if saved is not None:  # warm-up pushes must not advance the frame stacks
@@ -300,7 +336,10 @@ class HybridRolloutWorker(GPURolloutWorker):
         base_seed = seed if seed is not None else self.config.get("seed")
         s = (int(base_seed or 0) * 1000 + worker_index) & 0x7FFFFFFF
         n = int(self.config.get("num_envs_per_worker", 1))
-        groups = 2 if n >= 2 and self.config.get("rollout_double_buffer", True) else 1
+        dbl = self.config.get("rollout_double_buffer", True)
+        if os.environ.get("RMM_ROLLOUT_DOUBLE_BUFFER") is not None:  # A/B override
+            dbl = os.environ["RMM_ROLLOUT_DOUBLE_BUFFER"] != "0"
+        groups = 2 if n >= 2 and dbl else 1
         sizes = [n // groups + (1 if g < n % groups else 0) for g in range(groups)]
         envs = [make_vector_env(self.config.get("env"), k, {**ec, "seed": s * 7 + g}) for g, k in enumerate(sizes)]
         if any(e is None for e in envs):
@@ -361,6 +400,7 @@ class HybridRolloutWorker(GPURolloutWorker):
             for g, gs in zip(G, S):
                 with torch.cuda.stream(gs):
                     g.ctr_t[1].zero_()
+                g.resync(gs)
             shared = all(gs is st for gs in S)
             with torch.cuda.stream(st):  # one stream switch per fragment (per launch with group streams)
                 try:
@@ -368,9 +408,27 @@ class HybridRolloutWorker(GPURolloutWorker):
                     for g, gs in zip(G, S):
                         torch.cuda.set_stream(gs)
                         evs.append(g.launch(gs, current=True))
+                        if g.gate:
+                            g.release()  # step 0's frames are already staged
+                    # RMM_ROLLOUT_SPIN=1: poll each step's event instead of a blocking wait (measured no gain)
+                    spin = os.environ.get("RMM_ROLLOUT_SPIN", "0") != "0"
                     for t in range(T):
                         for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
-                            evs[i].synchronize()
+                            if spin:  # poll the event: no blocking-wait wake-up latency on the step's critical path
+                                ev = evs[i]
+                                while not ev.query():
+                                    pass
+                            else:
+                                evs[i].synchronize()
+                            if g.gate:  # enqueue step t+1 first; it waits on the device for release()
+                                if t + 1 < T:
+                                    if not shared:
+                                        torch.cuda.set_stream(S[i])
+                                    evs[i] = g.launch(S[i], current=True)
+                                g.env_step(t, self._completed)
+                                if t + 1 < T:
+                                    g.release()
+                                continue
                             g.env_step(t, self._completed)
                             if t + 1 < T:
                                 if not shared:

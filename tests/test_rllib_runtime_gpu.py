@@ -284,3 +284,31 @@ def test_ppo_hybrid_rollouts(cuda):
         algo.stop()
     finally:
         ray.shutdown()
+
+
+@pytest.mark.parametrize("double_buffer", [False, True])
+def test_hybrid_step_gate_matches_ungated(cuda, double_buffer, monkeypatch):
+    """Step gate (opt-in; step t+1 enqueued before step t's env step, held on the device until the
+    host releases it) yields the same fragments, bit for bit, as launching after the env step; the gate
+    never times out, and the device / host sequence counters agree."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 20}, "num_envs_per_worker": 6,
+           "rollout_fragment_length": 12, "seed": 7, "rollout_double_buffer": double_buffer}
+    monkeypatch.setenv("RMM_ROLLOUT_GATE", "1")
+    a = HybridRolloutWorker(config=cfg)
+    fa = [a.sample() for _ in range(3)]
+    assert all(g.gate for g in a.groups)
+    monkeypatch.setenv("RMM_ROLLOUT_GATE", "0")
+    b = HybridRolloutWorker(config=cfg)
+    fb = [b.sample() for _ in range(3)]
+    assert not any(g.gate for g in b.groups)
+    for x, y in zip(fa, fb):
+        for k in ("obs", "_raw", "_boot"):
+            assert torch.equal(x[k], y[k]), k
+    torch.cuda.synchronize()
+    for g in a.groups:
+        assert int(g.gate_err.item()) == 0
+        assert int(g.dev_seq.item()) == int(g._rel[0]) == 2 + 3 * 12  # 2 warm-up steps + 3 fragments
