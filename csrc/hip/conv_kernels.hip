@@ -684,10 +684,27 @@ __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ 
                                                       unsigned short* __restrict__ dW1, WStrides w1,
                                                       unsigned short* __restrict__ db1,
                                                       unsigned short* __restrict__ dW2, WStrides w2,
-                                                      unsigned short* __restrict__ db2) {
+                                                      unsigned short* __restrict__ db2, const FusedAdam fa) {
   __shared__ float red[RED_SLICES][64];
   const int c = threadIdx.x & 63, slice = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + c;
+  const bool owner = slice == 0 && e < PART;  // the thread that finishes output e
+  unsigned short* dst = nullptr;
+  AdamState st{0.f, 0.f, 0.f};
+  if (owner) {
+    if (e < C1 * 256) {  // k = (ky, kx, ci)
+      const int co = e >> 8, k = e & 255, ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
+      dst = &dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3];
+    } else if (e < C1 * 256 + C2 * 256) {  // k = (ky, kx, ci)
+      const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+      dst = &dW2[co * w2.s0 + ci * w2.s1 + ky * w2.s2 + kx * w2.s3];
+    } else if (e < C1 * 256 + C2 * 256 + C1) {
+      dst = &db1[e - C1 * 256 - C2 * 256];
+    } else {
+      dst = &db2[e - C1 * 256 - C2 * 256 - C1];
+    }
+    st = adam_prefetch(fa, dst);  // fused Adam: state loads fly during the partial sums
+  }
   float s = 0.f;
   if (e < PART) {
     int gi = slice;
@@ -702,22 +719,16 @@ __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ 
   }
   red[slice][c] = s;
   __syncthreads();
-  if (slice != 0 || e >= PART) return;
-  float t = 0.f;
+  if (owner) {
+    float t = 0.f;
 #pragma unroll
-  for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
-  const unsigned short v = f2bf(t);
-  if (e < C1 * 256) {  // k = (ky, kx, ci)
-    const int co = e >> 8, k = e & 255, ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
-    dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3] = v;
-  } else if (e < C1 * 256 + C2 * 256) {  // k = (ky, kx, ci)
-    const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
-    dW2[co * w2.s0 + ci * w2.s1 + ky * w2.s2 + kx * w2.s3] = v;
-  } else if (e < C1 * 256 + C2 * 256 + C1) {
-    db1[e - C1 * 256 - C2 * 256] = v;
-  } else {
-    db2[e - C1 * 256 - C2 * 256 - C1] = v;
+    for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
+    // the trunk gradients are final here: store them, or (FusedAdam) apply Adam to them
+    const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
+    grad_store_pf(fa, ac, dst, t, st);
   }
+  // fused Adam: this launch is the last reader of the step counters in the SGD step
+  last_block_bump(fa.bump, fa.nbump, fa.done);
 }
 
 }  // namespace trunk
@@ -760,7 +771,7 @@ int64_t nature_trunk_partial_floats(int64_t B) { return int64_t(nature_trunk_bwd
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream, int dbg) {
+                      hipStream_t stream, int dbg, const FusedAdam& fa) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
   const int G = nature_trunk_bwd_groups(B);
@@ -771,7 +782,7 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
   hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3((trunk::PART + 63) / 64), dim3(64 * trunk::RED_SLICES), 0, stream,
                      partial, G,
                      static_cast<unsigned short*>(dW1), ws(w1s), static_cast<unsigned short*>(db1),
-                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2));
+                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2), fa);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -373,7 +373,7 @@ static_assert((K12_LDS_DM + K12_RB) * 2 <= 160 * 1024, "K12 LDS");
 __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
                                          const unsigned short* __restrict__ dpre, int64_t M, int64_t K, int64_t J0,
                                          unsigned short* __restrict__ dx, unsigned short* __restrict__ dw,
-                                         unsigned short* dm, unsigned short* rb) {
+                                         unsigned short* dm, unsigned short* rb, const FusedAdam& fa) {
   unsigned short* ws = rb;                    // [jt][h][16]  W[:, J] (setup only)
   unsigned short* xs = rb + K12_WS;           // [buf][jt][m][16]
   unsigned short* dxs = rb + K12_WS + K12_XS; // [m][DXP]
@@ -437,6 +437,15 @@ __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, c
   f32x4 adw[2][2];
 #pragma unroll
   for (int i = 0; i < 2; i++) adw[i][0] = adw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused Adam: this lane's 16 dW elements' master / moments, in flight during the chunk loop
+  auto dw_at = [&](int hi, int jt, int i) { return &dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + J0 + 16 * jt + r]; };
+  AdamState ast[2][2][4];
+#pragma unroll
+  for (int hi = 0; hi < 2; hi++)
+#pragma unroll
+    for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) ast[hi][jt][i] = adam_prefetch(fa, dw_at(hi, jt, i));
 
   for (int c = 0; c < NC; c++) {
     const unsigned short* d = dm + (c & 1) * MC2 * DMP;
@@ -480,13 +489,15 @@ __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, c
     const int row = v >> 2, pc = v & 3;
     *reinterpret_cast<uint4*>(&dx[int64_t(row) * K + J0 + 8 * pc]) = *reinterpret_cast<const uint4*>(&dxs[row * DXP + 8 * pc]);
   }
+  // dW[:, J] is final here (this workgroup reduced every row): store it, or apply Adam to it
+  const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
 #pragma unroll
   for (int hi = 0; hi < 2; hi++)
 #pragma unroll
     for (int jt = 0; jt < 2; jt++)
 #pragma unroll
       for (int i = 0; i < 4; i++)
-        dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + J0 + 16 * jt + r] = f2bf(adw[hi][jt][i]);
+        grad_store_pf(fa, ac, dw_at(hi, jt, i), adw[hi][jt][i], ast[hi][jt][i]);
 }
 
 // head role: dWh = dheadsᵀ hidden [A1, 256], db = Σ_m dpre, dbh = Σ_m dheads
@@ -494,7 +505,8 @@ template <int A1>
 __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, const unsigned short* __restrict__ y,
                                          const unsigned short* __restrict__ dpre, int64_t M,
                                          unsigned short* __restrict__ db, unsigned short* __restrict__ dwh,
-                                         unsigned short* __restrict__ dbh, unsigned short* dm, unsigned short* rb) {
+                                         unsigned short* __restrict__ dbh, unsigned short* dm, unsigned short* rb,
+                                         const FusedAdam& fa) {
   unsigned short* ys = rb;            // [buf][m][DMP]
   unsigned short* dzs = rb + K12_YS;  // [m][16] (a >= A1 and rows >= M zero)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
@@ -549,6 +561,17 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
   f32x4 awh[2], adb[2], abh = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 2; i++) awh[i] = adb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused Adam: prefetch this lane's dWh / db / dbh elements' state (clamped addresses; unused if out of range)
+  AdamState swh[2][4], sdb[2], sbh[4];
+#pragma unroll
+  for (int hi = 0; hi < 2; hi++) {
+    const int h = 16 * (wave + 8 * hi) + r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) swh[hi][i] = adam_prefetch(fa, &dwh[min(4 * g + i, A1 - 1) * H + h]);
+    sdb[hi] = adam_prefetch(fa, &db[h]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) sbh[i] = adam_prefetch(fa, &dbh[min(4 * g + i, A1 - 1)]);
 
   for (int c = 0; c < NC; c++) {
     const int o = (c & 1) * MC2 * DMP;
@@ -570,18 +593,19 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
     if (c + 2 < NC) load(c + 2);
     lds_barrier();
   }
+  const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
 #pragma unroll
   for (int hi = 0; hi < 2; hi++) {
     const int h = 16 * (wave + 8 * hi) + r;
 #pragma unroll
     for (int i = 0; i < 4; i++)
-      if (4 * g + i < A1) dwh[(4 * g + i) * H + h] = f2bf(awh[hi][i]);
-    if (g == 0) db[h] = f2bf(adb[hi][0]);
+      if (4 * g + i < A1) grad_store_pf(fa, ac, &dwh[(4 * g + i) * H + h], awh[hi][i], swh[hi][i]);
+    if (g == 0) grad_store_pf(fa, ac, &db[h], adb[hi][0], sdb[hi]);
   }
   if (wave == 0 && r == 0) {
 #pragma unroll
     for (int i = 0; i < 4; i++)
-      if (4 * g + i < A1) dbh[4 * g + i] = f2bf(abh[i]);
+      if (4 * g + i < A1) grad_store_pf(fa, ac, &dbh[4 * g + i], abh[i], sbh[i]);
   }
 }
 
@@ -590,13 +614,13 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd2(
     const unsigned short* __restrict__ dz, const unsigned short* __restrict__ y, const unsigned short* __restrict__ x,
     const unsigned short* __restrict__ w, const unsigned short* __restrict__ dpre, int64_t M, int64_t K,
     unsigned short* __restrict__ dx, unsigned short* __restrict__ dw, unsigned short* __restrict__ db,
-    unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh) {
+    unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh, const FusedAdam fa) {
   __shared__ __attribute__((aligned(16))) unsigned short dm[K12_LDS_DM];
   __shared__ __attribute__((aligned(16))) unsigned short rb[K12_RB];
   if (int64_t(blockIdx.x) * JB == K)
-    k12_head<A1>(dz, y, dpre, M, db, dwh, dbh, dm, rb);
+    k12_head<A1>(dz, y, dpre, M, db, dwh, dbh, dm, rb, fa);
   else
-    k12_cols(x, w, dpre, M, K, int64_t(blockIdx.x) * JB, dx, dw, dm, rb);
+    k12_cols(x, w, dpre, M, K, int64_t(blockIdx.x) * JB, dx, dw, dm, rb, fa);
 }
 
 // K13: hidden = ReLU(x Wᵀ + b) for small M (PPO minibatch / rollout batch). One 4-wave workgroup
@@ -1254,7 +1278,7 @@ void dense_fwd_part(const void* x, const void* w, int64_t M, int64_t K, int N, f
 
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
-                     hipStream_t stream, bool dpre_ready) {
+                     hipStream_t stream, bool dpre_ready, const FusedAdam& fa) {
   if (M <= 0) return;
   if (K % dense::JB != 0) throw std::invalid_argument("dense_heads_bwd: K must be a multiple of 32");
   if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_bwd: 1 <= A+1 <= 16");
@@ -1266,6 +1290,8 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
     const char* e = std::getenv("RMM_K12_V1");
     return !(e && e[0] == '1');
   }();
+  if (fa.grad_base && !v2) throw std::invalid_argument("dense_heads_bwd: fused Adam needs the K12 v2 kernel");
+  if (fa.grad_base && fa.bump) throw std::invalid_argument("dense_heads_bwd: the step counters advance in the trunk reduce");
   const dim3 pgrid(uint32_t((M + dense::MC - 1) / dense::MC));
   auto* dp = V(dpre_scratch);
 #define RMM_K12(N)                                                                                               \
@@ -1274,7 +1300,7 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
       hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);            \
     if (v2)                                                                                                      \
       hipLaunchKernelGGL(dense::k_dense_heads_bwd2<N>, grid2, block, 0, stream, U(dz), U(y), U(x), U(w), dp, M, \
-                         K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                                \
+                         K, V(dx), V(dw), V(db), V(dwh), V(dbh), fa);                                            \
     else                                                                                                         \
       hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w),   \
                          dp, M, K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                         \

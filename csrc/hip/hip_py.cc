@@ -23,6 +23,27 @@ inline T* P(uint64_t p) {
   return reinterpret_cast<T*>(p);
 }
 
+// [grad_base, master, m1, m2, wbf16, hp, step_ctr, bump, nbump, done] (empty: plain gradient stores)
+FusedAdam fused_adam(const std::vector<uint64_t>& v) {
+  FusedAdam fa;
+  if (v.empty()) return fa;
+  if (v.size() != 10) throw std::invalid_argument("fused adam: 10 fields");
+  for (int k : {0, 1, 2, 3, 4, 5, 6})
+    if (v[k] == 0) throw std::invalid_argument("fused adam: null buffer");
+  if (v[7] && (v[8] <= 0 || v[9] == 0)) throw std::invalid_argument("fused adam: bump needs nbump and done");
+  fa.grad_base = P<const void>(v[0]);
+  fa.master = P<float>(v[1]);
+  fa.m1 = P<float>(v[2]);
+  fa.m2 = P<float>(v[3]);
+  fa.wbf16 = P<void>(v[4]);
+  fa.hp = P<const float>(v[5]);
+  fa.step_ctr = P<const int64_t>(v[6]);
+  fa.bump = v[7] ? P<int64_t>(v[7]) : nullptr;
+  fa.nbump = int(v[8]);
+  fa.done = v[9] ? P<uint32_t>(v[9]) : nullptr;
+  return fa;
+}
+
 // ---- minimal DLPack ABI (stable C ABI, v0.x "dltensor" capsule)
 struct DLDevice {
   int32_t device_type;
@@ -330,13 +351,13 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("dense_heads_bwd", [](uint64_t dz, int A1, uint64_t wh, uint64_t y, uint64_t x, uint64_t w, int64_t M,
                               int64_t K, uint64_t dx, uint64_t dw, uint64_t db, uint64_t dwh, uint64_t dbh,
-                              uint64_t scratch, uint64_t stream, bool dpre_ready) {
+                              uint64_t scratch, uint64_t stream, bool dpre_ready, std::vector<uint64_t> adam) {
     dense_heads_bwd(P<const void>(dz), A1, P<const void>(wh), P<const void>(y), P<const void>(x), P<const void>(w), M,
                     K, P<void>(dx), P<void>(dw), P<void>(db), P<void>(dwh), P<void>(dbh), P<void>(scratch),
-                    S(stream), dpre_ready);
+                    S(stream), dpre_ready, fused_adam(adam));
   }, py::arg("dz"), py::arg("A1"), py::arg("wh"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("M"), py::arg("K"),
      py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("dwh"), py::arg("dbh"), py::arg("scratch"), py::arg("stream"),
-     py::arg("dpre_ready") = false);
+     py::arg("dpre_ready") = false, py::arg("adam") = std::vector<uint64_t>{});
   m.def("dense_heads_sample", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t t_ptr, uint64_t ctr,
                                  uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
                                  uint64_t act_now, int64_t B, int A1, uint64_t stream, uint64_t done, uint64_t hpart,
@@ -368,15 +389,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,
                                uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
-                               uint64_t stream, int dbg) {
+                               uint64_t stream, int dbg, std::vector<uint64_t> adam) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("nature_trunk_bwd: 4 strides per weight");
     nature_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr,
                      ctr ? P<const int64_t>(ctr) : nullptr, period, B, P<const void>(W2), w2s.data(),
                      P<const void>(h1), P<const void>(h2), P<const void>(dh2), P<float>(partial), P<void>(dW1),
-                     w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream), dbg);
+                     w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream), dbg, fused_adam(adam));
   }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W2"), py::arg("w2s"),
      py::arg("h1"), py::arg("h2"), py::arg("dh2"), py::arg("partial"), py::arg("dW1"), py::arg("w1s"), py::arg("db1"),
-     py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0);
+     py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0, py::arg("adam") = std::vector<uint64_t>{});
 
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {

@@ -6,6 +6,8 @@
 #include <string>
 #include <vector>
 
+#include "common.h"
+
 namespace rmm {
 namespace hip {
 
@@ -112,7 +114,8 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
 // K % 32 == 0, A1 <= 16, M <= 640 (a PPO minibatch; larger batches take the hipBLASLt path).
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
-                     hipStream_t stream, bool dpre_ready = false);  // dpre_scratch: M*256 bf16
+                     hipStream_t stream, bool dpre_ready = false,
+                     const FusedAdam& fa = FusedAdam{});  // dpre_scratch: M*256 bf16; fa: Adam epilogue
 
 // K11: shuffle partitioning. dest = splitmix64(key) % R (mode 0) or key mod R (mode 1), R <= 1024.
 // partition_hist writes counts[G][R] (G = partition_groups(n)); the caller turns them into
@@ -164,7 +167,7 @@ int64_t nature_trunk_partial_floats(int64_t B);
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream, int dbg = 0);
+                      hipStream_t stream, int dbg = 0, const FusedAdam& fa = FusedAdam{});
 // dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
 // load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores.
 

@@ -284,34 +284,6 @@ void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float*
   RMM_HIP_CHECK(hipGetLastError());
 }
 
-// Device step counters advanced by the LAST workgroup of the kernel that reads them, instead of a
-// separate 1-element add launch per step (~4 µs each in a HIP graph). Every workgroup reads the
-// counters at its start, so once all of them have drawn a ticket nobody reads them any more;
-// the kernel boundary publishes the new values to the next launch. Tickets are relaxed (nothing
-// is published between workgroups; an acq_rel agent-scope atomic costs an L2 writeback per
-// workgroup) and two-level: 16 sub-counters on separate 128-B lines, then one top counter, so
-// ~2000 workgroups do not serialise on a single address (one address cost ~2 µs/1000 WGs).
-// `done` = kBumpWords zero-initialised u32 owned by the call site; counters reset themselves.
-constexpr int kBumpSubs = 16, kBumpStride = 32, kBumpWords = (kBumpSubs + 1) * kBumpStride;
-__device__ __forceinline__ void last_block_bump(int64_t* bump, int nbump, uint32_t* done) {
-  if (!bump) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t G = gridDim.x, sub = blockIdx.x % kBumpSubs;
-    const uint32_t members = (G - sub + kBumpSubs - 1) / kBumpSubs;
-    uint32_t* sc = done + sub * kBumpStride;
-    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
-      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t* top = done + kBumpSubs * kBumpStride;
-      const uint32_t nsubs = G < uint32_t(kBumpSubs) ? G : uint32_t(kBumpSubs);
-      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsubs - 1) {
-        for (int k = 0; k < nbump; k++) bump[k] += 1;
-        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-}
-
 // ============================================================== K6 flat Adam (fp32 master -> bf16 weights)
 
 // hp layout (device): [lr, beta1, beta2, eps, weight_decay, step]; step is incremented by the caller
@@ -330,17 +302,6 @@ __device__ __forceinline__ uint32_t bf16x2_rn(float a, float b) {
   return lo | (hi << 16);
 }
 
-struct AdamCoef {
-  float lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt;
-};
-
-__device__ __forceinline__ float adam_one(float w, float g, float& a, float& b, const AdamCoef& c) {
-  if (c.wd != 0.f) w -= c.lr * c.wd * w;  // decoupled (AdamW) decay
-  a = c.b1 * a + (1.f - c.b1) * g;
-  b = c.b2 * b + (1.f - c.b2) * g * g;
-  return w - c.step_size * a / (sqrtf(b) * c.inv_bc2_sqrt + c.eps);
-}
-
 // Each thread updates 4 consecutive elements with 16-B fp32 and 8-B bf16 accesses (the step is
 // HBM-bound: 28 B/param); the n % 4 tail is done by the first threads of the grid. Requires the
 // host-checked alignment of every pointer (adam_flat falls back to vec=false otherwise).
@@ -354,12 +315,7 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
   // step: hp[5], or (device step counter + 1) when the counter is given (graph-friendly)
   // scale_ptr (optional): a device-side factor, e.g. the global-norm clip coefficient of K6b
   if (scale_ptr) grad_scale *= scale_ptr[0];
-  AdamCoef c;
-  c.lr = hp[0], c.b1 = hp[1], c.b2 = hp[2], c.eps = hp[3], c.wd = hp[4];
-  const float step = step_ctr ? float(step_ctr[0] + 1) : hp[5];
-  const float bc1 = 1.f - __powf(c.b1, step), bc2 = 1.f - __powf(c.b2, step);
-  c.step_size = c.lr / bc1;
-  c.inv_bc2_sqrt = 1.f / sqrtf(bc2);
+  const AdamCoef c = adam_coef(hp, step_ctr);
   const int64_t tid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, nthr = int64_t(gridDim.x) * blockDim.x;
   int64_t scalar_from = 0;
   if constexpr (VEC) {

@@ -75,6 +75,31 @@ def test_manual_step_matches_autograd_step(cuda, graphs):
     assert abs(s1["total_loss"] - s2["total_loss"]) < 1e-5 * max(1.0, abs(s1["total_loss"]))
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_adam_epilogues_match_k6(cuda, graphs, monkeypatch):
+    """Adam folded into the K12 / K10-trunk-reduce epilogues (world of one) vs the separate K6 launch:
+    same weights, moments and step counters after two updates (4 minibatches x 2 epochs each)."""
+    outs = []
+    for fused in (True, False):
+        if fused:
+            monkeypatch.setenv("RMM_FUSED_ADAM", "1")
+        else:
+            monkeypatch.delenv("RMM_FUSED_ADAM", raising=False)
+        L = _learner(cuda, use_graphs=graphs, lr=1e-3, weight_decay=0.01)
+        assert L._fused_adam() == fused
+        obs, cols = _tables(cuda)
+        torch.manual_seed(5)
+        st = L._update_tables(obs, cols, 4)
+        torch.manual_seed(6)
+        L._update_tables(obs, cols, 4)
+        outs.append((L.master.clone(), L.m1.clone(), L.m2.clone(), L.w_bf16.clone(), L.ctr.clone(), st))
+    a, b = outs
+    assert torch.equal(a[4], b[4])                               # step counters advanced identically
+    for x, y in zip(a[:4], b[:4]):  # bf16-rounded gradients, uncontracted Adam math: bit-identical
+        assert torch.equal(x, y), float((x.float() - y.float()).abs().max())
+    assert abs(a[5]["total_loss"] - b[5]["total_loss"]) < 1e-5 * max(1.0, abs(a[5]["total_loss"]))
+
+
 def test_grad_clip_coef_matches_torch(cuda):
     from ray_memory_management_amd._native import require_hip
 

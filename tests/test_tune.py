@@ -402,7 +402,10 @@ def test_experiment_analysis_from_disk_and_cli(ray_start, tmp_path):
     assert len(a.trials) == 3 and a.best_config == {"x": 3} and a.best_result["score"] == 6
     assert len(a.trial_dataframes) == 3
     table = list_trials(str(tmp_path / "exp"), sort=["config/x"], desc=True, limit=2)
-    assert table.index("3") < table.index("2") and "1 " not in table.split("\n")[-2]
+    rows = [[c.strip() for c in ln.strip("|").split("|")] for ln in table.split("\n")
+            if ln.startswith("|") and not ln.startswith("|-")]
+    col = rows[0].index("config/x")
+    assert [r[col] for r in rows[1:]] == ["3", "2"]  # sorted descending, limited to 2 rows
     out = tmp_path / "t.csv"
     list_trials(str(tmp_path / "exp"), output=str(out), filter_op="config/x >= 2")
     import pandas as pd
