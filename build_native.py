@@ -2,7 +2,8 @@
 
 * ``_store``  — shared-memory object store (C++17, g++)
 * ``_sched``  — scheduler core: resource sets, policies, dependency-gated queue (C++17, g++)
-* ``_hip``    — CDNA4 kernels + HBM GPU object store (HIP, hipcc --offload-arch=gfx950)
+* ``_envs``   — native env cores (synthetic Atari vector env) for CPU rollout workers (C++17, g++)
+* ``_hip``    — CDNA4 kernels + HBM GPU object store + native hybrid rollout loop (HIP, hipcc --offload-arch=gfx950)
 
 Usage: ``python build_native.py [--force] [--only NAME]``. Rebuilds an extension only when a
 source is newer than the built ``.so``. hipcc cross-compiles for gfx950 without a GPU.
@@ -57,6 +58,7 @@ def extensions():
              common + ["-march=x86-64-v2"], ["-lrt", "-lpthread"], ["csrc/store/shm_store.h"]),
         _ext("_sched", ["csrc/sched/scheduler.cc", "csrc/sched/sched_py.cc"], "g++",
              common, ["-lpthread"], ["csrc/sched/scheduler.h"]),
+        _ext("_envs", ["csrc/rl/envs_py.cc"], "g++", common, [], ["csrc/rl/synth_env.h"]),
     ]
     tl = _torch_lib()
     hip_ld = ["-lpthread"]
@@ -65,10 +67,11 @@ def extensions():
     if tl:
         hip_ld = [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"] + hip_ld
     exts.append(
-        _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/ingest_kernels.hip", "csrc/hip/vtrace_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/rccl_comm.cc", "csrc/hip/hip_py.cc",
+        _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/ingest_kernels.hip", "csrc/hip/vtrace_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/rccl_comm.cc", "csrc/hip/rollout_loop.cc", "csrc/hip/hip_py.cc",
               "csrc/store/shm_store.cc"], HIPCC,
              common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"],
-             hip_ld, ["csrc/hip/kernels.h", "csrc/hip/gpu_store.h", "csrc/hip/rccl_comm.h", "csrc/hip/common.h", "csrc/store/shm_store.h"]))
+             hip_ld, ["csrc/hip/kernels.h", "csrc/hip/gpu_store.h", "csrc/hip/rccl_comm.h", "csrc/hip/common.h", "csrc/store/shm_store.h",
+                     "csrc/hip/rollout_loop.h", "csrc/rl/synth_env.h"]))
     return exts
 
 

@@ -11,6 +11,7 @@
 #include "gpu_store.h"
 #include "kernels.h"
 #include "rccl_comm.h"
+#include "rollout_loop.h"
 
 namespace py = pybind11;
 using namespace rmm::hip;
@@ -277,6 +278,35 @@ PYBIND11_MODULE(_hip, m) {
     }
     return reinterpret_cast<uint64_t>(d);
   }, py::arg("host_ptr"));
+  // native hybrid rollout loop: groups = [(graph_exec, stream, pools, t, step, seed, n, A, episode_len, act,
+  // new_frames, rew, done, ep_rew, ep_len)], all raw addresses; returns finished (return, length) episodes
+  m.def("hybrid_rollout", [](const std::vector<std::vector<uint64_t>>& groups, int64_t T) {
+    std::vector<RolloutGroup> G;
+    for (const auto& v : groups) {
+      if (v.size() != 15) throw std::invalid_argument("hybrid_rollout: 15 fields per group");
+      RolloutGroup g;
+      g.exec = reinterpret_cast<hipGraphExec_t>(v[0]);
+      g.stream = S(v[1]);
+      g.env.pools = P<const uint8_t>(v[2]);
+      g.env.t = P<int64_t>(v[3]);
+      g.env.step = P<uint64_t>(v[4]);
+      g.env.seed = v[5];
+      g.env.n = int64_t(v[6]);
+      g.env.num_actions = int64_t(v[7]);
+      g.env.episode_len = int64_t(v[8]);
+      g.act = P<const int64_t>(v[9]);
+      g.new_frames = P<uint8_t>(v[10]);
+      g.rew = P<float>(v[11]);
+      g.done = P<float>(v[12]);
+      g.ep_rew = P<double>(v[13]);
+      g.ep_len = P<int64_t>(v[14]);
+      if (g.env.n <= 0 || g.env.num_actions <= 0 || g.env.episode_len <= 0)
+        throw std::invalid_argument("hybrid_rollout: bad env shape");
+      G.push_back(g);
+    }
+    py::gil_scoped_release nogil;
+    return hybrid_rollout(G, T);
+  }, py::arg("groups"), py::arg("T"));
   m.def("step_gate", [](uint64_t host_release, uint64_t dev_seq, int64_t max_polls, uint64_t err, uint64_t stream) {
     step_gate(P<const int64_t>(host_release), P<int64_t>(dev_seq), max_polls, P<int>(err), S(stream));
   });

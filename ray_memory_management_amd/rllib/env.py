@@ -245,14 +245,38 @@ class VectorEnv:
         return obs, rew, done, info
 
 
+def _mix64_np(seed: int, step: int, n: int) -> np.ndarray:
+    """numpy twin of csrc/rl/synth_env.h mix64(seed, step, env) for env = 0..n-1 (uint64 wrap-around)."""
+    with np.errstate(over="ignore"):
+        env = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) ^ (np.uint64(step) * np.uint64(0x9E3779B97F4A7C15)) ^ (env * np.uint64(0xD1B54A32D192ED03))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _native_envs():
+    try:
+        from ray_memory_management_amd import _envs
+
+        return _envs
+    except ImportError:
+        return None
+
+
 class CPUSyntheticAtariVectorEnv:
-    """numpy-vectorised synthetic Atari env for CPU rollout workers: `num_envs` envs stepped in
-    lock-step, frame stacks [n, 4, 84, 84] uint8 (channels-first, the layout the learner's fused
-    trunk reads, so ingest is a straight DMA). A step shifts in one pooled random frame per env,
-    column-rolled by an action-dependent amount (a cheap stand-in for game dynamics); rewards are
-    sparse Bernoulli(0.05); episodes truncate at `episode_len` (staggered starts). Same statistics
-    as SyntheticAtariEnv / GPUSyntheticAtariVectorEnv. Reference role: the vector env a RolloutWorker
-    steps (rllib/env/vector_env.py) with the Atari frame-stack wrapper (rllib/env/wrappers/atari_wrappers.py)."""
+    """Synthetic Atari vector env for CPU rollout workers: `num_envs` envs stepped in lock-step,
+    frame stacks [n, 4, 84, 84] uint8 (channels-first, the layout the learner's fused trunk reads,
+    so ingest is a straight DMA). A step shifts in one pooled random frame per env, column-rolled by
+    an action-dependent amount (a cheap stand-in for game dynamics); rewards are sparse
+    Bernoulli(0.05); episodes truncate at `episode_len` (staggered starts). Same statistics as
+    SyntheticAtariEnv / GPUSyntheticAtariVectorEnv. Reference role: the vector env a RolloutWorker
+    steps (rllib/env/vector_env.py) with the Atari frame-stack wrapper
+    (rllib/env/wrappers/atari_wrappers.py), whose emulator (ALE) is native code.
+
+    A step runs in C++ (``_envs``, csrc/rl/synth_env.h: one call for all envs, randomness from a
+    counter hash of (seed, step, env)); the numpy path below reproduces the same stream exactly.
+    Hybrid rollout workers drive the native core from their native rollout loop (``native_state``)."""
 
     is_native_vector_env = True
 
@@ -261,49 +285,70 @@ class CPUSyntheticAtariVectorEnv:
         self.num_envs = int(num_envs)
         self.num_actions = int(config.get("num_actions", 4))
         self.episode_len = int(config.get("episode_len", 1000))
-        self.rng = np.random.default_rng(config.get("seed"))
-        pool = self.rng.integers(0, 256, size=(64, 84, 84), dtype=np.uint8)
-        # one pre-rolled copy of the pool per action: a step is a single fancy-index gather
-        self._pools = np.stack([np.roll(pool, 3 * (a % 4) + 1, axis=2) for a in range(self.num_actions)])
-        self.frames = np.ascontiguousarray(pool[self.rng.integers(0, 64, size=(self.num_envs, 4))])
-        self.t = self.rng.integers(0, self.episode_len, size=self.num_envs)
+        rng = np.random.default_rng(config.get("seed"))
+        pool = rng.integers(0, 256, size=(64, 84, 84), dtype=np.uint8)
+        # one pre-rolled copy of the pool per action: a step is a single gather
+        self._pools = np.ascontiguousarray(np.stack([np.roll(pool, 3 * (a % 4) + 1, axis=2)
+                                                     for a in range(self.num_actions)]))
+        self.frames = np.ascontiguousarray(pool[rng.integers(0, 64, size=(self.num_envs, 4))])
+        self.t = np.ascontiguousarray(rng.integers(0, self.episode_len, size=self.num_envs), dtype=np.int64)
+        self.seed = int(rng.integers(0, 2 ** 63))
+        self._stepc = np.zeros(1, dtype=np.uint64)  # global step: position in the random stream
+        self._rew = np.zeros(self.num_envs, dtype=np.float32)
+        self._done = np.zeros(self.num_envs, dtype=np.float32)
+        self._native = _native_envs() if not config.get("numpy_env") else None
         self.observation_space = Box(0, 255, shape=(4, 84, 84), dtype=np.uint8)
         self.action_space = Discrete(self.num_actions)
+
+    def native_state(self):
+        """Raw addresses + shape of the env state for native callers (synth_env.h SynthAtariState):
+        (pools, t, step, seed, n, num_actions, episode_len)."""
+        return (self._pools.ctypes.data, self.t.ctypes.data, self._stepc.ctypes.data, self.seed, self.num_envs,
+                self.num_actions, self.episode_len)
 
     def vector_reset(self):
         return self.frames
 
-    def vector_step(self, actions):
+    def _step_numpy(self, actions, out: np.ndarray, stacks: bool):
         a = np.asarray(actions, dtype=np.int64) % self.num_actions
-        k = self.rng.integers(0, 64, size=self.num_envs)
-        self.frames[:, :3] = self.frames[:, 1:].copy()
-        self.frames[:, 3] = self._pools[a, k]
+        h = _mix64_np(self.seed, int(self._stepc[0]), self.num_envs)
+        self._stepc[0] += 1
+        src = self._pools.reshape(-1, 84, 84)[a * 64 + (h & np.uint64(63)).astype(np.int64)]
+        if stacks:
+            out[:, :3] = out[:, 1:].copy()
+            out[:, 3] = src
+        else:
+            out[:] = src
+        self._rew[:] = (((h >> np.uint64(32)) & np.uint64(0xFFFFFF)) < np.uint64(838861)).astype(np.float32)
         self.t += 1
-        rew = (self.rng.random(self.num_envs) < 0.05).astype(np.float32)
         done = self.t >= self.episode_len
         self.t[done] = 0
-        return self.frames, rew, done.astype(np.float32)
+        self._done[:] = done
+
+    def _step(self, actions, out: np.ndarray, stacks: bool):
+        if self._native is not None and out.flags.c_contiguous and out.dtype == np.uint8:
+            ns = getattr(self, "_ns", None)
+            if ns is None:  # addresses of the env's own buffers, looked up once
+                ns = self._ns = self.native_state()
+                self._rd = (self._rew.ctypes.data, self._done.ctypes.data)
+            self._native.synth_step_arrays(*ns, actions, out, stacks, *self._rd)
+        else:
+            self._step_numpy(actions, out, stacks)
+        return self._rew.copy(), self._done.copy()
+
+    def vector_step(self, actions):
+        rew, done = self._step(actions, self.frames, True)
+        return self.frames, rew, done
 
     # frames never reset at episode boundaries (truncation only): a consumer may keep the stacks
     frame_stack_continuous = True
 
     def vector_step_frames(self, actions, out: np.ndarray):
-        """Same transition and RNG stream as `vector_step`, but only the NEWEST frame of every env is
-        produced, written straight into `out` ([n, 84, 84] u8, e.g. pinned staging memory); the
+        """Same transition and random stream as `vector_step`, but only the NEWEST frame of every env
+        is produced, written straight into `out` ([n, 84, 84] u8, e.g. pinned staging memory); the
         consumer keeps the frame stacks (hybrid workers: in HBM, K19). `self.frames` is not
         maintained in this mode. Returns (rewards, dones)."""
-        a = np.asarray(actions, dtype=np.int64) % self.num_actions
-        k = self.rng.integers(0, 64, size=self.num_envs)
-        np.take(self._pools_flat, a * 64 + k, axis=0, out=out)
-        self.t += 1
-        rew = (self.rng.random(self.num_envs) < 0.05).astype(np.float32)
-        done = self.t >= self.episode_len
-        self.t[done] = 0
-        return rew, done.astype(np.float32)
-
-    @property
-    def _pools_flat(self):
-        return self._pools.reshape(-1, 84, 84)
+        return self._step(actions, out, False)
 
 
 class GPUSyntheticAtariVectorEnv:

@@ -402,40 +402,13 @@ class HybridRolloutWorker(GPURolloutWorker):
                     g.ctr_t[1].zero_()
                 g.resync(gs)
             shared = all(gs is st for gs in S)
-            with torch.cuda.stream(st):  # one stream switch per fragment (per launch with group streams)
-                try:
-                    evs = []
-                    for g, gs in zip(G, S):
-                        torch.cuda.set_stream(gs)
-                        evs.append(g.launch(gs, current=True))
-                        if g.gate:
-                            g.release()  # step 0's frames are already staged
-                    # RMM_ROLLOUT_SPIN=1: poll each step's event instead of a blocking wait (measured no gain)
-                    spin = os.environ.get("RMM_ROLLOUT_SPIN", "0") != "0"
-                    for t in range(T):
-                        for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
-                            if spin:  # poll the event: no blocking-wait wake-up latency on the step's critical path
-                                ev = evs[i]
-                                while not ev.query():
-                                    pass
-                            else:
-                                evs[i].synchronize()
-                            if g.gate:  # enqueue step t+1 first; it waits on the device for release()
-                                if t + 1 < T:
-                                    if not shared:
-                                        torch.cuda.set_stream(S[i])
-                                    evs[i] = g.launch(S[i], current=True)
-                                g.env_step(t, self._completed)
-                                if t + 1 < T:
-                                    g.release()
-                                continue
-                            g.env_step(t, self._completed)
-                            if t + 1 < T:
-                                if not shared:
-                                    torch.cuda.set_stream(S[i])
-                                evs[i] = g.launch(S[i], current=True)
-                finally:
-                    torch.cuda.set_stream(st)
+            native = self._native_loop(G, S)
+            if native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
+                from ray_memory_management_amd._native import require_hip
+
+                self._completed.extend(require_hip().hybrid_rollout(native, T))
+            else:
+                self._python_loop(G, S, T, st, shared)
             with torch.cuda.stream(st):
                 for gs in dict.fromkeys(S):
                     if gs is not st:
@@ -459,6 +432,69 @@ class HybridRolloutWorker(GPURolloutWorker):
             st.synchronize()
         self._sample_time += time.perf_counter() - t0
         return frag
+
+    def _native_loop(self, G, S):
+        """Per-group descriptors for the native rollout loop (csrc/hip/rollout_loop.cc), or None when
+        a group needs the Python loop: the env must be the native synthetic vector env, the policy
+        step a captured HIP graph reading the newest frames from mapped pinned memory and storing the
+        actions into it (K10 push mode + K16 direct store), no step gate. RMM_NO_NATIVE_ROLLOUT=1
+        forces the Python loop."""
+        if os.environ.get("RMM_NO_NATIVE_ROLLOUT") or os.environ.get("RMM_ROLLOUT_SPIN", "0") != "0":
+            return None
+        cached = getattr(self, "_native_desc", None)
+        if cached is not None:
+            return cached
+        desc = []
+        for g, gs in zip(G, S):
+            ok = (g.graph not in (None, False) and not g.gate and g.device_stack and g.h_new_dev and g.fused
+                  and g.h_act_dev and getattr(g.env, "_native", None) is not None
+                  and hasattr(g.env, "native_state") and hasattr(g.graph, "raw_cuda_graph_exec"))
+            if not ok:
+                return None
+            desc.append([int(g.graph.raw_cuda_graph_exec()), int(gs.cuda_stream), *map(int, g.env.native_state()),
+                         g.h_act.data_ptr(), g.h_new.data_ptr(), g.h_rew.data_ptr(), g.h_done.data_ptr(),
+                         g.ep_rew.ctypes.data, g.ep_len.ctypes.data])
+        self._native_desc = desc
+        return desc
+
+    def _python_loop(self, G, S, T, st, shared):
+        """The rollout loop in Python (any vector env; also the step-gate / event-polling variants)."""
+        import torch
+
+        with torch.cuda.stream(st):  # one stream switch per fragment (per launch with group streams)
+            try:
+                evs = []
+                for g, gs in zip(G, S):
+                    torch.cuda.set_stream(gs)
+                    evs.append(g.launch(gs, current=True))
+                    if g.gate:
+                        g.release()  # step 0's frames are already staged
+                # RMM_ROLLOUT_SPIN=1: poll each step's event instead of a blocking wait (measured no gain)
+                spin = os.environ.get("RMM_ROLLOUT_SPIN", "0") != "0"
+                for t in range(T):
+                    for i, g in enumerate(G):  # group i's env step overlaps the other group's inference
+                        if spin:  # poll the event: no blocking-wait wake-up latency on the step's critical path
+                            ev = evs[i]
+                            while not ev.query():
+                                pass
+                        else:
+                            evs[i].synchronize()
+                        if g.gate:  # enqueue step t+1 first; it waits on the device for release()
+                            if t + 1 < T:
+                                if not shared:
+                                    torch.cuda.set_stream(S[i])
+                                evs[i] = g.launch(S[i], current=True)
+                            g.env_step(t, self._completed)
+                            if t + 1 < T:
+                                g.release()
+                            continue
+                        g.env_step(t, self._completed)
+                        if t + 1 < T:
+                            if not shared:
+                                torch.cuda.set_stream(S[i])
+                            evs[i] = g.launch(S[i], current=True)
+            finally:
+                torch.cuda.set_stream(st)
 
     def set_weights(self, weights, global_vars=None):
         import time
