@@ -170,9 +170,10 @@ def _runtime(args, n_gpus):
     if args.rollout in ("cpu", "hybrid"):
         w_per, envs = _rollout_layout(n_gpus, budget, args.fragment)
         if args.rollout == "hybrid" and not args.workers_per_learner:
-            # GPU policy: 2 workers x 25 envs per learner GPU measured best on MI355X
-            # (profiles/bench_r2_hybrid_sweep.txt): bigger inference batches, fewer GPU contexts
-            w_per, envs = 2, TRAIN_BATCH // (args.fragment * 2)
+            # GPU policy: ONE worker x 50 envs per learner GPU measured best on MI355X with the native
+            # rollout loop (profiles/native_rollout_r3.txt: 15.4-15.9 ms/iter vs 16.9-17.0 for 2 x 25
+            # and 34-35 for 5 x 10): one policy step of all 50 envs per env step, one GPU context
+            w_per, envs = 1, TRAIN_BATCH // args.fragment
         if args.workers_per_learner:
             w_per = args.workers_per_learner
             envs = max(1, TRAIN_BATCH // (args.fragment * w_per))

@@ -336,12 +336,21 @@ class HybridRolloutWorker(GPURolloutWorker):
         base_seed = seed if seed is not None else self.config.get("seed")
         s = (int(base_seed or 0) * 1000 + worker_index) & 0x7FFFFFFF
         n = int(self.config.get("num_envs_per_worker", 1))
-        dbl = self.config.get("rollout_double_buffer", True)
+        # double-buffered env groups hide a SLOW env step behind the other group's policy step. With
+        # the native env core the env step is a few µs and the native loop runs, so one group (one
+        # policy step of all n envs per env step) is faster: runtime PPO 15.4-15.9 vs 17.5-19.7
+        # ms/iter on MI355X (profiles/native_rollout_r3.txt). "auto" (default) = split only envs
+        # without a native core.
+        dbl = self.config.get("rollout_double_buffer", "auto")
         if os.environ.get("RMM_ROLLOUT_DOUBLE_BUFFER") is not None:  # A/B override
             dbl = os.environ["RMM_ROLLOUT_DOUBLE_BUFFER"] != "0"
+        first = make_vector_env(self.config.get("env"), n, {**ec, "seed": s * 7})
+        if dbl == "auto":
+            dbl = getattr(first, "_native", None) is None or os.environ.get("RMM_NO_NATIVE_ROLLOUT") is not None
         groups = 2 if n >= 2 and dbl else 1
         sizes = [n // groups + (1 if g < n % groups else 0) for g in range(groups)]
-        envs = [make_vector_env(self.config.get("env"), k, {**ec, "seed": s * 7 + g}) for g, k in enumerate(sizes)]
+        envs = [first if groups == 1 else make_vector_env(self.config.get("env"), k, {**ec, "seed": s * 7 + g})
+                for g, k in enumerate(sizes)]
         if any(e is None for e in envs):
             raise ValueError("HybridRolloutWorker needs a native CPU vector env")
         self.env = envs[0]
