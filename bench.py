@@ -177,9 +177,13 @@ def _runtime(args, n_gpus):
         if args.workers_per_learner:
             w_per = args.workers_per_learner
             envs = max(1, TRAIN_BATCH // (args.fragment * w_per))
-        n_cpus = max(budget, n_gpus * (w_per + 1) + 1)
+        # hybrid: a worker splits each env step over its CPUs (native rollout loop), up to 4
+        cpw = 1 if args.rollout == "cpu" else max(1, min(4, ((budget - 1) // n_gpus - 1) // w_per))
+        if args.env_threads:
+            cpw = args.env_threads
+        n_cpus = max(budget, n_gpus * (w_per * cpw + 1) + 1)
     else:
-        w_per, envs = 1, TRAIN_BATCH // args.fragment
+        w_per, envs, cpw = 1, TRAIN_BATCH // args.fragment, 1
         n_cpus = max(budget, 2 * n_gpus + 1)
     phys = 1 if args.same_device else n_gpus
     # the runtime's processes (head, learner / rollout actors) do not inherit the launcher's torchrun
@@ -207,14 +211,15 @@ def _runtime(args, n_gpus):
                .training(train_batch_size=TRAIN_BATCH * n_gpus, sgd_minibatch_size=args.minibatch * n_gpus,
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
                          vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99)
-               .resources(num_learner_workers=n_gpus,
+               .resources(num_learner_workers=n_gpus, num_cpus_per_worker=cpw,
                           num_gpus_per_learner_worker=(0.5 if args.rollout != "cpu" else 1.0) * phys / n_gpus,
                           # hybrid: CPU env, policy on the worker's slice of the learner's GPU
                           num_gpus_per_worker={"gpu": 0.5, "hybrid": 0.5 / w_per}.get(args.rollout, 0) * phys / n_gpus,
                           learner_collective_backend=args.dist_backend)
                .debugging(seed=0))
         algo = cfg.build()
-        info = {"rollout_workers": w_per * n_gpus, "envs_per_worker": envs, "learner_actors": n_gpus,
+        info = {"rollout_workers": w_per * n_gpus, "envs_per_worker": envs, "cpus_per_rollout_worker": cpw,
+                "learner_actors": n_gpus,
                 "cpu_budget": budget, "learners": algo.learner_group.device_info()}
         for _ in range(args.warmup):
             algo.train()
@@ -234,6 +239,7 @@ def main():
                     help="cpu: CPU env + CPU policy (atari-ppo.yaml); hybrid: CPU env + policy on the rollout "
                          "worker's GPU slice (num_gpus_per_worker > 0); gpu: device env + GPU policy")
     ap.add_argument("--workers-per-learner", type=int, default=0)
+    ap.add_argument("--env-threads", type=int, default=0, help="CPUs per hybrid rollout worker (0: auto, <= 4)")
     ap.add_argument("--fragment", type=int, default=100)
     ap.add_argument("--minibatch", type=int, default=500)
     ap.add_argument("--sgd-iters", type=int, default=10)

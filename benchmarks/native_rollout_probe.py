@@ -24,8 +24,12 @@ def main(n: int = 50, T: int = 100, groups: int = 1, frags: int = 20):
     for _ in range(frags):
         w.sample()
     dt = (time.perf_counter() - t0) / frags
-    print(json.dumps({"n_envs": n, "T": T, "groups": len(w.groups), "native_loop": w._native_desc is not None,
-                      "ms_per_fragment": round(dt * 1e3, 3), "us_per_step": round(dt / T * 1e6, 2)}), flush=True)
+    from ray_memory_management_amd._native import require_hip
+
+    ph = [round(x / T, 2) for x in require_hip().hybrid_rollout_phases()] if getattr(w, "_native_desc", None) else None
+    print(json.dumps({"n_envs": n, "T": T, "groups": len(w.groups), "native_loop": getattr(w, "_native_desc", None) is not None,
+                      "ms_per_fragment": round(dt * 1e3, 3), "us_per_step": round(dt / T * 1e6, 2),
+                      "us_per_step_wait_env_launch": ph}), flush=True)
 
 
 if __name__ == "__main__":

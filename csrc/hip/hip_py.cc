@@ -279,11 +279,12 @@ PYBIND11_MODULE(_hip, m) {
     return reinterpret_cast<uint64_t>(d);
   }, py::arg("host_ptr"));
   // native hybrid rollout loop: groups = [(graph_exec, stream, pools, t, step, seed, n, A, episode_len, act,
-  // new_frames, rew, done, ep_rew, ep_len)], all raw addresses; returns finished (return, length) episodes
-  m.def("hybrid_rollout", [](const std::vector<std::vector<uint64_t>>& groups, int64_t T) {
+  // new_frames, rew, done, ep_rew, ep_len[, gate release counter])], all raw addresses; returns finished
+  // (return, length) episodes
+  m.def("hybrid_rollout", [](const std::vector<std::vector<uint64_t>>& groups, int64_t T, int threads, bool spin) {
     std::vector<RolloutGroup> G;
     for (const auto& v : groups) {
-      if (v.size() != 15) throw std::invalid_argument("hybrid_rollout: 15 fields per group");
+      if (v.size() != 15 && v.size() != 16) throw std::invalid_argument("hybrid_rollout: 15 or 16 fields per group");
       RolloutGroup g;
       g.exec = reinterpret_cast<hipGraphExec_t>(v[0]);
       g.stream = S(v[1]);
@@ -300,13 +301,15 @@ PYBIND11_MODULE(_hip, m) {
       g.done = P<float>(v[12]);
       g.ep_rew = P<double>(v[13]);
       g.ep_len = P<int64_t>(v[14]);
+      g.release = v.size() > 15 && v[15] ? P<int64_t>(v[15]) : nullptr;
       if (g.env.n <= 0 || g.env.num_actions <= 0 || g.env.episode_len <= 0)
         throw std::invalid_argument("hybrid_rollout: bad env shape");
       G.push_back(g);
     }
     py::gil_scoped_release nogil;
-    return hybrid_rollout(G, T);
-  }, py::arg("groups"), py::arg("T"));
+    return hybrid_rollout(G, T, threads, spin);
+  }, py::arg("groups"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false);
+  m.def("hybrid_rollout_phases", &hybrid_rollout_phases);
   m.def("step_gate", [](uint64_t host_release, uint64_t dev_seq, int64_t max_polls, uint64_t err, uint64_t stream) {
     step_gate(P<const int64_t>(host_release), P<int64_t>(dev_seq), max_polls, P<int>(err), S(stream));
   });

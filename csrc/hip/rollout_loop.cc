@@ -11,7 +11,11 @@
 // and a graph launch — no Python, no per-step torch wrappers — so the loop runs at the GPU's pace.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <stdexcept>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -22,7 +26,95 @@
 namespace rmm {
 namespace hip {
 
-std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<RolloutGroup>& G, int64_t T) {
+namespace {
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Helper threads that split each env step by env range. They spin on a job sequence number for
+// the duration of one hybrid_rollout call (a fragment, a few ms), so handing out a step costs two
+// cache-line transfers instead of a futex wake-up. A step of 50 envs writes ~350 KB of frames into
+// pinned memory: ~15-20 µs on one core, the largest host cost of a rollout step.
+class EnvThreads {
+ public:
+  explicit EnvThreads(int n) : n_(std::max(0, n - 1)) {
+    for (int k = 0; k < n_; k++) th_.emplace_back([this, k] { run(k + 1); });
+  }
+  ~EnvThreads() {
+    stop_.store(true, std::memory_order_release);
+    seq_.fetch_add(1, std::memory_order_acq_rel);
+    for (auto& t : th_) t.join();
+  }
+  // env step of group g at row t, split over all threads (the caller takes part)
+  void step(const RolloutGroup& g, uint64_t step, int64_t t) {
+    job_ = Job{&g, step, t};
+    if (n_ == 0) {
+      work(0);
+      return;
+    }
+    done_.store(0, std::memory_order_relaxed);
+    seq_.fetch_add(1, std::memory_order_release);
+    work(0);
+    while (done_.load(std::memory_order_acquire) != n_) cpu_relax();
+  }
+
+ private:
+  struct Job {
+    const RolloutGroup* g;
+    uint64_t step;
+    int64_t t;
+  };
+  void work(int k) {
+    const RolloutGroup& g = *job_.g;
+    const int64_t n = g.env.n, parts = n_ + 1;
+    const int64_t i0 = n * k / parts, i1 = n * (k + 1) / parts;
+    rl::synth_step_range(g.env, job_.step, i0, i1, g.act, g.new_frames, false, g.rew + job_.t * n, g.done + job_.t * n);
+  }
+  void run(int k) {
+    uint64_t seen = seq_.load(std::memory_order_acquire);
+    for (;;) {
+      uint64_t s;
+      while ((s = seq_.load(std::memory_order_acquire)) == seen) cpu_relax();
+      seen = s;
+      if (stop_.load(std::memory_order_acquire)) return;
+      work(k);
+      done_.fetch_add(1, std::memory_order_acq_rel);
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  Job job_{};
+  alignas(64) std::atomic<uint64_t> seq_{0};
+  alignas(64) std::atomic<int> done_{0};
+  alignas(64) std::atomic<bool> stop_{false};
+};
+
+// Wait for a step's event: poll (the step takes tens of µs; a blocking wait adds a wake-up) or block.
+void wait_event(hipEvent_t e, bool spin) {
+  if (!spin) {
+    RMM_HIP_CHECK(hipEventSynchronize(e));
+    return;
+  }
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) RMM_HIP_CHECK(r);
+    cpu_relax();
+  }
+}
+
+using Clock = std::chrono::steady_clock;
+double g_phase_us[3] = {0, 0, 0};  // last call: time waiting for steps, in env steps, in launches
+
+inline double us_since(Clock::time_point a) {
+  return std::chrono::duration<double, std::micro>(Clock::now() - a).count();
+}
+
+}  // namespace
+
+std::vector<double> hybrid_rollout_phases() { return {g_phase_us[0], g_phase_us[1], g_phase_us[2]}; }
+
+std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<RolloutGroup>& G, int64_t T, int threads,
+                                                       bool spin) {
   if (T <= 0 || G.empty()) return {};
   for (const auto& g : G)
     if (!g.exec || !g.env.pools || !g.act || !g.new_frames || !g.rew || !g.done || !g.ep_rew || !g.ep_len)
@@ -34,19 +126,44 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
     RMM_HIP_CHECK(hipEventRecord(ev[i], G[i].stream));
   };
   try {
+    EnvThreads pool(std::max(1, std::min(threads, 16)));
     for (auto& e : ev) RMM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (size_t i = 0; i < G.size(); i++) launch(i);
+    auto release = [&](size_t i) {  // frames of the step are written: open the gate of the launched step
+      __atomic_fetch_add(G[i].release, int64_t(1), __ATOMIC_RELEASE);
+    };
+    for (size_t i = 0; i < G.size(); i++) {
+      launch(i);
+      if (G[i].release) release(i);  // step 0's frames are already staged
+    }
+    double ph[3] = {0, 0, 0};
     for (int64_t t = 0; t < T; t++) {
       for (size_t i = 0; i < G.size(); i++) {  // group i's env step overlaps the other groups' policy steps
         const RolloutGroup& g = G[i];
-        RMM_HIP_CHECK(hipEventSynchronize(ev[i]));  // step t's actions are in g.act
-        float* rew = g.rew + t * g.env.n;
-        float* done = g.done + t * g.env.n;
-        rl::synth_step(g.env, g.act, g.new_frames, false, rew, done);
-        rl::episode_update(g.env.n, rew, done, g.ep_rew, g.ep_len, completed);
-        if (t + 1 < T) launch(i);
+        auto c0 = Clock::now();
+        wait_event(ev[i], spin);  // step t's actions are in g.act
+        ph[0] += us_since(c0);
+        const bool gated = g.release != nullptr;
+        if (gated && t + 1 < T) {  // step t+1 is enqueued now; it waits on the device for release()
+          c0 = Clock::now();
+          launch(i);
+          ph[2] += us_since(c0);
+        }
+        c0 = Clock::now();
+        pool.step(g, g.env.step[0]++, t);
+        rl::episode_update(g.env.n, g.rew + t * g.env.n, g.done + t * g.env.n, g.ep_rew, g.ep_len, completed);
+        ph[1] += us_since(c0);
+        if (t + 1 < T) {
+          if (gated) {
+            release(i);
+          } else {
+            c0 = Clock::now();
+            launch(i);
+            ph[2] += us_since(c0);
+          }
+        }
       }
     }
+    for (int k = 0; k < 3; k++) g_phase_us[k] = ph[k];
   } catch (...) {
     for (const auto& g : G) (void)hipStreamSynchronize(g.stream);  // no launch may outlive the buffers
     for (auto e : ev)

@@ -21,12 +21,18 @@ struct RolloutGroup {
   float* done = nullptr;          // pinned host [T][n]
   double* ep_rew = nullptr;       // [n] running episode returns
   int64_t* ep_len = nullptr;      // [n] running episode lengths
+  // step gate (optional): the graph starts with a device-side wait until *release passes its
+  // sequence number, so step t+1 is launched BEFORE step t's env step and only released after it
+  int64_t* release = nullptr;     // pinned host release counter (null: no gate)
 };
 
-// Launch step 0 of every group, then for t < T and each group: wait for its step, step its envs
-// (actions → newest frames, rewards, dones at row t), and launch its next step. Blocking; returns
-// the episodes that finished as (return, length).
-std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<RolloutGroup>& G, int64_t T);
+// Launch step 0 of every group, then for t < T and each group: wait for its step (poll when
+// `spin`), step its envs (actions → newest frames, rewards, dones at row t) on `threads` CPU threads,
+// and launch its next step. Blocking; returns the episodes that finished as (return, length).
+std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<RolloutGroup>& G, int64_t T,
+                                                       int threads = 1, bool spin = false);
+// µs the last hybrid_rollout call spent {waiting for policy steps, in env steps, launching steps}
+std::vector<double> hybrid_rollout_phases();
 
 }  // namespace hip
 }  // namespace rmm

@@ -34,13 +34,13 @@ inline uint64_t mix64(uint64_t seed, uint64_t step, uint64_t env) {
   return z ^ (z >> 31);
 }
 
-// One step of all n envs. act: [n] int64 (taken mod num_actions). stacks = false: out is [n][84*84]
-// and receives each env's NEWEST frame only; stacks = true: out is [n][4][84*84], shifted by one
-// frame in place with the newest appended. rew / done: [n] float (0/1).
-inline void synth_step(const SynthAtariState& s, const int64_t* act, uint8_t* out, bool stacks, float* rew,
-                       float* done) {
-  const uint64_t step = s.step[0]++;
-  for (int64_t i = 0; i < s.n; i++) {
+// Envs [i0, i1) of one step at random-stream position `step` (threads split a step by env range).
+// act: [n] int64 (taken mod num_actions). stacks = false: out is [n][84*84] and receives each env's
+// NEWEST frame only; stacks = true: out is [n][4][84*84], shifted by one frame in place with the
+// newest appended. rew / done: [n] float (0/1).
+inline void synth_step_range(const SynthAtariState& s, uint64_t step, int64_t i0, int64_t i1, const int64_t* act,
+                             uint8_t* out, bool stacks, float* rew, float* done) {
+  for (int64_t i = i0; i < i1; i++) {
     int64_t a = act[i] % s.num_actions;
     if (a < 0) a += s.num_actions;
     const uint64_t h = mix64(s.seed, step, uint64_t(i));
@@ -57,6 +57,12 @@ inline void synth_step(const SynthAtariState& s, const int64_t* act, uint8_t* ou
     if (d) s.t[i] = 0;
     done[i] = d ? 1.f : 0.f;
   }
+}
+
+// One step of all n envs (advances the random-stream position).
+inline void synth_step(const SynthAtariState& s, const int64_t* act, uint8_t* out, bool stacks, float* rew,
+                       float* done) {
+  synth_step_range(s, s.step[0]++, 0, s.n, act, out, stacks, rew, done);
 }
 
 // Episode bookkeeping of a rollout worker after a step: running return / length per env, and the

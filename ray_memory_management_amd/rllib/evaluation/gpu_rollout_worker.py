@@ -415,7 +415,10 @@ class HybridRolloutWorker(GPURolloutWorker):
             if native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
                 from ray_memory_management_amd._native import require_hip
 
-                self._completed.extend(require_hip().hybrid_rollout(native, T))
+                # the env step is split over the worker's CPUs (num_cpus_per_worker); RMM_ENV_THREADS overrides
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("num_cpus_per_worker", 1) or 1)
+                spin = os.environ.get("RMM_NATIVE_SPIN", "1") != "0"
+                self._completed.extend(require_hip().hybrid_rollout(native, T, threads=max(1, th), spin=spin))
             else:
                 self._python_loop(G, S, T, st, shared)
             with torch.cuda.stream(st):
@@ -446,7 +449,8 @@ class HybridRolloutWorker(GPURolloutWorker):
         """Per-group descriptors for the native rollout loop (csrc/hip/rollout_loop.cc), or None when
         a group needs the Python loop: the env must be the native synthetic vector env, the policy
         step a captured HIP graph reading the newest frames from mapped pinned memory and storing the
-        actions into it (K10 push mode + K16 direct store), no step gate. RMM_NO_NATIVE_ROLLOUT=1
+        actions into it (K10 push mode + K16 direct store); with the step gate (RMM_ROLLOUT_GATE=1)
+        step t+1 is launched before step t's env step and released after it. RMM_NO_NATIVE_ROLLOUT=1
         forces the Python loop."""
         if os.environ.get("RMM_NO_NATIVE_ROLLOUT") or os.environ.get("RMM_ROLLOUT_SPIN", "0") != "0":
             return None
@@ -455,14 +459,14 @@ class HybridRolloutWorker(GPURolloutWorker):
             return cached
         desc = []
         for g, gs in zip(G, S):
-            ok = (g.graph not in (None, False) and not g.gate and g.device_stack and g.h_new_dev and g.fused
+            ok = (g.graph not in (None, False) and g.device_stack and g.h_new_dev and g.fused
                   and g.h_act_dev and getattr(g.env, "_native", None) is not None
                   and hasattr(g.env, "native_state") and hasattr(g.graph, "raw_cuda_graph_exec"))
             if not ok:
                 return None
             desc.append([int(g.graph.raw_cuda_graph_exec()), int(gs.cuda_stream), *map(int, g.env.native_state()),
                          g.h_act.data_ptr(), g.h_new.data_ptr(), g.h_rew.data_ptr(), g.h_done.data_ptr(),
-                         g.ep_rew.ctypes.data, g.ep_len.ctypes.data])
+                         g.ep_rew.ctypes.data, g.ep_len.ctypes.data, g.h_release.data_ptr() if g.gate else 0])
         self._native_desc = desc
         return desc
 

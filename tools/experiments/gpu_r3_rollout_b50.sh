@@ -4,7 +4,6 @@ set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 120 python -u benchmarks/native_rollout_probe.py 50 100 1 > gpurun_out/rp_50_1.log 2>&1 && tail -1 gpurun_out/rp_50_1.log || exit 1
-timeout -k 10 120 python -u benchmarks/native_rollout_probe.py 50 100 2 > gpurun_out/rp_50_2.log 2>&1 && tail -1 gpurun_out/rp_50_2.log || exit 1
 RMM_NO_NATIVE_ROLLOUT=1 timeout -k 10 120 python -u benchmarks/native_rollout_probe.py 50 100 1 > gpurun_out/rp_50_1py.log 2>&1 && tail -1 gpurun_out/rp_50_1py.log || exit 1
 timeout -k 10 120 python -u benchmarks/native_rollout_probe.py 25 100 1 > gpurun_out/rp_25_1.log 2>&1 && tail -1 gpurun_out/rp_25_1.log || exit 1
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_prof -o rp -- python -u benchmarks/native_rollout_probe.py 50 100 1 > gpurun_out/rp_prof.log 2>&1 || { tail -5 gpurun_out/rp_prof.log; exit 1; }
