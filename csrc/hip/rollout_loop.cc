@@ -119,48 +119,47 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
   for (const auto& g : G)
     if (!g.exec || !g.env.pools || !g.act || !g.new_frames || !g.rew || !g.done || !g.ep_rew || !g.ep_len)
       throw std::invalid_argument("hybrid_rollout: incomplete group");
-  std::vector<hipEvent_t> ev(G.size(), nullptr);
+  // two events per group: with the gate, steps t and t+1 are in flight together
+  std::vector<hipEvent_t> ev(2 * G.size(), nullptr);
   std::vector<std::pair<double, int64_t>> completed;
-  auto launch = [&](size_t i) {
+  auto launch = [&](size_t i, int64_t step) {
     RMM_HIP_CHECK(hipGraphLaunch(G[i].exec, G[i].stream));
-    RMM_HIP_CHECK(hipEventRecord(ev[i], G[i].stream));
+    RMM_HIP_CHECK(hipEventRecord(ev[2 * i + (step & 1)], G[i].stream));
+  };
+  auto release = [&](size_t i) {  // frames of the next step are written: open its gate
+    __atomic_fetch_add(G[i].release, int64_t(1), __ATOMIC_RELEASE);
   };
   try {
     EnvThreads pool(std::max(1, std::min(threads, 16)));
     for (auto& e : ev) RMM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    auto release = [&](size_t i) {  // frames of the step are written: open the gate of the launched step
-      __atomic_fetch_add(G[i].release, int64_t(1), __ATOMIC_RELEASE);
-    };
     for (size_t i = 0; i < G.size(); i++) {
-      launch(i);
-      if (G[i].release) release(i);  // step 0's frames are already staged
+      launch(i, 0);
+      if (G[i].release) {
+        release(i);                  // step 0's frames are already staged
+        if (T > 1) launch(i, 1);     // step 1 waits on the device for its frames
+      }
     }
     double ph[3] = {0, 0, 0};
     for (int64_t t = 0; t < T; t++) {
       for (size_t i = 0; i < G.size(); i++) {  // group i's env step overlaps the other groups' policy steps
         const RolloutGroup& g = G[i];
         auto c0 = Clock::now();
-        wait_event(ev[i], spin);  // step t's actions are in g.act
+        wait_event(ev[2 * i + (t & 1)], spin);  // step t's actions are in g.act
         ph[0] += us_since(c0);
-        const bool gated = g.release != nullptr;
-        if (gated && t + 1 < T) {  // step t+1 is enqueued now; it waits on the device for release()
-          c0 = Clock::now();
-          launch(i);
-          ph[2] += us_since(c0);
-        }
         c0 = Clock::now();
         pool.step(g, g.env.step[0]++, t);
         rl::episode_update(g.env.n, g.rew + t * g.env.n, g.done + t * g.env.n, g.ep_rew, g.ep_len, completed);
         ph[1] += us_since(c0);
-        if (t + 1 < T) {
-          if (gated) {
-            release(i);
-          } else {
-            c0 = Clock::now();
-            launch(i);
-            ph[2] += us_since(c0);
-          }
+        c0 = Clock::now();
+        if (g.release) {
+          // gate: step t+1 is already enqueued (its launch latency hid behind step t); open it, then
+          // enqueue step t+2 while step t+1 runs
+          if (t + 1 < T) release(i);
+          if (t + 2 < T) launch(i, t + 2);
+        } else if (t + 1 < T) {
+          launch(i, t + 1);
         }
+        ph[2] += us_since(c0);
       }
     }
     for (int k = 0; k < 3; k++) g_phase_us[k] = ph[k];
