@@ -177,10 +177,9 @@ def _runtime(args, n_gpus):
         if args.workers_per_learner:
             w_per = args.workers_per_learner
             envs = max(1, TRAIN_BATCH // (args.fragment * w_per))
-        # hybrid: a worker splits each env step over its CPUs (native rollout loop), up to 4
-        cpw = 1 if args.rollout == "cpu" else max(1, min(4, ((budget - 1) // n_gpus - 1) // w_per))
-        if args.env_threads:
-            cpw = args.env_threads
+        # hybrid: --env-threads N gives each rollout worker N CPUs and splits its env steps over them
+        # (native rollout loop); 1 by default (measured neutral, profiles/native_rollout_r3.txt)
+        cpw = max(1, args.env_threads) if args.rollout != "cpu" else 1
         n_cpus = max(budget, n_gpus * (w_per * cpw + 1) + 1)
     else:
         w_per, envs, cpw = 1, TRAIN_BATCH // args.fragment, 1
@@ -206,7 +205,7 @@ def _runtime(args, n_gpus):
                .environment("GPUSyntheticAtari-v0" if args.rollout == "gpu" else "SyntheticAtariVec-v0",
                             env_config={"num_actions": 4, "episode_len": 1000})
                .rollouts(num_rollout_workers=w_per * n_gpus, num_envs_per_worker=envs,
-                         rollout_fragment_length=args.fragment, postprocess_on_learner=True,
+                         rollout_fragment_length=args.fragment, postprocess_on_learner=True, rollout_env_threads=cpw,
                          gpu_rollouts=args.rollout == "gpu")
                .training(train_batch_size=TRAIN_BATCH * n_gpus, sgd_minibatch_size=args.minibatch * n_gpus,
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
@@ -239,7 +238,7 @@ def main():
                     help="cpu: CPU env + CPU policy (atari-ppo.yaml); hybrid: CPU env + policy on the rollout "
                          "worker's GPU slice (num_gpus_per_worker > 0); gpu: device env + GPU policy")
     ap.add_argument("--workers-per-learner", type=int, default=0)
-    ap.add_argument("--env-threads", type=int, default=0, help="CPUs per hybrid rollout worker (0: auto, <= 4)")
+    ap.add_argument("--env-threads", type=int, default=1, help="CPUs (env-step threads) per hybrid rollout worker")
     ap.add_argument("--fragment", type=int, default=100)
     ap.add_argument("--minibatch", type=int, default=500)
     ap.add_argument("--sgd-iters", type=int, default=10)

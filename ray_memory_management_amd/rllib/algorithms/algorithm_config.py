@@ -106,6 +106,9 @@ class AlgorithmConfig:
             self.batch_mode = batch_mode
         if gpu_rollouts is not None:
             self.gpu_rollouts = gpu_rollouts
+        for k, v in kw.items():  # e.g. rollout_env_threads, rollout_double_buffer (hybrid rollout workers)
+            if v is not None:
+                setattr(self, k, v)
         return self
 
     def training(self, *, gamma=None, lr=None, train_batch_size=None, model=None, optimizer=None,

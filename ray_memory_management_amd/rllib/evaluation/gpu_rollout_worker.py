@@ -415,8 +415,9 @@ class HybridRolloutWorker(GPURolloutWorker):
             if native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
                 from ray_memory_management_amd._native import require_hip
 
-                # the env step is split over the worker's CPUs (num_cpus_per_worker); RMM_ENV_THREADS overrides
-                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("num_cpus_per_worker", 1) or 1)
+                # rollout_env_threads (default 1) splits each env step over that many CPU threads; measured
+                # neutral for the synthetic env (profiles/native_rollout_r3.txt); RMM_ENV_THREADS overrides
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
                 spin = os.environ.get("RMM_NATIVE_SPIN", "1") != "0"
                 self._completed.extend(require_hip().hybrid_rollout(native, T, threads=max(1, th), spin=spin))
             else:
