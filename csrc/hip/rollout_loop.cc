@@ -88,18 +88,24 @@ class EnvThreads {
   alignas(64) std::atomic<bool> stop_{false};
 };
 
-// Wait for a step's event: poll (the step takes tens of µs; a blocking wait adds a wake-up) or block.
+// Wait for a step's event. `spin`: poll for up to kSpinUs (a policy step takes ~30-40 µs; a blocking
+// wait adds a wake-up), then block — on a host whose CPUs are shared, an unbounded poll that loses its
+// core costs more than it saves (measured outliers, profiles/native_rollout_r3.txt).
+constexpr double kSpinUs = 150.0;
 void wait_event(hipEvent_t e, bool spin) {
-  if (!spin) {
-    RMM_HIP_CHECK(hipEventSynchronize(e));
-    return;
+  if (spin) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; k++) {
+      const hipError_t r = hipEventQuery(e);
+      if (r == hipSuccess) return;
+      if (r != hipErrorNotReady) RMM_HIP_CHECK(r);
+      cpu_relax();
+      if ((k & 15) == 15 &&
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kSpinUs)
+        break;
+    }
   }
-  for (;;) {
-    const hipError_t r = hipEventQuery(e);
-    if (r == hipSuccess) return;
-    if (r != hipErrorNotReady) RMM_HIP_CHECK(r);
-    cpu_relax();
-  }
+  RMM_HIP_CHECK(hipEventSynchronize(e));
 }
 
 using Clock = std::chrono::steady_clock;

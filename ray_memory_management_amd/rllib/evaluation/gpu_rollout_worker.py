@@ -418,7 +418,9 @@ class HybridRolloutWorker(GPURolloutWorker):
                 # rollout_env_threads (default 1) splits each env step over that many CPU threads; measured
                 # neutral for the synthetic env (profiles/native_rollout_r3.txt); RMM_ENV_THREADS overrides
                 th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
-                spin = os.environ.get("RMM_NATIVE_SPIN", "1") != "0"
+                # blocking event waits by default: a bounded poll was faster on an idle host but gave
+                # outliers when the host's CPUs were shared (profiles/native_rollout_r3.txt)
+                spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
                 self._completed.extend(require_hip().hybrid_rollout(native, T, threads=max(1, th), spin=spin))
             else:
                 self._python_loop(G, S, T, st, shared)
