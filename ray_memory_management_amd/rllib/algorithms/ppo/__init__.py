@@ -187,17 +187,21 @@ class PPO(Algorithm):
                 refs.append(w.sample.remote())
             steps += per_round
         if c.postprocess_on_learner:
-            stats = self.learner_group.update(split_for_learners(refs, n_l))
+            pending = self.learner_group.update_async(split_for_learners(refs, n_l))
         else:
             from ray_memory_management_amd.rllib.sample_batch import concat_samples
 
             shards = split_for_learners(refs, n_l)
-            stats = ray.get([l.update_batch.remote(concat_samples(ray.get(s)))
-                             for l, s in zip(self.learner_group.learners, shards)])
+            pending = [l.update_batch.remote(concat_samples(ray.get(s)))
+                       for l, s in zip(self.learner_group.learners, shards)]
+        # the weight publication is queued right behind the update on each learner (actor calls run
+        # in order), so it runs while the driver is still collecting the update's stats: no extra
+        # driver round trip before the next iteration's set_weights + sample
         if dev:  # GPU rollout workers read the learners' bf16 weights from HBM (hipIPC)
             self._dev_refs = self.learner_group.device_weights_refs()
         else:
             self._weights_ref = self.learner_group.weights_ref()
+        stats = ray.get(pending)
         self._counters["num_env_steps_sampled"] += steps
         self._counters["num_env_steps_trained"] += steps
         self._counters["num_agent_steps_trained"] += steps

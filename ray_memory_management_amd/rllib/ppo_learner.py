@@ -548,6 +548,7 @@ class PPOLearner:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._graph = self._graphs_split = None
         self._graph_has_comm = False
+        self._chain = 1
         if self.world > 1 and manual and getattr(self.comm, "graph_capturable", False) \
                 and os.environ.get("RMM_RCCL_IN_GRAPH") == "1":
             # ONE graph per SGD step with the all-reduces inside it: after K12 the graph forks onto
@@ -577,20 +578,26 @@ class PPOLearner:
                 self._overlapped_tail(full)
             self._graph = g
         elif self.world == 1 or self.cfg["allreduce_in_graph"]:
+            # world of one: `chain` consecutive SGD steps per graph (the device counters index each
+            # step's minibatch and Adam step) — consecutive replays of a one-step graph leave ~8 µs
+            # idle between them on MI355X (profiles/sgd_chain_r3.txt), a chained graph none
+            chain = self._sgd_chain(int(full["period"])) if self.world == 1 else 1
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                if manual:
-                    self._manual_fwd_dense_bwd(full)
-                    if self.world > 1:
-                        self.comm.allreduce(self.flat_grad[self._manual:])
-                    self._manual_trunk_bwd(full)
-                    if self.world > 1:
-                        self.comm.allreduce(self.flat_grad[:self._manual])
-                    if not self._fused_adam():
-                        self._opt_launch()
-                else:
-                    self._fast_step(full, True)
+                for _ in range(chain):
+                    if manual:
+                        self._manual_fwd_dense_bwd(full)
+                        if self.world > 1:
+                            self.comm.allreduce(self.flat_grad[self._manual:])
+                        self._manual_trunk_bwd(full)
+                        if self.world > 1:
+                            self.comm.allreduce(self.flat_grad[:self._manual])
+                        if not self._fused_adam():
+                            self._opt_launch()
+                    else:
+                        self._fast_step(full, True)
             self._graph = g
+            self._chain = chain
         elif manual and _comm_overlap():
             # multi-rank, RMM_COMM_OVERLAP=1: three graphs with the two bucket all-reduces between
             # them, the dense+heads all-reduce forked onto the comm stream during graph B
@@ -622,6 +629,12 @@ class PPOLearner:
             self._graph = g
         for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc), saved):
             dst.copy_(src)  # undo warm-up updates
+
+    def _sgd_chain(self, total: int) -> int:
+        """SGD steps captured per graph (world of one): the largest divisor of the update's step
+        count that is <= RMM_SGD_CHAIN (default 25)."""
+        cap = max(1, int(os.environ.get("RMM_SGD_CHAIN", "25")))
+        return max(d for d in range(1, min(cap, max(total, 1)) + 1) if total % d == 0)
 
     def _replay(self):
         if self._graphs_split is not None and self._graphs_split[1] is None:
@@ -718,13 +731,16 @@ class PPOLearner:
         else:
             full = packed
         self.ctr[0:1].zero_()
-        steps = 0
-        for _ in range(c["num_sgd_iter"] * nmb):
+        steps, total = 0, c["num_sgd_iter"] * nmb
+        chain = getattr(self, "_chain", 1) if self.graphs and self._graph is not None else 1
+        if total % chain:  # not expected: the chain divides the period it was captured for
+            raise RuntimeError(f"SGD graph chains {chain} steps, update has {total}")
+        while steps < total:
             if self.graphs:
                 self._replay()
             else:
                 self._step_eager(full)
-            steps += 1
+            steps += chain
         if self.world > 1:  # KL adaptation and stats from the global batch, identical on every rank
             self.comm.allreduce(self.acc)
             self.acc.mul_(1.0 / self.world)
