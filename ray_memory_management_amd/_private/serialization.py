@@ -50,6 +50,11 @@ class _Pickler(cloudpickle.CloudPickler):
         t = type(obj)
         if _custom_serializers:
             ent = _custom_serializers.get(t)
+            if ent is None:  # a serializer registered for a base class covers its subclasses
+                for base in t.__mro__[1:-1]:
+                    ent = _custom_serializers.get(base)
+                    if ent is not None:
+                        break
             if ent is not None:
                 return _rebuild_custom, (ent[1], ent[0](obj))
         mod = t.__module__

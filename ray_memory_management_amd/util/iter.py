@@ -17,9 +17,11 @@ from __future__ import annotations
 import collections
 import itertools
 import random
+import threading
 from typing import Any, Callable, Iterable, List, Optional
 
 import ray_memory_management_amd as ray
+from ray_memory_management_amd.util.iter_metrics import MetricsContext, SharedMetrics
 
 _NEXT_BATCH = 32
 
@@ -280,7 +282,11 @@ class ParallelIterator:
                 ready, _ = ray.wait(list(inflight), num_returns=1)
                 a = inflight.pop(ready[0])
                 items, done = ray.get(ready[0])
-                yield from items
+                for x in items:
+                    stack = getattr(_metrics_tls, "stack", None)
+                    if stack:  # the consumer's metrics: which shard produced this item
+                        stack[-1].current_actor = a
+                    yield x
                 if done:
                     finished.add(id(a))
                 elif id(a) not in finished:
@@ -314,13 +320,20 @@ class ParallelIterator:
             print(x)
 
 
-class LocalIterator:
-    """Driver-side iterator with lazy transforms (reference iter.py LocalIterator)."""
+_metrics_tls = threading.local()
 
-    def __init__(self, base_iterator: Callable[[], Iterable], name: Optional[str] = None):
+
+class LocalIterator:
+    """Driver-side iterator with lazy transforms (reference iter.py LocalIterator). Every operator of
+    a chain shares one MetricsContext (util.iter_metrics), readable from inside the operators'
+    functions through ``LocalIterator.get_metrics()``."""
+
+    def __init__(self, base_iterator: Callable[[], Iterable], name: Optional[str] = None,
+                 shared_metrics: Optional[SharedMetrics] = None):
         self.base_iterator = base_iterator
         self.built_iterator = None
         self.name = name or "LocalIterator"
+        self.shared_metrics = shared_metrics or SharedMetrics()
 
     def _build(self):
         if self.built_iterator is None:
@@ -332,14 +345,30 @@ class LocalIterator:
 
     def __next__(self):
         self._build()
-        return next(self.built_iterator)
+        stack = getattr(_metrics_tls, "stack", None)
+        if stack is None:
+            stack = _metrics_tls.stack = []
+        stack.append(self.shared_metrics.get())
+        try:
+            return next(self.built_iterator)
+        finally:
+            stack.pop()
+
+    @staticmethod
+    def get_metrics() -> MetricsContext:
+        """The metrics context of the iterator whose item is being computed (call it only from inside
+        an operator function of a LocalIterator chain)."""
+        stack = getattr(_metrics_tls, "stack", None)
+        if not stack:
+            raise ValueError("get_metrics() may only be called from inside a LocalIterator operator")
+        return stack[-1]
 
     def __repr__(self):
         return f"LocalIterator[{self.name}]"
 
     def _chain(self, f, label):
         parent = self
-        return LocalIterator(lambda: f(iter(parent)), self.name + label)
+        return LocalIterator(lambda: f(iter(parent)), self.name + label, shared_metrics=self.shared_metrics)
 
     def for_each(self, fn: Callable, max_concurrency: int = 1, resources=None) -> "LocalIterator":
         return self._chain(lambda it: map(fn, it), ".for_each()")
@@ -390,7 +419,8 @@ class LocalIterator:
                         nxt_w.append(k)
                 live, w = nxt_live, nxt_w
 
-        return LocalIterator(gen, f"LocalUnion[{', '.join(i.name for i in its)}]")
+        return LocalIterator(gen, f"LocalUnion[{', '.join(i.name for i in its)}]",
+                             shared_metrics=SharedMetrics(parents=[i.shared_metrics for i in its]))
 
     def duplicate(self, n: int) -> List["LocalIterator"]:
         """n iterators over the same items (buffers what the slowest has not consumed)."""
@@ -410,4 +440,5 @@ class LocalIterator:
                     yield queues[i].popleft()
             return gen
 
-        return [LocalIterator(make(i), self.name + f".duplicate[{i}]") for i in range(n)]
+        return [LocalIterator(make(i), self.name + f".duplicate[{i}]", shared_metrics=self.shared_metrics)
+                for i in range(n)]

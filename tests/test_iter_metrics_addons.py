@@ -1,0 +1,80 @@
+"""util.iter_metrics (MetricsContext / SharedMetrics through LocalIterator.get_metrics), subclass-aware
+custom serializers and util.serialization_addons (pydantic models and starlette requests through the
+runtime's pickler), deprecated experimental aliases."""
+import pytest
+
+
+def test_local_iterator_shared_metrics():
+    from ray_memory_management_amd.util.iter import LocalIterator, from_items  # noqa: F401
+    from ray_memory_management_amd.util.iter_metrics import MetricsContext, SharedMetrics
+
+    def count(x):
+        m = LocalIterator.get_metrics()
+        m.counters["seen"] += 1
+        m.info["last"] = x
+        return x * 2
+
+    a = LocalIterator(lambda: iter(range(5))).for_each(count)
+    b = LocalIterator(lambda: iter(range(10, 13))).for_each(count)
+    u = a.union(b)
+    assert sorted(u.take(100)) == sorted([0, 2, 4, 6, 8, 20, 22, 24])
+    m = u.shared_metrics.get()
+    assert m is a.shared_metrics.get() is b.shared_metrics.get()  # union re-points both chains
+    assert m.counters["seen"] == 8
+    snap = m.save()
+    m2 = MetricsContext()
+    m2.restore(snap)
+    assert m2.counters["seen"] == 8 and m2.info["last"] in (4, 12)
+    with pytest.raises(ValueError):
+        LocalIterator.get_metrics()  # outside an operator
+    s = SharedMetrics(parents=[SharedMetrics()])
+    s.set(m2)
+    assert s.parents[0].get() is m2
+
+
+def test_subclass_serializer_and_addons():
+    import pydantic
+
+    from ray_memory_management_amd._private import serialization as ser
+    from ray_memory_management_amd.util import serialization_addons
+    from ray_memory_management_amd.util.serialization import deregister_serializer
+
+    class Point(pydantic.BaseModel):
+        x: int
+        y: float = 0.5
+
+    try:
+        serialization_addons.apply()
+        data = ser._Pickler.__module__  # module import sanity
+        assert data
+        import io
+        import pickle
+
+        buf = io.BytesIO()
+        ser._Pickler(buf, protocol=5).dump(Point(x=3))
+        p = pickle.loads(buf.getvalue())
+        assert isinstance(p, Point) and p.x == 3 and p.y == 0.5
+
+        from starlette.requests import Request
+
+        async def receive():
+            return {"type": "http.request", "body": b"hi", "more_body": False}
+
+        req = Request({"type": "http", "method": "POST", "path": "/a", "headers": [], "query_string": b"q=1"}, receive)
+        req._body = b"hi"
+        buf = io.BytesIO()
+        ser._Pickler(buf, protocol=5).dump(req)
+        r2 = pickle.loads(buf.getvalue())
+        assert r2.method == "POST" and r2.url.path == "/a" and r2.query_params["q"] == "1"
+    finally:
+        deregister_serializer(pydantic.BaseModel)
+        deregister_serializer(Request)
+
+
+def test_deprecated_experimental_aliases():
+    from ray_memory_management_amd.experimental.multiprocessing import Pool
+    from ray_memory_management_amd.experimental.queue import Empty, Queue
+    from ray_memory_management_amd.util.multiprocessing import Pool as P2
+    from ray_memory_management_amd.util.queue import Queue as Q2
+
+    assert Pool is P2 and Queue is Q2 and issubclass(Empty, Exception)
