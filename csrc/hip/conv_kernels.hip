@@ -410,6 +410,143 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
     *reinterpret_cast<uint4*>(&h2_out[b * NP2 * C2 + 8 * v]) = *reinterpret_cast<const uint4*>(&h2s[8 * v]);
 }
 
+
+// ================================================================ forward, rollout band mode
+// Rollout step at small B (one env per frame, B ~ 12-50): one workgroup per frame leaves most CUs
+// idle and the launch is a single frame's latency chain (~12 µs at any B <= 256). Here each frame
+// is split into NBAND workgroups by bands of conv2 output rows; a band computes the conv1 rows its
+// conv2 rows need (a 1-2 row halo, ~25% extra conv1 work) from the frame rows those need.
+// The frame stack is the previous rollout row: rows[(t-1) mod T] planes 1..3 + the env's newest
+// frame (may be device-mapped pinned host memory); each band writes its own disjoint 21 frame rows
+// of all 4 planes into rollout row t, and reads only row t-1 — so no band reads what another band
+// writes in the same launch, and no separate frame-stack buffer exists.
+constexpr int NBAND = 4, NTFB = 512;
+constexpr int BAND_FR = 36;              // padded frame rows per band tile (band 1: input rows 14..49)
+constexpr int BAND_H1R = 8;              // padded h1 rows per band tile
+__device__ __forceinline__ void band_geom(int s, int& o0, int& o1, int& ya, int& yb) {
+  o0 = 3 * s;                            // conv2 rows [o0, o1)
+  o1 = min(H2, o0 + 3);
+  ya = max(0, 2 * o0 - 2);               // conv1 (h1) rows [ya, yb] they read
+  yb = min(H1 - 1, 2 * o1 - 1);
+}
+__global__ __launch_bounds__(NTFB) void k_trunk_fwd_band(
+    const unsigned short* __restrict__ W1, WStrides w1, const unsigned short* __restrict__ b1,
+    const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ b2,
+    unsigned short* __restrict__ h2_out, int64_t B, uint8_t* rows, int64_t T, const uint8_t* __restrict__ nf,
+    const int64_t* __restrict__ t_ptr) {
+  __shared__ __attribute__((aligned(16))) uint8_t frame[BAND_FR * P0 * 4];
+  __shared__ __attribute__((aligned(16))) unsigned short h1p[BAND_H1R * P1 * C1];
+  __shared__ __attribute__((aligned(16))) unsigned short w1s[C1 * W1_PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short w2s[C2 * W2_PITCH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t b = blockIdx.x / NBAND;
+  const int s = blockIdx.x % NBAND;
+  int o0, o1, ya, yb;
+  band_geom(s, o0, o1, ya, yb);
+  const int fr0 = max(0, 4 * ya - 2), fr1 = min(H0 - 1, 4 * yb + 5);  // frame rows read
+  const int pr0 = 4 * ya;                                              // padded row of tile row 0
+  constexpr int64_t FB = C0 * H0 * H0;
+  constexpr int NWP = H0 * H0 / 4;                                     // u32 words per plane
+  const int64_t t = t_ptr[0];
+  const uint8_t* prev = rows + (((t == 0 ? T : t) - 1) * B + b) * FB;
+  uint32_t* cur32 = reinterpret_cast<uint32_t*>(rows + (t * B + b) * FB);
+  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(prev);
+  const uint32_t* n32 = reinterpret_cast<const uint32_t*>(nf + b * (H0 * H0));
+  constexpr int PER = (BAND_FR * 21 + NTFB - 1) / NTFB;
+  const int w0 = fr0 * 21, nw = (fr1 - fr0 + 1) * 21;
+  uint32_t v[PER][C0];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {  // all loads first (unconditional, clamped): one round trip
+    const int o = w0 + min(tid + NTFB * k, nw - 1);
+#pragma unroll
+    for (int c = 0; c < C0 - 1; c++) v[k][c] = p32[(c + 1) * NWP + o];
+    v[k][C0 - 1] = n32[o];
+  }
+  zero_lds(frame, BAND_FR * P0 * 4);
+  zero_lds(h1p, BAND_H1R * P1 * C1 * 2);
+  stage_weight<NTFB, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
+  stage_weight<NTFB, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
+  __syncthreads();
+  const int own0 = 21 * s, own1 = own0 + 21;  // the frame rows this band stores into rollout row t
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int i = tid + NTFB * k;
+    if (i < nw) {
+      const int o = w0 + i, y = o / 21, xw = o - y * 21;
+      uint32_t px[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        px[q] = ((v[k][0] >> (8 * q)) & 0xffu) | (((v[k][1] >> (8 * q)) & 0xffu) << 8) |
+                (((v[k][2] >> (8 * q)) & 0xffu) << 16) | (((v[k][3] >> (8 * q)) & 0xffu) << 24);
+      uint2* d = reinterpret_cast<uint2*>(frame + ((y + 2 - pr0) * P0 + 4 * xw + 2) * 4);
+      d[0] = make_uint2(px[0], px[1]);
+      d[1] = make_uint2(px[2], px[3]);
+      if (y >= own0 && y < own1) {
+#pragma unroll
+        for (int c = 0; c < C0; c++) cur32[c * NWP + o] = v[k][c];
+      }
+    }
+  }
+  __syncthreads();
+
+  bf16x8 wf1[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) wf1[k] = as_bf(*reinterpret_cast<const u16x8*>(&w1s[r * W1_PITCH + (k * 8 + 2 * g) * 4]));
+  const float bias1 = bf2f(b1[r]);
+  // ---- conv1 over h1 rows [ya, yb]: position p -> (y = ya + p / 21, x = p % 21)
+  const int np1 = (yb - ya + 1) * H1;
+  for (int mt = wave; mt * 16 < np1; mt += NTFB / 64) {
+    const int p = min(mt * 16 + r, np1 - 1);
+    const int oy = ya + p / H1, ox = p - (p / H1) * H1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc = mfma(frame8(frame, ((4 * (oy - ya) + k) * P0 + 4 * ox + 2 * g) * 4), wf1[k], acc);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int q = mt * 16 + 4 * g + i;
+      if (q < np1) {
+        const int y = ya + q / H1, x = q - (q / H1) * H1;
+        h1p[((y + 2 - 2 * o0) * P1 + (x + 2)) * C1 + r] = f2bf(fmaxf(acc[i] * (1.0f / 255.0f) + bias1, 0.f));
+      }
+    }
+  }
+  bf16x8 wf2[2][8];
+#pragma unroll
+  for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int pp = 2 * k + (g >> 1), co = nt * 16 + r;
+      wf2[nt][k] = as_bf(*reinterpret_cast<const u16x8*>(&w2s[co * W2_PITCH + pp * 16 + 8 * (g & 1)]));
+    }
+  const float bias2[2] = {bf2f(b2[r]), bf2f(b2[16 + r])};
+  __syncthreads();
+  // ---- conv2 over rows [o0, o1): position q -> (oy = o0 + q / 11, ox = q % 11)
+  const int np2 = (o1 - o0) * H2;
+  for (int mt = wave; mt * 16 < np2; mt += NTFB / 64) {
+    const int q = min(mt * 16 + r, np2 - 1);
+    const int oy = o0 + q / H2, ox = q - (q / H2) * H2;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int pp = 2 * k + (g >> 1), ky = pp >> 2, kx = pp & 3;
+      const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(
+          &h1p[((2 * (oy - o0) + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1)]));
+      acc0 = mfma(a, wf2[0][k], acc0);
+      acc1 = mfma(a, wf2[1][k], acc1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int qq = mt * 16 + 4 * g + i;
+      if (qq < np2) {
+        const int64_t pos = int64_t(o0) * H2 + qq;  // = oy * 11 + ox
+        h2_out[(b * NP2 + pos) * C2 + r] = f2bf(fmaxf(acc0[i] + bias2[0], 0.f));
+        h2_out[(b * NP2 + pos) * C2 + 16 + r] = f2bf(fmaxf(acc1[i] + bias2[1], 0.f));
+      }
+    }
+  }
+}
+
 // ================================================================ backward
 constexpr int PART = C1 * 256 + C2 * 256 + C1 + C2;  // per-workgroup fp32 partial: dW1, dW2, db1, db2
 // row pitches of the transposed dpre tiles: +8 elements so the 16 rows written by one lane
@@ -745,6 +882,21 @@ void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(b2),
                      static_cast<unsigned short*>(h1), static_cast<unsigned short*>(h2), dbg, nullptr, nullptr,
                      nullptr, nullptr);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void nature_trunk_fwd_push_rows(uint8_t* rows, int64_t T, const uint8_t* new_frames, const int64_t* t_ptr, int64_t B,
+                                const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
+                                const void* b2, void* h2, hipStream_t stream) {
+  if (B <= 0) return;
+  if (rows == nullptr || new_frames == nullptr || t_ptr == nullptr || T < 1)
+    throw std::invalid_argument("nature_trunk_fwd_push_rows: rollout rows, T, new frames and the row counter");
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(new_frames)) & 3)
+    throw std::invalid_argument("nature_trunk_fwd_push_rows: buffers must be 4-byte aligned");
+  hipLaunchKernelGGL(trunk::k_trunk_fwd_band, dim3(uint32_t(B * trunk::NBAND)), dim3(trunk::NTFB), 0, stream,
+                     static_cast<const unsigned short*>(W1), ws(w1s), static_cast<const unsigned short*>(b1),
+                     static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(b2),
+                     static_cast<unsigned short*>(h2), B, rows, T, new_frames, t_ptr);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

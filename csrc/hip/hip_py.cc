@@ -363,6 +363,14 @@ PYBIND11_MODULE(_hip, m) {
                           t_ptr ? P<const int64_t>(t_ptr) : nullptr, B, P<const void>(W1), w1s.data(), P<const void>(b1),
                           P<const void>(W2), w2s.data(), P<const void>(b2), P<void>(h2), S(stream));
   });
+  m.def("nature_trunk_fwd_push_rows", [](uint64_t rows, int64_t T, uint64_t nf, uint64_t t_ptr, int64_t B, uint64_t W1,
+                                         std::vector<int64_t> w1s, uint64_t b1, uint64_t W2, std::vector<int64_t> w2s,
+                                         uint64_t b2, uint64_t h2, uint64_t stream) {
+    if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("nature_trunk_fwd_push_rows: 4 strides per weight");
+    nature_trunk_fwd_push_rows(P<uint8_t>(rows), T, P<const uint8_t>(nf), P<const int64_t>(t_ptr), B, P<const void>(W1),
+                               w1s.data(), P<const void>(b1), P<const void>(W2), w2s.data(), P<const void>(b2), P<void>(h2),
+                               S(stream));
+  });
   m.def("nature_trunk_partial_floats", &nature_trunk_partial_floats);
   m.def("dense_relu_fwd", [](uint64_t x, uint64_t w, uint64_t b, int64_t M, int64_t K, int N, uint64_t y,
                              uint64_t stream) {

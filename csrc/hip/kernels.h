@@ -162,6 +162,11 @@ void nature_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
 void nature_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
                            const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
                            const void* b2, void* h2, hipStream_t stream);
+// K10 rollout band mode: each frame split over 4 workgroups (conv2 row bands); the frame stack is
+// rollout row (t-1) mod T planes 1..3 + new_frames[b]; writes rollout row t ([T, B, 4, 84, 84] u8) and h2.
+void nature_trunk_fwd_push_rows(uint8_t* rows, int64_t T, const uint8_t* new_frames, const int64_t* t_ptr, int64_t B,
+                                const void* W1, const int64_t* w1s, const void* b1, const void* W2, const int64_t* w2s,
+                                const void* b2, void* h2, hipStream_t stream);
 int nature_trunk_bwd_groups(int64_t B);
 int64_t nature_trunk_partial_floats(int64_t B);
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,

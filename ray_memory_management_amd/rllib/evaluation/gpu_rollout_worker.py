@@ -136,13 +136,18 @@ class _EnvGroup:
         # device frame stacks (K19): upload only each env's newest frame, shift the stack in HBM
         self.device_stack = (bool(getattr(env, "frame_stack_continuous", False)) and hasattr(env, "vector_step_frames")
                              and obs.ndim == 4 and obs.shape[1] == 4 and (obs.shape[2] * obs.shape[3]) % 16 == 0)
+        # K10 band mode (rollout): each frame split over 4 workgroups; the frame stack of step t is
+        # rollout row t-1 (mod T), so no separate stack buffer is kept (RMM_NO_BAND_PUSH=1: stack mode)
+        self.band = (self.device_stack and self.fused and not os.environ.get("RMM_NO_BAND_PUSH")
+                     and os.environ.get("RMM_NO_FOLD_PUSH") is None
+                     and bool(getattr(model, "fused_trunk_ok", lambda o: False)(self.s_obs)))
         if self.device_stack:
             self.hw = obs.shape[2] * obs.shape[3]
             self.h_new = torch.empty((n,) + obs.shape[2:], dtype=torch.uint8).pin_memory()
             self.s_new = torch.empty((n,) + obs.shape[2:], dtype=torch.uint8, device=dev)
             # stack state such that the first push yields the reset observation
             init = torch.from_numpy(np.ascontiguousarray(obs))
-            self.s_obs[:, 1:].copy_(init[:, :3].to(dev))
+            (self.buf_obs[T - 1] if self.band else self.s_obs)[:, 1:].copy_(init[:, :3].to(dev))
             self.h_new.copy_(init[:, 3])
             # K19 reads the newest frames straight from pinned host memory (zero-copy over the host
             # link) when the pinned buffer is device-mapped: no separate H2D blit per step
@@ -202,7 +207,9 @@ class _EnvGroup:
             if not src:
                 self.s_new.copy_(self.h_new, non_blocking=True)
                 src = self.s_new.data_ptr()
-            if self.fused and self.fold_push and self.model.fused_trunk_ok(self.s_obs):
+            if self.band:
+                push = (src, self.buf_obs, "rows")  # K10 reads row t-1 + new frames, stores row t
+            elif self.fused and self.fold_push and self.model.fused_trunk_ok(self.s_obs):
                 push = (src, self.buf_obs)  # K10 shifts the stack and stores row t itself
             else:
                 require_hip().frame_push(self.s_obs.data_ptr(), src, self.buf_obs.data_ptr(),
@@ -432,7 +439,8 @@ class HybridRolloutWorker(GPURolloutWorker):
                 for g in G:
                     if g.device_stack:  # observation after the last env step (pushed next fragment)
                         g.s_new.copy_(g.h_new, non_blocking=True)
-                        _, last_v = self.model(torch.cat([g.s_obs[:, 1:], g.s_new.unsqueeze(1)], dim=1))
+                        stack = g.buf_obs[T - 1] if g.band else g.s_obs  # the last step's frame stack
+                        _, last_v = self.model(torch.cat([stack[:, 1:], g.s_new.unsqueeze(1)], dim=1))
                     else:
                         g.s_obs.copy_(g.h_obs, non_blocking=True)
                         _, last_v = self.model(g.s_obs)

@@ -452,6 +452,8 @@ class VisionNetwork(nn.Module):
                 and layer.bias is not None and heads.bias is not None and layer.weight.is_contiguous()
                 and heads.weight.is_contiguous() and not os.environ.get("RMM_NO_K16")):
             if push is not None:
+                if len(push) == 3:
+                    raise RuntimeError("band-mode push needs the fused rollout step")
                 nf, rows = push
                 require_hip().frame_push(obs.data_ptr(), int(nf), rows.data_ptr() if rows is not None else 0,
                                          t_ptr.data_ptr(), B, obs.shape[2] * obs.shape[3],
@@ -461,8 +463,16 @@ class VisionNetwork(nn.Module):
         c1, c2 = self.convs[0], self.convs[1]
         hip = require_hip()
         stream = torch.cuda.current_stream(obs.device).cuda_stream
-        if push is not None:
-            nf, rows = push
+        if push is not None and len(push) == 3 and push[2] == "rows":
+            # band mode: 4 workgroups per frame; the frame stack is rollout row t-1 (mod T)
+            nf, rows, _ = push
+            h = torch.empty((B, 11 * 11 * 32), dtype=torch.bfloat16, device=obs.device)
+            hip.nature_trunk_fwd_push_rows(rows.data_ptr(), rows.shape[0], int(nf), t_ptr.data_ptr(), B,
+                                           c1.weight.data_ptr(), list(c1.weight.stride()), c1.bias.data_ptr(),
+                                           c2.weight.data_ptr(), list(c2.weight.stride()), c2.bias.data_ptr(),
+                                           h.data_ptr(), stream)
+        elif push is not None:
+            nf, rows = push[:2]
             h = torch.empty((B, 11 * 11 * 32), dtype=torch.bfloat16, device=obs.device)
             hip.nature_trunk_fwd_push(obs.data_ptr(), int(nf), rows.data_ptr() if rows is not None else 0,
                                       t_ptr.data_ptr(), B, c1.weight.data_ptr(), list(c1.weight.stride()),

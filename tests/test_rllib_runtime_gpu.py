@@ -362,3 +362,25 @@ def test_native_rollout_loop_matches_python_loop(cuda, double_buffer, monkeypatc
         for k in ("obs", "_raw", "_boot"):
             assert torch.equal(x[k], y[k]), k
     assert len(a._completed) > 0 and a._completed == b._completed
+
+
+def test_k10_band_push_matches_stack_push(cuda, monkeypatch):
+    """K10 rollout band mode (4 workgroups per frame, frame stack = rollout row t-1) yields the same
+    fragments, bit for bit, as the one-workgroup-per-frame push over a separate device frame stack."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 7}, "num_envs_per_worker": 9,
+           "rollout_fragment_length": 6, "seed": 5}
+    monkeypatch.delenv("RMM_NO_BAND_PUSH", raising=False)
+    a = HybridRolloutWorker(config=cfg)
+    fa = [a.sample() for _ in range(3)]
+    assert all(g.band for g in a.groups)
+    monkeypatch.setenv("RMM_NO_BAND_PUSH", "1")
+    b = HybridRolloutWorker(config=cfg)
+    fb = [b.sample() for _ in range(3)]
+    assert not any(g.band for g in b.groups)
+    for x, y in zip(fa, fb):
+        for k in ("obs", "_raw", "_boot"):
+            assert torch.equal(x[k], y[k]), k
