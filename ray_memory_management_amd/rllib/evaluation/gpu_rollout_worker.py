@@ -137,8 +137,9 @@ class _EnvGroup:
         self.device_stack = (bool(getattr(env, "frame_stack_continuous", False)) and hasattr(env, "vector_step_frames")
                              and obs.ndim == 4 and obs.shape[1] == 4 and (obs.shape[2] * obs.shape[3]) % 16 == 0)
         # K10 band mode (rollout): each frame split over 4 workgroups; the frame stack of step t is
-        # rollout row t-1 (mod T), so no separate stack buffer is kept (RMM_NO_BAND_PUSH=1: stack mode)
-        self.band = (self.device_stack and self.fused and not os.environ.get("RMM_NO_BAND_PUSH")
+        # rollout row t-1 (mod T), so no separate stack buffer is kept. Opt-in (RMM_BAND_PUSH=1) until
+        # measured on the GPU
+        self.band = (self.device_stack and self.fused and os.environ.get("RMM_BAND_PUSH") == "1"
                      and os.environ.get("RMM_NO_FOLD_PUSH") is None
                      and bool(getattr(model, "fused_trunk_ok", lambda o: False)(self.s_obs)))
         if self.device_stack:

@@ -373,11 +373,11 @@ def test_k10_band_push_matches_stack_push(cuda, monkeypatch):
 
     cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 7}, "num_envs_per_worker": 9,
            "rollout_fragment_length": 6, "seed": 5}
-    monkeypatch.delenv("RMM_NO_BAND_PUSH", raising=False)
+    monkeypatch.setenv("RMM_BAND_PUSH", "1")
     a = HybridRolloutWorker(config=cfg)
     fa = [a.sample() for _ in range(3)]
     assert all(g.band for g in a.groups)
-    monkeypatch.setenv("RMM_NO_BAND_PUSH", "1")
+    monkeypatch.setenv("RMM_BAND_PUSH", "0")
     b = HybridRolloutWorker(config=cfg)
     fb = [b.sample() for _ in range(3)]
     assert not any(g.band for g in b.groups)
