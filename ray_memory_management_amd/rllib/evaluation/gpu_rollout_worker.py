@@ -72,26 +72,6 @@ class GPURolloutWorker:
     def set_weights(self, weights, global_vars=None):
         import torch
 
-        if isinstance(weights, dict) and "__rmm_shared_bf16__" in weights:  # learner's live HBM weights
-            import ray_memory_management_amd as rt
-
-            ref = weights["__rmm_shared_bf16__"][0]
-            if getattr(self, "_shared_key", None) == ref.binary():
-                return  # already aliased: the learner updated them in place
-            flat = rt.get(ref)  # zero-copy (hipIPC) view of the learner's weights
-            params = dict(self.model.named_parameters())
-            with torch.no_grad():
-                if flat.device == self.device:  # same GPU: point the parameters at the learner's HBM
-                    for name, off, shape, stride in weights["__rmm_layout__"]:
-                        if name in params:
-                            params[name].data = flat.as_strided(shape, stride, off)
-                    self._shared_key, self._shared_flat = ref.binary(), flat
-                    self._on_params_rebound()
-                    return
-                for name, off, shape, stride in weights["__rmm_layout__"]:  # another GPU: copy
-                    if name in params:
-                        params[name].copy_(flat.to(self.device).as_strided(shape, stride, off))
-            return
         if isinstance(weights, dict) and "__rmm_flat_bf16__" in weights:  # learner's HBM weights object
             flat = weights["__rmm_flat_bf16__"]
             if flat.device != self.device:
@@ -110,10 +90,6 @@ class GPURolloutWorker:
 
     def get_weights(self, policies=None):
         return {k: v.detach().float().cpu().numpy() for k, v in self.model.state_dict().items()}
-
-    def _on_params_rebound(self):
-        """Parameters now live elsewhere: captured graphs hold the old pointers."""
-        self.sampler._graph = None
 
     def get_metrics(self) -> List[tuple]:
         out, self._completed = self._completed, []
@@ -555,12 +531,6 @@ class HybridRolloutWorker(GPURolloutWorker):
         super().set_weights(weights, global_vars)
         torch.cuda.synchronize(self.device)
         self._set_weights_time = getattr(self, "_set_weights_time", 0.0) + time.perf_counter() - t0
-
-    def _on_params_rebound(self):
-        """Parameters now alias the learner's HBM weights: recapture the policy-step graphs (and the
-        native loop's graph handles) at the next sample."""
-        self._captured = False
-        self._native_desc = None
 
     def timing(self):
         """Accumulated seconds in sample() and set_weights() (phase breakdown probes)."""

@@ -384,37 +384,3 @@ def test_k10_band_push_matches_stack_push(cuda, monkeypatch):
     for x, y in zip(fa, fb):
         for k in ("obs", "_raw", "_boot"):
             assert torch.equal(x[k], y[k]), k
-
-
-@pytest.mark.parametrize("shared", [True, False])
-def test_ppo_hybrid_shared_weights(cuda, shared, monkeypatch):
-    """Rollout workers alias the learner's live bf16 HBM weights (zero-copy, hipIPC, set once): right
-    after train() the worker already holds the just-updated weights. With RMM_NO_SHARED_WEIGHTS=1 the
-    worker holds the previous iteration's copy until the next iteration's set_weights."""
-    import ray_memory_management_amd as ray
-    from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
-
-    monkeypatch.setenv("RMM_NO_SHARED_WEIGHTS", "0" if shared else "1")
-    ray.init(num_cpus=4, num_gpus=1, object_store_memory=1 << 30)
-    try:
-        cfg = (PPOConfig().environment("SyntheticAtariVec-v0", env_config={"episode_len": 50})
-               .rollouts(num_rollout_workers=1, num_envs_per_worker=10, rollout_fragment_length=20,
-                         postprocess_on_learner=True)
-               .training(train_batch_size=200, sgd_minibatch_size=50, num_sgd_iter=2, lr=1e-3)
-               .resources(num_learner_workers=1, num_gpus_per_learner_worker=0.5, num_gpus_per_worker=0.5)
-               .debugging(seed=0))
-        algo = cfg.build()
-        for _ in range(3):
-            r = algo.train()
-        assert np.isfinite(r["info"]["learner"]["default_policy"]["learner_stats"]["total_loss"])
-        w0 = algo.workers.remote_workers()[0]
-        aliased = ray.get(w0.apply.remote(lambda x: getattr(x, "_shared_key", None) is not None))
-        assert aliased == shared
-        got = ray.get(w0.get_weights.remote())
-        master = algo.learner_group.get_weights()
-        same = all(np.array_equal(got[k], torch.from_numpy(np.ascontiguousarray(v)).to(torch.bfloat16).float().numpy())
-                   for k, v in master.items())
-        assert same == shared
-        algo.stop()
-    finally:
-        ray.shutdown()
