@@ -1,0 +1,155 @@
+// Multi-threaded stress test of the shared-memory object store, built only for the host race /
+// memory checkers (tests/test_native_sanitizers.py builds it with ThreadSanitizer and with
+// AddressSanitizer + UBSan). Every thread shares ONE Store mapping so the race checker sees
+// every access to the segment at one address.
+//
+// Parity: the reference exercises plasma concurrency through
+// src/ray/object_manager/plasma/test/ and python/ray/tests/test_object_spilling*.py
+// (concurrent create / get / delete while spilling and restoring); this drives the same
+// lifecycle paths of csrc/store/shm_store.cc directly: create -> seal -> get/release -> delete,
+// proactive and explicit spilling, restore-on-get, sealed-notification polling, batched wait.
+//
+// usage: store_stress <spill_dir> [threads] [iters]
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+#include <unistd.h>
+
+#include "../store/shm_store.h"
+
+using rmm::ObjectId;
+using rmm::Store;
+
+namespace {
+
+constexpr int kKeys = 384;
+
+ObjectId Id(int key) {
+  ObjectId id{};
+  std::memcpy(id.b, &key, sizeof(key));
+  id.b[19] = 0x5a;
+  return id;
+}
+
+uint8_t Pat(int key, uint64_t i) { return static_cast<uint8_t>(key * 131 + i * 7); }
+
+std::atomic<long> g_bad{0};
+std::atomic<long> g_ops[8];
+
+void Worker(Store* s, int tid, int iters) {
+  std::mt19937_64 rng(1234 + tid);
+  uint64_t cursor = 0;
+  for (int it = 0; it < iters; it++) {
+    int key = static_cast<int>(rng() % kKeys);
+    ObjectId id = Id(key);
+    int r = static_cast<int>(rng() % 100);
+    if (r < 30) {
+      uint64_t n = 64 + rng() % (key % 4 == 0 ? (512u << 10) : (16u << 10));
+      bool exists = false;
+      uint8_t* p = nullptr;
+      try {
+        p = s->CreateObject(id, n, 0, 0, 0, &exists);
+      } catch (const std::runtime_error&) {
+        g_ops[7]++;  // out of memory even after spilling: legal under this pressure
+        continue;
+      }
+      if (!p || exists) continue;
+      for (uint64_t i = 0; i < n; i++) p[i] = Pat(key, i);
+      s->Seal(id);
+      s->Release(id);  // creator's pin (plasma semantics: the creator releases after seal)
+      g_ops[0]++;
+    } else if (r < 62) {
+      Store::View v;
+      bool got = false;
+      try {
+        got = s->Get(id, 0, &v);
+      } catch (const std::runtime_error&) {
+        g_ops[7]++;  // restore of a spilled object found no room: legal under this pressure
+      }
+      if (got) {
+        // sealed payloads never change while pinned (spill keeps the heap copy readable,
+        // restore rewrites the bytes before the object is visible again)
+        uint64_t n = v.data_size;
+        if (n && (v.data[0] != Pat(key, 0) || v.data[n - 1] != Pat(key, n - 1) ||
+                  v.data[n / 2] != Pat(key, n / 2)))
+          g_bad++;
+        s->Release(id);
+        g_ops[1]++;
+      }
+    } else if (r < 76) {
+      s->Delete(id);
+      g_ops[2]++;
+    } else if (r < 82) {
+      (void)s->Contains(id);
+      (void)s->State(id);
+    } else if (r < 88) {
+      std::vector<ObjectId> ids;
+      for (int k = 0; k < 4; k++) ids.push_back(Id(static_cast<int>(rng() % kKeys)));
+      std::vector<uint8_t> ready;
+      s->Wait(ids, 4, 0, &ready);
+      (void)s->Sizes(ids);
+      g_ops[3]++;
+    } else if (r < 91) {
+      s->SpillBytes(1u << 20);
+      g_ops[4]++;
+    } else if (r < 96) {
+      std::vector<ObjectId> out;
+      bool overflow = false;
+      cursor = s->PollSealed(cursor, &out, &overflow);
+      g_ops[5]++;
+    } else {
+      (void)s->GetStats();
+      (void)s->ListObjects();
+      g_ops[6]++;
+    }
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s <spill_dir> [threads] [iters]\n", argv[0]);
+    return 2;
+  }
+  int threads = argc > 2 ? std::atoi(argv[2]) : 6;
+  int iters = argc > 3 ? std::atoi(argv[3]) : 4000;
+  std::string name = "/rmm_stress_" + std::to_string(getpid());
+  // 24 MiB arena against up to ~100 x 512 KiB live objects: creates spill, gets restore
+  Store* s = Store::Create(name, 24ull << 20, argv[1], 0.8, 1u << 20, /*fallback=*/false,
+                           /*oom_grace_s=*/0.05);
+  std::atomic<bool> stop{false};
+  std::thread waiter([&] {
+    uint64_t seq = s->SealSeq();
+    while (!stop.load()) seq = s->WaitSealSeq(seq, 5);
+  });
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; t++) ts.emplace_back(Worker, s, t, iters);
+  for (auto& t : ts) t.join();
+  stop = true;
+  s->Wake();
+  waiter.join();
+
+  uint64_t free_before = s->CheckHeap();
+  for (int k = 0; k < kKeys; k++) s->Delete(Id(k));
+  uint64_t free_after = s->CheckHeap();
+  rmm::Stats st = s->GetStats();
+  std::printf("ops create=%ld get=%ld delete=%ld wait=%ld spill=%ld poll=%ld stats=%ld oom=%ld\n",
+              g_ops[0].load(), g_ops[1].load(), g_ops[2].load(), g_ops[3].load(), g_ops[4].load(),
+              g_ops[5].load(), g_ops[6].load(), g_ops[7].load());
+  std::printf("spilled=%lu restored=%lu free_before=%lu free_after=%lu in_use=%lu objects=%lu bad=%ld\n",
+              (unsigned long)st.objects_spilled_total, (unsigned long)st.objects_restored_total,
+              (unsigned long)free_before, (unsigned long)free_after, (unsigned long)st.bytes_in_use,
+              (unsigned long)st.num_objects, g_bad.load());
+  bool ok = g_bad.load() == 0 && st.num_objects == 0 && st.bytes_in_use == 0 && g_ops[0] > 0 &&
+            g_ops[1] > 0;
+  delete s;
+  std::printf(ok ? "STRESS OK\n" : "STRESS FAILED\n");
+  return ok ? 0 : 1;
+}
