@@ -15,6 +15,9 @@
 // Small-A categorical heads (A <= 32): one thread per sample, logits held in registers.
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -302,10 +305,12 @@ __device__ __forceinline__ uint32_t bf16x2_rn(float a, float b) {
   return lo | (hi << 16);
 }
 
-// Each thread updates 4 consecutive elements with 16-B fp32 and 8-B bf16 accesses (the step is
-// HBM-bound: 28 B/param); the n % 4 tail is done by the first threads of the grid. Requires the
-// host-checked alignment of every pointer (adam_flat falls back to vec=false otherwise).
-template <typename TG, bool VEC>
+// Each thread updates U groups of 4 consecutive elements with 16-B fp32 and 8-B bf16 accesses (the
+// step is HBM / Infinity-Cache bound: 28 B/param), issuing every group's loads before the first
+// update so U x 4 vector loads are in flight per lane; the n % 4 tail is done by the first threads
+// of the grid. Requires the host-checked alignment of every pointer (adam_flat falls back to
+// vec=false otherwise).
+template <typename TG, bool VEC, int U>
 __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, float* __restrict__ m1,
                                                   float* __restrict__ m2, const TG* __restrict__ grad,
                                                   __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
@@ -320,21 +325,36 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
   int64_t scalar_from = 0;
   if constexpr (VEC) {
     const int64_t nv = n >> 2;
-    for (int64_t v = tid; v < nv; v += nthr) {
-      const int64_t i = v << 2;
-      float g[4];
-      adam_load4(grad, i, g);
-      float4 w = *reinterpret_cast<const float4*>(master + i);
-      float4 a = *reinterpret_cast<const float4*>(m1 + i);
-      float4 b = *reinterpret_cast<const float4*>(m2 + i);
-      w.x = adam_one(w.x, g[0] * grad_scale, a.x, b.x, c);
-      w.y = adam_one(w.y, g[1] * grad_scale, a.y, b.y, c);
-      w.z = adam_one(w.z, g[2] * grad_scale, a.z, b.z, c);
-      w.w = adam_one(w.w, g[3] * grad_scale, a.w, b.w, c);
-      *reinterpret_cast<float4*>(master + i) = w;
-      *reinterpret_cast<float4*>(m1 + i) = a;
-      *reinterpret_cast<float4*>(m2 + i) = b;
-      if (wbf16) *reinterpret_cast<uint2*>(wbf16 + i) = make_uint2(bf16x2_rn(w.x, w.y), bf16x2_rn(w.z, w.w));
+    for (int64_t v0 = tid; v0 < nv; v0 += nthr * U) {
+      float g[U][4];
+      float4 w[U], a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t v = v0 + u * nthr;
+        if (v < nv) {
+          const int64_t i = v << 2;
+          adam_load4(grad, i, g[u]);
+          w[u] = *reinterpret_cast<const float4*>(master + i);
+          a[u] = *reinterpret_cast<const float4*>(m1 + i);
+          b[u] = *reinterpret_cast<const float4*>(m2 + i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t v = v0 + u * nthr;
+        if (v < nv) {
+          const int64_t i = v << 2;
+          w[u].x = adam_one(w[u].x, g[u][0] * grad_scale, a[u].x, b[u].x, c);
+          w[u].y = adam_one(w[u].y, g[u][1] * grad_scale, a[u].y, b[u].y, c);
+          w[u].z = adam_one(w[u].z, g[u][2] * grad_scale, a[u].z, b[u].z, c);
+          w[u].w = adam_one(w[u].w, g[u][3] * grad_scale, a[u].w, b[u].w, c);
+          *reinterpret_cast<float4*>(master + i) = w[u];
+          *reinterpret_cast<float4*>(m1 + i) = a[u];
+          *reinterpret_cast<float4*>(m2 + i) = b[u];
+          if (wbf16)
+            *reinterpret_cast<uint2*>(wbf16 + i) = make_uint2(bf16x2_rn(w[u].x, w[u].y), bf16x2_rn(w[u].z, w[u].w));
+        }
+      }
     }
     scalar_from = nv << 2;
   }
@@ -358,7 +378,17 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
   auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
   const bool vec = al(master, 16) && al(m1, 16) && al(m2, 16) && al(grad, grad_bf16 ? 8 : 16) &&
                    (wbf16 == nullptr || al(wbf16, 8));
-  const int64_t work = vec ? (n + 3) / 4 : n;
+  // groups of 4 per lane per loop trip (vector path), RMM_ADAM_UNROLL=1/2/4, read once. Default 2:
+  // 7.8-8.0 us vs 8.8 us per launch at 1M params with U=1 on MI355X (benchmarks/bench_adam.py,
+  // profiles/adam_unroll_r3.txt: half the workgroups, two groups of loads in flight per lane);
+  // the per-element math is unchanged, so every U gives bit-identical results
+  static const int unroll = [] {
+    const char* e = getenv("RMM_ADAM_UNROLL");
+    const int u = e ? atoi(e) : 2;
+    return u == 1 || u == 4 ? u : 2;
+  }();
+  const int u = vec ? unroll : 1;
+  const int64_t work = vec ? ((n + 3) / 4 + u - 1) / u : n;
   // max_blocks > 0 caps the grid (an Adam that runs BESIDE another kernel takes few wave slots)
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, max_blocks > 0 ? max_blocks : 256 * 8));
   auto go = [&](auto kern, const auto* g) {
@@ -366,12 +396,17 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
                        static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n, step_ctr, bump, nbump, done,
                        scale_ptr);
   };
-  const auto* gb = static_cast<const __hip_bfloat16*>(grad);
-  const auto* gf = static_cast<const float*>(grad);
+  auto dispatch = [&](const auto* g) {
+    using TG = std::remove_const_t<std::remove_pointer_t<decltype(g)>>;
+    if (!vec) go(k_adam_flat<TG, false, 1>, g);
+    else if (u == 4) go(k_adam_flat<TG, true, 4>, g);
+    else if (u == 2) go(k_adam_flat<TG, true, 2>, g);
+    else go(k_adam_flat<TG, true, 1>, g);
+  };
   if (grad_bf16)
-    vec ? go(k_adam_flat<__hip_bfloat16, true>, gb) : go(k_adam_flat<__hip_bfloat16, false>, gb);
+    dispatch(static_cast<const __hip_bfloat16*>(grad));
   else
-    vec ? go(k_adam_flat<float, true>, gf) : go(k_adam_flat<float, false>, gf);
+    dispatch(static_cast<const float*>(grad));
   RMM_HIP_CHECK(hipGetLastError());
 }
 
