@@ -47,16 +47,22 @@ def main():
     ctr = torch.zeros(2, dtype=torch.int64, device=dev)
     done = torch.zeros(h.bump_done_words(), dtype=torch.int32, device=dev)
 
-    def adam(nn=n, mb=0):
+    def adam(nn=n, mb=0, bump=True):
         st = torch.cuda.current_stream().cuda_stream
         h.adam_flat(master.data_ptr(), m1.data_ptr(), m2.data_ptr(), grad.data_ptr(), True, wbf.data_ptr(),
-                    hp.data_ptr(), 1.0, nn, st, step_ctr=ctr.data_ptr() + 8, bump=ctr.data_ptr(), nbump=2,
-                    done=done.data_ptr(), max_blocks=mb)
+                    hp.data_ptr(), 1.0, nn, st, step_ctr=ctr.data_ptr() + 8, bump=ctr.data_ptr() if bump else 0,
+                    nbump=2 if bump else 0, done=done.data_ptr() if bump else 0, max_blocks=mb)
 
     out = {"n_params": n, "bytes_per_launch": 28 * n}
     for mb in (0, 256, 512, 1024, 2048):
         out[f"adam_us_maxblocks{mb}"] = round(_time_graph(lambda mb=mb: adam(mb=mb)), 2)
     out["adam_us_n256"] = round(_time_graph(lambda: adam(nn=256)), 2)
+    # the step-counter bump of the last workgroup (two relaxed agent-scope tickets) vs none
+    out["adam_us_nobump"] = round(_time_graph(lambda: adam(bump=False)), 2)
+    out["adam_us_n256_nobump"] = round(_time_graph(lambda: adam(nn=256, bump=False)), 2)
+    src1 = torch.empty(256, dtype=torch.uint8, device=dev)
+    dst1 = torch.empty_like(src1)
+    out["copy_us_256B"] = round(_time_graph(lambda: dst1.copy_(src1)), 2)
     src = torch.empty(14 * n, dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
     out["copy_us_same_bytes"] = round(_time_graph(lambda: dst.copy_(src)), 2)
