@@ -212,15 +212,16 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("adam_flat", [](uint64_t master, uint64_t m1, uint64_t m2, uint64_t grad, bool grad_bf16, uint64_t wbf16,
                         uint64_t hp, float grad_scale, int64_t n, uint64_t stream, uint64_t step_ctr, uint64_t bump,
-                        int nbump, uint64_t done, uint64_t scale_ptr, int max_blocks) {
+                        int nbump, uint64_t done, uint64_t scale_ptr, int max_blocks, uint64_t bump_next) {
     adam_flat(P<float>(master), P<float>(m1), P<float>(m2), P<const void>(grad), grad_bf16,
               wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream),
               step_ctr ? P<const int64_t>(step_ctr) : nullptr, bump ? P<int64_t>(bump) : nullptr, nbump,
-              done ? P<uint32_t>(done) : nullptr, scale_ptr ? P<const float>(scale_ptr) : nullptr, max_blocks);
+              done ? P<uint32_t>(done) : nullptr, scale_ptr ? P<const float>(scale_ptr) : nullptr, max_blocks,
+              bump_next ? P<int64_t>(bump_next) : nullptr);
   }, py::arg("master"), py::arg("m1"), py::arg("m2"), py::arg("grad"), py::arg("grad_bf16"), py::arg("wbf16"),
      py::arg("hp"), py::arg("grad_scale"), py::arg("n"), py::arg("stream"), py::arg("step_ctr") = 0,
      py::arg("bump") = 0, py::arg("nbump") = 0, py::arg("done") = 0, py::arg("scale_ptr") = 0,
-     py::arg("max_blocks") = 0);
+     py::arg("max_blocks") = 0, py::arg("bump_next") = 0);
   m.def("grad_clip_workspace_floats", &grad_clip_workspace_floats);
   m.def("ingest_gae", [](uint64_t raw, uint64_t boot, uint64_t blocks, int nblocks, int A, float gamma, float lam,
                          uint64_t cols, uint64_t stats, uint64_t stream) {

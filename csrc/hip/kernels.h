@@ -66,7 +66,8 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
 // K6: flat Adam/AdamW with fp32 master weights, bf16 or fp32 grads, optional bf16 weight output.
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr = nullptr,
-               int64_t* bump = nullptr, int nbump = 0, uint32_t* done = nullptr, const float* scale_ptr = nullptr, int max_blocks = 0);
+               int64_t* bump = nullptr, int nbump = 0, uint32_t* done = nullptr, const float* scale_ptr = nullptr, int max_blocks = 0,
+               int64_t* bump_next = nullptr);
 // K6b: out[0] = min(1, max_norm / ||grad*grad_scale||), out[1] = the norm (device; feeds K6 scale_ptr).
 // workspace: grad_clip_workspace_floats() floats, zero-initialised once (its ticket resets itself).
 int64_t grad_clip_workspace_floats();

@@ -16,6 +16,7 @@
 #include <hip/hip_bf16.h>
 
 #include <cstdlib>
+#include <stdexcept>
 #include <type_traits>
 
 #include "common.h"
@@ -316,11 +317,20 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
                                                   __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
                                                   float grad_scale, int64_t n, const int64_t* __restrict__ step_ctr,
                                                   int64_t* bump, int nbump, uint32_t* done,
-                                                  const float* __restrict__ scale_ptr) {
+                                                  const float* __restrict__ scale_ptr, int64_t* bump_next) {
   // step: hp[5], or (device step counter + 1) when the counter is given (graph-friendly)
   // scale_ptr (optional): a device-side factor, e.g. the global-norm clip coefficient of K6b
   if (scale_ptr) grad_scale *= scale_ptr[0];
   const AdamCoef c = adam_coef(hp, step_ctr);
+  if (bump_next) {
+    // parity counters: this step's kernels read `bump`, the next step's read `bump_next`, so one lane
+    // writes the advanced values straight away — no ticket, nothing waits for the other workgroups
+    // (every reader of `bump_next` runs after this kernel's boundary; `bump` is rewritten only by
+    // the following step's K6, after every reader of this step has finished)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      for (int k = 0; k < nbump; k++) bump_next[k] = bump[k] + 1;
+    bump = nullptr;
+  }
   const int64_t tid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, nthr = int64_t(gridDim.x) * blockDim.x;
   int64_t scalar_from = 0;
   if constexpr (VEC) {
@@ -373,8 +383,9 @@ int bump_done_words() { return kBumpWords; }
 
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr, int64_t* bump, int nbump,
-               uint32_t* done, const float* scale_ptr, int max_blocks) {
+               uint32_t* done, const float* scale_ptr, int max_blocks, int64_t* bump_next) {
   if (n <= 0) return;
+  if (bump_next && (!bump || nbump <= 0)) throw std::invalid_argument("adam_flat: bump_next needs bump / nbump");
   auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
   const bool vec = al(master, 16) && al(m1, 16) && al(m2, 16) && al(grad, grad_bf16 ? 8 : 16) &&
                    (wbf16 == nullptr || al(wbf16, 8));
@@ -394,7 +405,7 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
   auto go = [&](auto kern, const auto* g) {
     hipLaunchKernelGGL(kern, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2, g,
                        static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n, step_ctr, bump, nbump, done,
-                       scale_ptr);
+                       scale_ptr, bump_next);
   };
   auto dispatch = [&](const auto* g) {
     using TG = std::remove_const_t<std::remove_pointer_t<decltype(g)>>;

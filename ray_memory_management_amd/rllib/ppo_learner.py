@@ -250,7 +250,15 @@ class PPOLearner:
         # device counters {minibatch step within the update, Adam step}: the SGD-step graph reads
         # its minibatch indices at idx_all[ctr[0]] and the Adam bias correction from ctr[1]; one
         # add per step advances both, so no host→device copy happens between graph replays.
-        self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        # Two copies (parity pair): inside a chained SGD graph step k reads copy k % 2 and its K6 writes
+        # the advanced counters into the other copy from one lane (no last-workgroup ticket on the
+        # critical path, 1.4 us per step on MI355X, profiles/adam_unroll_r3.txt); the chain's last
+        # step leaves them in copy 0 (`self.ctr`), which everything outside the chain uses.
+        self._ctrs = torch.zeros(2, 2, dtype=torch.int64, device=dev)
+        self.ctr = self._ctrs[0]
+        self._par = 0            # copy the next launched step reads
+        self._parity = False     # set while capturing a chained graph
+        self._parity_last = False
         self._bump_done = torch.zeros(require_hip().bump_done_words(), dtype=torch.int32, device=dev)
         self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.heads_ok = hasattr(self.model, "forward_heads")
@@ -326,7 +334,7 @@ class PPOLearner:
         h = require_hip()
         m = self.model
         c1, c2, dl, hd = m.convs[0], m.convs[1], m.dense_tail, m.heads
-        mbs, period, idx, ctr = full["mbs"], full["period"], full["idx"], self.ctr
+        mbs, period, idx, ctr = full["mbs"], full["period"], full["idx"], self._ctr()
         ws = self._manual_ws(mbs)
         st = _stream()
         K, A1 = dl.in_features, hd.out_features
@@ -357,7 +365,7 @@ class PPOLearner:
         c1, c2 = self.model.convs[0], self.model.convs[1]
         ws = self._manual_ws(full["mbs"])
         g = [p._rmm_grad_out for p in self.params]
-        h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), self.ctr.data_ptr(), int(full["period"]),
+        h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), self._ctr().data_ptr(), int(full["period"]),
                            int(full["mbs"]), c2.weight.data_ptr(), list(c2.weight.stride()), ws["h1"].data_ptr(),
                            ws["h2"].data_ptr(), ws["dx"].data_ptr(), ws["part"].data_ptr(), g[0].data_ptr(),
                            list(c1.weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
@@ -392,10 +400,17 @@ class PPOLearner:
                              float(self.cfg["grad_clip"]), self.clip_ws.data_ptr(), self.clip_out.data_ptr(),
                              _stream())
             scale_ptr = self.clip_out.data_ptr()
-        h.adam_flat(self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
-                    self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream(),
-                    step_ctr=self.ctr.data_ptr() + 8, bump=self.ctr.data_ptr(), nbump=2,
-                    done=self._bump_done.data_ptr(), scale_ptr=scale_ptr)
+        cur = self._ctr()
+        args = (self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
+                self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream())
+        if self._parity and not (self._parity_last and self._par == 0):
+            # chained graph: advance into the other copy from one lane (see __init__)
+            h.adam_flat(*args, step_ctr=cur.data_ptr() + 8, bump=cur.data_ptr(), nbump=2, scale_ptr=scale_ptr,
+                        bump_next=self._ctrs[1 - self._par].data_ptr())
+            self._par ^= 1
+        else:  # in place: the last workgroup advances the counters after every workgroup read them
+            h.adam_flat(*args, step_ctr=cur.data_ptr() + 8, bump=cur.data_ptr(), nbump=2,
+                        done=self._bump_done.data_ptr(), scale_ptr=scale_ptr)
 
     def _adam_range(self, lo: int, hi: int, stream: int, bump: bool, max_blocks: int = 0):
         """K6 over params [lo, hi) of the flat buckets on `stream`; `bump` advances the device
@@ -437,6 +452,10 @@ class PPOLearner:
             s = self._side = torch.cuda.Stream(self.device)
         return s
 
+    def _ctr(self):
+        """The device counter copy the step being launched / captured reads."""
+        return self._ctrs[self._par]
+
     def _opt_step(self):
         if self.world > 1:
             self.comm.allreduce(self.flat_grad)
@@ -445,7 +464,7 @@ class PPOLearner:
     def _fast_step(self, full, with_opt: bool):
         h = require_hip()
         mbs, period = full["mbs"], full["period"]
-        ctr = self.ctr
+        ctr = self._ctr()
         # K2b: minibatch gather + u8→bf16 NHWC; K2: ONE gather for every per-sample column —
         # both index idx_all at the device step counter
         frames = full["obs"].dtype == torch.uint8 and full["obs"].dim() == 4
@@ -582,20 +601,30 @@ class PPOLearner:
             # step's minibatch and Adam step) — consecutive replays of a one-step graph leave ~8 µs
             # idle between them on MI355X (profiles/sgd_chain_r3.txt), a chained graph none
             chain = self._sgd_chain(int(full["period"])) if self.world == 1 else 1
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(chain):
-                    if manual:
-                        self._manual_fwd_dense_bwd(full)
-                        if self.world > 1:
-                            self.comm.allreduce(self.flat_grad[self._manual:])
-                        self._manual_trunk_bwd(full)
-                        if self.world > 1:
-                            self.comm.allreduce(self.flat_grad[:self._manual])
-                        if not self._fused_adam():
-                            self._opt_launch()
-                    else:
-                        self._fast_step(full, True)
+            self._parity = (manual and chain > 1 and not self._fused_adam()
+                            and os.environ.get("RMM_CTR_PARITY", "0") == "1")
+            self._par = 0
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for k in range(chain):
+                        self._parity_last = k == chain - 1
+                        if manual:
+                            self._manual_fwd_dense_bwd(full)
+                            if self.world > 1:
+                                self.comm.allreduce(self.flat_grad[self._manual:])
+                            self._manual_trunk_bwd(full)
+                            if self.world > 1:
+                                self.comm.allreduce(self.flat_grad[:self._manual])
+                            if not self._fused_adam():
+                                self._opt_launch()
+                        else:
+                            self._fast_step(full, True)
+            finally:
+                par, self._par = self._par, 0
+                self._parity = self._parity_last = False
+            if par != 0:
+                raise RuntimeError("chained SGD graph must leave the step counters in copy 0")
             self._graph = g
             self._chain = chain
         elif manual and _comm_overlap():
