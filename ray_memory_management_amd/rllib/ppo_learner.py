@@ -602,7 +602,7 @@ class PPOLearner:
             # idle between them on MI355X (profiles/sgd_chain_r3.txt), a chained graph none
             chain = self._sgd_chain(int(full["period"])) if self.world == 1 else 1
             self._parity = (manual and chain > 1 and not self._fused_adam()
-                            and os.environ.get("RMM_CTR_PARITY", "0") == "1")
+                            and os.environ.get("RMM_CTR_PARITY", "1") != "0")
             self._par = 0
             try:
                 g = torch.cuda.CUDAGraph()
