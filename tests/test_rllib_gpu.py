@@ -577,3 +577,4 @@ print(json.dumps({{"ct": ct.tolist(), "act": act.tolist(), "logp": logp.tolist()
     assert a["act"] == b["act"] and a["logp"] == b["logp"]
     assert a["act"][0] == [0] * B and any(a["act"][1]) and any(a["act"][2])
     assert a["done"] == 0 and b["done"] == 0
+
