@@ -10,6 +10,7 @@
 #include "common.h"
 #include "gpu_store.h"
 #include "kernels.h"
+#include "peer_allreduce.h"
 #include "rccl_comm.h"
 #include "rollout_loop.h"
 
@@ -574,6 +575,28 @@ PYBIND11_MODULE(_hip, m) {
     if (!ptr) throw std::runtime_error("GPU object not found");
     return make_dlpack(ptr, std::move(shape), code, bits, s->device(), s, sid, py::none());
   });
+
+  // ---------------------------------------------------------------- peer-memory all-reduce (xGMI / hipIPC)
+  py::class_<PeerAllReduce, std::shared_ptr<PeerAllReduce>>(m, "PeerAllReduce")
+      .def(py::init<int, int, int, uint64_t, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("cap_bytes") = 8ull << 20, py::arg("nblocks") = 64, py::arg("timeout_s") = 30.0)
+      .def("handles", [](const PeerAllReduce& c) { return py::bytes(c.Handles()); })
+      .def("open", [](PeerAllReduce& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (const auto& h : hs) v.emplace_back(std::string(h));
+        c.Open(v);
+      })
+      .def("all_reduce", &PeerAllReduce::AllReduce, py::arg("buf"), py::arg("count"), py::arg("dtype"),
+           py::arg("stream"), py::arg("algo") = 0)
+      .def("error", &PeerAllReduce::Error)
+      .def("clear_error", &PeerAllReduce::ClearError)
+      .def("close", &PeerAllReduce::Close)
+      .def_property_readonly("launches", &PeerAllReduce::launches)
+      .def_property_readonly("world", &PeerAllReduce::world)
+      .def_property_readonly("rank", &PeerAllReduce::rank)
+      .def_property_readonly("nblocks", &PeerAllReduce::nblocks)
+      .def_property_readonly("cap_bytes", &PeerAllReduce::cap_bytes)
+      .def_property_readonly("uncached_signals", &PeerAllReduce::uncached_signals);
 
   // ---------------------------------------------------------------- RCCL (framework-owned communicator)
   m.def("rccl_load", &rccl_load, py::arg("path"));

@@ -15,6 +15,7 @@ the dense-bucket all-reduce behind the trunk backward).
 from __future__ import annotations
 
 import os
+import time
 from typing import Optional
 
 import torch
@@ -220,6 +221,140 @@ class RcclComm(Comm):
             self._c.destroy()
         except Exception:
             self._c.abort()
+
+
+_PEER_DT = {torch.bfloat16: 0, torch.float32: 1}
+
+
+class PeerUnavailable(RuntimeError):
+    """Some rank could not export or map the peer regions (e.g. no IPC / peer access)."""
+
+
+def _store_barrier(store, key: str, world: int, timeout_s: float = 300.0) -> None:
+    store.add(key, 1)
+    t0 = time.monotonic()
+    while int(store.add(key, 0)) < world:
+        if time.monotonic() - t0 > timeout_s:
+            raise TimeoutError(f"store barrier {key}: {int(store.add(key, 0))}/{world} ranks arrived")
+        time.sleep(0.002)
+
+
+class PeerComm(Comm):
+    """MI355X-native intra-node all-reduce (csrc/hip/peer_allreduce.hip): every rank exports a
+    staging region once through hipIPC and maps every peer's; one kernel per all-reduce reads the
+    peers' slices over xGMI, sums them in fp32 in rank order and rounds once, with per-workgroup
+    flag barriers (bounded spins that report a dead peer instead of hanging). No host involvement
+    per call, so the collective lives INSIDE the learner's chained SGD graph (``in_graph``).
+
+    bf16 / fp32 sums natively; `broadcast` of a float tensor is an all-reduce against zeros from
+    the other ranks (exact); anything else goes to `fallback` (an RcclComm or a torch group) when
+    one is given. Reference parity: rllib/execution/multi_gpu_learner_thread.py:20 (tower gradient
+    averaging), rllib/execution/train_ops.py:98."""
+
+    graph_capturable = True
+    in_graph = True
+
+    def __init__(self, store, rank: int, world: int, key: str = "rmm-peer", device=None,
+                 cap_bytes: int = 8 << 20, nblocks: int = 0, timeout_s: float = 0.0, fallback: Optional[Comm] = None):
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.world, self.rank = int(world), int(rank)
+        timeout_s = timeout_s or float(os.environ.get("RMM_PEER_TIMEOUT_S", "60"))
+        # one workgroup per CU would saturate the links long before the payload does; 64 keeps the
+        # barrier fan-in small (64 x W flags) and still leaves most of the chip to the trunk kernels
+        nblocks = nblocks or int(os.environ.get("RMM_PEER_BLOCKS", "64"))
+        # every rank reaches every store key even when its own setup fails, so the ranks agree on
+        # the outcome (all PeerComm, or all raise PeerUnavailable and fall back) instead of hanging
+        err, blob, self._c = None, b"", None
+        try:
+            self._c = h.PeerAllReduce(self.rank, self.world, self.device.index, int(cap_bytes), int(nblocks),
+                                      float(timeout_s))
+            blob = self._c.handles()
+        except Exception as e:  # noqa: BLE001
+            err = e
+        store.set(f"{key}/h{self.rank}", blob)
+        hs = [store.get(f"{key}/h{r}") for r in range(self.world)]
+        ok = err is None and all(len(b) > 0 for b in hs)
+        if ok:
+            try:
+                self._c.open(hs)
+            except Exception as e:  # noqa: BLE001
+                err, ok = e, False
+        store.set(f"{key}/ok{self.rank}", b"1" if ok else b"0")
+        bad = [r for r in range(self.world) if store.get(f"{key}/ok{r}") != b"1"]
+        if bad:
+            if self._c is not None:
+                self._c.close()
+            raise PeerUnavailable(f"peer all-reduce unavailable (ranks {bad} failed; here: {err!r})")
+        # nobody launches before every rank mapped every region
+        _store_barrier(store, f"{key}/ready", self.world)
+        self.fallback = fallback
+        self.stream = torch.cuda.Stream(self.device)
+        self.algo = int(os.environ.get("RMM_PEER_ALGO", "0"))
+
+    @property
+    def launches(self) -> int:
+        return int(self._c.launches)
+
+    def allreduce_on(self, t, stream, op="sum"):
+        if op != "sum" or t.dtype not in _PEER_DT or not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16:
+            if self.fallback is None:
+                raise ValueError(f"PeerComm: sum of contiguous 16-B aligned bf16/fp32 device tensors only "
+                                 f"(got op={op}, dtype={t.dtype})")
+            return self.fallback.allreduce(t, op)
+        self._c.all_reduce(t.data_ptr(), t.numel(), _PEER_DT[t.dtype], stream.cuda_stream, self.algo)
+
+    def allreduce(self, t, op="sum"):
+        if t.data_ptr() % 16 and op == "sum" and t.dtype in _PEER_DT and t.is_cuda:
+            tmp = t.contiguous().clone()
+            self.allreduce_on(tmp, torch.cuda.current_stream(self.device), op)
+            t.copy_(tmp)
+            return
+        self.allreduce_on(t, torch.cuda.current_stream(self.device), op)
+
+    def allreduce_async(self, t, op="sum"):
+        """Fork onto the comm stream; wait() joins the caller's current stream back."""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        self.allreduce_on(t, self.stream, op)
+        t.record_stream(self.stream)
+        return _StreamJoin(self.stream)
+
+    def broadcast(self, t, src=0):
+        if t.dtype in _PEER_DT and t.is_cuda:
+            buf = t if (t.is_contiguous() and t.data_ptr() % 16 == 0) else t.contiguous().clone()
+            if self.rank != src:
+                buf.zero_()
+            self.allreduce(buf)
+            if buf is not t:
+                t.copy_(buf)
+            return
+        if t.is_floating_point() and t.is_cuda:
+            f = t.float()
+            self.broadcast(f, src)
+            t.copy_(f)
+            return
+        if self.fallback is None:
+            raise ValueError(f"PeerComm.broadcast: unsupported tensor {t.dtype} on {t.device}")
+        self.fallback.broadcast(t, src)
+
+    def barrier(self):
+        x = torch.zeros(4, device=self.device)
+        self.allreduce(x)
+        torch.cuda.current_stream(self.device).synchronize()
+        self.check()
+
+    def check(self):
+        """Raise if a flag wait timed out (a peer died or never launched its side)."""
+        e = int(self._c.error())
+        if e:
+            raise RuntimeError(f"PeerComm rank {self.rank}: all-reduce flag wait timed out "
+                               f"(peer {(e - 1) & 0xff}, workgroup {((e - 1) >> 8) & 0xffff}, phase {(e - 1) >> 24})")
+
+    def close(self):
+        self._c.close()
 
 
 def default_comm(process_group=None) -> Comm:

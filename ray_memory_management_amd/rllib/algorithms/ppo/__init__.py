@@ -220,8 +220,12 @@ class PPO(Algorithm):
         if getattr(self, "_dev_w", None) is None:
             import os
 
+            # only the GPU rollout-worker classes load the flat bf16 HBM layout; WorkerSet falls back
+            # to a plain RolloutWorker for envs outside the vector registry or with an env_creator
+            cls = getattr(self.workers, "remote_worker_class", None)
+            gpu_cls = getattr(cls, "__name__", "") in ("GPURolloutWorker", "HybridRolloutWorker")
             self._dev_w = bool(c.num_gpus_per_learner_worker and (c.num_gpus_per_worker or c.gpu_rollouts)
-                               and not os.environ.get("RMM_HOST_WEIGHTS"))
+                               and gpu_cls and not os.environ.get("RMM_HOST_WEIGHTS"))
         return self._dev_w
 
     def _extra_state(self):
@@ -255,6 +259,8 @@ class PPO(Algorithm):
         if self.learner_group is not None:
             self.learner_group.set_weights(weights)
             self._weights_ref = self.learner_group.weights_ref()
+            if self._dev_refs is not None:  # the next iteration must not push pre-restore HBM weights
+                self._dev_refs = self.learner_group.device_weights_refs()
             self.workers.local_worker().set_weights(weights)
             self.workers.sync_weights(ref=self._weights_ref)
             return

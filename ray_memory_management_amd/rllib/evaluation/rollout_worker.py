@@ -17,6 +17,19 @@ from ray_memory_management_amd.rllib.policy import TorchPolicy, compute_gae_for_
 from ray_memory_management_amd.rllib.sample_batch import SampleBatch, concat_samples
 
 
+def unpack_flat_weights(weights: Dict) -> Dict:
+    """A learner actor's flat bf16 weight publication ({'__rmm_flat_bf16__': flat, '__rmm_layout__':
+    [(name, offset, shape, stride)]}, LearnerActor.get_weights_device) → per-parameter fp32 CPU
+    tensors, for rollout workers that run the policy on the CPU."""
+    import torch
+
+    flat = weights["__rmm_flat_bf16__"]
+    flat = flat.detach().to("cpu", torch.float32) if isinstance(flat, torch.Tensor) else \
+        torch.as_tensor(np.asarray(flat)).float()
+    return {name: flat.as_strided(tuple(shape), tuple(stride), int(off)).contiguous()
+            for name, off, shape, stride in weights["__rmm_layout__"]}
+
+
 class RolloutWorker:
     def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
                  num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
@@ -338,6 +351,9 @@ class RolloutWorker:
 
         import torch
 
+        if "__rmm_flat_bf16__" in weights:  # a learner's flat bf16 HBM publication (LearnerActor)
+            weights = {**{k: v.detach().cpu() for k, v in self.policy.model.state_dict().items()},
+                       **unpack_flat_weights(weights)}  # buffers keep their current values
         with warnings.catch_warnings():  # store-backed arrays are read-only; load_state_dict copies them
             warnings.simplefilter("ignore", UserWarning)
             self.policy.set_weights({k: (v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v)))

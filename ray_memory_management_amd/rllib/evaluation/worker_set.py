@@ -49,6 +49,7 @@ class WorkerSet:
             q = self._config.get("rollout_worker_hw_queues", int(os.environ.get("RMM_ROLLOUT_HW_QUEUES", "1")))
             if q:
                 opts["runtime_env"] = {"env_vars": {"GPU_MAX_HW_QUEUES": str(int(q))}}
+        self.remote_worker_class = cls  # which rollout-worker class the remote actors run
         self._remote_cls = ray.remote(cls).options(**opts)
         self._strategy = worker_strategy
         self._remote: List = []

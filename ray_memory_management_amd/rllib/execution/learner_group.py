@@ -57,11 +57,20 @@ class LearnerActor:
             # aborts on captured collectives on ROCm)
             import torch.distributed as dist
 
-            from ray_memory_management_amd.parallel.comm import RcclComm
+            from ray_memory_management_amd.parallel.comm import PeerComm, PeerUnavailable, RcclComm
             from ray_memory_management_amd.util.collective.collective import _store_path
 
             store = dist.FileStore(_store_path(group_name), world)
-            comm = RcclComm(store, rank, world, key=f"{group_name}-rccl")
+            comm = None
+            if os.environ.get("RMM_PEER_COMM", "1") != "0":
+                # MI355X-native peer-memory all-reduce over xGMI (hipIPC), captured inside the chained
+                # SGD graph; RCCL only when some rank cannot map its peers
+                try:
+                    comm = PeerComm(store, rank, world, key=f"{group_name}-peer", device=idx)
+                except PeerUnavailable as e:
+                    print(f"[LearnerActor {rank}] {e}; using RCCL", flush=True)
+            if comm is None:
+                comm = RcclComm(store, rank, world, key=f"{group_name}-rccl")
         elif world > 1:
             from ray_memory_management_amd.util.collective import collective as col
 
@@ -149,7 +158,8 @@ class LearnerActor:
         """Which communicator carries the gradients and whether the SGD-step graph contains them."""
         L = self.learner
         return {"comm": type(L.comm).__name__, "graph_has_comm": bool(L._graph_has_comm),
-                "split_graphs": L._graphs_split is not None, "graphs": bool(L.graphs)}
+                "split_graphs": L._graphs_split is not None, "graphs": bool(L.graphs),
+                "chain": int(getattr(L, "_chain", 1)), "launches": int(getattr(L.comm, "launches", 0))}
 
     def device_info(self):
         import torch

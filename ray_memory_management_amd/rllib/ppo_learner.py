@@ -446,6 +446,41 @@ class PPOLearner:
         cap.wait_stream(side)
         self._adam_range(0, self._manual, cap.cuda_stream, bump=True)
 
+    def _peer_in_graph(self) -> bool:
+        """The communicator's collectives are plain kernels with no host step (PeerComm): they can
+        sit inside a chained multi-step SGD graph."""
+        return self.world > 1 and bool(getattr(self.comm, "in_graph", False)) \
+            and os.environ.get("RMM_PEER_IN_GRAPH", "1") != "0"
+
+    def _peer_mode(self) -> str:
+        """How a peer-comm SGD step reduces its bucket (RMM_PEER_MODE):
+        ``one`` (default): one all-reduce of the whole bucket after both backwards;
+        ``split``: the dense+heads bucket right after K12, the trunk bucket after K10 bwd (same stream);
+        ``fork``: the dense+heads all-reduce forked onto the comm stream beside the K10 backward."""
+        return os.environ.get("RMM_PEER_MODE", "one")
+
+    def _manual_peer_step(self, full):
+        """One multi-rank SGD step with the peer-memory all-reduce (eager or under capture): every
+        rank issues the same all-reduce sequence, so the device epoch counters stay in step."""
+        mode = self._peer_mode()
+        self._manual_fwd_dense_bwd(full)
+        if mode == "fork":
+            cap = torch.cuda.current_stream(self.device)
+            cs = self.comm.stream
+            cs.wait_stream(cap)
+            self.comm.allreduce_on(self.flat_grad[self._manual:], cs)
+            self._manual_trunk_bwd(full)
+            self.comm.allreduce_on(self.flat_grad[:self._manual], cap)
+            cap.wait_stream(cs)
+        elif mode == "split":
+            self.comm.allreduce(self.flat_grad[self._manual:])
+            self._manual_trunk_bwd(full)
+            self.comm.allreduce(self.flat_grad[:self._manual])
+        else:
+            self._manual_trunk_bwd(full)
+            self.comm.allreduce(self.flat_grad)
+        self._opt_launch()
+
     def _side_stream(self):
         s = getattr(self, "_side", None)
         if s is None:
@@ -517,7 +552,9 @@ class PPOLearner:
     # ------------------------------------------------------------------ one SGD step (any mode)
     def _step_eager(self, full):
         """One minibatch step without graphs: manual kernels (overlapped all-reduce) or autograd."""
-        if self._manual_ok(full):
+        if self._manual_ok(full) and self._peer_in_graph():
+            self._manual_peer_step(full)
+        elif self._manual_ok(full):
             self._manual_fwd_dense_bwd(full)
             if self.world > 1 and _comm_overlap():
                 work = self.comm.allreduce_async(self.flat_grad[self._manual:])   # dense+heads bucket
@@ -596,11 +633,15 @@ class PPOLearner:
                 self._manual_fwd_dense_bwd(full)
                 self._overlapped_tail(full)
             self._graph = g
-        elif self.world == 1 or self.cfg["allreduce_in_graph"]:
+        elif self.world == 1 or self.cfg["allreduce_in_graph"] or self._peer_in_graph():
             # world of one: `chain` consecutive SGD steps per graph (the device counters index each
             # step's minibatch and Adam step) — consecutive replays of a one-step graph leave ~8 µs
-            # idle between them on MI355X (profiles/sgd_chain_r3.txt), a chained graph none
-            chain = self._sgd_chain(int(full["period"])) if self.world == 1 else 1
+            # idle between them on MI355X (profiles/sgd_chain_r3.txt), a chained graph none.
+            # Multi-rank with the peer-memory all-reduce (parallel/comm.py:PeerComm): the same chain,
+            # with the bucket all-reduce kernel inside every step (no host between SGD steps)
+            peer = self.world > 1 and self._peer_in_graph()
+            chain = self._sgd_chain(int(full["period"])) if (self.world == 1 or peer) else 1
+            self._graph_has_comm = self.world > 1
             self._parity = (manual and chain > 1 and not self._fused_adam()
                             and os.environ.get("RMM_CTR_PARITY", "1") != "0")
             self._par = 0
@@ -609,7 +650,9 @@ class PPOLearner:
                 with torch.cuda.graph(g):
                     for k in range(chain):
                         self._parity_last = k == chain - 1
-                        if manual:
+                        if manual and peer:
+                            self._manual_peer_step(full)
+                        elif manual:
                             self._manual_fwd_dense_bwd(full)
                             if self.world > 1:
                                 self.comm.allreduce(self.flat_grad[self._manual:])
@@ -779,6 +822,8 @@ class PPOLearner:
             self.comm.allreduce(self.acc)
             self.acc.mul_(1.0 / self.world)
         acc = (self.acc / float(max(steps, 1) * mbs)).tolist()  # one host sync per update
+        if self.world > 1 and hasattr(self.comm, "check"):
+            self.comm.check()  # a peer all-reduce that timed out (dead peer) fails the update here
         self.timesteps += n * self.world
         st = self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
         if self.clip_out is not None:
