@@ -41,6 +41,23 @@ def _contained():
 _custom_serializers: dict = {}
 
 
+_mro_cache: dict = {}  # type -> inherited serializer entry (or None); cleared on (de)registration
+
+
+def _mro_lookup(t):
+    try:
+        return _mro_cache[t]
+    except KeyError:
+        pass
+    ent = None
+    for base in t.__mro__[1:-1]:
+        ent = _custom_serializers.get(base)
+        if ent is not None:
+            break
+    _mro_cache[t] = ent
+    return ent
+
+
 def _rebuild_custom(deserializer, payload):
     return deserializer(payload)
 
@@ -51,10 +68,7 @@ class _Pickler(cloudpickle.CloudPickler):
         if _custom_serializers:
             ent = _custom_serializers.get(t)
             if ent is None:  # a serializer registered for a base class covers its subclasses
-                for base in t.__mro__[1:-1]:
-                    ent = _custom_serializers.get(base)
-                    if ent is not None:
-                        break
+                ent = _mro_lookup(t)
             if ent is not None:
                 return _rebuild_custom, (ent[1], ent[0](obj))
         mod = t.__module__

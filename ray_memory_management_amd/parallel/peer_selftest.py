@@ -34,7 +34,50 @@ def _ref(xs):
     return acc.to(xs[0].dtype)
 
 
-def _rank_main(rank, world, path, out_dir, bench_iters):
+def _sweep(rank, world, store, d, dev, iters):
+    """µs per all-reduce over payload sizes x workgroup counts (eager back-to-back and 25 per graph)."""
+    import torch
+
+    from ray_memory_management_amd.parallel.comm import PeerComm
+
+    out = []
+    for nb in (8, 32, 64, 128, 256):
+        comm = PeerComm(store, rank, world, key=f"sw{nb}", device=dev, cap_bytes=16 << 20, nblocks=nb)
+        for nbytes in (4 << 10, 64 << 10, 1354858, 8 << 20):
+            for algo in ((1, 2) if world > 2 else (1,)):
+                comm.algo = algo
+                x = torch.zeros(nbytes // 2, dtype=torch.bfloat16, device=d)
+                for _ in range(5):
+                    comm.allreduce(x)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.allreduce(x)
+                torch.cuda.synchronize()
+                eager = (time.perf_counter() - t0) / iters * 1e6
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(25):
+                        comm.allreduce(x)
+                g.replay()
+                torch.cuda.synchronize()
+                reps = max(1, iters // 25)
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    g.replay()
+                torch.cuda.synchronize()
+                graph = (time.perf_counter() - t0) / (reps * 25) * 1e6
+                out.append({"nblocks": nb, "bytes": nbytes, "algo": algo, "us_eager": round(eager, 2),
+                            "us_graph": round(graph, 2)})
+        comm.check()
+        store.add(f"sw{nb}/done", 1)
+        while int(store.add(f"sw{nb}/done", 0)) < world:
+            time.sleep(0.001)
+        comm.close()
+    return out
+
+
+def _rank_main(rank, world, path, out_dir, bench_iters, sweep=False):
     import torch
     import torch.distributed as dist
 
@@ -45,6 +88,11 @@ def _rank_main(rank, world, path, out_dir, bench_iters):
     torch.cuda.set_device(dev)
     d = torch.device("cuda", dev)
     store = dist.FileStore(path, world)
+    if sweep:
+        res = {"rank": rank, "device": dev, "sweep": _sweep(rank, world, store, d, dev, bench_iters), "ok": True}
+        with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+        return
     res = {"rank": rank, "device": dev, "cases": {}}
     comm = PeerComm(store, rank, world, key="t", device=dev, cap_bytes=1 << 20)
     res["uncached_signals"] = bool(comm._c.uncached_signals)
@@ -173,9 +221,10 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--rank", type=int, default=-1)
     ap.add_argument("--store", default="")
+    ap.add_argument("--sweep", action="store_true", help="timing sweep over sizes x workgroup counts")
     a = ap.parse_args()
     if a.rank >= 0:
-        _rank_main(a.rank, a.world, a.store, a.out, a.iters)
+        _rank_main(a.rank, a.world, a.store, a.out, a.iters, a.sweep)
         return
     os.makedirs(a.out, exist_ok=True)
     store = os.path.join(a.out, f"store-{os.getpid()}")
@@ -183,7 +232,7 @@ def main():
         os.unlink(store)
     procs = [subprocess.Popen([sys.executable, "-m", "ray_memory_management_amd.parallel.peer_selftest", "--world",
                                str(a.world), "--out", a.out, "--iters", str(a.iters), "--rank", str(r), "--store",
-                               store]) for r in range(a.world)]
+                               store] + (["--sweep"] if a.sweep else [])) for r in range(a.world)]
     rcs = [p.wait() for p in procs]
     results = []
     for r in range(a.world):

@@ -454,6 +454,11 @@ class HybridRolloutWorker(GPURolloutWorker):
                     cat = [torch.cat(xs, dim=0 if k == 7 else 1) for k, xs in enumerate(zip(*parts))]
                     frag = pack_fragment_device(*cat)
             st.synchronize()
+            for g in G:  # a gated step that timed out ran on stale frames: never hand that fragment out
+                if g.gate and int(g.gate_err.item()):
+                    g.gate_err.zero_()
+                    raise RuntimeError("rollout step gate timed out during this fragment (a policy step ran "
+                                       "without its frames); fragment discarded")
         self._sample_time += time.perf_counter() - t0
         return frag
 

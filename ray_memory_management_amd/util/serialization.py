@@ -12,7 +12,9 @@ def register_serializer(cls: type, *, serializer: Callable[[Any], Any], deserial
     if not isinstance(cls, type):
         raise TypeError("register_serializer expects a class")
     _ser._custom_serializers[cls] = (serializer, deserializer)
+    _ser._mro_cache.clear()
 
 
 def deregister_serializer(cls: type) -> None:
     _ser._custom_serializers.pop(cls, None)
+    _ser._mro_cache.clear()

@@ -1,37 +1,57 @@
 """Serializers for third-party types that plain pickling handles badly, registered on demand.
 
-Role parity: reference python/ray/util/serialization_addons.py (``apply`` registers pydantic model
-classes and starlette requests so Serve can pass them between processes). Here they go through the
-runtime's custom-serializer registry (util/serialization.py): pydantic models travel as
-(class, field dict), starlette requests as (scope, body).
+Parity: reference python/ray/util/serialization_addons.py registers the same two types:
+pydantic's ``ModelField`` (its Cython validators do not pickle) rebuilt from its constructor
+arguments, and starlette's ``datastructures.State`` (its ``__getattr__`` override defeats
+pickling) rebuilt from its state dict; plus buffered starlette requests as (scope, body). Both go through the runtime's custom-serializer registry
+(util/serialization.py). Pydantic v2 models pickle natively; v2 keeps the v1 ``ModelField`` under
+``pydantic.v1``, which is what is registered there.
 """
 from __future__ import annotations
 
 
-def register_pydantic_serializer(serialization_context=None) -> bool:
+def _model_field_cls():
     try:
-        import pydantic
+        from pydantic.fields import ModelField  # pydantic v1
+        return ModelField
     except ImportError:
+        pass
+    try:
+        from pydantic.v1.fields import ModelField  # pydantic v2's bundled v1 API
+        return ModelField
+    except ImportError:
+        return None
+
+
+def register_pydantic_serializer(serialization_context=None) -> bool:
+    ModelField = _model_field_cls()
+    if ModelField is None:
         return False
     from ray_memory_management_amd.util.serialization import register_serializer
 
-    def _ser(m):
-        return type(m), m.model_dump() if hasattr(m, "model_dump") else m.dict()
+    def _ser(o):
+        # outer_type_ is the declared type (type_ may have been narrowed to e.g. int for List[int])
+        return {"name": o.name, "type_": o.outer_type_, "class_validators": o.class_validators,
+                "model_config": o.model_config, "default": o.default, "default_factory": o.default_factory,
+                "required": o.required, "alias": o.alias, "field_info": o.field_info}
 
-    def _de(v):
-        cls, fields = v
-        return cls(**fields)
-
-    register_serializer(pydantic.BaseModel, serializer=_ser, deserializer=_de)
+    register_serializer(ModelField, serializer=_ser, deserializer=lambda kw: ModelField(**kw))
     return True
 
 
 def register_starlette_serializer(serialization_context=None) -> bool:
     try:
-        from starlette.requests import Request
+        import starlette.datastructures
     except ImportError:
         return False
     from ray_memory_management_amd.util.serialization import register_serializer
+
+    State = starlette.datastructures.State
+    register_serializer(State, serializer=lambda st: dict(st._state), deserializer=lambda d: State(d))
+    try:  # beyond the reference: Serve here can hand a buffered HTTP request to a replica as-is
+        from starlette.requests import Request
+    except ImportError:
+        return True
 
     def _ser(req):
         scope = {k: v for k, v in req.scope.items() if k not in ("app", "router", "endpoint", "state")}

@@ -55,7 +55,14 @@ def test_subclass_serializer_and_addons():
         p = pickle.loads(buf.getvalue())
         assert isinstance(p, Point) and p.x == 3 and p.y == 0.5
 
+        from starlette.datastructures import State
         from starlette.requests import Request
+
+        st = State({"a": 1, "b": [2]})
+        buf = io.BytesIO()
+        ser._Pickler(buf, protocol=5).dump(st)
+        st2 = pickle.loads(buf.getvalue())
+        assert isinstance(st2, State) and st2.a == 1 and st2.b == [2]
 
         async def receive():
             return {"type": "http.request", "body": b"hi", "more_body": False}
@@ -67,8 +74,11 @@ def test_subclass_serializer_and_addons():
         r2 = pickle.loads(buf.getvalue())
         assert r2.method == "POST" and r2.url.path == "/a" and r2.query_params["q"] == "1"
     finally:
-        deregister_serializer(pydantic.BaseModel)
         deregister_serializer(Request)
+        deregister_serializer(State)
+        mf = serialization_addons._model_field_cls()
+        if mf is not None:
+            deregister_serializer(mf)
 
 
 def test_deprecated_experimental_aliases():

@@ -578,3 +578,40 @@ print(json.dumps({{"ct": ct.tolist(), "act": act.tolist(), "logp": logp.tolist()
     assert a["act"][0] == [0] * B and any(a["act"][1]) and any(a["act"][2])
     assert a["done"] == 0 and b["done"] == 0
 
+
+
+@pytest.mark.parametrize("chain_cap", [3, 4])
+def test_parity_counters_match_ticket_bump(cuda, monkeypatch, chain_cap):
+    """Chained SGD graphs with parity step counters (K6 writes the advanced counters into the other
+    copy) vs the last-workgroup ticket bump in place: bit-identical weights and counters over two
+    updates, for an odd chain (3: the last step bumps in place) and an even one (4)."""
+    from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler, PPOLearner
+    from ray_memory_management_amd.rllib.env import GPUSyntheticAtariVectorEnv
+    from ray_memory_management_amd.rllib.models import VisionNetwork
+
+    monkeypatch.setenv("RMM_SGD_CHAIN", str(chain_cap))
+    env = GPUSyntheticAtariVectorEnv(16, cuda, num_actions=4, seed=0)
+    torch.manual_seed(0)
+    base = VisionNetwork(4)
+    cfg = {"sgd_minibatch_size": 64, "num_sgd_iter": 3, "use_graphs": True}  # 12 SGD steps per update
+    learners = {}
+    for parity in ("0", "1"):
+        monkeypatch.setenv("RMM_CTR_PARITY", parity)
+        m = VisionNetwork(4)
+        m.load_state_dict(base.state_dict())
+        learners[parity] = PPOLearner(m, dict(cfg), device=cuda, action_space=env.action_space)
+    sampler = GPURolloutSampler(env, learners["0"].model, fragment=16, use_graphs=False)
+    first = sampler.sample()
+    Batch = type(first)
+    batches = [{k: v.clone() for k, v in first.items()}, {k: v.clone() for k, v in sampler.sample().items()}]
+    for parity, ln in learners.items():
+        monkeypatch.setenv("RMM_CTR_PARITY", parity)
+        for i, b in enumerate(batches):
+            torch.manual_seed(100 + i)
+            ln.update(Batch({k: v.clone() for k, v in b.items()}))
+        assert ln.graphs and ln._chain == chain_cap
+    a, b = learners["0"], learners["1"]
+    assert torch.equal(a.master, b.master)
+    assert torch.equal(a.w_bf16, b.w_bf16)
+    assert torch.equal(a.ctr, b.ctr)
+    assert int(b.ctr[1]) == 24  # Adam steps: 2 updates x 12
