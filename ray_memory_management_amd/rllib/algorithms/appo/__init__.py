@@ -51,13 +51,13 @@ class APPOLearner(VTraceLearner):
 
     def loss(self, T, b, last_obs):
         c = self.cfg
-        logits, values, boot = self._forward(self.model, b["obs"], last_obs)
+        logits, values, boot = self._forward(self.model, b, last_obs)
         lsm = torch.log_softmax(logits, -1)
         act = b["actions"].unsqueeze(-1)
         logp = lsm.gather(2, act).squeeze(-1)
         blogp = b["action_logp"]
         with torch.no_grad():
-            tlogits, _, _ = self._forward(self.target, b["obs"], last_obs)
+            tlogits, _, _ = self._forward(self.target, b, last_obs)
             old_logp = torch.log_softmax(tlogits, -1).gather(2, act).squeeze(-1)
             vs, adv = ops.vtrace(blogp, old_logp, b["rewards"], values, b["dones"], boot, c["gamma"],
                                  c["vtrace_clip_rho_threshold"], c["vtrace_clip_pg_rho_threshold"],

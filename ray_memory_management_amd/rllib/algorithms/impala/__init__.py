@@ -103,11 +103,30 @@ class VTraceLearner:
                 np.array(frags[0][k], copy=True)
             return torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=nb)
 
-        return T, {k: cat(k) for k in ("obs", "actions", "action_logp", "action_dist_inputs", "rewards", "dones")}, \
-            cat("last_obs", axis=0)
+        keys = ["obs", "actions", "action_logp", "action_dist_inputs", "rewards", "dones"]
+        b = {k: cat(k) for k in keys}
+        if "state_in" in frags[0]:  # recurrent unrolls (RolloutWorker.sample_time_major)
+            for k in ("prev_actions", "prev_rewards", "resets"):
+                b[k] = cat(k)
+            for k in ("last_prev_actions", "last_prev_rewards"):
+                b[k] = cat(k, axis=0)
+            b["state_in"] = [torch.from_numpy(np.ascontiguousarray(np.concatenate(
+                [np.asarray(f["state_in"][i]) for f in frags], axis=0))).to(dev).float()
+                for i in range(len(frags[0]["state_in"]))]
+        return T, b, cat("last_obs", axis=0)
 
-    def _forward(self, model, obs, last_obs):
+    def _forward(self, model, b, last_obs):
+        obs = b["obs"]
         T, B = obs.shape[:2]
+        if getattr(model, "is_recurrent", False):
+            # the unroll re-run from its start state ([B, T] sequences, resets at episode starts), then
+            # one step on the bootstrap observation from the final state
+            bt = lambda x: x.transpose(0, 1)  # noqa: E731
+            logits, values, st = model.seq(bt(obs), b["state_in"], bt(b["resets"]), bt(b["prev_actions"]),
+                                           bt(b["prev_rewards"]))
+            st = model.reset_state(st, b["dones"][-1] > 0)
+            _, boot, _ = model.step(last_obs, st, b["last_prev_actions"], b["last_prev_rewards"])
+            return bt(logits.float()), bt(values.float()), boot.float()
         x = torch.cat([obs.reshape((T * B,) + tuple(obs.shape[2:])), last_obs.to(obs.dtype)], 0)
         logits, values = model(x)
         logits, values = logits.float(), values.float()
@@ -115,7 +134,7 @@ class VTraceLearner:
 
     def loss(self, T, b, last_obs):
         c = self.cfg
-        logits, values, boot = self._forward(self.model, b["obs"], last_obs)
+        logits, values, boot = self._forward(self.model, b, last_obs)
         lsm = torch.log_softmax(logits, -1)
         tlogp = lsm.gather(2, b["actions"].unsqueeze(-1)).squeeze(-1)
         with torch.no_grad():
@@ -204,6 +223,7 @@ class LearnerThread(threading.Thread):
 class Impala(Algorithm):
     _config_class = ImpalaConfig
     _learner_class = VTraceLearner
+    _supports_sequence_models = True
 
     def validate_config(self, c):
         super().validate_config(c)

@@ -63,6 +63,7 @@ class PPOConfig(AlgorithmConfig):
 
 class PPO(Algorithm):
     _config_class = PPOConfig
+    _supports_sequence_models = True
     learner = None
     learner_group = None
     _weights_ref = None
@@ -74,6 +75,16 @@ class PPO(Algorithm):
                              f"({c.train_batch_size}).")
         if c.entropy_coeff < 0:
             raise ValueError("`entropy_coeff` must be >= 0.0")
+        from ray_memory_management_amd.rllib.recurrent_net import wants_sequence_model
+
+        if wants_sequence_model(c.model):
+            if type(self).__name__ != "PPO":
+                raise ValueError(f"{type(self).__name__} does not train recurrent / attention models")
+            if getattr(c, "gpu_rollouts", False):
+                raise ValueError("gpu_rollouts (device env + fused sampler) runs feed-forward policies only; "
+                                 "use CPU rollout workers with use_lstm / use_attention")
+            # sequences need the state recorded by the rollout: GAE + sequence layout on the workers
+            c.postprocess_on_learner = False
         if c.num_learner_workers and c.num_learner_workers > 1:
             if c.train_batch_size % c.num_learner_workers or c.sgd_minibatch_size % c.num_learner_workers:
                 raise ValueError("train_batch_size and sgd_minibatch_size are totals across learner workers: "

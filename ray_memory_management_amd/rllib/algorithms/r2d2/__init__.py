@@ -245,6 +245,7 @@ class R2D2Learner:
 
 class R2D2(DQN):
     _config_class = R2D2Config
+    _supports_sequence_models = True  # its own recurrent Q-model (RecurrentQModel)
 
     def validate_config(self, c):
         super().validate_config(c)

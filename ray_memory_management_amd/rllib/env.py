@@ -62,6 +62,66 @@ class Box(Space):
         return f"Box({self.shape}, {self.dtype})"
 
 
+class Dict(Space):
+    """Composite space of named sub-spaces (gym.spaces.Dict): observations are dicts. Rollout
+    workers flatten them (DictFlatteningPreprocessor, keys in sorted order) and the model restores
+    the components (ComplexInputNetwork)."""
+
+    def __init__(self, spaces=None, **kw):
+        spaces = dict(spaces or {}, **kw)
+        self.spaces = {k: spaces[k] for k in sorted(spaces)}
+        self.shape = None
+        self.dtype = None
+
+    def __getitem__(self, k):
+        return self.spaces[k]
+
+    def keys(self):
+        return self.spaces.keys()
+
+    def items(self):
+        return self.spaces.items()
+
+    def sample(self):
+        return {k: s.sample() for k, s in self.spaces.items()}
+
+    def contains(self, x):
+        return isinstance(x, dict) and set(x) == set(self.spaces) and all(
+            s.contains(x[k]) for k, s in self.spaces.items())
+
+    def __repr__(self):
+        return f"Dict({', '.join(f'{k}: {s!r}' for k, s in self.spaces.items())})"
+
+
+class Tuple(Space):
+    """Composite space of positional sub-spaces (gym.spaces.Tuple): observations are tuples."""
+
+    def __init__(self, spaces):
+        self.spaces = tuple(spaces)
+        self.shape = None
+        self.dtype = None
+
+    def __getitem__(self, i):
+        return self.spaces[i]
+
+    def __len__(self):
+        return len(self.spaces)
+
+    def sample(self):
+        return tuple(s.sample() for s in self.spaces)
+
+    def contains(self, x):
+        return isinstance(x, (tuple, list)) and len(x) == len(self.spaces) and all(
+            s.contains(v) for s, v in zip(self.spaces, x))
+
+    def __repr__(self):
+        return f"Tuple({', '.join(repr(s) for s in self.spaces)})"
+
+
+def is_composite(space) -> bool:
+    return isinstance(space, (Dict, Tuple))
+
+
 class Env:
     observation_space: Space
     action_space: Space
@@ -120,6 +180,97 @@ class CartPoleEnv(Env):
         done = bool(x < -self.x_threshold or x > self.x_threshold or theta < -self.theta_threshold
                     or theta > self.theta_threshold or self.steps >= self.max_steps)
         return self.state.astype(np.float32), 1.0, done, {}
+
+
+class StatelessCartPoleEnv(CartPoleEnv):
+    """CartPole without the velocity components (obs = [x, theta]): a policy needs memory to
+    estimate them. Parity: reference rllib/examples/env/stateless_cartpole.py."""
+
+    def __init__(self, config=None):
+        super().__init__(config)
+        high = np.array([self.x_threshold * 2, self.theta_threshold * 2], dtype=np.float32)
+        self.observation_space = Box(-high, high, dtype=np.float32)
+
+    def reset(self, *, seed=None):
+        return super().reset(seed=seed)[[0, 2]]
+
+    def step(self, action):
+        o, r, d, i = super().step(action)
+        return o[[0, 2]], r, d, i
+
+
+class RepeatAfterMeEnv(Env):
+    """Memory test env (reference rllib/examples/env/repeat_after_me_env.py): each step shows a
+    random token in {0, .., n-1} (one-hot) and rewards +1 for repeating the token shown
+    `repeat_delay` steps earlier, -1 otherwise (0 during the first `repeat_delay` steps). A
+    feed-forward policy earns ~(2/n - 1) per step on average; a policy with memory earns +1."""
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.n = int(config.get("num_tokens", 2))
+        self.delay = int(config.get("repeat_delay", 1))
+        self.episode_len = int(config.get("episode_len", 100))
+        self.observation_space = Box(0.0, 1.0, shape=(self.n,), dtype=np.float32)
+        self.action_space = Discrete(self.n)
+        self.rng = np.random.default_rng(config.get("seed"))
+        self.history = []
+
+    def _obs(self):
+        tok = int(self.rng.integers(self.n))
+        self.history.append(tok)
+        o = np.zeros(self.n, np.float32)
+        o[tok] = 1.0
+        return o
+
+    def reset(self, *, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.history = []
+        return self._obs()
+
+    def step(self, action):
+        t = len(self.history) - 1
+        if t >= self.delay:
+            r = 1.0 if int(action) == self.history[t - self.delay] else -1.0
+        else:
+            r = 0.0
+        obs = self._obs()
+        return obs, r, len(self.history) > self.episode_len, {}
+
+
+class DictObsEnv(Env):
+    """Composite-observation test env: obs = {"image": uint8 [8, 8, 3] whose brightest channel is
+    the target, "pos": Box(2,), "flag": Discrete(3)}; action Discrete(3); reward +1 when the action
+    names the brightest image channel XOR-shifted by the flag ((c + flag) % 3), else 0. Every obs
+    component matters, so a network must read all of them (ComplexInputNetwork)."""
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.observation_space = Dict({"image": Box(0, 255, shape=(8, 8, 3), dtype=np.uint8),
+                                       "pos": Box(-1.0, 1.0, shape=(2,), dtype=np.float32),
+                                       "flag": Discrete(3)})
+        self.action_space = Discrete(3)
+        self.episode_len = int(config.get("episode_len", 20))
+        self.rng = np.random.default_rng(config.get("seed"))
+        self.t = 0
+
+    def _obs(self):
+        c = int(self.rng.integers(3))
+        img = self.rng.integers(0, 60, size=(8, 8, 3)).astype(np.uint8)
+        img[..., c] += 150
+        self._answer = (c + int(f := self.rng.integers(3))) % 3
+        return {"image": img, "pos": self.rng.uniform(-1, 1, 2).astype(np.float32), "flag": int(f)}
+
+    def reset(self, *, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.t = 0
+        return self._obs()
+
+    def step(self, action):
+        r = 1.0 if int(action) == self._answer else 0.0
+        self.t += 1
+        return self._obs(), r, self.t >= self.episode_len, {}
 
 
 class PendulumEnv(Env):
@@ -425,6 +576,9 @@ _REGISTRY = {
     "BreakoutNoFrameskip-v4": SyntheticAtariEnv,
     "Pendulum-v1": PendulumEnv,
     "ContinuousTarget-v0": ContinuousTargetEnv,
+    "StatelessCartPole-v1": StatelessCartPoleEnv,
+    "RepeatAfterMe-v0": RepeatAfterMeEnv,
+    "DictObs-v0": DictObsEnv,
 }
 
 

@@ -30,6 +30,35 @@ def unpack_flat_weights(weights: Dict) -> Dict:
             for name, off, shape, stride in weights["__rmm_layout__"]}
 
 
+class _FlattenObsVectorEnv:
+    """Dict / Tuple observations → flat float32 vectors at the env boundary (the reference's
+    preprocessor step in the sampler), so every sampling path handles plain [n, N] arrays; the
+    observation space stays the composite one for the model (ComplexInputNetwork restores it)."""
+
+    def __init__(self, env):
+        from ray_memory_management_amd.rllib.modelv2 import flatten_observation
+
+        self._env, self._flat = env, flatten_observation
+        self.num_envs = env.num_envs
+        self.observation_space, self.action_space = env.observation_space, env.action_space
+
+    def _f(self, o):
+        return self._flat(self.observation_space, o)
+
+    def vector_reset(self):
+        return [self._f(o) for o in self._env.vector_reset()]
+
+    def reset_at(self, i):
+        return self._f(self._env.reset_at(i))
+
+    def vector_step(self, actions):
+        obs, rew, done, info = self._env.vector_step(actions)
+        return [self._f(o) for o in obs], rew, done, info
+
+    def __getattr__(self, k):
+        return getattr(self._env, k)
+
+
 class RolloutWorker:
     def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
                  num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
@@ -61,6 +90,8 @@ class RolloutWorker:
             vcfg.setdefault("seed", int(base_seed) * 1000 + worker_index)
         self.vec_env = None if env_creator is not None else make_vector_env(env, n_envs, vcfg)
         self.env = self.vec_env if self.vec_env is not None else VectorEnv(mk, n_envs)
+        if hasattr(self.env.observation_space, "spaces"):
+            self.env = _FlattenObsVectorEnv(self.env)
         pcls = self.config.get("policy_class") or TorchPolicy
         if isinstance(pcls, str):
             import importlib
@@ -104,7 +135,10 @@ class RolloutWorker:
     def sample(self) -> SampleBatch:
         if self.input_reader is not None:  # offline data replaces the env sampler
             return self.input_reader.next()
-        batch = self._sample_vector() if self.vec_env is not None else self._sample_env()
+        if getattr(self.policy.model, "is_recurrent", False):
+            batch = self._sample_recurrent()
+        else:
+            batch = self._sample_vector() if self.vec_env is not None else self._sample_env()
         if self.output_writer is not None and "_raw" not in batch:
             self.output_writer.write(batch)
         return batch
@@ -282,6 +316,111 @@ class RolloutWorker:
         self._sample_time += time.perf_counter() - t0
         return out
 
+    # ------------------------------------------------------------------ recurrent / attention policies
+    def _env_reset_all(self):
+        return np.asarray(self._obs) if self.vec_env is not None else np.stack([np.asarray(o) for o in self._obs])
+
+    def _recurrent_rollout(self, T: int, snapshot_every: int):
+        """T env steps of a sequence model with per-env state carried across fragments. Returns the
+        time-major buffers, the state snapshots taken every `snapshot_every` steps (t = 0, L, ..),
+        the state / previous action / reward after the last step and the last observation."""
+        import torch
+
+        n = self.env.num_envs
+        model = self.policy.model
+        dist_cls = self.policy.dist_class
+        discrete = hasattr(self.env.action_space, "n")
+        if getattr(self, "_rstate", None) is None:
+            self._rstate = model.initial_state(n, torch.device("cpu"))
+            self._prev_a = np.zeros(n, np.int64) if discrete else np.zeros((n,) + tuple(self.env.action_space.shape),
+                                                                           np.float32)
+            self._prev_r = np.zeros(n, np.float32)
+        explore = self.config.get("explore", True)
+        obs = self._env_reset_all()
+        buf = {"obs": [], "actions": [], "action_logp": [], "vf_preds": [], "action_dist_inputs": [], "rewards": [],
+               "dones": [], "prev_actions": [], "prev_rewards": []}
+        snaps = [[] for _ in self._rstate]
+        state = self._rstate
+        with torch.no_grad():
+            for t in range(T):
+                if t % snapshot_every == 0:
+                    for k, s_ in enumerate(state):
+                        snaps[k].append(s_.numpy().copy())
+                logits, v, new = model.step(torch.as_tensor(obs), state, torch.as_tensor(self._prev_a),
+                                            torch.as_tensor(self._prev_r))
+                d = dist_cls(logits.float())
+                a = d.sample() if explore else d.deterministic_sample()
+                an = a.numpy()
+                buf["obs"].append(obs)
+                buf["actions"].append(an)
+                buf["action_logp"].append(d.logp(a).numpy())
+                buf["vf_preds"].append(v.float().numpy())
+                buf["action_dist_inputs"].append(logits.float().numpy())
+                buf["prev_actions"].append(self._prev_a.copy())
+                buf["prev_rewards"].append(self._prev_r.copy())
+                if self.vec_env is not None:
+                    nobs, rew, done = self.env.vector_step(an)
+                    rew, done = np.asarray(rew, np.float32), np.asarray(done, bool)
+                else:
+                    nl, rew, done, _ = self.env.vector_step(list(an))
+                    rew, done = np.asarray(rew, np.float32), np.asarray(done, bool)
+                    for i in np.nonzero(done)[0]:
+                        nl[i] = self.env.reset_at(i)
+                    nobs = np.stack([np.asarray(o) for o in nl])
+                buf["rewards"].append(rew)
+                buf["dones"].append(done.astype(np.float32))
+                self._ep_reward += rew
+                self._ep_len += 1
+                for i in np.nonzero(done)[0]:
+                    self._completed.append((float(self._ep_reward[i]), int(self._ep_len[i])))
+                    self._ep_reward[i] = 0.0
+                    self._ep_len[i] = 0
+                state = new
+                self._prev_a = an.copy()
+                self._prev_r = rew.copy()
+                if done.any():  # a new episode starts from the initial state, no previous action / reward
+                    state = model.reset_state(state, done)
+                    self._prev_a[done] = 0
+                    self._prev_r[done] = 0.0
+                obs = np.asarray(nobs)
+            _, last_v, _ = model.step(torch.as_tensor(obs), state, torch.as_tensor(self._prev_a),
+                                      torch.as_tensor(self._prev_r))
+        self._rstate = state
+        self._obs = obs if self.vec_env is not None else list(obs)
+        self.policy.global_timestep += T * n
+        return {k: np.stack(v) for k, v in buf.items()}, [np.stack(s_) for s_ in snaps], last_v.float().numpy(), obs
+
+    def _sample_recurrent(self) -> SampleBatch:
+        """On-policy sample for a sequence model (LSTM / attention): GAE time-major, then the
+        fixed-length sequence layout of rllib/policy/rnn_sequencing.fragment_to_sequences (state at
+        every sequence start, `resets` where an episode begins inside a sequence)."""
+        from ray_memory_management_amd.rllib.policy.rnn_sequencing import SEQ_LENS, RESETS, fragment_to_sequences, \
+            state_key
+
+        t0 = time.perf_counter()
+        T = int(self.config.get("rollout_fragment_length", 200))
+        L = int(self.policy.model.max_seq_len)
+        buf, snaps, last_v, _ = self._recurrent_rollout(T, L)
+        vf = buf["vf_preds"] if self.config.get("use_critic", True) else np.zeros_like(buf["vf_preds"])
+        if not self.config.get("use_critic", True):
+            last_v = np.zeros_like(last_v)
+        adv, ret = compute_gae_for_trajectories(buf["rewards"], vf, buf["dones"], last_v, self.config.get("gamma", 0.99),
+                                                self.config.get("lambda", self.config.get("lambda_", 1.0)))
+        cols = dict(buf)
+        cols[SampleBatch.ADVANTAGES] = adv.astype(np.float32)
+        cols[SampleBatch.VALUE_TARGETS] = ret.astype(np.float32)
+        seq_cols, state_in, seq_lens, resets = fragment_to_sequences(cols, buf["dones"], snaps, L)
+        out = SampleBatch({SampleBatch.OBS: seq_cols.pop("obs"), **seq_cols})
+        for k, st in enumerate(state_in):
+            dict.__setitem__(out, state_key(k), st)
+        dict.__setitem__(out, SEQ_LENS, seq_lens)
+        dict.__setitem__(out, RESETS, resets)
+        out.count = len(resets)
+        if self.callbacks is not None:
+            self.callbacks.on_sample_end(worker=self, samples=out)
+        self._sample_time += time.perf_counter() - t0
+        return out
+
     def sample_time_major(self) -> Dict[str, Any]:
         """One unroll for an off-policy (V-trace) learner: time-major [T, n] columns + each env's
         observation after the last step (the learner bootstraps from its own value of it).
@@ -293,6 +432,19 @@ class RolloutWorker:
         t0 = time.perf_counter()
         T = int(self.config.get("rollout_fragment_length", 50))
         n = self.env.num_envs
+        if getattr(self.policy.model, "is_recurrent", False):
+            # recurrent V-trace unroll: the state at the unroll start, previous actions / rewards, and
+            # `resets` where an episode begins inside the unroll; the learner re-runs the sequence
+            buf, snaps, _, last_obs = self._recurrent_rollout(T, T)
+            resets = np.zeros((T, n), np.float32)
+            resets[1:] = buf["dones"][:-1]
+            out = {"obs": buf["obs"], "actions": buf["actions"], "action_logp": buf["action_logp"],
+                   "action_dist_inputs": buf["action_dist_inputs"], "rewards": buf["rewards"], "dones": buf["dones"],
+                   "prev_actions": buf["prev_actions"], "prev_rewards": buf["prev_rewards"], "resets": resets,
+                   "state_in": [s_[0] for s_ in snaps], "last_prev_actions": self._prev_a.copy(),
+                   "last_prev_rewards": self._prev_r.copy(), "T": T, "n": n, "last_obs": np.array(last_obs, copy=True)}
+            self._sample_time += time.perf_counter() - t0
+            return out
         explore = self.config.get("explore", True)
         obs0 = np.asarray(self._obs) if self.vec_env is not None else np.stack([np.asarray(o) for o in self._obs])
         A = getattr(self.env.action_space, "n", 1)

@@ -32,7 +32,8 @@ class WorkerSet:
             from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import GPURolloutWorker
 
             cls = GPURolloutWorker
-        elif self._config.get("num_gpus_per_worker", 0) and env_creator is None:
+        elif self._config.get("num_gpus_per_worker", 0) and env_creator is None and not (
+                (self._config.get("model") or {}).get("use_lstm") or (self._config.get("model") or {}).get("use_attention")):
             from ray_memory_management_amd.rllib.env import _VECTOR_REGISTRY
 
             env = self._config.get("env")

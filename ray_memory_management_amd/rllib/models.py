@@ -530,13 +530,26 @@ def _same_pad(hw, k, s):
 
 def build_model(obs_space, action_space, model_config=None) -> nn.Module:
     model_config = model_config or {}
+    from ray_memory_management_amd.rllib.recurrent_net import build_sequence_model, wants_sequence_model
+
     if model_config.get("custom_model"):  # a registered ModelV2 (ModelCatalog), behind (logits, value)
+        if wants_sequence_model(model_config):
+            raise ValueError("use_lstm / use_attention wrap the built-in networks; a custom_model must implement "
+                             "its own memory (ModelV2 state) instead")
         from ray_memory_management_amd.rllib.modelv2 import build_custom_model
 
         return build_custom_model(obs_space, action_space, model_config)
     n = getattr(action_space, "n", None)
     if n is None:
         n = 2 * int(torch.tensor(action_space.shape).prod())  # diag-gaussian mean+logstd
+    if wants_sequence_model(model_config):  # reference catalog.py:492: LSTM / attention wrapper
+        from ray_memory_management_amd.rllib.modelv2 import MODEL_DEFAULTS
+
+        return build_sequence_model(obs_space, action_space, n, {**MODEL_DEFAULTS, **model_config})
+    if hasattr(obs_space, "spaces"):  # Dict / Tuple observations (reference complex_input_net.py)
+        from ray_memory_management_amd.rllib.complex_input_net import ComplexInputNetwork
+
+        return ComplexInputNetwork(obs_space, n, model_config)
     shape = tuple(obs_space.shape)
     if len(shape) == 3:
         in_ch = shape[0] if shape[0] in (1, 3, 4) and shape[-1] not in (1, 3, 4) else shape[-1]
@@ -555,3 +568,11 @@ def build_model(obs_space, action_space, model_config=None) -> nn.Module:
 from ray_memory_management_amd.rllib.modelv2 import (  # noqa: E402,F401
     MODEL_DEFAULTS, ActionDistribution, ModelCatalog, ModelV2, Preprocessor, TorchCategorical, TorchDiagGaussian,
     TorchModelV2, get_preprocessor)
+
+# sequence / composite-input networks (reference rllib/models/torch/{recurrent_net,attention_net,
+# complex_input_net}.py)
+from ray_memory_management_amd.rllib.recurrent_net import (  # noqa: E402,F401
+    GTrXLNet, LSTMWrapper, SeqNet as RecurrentNetwork)
+from ray_memory_management_amd.rllib.complex_input_net import ComplexInputNetwork  # noqa: E402,F401
+
+AttentionWrapper = GTrXLNet

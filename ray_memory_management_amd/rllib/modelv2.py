@@ -376,8 +376,92 @@ class AtariRamPreprocessor(Preprocessor):
         return (np.asarray(observation, dtype=np.float32) - 128.0) / 128.0
 
 
+def _component_size(space) -> int:
+    if hasattr(space, "n"):
+        return int(space.n)
+    if hasattr(space, "spaces"):
+        subs = space.spaces.values() if isinstance(space.spaces, dict) else space.spaces
+        return sum(_component_size(s) for s in subs)
+    return int(np.prod(space.shape)) if space.shape else 1
+
+
+def _write_component(space, value, array, offset: int) -> int:
+    """Flatten one (possibly nested) observation component into array[offset:], return the new offset."""
+    if hasattr(space, "n"):
+        array[offset:offset + space.n] = 0.0
+        array[offset + int(value)] = 1.0
+        return offset + int(space.n)
+    if hasattr(space, "spaces"):
+        items = space.spaces.items() if isinstance(space.spaces, dict) else enumerate(space.spaces)
+        for k, s in items:
+            offset = _write_component(s, value[k], array, offset)
+        return offset
+    n = _component_size(space)
+    array[offset:offset + n] = np.asarray(value, dtype=np.float32).reshape(-1)
+    return offset + n
+
+
+class DictFlatteningPreprocessor(Preprocessor):
+    """Dict observation → one flat float32 vector: components in sorted-key order, Discrete as
+    one-hot, Box flattened (reference preprocessors.DictFlatteningPreprocessor). The model gets the
+    structure back with :func:`restore_original_dimensions`."""
+
+    def _init_shape(self, obs_space, options):
+        return (_component_size(obs_space),)
+
+    def transform(self, observation):
+        out = np.empty(self.shape, np.float32)
+        _write_component(self._obs_space, observation, out, 0)
+        return out
+
+    def write(self, observation, array, offset: int):
+        _write_component(self._obs_space, observation, array, offset)
+
+
+class TupleFlatteningPreprocessor(DictFlatteningPreprocessor):
+    """Tuple observation → one flat float32 vector (reference preprocessors.TupleFlatteningPreprocessor)."""
+
+
+def restore_original_dimensions(obs, obs_space, tensorlib="torch"):
+    """Unflatten a [B, N] flat observation batch into the Dict / Tuple structure of `obs_space`:
+    Box components get their shape back, Discrete components stay one-hot [B, n]
+    (reference rllib/models/modelv2.py restore_original_dimensions)."""
+    if not hasattr(obs_space, "spaces"):
+        return obs
+
+    def rec(space, flat, off):
+        if hasattr(space, "n"):
+            return flat[:, off:off + space.n], off + int(space.n)
+        if hasattr(space, "spaces"):
+            if isinstance(space.spaces, dict):
+                out = {}
+                for k, s in space.spaces.items():
+                    out[k], off = rec(s, flat, off)
+                return out, off
+            out = []
+            for s in space.spaces:
+                v, off = rec(s, flat, off)
+                out.append(v)
+            return tuple(out), off
+        n = _component_size(space)
+        return flat[:, off:off + n].reshape((flat.shape[0],) + tuple(space.shape)), off + n
+
+    return rec(obs_space, obs, 0)[0]
+
+
+def flatten_observation(space, obs) -> np.ndarray:
+    """One Dict / Tuple observation → its flat float32 vector (identity for other spaces)."""
+    if not hasattr(space, "spaces"):
+        return obs
+    out = np.empty(_component_size(space), np.float32)
+    _write_component(space, obs, out, 0)
+    return out
+
+
 def get_preprocessor(space):
     """Preprocessor class for an observation space (reference preprocessors.get_preprocessor)."""
+    if hasattr(space, "spaces"):
+        return DictFlatteningPreprocessor if isinstance(space.spaces, dict) else TupleFlatteningPreprocessor
     if hasattr(space, "n"):
         return OneHotPreprocessor
     shape = tuple(getattr(space, "shape", ()) or ())

@@ -63,24 +63,67 @@ class TorchPolicy(Policy):
         self.dist_class = dist_class_for(action_space)
         self.global_timestep = 0
 
+    def is_recurrent(self) -> bool:
+        return bool(getattr(self.model, "is_recurrent", False))
+
+    def get_initial_state(self):
+        """Per-env initial recurrent state (no batch dim), [] for stateless models."""
+        if not self.is_recurrent():
+            return []
+        return [s[0].cpu().numpy() for s in self.model.initial_state(1, self.device)]
+
+    def _obs_tensor(self, obs_batch):
+        from ray_memory_management_amd.rllib.modelv2 import flatten_observation
+
+        if hasattr(self.observation_space, "spaces"):  # Dict / Tuple observations: flat float32 rows
+            obs_batch = [o if isinstance(o, np.ndarray) and o.ndim == 1 else flatten_observation(
+                self.observation_space, o) for o in obs_batch]
+        return torch.as_tensor(np.asarray(obs_batch), device=self.device)
+
     @torch.no_grad()
-    def compute_actions(self, obs_batch, explore: bool = True):
-        obs = torch.as_tensor(np.asarray(obs_batch), device=self.device)
-        logits, v = self.model(obs)
+    def compute_actions(self, obs_batch, state_batches=None, prev_action_batch=None, prev_reward_batch=None,
+                        explore: bool = True, **kwargs):
+        """(actions, state_outs, extra) — reference Policy.compute_actions. Recurrent models take and
+        return the per-env state (list of [B, ...] arrays; the initial state when None)."""
+        if not isinstance(state_batches, (list, tuple)) and state_batches is not None and not isinstance(
+                state_batches, np.ndarray):
+            explore = bool(state_batches)  # legacy positional call compute_actions(obs, explore)
+            state_batches = None
+        obs = self._obs_tensor(obs_batch)
+        state_out = []
+        if self.is_recurrent():
+            st = [torch.as_tensor(np.asarray(s), device=self.device) for s in state_batches] if state_batches \
+                else self.model.initial_state(obs.shape[0], self.device)
+            pa = None if prev_action_batch is None else torch.as_tensor(np.asarray(prev_action_batch), device=self.device)
+            pr = None if prev_reward_batch is None else torch.as_tensor(np.asarray(prev_reward_batch, np.float32),
+                                                                        device=self.device)
+            logits, v, new = self.model.step(obs, st, pa, pr)
+            state_out = [s.cpu().numpy() for s in new]
+        else:
+            logits, v = self.model(obs)
         dist = self.dist_class(logits.float())
         a = dist.sample() if explore else dist.deterministic_sample()
         extra = {SampleBatch.ACTION_LOGP: dist.logp(a).cpu().numpy(), SampleBatch.VF_PREDS: v.float().cpu().numpy(),
                  SampleBatch.ACTION_DIST_INPUTS: logits.float().cpu().numpy()}
         self.global_timestep += len(obs)
-        return a.cpu().numpy(), [], extra
+        return a.cpu().numpy(), state_out, extra
 
-    def compute_single_action(self, obs, explore: bool = False):
+    def compute_single_action(self, obs, state=None, prev_action=None, prev_reward=None, explore: bool = False,
+                              **kwargs):
+        """The action for one observation; with a recurrent model (or when `state` is given) the
+        reference's (action, state_out, extra) tuple."""
+        if self.is_recurrent() or state is not None:
+            st = [np.asarray(s)[None] for s in (state if state is not None else self.get_initial_state())]
+            a, so, extra = self.compute_actions(
+                [obs], st, None if prev_action is None else [prev_action],
+                None if prev_reward is None else [prev_reward], explore=explore)
+            return a[0], [s[0] for s in so], {k: v[0] for k, v in extra.items()}
         a, _, extra = self.compute_actions([obs], explore=explore)
         return a[0]
 
     @torch.no_grad()
     def value(self, obs_batch) -> np.ndarray:
-        _, v = self.model(torch.as_tensor(np.asarray(obs_batch), device=self.device))
+        _, v = self.model(self._obs_tensor(obs_batch))
         return v.float().cpu().numpy()
 
     def get_weights(self):

@@ -177,7 +177,9 @@ class PPOLearner:
         self.cfg = {**DEFAULT_PPO, **(config or {})}
         self.device = torch.device(device)
         self.dist_cls = dist_class_for(action_space) if action_space is not None else Categorical
-        self.fast = (self.device.type == "cuda" and bool(self.cfg["fused"]) and self.dist_cls is Categorical)
+        self.recurrent = bool(getattr(model, "is_recurrent", False))
+        self.fast = (self.device.type == "cuda" and bool(self.cfg["fused"]) and self.dist_cls is Categorical
+                     and not self.recurrent)
         self.comm = as_comm(comm if comm is not None else process_group)
         self.world = self.comm.world
         model = model.to(self.device)
@@ -744,6 +746,8 @@ class PPOLearner:
     def update(self, batch: SampleBatch) -> Dict[str, float]:
         """num_sgd_iter epochs of shuffled minibatch SGD over a (device-resident) batch."""
         c = self.cfg
+        if self.recurrent:
+            return self._update_seq(batch)
         if c["standardize_advantages"]:
             a = batch[SampleBatch.ADVANTAGES].float()
             batch[SampleBatch.ADVANTAGES] = (a - a.mean()) / a.std(unbiased=False).clamp_min(1e-4)
@@ -880,6 +884,93 @@ class PPOLearner:
         acc = (acc / max(steps, 1)).tolist()
         self.timesteps += batch.count * self.world
         return self._finish(acc[0], acc[1], acc[2], acc[3], acc[5], steps)
+
+    def _update_seq(self, batch) -> Dict[str, float]:
+        """PPO over fixed-length sequences (LSTM / attention models, rllib/recurrent_net.py):
+        minibatches are whole sequences (sgd_minibatch_size // max_seq_len of them), each re-run
+        from its recorded state_in with `resets` at episode starts; padded steps (seq_lens) are
+        masked out of every mean. Reference: ppo_torch_policy.py loss with sequence_mask /
+        reduce_mean_valid."""
+        from ray_memory_management_amd.rllib.policy.rnn_sequencing import PREV_ACTIONS, PREV_REWARDS, RESETS, \
+            SEQ_LENS, state_key
+
+        c = self.cfg
+        dev = self.device
+        t = lambda k: torch.as_tensor(batch[k], device=dev)  # noqa: E731
+        seq_lens = t(SEQ_LENS).long()
+        S = int(seq_lens.shape[0])
+        rows = int(torch.as_tensor(batch[SampleBatch.OBS]).shape[0])
+        L = rows // S
+        obs = t(SampleBatch.OBS)
+        obs = obs.reshape((S, L) + tuple(obs.shape[1:]))
+        mask = (torch.arange(L, device=dev).unsqueeze(0) < seq_lens.unsqueeze(1))          # [S, L]
+        cols = {k: t(k).reshape((S, L) + tuple(t(k).shape[1:])) for k in (
+            SampleBatch.ACTIONS, SampleBatch.ACTION_LOGP, SampleBatch.ACTION_DIST_INPUTS, SampleBatch.ADVANTAGES,
+            SampleBatch.VALUE_TARGETS, RESETS)}
+        pa = t(PREV_ACTIONS).reshape((S, L) + tuple(t(PREV_ACTIONS).shape[1:])) if PREV_ACTIONS in batch else None
+        pr = t(PREV_REWARDS).reshape(S, L) if PREV_REWARDS in batch else None
+        states = []
+        k = 0
+        while state_key(k) in batch:
+            states.append(t(state_key(k)).float())
+            k += 1
+        adv = cols[SampleBatch.ADVANTAGES].float()
+        if c["standardize_advantages"]:
+            m = mask.float()
+            mu = (adv * m).sum() / m.sum()
+            sd = (((adv - mu) ** 2 * m).sum() / m.sum()).sqrt().clamp_min(1e-4)
+            adv = (adv - mu) / sd
+        self._apply_schedules()
+        clip, vf_clip, vf_coeff = c["clip_param"], c["vf_clip_param"], c["vf_loss_coeff"]
+        n_mb = max(1, int(c["sgd_minibatch_size"]) // max(L, 1))
+        acc = torch.zeros(6, device=dev)
+        steps, valid_total = 0, 0.0
+        for _ in range(c["num_sgd_iter"]):
+            perm = torch.randperm(S, device=dev)
+            for i in range(0, S, n_mb):
+                idx = perm[i:i + n_mb]
+                m = mask[idx].float()
+                nv = m.sum().clamp_min(1.0)
+                logits, values, _ = self.model.seq(obs[idx], [s[idx] for s in states], cols[RESETS][idx],
+                                                   None if pa is None else pa[idx], None if pr is None else pr[idx])
+                d = self.dist_cls(logits.float())
+                old = self.dist_cls(cols[SampleBatch.ACTION_DIST_INPUTS][idx].float())
+                logp = d.logp(cols[SampleBatch.ACTIONS][idx])
+                ratio = torch.exp(logp - cols[SampleBatch.ACTION_LOGP][idx].float())
+                a_mb = adv[idx]
+                surr = torch.min(a_mb * ratio, a_mb * torch.clamp(ratio, 1 - clip, 1 + clip))
+                vf = torch.clamp((values.float() - cols[SampleBatch.VALUE_TARGETS][idx].float()) ** 2, max=vf_clip)
+                ent = d.entropy()
+                kl = old.kl(d)
+                per = -surr + vf_coeff * vf - self.cur_entropy_coeff * ent + self.kl_coeff * kl
+                loss = (per * m).sum() / nv
+                self.opt.zero_grad(set_to_none=False)
+                loss.backward()
+                if self.world > 1:
+                    for p in self.params:
+                        if p.grad is None:
+                            p.grad = torch.zeros_like(p)
+                    flat = torch.cat([p.grad.reshape(-1) for p in self.params])
+                    self.comm.allreduce(flat)
+                    flat.mul_(1.0 / self.world)
+                    off = 0
+                    for p in self.params:
+                        p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+                        off += p.numel()
+                if c["grad_clip"]:
+                    nn.utils.clip_grad_norm_(self.params, c["grad_clip"])
+                self.opt.step()
+                with torch.no_grad():
+                    acc += torch.stack([((-surr) * m).sum(), (vf * m).sum(), (ent * m).sum(), (kl * m).sum(),
+                                        (((ratio - 1).abs() > clip).float() * m).sum(), (per * m).sum()])
+                valid_total += float(nv)
+                steps += 1
+        if self.world > 1:
+            self.comm.allreduce(acc)
+            acc.mul_(1.0 / self.world)
+        a = (acc / max(valid_total, 1.0)).tolist()
+        self.timesteps += int(mask.sum()) * self.world
+        return self._finish(a[0], a[1], a[2], a[3], a[5], steps)
 
     def get_weights(self, numpy: bool = False):
         """fp32 weights keyed like the model's state_dict (ONE device→host copy of the flat masters
