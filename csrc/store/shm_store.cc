@@ -3,6 +3,7 @@
 
 #include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/types.h>
@@ -18,7 +19,7 @@ namespace rmm {
 namespace {
 
 constexpr uint64_t kMagic = 0x524d4d53544f5245ull;  // "RMMSTORE"
-constexpr uint64_t kVersion = 3;
+constexpr uint64_t kVersion = 4;
 constexpr uint64_t kFreeBit = 1;
 constexpr uint64_t kSizeMask = ~uint64_t(kAlign - 1);
 
@@ -50,6 +51,12 @@ inline uint64_t HashId(const ObjectId& id) {
   h *= 0xBF58476D1CE4E5B9ull;
   h ^= h >> 32;
   return h;
+}
+
+int g_crash_point = 0;
+
+inline void CrashPoint(int p) {
+  if (g_crash_point == p) kill(getpid(), SIGKILL);  // dies holding the store mutex (test hook)
 }
 
 inline void MappingInsert(uint64_t size, int* fl, int* sl) {
@@ -186,17 +193,151 @@ Store::~Store() {
   if (owner_) shm_unlink(name_.c_str());
 }
 
-void Store::Lock() {
-  int rc = pthread_mutex_lock(&hdr_->mu);
+void Store::SetCrashPointForTest(int p) { g_crash_point = p; }
+
+void Store::OnLocked(int rc) {
   if (rc == EOWNERDEAD) {
-    // A process died holding the lock. Our state changes are short and mostly
-    // single-word updates, so mark it consistent and carry on.
+    // A process died inside a critical section: any multi-word update it was making (TLSF split /
+    // merge, table insert, LRU links) may be half done. Rebuild every derived structure from the
+    // entries that validate before anyone reads them (reference: plasma's store owns the
+    // allocator, so a dead client is only a disconnect -- store.cc:323 DisconnectClient).
+    const int dead = hdr_->lock_pid;
     pthread_mutex_consistent(&hdr_->mu);
+    Recover(dead);
   } else if (rc != 0) {
     throw std::runtime_error("store mutex lock failed");
   }
+  hdr_->lock_pid = int32_t(getpid());
 }
-void Store::Unlock() { pthread_mutex_unlock(&hdr_->mu); }
+
+void Store::Lock() { OnLocked(pthread_mutex_lock(&hdr_->mu)); }
+
+void Store::Unlock() {
+  hdr_->lock_pid = 0;
+  pthread_mutex_unlock(&hdr_->mu);
+}
+
+void Store::Recover(int dead_pid) {
+  const uint64_t cap = hdr_->table_cap;
+  const uint64_t heap_lo = hdr_->heap_off, heap_hi = hdr_->heap_off + hdr_->heap_size - kBlockHdr;
+  auto alive = [&](int pid) { return pid > 0 && pid != dead_pid && (kill(pid, 0) == 0 || errno == EPERM); };
+  auto resident = [](const Entry& e) {
+    return !(e.flags & kFlagFallback) &&
+           (e.state == kCreating || e.state == kSealed || e.state == kSpilling || e.state == kRestoring);
+  };
+  // 1) entries that validate
+  std::vector<Entry> keep;
+  uint64_t dropped = 0;
+  for (uint64_t i = 0; i < cap; i++) {
+    Entry e = table_[i];
+    if (e.state == kEmpty || e.state == kTombstone) continue;
+    bool ok = e.state <= kRestoring && e.pin_count >= 0 && e.data_size + e.meta_size <= hdr_->heap_size;
+    if (ok && e.state == kCreating && !alive(e.creator_pid)) ok = false;  // its creator is gone: abort
+    if (ok && resident(e)) {
+      const uint64_t need = std::max(AlignUp(e.data_size + e.meta_size, kAlign) + kBlockHdr, kMinBlock);
+      const bool placed = e.offset >= heap_lo + kBlockHdr && e.offset % kAlign == 0 &&
+                          e.offset - kBlockHdr + need <= heap_hi;
+      // a creator between its entry insert and heap allocation (or inside the unlocked fallback
+      // mapping) owns no block yet: keep it, without storage
+      if (!placed && (e.state == kCreating || e.state == kRestoring)) e.offset = 0;
+      else if (!placed) ok = false;
+    }
+    if (!ok) {
+      dropped++;
+      continue;
+    }
+    e.in_lru = 0;
+    e.lru_prev = e.lru_next = -1;
+    keep.push_back(e);
+  }
+  // 2) heap-resident blocks must not overlap: keep the older entry
+  std::vector<size_t> order;
+  for (size_t k = 0; k < keep.size(); k++)
+    if (resident(keep[k]) && keep[k].offset) order.push_back(k);
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return keep[a].offset < keep[b].offset; });
+  std::vector<uint8_t> gone(keep.size(), 0);
+  uint64_t end = heap_lo;
+  size_t last = SIZE_MAX;
+  for (size_t k : order) {
+    const Entry& e = keep[k];
+    const uint64_t blk = e.offset - kBlockHdr;
+    if (blk < end) {
+      size_t victim = (last != SIZE_MAX && keep[last].create_ns > e.create_ns) ? last : k;
+      gone[victim] = 1;
+      if (victim == k) continue;
+    }
+    end = blk + std::max(AlignUp(e.data_size + e.meta_size, kAlign) + kBlockHdr, kMinBlock);
+    last = k;
+  }
+  // 3) object table: clean re-insert
+  memset(table_, 0, cap * sizeof(Entry));
+  hdr_->table_used = 0;
+  hdr_->lru_head = hdr_->lru_tail = -1;
+  Stats& st = hdr_->stats;
+  st.num_objects = st.num_sealed = st.spilled_bytes_current = st.spilled_objects_current = 0;
+  st.fallback_bytes_current = 0;
+  for (uint64_t i = 0; i < kSpillSlots; i++) spill_[i].file_id = 0, spill_[i].live = 0;
+  std::vector<std::pair<uint64_t, int64_t>> lru;  // (create_ns, slot)
+  for (size_t k = 0; k < keep.size(); k++) {
+    if (gone[k]) {
+      dropped++;
+      continue;
+    }
+    const Entry& e = keep[k];
+    ObjectId o;
+    memcpy(o.b, e.id, kIdSize);
+    uint64_t j = HashId(o) & (cap - 1);
+    while (table_[j].state != kEmpty) j = (j + 1) & (cap - 1);
+    table_[j] = e;
+    hdr_->table_used++;
+    st.num_objects++;
+    if (e.state == kSealed) st.num_sealed++;
+    if (e.state == kSpilled) st.spilled_bytes_current += e.data_size + e.meta_size, st.spilled_objects_current++;
+    if (e.flags & kFlagFallback) st.fallback_bytes_current += e.data_size + e.meta_size;
+    if (e.flags & kFlagHasSpillCopy) {
+      int64_t sl = SpillSlot(e.spill_file, true);
+      if (sl >= 0) spill_[sl].live++;
+    }
+    if (e.state == kSealed && e.pin_count == 0 && resident(e)) lru.push_back({e.create_ns, int64_t(j)});
+  }
+  std::sort(lru.begin(), lru.end());
+  for (auto& x : lru) LruPush(x.second);
+  // 4) heap: used blocks exactly where live payloads are, every gap one free block
+  hdr_->fl_bitmap = 0;
+  memset(hdr_->sl_bitmap, 0, sizeof(hdr_->sl_bitmap));
+  memset(hdr_->free_heads, 0, sizeof(hdr_->free_heads));
+  std::vector<std::pair<uint64_t, uint64_t>> used;  // (block offset, block size)
+  for (uint64_t i = 0; i < cap; i++) {
+    const Entry& e = table_[i];
+    if (e.state != kEmpty && e.state != kTombstone && resident(e) && e.offset)
+      used.push_back({e.offset - kBlockHdr, std::max(AlignUp(e.data_size + e.meta_size, kAlign) + kBlockHdr,
+                                                     kMinBlock)});
+  }
+  std::sort(used.begin(), used.end());
+  uint64_t cur = heap_lo, prev = 0;
+  st.bytes_in_use = 0;
+  auto put = [&](uint64_t off, uint64_t size, bool free_blk) {
+    Blk* b = reinterpret_cast<Blk*>(base_ + off);
+    b->size = size | (free_blk ? kFreeBit : 0);
+    b->prev_phys = prev;
+    b->next_free = b->prev_free = kNil;
+    if (free_blk) TlsfInsert(off);
+    else st.bytes_in_use += size;
+    prev = off;
+  };
+  for (auto& u : used) {
+    if (u.first > cur) put(cur, u.first - cur, true);
+    put(u.first, u.second, false);
+    cur = u.first + u.second;
+  }
+  if (heap_hi > cur) put(cur, heap_hi - cur, true);
+  Blk* sentinel = reinterpret_cast<Blk*>(base_ + heap_hi);
+  sentinel->size = kBlockHdr;
+  sentinel->prev_phys = prev;
+  hdr_->recovered_dropped_total += dropped;
+  __atomic_add_fetch(&hdr_->recoveries_total, 1, __ATOMIC_RELEASE);
+  Broadcast();
+}
 
 void Store::CondWait(int64_t deadline_ns) {
   if (deadline_ns < 0) {
@@ -206,8 +347,9 @@ void Store::CondWait(int64_t deadline_ns) {
   timespec ts;
   ts.tv_sec = deadline_ns / 1000000000ll;
   ts.tv_nsec = deadline_ns % 1000000000ll;
+  hdr_->lock_pid = 0;
   int rc = pthread_cond_timedwait(&hdr_->cv, &hdr_->mu, &ts);
-  if (rc == EOWNERDEAD) pthread_mutex_consistent(&hdr_->mu);
+  OnLocked(rc == ETIMEDOUT ? 0 : rc);
 }
 
 void Store::Wake() {
@@ -285,6 +427,7 @@ uint64_t Store::HeapAlloc(uint64_t n) {
     TlsfInsert(nb);
     bsize = need;
   }
+  CrashPoint(1);  // the remainder is listed free, the block itself still carries its free bit
   b->size = bsize;  // used
   hdr_->stats.bytes_in_use += bsize;
   return blk + kBlockHdr;
@@ -300,6 +443,7 @@ void Store::HeapFree(uint64_t payload_off) {
     Blk* p = reinterpret_cast<Blk*>(base_ + b->prev_phys);
     if (p->size & kFreeBit) {
       TlsfRemove(b->prev_phys);
+      CrashPoint(2);  // a free block unlisted but still marked free
       uint64_t psize = p->size & kSizeMask;
       blk = b->prev_phys;
       bsize += psize;
@@ -450,6 +594,7 @@ int64_t Store::Insert(const ObjectId& id) {
   Entry* e = &table_[slot];
   memset(e, 0, sizeof(Entry));
   memcpy(e->id, id.b, kIdSize);
+  CrashPoint(3);  // table_used counted, entry half written, num_objects not yet
   e->lru_prev = e->lru_next = -1;
   hdr_->stats.num_objects++;
   return slot;
@@ -478,6 +623,7 @@ void Store::LruRemove(int64_t idx) {
   if (!e->in_lru) return;
   if (e->lru_prev >= 0) table_[e->lru_prev].lru_next = e->lru_next;
   else hdr_->lru_head = e->lru_next;
+  CrashPoint(4);  // the list skips the entry one way but not the other
   if (e->lru_next >= 0) table_[e->lru_next].lru_prev = e->lru_prev;
   else hdr_->lru_tail = e->lru_prev;
   e->lru_prev = e->lru_next = -1;
@@ -730,6 +876,7 @@ bool Store::RestoreLocked(int64_t idx) {
   memcpy(id.b, e->id, kIdSize);
   uint64_t len = e->data_size + e->meta_size;
   e->state = kRestoring;
+  e->offset = 0;  // no heap block yet (the allocation below may spill with the lock dropped)
   e->pin_count++;
   uint64_t off = HeapAlloc(len);
   while (off == kNil) {
@@ -747,6 +894,7 @@ bool Store::RestoreLocked(int64_t idx) {
   }
   uint64_t fid = e->spill_file, foff = e->spill_off;
   uint8_t* dst = base_ + off;
+  e->offset = off;  // the block is owned by this entry while the lock is dropped (crash recovery)
   Unlock();
   bool ok = true;
   int fd = open(SpillPath(fid).c_str(), O_RDONLY);

@@ -148,6 +148,13 @@ struct Header {
   uint64_t gc_requests;        // bumped by a starved create: the node broadcasts a global GC
   uint64_t oom_waits_total;    // creates that had to wait for memory
   uint64_t oom_errors_total;   // creates that failed after the grace period
+  // crash consistency: the pid holding the mutex (0 when free). A process killed inside a critical
+  // section leaves its pid here; the next locker gets EOWNERDEAD and rebuilds the metadata
+  // (Store::Recover), counted in recoveries_total.
+  int32_t lock_pid;
+  int32_t pad1;
+  uint64_t recoveries_total;
+  uint64_t recovered_dropped_total;  // entries the rebuild could not validate (lost objects)
   Stats stats;
 };
 
@@ -228,12 +235,22 @@ class Store {
   // Allocator self-check (used by tests): verifies heap walk + free lists. Returns free bytes.
   uint64_t CheckHeap();
   void Wake();
+  uint64_t Recoveries() const { return __atomic_load_n(&hdr_->recoveries_total, __ATOMIC_ACQUIRE); }
+  uint64_t RecoveredDropped() const { return hdr_->recovered_dropped_total; }
+  // Test hook: SIGKILL this process at crash point `p` (1 = mid heap split, 2 = mid heap merge,
+  // 3 = mid table insert, 4 = mid LRU unlink), i.e. while holding the store mutex in the middle
+  // of a multi-word metadata update. 0 disables. Process-local.
+  static void SetCrashPointForTest(int p);
 
  private:
   Store() = default;
   // All Locked* helpers require hdr_->mu held.
   void Lock();
   void Unlock();
+  void OnLocked(int rc);
+  // Rebuild allocator, object table, LRU list, spill-file refcounts and derived statistics from
+  // the entries that validate, after `dead_pid` died holding the lock (mutex already consistent).
+  void Recover(int dead_pid);
   int64_t Find(const ObjectId& id);
   int64_t Insert(const ObjectId& id);
   void RemoveEntry(int64_t idx);

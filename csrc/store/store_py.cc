@@ -392,6 +392,9 @@ PYBIND11_MODULE(_store, m) {
       .def("base_address", [](PyStore& self) { return reinterpret_cast<uintptr_t>(self.s->Base()); })
       .def("mapped_size", [](PyStore& self) { return self.s->MappedSize(); })
       .def("check_heap", [](PyStore& self) { return self.s->CheckHeap(); })
+      .def("recoveries", [](PyStore& self) { return self.s->Recoveries(); })
+      .def("recovered_dropped", [](PyStore& self) { return self.s->RecoveredDropped(); })
+      .def_static("set_crash_point_for_test", &rmm::Store::SetCrashPointForTest)
       .def("list_objects", [](PyStore& self) {
         py::list out;
         static const char* names[] = {"EMPTY", "CREATING", "SEALED", "SPILLING", "SPILLED", "RESTORING", "TOMBSTONE"};

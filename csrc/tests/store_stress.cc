@@ -9,6 +9,10 @@
 // lifecycle paths of csrc/store/shm_store.cc directly: create -> seal -> get/release -> delete,
 // proactive and explicit spilling, restore-on-get, sealed-notification polling, batched wait.
 //
+// Then a crash phase: for each Store::SetCrashPointForTest point a forked child attaches, and is
+// SIGKILLed while holding the store mutex in the middle of a multi-word update; the parent's next
+// lock recovers (Store::Recover) and the heap self-check and every surviving payload must pass.
+//
 // usage: store_stress <spill_dir> [threads] [iters]
 #include <atomic>
 #include <cstdio>
@@ -19,6 +23,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include "../store/shm_store.h"
@@ -135,6 +140,56 @@ int main(int argc, char** argv) {
   stop = true;
   s->Wake();
   waiter.join();
+
+  // ---- crash phase: a client killed inside the critical section, the parent recovers
+  long crash_bad = 0;
+  for (int point = 1; point <= 4; point++) {
+    ObjectId a = Id(10000 + point * 4), b = Id(10001 + point * 4), c = Id(10002 + point * 4),
+             d = Id(10003 + point * 4);
+    for (ObjectId x : {a, b, c}) {
+      bool ex = false;
+      uint8_t* p = s->CreateObject(x, 4096, 0, 0, 0, &ex);
+      if (p) {
+        std::memset(p, 0x3c, 4096);
+        s->Seal(x);
+        s->Release(x);
+      }
+    }
+    s->Delete(a);
+    pid_t pid = fork();
+    if (pid == 0) {
+      Store* cs = Store::Attach(name);
+      Store::SetCrashPointForTest(point);
+      bool ex = false;
+      Store::View v;
+      if (point == 1 || point == 3) (void)cs->CreateObject(d, 2048, 0, 0, 0, &ex);
+      else if (point == 2) cs->Delete(b);  // merges with the free block `a` left
+      else (void)cs->Get(c, 0, &v);        // unpins from the LRU list
+      _exit(3);                            // crash point not reached
+    }
+    int status = 0;
+    waitpid(pid, &status, 0);
+    const uint64_t rec = s->Recoveries();
+    if (!(WIFSIGNALED(status) && WTERMSIG(status) == SIGKILL)) crash_bad++;
+    (void)s->Contains(c);  // first lock after the kill: EOWNERDEAD -> Recover
+    if (s->Recoveries() != rec + 1) crash_bad++;
+    try {
+      s->CheckHeap();
+    } catch (const std::runtime_error&) {
+      crash_bad++;
+    }
+    Store::View v;
+    if (s->Get(c, 0, &v)) {
+      if (v.data_size != 4096 || v.data[0] != 0x3c || v.data[4095] != 0x3c) crash_bad++;
+      s->Release(c);
+    } else {
+      crash_bad++;
+    }
+    for (ObjectId x : {a, b, c, d}) s->Delete(x);  // the final num_objects == 0 check catches leaks
+  }
+  std::printf("crash phase: recoveries=%lu dropped=%lu bad=%ld\n", (unsigned long)s->Recoveries(),
+              (unsigned long)s->RecoveredDropped(), crash_bad);
+  g_bad += crash_bad;
 
   uint64_t free_before = s->CheckHeap();
   for (int k = 0; k < kKeys; k++) s->Delete(Id(k));

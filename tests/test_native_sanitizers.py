@@ -66,6 +66,10 @@ def test_object_store_concurrent_lifecycle(tmp_path, san):
     line = next(ln for ln in report.splitlines() if ln.startswith("spilled="))
     stats = dict(kv.split("=") for kv in line.split())
     assert int(stats["spilled"]) > 0 and int(stats["restored"]) > 0, report
+    # clients SIGKILLed holding the store mutex mid-update (4 crash points): recovered every time
+    crash = next(ln for ln in report.splitlines() if ln.startswith("crash phase:"))
+    cs = dict(kv.split("=") for kv in crash.split(":", 1)[1].split())
+    assert int(cs["recoveries"]) >= 4 and int(cs["bad"]) == 0, crash
 
 
 def test_scheduler_fuzz_resource_conservation(tmp_path):
