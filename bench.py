@@ -11,15 +11,23 @@ synthetic 84x84 frames, sample-batch GPU ingest + GAE HIP scan"):
 
 * ``PPO`` with ``num_learner_workers=N``: N learner ACTORS, one per GPU, each running the fused
   bf16 learner (HIP graphs, MFMA kernels) and all-reducing gradients over RCCL (xGMI);
-* CPU rollout-worker ACTORS stepping the numpy-vectorised synthetic Atari env on their CPU, with the
-  policy on the worker's slice of the learner GPU (RLlib ``num_gpus_per_worker > 0``; default
-  ``--rollout hybrid``): every env step is one HIP-graph replay (pinned H2D obs copy → K10 trunk →
-  K13 dense → K16 heads + Gumbel sampling → D2H actions), 2 workers x 25 envs x 100 steps = 5000
-  samples per learner per iteration (atari-ppo.yaml: train_batch_size 5000, rollout_fragment_length
-  100, sgd_minibatch_size 500, num_sgd_iter 10; its 10 workers x 5 envs layout is what
-  ``--rollout cpu`` runs, with the policy on the worker CPUs as num_gpus_per_worker: 0 does);
-* fragments travel rollout worker → shared-memory object store → learner, where they are DMA'd
-  onto the GPU and GAE + advantage standardisation run as one kernel (K17).
+* CPU rollout-worker ACTORS stepping the synthetic Atari vector env (native env core) on their CPU,
+  with the policy on the worker's slice of the learner GPU (RLlib ``num_gpus_per_worker > 0``;
+  default ``--rollout hybrid``): the whole fragment loop runs in C++ (csrc/hip/rollout_loop.cc) and
+  every env step is one HIP-graph launch (K10 trunk reading the newest frames from mapped pinned
+  memory → K13s dense → K16 heads + Gumbel sampling → actions into mapped pinned memory); ONE worker
+  x 50 envs x 100 steps = 5000 samples per learner per iteration (atari-ppo.yaml: train_batch_size
+  5000, rollout_fragment_length 100, sgd_minibatch_size 500, num_sgd_iter 10; its 10 workers x 5
+  envs layout is what ``--rollout cpu`` runs, with the policy on the worker CPUs as
+  num_gpus_per_worker: 0 does);
+* fragments stay in HBM: rollout worker → HBM object store (hipIPC, same GPU) → learner, where
+  GAE + advantage standardisation run as one kernel (K17); with N learners the gradient bucket is
+  all-reduced by the peer-memory kernel (csrc/hip/peer_allreduce.hip) inside the chained SGD graph.
+
+``--dtype bf16`` (default): bf16 MFMA kernels with fp32 master weights / Adam moments. ``--dtype fp32``:
+the precision-matched learner (fp32 weights, gradients and convolutions, as the reference's fp32
+torch PPO) and an fp32 rollout policy; at N=1 the bf16 run also reports it as
+``runtime_fp32_samples_per_s``.
 
 One timed step = one ``algo.train()`` iteration: sample 5000·N env steps, ingest, 10 epochs of
 500-sample minibatch SGD on every learner, publish weights. Weak scaling (per-GPU batch fixed).
@@ -209,7 +217,8 @@ def _runtime(args, n_gpus):
                          gpu_rollouts=args.rollout == "gpu")
                .training(train_batch_size=TRAIN_BATCH * n_gpus, sgd_minibatch_size=args.minibatch * n_gpus,
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
-                         vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99)
+                         vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99,
+                         compute_dtype=getattr(args, "dtype", "bf16"))
                .resources(num_learner_workers=n_gpus, num_cpus_per_worker=cpw,
                           num_gpus_per_learner_worker=(0.5 if args.rollout != "cpu" else 1.0) * phys / n_gpus,
                           # hybrid: CPU env, policy on the worker's slice of the learner's GPU
@@ -248,6 +257,9 @@ def main():
     ap.add_argument("--no-gpu-rollout", action="store_true",
                     help="skip the extra runtime measurement with GPU rollout actors")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="learner / GPU policy compute precision (fp32 = precision-matched with the reference)")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the extra fp32 runtime measurement (N=1)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every learner on GPU 0 (RCCL ranks get distinct host ids "
                          "and use the socket transport; or --dist-backend gloo)")
@@ -334,9 +346,15 @@ def main():
 
             import ray_memory_management_amd as ray
 
-            for mode in [m for m in ("cpu", "hybrid", "gpu") if m != args.rollout]:
+            modes = [m for m in ("cpu", "hybrid", "gpu") if m != args.rollout]
+            if args.dtype == "bf16" and not args.no_fp32:
+                modes.append("fp32")  # precision-matched learner + policy, same runtime path as `value`
+            for mode in modes:
                 a2 = copy.copy(args)
-                a2.rollout = mode
+                if mode == "fp32":
+                    a2.dtype = "fp32"
+                else:
+                    a2.rollout = mode
                 algo2 = None
                 try:
                     algo2, info2 = _runtime(a2, n_gpus)
@@ -344,8 +362,9 @@ def main():
                     for _ in range(args.steps):
                         algo2.train()
                     e2 = time.perf_counter() - t0
-                    extra[f"runtime_{mode}_rollout_samples_per_s"] = round(TRAIN_BATCH * n_gpus * args.steps / e2, 1)
-                    extra[f"runtime_{mode}_rollout_ms_per_step"] = round(e2 / args.steps * 1e3, 3)
+                    key = "runtime_fp32" if mode == "fp32" else f"runtime_{mode}_rollout"
+                    extra[f"{key}_samples_per_s"] = round(TRAIN_BATCH * n_gpus * args.steps / e2, 1)
+                    extra[f"{key}_ms_per_step"] = round(e2 / args.steps * 1e3, 3)
                 except Exception as ex:  # noqa: BLE001
                     print(f"[bench] {mode}-rollout runtime mode failed: {ex!r}", file=sys.stderr)
                     extra[f"runtime_{mode}_rollout_error"] = repr(ex)[:300]
@@ -375,7 +394,7 @@ def main():
         out = {
             "metric": METRIC, "value": round(sps, 1), "unit": "samples/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": round(sps / BASE_PPO, 3), "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": round(sps / BASE_PPO, 3), "dtype": args.dtype,
             "data": "synthetic 84x84x4 uint8 frames (vectorised synthetic Atari env), random-init weights",
             "config": {"model": "RLlib PPO VisionNetwork (Atari filters 16/32/256), atari-ppo.yaml hyper-parameters",
                        "global_batch": TRAIN_BATCH * n_gpus, "seq_len": args.fragment,

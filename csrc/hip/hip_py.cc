@@ -177,6 +177,12 @@ PYBIND11_MODULE(_hip, m) {
                         scale, S(stream), ctr ? P<const int64_t>(ctr) : nullptr, period);
   }, py::arg("src"), py::arg("idx"), py::arg("dst"), py::arg("B"), py::arg("C"), py::arg("H"), py::arg("W"),
      py::arg("scale"), py::arg("stream"), py::arg("ctr") = 0, py::arg("period") = 1);
+  m.def("frames_to_nhwc_f32", [](uint64_t src, uint64_t idx, uint64_t dst, int64_t B, int64_t C, int64_t H,
+                                 int64_t W, float scale, uint64_t stream, uint64_t ctr, int64_t period) {
+    frames_to_nhwc_f32(P<const uint8_t>(src), idx ? P<const int64_t>(idx) : nullptr, P<float>(dst), B, C, H, W, scale,
+                       S(stream), ctr ? P<const int64_t>(ctr) : nullptr, period);
+  }, py::arg("src"), py::arg("idx"), py::arg("dst"), py::arg("B"), py::arg("C"), py::arg("H"), py::arg("W"),
+     py::arg("scale"), py::arg("stream"), py::arg("ctr") = 0, py::arg("period") = 1);
   m.def("gae", [](uint64_t rew, uint64_t val, uint64_t done, uint64_t last, uint64_t adv, uint64_t ret,
                   int64_t T, int64_t B, float gamma, float lam, uint64_t stream) {
     gae(P<const float>(rew), P<const float>(val), P<const float>(done), P<const float>(last), P<float>(adv),
@@ -596,7 +602,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("rank", &PeerAllReduce::rank)
       .def_property_readonly("nblocks", &PeerAllReduce::nblocks)
       .def_property_readonly("cap_bytes", &PeerAllReduce::cap_bytes)
-      .def_property_readonly("uncached_signals", &PeerAllReduce::uncached_signals);
+      .def_property_readonly("uncached_signals", &PeerAllReduce::uncached_signals)
+      .def_property_readonly("alloc_attempts", &PeerAllReduce::alloc_attempts);
 
   // ---------------------------------------------------------------- RCCL (framework-owned communicator)
   m.def("rccl_load", &rccl_load, py::arg("path"));

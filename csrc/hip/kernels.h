@@ -29,6 +29,9 @@ void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, in
 void frames_to_nhwc_bf16(const uint8_t* src, const int64_t* idx, void* dst, int64_t B, int64_t C, int64_t H,
                          int64_t W, float scale, hipStream_t stream, const int64_t* ctr = nullptr,
                          int64_t period = 1);
+// fp32 output twin of K2b (precision-matched learner)
+void frames_to_nhwc_f32(const uint8_t* src, const int64_t* idx, float* dst, int64_t B, int64_t C, int64_t H,
+                        int64_t W, float scale, hipStream_t stream, const int64_t* ctr = nullptr, int64_t period = 1);
 
 // K3: GAE over time-major [T,B] fp32 tensors. dones is fp32 0/1 (1 = episode ended after t).
 // adv[t] = delta[t] + gamma*lam*(1-d[t])*adv[t+1];  ret = adv + values.

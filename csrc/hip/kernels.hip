@@ -178,6 +178,49 @@ void gather_rows(const void* in, const int64_t* idx, void* out, int64_t rows, in
 template <int C>
 __global__ __launch_bounds__(256) void k_frames_nhwc(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx0,
                                                     __hip_bfloat16* __restrict__ dst, int64_t B, int64_t HW,
+                                                    float scale, const int64_t* __restrict__ ctr, int64_t period);
+
+// fp32 twin of K2b for the precision-matched (fp32) learner: one float4 store per 4-channel pixel.
+template <int C>
+__global__ __launch_bounds__(256) void k_frames_nhwc_f32(const uint8_t* __restrict__ src,
+                                                        const int64_t* __restrict__ idx0, float* __restrict__ dst,
+                                                        int64_t B, int64_t HW, float scale,
+                                                        const int64_t* __restrict__ ctr, int64_t period) {
+  const int64_t* idx = offset_idx(idx0, ctr, period, B);
+  const int64_t total = B * HW;
+  for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < total;
+       p += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = p / HW, s = p - b * HW;
+    const int64_t sb = idx ? idx[b] : b;
+    const uint8_t* in = src + sb * C * HW + s;
+    if constexpr (C == 4) {
+      *reinterpret_cast<float4*>(dst + p * 4) =
+          make_float4(float(in[0]) * scale, float(in[HW]) * scale, float(in[2 * HW]) * scale, float(in[3 * HW]) * scale);
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; c++) dst[p * C + c] = float(in[c * HW]) * scale;
+    }
+  }
+}
+
+void frames_to_nhwc_f32(const uint8_t* src, const int64_t* idx, float* dst, int64_t B, int64_t C, int64_t H,
+                        int64_t W, float scale, hipStream_t stream, const int64_t* ctr, int64_t period) {
+  int64_t total = B * H * W;
+  if (total <= 0) return;
+  if (period <= 0) period = 1;
+  int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 32);
+  switch (C) {
+    case 1: hipLaunchKernelGGL(k_frames_nhwc_f32<1>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, dst, B, H * W, scale, ctr, period); break;
+    case 3: hipLaunchKernelGGL(k_frames_nhwc_f32<3>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, dst, B, H * W, scale, ctr, period); break;
+    case 4: hipLaunchKernelGGL(k_frames_nhwc_f32<4>, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, idx, dst, B, H * W, scale, ctr, period); break;
+    default: throw std::invalid_argument("frames_to_nhwc_f32: C must be 1, 3 or 4");
+  }
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void k_frames_nhwc(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx0,
+                                                    __hip_bfloat16* __restrict__ dst, int64_t B, int64_t HW,
                                                     float scale, const int64_t* __restrict__ ctr, int64_t period) {
   const int64_t* idx = offset_idx(idx0, ctr, period, B);
   const int64_t total = B * HW;

@@ -40,6 +40,7 @@ class PeerAllReduce {
   int nblocks() const { return nblocks_; }
   uint64_t cap_bytes() const { return cap_; }
   bool uncached_signals() const { return sig_uncached_; }
+  int alloc_attempts() const { return alloc_attempts_; }
   void Close();
 
  private:
@@ -52,6 +53,7 @@ class PeerAllReduce {
   int64_t* err_host_ = nullptr;  // mapped pinned host word the kernel reports timeouts to
   int64_t* err_dev_ = nullptr;
   bool sig_uncached_ = false;
+  int alloc_attempts_ = 0;
   bool open_ = false;
   char* peer_data_[kPeerMaxRanks] = {};
   uint64_t* peer_sig_[kPeerMaxRanks] = {};

@@ -34,6 +34,7 @@
 
 #include <cstring>
 #include <stdexcept>
+#include <vector>
 
 namespace rmm::hip {
 namespace {
@@ -251,7 +252,32 @@ PeerAllReduce::PeerAllReduce(int rank, int world, int device, uint64_t cap_bytes
   if (cap_ < 4096) cap_ = 4096;
   timeout_ticks_ = uint64_t(timeout_s > 0 ? timeout_s * 1e8 : 1e8);
   RMM_HIP_CHECK(hipSetDevice(device));
-  RMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&data_), 4 * cap_));
+  // The data region must be exportable: a process's first allocation has been seen to come back
+  // non-exportable (hipIpcGetMemHandle: invalid argument, 1 of 3 ranks sharing one MI355X), so
+  // probe the export here and retry with a fresh allocation (keeping the failed one until the end
+  // so the allocator cannot hand the same range back) before giving up.
+  {
+    std::vector<void*> rejected;
+    for (int attempt = 0; attempt < 4 && !data_; attempt++) {
+      void* p = nullptr;
+      const size_t bytes = size_t(4 * cap_) + (attempt ? (size_t(2) << 20) * size_t(attempt) : 0);
+      hipError_t e = attempt % 2 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocDefault) : hipMalloc(&p, bytes);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
+      hipIpcMemHandle_t probe;
+      if (hipIpcGetMemHandle(&probe, p) == hipSuccess) {
+        data_ = static_cast<char*>(p);
+        alloc_attempts_ = attempt + 1;
+      } else {
+        (void)hipGetLastError();
+        rejected.push_back(p);
+      }
+    }
+    for (void* p : rejected) (void)hipFree(p);
+    if (!data_) throw std::runtime_error("PeerAllReduce: no IPC-exportable device allocation");
+  }
   const size_t sig_bytes = size_t(2) * size_t(nblocks) * kPeerMaxRanks * sizeof(uint64_t);
   // flags in uncached (fine-grained) device memory: peers' remote stores and the local spin meet in
   // HBM, not in an XCD's L2

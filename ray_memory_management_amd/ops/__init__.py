@@ -135,30 +135,33 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor, rows: int = None, ctr: torch
 
 
 def frames_to_nhwc(x: torch.Tensor, idx: torch.Tensor = None, scale: float = 1.0 / 255.0, rows: int = None,
-                   ctr: torch.Tensor = None, period: int = 1) -> torch.Tensor:
+                   ctr: torch.Tensor = None, period: int = 1, dtype=torch.bfloat16) -> torch.Tensor:
     """uint8 frames [B, C, H, W] (rows optionally gathered by `idx`, or by the device-counter
-    window of idx as in gather_rows) → bf16 scaled, returned as a [B', C, H, W] tensor in
-    channels_last memory (what the NHWC conv kernels consume), one pass."""
+    window of idx as in gather_rows) → scaled `dtype` (bf16, or fp32 for the precision-matched
+    learner), returned as a [B', C, H, W] tensor in channels_last memory (what the NHWC conv
+    kernels consume), one pass."""
     if ctr is not None and (rows is None or idx is None):
         raise ValueError("frames_to_nhwc: idx and rows are required with ctr")
+    if dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError(f"frames_to_nhwc: bf16 or fp32 output, not {dtype}")
     if x.device.type != "cuda":
         if ctr is not None:
             idx = _counter_window(idx, rows, ctr, period)
         y = x[idx] if idx is not None else x
-        return (y.float() * scale).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return (y.float() * scale).to(dtype).contiguous(memory_format=torch.channels_last)
     h = require_hip()
     x = x.contiguous()
     B0, C, H, W = x.shape
     B = int(rows) if rows is not None else (idx.numel() if idx is not None else B0)
-    out = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=x.device)
+    out = torch.empty((B, H, W, C), dtype=dtype, device=x.device)
     if idx is not None:
         idx = idx.to(device=x.device, dtype=torch.int64).contiguous()
     if ctr is not None:
         assert ctr.dtype == torch.int64 and ctr.device == x.device and idx.numel() >= B * period
     if B:
-        h.frames_to_nhwc_bf16(x.data_ptr(), idx.data_ptr() if idx is not None else 0, out.data_ptr(), B, C, H, W,
-                              float(scale), _stream(x), ctr=ctr.data_ptr() if ctr is not None else 0,
-                              period=int(period))
+        fn = h.frames_to_nhwc_bf16 if dtype == torch.bfloat16 else h.frames_to_nhwc_f32
+        fn(x.data_ptr(), idx.data_ptr() if idx is not None else 0, out.data_ptr(), B, C, H, W, float(scale),
+           _stream(x), ctr=ctr.data_ptr() if ctr is not None else 0, period=int(period))
     return out.permute(0, 3, 1, 2)
 
 

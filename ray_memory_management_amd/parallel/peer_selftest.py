@@ -96,6 +96,7 @@ def _rank_main(rank, world, path, out_dir, bench_iters, sweep=False):
     res = {"rank": rank, "device": dev, "cases": {}}
     comm = PeerComm(store, rank, world, key="t", device=dev, cap_bytes=1 << 20)
     res["uncached_signals"] = bool(comm._c.uncached_signals)
+    res["alloc_attempts"] = int(comm._c.alloc_attempts)
 
     def case(name, n, dtype, seed, algo=0):
         xs = _inputs(n, dtype, world, seed, d)

@@ -52,6 +52,10 @@ class AlgorithmConfig:
         self.recreate_failed_workers = False
         # MI355X fast path: on-device vectorised env + fused learner
         self.gpu_rollouts = False
+        # GPU compute precision of the fused learner and the GPU rollout policy: "bf16" (fp32 master
+        # weights + moments, bf16 MFMA kernels) or "fp32" (precision-matched with the reference's
+        # fp32 torch PPO: fp32 weights, gradients and convolutions end to end)
+        self.compute_dtype = "bf16"
         # learner actors: one data-parallel learner per GPU, gradients all-reduced over RCCL
         # (0 = one learner in the driver process, the reference's default)
         self.num_learner_workers = 0

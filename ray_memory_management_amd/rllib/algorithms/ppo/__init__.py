@@ -100,7 +100,8 @@ class PPO(Algorithm):
                     entropy_coeff=c.entropy_coeff, lr=c.lr, train_batch_size=c.train_batch_size // n_learners,
                     sgd_minibatch_size=c.sgd_minibatch_size // n_learners, num_sgd_iter=c.num_sgd_iter,
                     grad_clip=c.grad_clip, lr_schedule=c.lr_schedule,
-                    entropy_coeff_schedule=c.entropy_coeff_schedule)
+                    entropy_coeff_schedule=c.entropy_coeff_schedule,
+                    compute_dtype=getattr(c, "compute_dtype", "bf16"))
 
     def _setup_learner(self):
         from ray_memory_management_amd.rllib.ppo_learner import PPOLearner

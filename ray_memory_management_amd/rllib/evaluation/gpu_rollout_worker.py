@@ -42,7 +42,8 @@ class GPURolloutWorker:
         torch.manual_seed(s)
         model = build_model(self.env.observation_space, self.env.action_space, self.config.get("model") or {})
         # bf16 inference weights in the layout the fused kernels read
-        self.model = model.to(self.device).to(torch.bfloat16).to(memory_format=torch.channels_last)
+        cdt = torch.float32 if str(self.config.get("compute_dtype", "bf16")) in ("fp32", "float32") else torch.bfloat16
+        self.model = model.to(self.device).to(cdt).to(memory_format=torch.channels_last)
         self.T = int(self.config.get("rollout_fragment_length", 200))
         self.sampler = GPURolloutSampler(self.env, self.model, fragment=self.T, seed=s)
         self._ep_len = np.zeros(n, dtype=np.int64)
@@ -367,7 +368,8 @@ class HybridRolloutWorker(GPURolloutWorker):
         torch.cuda.set_device(0)
         torch.manual_seed(s)
         model = build_model(self.env.observation_space, self.env.action_space, self.config.get("model") or {})
-        self.model = model.to(self.device).to(torch.bfloat16).to(memory_format=torch.channels_last)
+        cdt = torch.float32 if str(self.config.get("compute_dtype", "bf16")) in ("fp32", "float32") else torch.bfloat16
+        self.model = model.to(self.device).to(cdt).to(memory_format=torch.channels_last)
         self.T = int(self.config.get("rollout_fragment_length", 200))
         self.n = n
         probe = torch.zeros((1,) + tuple(np.asarray(self.env.vector_reset()).shape[1:]), dtype=torch.uint8,

@@ -130,7 +130,9 @@ class LearnerActor:
         for p in L.params:
             layout.append((names[id(p)], off, tuple(p.shape), tuple(p.stride())))
             off += p.numel()
-        return {"__rmm_flat_bf16__": L.w_bf16.detach().clone(), "__rmm_layout__": layout}
+        # bf16 compute weights, or the fp32 master for a precision-matched (compute_dtype fp32) learner
+        flat = L.w_bf16 if L.w_bf16 is not None else L.master
+        return {"__rmm_flat_bf16__": flat.detach().clone(), "__rmm_layout__": layout}
 
     def set_weights(self, w):
         self.learner.set_weights(w)

@@ -42,7 +42,7 @@ DEFAULT_PPO = dict(
     vf_loss_coeff=1.0, entropy_coeff=0.01, lr=5e-5, train_batch_size=5000, sgd_minibatch_size=500,
     num_sgd_iter=10, grad_clip=None, standardize_advantages=True, use_graphs=True, fused=True,
     allreduce_in_graph=False, adam_betas=(0.9, 0.999), adam_eps=1e-8, weight_decay=0.0,
-    lr_schedule=None, entropy_coeff_schedule=None, manual_step=True,
+    lr_schedule=None, entropy_coeff_schedule=None, manual_step=True, compute_dtype="bf16",
 )
 
 _LOSS_KEYS = (SampleBatch.OBS, SampleBatch.ACTIONS, SampleBatch.ACTION_LOGP, SampleBatch.ACTION_DIST_INPUTS,
@@ -220,8 +220,13 @@ class PPOLearner:
         n = sum(p.numel() for p in params)
         self.n_params = n
         # fp32 master + moments (flat), bf16 compute weights (flat; params become views into it)
+        # compute_dtype "fp32" (precision-matched with the reference's fp32 PPO): the parameters ARE
+        # views of the fp32 master, gradients land in an fp32 bucket, K6 updates the master only
+        self.fp32 = str(self.cfg.get("compute_dtype", "bf16")) in ("fp32", "float32")
+        self.cdt = torch.float32 if self.fp32 else torch.bfloat16
+        self.grad_bf16 = not self.fp32
         self.master = torch.empty(n, dtype=torch.float32, device=dev)
-        self.w_bf16 = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        self.w_bf16 = None if self.fp32 else torch.empty(n, dtype=torch.bfloat16, device=dev)
         off = 0
         self.params = []
         with torch.no_grad():
@@ -229,14 +234,15 @@ class PPOLearner:
                 k = p.numel()
                 # lay the master out in the param's MEMORY order so one flat kernel updates both
                 self.master.as_strided(p.size(), p.stride(), off).copy_(p.detach().float())
-                view = self.w_bf16.as_strided(p.size(), p.stride(), off)
-                view.copy_(p.detach())
+                view = (self.master if self.fp32 else self.w_bf16).as_strided(p.size(), p.stride(), off)
+                if not self.fp32:
+                    view.copy_(p.detach())
                 p.data = view
                 self.params.append(p)
                 off += k
         self.m1 = torch.zeros(n, dtype=torch.float32, device=dev)
         self.m2 = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.flat_grad = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        self.flat_grad = torch.zeros(n, dtype=self.cdt, device=dev)
         # each param's slice of the flat bucket: fused backward kernels (K10 trunk, K8b dense) write
         # their gradients there directly and the bucket copy skips them
         off = 0
@@ -263,13 +269,17 @@ class PPOLearner:
         self._parity_last = False
         self._bump_done = torch.zeros(require_hip().bump_done_words(), dtype=torch.int32, device=dev)
         self._one = torch.ones((), dtype=torch.float32, device=dev)
-        self.heads_ok = hasattr(self.model, "forward_heads")
+        self.heads_ok = hasattr(self.model, "forward_heads") and not self.fp32  # K5c reads bf16 heads
         # global-norm gradient clipping on the device (K6b → K6 scale pointer), graph-capturable
         self.clip_ws = self.clip_out = None
         if self.cfg["grad_clip"]:
             self.clip_ws = torch.zeros(require_hip().grad_clip_workspace_floats(), dtype=torch.float32, device=dev)
             self.clip_out = torch.ones(2, dtype=torch.float32, device=dev)
         self._manual = self._manual_layout()
+
+    def _wptr(self) -> int:
+        """K6's bf16 weight output (0 for the fp32 learner: its parameters are the master)."""
+        return self.w_bf16.data_ptr() if self.w_bf16 is not None else 0
 
     def _bucket_order(self, params):
         """Flat-bucket order: for the Nature-CNN layout the trunk (conv) parameters first, then
@@ -294,6 +304,8 @@ class PPOLearner:
         from ray_memory_management_amd.rllib.models import VisionNetwork
 
         m = self.model
+        if self.fp32:  # the hand-written SGD-step kernels (K10 / K12 / K13 / K15) compute in bf16
+            return None
         if not (self.cfg.get("manual_step", True) and isinstance(m, VisionNetwork) and m.nature
                 and m.dense_tail is not None and not os.environ.get("RMM_NO_MANUAL_STEP")):
             return None
@@ -389,7 +401,7 @@ class PPOLearner:
             return []
         c = self.ctr.data_ptr()
         return [self.flat_grad.data_ptr(), self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(),
-                self.w_bf16.data_ptr(), self.hp.data_ptr(), c + 8, c if bump else 0, 2 if bump else 0,
+                self._wptr(), self.hp.data_ptr(), c + 8, c if bump else 0, 2 if bump else 0,
                 self._bump_done.data_ptr() if bump else 0]
 
     def _opt_launch(self):
@@ -398,13 +410,13 @@ class PPOLearner:
         h = require_hip()
         scale_ptr = 0
         if self.clip_out is not None:
-            h.grad_clip_coef(self.flat_grad.data_ptr(), True, self.n_params, 1.0 / self.world,
+            h.grad_clip_coef(self.flat_grad.data_ptr(), self.grad_bf16, self.n_params, 1.0 / self.world,
                              float(self.cfg["grad_clip"]), self.clip_ws.data_ptr(), self.clip_out.data_ptr(),
                              _stream())
             scale_ptr = self.clip_out.data_ptr()
         cur = self._ctr()
-        args = (self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(), True,
-                self.w_bf16.data_ptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream())
+        args = (self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(),
+                self.grad_bf16, self._wptr(), self.hp.data_ptr(), 1.0 / self.world, self.n_params, _stream())
         if self._parity and not (self._parity_last and self._par == 0):
             # chained graph: advance into the other copy from one lane (see __init__)
             h.adam_flat(*args, step_ctr=cur.data_ptr() + 8, bump=cur.data_ptr(), nbump=2, scale_ptr=scale_ptr,
@@ -420,7 +432,7 @@ class PPOLearner:
         h = require_hip()
         f4, b2 = 4 * lo, 2 * lo
         h.adam_flat(self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
-                    self.flat_grad.data_ptr() + b2, True, self.w_bf16.data_ptr() + b2, self.hp.data_ptr(),
+                    self.flat_grad.data_ptr() + b2, True, self._wptr() + b2, self.hp.data_ptr(),
                     1.0 / self.world, hi - lo, stream, step_ctr=self.ctr.data_ptr() + 8,
                     bump=self.ctr.data_ptr() if bump else 0, nbump=2 if bump else 0,
                     done=self._bump_done.data_ptr() if bump else 0, max_blocks=max_blocks)
@@ -510,7 +522,7 @@ class PPOLearner:
         if fused:  # K10: gather + both convs inside one MFMA kernel
             x = None
         elif frames:
-            x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
+            x = ops.frames_to_nhwc(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period, dtype=self.cdt)
         else:  # vector observations (e.g. CartPole): plain row gather
             x = ops.gather_rows(full["obs"], full["idx"], rows=mbs, ctr=ctr, period=period)
         cols = None if fused else ops.gather_rows(full["cols"], full["idx"], rows=mbs, ctr=ctr, period=period)
@@ -541,8 +553,9 @@ class PPOLearner:
         segs = []
         off = 0
         for g, p in zip(grads, self.params):
-            nb = g.numel() * 2
-            dst = self.flat_grad.data_ptr() + off * 2
+            esz = self.flat_grad.element_size()
+            nb = g.numel() * esz
+            dst = self.flat_grad.data_ptr() + off * esz
             if g.data_ptr() != dst:  # fused backward kernels already wrote into the bucket
                 segs.append((g.data_ptr(), dst, nb))
             off += p.numel()
@@ -595,7 +608,8 @@ class PPOLearner:
         return {"obs": obs.contiguous(), "cols": cols, "idx": idx, "A": A, "mbs": mbs, "period": iters * nmb}
 
     def _capture(self, full):
-        saved = (self.master.clone(), self.m1.clone(), self.m2.clone(), self.w_bf16.clone(), self.ctr.clone(),
+        saved = (self.master.clone(), self.m1.clone(), self.m2.clone(),
+                 self.w_bf16.clone() if self.w_bf16 is not None else None, self.ctr.clone(),
                  self.acc.clone())
         manual = self._manual_ok(full)
         s = torch.cuda.Stream(self.device)
@@ -702,7 +716,8 @@ class PPOLearner:
                 self._fast_step(full, False)
             self._graph = g
         for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc), saved):
-            dst.copy_(src)  # undo warm-up updates
+            if dst is not None:
+                dst.copy_(src)  # undo warm-up updates
 
     def _sgd_chain(self, total: int) -> int:
         """SGD steps captured per graph (world of one): the largest divisor of the update's step

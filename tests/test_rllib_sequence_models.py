@@ -231,3 +231,21 @@ def test_appo_attention_learns_memory_task(ray_shared):
                   "attention_memory_inference": 10, "attention_memory_training": 10, "attention_num_heads": 2,
                   "attention_head_dim": 16}, 90, 15)
     assert best >= 15, best
+
+
+@pytest.mark.gpu
+def test_ppo_lstm_gpu_learner(ray_shared):
+    """The sequence learner on the GPU (driver-side learner with num_gpus=1)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
+
+    algo = (PPOConfig().environment("RepeatAfterMe-v0", env_config={"episode_len": 50})
+            .rollouts(num_rollout_workers=2, num_envs_per_worker=4, rollout_fragment_length=100)
+            .training(train_batch_size=800, sgd_minibatch_size=200, num_sgd_iter=8, lr=3e-3, lambda_=0.95,
+                      gamma=0.5, vf_loss_coeff=0.5, kl_coeff=0.0, clip_param=0.2, entropy_coeff=0.0,
+                      model={"fcnet_hiddens": [32], "use_lstm": True, "lstm_cell_size": 32, "max_seq_len": 10})
+            .resources(num_gpus=1).debugging(seed=0)).build()
+    assert algo.learner.device.type == "cuda" and algo.learner.recurrent
+    best = _best(algo, 25, 40)
+    assert best >= 40, best

@@ -1,0 +1,11 @@
+# Round 4 (b): precision tests, sequence-model GPU learner, peer sweep at 3 ranks, fp32 + bf16 bench.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_rllib_precision_gpu.py tests/test_rllib_sequence_models.py -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_r4b.log 2>&1 || { tail -40 gpurun_out/pytest_r4b.log; exit 1; }
+grep -E "PASSED|FAILED|^bf16|^fp32|passed|failed" gpurun_out/pytest_r4b.log | tail -8
+timeout -k 10 300 python -u -m ray_memory_management_amd.parallel.peer_selftest --world 3 --sweep --iters 100 --out gpurun_out/sweep3 > gpurun_out/sweep3.log 2>&1 || { tail -5 gpurun_out/sweep3.log; exit 1; }
+python3 -c "
+import json;d=json.load(open('gpurun_out/sweep3/rank0.json'))
+for r in d['sweep']: print(r)"
+timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 --no-putget > gpurun_out/bench_r4b.log 2>&1 || { tail -30 gpurun_out/bench_r4b.log; exit 1; }
+grep '"metric"' gpurun_out/bench_r4b.log | tail -1 | cut -c1-2500
