@@ -61,7 +61,8 @@ class _WorkerConn:
 
 
 class _Lease:
-    __slots__ = ("lease_id", "conn", "node", "gpu_ids", "key", "tasks", "blocked", "lineage", "idle_since")
+    __slots__ = ("lease_id", "conn", "node", "gpu_ids", "key", "tasks", "blocked", "lineage", "idle_since", "sent",
+                 "last_ack")
 
     def __init__(self, lease_id, conn, node, gpu_ids, key, lineage=True):
         self.lease_id, self.conn, self.node, self.gpu_ids, self.key = lease_id, conn, node, gpu_ids, key
@@ -69,16 +70,19 @@ class _Lease:
         self.idle_since = 0.0
         self.tasks: Dict[bytes, list] = {}  # task_id -> [spec, keep, attempt] pushed to the worker
         self.blocked = False  # the worker's running task blocked in get(): push nothing more
+        self.sent: Dict[bytes, float] = {}  # task_id -> push time (service-time estimate)
+        self.last_ack = 0.0
 
 
 class _KeyState:
-    __slots__ = ("queue", "leases", "pending", "runtime_env")
+    __slots__ = ("queue", "leases", "pending", "runtime_env", "svc")
 
     def __init__(self, runtime_env):
         self.queue: "collections.deque" = collections.deque()
         self.leases: List[_Lease] = []
         self.pending = 0
         self.runtime_env = runtime_env
+        self.svc = -1.0  # EMA of this key's task service time (s); -1 until the first completion
 
 
 class DirectTaskSubmitter:
@@ -87,6 +91,10 @@ class DirectTaskSubmitter:
         # pipelining depth per leased worker: hides the owner's ack → push turnaround (a worker whose
         # task blocks in get() bounces the queued rest back, so nesting cannot deadlock)
         self.depth = max(1, int(max_tasks_in_flight))
+        # ...but only for SHORT tasks: a pipelined task waits behind its lease's running one, which for
+        # long tasks serialises work that fresh leases would run in parallel (reference Ray 2.0 keeps
+        # max_tasks_in_flight_per_worker = 1). Keys whose tasks take longer than this stay 1 deep.
+        self.deepen_max_s = float(worker.config.get("direct_task_pipeline_max_task_ms", 2.0)) / 1000.0
         self.lock = threading.RLock()
         self.keys: Dict[tuple, _KeyState] = {}
         self.conns: Dict[str, _WorkerConn] = {}
@@ -219,9 +227,10 @@ class DirectTaskSubmitter:
         want = min(len(ks.queue), self.max_pending_leases) - ks.pending
         for _ in range(max(0, want)):
             self._request_lease(sk, ks)
-        # 3) deepen pipelines only with more work queued than lease requests in flight: a few
-        #    long tasks spread over fresh workers, a stream of tiny ones fills the pipelines
-        if len(ks.queue) > ks.pending:
+        # 3) deepen pipelines only with more work queued than lease requests in flight, and only for
+        #    short tasks: a few long tasks spread over fresh workers, a stream of tiny ones fills the
+        #    pipelines
+        if len(ks.queue) > ks.pending and 0.0 <= ks.svc < self.deepen_max_s:
             self._fill(ks, self.depth)
 
     def _fill(self, ks: _KeyState, depth: int):
@@ -260,6 +269,7 @@ class DirectTaskSubmitter:
             lease.idle_since = 0.0
             self.idle_leases -= 1
         lease.tasks[tid] = item
+        lease.sent[tid] = time.perf_counter()
         self.inflight[tid] = lease
         fid = spec["fn_id"]
         blob = None
@@ -301,7 +311,7 @@ class DirectTaskSubmitter:
                 if ks.leases or ks.pending > 0:
                     # other leases of this key are live or still on their way: they run the queue
                     # (pipelined), as the head path would keep the tasks waiting
-                    self._fill(ks, self.depth)
+                    self._fill(ks, self.depth if 0.0 <= ks.svc < self.deepen_max_s else 1)
                 else:
                     self._fail_queue(ks, exc.RaySystemError(f"worker lease failed: {reply!r}"))
             return
@@ -337,6 +347,12 @@ class DirectTaskSubmitter:
                 item = lease.tasks.pop(tid)
                 ks = self.keys[lease.key]
                 touched[id(ks)] = (lease.key, ks)
+                now = time.perf_counter()
+                t_sent = lease.sent.pop(tid, now)
+                if status not in ("requeue", "retry"):  # service time: since push or the previous finish
+                    svc = now - max(t_sent, lease.last_ack)
+                    ks.svc = svc if ks.svc < 0 else 0.8 * ks.svc + 0.2 * svc
+                    lease.last_ack = now
                 if status == "requeue":  # bounced unstarted by a worker whose running task blocked
                     lease.blocked = True
                     ks.queue.appendleft(item)

@@ -113,6 +113,12 @@ def process_store(worker, device: int):
         s = h.GpuStore(device, cap, slab, worker.store_name, bool(cfg.get("gpu_spill_compression", True)),
                        float(cfg.get("gpu_object_spilling_threshold", 0.0)))
         stores[device] = s
+        try:  # occupancy / spill counters for the dashboard's GPU reporter (internal KV)
+            from ray_memory_management_amd.dashboard.gpu_reporter import publish_store_stats
+
+            publish_store_stats(worker)
+        except Exception:  # noqa: BLE001 - reporting is best effort
+            pass
     return s
 
 

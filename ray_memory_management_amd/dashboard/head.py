@@ -3,7 +3,8 @@ APIs.
 
 Parity: reference dashboard/head.py + dashboard/modules/{state (state_head.py: /api/v0/{actors,
 tasks,objects,nodes,workers,jobs,placement_groups} + summaries), node (/nodes),
-reporter (/api/cluster_status, Prometheus metrics), job (job_head.py: REST job submission
+reporter (/api/cluster_status, Prometheus metrics, per-GPU utilization / HBM and GPU object-store
+occupancy + spill state: /api/gpus, dashboard/gpu_reporter.py), job (job_head.py: REST job submission
 /api/jobs/ — submit / list / info / logs / stop / delete), log (/api/v0/logs),
 healthz (/api/gcs_healthz)}. The reference dashboard also ships a React UI; this one serves JSON
 and Prometheus text only.
@@ -100,6 +101,9 @@ class DashboardHead:
             sid, int(q.get("offset", ["0"])[0]))})
         r("POST", r"/api/jobs/(?P<sid>[^/]+)/stop", lambda q, b, sid: {"stopped": self._job_client().stop_job(sid)})
         r("DELETE", r"/api/jobs/(?P<sid>[^/]+)", lambda q, b, sid: {"deleted": self._job_client().delete_job(sid)})
+        # GPUs (reference reporter_agent.py _get_gpu_usage) + GPU object stores
+        r("GET", r"/api/gpus", lambda q, b: {"gpus": _gpu().gpu_devices(),
+                                             "gpu_object_stores": _gpu().gpu_object_stores()})
         # metrics (Prometheus text)
         r("GET", r"/metrics", self._metrics)
 
@@ -113,7 +117,9 @@ class DashboardHead:
     def _cluster_status(self, q, b):
         w = _w()
         return {"cluster_resources": w.cluster_resources(), "available_resources": w.available_resources(),
-                "summary": w._state("summary"), "uptime_s": time.time() - self.started}
+                "summary": w._state("summary"), "uptime_s": time.time() - self.started,
+                "gpus": _gpu().gpu_devices(),
+                "gpu_object_stores": [s for s in _gpu().gpu_object_stores() if s.get("alive")]}
 
     def _list_logs(self, q, b):
         d = os.path.join(self.session_dir or "", "logs")
@@ -164,7 +170,7 @@ class DashboardHead:
     def _metrics(self, q, b):
         from ray_memory_management_amd.util import metrics
 
-        lines = [_builtin_metrics(), metrics.prometheus_text()]
+        lines = [_builtin_metrics(), _gpu().prometheus_lines(), metrics.prometheus_text()]
         return _Text("".join(lines), "text/plain; version=0.0.4")
 
     # ------------------------------------------------------------------ server
@@ -263,6 +269,12 @@ def _state():
     from ray_memory_management_amd.util import state
 
     return state
+
+
+def _gpu():
+    from ray_memory_management_amd.dashboard import gpu_reporter
+
+    return gpu_reporter
 
 
 def _internal():

@@ -199,3 +199,149 @@ def run_gpu_shuffle(num_workers: int = 2, rows_per_worker: int = 1 << 20, row_by
     return {"ok": all(r["ok"] for r in res) and sum(r["rows_out"] for r in res) == rows_per_worker * num_workers
             and sum(sums_in) % (1 << 61) == sum(r["key_sum"] for r in res) % (1 << 61),
             "GBps": total_bytes / secs / 1e9, "seconds": secs, "bytes": total_bytes, "workers": num_workers}
+
+
+# ================================================================== out-of-core (multi-round) shuffle
+def _payload(keys: torch.Tensor, row_bytes: int) -> torch.Tensor:
+    """Row payload derived from its key (so the reduce side can verify every byte after the block
+    was spilled, compressed, restored and moved): byte j of row i = low byte of (key_i * 0x9E3779B1 + j)."""
+    j = torch.arange(row_bytes, device=keys.device, dtype=torch.int64)
+    return ((keys.unsqueeze(1) * 0x9E3779B1 + j.unsqueeze(0)) & 0xFF).to(torch.uint8)
+
+
+class OutOfCoreShuffleWorker(ShuffleWorker):
+    """One rank of the multi-round Exoshuffle (reference python/ray/experimental/shuffle.py:152
+    simple_shuffle / :231 run, map → merge → reduce). Per round the rank generates its next input
+    block in HBM, and in ONE collective round K11 partitions it by destination rank, the all-to-all
+    exchanges the pieces over xGMI, and K11 partitions what arrived into this rank's P output
+    partitions — the merged map output of every mapper for this round. Each (round, partition)
+    block is ``ray.put`` into the HBM object store; once the store is at its quota it spills the
+    least recently used blocks to host memory (K4-compressed, pinned DMA). The reduce of partition
+    p gathers its blocks (restoring spilled ones) and sorts them by key on the GPU."""
+
+    def setup(self, partitions: int, row_bytes: int, rows_per_round: int, mode: str = "range"):
+        self.P, self.row_bytes, self.rows = int(partitions), int(row_bytes), int(rows_per_round)
+        self.mode = mode
+        self.blocks = [[] for _ in range(self.P)]
+        self.in_rows = 0
+        self.in_key_sum = 0
+        return True
+
+    def map_round(self, r: int):
+        import ray_memory_management_amd as ray
+
+        dev = self.device
+        t0 = time.perf_counter()
+        g = torch.Generator(device="cpu").manual_seed(7919 * (r + 1) + self.rank)
+        keys = torch.randint(0, 2 ** 62, (self.rows,), generator=g, dtype=torch.int64).to(dev)
+        vals = _payload(keys, self.row_bytes)
+        self.in_rows += int(keys.numel())
+        self.in_key_sum = (self.in_key_sum + int(keys.sum().item())) % (1 << 61)
+        if self.world > 1:
+            from ray_memory_management_amd.util.collective.collective import get_group_handle
+
+            pg = get_group_handle(self.group_name).pg
+            keys, vals = shuffle(keys, vals, group=pg, mode=self.mode, world_size=self.world, rank=self.rank)
+        # merge: this rank's P partitions of everything that arrived (global partition ids
+        # rank*P .. rank*P + P - 1 under the same range function)
+        k, v, counts = partition(keys, vals, self.world * self.P, self.mode)
+        cs = counts.tolist()[self.rank * self.P:(self.rank + 1) * self.P]
+        off = 0
+        for p, c in enumerate(cs):
+            self.blocks[p].append(ray.put((k[off:off + c].clone(), v[off:off + c].clone())))
+            off += c
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        return {"round": r, "seconds": time.perf_counter() - t0, "rows": int(k.numel())}
+
+    def reduce_partition(self, p: int):
+        import ray_memory_management_amd as ray
+
+        t0 = time.perf_counter()
+        parts = ray.get(self.blocks[p])
+        keys = torch.cat([x[0].to(self.device) for x in parts]) if parts else torch.empty(0, dtype=torch.int64)
+        vals = torch.cat([x[1].to(self.device) for x in parts]) if parts else torch.empty(0, dtype=torch.uint8)
+        del parts
+        keys, order = torch.sort(keys)
+        vals = vals[order]
+        gid = self.rank * self.P + p
+        dest_ok = bool((destinations(keys, self.world * self.P, self.mode) == gid).all().item()) if keys.numel() else True
+        payload_ok = bool(torch.equal(vals, _payload(keys, self.row_bytes))) if keys.numel() else True
+        sorted_ok = bool((keys[1:] >= keys[:-1]).all().item()) if keys.numel() > 1 else True
+        out = {"partition": gid, "rows": int(keys.numel()), "key_sum": int(keys.sum().item()) % (1 << 61),
+               "ok": dest_ok and payload_ok and sorted_ok, "payload_ok": payload_ok,
+               "seconds": time.perf_counter() - t0}
+        self.blocks[p] = []  # the partition's blocks are freed with their last reference
+        return out
+
+    def inputs(self):
+        return {"rows": self.in_rows, "key_sum": self.in_key_sum}
+
+    def gpu_store_stats(self):
+        from ray_memory_management_amd._private import gpu_object_store as gos
+        from ray_memory_management_amd._private.worker import global_worker
+
+        st = {int(k): dict(v) for k, v in gos.stats(global_worker).items()}
+        hs = global_worker.store.stats()  # the host shm store (spill target of HBM blocks / CPU blocks)
+        st[-1] = {"host_spilled_bytes_total": int(hs.get("bytes_spilled_total", 0)),
+                  "host_restored_bytes_total": int(hs.get("bytes_restored_total", 0))}
+        return st
+
+
+def run_out_of_core_gpu_shuffle(num_workers: int = 1, total_bytes: int = 16 << 30, rounds: int = 16,
+                                partitions_per_worker: int = 8, row_bytes: int = 248, backend: str = "nccl",
+                                mode: str = "range") -> dict:
+    """Driver API (BASELINE config #5): shuffle `total_bytes` of synthetic keyed rows through
+    `num_workers` GPU actors in `rounds` rounds, more data than their HBM object-store quota
+    (``gpu_object_store_memory``) holds, so partition blocks spill to host memory and are restored
+    for the reduce. Returns end-to-end GB/s, per-phase times, spilled / restored bytes and the
+    correctness checks (every row once, at its partition, payload intact, partitions sorted)."""
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd.util import collective as col
+
+    gpu = backend == "nccl"
+    row = 8 + int(row_bytes)
+    rows_per_round = max(1, int(total_bytes) // (num_workers * rounds * row))
+    Actor = ray.remote(num_gpus=1 if gpu else 0, num_cpus=1)(OutOfCoreShuffleWorker)
+    workers = [Actor.remote(r, num_workers, "cuda" if gpu else "cpu") for r in range(num_workers)]
+    try:
+        if num_workers > 1:
+            col.create_collective_group(workers, num_workers, list(range(num_workers)), backend=backend,
+                                        group_name=f"oocshuffle-{time.time_ns()}")
+        ray.get([w.setup.remote(partitions_per_worker, row_bytes, rows_per_round, mode) for w in workers])
+        t0 = time.perf_counter()
+        map_s = []
+        for r in range(rounds):
+            res = ray.get([w.map_round.remote(r) for w in workers])
+            map_s.append(max(x["seconds"] for x in res))
+        t_map = time.perf_counter() - t0
+        st_map = ray.get([w.gpu_store_stats.remote() for w in workers])
+        red = []
+        for p in range(partitions_per_worker):
+            red.extend(ray.get([w.reduce_partition.remote(p) for w in workers]))
+        elapsed = time.perf_counter() - t0
+        st_end = ray.get([w.gpu_store_stats.remote() for w in workers])
+        ins = ray.get([w.inputs.remote() for w in workers])
+    finally:
+        for w in workers:
+            ray.kill(w)
+    in_rows = sum(x["rows"] for x in ins)
+    in_sum = sum(x["key_sum"] for x in ins) % (1 << 61)
+    out_rows = sum(x["rows"] for x in red)
+    out_sum = sum(x["key_sum"] for x in red) % (1 << 61)
+
+    def tot(stats, key):
+        return sum(int(v.get(key, 0)) for s in stats for v in s.values())
+
+    data = in_rows * row
+    return {"ok": all(x["ok"] for x in red) and in_rows == out_rows and in_sum == out_sum,
+            "rows": in_rows, "bytes": data, "GBps": data / elapsed / 1e9, "seconds": elapsed,
+            "map_seconds": t_map, "reduce_seconds": elapsed - t_map, "rounds": rounds,
+            "partitions": partitions_per_worker * num_workers, "workers": num_workers,
+            "payload_ok": all(x["payload_ok"] for x in red),
+            "spilled_bytes": tot(st_end, "spilled_bytes_total"), "spilled_host_bytes": tot(st_end, "spilled_host_bytes_total"),
+            "restored_bytes": tot(st_end, "restored_bytes_total"), "spilled_after_map": tot(st_map, "spilled_bytes_total"),
+            "gpu_store_capacity": tot(st_end, "capacity"),
+            # one host store per node: every worker reports the same counters
+            "host_store_spilled_bytes": max(int(s.get(-1, {}).get("host_spilled_bytes_total", 0)) for s in st_end),
+            "host_store_restored_bytes": max(int(s.get(-1, {}).get("host_restored_bytes_total", 0)) for s in st_end)}

@@ -128,3 +128,54 @@ def test_rest_job_submission(dash, tmp_path):
     with pytest.raises(urllib.error.HTTPError) as e:
         urllib.request.urlopen(req, timeout=30)
     assert e.value.code == 400
+
+
+def _fake_sysfs(root):
+    import os
+
+    dev = root / "card0" / "device"
+    (dev / "hwmon" / "hwmon3").mkdir(parents=True)
+    for name, val in (("vendor", "0x1002"), ("mem_info_vram_total", str(288 << 30)),
+                      ("mem_info_vram_used", str(12 << 30)), ("mem_info_gtt_used", "4096"),
+                      ("gpu_busy_percent", "37"), ("uevent", "DRIVER=amdgpu\nPCI_SLOT_NAME=0000:75:00.0\n")):
+        (dev / name).write_text(val)
+    (dev / "hwmon" / "hwmon3" / "temp1_input").write_text("41000")
+    (dev / "hwmon" / "hwmon3" / "power1_average").write_text("350000000")
+    other = root / "card1" / "device"  # not an AMD GPU: skipped
+    other.mkdir(parents=True)
+    (other / "vendor").write_text("0x8086")
+    return os.fspath(root)
+
+
+def test_gpu_reporter_endpoints(tmp_path, monkeypatch):
+    """Per-GPU utilization / HBM (amdgpu sysfs) and GPU object-store occupancy in /api/gpus,
+    /api/cluster_status and /metrics (reference reporter_agent.py:92-98 GPU usage)."""
+    import os
+
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd import internal
+    from ray_memory_management_amd.dashboard import gpu_reporter
+
+    monkeypatch.setenv("RMM_SYSFS_DRM_ROOT", _fake_sysfs(tmp_path / "drm"))
+    devs = gpu_reporter.gpu_devices()
+    assert len(devs) == 1 and devs[0]["pci_bus_id"] == "0000:75:00.0" and devs[0]["busy_percent"] == 37
+    assert devs[0]["vram_used_bytes"] == 12 << 30 and devs[0]["temperature_c"] == 41.0 and devs[0]["power_w"] == 350.0
+    if ray.is_initialized():
+        ray.shutdown()
+    ctx = ray.init(num_cpus=2, include_dashboard=True, dashboard_port=0)
+    try:
+        rec = {"pid": os.getpid(), "device": 0, "pci_bus_id": "0000:75:00.0", "time": time.time(),
+               "stats": {"capacity": 8 << 30, "bytes_in_use": 3 << 30, "num_objects": 5, "spilled_bytes_total": 1 << 30,
+                         "restored_bytes_total": 1 << 29, "spilled_objects": 2}}
+        internal._internal_kv_put(f"gpu_store/{os.getpid()}/0", json.dumps(rec), True, namespace=gpu_reporter.NAMESPACE)
+        g = _get(ctx.dashboard_url + "/api/gpus")
+        assert g["gpus"][0]["vram_total_bytes"] == 288 << 30
+        st = [s for s in g["gpu_object_stores"] if s["pid"] == os.getpid()]
+        assert st and st[0]["alive"] and st[0]["stats"]["bytes_in_use"] == 3 << 30
+        cs = _get(ctx.dashboard_url + "/api/cluster_status")
+        assert cs["gpus"][0]["busy_percent"] == 37 and cs["gpu_object_stores"]
+        m = _get(ctx.dashboard_url + "/metrics", raw=True)
+        assert 'rmm_gpu_utilization_percent{gpu="0",pci_bus_id="0000:75:00.0"} 37.0' in m
+        assert "rmm_gpu_object_store_spilled_bytes_total{" in m and "rmm_gpu_vram_used_bytes" in m
+    finally:
+        ray.shutdown()

@@ -9,3 +9,7 @@ import json;d=json.load(open('gpurun_out/sweep3/rank0.json'))
 for r in d['sweep']: print(r)"
 timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 --no-putget > gpurun_out/bench_r4b.log 2>&1 || { tail -30 gpurun_out/bench_r4b.log; exit 1; }
 grep '"metric"' gpurun_out/bench_r4b.log | tail -1 | cut -c1-2500
+timeout -k 10 400 python -u -m pytest tests/test_gpu_shuffle.py -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_shuffle.log 2>&1 || { tail -30 gpurun_out/pytest_shuffle.log; exit 1; }
+grep -E "PASSED|FAILED|passed|failed" gpurun_out/pytest_shuffle.log | tail -5
+timeout -k 10 600 python -u benchmarks/gpu_shuffle_ooc.py --quota-gb 8 --factor 4 --rounds 16 --partitions 8 > gpurun_out/shuffle_ooc.log 2>&1 || { tail -30 gpurun_out/shuffle_ooc.log; exit 1; }
+tail -1 gpurun_out/shuffle_ooc.log
