@@ -19,7 +19,7 @@ namespace rmm {
 namespace {
 
 constexpr uint64_t kMagic = 0x524d4d53544f5245ull;  // "RMMSTORE"
-constexpr uint64_t kVersion = 4;
+constexpr uint64_t kVersion = 5;
 constexpr uint64_t kFreeBit = 1;
 constexpr uint64_t kSizeMask = ~uint64_t(kAlign - 1);
 
@@ -302,6 +302,8 @@ void Store::Recover(int dead_pid) {
   }
   std::sort(lru.begin(), lru.end());
   for (auto& x : lru) LruPush(x.second);
+  hdr_->creating_now = 0;
+  for (uint64_t i = 0; i < cap; i++) hdr_->creating_now += table_[i].state == kCreating;
   // 4) heap: used blocks exactly where live payloads are, every gap one free block
   hdr_->fl_bitmap = 0;
   memset(hdr_->sl_bitmap, 0, sizeof(hdr_->sl_bitmap));
@@ -947,6 +949,7 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   }
   Entry* e = E(idx);
   e->state = kCreating;
+  hdr_->creating_now++;
   e->flags = flags & kFlagError;
   e->user_tag = user_tag;
   e->data_size = data_size;
@@ -1003,6 +1006,7 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   }
   if (!ptr) {
     RemoveEntry(idx);
+    hdr_->creating_now--;
     hdr_->oom_errors_total++;
     const bool disk = hdr_->disk_full != 0;
     Unlock();
@@ -1025,6 +1029,7 @@ void Store::Seal(const ObjectId& id) {
   }
   Entry* e = E(idx);
   e->state = kSealed;
+  hdr_->creating_now--;
   hdr_->stats.num_sealed++;
   hdr_->seal_seq++;
   memcpy(ring_[hdr_->ring_head & (kRingCap - 1)].b, e->id, kIdSize);
@@ -1039,6 +1044,7 @@ void Store::Abort(const ObjectId& id) {
   if (idx >= 0 && E(idx)->state == kCreating) {
     FreeEntryStorage(idx);
     RemoveEntry(idx);
+    hdr_->creating_now--;
   }
   Unlock();
 }
@@ -1046,11 +1052,14 @@ void Store::Abort(const ObjectId& id) {
 int Store::AbortCreator(int pid) {
   int n = 0;
   Lock();
-  for (uint64_t i = 0; i < hdr_->table_cap; i++) {
+  // a dead worker usually created nothing still unsealed: skip the O(table) scan then (the head
+  // calls this for every worker that exits; the table has one slot per 4 KiB of arena)
+  for (uint64_t i = 0; hdr_->creating_now > 0 && i < hdr_->table_cap; i++) {
     Entry* e = &table_[i];
     if (e->state == kCreating && e->creator_pid == pid) {
       FreeEntryStorage(int64_t(i));
       RemoveEntry(int64_t(i));
+      hdr_->creating_now--;
       n++;
     }
   }
@@ -1136,6 +1145,7 @@ void Store::Release(const ObjectId& id) {
   if (e->pin_count > 0) e->pin_count--;
   if (e->pin_count == 0) {
     if (e->flags & kFlagDeletePending) {
+      if (e->state == kCreating) hdr_->creating_now--;
       FreeEntryStorage(idx);
       RemoveEntry(idx);
     } else if (e->state == kSealed && !(e->flags & kFlagFallback)) {

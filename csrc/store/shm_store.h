@@ -155,6 +155,7 @@ struct Header {
   int32_t pad1;
   uint64_t recoveries_total;
   uint64_t recovered_dropped_total;  // entries the rebuild could not validate (lost objects)
+  uint64_t creating_now;             // entries in kCreating (AbortCreator skips its table scan at 0)
   Stats stats;
 };
 

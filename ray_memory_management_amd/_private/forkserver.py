@@ -1,0 +1,248 @@
+"""Worker fork server: start worker processes by fork() from a pre-imported template process.
+
+Role parity: the reference's raylet worker pool starts worker processes (src/ray/raylet/
+worker_pool.cc StartWorkerProcess, with prestart and maximum_startup_concurrency) — each a fresh
+interpreter. Starting a Python interpreter and importing the runtime costs ~100+ ms of CPU per
+worker, which bounds actor creation on one node (release/benchmarks/distributed/test_many_actors.py)
+at a few dozen per second per CPU. Here the head starts ONE template process that imports the worker
+modules once and never touches a GPU; each worker is a fork() of it (copy-on-write pages, a few
+milliseconds), which then applies the worker's own environment (GPU visibility, runtime env) before
+anything reads it and runs ``worker_main.main()``.
+
+Protocol (Unix socket, one JSON line per request): {"env": {...}, "log": path} →
+{"pid": child_pid} or {"error": msg}. The template reaps its children (SIGCHLD), so a dead worker
+never lingers as a zombie whose pid still answers kill(pid, 0).
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import socket
+import sys
+import time
+
+
+def _child(env: dict, log: str, listen: socket.socket, conn: socket.socket):
+    try:
+        listen.close()
+        conn.close()
+        os.setsid()
+        signal.signal(signal.SIGCHLD, signal.SIG_DFL)
+        signal.signal(signal.SIGINT, signal.SIG_DFL)
+        signal.signal(signal.SIGTERM, signal.SIG_DFL)
+        fd = os.open(log, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+        os.dup2(fd, 1)
+        os.dup2(fd, 2)
+        os.close(fd)
+        nul = os.open(os.devnull, os.O_RDONLY)
+        os.dup2(nul, 0)
+        os.close(nul)
+        sys.stdout = os.fdopen(1, "w", buffering=1)
+        sys.stderr = os.fdopen(2, "w", buffering=1)
+        os.environ.clear()
+        os.environ.update(env)
+        import random
+
+        random.seed()
+        try:
+            import numpy as np
+
+            np.random.seed(None)
+        except ImportError:
+            pass
+        from ray_memory_management_amd._private import worker_main
+
+        worker_main.main()
+    except SystemExit as e:
+        os._exit(int(e.code or 0) if isinstance(e.code, int) else 1)
+    except BaseException:  # noqa: BLE001
+        import traceback
+
+        traceback.print_exc()
+        os._exit(1)
+    os._exit(0)
+
+
+def serve(path: str):
+    # the modules every worker needs, imported ONCE here (none of them initialises a GPU)
+    import numpy  # noqa: F401
+    import cloudpickle  # noqa: F401
+
+    from ray_memory_management_amd._private import worker_main  # noqa: F401
+
+    for mod in filter(None, os.environ.get("RMM_FORKSERVER_PRELOAD", "").split(",")):
+        try:
+            __import__(mod)
+        except ImportError:
+            pass
+
+    def reap(*_):
+        while True:
+            try:
+                pid, _ = os.waitpid(-1, os.WNOHANG)
+            except ChildProcessError:
+                return
+            if pid == 0:
+                return
+
+    signal.signal(signal.SIGCHLD, reap)
+    listen = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    listen.bind(path)
+    listen.listen(64)
+    head_pid = os.getppid()
+    listen.settimeout(1.0)
+    conn = None
+    buf = b""
+    while True:
+        if conn is None:
+            try:
+                conn, _ = listen.accept()
+                conn.settimeout(1.0)
+            except socket.timeout:
+                if os.getppid() != head_pid:  # the head is gone
+                    return
+                continue
+            except InterruptedError:
+                continue
+        try:
+            data = conn.recv(1 << 20)
+        except socket.timeout:
+            if os.getppid() != head_pid:
+                return
+            continue
+        except InterruptedError:
+            continue
+        except OSError:
+            data = b""
+        if not data:
+            conn.close()
+            conn, buf = None, b""
+            continue
+        buf += data
+        while b"\n" in buf:
+            line, buf = buf.split(b"\n", 1)
+            try:
+                req = json.loads(line)
+                pid = os.fork()
+                if pid == 0:
+                    _child(req["env"], req["log"], listen, conn)
+                reply = {"pid": pid}
+            except Exception as e:  # noqa: BLE001
+                reply = {"error": repr(e)}
+            try:
+                conn.sendall(json.dumps(reply).encode() + b"\n")
+            except OSError:
+                pass
+
+
+class ForkedProc:
+    """Popen-like handle of a worker forked by the template (not our child: poll by pid)."""
+
+    def __init__(self, pid: int):
+        self.pid = pid
+        self.returncode = None
+
+    def poll(self):
+        if self.returncode is None:
+            try:
+                os.kill(self.pid, 0)
+            except ProcessLookupError:
+                self.returncode = -1
+            except PermissionError:
+                pass
+        return self.returncode
+
+    def wait(self, timeout=None):
+        # the template reaps the process, so there is no zombie for the caller to collect: a short
+        # wait (the head's reap-after-death) is one poll, never a sleep on the head's event loop
+        if timeout is not None and timeout <= 0.1:
+            if self.poll() is None:
+                import subprocess
+
+                raise subprocess.TimeoutExpired(f"pid {self.pid}", timeout)
+            return self.returncode
+        deadline = None if timeout is None else time.time() + timeout
+        while self.poll() is None:
+            if deadline is not None and time.time() >= deadline:
+                import subprocess
+
+                raise subprocess.TimeoutExpired(f"pid {self.pid}", timeout)
+            time.sleep(0.005)
+        return self.returncode
+
+    def kill(self):
+        try:
+            os.kill(self.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+
+    def terminate(self):
+        try:
+            os.kill(self.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+
+
+class ForkClient:
+    """The head's side: start the template, ask it for workers."""
+
+    def __init__(self, session_dir: str, env: dict):
+        import subprocess
+
+        self.path = os.path.join(session_dir, f"forkserver-{os.getpid()}.sock")
+        try:
+            os.unlink(self.path)
+        except OSError:
+            pass
+        log = open(os.path.join(session_dir, "logs", "forkserver.log"), "ab")
+        self.proc = subprocess.Popen([sys.executable, "-u", "-m", "ray_memory_management_amd._private.forkserver",
+                                      self.path], env=env, stdout=log, stderr=subprocess.STDOUT,
+                                     stdin=subprocess.DEVNULL, start_new_session=True)
+        log.close()
+        self.sock = None
+        self.buf = b""
+        t0 = time.time()
+        while time.time() - t0 < 30.0:
+            if self.proc.poll() is not None:
+                raise RuntimeError("fork server exited at startup")
+            try:
+                s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+                s.connect(self.path)
+                s.settimeout(10.0)
+                self.sock = s
+                break
+            except OSError:
+                time.sleep(0.01)
+        if self.sock is None:
+            raise RuntimeError("fork server did not come up")
+
+    def spawn(self, env: dict, log: str) -> ForkedProc:
+        self.sock.sendall(json.dumps({"env": env, "log": log}).encode() + b"\n")
+        while b"\n" not in self.buf:
+            data = self.sock.recv(4096)
+            if not data:
+                raise RuntimeError("fork server closed the connection")
+            self.buf += data
+        line, self.buf = self.buf.split(b"\n", 1)
+        rep = json.loads(line)
+        if "pid" not in rep:
+            raise RuntimeError(f"fork server: {rep.get('error')}")
+        return ForkedProc(int(rep["pid"]))
+
+    def close(self):
+        try:
+            if self.sock is not None:
+                self.sock.close()
+        except OSError:
+            pass
+        if self.proc.poll() is None:
+            self.proc.kill()
+        try:
+            os.unlink(self.path)
+        except OSError:
+            pass
+
+
+if __name__ == "__main__":
+    serve(sys.argv[1])

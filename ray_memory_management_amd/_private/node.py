@@ -698,17 +698,46 @@ class Head:
         env.pop("RMM_DRIVER", None)
         return env
 
+    _forker = None
+    _fork_ok = None
+
+    def _fork_client(self):
+        """The worker fork server (_private/forkserver.py): workers are fork()s of a template that
+        imported the runtime once (~ms each instead of a fresh interpreter). Off with
+        worker_fork_server=False / RMM_NO_FORKSERVER=1; any failure falls back to Popen."""
+        if self._fork_ok is None:
+            self._fork_ok = bool(self.config.get("worker_fork_server", True)) and not os.environ.get("RMM_NO_FORKSERVER")
+            if self._fork_ok:
+                try:
+                    from ray_memory_management_amd._private.forkserver import ForkClient
+
+                    self._forker = ForkClient(self.session_dir, self._worker_env(1, "", None, None))
+                except Exception as e:  # noqa: BLE001
+                    print(f"[head] worker fork server unavailable ({e!r}); spawning interpreters", file=sys.stderr)
+                    self._fork_ok = False
+        return self._forker if self._fork_ok else None
+
     def _start_worker(self, node, key, gpu_ids, actor_id=None, runtime_env=None):
         env_key, gpu_key = key
         wid = os.urandom(16)
         env = self._worker_env(node, env_key, gpu_ids, runtime_env)
         env["RMM_WORKER_ID"] = wid.hex()
         log_dir = os.path.join(self.session_dir, "logs")
-        out = open(os.path.join(log_dir, f"worker-{wid.hex()[:12]}.log"), "ab")
-        cmd = [sys.executable, "-u", "-m", "ray_memory_management_amd._private.worker_main"]
-        proc = subprocess.Popen(cmd, env=env, stdout=out, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
-                                start_new_session=True)
-        out.close()
+        log_path = os.path.join(log_dir, f"worker-{wid.hex()[:12]}.log")
+        proc = None
+        fk = self._fork_client()
+        if fk is not None:
+            try:
+                proc = fk.spawn(env, log_path)
+            except Exception as e:  # noqa: BLE001
+                print(f"[head] fork server failed ({e!r}); spawning interpreters", file=sys.stderr)
+                self._fork_ok = False
+        if proc is None:
+            out = open(log_path, "ab")
+            cmd = [sys.executable, "-u", "-m", "ray_memory_management_amd._private.worker_main"]
+            proc = subprocess.Popen(cmd, env=env, stdout=out, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                    start_new_session=True)
+            out.close()
         w = WorkerRec(wid, proc, node, env_key, gpu_key)
         w.actor_id = actor_id
         self.workers[wid] = w
@@ -1638,6 +1667,11 @@ class Head:
                         pass
         try:
             os.unlink(self.sock_path)
+        except OSError:
+            pass
+        try:
+            if self._forker is not None:
+                self._forker.close()
         except OSError:
             pass
         del self.store
