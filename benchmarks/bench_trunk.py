@@ -1,6 +1,9 @@
 """Microbenchmark of the K10 fused Nature-CNN trunk kernels (csrc/hip/conv_kernels.hip) with the
-profiling phase masks: prints µs per launch for fwd (B=500 SGD minibatch, B=50 rollout step) and
-bwd (B=500), each phase skipped in turn to attribute time. Usage: python benchmarks/bench_trunk.py"""
+profiling phase masks: prints µs per launch (graph-replayed: GPU time, not host launch rate) for fwd
+(B=500 SGD minibatch, B=50 rollout step) and bwd (B=500), each phase skipped in turn to attribute time.
+fwd dbg bits: 1 conv1 MFMA, 2 conv2 MFMA, 8 weight staging, 16 h1 store, 32 frame loads, 64 h2 store,
+128 return at once (launch + dispatch floor). bwd bits: 1 dW2, 2 dh1, 4 dW1, 8 P0 loads, 16 partial
+stores, 32 LDS zeroing, 64 return at once, 128 skip the reduce launch. Usage: python benchmarks/bench_trunk.py"""
 import json
 import os
 import sys
@@ -12,16 +15,24 @@ from ray_memory_management_amd._native import require_hip  # noqa: E402
 
 
 def timeit(fn, iters=200):
-    for _ in range(10):
+    """µs per call on the GPU: `iters` calls captured in one HIP graph and replayed (eager launches
+    from Python cost more host time than these kernels take, which would time the host instead)."""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(3):
+        g.replay()
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3
+    return s.elapsed_time(e) / (3 * iters) * 1e3
 
 
 def main():
@@ -67,7 +78,7 @@ def main():
         idx = torch.randperm(5000, device=dev)[:B].contiguous()
         h1 = torch.empty(B, 441, 16, dtype=torch.bfloat16, device=dev)
         h2 = torch.empty(B, 3872, dtype=torch.bfloat16, device=dev)
-        for dbg in (0, 1, 2, 3, 4, 7):
+        for dbg in (0, 1, 2, 3, 7, 8, 16, 32, 64, 120, 127, 128):
             out[f"fwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_fwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w1.data_ptr(), list(w1.stride()), b1.data_ptr(),
                 w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), st, dbg=dbg)), 1)
@@ -76,7 +87,7 @@ def main():
             part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
             dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
             db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
-            for dbg in (0, 1, 2, 4, 7, 8, 15, 31):
+            for dbg in (0, 1, 2, 4, 7, 8, 15, 16, 31, 63, 64, 128, 128 + 31, 128 + 64):
                 out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                     obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                     h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
@@ -90,7 +101,7 @@ def main():
         part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
         dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
         db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
-        for dbg in (0, 15, 31):
+        for dbg in (0, 15, 31, 128 + 31):
             out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                 h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),

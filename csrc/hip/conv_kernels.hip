@@ -317,17 +317,20 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
 
   // the frame's HBM loads go out first and stay in flight through the weight staging (L2) and the
   // LDS zeroing; one barrier then covers weights, zeros and the frame interior
+  if (dbg & 128) return;  // profiling: launch + dispatch floor
   FrameRegs<NTF> fr;
   constexpr int64_t FB = C0 * H0 * H0;
   if (push_stack)
     frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
-  else
+  else if (!(dbg & 32))
     frame_issue<NTF>(obs + src * FB, fr);
   zero_frame_border(frame);
   zero_lds(h1p, H1P_ELEMS * 2);
-  stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
-  stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
-  frame_store<NTF>(fr, frame);
+  if (!(dbg & 8)) {
+    stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
+    stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
+  }
+  if (!(dbg & 32)) frame_store<NTF>(fr, frame);
   if (push_stack) frame_push_store<NTF>(fr, push_stack + b * FB, push_rows ? push_rows + (push_t[0] * B + b) * FB : nullptr);
   __syncthreads();
 
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
   const float bias2[2] = {bf2f(b2[r]), bf2f(b2[16 + r])};
   __syncthreads();
   // h1 out for backward: coalesced 16-B rows from the LDS tile
-  if (h1_out) {
+  if (h1_out && !(dbg & 16)) {
     for (int v = threadIdx.x; v < NP1 * 2; v += NTF) {
       const int p = v >> 1, y = p / H1, x = p - y * H1;
       *reinterpret_cast<uint4*>(&h1_out[(b * NP1 + p) * C1 + 8 * (v & 1)]) =
@@ -406,6 +409,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
     }
   }
   __syncthreads();
+  if (dbg & 64) return;
   for (int v = threadIdx.x; v < NP2 * C2 / 8; v += NTF)
     *reinterpret_cast<uint4*>(&h2_out[b * NP2 * C2 + 8 * v]) = *reinterpret_cast<const uint4*>(&h2s[8 * v]);
 }
@@ -931,6 +935,7 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(h1),
                      static_cast<const unsigned short*>(h2), static_cast<const unsigned short*>(dh2), partial, dbg);
   RMM_HIP_CHECK(hipGetLastError());
+  if (dbg & 128) return;  // profiling: the backward kernel alone
   hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3((trunk::PART + 63) / 64), dim3(64 * trunk::RED_SLICES), 0, stream,
                      partial, G,
                      static_cast<unsigned short*>(dW1), ws(w1s), static_cast<unsigned short*>(db1),

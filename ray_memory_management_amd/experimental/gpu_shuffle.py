@@ -233,7 +233,8 @@ class OutOfCoreShuffleWorker(ShuffleWorker):
         dev = self.device
         t0 = time.perf_counter()
         g = torch.Generator(device="cpu").manual_seed(7919 * (r + 1) + self.rank)
-        keys = torch.randint(0, 2 ** 62, (self.rows,), generator=g, dtype=torch.int64).to(dev)
+        # keys over the whole u64 range: "range" partitioning splits the UNSIGNED key space evenly
+        keys = torch.randint(-(2 ** 63), 2 ** 63 - 1, (self.rows,), generator=g, dtype=torch.int64).to(dev)
         vals = _payload(keys, self.row_bytes)
         self.in_rows += int(keys.numel())
         self.in_key_sum = (self.in_key_sum + int(keys.sum().item())) % (1 << 61)
@@ -339,6 +340,8 @@ def run_out_of_core_gpu_shuffle(num_workers: int = 1, total_bytes: int = 16 << 3
             "map_seconds": t_map, "reduce_seconds": elapsed - t_map, "rounds": rounds,
             "partitions": partitions_per_worker * num_workers, "workers": num_workers,
             "payload_ok": all(x["payload_ok"] for x in red),
+            "partition_rows_min": min((x["rows"] for x in red), default=0),
+            "partition_rows_max": max((x["rows"] for x in red), default=0),
             "spilled_bytes": tot(st_end, "spilled_bytes_total"), "spilled_host_bytes": tot(st_end, "spilled_host_bytes_total"),
             "restored_bytes": tot(st_end, "restored_bytes_total"), "spilled_after_map": tot(st_map, "spilled_bytes_total"),
             "gpu_store_capacity": tot(st_end, "capacity"),

@@ -9,8 +9,13 @@ dreamer_model.py (RSSM: GRU deterministic state + diagonal-Gaussian stochastic s
 p(z|h) and posterior q(z|h, e); observation decoder, reward head, value head, tanh-Gaussian actor)
 and dreamer_torch_policy.py (model loss = recon + reward NLL + max(free_nats, KL(q‖p)); actor
 maximises λ-returns back-propagated through the imagined dynamics; critic regresses them).
-Vector observations here (the reference's conv encoder/decoder target pixels; the RSSM, the
-imagination and the losses are the same).
+Observations: image observations ([C, 64, 64] uint8, channels first, as the reference's
+dm_control wrapper produces) go through the reference's PlaNet ConvEncoder / ConvDecoder
+(dreamer_model.py:23 ConvEncoder: four 4x4 stride-2 convs depth 32..256 -> 1024 features; :71
+ConvDecoder: Linear -> 1024x1x1 -> transposed convs 5/5/6/6 stride 2 -> [C, 64, 64] mean of a unit
+Gaussian), pixels scaled to [-0.5, 0.5]; vector observations use MLP encoder / decoder. On a GPU
+the conv stacks run channels-last (MIOpen NHWC kernels). The RSSM, imagination and losses are
+shared by both paths.
 """
 from __future__ import annotations
 
@@ -36,16 +41,75 @@ def _mlp(i, o, h, n=2, act=nn.ELU):
     return nn.Sequential(*layers)
 
 
+class ConvEncoder(nn.Module):
+    """PlaNet image encoder: [..., C, 64, 64] in [-0.5, 0.5] -> [..., 32 * depth] (64 -> 31 -> 14 -> 6 -> 2)."""
+
+    def __init__(self, depth: int = 32, shape=(3, 64, 64)):
+        super().__init__()
+        self.depth, self.shape = depth, tuple(shape)
+        c = self.shape[0]
+        self.net = nn.Sequential(nn.Conv2d(c, depth, 4, 2), nn.ReLU(), nn.Conv2d(depth, 2 * depth, 4, 2), nn.ReLU(),
+                                 nn.Conv2d(2 * depth, 4 * depth, 4, 2), nn.ReLU(),
+                                 nn.Conv2d(4 * depth, 8 * depth, 4, 2), nn.ReLU())
+        self.out_dim = 32 * depth
+
+    def forward(self, x):
+        lead = x.shape[:-3]
+        x = x.reshape(-1, *self.shape)
+        if x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return self.net(x).reshape(*lead, self.out_dim)
+
+
+class ConvDecoder(nn.Module):
+    """PlaNet image decoder: features [..., F] -> image mean [..., C, 64, 64] (1 -> 5 -> 13 -> 30 -> 64)."""
+
+    def __init__(self, input_size: int, depth: int = 32, shape=(3, 64, 64)):
+        super().__init__()
+        self.depth, self.shape = depth, tuple(shape)
+        self.fc = nn.Linear(input_size, 32 * depth)
+        self.net = nn.Sequential(nn.ConvTranspose2d(32 * depth, 4 * depth, 5, 2), nn.ReLU(),
+                                 nn.ConvTranspose2d(4 * depth, 2 * depth, 5, 2), nn.ReLU(),
+                                 nn.ConvTranspose2d(2 * depth, depth, 6, 2), nn.ReLU(),
+                                 nn.ConvTranspose2d(depth, self.shape[0], 6, 2))
+
+    def forward(self, f):
+        lead = f.shape[:-1]
+        x = self.fc(f).reshape(-1, 32 * self.depth, 1, 1)
+        if x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return self.net(x).reshape(*lead, *self.shape)
+
+
+def is_image_space(space) -> bool:
+    shp = getattr(space, "shape", None)
+    return shp is not None and len(shp) == 3
+
+
+def preprocess_obs(obs: torch.Tensor, image: bool) -> torch.Tensor:
+    """uint8 images -> float in [-0.5, 0.5] (the reference's Dreamer image normalisation)."""
+    if image:
+        return obs.float() / 255.0 - 0.5
+    return obs.float()
+
+
 class RSSM(nn.Module):
-    def __init__(self, obs_dim, act_dim, deter=64, stoch=16, hidden=128):
+    def __init__(self, obs_dim, act_dim, deter=64, stoch=16, hidden=128, obs_shape=None, depth=32):
         super().__init__()
         self.deter, self.stoch = deter, stoch
-        self.encoder = _mlp(obs_dim, hidden, hidden, 1)
+        self.image = obs_shape is not None and len(obs_shape) == 3
+        if self.image:  # pixel path: PlaNet conv encoder / decoder
+            self.encoder = ConvEncoder(depth, obs_shape)
+            emb = self.encoder.out_dim
+            self.decoder = ConvDecoder(deter + stoch, depth, obs_shape)
+        else:
+            self.encoder = _mlp(obs_dim, hidden, hidden, 1)
+            emb = hidden
+            self.decoder = _mlp(deter + stoch, obs_dim, hidden)
         self.img_in = nn.Sequential(nn.Linear(stoch + act_dim, hidden), nn.ELU())
         self.gru = nn.GRUCell(hidden, deter)
         self.prior = _mlp(deter, 2 * stoch, hidden, 1)
-        self.post = _mlp(deter + hidden, 2 * stoch, hidden, 1)
-        self.decoder = _mlp(deter + stoch, obs_dim, hidden)
+        self.post = _mlp(deter + emb, 2 * stoch, hidden, 1)
         self.reward = _mlp(deter + stoch, 1, hidden)
 
     @staticmethod
@@ -101,7 +165,8 @@ class DreamerConfig(AlgorithmConfig):
         self.action_repeat = 1
         self.episodes_per_iteration = 1
         self.num_workers = 0
-        self.dreamer_model = {"deter_size": 64, "stoch_size": 16, "hidden_size": 128}
+        # depth_size: the conv encoder / decoder width for image observations (reference default 32)
+        self.dreamer_model = {"deter_size": 64, "stoch_size": 16, "hidden_size": 128, "depth_size": 32}
 
 
 class Dreamer(Algorithm):
@@ -119,7 +184,10 @@ class Dreamer(Algorithm):
         if c.seed is not None:
             torch.manual_seed(int(c.seed))
         self.device = torch.device("cuda" if c.num_gpus and torch.cuda.is_available() else "cpu")
-        self.model = RSSM(od, ad, dm["deter_size"], dm["stoch_size"], dm["hidden_size"]).to(self.device)
+        self.image = is_image_space(self.env.observation_space)
+        self.model = RSSM(od, ad, dm["deter_size"], dm["stoch_size"], dm["hidden_size"],
+                          obs_shape=tuple(self.env.observation_space.shape) if self.image else None,
+                          depth=int(dm.get("depth_size", 32))).to(self.device)
         feat = dm["deter_size"] + dm["stoch_size"]
         self.actor = ActorNet(feat, ad, dm["hidden_size"]).to(self.device)
         self.critic = _mlp(feat, 1, dm["hidden_size"]).to(self.device)
@@ -142,9 +210,11 @@ class Dreamer(Algorithm):
             o, done = self.env.reset(), False
             h, z = self.model.initial(1, dev)
             a_prev = torch.zeros(1, self.ad, device=dev)
-            obs, acts, rews, ret = [np.asarray(o, np.float32)], [], [], 0.0
+            # images stay uint8 in the episode buffer (12 KB per 3x64x64 step), scaled at use
+            odt = np.uint8 if self.image else np.float32
+            obs, acts, rews, ret = [np.asarray(o, odt)], [], [], 0.0
             while not done:
-                e = self.model.encoder(torch.as_tensor(obs[-1], device=dev)[None])
+                e = self.model.encoder(preprocess_obs(torch.as_tensor(obs[-1], device=dev)[None], self.image))
                 h, z, _, _ = self.model.obs_step(h, z, a_prev, e)
                 if random:
                     a = torch.as_tensor(self.rng.uniform(-1, 1, (1, self.ad)).astype(np.float32), device=dev)
@@ -157,7 +227,7 @@ class Dreamer(Algorithm):
                     r += ri
                     if done:
                         break
-                obs.append(np.asarray(o, np.float32))
+                obs.append(np.asarray(o, odt))
                 acts.append(a[0].cpu().numpy())
                 rews.append(r)
                 ret += r
@@ -184,7 +254,7 @@ class Dreamer(Algorithm):
             A.append(e["act"][s:s + L])
             R.append(e["rew"][s:s + L])
         t = lambda x: torch.as_tensor(np.stack(x), device=self.device)  # noqa: E731
-        return t(O), t(A), t(R)
+        return preprocess_obs(t(O), self.image), t(A), t(R)
 
     def _train_once(self) -> Dict:
         c = self.algo_config
@@ -201,7 +271,8 @@ class Dreamer(Algorithm):
             kls.append(kl)
         H, Z = torch.stack(hs, 1), torch.stack(zs, 1)
         feat = self.model.feat(H, Z)
-        recon = ((self.model.decoder(feat) - obs) ** 2).sum(-1).mean()
+        err = (self.model.decoder(feat) - obs) ** 2
+        recon = err.flatten(2).sum(-1).mean()  # -log N(obs; mean, 1) up to a constant, summed per frame
         rew_loss = ((self.model.reward(feat).squeeze(-1) - rew) ** 2).mean()
         kl = torch.stack(kls, 1).mean()
         model_loss = recon + rew_loss + c.kl_coeff * torch.clamp(kl, min=c.free_nats)

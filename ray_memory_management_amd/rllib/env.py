@@ -341,6 +341,55 @@ class ContinuousTargetEnv(Env):
         return self.target.copy(), r, self.t >= self.episode_len, {}
 
 
+class PixelPointMassEnv(Env):
+    """Continuous control from pixels (the Dreamer pixel path's test task, in the spirit of the
+    dm_control image tasks the reference trains Dreamer on): a point mass with velocity in [-1, 1]^2
+    pushed by a 2-D force, rewarded by -distance to a goal; observed ONLY as a 3x64x64 uint8 image
+    (channel 0: the mass, channel 1: the goal, channel 2: the velocity direction as a short trail)."""
+
+    SIZE = 64
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.episode_len = int(config.get("episode_len", 100))
+        self.observation_space = Box(0, 255, shape=(3, self.SIZE, self.SIZE), dtype=np.uint8)
+        self.action_space = Box(-1.0, 1.0, shape=(2,), dtype=np.float32)
+        self.rng = np.random.default_rng(config.get("seed"))
+        g = (np.arange(self.SIZE, dtype=np.float32) + 0.5) / self.SIZE * 2.0 - 1.0
+        self._yy, self._xx = np.meshgrid(g, g, indexing="ij")
+        self.t = 0
+        self.pos = np.zeros(2, np.float32)
+        self.vel = np.zeros(2, np.float32)
+        self.goal = np.zeros(2, np.float32)
+
+    def _disk(self, c, r):
+        return ((self._xx - c[0]) ** 2 + (self._yy - c[1]) ** 2) < r * r
+
+    def _obs(self):
+        img = np.zeros((3, self.SIZE, self.SIZE), np.uint8)
+        img[0][self._disk(self.pos, 0.12)] = 255
+        img[1][self._disk(self.goal, 0.12)] = 255
+        img[2][self._disk(self.pos - 0.5 * self.vel, 0.08)] = 255
+        return img
+
+    def reset(self, *, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.t = 0
+        self.pos = self.rng.uniform(-0.8, 0.8, 2).astype(np.float32)
+        self.goal = self.rng.uniform(-0.8, 0.8, 2).astype(np.float32)
+        self.vel = np.zeros(2, np.float32)
+        return self._obs()
+
+    def step(self, action):
+        a = np.clip(np.asarray(action, dtype=np.float32).reshape(2), -1.0, 1.0)
+        self.vel = np.clip(0.8 * self.vel + 0.1 * a, -0.3, 0.3).astype(np.float32)
+        self.pos = np.clip(self.pos + self.vel, -1.0, 1.0).astype(np.float32)
+        self.t += 1
+        r = -float(np.linalg.norm(self.pos - self.goal))
+        return self._obs(), r, self.t >= self.episode_len, {}
+
+
 class SyntheticAtariEnv(Env):
     """84x84x4 uint8 frame-stacked observations with Atari-like dynamics statistics (CPU)."""
 
@@ -579,6 +628,7 @@ _REGISTRY = {
     "StatelessCartPole-v1": StatelessCartPoleEnv,
     "RepeatAfterMe-v0": RepeatAfterMeEnv,
     "DictObs-v0": DictObsEnv,
+    "PixelPointMass-v0": PixelPointMassEnv,
 }
 
 

@@ -1006,6 +1006,24 @@ class PPOLearner:
             return {k: v.numpy() for k, v in out.items()}
         return out
 
+    def rebind_bf16(self, flat: torch.Tensor) -> None:
+        """Move the bf16 compute weights (and every parameter view) to `flat`: same layout, e.g. an
+        HBM object of the GPU object store that co-located rollout workers map zero-copy. Captured
+        graphs hold the old pointers, so they are dropped (recaptured by the next update)."""
+        if not self.fast or self.w_bf16 is None:
+            raise RuntimeError("rebind_bf16 needs the fused bf16 learner")
+        if flat.dtype != torch.bfloat16 or flat.numel() != self.n_params or flat.device != self.w_bf16.device:
+            raise ValueError("rebind_bf16: flat bf16 buffer of the learner's size on its device expected")
+        torch.cuda.synchronize(self.device)
+        with torch.no_grad():
+            flat.copy_(self.w_bf16)
+            off = 0
+            for p in self.params:
+                p.data = flat.as_strided(p.size(), p.stride(), off)
+                off += p.numel()
+        self.w_bf16 = flat
+        self._graph = self._graphs_split = None
+
     def set_weights(self, w):
         with torch.no_grad():
             w = {k: torch.as_tensor(v) for k, v in w.items()}

@@ -85,6 +85,8 @@ def test_out_of_core_shuffle_cpu_spills_and_verifies(ray_start):
                                        row_bytes=56, backend="gloo")
     assert r["ok"] and r["payload_ok"] and r["partitions"] == 6, r
     assert r["rows"] * 64 == r["bytes"] and r["host_store_spilled_bytes"] > 0, r
+    # range partitioning splits the unsigned key space evenly: no partition gets everything
+    assert r["partition_rows_max"] < 1.3 * r["rows"] / r["partitions"], r
 
 
 @pytest.mark.gpu
@@ -102,4 +104,5 @@ def test_out_of_core_gpu_shuffle_spills_hbm_blocks(ray_start):
                                        row_bytes=248, backend="nccl")
     print(r)
     assert r["ok"] and r["payload_ok"], r
+    assert r["partition_rows_max"] < 1.3 * r["rows"] / r["partitions"], r
     assert r["spilled_bytes"] > (1 << 30) and r["restored_bytes"] > (1 << 30), r

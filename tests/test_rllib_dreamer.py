@@ -2,6 +2,7 @@
 losses fall), imagination trains actor and critic, losses stay finite. Mirrors reference
 rllib/algorithms/dreamer/tests/test_dreamer.py (compilation)."""
 import numpy as np
+import pytest
 import torch
 
 
@@ -22,4 +23,56 @@ def test_dreamer_world_model_learns(ray_shared):
     assert all(np.isfinite(v) for v in st.values())
     assert st["recon_loss"] < 0.5 * first["recon_loss"] and st["reward_loss"] < first["reward_loss"]
     assert r["episodes_total"] >= 5 + 4
+    a.stop()
+
+
+def test_dreamer_pixel_path_conv_encoder_decoder(ray_shared):
+    """Image observations (3x64x64 uint8) go through the PlaNet conv encoder / decoder (reference
+    dreamer_model.py:23 ConvEncoder, :71 ConvDecoder): shapes, pixel scaling, and the world model's
+    reconstruction loss falls on the pixel point-mass task."""
+    from ray_memory_management_amd.rllib.algorithms import get_algorithm_class
+    from ray_memory_management_amd.rllib.algorithms.dreamer import ConvDecoder, ConvEncoder
+
+    enc, dec = ConvEncoder(8), ConvDecoder(40, 8)
+    x = torch.rand(2, 5, 3, 64, 64) - 0.5
+    e = enc(x)
+    assert e.shape == (2, 5, 256)
+    assert dec(torch.randn(2, 5, 40)).shape == (2, 5, 3, 64, 64)
+
+    torch.set_num_threads(4)
+    cfg = (get_algorithm_class("Dreamer").get_default_config()
+           .environment("PixelPointMass-v0", env_config={"episode_len": 30}).debugging(seed=0))
+    cfg.prefill_timesteps, cfg.batch_size, cfg.batch_length = 120, 8, 12
+    cfg.dreamer_train_iters, cfg.imagine_horizon = 12, 5
+    cfg.dreamer_model = {"deter_size": 32, "stoch_size": 8, "hidden_size": 64, "depth_size": 8}
+    a = cfg.build()
+    assert a.image and a.episodes[0]["obs"].dtype == np.uint8 and a.episodes[0]["obs"].shape[1:] == (3, 64, 64)
+    first = a._train_once()
+    for _ in range(3):
+        r = a.train()
+    st = r["info"]["learner"]["default_policy"]["learner_stats"]
+    assert all(np.isfinite(v) for v in st.values())
+    assert st["recon_loss"] < 0.7 * first["recon_loss"], (first, st)
+    a.stop()
+
+
+@pytest.mark.gpu
+def test_dreamer_pixel_path_gpu(ray_shared):
+    """The pixel path at the reference's widths (depth 32) on the GPU (channels-last conv stacks)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ray_memory_management_amd.rllib.algorithms import get_algorithm_class
+
+    cfg = (get_algorithm_class("Dreamer").get_default_config()
+           .environment("PixelPointMass-v0", env_config={"episode_len": 50}).resources(num_gpus=1).debugging(seed=0))
+    cfg.prefill_timesteps, cfg.batch_size, cfg.batch_length = 500, 16, 25
+    cfg.dreamer_train_iters, cfg.imagine_horizon = 25, 10
+    a = cfg.build()
+    assert a.device.type == "cuda" and a.image
+    first = a._train_once()
+    for _ in range(3):
+        r = a.train()
+    st = r["info"]["learner"]["default_policy"]["learner_stats"]
+    assert all(np.isfinite(v) for v in st.values())
+    assert st["recon_loss"] < 0.7 * first["recon_loss"], (first, st)
     a.stop()
