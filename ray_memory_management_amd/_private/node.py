@@ -176,6 +176,7 @@ class Head:
     def __init__(self, args):
         self.args = args
         self.session_dir = args.session_dir
+        self._event_loggers = {}
         self.sock_path = os.path.join(self.session_dir, "sockets", "head.sock")
         self.store_name = args.store_name
         self.config = json.loads(args.config) if args.config else {}
@@ -326,6 +327,8 @@ class Head:
         if node_id not in self.nodes or node_id == self.head_node:
             return False
         self.nodes[node_id]["alive"] = False
+        self._event("CLUSTER_LIFECYCLE", "ERROR", "NODE_REMOVED", f"Node {self._hex(node_id)} was removed; "
+                    "its running work is retried or reconstructed.", node_id=self._hex(node_id))
         # returns a running task already sealed on the node die with it (its TaskDone may still be
         # in flight); the task itself is retried when its worker's death is processed
         for t in list(self.tasks.values()):
@@ -641,6 +644,8 @@ class Head:
             self.gcs_dirty = True
             self.jobs[job_id] = {"job_id": job_id, "pid": c.pid, "start_time": time.time(), "end_time": None,
                                  "namespace": info.get("namespace"), "alive": True, "conn": c}
+            self._event("JOBS", "INFO", "JOB_STARTED", f"Driver pid {c.pid} connected.",
+                        job_id=self._hex(job_id), pid=c.pid, namespace=info.get("namespace"))
             if self.driver_conn is None:
                 self.driver_conn = c
             self._reply(c, info["req_id"], {
@@ -744,6 +749,22 @@ class Head:
         self.starting[(node, env_key, gpu_key)] += 1
         return w
 
+    def _event(self, source: str, severity: str, label: str, message: str, **fields):
+        """Append a cluster event (reference RAY_EVENT) under <session>/logs/events/."""
+        lg = self._event_loggers.get(source)
+        if lg is None:
+            from ray_memory_management_amd._private.event_log import EventLogger
+
+            lg = self._event_loggers[source] = EventLogger(self.session_dir, source)
+        try:
+            lg.emit(severity, label, message, **fields)
+        except Exception:  # noqa: BLE001 - events never fail the head
+            pass
+
+    @staticmethod
+    def _hex(x):
+        return x.hex() if isinstance(x, (bytes, bytearray)) else x
+
     def _kill_worker(self, w: WorkerRec, force=True):
         if w.proc is not None and w.proc.poll() is None:
             try:
@@ -780,6 +801,8 @@ class Head:
             job["alive"] = False
             job["end_time"] = time.time()
             self.gcs_dirty = True
+            self._event("JOBS", "INFO", "JOB_FINISHED", f"Driver pid {job.get('pid')} exited.",
+                        job_id=self._hex(c.job_id), pid=job.get("pid"))
         # kill non-detached actors of this job
         for a in list(self.actors.values()):
             if a.job_id == c.job_id and not a.detached and a.state != ACTOR_DEAD:
@@ -810,6 +833,15 @@ class Head:
                 w.proc.wait(timeout=0.05)
             except Exception:
                 pass
+        if prev_state != "DEAD":  # not a kill the head asked for (those report their own reason)
+            t0 = self.tasks.get(w.task) if w.task is not None else None
+            code = w.proc.poll() if w.proc is not None else None
+            self._event("RAYLET", "ERROR", "WORKER_DIED",
+                        f"Worker pid {w.pid} died unexpectedly (exit code {code}) in state {prev_state}.",
+                        pid=w.pid, worker_id=self._hex(w.worker_id), exit_code=code,
+                        task_id=self._hex(t0.spec["task_id"]) if t0 is not None else None,
+                        job_id=self._hex(t0.spec.get("job_id")) if t0 is not None else None,
+                        actor_id=self._hex(w.actor_id))
         if w.task is not None:
             t = self.tasks.get(w.task)
             w.task = None
@@ -1335,8 +1367,15 @@ class Head:
                 a.restarts_left -= 1
             a.num_restarts += 1
             a.state = ACTOR_RESTARTING
+            self._event("GCS", "WARNING", "ACTOR_RESTARTED", f"Actor {a.actor_id.hex()} is restarting "
+                        f"(restart {a.num_restarts}).", actor_id=a.actor_id.hex(), job_id=self._hex(a.job_id),
+                        num_restarts=a.num_restarts, class_name=a.spec.get("class_name"))
             self._schedule_actor(a)
             return
+        if a.state != ACTOR_DEAD:
+            self._event("GCS", "ERROR", "ACTOR_DIED", f"Actor {a.actor_id.hex()} died: "
+                        f"{a.death_cause or 'the actor process died unexpectedly'}.", actor_id=a.actor_id.hex(),
+                        job_id=self._hex(a.job_id), class_name=a.spec.get("class_name"))
         self._mark_actor_dead(a, a.death_cause or "The actor process died unexpectedly.")
 
     def _mark_actor_dead(self, a: ActorRec, cause):
@@ -1590,6 +1629,13 @@ class Head:
                 t = self.tasks.get(victim.task) if victim.task else None
                 if t is not None:
                     t.error = "oom"
+                mm = self.memory_monitor
+                self._event("RAYLET", "ERROR", "OUT_OF_MEMORY",
+                            f"Killed worker pid {victim.pid} to relieve memory pressure (used "
+                            f"{getattr(mm, 'last_used', None)} of {getattr(mm, 'last_total', None)} bytes, "
+                            f"threshold {mm.threshold}).",
+                            pid=victim.pid, task_id=self._hex(t.spec["task_id"]) if t is not None else None,
+                            job_id=self._hex(t.spec.get("job_id")) if t is not None else None)
                 self._kill_worker(victim)
 
     def _io_spill(self, nbytes):
@@ -1622,6 +1668,12 @@ class Head:
         if full != self.store.disk_full():
             self.store.set_disk_full(full)
             self.mem_stats["disk_full_transitions"] += 1
+            if full:
+                self._event("RAYLET", "WARNING", "DISK_FULL", "A spill directory's filesystem is over "
+                            f"local_fs_capacity_threshold {self.disk_threshold}: spilling stops.",
+                            dirs=list(self.spill_dirs))
+            else:
+                self._event("RAYLET", "INFO", "DISK_OK", "Spill directories have space again.")
 
     def _maybe_global_gc(self, now, st):
         """A create starved past its first retry bumps the store's gc_requests; the head then

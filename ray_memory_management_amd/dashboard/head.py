@@ -6,7 +6,9 @@ tasks,objects,nodes,workers,jobs,placement_groups} + summaries), node (/nodes),
 reporter (/api/cluster_status, Prometheus metrics, per-GPU utilization / HBM and GPU object-store
 occupancy + spill state: /api/gpus, dashboard/gpu_reporter.py), job (job_head.py: REST job submission
 /api/jobs/ — submit / list / info / logs / stop / delete), log (/api/v0/logs),
-healthz (/api/gcs_healthz)}. The reference dashboard also ships a React UI; this one serves JSON
+healthz (/api/gcs_healthz), event (/events), snapshot (/api/snapshot, /api/actors/kill), actor
+(/logical/actors, /logical/actor_groups, /logical/kill_actor), serve (/api/serve/deployments/) and
+tune (/tune/info) — the last five in dashboard/modules.py}. The reference dashboard also ships a React UI; this one serves JSON
 and Prometheus text only.
 
 It runs as its own process that connects to the cluster as a client driver (like the reference's
@@ -106,6 +108,12 @@ class DashboardHead:
                                              "gpu_object_stores": _gpu().gpu_object_stores()})
         # metrics (Prometheus text)
         r("GET", r"/metrics", self._metrics)
+        # event / snapshot / actor / serve / tune modules (dashboard/modules.py)
+        from ray_memory_management_amd.dashboard.modules import MODULES
+
+        self.modules = [m(self) for m in MODULES]
+        for m in self.modules:
+            m.register(r)
 
     def _lister(self, kind):
         def fn(q, b):
@@ -201,6 +209,8 @@ class DashboardHead:
                 except (ValueError, RuntimeError, KeyError) as e:
                     self._send(400 if isinstance(e, ValueError) else 404 if isinstance(e, KeyError) else 500,
                                {"error": f"{type(e).__name__}: {e}"})
+                except Exception as e:  # noqa: BLE001 - a handler bug answers 500, never drops the socket
+                    self._send(500, {"error": f"{type(e).__name__}: {e}"})
 
             def _send(self, code, out):
                 if isinstance(out, _Text):
@@ -221,6 +231,9 @@ class DashboardHead:
 
             def do_DELETE(self):
                 self._do("DELETE")
+
+            def do_PUT(self):
+                self._do("PUT")
 
             def log_message(self, *a):
                 pass

@@ -147,6 +147,90 @@ def _fake_sysfs(root):
     return os.fspath(root)
 
 
+def test_event_snapshot_actor_modules(dash):
+    """reference dashboard/modules/{event,snapshot,actor}: a worker that dies unexpectedly and an
+    actor restart show up as events (event_head.py /events), the snapshot lists jobs and actors,
+    actors are grouped by class and can be killed over HTTP."""
+    import os
+    import signal
+
+    ray, url = dash
+
+    @ray.remote(max_restarts=1)
+    class Phoenix:
+        def pid(self):
+            return os.getpid()
+
+    a = Phoenix.remote()
+    pid = ray.get(a.pid.remote())
+    os.kill(pid, signal.SIGKILL)
+    deadline = time.time() + 30
+    labels = set()
+    while time.time() < deadline:
+        ev = _get(url + "/events")
+        assert ev["result"] is True
+        labels = {e["label"] for evs in ev["data"]["events"].values() for e in evs}
+        if {"WORKER_DIED", "ACTOR_RESTARTED", "JOB_STARTED"} <= labels:
+            break
+        time.sleep(0.2)
+    assert {"WORKER_DIED", "ACTOR_RESTARTED", "JOB_STARTED"} <= labels, labels
+    died = [e for evs in _get(url + "/events")["data"]["events"].values() for e in evs if e["label"] == "WORKER_DIED"]
+    assert any(e["custom_fields"]["pid"] == pid and e["severity"] == "ERROR" for e in died), died
+    assert ray.get(a.pid.remote()) != pid  # restarted
+
+    snap = _get(url + "/api/snapshot")["data"]["snapshot"]
+    aid = a._actor_id.hex()
+    assert aid in snap["actors"] and snap["jobs"] and "deployments" in snap
+    groups = _get(url + "/logical/actor_groups")["data"]["actor_groups"]
+    assert any(aid in [e["actor_id"] for e in g["entries"]] for g in groups.values())
+    assert aid in _get(url + "/logical/actors")["data"]["actors"]
+    r = _get(url + f"/api/actors/kill?actor_id={aid}&force_kill=true&no_restart=true")
+    assert r["result"] is True
+    deadline = time.time() + 30
+    while time.time() < deadline and _get(url + "/logical/actors")["data"]["actors"][aid]["state"] != "DEAD":
+        time.sleep(0.1)
+    assert _get(url + "/logical/actors")["data"]["actors"][aid]["state"] == "DEAD"
+    with pytest.raises(Exception):
+        _get(url + "/api/actors/kill?actor_id=" + "ab" * 16)
+    # Serve not running: empty deployment list, NOT_STARTED-free status shape
+    assert _get(url + "/api/serve/deployments/")["deployments"] == []
+
+
+def test_tune_module_reads_experiment(dash, tmp_path):
+    ray, url = dash
+    exp = tmp_path / "exp"
+    for i, lr in enumerate((0.1, 0.01)):
+        d = exp / f"train_{i:05d}"
+        d.mkdir(parents=True)
+        (d / "params.json").write_text(json.dumps({"lr": lr}))
+        (d / "result.json").write_text("".join(json.dumps({"loss": 1.0 / (k + 1 + i), "training_iteration": k + 1})
+                                               + "\n" for k in range(3)))
+    assert _get(url + "/tune/set_experiment?experiment=" + str(exp))["result"] is True
+    assert _get(url + "/tune/availability")["data"]["result"]["trials_available"] is True
+    info = _get(url + "/tune/info")["data"]["result"]["trial_records"]
+    assert len(info) == 2 and {t["params"]["lr"] for t in info.values()} == {0.1, 0.01}
+    assert all(t["num_results"] == 3 and t["metrics"]["training_iteration"] == 3 for t in info.values())
+
+
+def test_event_log_reader(tmp_path):
+    from ray_memory_management_amd._private.event_log import EventLogger, events_by_job, read_events
+
+    lg = EventLogger(str(tmp_path), "RAYLET")
+    lg.emit("INFO", "A", "first", job_id="01")
+    lg.emit("ERROR", "B", "second", job_id="02", pid=7)
+    lg.emit("WARNING", "C", "third")
+    lg.close()
+    with open(lg.path, "a") as f:
+        f.write('{"truncated": ')  # a line being written
+    assert [e["label"] for e in read_events(str(tmp_path))] == ["A", "B", "C"]
+    assert [e["label"] for e in read_events(str(tmp_path), severity="WARNING")] == ["B", "C"]
+    assert [e["label"] for e in read_events(str(tmp_path), job_id="02")] == ["B"]
+    by = events_by_job(str(tmp_path))
+    assert set(by) == {"01", "02", "global"} and by["02"][0]["custom_fields"]["pid"] == 7
+    with pytest.raises(ValueError):
+        lg.emit("LOUD", "X", "bad severity")
+
+
 def test_gpu_reporter_endpoints(tmp_path, monkeypatch):
     """Per-GPU utilization / HBM (amdgpu sysfs) and GPU object-store occupancy in /api/gpus,
     /api/cluster_status and /metrics (reference reporter_agent.py:92-98 GPU usage)."""
