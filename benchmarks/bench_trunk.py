@@ -46,7 +46,6 @@ def main():
     a = ap.parse_args()
     h = require_hip()
     dev = torch.device("cuda:0")
-    st = torch.cuda.current_stream().cuda_stream
     obs = torch.randint(0, 256, (5000, 4, 84, 84), dtype=torch.uint8, device=dev)
     w1 = (torch.randn(16, 4, 8, 8, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w2 = (torch.randn(32, 16, 4, 4, device=dev) * 0.1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -61,7 +60,7 @@ def main():
         if a.only == "fwd":
             t = timeit(lambda: h.nature_trunk_fwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w1.data_ptr(), list(w1.stride()), b1.data_ptr(),
-                w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), st, dbg=a.dbg), a.iters)
+                w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), torch.cuda.current_stream().cuda_stream, dbg=a.dbg), a.iters)
         else:
             dh2 = torch.randn(B, 3872, device=dev).to(torch.bfloat16)
             part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
@@ -70,7 +69,7 @@ def main():
             t = timeit(lambda: h.nature_trunk_bwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                 h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
-                dw2.data_ptr(), db2.data_ptr(), st, dbg=a.dbg), a.iters)
+                dw2.data_ptr(), db2.data_ptr(), torch.cuda.current_stream().cuda_stream, dbg=a.dbg), a.iters)
         print(json.dumps({f"{a.only}_B{B}_dbg{a.dbg}": round(t, 1),
                           "cus": torch.cuda.get_device_properties(0).multi_processor_count}))
         return
@@ -81,7 +80,7 @@ def main():
         for dbg in (0, 1, 2, 3, 7, 8, 16, 32, 64, 120, 127, 128):
             out[f"fwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_fwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w1.data_ptr(), list(w1.stride()), b1.data_ptr(),
-                w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), st, dbg=dbg)), 1)
+                w2.data_ptr(), list(w2.stride()), b2.data_ptr(), h1.data_ptr(), h2.data_ptr(), torch.cuda.current_stream().cuda_stream, dbg=dbg)), 1)
         if B == 500:
             dh2 = torch.randn(B, 3872, device=dev).to(torch.bfloat16)
             part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
@@ -91,7 +90,7 @@ def main():
                 out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                     obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                     h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
-                    dw2.data_ptr(), db2.data_ptr(), st, dbg=dbg)), 1)
+                    dw2.data_ptr(), db2.data_ptr(), torch.cuda.current_stream().cuda_stream, dbg=dbg)), 1)
     # latency vs throughput: backward at growing B (G = min(B, 256) workgroups)
     for B in (1, 16, 64, 256):
         idx = torch.randperm(5000, device=dev)[:B].contiguous()
@@ -105,7 +104,7 @@ def main():
             out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                 h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
-                dw2.data_ptr(), db2.data_ptr(), st, dbg=dbg)), 1)
+                dw2.data_ptr(), db2.data_ptr(), torch.cuda.current_stream().cuda_stream, dbg=dbg)), 1)
     print(json.dumps(out))
 
 

@@ -27,274 +27,12 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "trunk_device.h"
 
 namespace rmm {
 namespace hip {
 namespace trunk {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int C0 = 4, H0 = 84, P0 = 88;            // frame, padded by 2 each side
-constexpr int H1 = 21, C1 = 16, NP1 = 441, NP1P = 448;
-constexpr int P1 = 25;                              // h1 padded by 2 each side
-constexpr int H2 = 11, C2 = 32, NP2 = 121, NP2P = 128;
-constexpr int FRAME_BYTES = C0 * P0 * P0;          // 30976
-constexpr int H1P_ELEMS = P1 * P1 * C1;            // 10000 bf16
-
-__device__ __forceinline__ unsigned short f2bf(float f) {  // round-to-nearest-even
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<unsigned short>(u >> 16);
-}
-__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(uint32_t(h) << 16); }
-__device__ __forceinline__ unsigned short u8bf(uint32_t b) { return static_cast<unsigned short>(__float_as_uint(float(b)) >> 16); }
-
-__device__ __forceinline__ bf16x8 as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
-
-__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-struct WStrides { int64_t s0, s1, s2, s3; };  // [co][ci][ky][kx] element strides
-
-__device__ __forceinline__ const int64_t* window(const int64_t* idx, const int64_t* ctr, int64_t period, int64_t rows) {
-  return (ctr && idx) ? idx + (ctr[0] % period) * rows : idx;
-}
-
-// Copy one u8 frame [4][84][84] (NCHW) into the padded HWC LDS image: pixel (y, x) channel c at
-// byte ((y+2)*88 + x+2)*4 + c. A thread takes the same 4-pixel word from the 4 channel planes
-// (4 coalesced u32 loads), transposes the 4x4 bytes in registers and writes 16 B of HWC pixels.
-// All of a thread's loads are issued before any LDS write (28 in flight): a load→store per
-// iteration would serialise ~28 HBM round trips per frame. NT = blockDim.
-template <int NT>
-__device__ __forceinline__ void load_frame(const uint8_t* __restrict__ src, uint8_t* frame) {
-  constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;  // 1764 words per plane
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
-  uint32_t v[PER][C0];
-  // unconditional loads at a clamped index: a guarded load inside an unrolled batch makes hipcc
-  // branch around each one and wait vmcnt(0) per load (an HBM round trip each)
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
-#pragma unroll
-    for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
-  }
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
-      const int y = o / 21, x = 4 * (o - y * 21);
-      uint32_t px[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++)  // pixel q: bytes (c0, c1, c2, c3) = byte q of each plane word
-        px[q] = ((v[k][0] >> (8 * q)) & 0xffu) | (((v[k][1] >> (8 * q)) & 0xffu) << 8) |
-                (((v[k][2] >> (8 * q)) & 0xffu) << 16) | (((v[k][3] >> (8 * q)) & 0xffu) << 24);
-      uint2* d = reinterpret_cast<uint2*>(frame + ((y + 2) * P0 + x + 2) * 4);  // 8-B aligned
-      d[0] = make_uint2(px[0], px[1]);
-      d[1] = make_uint2(px[2], px[3]);
-    }
-  }
-}
-
-// load_frame split in two so the HBM frame loads can be issued before the weight staging and the
-// LDS zeroing (they are independent): frame_issue starts the loads, frame_store transposes and writes
-// the interior; only the 2-pixel border needs zeros (zero_frame_border), so no barrier separates
-// zeroing from the interior stores.
-template <int NT>
-struct FrameRegs {
-  static constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
-  uint32_t v[PER][C0];
-};
-template <int NT>
-__device__ __forceinline__ void frame_issue(const uint8_t* __restrict__ src, FrameRegs<NT>& f) {
-  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
-#pragma unroll
-    for (int c = 0; c < C0; c++) f.v[k][c] = s32[c * NW + o];
-  }
-}
-template <int NT>
-__device__ __forceinline__ void frame_store(const FrameRegs<NT>& f, uint8_t* frame) {
-  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
-      const int y = o / 21, x = 4 * (o - y * 21);
-      uint32_t px[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        px[q] = ((f.v[k][0] >> (8 * q)) & 0xffu) | (((f.v[k][1] >> (8 * q)) & 0xffu) << 8) |
-                (((f.v[k][2] >> (8 * q)) & 0xffu) << 16) | (((f.v[k][3] >> (8 * q)) & 0xffu) << 24);
-      uint2* d = reinterpret_cast<uint2*>(frame + ((y + 2) * P0 + x + 2) * 4);
-      d[0] = make_uint2(px[0], px[1]);
-      d[1] = make_uint2(px[2], px[3]);
-    }
-  }
-}
-// Rollout push mode (K19 folded into the trunk): the frame to run is the env's device stack
-// shifted by one with the newest frame appended. The thread that loads word o of planes 1..3 of
-// the stack and of the new frame also writes word o of the 4 shifted planes back (stack, in place:
-// no other thread touches word o of this env) and into rollout row t — so the rollout step needs
-// no separate frame-push launch. `nf` may be device-mapped pinned host memory (zero-copy upload).
-template <int NT>
-__device__ __forceinline__ void frame_issue_push(const uint8_t* stack, const uint8_t* __restrict__ nf,
-                                                 FrameRegs<NT>& f) {
-  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stack);
-  const uint32_t* n32 = reinterpret_cast<const uint32_t*>(nf);
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
-#pragma unroll
-    for (int c = 0; c < C0 - 1; c++) f.v[k][c] = s32[(c + 1) * NW + o];
-    f.v[k][C0 - 1] = n32[o];
-  }
-}
-template <int NT>
-__device__ __forceinline__ void frame_push_store(const FrameRegs<NT>& f, uint8_t* stack, uint8_t* row) {
-  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
-  uint32_t* s32 = reinterpret_cast<uint32_t*>(stack);
-  uint32_t* r32 = reinterpret_cast<uint32_t*>(row);
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
-#pragma unroll
-      for (int c = 0; c < C0; c++) {
-        s32[c * NW + o] = f.v[k][c];
-        if (row) r32[c * NW + o] = f.v[k][c];
-      }
-    }
-  }
-}
-
-// zero rows 0, 1, 86, 87 and columns 0, 1, 86, 87 of the padded HWC frame (one u32 = one pixel)
-__device__ __forceinline__ void zero_frame_border(uint8_t* frame) {
-  uint32_t* f32 = reinterpret_cast<uint32_t*>(frame);
-  constexpr int NROW = 4 * P0, NCOL = (P0 - 4) * 4;
-  for (int i = threadIdx.x; i < NROW + NCOL; i += blockDim.x) {
-    int y, x;
-    if (i < NROW) {
-      const int r = i / P0;
-      y = r < 2 ? r : r + (P0 - 4);
-      x = i - r * P0;
-    } else {
-      const int j = i - NROW, c = j & 3;
-      y = 2 + (j >> 2);
-      x = c < 2 ? c : c + (P0 - 4);
-    }
-    f32[y * P0 + x] = 0u;
-  }
-}
-
-// Backward variant: the padded frame in space-to-depth form, transposed, bf16 (exact for 0..255):
-// padded pixel (yp, xp) = (y+2, x+2) = (4Y+ry, 4X+rx), channel ci → st[c][Y*ST_W + X] with
-// c = 16ry + 4rx + ci. conv1 (8x8/4) is then a 2x2 stride-1 correlation over a 64-channel 22x22
-// grid: ky = 4a+ry, kx = 4b+rx, input (Y, X) = (oy+a, ox+b). Its weight gradient reduces over
-// grid positions, which are CONTIGUOUS per channel here (one 16-B LDS read per MFMA operand
-// instead of 8 strided 2-B gathers). Row pitch ST_W = 24 (3 chunks of 8), 23 rows (row 22 and
-// columns 22, 23 stay zero: K padding), channel pitch 552 el = 276 dwords (8 lanes reading 8
-// channels hit distinct 4-bank groups).
-constexpr int ST_W = 24, ST_CP = 23 * ST_W, ST_C = 64;
-template <int NT>
-__device__ __forceinline__ void frame_store_s2d(const FrameRegs<NT>& f, unsigned short* st) {
-  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
-      const int y = o / 21, xw = o - y * 21;  // pixels x = 4xw .. 4xw+3 → xp = 4xw+2 .. 4xw+5
-      const int yp = y + 2;
-      unsigned short* row = st + (16 * (yp & 3)) * ST_CP + (yp >> 2) * ST_W + xw;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int rx = (q + 2) & 3, dX = (q + 2) >> 2;
-#pragma unroll
-        for (int c = 0; c < C0; c++) row[(4 * rx + c) * ST_CP + dX] = u8bf((f.v[k][c] >> (8 * q)) & 0xffu);
-      }
-    }
-  }
-}
-template <int NT>
-__device__ __forceinline__ void load_frame_s2d(const uint8_t* __restrict__ src, unsigned short* st) {
-  constexpr int NW = H0 * H0 / 4, PER = (NW + NT - 1) / NT;
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
-  uint32_t v[PER][C0];
-  // unconditional loads at a clamped index: a guarded load inside an unrolled batch makes hipcc
-  // branch around each one and wait vmcnt(0) per load (an HBM round trip each)
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = min(int(threadIdx.x) + NT * k, NW - 1);
-#pragma unroll
-    for (int c = 0; c < C0; c++) v[k][c] = s32[c * NW + o];
-  }
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const int o = threadIdx.x + NT * k;
-    if (o < NW) {
-      const int y = o / 21, xw = o - y * 21;  // pixels x = 4xw .. 4xw+3 → xp = 4xw+2 .. 4xw+5
-      const int yp = y + 2;
-      unsigned short* row = st + (16 * (yp & 3)) * ST_CP + (yp >> 2) * ST_W + xw;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int rx = (q + 2) & 3, dX = (q + 2) >> 2;  // compile-time after unrolling
-#pragma unroll
-        for (int c = 0; c < C0; c++) row[(4 * rx + c) * ST_CP + dX] = u8bf((v[k][c] >> (8 * q)) & 0xffu);
-      }
-    }
-  }
-}
-
-// Stage a conv weight into LDS as canonical [co][ky][kx][ci] rows of `pitch` elements (row = co).
-// Every workgroup needs the whole (tiny) weight: per-lane fragment loads straight from global make
-// all workgroups hammer the same few L2 lines (measured: skeleton cost grew 7→20-30 µs from 1 to
-// 256 workgroups). Here each element is read once per workgroup, 16 B at a time when the weight
-// is channels-last contiguous ([co][ky][kx][ci] in memory).
-template <int NT, int CO, int CI, int KH>
-__device__ __forceinline__ void stage_weight(const unsigned short* __restrict__ W, WStrides ws_, unsigned short* dst,
-                                             int pitch) {
-  constexpr int ROW = KH * KH * CI;  // elements per output channel
-  if (ws_.s1 == 1 && ws_.s3 == CI && ws_.s2 == KH * CI && ws_.s0 == ROW) {
-    for (int v = threadIdx.x; v < CO * ROW / 8; v += NT) {
-      const int co = (8 * v) / ROW, e = 8 * v - co * ROW;
-      *reinterpret_cast<uint4*>(&dst[co * pitch + e]) = *reinterpret_cast<const uint4*>(&W[8 * v]);
-    }
-  } else {
-    for (int v = threadIdx.x; v < CO * ROW; v += NT) {
-      const int co = v / ROW, e = v - co * ROW, ky = e / (KH * CI), kx = (e / CI) % KH, ci = e % CI;
-      dst[co * pitch + e] = W[co * ws_.s0 + ci * ws_.s1 + ky * ws_.s2 + kx * ws_.s3];
-    }
-  }
-}
-constexpr int W1_PITCH = 256 + 8, W2_PITCH = 256 + 8;  // +16 B: 16 lanes x 16-B reads hit distinct banks
-
-__device__ __forceinline__ void zero_lds(void* p, int bytes) {
-  uint4* q = reinterpret_cast<uint4*>(p);
-  for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) q[i] = make_uint4(0, 0, 0, 0);
-}
-
-// 8 consecutive bytes of the HWC frame (8-byte aligned: 2 pixels x 4 channels) → bf16x8
-__device__ __forceinline__ bf16x8 frame8(const uint8_t* frame, int off) {
-  const uint2 w = *reinterpret_cast<const uint2*>(frame + off);
-  const uint32_t a = w.x, b = w.y;
-  u16x8 v;
-  v[0] = u8bf(a & 0xff); v[1] = u8bf((a >> 8) & 0xff); v[2] = u8bf((a >> 16) & 0xff); v[3] = u8bf(a >> 24);
-  v[4] = u8bf(b & 0xff); v[5] = u8bf((b >> 8) & 0xff); v[6] = u8bf((b >> 16) & 0xff); v[7] = u8bf(b >> 24);
-  return as_bf(v);
-}
-
-
-// Weight-grad GEMMs reduce over positions (MFMA K). Lane group g's 8 K values are taken as
-// positions 32s + g + 4j (j = 0..7) so the four lane groups gather NEIGHBOURING pixels (distinct
-// LDS banks; with 8g + j they sit 8 positions apart, on the same bank: 4-way conflicts). The
-// transposed dpre tiles are stored in that permuted order so the A operand stays one 16-B read.
-__device__ __forceinline__ int kperm(int p) { return (p & ~31) + 8 * (p & 3) + ((p & 31) >> 2); }
 
 // ================================================================ forward
 // grid = B workgroups (one frame each), NTF threads.
@@ -305,12 +43,10 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
     const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ b2,
     unsigned short* __restrict__ h1_out, unsigned short* __restrict__ h2_out, int dbg, uint8_t* push_stack,
     const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t) {
-  __shared__ __attribute__((aligned(16))) uint8_t frame[FRAME_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned short fh[HF_ELEMS];  // bf16 half image (two passes)
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short w1s[C1 * W1_PITCH];
   __shared__ __attribute__((aligned(16))) unsigned short w2s[C2 * W2_PITCH];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
   const int64_t b = blockIdx.x;
   const int64_t* idx = window(idx0, ctr, period, B);
   const int64_t src = idx ? idx[b] : b;
@@ -324,94 +60,16 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
     frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
   else if (!(dbg & 32))
     frame_issue<NTF>(obs + src * FB, fr);
-  zero_frame_border(frame);
+  const TrunkBias tb = trunk_bias(b1, b2);
+  zero_half_frame_border(fh);
   zero_lds(h1p, H1P_ELEMS * 2);
   if (!(dbg & 8)) {
     stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
     stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   }
-  if (!(dbg & 32)) frame_store<NTF>(fr, frame);
   if (push_stack) frame_push_store<NTF>(fr, push_stack + b * FB, push_rows ? push_rows + (push_t[0] * B + b) * FB : nullptr);
-  __syncthreads();
-
-  // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
-  // j → (kx = 2g + (j>>2), ci = j&3); col = co = r: one 16-B LDS read each.
-  bf16x8 wf1[8];
-#pragma unroll
-  for (int s = 0; s < 8; s++) wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&w1s[r * W1_PITCH + (s * 8 + 2 * g) * 4]));
-  const float bias1 = bf2f(b1[r]);
-
-  // ---- conv1: 28 M-tiles of 16 positions over 4 waves
-  for (int mt = wave; mt < NP1P / 16; mt += NTF / 64) {
-    const int p = min(mt * 16 + r, NP1 - 1);
-    const int oy = p / H1, ox = p - oy * H1;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (!(dbg & 1)) {
-#pragma unroll
-      for (int s = 0; s < 8; s++)
-        acc = mfma(frame8(frame, ((4 * oy + s) * P0 + 4 * ox + 2 * g) * 4), wf1[s], acc);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int q = mt * 16 + 4 * g + i;
-      if (q < NP1) {
-        const float v = fmaxf(acc[i] * (1.0f / 255.0f) + bias1, 0.f);
-        const int y = q / H1, x = q - y * H1;
-        h1p[((y + 2) * P1 + (x + 2)) * C1 + r] = f2bf(v);
-      }
-    }
-  }
-  // conv2 weight fragments (two 16-wide N tiles): k = 32s + 8g + j → pixel pp = 2s + (g>>1)
-  // (ky = pp>>2, kx = pp&3), ci = 8(g&1) + j
-  bf16x8 wf2[2][8];
-#pragma unroll
-  for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-    for (int s = 0; s < 8; s++) {  // pixel pp = (ky, kx) → canonical offset pp*16 + ci
-      const int pp = 2 * s + (g >> 1), co = nt * 16 + r;
-      wf2[nt][s] = as_bf(*reinterpret_cast<const u16x8*>(&w2s[co * W2_PITCH + pp * 16 + 8 * (g & 1)]));
-    }
-  const float bias2[2] = {bf2f(b2[r]), bf2f(b2[16 + r])};
-  __syncthreads();
-  // h1 out for backward: coalesced 16-B rows from the LDS tile
-  if (h1_out && !(dbg & 16)) {
-    for (int v = threadIdx.x; v < NP1 * 2; v += NTF) {
-      const int p = v >> 1, y = p / H1, x = p - y * H1;
-      *reinterpret_cast<uint4*>(&h1_out[(b * NP1 + p) * C1 + 8 * (v & 1)]) =
-          *reinterpret_cast<const uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1)]);
-    }
-  }
-  unsigned short* h2s = reinterpret_cast<unsigned short*>(frame);  // frame is dead after conv1
-
-  // ---- conv2: 8 M-tiles (wave w: w, w+4) x 2 N-tiles
-  for (int mt = wave; mt < NP2P / 16; mt += NTF / 64) {
-    const int q = min(mt * 16 + r, NP2 - 1);
-    const int oy = q / H2, ox = q - oy * H2;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    if (!(dbg & 2)) {
-#pragma unroll
-      for (int s = 0; s < 8; s++) {
-        const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
-        const u16x8 av =
-            *reinterpret_cast<const u16x8*>(&h1p[((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1)]);
-        const bf16x8 a = as_bf(av);
-        acc0 = mfma(a, wf2[0][s], acc0);
-        acc1 = mfma(a, wf2[1][s], acc1);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int qq = mt * 16 + 4 * g + i;
-      if (qq < NP2) {
-        h2s[qq * C2 + r] = f2bf(fmaxf(acc0[i] + bias2[0], 0.f));
-        h2s[qq * C2 + 16 + r] = f2bf(fmaxf(acc1[i] + bias2[1], 0.f));
-      }
-    }
-  }
-  __syncthreads();
-  if (dbg & 64) return;
-  for (int v = threadIdx.x; v < NP2 * C2 / 8; v += NTF)
-    *reinterpret_cast<uint4*>(&h2_out[b * NP2 * C2 + 8 * v]) = *reinterpret_cast<const uint4*>(&h2s[8 * v]);
+  // trunk_convs' first barrier covers the border / h1p zeros, the weights and pass 0's frame rows
+  trunk_convs<NTF>(fr, fh, h1p, w1s, w2s, tb, h1_out ? h1_out + b * NP1 * C1 : nullptr, h2_out + b * NP2 * C2, dbg);
 }
 
 
@@ -818,9 +476,25 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
 }
 
 // Sum the G partials in a fixed order and write bf16 grads in each parameter's memory order.
-// Workgroup = 64 consecutive outputs x 8 slices of G (coalesced 256-B rows, 8 loads in flight per
-// lane), slices combined in LDS in a fixed order → deterministic.
-constexpr int RED_SLICES = 8;
+// Workgroup = 64 consecutive outputs x 8 slices of G; a slice's loads (G / 8 = 32 at G = 256) are
+// ALL issued before the first add: the partials were just written and sit in the MALL / L2, so the
+// cost is round trips, not bytes (a 4-load loop paid ~8 of them; float4 columns over 49 workgroups
+// measured slower: 6.3 vs 4.9 µs). The 8 slice sums are combined in LDS in a fixed order →
+// deterministic.
+constexpr int RED_SLICES = 8, RED_BATCH = 32;
+__device__ __forceinline__ unsigned short* trunk_grad_dst(int e, unsigned short* dW1, WStrides w1, unsigned short* db1,
+                                                          unsigned short* dW2, WStrides w2, unsigned short* db2) {
+  if (e < C1 * 256) {  // k = (ky, kx, ci)
+    const int co = e >> 8, k = e & 255, ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
+    return &dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3];
+  }
+  if (e < C1 * 256 + C2 * 256) {  // k = (ky, kx, ci)
+    const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+    return &dW2[co * w2.s0 + ci * w2.s1 + ky * w2.s2 + kx * w2.s3];
+  }
+  if (e < C1 * 256 + C2 * 256 + C1) return &db1[e - C1 * 256 - C2 * 256];
+  return &db2[e - C1 * 256 - C2 * 256 - C1];
+}
 __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ partial, int G,
                                                       unsigned short* __restrict__ dW1, WStrides w1,
                                                       unsigned short* __restrict__ db1,
@@ -833,30 +507,20 @@ __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ 
   unsigned short* dst = nullptr;
   AdamState st{0.f, 0.f, 0.f};
   if (owner) {
-    if (e < C1 * 256) {  // k = (ky, kx, ci)
-      const int co = e >> 8, k = e & 255, ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
-      dst = &dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3];
-    } else if (e < C1 * 256 + C2 * 256) {  // k = (ky, kx, ci)
-      const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
-      dst = &dW2[co * w2.s0 + ci * w2.s1 + ky * w2.s2 + kx * w2.s3];
-    } else if (e < C1 * 256 + C2 * 256 + C1) {
-      dst = &db1[e - C1 * 256 - C2 * 256];
-    } else {
-      dst = &db2[e - C1 * 256 - C2 * 256 - C1];
-    }
+    dst = trunk_grad_dst(e, dW1, w1, db1, dW2, w2, db2);
     st = adam_prefetch(fa, dst);  // fused Adam: state loads fly during the partial sums
   }
   float s = 0.f;
   if (e < PART) {
-    int gi = slice;
-    for (; gi + 3 * RED_SLICES < G; gi += 4 * RED_SLICES) {
-      const float a0 = partial[int64_t(gi) * PART + e];
-      const float a1 = partial[int64_t(gi + RED_SLICES) * PART + e];
-      const float a2 = partial[int64_t(gi + 2 * RED_SLICES) * PART + e];
-      const float a3 = partial[int64_t(gi + 3 * RED_SLICES) * PART + e];
-      s += (a0 + a1) + (a2 + a3);
+    for (int g0 = slice; g0 < G; g0 += RED_SLICES * RED_BATCH) {
+      float v[RED_BATCH];
+#pragma unroll
+      for (int j = 0; j < RED_BATCH; j++)  // clamped, unconditional: every load of the batch in flight
+        v[j] = partial[int64_t(min(g0 + RED_SLICES * j, G - 1)) * PART + e];
+#pragma unroll
+      for (int j = 0; j < RED_BATCH; j++)
+        if (g0 + RED_SLICES * j < G) s += v[j];
     }
-    for (; gi < G; gi += RED_SLICES) s += partial[int64_t(gi) * PART + e];
   }
   red[slice][c] = s;
   __syncthreads();

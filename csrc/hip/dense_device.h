@@ -1,0 +1,207 @@
+// Device helpers of the dense-tail kernels (dense_kernels.hip) shared with the persistent rollout
+// server (rollout_server.hip): bf16 / MFMA helpers, the K13s split-K unit, the K16 head + sampling row.
+#pragma once
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+
+namespace rmm {
+namespace hip {
+namespace dense {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int H = 256;       // hidden width
+constexpr int AMAX = 16;     // head width (A+1) limit
+
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<unsigned short>(u >> 16);
+}
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(uint32_t(h) << 16); }
+__device__ __forceinline__ bf16x8 as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// One K13s unit (a WM x WN-wave tile of FM x FN 16x16 fragments over K slice `sl`, KW = 4 / (WM WN)
+// waves splitting its k-steps and combining through LDS), executed by the 4 waves wave0 .. wave0+3 of
+// the calling workgroup. `red` holds (KW-1) x FM*FN x 64 f32x4. Every wave of the workgroup must
+// call it the same number of times (it holds a workgroup barrier when KW > 1); a call with
+// valid == false computes nothing and stores nothing. Shared by k_dense_fwd_part and the
+// persistent rollout server (rollout_server.hip): identical arithmetic → identical partials.
+template <int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void dense_part_unit(const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
+                                                int64_t M, int64_t K, int N, int S, float* __restrict__ part,
+                                                int64_t sl, int64_t tm, int64_t tn, int wave, bool valid,
+                                                f32x4 (*red)[FM * FN][64]) {
+  constexpr int KW = 4 / (WM * WN);
+  static_assert(WM * WN * KW == 4, "4 waves per unit");
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int sub = wave / KW, kw = wave % KW;
+  const int64_t m0 = tm * 16 * FM * WM + (sub / WN) * 16 * FM, n0 = tn * 16 * FN * WN + (sub % WN) * 16 * FN;
+  const int64_t steps = K / 32, lo = valid ? steps * sl / S : 0, hi = valid ? steps * (sl + 1) / S : 0;
+  const unsigned short* xa[FM];
+  const unsigned short* wb[FN];
+#pragma unroll
+  for (int i = 0; i < FM; i++) xa[i] = x + min(m0 + 16 * i + r, M - 1) * K + 8 * g;
+#pragma unroll
+  for (int j = 0; j < FN; j++) wb[j] = w + (valid ? (n0 + 16 * j + r) : 0) * K + 8 * g;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; i++)
+#pragma unroll
+    for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int64_t k = lo + kw;
+  for (; k + KW < hi; k += 2 * KW) {  // two of this wave's k-steps per batch: 2 (FM + FN) loads in flight
+    u16x8 av[2][FM], bv[2][FN];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+#pragma unroll
+      for (int i = 0; i < FM; i++) av[c][i] = *reinterpret_cast<const u16x8*>(xa[i] + (k + KW * c) * 32);
+#pragma unroll
+      for (int j = 0; j < FN; j++) bv[c][j] = *reinterpret_cast<const u16x8*>(wb[j] + (k + KW * c) * 32);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+      for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = mfma(as_bf(av[c][i]), as_bf(bv[c][j]), acc[i][j]);
+  }
+  if (k < hi) {
+    u16x8 av[FM], bv[FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++) av[i] = *reinterpret_cast<const u16x8*>(xa[i] + k * 32);
+#pragma unroll
+    for (int j = 0; j < FN; j++) bv[j] = *reinterpret_cast<const u16x8*>(wb[j] + k * 32);
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+      for (int j = 0; j < FN; j++) acc[i][j] = mfma(as_bf(av[i]), as_bf(bv[j]), acc[i][j]);
+  }
+  if constexpr (KW > 1) {
+    if (kw > 0) {
+#pragma unroll
+      for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) red[kw - 1][i * FN + j][lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (kw == 0) {
+#pragma unroll
+      for (int q = 0; q < KW - 1; q++)
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+          for (int j = 0; j < FN; j++) acc[i][j] += red[q][i * FN + j][lane];
+    }
+    __syncthreads();  // red is free for the next unit
+    if (kw != 0) return;
+  }
+  if (!valid) return;
+  float* out = part + (sl * M) * N + n0 + r;
+#pragma unroll
+  for (int i = 0; i < FM; i++)
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t row = m0 + 16 * i + 4 * g + e;
+      if (row < M)
+#pragma unroll
+        for (int j = 0; j < FN; j++) out[row * N + 16 * j] = acc[i][j][e];
+    }
+}
+
+// Consumer prologue of K13s: a lane's 4 hidden values of row rr = bf16(ReLU(Σ_s part[s] + b)),
+// summed in slice order (deterministic), rounded exactly like K13's epilogue. Without partials
+// (hpart == nullptr) the bf16 hidden row is read as before.
+__device__ __forceinline__ void load_hidden4(const unsigned short* __restrict__ hid, const float* __restrict__ hpart,
+                                             int S, const unsigned short* __restrict__ hb, int64_t M, int64_t rr,
+                                             int lane, float hv[4], uint2& bits) {
+  if (hpart == nullptr) {
+    bits = *reinterpret_cast<const uint2*>(&hid[rr * H + 4 * lane]);
+  } else {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* p = hpart + rr * H + 4 * lane;
+    for (int s = 0; s < S; s++) {
+      const float4 v = *reinterpret_cast<const float4*>(p + int64_t(s) * M * H);
+      a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
+    }
+    const uint2 bb = *reinterpret_cast<const uint2*>(&hb[4 * lane]);
+    const unsigned short o0 = f2bf(fmaxf(a.x + __uint_as_float(bb.x << 16), 0.f));
+    const unsigned short o1 = f2bf(fmaxf(a.y + __uint_as_float(bb.x & 0xffff0000u), 0.f));
+    const unsigned short o2 = f2bf(fmaxf(a.z + __uint_as_float(bb.y << 16), 0.f));
+    const unsigned short o3 = f2bf(fmaxf(a.w + __uint_as_float(bb.y & 0xffff0000u), 0.f));
+    bits = make_uint2(uint32_t(o0) | (uint32_t(o1) << 16), uint32_t(o2) | (uint32_t(o3) << 16));
+  }
+  hv[0] = __uint_as_float(bits.x << 16), hv[1] = __uint_as_float(bits.x & 0xffff0000u);
+  hv[2] = __uint_as_float(bits.y << 16), hv[3] = __uint_as_float(bits.y & 0xffff0000u);
+}
+
+// one env row of K16 (one wave): head GEMV + bias, bf16 rounding, Gumbel-max draw, row stores
+template <int A1>
+__device__ __forceinline__ void heads_sample_row(const unsigned short* __restrict__ hid, const float* whs,
+                                                 const float* bhs, const int64_t t, const uint32_t c, uint32_t seed,
+                                                 int64_t* __restrict__ act, float* __restrict__ logp,
+                                                 float* __restrict__ vf, float* __restrict__ lout,
+                                                 int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane,
+                                                 const float* __restrict__ hpart, int S,
+                                                 const unsigned short* __restrict__ hb) {
+  constexpr int A = A1 - 1;
+  float hv[4];
+  uint2 hbits;
+  load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
+  const float h0 = hv[0], h1 = hv[1], h2 = hv[2], h3 = hv[3];
+  float hd[A1];
+#pragma unroll
+  for (int a = 0; a < A1; a++) {
+    const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+    hd[a] = h0 * w.x + h1 * w.y + h2 * w.z + h3 * w.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
+#pragma unroll
+  for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));
+  const int64_t o = t * B + b;
+  if (lane < A) {
+    float l = hd[0];
+#pragma unroll
+    for (int j = 1; j < A; j++)
+      if (lane == j) l = hd[j];
+    lout[o * A + lane] = l;
+  }
+  if (lane == 0) {
+    float best = -INFINITY, mx = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int j = 0; j < A; j++) {
+      mx = fmaxf(mx, hd[j]);
+      const uint32_t hh = hash3(seed, c, uint32_t(b * A + j));
+      const float u = (float(hh >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float gmb = hd[j] - __logf(-__logf(u));
+      if (gmb > best) {
+        best = gmb;
+        arg = j;
+      }
+    }
+    float se = 0.f, la = hd[0];
+#pragma unroll
+    for (int j = 0; j < A; j++) {
+      se += __expf(hd[j] - mx);
+      if (j == arg) la = hd[j];
+    }
+    act[o] = arg;
+    act_now[b] = arg;
+    logp[o] = la - mx - __logf(se);
+    vf[o] = hd[A];
+  }
+}
+
+}  // namespace dense
+}  // namespace hip
+}  // namespace rmm

@@ -17,21 +17,21 @@
 // C/D col l&15, row 4(l>>4)+i.
 #include <hip/hip_bf16.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "common.h"
+#include "dense_device.h"
 #include "kernels.h"
 
 namespace rmm {
 namespace hip {
 namespace dense {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int H = 256;       // hidden width
 constexpr int MC = 32;       // rows per chunk
 constexpr int JB = 32;       // columns of x / W per workgroup
-constexpr int AMAX = 16;     // head width (A+1) limit
 constexpr int NT = 512;      // 8 waves
 constexpr int HP = H + 8;    // padded pitches (bank spread, keep 16-B alignment)
 constexpr int MP = MC + 8;
@@ -43,16 +43,6 @@ static_assert(MC * JB / 2 == NT, "x staging: one (row, column pair) per thread")
 // (__syncthreads() carries a workgroup fence that drains vmcnt to 0 first.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__device__ __forceinline__ unsigned short f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<unsigned short>(u >> 16);
-}
-__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(uint32_t(h) << 16); }
-__device__ __forceinline__ bf16x8 as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
-__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 
 // dpre = (dheads · Wh) ⊙ [hidden > 0], computed ONCE for the batch (32 rows per workgroup) and
 // read by every column-block workgroup of k_dense_heads_bwd. Recomputing it inside each of those
@@ -369,11 +359,50 @@ constexpr int K12_RB = (K12_WS + K12_XS + K12_DXS) > (K12_YS + K12_DZS) ? (K12_W
                                                                        : (K12_YS + K12_DZS);
 static_assert((K12_LDS_DM + K12_RB) * 2 <= 160 * 1024, "K12 LDS");
 
+// Row split of K12 (round 4): each column block (and the head role) runs as RS workgroups over
+// disjoint chunk ranges of the batch — 244 instead of 122 workgroups at M = 500, half the serial
+// chunk chain each. dx rows are independent; the dW / head partials (fp32, 16-20 per lane) are
+// combined by the LAST workgroup of the group to finish (device-scope arrival counter, reset by
+// that workgroup for the next launch), summed in group order (h = 0, 1, ...) whoever arrives last
+// → deterministic. No workgroup waits for another (no co-residency assumption).
+constexpr int K12_PSLOTS = 20;  // partial floats per lane (head role: 8 dWh + 8 db + 4 dbh)
+struct RowSplit {
+  float* part = nullptr;      // [groups][rs][K12_PSLOTS][NT]
+  unsigned int* cnt = nullptr;  // [groups] arrival counters (zero between launches)
+  int rs = 1, h = 0, group = 0;
+};
+// Publish this workgroup's `n` partial slots and arrive; true in the workgroup that must finish
+// the group (it then reads every member's slots through k12_sum).
+__device__ __forceinline__ bool k12_arrive(const RowSplit& rsp, const float* v, int n) {
+  __shared__ unsigned int last;
+  float* my = rsp.part + ((int64_t(rsp.group) * rsp.rs + rsp.h) * K12_PSLOTS) * NT + threadIdx.x;
+  for (int i = 0; i < n; i++) my[i * NT] = v[i];
+  __syncthreads();  // every wave's stores have reached the L2
+  if (threadIdx.x == 0) {
+    __threadfence();  // release: write the partials back for the other XCDs
+    last = atomicAdd(&rsp.cnt[rsp.group], 1u) == unsigned(rsp.rs - 1);
+    if (last) {
+      __threadfence();  // acquire: drop stale lines before reading the other members' partials
+      rsp.cnt[rsp.group] = 0u;
+    }
+  }
+  __syncthreads();
+  return last;
+}
+// slot i summed over the group's members in order h = 0 .. rs-1 (own value taken from registers)
+__device__ __forceinline__ float k12_sum(const RowSplit& rsp, int i, float own) {
+  float t = 0.f;
+  for (int h = 0; h < rsp.rs; h++)
+    t += h == rsp.h ? own : rsp.part[((int64_t(rsp.group) * rsp.rs + h) * K12_PSLOTS + i) * NT + threadIdx.x];
+  return t;
+}
+
 // column-block role: dx[:, J] and dW[:, J] for J = [J0, J0+32)
 __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
                                          const unsigned short* __restrict__ dpre, int64_t M, int64_t K, int64_t J0,
                                          unsigned short* __restrict__ dx, unsigned short* __restrict__ dw,
-                                         unsigned short* dm, unsigned short* rb, const FusedAdam& fa) {
+                                         unsigned short* dm, unsigned short* rb, const FusedAdam& fa, int c0, int c1,
+                                         const RowSplit& rsp) {
   unsigned short* ws = rb;                    // [jt][h][16]  W[:, J] (setup only)
   unsigned short* xs = rb + K12_WS;           // [buf][jt][m][16]
   unsigned short* dxs = rb + K12_WS + K12_XS; // [m][DXP]
@@ -415,15 +444,15 @@ __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, c
       const int v = tid + NT * k, h = v >> 2, pc = v & 3;
       wv[k] = *reinterpret_cast<const uint4*>(&w[int64_t(h) * K + J0 + 8 * pc]);
     }
-    load(0);
+    load(c0);
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int v = tid + NT * k, h = v >> 2, pc = v & 3;
       *reinterpret_cast<uint4*>(&ws[((pc >> 1) * H + h) * 16 + 8 * (pc & 1)]) = wv[k];
     }
   }
-  store(0);
-  if (NC > 1) load(1);
+  store(c0);
+  if (c0 + 1 < c1) load(c0 + 1);
   lds_barrier();
 
   // Wᵀ fragments for this wave's column tile nt: A[row j = 16nt + r][k = h = 32s + 8g + e]
@@ -447,7 +476,7 @@ __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, c
 #pragma unroll
       for (int i = 0; i < 4; i++) ast[hi][jt][i] = adam_prefetch(fa, dw_at(hi, jt, i));
 
-  for (int c = 0; c < NC; c++) {
+  for (int c = c0; c < c1; c++) {
     const unsigned short* d = dm + (c & 1) * MC2 * DMP;
     const unsigned short* xb = xs + (c & 1) * 2 * MC2 * 16;
     {  // dxᵀ tile: D[j][m] = Σ_h Wᵀ[j][h] · dpre[m][h]  (B = dpre row reads)
@@ -480,16 +509,34 @@ __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, c
         adw[hi][1] = mfma(ad, bx[1], adw[hi][1]);
       }
     }
-    if (c + 1 < NC) store(c + 1);  // loaded one chunk ago
-    if (c + 2 < NC) load(c + 2);   // in flight across the barrier and the next chunk's MFMAs
+    if (c + 1 < c1) store(c + 1);  // loaded one chunk ago
+    if (c + 2 < c1) load(c + 2);   // in flight across the barrier and the next chunk's MFMAs
     lds_barrier();
   }
+  (void)NC;
 
-  for (int v = tid; v < int(M) * (JB / 8); v += NT) {
+  const int r0 = c0 * MC2, r1 = int(min(int64_t(c1) * MC2, M));
+  for (int v = tid + r0 * (JB / 8); v < r1 * (JB / 8); v += NT) {
     const int row = v >> 2, pc = v & 3;
     *reinterpret_cast<uint4*>(&dx[int64_t(row) * K + J0 + 8 * pc]) = *reinterpret_cast<const uint4*>(&dxs[row * DXP + 8 * pc]);
   }
-  // dW[:, J] is final here (this workgroup reduced every row): store it, or apply Adam to it
+  if (rsp.rs > 1) {  // dW[:, J] over this workgroup's rows only: the group's last finisher sums them
+    float pv[16];
+#pragma unroll
+    for (int hi = 0; hi < 2; hi++)
+#pragma unroll
+      for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) pv[(hi * 2 + jt) * 4 + i] = adw[hi][jt][i];
+    if (!k12_arrive(rsp, pv, 16)) return;
+#pragma unroll
+    for (int hi = 0; hi < 2; hi++)
+#pragma unroll
+      for (int jt = 0; jt < 2; jt++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) adw[hi][jt][i] = k12_sum(rsp, (hi * 2 + jt) * 4 + i, pv[(hi * 2 + jt) * 4 + i]);
+  }
+  // dW[:, J] is final here (every row reduced): store it, or apply Adam to it
   const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
 #pragma unroll
   for (int hi = 0; hi < 2; hi++)
@@ -506,7 +553,7 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
                                          const unsigned short* __restrict__ dpre, int64_t M,
                                          unsigned short* __restrict__ db, unsigned short* __restrict__ dwh,
                                          unsigned short* __restrict__ dbh, unsigned short* dm, unsigned short* rb,
-                                         const FusedAdam& fa) {
+                                         const FusedAdam& fa, int c0, int c1, const RowSplit& rsp) {
   unsigned short* ys = rb;            // [buf][m][DMP]
   unsigned short* dzs = rb + K12_YS;  // [m][16] (a >= A1 and rows >= M zero)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
@@ -543,16 +590,17 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
       const int e = tid + NT * k, m = e >> 4, a = e & 15;
       zv[k] = dz[int64_t(min(int64_t(m), M - 1)) * A1 + min(a, A1 - 1)];
     }
-    load(0);
+    load(c0);
 #pragma unroll
     for (int k = 0; k < PZ; k++) {
       const int e = tid + NT * k, m = e >> 4, a = e & 15;
       dzs[e] = (m < M && a < A1) ? zv[k] : static_cast<unsigned short>(0);
     }
   }
-  store(0);
-  if (NC > 1) load(1);
+  store(c0);
+  if (c0 + 1 < c1) load(c0 + 1);
   lds_barrier();
+  (void)NC;
 
   u16x8 onev;
 #pragma unroll
@@ -573,7 +621,7 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
 #pragma unroll
   for (int i = 0; i < 4; i++) sbh[i] = adam_prefetch(fa, &dbh[min(4 * g + i, A1 - 1)]);
 
-  for (int c = 0; c < NC; c++) {
+  for (int c = c0; c < c1; c++) {
     const int o = (c & 1) * MC2 * DMP;
 #pragma unroll
     for (int ks = 0; ks < MC2 / 32; ks++) {
@@ -589,9 +637,25 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
       }
       if (wave == 0) abh = mfma(az, ones, abh);
     }
-    if (c + 1 < NC) store(c + 1);
-    if (c + 2 < NC) load(c + 2);
+    if (c + 1 < c1) store(c + 1);
+    if (c + 2 < c1) load(c + 2);
     lds_barrier();
+  }
+  if (rsp.rs > 1) {  // partial over this workgroup's rows: the group's last finisher sums them
+    float pv[K12_PSLOTS];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      pv[i] = awh[0][i], pv[4 + i] = awh[1][i], pv[8 + i] = adb[0][i], pv[12 + i] = adb[1][i], pv[16 + i] = abh[i];
+    }
+    if (!k12_arrive(rsp, pv, K12_PSLOTS)) return;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      awh[0][i] = k12_sum(rsp, i, pv[i]);
+      awh[1][i] = k12_sum(rsp, 4 + i, pv[4 + i]);
+      adb[0][i] = k12_sum(rsp, 8 + i, pv[8 + i]);
+      adb[1][i] = k12_sum(rsp, 12 + i, pv[12 + i]);
+      abh[i] = k12_sum(rsp, 16 + i, pv[16 + i]);
+    }
   }
   const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
 #pragma unroll
@@ -614,13 +678,19 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd2(
     const unsigned short* __restrict__ dz, const unsigned short* __restrict__ y, const unsigned short* __restrict__ x,
     const unsigned short* __restrict__ w, const unsigned short* __restrict__ dpre, int64_t M, int64_t K,
     unsigned short* __restrict__ dx, unsigned short* __restrict__ dw, unsigned short* __restrict__ db,
-    unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh, const FusedAdam fa) {
+    unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh, const FusedAdam fa, float* __restrict__ rs_part,
+    unsigned int* __restrict__ rs_cnt, int rs) {
   __shared__ __attribute__((aligned(16))) unsigned short dm[K12_LDS_DM];
   __shared__ __attribute__((aligned(16))) unsigned short rb[K12_RB];
-  if (int64_t(blockIdx.x) * JB == K)
-    k12_head<A1>(dz, y, dpre, M, db, dwh, dbh, dm, rb, fa);
+  // block = (role group, row split h); the RS members of a group are consecutive blocks
+  RowSplit rsp;
+  rsp.part = rs_part, rsp.cnt = rs_cnt, rsp.rs = rs, rsp.h = int(blockIdx.x) % rs, rsp.group = int(blockIdx.x) / rs;
+  const int NC = int((M + MC2 - 1) / MC2);
+  const int c0 = NC * rsp.h / rs, c1 = NC * (rsp.h + 1) / rs;
+  if (int64_t(rsp.group) * JB == K)
+    k12_head<A1>(dz, y, dpre, M, db, dwh, dbh, dm, rb, fa, c0, c1, rsp);
   else
-    k12_cols(x, w, dpre, M, K, int64_t(blockIdx.x) * JB, dx, dw, dm, rb, fa);
+    k12_cols(x, w, dpre, M, K, int64_t(rsp.group) * JB, dx, dw, dm, rb, fa, c0, c1, rsp);
 }
 
 // K13: hidden = ReLU(x Wᵀ + b) for small M (PPO minibatch / rollout batch). One 4-wave workgroup
@@ -699,110 +769,17 @@ __global__ __launch_bounds__(256) void k_dense_fwd_part(const unsigned short* __
                                                         const unsigned short* __restrict__ w, int64_t M, int64_t K,
                                                         int N, int S, float* __restrict__ part) {
   constexpr int KW = 4 / (WM * WN);
-  static_assert(WM * WN * KW == 4, "4 waves per workgroup");
-  __shared__ f32x4 red[KW > 1 ? KW - 1 : 1][KW > 1 ? FM * FN : 1][64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  __shared__ f32x4 red[KW > 1 ? KW - 1 : 1][FM * FN][64];
+  const int wave = threadIdx.x >> 6;
   const int nt = N / (16 * FN * WN);
   const int64_t mt = (M + 16 * FM * WM - 1) / (16 * FM * WM);
   const int64_t tiles = mt * nt, total = gridDim.x;
   int64_t id = blockIdx.x;
   if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
   const int64_t sl = id / tiles, rem = id % tiles, tm = rem / nt, tn = rem % nt;
-  const int sub = wave / KW, kw = wave % KW;
-  const int64_t m0 = tm * 16 * FM * WM + (sub / WN) * 16 * FM, n0 = tn * 16 * FN * WN + (sub % WN) * 16 * FN;
-  const int64_t steps = K / 32, lo = steps * sl / S, hi = steps * (sl + 1) / S;
-  const unsigned short* xa[FM];
-  const unsigned short* wb[FN];
-#pragma unroll
-  for (int i = 0; i < FM; i++) xa[i] = x + min(m0 + 16 * i + r, M - 1) * K + 8 * g;
-#pragma unroll
-  for (int j = 0; j < FN; j++) wb[j] = w + (n0 + 16 * j + r) * K + 8 * g;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; i++)
-#pragma unroll
-    for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int64_t k = lo + kw;
-  for (; k + KW < hi; k += 2 * KW) {  // two of this wave's k-steps per batch: 2 (FM + FN) loads in flight
-    u16x8 av[2][FM], bv[2][FN];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-#pragma unroll
-      for (int i = 0; i < FM; i++) av[c][i] = *reinterpret_cast<const u16x8*>(xa[i] + (k + KW * c) * 32);
-#pragma unroll
-      for (int j = 0; j < FN; j++) bv[c][j] = *reinterpret_cast<const u16x8*>(wb[j] + (k + KW * c) * 32);
-    }
-#pragma unroll
-    for (int c = 0; c < 2; c++)
-#pragma unroll
-      for (int i = 0; i < FM; i++)
-#pragma unroll
-        for (int j = 0; j < FN; j++) acc[i][j] = mfma(as_bf(av[c][i]), as_bf(bv[c][j]), acc[i][j]);
-  }
-  if (k < hi) {
-    u16x8 av[FM], bv[FN];
-#pragma unroll
-    for (int i = 0; i < FM; i++) av[i] = *reinterpret_cast<const u16x8*>(xa[i] + k * 32);
-#pragma unroll
-    for (int j = 0; j < FN; j++) bv[j] = *reinterpret_cast<const u16x8*>(wb[j] + k * 32);
-#pragma unroll
-    for (int i = 0; i < FM; i++)
-#pragma unroll
-      for (int j = 0; j < FN; j++) acc[i][j] = mfma(as_bf(av[i]), as_bf(bv[j]), acc[i][j]);
-  }
-  if constexpr (KW > 1) {
-    if (kw > 0) {
-#pragma unroll
-      for (int i = 0; i < FM; i++)
-#pragma unroll
-        for (int j = 0; j < FN; j++) red[kw - 1][i * FN + j][lane] = acc[i][j];
-    }
-    __syncthreads();
-    if (kw != 0) return;
-#pragma unroll
-    for (int q = 0; q < KW - 1; q++)
-#pragma unroll
-      for (int i = 0; i < FM; i++)
-#pragma unroll
-        for (int j = 0; j < FN; j++) acc[i][j] += red[q][i * FN + j][lane];
-  }
-  float* out = part + (sl * M) * N + n0 + r;
-#pragma unroll
-  for (int i = 0; i < FM; i++)
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const int64_t row = m0 + 16 * i + 4 * g + e;
-      if (row < M)
-#pragma unroll
-        for (int j = 0; j < FN; j++) out[row * N + 16 * j] = acc[i][j][e];
-    }
+  dense_part_unit<FM, FN, WM, WN>(x, w, M, K, N, S, part, sl, tm, tn, wave, true, red);
 }
 
-// Consumer prologue of K13s: a lane's 4 hidden values of row rr = bf16(ReLU(Σ_s part[s] + b)),
-// summed in slice order (deterministic), rounded exactly like K13's epilogue. Without partials
-// (hpart == nullptr) the bf16 hidden row is read as before.
-__device__ __forceinline__ void load_hidden4(const unsigned short* __restrict__ hid, const float* __restrict__ hpart,
-                                             int S, const unsigned short* __restrict__ hb, int64_t M, int64_t rr,
-                                             int lane, float hv[4], uint2& bits) {
-  if (hpart == nullptr) {
-    bits = *reinterpret_cast<const uint2*>(&hid[rr * H + 4 * lane]);
-  } else {
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* p = hpart + rr * H + 4 * lane;
-    for (int s = 0; s < S; s++) {
-      const float4 v = *reinterpret_cast<const float4*>(p + int64_t(s) * M * H);
-      a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
-    }
-    const uint2 bb = *reinterpret_cast<const uint2*>(&hb[4 * lane]);
-    const unsigned short o0 = f2bf(fmaxf(a.x + __uint_as_float(bb.x << 16), 0.f));
-    const unsigned short o1 = f2bf(fmaxf(a.y + __uint_as_float(bb.x & 0xffff0000u), 0.f));
-    const unsigned short o2 = f2bf(fmaxf(a.z + __uint_as_float(bb.y << 16), 0.f));
-    const unsigned short o3 = f2bf(fmaxf(a.w + __uint_as_float(bb.y & 0xffff0000u), 0.f));
-    bits = make_uint2(uint32_t(o0) | (uint32_t(o1) << 16), uint32_t(o2) | (uint32_t(o3) << 16));
-  }
-  hv[0] = __uint_as_float(bits.x << 16), hv[1] = __uint_as_float(bits.x & 0xffff0000u);
-  hv[2] = __uint_as_float(bits.y << 16), hv[3] = __uint_as_float(bits.y & 0xffff0000u);
-}
 
 
 // K14 — the A1-wide head GEMM heads[M, A1] = hidden[M, 256] Whᵀ + bh (bf16 in/out, fp32 accumulate).
@@ -980,66 +957,6 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
   }
 }
 
-// one env row of K16 (one wave): head GEMV + bias, bf16 rounding, Gumbel-max draw, row stores
-template <int A1>
-__device__ __forceinline__ void heads_sample_row(const unsigned short* __restrict__ hid, const float* whs,
-                                                 const float* bhs, const int64_t t, const uint32_t c, uint32_t seed,
-                                                 int64_t* __restrict__ act, float* __restrict__ logp,
-                                                 float* __restrict__ vf, float* __restrict__ lout,
-                                                 int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane,
-                                                 const float* __restrict__ hpart, int S,
-                                                 const unsigned short* __restrict__ hb) {
-  constexpr int A = A1 - 1;
-  float hv[4];
-  uint2 hbits;
-  load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
-  const float h0 = hv[0], h1 = hv[1], h2 = hv[2], h3 = hv[3];
-  float hd[A1];
-#pragma unroll
-  for (int a = 0; a < A1; a++) {
-    const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
-    hd[a] = h0 * w.x + h1 * w.y + h2 * w.z + h3 * w.w;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
-#pragma unroll
-  for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));
-  const int64_t o = t * B + b;
-  if (lane < A) {
-    float l = hd[0];
-#pragma unroll
-    for (int j = 1; j < A; j++)
-      if (lane == j) l = hd[j];
-    lout[o * A + lane] = l;
-  }
-  if (lane == 0) {
-    float best = -INFINITY, mx = -INFINITY;
-    int arg = 0;
-#pragma unroll
-    for (int j = 0; j < A; j++) {
-      mx = fmaxf(mx, hd[j]);
-      const uint32_t hh = hash3(seed, c, uint32_t(b * A + j));
-      const float u = (float(hh >> 8) + 0.5f) * (1.0f / 16777216.0f);
-      const float gmb = hd[j] - __logf(-__logf(u));
-      if (gmb > best) {
-        best = gmb;
-        arg = j;
-      }
-    }
-    float se = 0.f, la = hd[0];
-#pragma unroll
-    for (int j = 0; j < A; j++) {
-      se += __expf(hd[j] - mx);
-      if (j == arg) la = hd[j];
-    }
-    act[o] = arg;
-    act_now[b] = arg;
-    logp[o] = la - mx - __logf(se);
-    vf[o] = hd[A];
-  }
-}
 
 // K16 — the rollout step's head layer + action sampling in ONE launch (replaces K14 + K7). One wave
 // per env row as in K14; after the butterfly every lane holds the bf16-rounded head row; lane 0
@@ -1113,6 +1030,33 @@ __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __
     *t_ptr = t + 1;
     if (ctr != t_ptr) *ctr = int64_t(c) + 1;
   }
+}
+// K12 row-split workspace: partials + zeroed arrival counters, one per (device, groups, rs),
+// allocated on first use (outside any graph capture: the learner's eager warm-up steps come first)
+// and kept for the process lifetime.
+void k12_split_ws(int groups, int rs, hipStream_t stream, float** part, unsigned int** cnt) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int>, std::pair<float*, unsigned int*>> cache;
+  int dev = 0;
+  RMM_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto key = std::make_tuple(dev, groups, rs);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    RMM_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("dense_heads_bwd: run one step eagerly before capturing (K12 row-split workspace)");
+    float* p = nullptr;
+    unsigned int* c = nullptr;
+    RMM_HIP_CHECK(hipMalloc(&p, sizeof(float) * size_t(groups) * rs * K12_PSLOTS * NT));
+    RMM_HIP_CHECK(hipMalloc(&c, sizeof(unsigned int) * size_t(groups)));
+    RMM_HIP_CHECK(hipMemset(c, 0, sizeof(unsigned int) * size_t(groups)));
+    RMM_HIP_CHECK(hipDeviceSynchronize());
+    it = cache.emplace(key, std::make_pair(p, c)).first;
+  }
+  *part = it->second.first;
+  *cnt = it->second.second;
 }
 }  // namespace dense
 
@@ -1294,13 +1238,27 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   if (fa.grad_base && fa.bump) throw std::invalid_argument("dense_heads_bwd: the step counters advance in the trunk reduce");
   const dim3 pgrid(uint32_t((M + dense::MC - 1) / dense::MC));
   auto* dp = V(dpre_scratch);
+  // K12 row split (RMM_K12_SPLIT=2 enables): measured SLOWER on MI355X (fused loop 12.38 vs 10.89
+  // ms/iter, K12 29.1 vs 13.2 µs): each of the 244 workgroups' agent-scope release fence writes
+  // back its XCD's whole L2 (dx included) before the arrival atomic. Kept opt-in for A/B.
+  static const int split_env = [] {
+    const char* e = std::getenv("RMM_K12_SPLIT");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int nc = int((M + dense::MC2 - 1) / dense::MC2);
+  const int rs = v2 ? std::max(1, std::min(split_env, nc)) : 1;
+  const int groups = int(K / dense::JB + 1);
+  float* rs_part = nullptr;
+  unsigned int* rs_cnt = nullptr;
+  if (rs > 1) dense::k12_split_ws(groups, rs, stream, &rs_part, &rs_cnt);
+  const dim3 grid3(uint32_t(groups * rs));
 #define RMM_K12(N)                                                                                               \
   case N:                                                                                                        \
     if (!dpre_ready || !v2)                                                                                      \
       hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);            \
     if (v2)                                                                                                      \
-      hipLaunchKernelGGL(dense::k_dense_heads_bwd2<N>, grid2, block, 0, stream, U(dz), U(y), U(x), U(w), dp, M, \
-                         K, V(dx), V(dw), V(db), V(dwh), V(dbh), fa);                                            \
+      hipLaunchKernelGGL(dense::k_dense_heads_bwd2<N>, grid3, block, 0, stream, U(dz), U(y), U(x), U(w), dp, M, \
+                         K, V(dx), V(dw), V(db), V(dwh), V(dbh), fa, rs_part, rs_cnt, rs);                       \
     else                                                                                                         \
       hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w),   \
                          dp, M, K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                         \

@@ -202,6 +202,34 @@ void vtrace(const float* blogp, const float* tlogp, const float* rew, const floa
             float* vs, float* pg, hipStream_t stream);
 // Page-locked DMA out of a shared-memory object-store segment: chunks of the registered segment
 // are hipHostRegister'ed on first use. Returns the bytes newly registered by this call.
+// K21 persistent rollout server (rollout_server.hip): one launch runs a hybrid worker's T policy
+// steps, synchronising with the host through mapped words (go / done_seq). Returns the grid size.
+struct RolloutServerArgs {
+  const void *W1 = nullptr, *b1 = nullptr, *W2 = nullptr, *b2 = nullptr;
+  int64_t w1s[4] = {0, 0, 0, 0}, w2s[4] = {0, 0, 0, 0};
+  const void *Wd = nullptr, *bd = nullptr, *Wh = nullptr, *bh = nullptr;
+  int64_t B = 0, T = 0;
+  int S = 0, A1 = 0;
+  uint32_t seed = 0;
+  uint8_t* stack = nullptr;
+  const uint8_t* nf = nullptr;
+  uint8_t* rows = nullptr;
+  void* h2 = nullptr;
+  float* hpart = nullptr;
+  int64_t* act = nullptr;
+  float *logp = nullptr, *vf = nullptr, *lout = nullptr;
+  int64_t* act_now = nullptr;
+  int64_t* ctr_t = nullptr;
+  const int64_t* go = nullptr;   // device view of the host word
+  int64_t* done_seq = nullptr;   // device view of the host word
+  unsigned int* bar = nullptr;   // 2 device words
+  int64_t* err_dev = nullptr;
+  int64_t* err_host = nullptr;   // device view of the host word
+  double go_timeout_s = 20.0, barrier_timeout_s = 5.0;
+  int workgroups = 0;            // 0: one per CU
+};
+int rollout_server_launch(const RolloutServerArgs& a, hipStream_t stream);
+
 void host_register_segment(uintptr_t base, uint64_t size);
 // Page-lock the registered-segment chunks covering [p, p+n); true if all of them are pinned
 // (then DMA straight from/to the range is safe). newly (optional) accumulates bytes pinned now.

@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <string>
 #include <chrono>
 #include <stdexcept>
 #include <thread>
@@ -176,6 +178,81 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
     throw;
   }
   for (auto e : ev) RMM_HIP_CHECK(hipEventDestroy(e));
+  return completed;
+}
+
+namespace {
+// Host words the rollout server synchronises through (pinned, device-mapped) and its device words,
+// allocated once per process (one hybrid worker runs one fragment at a time).
+struct ServerSync {
+  int64_t* host = nullptr;       // [0] go, [8] done_seq, [16] err  (separate 64-B lines)
+  int64_t* host_dev = nullptr;   // device view of `host`
+  unsigned int* bar = nullptr;   // 2 device words
+  int64_t* err_dev = nullptr;
+};
+ServerSync& server_sync() {
+  static ServerSync s;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    RMM_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.host), 256, hipHostMallocMapped));
+    RMM_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.host_dev), s.host, 0));
+    void* d = nullptr;
+    RMM_HIP_CHECK(hipMalloc(&d, 64));
+    s.bar = static_cast<unsigned int*>(d);
+    s.err_dev = reinterpret_cast<int64_t*>(static_cast<char*>(d) + 32);
+  });
+  return s;
+}
+}  // namespace
+
+std::vector<std::pair<double, int64_t>> hybrid_rollout_server(const RolloutGroup& g, RolloutServerArgs a, int64_t T,
+                                                              int threads, double wait_timeout_s) {
+  if (T <= 0) return {};
+  if (!g.env.pools || !g.act || !g.new_frames || !g.rew || !g.done || !g.ep_rew || !g.ep_len)
+    throw std::invalid_argument("hybrid_rollout_server: incomplete group");
+  ServerSync& sy = server_sync();
+  volatile int64_t* go = sy.host;
+  volatile int64_t* done_seq = sy.host + 8;
+  volatile int64_t* err = sy.host + 16;
+  *go = 0;
+  *done_seq = 0;
+  *err = 0;
+  a.T = T;
+  a.go = sy.host_dev;
+  a.done_seq = sy.host_dev + 8;
+  a.err_host = sy.host_dev + 16;
+  a.bar = sy.bar;
+  a.err_dev = sy.err_dev;
+  std::vector<std::pair<double, int64_t>> completed;
+  rollout_server_launch(a, g.stream);
+  double ph[3] = {0, 0, 0};
+  try {
+    EnvThreads pool(std::max(1, std::min(threads, 16)));
+    for (int64_t t = 0; t < T; t++) {
+      auto c0 = Clock::now();
+      __atomic_store_n(const_cast<int64_t*>(go), t + 1, __ATOMIC_RELEASE);  // step t's frames are staged
+      for (uint64_t k = 0;; k++) {  // the server stores step t's actions, then done_seq = t + 1
+        if (__atomic_load_n(const_cast<int64_t*>(done_seq), __ATOMIC_ACQUIRE) >= t + 1) break;
+        cpu_relax();
+        if ((k & 1023) == 1023) {
+          if (*err) throw std::runtime_error("rollout server error " + std::to_string(*err));
+          if (us_since(c0) > wait_timeout_s * 1e6) throw std::runtime_error("rollout server: step timed out");
+        }
+      }
+      ph[0] += us_since(c0);
+      c0 = Clock::now();
+      pool.step(g, g.env.step[0]++, t);
+      rl::episode_update(g.env.n, g.rew + t * g.env.n, g.done + t * g.env.n, g.ep_rew, g.ep_len, completed);
+      ph[1] += us_since(c0);
+    }
+    RMM_HIP_CHECK(hipStreamSynchronize(g.stream));
+    if (*err) throw std::runtime_error("rollout server error " + std::to_string(*err));
+  } catch (...) {
+    __atomic_store_n(const_cast<int64_t*>(go), int64_t(-1), __ATOMIC_RELEASE);  // abort: every wait exits
+    (void)hipStreamSynchronize(g.stream);
+    throw;
+  }
+  for (int k = 0; k < 3; k++) g_phase_us[k] = ph[k];
   return completed;
 }
 

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "../rl/synth_env.h"
+#include "kernels.h"
 
 namespace rmm {
 namespace hip {
@@ -33,6 +34,13 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
                                                        int threads = 1, bool spin = false);
 // µs the last hybrid_rollout call spent {waiting for policy steps, in env steps, launching steps}
 std::vector<double> hybrid_rollout_phases();
+
+// The same loop over ONE group with the K21 persistent rollout server: one kernel launch for the
+// fragment; per step the host releases the step (`go`), waits for the server's `done_seq` (spin,
+// bounded), steps the envs. `a` carries the weights / buffers; its sync words are filled in here.
+// Throws (after aborting and draining the kernel) on a server timeout or a host-side failure.
+std::vector<std::pair<double, int64_t>> hybrid_rollout_server(const RolloutGroup& g, RolloutServerArgs a, int64_t T,
+                                                              int threads = 1, double wait_timeout_s = 30.0);
 
 }  // namespace hip
 }  // namespace rmm

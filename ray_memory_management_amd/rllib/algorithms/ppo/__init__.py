@@ -192,6 +192,7 @@ class PPO(Algorithm):
         per_round = c.num_workers * c.rollout_fragment_length * c.num_envs_per_worker
         rounds = max(1, -(-c.train_batch_size // max(per_round, 1)))
         dev = self._device_weights_ok()
+        shared = dev and self._shared_weights_ok()
         for r in range(rounds):
             for i, w in enumerate(remote):
                 if r == 0 and self._weights_ref is not None:
@@ -209,7 +210,10 @@ class PPO(Algorithm):
         # the weight publication is queued right behind the update on each learner (actor calls run
         # in order), so it runs while the driver is still collecting the update's stats: no extra
         # driver round trip before the next iteration's set_weights + sample
-        if dev:  # GPU rollout workers read the learners' bf16 weights from HBM (hipIPC)
+        if shared:  # once: the learners move their bf16 weights into HBM objects the workers alias
+            if self._dev_refs is None:
+                self._dev_refs = self.learner_group.shared_weights_refs()
+        elif dev:  # GPU rollout workers read the learners' bf16 weights from HBM (hipIPC)
             self._dev_refs = self.learner_group.device_weights_refs()
         else:
             self._weights_ref = self.learner_group.weights_ref()
@@ -224,6 +228,17 @@ class PPO(Algorithm):
         return st
 
     _dev_refs = None
+
+    def _shared_weights_ok(self) -> bool:
+        """Rollout workers alias the learners' live HBM weights (zero-copy, set once) instead of
+        receiving a copy per iteration. Opt-in (RMM_SHARED_WEIGHTS=1 or config
+        share_device_weights=True): profiles/shared_weights_r3_fault.txt."""
+        import os
+
+        env = os.environ.get("RMM_SHARED_WEIGHTS")
+        if env is not None:
+            return env == "1"
+        return bool(getattr(self.algo_config, "share_device_weights", False))
 
     def _device_weights_ok(self) -> bool:
         """Weights go learner → rollout workers through HBM when both sides are GPU processes:

@@ -73,6 +73,32 @@ class GPURolloutWorker:
     def set_weights(self, weights, global_vars=None):
         import torch
 
+        if isinstance(weights, dict) and "__rmm_shared_bf16__" in weights:  # learner's live HBM weights
+            import ray_memory_management_amd as rt
+
+            ref = weights["__rmm_shared_bf16__"][0]
+            if getattr(self, "_shared_key", None) == ref.binary():
+                return  # already aliased: the learner updated them in place
+            flat = rt.get(ref)  # zero-copy (hipIPC) view of the learner's weights
+            params = dict(self.model.named_parameters())
+            with torch.no_grad():
+                if flat.device == self.device:  # same GPU: point the parameters at the learner's HBM
+                    for name, off, shape, stride in weights["__rmm_layout__"]:
+                        if name in params:
+                            params[name].data = flat.as_strided(shape, stride, off)
+                    self._shared_key, self._shared_flat = ref.binary(), flat
+                    if os.environ.get("RMM_SHARED_WEIGHTS_DEBUG"):
+                        import sys
+
+                        print(f"[shared-weights] worker pid {os.getpid()}: params alias {flat.data_ptr():#x} .. "
+                              f"{flat.data_ptr() + flat.numel() * flat.element_size():#x}", file=sys.stderr,
+                              flush=True)
+                    self._on_params_rebound()
+                    return
+                for name, off, shape, stride in weights["__rmm_layout__"]:  # another GPU: copy
+                    if name in params:
+                        params[name].copy_(flat.to(self.device).as_strided(shape, stride, off))
+            return
         if isinstance(weights, dict) and "__rmm_flat_bf16__" in weights:  # learner's HBM weights object
             flat = weights["__rmm_flat_bf16__"]
             if flat.device != self.device:
@@ -91,6 +117,10 @@ class GPURolloutWorker:
 
     def get_weights(self, policies=None):
         return {k: v.detach().float().cpu().numpy() for k, v in self.model.state_dict().items()}
+
+    def _on_params_rebound(self):
+        """Parameters now live elsewhere: captured graphs hold the old pointers."""
+        self.sampler._graph = None
 
     def get_metrics(self) -> List[tuple]:
         out, self._completed = self._completed, []
@@ -403,6 +433,7 @@ class HybridRolloutWorker(GPURolloutWorker):
         G, T, st = self.groups, self.T, self.stream
         with torch.no_grad():
             S = self.group_streams
+            dbg = os.environ.get("RMM_CAPTURE_DEBUG")
             if not self._captured:
                 self._captured = True
                 for g, gs in zip(G, S):
@@ -411,6 +442,12 @@ class HybridRolloutWorker(GPURolloutWorker):
                     except Exception as e:  # pragma: no cover
                         print(f"[HybridRolloutWorker] HIP graph capture failed ({e!r}); running eagerly")
                         g.graph = False
+                if dbg:
+                    import sys
+
+                    torch.cuda.synchronize(self.device)
+                    print(f"[hybrid-worker pid {os.getpid()}] policy-step graphs captured ok", file=sys.stderr,
+                          flush=True)
             # the previous fragment's frames (views of the group buffers) were copied into the HBM
             # object store on the default stream at task return: finish that before overwriting
             cur = torch.cuda.current_stream(self.device)
@@ -421,8 +458,20 @@ class HybridRolloutWorker(GPURolloutWorker):
                     g.ctr_t[1].zero_()
                 g.resync(gs)
             shared = all(gs is st for gs in S)
-            native = self._native_loop(G, S)
-            if native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
+            server = self._server_args(G, S)
+            native = None if server is not None else self._native_loop(G, S)
+            if server is not None:  # K21: the whole fragment in ONE persistent kernel launch
+                from ray_memory_management_amd._native import require_hip
+
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
+                try:
+                    self._completed.extend(require_hip().hybrid_rollout_server(**server, T=T, threads=max(1, th)))
+                except RuntimeError:
+                    # a server timeout (e.g. another process held the CUs) aborts this fragment; the
+                    # worker falls back to the per-step graph loop for good
+                    self._server_off = True
+                    raise
+            elif native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
                 from ray_memory_management_amd._native import require_hip
 
                 # rollout_env_threads (default 1) splits each env step over that many CPU threads; measured
@@ -434,6 +483,11 @@ class HybridRolloutWorker(GPURolloutWorker):
                 self._completed.extend(require_hip().hybrid_rollout(native, T, threads=max(1, th), spin=spin))
             else:
                 self._python_loop(G, S, T, st, shared)
+            if dbg:
+                import sys
+
+                torch.cuda.synchronize(self.device)
+                print(f"[hybrid-worker pid {os.getpid()}] fragment loop ok", file=sys.stderr, flush=True)
             with torch.cuda.stream(st):
                 for gs in dict.fromkeys(S):
                     if gs is not st:
@@ -463,6 +517,57 @@ class HybridRolloutWorker(GPURolloutWorker):
                                        "without its frames); fragment discarded")
         self._sample_time += time.perf_counter() - t0
         return frag
+
+    def _server_args(self, G, S):
+        """Arguments of the K21 persistent rollout server (csrc/hip/rollout_server.hip) for this
+        worker, or None when it does not apply: opt-in (RMM_ROLLOUT_SERVER=1 or config
+        rollout_server=True), one env group of <= 64 native synthetic envs with device frame stacks
+        (not band mode), the fused bf16 Nature-CNN policy, device-mapped pinned frame / action
+        buffers. One launch per fragment; bit-identical to the per-step graph loop."""
+        if getattr(self, "_server_off", False) or os.environ.get("RMM_NO_NATIVE_ROLLOUT"):
+            return None
+        on = os.environ.get("RMM_ROLLOUT_SERVER")
+        if not (on == "1" if on is not None else bool(self.config.get("rollout_server", False))):
+            return None
+        cached = getattr(self, "_server_cache", None)
+        if cached is not None:
+            return cached
+        import torch
+
+        from ray_memory_management_amd._native import require_hip
+
+        if len(G) != 1:
+            return None
+        g, gs = G[0], S[0]
+        m = self.model
+        ok = (g.device_stack and not g.band and g.fused and g.h_new_dev and g.h_act_dev and g.n <= 64
+              and getattr(g.env, "_native", None) is not None and hasattr(g.env, "native_state")
+              and getattr(m, "nature", False) and m.fused_trunk_ok(g.s_obs) and m.dense_tail is not None
+              and m.dense_tail.out_features == 256 and m.dense_tail.in_features == 3872
+              and m.dense_tail.weight.is_contiguous() and m.heads.weight.is_contiguous()
+              and 3 <= m.heads.out_features <= 16)
+        if not ok:
+            return None
+        hip = require_hip()
+        B, A1 = g.n, m.heads.out_features
+        S_ = hip.dense_fwd_part_slices(B, 3872, 256)
+        self._server_h2 = torch.empty((B, 3872), dtype=torch.bfloat16, device=self.device)
+        self._server_hpart = torch.empty(S_ * B * 256, dtype=torch.float32, device=self.device)
+        c1, c2, dl, hd = m.convs[0], m.convs[1], m.dense_tail, m.heads
+        group = [0, int(gs.cuda_stream), *map(int, g.env.native_state()), g.h_act.data_ptr(), g.h_new.data_ptr(),
+                 g.h_rew.data_ptr(), g.h_done.data_ptr(), g.ep_rew.ctypes.data, g.ep_len.ctypes.data]
+        weights = [c1.weight.data_ptr(), c1.bias.data_ptr(), c2.weight.data_ptr(), c2.bias.data_ptr(),
+                   dl.weight.data_ptr(), dl.bias.data_ptr(), hd.weight.data_ptr(), hd.bias.data_ptr()]
+        bufs = [g.s_obs.data_ptr(), int(g.h_new_dev), g.buf_obs.data_ptr(), self._server_h2.data_ptr(),
+                self._server_hpart.data_ptr(), g.buf_act.data_ptr(), g.buf_logp.data_ptr(), g.buf_vf.data_ptr(),
+                g.buf_logits.data_ptr(), int(g.h_act_dev), g.ctr_t.data_ptr()]
+        # grid: 128 workgroups by default (phase B's 512 K13s units in two passes; fewer workgroups
+        # than CUs keeps barrier arrivals cheap and leaves CUs to other processes); RMM_ROLLOUT_SERVER_WGS
+        wgs = int(os.environ.get("RMM_ROLLOUT_SERVER_WGS", "128"))
+        self._server_cache = dict(group=group, weights=weights, w1s=list(c1.weight.stride()),
+                                  w2s=list(c2.weight.stride()), bufs=bufs, B=B, S=S_, A1=A1, seed=int(g.seed),
+                                  workgroups=max(wgs, B))
+        return self._server_cache
 
     def _native_loop(self, G, S):
         """Per-group descriptors for the native rollout loop (csrc/hip/rollout_loop.cc), or None when
@@ -538,6 +643,13 @@ class HybridRolloutWorker(GPURolloutWorker):
         super().set_weights(weights, global_vars)
         torch.cuda.synchronize(self.device)
         self._set_weights_time = getattr(self, "_set_weights_time", 0.0) + time.perf_counter() - t0
+
+    def _on_params_rebound(self):
+        """Parameters now alias the learner's HBM weights: recapture the policy-step graphs (and the
+        native loop's graph handles) at the next sample."""
+        self._captured = False
+        self._native_desc = None
+        self._server_cache = None
 
     def timing(self):
         """Accumulated seconds in sample() and set_weights() (phase breakdown probes)."""

@@ -134,6 +134,39 @@ class LearnerActor:
         flat = L.w_bf16 if L.w_bf16 is not None else L.master
         return {"__rmm_flat_bf16__": flat.detach().clone(), "__rmm_layout__": layout}
 
+    def shared_weights_device(self):
+        """Zero-copy weight sharing with co-located rollout workers (opt-in, RMM_SHARED_WEIGHTS=1):
+        the bf16 compute weights move ONCE into an HBM object of this process's GPU object store
+        and the learner keeps updating them in place there; a rollout worker on the same GPU maps
+        the object (hipIPC) and points its parameters at it, so no weights move per iteration. Safe
+        because the training loop orders every update (ends with a host sync) before the next
+        sample, and every sample (ends with a stream sync) before the next update. The owner's view
+        pins the object (never spilled)."""
+        L = self.learner
+        if self.device == "cpu" or not getattr(L, "fast", False) or L.w_bf16 is None:
+            return self.get_weights_device()
+        if getattr(self, "_shared", None) is None:
+            import os
+            import sys
+
+            import ray_memory_management_amd as rt
+
+            ref = rt.put(L.w_bf16.detach().clone())
+            view = rt.get(ref)  # owner-side zero-copy view of the HBM object (pins it)
+            old = L.w_bf16.data_ptr()
+            L.rebind_bf16(view)
+            if os.environ.get("RMM_SHARED_WEIGHTS_DEBUG"):
+                print(f"[shared-weights] learner pid {os.getpid()}: w_bf16 {old:#x} -> store view "
+                      f"{view.data_ptr():#x} .. {view.data_ptr() + view.numel() * 2:#x}", file=sys.stderr, flush=True)
+            names = {id(p): n for n, p in L.model.named_parameters()}
+            layout, off = [], 0
+            for p in L.params:
+                layout.append((names[id(p)], off, tuple(p.shape), tuple(p.stride())))
+                off += p.numel()
+            self._shared = (ref, view, layout)
+        ref, _, layout = self._shared
+        return {"__rmm_shared_bf16__": [ref], "__rmm_layout__": layout}
+
     def set_weights(self, w):
         self.learner.set_weights(w)
 
@@ -210,6 +243,10 @@ class LearnerGroup:
 
     def get_weights(self):
         return ray.get(self.weights_ref())
+
+    def shared_weights_refs(self) -> List:
+        """One shared-weights descriptor per learner (LearnerActor.shared_weights_device)."""
+        return [l.shared_weights_device.remote() for l in self.learners]
 
     def device_weights_refs(self) -> List:
         """One device-weights object per learner (identical replicas): rollout worker i reads

@@ -607,7 +607,17 @@ class PPOLearner:
         idx = torch.rand(iters, n, device=self.device).argsort(dim=1)[:, :nmb * mbs].reshape(-1).contiguous()
         return {"obs": obs.contiguous(), "cols": cols, "idx": idx, "A": A, "mbs": mbs, "period": iters * nmb}
 
+    def _dbg(self, what: str):
+        """RMM_CAPTURE_DEBUG=1: synchronise and log each capture / replay phase (fault hunting:
+        the last line in the process log names the phase whose kernels faulted)."""
+        if os.environ.get("RMM_CAPTURE_DEBUG"):
+            import sys
+
+            torch.cuda.synchronize(self.device)
+            print(f"[ppo-learner pid {os.getpid()}] {what} ok (w_bf16 {self._wptr():#x})", file=sys.stderr, flush=True)
+
     def _capture(self, full):
+        self._dbg("capture: start")
         saved = (self.master.clone(), self.m1.clone(), self.m2.clone(),
                  self.w_bf16.clone() if self.w_bf16 is not None else None, self.ctr.clone(),
                  self.acc.clone())
@@ -618,6 +628,7 @@ class PPOLearner:
             for _ in range(3):  # warm up (MIOpen find, allocator, RCCL communicator) before capture
                 self._step_eager(full)
         torch.cuda.current_stream(self.device).wait_stream(s)
+        self._dbg("capture: eager warm-up steps")
         self._graph = self._graphs_split = None
         self._graph_has_comm = False
         self._chain = 1
@@ -715,9 +726,11 @@ class PPOLearner:
             with torch.cuda.graph(g):
                 self._fast_step(full, False)
             self._graph = g
+        self._dbg("capture: graphs captured")
         for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc), saved):
             if dst is not None:
                 dst.copy_(src)  # undo warm-up updates
+        self._dbg("capture: state restored")
 
     def _sgd_chain(self, total: int) -> int:
         """SGD steps captured per graph (world of one): the largest divisor of the update's step
@@ -837,6 +850,7 @@ class PPOLearner:
             else:
                 self._step_eager(full)
             steps += chain
+        self._dbg(f"update: {steps} SGD steps")
         if self.world > 1:  # KL adaptation and stats from the global batch, identical on every rank
             self.comm.allreduce(self.acc)
             self.acc.mul_(1.0 / self.world)

@@ -100,7 +100,8 @@ def test_out_of_core_gpu_shuffle_spills_hbm_blocks(ray_start):
     ray.shutdown()
     ray.init(num_cpus=4, num_gpus=1, object_store_memory=6 << 30,
              _system_config={"gpu_object_store_memory": 512 << 20, "prestart_workers": 0})
-    r = gs.run_out_of_core_gpu_shuffle(num_workers=1, total_bytes=2 << 30, rounds=8, partitions_per_worker=4,
+    # a reduce holds its whole partition in HBM: 8 partitions of 256 MiB fit the 512 MiB quota
+    r = gs.run_out_of_core_gpu_shuffle(num_workers=1, total_bytes=2 << 30, rounds=8, partitions_per_worker=8,
                                        row_bytes=248, backend="nccl")
     print(r)
     assert r["ok"] and r["payload_ok"], r

@@ -364,6 +364,32 @@ def test_native_rollout_loop_matches_python_loop(cuda, double_buffer, monkeypatc
     assert len(a._completed) > 0 and a._completed == b._completed
 
 
+@pytest.mark.parametrize("n_envs,T", [(6, 12), (50, 20)])
+def test_rollout_server_matches_graph_loop(cuda, monkeypatch, n_envs, T):
+    """K21 persistent rollout server (one launch per fragment, host ↔ GPU through mapped words,
+    grid barriers between the trunk / dense / heads phases) yields the same fragments, bit for bit,
+    and the same finished episodes as the per-step graph loop; its workgroups drain cleanly."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": n_envs,
+           "rollout_fragment_length": T, "seed": 3}
+    monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
+    monkeypatch.setenv("RMM_ROLLOUT_SERVER", "1")
+    a = HybridRolloutWorker(config=cfg)
+    fa = [a.sample() for _ in range(3)]
+    assert getattr(a, "_server_cache", None) is not None and not getattr(a, "_server_off", False)
+    monkeypatch.setenv("RMM_ROLLOUT_SERVER", "0")
+    b = HybridRolloutWorker(config=cfg)
+    fb = [b.sample() for _ in range(3)]
+    assert getattr(b, "_server_cache", None) is None and b._native_desc is not None
+    for x, y in zip(fa, fb):
+        for k in ("obs", "_raw", "_boot"):
+            assert torch.equal(x[k], y[k]), k
+    assert len(a._completed) > 0 and a._completed == b._completed
+
+
 def test_k10_band_push_matches_stack_push(cuda, monkeypatch):
     """K10 rollout band mode (4 workgroups per frame, frame stack = rollout row t-1) yields the same
     fragments, bit for bit, as the one-workgroup-per-frame push over a separate device frame stack."""
