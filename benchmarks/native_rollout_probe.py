@@ -26,7 +26,17 @@ def main(n: int = 50, T: int = 100, groups: int = 1, frags: int = 20):
     dt = (time.perf_counter() - t0) / frags
     from ray_memory_management_amd._native import require_hip
 
-    ph = [round(x / T, 2) for x in require_hip().hybrid_rollout_phases()] if getattr(w, "_native_desc", None) else None
+    srv = getattr(w, "_server_cache", None) is not None
+    ph = ([round(x / T, 2) for x in require_hip().hybrid_rollout_phases()]
+          if (getattr(w, "_native_desc", None) or srv) else None)
+    prof = getattr(w, "_server_prof", None)
+    if prof is not None:  # K21 stamps (100 MHz): go seen → trunk done → barrier 1 → barrier 2 → actions signalled
+        p = prof.cpu().double()
+        d = (p[1:, 1:] - p[1:, :-1]).mean(0) / 100.0  # µs, steps 1.. (step 0 includes the weight staging)
+        gap = (p[1:, 0] - p[:-1, 4]).mean() / 100.0  # actions signalled → next step's go seen (host round trip)
+        print(json.dumps({"server_us": {"trunk": round(float(d[0]), 2), "barrier1": round(float(d[1]), 2),
+                                        "dense": round(float(d[2]), 2), "heads_signal": round(float(d[3]), 2),
+                                        "host_round_trip": round(float(gap), 2)}}), flush=True)
     print(json.dumps({"n_envs": n, "T": T, "groups": len(w.groups), "native_loop": getattr(w, "_native_desc", None) is not None,
                       "ms_per_fragment": round(dt * 1e3, 3), "us_per_step": round(dt / T * 1e6, 2),
                       "us_per_step_wait_env_launch": ph}), flush=True)

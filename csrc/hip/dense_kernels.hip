@@ -359,42 +359,50 @@ constexpr int K12_RB = (K12_WS + K12_XS + K12_DXS) > (K12_YS + K12_DZS) ? (K12_W
                                                                        : (K12_YS + K12_DZS);
 static_assert((K12_LDS_DM + K12_RB) * 2 <= 160 * 1024, "K12 LDS");
 
-// Row split of K12 (round 4): each column block (and the head role) runs as RS workgroups over
-// disjoint chunk ranges of the batch — 244 instead of 122 workgroups at M = 500, half the serial
-// chunk chain each. dx rows are independent; the dW / head partials (fp32, 16-20 per lane) are
-// combined by the LAST workgroup of the group to finish (device-scope arrival counter, reset by
-// that workgroup for the next launch), summed in group order (h = 0, 1, ...) whoever arrives last
-// → deterministic. No workgroup waits for another (no co-residency assumption).
+// Row split of K12 (RMM_K12_SPLIT=2): each column block (and the head role) runs as RS workgroups
+// over disjoint chunk ranges of the batch — 244 instead of 122 workgroups at M = 500, half the
+// serial chunk chain each. dx rows are independent; the dW / head partials (fp32, 16-20 per lane,
+// lane-major so the stores coalesce) go to a workspace that k_dense_split_finalize sums in member
+// order (deterministic) into the gradients. A last-arriver combine inside K12 measured 2x SLOWER:
+// each workgroup's agent-scope release fence wrote back its XCD's whole L2 (dx included).
 constexpr int K12_PSLOTS = 20;  // partial floats per lane (head role: 8 dWh + 8 db + 4 dbh)
 struct RowSplit {
-  float* part = nullptr;      // [groups][rs][K12_PSLOTS][NT]
-  unsigned int* cnt = nullptr;  // [groups] arrival counters (zero between launches)
+  float* part = nullptr;  // [groups][rs][K12_PSLOTS][NT]
   int rs = 1, h = 0, group = 0;
 };
-// Publish this workgroup's `n` partial slots and arrive; true in the workgroup that must finish
-// the group (it then reads every member's slots through k12_sum).
-__device__ __forceinline__ bool k12_arrive(const RowSplit& rsp, const float* v, int n) {
-  __shared__ unsigned int last;
+__device__ __forceinline__ void k12_publish(const RowSplit& rsp, const float* v, int n) {
   float* my = rsp.part + ((int64_t(rsp.group) * rsp.rs + rsp.h) * K12_PSLOTS) * NT + threadIdx.x;
   for (int i = 0; i < n; i++) my[i * NT] = v[i];
-  __syncthreads();  // every wave's stores have reached the L2
-  if (threadIdx.x == 0) {
-    __threadfence();  // release: write the partials back for the other XCDs
-    last = atomicAdd(&rsp.cnt[rsp.group], 1u) == unsigned(rsp.rs - 1);
-    if (last) {
-      __threadfence();  // acquire: drop stale lines before reading the other members' partials
-      rsp.cnt[rsp.group] = 0u;
+}
+
+// grid (groups, K12_PSLOTS) x NT: thread = (group, slot, lane-of-K12) → one gradient element
+__global__ __launch_bounds__(NT) void k_dense_split_finalize(const float* __restrict__ part, int rs, int64_t K, int A1,
+                                                             unsigned short* __restrict__ dw,
+                                                             unsigned short* __restrict__ db,
+                                                             unsigned short* __restrict__ dwh,
+                                                             unsigned short* __restrict__ dbh) {
+  const int group = blockIdx.x, slot = blockIdx.y, tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const bool head = int64_t(group) * JB == K;
+  if (!head && slot >= 16) return;
+  unsigned short* dst = nullptr;
+  if (!head) {  // slot = (hi * 2 + jt) * 4 + i  →  dW[16 (wave + 8 hi) + 4 g + i][J0 + 16 jt + r]
+    const int hi = slot >> 3, jt = (slot >> 2) & 1, i = slot & 3;
+    dst = &dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + int64_t(group) * JB + 16 * jt + r];
+  } else {
+    const int i = slot & 3, q = slot >> 2;  // q: 0,1 dWh (hi), 2,3 db (hi), 4 dbh
+    if (q < 2) {
+      if (4 * g + i < A1) dst = &dwh[(4 * g + i) * H + 16 * (wave + 8 * q) + r];
+    } else if (q < 4) {
+      if (g == 0 && i == 0) dst = &db[16 * (wave + 8 * (q - 2)) + r];
+    } else if (wave == 0 && r == 0 && 4 * g + i < A1) {
+      dst = &dbh[4 * g + i];
     }
   }
-  __syncthreads();
-  return last;
-}
-// slot i summed over the group's members in order h = 0 .. rs-1 (own value taken from registers)
-__device__ __forceinline__ float k12_sum(const RowSplit& rsp, int i, float own) {
+  if (dst == nullptr) return;
   float t = 0.f;
-  for (int h = 0; h < rsp.rs; h++)
-    t += h == rsp.h ? own : rsp.part[((int64_t(rsp.group) * rsp.rs + h) * K12_PSLOTS + i) * NT + threadIdx.x];
-  return t;
+  for (int h = 0; h < rs; h++) t += part[((int64_t(group) * rs + h) * K12_PSLOTS + slot) * NT + tid];
+  *dst = f2bf(t);
 }
 
 // column-block role: dx[:, J] and dW[:, J] for J = [J0, J0+32)
@@ -528,13 +536,8 @@ __device__ __forceinline__ void k12_cols(const unsigned short* __restrict__ x, c
       for (int jt = 0; jt < 2; jt++)
 #pragma unroll
         for (int i = 0; i < 4; i++) pv[(hi * 2 + jt) * 4 + i] = adw[hi][jt][i];
-    if (!k12_arrive(rsp, pv, 16)) return;
-#pragma unroll
-    for (int hi = 0; hi < 2; hi++)
-#pragma unroll
-      for (int jt = 0; jt < 2; jt++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) adw[hi][jt][i] = k12_sum(rsp, (hi * 2 + jt) * 4 + i, pv[(hi * 2 + jt) * 4 + i]);
+    k12_publish(rsp, pv, 16);  // k_dense_split_finalize sums the members' partials
+    return;
   }
   // dW[:, J] is final here (every row reduced): store it, or apply Adam to it
   const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
@@ -647,15 +650,8 @@ __device__ __forceinline__ void k12_head(const unsigned short* __restrict__ dz, 
     for (int i = 0; i < 4; i++) {
       pv[i] = awh[0][i], pv[4 + i] = awh[1][i], pv[8 + i] = adb[0][i], pv[12 + i] = adb[1][i], pv[16 + i] = abh[i];
     }
-    if (!k12_arrive(rsp, pv, K12_PSLOTS)) return;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      awh[0][i] = k12_sum(rsp, i, pv[i]);
-      awh[1][i] = k12_sum(rsp, 4 + i, pv[4 + i]);
-      adb[0][i] = k12_sum(rsp, 8 + i, pv[8 + i]);
-      adb[1][i] = k12_sum(rsp, 12 + i, pv[12 + i]);
-      abh[i] = k12_sum(rsp, 16 + i, pv[16 + i]);
-    }
+    k12_publish(rsp, pv, K12_PSLOTS);
+    return;
   }
   const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
 #pragma unroll
@@ -679,12 +675,12 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd2(
     const unsigned short* __restrict__ w, const unsigned short* __restrict__ dpre, int64_t M, int64_t K,
     unsigned short* __restrict__ dx, unsigned short* __restrict__ dw, unsigned short* __restrict__ db,
     unsigned short* __restrict__ dwh, unsigned short* __restrict__ dbh, const FusedAdam fa, float* __restrict__ rs_part,
-    unsigned int* __restrict__ rs_cnt, int rs) {
+    int rs) {
   __shared__ __attribute__((aligned(16))) unsigned short dm[K12_LDS_DM];
   __shared__ __attribute__((aligned(16))) unsigned short rb[K12_RB];
   // block = (role group, row split h); the RS members of a group are consecutive blocks
   RowSplit rsp;
-  rsp.part = rs_part, rsp.cnt = rs_cnt, rsp.rs = rs, rsp.h = int(blockIdx.x) % rs, rsp.group = int(blockIdx.x) / rs;
+  rsp.part = rs_part, rsp.rs = rs, rsp.h = int(blockIdx.x) % rs, rsp.group = int(blockIdx.x) / rs;
   const int NC = int((M + MC2 - 1) / MC2);
   const int c0 = NC * rsp.h / rs, c1 = NC * (rsp.h + 1) / rs;
   if (int64_t(rsp.group) * JB == K)
@@ -847,18 +843,25 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
   __shared__ float red[6][4];
-  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
-  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) + wave;
   const bool valid = row < M;  // wave-uniform
   const int64_t rr = valid ? row : M - 1;
-  const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
-  const float gs = gout[0] / float(M);
+  // the cols row (ctr → index window → row: three dependent loads) and the hidden partials go out
+  // first, so their round trips overlap the head-weight staging below instead of following it
+  const int64_t crr = cidx ? (ctr ? cidx[(ctr[0] % period) * M + rr] : cidx[rr]) : rr;
+  const float* crow = cols + crr * (A + 4);
+  float cv[A + 4];
+#pragma unroll
+  for (int j = 0; j < A + 4; j++) cv[j] = crow[j];
   float hv[4];
   uint2 hbits;
   load_hidden4(hid, hpart, S, hb, M, rr, lane, hv, hbits);
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
+  __syncthreads();
+  const float clip = coef[0], vf_clip = coef[1], vf_coeff = coef[2], ent_coeff = coef[3], kl_coeff = coef[4];
+  const float gs = gout[0] / float(M);
   if (hid_out != nullptr && valid) *reinterpret_cast<uint2*>(&hid_out[row * H + 4 * lane]) = hbits;  // for K12
   float hd[A1];
 #pragma unroll
@@ -872,13 +875,11 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
     for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
 #pragma unroll
   for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));  // the bf16 head output
-  // cols row: gathered in place through the minibatch index window (as K2) when cidx is given
-  const int64_t crr = cidx ? (ctr ? cidx[(ctr[0] % period) * M + rr] : cidx[rr]) : rr;
-  const float* crow = cols + crr * (A + 4);
+  // cols row (loaded above): gathered through the minibatch index window (as K2) when cidx is given
   float mx = -INFINITY, mxo = -INFINITY, lo[A > 0 ? A : 1];
 #pragma unroll
   for (int j = 0; j < A; j++) {
-    lo[j] = crow[j];
+    lo[j] = cv[j];
     mx = fmaxf(mx, hd[j]);
     mxo = fmaxf(mxo, lo[j]);
   }
@@ -897,15 +898,15 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
     m += p[j] * hd[j];
     kl += po[j] * ((lo[j] - lseo) - (hd[j] - lse));
   }
-  const int act = min(max(int(crow[A + 3]), 0), A - 1);
+  const int act = min(max(int(cv[A + 3]), 0), A - 1);
   float la = hd[0];
 #pragma unroll
   for (int j = 1; j < A; j++)
     if (j == act) la = hd[j];
-  const float r = __expf((la - lse) - crow[A]);
-  const float ad = crow[A + 1];
+  const float r = __expf((la - lse) - cv[A]);
+  const float ad = cv[A + 1];
   const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
-  const float d = hd[A] - crow[A + 2];
+  const float d = hd[A] - cv[A + 2];
   // statistics (lane 0 of each valid row)
   float s[6] = {0, 0, 0, 0, 0, 0};
   if (valid && lane == 0) {
@@ -1031,12 +1032,12 @@ __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __
     if (ctr != t_ptr) *ctr = int64_t(c) + 1;
   }
 }
-// K12 row-split workspace: partials + zeroed arrival counters, one per (device, groups, rs),
+// K12 row-split workspace (partials), one per (device, groups, rs),
 // allocated on first use (outside any graph capture: the learner's eager warm-up steps come first)
 // and kept for the process lifetime.
-void k12_split_ws(int groups, int rs, hipStream_t stream, float** part, unsigned int** cnt) {
+void k12_split_ws(int groups, int rs, hipStream_t stream, float** part) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int>, std::pair<float*, unsigned int*>> cache;
+  static std::map<std::tuple<int, int, int>, float*> cache;
   int dev = 0;
   RMM_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> g(mu);
@@ -1048,15 +1049,10 @@ void k12_split_ws(int groups, int rs, hipStream_t stream, float** part, unsigned
     if (cs != hipStreamCaptureStatusNone)
       throw std::runtime_error("dense_heads_bwd: run one step eagerly before capturing (K12 row-split workspace)");
     float* p = nullptr;
-    unsigned int* c = nullptr;
     RMM_HIP_CHECK(hipMalloc(&p, sizeof(float) * size_t(groups) * rs * K12_PSLOTS * NT));
-    RMM_HIP_CHECK(hipMalloc(&c, sizeof(unsigned int) * size_t(groups)));
-    RMM_HIP_CHECK(hipMemset(c, 0, sizeof(unsigned int) * size_t(groups)));
-    RMM_HIP_CHECK(hipDeviceSynchronize());
-    it = cache.emplace(key, std::make_pair(p, c)).first;
+    it = cache.emplace(key, p).first;
   }
-  *part = it->second.first;
-  *cnt = it->second.second;
+  *part = it->second;
 }
 }  // namespace dense
 
@@ -1238,19 +1234,16 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   if (fa.grad_base && fa.bump) throw std::invalid_argument("dense_heads_bwd: the step counters advance in the trunk reduce");
   const dim3 pgrid(uint32_t((M + dense::MC - 1) / dense::MC));
   auto* dp = V(dpre_scratch);
-  // K12 row split (RMM_K12_SPLIT=2 enables): measured SLOWER on MI355X (fused loop 12.38 vs 10.89
-  // ms/iter, K12 29.1 vs 13.2 µs): each of the 244 workgroups' agent-scope release fence writes
-  // back its XCD's whole L2 (dx included) before the arrival atomic. Kept opt-in for A/B.
+  // K12 row split + finalize kernel (RMM_K12_SPLIT=2; plain gradients only, not the fused-Adam epilogues)
   static const int split_env = [] {
     const char* e = std::getenv("RMM_K12_SPLIT");
     return e ? std::atoi(e) : 1;
   }();
   const int nc = int((M + dense::MC2 - 1) / dense::MC2);
-  const int rs = v2 ? std::max(1, std::min(split_env, nc)) : 1;
+  const int rs = (v2 && !fa.grad_base) ? std::max(1, std::min(split_env, nc)) : 1;
   const int groups = int(K / dense::JB + 1);
   float* rs_part = nullptr;
-  unsigned int* rs_cnt = nullptr;
-  if (rs > 1) dense::k12_split_ws(groups, rs, stream, &rs_part, &rs_cnt);
+  if (rs > 1) dense::k12_split_ws(groups, rs, stream, &rs_part);
   const dim3 grid3(uint32_t(groups * rs));
 #define RMM_K12(N)                                                                                               \
   case N:                                                                                                        \
@@ -1258,7 +1251,7 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
       hipLaunchKernelGGL(dense::k_dense_dpre<N>, pgrid, block, 0, stream, U(dz), U(wh), U(y), M, dp);            \
     if (v2)                                                                                                      \
       hipLaunchKernelGGL(dense::k_dense_heads_bwd2<N>, grid3, block, 0, stream, U(dz), U(y), U(x), U(w), dp, M, \
-                         K, V(dx), V(dw), V(db), V(dwh), V(dbh), fa, rs_part, rs_cnt, rs);                       \
+                         K, V(dx), V(dw), V(db), V(dwh), V(dbh), fa, rs_part, rs);                                \
     else                                                                                                         \
       hipLaunchKernelGGL(dense::k_dense_heads_bwd<N>, grid, block, 0, stream, U(dz), U(wh), U(y), U(x), U(w),   \
                          dp, M, K, V(dx), V(dw), V(db), V(dwh), V(dbh));                                         \
@@ -1269,6 +1262,11 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   }
 #undef RMM_K12
   RMM_HIP_CHECK(hipGetLastError());
+  if (rs > 1) {
+    hipLaunchKernelGGL(dense::k_dense_split_finalize, dim3(uint32_t(groups), uint32_t(dense::K12_PSLOTS)), block, 0,
+                       stream, rs_part, rs, K, A1, V(dw), V(db), V(dwh), V(dbh));
+    RMM_HIP_CHECK(hipGetLastError());
+  }
 }
 
 }  // namespace hip

@@ -326,8 +326,9 @@ PYBIND11_MODULE(_hip, m) {
                                     const std::vector<uint64_t>& bufs, int64_t B, int64_t T, int slices, int A1,
                                     uint32_t seed, int threads, int workgroups, double go_timeout,
                                     double barrier_timeout, double wait_timeout) {
-    if (v.size() < 15 || wts.size() != 8 || bufs.size() != 11 || w1s.size() != 4 || w2s.size() != 4)
-      throw std::invalid_argument("hybrid_rollout_server: 15 group fields, 8 weights, 11 buffers, 4+4 strides");
+    if (v.size() < 15 || wts.size() != 8 || (bufs.size() != 11 && bufs.size() != 12) || w1s.size() != 4 ||
+        w2s.size() != 4)
+      throw std::invalid_argument("hybrid_rollout_server: 15 group fields, 8 weights, 11 (+prof) buffers, 4+4 strides");
     RolloutGroup g;
     g.stream = S(v[1]);
     g.env.pools = P<const uint8_t>(v[2]);
@@ -365,6 +366,7 @@ PYBIND11_MODULE(_hip, m) {
     a.lout = P<float>(bufs[8]);
     a.act_now = P<int64_t>(bufs[9]);
     a.ctr_t = P<int64_t>(bufs[10]);
+    a.prof = bufs.size() > 11 && bufs[11] ? P<uint64_t>(bufs[11]) : nullptr;
     a.B = B;
     a.S = slices;
     a.A1 = A1;

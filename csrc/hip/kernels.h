@@ -222,11 +222,12 @@ struct RolloutServerArgs {
   int64_t* ctr_t = nullptr;
   const int64_t* go = nullptr;   // device view of the host word
   int64_t* done_seq = nullptr;   // device view of the host word
-  unsigned int* bar = nullptr;   // 2 device words
+  unsigned int* bar = nullptr;   // 10 device words (global / phase-C / 8 per-XCD counters)
   int64_t* err_dev = nullptr;
   int64_t* err_host = nullptr;   // device view of the host word
   double go_timeout_s = 20.0, barrier_timeout_s = 5.0;
   int workgroups = 0;            // 0: one per CU
+  uint64_t* prof = nullptr;      // optional device [T][5] phase timestamps (s_memrealtime)
 };
 int rollout_server_launch(const RolloutServerArgs& a, hipStream_t stream);
 

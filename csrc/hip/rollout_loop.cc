@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <chrono>
@@ -187,7 +188,7 @@ namespace {
 struct ServerSync {
   int64_t* host = nullptr;       // [0] go, [8] done_seq, [16] err  (separate 64-B lines)
   int64_t* host_dev = nullptr;   // device view of `host`
-  unsigned int* bar = nullptr;   // 2 device words
+  unsigned int* bar = nullptr;   // 10 device words
   int64_t* err_dev = nullptr;
 };
 ServerSync& server_sync() {
@@ -197,9 +198,9 @@ ServerSync& server_sync() {
     RMM_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.host), 256, hipHostMallocMapped));
     RMM_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.host_dev), s.host, 0));
     void* d = nullptr;
-    RMM_HIP_CHECK(hipMalloc(&d, 64));
-    s.bar = static_cast<unsigned int*>(d);
-    s.err_dev = reinterpret_cast<int64_t*>(static_cast<char*>(d) + 32);
+    RMM_HIP_CHECK(hipMalloc(&d, 128));
+    s.bar = static_cast<unsigned int*>(d);  // 10 counters (40 B)
+    s.err_dev = reinterpret_cast<int64_t*>(static_cast<char*>(d) + 64);
   });
   return s;
 }

@@ -74,11 +74,12 @@ struct Args {
   int64_t* ctr_t;            // device {rng counter, row}: read at start, advanced by T at the end
   const int64_t* go;         // mapped host: step t may run once *go >= t + 1; *go < 0 aborts
   int64_t* done_seq;         // mapped host: t + 1 once step t's actions are stored
-  unsigned int* bar;         // device: grid-barrier arrivals (zeroed before the launch)
+  unsigned int* bar;         // device: [0] global barrier arrivals, [2..9] per-XCD arrivals (zeroed at launch)
   unsigned int* cdone;       // device: phase-C completion counter (zeroed before the launch)
   int64_t* err_dev;          // device error word (first error wins)
   int64_t* err_host;         // mapped host error word
   uint64_t go_ticks, bar_ticks;  // wait bounds in s_memrealtime ticks
+  uint64_t* prof;            // optional [T][5] s_memrealtime stamps of workgroup 0 (phase timing)
 };
 
 // error codes (err = code | step << 8)
@@ -127,14 +128,32 @@ __device__ __forceinline__ bool wait_go(const Args& a, int64_t t) {
   return ok != 0;
 }
 
-// grid barrier number k (1-based) of this launch: every workgroup arrives, waits for G * k arrivals
-__device__ __forceinline__ bool grid_barrier(const Args& a, uint32_t target, int64_t t) {
+// XCC (XCD) this workgroup runs on: hardware register XCC_ID (gfx940+: HW_REG id 20, bits [3:0])
+__device__ __forceinline__ int xcc_id() {
+  return int(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20)) & 15;
+}
+
+// Grid barrier number k (1-based): hierarchical over the 8 XCDs. A workgroup's global stores
+// reach its XCD's L2 (s_barrier drains vmcnt); the L2s of different XCDs are not coherent, so the
+// stores must be written back before workgroups elsewhere read them — but ONE write-back per XCD
+// suffices: workgroups arrive on a per-XCD counter (blockIdx % 8 = the dispatcher's round-robin
+// XCD; a workgroup whose hardware XCC_ID differs writes back its own L2 first), the last arriver
+// of each XCD group writes that L2 back and arrives on the global counter. Everyone waits for 8 k
+// global arrivals, then invalidates (acquire) before reading other workgroups' results. A
+// per-workgroup write-back (64-128 of them serialised per XCD) measured ~5-8 µs per barrier.
+__device__ __forceinline__ bool grid_barrier(const Args& a, uint32_t k, int64_t t) {
   __shared__ int ok;
   __syncthreads();  // every wave's global stores have reached the L2
   if (threadIdx.x == 0) {
     ok = 1;
-    __threadfence();  // release: write back this workgroup's results for the other XCDs
-    atomicAdd(a.bar, 1u);
+    const int G = int(gridDim.x), grp = int(blockIdx.x) & 7;
+    const uint32_t members = uint32_t((G - grp + 7) / 8);  // workgroups with blockIdx % 8 == grp
+    if (xcc_id() != grp) __threadfence();                  // not where the grouping assumed: own write-back
+    if (atomicAdd(&a.bar[2 + grp], 1u) == members * k - 1) {
+      __threadfence();  // release: write back this XCD's L2 (every member's stores are in it)
+      atomicAdd(a.bar, 1u);
+    }
+    const uint32_t target = uint32_t(G < 8 ? G : 8) * k;
     const uint64_t t0 = now_ticks();
     while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (failed(a)) {
@@ -191,15 +210,19 @@ __global__ __launch_bounds__(NT) void k_rollout_server(const Args a) {
   uint32_t nbar = 0;
   for (int64_t t = 0; t < T; t++) {
     // ---- A: K10 trunk of env `wg` (push mode: stack shift + new frame + row t store)
+    uint64_t* pr = (a.prof && wg == 0 && tid == 0) ? a.prof + t * 5 : nullptr;
     if (trunk_wg) {
       if (!wait_go(a, t)) return;
+      if (pr) pr[0] = now_ticks();
       FrameRegs<NT> fr;
       frame_issue_push<NT>(a.stack + wg * FB, a.nf + wg * (H0 * H0), fr);
       zero_half_frame_border(fh);  // the previous step's h2 staging overwrote part of it
       frame_push_store<NT>(fr, a.stack + wg * FB, a.rows + (t * B + wg) * FB);
       trunk_convs<NT>(fr, fh, h1p, w1s, w2s, tb, nullptr, a.h2 + wg * NP2 * C2, 0);
     }
-    if (!grid_barrier(a, uint32_t(G) * ++nbar, t)) return;
+    if (pr) pr[1] = now_ticks();
+    if (!grid_barrier(a, ++nbar, t)) return;
+    if (pr) pr[2] = now_ticks();
     // ---- B: K13s split-K dense partials over all waves (two 4-wave units per workgroup pass)
     for (int64_t u0 = 2 * int64_t(wg); u0 < units; u0 += 2 * int64_t(G)) {
       const int64_t u = u0 + (wave >> 2);
@@ -208,7 +231,8 @@ __global__ __launch_bounds__(NT) void k_rollout_server(const Args a) {
       dense::dense_part_unit<1, 1, 1, 1>(a.h2, a.Wd, B, KDENSE, dense::H, a.S, a.hpart, sl, tm, tn, wave & 3, valid,
                                          red[wave >> 2]);
     }
-    if (!grid_barrier(a, uint32_t(G) * ++nbar, t)) return;
+    if (!grid_barrier(a, ++nbar, t)) return;
+    if (pr) pr[3] = now_ticks();
     // ---- C: K16 heads + sampling, one wave per env row; the last workgroup to finish signals the host
     if (head_wg) {
       const int64_t b = int64_t(wg) * 8 + wave;
@@ -217,11 +241,15 @@ __global__ __launch_bounds__(NT) void k_rollout_server(const Args a) {
                                     a.act_now, B, b, lane, a.hpart, a.S, a.bd);
       __syncthreads();
       if (tid == 0) {
-        __threadfence_system();  // the rows' act_now stores (host memory) land before done_seq
+        // system-scope release per workgroup: an acknowledged host-memory store is not yet visible
+        // to the CPU, and stores from different CUs may overtake each other in the fabric (a relaxed
+        // done_seq after the arrival count let the host read stale actions: parity test failed)
+        __threadfence_system();
         if (atomicAdd(a.cdone, 1u) == unsigned(nC - 1)) {
           __hip_atomic_store(a.cdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(a.done_seq, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        if (pr) pr[4] = now_ticks();
       }
     }
   }
@@ -274,12 +302,13 @@ int rollout_server_launch(const RolloutServerArgs& r, hipStream_t stream) {
   a.go = r.go;
   a.done_seq = r.done_seq;
   a.bar = r.bar;
-  a.cdone = r.bar + 1;
+  a.cdone = r.bar + 1;  // bar[0] global, bar[1] phase C, bar[2..9] per XCD
   a.err_dev = r.err_dev;
   a.err_host = r.err_host;
   a.go_ticks = uint64_t(r.go_timeout_s * 1e8);
   a.bar_ticks = uint64_t(r.barrier_timeout_s * 1e8);
-  RMM_HIP_CHECK(hipMemsetAsync(r.bar, 0, 2 * sizeof(unsigned int), stream));
+  a.prof = r.prof;
+  RMM_HIP_CHECK(hipMemsetAsync(r.bar, 0, 10 * sizeof(unsigned int), stream));
   RMM_HIP_CHECK(hipMemsetAsync(r.err_dev, 0, sizeof(int64_t), stream));
 #define RMM_K21(N)                                                                                 \
   case N:                                                                                          \

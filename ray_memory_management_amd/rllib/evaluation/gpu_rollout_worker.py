@@ -561,6 +561,9 @@ class HybridRolloutWorker(GPURolloutWorker):
         bufs = [g.s_obs.data_ptr(), int(g.h_new_dev), g.buf_obs.data_ptr(), self._server_h2.data_ptr(),
                 self._server_hpart.data_ptr(), g.buf_act.data_ptr(), g.buf_logp.data_ptr(), g.buf_vf.data_ptr(),
                 g.buf_logits.data_ptr(), int(g.h_act_dev), g.ctr_t.data_ptr()]
+        if os.environ.get("RMM_ROLLOUT_SERVER_PROF"):  # per-step phase stamps of workgroup 0 (probe)
+            self._server_prof = torch.zeros((self.T, 5), dtype=torch.int64, device=self.device)
+            bufs.append(self._server_prof.data_ptr())
         # grid: 128 workgroups by default (phase B's 512 K13s units in two passes; fewer workgroups
         # than CUs keeps barrier arrivals cheap and leaves CUs to other processes); RMM_ROLLOUT_SERVER_WGS
         wgs = int(os.environ.get("RMM_ROLLOUT_SERVER_WGS", "128"))
