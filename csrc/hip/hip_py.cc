@@ -657,6 +657,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("stream"), py::arg("algo") = 0)
       .def("error", &PeerAllReduce::Error)
       .def("clear_error", &PeerAllReduce::ClearError)
+      .def("set_timeout", &PeerAllReduce::set_timeout)
       .def("close", &PeerAllReduce::Close)
       .def_property_readonly("launches", &PeerAllReduce::launches)
       .def_property_readonly("world", &PeerAllReduce::world)

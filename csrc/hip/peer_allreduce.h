@@ -41,6 +41,7 @@ class PeerAllReduce {
   uint64_t cap_bytes() const { return cap_; }
   bool uncached_signals() const { return sig_uncached_; }
   int alloc_attempts() const { return alloc_attempts_; }
+  void set_timeout(double s) { timeout_ticks_ = uint64_t(s > 0 ? s * 1e8 : 1e8); }
   void Close();
 
  private:

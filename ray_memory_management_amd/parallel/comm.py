@@ -293,6 +293,29 @@ class PeerComm(Comm):
         self.fallback = fallback
         self.stream = torch.cuda.Stream(self.device)
         self.algo = int(os.environ.get("RMM_PEER_ALGO", "0"))
+        # self-test before anyone relies on it: one small all-reduce under a short flag timeout,
+        # checked on every rank; the ranks agree through the store, and any failure (a peer mapping
+        # the kernel cannot reach, a timeout, a wrong sum) makes ALL of them fall back together
+        ok = True
+        try:
+            self._c.set_timeout(5.0)
+            x = torch.full((1024,), float(self.rank + 1), dtype=torch.float32, device=self.device)
+            self.allreduce(x)
+            torch.cuda.synchronize(self.device)
+            want = self.world * (self.world + 1) / 2.0
+            ok = int(self._c.error()) == 0 and bool((x == want).all().item())
+        except Exception:  # noqa: BLE001
+            ok = False
+        finally:
+            try:
+                self._c.set_timeout(float(timeout_s))
+            except Exception:  # noqa: BLE001
+                pass
+        store.set(f"{key}/test{self.rank}", b"1" if ok else b"0")
+        bad = [r for r in range(self.world) if store.get(f"{key}/test{r}") != b"1"]
+        if bad:
+            self._c.close()
+            raise PeerUnavailable(f"peer all-reduce self-test failed on ranks {bad}")
 
     @property
     def launches(self) -> int:
