@@ -54,6 +54,14 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
   // the frame's HBM loads go out first and stay in flight through the weight staging (L2) and the
   // LDS zeroing; one barrier then covers weights, zeros and the frame interior
   if (dbg & 128) return;  // profiling: launch + dispatch floor
+  // weight loads first (L2-resident, shorter round trip): their LDS stores below then wait for them
+  // alone while the frame's loads stay in flight
+  WeightRegs<NTF, C1, C0, 8> wr1;
+  WeightRegs<NTF, C2, C1, 4> wr2;
+  if (!(dbg & 8)) {
+    weight_issue(W1, w1, wr1);
+    weight_issue(W2, w2, wr2);
+  }
   FrameRegs<NTF> fr;
   constexpr int64_t FB = C0 * H0 * H0;
   if (push_stack)
@@ -64,8 +72,8 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd(
   zero_half_frame_border(fh);
   zero_lds(h1p, H1P_ELEMS * 2);
   if (!(dbg & 8)) {
-    stage_weight<NTF, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
-    stage_weight<NTF, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
+    weight_store(wr1, W1, w1, w1s, W1_PITCH);
+    weight_store(wr2, W2, w2, w2s, W2_PITCH);
   }
   if (push_stack) frame_push_store<NTF>(fr, push_stack + b * FB, push_rows ? push_rows + (push_t[0] * B + b) * FB : nullptr);
   // trunk_convs' first barrier covers the border / h1p zeros, the weights and pass 0's frame rows
@@ -117,6 +125,10 @@ __global__ __launch_bounds__(NTFB) void k_trunk_fwd_band(
   const uint32_t* n32 = reinterpret_cast<const uint32_t*>(nf + b * (H0 * H0));
   constexpr int PER = (BAND_FR * 21 + NTFB - 1) / NTFB;
   const int w0 = fr0 * 21, nw = (fr1 - fr0 + 1) * 21;
+  WeightRegs<NTFB, C1, C0, 8> wr1;
+  WeightRegs<NTFB, C2, C1, 4> wr2;
+  weight_issue(W1, w1, wr1);
+  weight_issue(W2, w2, wr2);
   uint32_t v[PER][C0];
 #pragma unroll
   for (int k = 0; k < PER; k++) {  // all loads first (unconditional, clamped): one round trip
@@ -127,8 +139,8 @@ __global__ __launch_bounds__(NTFB) void k_trunk_fwd_band(
   }
   zero_lds(frame, BAND_FR * P0 * 4);
   zero_lds(h1p, BAND_H1R * P1 * C1 * 2);
-  stage_weight<NTFB, C1, C0, 8>(W1, w1, w1s, W1_PITCH);
-  stage_weight<NTFB, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
+  weight_store(wr1, W1, w1, w1s, W1_PITCH);
+  weight_store(wr2, W2, w2, w2s, W2_PITCH);
   __syncthreads();
   const int own0 = 21 * s, own1 = own0 + 21;  // the frame rows this band stores into rollout row t
 #pragma unroll
@@ -229,11 +241,18 @@ static_assert(KSTEPS1 * 32 + ST_W <= 24 * ST_W, "dpre1 copy K padding");
 constexpr int NTB = 512;
 constexpr int BWD_NH1 = NP1 * 2, BWD_PH1 = (BWD_NH1 + NTB - 1) / NTB;  // 882 x 16 B
 constexpr int BWD_NH2 = NP2 * 4, BWD_PH2 = (BWD_NH2 + NTB - 1) / NTB;  // 484 x 16 B
+__device__ __forceinline__ void h1_issue(int64_t bb, const unsigned short* __restrict__ h1, u16x8 (&hv1)[BWD_PH1]) {
+#pragma unroll
+  for (int k = 0; k < BWD_PH1; k++) {
+    const int v = min(int(threadIdx.x) + NTB * k, BWD_NH1 - 1);
+    hv1[k] = *reinterpret_cast<const u16x8*>(&h1[(bb * NP1 + (v >> 1)) * C1 + 8 * (v & 1)]);
+  }
+}
 // P0 global loads of frame bb (clamped and unconditional, see load_frame)
 __device__ __forceinline__ void bwd_issue(int64_t bb, const int64_t* __restrict__ idx, const uint8_t* __restrict__ obs,
                                           const unsigned short* __restrict__ h1, const unsigned short* __restrict__ h2,
                                           const unsigned short* __restrict__ dh2, FrameRegs<NTB>& fr,
-                                          uint4 (&hv1)[BWD_PH1], u16x8 (&hv2)[BWD_PH2], u16x8 (&gv2)[BWD_PH2]) {
+                                          u16x8 (&hv1)[BWD_PH1], u16x8 (&hv2)[BWD_PH2], u16x8 (&gv2)[BWD_PH2]) {
   const int64_t src = idx ? idx[bb] : bb;
   frame_issue<NTB>(obs + src * (C0 * H0 * H0), fr);
 #pragma unroll
@@ -261,11 +280,23 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   const int64_t* idx = window(idx0, ctr, period, B);
   if (dbg & 64) return;
 
+  // prologue: the W2 loads (L2), then the first frame's HBM loads (frame, h1, h2, dh2) go out
+  // before the LDS zeroing, so the weight round trip and the frame's hide behind it
+  constexpr int NH1 = BWD_NH1, PH1 = BWD_PH1, NH2 = BWD_NH2, PH2 = BWD_PH2;
+  WeightRegs<NTB, C2, C1, 4> wr;
+  weight_issue(W2, w2, wr);
+  FrameRegs<NTB> fr;
+  u16x8 hv1[PH1];
+  u16x8 hv2[PH2], gv2[PH2];
+  if (!(dbg & 8) && int64_t(blockIdx.x) < B) {
+    bwd_issue(blockIdx.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);
+    h1_issue(blockIdx.x, h1, hv1);
+  }
   if (!(dbg & 32)) zero_lds(st, ST_C * ST_CP * 2);
-  stage_weight<NTB, C2, C1, 4>(W2, w2, w2s, W2_PITCH);
   zero_lds(h1p, H1P_ELEMS * 2);
   zero_lds(dp2, D2W * D2W * C2 * 2);
   zero_lds(dp2t, C2 * DP2_PITCH * 2);
+  weight_store(wr, W2, w2, w2s, W2_PITCH);
 
   // dh1 = conv2ᵀ(dpre2): waves 2c, 2c+1 own stride-parity class c = (py, px). In a class,
   // input pixel (y, x) = (2a+py, 2c+px) receives taps ky ∈ {py, py+2}, kx ∈ {px, px+2} from
@@ -302,26 +333,16 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   // P0 is software-pipelined across this workgroup's frames: the global loads of frame b + G are
   // issued right after frame b's LDS tiles are written and stay in flight (registers) through
   // frame b's P1 / P2 MFMA phases, so only the first frame pays the HBM latency in the open.
-  constexpr int NH1 = BWD_NH1, PH1 = BWD_PH1, NH2 = BWD_NH2, PH2 = BWD_PH2;
-  FrameRegs<NTB> fr;
-  uint4 hv1[PH1];
-  u16x8 hv2[PH2], gv2[PH2];
-  if (!(dbg & 8) && int64_t(blockIdx.x) < B) bwd_issue(blockIdx.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
     // ---- P0: frame (space-to-depth), h1 → padded tile, h2 / dh2 → dpre2 (both layouts) + db2
     if (!(dbg & 8)) {
-#pragma unroll
-      for (int k = 0; k < PH1; k++) {  // h1 of this frame: loaded here (prefetching it too spills)
-        const int v = min(int(threadIdx.x) + NTB * k, NH1 - 1);
-        hv1[k] = *reinterpret_cast<const uint4*>(&h1[(b * NP1 + (v >> 1)) * C1 + 8 * (v & 1)]);
-      }
       frame_store_s2d<NTB>(fr, st);
 #pragma unroll
       for (int k = 0; k < PH1; k++) {
         const int v = threadIdx.x + NTB * k;
         if (v < NH1) {
           const int p = v >> 1, y = p / H1, x = p - y * H1;
-          *reinterpret_cast<uint4*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1)]) = hv1[k];
+          *reinterpret_cast<u16x8*>(&h1p[((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1)]) = hv1[k];
         }
       }
 #pragma unroll
@@ -343,7 +364,10 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
       }
     }
     __syncthreads();
-    if (!(dbg & 8) && b + gridDim.x < B) bwd_issue(b + gridDim.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);  // next frame: in flight through P1 / P2
+    if (!(dbg & 8) && b + gridDim.x < B) {  // next frame: in flight through P1 / P2
+      bwd_issue(b + gridDim.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);
+      h1_issue(b + gridDim.x, h1, hv1);
+    }
 
     // ---- P1a: dW2[co2][k=(ky,kx,ci)] += Σ_q dpre2[q][co2] · h1p[2oy+ky][2ox+kx][ci]
 #pragma unroll

@@ -234,14 +234,38 @@ __device__ __forceinline__ void load_frame_s2d(const uint8_t* __restrict__ src, 
 // all workgroups hammer the same few L2 lines (measured: skeleton cost grew 7→20-30 µs from 1 to
 // 256 workgroups). Here each element is read once per workgroup, 16 B at a time when the weight
 // is channels-last contiguous ([co][ky][kx][ci] in memory).
+// Split in issue / store: all of a lane's 16-B loads go out at once (a load→store loop waits one L2
+// round trip per trip: the bwd kernel's prologue paid 2, the fwd's 3, ~1 µs each) and the kernels
+// issue them FIRST, so the round trip hides behind the frame issue and the LDS zeroing.
 template <int NT, int CO, int CI, int KH>
-__device__ __forceinline__ void stage_weight(const unsigned short* __restrict__ W, WStrides ws_, unsigned short* dst,
-                                             int pitch) {
-  constexpr int ROW = KH * KH * CI;  // elements per output channel
-  if (ws_.s1 == 1 && ws_.s3 == CI && ws_.s2 == KH * CI && ws_.s0 == ROW) {
-    for (int v = threadIdx.x; v < CO * ROW / 8; v += NT) {
-      const int co = (8 * v) / ROW, e = 8 * v - co * ROW;
-      *reinterpret_cast<uint4*>(&dst[co * pitch + e]) = *reinterpret_cast<const uint4*>(&W[8 * v]);
+struct WeightRegs {
+  static constexpr int ROW = KH * KH * CI, N = CO * ROW / 8, PER = (N + NT - 1) / NT;
+  u16x8 v[PER];
+  bool fast;  // channels-last contiguous: 16-B copies; otherwise weight_store gathers elements
+};
+template <int NT, int CO, int CI, int KH>
+__device__ __forceinline__ void weight_issue(const unsigned short* __restrict__ W, WStrides ws_,
+                                             WeightRegs<NT, CO, CI, KH>& r) {
+  using R = WeightRegs<NT, CO, CI, KH>;
+  r.fast = ws_.s1 == 1 && ws_.s3 == CI && ws_.s2 == KH * CI && ws_.s0 == R::ROW;
+  if (!r.fast) return;
+#pragma unroll
+  for (int k = 0; k < R::PER; k++)
+    r.v[k] = *reinterpret_cast<const u16x8*>(&W[8 * min(int(threadIdx.x) + NT * k, R::N - 1)]);
+}
+template <int NT, int CO, int CI, int KH>
+__device__ __forceinline__ void weight_store(const WeightRegs<NT, CO, CI, KH>& r, const unsigned short* __restrict__ W,
+                                             WStrides ws_, unsigned short* dst, int pitch) {
+  using R = WeightRegs<NT, CO, CI, KH>;
+  constexpr int ROW = R::ROW;
+  if (r.fast) {
+#pragma unroll
+    for (int k = 0; k < R::PER; k++) {
+      const int v = threadIdx.x + NT * k;
+      if (v < R::N) {
+        const int co = (8 * v) / ROW, e = 8 * v - co * ROW;
+        *reinterpret_cast<u16x8*>(&dst[co * pitch + e]) = r.v[k];
+      }
     }
   } else {
     for (int v = threadIdx.x; v < CO * ROW; v += NT) {
@@ -249,6 +273,13 @@ __device__ __forceinline__ void stage_weight(const unsigned short* __restrict__ 
       dst[co * pitch + e] = W[co * ws_.s0 + ci * ws_.s1 + ky * ws_.s2 + kx * ws_.s3];
     }
   }
+}
+template <int NT, int CO, int CI, int KH>
+__device__ __forceinline__ void stage_weight(const unsigned short* __restrict__ W, WStrides ws_, unsigned short* dst,
+                                             int pitch) {
+  WeightRegs<NT, CO, CI, KH> r;
+  weight_issue(W, ws_, r);
+  weight_store(r, W, ws_, dst, pitch);
 }
 constexpr int W1_PITCH = 256 + 8, W2_PITCH = 256 + 8;  // +16 B: 16 lanes x 16-B reads hit distinct banks
 
@@ -361,11 +392,7 @@ __device__ __forceinline__ void trunk_convs(const FrameRegs<NT>& fr, unsigned sh
                                             int dbg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
-  // j → (kx = 2g + (j>>2), ci = j&3); col = co = r: one 16-B LDS read each.
   bf16x8 wf1[8];
-#pragma unroll
-  for (int s = 0; s < 8; s++) wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&w1s[r * W1_PITCH + (s * 8 + 2 * g) * 4]));
   const float bias1 = tb.b1;
 
   // ---- conv1 in two half-image passes of 14 M-tiles (16 positions each) over the waves
@@ -379,6 +406,15 @@ __device__ __forceinline__ void trunk_convs(const FrameRegs<NT>& fr, unsigned sh
     }
     if (!(dbg & 32)) half_frame_store<NT>(fr, fh, base);
     __syncthreads();
+    if (pass == 0) {
+      // conv1 weight fragments, k = (ky, kx, ci): k-step s = ky, lane group g → kx ∈ {2g, 2g+1},
+      // j → (kx = 2g + (j>>2), ci = j&3); col = co = r: one 16-B LDS read each. Read AFTER the
+      // barrier: w1s is staged by every thread of the workgroup (a read before it raced with
+      // slower waves' stores — wrong conv1 weights for a frame, seen with two workgroups per CU)
+#pragma unroll
+      for (int s = 0; s < 8; s++)
+        wf1[s] = as_bf(*reinterpret_cast<const u16x8*>(&w1s[r * W1_PITCH + (s * 8 + 2 * g) * 4]));
+    }
     for (int mt = pass * HF_TILES + wave; mt < (pass + 1) * HF_TILES; mt += NT / 64) {
       const int p = min(mt * 16 + r, NP1 - 1);
       const int oy = p / H1, ox = p - oy * H1;

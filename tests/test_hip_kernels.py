@@ -155,11 +155,14 @@ def _trunk_reference(frames_u8, w1, b1, w2, b2):
     return h2.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten
 
 
+@pytest.mark.parametrize("rows", [23, 300])
 @pytest.mark.parametrize("use_ctr", [False, True])
 @pytest.mark.parametrize("channels_last", [False, True])
-def test_nature_trunk_fwd_bwd_match_fp32(cuda, use_ctr, channels_last):
+def test_nature_trunk_fwd_bwd_match_fp32(cuda, use_ctr, channels_last, rows):
     """K10 fused trunk (MFMA) vs fp32 torch conv2d with the same bf16 weights: forward values and
-    all four weight/bias gradients for a random upstream gradient, with minibatch gathering."""
+    all four weight/bias gradients for a random upstream gradient, with minibatch gathering.
+    rows=300 > 256 backward workgroups: workgroups loop over two frames (the prefetch path).
+    The backward also runs twice and must give bit-identical gradients."""
     from ray_memory_management_amd.rllib.models import nature_trunk
 
     torch.manual_seed(0)
@@ -169,7 +172,7 @@ def test_nature_trunk_fwd_bwd_match_fp32(cuda, use_ctr, channels_last):
     b1 = (torch.randn(16, device=cuda) * 0.1).to(torch.bfloat16)
     w2 = (torch.randn(32, 16, 4, 4, device=cuda) * 0.1).to(torch.bfloat16).contiguous(memory_format=fmt)
     b2 = (torch.randn(32, device=cuda) * 0.1).to(torch.bfloat16)
-    rows, period = 23, 3
+    period = 3
     idx = torch.randint(0, 57, (rows * period,), device=cuda)
     ctr = torch.tensor([4, 0], dtype=torch.int64, device=cuda) if use_ctr else None
     sel = idx[(4 % period) * rows:(4 % period + 1) * rows] if use_ctr else idx[:rows]
@@ -181,7 +184,13 @@ def test_nature_trunk_fwd_bwd_match_fp32(cuda, use_ctr, channels_last):
     err = (out.float() - ref).abs().max() / ref.abs().max()
     assert err < 1e-2, f"forward rel err {err}"
     g = torch.randn_like(ref)
+    out.backward(g.to(torch.bfloat16), retain_graph=True)
+    first = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = None
     out.backward(g.to(torch.bfloat16))
+    for a, p in zip(first, params):
+        assert torch.equal(a, p.grad), "K10 backward is not deterministic"
     ref.backward(g)
     errs = {}
     for name, p, rp in zip(("dW1", "db1", "dW2", "db2"), params, ref_params):
