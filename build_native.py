@@ -72,7 +72,7 @@ def extensions():
              common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"],
              hip_ld, ["csrc/hip/kernels.h", "csrc/hip/gpu_store.h", "csrc/hip/rccl_comm.h", "csrc/hip/peer_allreduce.h", "csrc/hip/common.h", "csrc/store/shm_store.h",
                      "csrc/hip/rollout_loop.h", "csrc/rl/synth_env.h", "csrc/hip/trunk_device.h",
-                     "csrc/hip/dense_device.h"]))
+                     "csrc/hip/dense_device.h", "csrc/hip/adam_device.h"]))
     return exts
 
 

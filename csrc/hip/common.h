@@ -38,6 +38,27 @@ struct FusedAdam {
   uint32_t* done = nullptr;
 };
 
+// K6 folded into the K10 trunk-reduce LAUNCH (world of one, no global-norm clip): extra workgroups
+// beside the partial-sum workgroups run K6's pass over the dense + heads range of the flat
+// buffers (the trunk range goes through FusedAdam in the reduce epilogue), so the SGD step loses
+// the K6 launch and the two latency-bound passes overlap. Pointers are already offset to the range
+// start; `bump_next` set = parity step counters (one lane writes the advanced copy), else the
+// FusedAdam ticket bump advances them in place.
+struct AdamTail {
+  float* master = nullptr;  // null: no Adam workgroups
+  float* m1 = nullptr;
+  float* m2 = nullptr;
+  const void* grad = nullptr;  // bf16
+  void* wbf16 = nullptr;
+  int64_t n = 0;
+  const float* hp = nullptr;
+  const int64_t* step_ctr = nullptr;
+  float grad_scale = 1.f;
+  int64_t* bump = nullptr;
+  int nbump = 0;
+  int64_t* bump_next = nullptr;
+};
+
 // XCD-aware remap of a linear workgroup id (bijective for any grid size): consecutive
 // logical ids land on the same XCD so neighbouring tiles share an L2.
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {

@@ -25,6 +25,7 @@
 // B[k 8(l>>4)+j][col l&15], j = 0..7; C/D: col l&15, row 4(l>>4)+i, i = 0..3.
 #include <hip/hip_bf16.h>
 
+#include "adam_device.h"
 #include "common.h"
 #include "kernels.h"
 #include "trunk_device.h"
@@ -519,12 +520,11 @@ __device__ __forceinline__ unsigned short* trunk_grad_dst(int e, unsigned short*
   if (e < C1 * 256 + C2 * 256 + C1) return &db1[e - C1 * 256 - C2 * 256];
   return &db2[e - C1 * 256 - C2 * 256 - C1];
 }
-__global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ partial, int G,
-                                                      unsigned short* __restrict__ dW1, WStrides w1,
-                                                      unsigned short* __restrict__ db1,
-                                                      unsigned short* __restrict__ dW2, WStrides w2,
-                                                      unsigned short* __restrict__ db2, const FusedAdam fa) {
-  __shared__ float red[RED_SLICES][64];
+// one partial-sum workgroup of k_trunk_reduce: 64 consecutive outputs x RED_SLICES slices of G
+__device__ __forceinline__ void trunk_reduce_block(const float* __restrict__ partial, int G, unsigned short* dW1,
+                                                   WStrides w1, unsigned short* db1, unsigned short* dW2, WStrides w2,
+                                                   unsigned short* db2, const FusedAdam& fa,
+                                                   float (&red)[RED_SLICES][64]) {
   const int c = threadIdx.x & 63, slice = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + c;
   const bool owner = slice == 0 && e < PART;  // the thread that finishes output e
@@ -555,6 +555,28 @@ __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ 
     // the trunk gradients are final here: store them, or (FusedAdam) apply Adam to them
     const AdamCoef ac = fa.grad_base ? adam_coef(fa.hp, fa.step_ctr) : AdamCoef{};
     grad_store_pf(fa, ac, dst, t, st);
+  }
+}
+__global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ partial, int G,
+                                                      unsigned short* __restrict__ dW1, WStrides w1,
+                                                      unsigned short* __restrict__ db1,
+                                                      unsigned short* __restrict__ dW2, WStrides w2,
+                                                      unsigned short* __restrict__ db2, const FusedAdam fa,
+                                                      const AdamTail at, int nred) {
+  __shared__ float red[RED_SLICES][64];
+  if (int(blockIdx.x) >= nred) {  // Adam workgroups (AdamTail): K6's pass over the dense + heads range
+    const AdamCoef ac = adam_coef(at.hp, at.step_ctr);
+    const int64_t tid = int64_t(blockIdx.x - nred) * blockDim.x + threadIdx.x;
+    const int64_t nthr = int64_t(gridDim.x - nred) * blockDim.x;
+    adam_span<__hip_bfloat16, true, 2>(at.master, at.m1, at.m2, static_cast<const __hip_bfloat16*>(at.grad),
+                                       static_cast<__hip_bfloat16*>(at.wbf16), at.grad_scale, ac, tid, nthr, at.n);
+  } else {
+    trunk_reduce_block(partial, G, dW1, w1, db1, dW2, w2, db2, fa, red);
+  }
+  if (at.bump_next) {  // parity counters (see k_adam_flat): the next step reads the other copy
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      for (int k = 0; k < at.nbump; k++) at.bump_next[k] = at.bump[k] + 1;
+    return;
   }
   // fused Adam: this launch is the last reader of the step counters in the SGD step
   last_block_bump(fa.bump, fa.nbump, fa.done);
@@ -615,19 +637,27 @@ int64_t nature_trunk_partial_floats(int64_t B) { return int64_t(nature_trunk_bwd
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream, int dbg, const FusedAdam& fa) {
+                      hipStream_t stream, int dbg, const FusedAdam& fa, const AdamTail& at) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
+  if (at.master) {
+    auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+    if (!(al(at.master, 16) && al(at.m1, 16) && al(at.m2, 16) && al(at.grad, 8) && al(at.wbf16, 8)) || at.n <= 0 ||
+        !fa.grad_base || !at.hp || !at.step_ctr || (at.bump_next && (!at.bump || at.nbump <= 0)))
+      throw std::invalid_argument("nature_trunk_bwd: Adam tail needs aligned buffers, the trunk FusedAdam and counters");
+  }
   const int G = nature_trunk_bwd_groups(B);
   hipLaunchKernelGGL(trunk::k_trunk_bwd, dim3(uint32_t(G)), dim3(trunk::NTB), 0, stream, obs, idx, ctr, period, B,
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(h1),
                      static_cast<const unsigned short*>(h2), static_cast<const unsigned short*>(dh2), partial, dbg);
   RMM_HIP_CHECK(hipGetLastError());
   if (dbg & 128) return;  // profiling: the backward kernel alone
-  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3((trunk::PART + 63) / 64), dim3(64 * trunk::RED_SLICES), 0, stream,
-                     partial, G,
+  const int nred = (trunk::PART + 63) / 64, NTR = 64 * trunk::RED_SLICES;
+  // Adam workgroups: two groups of 4 elements per lane (K6's default unroll)
+  const int nadam = at.master ? int(std::max<int64_t>(1, ((at.n + 3) / 4 + 2 * NTR - 1) / (2 * NTR))) : 0;
+  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3(nred + nadam), dim3(NTR), 0, stream, partial, G,
                      static_cast<unsigned short*>(dW1), ws(w1s), static_cast<unsigned short*>(db1),
-                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2), fa);
+                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2), fa, at, nred);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

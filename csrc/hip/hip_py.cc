@@ -25,6 +25,29 @@ inline T* P(uint64_t p) {
   return reinterpret_cast<T*>(p);
 }
 
+// [master, m1, m2, grad, wbf16, n, hp, step_ctr, bump, nbump, bump_next] (empty: no Adam workgroups);
+// pointers already offset to the range start, bump_next = 0 for the in-place ticket bump
+AdamTail adam_tail(const std::vector<uint64_t>& v, float grad_scale) {
+  AdamTail at;
+  if (v.empty()) return at;
+  if (v.size() != 11) throw std::invalid_argument("adam tail: 11 fields");
+  for (int k : {0, 1, 2, 3, 4, 6, 7})
+    if (v[k] == 0) throw std::invalid_argument("adam tail: null buffer");
+  at.master = P<float>(v[0]);
+  at.m1 = P<float>(v[1]);
+  at.m2 = P<float>(v[2]);
+  at.grad = P<const void>(v[3]);
+  at.wbf16 = P<void>(v[4]);
+  at.n = int64_t(v[5]);
+  at.hp = P<const float>(v[6]);
+  at.step_ctr = P<const int64_t>(v[7]);
+  at.bump = v[8] ? P<int64_t>(v[8]) : nullptr;
+  at.nbump = int(v[9]);
+  at.bump_next = v[10] ? P<int64_t>(v[10]) : nullptr;
+  at.grad_scale = grad_scale;
+  return at;
+}
+
 // [grad_base, master, m1, m2, wbf16, hp, step_ctr, bump, nbump, done] (empty: plain gradient stores)
 FusedAdam fused_adam(const std::vector<uint64_t>& v) {
   FusedAdam fa;
@@ -499,15 +522,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("nature_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, uint64_t W2,
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,
                                uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
-                               uint64_t stream, int dbg, std::vector<uint64_t> adam) {
+                               uint64_t stream, int dbg, std::vector<uint64_t> adam, std::vector<uint64_t> tail,
+                               float tail_scale) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("nature_trunk_bwd: 4 strides per weight");
     nature_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr,
                      ctr ? P<const int64_t>(ctr) : nullptr, period, B, P<const void>(W2), w2s.data(),
                      P<const void>(h1), P<const void>(h2), P<const void>(dh2), P<float>(partial), P<void>(dW1),
-                     w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream), dbg, fused_adam(adam));
+                     w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream), dbg, fused_adam(adam),
+                     adam_tail(tail, tail_scale));
   }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W2"), py::arg("w2s"),
      py::arg("h1"), py::arg("h2"), py::arg("dh2"), py::arg("partial"), py::arg("dW1"), py::arg("w1s"), py::arg("db1"),
-     py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0, py::arg("adam") = std::vector<uint64_t>{});
+     py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0, py::arg("adam") = std::vector<uint64_t>{},
+     py::arg("tail") = std::vector<uint64_t>{}, py::arg("tail_scale") = 1.0f);
 
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {

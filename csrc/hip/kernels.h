@@ -176,7 +176,8 @@ int64_t nature_trunk_partial_floats(int64_t B);
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream, int dbg = 0, const FusedAdam& fa = FusedAdam{});
+                      hipStream_t stream, int dbg = 0, const FusedAdam& fa = FusedAdam{},
+                      const AdamTail& at = AdamTail{});
 // dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
 // load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores.
 

@@ -19,6 +19,7 @@
 #include <stdexcept>
 #include <type_traits>
 
+#include "adam_device.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -290,22 +291,9 @@ void ppo_heads_loss(bool bwd, const void* heads, const float* cols, const float*
 
 // ============================================================== K6 flat Adam (fp32 master -> bf16 weights)
 
-// hp layout (device): [lr, beta1, beta2, eps, weight_decay, step]; step is incremented by the caller
-// before the launch (a 1-element add in the same stream / graph).
-__device__ __forceinline__ void adam_load4(const float* g, int64_t i, float (&o)[4]) {
-  const float4 v = *reinterpret_cast<const float4*>(g + i);
-  o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = v.w;
-}
-__device__ __forceinline__ void adam_load4(const __hip_bfloat16* g, int64_t i, float (&o)[4]) {
-  const uint2 v = *reinterpret_cast<const uint2*>(g + i);  // 4 bf16 = 8 B
-  o[0] = __uint_as_float(v.x << 16), o[1] = __uint_as_float(v.x & 0xffff0000u);
-  o[2] = __uint_as_float(v.y << 16), o[3] = __uint_as_float(v.y & 0xffff0000u);
-}
-__device__ __forceinline__ uint32_t bf16x2_rn(float a, float b) {
-  const uint32_t lo = __bfloat16_as_ushort(__float2bfloat16(a)), hi = __bfloat16_as_ushort(__float2bfloat16(b));
-  return lo | (hi << 16);
-}
-
+// hp layout (device): [lr, beta1, beta2, eps, weight_decay, step]; the step comes from the device
+// counter when given. The per-element pass is adam_span (adam_device.h), shared with the Adam
+// workgroups of the trunk-reduce launch.
 // Each thread updates U groups of 4 consecutive elements with 16-B fp32 and 8-B bf16 accesses (the
 // step is HBM / Infinity-Cache bound: 28 B/param), issuing every group's loads before the first
 // update so U x 4 vector loads are in flight per lane; the n % 4 tail is done by the first threads
@@ -332,50 +320,7 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
     bump = nullptr;
   }
   const int64_t tid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, nthr = int64_t(gridDim.x) * blockDim.x;
-  int64_t scalar_from = 0;
-  if constexpr (VEC) {
-    const int64_t nv = n >> 2;
-    for (int64_t v0 = tid; v0 < nv; v0 += nthr * U) {
-      float g[U][4];
-      float4 w[U], a[U], b[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int64_t v = v0 + u * nthr;
-        if (v < nv) {
-          const int64_t i = v << 2;
-          adam_load4(grad, i, g[u]);
-          w[u] = *reinterpret_cast<const float4*>(master + i);
-          a[u] = *reinterpret_cast<const float4*>(m1 + i);
-          b[u] = *reinterpret_cast<const float4*>(m2 + i);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int64_t v = v0 + u * nthr;
-        if (v < nv) {
-          const int64_t i = v << 2;
-          w[u].x = adam_one(w[u].x, g[u][0] * grad_scale, a[u].x, b[u].x, c);
-          w[u].y = adam_one(w[u].y, g[u][1] * grad_scale, a[u].y, b[u].y, c);
-          w[u].z = adam_one(w[u].z, g[u][2] * grad_scale, a[u].z, b[u].z, c);
-          w[u].w = adam_one(w[u].w, g[u][3] * grad_scale, a[u].w, b[u].w, c);
-          *reinterpret_cast<float4*>(master + i) = w[u];
-          *reinterpret_cast<float4*>(m1 + i) = a[u];
-          *reinterpret_cast<float4*>(m2 + i) = b[u];
-          if (wbf16)
-            *reinterpret_cast<uint2*>(wbf16 + i) = make_uint2(bf16x2_rn(w[u].x, w[u].y), bf16x2_rn(w[u].z, w[u].w));
-        }
-      }
-    }
-    scalar_from = nv << 2;
-  }
-  for (int64_t i = scalar_from + tid; i < n; i += nthr) {
-    float a = m1[i], b = m2[i];
-    const float w = adam_one(master[i], ldf(grad, i) * grad_scale, a, b, c);
-    m1[i] = a;
-    m2[i] = b;
-    master[i] = w;
-    if (wbf16) wbf16[i] = __float2bfloat16(w);
-  }
+  adam_span<TG, VEC, U>(master, m1, m2, grad, wbf16, grad_scale, c, tid, nthr, n);
   last_block_bump(bump, nbump, done);
 }
 

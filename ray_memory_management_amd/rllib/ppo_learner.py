@@ -379,11 +379,42 @@ class PPOLearner:
         c1, c2 = self.model.convs[0], self.model.convs[1]
         ws = self._manual_ws(full["mbs"])
         g = [p._rmm_grad_out for p in self.params]
-        h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), self._ctr().data_ptr(), int(full["period"]),
+        ctr = self._ctr().data_ptr()
+        adam, tail = (self._tail_adam_args() if self._tail_adam() else (self._fused_adam_args(bump=True), []))
+        h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), ctr, int(full["period"]),
                            int(full["mbs"]), c2.weight.data_ptr(), list(c2.weight.stride()), ws["h1"].data_ptr(),
                            ws["h2"].data_ptr(), ws["dx"].data_ptr(), ws["part"].data_ptr(), g[0].data_ptr(),
                            list(c1.weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
-                           adam=self._fused_adam_args(bump=True))
+                           adam=adam, tail=tail, tail_scale=1.0 / self.world)
+
+    def _tail_adam(self) -> bool:
+        """World of one without a global-norm clip: K6 folds into the K10 trunk-reduce LAUNCH — the
+        reduce's epilogue applies Adam to the trunk parameters (FusedAdam) while extra workgroups of
+        the same launch run K6's pass over the dense + heads range (adam_device.h: the same code as
+        K6, so the update is bit-identical). The SGD step loses the K6 launch and the two
+        latency-bound passes (trunk partial sums, 28 MB of Adam traffic) overlap. RMM_TAIL_ADAM=0
+        restores the separate K6."""
+        return (self._manual is not None and self.world == 1 and self.clip_out is None and self._manual % 4 == 0
+                and not self._fused_adam() and not self._split_adam_ok()
+                and os.environ.get("RMM_TAIL_ADAM", "0") == "1")
+
+    def _tail_adam_args(self):
+        """(FusedAdam fields for the trunk range, AdamTail fields for the dense + heads range). In a
+        chained graph with parity counters the launch writes the advanced counters into the other
+        copy from one lane (as K6 does); otherwise the reduce's last workgroup bumps them in place."""
+        cur = self._ctr().data_ptr()
+        parity = self._parity and not (self._parity_last and self._par == 0)
+        lo = self._manual
+        f4, b2 = 4 * lo, 2 * lo
+        adam = [self.flat_grad.data_ptr(), self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(),
+                self._wptr(), self.hp.data_ptr(), cur + 8, 0 if parity else cur, 0 if parity else 2,
+                0 if parity else self._bump_done.data_ptr()]
+        tail = [self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
+                self.flat_grad.data_ptr() + b2, self._wptr() + b2, self.n_params - lo, self.hp.data_ptr(), cur + 8,
+                cur, 2, self._ctrs[1 - self._par].data_ptr() if parity else 0]
+        if parity:
+            self._par ^= 1
+        return adam, tail
 
     def _fused_adam(self) -> bool:
         """World of one without a global-norm clip: K6 folds into the gradient epilogues — K12 applies
@@ -585,7 +616,7 @@ class PPOLearner:
                 return
             else:
                 self._manual_trunk_bwd(full)
-                if self._fused_adam():
+                if self._fused_adam() or self._tail_adam():
                     return
             self._opt_launch()
         else:
@@ -686,7 +717,7 @@ class PPOLearner:
                             self._manual_trunk_bwd(full)
                             if self.world > 1:
                                 self.comm.allreduce(self.flat_grad[:self._manual])
-                            if not self._fused_adam():
+                            if not (self._fused_adam() or self._tail_adam()):
                                 self._opt_launch()
                         else:
                             self._fast_step(full, True)

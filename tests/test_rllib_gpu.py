@@ -615,3 +615,41 @@ def test_parity_counters_match_ticket_bump(cuda, monkeypatch, chain_cap):
     assert torch.equal(a.w_bf16, b.w_bf16)
     assert torch.equal(a.ctr, b.ctr)
     assert int(b.ctr[1]) == 24  # Adam steps: 2 updates x 12
+
+
+@pytest.mark.parametrize("chain_cap,graphs", [(3, True), (4, True), (4, False)])
+def test_tail_adam_matches_k6(cuda, monkeypatch, chain_cap, graphs):
+    """K6 folded into the K10 trunk-reduce launch (RMM_TAIL_ADAM=1: FusedAdam on the trunk range in
+    the reduce epilogue + extra Adam workgroups over the dense + heads range) vs the separate K6:
+    bit-identical master / moments / bf16 weights / step counters over two updates — chained graphs
+    with parity counters (odd chain: the last step bumps in place) and the eager path."""
+    from ray_memory_management_amd.rllib.ppo_learner import GPURolloutSampler, PPOLearner
+    from ray_memory_management_amd.rllib.env import GPUSyntheticAtariVectorEnv
+    from ray_memory_management_amd.rllib.models import VisionNetwork
+
+    monkeypatch.setenv("RMM_SGD_CHAIN", str(chain_cap))
+    env = GPUSyntheticAtariVectorEnv(16, cuda, num_actions=4, seed=0)
+    torch.manual_seed(0)
+    base = VisionNetwork(4)
+    cfg = {"sgd_minibatch_size": 64, "num_sgd_iter": 3, "use_graphs": graphs}  # 12 SGD steps per update
+    learners = {}
+    for tail in ("0", "1"):
+        monkeypatch.setenv("RMM_TAIL_ADAM", tail)
+        m = VisionNetwork(4)
+        m.load_state_dict(base.state_dict())
+        learners[tail] = PPOLearner(m, dict(cfg), device=cuda, action_space=env.action_space)
+    assert learners["1"]._tail_adam() and not learners["0"]._tail_adam()
+    sampler = GPURolloutSampler(env, learners["0"].model, fragment=16, use_graphs=False)
+    first = sampler.sample()
+    Batch = type(first)
+    batches = [{k: v.clone() for k, v in first.items()}, {k: v.clone() for k, v in sampler.sample().items()}]
+    for tail, ln in learners.items():
+        monkeypatch.setenv("RMM_TAIL_ADAM", tail)
+        for i, b in enumerate(batches):
+            torch.manual_seed(100 + i)
+            ln.update(Batch({k: v.clone() for k, v in b.items()}))
+        assert ln.graphs == graphs
+    a, b = learners["0"], learners["1"]
+    for name in ("master", "m1", "m2", "w_bf16", "ctr"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert int(b.ctr[1]) == 24  # Adam steps: 2 updates x 12
