@@ -392,11 +392,12 @@ class PPOLearner:
         reduce's epilogue applies Adam to the trunk parameters (FusedAdam) while extra workgroups of
         the same launch run K6's pass over the dense + heads range (adam_device.h: the same code as
         K6, so the update is bit-identical). The SGD step loses the K6 launch and the two
-        latency-bound passes (trunk partial sums, 28 MB of Adam traffic) overlap. RMM_TAIL_ADAM=0
+        latency-bound passes (trunk partial sums, 28 MB of Adam traffic) overlap: fused loop 10.88 /
+        11.04 -> 10.62 / 10.67 ms per iteration on MI355X (profiles/tail_adam_r4.txt). RMM_TAIL_ADAM=0
         restores the separate K6."""
         return (self._manual is not None and self.world == 1 and self.clip_out is None and self._manual % 4 == 0
                 and not self._fused_adam() and not self._split_adam_ok()
-                and os.environ.get("RMM_TAIL_ADAM", "0") == "1")
+                and os.environ.get("RMM_TAIL_ADAM", "1") != "0")
 
     def _tail_adam_args(self):
         """(FusedAdam fields for the trunk range, AdamTail fields for the dense + heads range). In a
