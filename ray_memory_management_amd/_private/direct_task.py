@@ -421,7 +421,9 @@ class DirectTaskSubmitter:
             lineage = spec
         self.done_buf.append((lineage, (spec["task_id"], spec.get("name"), status == "ok", lease.node, attempt,
                                         t0, t1, spec["resources"])))
-        if len(self.done_buf) >= 512:
+        # a lineage record goes out at once: the head reconstructs from it when the outputs are lost
+        # (e.g. the GPU worker holding them dies), which can happen right after the owner's get
+        if len(self.done_buf) >= 512 or lineage is not None:
             self.flush()
 
     def flush(self):

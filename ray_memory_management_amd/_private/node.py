@@ -1586,6 +1586,8 @@ class Head:
     # ------------------------------------------------------------------ housekeeping
     def _housekeeping(self):
         now = time.time()
+        if self.recovery.awaiting:
+            self.recovery.expire_awaiting(now)
         # reap dead worker processes that never connected / crashed
         for w in list(self.workers.values()):
             if w.proc is not None and w.proc.poll() is not None:

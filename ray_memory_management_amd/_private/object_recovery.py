@@ -52,6 +52,11 @@ class ObjectRecoveryManager:
         self.obj_node: Dict[bytes, int] = {}         # return oid -> node its primary copy lives on
         self.num_reconstructions = 0
         self.num_lost = 0
+        # lost objects whose lineage may still be in flight: a directly submitted task's completion
+        # record travels owner -> head separately from the worker's death, so a loss can arrive
+        # first; oid -> (deadline, cause, owner_died), settled by task_finished or the deadline
+        self.awaiting: Dict[bytes, tuple] = {}
+        self.lineage_grace_s = 2.0
 
     # ------------------------------------------------------------------ recording
     @staticmethod
@@ -82,7 +87,8 @@ class ObjectRecoveryManager:
             return
         rec = LineageRec(spec, rets, node)
         rec.live = {o for o in rets if o in self.head.refcounts}
-        if not rec.live:
+        late = [o for o in rets if o in self.awaiting]  # lost before this record arrived
+        if not rec.live and not late:
             return  # nobody references the outputs any more: nothing to protect
         for r in spec.get("arg_refs", ()):
             ptid = self.obj_task.get(r)
@@ -95,6 +101,23 @@ class ObjectRecoveryManager:
         while len(self.lineage) > self.max_entries:
             otid, orec = self.lineage.popitem(last=False)
             self._forget(otid, orec)
+        for oid in late:
+            _, cause, owner_died = self.awaiting.pop(oid)
+            if not self.recover(oid):
+                self._lost_error(oid, cause, owner_died)
+
+    def expire_awaiting(self, now: float) -> None:
+        """Lost objects whose lineage never arrived within the grace period fail (head housekeeping)."""
+        for oid, (deadline, cause, owner_died) in list(self.awaiting.items()):
+            if now >= deadline:
+                del self.awaiting[oid]
+                self._lost_error(oid, cause, owner_died)
+
+    def _lost_error(self, oid: bytes, cause: str, owner_died: bool) -> None:
+        err = (exc.OwnerDiedError if owner_died else exc.ObjectLostError)(
+            oid.hex(), message=f"Object {oid.hex()} was lost ({cause}) and cannot be reconstructed "
+                               "(no lineage, or the task's max_retries is exhausted).")
+        self._store_error(oid, err)
 
     def object_freed(self, oid: bytes) -> None:
         self.obj_node.pop(oid, None)
@@ -155,11 +178,14 @@ class ObjectRecoveryManager:
             handled.append(oid)
             to_recover.append(oid)
         for oid in to_recover:
-            if not self.recover(oid):
-                err = (exc.OwnerDiedError if owner_died else exc.ObjectLostError)(
-                    oid.hex(), message=f"Object {oid.hex()} was lost ({cause}) and cannot be reconstructed "
-                               "(no lineage, or the task's max_retries is exhausted).")
-                self._store_error(oid, err)
+            if self.recover(oid):
+                continue
+            if oid not in self.obj_task and self.lineage_grace_s > 0:
+                import time
+
+                self.awaiting[oid] = (time.time() + self.lineage_grace_s, cause, owner_died)
+                continue
+            self._lost_error(oid, cause, owner_died)
         return handled
 
     def recover(self, oid: bytes, _depth: int = 0) -> bool:

@@ -152,6 +152,7 @@ def test_ppo_learner_actors_rccl_identical(ray_start):
 
     ray.shutdown()
     os.environ["RMM_RCCL_SAME_DEVICE"] = "1"
+    os.environ["RMM_PEER_COMM"] = "0"  # this test is about RCCL: the peer-memory comm would win on one GPU
     try:
         ray.init(num_cpus=6, num_gpus=1, object_store_memory=1 << 30, _system_config={"prestart_workers": 0})
         algo = (PPOConfig().environment("SyntheticAtariVec-v0", env_config={"num_actions": 4, "episode_len": 50})
@@ -174,3 +175,4 @@ def test_ppo_learner_actors_rccl_identical(ray_start):
             algo.stop()
     finally:
         os.environ.pop("RMM_RCCL_SAME_DEVICE", None)
+        os.environ.pop("RMM_PEER_COMM", None)
