@@ -3,7 +3,8 @@ profiling phase masks: prints µs per launch (graph-replayed: GPU time, not host
 (B=500 SGD minibatch, B=50 rollout step) and bwd (B=500), each phase skipped in turn to attribute time.
 fwd dbg bits: 1 conv1 MFMA, 2 conv2 MFMA, 8 weight staging, 16 h1 store, 32 frame loads, 64 h2 store,
 128 return at once (launch + dispatch floor). bwd bits: 1 dW2, 2 dh1, 4 dW1, 8 P0 loads, 16 partial
-stores, 32 LDS zeroing, 64 return at once, 128 skip the reduce launch. Usage: python benchmarks/bench_trunk.py"""
+stores, 32 st zeroing, 64 return at once, 128 skip the reduce launch, 256 all LDS zeroing, 512 W2 staging,
+1024 the bias-gradient epilogue. Usage: python benchmarks/bench_trunk.py"""
 import json
 import os
 import sys
@@ -86,7 +87,8 @@ def main():
             part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
             dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
             db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
-            for dbg in (0, 1, 2, 4, 7, 8, 15, 16, 31, 63, 64, 128, 128 + 31, 128 + 64):
+            for dbg in (0, 1, 2, 4, 7, 8, 15, 16, 31, 63, 64, 128, 128 + 31, 128 + 64, 159 + 256, 159 + 512,
+                        159 + 1024, 159 + 256 + 512 + 1024):
                 out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                     obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                     h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),
@@ -100,7 +102,7 @@ def main():
         part = torch.empty(h.nature_trunk_partial_floats(B), dtype=torch.float32, device=dev)
         dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
         db1, db2 = torch.empty_like(b1), torch.empty_like(b2)
-        for dbg in (0, 15, 31, 128 + 31):
+        for dbg in (0, 15, 31, 128 + 31, 159 + 256 + 512 + 1024):
             out[f"bwd_B{B}_dbg{dbg}"] = round(timeit(lambda: h.nature_trunk_bwd(
                 obs.data_ptr(), idx.data_ptr(), 0, 1, B, w2.data_ptr(), list(w2.stride()), h1.data_ptr(),
                 h2.data_ptr(), dh2.data_ptr(), part.data_ptr(), dw1.data_ptr(), list(w1.stride()), db1.data_ptr(),

@@ -285,7 +285,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   // before the LDS zeroing, so the weight round trip and the frame's hide behind it
   constexpr int NH1 = BWD_NH1, PH1 = BWD_PH1, NH2 = BWD_NH2, PH2 = BWD_PH2;
   WeightRegs<NTB, C2, C1, 4> wr;
-  weight_issue(W2, w2, wr);
+  if (!(dbg & 512)) weight_issue(W2, w2, wr);
   FrameRegs<NTB> fr;
   u16x8 hv1[PH1];
   u16x8 hv2[PH2], gv2[PH2];
@@ -293,11 +293,13 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     bwd_issue(blockIdx.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);
     h1_issue(blockIdx.x, h1, hv1);
   }
-  if (!(dbg & 32)) zero_lds(st, ST_C * ST_CP * 2);
-  zero_lds(h1p, H1P_ELEMS * 2);
-  zero_lds(dp2, D2W * D2W * C2 * 2);
-  zero_lds(dp2t, C2 * DP2_PITCH * 2);
-  weight_store(wr, W2, w2, w2s, W2_PITCH);
+  if (!(dbg & (32 | 256))) zero_lds(st, ST_C * ST_CP * 2);
+  if (!(dbg & 256)) {
+    zero_lds(h1p, H1P_ELEMS * 2);
+    zero_lds(dp2, D2W * D2W * C2 * 2);
+    zero_lds(dp2t, C2 * DP2_PITCH * 2);
+  }
+  if (!(dbg & 512)) weight_store(wr, W2, w2, w2s, W2_PITCH);
 
   // dh1 = conv2ᵀ(dpre2): waves 2c, 2c+1 own stride-parity class c = (py, px). In a class,
   // input pixel (y, x) = (2a+py, 2c+px) receives taps ky ∈ {py, py+2}, kx ∈ {px, px+2} from
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
   float db1 = 0.f;                       // this lane's ci = r
   float db2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // co2 = 8(tid&3) + j
   __syncthreads();  // wt read from w2s
-  zero_lds(dp1s, 2 * DB_B * 2);
+  if (!(dbg & 256)) zero_lds(dp1s, 2 * DB_B * 2);
   __syncthreads();
 
   // P0 is software-pipelined across this workgroup's frames: the global loads of frame b + G are
@@ -468,6 +470,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
 #pragma unroll
     for (int e = 0; e < 4; e++) out[r * 256 + ky * 32 + kx * 4 + e] = aw1[bb][e] * (1.0f / 255.0f);
   }
+  if (dbg & 1024) return;  // profiling: no bias-gradient epilogue
   // db1: lanes r, r+16, r+32, r+48 of every wave share ci = r
   db1 += __shfl_xor(db1, 16);
   db1 += __shfl_xor(db1, 32);

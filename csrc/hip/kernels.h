@@ -179,7 +179,9 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                       hipStream_t stream, int dbg = 0, const FusedAdam& fa = FusedAdam{},
                       const AdamTail& at = AdamTail{});
 // dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
-// load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores.
+// load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores,
+// bit5 the st zeroing, bit6 return at once, bit7 the reduce launch, bit8 all LDS zeroing, bit9 the W2
+// staging, bit10 the bias-gradient epilogue.
 
 // K17: learner-side sample-batch ingest (see ingest_kernels.hip). raw [rows, A+5] fp32 =
 // [logits(A) | logp | vf | reward | done | action], blocks = one entry per rollout fragment

@@ -10,3 +10,8 @@ for i in 1 2; do
 done
 timeout -k 10 200 python -u benchmarks/native_rollout_probe.py > gpurun_out/probe_p.log 2>&1 || { tail -5 gpurun_out/probe_p.log; exit 1; }
 tail -12 gpurun_out/probe_p.log
+timeout -k 10 240 python3 -u benchmarks/bench_trunk.py > gpurun_out/trunk_phases_p.json 2> gpurun_out/trunk_phases_p.err || { tail -5 gpurun_out/trunk_phases_p.err; exit 1; }
+cat gpurun_out/trunk_phases_p.json
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_p -o run -- python3 bench.py --mode fused --steps 5 --warmup 2 --no-putget > gpurun_out/prof_p.log 2>&1 || { tail -5 gpurun_out/prof_p.log; exit 1; }
+find gpurun_out/prof_p -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -14 {} | cut -d, -f1-8'
