@@ -345,6 +345,11 @@ def get_tensor(worker, oid: bytes, _ignored=None):
                 _map_release(owner, ipc, local)
 
             cap = h.dlpack(m.base + off, list(meta["shape"]), code, bits, local, _done)
+            if os.environ.get("RMM_SHARED_WEIGHTS_DEBUG"):
+                import sys
+
+                print(f"[gpu-store] pid {os.getpid()} get {oid.hex()[:16]}: owner {owner} slab {slab} off {off:#x} "
+                      f"nbytes {nbytes} mapping base {m.base:#x} device {local}", file=sys.stderr, flush=True)
             import torch
 
             t = torch.from_dlpack(cap)

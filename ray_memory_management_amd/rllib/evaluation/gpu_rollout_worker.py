@@ -90,9 +90,19 @@ class GPURolloutWorker:
                     if os.environ.get("RMM_SHARED_WEIGHTS_DEBUG"):
                         import sys
 
-                        print(f"[shared-weights] worker pid {os.getpid()}: params alias {flat.data_ptr():#x} .. "
-                              f"{flat.data_ptr() + flat.numel() * flat.element_size():#x}", file=sys.stderr,
-                              flush=True)
+                        lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * flat.element_size()
+                        print(f"[shared-weights] worker pid {os.getpid()}: params alias {lo:#x} .. {hi:#x}",
+                              file=sys.stderr, flush=True)
+                        for name, p in self.model.named_parameters():
+                            end = p.data_ptr() + p.numel() * p.element_size()
+                            print(f"[shared-weights]   {name} {tuple(p.shape)} {tuple(p.stride())} {p.dtype} "
+                                  f"{p.data_ptr():#x}..{end:#x} {'in' if lo <= p.data_ptr() and end <= hi else 'OUTSIDE'}",
+                                  file=sys.stderr, flush=True)
+                        torch.cuda.synchronize(self.device)
+                        chk = float(flat.float().abs().sum())  # reads every byte through the mapping
+                        torch.cuda.synchronize(self.device)
+                        print(f"[shared-weights] worker pid {os.getpid()}: read the whole alias ok (sum|w| {chk:.4g})",
+                              file=sys.stderr, flush=True)
                     self._on_params_rebound()
                     return
                 for name, off, shape, stride in weights["__rmm_layout__"]:  # another GPU: copy

@@ -48,6 +48,16 @@ class _ConvBiasReLUFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+def _dbg_sync(what: str) -> None:
+    """RMM_KERNEL_SYNC_DEBUG=1 (fault hunting): synchronise after a launch and log it, so the last line a
+    faulting process printed names the kernel. Never while a HIP graph is being captured."""
+    if os.environ.get("RMM_KERNEL_SYNC_DEBUG") and not torch.cuda.is_current_stream_capturing():
+        import sys
+
+        torch.cuda.synchronize()
+        print(f"[kernel-sync pid {os.getpid()}] {what} ok", file=sys.stderr, flush=True)
+
+
 class _NatureTrunkFn(torch.autograd.Function):
     """K10: both Nature-CNN convs (+bias/ReLU, + the u8 frame gather/scale) as ONE MFMA kernel
     forward and one kernel (+ a deterministic partial-sum reduce) backward — see
@@ -478,12 +488,14 @@ class VisionNetwork(nn.Module):
                                       t_ptr.data_ptr(), B, c1.weight.data_ptr(), list(c1.weight.stride()),
                                       c1.bias.data_ptr(), c2.weight.data_ptr(), list(c2.weight.stride()),
                                       c2.bias.data_ptr(), h.data_ptr(), stream)
+            _dbg_sync(f"K10 push (W1 {c1.weight.data_ptr():#x} b1 {c1.bias.data_ptr():#x} W2 {c2.weight.data_ptr():#x})")
         else:
             h = nature_trunk(obs, c1.weight, c1.bias, c2.weight, c2.bias)
         if os.environ.get("RMM_NO_K13S") is None:  # K13s: split-K partials, summed in K16's prologue
             S = hip.dense_fwd_part_slices(B, h.shape[1], 256)
             hpart = torch.empty(S * B * 256, dtype=torch.float32, device=h.device)
             hip.dense_fwd_part(h.data_ptr(), layer.weight.data_ptr(), B, h.shape[1], 256, hpart.data_ptr(), S, stream)
+            _dbg_sync(f"K13s (W {layer.weight.data_ptr():#x})")
             hidden_ptr, part = 0, dict(hpart=hpart.data_ptr(), S=S, hb=layer.bias.data_ptr())
         else:
             hidden = torch.empty((B, 256), dtype=h.dtype, device=h.device)
@@ -495,6 +507,7 @@ class VisionNetwork(nn.Module):
                                act_now.data_ptr() if hasattr(act_now, "data_ptr") else int(act_now), B,
                                heads.out_features, stream,
                                done.data_ptr() if done is not None else 0, **part)  # K16 (act_now: maybe device-mapped host)
+        _dbg_sync(f"K16 (Wh {heads.weight.data_ptr():#x} bh {heads.bias.data_ptr():#x})")
         return True
 
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,
