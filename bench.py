@@ -231,6 +231,9 @@ def _runtime(args, n_gpus):
                 "cpu_budget": budget, "learners": algo.learner_group.device_info()}
         for _ in range(args.warmup):
             algo.train()
+        dev = bool(getattr(algo, "_device_weights_ok", lambda: False)())
+        info["weights_sync"] = ("shared-hbm" if dev and algo._shared_weights_ok() else "hbm-object" if dev
+                                else "host")
         return algo, info
     except BaseException:
         ray.shutdown()

@@ -231,14 +231,17 @@ class PPO(Algorithm):
 
     def _shared_weights_ok(self) -> bool:
         """Rollout workers alias the learners' live HBM weights (zero-copy, set once) instead of
-        receiving a copy per iteration. Opt-in (RMM_SHARED_WEIGHTS=1 or config
-        share_device_weights=True): profiles/shared_weights_r3_fault.txt."""
+        receiving a copy per iteration. Default on (RMM_SHARED_WEIGHTS=0 or config
+        share_device_weights=False turns it off): runtime bench 338-348k -> 350-354k samples/s on
+        MI355X. The GPU memory fault this path hit in rounds 3-4 was the hybrid worker's graph
+        recapture after the rebind: its warm-up steps ran at rollout row T and wrote past the
+        rollout buffers (fixed in HybridGroup.capture; profiles/shared_weights_r4.txt)."""
         import os
 
         env = os.environ.get("RMM_SHARED_WEIGHTS")
         if env is not None:
             return env == "1"
-        return bool(getattr(self.algo_config, "share_device_weights", False))
+        return bool(getattr(self.algo_config, "share_device_weights", True))
 
     def _device_weights_ok(self) -> bool:
         """Weights go learner → rollout workers through HBM when both sides are GPU processes:

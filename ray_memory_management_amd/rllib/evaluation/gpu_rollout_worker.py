@@ -298,9 +298,16 @@ class _EnvGroup:
         self.gate = bool(self.h_release_dev) and os.environ.get("RMM_ROLLOUT_GATE", "0") != "0"
         with torch.cuda.stream(stream):
             saved = self.s_obs.clone() if self.device_stack else None
+            saved_ctr = self.ctr_t.clone()  # a capture has no effect on the sampling stream
             for _ in range(2):
+                # the warm-up steps write rollout row *t: a recapture after a fragment (parameters
+                # rebound, e.g. zero-copy shared weights) finds t == T there, and rows T, T+1 lie past
+                # the end of the rollout buffers (the K10 push stores a whole frame row: the GPU
+                # memory fault of the round-3/4 shared-weights runs, profiles/shared_weights_r4.txt)
+                self.ctr_t[1].zero_()
                 self.release()
                 self.policy_step()
+            self.ctr_t.copy_(saved_ctr)
             self.ctr_t[1].zero_()
             if saved is not None:  # warm-up pushes must not advance the frame stacks
                 self.s_obs.copy_(saved)

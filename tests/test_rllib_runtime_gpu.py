@@ -410,3 +410,59 @@ def test_k10_band_push_matches_stack_push(cuda, monkeypatch):
     for x, y in zip(fa, fb):
         for k in ("obs", "_raw", "_boot"):
             assert torch.equal(x[k], y[k]), k
+
+
+def test_hybrid_recapture_mid_life_keeps_fragments(cuda):
+    """A hybrid worker that recaptures its policy-step graphs after a fragment (parameters rebound:
+    zero-copy shared weights) must produce the same fragments as one that never recaptured. The
+    recapture's warm-up steps used to run at rollout row T (the previous fragment's end) and store
+    rows T, T+1 past the rollout buffers — a GPU memory fault (profiles/shared_weights_r4.txt)."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 20}, "num_envs_per_worker": 6,
+           "rollout_fragment_length": 12, "seed": 5}
+    a = HybridRolloutWorker(config=cfg)
+    b = HybridRolloutWorker(config=cfg)
+    for i in range(3):
+        if i:
+            a._on_params_rebound()  # recapture before this fragment
+        fa, fb = a.sample(), b.sample()
+        assert torch.equal(fa["obs"], fb["obs"])
+        assert torch.equal(fa["_raw"], fb["_raw"]) and torch.equal(fa["_boot"], fb["_boot"])
+
+
+def test_ppo_hybrid_shared_weights(cuda, monkeypatch):
+    """Zero-copy weights (RMM_SHARED_WEIGHTS=1): the learner's bf16 weights move once into an HBM
+    object that the co-located hybrid rollout workers alias over hipIPC; after the learner's next
+    in-place Adam steps the workers' parameters ARE the new weights (no per-iteration publish)."""
+    import ray_memory_management_amd as ray
+    from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
+
+    monkeypatch.setenv("RMM_SHARED_WEIGHTS", "1")
+    ray.init(num_cpus=4, num_gpus=1, object_store_memory=1 << 30)
+    try:
+        cfg = (PPOConfig().environment("SyntheticAtariVec-v0", env_config={"episode_len": 50})
+               .rollouts(num_rollout_workers=2, num_envs_per_worker=5, rollout_fragment_length=20,
+                         postprocess_on_learner=True)
+               .training(train_batch_size=200, sgd_minibatch_size=50, num_sgd_iter=2)
+               .resources(num_learner_workers=1, num_gpus_per_learner_worker=0.5, num_gpus_per_worker=0.25)
+               .debugging(seed=0))
+        algo = cfg.build()
+        for _ in range(3):
+            r = algo.train()
+        st = r["info"]["learner"]["default_policy"]["learner_stats"]
+        assert np.isfinite(st["total_loss"]) and st["num_sgd_steps"] == 8
+        assert algo._shared_weights_ok() and algo._dev_refs is not None
+        ws = algo.workers.remote_workers()
+        assert all(ray.get([w.apply.remote(lambda x: getattr(x, "_shared_key", None) is not None) for w in ws]))
+        master = algo.learner_group.get_weights()
+        for w in ws:  # no set_weights here: the aliased parameters already hold the last update
+            got = ray.get(w.get_weights.remote())
+            for k, v in master.items():
+                want = torch.from_numpy(np.ascontiguousarray(v)).to(torch.bfloat16).float().numpy()
+                np.testing.assert_array_equal(got[k], want)
+        algo.stop()
+    finally:
+        ray.shutdown()
