@@ -341,6 +341,63 @@ PYBIND11_MODULE(_hip, m) {
     return hybrid_rollout(G, T, threads, spin);
   }, py::arg("groups"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false);
   m.def("hybrid_rollout_phases", &hybrid_rollout_phases);
+  // the native loop over ONE group with direct kernel launches per step (no graph): `group` =
+  // hybrid_rollout's 15 fields (exec ignored), weights / strides / bufs as hybrid_rollout_server,
+  // k16_done = K16's zero-initialised completion counter
+  m.def("hybrid_rollout_direct", [](const std::vector<uint64_t>& v, const std::vector<uint64_t>& wts,
+                                    std::vector<int64_t> w1s, std::vector<int64_t> w2s,
+                                    const std::vector<uint64_t>& bufs, int64_t B, int slices, int A1, uint32_t seed,
+                                    uint64_t k16_done, int64_t T, int threads, bool spin) {
+    if (v.size() < 15 || wts.size() != 8 || bufs.size() < 11 || w1s.size() != 4 || w2s.size() != 4 || !k16_done)
+      throw std::invalid_argument("hybrid_rollout_direct: 15 group fields, 8 weights, 11 buffers, 4+4 strides, done");
+    RolloutGroup g;
+    g.stream = S(v[1]);
+    g.env.pools = P<const uint8_t>(v[2]);
+    g.env.t = P<int64_t>(v[3]);
+    g.env.step = P<uint64_t>(v[4]);
+    g.env.seed = v[5];
+    g.env.n = int64_t(v[6]);
+    g.env.num_actions = int64_t(v[7]);
+    g.env.episode_len = int64_t(v[8]);
+    g.act = P<const int64_t>(v[9]);
+    g.new_frames = P<uint8_t>(v[10]);
+    g.rew = P<float>(v[11]);
+    g.done = P<float>(v[12]);
+    g.ep_rew = P<double>(v[13]);
+    g.ep_len = P<int64_t>(v[14]);
+    if (g.env.n != B) throw std::invalid_argument("hybrid_rollout_direct: env count != B");
+    RolloutServerArgs a;
+    a.W1 = P<const void>(wts[0]);
+    a.b1 = P<const void>(wts[1]);
+    a.W2 = P<const void>(wts[2]);
+    a.b2 = P<const void>(wts[3]);
+    a.Wd = P<const void>(wts[4]);
+    a.bd = P<const void>(wts[5]);
+    a.Wh = P<const void>(wts[6]);
+    a.bh = P<const void>(wts[7]);
+    for (int k = 0; k < 4; k++) a.w1s[k] = w1s[k], a.w2s[k] = w2s[k];
+    a.stack = P<uint8_t>(bufs[0]);
+    a.nf = P<const uint8_t>(bufs[1]);
+    a.rows = P<uint8_t>(bufs[2]);
+    a.h2 = P<void>(bufs[3]);
+    a.hpart = P<float>(bufs[4]);
+    a.act = P<int64_t>(bufs[5]);
+    a.logp = P<float>(bufs[6]);
+    a.vf = P<float>(bufs[7]);
+    a.lout = P<float>(bufs[8]);
+    a.act_now = P<int64_t>(bufs[9]);
+    a.ctr_t = P<int64_t>(bufs[10]);
+    a.B = B;
+    a.S = slices;
+    a.A1 = A1;
+    a.seed = seed;
+    g.direct = &a;
+    g.k16_done = P<unsigned int>(k16_done);
+    std::vector<RolloutGroup> G{g};
+    py::gil_scoped_release nogil;
+    return hybrid_rollout(G, T, threads, spin);
+  }, py::arg("group"), py::arg("weights"), py::arg("w1s"), py::arg("w2s"), py::arg("bufs"), py::arg("B"), py::arg("S"),
+     py::arg("A1"), py::arg("seed"), py::arg("k16_done"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false);
   // K21 persistent rollout server over one group: `group` = hybrid_rollout's 15 group fields (exec
   // ignored); weights = [W1, b1, W2, b2, Wd, bd, Wh, bh]; bufs = [stack, nf, rows, h2, hpart, act,
   // logp, vf, lout, act_now, ctr_t]

@@ -122,17 +122,29 @@ inline double us_since(Clock::time_point a) {
 
 std::vector<double> hybrid_rollout_phases() { return {g_phase_us[0], g_phase_us[1], g_phase_us[2]}; }
 
+void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream) {
+  // ctr_t = {rng counter, rollout row}: K10 stores row *t, K16 samples with the counter and advances both
+  nature_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, a.W1, a.w1s, a.b1, a.W2, a.w2s, a.b2, a.h2, stream);
+  dense_fwd_part(a.h2, a.Wd, a.B, 3872, 256, a.hpart, a.S, stream);
+  dense_heads_sample(nullptr, a.Wh, a.bh, a.ctr_t + 1, a.ctr_t, a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B,
+                     a.A1, stream, k16_done, a.hpart, a.S, a.bd);
+}
+
 std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<RolloutGroup>& G, int64_t T, int threads,
                                                        bool spin) {
   if (T <= 0 || G.empty()) return {};
   for (const auto& g : G)
-    if (!g.exec || !g.env.pools || !g.act || !g.new_frames || !g.rew || !g.done || !g.ep_rew || !g.ep_len)
+    if ((!g.exec && !g.direct) || (g.direct && !g.k16_done) || !g.env.pools || !g.act || !g.new_frames || !g.rew ||
+        !g.done || !g.ep_rew || !g.ep_len)
       throw std::invalid_argument("hybrid_rollout: incomplete group");
   // two events per group: with the gate, steps t and t+1 are in flight together
   std::vector<hipEvent_t> ev(2 * G.size(), nullptr);
   std::vector<std::pair<double, int64_t>> completed;
   auto launch = [&](size_t i, int64_t step) {
-    RMM_HIP_CHECK(hipGraphLaunch(G[i].exec, G[i].stream));
+    if (G[i].direct)
+      rollout_step_direct(*G[i].direct, G[i].k16_done, G[i].stream);
+    else
+      RMM_HIP_CHECK(hipGraphLaunch(G[i].exec, G[i].stream));
     RMM_HIP_CHECK(hipEventRecord(ev[2 * i + (step & 1)], G[i].stream));
   };
   auto release = [&](size_t i) {  // frames of the next step are written: open its gate

@@ -25,7 +25,14 @@ struct RolloutGroup {
   // step gate (optional): the graph starts with a device-side wait until *release passes its
   // sequence number, so step t+1 is launched BEFORE step t's env step and only released after it
   int64_t* release = nullptr;     // pinned host release counter (null: no gate)
+  // direct launches (optional): the policy step as its three kernel launches (K10 push → K13s →
+  // K16 with the step advance) from this thread instead of a graph launch; `exec` is then unused
+  const RolloutServerArgs* direct = nullptr;
+  unsigned int* k16_done = nullptr;  // K16's zero-initialised completion counter (advances t / ctr)
 };
+
+// One policy step of `a` as direct launches on `stream` (the kernels a captured step graph holds).
+void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream);
 
 // Launch step 0 of every group, then for t < T and each group: wait for its step (poll when
 // `spin`), step its envs (actions → newest frames, rewards, dones at row t) on `threads` CPU threads,

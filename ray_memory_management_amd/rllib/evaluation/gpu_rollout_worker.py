@@ -476,8 +476,16 @@ class HybridRolloutWorker(GPURolloutWorker):
                 g.resync(gs)
             shared = all(gs is st for gs in S)
             server = self._server_args(G, S)
-            native = None if server is not None else self._native_loop(G, S)
-            if server is not None:  # K21: the whole fragment in ONE persistent kernel launch
+            direct = None if server is not None else self._direct_args(G, S)
+            native = None if (server is not None or direct is not None) else self._native_loop(G, S)
+            if direct is not None:  # the native loop, launching the step's kernels directly
+                from ray_memory_management_amd._native import require_hip
+
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
+                spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
+                self._completed.extend(require_hip().hybrid_rollout_direct(**direct, T=T, threads=max(1, th),
+                                                                          spin=spin))
+            elif server is not None:  # K21: the whole fragment in ONE persistent kernel launch
                 from ray_memory_management_amd._native import require_hip
 
                 th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
@@ -546,6 +554,28 @@ class HybridRolloutWorker(GPURolloutWorker):
         on = os.environ.get("RMM_ROLLOUT_SERVER")
         if not (on == "1" if on is not None else bool(self.config.get("rollout_server", False))):
             return None
+        return self._kernel_args(G, S)
+
+    def _direct_args(self, G, S):
+        """Arguments of the native loop with DIRECT kernel launches per policy step (K10 push → K13s →
+        K16, rollout_loop.cc:rollout_step_direct) instead of a HIP-graph launch; same conditions as
+        the server. Default on (RMM_ROLLOUT_DIRECT=0 or config rollout_direct=False: graph launches):
+        a 3-kernel graph launch cost more host time than the three launches, 48-49 -> 43-44 µs per
+        50-env step, runtime bench 351k -> 370k samples/s (profiles/rollout_direct_r4.txt)."""
+        if os.environ.get("RMM_NO_NATIVE_ROLLOUT") or os.environ.get("RMM_ROLLOUT_SPIN", "0") != "0":
+            return None
+        on = os.environ.get("RMM_ROLLOUT_DIRECT")
+        if not (on == "1" if on is not None else bool(self.config.get("rollout_direct", True))):
+            return None
+        k = self._kernel_args(G, S)
+        if k is None or G[0].k16_done is None:
+            return None
+        return dict(group=k["group"], weights=k["weights"], w1s=k["w1s"], w2s=k["w2s"], bufs=k["bufs"][:11],
+                    B=k["B"], S=k["S"], A1=k["A1"], seed=k["seed"], k16_done=G[0].k16_done.data_ptr())
+
+    def _kernel_args(self, G, S):
+        """Weights / buffers / strides of the fused rollout step for one native env group (shared by
+        the K21 server and the direct-launch loop), or None when the group does not qualify."""
         cached = getattr(self, "_server_cache", None)
         if cached is not None:
             return cached

@@ -466,3 +466,29 @@ def test_ppo_hybrid_shared_weights(cuda, monkeypatch):
         algo.stop()
     finally:
         ray.shutdown()
+
+
+@pytest.mark.parametrize("n_envs,T", [(6, 12), (50, 20)])
+def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T):
+    """The native loop with direct kernel launches per policy step (RMM_ROLLOUT_DIRECT=1: K10 push →
+    K13s → K16 launched from the loop's thread, no graph) yields the same fragments, bit for bit, and
+    the same finished episodes as the per-step graph launches."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": n_envs,
+           "rollout_fragment_length": T, "seed": 3}
+    monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "1")
+    a = HybridRolloutWorker(config=cfg)
+    fa = [a.sample() for _ in range(3)]
+    assert getattr(a, "_server_cache", None) is not None  # the direct path's argument cache
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "0")
+    b = HybridRolloutWorker(config=cfg)
+    fb = [b.sample() for _ in range(3)]
+    assert getattr(b, "_server_cache", None) is None and b._native_desc is not None
+    for x, y in zip(fa, fb):
+        for k in ("obs", "_raw", "_boot"):
+            assert torch.equal(x[k], y[k]), k
+    assert len(a._completed) > 0 and a._completed == b._completed
