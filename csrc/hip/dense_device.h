@@ -143,6 +143,12 @@ __device__ __forceinline__ void load_hidden4(const unsigned short* __restrict__ 
 
 // one env row of K16 (one wave): head GEMV + bias, bf16 rounding, Gumbel-max draw, row stores
 template <int A1>
+__device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const float* whs, const float* bhs,
+                                                     const int64_t t, const uint32_t c, uint32_t seed,
+                                                     int64_t* __restrict__ act, float* __restrict__ logp,
+                                                     float* __restrict__ vf, float* __restrict__ lout,
+                                                     int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane);
+template <int A1>
 __device__ __forceinline__ void heads_sample_row(const unsigned short* __restrict__ hid, const float* whs,
                                                  const float* bhs, const int64_t t, const uint32_t c, uint32_t seed,
                                                  int64_t* __restrict__ act, float* __restrict__ logp,
@@ -150,10 +156,21 @@ __device__ __forceinline__ void heads_sample_row(const unsigned short* __restric
                                                  int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane,
                                                  const float* __restrict__ hpart, int S,
                                                  const unsigned short* __restrict__ hb) {
-  constexpr int A = A1 - 1;
   float hv[4];
   uint2 hbits;
   load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
+  heads_sample_row_pre<A1>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
+}
+
+// heads_sample_row with this lane's 4 hidden values already loaded (load_hidden4): kernels issue those
+// loads before staging Wh into LDS, so the partial-sum round trip overlaps the staging
+template <int A1>
+__device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const float* whs, const float* bhs,
+                                                     const int64_t t, const uint32_t c, uint32_t seed,
+                                                     int64_t* __restrict__ act, float* __restrict__ logp,
+                                                     float* __restrict__ vf, float* __restrict__ lout,
+                                                     int64_t* __restrict__ act_now, int64_t B, int64_t b, int lane) {
+  constexpr int A = A1 - 1;
   const float h0 = hv[0], h1 = hv[1], h2 = hv[2], h3 = hv[3];
   float hd[A1];
 #pragma unroll

@@ -979,13 +979,18 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
                                                       const unsigned short* __restrict__ hb) {
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
+  const int lane = threadIdx.x & 63;
+  const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // the row's hidden partials and the step counters load first: their round trips overlap the Wh staging
+  float hv[4] = {0.f, 0.f, 0.f, 0.f};
+  uint2 hbits;
+  if (b < B) load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);  // wave-uniform
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
   for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
   if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (b < B) heads_sample_row<A1>(hid, whs, bhs, *t_ptr, uint32_t(*ctr), seed, act, logp, vf, lout, act_now, B, b,
-                                  lane, hpart, S, hb);  // wave-uniform
+  if (b < B) heads_sample_row_pre<A1>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
   if (done) {
     __shared__ unsigned int last;
     __syncthreads();
@@ -1018,14 +1023,20 @@ __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __
                                                         const unsigned short* __restrict__ hb) {
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
+  const int lane = threadIdx.x & 63;
+  const int64_t b0 = threadIdx.x >> 6;
+  float hv[4] = {0.f, 0.f, 0.f, 0.f};
+  uint2 hbits;
+  if (b0 < B) load_hidden4(hid, hpart, S, hb, B, b0, lane, hv, hbits);  // overlaps the Wh staging
   for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
   if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
   const int64_t t = *t_ptr;
   const uint32_t c = uint32_t(*ctr);
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  for (int64_t b = threadIdx.x >> 6; b < B; b += blockDim.x >> 6)  // wave-uniform
-    heads_sample_row<A1>(hid, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane, hpart, S, hb);
+  for (int64_t b = b0; b < B; b += blockDim.x >> 6) {  // wave-uniform
+    if (b != b0) load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
+    heads_sample_row_pre<A1>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
+  }
   __syncthreads();  // every wave has read t / ctr
   if (threadIdx.x == 0) {
     *t_ptr = t + 1;

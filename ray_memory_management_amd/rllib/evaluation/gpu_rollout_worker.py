@@ -567,6 +567,8 @@ class HybridRolloutWorker(GPURolloutWorker):
         on = os.environ.get("RMM_ROLLOUT_DIRECT")
         if not (on == "1" if on is not None else bool(self.config.get("rollout_direct", True))):
             return None
+        if any(g.gate for g in G):  # the step gate lives in the captured graph
+            return None
         k = self._kernel_args(G, S)
         if k is None or G[0].k16_done is None:
             return None

@@ -351,6 +351,7 @@ def test_native_rollout_loop_matches_python_loop(cuda, double_buffer, monkeypatc
     cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": 6,
            "rollout_fragment_length": 12, "seed": 3, "rollout_double_buffer": double_buffer}
     monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "0")  # the graph-launch loop (direct launches: their own test)
     a = HybridRolloutWorker(config=cfg)
     fa = [a.sample() for _ in range(3)]
     assert a._native_desc is not None and len(a._native_desc) == (2 if double_buffer else 1)
@@ -376,6 +377,7 @@ def test_rollout_server_matches_graph_loop(cuda, monkeypatch, n_envs, T):
     cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": n_envs,
            "rollout_fragment_length": T, "seed": 3}
     monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "0")  # reference side: the per-step graph-launch loop
     monkeypatch.setenv("RMM_ROLLOUT_SERVER", "1")
     a = HybridRolloutWorker(config=cfg)
     fa = [a.sample() for _ in range(3)]
