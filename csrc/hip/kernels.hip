@@ -19,6 +19,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace rmm {
@@ -37,6 +38,10 @@ struct SegTable {
   int nseg;
 };
 
+// U independent 16 B loads in flight per lane, then U nontemporal stores; NTL: nontemporal loads too
+// (the source is read once: keep it out of the L2 / MALL). RMM_COPY_VARIANT picks (U, NTL):
+// 0 = (4, no) (round-3 default), 1 = (8, yes), 2 = (4, yes), 3 = (8, no).
+template <int U, bool NTL>
 __device__ __forceinline__ void copy_range(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                            uint64_t n) {
   const int tid = threadIdx.x;
@@ -49,15 +54,14 @@ __device__ __forceinline__ void copy_range(const uint8_t* __restrict__ src, uint
     const u32x4* vs = reinterpret_cast<const u32x4*>(src + head);
     u32x4* vd = reinterpret_cast<u32x4*>(dst + head);
     uint64_t nv = (n - head) >> 4;
-    // 4 independent 16 B loads in flight per lane
     uint64_t i = tid;
     const uint64_t step = kCopyThreads;
-    for (; i + 3 * step < nv; i += 4 * step) {
-      u32x4 a = vs[i], b = vs[i + step], c = vs[i + 2 * step], e = vs[i + 3 * step];
-      __builtin_nontemporal_store(a, vd + i);
-      __builtin_nontemporal_store(b, vd + i + step);
-      __builtin_nontemporal_store(c, vd + i + 2 * step);
-      __builtin_nontemporal_store(e, vd + i + 3 * step);
+    for (; i + (U - 1) * step < nv; i += U * step) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = NTL ? __builtin_nontemporal_load(vs + i + u * step) : vs[i + u * step];
+#pragma unroll
+      for (int u = 0; u < U; u++) __builtin_nontemporal_store(v[u], vd + i + u * step);
     }
     for (; i < nv; i += step) __builtin_nontemporal_store(vs[i], vd + i);
     uint64_t tail0 = head + (nv << 4);
@@ -76,6 +80,7 @@ __device__ __forceinline__ void copy_range(const uint8_t* __restrict__ src, uint
   }
 }
 
+template <int U, bool NTL>
 __global__ __launch_bounds__(kCopyThreads) void k_multi_copy(SegTable tab) {
   const uint64_t chunk = blockIdx.x;
   // wave-uniform binary search for the owning segment
@@ -90,7 +95,7 @@ __global__ __launch_bounds__(kCopyThreads) void k_multi_copy(SegTable tab) {
   if (off >= sg.nbytes) return;
   uint64_t n = sg.nbytes - off;
   if (n > kChunk) n = kChunk;
-  copy_range(reinterpret_cast<const uint8_t*>(sg.src) + off, reinterpret_cast<uint8_t*>(sg.dst) + off, n);
+  copy_range<U, NTL>(reinterpret_cast<const uint8_t*>(sg.src) + off, reinterpret_cast<uint8_t*>(sg.dst) + off, n);
 }
 
 void multi_copy(const std::vector<CopySeg>& segs, hipStream_t stream) {
@@ -111,7 +116,17 @@ void multi_copy(const std::vector<CopySeg>& segs, hipStream_t stream) {
     tab.nseg = k;
     if (k == 0 || chunks == 0) continue;
     // grid is bounded by 2^31-1 blocks; 256 KiB chunks => > 500 TB per launch.
-    hipLaunchKernelGGL(k_multi_copy, dim3(uint32_t(chunks)), dim3(kCopyThreads), 0, stream, tab);
+    static const int variant = [] {
+      const char* e = getenv("RMM_COPY_VARIANT");
+      return e ? atoi(e) : 0;
+    }();
+    const dim3 grid(uint32_t(chunks)), block(kCopyThreads);
+    switch (variant) {
+      case 1: hipLaunchKernelGGL((k_multi_copy<8, true>), grid, block, 0, stream, tab); break;
+      case 2: hipLaunchKernelGGL((k_multi_copy<4, true>), grid, block, 0, stream, tab); break;
+      case 3: hipLaunchKernelGGL((k_multi_copy<8, false>), grid, block, 0, stream, tab); break;
+      default: hipLaunchKernelGGL((k_multi_copy<4, false>), grid, block, 0, stream, tab); break;
+    }
     RMM_HIP_CHECK(hipGetLastError());
   }
 }
