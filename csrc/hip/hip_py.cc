@@ -341,6 +341,10 @@ PYBIND11_MODULE(_hip, m) {
     return hybrid_rollout(G, T, threads, spin);
   }, py::arg("groups"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false);
   m.def("hybrid_rollout_phases", &hybrid_rollout_phases);
+  m.def("launch_overhead_probe", [](int n, uint64_t stream) {
+    py::gil_scoped_release nogil;
+    return launch_overhead_probe(n, S(stream));
+  }, py::arg("n"), py::arg("stream"));
   // the native loop over ONE group with direct kernel launches per step (no graph): `group` =
   // hybrid_rollout's 15 fields (exec ignored), weights / strides / bufs as hybrid_rollout_server,
   // k16_done = K16's zero-initialised completion counter

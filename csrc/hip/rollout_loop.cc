@@ -122,6 +122,36 @@ inline double us_since(Clock::time_point a) {
 
 std::vector<double> hybrid_rollout_phases() { return {g_phase_us[0], g_phase_us[1], g_phase_us[2]}; }
 
+namespace {
+__global__ void k_launch_probe(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1;
+}
+}  // namespace
+
+std::vector<double> launch_overhead_probe(int n, hipStream_t stream) {
+  // host µs per {empty kernel launch, hipEventRecord, rollout-step-sized kernel argument block launch}
+  hipEvent_t e;
+  RMM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  std::vector<double> out;
+  auto t0 = Clock::now();
+  for (int i = 0; i < n; i++) hipLaunchKernelGGL(k_launch_probe, dim3(1), dim3(64), 0, stream, nullptr);
+  out.push_back(us_since(t0) / n);
+  RMM_HIP_CHECK(hipStreamSynchronize(stream));
+  t0 = Clock::now();
+  for (int i = 0; i < n; i++) RMM_HIP_CHECK(hipEventRecord(e, stream));
+  out.push_back(us_since(t0) / n);
+  RMM_HIP_CHECK(hipStreamSynchronize(stream));
+  t0 = Clock::now();
+  for (int i = 0; i < n; i++) {
+    hipLaunchKernelGGL(k_launch_probe, dim3(200), dim3(512), 0, stream, nullptr);
+    RMM_HIP_CHECK(hipGetLastError());
+  }
+  out.push_back(us_since(t0) / n);
+  RMM_HIP_CHECK(hipStreamSynchronize(stream));
+  RMM_HIP_CHECK(hipEventDestroy(e));
+  return out;
+}
+
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream) {
   // ctr_t = {rng counter, rollout row}: K10 stores row *t, K16 samples with the counter and advances both
   nature_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, a.W1, a.w1s, a.b1, a.W2, a.w2s, a.b2, a.h2, stream);

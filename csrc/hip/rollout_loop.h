@@ -31,6 +31,8 @@ struct RolloutGroup {
   unsigned int* k16_done = nullptr;  // K16's zero-initialised completion counter (advances t / ctr)
 };
 
+// host µs per empty-kernel launch, per hipEventRecord, per 200x512 launch + error check (n of each)
+std::vector<double> launch_overhead_probe(int n, hipStream_t stream);
 // One policy step of `a` as direct launches on `stream` (the kernels a captured step graph holds).
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream);
 
