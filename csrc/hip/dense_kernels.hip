@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
                                                       int64_t* __restrict__ act_now, int64_t B,
                                                       unsigned int* __restrict__ done,
                                                       const float* __restrict__ hpart, int S,
-                                                      const unsigned short* __restrict__ hb) {
+                                                      const unsigned short* __restrict__ hb, int64_t* host_seq) {
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
   const int lane = threadIdx.x & 63;
@@ -993,6 +993,7 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
   if (b < B) heads_sample_row_pre<A1>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
   if (done) {
     __shared__ unsigned int last;
+    if (host_seq) __threadfence_system();  // this wave's action stores to host memory, visible to the CPU
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
@@ -1005,6 +1006,9 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
       *tw += 1;
       if (cw != tw) *cw += 1;
       atomicExch(done, 0u);
+      // host_seq: the step's completion word in mapped host memory (the native loop polls it instead of
+      // recording and waiting on an event); every workgroup's actions were made system-visible above
+      if (host_seq) __hip_atomic_store(host_seq, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1020,7 +1024,7 @@ __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __
                                                         float* __restrict__ logp, float* __restrict__ vf,
                                                         float* __restrict__ lout, int64_t* __restrict__ act_now,
                                                         int64_t B, const float* __restrict__ hpart, int S,
-                                                        const unsigned short* __restrict__ hb) {
+                                                        const unsigned short* __restrict__ hb, int64_t* host_seq) {
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
   const int lane = threadIdx.x & 63;
@@ -1037,10 +1041,12 @@ __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __
     if (b != b0) load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
     heads_sample_row_pre<A1>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
   }
+  if (host_seq) __threadfence_system();  // this wave's action stores to host memory, visible to the CPU
   __syncthreads();  // every wave has read t / ctr
   if (threadIdx.x == 0) {
     *t_ptr = t + 1;
     if (ctr != t_ptr) *ctr = int64_t(c) + 1;
+    if (host_seq) __hip_atomic_store(host_seq, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 // K12 row-split workspace (partials), one per (device, groups, rs),
@@ -1112,8 +1118,10 @@ void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const f
 
 void dense_heads_sample(const void* hidden, const void* wh, const void* bh, const int64_t* t_ptr, const int64_t* ctr,
                         uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B,
-                        int A1, hipStream_t stream, unsigned int* done, const float* hpart, int S, const void* hb) {
+                        int A1, hipStream_t stream, unsigned int* done, const float* hpart, int S, const void* hb,
+                        int64_t* host_seq) {
   if (B <= 0) return;
+  if (host_seq != nullptr && done == nullptr) throw std::invalid_argument("dense_heads_sample: host_seq needs done");
   if (hpart != nullptr && (S < 1 || hb == nullptr)) throw std::invalid_argument("dense_heads_sample: partials need S >= 1 and the dense bias");
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_sample: 2 <= A <= 15 actions");
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
@@ -1127,7 +1135,7 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
 #define RMM_K16S(N)                                                                                            \
   case N:                                                                                                      \
     hipLaunchKernelGGL(dense::k_heads_sample1<N>, dim3(1), dim3(1024), 0, stream, U(hidden), U(wh), U(bh), tw, cw, \
-                       seed, act, logp, vf, lout, act_now, B, hpart, S, U(hb));                                \
+                       seed, act, logp, vf, lout, act_now, B, hpart, S, U(hb), host_seq);                      \
     break;
     switch (A1) {
       RMM_K16S(3) RMM_K16S(4) RMM_K16S(5) RMM_K16S(6) RMM_K16S(7) RMM_K16S(8) RMM_K16S(9)
@@ -1141,7 +1149,7 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
 #define RMM_K16(N)                                                                                          \
   case N:                                                                                                   \
     hipLaunchKernelGGL(dense::k_heads_sample<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), t_ptr, ctr, \
-                       seed, act, logp, vf, lout, act_now, B, done, hpart, S, U(hb));                       \
+                       seed, act, logp, vf, lout, act_now, B, done, hpart, S, U(hb), host_seq);             \
     break;
   switch (A1) {
     RMM_K16(3) RMM_K16(4) RMM_K16(5) RMM_K16(6) RMM_K16(7) RMM_K16(8) RMM_K16(9)

@@ -351,7 +351,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hybrid_rollout_direct", [](const std::vector<uint64_t>& v, const std::vector<uint64_t>& wts,
                                     std::vector<int64_t> w1s, std::vector<int64_t> w2s,
                                     const std::vector<uint64_t>& bufs, int64_t B, int slices, int A1, uint32_t seed,
-                                    uint64_t k16_done, int64_t T, int threads, bool spin) {
+                                    uint64_t k16_done, int64_t T, int threads, bool spin, uint64_t host_seq,
+                                    uint64_t host_seq_dev) {
     if (v.size() < 15 || wts.size() != 8 || bufs.size() < 11 || w1s.size() != 4 || w2s.size() != 4 || !k16_done)
       throw std::invalid_argument("hybrid_rollout_direct: 15 group fields, 8 weights, 11 buffers, 4+4 strides, done");
     RolloutGroup g;
@@ -397,11 +398,16 @@ PYBIND11_MODULE(_hip, m) {
     a.seed = seed;
     g.direct = &a;
     g.k16_done = P<unsigned int>(k16_done);
+    if ((host_seq == 0) != (host_seq_dev == 0))
+      throw std::invalid_argument("hybrid_rollout_direct: host_seq needs its device view and vice versa");
+    g.host_seq = host_seq ? P<int64_t>(host_seq) : nullptr;
+    g.host_seq_dev = host_seq_dev ? P<int64_t>(host_seq_dev) : nullptr;
     std::vector<RolloutGroup> G{g};
     py::gil_scoped_release nogil;
     return hybrid_rollout(G, T, threads, spin);
   }, py::arg("group"), py::arg("weights"), py::arg("w1s"), py::arg("w2s"), py::arg("bufs"), py::arg("B"), py::arg("S"),
-     py::arg("A1"), py::arg("seed"), py::arg("k16_done"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false);
+     py::arg("A1"), py::arg("seed"), py::arg("k16_done"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false,
+     py::arg("host_seq") = 0, py::arg("host_seq_dev") = 0);
   // K21 persistent rollout server over one group: `group` = hybrid_rollout's 15 group fields (exec
   // ignored); weights = [W1, b1, W2, b2, Wd, bd, Wh, bh]; bufs = [stack, nf, rows, h2, hpart, act,
   // logp, vf, lout, act_now, ctr_t]

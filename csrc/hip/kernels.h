@@ -136,7 +136,7 @@ void partition_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t
 void dense_heads_sample(const void* hidden, const void* wh, const void* bh, const int64_t* t_ptr, const int64_t* ctr,
                         uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B,
                         int A1, hipStream_t stream, unsigned int* done = nullptr, const float* hpart = nullptr,
-                        int S = 0, const void* hb = nullptr);
+                        int S = 0, const void* hb = nullptr, int64_t* host_seq = nullptr);
 // K15: K14 + fused PPO loss stats + dheads + dpre (for dense_heads_bwd(dpre_ready=true))
 void dense_heads_ppo(const void* hidden, const void* wh, const void* bh, const float* cols, const float* coef,
                      float* acc, const float* gout, int64_t M, int A1, void* dz, void* dpre, hipStream_t stream,

@@ -152,13 +152,35 @@ std::vector<double> launch_overhead_probe(int n, hipStream_t stream) {
   return out;
 }
 
-void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream) {
+void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
+                         int64_t* host_seq_dev) {
   // ctr_t = {rng counter, rollout row}: K10 stores row *t, K16 samples with the counter and advances both
   nature_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, a.W1, a.w1s, a.b1, a.W2, a.w2s, a.b2, a.h2, stream);
   dense_fwd_part(a.h2, a.Wd, a.B, 3872, 256, a.hpart, a.S, stream);
   dense_heads_sample(nullptr, a.Wh, a.bh, a.ctr_t + 1, a.ctr_t, a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B,
-                     a.A1, stream, k16_done, a.hpart, a.S, a.bd);
+                     a.A1, stream, k16_done, a.hpart, a.S, a.bd, host_seq_dev);
 }
+
+namespace {
+// Poll a step's completion word (pinned host memory written by K16 with a system-scope release): the
+// CPU sees the step ~1 µs after its last store instead of after an event's interrupt + wake-up.
+// Bounded: a step that never completes (device fault, hung kernel) fails the fragment after `limit_s`.
+void wait_seq(const int64_t* seq, int64_t want, double limit_s = 10.0) {
+  if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) >= want) return;
+  const auto t0 = Clock::now();
+  for (int k = 0;; k++) {
+    for (int i = 0; i < 64; i++) {
+      if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) >= want) return;
+      cpu_relax();
+    }
+    if ((k & 63) == 63) {
+      if (std::chrono::duration<double>(Clock::now() - t0).count() > limit_s)
+        throw std::runtime_error("hybrid_rollout: a policy step did not complete (completion word timeout)");
+      std::this_thread::yield();
+    }
+  }
+}
+}  // namespace
 
 std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<RolloutGroup>& G, int64_t T, int threads,
                                                        bool spin) {
@@ -171,10 +193,12 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
   std::vector<hipEvent_t> ev(2 * G.size(), nullptr);
   std::vector<std::pair<double, int64_t>> completed;
   auto launch = [&](size_t i, int64_t step) {
-    if (G[i].direct)
-      rollout_step_direct(*G[i].direct, G[i].k16_done, G[i].stream);
-    else
+    if (G[i].direct) {
+      rollout_step_direct(*G[i].direct, G[i].k16_done, G[i].stream, G[i].host_seq_dev);
+      if (G[i].host_seq) return;  // completion comes through the host word
+    } else {
       RMM_HIP_CHECK(hipGraphLaunch(G[i].exec, G[i].stream));
+    }
     RMM_HIP_CHECK(hipEventRecord(ev[2 * i + (step & 1)], G[i].stream));
   };
   auto release = [&](size_t i) {  // frames of the next step are written: open its gate
@@ -184,6 +208,7 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
     EnvThreads pool(std::max(1, std::min(threads, 16)));
     for (auto& e : ev) RMM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (size_t i = 0; i < G.size(); i++) {
+      if (G[i].host_seq) __atomic_store_n(G[i].host_seq, int64_t(0), __ATOMIC_RELEASE);  // rows restart at 0
       launch(i, 0);
       if (G[i].release) {
         release(i);                  // step 0's frames are already staged
@@ -195,7 +220,10 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
       for (size_t i = 0; i < G.size(); i++) {  // group i's env step overlaps the other groups' policy steps
         const RolloutGroup& g = G[i];
         auto c0 = Clock::now();
-        wait_event(ev[2 * i + (t & 1)], spin);  // step t's actions are in g.act
+        if (g.host_seq)
+          wait_seq(g.host_seq, t + 1);  // step t (row t) stored its actions, then row + 1 here
+        else
+          wait_event(ev[2 * i + (t & 1)], spin);  // step t's actions are in g.act
         ph[0] += us_since(c0);
         c0 = Clock::now();
         pool.step(g, g.env.step[0]++, t);

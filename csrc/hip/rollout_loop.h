@@ -29,12 +29,18 @@ struct RolloutGroup {
   // K16 with the step advance) from this thread instead of a graph launch; `exec` is then unused
   const RolloutServerArgs* direct = nullptr;
   unsigned int* k16_done = nullptr;  // K16's zero-initialised completion counter (advances t / ctr)
+  // completion word (direct launches, optional): pinned host int64 and its device view; K16 stores
+  // row + 1 there with a system-scope release after the step's actions, and the loop polls it
+  // instead of recording / waiting on an event
+  int64_t* host_seq = nullptr;
+  int64_t* host_seq_dev = nullptr;
 };
 
 // host µs per empty-kernel launch, per hipEventRecord, per 200x512 launch + error check (n of each)
 std::vector<double> launch_overhead_probe(int n, hipStream_t stream);
 // One policy step of `a` as direct launches on `stream` (the kernels a captured step graph holds).
-void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream);
+void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
+                         int64_t* host_seq_dev = nullptr);
 
 // Launch step 0 of every group, then for t < T and each group: wait for its step (poll when
 // `spin`), step its envs (actions → newest frames, rewards, dones at row t) on `threads` CPU threads,

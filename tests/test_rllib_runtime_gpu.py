@@ -470,8 +470,9 @@ def test_ppo_hybrid_shared_weights(cuda, monkeypatch):
         ray.shutdown()
 
 
+@pytest.mark.parametrize("seq", ["0", "1"])
 @pytest.mark.parametrize("n_envs,T", [(6, 12), (50, 20)])
-def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T):
+def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T, seq):
     """The native loop with direct kernel launches per policy step (RMM_ROLLOUT_DIRECT=1: K10 push →
     K13s → K16 launched from the loop's thread, no graph) yields the same fragments, bit for bit, and
     the same finished episodes as the per-step graph launches."""
@@ -483,9 +484,12 @@ def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T):
            "rollout_fragment_length": T, "seed": 3}
     monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
     monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "1")
+    monkeypatch.setenv("RMM_ROLLOUT_SEQ", seq)  # "1": completion through K16's host word, no events
     a = HybridRolloutWorker(config=cfg)
     fa = [a.sample() for _ in range(3)]
     assert getattr(a, "_server_cache", None) is not None  # the direct path's argument cache
+    if seq == "1":
+        assert int(a._h_seq[0]) == T  # the last step (row T-1) stored T
     monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "0")
     b = HybridRolloutWorker(config=cfg)
     fb = [b.sample() for _ in range(3)]
