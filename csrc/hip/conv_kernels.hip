@@ -27,6 +27,7 @@
 
 #include "adam_device.h"
 #include "common.h"
+#include "dense_device.h"
 #include "kernels.h"
 #include "trunk_device.h"
 
@@ -565,14 +566,21 @@ __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ 
                                                       unsigned short* __restrict__ db1,
                                                       unsigned short* __restrict__ dW2, WStrides w2,
                                                       unsigned short* __restrict__ db2, const FusedAdam fa,
-                                                      const AdamTail at, int nred) {
+                                                      const AdamTail at, int nred, const DenseFinalize df, int nfin) {
   __shared__ float red[RED_SLICES][64];
-  if (int(blockIdx.x) >= nred) {  // Adam workgroups (AdamTail): K6's pass over the dense + heads range
+  if (int(blockIdx.x) >= nred + nfin) {  // Adam workgroups (AdamTail): K6's pass over the dense + heads range
     const AdamCoef ac = adam_coef(at.hp, at.step_ctr);
-    const int64_t tid = int64_t(blockIdx.x - nred) * blockDim.x + threadIdx.x;
-    const int64_t nthr = int64_t(gridDim.x - nred) * blockDim.x;
+    const int64_t tid = int64_t(blockIdx.x - nred - nfin) * blockDim.x + threadIdx.x;
+    const int64_t nthr = int64_t(gridDim.x - nred - nfin) * blockDim.x;
     adam_span<__hip_bfloat16, true, 2>(at.master, at.m1, at.m2, static_cast<const __hip_bfloat16*>(at.grad),
                                        static_cast<__hip_bfloat16*>(at.wbf16), at.grad_scale, ac, tid, nthr, at.n);
+  } else if (int(blockIdx.x) >= nred) {  // the deferred K12 row-split finalize, each element through FusedAdam
+    const int j = int(blockIdx.x) - nred;
+    const AdamCoef ac = adam_coef(fa.hp, fa.step_ctr);
+    dense::split_finalize_elem(df.part, df.rs, df.K, df.A1, static_cast<unsigned short*>(df.dw),
+                               static_cast<unsigned short*>(df.db), static_cast<unsigned short*>(df.dwh),
+                               static_cast<unsigned short*>(df.dbh), j / dense::kK12PSlots, j % dense::kK12PSlots,
+                               fa, ac);
   } else {
     trunk_reduce_block(partial, G, dW1, w1, db1, dW2, w2, db2, fa, red);
   }
@@ -640,7 +648,8 @@ int64_t nature_trunk_partial_floats(int64_t B) { return int64_t(nature_trunk_bwd
 void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B,
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
-                      hipStream_t stream, int dbg, const FusedAdam& fa, const AdamTail& at) {
+                      hipStream_t stream, int dbg, const FusedAdam& fa, const AdamTail& at,
+                      const DenseFinalize& df) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
   if (at.master) {
@@ -649,18 +658,25 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
         !fa.grad_base || !at.hp || !at.step_ctr || (at.bump_next && (!at.bump || at.nbump <= 0)))
       throw std::invalid_argument("nature_trunk_bwd: Adam tail needs aligned buffers, the trunk FusedAdam and counters");
   }
+  if (at.bump_next && (!at.bump || at.nbump <= 0))
+    throw std::invalid_argument("nature_trunk_bwd: parity counters need bump / nbump");
   const int G = nature_trunk_bwd_groups(B);
   hipLaunchKernelGGL(trunk::k_trunk_bwd, dim3(uint32_t(G)), dim3(trunk::NTB), 0, stream, obs, idx, ctr, period, B,
                      static_cast<const unsigned short*>(W2), ws(w2s), static_cast<const unsigned short*>(h1),
                      static_cast<const unsigned short*>(h2), static_cast<const unsigned short*>(dh2), partial, dbg);
   RMM_HIP_CHECK(hipGetLastError());
   if (dbg & 128) return;  // profiling: the backward kernel alone
+  if (df.part && (!fa.grad_base || df.rs < 1 || df.groups < 1 || !df.dw || !df.db || !df.dwh || !df.dbh))
+    throw std::invalid_argument("nature_trunk_bwd: the deferred K12 finalize needs FusedAdam and all four gradients");
   const int nred = (trunk::PART + 63) / 64, NTR = 64 * trunk::RED_SLICES;
+  static_assert(64 * trunk::RED_SLICES == dense::kK12NT, "finalize workgroups are K12-sized");
+  const int nfin = df.part ? df.groups * dense::kK12PSlots : 0;
   // Adam workgroups: two groups of 4 elements per lane (K6's default unroll)
   const int nadam = at.master ? int(std::max<int64_t>(1, ((at.n + 3) / 4 + 2 * NTR - 1) / (2 * NTR))) : 0;
-  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3(nred + nadam), dim3(NTR), 0, stream, partial, G,
+  hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3(nred + nfin + nadam), dim3(NTR), 0, stream, partial, G,
                      static_cast<unsigned short*>(dW1), ws(w1s), static_cast<unsigned short*>(db1),
-                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2), fa, at, nred);
+                     static_cast<unsigned short*>(dW2), ws(w2s), static_cast<unsigned short*>(db2), fa, at, nred, df,
+                     nfin);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

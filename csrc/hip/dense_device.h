@@ -231,6 +231,46 @@ __device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const
   }
 }
 
+// One gradient element of the K12 row split's deferred finalize: (group, slot, lane-of-K12) → the
+// element's destination in dW / db / dWh / dbh; sums the rs member partials (workspace
+// [groups][rs][kK12PSlots][kK12NT]). Used by k_dense_split_finalize and by the finalize-Adam
+// workgroups of the K10 trunk-reduce launch.
+constexpr int kK12JB = 32, kK12NT = 512, kK12PSlots = 20;
+__device__ __forceinline__ void split_finalize_elem(const float* __restrict__ part, int rs, int64_t K, int A1,
+                                                    unsigned short* dw, unsigned short* db, unsigned short* dwh,
+                                                    unsigned short* dbh, int group, int slot, const FusedAdam& fa,
+                                                    const AdamCoef& ac) {
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const bool head = int64_t(group) * kK12JB == K;
+  if (!head && slot >= 16) return;
+  unsigned short* dst = nullptr;
+  if (!head) {  // slot = (hi * 2 + jt) * 4 + i  →  dW[16 (wave + 8 hi) + 4 g + i][J0 + 16 jt + r]
+    const int hi = slot >> 3, jt = (slot >> 2) & 1, i = slot & 3;
+    dst = &dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + int64_t(group) * kK12JB + 16 * jt + r];
+  } else {
+    const int i = slot & 3, q = slot >> 2;  // q: 0,1 dWh (hi), 2,3 db (hi), 4 dbh
+    if (q < 2) {
+      if (4 * g + i < A1) dst = &dwh[(4 * g + i) * H + 16 * (wave + 8 * q) + r];
+    } else if (q < 4) {
+      if (g == 0 && i == 0) dst = &db[16 * (wave + 8 * (q - 2)) + r];
+    } else if (wave == 0 && r == 0 && 4 * g + i < A1) {
+      dst = &dbh[4 * g + i];
+    }
+  }
+  if (dst == nullptr) return;
+  float t = 0.f;
+  for (int h = 0; h < rs; h++) t += part[((int64_t(group) * rs + h) * kK12PSlots + slot) * kK12NT + tid];
+  // the members' partials in member order (deterministic), rounded to bf16: stored, or (FusedAdam)
+  // applied to the parameter — bit-identical to storing and running K6 on the bf16 gradient
+  if (fa.grad_base) {
+    grad_store(fa, ac, dst, t);
+  } else {
+    *dst = f2bf(t);
+  }
+}
+
 }  // namespace dense
 }  // namespace hip
 }  // namespace rmm

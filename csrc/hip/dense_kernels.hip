@@ -366,6 +366,7 @@ static_assert((K12_LDS_DM + K12_RB) * 2 <= 160 * 1024, "K12 LDS");
 // order (deterministic) into the gradients. A last-arriver combine inside K12 measured 2x SLOWER:
 // each workgroup's agent-scope release fence wrote back its XCD's whole L2 (dx included).
 constexpr int K12_PSLOTS = 20;  // partial floats per lane (head role: 8 dWh + 8 db + 4 dbh)
+static_assert(K12_PSLOTS == kK12PSlots && JB == kK12JB && NT == kK12NT, "split_finalize_elem layout");
 struct RowSplit {
   float* part = nullptr;  // [groups][rs][K12_PSLOTS][NT]
   int rs = 1, h = 0, group = 0;
@@ -381,28 +382,7 @@ __global__ __launch_bounds__(NT) void k_dense_split_finalize(const float* __rest
                                                              unsigned short* __restrict__ db,
                                                              unsigned short* __restrict__ dwh,
                                                              unsigned short* __restrict__ dbh) {
-  const int group = blockIdx.x, slot = blockIdx.y, tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const bool head = int64_t(group) * JB == K;
-  if (!head && slot >= 16) return;
-  unsigned short* dst = nullptr;
-  if (!head) {  // slot = (hi * 2 + jt) * 4 + i  →  dW[16 (wave + 8 hi) + 4 g + i][J0 + 16 jt + r]
-    const int hi = slot >> 3, jt = (slot >> 2) & 1, i = slot & 3;
-    dst = &dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + int64_t(group) * JB + 16 * jt + r];
-  } else {
-    const int i = slot & 3, q = slot >> 2;  // q: 0,1 dWh (hi), 2,3 db (hi), 4 dbh
-    if (q < 2) {
-      if (4 * g + i < A1) dst = &dwh[(4 * g + i) * H + 16 * (wave + 8 * q) + r];
-    } else if (q < 4) {
-      if (g == 0 && i == 0) dst = &db[16 * (wave + 8 * (q - 2)) + r];
-    } else if (wave == 0 && r == 0 && 4 * g + i < A1) {
-      dst = &dbh[4 * g + i];
-    }
-  }
-  if (dst == nullptr) return;
-  float t = 0.f;
-  for (int h = 0; h < rs; h++) t += part[((int64_t(group) * rs + h) * K12_PSLOTS + slot) * NT + tid];
-  *dst = f2bf(t);
+  split_finalize_elem(part, rs, K, A1, dw, db, dwh, dbh, blockIdx.x, blockIdx.y, FusedAdam{}, AdamCoef{});
 }
 
 // column-block role: dx[:, J] and dW[:, J] for J = [J0, J0+32)
@@ -1235,9 +1215,22 @@ void dense_fwd_part(const void* x, const void* w, int64_t M, int64_t K, int N, f
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+DenseSplitPlan dense_split_plan(int64_t M, int64_t K, hipStream_t stream) {
+  static const int split_env = [] {
+    const char* e = std::getenv("RMM_K12_SPLIT");
+    return e ? std::atoi(e) : 1;
+  }();
+  DenseSplitPlan p;
+  const int nc = int((M + dense::MC2 - 1) / dense::MC2);
+  p.rs = std::max(1, std::min(split_env, nc));
+  p.groups = int(K / dense::JB + 1);
+  if (p.rs > 1) dense::k12_split_ws(p.groups, p.rs, stream, &p.part);
+  return p;
+}
+
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
-                     hipStream_t stream, bool dpre_ready, const FusedAdam& fa) {
+                     hipStream_t stream, bool dpre_ready, const FusedAdam& fa, bool defer_finalize) {
   if (M <= 0) return;
   if (K % dense::JB != 0) throw std::invalid_argument("dense_heads_bwd: K must be a multiple of 32");
   if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_bwd: 1 <= A+1 <= 16");
@@ -1281,7 +1274,7 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   }
 #undef RMM_K12
   RMM_HIP_CHECK(hipGetLastError());
-  if (rs > 1) {
+  if (rs > 1 && !defer_finalize) {  // deferred: the K10 trunk-reduce launch finalizes (+ Adam)
     hipLaunchKernelGGL(dense::k_dense_split_finalize, dim3(uint32_t(groups), uint32_t(dense::K12_PSLOTS)), block, 0,
                        stream, rs_part, rs, K, A1, V(dw), V(db), V(dwh), V(dbh));
     RMM_HIP_CHECK(hipGetLastError());

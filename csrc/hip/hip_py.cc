@@ -31,9 +31,10 @@ AdamTail adam_tail(const std::vector<uint64_t>& v, float grad_scale) {
   AdamTail at;
   if (v.empty()) return at;
   if (v.size() != 11) throw std::invalid_argument("adam tail: 11 fields");
-  for (int k : {0, 1, 2, 3, 4, 6, 7})
-    if (v[k] == 0) throw std::invalid_argument("adam tail: null buffer");
-  at.master = P<float>(v[0]);
+  if (v[0])  // master == 0: counters only (no linear Adam workgroups)
+    for (int k : {0, 1, 2, 3, 4, 6, 7})
+      if (v[k] == 0) throw std::invalid_argument("adam tail: null buffer");
+  at.master = v[0] ? P<float>(v[0]) : nullptr;
   at.m1 = P<float>(v[1]);
   at.m2 = P<float>(v[2]);
   at.grad = P<const void>(v[3]);
@@ -551,13 +552,18 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("dense_heads_bwd", [](uint64_t dz, int A1, uint64_t wh, uint64_t y, uint64_t x, uint64_t w, int64_t M,
                               int64_t K, uint64_t dx, uint64_t dw, uint64_t db, uint64_t dwh, uint64_t dbh,
-                              uint64_t scratch, uint64_t stream, bool dpre_ready, std::vector<uint64_t> adam) {
+                              uint64_t scratch, uint64_t stream, bool dpre_ready, std::vector<uint64_t> adam,
+                              bool defer_finalize) {
     dense_heads_bwd(P<const void>(dz), A1, P<const void>(wh), P<const void>(y), P<const void>(x), P<const void>(w), M,
                     K, P<void>(dx), P<void>(dw), P<void>(db), P<void>(dwh), P<void>(dbh), P<void>(scratch),
-                    S(stream), dpre_ready, fused_adam(adam));
+                    S(stream), dpre_ready, fused_adam(adam), defer_finalize);
   }, py::arg("dz"), py::arg("A1"), py::arg("wh"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("M"), py::arg("K"),
      py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("dwh"), py::arg("dbh"), py::arg("scratch"), py::arg("stream"),
-     py::arg("dpre_ready") = false, py::arg("adam") = std::vector<uint64_t>{});
+     py::arg("dpre_ready") = false, py::arg("adam") = std::vector<uint64_t>{}, py::arg("defer_finalize") = false);
+  m.def("dense_split_plan", [](int64_t M, int64_t K, uint64_t stream) {
+    const DenseSplitPlan p = dense_split_plan(M, K, S(stream));
+    return py::make_tuple(reinterpret_cast<uint64_t>(p.part), p.rs, p.groups);
+  }, py::arg("M"), py::arg("K"), py::arg("stream"));
   m.def("dense_heads_sample", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t t_ptr, uint64_t ctr,
                                  uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
                                  uint64_t act_now, int64_t B, int A1, uint64_t stream, uint64_t done, uint64_t hpart,
@@ -590,17 +596,30 @@ PYBIND11_MODULE(_hip, m) {
                                std::vector<int64_t> w2s, uint64_t h1, uint64_t h2, uint64_t dh2, uint64_t partial,
                                uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
                                uint64_t stream, int dbg, std::vector<uint64_t> adam, std::vector<uint64_t> tail,
-                               float tail_scale) {
+                               float tail_scale, std::vector<uint64_t> fin) {
+    DenseFinalize df;
+    if (!fin.empty()) {  // [part, rs, groups, K, A1, dw, db, dwh, dbh]
+      if (fin.size() != 9) throw std::invalid_argument("nature_trunk_bwd: fin = 9 fields");
+      df.part = P<const float>(fin[0]);
+      df.rs = int(fin[1]);
+      df.groups = int(fin[2]);
+      df.K = int64_t(fin[3]);
+      df.A1 = int(fin[4]);
+      df.dw = P<void>(fin[5]);
+      df.db = P<void>(fin[6]);
+      df.dwh = P<void>(fin[7]);
+      df.dbh = P<void>(fin[8]);
+    }
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("nature_trunk_bwd: 4 strides per weight");
     nature_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr,
                      ctr ? P<const int64_t>(ctr) : nullptr, period, B, P<const void>(W2), w2s.data(),
                      P<const void>(h1), P<const void>(h2), P<const void>(dh2), P<float>(partial), P<void>(dW1),
                      w1s.data(), P<void>(db1), P<void>(dW2), P<void>(db2), S(stream), dbg, fused_adam(adam),
-                     adam_tail(tail, tail_scale));
+                     adam_tail(tail, tail_scale), df);
   }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W2"), py::arg("w2s"),
      py::arg("h1"), py::arg("h2"), py::arg("dh2"), py::arg("partial"), py::arg("dW1"), py::arg("w1s"), py::arg("db1"),
      py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0, py::arg("adam") = std::vector<uint64_t>{},
-     py::arg("tail") = std::vector<uint64_t>{}, py::arg("tail_scale") = 1.0f);
+     py::arg("tail") = std::vector<uint64_t>{}, py::arg("tail_scale") = 1.0f, py::arg("fin") = std::vector<uint64_t>{});
 
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {

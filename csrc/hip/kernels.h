@@ -119,7 +119,21 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
                      hipStream_t stream, bool dpre_ready = false,
-                     const FusedAdam& fa = FusedAdam{});  // dpre_scratch: M*256 bf16; fa: Adam epilogue
+                     const FusedAdam& fa = FusedAdam{}, bool defer_finalize = false);  // dpre_scratch: M*256 bf16; fa: Adam epilogue
+// K12 row split (RMM_K12_SPLIT=rs): the partial workspace [groups][rs][20][512] fp32 of a deferred finalize
+struct DenseSplitPlan {
+  float* part = nullptr;
+  int rs = 1, groups = 0;
+};
+DenseSplitPlan dense_split_plan(int64_t M, int64_t K, hipStream_t stream);
+// The deferred K12 finalize run by the K10 trunk-reduce launch (with its FusedAdam): destinations are the
+// dense / heads gradient views inside the flat bucket (so FusedAdam applies Adam to them)
+struct DenseFinalize {
+  const float* part = nullptr;  // null: none
+  int rs = 0, groups = 0, A1 = 0;
+  int64_t K = 0;
+  void *dw = nullptr, *db = nullptr, *dwh = nullptr, *dbh = nullptr;
+};
 
 // K11: shuffle partitioning. dest = splitmix64(key) % R (mode 0) or key mod R (mode 1), R <= 1024.
 // partition_hist writes counts[G][R] (G = partition_groups(n)); the caller turns them into
@@ -177,7 +191,7 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
                       const void* W2, const int64_t* w2s, const void* h1, const void* h2, const void* dh2,
                       float* partial, void* dW1, const int64_t* w1s, void* db1, void* dW2, void* db2,
                       hipStream_t stream, int dbg = 0, const FusedAdam& fa = FusedAdam{},
-                      const AdamTail& at = AdamTail{});
+                      const AdamTail& at = AdamTail{}, const DenseFinalize& df = DenseFinalize{});
 // dbg (profiling only, 0 in production): fwd bit0/1 skip conv1/conv2 MFMA, bit2 skip the frame
 // load; bwd bit0/1/2 skip the dW2 / dh1 / dW1 phases, bit3 the staging loads, bit4 the partial stores,
 // bit5 the st zeroing, bit6 return at once, bit7 the reduce launch, bit8 all LDS zeroing, bit9 the W2

@@ -371,7 +371,7 @@ class PPOLearner:
         h.dense_heads_bwd(ws["dz"].data_ptr(), A1, hd.weight.data_ptr(), ws["hidden"].data_ptr(), ws["h2"].data_ptr(),
                           dl.weight.data_ptr(), mbs, K, ws["dx"].data_ptr(), g[4].data_ptr(), g[5].data_ptr(),
                           g[6].data_ptr(), g[7].data_ptr(), ws["dpre"].data_ptr(), st, dpre_ready=True,
-                          adam=self._fused_adam_args(bump=False))
+                          adam=self._fused_adam_args(bump=False), defer_finalize=self._split_fin())
 
     def _manual_trunk_bwd(self, full):
         """K10 backward: trunk grads (conv1/conv2 weights + biases) into the bucket."""
@@ -381,11 +381,25 @@ class PPOLearner:
         g = [p._rmm_grad_out for p in self.params]
         ctr = self._ctr().data_ptr()
         adam, tail = (self._tail_adam_args() if self._tail_adam() else (self._fused_adam_args(bump=True), []))
+        fin = []
+        if self._split_fin():  # the deferred K12 finalize (+ Adam) runs in the trunk-reduce launch
+            part, rs, groups = require_hip().dense_split_plan(int(full["mbs"]), self.model.dense_tail.in_features,
+                                                             _stream())
+            fin = [part, rs, groups, self.model.dense_tail.in_features, self.model.heads.out_features,
+                   g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr()]
         h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), ctr, int(full["period"]),
                            int(full["mbs"]), c2.weight.data_ptr(), list(c2.weight.stride()), ws["h1"].data_ptr(),
                            ws["h2"].data_ptr(), ws["dx"].data_ptr(), ws["part"].data_ptr(), g[0].data_ptr(),
                            list(c1.weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
-                           adam=adam, tail=tail, tail_scale=1.0 / self.world)
+                           adam=adam, tail=tail, tail_scale=1.0 / self.world, fin=fin)
+
+    def _split_fin(self) -> bool:
+        """K12 row split (RMM_K12_SPLIT=2: twice the workgroups, half the serial row-chunk chain each)
+        with its finalize deferred into the trunk-reduce launch, where each finalized dense / heads
+        gradient element goes straight through FusedAdam: no finalize kernel boundary, and the
+        bf16-rounded sums equal the finalize kernel's, so the update is bit-identical to split K12 →
+        finalize → K6. Needs tail Adam (world of one, no clip)."""
+        return self._tail_adam() and int(os.environ.get("RMM_K12_SPLIT", "1")) > 1
 
     def _tail_adam(self) -> bool:
         """World of one without a global-norm clip: K6 folds into the K10 trunk-reduce LAUNCH — the
@@ -410,9 +424,13 @@ class PPOLearner:
         adam = [self.flat_grad.data_ptr(), self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(),
                 self._wptr(), self.hp.data_ptr(), cur + 8, 0 if parity else cur, 0 if parity else 2,
                 0 if parity else self._bump_done.data_ptr()]
-        tail = [self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
-                self.flat_grad.data_ptr() + b2, self._wptr() + b2, self.n_params - lo, self.hp.data_ptr(), cur + 8,
-                cur, 2, self._ctrs[1 - self._par].data_ptr() if parity else 0]
+        nxt = self._ctrs[1 - self._par].data_ptr() if parity else 0
+        if self._split_fin():  # the dense + heads Adam runs in the finalize workgroups: counters only
+            tail = [0, 0, 0, 0, 0, 0, 0, 0, cur, 2, nxt]
+        else:
+            tail = [self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
+                    self.flat_grad.data_ptr() + b2, self._wptr() + b2, self.n_params - lo, self.hp.data_ptr(),
+                    cur + 8, cur, 2, nxt]
         if parity:
             self._par ^= 1
         return adam, tail
