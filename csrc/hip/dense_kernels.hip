@@ -1215,14 +1215,18 @@ void dense_fwd_part(const void* x, const void* w, int64_t M, int64_t K, int N, f
   RMM_HIP_CHECK(hipGetLastError());
 }
 
-DenseSplitPlan dense_split_plan(int64_t M, int64_t K, hipStream_t stream) {
-  static const int split_env = [] {
+static int k12_split_env() {
+  static const int v = [] {
     const char* e = std::getenv("RMM_K12_SPLIT");
     return e ? std::atoi(e) : 1;
   }();
+  return v;
+}
+
+DenseSplitPlan dense_split_plan(int64_t M, int64_t K, int split, hipStream_t stream) {
   DenseSplitPlan p;
   const int nc = int((M + dense::MC2 - 1) / dense::MC2);
-  p.rs = std::max(1, std::min(split_env, nc));
+  p.rs = std::max(1, std::min(split >= 1 ? split : k12_split_env(), nc));
   p.groups = int(K / dense::JB + 1);
   if (p.rs > 1) dense::k12_split_ws(p.groups, p.rs, stream, &p.part);
   return p;
@@ -1230,7 +1234,7 @@ DenseSplitPlan dense_split_plan(int64_t M, int64_t K, hipStream_t stream) {
 
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
-                     hipStream_t stream, bool dpre_ready, const FusedAdam& fa, bool defer_finalize) {
+                     hipStream_t stream, bool dpre_ready, const FusedAdam& fa, bool defer_finalize, int split) {
   if (M <= 0) return;
   if (K % dense::JB != 0) throw std::invalid_argument("dense_heads_bwd: K must be a multiple of 32");
   if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_bwd: 1 <= A+1 <= 16");
@@ -1246,13 +1250,11 @@ void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, cons
   if (fa.grad_base && fa.bump) throw std::invalid_argument("dense_heads_bwd: the step counters advance in the trunk reduce");
   const dim3 pgrid(uint32_t((M + dense::MC - 1) / dense::MC));
   auto* dp = V(dpre_scratch);
-  // K12 row split + finalize kernel (RMM_K12_SPLIT=2; plain gradients only, not the fused-Adam epilogues)
-  static const int split_env = [] {
-    const char* e = std::getenv("RMM_K12_SPLIT");
-    return e ? std::atoi(e) : 1;
-  }();
+  // K12 row split + finalize kernel (split >= 1 explicit, else RMM_K12_SPLIT; plain gradients only, not
+  // the fused-Adam epilogues). A deferred finalize must use the same `split` in dense_split_plan.
   const int nc = int((M + dense::MC2 - 1) / dense::MC2);
-  const int rs = (v2 && !fa.grad_base) ? std::max(1, std::min(split_env, nc)) : 1;
+  const int rs = (v2 && !fa.grad_base) ? std::max(1, std::min(split >= 1 ? split : k12_split_env(), nc)) : 1;
+  if (defer_finalize && rs < 2) throw std::invalid_argument("dense_heads_bwd: a deferred finalize needs the row split");
   const int groups = int(K / dense::JB + 1);
   float* rs_part = nullptr;
   if (rs > 1) dense::k12_split_ws(groups, rs, stream, &rs_part);

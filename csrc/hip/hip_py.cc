@@ -553,17 +553,17 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dense_heads_bwd", [](uint64_t dz, int A1, uint64_t wh, uint64_t y, uint64_t x, uint64_t w, int64_t M,
                               int64_t K, uint64_t dx, uint64_t dw, uint64_t db, uint64_t dwh, uint64_t dbh,
                               uint64_t scratch, uint64_t stream, bool dpre_ready, std::vector<uint64_t> adam,
-                              bool defer_finalize) {
+                              bool defer_finalize, int split) {
     dense_heads_bwd(P<const void>(dz), A1, P<const void>(wh), P<const void>(y), P<const void>(x), P<const void>(w), M,
                     K, P<void>(dx), P<void>(dw), P<void>(db), P<void>(dwh), P<void>(dbh), P<void>(scratch),
-                    S(stream), dpre_ready, fused_adam(adam), defer_finalize);
+                    S(stream), dpre_ready, fused_adam(adam), defer_finalize, split);
   }, py::arg("dz"), py::arg("A1"), py::arg("wh"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("M"), py::arg("K"),
      py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("dwh"), py::arg("dbh"), py::arg("scratch"), py::arg("stream"),
-     py::arg("dpre_ready") = false, py::arg("adam") = std::vector<uint64_t>{}, py::arg("defer_finalize") = false);
-  m.def("dense_split_plan", [](int64_t M, int64_t K, uint64_t stream) {
-    const DenseSplitPlan p = dense_split_plan(M, K, S(stream));
+     py::arg("dpre_ready") = false, py::arg("adam") = std::vector<uint64_t>{}, py::arg("defer_finalize") = false, py::arg("split") = -1);
+  m.def("dense_split_plan", [](int64_t M, int64_t K, int split, uint64_t stream) {
+    const DenseSplitPlan p = dense_split_plan(M, K, split, S(stream));
     return py::make_tuple(reinterpret_cast<uint64_t>(p.part), p.rs, p.groups);
-  }, py::arg("M"), py::arg("K"), py::arg("stream"));
+  }, py::arg("M"), py::arg("K"), py::arg("split"), py::arg("stream"));
   m.def("dense_heads_sample", [](uint64_t hidden, uint64_t wh, uint64_t bh, uint64_t t_ptr, uint64_t ctr,
                                  uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout,
                                  uint64_t act_now, int64_t B, int A1, uint64_t stream, uint64_t done, uint64_t hpart,

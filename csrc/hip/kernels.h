@@ -119,13 +119,13 @@ void mask_colsum(const void* dy, const void* y, void* dpre, void* db, int64_t M,
 void dense_heads_bwd(const void* dz, int A1, const void* wh, const void* y, const void* x, const void* w, int64_t M,
                      int64_t K, void* dx, void* dw, void* db, void* dwh, void* dbh, void* dpre_scratch,
                      hipStream_t stream, bool dpre_ready = false,
-                     const FusedAdam& fa = FusedAdam{}, bool defer_finalize = false);  // dpre_scratch: M*256 bf16; fa: Adam epilogue
+                     const FusedAdam& fa = FusedAdam{}, bool defer_finalize = false, int split = -1);  // dpre_scratch: M*256 bf16; fa: Adam epilogue
 // K12 row split (RMM_K12_SPLIT=rs): the partial workspace [groups][rs][20][512] fp32 of a deferred finalize
 struct DenseSplitPlan {
   float* part = nullptr;
   int rs = 1, groups = 0;
 };
-DenseSplitPlan dense_split_plan(int64_t M, int64_t K, hipStream_t stream);
+DenseSplitPlan dense_split_plan(int64_t M, int64_t K, int split, hipStream_t stream);
 // The deferred K12 finalize run by the K10 trunk-reduce launch (with its FusedAdam): destinations are the
 // dense / heads gradient views inside the flat bucket (so FusedAdam applies Adam to them)
 struct DenseFinalize {

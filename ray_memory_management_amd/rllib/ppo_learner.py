@@ -371,7 +371,8 @@ class PPOLearner:
         h.dense_heads_bwd(ws["dz"].data_ptr(), A1, hd.weight.data_ptr(), ws["hidden"].data_ptr(), ws["h2"].data_ptr(),
                           dl.weight.data_ptr(), mbs, K, ws["dx"].data_ptr(), g[4].data_ptr(), g[5].data_ptr(),
                           g[6].data_ptr(), g[7].data_ptr(), ws["dpre"].data_ptr(), st, dpre_ready=True,
-                          adam=self._fused_adam_args(bump=False), defer_finalize=self._split_fin())
+                          adam=self._fused_adam_args(bump=False), defer_finalize=self._split_fin(),
+                          split=self._k12_split(mbs))
 
     def _manual_trunk_bwd(self, full):
         """K10 backward: trunk grads (conv1/conv2 weights + biases) into the bucket."""
@@ -384,7 +385,7 @@ class PPOLearner:
         fin = []
         if self._split_fin():  # the deferred K12 finalize (+ Adam) runs in the trunk-reduce launch
             part, rs, groups = require_hip().dense_split_plan(int(full["mbs"]), self.model.dense_tail.in_features,
-                                                             _stream())
+                                                             self._k12_split(int(full["mbs"])), _stream())
             fin = [part, rs, groups, self.model.dense_tail.in_features, self.model.heads.out_features,
                    g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr()]
         h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), ctr, int(full["period"]),
@@ -393,13 +394,19 @@ class PPOLearner:
                            list(c1.weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
                            adam=adam, tail=tail, tail_scale=1.0 / self.world, fin=fin)
 
+    def _k12_split(self, mbs: int) -> int:
+        """K12 row-split factor (RMM_K12_SPLIT, read per call so K12 and a deferred finalize agree),
+        capped by the minibatch's 64-row chunks."""
+        return max(1, min(int(os.environ.get("RMM_K12_SPLIT", "1")), (int(mbs) + 63) // 64))
+
     def _split_fin(self) -> bool:
         """K12 row split (RMM_K12_SPLIT=2: twice the workgroups, half the serial row-chunk chain each)
         with its finalize deferred into the trunk-reduce launch, where each finalized dense / heads
         gradient element goes straight through FusedAdam: no finalize kernel boundary, and the
         bf16-rounded sums equal the finalize kernel's, so the update is bit-identical to split K12 →
         finalize → K6. Needs tail Adam (world of one, no clip)."""
-        return self._tail_adam() and int(os.environ.get("RMM_K12_SPLIT", "1")) > 1
+        mbs = getattr(self, "_mws", {}).get("mbs", 0) if isinstance(getattr(self, "_mws", None), dict) else 0
+        return self._tail_adam() and self._k12_split(mbs or 640) > 1
 
     def _tail_adam(self) -> bool:
         """World of one without a global-norm clip: K6 folds into the K10 trunk-reduce LAUNCH — the
