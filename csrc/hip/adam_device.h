@@ -80,5 +80,63 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
   }
 }
 
+// adam_span's vector pass over the dense weight [256][K] of a K12 row split whose finalize was deferred:
+// each group of 4 gradients (same row m, columns k..k+3 of one 32-column K12 group) is a float4 at the
+// same place of every member's partial block; the members are summed in order and rounded to bf16
+// exactly as k_dense_split_finalize does, so the update is bit-identical to finalize -> K6.
+__device__ __forceinline__ int64_t k12_part_index(int64_t e, int64_t K, int rs, int h) {
+  const int64_t m = e / K, k = e - m * K;
+  const int64_t group = k >> 5;
+  const int c = int(k & 31), jt = c >> 4, r = c & 15;
+  const int hi = int(m >> 7), wave = int((m >> 4) & 7), g = int((m & 15) >> 2), i = int(m & 3);
+  const int slot = (hi * 2 + jt) * 4 + i, tid = wave * 64 + g * 16 + r;
+  return ((group * rs + h) * 20 + slot) * 512 + tid;
+}
+template <int U>
+__device__ __forceinline__ void adam_span_split(float* __restrict__ master, float* __restrict__ m1,
+                                                float* __restrict__ m2, const float* __restrict__ part, int rs,
+                                                int64_t K, __hip_bfloat16* __restrict__ wbf16, float grad_scale,
+                                                const AdamCoef& c, int64_t tid, int64_t nthr, int64_t n) {
+  const int64_t nv = n >> 2;  // n = 256 K, K % 32 == 0: whole groups of 4 in one 32-column K12 group
+  for (int64_t v0 = tid; v0 < nv; v0 += nthr * U) {
+    float g[U][4];
+    float4 w[U], a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t v = v0 + u * nthr;
+      if (v < nv) {
+        const int64_t i = v << 2;
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int h = 0; h < rs; h++) {
+          const float4 p = *reinterpret_cast<const float4*>(part + k12_part_index(i, K, rs, h));
+          t.x += p.x, t.y += p.y, t.z += p.z, t.w += p.w;
+        }
+        g[u][0] = __uint_as_float(uint32_t(bf16_bits_rn(t.x)) << 16);
+        g[u][1] = __uint_as_float(uint32_t(bf16_bits_rn(t.y)) << 16);
+        g[u][2] = __uint_as_float(uint32_t(bf16_bits_rn(t.z)) << 16);
+        g[u][3] = __uint_as_float(uint32_t(bf16_bits_rn(t.w)) << 16);
+        w[u] = *reinterpret_cast<const float4*>(master + i);
+        a[u] = *reinterpret_cast<const float4*>(m1 + i);
+        b[u] = *reinterpret_cast<const float4*>(m2 + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t v = v0 + u * nthr;
+      if (v < nv) {
+        const int64_t i = v << 2;
+        w[u].x = adam_one(w[u].x, g[u][0] * grad_scale, a[u].x, b[u].x, c);
+        w[u].y = adam_one(w[u].y, g[u][1] * grad_scale, a[u].y, b[u].y, c);
+        w[u].z = adam_one(w[u].z, g[u][2] * grad_scale, a[u].z, b[u].z, c);
+        w[u].w = adam_one(w[u].w, g[u][3] * grad_scale, a[u].w, b[u].w, c);
+        *reinterpret_cast<float4*>(master + i) = w[u];
+        *reinterpret_cast<float4*>(m1 + i) = a[u];
+        *reinterpret_cast<float4*>(m2 + i) = b[u];
+        *reinterpret_cast<uint2*>(wbf16 + i) = make_uint2(bf16x2_rn(w[u].x, w[u].y), bf16x2_rn(w[u].z, w[u].w));
+      }
+    }
+  }
+}
+
 }  // namespace hip
 }  // namespace rmm

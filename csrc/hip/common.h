@@ -57,6 +57,12 @@ struct AdamTail {
   int64_t* bump = nullptr;
   int nbump = 0;
   int64_t* bump_next = nullptr;
+  // K12 row split with a deferred finalize: the range is the dense weight [256][K] and each gradient
+  // is the sum of the rs fp32 member partials (workspace [groups][rs][20][512], see
+  // dense_device.h:split_finalize_elem), rounded to bf16 — read 4 consecutive elements at a time
+  const float* part = nullptr;
+  int rs = 0;
+  int64_t K = 0;
 };
 
 // XCD-aware remap of a linear workgroup id (bijective for any grid size): consecutive

@@ -572,15 +572,19 @@ __global__ __launch_bounds__(512) void k_trunk_reduce(const float* __restrict__ 
     const AdamCoef ac = adam_coef(at.hp, at.step_ctr);
     const int64_t tid = int64_t(blockIdx.x - nred - nfin) * blockDim.x + threadIdx.x;
     const int64_t nthr = int64_t(gridDim.x - nred - nfin) * blockDim.x;
-    adam_span<__hip_bfloat16, true, 2>(at.master, at.m1, at.m2, static_cast<const __hip_bfloat16*>(at.grad),
-                                       static_cast<__hip_bfloat16*>(at.wbf16), at.grad_scale, ac, tid, nthr, at.n);
+    if (at.part)  // deferred K12 finalize: gradients summed from the row-split partials
+      adam_span_split<2>(at.master, at.m1, at.m2, at.part, at.rs, at.K, static_cast<__hip_bfloat16*>(at.wbf16),
+                         at.grad_scale, ac, tid, nthr, at.n);
+    else
+      adam_span<__hip_bfloat16, true, 2>(at.master, at.m1, at.m2, static_cast<const __hip_bfloat16*>(at.grad),
+                                         static_cast<__hip_bfloat16*>(at.wbf16), at.grad_scale, ac, tid, nthr, at.n);
   } else if (int(blockIdx.x) >= nred) {  // the deferred K12 row-split finalize, each element through FusedAdam
     const int j = int(blockIdx.x) - nred;
     const AdamCoef ac = adam_coef(fa.hp, fa.step_ctr);
     dense::split_finalize_elem(df.part, df.rs, df.K, df.A1, static_cast<unsigned short*>(df.dw),
                                static_cast<unsigned short*>(df.db), static_cast<unsigned short*>(df.dwh),
-                               static_cast<unsigned short*>(df.dbh), j / dense::kK12PSlots, j % dense::kK12PSlots,
-                               fa, ac);
+                               static_cast<unsigned short*>(df.dbh), df.group0 + j / dense::kK12PSlots,
+                               j % dense::kK12PSlots, fa, ac);
   } else {
     trunk_reduce_block(partial, G, dW1, w1, db1, dW2, w2, db2, fa, red);
   }
@@ -654,7 +658,8 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
   if (period <= 0) period = 1;
   if (at.master) {
     auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
-    if (!(al(at.master, 16) && al(at.m1, 16) && al(at.m2, 16) && al(at.grad, 8) && al(at.wbf16, 8)) || at.n <= 0 ||
+    if (!(al(at.master, 16) && al(at.m1, 16) && al(at.m2, 16) && (at.part || al(at.grad, 8)) && al(at.wbf16, 8)) ||
+        at.n <= 0 || (at.part && (at.rs < 1 || at.K % 32 != 0 || at.n != 256 * at.K || !al(at.part, 16))) ||
         !fa.grad_base || !at.hp || !at.step_ctr || (at.bump_next && (!at.bump || at.nbump <= 0)))
       throw std::invalid_argument("nature_trunk_bwd: Adam tail needs aligned buffers, the trunk FusedAdam and counters");
   }
@@ -670,7 +675,7 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
     throw std::invalid_argument("nature_trunk_bwd: the deferred K12 finalize needs FusedAdam and all four gradients");
   const int nred = (trunk::PART + 63) / 64, NTR = 64 * trunk::RED_SLICES;
   static_assert(64 * trunk::RED_SLICES == dense::kK12NT, "finalize workgroups are K12-sized");
-  const int nfin = df.part ? df.groups * dense::kK12PSlots : 0;
+  const int nfin = df.part ? (df.groups - df.group0) * dense::kK12PSlots : 0;
   // Adam workgroups: two groups of 4 elements per lane (K6's default unroll)
   const int nadam = at.master ? int(std::max<int64_t>(1, ((at.n + 3) / 4 + 2 * NTR - 1) / (2 * NTR))) : 0;
   hipLaunchKernelGGL(trunk::k_trunk_reduce, dim3(nred + nfin + nadam), dim3(NTR), 0, stream, partial, G,

@@ -30,7 +30,7 @@ inline T* P(uint64_t p) {
 AdamTail adam_tail(const std::vector<uint64_t>& v, float grad_scale) {
   AdamTail at;
   if (v.empty()) return at;
-  if (v.size() != 11) throw std::invalid_argument("adam tail: 11 fields");
+  if (v.size() != 11 && v.size() != 14) throw std::invalid_argument("adam tail: 11 (+3 split) fields");
   if (v[0])  // master == 0: counters only (no linear Adam workgroups)
     for (int k : {0, 1, 2, 3, 4, 6, 7})
       if (v[k] == 0) throw std::invalid_argument("adam tail: null buffer");
@@ -46,6 +46,11 @@ AdamTail adam_tail(const std::vector<uint64_t>& v, float grad_scale) {
   at.nbump = int(v[9]);
   at.bump_next = v[10] ? P<int64_t>(v[10]) : nullptr;
   at.grad_scale = grad_scale;
+  if (v.size() == 14 && v[11]) {  // [.., part, rs, K]: gradients from the K12 row-split partials
+    at.part = P<const float>(v[11]);
+    at.rs = int(v[12]);
+    at.K = int64_t(v[13]);
+  }
   return at;
 }
 
@@ -599,7 +604,8 @@ PYBIND11_MODULE(_hip, m) {
                                float tail_scale, std::vector<uint64_t> fin) {
     DenseFinalize df;
     if (!fin.empty()) {  // [part, rs, groups, K, A1, dw, db, dwh, dbh]
-      if (fin.size() != 9) throw std::invalid_argument("nature_trunk_bwd: fin = 9 fields");
+      if (fin.size() != 9 && fin.size() != 10) throw std::invalid_argument("nature_trunk_bwd: fin = 9 (+group0) fields");
+      df.group0 = fin.size() > 9 ? int(fin[9]) : 0;
       df.part = P<const float>(fin[0]);
       df.rs = int(fin[1]);
       df.groups = int(fin[2]);

@@ -131,6 +131,8 @@ DenseSplitPlan dense_split_plan(int64_t M, int64_t K, int split, hipStream_t str
 struct DenseFinalize {
   const float* part = nullptr;  // null: none
   int rs = 0, groups = 0, A1 = 0;
+  int group0 = 0;  // first K12 group finalized here (the head group K/32 when the dense weight goes through
+                   // the split-reading Adam tail)
   int64_t K = 0;
   void *dw = nullptr, *db = nullptr, *dwh = nullptr, *dbh = nullptr;
 };

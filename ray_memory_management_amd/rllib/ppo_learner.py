@@ -384,15 +384,22 @@ class PPOLearner:
         adam, tail = (self._tail_adam_args() if self._tail_adam() else (self._fused_adam_args(bump=True), []))
         fin = []
         if self._split_fin():  # the deferred K12 finalize (+ Adam) runs in the trunk-reduce launch
-            part, rs, groups = require_hip().dense_split_plan(int(full["mbs"]), self.model.dense_tail.in_features,
-                                                             self._k12_split(int(full["mbs"])), _stream())
-            fin = [part, rs, groups, self.model.dense_tail.in_features, self.model.heads.out_features,
-                   g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr()]
+            part, rs, groups = self._split_plan(int(full["mbs"]))
+            K = self.model.dense_tail.in_features
+            # the head group (db, dWh, dbh) through split_finalize_elem; the dense weight through the
+            # split-reading Adam tail (see _tail_adam_args)
+            fin = [part, rs, groups, K, self.model.heads.out_features,
+                   g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr(), K // 32]
         h.nature_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), ctr, int(full["period"]),
                            int(full["mbs"]), c2.weight.data_ptr(), list(c2.weight.stride()), ws["h1"].data_ptr(),
                            ws["h2"].data_ptr(), ws["dx"].data_ptr(), ws["part"].data_ptr(), g[0].data_ptr(),
                            list(c1.weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
                            adam=adam, tail=tail, tail_scale=1.0 / self.world, fin=fin)
+
+    def _split_plan(self, mbs: int):
+        """(workspace pointer, rs, groups) of the K12 row split at this minibatch size."""
+        return require_hip().dense_split_plan(int(mbs), self.model.dense_tail.in_features, self._k12_split(mbs),
+                                              _stream())
 
     def _k12_split(self, mbs: int) -> int:
         """K12 row-split factor (RMM_K12_SPLIT, read per call so K12 and a deferred finalize agree),
@@ -432,8 +439,12 @@ class PPOLearner:
                 self._wptr(), self.hp.data_ptr(), cur + 8, 0 if parity else cur, 0 if parity else 2,
                 0 if parity else self._bump_done.data_ptr()]
         nxt = self._ctrs[1 - self._par].data_ptr() if parity else 0
-        if self._split_fin():  # the dense + heads Adam runs in the finalize workgroups: counters only
-            tail = [0, 0, 0, 0, 0, 0, 0, 0, cur, 2, nxt]
+        if self._split_fin():  # dense weight: Adam on the summed row-split partials (vector pass)
+            part, rs, _ = self._split_plan(self._mws["mbs"])
+            K = self.model.dense_tail.in_features
+            tail = [self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
+                    self.flat_grad.data_ptr() + b2, self._wptr() + b2, 256 * K, self.hp.data_ptr(),
+                    cur + 8, cur, 2, nxt, part, rs, K]
         else:
             tail = [self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
                     self.flat_grad.data_ptr() + b2, self._wptr() + b2, self.n_params - lo, self.hp.data_ptr(),
