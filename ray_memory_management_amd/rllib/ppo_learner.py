@@ -403,8 +403,11 @@ class PPOLearner:
 
     def _k12_split(self, mbs: int) -> int:
         """K12 row-split factor (RMM_K12_SPLIT, read per call so K12 and a deferred finalize agree),
-        capped by the minibatch's 64-row chunks."""
-        return max(1, min(int(os.environ.get("RMM_K12_SPLIT", "1")), (int(mbs) + 63) // 64))
+        capped by the minibatch's 64-row chunks. Default 2 under tail Adam (the finalize folds into the
+        trunk-reduce launch: K12 15.5 -> 10.9 µs, reduce 9.3 -> 10.4 µs, fused loop 10.76 -> 10.38
+        ms/iter, profiles/tail_adam_r4.txt), else 1 (a separate finalize kernel measured no gain)."""
+        default = "2" if self._tail_adam() else "1"
+        return max(1, min(int(os.environ.get("RMM_K12_SPLIT", default)), (int(mbs) + 63) // 64))
 
     def _split_fin(self) -> bool:
         """K12 row split (RMM_K12_SPLIT=2: twice the workgroups, half the serial row-chunk chain each)
