@@ -60,7 +60,9 @@ def _tables(cuda, N=400, A=4, seed=1):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-def test_manual_step_matches_autograd_step(cuda, graphs):
+def test_manual_step_matches_autograd_step(cuda, graphs, monkeypatch):
+    # the autograd path runs K12 unsplit: pin the manual step's K12 to the same row order
+    monkeypatch.setenv("RMM_K12_SPLIT", "1")
     outs = []
     for manual in (True, False):
         L = _learner(cuda, manual_step=manual, use_graphs=graphs)
@@ -79,6 +81,7 @@ def test_manual_step_matches_autograd_step(cuda, graphs):
 def test_fused_adam_epilogues_match_k6(cuda, graphs, monkeypatch):
     """Adam folded into the K12 / K10-trunk-reduce epilogues (world of one) vs the separate K6 launch:
     same weights, moments and step counters after two updates (4 minibatches x 2 epochs each)."""
+    monkeypatch.setenv("RMM_K12_SPLIT", "1")  # the fused epilogues need K12 unsplit: same row order both sides
     outs = []
     for fused in (True, False):
         if fused:
