@@ -12,6 +12,8 @@ on-device GPURolloutSampler too (the bench.py configuration).
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict
 
 import torch
@@ -193,10 +195,17 @@ class PPO(Algorithm):
         rounds = max(1, -(-c.train_batch_size // max(per_round, 1)))
         dev = self._device_weights_ok()
         shared = dev and self._shared_weights_ok()
+        pre, self._prefetched = self._prefetched, None
         for r in range(rounds):
+            if r == 0 and pre is not None:  # queued behind last iteration's update (see below)
+                refs.extend(pre)
+                steps += per_round
+                continue
             for i, w in enumerate(remote):
                 if r == 0 and self._weights_ref is not None:
                     w.set_weights.remote(self._dev_refs[i % n_l] if dev and self._dev_refs else self._weights_ref)
+                    if shared and self._dev_refs:
+                        self._aliased = True
                 refs.append(w.sample.remote())
             steps += per_round
         if c.postprocess_on_learner:
@@ -217,6 +226,13 @@ class PPO(Algorithm):
             self._dev_refs = self.learner_group.device_weights_refs()
         else:
             self._weights_ref = self.learner_group.weights_ref()
+        if (shared and self._aliased and rounds == 1 and c.postprocess_on_learner
+                and os.environ.get("RMM_PREFETCH_SAMPLE", "1") != "0"):
+            # the workers alias the learners' live weights, so the next iteration's samples need only
+            # wait for this update: queue them now with the update's result refs as arguments (the
+            # runtime starts each sample the moment its learner's update finished) — the driver's
+            # get + submit round trip leaves the critical path; same samples, same weights
+            self._prefetched = [w.sample.remote(pending[i % n_l]) for i, w in enumerate(remote)]
         stats = ray.get(pending)
         self._counters["num_env_steps_sampled"] += steps
         self._counters["num_env_steps_trained"] += steps
@@ -228,6 +244,8 @@ class PPO(Algorithm):
         return st
 
     _dev_refs = None
+    _prefetched = None  # next iteration's sample refs, queued behind this iteration's update
+    _aliased = False    # the rollout workers were sent the learners' shared weights
 
     def _shared_weights_ok(self) -> bool:
         """Rollout workers alias the learners' live HBM weights (zero-copy, set once) instead of
@@ -286,6 +304,7 @@ class PPO(Algorithm):
         return self.learner.get_weights()
 
     def set_weights(self, weights):
+        self._prefetched = None  # samples queued with the previous weights must not be trained on
         if self.learner_group is not None:
             self.learner_group.set_weights(weights)
             self._weights_ref = self.learner_group.weights_ref()
@@ -305,6 +324,12 @@ class PPO(Algorithm):
         return super().get_policy(policy_id)
 
     def cleanup(self):
+        pre, self._prefetched = self._prefetched, None
+        if pre:  # let queued samples finish before the learners whose weights they alias go away
+            try:
+                ray.wait(pre, num_returns=len(pre), timeout=30.0)
+            except Exception:
+                pass
         if getattr(self, "learner_group", None) is not None and not getattr(self, "_multi_agent", False):
             self.learner_group.stop()
         super().cleanup()

@@ -53,7 +53,7 @@ class GPURolloutWorker:
     def get_custom_metrics(self):
         return {}
 
-    def sample(self):
+    def sample(self, *_after):  # _after: refs the runtime resolves first (prefetched samples)
         import time
 
         import torch
@@ -439,7 +439,7 @@ class HybridRolloutWorker(GPURolloutWorker):
         self._completed: List[tuple] = []
         self._sample_time = 0.0
 
-    def sample(self):
+    def sample(self, *_after):  # _after: refs the runtime resolves first (prefetched samples)
         import time
 
         import torch

@@ -132,7 +132,7 @@ class RolloutWorker:
                                               int(self.config.get("shuffle_buffer_size", 0) or 0), seed=base_seed)
 
     # ------------------------------------------------------------------ sampling
-    def sample(self) -> SampleBatch:
+    def sample(self, *_after) -> SampleBatch:  # _after: refs resolved before it runs (prefetch)
         if self.input_reader is not None:  # offline data replaces the env sampler
             return self.input_reader.next()
         if getattr(self.policy.model, "is_recurrent", False):

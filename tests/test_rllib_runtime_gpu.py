@@ -460,6 +460,8 @@ def test_ppo_hybrid_shared_weights(cuda, monkeypatch):
         st = r["info"]["learner"]["default_policy"]["learner_stats"]
         assert np.isfinite(st["total_loss"]) and st["num_sgd_steps"] == 8
         assert algo._shared_weights_ok() and algo._dev_refs is not None
+        # the next iteration's samples were queued behind the last update (RMM_PREFETCH_SAMPLE default)
+        assert algo._prefetched is not None and len(algo._prefetched) == 2
         ws = algo.workers.remote_workers()
         assert all(ray.get([w.apply.remote(lambda x: getattr(x, "_shared_key", None) is not None) for w in ws]))
         master = algo.learner_group.get_weights()
