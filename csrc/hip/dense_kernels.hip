@@ -17,6 +17,7 @@
 // C/D col l&15, row 4(l>>4)+i.
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -993,10 +994,12 @@ __global__ __launch_bounds__(256) void k_heads_sample(const unsigned short* __re
   }
 }
 
-// K16 for a small rollout batch with the step advance (B <= 32): ONE workgroup of 16 waves loops
-// the rows, then thread 0 bumps *t_ptr / *ctr after a workgroup barrier — no device-scope fence
-// and completion atomic (an L2 write-back across XCDs) as the multi-workgroup K16 needs.
-template <int A1>
+// K16 for a small rollout batch with the step advance (B <= 16 R): ONE workgroup of 16 waves, wave w
+// takes rows w, w + 16, ... (at most R); every row's hidden partials are loaded before the Wh staging,
+// so the R round trips overlap each other and the staging. Then thread 0 bumps *t_ptr / *ctr after a
+// workgroup barrier — no device-scope fence and completion atomic (an L2 write-back across XCDs) as
+// the multi-workgroup K16 needs. Same per-row code as K16, so the two launches are bit-identical.
+template <int A1, int R>
 __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __restrict__ hid,
                                                         const unsigned short* __restrict__ wh,
                                                         const unsigned short* __restrict__ bh, int64_t* t_ptr,
@@ -1007,20 +1010,23 @@ __global__ __launch_bounds__(1024) void k_heads_sample1(const unsigned short* __
                                                         const unsigned short* __restrict__ hb, int64_t* host_seq) {
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
+  constexpr int kWaves = 16;
   const int lane = threadIdx.x & 63;
   const int64_t b0 = threadIdx.x >> 6;
-  float hv[4] = {0.f, 0.f, 0.f, 0.f};
+  float hv[R][4];
   uint2 hbits;
-  if (b0 < B) load_hidden4(hid, hpart, S, hb, B, b0, lane, hv, hbits);  // overlaps the Wh staging
+#pragma unroll
+  for (int r = 0; r < R; r++)  // wave-uniform
+    if (b0 + r * kWaves < B) load_hidden4(hid, hpart, S, hb, B, b0 + r * kWaves, lane, hv[r], hbits);
   for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = bf2f(wh[e]);
   if (threadIdx.x < A1) bhs[threadIdx.x] = bf2f(bh[threadIdx.x]);
   const int64_t t = *t_ptr;
   const uint32_t c = uint32_t(*ctr);
   __syncthreads();
-  for (int64_t b = b0; b < B; b += blockDim.x >> 6) {  // wave-uniform
-    if (b != b0) load_hidden4(hid, hpart, S, hb, B, b, lane, hv, hbits);
-    heads_sample_row_pre<A1>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
-  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (b0 + r * kWaves < B) heads_sample_row_pre<A1>(hv[r], whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B,
+                                                      b0 + r * kWaves, lane);
   if (host_seq) __threadfence_system();  // this wave's action stores to host memory, visible to the CPU
   __syncthreads();  // every wave has read t / ctr
   if (threadIdx.x == 0) {
@@ -1105,17 +1111,26 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
   if (hpart != nullptr && (S < 1 || hb == nullptr)) throw std::invalid_argument("dense_heads_sample: partials need S >= 1 and the dense bias");
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("dense_heads_sample: 2 <= A <= 15 actions");
   auto U = [](const void* p) { return static_cast<const unsigned short*>(p); };
-  static const bool one_wg = [] {  // RMM_K16_MULTI=1: multi-workgroup K16 + completion counter (A/B)
-    const char* e = std::getenv("RMM_K16_MULTI");
-    return !(e && e[0] == '1');
+  // one-workgroup K16 up to one_wg_rows rows (RMM_K16_ONE_WG_ROWS: 32 or 64, default 32; RMM_K16_MULTI=1:
+  // always the multi-workgroup K16 + completion counter, for A/B). 64 measured 13 us/step SLOWER at 50
+  // rows (profiles/k16_layout_r4.txt): each wave runs its 4 rows (GEMV, butterfly, host stores) back to back
+  static const int64_t one_wg_rows = [] {
+    const char* m = std::getenv("RMM_K16_MULTI");
+    if (m && m[0] == '1') return int64_t(0);
+    const char* e = std::getenv("RMM_K16_ONE_WG_ROWS");
+    return (e && std::atoi(e) == 64) ? int64_t(64) : int64_t(32);
   }();
-  if (done != nullptr && B <= 32 && one_wg) {
+  if (done != nullptr && B <= one_wg_rows) {
     auto* tw = const_cast<int64_t*>(t_ptr);
     auto* cw = const_cast<int64_t*>(ctr);
-#define RMM_K16S(N)                                                                                            \
-  case N:                                                                                                      \
-    hipLaunchKernelGGL(dense::k_heads_sample1<N>, dim3(1), dim3(1024), 0, stream, U(hidden), U(wh), U(bh), tw, cw, \
-                       seed, act, logp, vf, lout, act_now, B, hpart, S, U(hb), host_seq);                      \
+#define RMM_K16S(N)                                                                                                 \
+  case N:                                                                                                           \
+    if (B <= 32)                                                                                                    \
+      hipLaunchKernelGGL((dense::k_heads_sample1<N, 2>), dim3(1), dim3(1024), 0, stream, U(hidden), U(wh), U(bh), tw, \
+                         cw, seed, act, logp, vf, lout, act_now, B, hpart, S, U(hb), host_seq);                    \
+    else                                                                                                            \
+      hipLaunchKernelGGL((dense::k_heads_sample1<N, 4>), dim3(1), dim3(1024), 0, stream, U(hidden), U(wh), U(bh), tw, \
+                         cw, seed, act, logp, vf, lout, act_now, B, hpart, S, U(hb), host_seq);                    \
     break;
     switch (A1) {
       RMM_K16S(3) RMM_K16S(4) RMM_K16S(5) RMM_K16S(6) RMM_K16S(7) RMM_K16S(8) RMM_K16S(9)
@@ -1125,7 +1140,13 @@ void dense_heads_sample(const void* hidden, const void* wh, const void* bh, cons
     RMM_HIP_CHECK(hipGetLastError());
     return;
   }
-  const dim3 grid(uint32_t((B + 3) / 4)), block(256);
+  // waves (= rows) per workgroup of the multi-workgroup K16 (RMM_K16_WPW: 1, 2 or 4, default 4)
+  static const int wpw = [] {
+    const char* e = std::getenv("RMM_K16_WPW");
+    const int v = e ? std::atoi(e) : 4;
+    return (v == 1 || v == 2) ? v : 4;
+  }();
+  const dim3 grid(uint32_t((B + wpw - 1) / wpw)), block(uint32_t(64 * wpw));
 #define RMM_K16(N)                                                                                          \
   case N:                                                                                                   \
     hipLaunchKernelGGL(dense::k_heads_sample<N>, grid, block, 0, stream, U(hidden), U(wh), U(bh), t_ptr, ctr, \

@@ -541,7 +541,7 @@ def test_trunk_push_mode_matches_frame_push_then_trunk(cuda):
     assert torch.equal(h2_a, h2_b)
 
 
-@pytest.mark.parametrize("B", [12, 25])
+@pytest.mark.parametrize("B", [12, 25, 33, 50, 64])  # 33-64: four rows per wave, all preloaded
 def test_heads_sample_single_workgroup_advance(cuda, B):
     """K16 with the step advance for small batches runs as ONE workgroup (no device-scope fence):
     same rows as the multi-workgroup launch and the counters advance by exactly one."""
@@ -566,15 +566,15 @@ torch.cuda.synchronize()
 print(json.dumps({{"ct": ct.tolist(), "act": act.tolist(), "logp": logp.tolist(), "done": int(done)}}))
 """
     outs = []
-    for multi in ("0", "1"):
-        env = dict(os.environ, RMM_K16_MULTI=multi)
+    for multi, wpw in (("0", "4"), ("1", "4"), ("1", "1")):  # one workgroup / 4 rows per WG / 1 row per WG
+        env = dict(os.environ, RMM_K16_MULTI=multi, RMM_K16_WPW=wpw)
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
                            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    a, b = outs
-    assert a["ct"] == [7, 3] and b["ct"] == [7, 3]  # two launches: rng counter 5 -> 7, row 1 -> 3
-    assert a["act"] == b["act"] and a["logp"] == b["logp"]
+    a, b, c = outs
+    assert a["ct"] == [7, 3] and b["ct"] == [7, 3] and c["ct"] == [7, 3]  # rng counter 5 -> 7, row 1 -> 3
+    assert a["act"] == b["act"] == c["act"] and a["logp"] == b["logp"] == c["logp"] and c["done"] == 0
     assert a["act"][0] == [0] * B and any(a["act"][1]) and any(a["act"][2])
     assert a["done"] == 0 and b["done"] == 0
 
