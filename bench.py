@@ -307,6 +307,8 @@ def main():
                 for _ in range(args.steps):
                     r = algo.train()  # learners end every update with a device sync
                 stats = r["info"]["learner"]["default_policy"]["learner_stats"]
+                # next iteration's samples queued behind the last update (RMM_PREFETCH_SAMPLE, shared weights)
+                info["sample_prefetch"] = getattr(algo, "_prefetched", None) is not None
             except BaseException as e:  # noqa: BLE001
                 err = e
         if world > 1:
