@@ -67,12 +67,12 @@ def extensions():
     if tl:
         hip_ld = [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"] + hip_ld
     exts.append(
-        _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/ingest_kernels.hip", "csrc/hip/vtrace_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/peer_allreduce.hip", "csrc/hip/rollout_server.hip", "csrc/hip/rccl_comm.cc", "csrc/hip/rollout_loop.cc", "csrc/hip/hip_py.cc",
+        _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/x3_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/ingest_kernels.hip", "csrc/hip/vtrace_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/peer_allreduce.hip", "csrc/hip/rollout_server.hip", "csrc/hip/rccl_comm.cc", "csrc/hip/rollout_loop.cc", "csrc/hip/hip_py.cc",
               "csrc/store/shm_store.cc"], HIPCC,
              common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"],
              hip_ld, ["csrc/hip/kernels.h", "csrc/hip/gpu_store.h", "csrc/hip/rccl_comm.h", "csrc/hip/peer_allreduce.h", "csrc/hip/common.h", "csrc/store/shm_store.h",
                      "csrc/hip/rollout_loop.h", "csrc/rl/synth_env.h", "csrc/hip/trunk_device.h",
-                     "csrc/hip/dense_device.h", "csrc/hip/adam_device.h"]))
+                     "csrc/hip/dense_device.h", "csrc/hip/adam_device.h", "csrc/hip/x3_device.h"]))
     return exts
 
 

@@ -30,10 +30,17 @@ __device__ __forceinline__ uint32_t bf16x2_rn(float a, float b) {
 // Cache bound: 28 B/param), issuing every group's loads before the first update so U x 4 vector
 // loads are in flight per lane; the n % 4 tail is done by the first threads. VEC requires 16-B
 // aligned fp32 and 8-B aligned bf16 pointers (checked by the host).
+// wlo (optional, the split-bf16 fp32 learner, x3_device.h): wbf16 receives hi = RNE(w) and wlo the
+// residual lo = RNE(w - hi), so the kernels read the fp32 master as the pair hi + lo.
+__device__ __forceinline__ uint32_t bf16x2_lo(float a, float b) {
+  const float ra = a - __bfloat162float(__float2bfloat16(a)), rb = b - __bfloat162float(__float2bfloat16(b));
+  return bf16x2_rn(ra, rb);
+}
 template <typename TG, bool VEC, int U>
 __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __restrict__ m1, float* __restrict__ m2,
                                           const TG* __restrict__ grad, __hip_bfloat16* __restrict__ wbf16,
-                                          float grad_scale, const AdamCoef& c, int64_t tid, int64_t nthr, int64_t n) {
+                                          float grad_scale, const AdamCoef& c, int64_t tid, int64_t nthr, int64_t n,
+                                          __hip_bfloat16* __restrict__ wlo = nullptr) {
   int64_t scalar_from = 0;
   if constexpr (VEC) {
     const int64_t nv = n >> 2;
@@ -65,6 +72,8 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
           *reinterpret_cast<float4*>(m2 + i) = b[u];
           if (wbf16)
             *reinterpret_cast<uint2*>(wbf16 + i) = make_uint2(bf16x2_rn(w[u].x, w[u].y), bf16x2_rn(w[u].z, w[u].w));
+          if (wlo)
+            *reinterpret_cast<uint2*>(wlo + i) = make_uint2(bf16x2_lo(w[u].x, w[u].y), bf16x2_lo(w[u].z, w[u].w));
         }
       }
     }
@@ -77,6 +86,7 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
     m2[i] = b;
     master[i] = w;
     if (wbf16) wbf16[i] = __float2bfloat16(w);
+    if (wlo) wlo[i] = __float2bfloat16(w - __bfloat162float(__float2bfloat16(w)));
   }
 }
 

@@ -154,7 +154,7 @@ __device__ __forceinline__ void load_hidden4(const unsigned short* __restrict__ 
 }
 
 // one env row of K16 (one wave): head GEMV + bias, bf16 rounding, Gumbel-max draw, row stores
-template <int A1>
+template <int A1, bool ROUND = true>
 __device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const float* whs, const float* bhs,
                                                      const int64_t t, const uint32_t c, uint32_t seed,
                                                      int64_t* __restrict__ act, float* __restrict__ logp,
@@ -175,8 +175,9 @@ __device__ __forceinline__ void heads_sample_row(const unsigned short* __restric
 }
 
 // heads_sample_row with this lane's 4 hidden values already loaded (load_hidden4): kernels issue those
-// loads before staging Wh into LDS, so the partial-sum round trip overlaps the staging
-template <int A1>
+// loads before staging Wh into LDS, so the partial-sum round trip overlaps the staging.
+// ROUND: the bf16 policy rounds the head row to bf16 (as K14 stores it); the fp32 policy keeps fp32.
+template <int A1, bool ROUND>
 __device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const float* whs, const float* bhs,
                                                      const int64_t t, const uint32_t c, uint32_t seed,
                                                      int64_t* __restrict__ act, float* __restrict__ logp,
@@ -195,7 +196,7 @@ __device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const
 #pragma unroll
     for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
 #pragma unroll
-  for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));
+  for (int a = 0; a < A1; a++) hd[a] = ROUND ? bf2f(f2bf(hd[a] + bhs[a])) : hd[a] + bhs[a];
   const int64_t o = t * B + b;
   if (lane < A) {
     float l = hd[0];
@@ -229,6 +230,71 @@ __device__ __forceinline__ void heads_sample_row_pre(const float (&hv)[4], const
     logp[o] = la - mx - __logf(se);
     vf[o] = hd[A];
   }
+}
+
+// The categorical PPO loss of one row given its head row hd = [logits (A) | value] (every lane of the
+// row's wave holds the whole row and evaluates it redundantly: no broadcast). cv = the row's packed
+// loss columns [old logits (A) | old logp | advantage | value target | action]. Returns the 6 loss
+// statistics (meaningful on `stat_lane`) and g = d(loss)/d(heads) scaled by gs (= upstream / M).
+// ROUND: the bf16 learner rounds g to bf16 (what K12 reads); the split-bf16 (fp32) learner keeps fp32.
+// Shared by K15 (bf16) and K15x (x3_kernels.hip): the same loss code on both paths.
+template <int A1, bool ROUND>
+__device__ __forceinline__ void ppo_loss_row(const float (&hd)[A1], const float* cv, float clip, float vf_clip,
+                                             float vf_coeff, float ent_coeff, float kl_coeff, float gs,
+                                             bool stat_lane, float (&s)[6], float (&g)[A1]) {
+  constexpr int A = A1 - 1;
+  float mx = -INFINITY, mxo = -INFINITY, lo[A > 0 ? A : 1];
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    lo[j] = cv[j];
+    mx = fmaxf(mx, hd[j]);
+    mxo = fmaxf(mxo, lo[j]);
+  }
+  float se = 0.f, seo = 0.f;
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    se += __expf(hd[j] - mx);
+    seo += __expf(lo[j] - mxo);
+  }
+  const float lse = mx + __logf(se), lseo = mxo + __logf(seo);
+  float m = 0.f, kl = 0.f, p[A > 0 ? A : 1], po[A > 0 ? A : 1];
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    p[j] = __expf(hd[j] - lse);
+    po[j] = __expf(lo[j] - lseo);
+    m += p[j] * hd[j];
+    kl += po[j] * ((lo[j] - lseo) - (hd[j] - lse));
+  }
+  const int act = min(max(int(cv[A + 3]), 0), A - 1);
+  float la = hd[0];
+#pragma unroll
+  for (int j = 1; j < A; j++)
+    if (j == act) la = hd[j];
+  const float r = __expf((la - lse) - cv[A]);
+  const float ad = cv[A + 1];
+  const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
+  const float d = hd[A] - cv[A + 2];
+#pragma unroll
+  for (int k = 0; k < 6; k++) s[k] = 0.f;
+  if (stat_lane) {
+    const float ent = lse - m, surr = fminf(r * ad, rc * ad), vf = fminf(d * d, vf_clip);
+    s[0] = -surr;
+    s[1] = vf;
+    s[2] = ent;
+    s[3] = kl;
+    s[4] = (fabsf(r - 1.f) > clip) ? 1.f : 0.f;
+    s[5] = -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl;
+  }
+  const bool unclipped = r * ad <= rc * ad;
+  const bool inside = (r >= 1.f - clip) && (r <= 1.f + clip);
+  const float spg = (unclipped || inside) ? -(r * ad) : 0.f;
+#pragma unroll
+  for (int j = 0; j < A; j++) {
+    const float v = (spg * ((j == act ? 1.f : 0.f) - p[j]) + ent_coeff * p[j] * (hd[j] - m) + kl_coeff * (p[j] - po[j])) * gs;
+    g[j] = ROUND ? bf2f(f2bf(v)) : v;
+  }
+  const float gv = (d * d < vf_clip) ? vf_coeff * 2.f * d * gs : 0.f;
+  g[A] = ROUND ? bf2f(f2bf(gv)) : gv;
 }
 
 // One gradient element of the K12 row split's deferred finalize: (group, slot, lane-of-K12) → the

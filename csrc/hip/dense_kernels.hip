@@ -856,59 +856,10 @@ __global__ __launch_bounds__(256) void k_heads_ppo(const unsigned short* __restr
     for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
 #pragma unroll
   for (int a = 0; a < A1; a++) hd[a] = bf2f(f2bf(hd[a] + bhs[a]));  // the bf16 head output
-  // cols row (loaded above): gathered through the minibatch index window (as K2) when cidx is given
-  float mx = -INFINITY, mxo = -INFINITY, lo[A > 0 ? A : 1];
-#pragma unroll
-  for (int j = 0; j < A; j++) {
-    lo[j] = cv[j];
-    mx = fmaxf(mx, hd[j]);
-    mxo = fmaxf(mxo, lo[j]);
-  }
-  float se = 0.f, seo = 0.f;
-#pragma unroll
-  for (int j = 0; j < A; j++) {
-    se += __expf(hd[j] - mx);
-    seo += __expf(lo[j] - mxo);
-  }
-  const float lse = mx + __logf(se), lseo = mxo + __logf(seo);
-  float m = 0.f, kl = 0.f, p[A > 0 ? A : 1], po[A > 0 ? A : 1];
-#pragma unroll
-  for (int j = 0; j < A; j++) {
-    p[j] = __expf(hd[j] - lse);
-    po[j] = __expf(lo[j] - lseo);
-    m += p[j] * hd[j];
-    kl += po[j] * ((lo[j] - lseo) - (hd[j] - lse));
-  }
-  const int act = min(max(int(cv[A + 3]), 0), A - 1);
-  float la = hd[0];
-#pragma unroll
-  for (int j = 1; j < A; j++)
-    if (j == act) la = hd[j];
-  const float r = __expf((la - lse) - cv[A]);
-  const float ad = cv[A + 1];
-  const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
-  const float d = hd[A] - cv[A + 2];
-  // statistics (lane 0 of each valid row)
-  float s[6] = {0, 0, 0, 0, 0, 0};
-  if (valid && lane == 0) {
-    const float ent = lse - m, surr = fminf(r * ad, rc * ad), vf = fminf(d * d, vf_clip);
-    s[0] = -surr;
-    s[1] = vf;
-    s[2] = ent;
-    s[3] = kl;
-    s[4] = (fabsf(r - 1.f) > clip) ? 1.f : 0.f;
-    s[5] = -surr + vf_coeff * vf - ent_coeff * ent + kl_coeff * kl;
-  }
-  // d(loss)/d(heads), rounded to bf16 (what K12 reads)
-  const bool unclipped = r * ad <= rc * ad;
-  const bool inside = (r >= 1.f - clip) && (r <= 1.f + clip);
-  const float spg = (unclipped || inside) ? -(r * ad) : 0.f;
-  float g[A1];
-#pragma unroll
-  for (int j = 0; j < A; j++)
-    g[j] = bf2f(f2bf((spg * ((j == act ? 1.f : 0.f) - p[j]) + ent_coeff * p[j] * (hd[j] - m) +
-                      kl_coeff * (p[j] - po[j])) * gs));
-  g[A] = bf2f(f2bf((d * d < vf_clip) ? vf_coeff * 2.f * d * gs : 0.f));
+  // cols row (loaded above): gathered through the minibatch index window (as K2) when cidx is given;
+  // statistics from lane 0 of each valid row, d(loss)/d(heads) rounded to bf16 (what K12 reads)
+  float s[6], g[A1];
+  ppo_loss_row<A1, true>(hd, cv, clip, vf_clip, vf_coeff, ent_coeff, kl_coeff, gs, valid && lane == 0, s, g);
   if (valid) {
     if (lane < A1) {
       float gl = g[0];

@@ -75,6 +75,10 @@ FusedAdam fused_adam(const std::vector<uint64_t>& v) {
   return fa;
 }
 
+using XP = std::pair<uint64_t, uint64_t>;  // split pair (hi_ptr, lo_ptr)
+X3In xin(const XP& p) { return X3In{reinterpret_cast<const void*>(p.first), reinterpret_cast<const void*>(p.second)}; }
+X3Out xout(const XP& p) { return X3Out{reinterpret_cast<void*>(p.first), reinterpret_cast<void*>(p.second)}; }
+
 // ---- minimal DLPack ABI (stable C ABI, v0.x "dltensor" capsule)
 struct DLDevice {
   int32_t device_type;
@@ -248,16 +252,17 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("adam_flat", [](uint64_t master, uint64_t m1, uint64_t m2, uint64_t grad, bool grad_bf16, uint64_t wbf16,
                         uint64_t hp, float grad_scale, int64_t n, uint64_t stream, uint64_t step_ctr, uint64_t bump,
-                        int nbump, uint64_t done, uint64_t scale_ptr, int max_blocks, uint64_t bump_next) {
+                        int nbump, uint64_t done, uint64_t scale_ptr, int max_blocks, uint64_t bump_next,
+                        uint64_t wlo) {
     adam_flat(P<float>(master), P<float>(m1), P<float>(m2), P<const void>(grad), grad_bf16,
               wbf16 ? P<void>(wbf16) : nullptr, P<const float>(hp), grad_scale, n, S(stream),
               step_ctr ? P<const int64_t>(step_ctr) : nullptr, bump ? P<int64_t>(bump) : nullptr, nbump,
               done ? P<uint32_t>(done) : nullptr, scale_ptr ? P<const float>(scale_ptr) : nullptr, max_blocks,
-              bump_next ? P<int64_t>(bump_next) : nullptr);
+              bump_next ? P<int64_t>(bump_next) : nullptr, wlo ? P<void>(wlo) : nullptr);
   }, py::arg("master"), py::arg("m1"), py::arg("m2"), py::arg("grad"), py::arg("grad_bf16"), py::arg("wbf16"),
      py::arg("hp"), py::arg("grad_scale"), py::arg("n"), py::arg("stream"), py::arg("step_ctr") = 0,
      py::arg("bump") = 0, py::arg("nbump") = 0, py::arg("done") = 0, py::arg("scale_ptr") = 0,
-     py::arg("max_blocks") = 0, py::arg("bump_next") = 0);
+     py::arg("max_blocks") = 0, py::arg("bump_next") = 0, py::arg("wlo") = 0);
   m.def("grad_clip_workspace_floats", &grad_clip_workspace_floats);
   m.def("ingest_gae", [](uint64_t raw, uint64_t boot, uint64_t blocks, int nblocks, int A, float gamma, float lam,
                          uint64_t cols, uint64_t stats, uint64_t stream) {
@@ -359,8 +364,11 @@ PYBIND11_MODULE(_hip, m) {
                                     const std::vector<uint64_t>& bufs, int64_t B, int slices, int A1, uint32_t seed,
                                     uint64_t k16_done, int64_t T, int threads, bool spin, uint64_t host_seq,
                                     uint64_t host_seq_dev) {
-    if (v.size() < 15 || wts.size() != 8 || bufs.size() < 11 || w1s.size() != 4 || w2s.size() != 4 || !k16_done)
-      throw std::invalid_argument("hybrid_rollout_direct: 15 group fields, 8 weights, 11 buffers, 4+4 strides, done");
+    // fp32 policy: 16 weights (8 hi planes, then the 8 lo planes) and a 12th buffer (the h2 lo plane)
+    const bool x3 = wts.size() == 16;
+    if (v.size() < 15 || (wts.size() != 8 && !x3) || bufs.size() < size_t(x3 ? 12 : 11) || w1s.size() != 4 ||
+        w2s.size() != 4 || !k16_done)
+      throw std::invalid_argument("hybrid_rollout_direct: 15 group fields, 8 (16) weights, 11 (12) buffers, 4+4 strides, done");
     RolloutGroup g;
     g.stream = S(v[1]);
     g.env.pools = P<const uint8_t>(v[2]);
@@ -402,6 +410,18 @@ PYBIND11_MODULE(_hip, m) {
     a.S = slices;
     a.A1 = A1;
     a.seed = seed;
+    if (x3) {
+      a.x3 = true;
+      a.W1lo = P<const void>(wts[8]);
+      a.b1lo = P<const void>(wts[9]);
+      a.W2lo = P<const void>(wts[10]);
+      a.b2lo = P<const void>(wts[11]);
+      a.Wdlo = P<const void>(wts[12]);
+      a.bdlo = P<const void>(wts[13]);
+      a.Whlo = P<const void>(wts[14]);
+      a.bhlo = P<const void>(wts[15]);
+      a.h2lo = P<void>(bufs[11]);
+    }
     g.direct = &a;
     g.k16_done = P<unsigned int>(k16_done);
     if ((host_seq == 0) != (host_seq_dev == 0))
@@ -626,6 +646,65 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("h1"), py::arg("h2"), py::arg("dh2"), py::arg("partial"), py::arg("dW1"), py::arg("w1s"), py::arg("db1"),
      py::arg("dW2"), py::arg("db2"), py::arg("stream"), py::arg("dbg") = 0, py::arg("adam") = std::vector<uint64_t>{},
      py::arg("tail") = std::vector<uint64_t>{}, py::arg("tail_scale") = 1.0f, py::arg("fin") = std::vector<uint64_t>{});
+
+  // ---------------------------------------------------------------- split-bf16 (fp32-level) kernels
+  // a split pair crosses as (hi_ptr, lo_ptr); (0, 0) = absent
+  m.def("x3_split", [](uint64_t src, uint64_t hi, uint64_t lo, int64_t n, uint64_t stream) {
+    x3_split(P<const float>(src), P<void>(hi), P<void>(lo), n, S(stream));
+  });
+  m.def("x3_trunk_fwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, XP W1,
+                           std::vector<int64_t> w1s, XP b1, XP W2, std::vector<int64_t> w2s, XP b2, XP h1, XP h2,
+                           uint64_t stream) {
+    if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_fwd: 4 strides per weight");
+    x3_trunk_fwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr,
+                 period, B, xin(W1), w1s.data(), xin(b1), xin(W2), w2s.data(), xin(b2), xout(h1), xout(h2), S(stream));
+  });
+  m.def("x3_trunk_fwd_push", [](uint64_t stack, uint64_t nf, uint64_t rows, uint64_t t_ptr, int64_t B, XP W1,
+                                std::vector<int64_t> w1s, XP b1, XP W2, std::vector<int64_t> w2s, XP b2, XP h2,
+                                uint64_t stream) {
+    if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_fwd_push: 4 strides per weight");
+    x3_trunk_fwd_push(P<uint8_t>(stack), P<const uint8_t>(nf), rows ? P<uint8_t>(rows) : nullptr,
+                      t_ptr ? P<const int64_t>(t_ptr) : nullptr, B, xin(W1), w1s.data(), xin(b1), xin(W2), w2s.data(),
+                      xin(b2), xout(h2), S(stream));
+  });
+  m.def("x3_trunk_partial_floats", &x3_trunk_partial_floats);
+  m.def("x3_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, XP W2,
+                           std::vector<int64_t> w2s, XP h1, uint64_t h2hi, XP dh2, XP dpre1, uint64_t partial,
+                           uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
+                           uint64_t stream) {
+    if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_bwd: 4 strides per weight");
+    x3_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr,
+                 period, B, xin(W2), w2s.data(), xin(h1), P<const void>(h2hi), xin(dh2), xout(dpre1), P<float>(partial),
+                 P<float>(dW1), w1s.data(), P<float>(db1), P<float>(dW2), P<float>(db2), S(stream));
+  });
+  m.def("x3_dense_fwd_part_slices", &x3_dense_fwd_part_slices);
+  m.def("x3_dense_fwd_part", [](XP x, XP w, int64_t M, int64_t K, int N, uint64_t part, int nslices, uint64_t stream) {
+    x3_dense_fwd_part(xin(x), xin(w), M, K, N, P<float>(part), nslices, S(stream));
+  });
+  m.def("x3_heads_ppo", [](uint64_t hpart, int nslices, XP hb, XP wh, XP bh, uint64_t cols, uint64_t coef, uint64_t acc,
+                           uint64_t gout, int64_t M, int A1, XP dz, XP dpre, XP hid, uint64_t stream, uint64_t cidx,
+                           uint64_t ctr, int64_t period) {
+    x3_heads_ppo(P<const float>(hpart), nslices, xin(hb), xin(wh), xin(bh), P<const float>(cols), P<const float>(coef),
+                 P<float>(acc), P<const float>(gout), M, A1, xout(dz), xout(dpre), xout(hid), S(stream),
+                 cidx ? P<const int64_t>(cidx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr, period);
+  }, py::arg("hpart"), py::arg("S"), py::arg("hb"), py::arg("wh"), py::arg("bh"), py::arg("cols"), py::arg("coef"),
+     py::arg("acc"), py::arg("gout"), py::arg("M"), py::arg("A1"), py::arg("dz"), py::arg("dpre"), py::arg("hid"),
+     py::arg("stream"), py::arg("cidx") = 0, py::arg("ctr") = 0, py::arg("period") = 1);
+  m.def("x3_heads_sample", [](uint64_t hpart, int nslices, XP hb, XP wh, XP bh, uint64_t t_ptr, uint64_t ctr,
+                              uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout, uint64_t act_now,
+                              int64_t B, int A1, uint64_t stream, uint64_t done, uint64_t host_seq) {
+    x3_heads_sample(P<const float>(hpart), nslices, xin(hb), xin(wh), xin(bh), P<const int64_t>(t_ptr),
+                    P<const int64_t>(ctr), seed, P<int64_t>(act), P<float>(logp), P<float>(vf), P<float>(lout),
+                    P<int64_t>(act_now), B, A1, S(stream), done ? P<unsigned int>(done) : nullptr,
+                    host_seq ? P<int64_t>(host_seq) : nullptr);
+  }, py::arg("hpart"), py::arg("S"), py::arg("hb"), py::arg("wh"), py::arg("bh"), py::arg("t_ptr"), py::arg("ctr"),
+     py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"), py::arg("lout"), py::arg("act_now"), py::arg("B"),
+     py::arg("A1"), py::arg("stream"), py::arg("done") = 0, py::arg("host_seq") = 0);
+  m.def("x3_dense_heads_bwd", [](XP dz, int A1, XP y, XP x, XP w, XP dpre, int64_t M, int64_t K, XP dx, uint64_t dw,
+                                 uint64_t db, uint64_t dwh, uint64_t dbh, uint64_t stream) {
+    x3_dense_heads_bwd(xin(dz), A1, xin(y), xin(x), xin(w), xin(dpre), M, K, xout(dx), P<float>(dw), P<float>(db),
+                       P<float>(dwh), P<float>(dbh), S(stream));
+  });
 
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {

@@ -70,7 +70,7 @@ void ppo_cat_loss(bool fwd, const void* logits, bool logits_bf16, const float* o
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr = nullptr,
                int64_t* bump = nullptr, int nbump = 0, uint32_t* done = nullptr, const float* scale_ptr = nullptr, int max_blocks = 0,
-               int64_t* bump_next = nullptr);
+               int64_t* bump_next = nullptr, void* wlo = nullptr);  // wlo: split-pair lo plane (wbf16 = hi)
 // K6b: out[0] = min(1, max_norm / ||grad*grad_scale||), out[1] = the norm (device; feeds K6 scale_ptr).
 // workspace: grad_clip_workspace_floats() floats, zero-initialised once (its ticket resets itself).
 int64_t grad_clip_workspace_floats();
@@ -199,6 +199,50 @@ void nature_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr
 // bit5 the st zeroing, bit6 return at once, bit7 the reduce launch, bit8 all LDS zeroing, bit9 the W2
 // staging, bit10 the bias-gradient epilogue.
 
+// ---- precision-matched (fp32-level) kernels over split-bf16 pairs (x3_kernels.hip, x3_device.h):
+// a split tensor is two bf16 planes hi / lo of the same shape with x = hi + lo; products are
+// hi*hi + hi*lo + lo*hi on the bf16 MFMA with fp32 accumulation; gradients are fp32.
+struct X3In {
+  const void* hi = nullptr;
+  const void* lo = nullptr;
+};
+struct X3Out {
+  void* hi = nullptr;
+  void* lo = nullptr;
+};
+// K10x: trunk forward (h1 may be {null, null}: inference); grid min(B, 256) workgroups loop over frames
+int x3_trunk_fwd_groups(int64_t B);
+void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W1,
+                  const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h1, X3Out h2,
+                  hipStream_t stream);
+void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
+                       X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
+                       hipStream_t stream);
+// K10x backward: conv2 launch (dW2, db2, dpre1 -> dpre1 pair, db1) + conv1 weight-grad launch + reduce;
+// fp32 gradients in the parameters' memory order. partial: x3_trunk_partial_floats(B) floats.
+int x3_conv2_bwd_groups(int64_t B);
+int x3_conv1_wgrad_groups(int64_t B);
+int64_t x3_trunk_partial_floats(int64_t B);
+void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W2,
+                  const int64_t* w2s, X3In h1, const void* h2hi, X3In dh2, X3Out dpre1, float* partial, float* dW1,
+                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream);
+// K13x: split-K dense layer -> fp32 partials part[S][M][N]
+int x3_dense_fwd_part_slices(int64_t M, int64_t K, int N);
+void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part, int S, hipStream_t stream);
+// K15x: hidden = ReLU(Σ partials + hb) (fp32), heads, PPO loss stats into acc, dz / dpre / hid split pairs
+void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const float* cols, const float* coef, float* acc,
+                  const float* gout, int64_t M, int A1, X3Out dz, X3Out dpre, X3Out hid, hipStream_t stream,
+                  const int64_t* cidx = nullptr, const int64_t* ctr = nullptr, int64_t period = 1);
+// K16x: fp32 head row + Gumbel-max sampling + rollout-row stores (+ the step advance with `done`)
+void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const int64_t* t_ptr, const int64_t* ctr,
+                     uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B, int A1,
+                     hipStream_t stream, unsigned int* done = nullptr, int64_t* host_seq = nullptr);
+// K12x: dx (split pair) and fp32 dW, db, dWh, dbh
+void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int64_t M, int64_t K, X3Out dx, float* dw,
+                        float* db, float* dwh, float* dbh, hipStream_t stream);
+// fp32 -> split pair (weights after a host-side update, tests)
+void x3_split(const float* src, void* hi, void* lo, int64_t n, hipStream_t stream);
+
 // K17: learner-side sample-batch ingest (see ingest_kernels.hip). raw [rows, A+5] fp32 =
 // [logits(A) | logp | vf | reward | done | action], blocks = one entry per rollout fragment
 // (time-major rows t*n+env starting at row0; bootstrap values at boot[boot0 .. boot0+n)).
@@ -247,6 +291,12 @@ struct RolloutServerArgs {
   double go_timeout_s = 20.0, barrier_timeout_s = 5.0;
   int workgroups = 0;            // 0: one per CU
   uint64_t* prof = nullptr;      // optional device [T][5] phase timestamps (s_memrealtime)
+  // fp32 policy (direct launches only): the weights above are the hi planes of split-bf16 pairs and these
+  // the lo planes; h2 / h2lo the trunk output pair (K10x push -> K13x -> K16x, x3_kernels.hip)
+  bool x3 = false;
+  const void *W1lo = nullptr, *b1lo = nullptr, *W2lo = nullptr, *b2lo = nullptr;
+  const void *Wdlo = nullptr, *bdlo = nullptr, *Whlo = nullptr, *bhlo = nullptr;
+  void* h2lo = nullptr;
 };
 int rollout_server_launch(const RolloutServerArgs& a, hipStream_t stream);
 

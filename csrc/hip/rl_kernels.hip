@@ -305,7 +305,8 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
                                                   __hip_bfloat16* __restrict__ wbf16, const float* __restrict__ hp,
                                                   float grad_scale, int64_t n, const int64_t* __restrict__ step_ctr,
                                                   int64_t* bump, int nbump, uint32_t* done,
-                                                  const float* __restrict__ scale_ptr, int64_t* bump_next) {
+                                                  const float* __restrict__ scale_ptr, int64_t* bump_next,
+                                                  __hip_bfloat16* __restrict__ wlo) {
   // step: hp[5], or (device step counter + 1) when the counter is given (graph-friendly)
   // scale_ptr (optional): a device-side factor, e.g. the global-norm clip coefficient of K6b
   if (scale_ptr) grad_scale *= scale_ptr[0];
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ master, f
     bump = nullptr;
   }
   const int64_t tid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, nthr = int64_t(gridDim.x) * blockDim.x;
-  adam_span<TG, VEC, U>(master, m1, m2, grad, wbf16, grad_scale, c, tid, nthr, n);
+  adam_span<TG, VEC, U>(master, m1, m2, grad, wbf16, grad_scale, c, tid, nthr, n, wlo);
   last_block_bump(bump, nbump, done);
 }
 
@@ -328,12 +329,13 @@ int bump_done_words() { return kBumpWords; }
 
 void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_bf16, void* wbf16, const float* hp,
                float grad_scale, int64_t n, hipStream_t stream, const int64_t* step_ctr, int64_t* bump, int nbump,
-               uint32_t* done, const float* scale_ptr, int max_blocks, int64_t* bump_next) {
+               uint32_t* done, const float* scale_ptr, int max_blocks, int64_t* bump_next, void* wlo) {
   if (n <= 0) return;
+  if (wlo && !wbf16) throw std::invalid_argument("adam_flat: the split lo plane needs the hi plane (wbf16)");
   if (bump_next && (!bump || nbump <= 0)) throw std::invalid_argument("adam_flat: bump_next needs bump / nbump");
   auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
   const bool vec = al(master, 16) && al(m1, 16) && al(m2, 16) && al(grad, grad_bf16 ? 8 : 16) &&
-                   (wbf16 == nullptr || al(wbf16, 8));
+                   (wbf16 == nullptr || al(wbf16, 8)) && (wlo == nullptr || al(wlo, 8));
   // groups of 4 per lane per loop trip (vector path), RMM_ADAM_UNROLL=1/2/4, read once. Default 2:
   // 7.8-8.0 us vs 8.8 us per launch at 1M params with U=1 on MI355X (benchmarks/bench_adam.py,
   // profiles/adam_unroll_r3.txt: half the workgroups, two groups of loads in flight per lane);
@@ -350,7 +352,7 @@ void adam_flat(float* master, float* m1, float* m2, const void* grad, bool grad_
   auto go = [&](auto kern, const auto* g) {
     hipLaunchKernelGGL(kern, dim3(uint32_t(blocks)), dim3(256), 0, stream, master, m1, m2, g,
                        static_cast<__hip_bfloat16*>(wbf16), hp, grad_scale, n, step_ctr, bump, nbump, done,
-                       scale_ptr, bump_next);
+                       scale_ptr, bump_next, static_cast<__hip_bfloat16*>(wlo));
   };
   auto dispatch = [&](const auto* g) {
     using TG = std::remove_const_t<std::remove_pointer_t<decltype(g)>>;

@@ -1,0 +1,1269 @@
+// Precision-matched (fp32-level) twins of the PPO SGD-step and rollout-step kernels, on the bf16 MFMA
+// through split-bf16 operands (x3_device.h): K10x (Nature-CNN trunk fwd / bwd), K13x (split-K dense),
+// K15x (heads + PPO loss + dheads + dpre), K12x (dense + heads backward), K16x (heads + sampling).
+//
+// Parity target: the reference trains PPO in fp32 torch (rllib/algorithms/ppo/ppo_torch_policy.py:70,
+// rllib/models/torch/visionnet.py). Here every tensor is fp32-equivalent: weights are the fp32 master
+// (carried to the kernels as its split pair), activations / activation gradients are split pairs
+// (≈17 significant bits), products use hi*hi + hi*lo + lo*hi with fp32 accumulation, gradients are
+// reduced and stored in fp32, the loss and the optimizer run in fp32. The bf16 learner rounds
+// activations, gradients and head outputs to 8 significant bits instead.
+//
+// Layout changes vs the bf16 kernels (the split pairs double the LDS images):
+//   * K10x fwd: one workgroup of 8 waves per CU loops over frames (the full bf16 frame image,
+//     h1 hi/lo, W1 hi/lo and W2 hi/lo = 149 KB of LDS), next frame's loads in flight;
+//   * K10x bwd: conv2's backward (dW2, db2, dh1 -> dpre1, db1; 76 KB, two workgroups per CU) and
+//     conv1's weight gradient (space-to-depth frame + dpre1; 145 KB) are two launches; dpre1 goes
+//     through HBM as a split pair;
+//   * K12x: 64-row chunks single-buffered in LDS with the next chunk's loads in registers (the bf16
+//     K12 double-buffers and keeps the whole dx block in LDS), dx stored per chunk.
+// MFMA 16x16x32 bf16 maps: lane l holds A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15];
+// C/D col l&15, row 4(l>>4)+i.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+#include "dense_device.h"
+#include "kernels.h"
+#include "trunk_device.h"
+#include "x3_device.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+namespace rmm {
+namespace hip {
+namespace x3 {
+
+using trunk::C0;
+using trunk::C1;
+using trunk::C2;
+using trunk::FrameRegs;
+using trunk::H0;
+using trunk::H1;
+using trunk::H1P_ELEMS;
+using trunk::H2;
+using trunk::NP1;
+using trunk::NP2;
+using trunk::NP2P;
+using trunk::P0;
+using trunk::P1;
+using trunk::W1_PITCH;
+using trunk::W2_PITCH;
+using trunk::WeightRegs;
+using trunk::WStrides;
+
+// ================================================================ K10x forward
+constexpr int NTF = 512;  // 8 waves (1024 threads cap a lane at 128 VGPRs: the W1 / W2 pair fragments spilled)
+constexpr int FIMG = P0 * P0 * C0;  // the whole padded HWC frame as bf16 (exact for 0..255)
+
+// frame words in registers -> bf16 HWC image interior (padded row y+2, column x+2)
+template <int NT>
+__device__ __forceinline__ void frame_image_store(const FrameRegs<NT>& f, unsigned short* img) {
+  constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int o = threadIdx.x + NT * k;
+    if (o < NW) {
+      const int y = o / 21, xw = o - y * 21;
+      uint32_t w[8];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t c0 = __float_as_uint(float((f.v[k][0] >> (8 * q)) & 0xffu));
+        const uint32_t c1 = __float_as_uint(float((f.v[k][1] >> (8 * q)) & 0xffu));
+        const uint32_t c2 = __float_as_uint(float((f.v[k][2] >> (8 * q)) & 0xffu));
+        const uint32_t c3 = __float_as_uint(float((f.v[k][3] >> (8 * q)) & 0xffu));
+        w[2 * q] = trunk::bf16pair(c0, c1);
+        w[2 * q + 1] = trunk::bf16pair(c2, c3);
+      }
+      uint4* d = reinterpret_cast<uint4*>(img + ((y + 2) * P0 + 4 * xw + 2) * C0);
+      d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+  }
+}
+// zero the 2-pixel border of the bf16 image (rows 0, 1, 86, 87; columns 0, 1, 86, 87)
+__device__ __forceinline__ void zero_image_border(unsigned short* img) {
+  uint2* f = reinterpret_cast<uint2*>(img);  // one uint2 = one pixel (4 bf16)
+  constexpr int NROW = 4 * P0, NCOL = (P0 - 4) * 4;
+  for (int i = threadIdx.x; i < NROW + NCOL; i += blockDim.x) {
+    int y, x;
+    if (i < NROW) {
+      const int r = i / P0;
+      y = r < 2 ? r : r + (P0 - 4);
+      x = i - r * P0;
+    } else {
+      const int j = i - NROW, c = j & 3;
+      y = 2 + (j >> 2);
+      x = c < 2 ? c : c + (P0 - 4);
+    }
+    f[y * P0 + x] = make_uint2(0u, 0u);
+  }
+}
+
+// grid = G workgroups, each loops over frames b = blockIdx.x, +G, ... (push mode: G = B, one frame each)
+__global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
+    const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
+    int64_t B, CPair W1, WStrides w1, CPair b1, CPair W2, WStrides w2, CPair b2, Pair h1_out, Pair h2_out,
+    uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t) {
+  __shared__ __attribute__((aligned(16))) unsigned short img[FIMG];
+  __shared__ __attribute__((aligned(16))) unsigned short h1h[H1P_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short h1l[H1P_ELEMS];
+  __shared__ __attribute__((aligned(16))) unsigned short w1h[C1 * W1_PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short w1l[C1 * W1_PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short w2h[C2 * W2_PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short w2l[C2 * W2_PITCH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t G = gridDim.x;
+  const int64_t* idx = trunk::window(idx0, ctr, period, B);
+  constexpr int64_t FB = C0 * H0 * H0;
+
+  // prologue: weight loads (L2), then the first frame's HBM loads, then zeroing and staging
+  WeightRegs<NTF, C1, C0, 8> r1h, r1l;
+  WeightRegs<NTF, C2, C1, 4> r2h, r2l;
+  trunk::weight_issue(W1.hi, w1, r1h);
+  trunk::weight_issue(W1.lo, w1, r1l);
+  trunk::weight_issue(W2.hi, w2, r2h);
+  trunk::weight_issue(W2.lo, w2, r2l);
+  FrameRegs<NTF> fr;
+  int64_t b = blockIdx.x;
+  if (push_stack)
+    trunk::frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
+  else
+    trunk::frame_issue<NTF>(obs + (idx ? idx[b] : b) * FB, fr);
+  const float bias1 = join(b1, r), bias2[2] = {join(b2, r), join(b2, 16 + r)};
+  zero_image_border(img);
+  trunk::zero_lds(h1h, H1P_ELEMS * 2);
+  trunk::zero_lds(h1l, H1P_ELEMS * 2);
+  trunk::weight_store(r1h, W1.hi, w1, w1h, W1_PITCH);
+  trunk::weight_store(r1l, W1.lo, w1, w1l, W1_PITCH);
+  trunk::weight_store(r2h, W2.hi, w2, w2h, W2_PITCH);
+  trunk::weight_store(r2l, W2.lo, w2, w2l, W2_PITCH);
+  if (push_stack)
+    trunk::frame_push_store<NTF>(fr, push_stack + b * FB, push_rows ? push_rows + (push_t[0] * B + b) * FB : nullptr);
+
+  for (; b < B; b += G) {
+    frame_image_store<NTF>(fr, img);
+    __syncthreads();  // image (+ first frame: border / h1 zeros, weights); the previous conv2 is done
+    if (b + G < B) trunk::frame_issue<NTF>(obs + (idx ? idx[b + G] : b + G) * FB, fr);  // in flight meanwhile
+
+    // ---- conv1: M = 441 positions (28 tiles) x N = 16 x K = 256 (k = ky, kx, ci); frame exact -> 2 MFMAs
+    for (int mt = wave; mt < 28; mt += NTF / 64) {
+      const int p = min(mt * 16 + r, NP1 - 1);
+      const int oy = p / H1, ox = p - oy * H1;
+      Acc acc = acc0();
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const bf16x8 a = ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]);
+        const int wo = r * W1_PITCH + (s * 8 + 2 * g) * 4;
+        mma2a(acc, a, ld8(&w1h[wo]), ld8(&w1l[wo]));
+      }
+      const f32x4 t = total(acc);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int q = mt * 16 + 4 * g + i;
+        if (q < NP1) {
+          const float v = fmaxf(t[i] * (1.0f / 255.0f) + bias1, 0.f);
+          const int y = q / H1, x = q - y * H1;
+          unsigned short hh, hl;
+          split(v, hh, hl);
+          const int o = ((y + 2) * P1 + (x + 2)) * C1 + r;
+          h1h[o] = hh;
+          h1l[o] = hl;
+          if (h1_out.hi) {
+            const int64_t go = (b * NP1 + q) * C1 + r;
+            h1_out.hi[go] = hh;
+            h1_out.lo[go] = hl;
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- conv2: 8 M-tiles x 2 N-tiles = 16 jobs over the waves, K = 256 (pixel pp = 2s + (g>>1), ci half g&1)
+    for (int job = wave; job < 16; job += NTF / 64) {
+      const int mt = job >> 1, nt = job & 1;
+      const int q = min(mt * 16 + r, NP2 - 1);
+      const int oy = q / H2, ox = q - oy * H2;
+      Acc acc = acc0();
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
+        const int ao = ((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1);
+        const int wo = (nt * 16 + r) * W2_PITCH + pp * 16 + 8 * (g & 1);
+        mma3(acc, ld8(&h1h[ao]), ld8(&h1l[ao]), ld8(&w2h[wo]), ld8(&w2l[wo]));
+      }
+      const f32x4 t = total(acc);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int qq = mt * 16 + 4 * g + i;
+        if (qq < NP2) store1(h2_out, (b * NP2 + qq) * C2 + nt * 16 + r, fmaxf(t[i] + bias2[nt], 0.f));
+      }
+    }
+  }
+}
+
+// ================================================================ K10x backward, launch 1: conv2
+// Per frame: dpre2 = dh2 * [h2 > 0] (db2), dW2 += dpre2ᵀ im2col(h1), dh1 = conv2ᵀ(dpre2) by stride-parity
+// class, dpre1 = dh1 * [h1 > 0] (db1) -> HBM (split pair [B][441][16], read by launch 2).
+// Per-workgroup fp32 partial: [dW2 32x256 (k = ky, kx, ci)][db2 32][db1 16].
+constexpr int NTB = 512;
+constexpr int DP2_PITCH = NP2P + 8, D2W = 12;
+constexpr int PART2 = C2 * 256 + C2 + C1;
+constexpr int B1_NH1 = NP1 * 2, B1_PH1 = (B1_NH1 + NTB - 1) / NTB;  // 882 x 16 B per plane
+constexpr int B1_NH2 = NP2 * 4, B1_PH2 = (B1_NH2 + NTB - 1) / NTB;  // 484 x 16 B per plane
+static_assert(B1_PH2 == 1, "one h2 / dh2 chunk per thread");
+
+struct B1Regs {
+  u16x8 h1h[B1_PH1], h1l[B1_PH1], h2[B1_PH2], dh[B1_PH2], dl[B1_PH2];
+};
+__device__ __forceinline__ void b1_issue(int64_t bb, CPair h1, const unsigned short* __restrict__ h2hi, CPair dh2,
+                                         B1Regs& R) {
+#pragma unroll
+  for (int k = 0; k < B1_PH1; k++) {
+    const int v = min(int(threadIdx.x) + NTB * k, B1_NH1 - 1);
+    const int64_t o = (bb * NP1 + (v >> 1)) * C1 + 8 * (v & 1);
+    R.h1h[k] = *reinterpret_cast<const u16x8*>(&h1.hi[o]);
+    R.h1l[k] = *reinterpret_cast<const u16x8*>(&h1.lo[o]);
+  }
+  const int v = min(int(threadIdx.x), B1_NH2 - 1);
+  const int64_t o = (bb * NP2 + (v >> 2)) * C2 + 8 * (v & 3);
+  R.h2[0] = *reinterpret_cast<const u16x8*>(&h2hi[o]);
+  R.dh[0] = *reinterpret_cast<const u16x8*>(&dh2.hi[o]);
+  R.dl[0] = *reinterpret_cast<const u16x8*>(&dh2.lo[o]);
+}
+
+__global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStrides w2, CPair h1,
+                                                      const unsigned short* __restrict__ h2hi, CPair dh2,
+                                                      Pair dpre1, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) unsigned short h1s[2 * H1P_ELEMS];      // hi plane, lo plane
+  __shared__ __attribute__((aligned(16))) unsigned short dp2[2 * D2W * D2W * C2];   // [plane][oy*12+ox][co2]
+  __shared__ __attribute__((aligned(16))) unsigned short dp2t[2 * C2 * DP2_PITCH];  // [plane][co2][kperm(q)]
+  __shared__ float red[8 * 64];
+  static_assert(2 * C2 * W2_PITCH <= 2 * H1P_ELEMS, "W2 staging aliases the h1 tile");
+  unsigned short* h1hs = h1s;
+  unsigned short* h1ls = h1s + H1P_ELEMS;
+  unsigned short* w2hs = h1s;                   // staging only (read into registers before the loop)
+  unsigned short* w2ls = h1s + C2 * W2_PITCH;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  constexpr int DPL = D2W * D2W * C2, DTL = C2 * DP2_PITCH;
+
+  WeightRegs<NTB, C2, C1, 4> wrh, wrl;
+  trunk::weight_issue(W2.hi, w2, wrh);
+  trunk::weight_issue(W2.lo, w2, wrl);
+  B1Regs R;
+  if (int64_t(blockIdx.x) < B) b1_issue(blockIdx.x, h1, h2hi, dh2, R);
+  trunk::zero_lds(dp2, 2 * DPL * 2);
+  trunk::zero_lds(dp2t, 2 * DTL * 2);
+  trunk::weight_store(wrh, W2.hi, w2, w2hs, W2_PITCH);
+  trunk::weight_store(wrl, W2.lo, w2, w2ls, W2_PITCH);
+  // dh1 = conv2ᵀ(dpre2): waves 2c, 2c+1 own stride-parity class c = (py, px); taps t = (ty, tx)
+  const int cls = wave >> 1, half = wave & 1;
+  const int py = cls >> 1, px = cls & 1;
+  const int nrow = py ? 10 : 11, ncol = px ? 10 : 11, ncls = nrow * ncol;
+  const uint32_t cdiv = px ? 6554u : 5958u;  // m / ncol for m < 200 as multiply-shift
+  __syncthreads();
+  bf16x8 wth[4], wtl[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+    u16x8 vh, vl;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      vh[j] = w2hs[(8 * g + j) * W2_PITCH + (ky * 4 + kx) * 16 + r];
+      vl[j] = w2ls[(8 * g + j) * W2_PITCH + (ky * 4 + kx) * 16 + r];
+    }
+    wth[t] = as_bf(vh);
+    wtl[t] = as_bf(vl);
+  }
+  __syncthreads();  // the W2 staging (aliasing the h1 tile) is read
+  trunk::zero_lds(h1s, 2 * H1P_ELEMS * 2);
+  Acc aw2[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) aw2[0][i] = aw2[1][i] = acc0();
+  float db1 = 0.f, db2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __syncthreads();
+
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    // ---- P0: h1 -> padded tile planes, dpre2 (both layouts, both planes) + db2
+#pragma unroll
+    for (int k = 0; k < B1_PH1; k++) {
+      const int v = threadIdx.x + NTB * k;
+      if (v < B1_NH1) {
+        const int p = v >> 1, y = p / H1, x = p - y * H1;
+        const int o = ((y + 2) * P1 + (x + 2)) * C1 + 8 * (v & 1);
+        *reinterpret_cast<u16x8*>(&h1hs[o]) = R.h1h[k];
+        *reinterpret_cast<u16x8*>(&h1ls[o]) = R.h1l[k];
+      }
+    }
+    if (int(threadIdx.x) < B1_NH2) {
+      const int v = threadIdx.x;
+      const int q = v >> 2, c0 = 8 * (v & 3), oy = q / H2, ox = q - oy * H2;
+      u16x8 oh, ol;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const unsigned short hj = R.h2[0][j];
+        const bool on = hj != 0 && !(hj & 0x8000);
+        oh[j] = on ? R.dh[0][j] : static_cast<unsigned short>(0);
+        ol[j] = on ? R.dl[0][j] : static_cast<unsigned short>(0);
+        db2[j] += bf2f(oh[j]) + bf2f(ol[j]);
+        dp2t[(c0 + j) * DP2_PITCH + trunk::kperm(q)] = oh[j];
+        dp2t[DTL + (c0 + j) * DP2_PITCH + trunk::kperm(q)] = ol[j];
+      }
+      *reinterpret_cast<u16x8*>(&dp2[(oy * D2W + ox) * C2 + c0]) = oh;
+      *reinterpret_cast<u16x8*>(&dp2[DPL + (oy * D2W + ox) * C2 + c0]) = ol;
+    }
+    __syncthreads();
+    if (b + gridDim.x < B) b1_issue(b + gridDim.x, h1, h2hi, dh2, R);  // next frame: in flight through P1
+
+    // ---- P1a: dW2[co2][k = (ky, kx, ci)] += Σ_q dpre2[q][co2] · h1[2oy+ky][2ox+kx][ci]
+#pragma unroll
+    for (int s = 0; s < NP2P / 32; s++) {
+      const int ao0 = r * DP2_PITCH + 32 * s + 8 * g, ao1 = (16 + r) * DP2_PITCH + 32 * s + 8 * g;
+      const bf16x8 a0h = ld8(&dp2t[ao0]), a0l = ld8(&dp2t[DTL + ao0]);
+      const bf16x8 a1h = ld8(&dp2t[ao1]), a1l = ld8(&dp2t[DTL + ao1]);
+      int qoff[8];
+      {
+        const int q0 = 32 * s + g;
+        int oy = q0 / H2, ox = q0 - oy * H2;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          qoff[j] = (q0 + 4 * j < NP2) ? (oy * 2 * P1 + ox * 2) * C1 : 0;  // dpre2 is 0 there
+          ox += 4;
+          if (ox >= H2) {
+            ox -= H2;
+            oy++;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int k = (wave + 8 * i) * 16 + r;
+        const int ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+        const int base = (ky * P1 + kx) * C1 + ci;
+        u16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          bh[j] = h1hs[base + qoff[j]];
+          bl[j] = h1ls[base + qoff[j]];
+        }
+        mma3(aw2[0][i], a0h, a0l, as_bf(bh), as_bf(bl));
+        mma3(aw2[1][i], a1h, a1l, as_bf(bh), as_bf(bl));
+      }
+    }
+    // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 -> dpre1 (HBM), db1
+    for (int mt = half; mt * 16 < ncls; mt += 2) {
+      const int m = min(mt * 16 + r, ncls - 1);
+      const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
+      Acc acc = acc0();
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
+        const int o = (oy * D2W + ox) * C2 + 8 * g;
+        mma3(acc, ld8(&dp2[o]), ld8(&dp2[DPL + o]), wth[t], wtl[t]);
+      }
+      const f32x4 tt = total(acc);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int mm = mt * 16 + 4 * g + i;
+        if (mm < ncls) {
+          const int aa = int((uint32_t(mm) * cdiv) >> 16), cc = mm - aa * ncol;
+          const int y = 2 * aa + py, x = 2 * cc + px;
+          const unsigned short hv = h1hs[((y + 2) * P1 + (x + 2)) * C1 + r];
+          const float d = (hv != 0 && !(hv & 0x8000)) ? tt[i] : 0.f;
+          unsigned short dh, dl;
+          split(d, dh, dl);
+          db1 += bf2f(dh) + bf2f(dl);
+          const int64_t go = (b * NP1 + y * H1 + x) * C1 + r;
+          dpre1.hi[go] = dh;
+          dpre1.lo[go] = dl;
+        }
+      }
+    }
+    __syncthreads();  // tiles free for the next frame
+  }
+
+  float* out = partial + int64_t(blockIdx.x) * PART2;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int col = (wave + 8 * i) * 16 + r;
+    const f32x4 t0 = total(aw2[0][i]), t1 = total(aw2[1][i]);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int row = 4 * g + e;
+      out[row * 256 + col] = t0[e];
+      out[(16 + row) * 256 + col] = t1[e];
+    }
+  }
+  // db2: thread t holds co2 = 8(t&3)+j (threads < 484 only touched it); db1: lanes r, r+16.. share ci = r
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    float v = db2[j];
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 4) red[wave * 64 + lane * 8 + j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int co = threadIdx.x, q4 = co >> 3, j = co & 7;
+    float s = 0.f;
+    for (int w = 0; w < 8; w++) s += red[w * 64 + q4 * 8 + j];
+    out[C2 * 256 + co] = s;
+  }
+  __syncthreads();
+  db1 += __shfl_xor(db1, 16);
+  db1 += __shfl_xor(db1, 32);
+  if (lane < 16) red[wave * 16 + lane] = db1;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float s = 0.f;
+    for (int w = 0; w < 8; w++) s += red[w * 16 + threadIdx.x];
+    out[C2 * 256 + C2 + threadIdx.x] = s;
+  }
+}
+
+// ================================================================ K10x backward, launch 2: conv1 dW1
+// dW1 in space-to-depth form (see conv_kernels.hip P2): D[(a, b, c)][co] = Σ_t st[c][t] · dpre1_b[co][t + (1-a)*24]
+// with the frame exact in bf16 (2 MFMAs) and dpre1 a split pair (two shifted copies b = 0, 1 per plane).
+using trunk::ST_C;
+using trunk::ST_CP;
+using trunk::ST_W;
+constexpr int DB_CP = 24 * ST_W + 8, DB_B = 16 * DB_CP;
+constexpr int KSTEPS1 = (22 * ST_W + 31) / 32;
+constexpr int PART1 = C1 * 256;
+constexpr int B2_N = NP1 * 2, B2_PER = (B2_N + NTB - 1) / NTB;  // 882 x 16 B per plane
+
+__global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restrict__ obs,
+                                                        const int64_t* __restrict__ idx0,
+                                                        const int64_t* __restrict__ ctr, int64_t period, int64_t B,
+                                                        CPair dpre1, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) unsigned short st[ST_C * ST_CP];    // space-to-depth frame (exact)
+  __shared__ __attribute__((aligned(16))) unsigned short dp[4 * DB_B];        // [hi b0][hi b1][lo b0][lo b1]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t* idx = trunk::window(idx0, ctr, period, B);
+  FrameRegs<NTB> fr;
+  u16x8 vh[B2_PER], vl[B2_PER];
+  auto issue = [&](int64_t bb) {
+    trunk::frame_issue<NTB>(obs + (idx ? idx[bb] : bb) * (C0 * H0 * H0), fr);
+#pragma unroll
+    for (int k = 0; k < B2_PER; k++) {
+      const int v = min(int(threadIdx.x) + NTB * k, B2_N - 1);
+      const int64_t o = (bb * NP1 + (v >> 1)) * C1 + 8 * (v & 1);
+      vh[k] = *reinterpret_cast<const u16x8*>(&dpre1.hi[o]);
+      vl[k] = *reinterpret_cast<const u16x8*>(&dpre1.lo[o]);
+    }
+  };
+  if (int64_t(blockIdx.x) < B) issue(blockIdx.x);
+  trunk::zero_lds(st, ST_C * ST_CP * 2);
+  trunk::zero_lds(dp, 4 * DB_B * 2);
+  Acc aw[2];
+  aw[0] = aw[1] = acc0();
+  __syncthreads();
+
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    trunk::frame_store_s2d<NTB>(fr, st);
+#pragma unroll
+    for (int k = 0; k < B2_PER; k++) {
+      const int v = threadIdx.x + NTB * k;
+      if (v < B2_N) {
+        const int p = v >> 1, c0 = 8 * (v & 1), y = p / H1, x = p - y * H1;
+        const int o = (y + 1) * ST_W + x;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int e = (c0 + j) * DB_CP + o;
+          dp[e] = vh[k][j];
+          dp[DB_B + e + 1] = vh[k][j];
+          dp[2 * DB_B + e] = vl[k][j];
+          dp[3 * DB_B + e + 1] = vl[k][j];
+        }
+      }
+    }
+    __syncthreads();
+    if (b + gridDim.x < B) issue(b + gridDim.x);
+    {
+      const int cb = wave & 3, a = wave >> 2;
+      const unsigned short* sa = st + (16 * cb + r) * ST_CP + 8 * g;
+      const unsigned short* d0 = dp + r * DB_CP + (1 - a) * ST_W + 8 * g;
+#pragma unroll
+      for (int s = 0; s < KSTEPS1; s++) {
+        const bf16x8 av = ld8(sa + 32 * s);
+        mma2a(aw[0], av, ld8(d0 + 32 * s), ld8(d0 + 2 * DB_B + 32 * s));
+        mma2a(aw[1], av, ld8(d0 + DB_B + 32 * s), ld8(d0 + 3 * DB_B + 32 * s));
+      }
+    }
+    __syncthreads();
+  }
+  // tile b holds D[m = 4g+e][co = r], channel c = 16cb + m -> ry = cb, rx = g, ci = e; ky = 4a+ry, kx = 4b+rx
+  float* out = partial + int64_t(blockIdx.x) * PART1;
+#pragma unroll
+  for (int bb = 0; bb < 2; bb++) {
+    const f32x4 t = total(aw[bb]);
+    const int ky = 4 * (wave >> 2) + (wave & 3), kx = 4 * bb + g;
+#pragma unroll
+    for (int e = 0; e < 4; e++) out[r * 256 + ky * 32 + kx * 4 + e] = t[e] * (1.0f / 255.0f);
+  }
+}
+
+// ================================================================ K10x reduce
+// Sum the two backward launches' per-workgroup partials in a fixed order into fp32 gradients in the
+// parameters' memory order (deterministic). Output index e as conv_kernels.hip: [dW1 4096][dW2 8192][db1 16][db2 32].
+constexpr int PARTX = C1 * 256 + C2 * 256 + C1 + C2;
+constexpr int RED_SLICES = 8, RED_BATCH = 16;
+__device__ __forceinline__ float* trunk_grad_dst_f32(int e, float* dW1, WStrides w1, float* db1, float* dW2,
+                                                     WStrides w2, float* db2) {
+  if (e < C1 * 256) {
+    const int co = e >> 8, k = e & 255, ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
+    return &dW1[co * w1.s0 + ci * w1.s1 + ky * w1.s2 + kx * w1.s3];
+  }
+  if (e < C1 * 256 + C2 * 256) {
+    const int f = e - C1 * 256, co = f >> 8, k = f & 255, ky = k >> 6, kx = (k >> 4) & 3, ci = k & 15;
+    return &dW2[co * w2.s0 + ci * w2.s1 + ky * w2.s2 + kx * w2.s3];
+  }
+  if (e < C1 * 256 + C2 * 256 + C1) return &db1[e - C1 * 256 - C2 * 256];
+  return &db2[e - C1 * 256 - C2 * 256 - C1];
+}
+__global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict__ part1, int G1,
+                                                         const float* __restrict__ part2, int G2, float* dW1,
+                                                         WStrides w1, float* db1, float* dW2, WStrides w2, float* db2) {
+  __shared__ float red[RED_SLICES][64];
+  const int c = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + c;
+  // source: dW1 from the conv1 launch (stride PART1), the rest from the conv2 launch: its layout is
+  // [dW2][db2][db1], the output order [dW2][db1][db2]
+  const float* src = nullptr;
+  int G = 0, stride = 0;
+  if (e < C1 * 256) {
+    src = part1 + e, G = G1, stride = PART1;
+  } else if (e < PARTX) {
+    const int f = e - C1 * 256;
+    const int o = f < C2 * 256 ? f : (f < C2 * 256 + C1 ? C2 * 256 + C2 + (f - C2 * 256) : C2 * 256 + (f - C2 * 256 - C1));
+    src = part2 + o, G = G2, stride = PART2;
+  }
+  float s = 0.f;
+  if (src) {
+    for (int g0 = slice; g0 < G; g0 += RED_SLICES * RED_BATCH) {
+      float v[RED_BATCH];
+#pragma unroll
+      for (int j = 0; j < RED_BATCH; j++) v[j] = src[int64_t(min(g0 + RED_SLICES * j, G - 1)) * stride];
+#pragma unroll
+      for (int j = 0; j < RED_BATCH; j++)
+        if (g0 + RED_SLICES * j < G) s += v[j];
+    }
+  }
+  red[slice][c] = s;
+  __syncthreads();
+  if (slice == 0 && e < PARTX) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
+    *trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2) = t;
+  }
+}
+
+}  // namespace x3
+
+// ---------------------------------------------------------------- host launchers (K10x)
+static trunk::WStrides wsx(const int64_t* s) { return trunk::WStrides{s[0], s[1], s[2], s[3]}; }
+static x3::CPair cp(const X3In& p) {
+  return x3::CPair{static_cast<const unsigned short*>(p.hi), static_cast<const unsigned short*>(p.lo)};
+}
+static x3::Pair pp(const X3Out& p) { return x3::Pair{static_cast<unsigned short*>(p.hi), static_cast<unsigned short*>(p.lo)}; }
+
+static void check_pair(const X3In& p, const char* what) {
+  if ((p.hi == nullptr) != (p.lo == nullptr)) throw std::invalid_argument(std::string(what) + ": hi and lo planes");
+}
+
+int x3_trunk_fwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 256))); }
+
+void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W1,
+                  const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h1, X3Out h2,
+                  hipStream_t stream) {
+  if (B <= 0) return;
+  if (period <= 0) period = 1;
+  for (const X3In* p : {&W1, &b1, &W2, &b2})
+    if (!p->hi || !p->lo) throw std::invalid_argument("x3_trunk_fwd: weights need hi and lo planes");
+  if (!h2.hi || !h2.lo || (h1.hi == nullptr) != (h1.lo == nullptr))
+    throw std::invalid_argument("x3_trunk_fwd: h2 (and h1) need hi and lo planes");
+  hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(x3_trunk_fwd_groups(B))), dim3(x3::NTF), 0, stream, obs, idx,
+                     ctr, period, B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), pp(h1), pp(h2), nullptr,
+                     nullptr, nullptr, nullptr);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
+                       X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
+                       hipStream_t stream) {
+  if (B <= 0) return;
+  if (stack == nullptr || new_frames == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: stack and new frames");
+  if (rows != nullptr && t_ptr == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: rows need the row counter");
+  if ((reinterpret_cast<uintptr_t>(stack) | reinterpret_cast<uintptr_t>(new_frames) | reinterpret_cast<uintptr_t>(rows)) & 3)
+    throw std::invalid_argument("x3_trunk_fwd_push: buffers must be 4-byte aligned");
+  for (const X3In* p : {&W1, &b1, &W2, &b2})
+    if (!p->hi || !p->lo) throw std::invalid_argument("x3_trunk_fwd_push: weights need hi and lo planes");
+  if (!h2.hi || !h2.lo) throw std::invalid_argument("x3_trunk_fwd_push: h2 needs hi and lo planes");
+  // push mode: one frame per workgroup (each workgroup shifts its own env's stack)
+  hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(B)), dim3(x3::NTF), 0, stream, nullptr, nullptr, nullptr,
+                     int64_t(1), B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), x3::Pair{}, pp(h2), stack,
+                     new_frames, rows, t_ptr);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+int x3_conv2_bwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 512))); }
+int x3_conv1_wgrad_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 256))); }
+int64_t x3_trunk_partial_floats(int64_t B) {
+  return int64_t(x3_conv2_bwd_groups(B)) * x3::PART2 + int64_t(x3_conv1_wgrad_groups(B)) * x3::PART1;
+}
+
+void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W2,
+                  const int64_t* w2s, X3In h1, const void* h2hi, X3In dh2, X3Out dpre1, float* partial, float* dW1,
+                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream) {
+  if (B <= 0) return;
+  if (period <= 0) period = 1;
+  for (const X3In* p : {&W2, &h1, &dh2})
+    if (!p->hi || !p->lo) throw std::invalid_argument("x3_trunk_bwd: W2 / h1 / dh2 need hi and lo planes");
+  if (!dpre1.hi || !dpre1.lo || !h2hi || !partial) throw std::invalid_argument("x3_trunk_bwd: dpre1 / h2 / partial");
+  const int G2 = x3_conv2_bwd_groups(B), G1 = x3_conv1_wgrad_groups(B);
+  float* p2 = partial;                              // conv2 launch partials [G2][PART2]
+  float* p1 = partial + int64_t(G2) * x3::PART2;    // conv1 launch partials [G1][PART1]
+  hipLaunchKernelGGL(x3::k_conv2_bwd_x3, dim3(uint32_t(G2)), dim3(x3::NTB), 0, stream, B, cp(W2), wsx(w2s), cp(h1),
+                     static_cast<const unsigned short*>(h2hi), cp(dh2), pp(dpre1), p2);
+  RMM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(x3::k_conv1_wgrad_x3, dim3(uint32_t(G1)), dim3(x3::NTB), 0, stream, obs, idx, ctr, period, B,
+                     x3::CPair{static_cast<const unsigned short*>(dpre1.hi), static_cast<const unsigned short*>(dpre1.lo)},
+                     p1);
+  RMM_HIP_CHECK(hipGetLastError());
+  const int nred = (x3::PARTX + 63) / 64;
+  hipLaunchKernelGGL(x3::k_trunk_reduce_x3, dim3(nred), dim3(512), 0, stream, p1, G1, p2, G2, dW1, wsx(w1s), db1,
+                     dW2, wsx(w2s), db2);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace rmm
+
+// ================================================================ dense tail (K13x, K15x, K12x, K16x)
+namespace rmm {
+namespace hip {
+namespace x3 {
+
+constexpr int H = dense::H;
+
+// ---- K13x: split-K dense layer hidden_pre = x Wᵀ over split pairs -> fp32 partials part[S][M][N]
+// (no bias / ReLU: the consumer K15x / K16x sums the S slices, adds the bias, applies ReLU in fp32).
+// Unit = FM x FN 16x16 fragments per wave, the workgroup's 4 waves split the slice's k-steps and
+// combine through LDS in a fixed order (deterministic).
+template <int FM, int FN>
+__global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
+                                                           float* __restrict__ part) {
+  __shared__ f32x4 red[3][FM * FN][64];
+  const int lane = threadIdx.x & 63, kw = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int nt = N / (16 * FN);
+  const int64_t mt = (M + 16 * FM - 1) / (16 * FM);
+  const int64_t tiles = mt * nt, total_ = gridDim.x;
+  int64_t id = blockIdx.x;
+  if ((total_ & 7) == 0) id = (id & 7) * (total_ >> 3) + (id >> 3);  // XCD-contiguous runs
+  const int64_t sl = id / tiles, rem = id % tiles, tm = rem / nt, tn = rem % nt;
+  const int64_t m0 = tm * 16 * FM, n0 = tn * 16 * FN;
+  const int64_t steps = K / 32, lo = steps * sl / S, hi = steps * (sl + 1) / S;
+  int64_t xo[FM], wo[FN];
+#pragma unroll
+  for (int i = 0; i < FM; i++) xo[i] = min(m0 + 16 * i + r, M - 1) * K + 8 * g;
+#pragma unroll
+  for (int j = 0; j < FN; j++) wo[j] = (n0 + 16 * j + r) * K + 8 * g;
+  Acc acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; i++)
+#pragma unroll
+    for (int j = 0; j < FN; j++) acc[i][j] = acc0();
+  for (int64_t k = lo + kw; k < hi; k += 4) {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++) ah[i] = ld8(x.hi + xo[i] + k * 32), al[i] = ld8(x.lo + xo[i] + k * 32);
+#pragma unroll
+    for (int j = 0; j < FN; j++) bh[j] = ld8(w.hi + wo[j] + k * 32), bl[j] = ld8(w.lo + wo[j] + k * 32);
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+      for (int j = 0; j < FN; j++) mma3(acc[i][j], ah[i], al[i], bh[j], bl[j]);
+  }
+  if (kw > 0) {
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+      for (int j = 0; j < FN; j++) red[kw - 1][i * FN + j][lane] = total(acc[i][j]);
+  }
+  __syncthreads();
+  if (kw != 0) return;
+  float* out = part + (sl * M) * N + n0 + r;
+#pragma unroll
+  for (int i = 0; i < FM; i++)
+#pragma unroll
+    for (int j = 0; j < FN; j++) {
+      const f32x4 t = ((total(acc[i][j]) + red[0][i * FN + j][lane]) + red[1][i * FN + j][lane]) + red[2][i * FN + j][lane];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int64_t row = m0 + 16 * i + 4 * g + e;
+        if (row < M) out[row * N + 16 * j] = t[e];
+      }
+    }
+}
+
+// consumer prologue: a lane's 4 hidden values of row rr = ReLU(Σ_s part[s] + b) in fp32 (slice order)
+__device__ __forceinline__ void load_hidden4_x3(const float* __restrict__ hpart, int S, CPair hb, int64_t M,
+                                                int64_t rr, int lane, float (&hv)[4]) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* p = hpart + rr * H + 4 * lane;
+  for (int s = 0; s < S; s++) {
+    const float4 v = *reinterpret_cast<const float4*>(p + int64_t(s) * M * H);
+    a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
+  }
+  hv[0] = fmaxf(a.x + join(hb, 4 * lane), 0.f);
+  hv[1] = fmaxf(a.y + join(hb, 4 * lane + 1), 0.f);
+  hv[2] = fmaxf(a.z + join(hb, 4 * lane + 2), 0.f);
+  hv[3] = fmaxf(a.w + join(hb, 4 * lane + 3), 0.f);
+}
+
+// ---- K15x: heads + PPO loss statistics + dheads + dpre, one wave per row, all fp32 math
+// (dense_kernels.hip K15 with fp32 heads / gradients). Outputs as split pairs: dz [M, A1], dpre [M, 256]
+// and the hidden row hid [M, 256] (K12x reads them).
+template <int A1>
+__global__ __launch_bounds__(256) void k_heads_ppo_x3(const float* __restrict__ hpart, int S, CPair hb, CPair wh,
+                                                      CPair bh, const float* __restrict__ cols,
+                                                      const float* __restrict__ coef, float* __restrict__ acc,
+                                                      const float* __restrict__ gout, int64_t M, Pair dz, Pair dpre,
+                                                      Pair hid, const int64_t* __restrict__ cidx,
+                                                      const int64_t* __restrict__ ctr, int64_t period) {
+  constexpr int A = A1 - 1;
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  __shared__ float red[6][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) + wave;
+  const bool valid = row < M;
+  const int64_t rr = valid ? row : M - 1;
+  const int64_t crr = cidx ? (ctr ? cidx[(ctr[0] % period) * M + rr] : cidx[rr]) : rr;
+  const float* crow = cols + crr * (A + 4);
+  float cv[A + 4];
+#pragma unroll
+  for (int j = 0; j < A + 4; j++) cv[j] = crow[j];
+  float hv[4];
+  load_hidden4_x3(hpart, S, hb, M, rr, lane, hv);
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  __syncthreads();
+  const float gs = gout[0] / float(M);
+  if (valid) store4(hid, row * H + 4 * lane, hv);
+  float hd[A1];
+#pragma unroll
+  for (int a = 0; a < A1; a++) {
+    const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+    hd[a] = hv[0] * w.x + hv[1] * w.y + hv[2] * w.z + hv[3] * w.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int a = 0; a < A1; a++) hd[a] += __shfl_xor(hd[a], o, 64);
+#pragma unroll
+  for (int a = 0; a < A1; a++) hd[a] += bhs[a];
+  float s[6], g[A1];
+  dense::ppo_loss_row<A1, false>(hd, cv, coef[0], coef[1], coef[2], coef[3], coef[4], gs, valid && lane == 0, s, g);
+  if (valid) {
+    if (lane < A1) {
+      float gl = g[0];
+#pragma unroll
+      for (int j = 1; j < A1; j++)
+        if (lane == j) gl = g[j];
+      store1(dz, row * A1 + lane, gl);
+    }
+    float dp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < A1; a++) {
+      const float4 w = *reinterpret_cast<const float4*>(&whs[a * H + 4 * lane]);
+      dp[0] += g[a] * w.x, dp[1] += g[a] * w.y, dp[2] += g[a] * w.z, dp[3] += g[a] * w.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) dp[k] = hv[k] > 0.f ? dp[k] : 0.f;
+    store4(dpre, row * H + 4 * lane, dp);
+  }
+  if (lane == 0)
+    for (int k = 0; k < 6; k++) red[k][wave] = s[k];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float t = 0.f;
+    for (int k = 0; k < int(blockDim.x >> 6); k++) t += red[threadIdx.x][k];
+    atomicAdd(&acc[threadIdx.x], t);
+  }
+}
+
+// ---- K16x: heads + Gumbel-max sampling + rollout-row stores (+ step advance), fp32 head row
+template <int A1>
+__global__ __launch_bounds__(256) void k_heads_sample_x3(const float* __restrict__ hpart, int S, CPair hb, CPair wh,
+                                                         CPair bh, const int64_t* t_ptr, const int64_t* ctr,
+                                                         uint32_t seed, int64_t* __restrict__ act,
+                                                         float* __restrict__ logp, float* __restrict__ vf,
+                                                         float* __restrict__ lout, int64_t* __restrict__ act_now,
+                                                         int64_t B, unsigned int* __restrict__ done, int64_t* host_seq) {
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  const int lane = threadIdx.x & 63;
+  const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  float hv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (b < B) load_hidden4_x3(hpart, S, hb, B, b, lane, hv);
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  __syncthreads();
+  if (b < B) dense::heads_sample_row_pre<A1, false>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
+  if (done) {
+    __shared__ unsigned int last;
+    if (host_seq) __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+      int64_t* tw = const_cast<int64_t*>(t_ptr);
+      int64_t* cw = const_cast<int64_t*>(ctr);
+      *tw += 1;
+      if (cw != tw) *cw += 1;
+      atomicExch(done, 0u);
+      if (host_seq) __hip_atomic_store(host_seq, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+// single-workgroup K16x (B <= 16 R rows) with the step advance after a workgroup barrier (as k_heads_sample1)
+template <int A1, int R>
+__global__ __launch_bounds__(1024) void k_heads_sample1_x3(const float* __restrict__ hpart, int S, CPair hb, CPair wh,
+                                                           CPair bh, int64_t* t_ptr, int64_t* ctr, uint32_t seed,
+                                                           int64_t* __restrict__ act, float* __restrict__ logp,
+                                                           float* __restrict__ vf, float* __restrict__ lout,
+                                                           int64_t* __restrict__ act_now, int64_t B, int64_t* host_seq) {
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  constexpr int kWaves = 16;
+  const int lane = threadIdx.x & 63;
+  const int64_t b0 = threadIdx.x >> 6;
+  float hv[R][4];
+#pragma unroll
+  for (int q = 0; q < R; q++)
+    if (b0 + q * kWaves < B) load_hidden4_x3(hpart, S, hb, B, b0 + q * kWaves, lane, hv[q]);
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < R; q++)
+    if (b0 + q * kWaves < B)
+      dense::heads_sample_row_pre<A1, false>(hv[q], whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B,
+                                             b0 + q * kWaves, lane);
+  if (host_seq) __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *t_ptr = t + 1;
+    if (ctr != t_ptr) *ctr = int64_t(c) + 1;
+    if (host_seq) __hip_atomic_store(host_seq, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---- K12x: backward of hidden = ReLU(x Wᵀ + b), heads = hidden Whᵀ + bh over split pairs.
+// Column-block role (workgroup j < K/32): dx[:, J] (split pair, for the trunk backward) and
+// dW[:, J] (fp32) for J = [32j, 32j+32); head role (workgroup K/32): dWh, db, dbh (fp32).
+// 64-row chunks, each staged once into LDS (hi and lo planes); the next chunk's global loads are in
+// registers while the current chunk's MFMAs run; two barriers per chunk.
+constexpr int MC = 64, JB = 32, NT = 512;
+constexpr int DMP = H + 16;  // row pitch of the [m][h] images (transposed reads conflict-free)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+__device__ __forceinline__ bf16x8 tr8(const unsigned short* p0, const unsigned short* p1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+__device__ __forceinline__ uint4 keep_if(bool ok, uint4 v) {
+  return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
+}
+constexpr int IMG = MC * DMP;                      // one plane of a 64-row [m][h] chunk image
+constexpr int K12X_COLS = 2 * IMG + 2 * 2 * MC * 16 + 2 * 2 * H * 16;
+constexpr int K12X_HEAD = 4 * IMG + 2 * MC * 16;
+constexpr int K12X_LDS = K12X_COLS > K12X_HEAD ? K12X_COLS : K12X_HEAD;
+static_assert(K12X_LDS * 2 <= 160 * 1024, "K12x LDS");
+
+__device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t M, int64_t K, int64_t J0, Pair dx,
+                                          float* __restrict__ dw, unsigned short* lds) {
+  unsigned short* dm = lds;                       // [plane][m][DMP]
+  unsigned short* xs = lds + 2 * IMG;             // [plane][jt][m][16]
+  unsigned short* ws = xs + 2 * 2 * MC * 16;      // [plane][jt][h][16]  (setup)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int q = r >> 2, p = r & 3;
+  const int NC = int((M + MC - 1) / MC);
+  uint4 sdh[4], sdl[4], sxh, sxl;
+  auto load = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const int64_t o = min(m0 + row, M - 1) * H + 8 * pc;
+      sdh[k] = *reinterpret_cast<const uint4*>(&dpre.hi[o]);
+      sdl[k] = *reinterpret_cast<const uint4*>(&dpre.lo[o]);
+    }
+    const int row = (tid >> 2) & (MC - 1), pc = tid & 3;
+    const int64_t o = min(m0 + row, M - 1) * K + J0 + 8 * pc;
+    sxh = *reinterpret_cast<const uint4*>(&x.hi[o]);
+    sxl = *reinterpret_cast<const uint4*>(&x.lo[o]);
+  };
+  auto store = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const bool ok = m0 + row < M;
+      *reinterpret_cast<uint4*>(&dm[row * DMP + 8 * pc]) = keep_if(ok, sdh[k]);
+      *reinterpret_cast<uint4*>(&dm[IMG + row * DMP + 8 * pc]) = keep_if(ok, sdl[k]);
+    }
+    if (tid < MC * 4) {
+      const int row = tid >> 2, pc = tid & 3;
+      const bool ok = m0 + row < M;
+      const int o = ((pc >> 1) * MC + row) * 16 + 8 * (pc & 1);
+      *reinterpret_cast<uint4*>(&xs[o]) = keep_if(ok, sxh);
+      *reinterpret_cast<uint4*>(&xs[2 * MC * 16 + o]) = keep_if(ok, sxl);
+    }
+  };
+  {  // W[:, J] -> ws planes, then the Wᵀ fragments into registers
+    uint4 wvh[2], wvl[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int v = tid + NT * k, h = v >> 2, pc = v & 3;
+      wvh[k] = *reinterpret_cast<const uint4*>(&w.hi[int64_t(h) * K + J0 + 8 * pc]);
+      wvl[k] = *reinterpret_cast<const uint4*>(&w.lo[int64_t(h) * K + J0 + 8 * pc]);
+    }
+    load(0);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int v = tid + NT * k, h = v >> 2, pc = v & 3;
+      const int o = ((pc >> 1) * H + h) * 16 + 8 * (pc & 1);
+      *reinterpret_cast<uint4*>(&ws[o]) = wvh[k];
+      *reinterpret_cast<uint4*>(&ws[2 * H * 16 + o]) = wvl[k];
+    }
+  }
+  __syncthreads();
+  const int mt = wave >> 1, nt = wave & 1;
+  bf16x8 wfh[H / 32], wfl[H / 32];
+#pragma unroll
+  for (int s = 0; s < H / 32; s++) {
+    const unsigned short* p0 = &ws[(nt * H + 32 * s + 8 * g + q) * 16 + 4 * p];
+    wfh[s] = tr8(p0, p0 + 4 * 16);
+    wfl[s] = tr8(p0 + 2 * H * 16, p0 + 2 * H * 16 + 4 * 16);
+  }
+  Acc adw[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) adw[i][0] = adw[i][1] = acc0();
+
+  for (int c = 0; c < NC; c++) {
+    store(c);
+    __syncthreads();
+    if (c + 1 < NC) load(c + 1);  // in flight during this chunk's MFMAs
+    {  // dxᵀ tile: D[j][m] = Σ_h Wᵀ[j][h] dpre[m][h]
+      Acc a = acc0();
+      const int ro = (16 * mt + r) * DMP + 8 * g;
+#pragma unroll
+      for (int s = 0; s < H / 32; s++) mma3(a, wfh[s], wfl[s], ld8(&dm[ro + 32 * s]), ld8(&dm[IMG + ro + 32 * s]));
+      const int64_t row = int64_t(c) * MC + 16 * mt + r;
+      if (row < M) {
+        const f32x4 t = total(a);
+        const float v[4] = {t[0], t[1], t[2], t[3]};
+        store4(dx, row * K + J0 + 16 * nt + 4 * g, v);
+      }
+    }
+    // dW[h][j] += Σ_m dpre[m][h] x[m][j] (both operands by transposed reads)
+#pragma unroll
+    for (int ks = 0; ks < MC / 32; ks++) {
+      bf16x8 bxh[2], bxl[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; jt++) {
+        const unsigned short* p0 = &xs[(jt * MC + 32 * ks + 4 * g + q) * 16 + 4 * p];
+        bxh[jt] = tr8(p0, p0 + 16 * 16);
+        bxl[jt] = tr8(p0 + 2 * MC * 16, p0 + 2 * MC * 16 + 16 * 16);
+      }
+#pragma unroll
+      for (int hi = 0; hi < 2; hi++) {
+        const unsigned short* p0 = &dm[(32 * ks + 4 * g + q) * DMP + 16 * (wave + 8 * hi) + 4 * p];
+        const bf16x8 adh = tr8(p0, p0 + 16 * DMP), adl = tr8(p0 + IMG, p0 + IMG + 16 * DMP);
+        mma3(adw[hi][0], adh, adl, bxh[0], bxl[0]);
+        mma3(adw[hi][1], adh, adl, bxh[1], bxl[1]);
+      }
+    }
+    __syncthreads();  // chunk images free
+  }
+#pragma unroll
+  for (int hi = 0; hi < 2; hi++)
+#pragma unroll
+    for (int jt = 0; jt < 2; jt++) {
+      const f32x4 t = total(adw[hi][jt]);
+#pragma unroll
+      for (int i = 0; i < 4; i++) dw[int64_t(16 * (wave + 8 * hi) + 4 * g + i) * K + J0 + 16 * jt + r] = t[i];
+    }
+}
+
+template <int A1>
+__device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t M, float* __restrict__ db,
+                                          float* __restrict__ dwh, float* __restrict__ dbh, unsigned short* lds) {
+  unsigned short* dm = lds;              // [plane][m][DMP]
+  unsigned short* ys = lds + 2 * IMG;    // [plane][m][DMP]
+  unsigned short* zs = lds + 4 * IMG;    // [plane][m][16] (a >= A1 and rows >= M zero)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int q = r >> 2, p = r & 3;
+  const int NC = int((M + MC - 1) / MC);
+  uint4 sdh[4], sdl[4], syh[4], syl[4];
+  unsigned short zh[2], zl[2];
+  auto load = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const int64_t o = min(m0 + row, M - 1) * H + 8 * pc;
+      sdh[k] = *reinterpret_cast<const uint4*>(&dpre.hi[o]);
+      sdl[k] = *reinterpret_cast<const uint4*>(&dpre.lo[o]);
+      syh[k] = *reinterpret_cast<const uint4*>(&y.hi[o]);
+      syl[k] = *reinterpret_cast<const uint4*>(&y.lo[o]);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int e = tid + NT * k, m = e >> 4, a = e & 15;
+      const int64_t o = min(m0 + m, M - 1) * A1 + min(a, A1 - 1);
+      zh[k] = dz.hi[o];
+      zl[k] = dz.lo[o];
+    }
+  };
+  auto store = [&](int c) {
+    const int64_t m0 = int64_t(c) * MC;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
+      const bool ok = m0 + row < M;
+      const int o = row * DMP + 8 * pc;
+      *reinterpret_cast<uint4*>(&dm[o]) = keep_if(ok, sdh[k]);
+      *reinterpret_cast<uint4*>(&dm[IMG + o]) = keep_if(ok, sdl[k]);
+      *reinterpret_cast<uint4*>(&ys[o]) = keep_if(ok, syh[k]);
+      *reinterpret_cast<uint4*>(&ys[IMG + o]) = keep_if(ok, syl[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int e = tid + NT * k, m = e >> 4, a = e & 15;
+      const bool ok = m0 + m < M && a < A1;
+      zs[e] = ok ? zh[k] : static_cast<unsigned short>(0);
+      zs[MC * 16 + e] = ok ? zl[k] : static_cast<unsigned short>(0);
+    }
+  };
+  u16x8 onev;
+#pragma unroll
+  for (int j = 0; j < 8; j++) onev[j] = (r == 0) ? static_cast<unsigned short>(0x3f80) : static_cast<unsigned short>(0);
+  const bf16x8 ones = as_bf(onev);  // as A: row 0 all ones; as B: column 0 all ones
+  Acc awh[2], adb[2], abh = acc0();
+  awh[0] = awh[1] = adb[0] = adb[1] = acc0();
+  load(0);
+  for (int c = 0; c < NC; c++) {
+    store(c);
+    __syncthreads();
+    if (c + 1 < NC) load(c + 1);
+#pragma unroll
+    for (int ks = 0; ks < MC / 32; ks++) {
+      const unsigned short* pz = &zs[(32 * ks + 4 * g + q) * 16 + 4 * p];
+      const bf16x8 azh = tr8(pz, pz + 16 * 16), azl = tr8(pz + MC * 16, pz + MC * 16 + 16 * 16);
+#pragma unroll
+      for (int hi = 0; hi < 2; hi++) {
+        const int off = (32 * ks + 4 * g + q) * DMP + 16 * (wave + 8 * hi) + 4 * p;
+        const bf16x8 byh = tr8(&ys[off], &ys[off + 16 * DMP]), byl = tr8(&ys[IMG + off], &ys[IMG + off + 16 * DMP]);
+        const bf16x8 bdh = tr8(&dm[off], &dm[off + 16 * DMP]), bdl = tr8(&dm[IMG + off], &dm[IMG + off + 16 * DMP]);
+        mma3(awh[hi], azh, azl, byh, byl);
+        mma2a(adb[hi], ones, bdh, bdl);
+      }
+      if (wave == 0) {  // dbh: dzᵀ times a ones column (B exact)
+        abh.x = mfma(azl, ones, abh.x);
+        abh.hh = mfma(azh, ones, abh.hh);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int hi = 0; hi < 2; hi++) {
+    const int h = 16 * (wave + 8 * hi) + r;
+    const f32x4 tw = total(awh[hi]), tb = total(adb[hi]);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * g + i < A1) dwh[(4 * g + i) * H + h] = tw[i];
+    if (g == 0) db[h] = tb[0];
+  }
+  if (wave == 0 && r == 0) {
+    const f32x4 tb = total(abh);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * g + i < A1) dbh[4 * g + i] = tb[i];
+  }
+}
+
+template <int A1>
+__global__ __launch_bounds__(NT) void k_dense_heads_bwd_x3(CPair dz, CPair y, CPair x, CPair w, CPair dpre, int64_t M,
+                                                           int64_t K, Pair dx, float* __restrict__ dw,
+                                                           float* __restrict__ db, float* __restrict__ dwh,
+                                                           float* __restrict__ dbh) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[K12X_LDS];
+  if (int64_t(blockIdx.x) * JB == K)
+    k12x_head<A1>(dz, y, dpre, M, db, dwh, dbh, lds);
+  else
+    k12x_cols(x, w, dpre, M, K, int64_t(blockIdx.x) * JB, dx, dw, lds);
+}
+
+}  // namespace x3
+
+// ---------------------------------------------------------------- host launchers (dense tail)
+// K13x configurations: M <= 64: 16x16 per wave (FM = FN = 1); larger M: 32x32 (FM = FN = 2)
+static void x3_part_cfg(int64_t M, int64_t K, int N, int* fm, int* S) {
+  const int f = M <= 64 ? 1 : 2;
+  const int64_t tiles = ((M + 16 * f - 1) / (16 * f)) * (N / (16 * f));
+  const int64_t steps = K / 32;
+  int64_t s = M <= 64 ? 8 : (512 + tiles - 1) / tiles;  // ~512+ workgroups
+  s = std::min<int64_t>(s, std::max<int64_t>(1, steps / 8));
+  s = std::max<int64_t>(1, std::min<int64_t>(s, 16));
+  *fm = f;
+  *S = int(s);
+}
+int x3_dense_fwd_part_slices(int64_t M, int64_t K, int N) {
+  int f, S;
+  x3_part_cfg(M, K, N, &f, &S);
+  return S;
+}
+void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part, int S, hipStream_t stream) {
+  if (M <= 0) return;
+  if (K % 32 != 0 || N % 32 != 0) throw std::invalid_argument("x3_dense_fwd_part: K % 32 == 0 and N % 32 == 0");
+  check_pair(x, "x3_dense_fwd_part x");
+  check_pair(w, "x3_dense_fwd_part w");
+  int f, s_cfg;
+  x3_part_cfg(M, K, N, &f, &s_cfg);
+  if (S != s_cfg) throw std::invalid_argument("x3_dense_fwd_part: S must be x3_dense_fwd_part_slices(M, K, N)");
+  const int64_t tiles = ((M + 16 * f - 1) / (16 * f)) * (N / (16 * f));
+  const dim3 grid(uint32_t(tiles * S)), block(256);
+  if (f == 1)
+    hipLaunchKernelGGL((x3::k_dense_fwd_part_x3<1, 1>), grid, block, 0, stream, cp(x), cp(w), M, K, N, S, part);
+  else
+    hipLaunchKernelGGL((x3::k_dense_fwd_part_x3<2, 2>), grid, block, 0, stream, cp(x), cp(w), M, K, N, S, part);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const float* cols, const float* coef, float* acc,
+                  const float* gout, int64_t M, int A1, X3Out dz, X3Out dpre, X3Out hid, hipStream_t stream,
+                  const int64_t* cidx, const int64_t* ctr, int64_t period) {
+  if (M <= 0) return;
+  if (period < 1) period = 1;
+  if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("x3_heads_ppo: 2 <= A <= 15 actions");
+  if (!hpart || S < 1 || !hb.hi || !hb.lo || !wh.hi || !wh.lo || !bh.hi || !bh.lo || !dz.hi || !dz.lo || !dpre.hi ||
+      !dpre.lo || !hid.hi || !hid.lo)
+    throw std::invalid_argument("x3_heads_ppo: partials, split weights and split outputs required");
+  const dim3 grid(uint32_t((M + 3) / 4)), block(256);
+#define RMM_K15X(N)                                                                                               \
+  case N:                                                                                                         \
+    hipLaunchKernelGGL(x3::k_heads_ppo_x3<N>, grid, block, 0, stream, hpart, S, cp(hb), cp(wh), cp(bh), cols, coef, \
+                       acc, gout, M, pp(dz), pp(dpre), pp(hid), cidx, ctr, period);                              \
+    break;
+  switch (A1) {
+    RMM_K15X(3) RMM_K15X(4) RMM_K15X(5) RMM_K15X(6) RMM_K15X(7) RMM_K15X(8) RMM_K15X(9)
+    RMM_K15X(10) RMM_K15X(11) RMM_K15X(12) RMM_K15X(13) RMM_K15X(14) RMM_K15X(15) RMM_K15X(16)
+  }
+#undef RMM_K15X
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const int64_t* t_ptr, const int64_t* ctr,
+                     uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B, int A1,
+                     hipStream_t stream, unsigned int* done, int64_t* host_seq) {
+  if (B <= 0) return;
+  if (host_seq != nullptr && done == nullptr) throw std::invalid_argument("x3_heads_sample: host_seq needs done");
+  if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("x3_heads_sample: 2 <= A <= 15 actions");
+  if (!hpart || S < 1 || !hb.hi || !hb.lo || !wh.hi || !wh.lo || !bh.hi || !bh.lo)
+    throw std::invalid_argument("x3_heads_sample: partials and split weights required");
+  if (done != nullptr && B <= 32) {  // one workgroup, thread 0 advances the step after a barrier
+    auto* tw = const_cast<int64_t*>(t_ptr);
+    auto* cw = const_cast<int64_t*>(ctr);
+#define RMM_K16X1(N)                                                                                               \
+  case N:                                                                                                          \
+    hipLaunchKernelGGL((x3::k_heads_sample1_x3<N, 2>), dim3(1), dim3(1024), 0, stream, hpart, S, cp(hb), cp(wh),    \
+                       cp(bh), tw, cw, seed, act, logp, vf, lout, act_now, B, host_seq);                           \
+    break;
+    switch (A1) {
+      RMM_K16X1(3) RMM_K16X1(4) RMM_K16X1(5) RMM_K16X1(6) RMM_K16X1(7) RMM_K16X1(8) RMM_K16X1(9)
+      RMM_K16X1(10) RMM_K16X1(11) RMM_K16X1(12) RMM_K16X1(13) RMM_K16X1(14) RMM_K16X1(15) RMM_K16X1(16)
+    }
+#undef RMM_K16X1
+    RMM_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const dim3 grid(uint32_t((B + 3) / 4)), block(256);
+#define RMM_K16X(N)                                                                                                \
+  case N:                                                                                                          \
+    hipLaunchKernelGGL(x3::k_heads_sample_x3<N>, grid, block, 0, stream, hpart, S, cp(hb), cp(wh), cp(bh), t_ptr,   \
+                       ctr, seed, act, logp, vf, lout, act_now, B, done, host_seq);                                \
+    break;
+  switch (A1) {
+    RMM_K16X(3) RMM_K16X(4) RMM_K16X(5) RMM_K16X(6) RMM_K16X(7) RMM_K16X(8) RMM_K16X(9)
+    RMM_K16X(10) RMM_K16X(11) RMM_K16X(12) RMM_K16X(13) RMM_K16X(14) RMM_K16X(15) RMM_K16X(16)
+  }
+#undef RMM_K16X
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int64_t M, int64_t K, X3Out dx, float* dw,
+                        float* db, float* dwh, float* dbh, hipStream_t stream) {
+  if (M <= 0) return;
+  if (K % x3::JB != 0) throw std::invalid_argument("x3_dense_heads_bwd: K must be a multiple of 32");
+  if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("x3_dense_heads_bwd: 1 <= A+1 <= 16");
+  for (const X3In* p : {&dz, &y, &x, &w, &dpre})
+    if (!p->hi || !p->lo) throw std::invalid_argument("x3_dense_heads_bwd: inputs need hi and lo planes");
+  if (!dx.hi || !dx.lo || !dw || !db || !dwh || !dbh) throw std::invalid_argument("x3_dense_heads_bwd: outputs");
+  const dim3 grid(uint32_t(K / x3::JB + 1)), block(x3::NT);
+#define RMM_K12X(N)                                                                                                 \
+  case N:                                                                                                           \
+    hipLaunchKernelGGL(x3::k_dense_heads_bwd_x3<N>, grid, block, 0, stream, cp(dz), cp(y), cp(x), cp(w), cp(dpre), M, \
+                       K, pp(dx), dw, db, dwh, dbh);                                                                \
+    break;
+  switch (A1) {
+    RMM_K12X(1) RMM_K12X(2) RMM_K12X(3) RMM_K12X(4) RMM_K12X(5) RMM_K12X(6) RMM_K12X(7) RMM_K12X(8)
+    RMM_K12X(9) RMM_K12X(10) RMM_K12X(11) RMM_K12X(12) RMM_K12X(13) RMM_K12X(14) RMM_K12X(15) RMM_K12X(16)
+  }
+#undef RMM_K12X
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace rmm
+
+namespace rmm {
+namespace hip {
+namespace x3 {
+__global__ __launch_bounds__(256) void k_split(const float* __restrict__ src, unsigned short* __restrict__ hi,
+                                               unsigned short* __restrict__ lo, int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    unsigned short h, l;
+    split(src[i], h, l);
+    hi[i] = h;
+    lo[i] = l;
+  }
+}
+}  // namespace x3
+void x3_split(const float* src, void* hi, void* lo, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(x3::k_split, dim3(uint32_t(blocks)), dim3(256), 0, stream, src, static_cast<unsigned short*>(hi),
+                     static_cast<unsigned short*>(lo), n);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+}  // namespace hip
+}  // namespace rmm
