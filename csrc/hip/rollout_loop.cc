@@ -155,6 +155,15 @@ std::vector<double> launch_overhead_probe(int n, hipStream_t stream) {
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
                          int64_t* host_seq_dev) {
   // ctr_t = {rng counter, rollout row}: K10 stores row *t, K16 samples with the counter and advances both
+  if (a.x3) {  // fp32 policy: the split-bf16 twins (K10x push -> K13x -> K16x)
+    const X3Out h2{a.h2, a.h2lo};
+    x3_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, X3In{a.W1, a.W1lo}, a.w1s, X3In{a.b1, a.b1lo},
+                      X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream);
+    x3_dense_fwd_part(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, 256, a.hpart, a.S, stream);
+    x3_heads_sample(a.hpart, a.S, X3In{a.bd, a.bdlo}, X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t,
+                    a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B, a.A1, stream, k16_done, host_seq_dev);
+    return;
+  }
   nature_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, a.W1, a.w1s, a.b1, a.W2, a.w2s, a.b2, a.h2, stream);
   dense_fwd_part(a.h2, a.Wd, a.B, 3872, 256, a.hpart, a.S, stream);
   dense_heads_sample(nullptr, a.Wh, a.bh, a.ctr_t + 1, a.ctr_t, a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B,

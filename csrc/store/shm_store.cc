@@ -19,7 +19,7 @@ namespace rmm {
 namespace {
 
 constexpr uint64_t kMagic = 0x524d4d53544f5245ull;  // "RMMSTORE"
-constexpr uint64_t kVersion = 5;
+constexpr uint64_t kVersion = 6;  // 6: per-client pin records, Entry.io_pid / anon_pins
 constexpr uint64_t kFreeBit = 1;
 constexpr uint64_t kSizeMask = ~uint64_t(kAlign - 1);
 
@@ -100,6 +100,8 @@ Store* Store::Create(const std::string& name, uint64_t size, const std::string& 
   off = AlignUp(off + kRingCap * sizeof(ObjectId), 4096);
   uint64_t spill_off = off;
   off = AlignUp(off + kSpillSlots * sizeof(SpillFileSlot), 4096);
+  uint64_t pins_off = off;
+  off = AlignUp(off + kPinCap * sizeof(PinRec), 4096);
   uint64_t heap_off = off;
   uint64_t heap_size = AlignUp(size, 4096);
   uint64_t total = heap_off + heap_size;
@@ -129,6 +131,7 @@ Store* Store::Create(const std::string& name, uint64_t size, const std::string& 
   h->table_cap = table_cap;
   h->ring_off = ring_off;
   h->spill_off = spill_off;
+  h->pins_off = pins_off;  // records are zero (empty) from ftruncate
   h->heap_off = heap_off;
   h->heap_size = heap_size;
   h->lru_head = h->lru_tail = -1;
@@ -231,8 +234,20 @@ void Store::Recover(int dead_pid) {
   for (uint64_t i = 0; i < cap; i++) {
     Entry e = table_[i];
     if (e.state == kEmpty || e.state == kTombstone) continue;
-    bool ok = e.state <= kRestoring && e.pin_count >= 0 && e.data_size + e.meta_size <= hdr_->heap_size;
+    bool ok = e.state <= kRestoring && e.pin_count >= 0 && e.anon_pins >= 0 &&
+              e.data_size + e.meta_size <= hdr_->heap_size;
     if (ok && e.state == kCreating && !alive(e.creator_pid)) ok = false;  // its creator is gone: abort
+    // a spill / restore whose IO process is gone never finishes: roll it back and drop its IO pin
+    if (ok && (e.state == kSpilling || e.state == kRestoring) && e.io_pid != 0 && !alive(e.io_pid)) {
+      if (e.state == kSpilling) {
+        e.state = kSealed;  // the partial spill file is never referenced
+      } else {
+        e.state = kSpilled;  // its heap block (if any) is freed by the rebuild below (not resident)
+        e.offset = 0;
+      }
+      e.io_pid = 0;
+      if (e.anon_pins > 0) e.anon_pins--;
+    }
     if (ok && resident(e)) {
       const uint64_t need = std::max(AlignUp(e.data_size + e.meta_size, kAlign) + kBlockHdr, kMinBlock);
       const bool placed = e.offset >= heap_lo + kBlockHdr && e.offset % kAlign == 0 &&
@@ -298,12 +313,35 @@ void Store::Recover(int dead_pid) {
       int64_t sl = SpillSlot(e.spill_file, true);
       if (sl >= 0) spill_[sl].live++;
     }
-    if (e.state == kSealed && e.pin_count == 0 && resident(e)) lru.push_back({e.create_ns, int64_t(j)});
+    if (e.state == kSealed && resident(e)) lru.push_back({e.create_ns, int64_t(j)});  // pushed if unpinned
+  }
+  // 3b) pins: keep the records of live clients whose object survived; every entry's pin count is
+  // its anonymous pins plus its records (the records are the truth: a dead reader's pins vanish here)
+  {
+    PinRec* pins = Pins();
+    std::vector<PinRec> recs;
+    for (uint64_t i = 0; i < kPinCap; i++)
+      if (pins[i].state == 1 && pins[i].count > 0 && alive(pins[i].pid)) recs.push_back(pins[i]);
+    memset(pins, 0, kPinCap * sizeof(PinRec));
+    hdr_->pins_used = hdr_->pins_live = 0;
+    for (uint64_t i = 0; i < cap; i++)
+      if (table_[i].state != kEmpty && table_[i].state != kTombstone) table_[i].pin_count = table_[i].anon_pins;
+    for (auto& r : recs) {
+      ObjectId o;
+      memcpy(o.b, r.id, kIdSize);
+      const int64_t idx = Find(o);
+      if (idx < 0) continue;
+      if (PinInsert(r.id, r.pid, r.count)) table_[idx].pin_count += r.count;
+    }
   }
   std::sort(lru.begin(), lru.end());
-  for (auto& x : lru) LruPush(x.second);
-  hdr_->creating_now = 0;
-  for (uint64_t i = 0; i < cap; i++) hdr_->creating_now += table_[i].state == kCreating;
+  for (auto& x : lru)
+    if (table_[x.second].pin_count == 0) LruPush(x.second);
+  hdr_->creating_now = hdr_->io_now = 0;
+  for (uint64_t i = 0; i < cap; i++) {
+    hdr_->creating_now += table_[i].state == kCreating;
+    hdr_->io_now += (table_[i].state == kSpilling || table_[i].state == kRestoring) && table_[i].io_pid != 0;
+  }
   // 4) heap: used blocks exactly where live payloads are, every gap one free block
   hdr_->fl_bitmap = 0;
   memset(hdr_->sl_bitmap, 0, sizeof(hdr_->sl_bitmap));
@@ -632,6 +670,134 @@ void Store::LruRemove(int64_t idx) {
   e->in_lru = 0;
 }
 
+// ---------------------------------------------------------------- per-client pins
+
+namespace {
+inline uint64_t PinHash(const uint8_t* id, int32_t pid) {
+  ObjectId o;
+  memcpy(o.b, id, kIdSize);
+  uint64_t h = HashId(o) ^ (uint64_t(uint32_t(pid)) * 0x9E3779B97F4A7C15ull);
+  h ^= h >> 31;
+  return h;
+}
+}  // namespace
+
+int64_t Store::PinFind(const uint8_t* id, int32_t pid) {
+  PinRec* P = Pins();
+  const uint64_t mask = kPinCap - 1;
+  uint64_t i = PinHash(id, pid) & mask;
+  for (uint64_t n = 0; n <= mask; n++, i = (i + 1) & mask) {
+    if (P[i].state == 0) return -1;
+    if (P[i].state == 1 && P[i].pid == pid && memcmp(P[i].id, id, kIdSize) == 0) return int64_t(i);
+  }
+  return -1;
+}
+
+void Store::PinRehash() {
+  PinRec* P = Pins();
+  std::vector<PinRec> live;
+  for (uint64_t i = 0; i < kPinCap; i++)
+    if (P[i].state == 1) live.push_back(P[i]);
+  memset(P, 0, kPinCap * sizeof(PinRec));
+  hdr_->pins_used = hdr_->pins_live = 0;
+  for (auto& r : live) PinInsert(r.id, r.pid, r.count);
+}
+
+// a new record (the caller checked there is none for (id, pid)); false when the table is full
+bool Store::PinInsert(const uint8_t* id, int32_t pid, int32_t count) {
+  if (hdr_->pins_used + 1 > kPinCap - kPinCap / 4) {
+    if (hdr_->pins_live + 1 > kPinCap / 2) return false;
+    PinRehash();  // mostly tombstones
+  }
+  PinRec* P = Pins();
+  const uint64_t mask = kPinCap - 1;
+  uint64_t i = PinHash(id, pid) & mask;
+  while (P[i].state == 1) i = (i + 1) & mask;
+  if (P[i].state == 0) hdr_->pins_used++;
+  memcpy(P[i].id, id, kIdSize);
+  P[i].pid = pid;
+  P[i].count = count;
+  P[i].state = 1;
+  hdr_->pins_live++;
+  return true;
+}
+
+void Store::PinAdd(int64_t idx, int32_t pid) {
+  Entry* e = E(idx);
+  const int64_t r = PinFind(e->id, pid);
+  if (r >= 0) {
+    Pins()[r].count++;
+  } else if (!PinInsert(e->id, pid, 1)) {
+    e->anon_pins++;  // no room for a record: this pin cannot be released on the client's death
+    hdr_->pin_overflow_total++;
+  }
+  e->pin_count++;
+}
+
+void Store::PinErase(const uint8_t* id, int32_t pid) {
+  const int64_t r = PinFind(id, pid);
+  if (r < 0) return;
+  Pins()[r].state = 2;
+  Pins()[r].count = 0;
+  hdr_->pins_live--;
+}
+
+// Release one pin of entry idx on behalf of `pid`: its own record first, then an anonymous pin, then
+// (a pin handed to another process, e.g. a view passed along) any record of the same object.
+void Store::PinDrop(int64_t idx, int32_t pid) {
+  Entry* e = E(idx);
+  if (e->pin_count <= 0) return;
+  PinRec* P = Pins();
+  int64_t r = PinFind(e->id, pid);
+  if (r < 0 && e->anon_pins > 0) {
+    e->anon_pins--;
+    e->pin_count--;
+    return;
+  }
+  if (r < 0)
+    for (uint64_t i = 0; i < kPinCap; i++)
+      if (P[i].state == 1 && memcmp(P[i].id, e->id, kIdSize) == 0) {
+        r = int64_t(i);
+        break;
+      }
+  if (r >= 0 && --P[r].count <= 0) {
+    P[r].state = 2;
+    P[r].count = 0;
+    hdr_->pins_live--;
+  }
+  e->pin_count--;
+}
+
+void Store::IoPin(int64_t idx) {
+  Entry* e = E(idx);
+  e->anon_pins++;
+  e->pin_count++;
+  e->io_pid = int32_t(getpid());
+  hdr_->io_now++;
+}
+
+void Store::IoUnpin(int64_t idx) {
+  Entry* e = E(idx);
+  if (e->anon_pins > 0) e->anon_pins--;
+  if (e->pin_count > 0) e->pin_count--;
+  if (e->io_pid != 0 && hdr_->io_now > 0) hdr_->io_now--;
+  e->io_pid = 0;
+}
+
+// entry idx just lost its last pin: free it if a delete is pending, else make it evictable
+void Store::FinishUnpinned(int64_t idx) {
+  Entry* e = E(idx);
+  if (e->pin_count != 0) return;
+  if (e->flags & kFlagDeletePending) {
+    if (e->state == kCreating) hdr_->creating_now--;
+    if (e->state == kSealed) hdr_->stats.num_sealed--;
+    FreeEntryStorage(idx);
+    RemoveEntry(idx);
+  } else if (e->state == kSealed && !(e->flags & kFlagFallback)) {
+    LruPush(idx);
+  }
+}
+
 // ---------------------------------------------------------------- spill files
 
 std::vector<std::string> Store::SpillDirs() const {
@@ -786,7 +952,7 @@ uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
         batch_bytes += AlignUp(e->data_size + e->meta_size, kAlign) + kBlockHdr;
         LruRemove(i);
         e->state = kSpilling;
-        e->pin_count++;
+        IoPin(i);
       }
     }
     i = nxt;
@@ -803,6 +969,7 @@ uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
     foff += AlignUp(len, 4096);
   }
   Unlock();
+  CrashPoint(6);  // spill IO in progress, lock released: the victims are kSpilling with this pid's IO pin
   bool ok = true;
   std::string path = SpillPath(fid);
   int fd = open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0600);
@@ -824,7 +991,7 @@ uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
     int64_t idx = Find(it.id);
     if (idx < 0) continue;
     Entry* e = E(idx);
-    e->pin_count--;
+    IoUnpin(idx);
     if (!ok || slot < 0) {
       e->state = kSealed;
       if (e->pin_count == 0) LruPush(idx);
@@ -879,7 +1046,7 @@ bool Store::RestoreLocked(int64_t idx) {
   uint64_t len = e->data_size + e->meta_size;
   e->state = kRestoring;
   e->offset = 0;  // no heap block yet (the allocation below may spill with the lock dropped)
-  e->pin_count++;
+  IoPin(idx);
   uint64_t off = HeapAlloc(len);
   while (off == kNil) {
     uint64_t f = SpillLocked(len, nullptr);
@@ -890,7 +1057,7 @@ bool Store::RestoreLocked(int64_t idx) {
   e = E(idx);
   if (off == kNil) {
     e->state = kSpilled;
-    e->pin_count--;
+    IoUnpin(idx);
     Broadcast();
     return false;
   }
@@ -898,6 +1065,7 @@ bool Store::RestoreLocked(int64_t idx) {
   uint8_t* dst = base_ + off;
   e->offset = off;  // the block is owned by this entry while the lock is dropped (crash recovery)
   Unlock();
+  CrashPoint(5);  // restore IO in progress, lock released: kRestoring with this pid's IO pin
   bool ok = true;
   int fd = open(SpillPath(fid).c_str(), O_RDONLY);
   if (fd < 0) ok = false;
@@ -911,7 +1079,7 @@ bool Store::RestoreLocked(int64_t idx) {
   Lock();
   idx = Find(id);
   e = E(idx);
-  e->pin_count--;
+  IoUnpin(idx);
   if (!ok) {
     HeapFree(off);
     e->state = kSpilled;
@@ -954,8 +1122,9 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
   e->user_tag = user_tag;
   e->data_size = data_size;
   e->meta_size = meta_size;
-  e->pin_count = 1;
+  e->pin_count = 0;
   e->creator_pid = getpid();
+  PinAdd(idx, e->creator_pid);  // the creator's pin (released after seal, or on its death)
   e->create_ns = uint64_t(NowNs());
   hdr_->stats.creates_total++;
   // proactive threshold spilling is driven by the node (SpillBytes); here only on demand.
@@ -1005,6 +1174,7 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
     }
   }
   if (!ptr) {
+    PinErase(e->id, e->creator_pid);
     RemoveEntry(idx);
     hdr_->creating_now--;
     hdr_->oom_errors_total++;
@@ -1042,6 +1212,7 @@ void Store::Abort(const ObjectId& id) {
   Lock();
   int64_t idx = Find(id);
   if (idx >= 0 && E(idx)->state == kCreating) {
+    PinErase(E(idx)->id, E(idx)->creator_pid);
     FreeEntryStorage(idx);
     RemoveEntry(idx);
     hdr_->creating_now--;
@@ -1057,6 +1228,7 @@ int Store::AbortCreator(int pid) {
   for (uint64_t i = 0; hdr_->creating_now > 0 && i < hdr_->table_cap; i++) {
     Entry* e = &table_[i];
     if (e->state == kCreating && e->creator_pid == pid) {
+      PinErase(e->id, pid);
       FreeEntryStorage(int64_t(i));
       RemoveEntry(int64_t(i));
       hdr_->creating_now--;
@@ -1076,7 +1248,7 @@ bool Store::Get(const ObjectId& id, int64_t timeout_ms, View* out) {
       Entry* e = E(idx);
       if (e->state == kSealed || e->state == kSpilling) {
         if (e->pin_count == 0 && e->in_lru) LruRemove(idx);
-        e->pin_count++;
+        PinAdd(idx, int32_t(getpid()));
         hdr_->stats.gets_total++;
         out->data_size = e->data_size;
         out->meta_size = e->meta_size;
@@ -1141,18 +1313,68 @@ void Store::Release(const ObjectId& id) {
   Lock();
   int64_t idx = Find(id);
   if (idx < 0) { Unlock(); return; }
-  Entry* e = E(idx);
-  if (e->pin_count > 0) e->pin_count--;
-  if (e->pin_count == 0) {
-    if (e->flags & kFlagDeletePending) {
-      if (e->state == kCreating) hdr_->creating_now--;
-      FreeEntryStorage(idx);
-      RemoveEntry(idx);
-    } else if (e->state == kSealed && !(e->flags & kFlagFallback)) {
-      LruPush(idx);
+  PinDrop(idx, int32_t(getpid()));
+  FinishUnpinned(idx);
+  Unlock();
+}
+
+int Store::ReleaseClient(int pid) {
+  if (pid <= 0) return 0;
+  int n = 0;
+  Lock();
+  // 1) the client's pin records (gets never released, its creator pins of sealed objects)
+  PinRec* P = Pins();
+  std::vector<std::pair<ObjectId, int32_t>> drop;
+  for (uint64_t i = 0; hdr_->pins_live > 0 && i < kPinCap; i++) {
+    if (P[i].state == 1 && P[i].pid == pid) {
+      ObjectId o;
+      memcpy(o.b, P[i].id, kIdSize);
+      drop.push_back({o, P[i].count});
+      P[i].state = 2;
+      P[i].count = 0;
+      hdr_->pins_live--;
     }
   }
+  for (auto& d : drop) {
+    const int64_t idx = Find(d.first);
+    if (idx < 0) continue;
+    Entry* e = E(idx);
+    e->pin_count = std::max(0, e->pin_count - d.second);
+    n += d.second;
+    FinishUnpinned(idx);
+  }
+  // 2) spills / restores it was doing with the lock dropped: roll back
+  for (uint64_t i = 0; hdr_->io_now > 0 && i < hdr_->table_cap; i++) {
+    Entry* e = &table_[i];
+    if ((e->state != kSpilling && e->state != kRestoring) || e->io_pid != pid) continue;
+    if (e->state == kRestoring) {
+      if (e->offset) HeapFree(e->offset);
+      e->offset = 0;
+      e->state = kSpilled;
+    } else {
+      e->state = kSealed;
+    }
+    IoUnpin(int64_t(i));
+    n++;
+    FinishUnpinned(int64_t(i));
+  }
+  if (n > 0) {
+    hdr_->clients_released_total++;
+    hdr_->client_pins_released_total += uint64_t(n);
+    Broadcast();
+  }
   Unlock();
+  return n;
+}
+
+int64_t Store::PinsHeldBy(int pid) {
+  int64_t n = 0;
+  Lock();
+  PinRec* P = Pins();
+  for (uint64_t i = 0; i < kPinCap; i++)
+    if (P[i].state == 1 && P[i].pid == pid) n += P[i].count;
+  Unlock();
+  return n;
 }
 
 bool Store::Delete(const ObjectId& id) {

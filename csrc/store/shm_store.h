@@ -73,12 +73,15 @@ struct Entry {
   uint8_t id[kIdSize];
   uint32_t state;
   uint32_t flags;
-  int32_t pin_count;
+  int32_t pin_count;    // = anon_pins + the counts of this object's PinRec records
   int32_t creator_pid;
   int32_t lru_prev;  // intrusive LRU list of evictable (sealed, unpinned) entries
   int32_t lru_next;
   uint32_t in_lru;
   uint32_t user_tag;    // opaque to the store (e.g. serialization format / GPU meta)
+  int32_t io_pid;       // kSpilling / kRestoring: the process doing the file IO (holds one anon pin)
+  int32_t anon_pins;    // pins without a per-client record (spill / restore IO, pin-table overflow)
+  uint32_t pad_;
   uint64_t offset;      // heap offset of payload (data followed by metadata)
   uint64_t data_size;
   uint64_t meta_size;
@@ -87,6 +90,18 @@ struct Entry {
   uint64_t fallback_id; // file id for kFlagFallback objects
   uint64_t create_ns;
 };
+
+// Per-client pin record (reference plasma/store.cc:323 DisconnectClient releases a dead client's
+// objects; here clients are processes, so pins are recorded per (object, pid) in an open-addressing
+// table inside the segment: a dead reader's pins are released by ReleaseClient(pid) or by the
+// crash-recovery rebuild).
+struct PinRec {
+  uint8_t id[kIdSize];
+  int32_t pid;
+  int32_t count;
+  uint32_t state;  // 0 empty, 1 live, 2 tombstone
+};
+constexpr uint64_t kPinCap = 1 << 16;
 
 struct SpillFileSlot {
   uint64_t file_id;  // 0 = free
@@ -156,6 +171,14 @@ struct Header {
   uint64_t recoveries_total;
   uint64_t recovered_dropped_total;  // entries the rebuild could not validate (lost objects)
   uint64_t creating_now;             // entries in kCreating (AbortCreator skips its table scan at 0)
+  // per-client pins (PinRec table at pins_off, kPinCap records)
+  uint64_t pins_off;
+  uint64_t pins_used;                // live + tombstone records
+  uint64_t pins_live;
+  uint64_t pin_overflow_total;       // pins taken without a record (table full): not released on death
+  uint64_t io_now;                   // entries holding a spill / restore IO pin (ReleaseClient skips its scan at 0)
+  uint64_t clients_released_total;   // ReleaseClient calls that found something to release
+  uint64_t client_pins_released_total;
   Stats stats;
 };
 
@@ -223,6 +246,14 @@ class Store {
   uint64_t SpillBytes(uint64_t bytes);
   // Abort all objects still being created by `pid` (crashed creator).
   int AbortCreator(int pid);
+  // A client process died: release every pin it held (gets it never released, its creator pins) and
+  // roll back spills / restores it was doing (kSpilling -> kSealed, kRestoring -> kSpilled); objects
+  // whose last pin this was are freed if a delete was pending, else become evictable. Returns the
+  // number of pins released. Reference plasma/store.cc:323 DisconnectClient.
+  int ReleaseClient(int pid);
+  // Pins currently recorded for `pid` (tests / memory summary).
+  int64_t PinsHeldBy(int pid);
+  uint64_t PinOverflows() const { return hdr_->pin_overflow_total; }
   // Sealed-notification ring: returns new cursor; sets overflow when the consumer fell behind.
   uint64_t PollSealed(uint64_t cursor, std::vector<ObjectId>* out, bool* overflow);
   uint64_t SealSeq();
@@ -240,7 +271,8 @@ class Store {
   uint64_t RecoveredDropped() const { return hdr_->recovered_dropped_total; }
   // Test hook: SIGKILL this process at crash point `p` (1 = mid heap split, 2 = mid heap merge,
   // 3 = mid table insert, 4 = mid LRU unlink), i.e. while holding the store mutex in the middle
-  // of a multi-word metadata update. 0 disables. Process-local.
+  // of a multi-word metadata update; 5 = mid restore IO, 6 = mid spill IO (lock released, the
+  // entries carry this process's IO pin). 0 disables. Process-local.
   static void SetCrashPointForTest(int p);
 
  private:
@@ -261,6 +293,17 @@ class Store {
   void HeapShrink(uint64_t payload_off, uint64_t n);
   void LruPush(int64_t idx);
   void LruRemove(int64_t idx);
+  // per-client pins (lock held)
+  PinRec* Pins() { return reinterpret_cast<PinRec*>(base_ + hdr_->pins_off); }
+  int64_t PinFind(const uint8_t* id, int32_t pid);
+  bool PinInsert(const uint8_t* id, int32_t pid, int32_t count);
+  void PinRehash();
+  void PinAdd(int64_t idx, int32_t pid);
+  void PinDrop(int64_t idx, int32_t pid);
+  void PinErase(const uint8_t* id, int32_t pid);
+  void IoPin(int64_t idx);
+  void IoUnpin(int64_t idx);
+  void FinishUnpinned(int64_t idx);
   void FreeEntryStorage(int64_t idx);
   void DropSpillRef(uint64_t file_id);
   int64_t SpillSlot(uint64_t file_id, bool create);

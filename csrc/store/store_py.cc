@@ -358,6 +358,12 @@ PYBIND11_MODULE(_store, m) {
              return self.s->SpillBytes(bytes);
            })
       .def("abort_creator", [](PyStore& self, int pid) { return self.s->AbortCreator(pid); })
+      .def("release_client", [](PyStore& self, int pid) {
+        py::gil_scoped_release nogil;
+        return self.s->ReleaseClient(pid);
+      })
+      .def("pins_held_by", [](PyStore& self, int pid) { return self.s->PinsHeldBy(pid); })
+      .def("pin_overflows", [](PyStore& self) { return self.s->PinOverflows(); })
       .def("poll_sealed",
            [](PyStore& self, uint64_t cursor) {
              std::vector<ObjectId> out;

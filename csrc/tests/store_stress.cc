@@ -191,6 +191,89 @@ int main(int argc, char** argv) {
               (unsigned long)s->RecoveredDropped(), crash_bad);
   g_bad += crash_bad;
 
+  // ---- client-death phase: a reader SIGKILLed while it holds pins (no lock held), then one killed
+  // inside a restore's and a spill's file IO (lock released); ReleaseClient releases / rolls back
+  long client_bad = 0;
+  {
+    ObjectId r0 = Id(20000), r1 = Id(20001), r2 = Id(20002);
+    for (ObjectId x : {r0, r1, r2}) {
+      bool ex = false;
+      uint8_t* p = s->CreateObject(x, 8192, 0, 0, 0, &ex);
+      if (p) {
+        std::memset(p, 0x5a, 8192);
+        s->Seal(x);
+        s->Release(x);
+      }
+    }
+    // (a) reader holds three pins and dies
+    pid_t pid = fork();
+    if (pid == 0) {
+      Store* cs = Store::Attach(name);
+      Store::View v;
+      for (ObjectId x : {r0, r1, r2}) (void)cs->Get(x, 1000, &v);
+      kill(getpid(), SIGKILL);
+      _exit(3);
+    }
+    int status = 0;
+    waitpid(pid, &status, 0);
+    if (s->PinsHeldBy(pid) != 3) client_bad++;
+    for (ObjectId x : {r0, r1}) s->Delete(x);  // deferred: the dead reader still pins them
+    if (s->State(r0) != rmm::kSealed) client_bad++;
+    if (s->ReleaseClient(pid) != 3) client_bad++;
+    if (s->State(r0) != -1 || s->State(r1) != -1 || s->State(r2) != rmm::kSealed) client_bad++;
+    // (b) killed inside a restore's file IO: r2 stuck kRestoring until its IO pin is released
+    s->SpillBytes(1ull << 40);
+    if (s->State(r2) == rmm::kSpilled) {
+      pid = fork();
+      if (pid == 0) {
+        Store* cs = Store::Attach(name);
+        Store::SetCrashPointForTest(5);
+        Store::View v;
+        (void)cs->Get(r2, 1000, &v);
+        _exit(3);
+      }
+      waitpid(pid, &status, 0);
+      if (s->State(r2) != rmm::kRestoring) client_bad++;
+      if (s->ReleaseClient(pid) != 1 || s->State(r2) != rmm::kSpilled) client_bad++;
+    }
+    // (c) killed inside a spill's file IO: its victims (r3 has no spill copy yet, so it needs IO) stuck
+    // kSpilling until rolled back
+    Store::View v;
+    if (!s->Get(r2, 1000, &v) || v.data[0] != 0x5a || v.data[8191] != 0x5a) client_bad++;
+    s->Release(r2);
+    ObjectId r3 = Id(20003);
+    {
+      bool ex = false;
+      uint8_t* p = s->CreateObject(r3, 8192, 0, 0, 0, &ex);
+      if (p) {
+        std::memset(p, 0x5b, 8192);
+        s->Seal(r3);
+        s->Release(r3);
+      }
+    }
+    pid = fork();
+    if (pid == 0) {
+      Store* cs = Store::Attach(name);
+      Store::SetCrashPointForTest(6);
+      cs->SpillBytes(1ull << 40);
+      _exit(3);
+    }
+    waitpid(pid, &status, 0);
+    if (s->State(r3) != rmm::kSpilling) client_bad++;
+    if (s->ReleaseClient(pid) < 1 || s->State(r3) != rmm::kSealed) client_bad++;
+    if (!s->Get(r3, 1000, &v) || v.data[0] != 0x5b || v.data[8191] != 0x5b) client_bad++;
+    s->Release(r3);
+    try {
+      s->CheckHeap();
+    } catch (const std::runtime_error&) {
+      client_bad++;
+    }
+    s->Delete(r2);
+    s->Delete(r3);
+  }
+  std::printf("client-death phase: bad=%ld\n", client_bad);
+  g_bad += client_bad;
+
   uint64_t free_before = s->CheckHeap();
   for (int k = 0; k < kKeys; k++) s->Delete(Id(k));
   uint64_t free_after = s->CheckHeap();

@@ -66,6 +66,21 @@ def _cpu_part(res: dict) -> dict:
     return {k: v for k, v in res.items() if k == "CPU" or k.startswith("CPU_group_")}
 
 
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    # a zombie child still answers kill(0): treat it as gone
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except OSError:
+        return False
+
 class Conn:
     __slots__ = ("sock", "reader", "kind", "worker", "pid", "lock", "job_id", "alive", "wbuf")
 
@@ -213,6 +228,7 @@ class Head:
         self.gc_high_usage = float(self.config.get("high_plasma_storage_usage", 0.7))
         self.gc_auto_interval = float(self.config.get("automatic_gc_min_interval_s", 30.0))
         self.mem_stats = collections.Counter()
+        self._pins_pending = {}  # pid -> proc: exited clients whose store pins are released once gone
         self.sched = sched_ext().Scheduler()
         self.sched.set_spread_threshold(float(self.config.get("scheduler_spread_threshold", 0.5)))
         self.nodes: Dict[int, dict] = {}
@@ -795,6 +811,24 @@ class Head:
         elif c.worker is not None:
             self._worker_died(c.worker)
 
+    def _release_client_pins(self, pid: int, proc=None) -> None:
+        """A client process is gone: release every object-store pin it still held (objects it was
+        reading when it was killed, its creator pins) so they can be freed / evicted / spilled again.
+        Reference plasma/store.cc:323 DisconnectClient. Only once the process has really exited (a
+        worker whose socket closed may still be unwinding its views); until then it is retried from
+        the housekeeping tick."""
+        alive = proc.poll() is None if proc is not None else _pid_alive(pid)
+        if alive:
+            self._pins_pending[pid] = proc
+            return
+        self._pins_pending.pop(pid, None)
+        try:
+            n = self.store.release_client(pid)
+        except Exception:
+            return
+        if n:
+            self.mem_stats["client_pins_released"] = self.mem_stats.get("client_pins_released", 0) + n
+
     def _driver_exit(self, c: Conn):
         job = self.jobs.get(c.job_id)
         if job:
@@ -833,6 +867,8 @@ class Head:
                 w.proc.wait(timeout=0.05)
             except Exception:
                 pass
+        if w.pid:
+            self._release_client_pins(w.pid, w.proc)
         if prev_state != "DEAD":  # not a kill the head asked for (those report their own reason)
             t0 = self.tasks.get(w.task) if w.task is not None else None
             code = w.proc.poll() if w.proc is not None else None
@@ -1588,6 +1624,9 @@ class Head:
         now = time.time()
         if self.recovery.awaiting:
             self.recovery.expire_awaiting(now)
+        # pins of exited clients whose release had to wait for the process to finish exiting
+        for pid, proc in list(self._pins_pending.items()):
+            self._release_client_pins(pid, proc)
         # reap dead worker processes that never connected / crashed
         for w in list(self.workers.values()):
             if w.proc is not None and w.proc.poll() is not None:

@@ -257,9 +257,10 @@ class PPO(Algorithm):
         import os
 
         env = os.environ.get("RMM_SHARED_WEIGHTS")
-        if env is not None:
-            return env == "1"
-        return bool(getattr(self.algo_config, "share_device_weights", True))
+        want = env == "1" if env is not None else bool(getattr(self.algo_config, "share_device_weights", True))
+        # only learners with live device weights (the bf16 compute weights or the fp32 learner's split
+        # pair) can be aliased; others publish a fresh copy every iteration
+        return want and self.learner_group is not None and self.learner_group.shared_kind() is not None
 
     def _device_weights_ok(self) -> bool:
         """Weights go learner → rollout workers through HBM when both sides are GPU processes:
@@ -308,7 +309,10 @@ class PPO(Algorithm):
         if self.learner_group is not None:
             self.learner_group.set_weights(weights)
             self._weights_ref = self.learner_group.weights_ref()
-            if self._dev_refs is not None:  # the next iteration must not push pre-restore HBM weights
+            if self._dev_refs is not None and not (self._device_weights_ok() and self._shared_weights_ok()):
+                # copies: the next iteration must not push pre-restore HBM weights. Shared mode keeps its
+                # descriptors: the learners wrote the restored weights into the aliased buffers in place,
+                # and a flat snapshot must never be copied into parameters that alias the learner
                 self._dev_refs = self.learner_group.device_weights_refs()
             self.workers.local_worker().set_weights(weights)
             self.workers.sync_weights(ref=self._weights_ref)

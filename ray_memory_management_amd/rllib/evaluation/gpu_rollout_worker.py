@@ -44,6 +44,7 @@ class GPURolloutWorker:
         # bf16 inference weights in the layout the fused kernels read
         cdt = torch.float32 if str(self.config.get("compute_dtype", "bf16")) in ("fp32", "float32") else torch.bfloat16
         self.model = model.to(self.device).to(cdt).to(memory_format=torch.channels_last)
+        _init_x3(self.model)
         self.T = int(self.config.get("rollout_fragment_length", 200))
         self.sampler = GPURolloutSampler(self.env, self.model, fragment=self.T, seed=s)
         self._ep_len = np.zeros(n, dtype=np.int64)
@@ -73,6 +74,9 @@ class GPURolloutWorker:
     def set_weights(self, weights, global_vars=None):
         import torch
 
+        if isinstance(weights, dict) and "__rmm_shared_x3__" in weights:  # fp32 learner's live split pair
+            self._set_shared_x3(weights)
+            return
         if isinstance(weights, dict) and "__rmm_shared_bf16__" in weights:  # learner's live HBM weights
             import ray_memory_management_amd as rt
 
@@ -110,6 +114,7 @@ class GPURolloutWorker:
                         params[name].copy_(flat.to(self.device).as_strided(shape, stride, off))
             return
         if isinstance(weights, dict) and "__rmm_flat_bf16__" in weights:  # learner's HBM weights object
+            self._unalias_x3()
             flat = weights["__rmm_flat_bf16__"]
             if flat.device != self.device:
                 flat = flat.to(self.device)
@@ -118,12 +123,68 @@ class GPURolloutWorker:
                 for name, off, shape, stride in weights["__rmm_layout__"]:
                     if name in sd:
                         sd[name].copy_(flat.as_strided(shape, stride, off))
+            self._after_weight_copy()
             return
+        self._unalias_x3()
         with torch.no_grad():
             sd = self.model.state_dict()
             for k, v in weights.items():
                 if k in sd:
                     sd[k].copy_(torch.as_tensor(np.asarray(v)).to(sd[k].dtype), non_blocking=False)
+        self._after_weight_copy()
+
+    def _unalias_x3(self):
+        """Before a weight COPY into an fp32 policy that aliases the learner (shared split pair): give the
+        parameters their own storage again, so the copy never writes the learner's buffers."""
+        if getattr(self.model, "x3_pairs", lambda: None)() is None or getattr(self, "_shared_key", None) is None:
+            return
+        import torch
+
+        with torch.no_grad():
+            for p in self.model.parameters():
+                p.data = p.data.clone()
+        self._shared_key = None
+        self._x3_rebound = True
+
+    def _after_weight_copy(self):
+        """Copied fp32 weights: re-split them into the model's own pair (its fused fp32 path reads pairs);
+        a worker that aliased the learner's pair before recaptures its graphs."""
+        if getattr(self.model, "x3_pairs", lambda: None)() is None:
+            return
+        self.model.refresh_x3()
+        if getattr(self, "_x3_rebound", False):
+            self._x3_rebound = False
+            self._on_params_rebound()
+
+    def _set_shared_x3(self, weights):
+        """Alias the fp32 learner's split pair (hipIPC views of its HBM objects): the model's fused path
+        reads the learner's live hi / lo planes, no copy per iteration. Another GPU: copy + re-split."""
+        import torch
+
+        import ray_memory_management_amd as rt
+        from ray_memory_management_amd.ops import x3
+
+        m_ref, hi_ref, lo_ref = weights["__rmm_shared_x3__"]
+        key = m_ref.binary() + hi_ref.binary() + lo_ref.binary()
+        if getattr(self, "_shared_key", None) == key:
+            return  # already aliased: the learner updates master and pair in place
+        master, hi, lo = rt.get(m_ref), rt.get(hi_ref), rt.get(lo_ref)
+        params = dict(self.model.named_parameters())
+        layout = weights["__rmm_layout__"]
+        with torch.no_grad():
+            if master.device == self.device:  # same GPU: parameters alias the fp32 master, kernels the pair
+                for name, off, shape, stride in layout:
+                    if name in params:
+                        params[name].data = master.as_strided(shape, stride, off)
+                self.model.attach_x3({name: x3.Pair(hi.as_strided(shape, stride, off), lo.as_strided(shape, stride, off))
+                                      for name, off, shape, stride in layout})
+                self._shared_key, self._shared_flat = key, (master, hi, lo)
+                self._on_params_rebound()
+                return
+            for name, off, shape, stride in layout:  # another GPU: copy + own pair
+                if name in params:
+                    params[name].copy_(master.to(self.device).as_strided(shape, stride, off))
+        self.model.refresh_x3()
 
     def get_weights(self, policies=None):
         return {k: v.detach().float().cpu().numpy() for k, v in self.model.state_dict().items()}
@@ -144,6 +205,20 @@ class GPURolloutWorker:
 
     def stop(self):
         pass
+
+
+def _init_x3(model) -> None:
+    """fp32 Nature-CNN policy: give the model its own split-bf16 weight pair so its rollout step runs on
+    the fused x3 kernels (K10x / K13x / K16x); bf16 models and other networks are left alone."""
+    import torch
+
+    if (getattr(model, "nature", False) and hasattr(model, "refresh_x3")
+            and getattr(getattr(model, "heads", None), "weight", None) is not None
+            and model.heads.weight.dtype == torch.float32 and model.heads.weight.is_cuda):
+        from ray_memory_management_amd.rllib.ppo_learner import _x3_available
+
+        if _x3_available():
+            model.refresh_x3()
 
 
 class _EnvGroup:
@@ -251,7 +326,8 @@ class _EnvGroup:
                 src = self.s_new.data_ptr()
             if self.band:
                 push = (src, self.buf_obs, "rows")  # K10 reads row t-1 + new frames, stores row t
-            elif self.fused and self.fold_push and self.model.fused_trunk_ok(self.s_obs):
+            elif self.fused and self.fold_push and (self.model.fused_trunk_ok(self.s_obs)
+                                                    or getattr(self.model, "fused_x3_ok", lambda o: False)(self.s_obs)):
                 push = (src, self.buf_obs)  # K10 shifts the stack and stores row t itself
             else:
                 require_hip().frame_push(self.s_obs.data_ptr(), src, self.buf_obs.data_ptr(),
@@ -417,6 +493,7 @@ class HybridRolloutWorker(GPURolloutWorker):
         model = build_model(self.env.observation_space, self.env.action_space, self.config.get("model") or {})
         cdt = torch.float32 if str(self.config.get("compute_dtype", "bf16")) in ("fp32", "float32") else torch.bfloat16
         self.model = model.to(self.device).to(cdt).to(memory_format=torch.channels_last)
+        _init_x3(self.model)
         self.T = int(self.config.get("rollout_fragment_length", 200))
         self.n = n
         probe = torch.zeros((1,) + tuple(np.asarray(self.env.vector_reset()).shape[1:]), dtype=torch.uint8,
@@ -554,7 +631,8 @@ class HybridRolloutWorker(GPURolloutWorker):
         on = os.environ.get("RMM_ROLLOUT_SERVER")
         if not (on == "1" if on is not None else bool(self.config.get("rollout_server", False))):
             return None
-        return self._kernel_args(G, S)
+        k = self._kernel_args(G, S)
+        return None if k is None or k.get("x3") else k
 
     def _direct_args(self, G, S):
         """Arguments of the native loop with DIRECT kernel launches per policy step (K10 push → K13s →
@@ -572,7 +650,8 @@ class HybridRolloutWorker(GPURolloutWorker):
         k = self._kernel_args(G, S)
         if k is None or G[0].k16_done is None:
             return None
-        out = dict(group=k["group"], weights=k["weights"], w1s=k["w1s"], w2s=k["w2s"], bufs=k["bufs"][:11],
+        out = dict(group=k["group"], weights=k["weights"], w1s=k["w1s"], w2s=k["w2s"],
+                   bufs=k["bufs"][:12] if k.get("x3") else k["bufs"][:11],
                    B=k["B"], S=k["S"], A1=k["A1"], seed=k["seed"], k16_done=G[0].k16_done.data_ptr())
         if os.environ.get("RMM_ROLLOUT_SEQ", "1") != "0":
             # completion word: K16 stores row + 1 into mapped pinned memory, the loop polls it (no event
@@ -603,9 +682,10 @@ class HybridRolloutWorker(GPURolloutWorker):
             return None
         g, gs = G[0], S[0]
         m = self.model
+        x3 = bool(getattr(m, "fused_x3_ok", lambda o: False)(g.s_obs))  # fp32 policy: split-bf16 kernels
         ok = (g.device_stack and not g.band and g.fused and g.h_new_dev and g.h_act_dev and g.n <= 64
               and getattr(g.env, "_native", None) is not None and hasattr(g.env, "native_state")
-              and getattr(m, "nature", False) and m.fused_trunk_ok(g.s_obs) and m.dense_tail is not None
+              and getattr(m, "nature", False) and (m.fused_trunk_ok(g.s_obs) or x3) and m.dense_tail is not None
               and m.dense_tail.out_features == 256 and m.dense_tail.in_features == 3872
               and m.dense_tail.weight.is_contiguous() and m.heads.weight.is_contiguous()
               and 3 <= m.heads.out_features <= 16)
@@ -613,17 +693,29 @@ class HybridRolloutWorker(GPURolloutWorker):
             return None
         hip = require_hip()
         B, A1 = g.n, m.heads.out_features
-        S_ = hip.dense_fwd_part_slices(B, 3872, 256)
-        self._server_h2 = torch.empty((B, 3872), dtype=torch.bfloat16, device=self.device)
-        self._server_hpart = torch.empty(S_ * B * 256, dtype=torch.float32, device=self.device)
         c1, c2, dl, hd = m.convs[0], m.convs[1], m.dense_tail, m.heads
         group = [0, int(gs.cuda_stream), *map(int, g.env.native_state()), g.h_act.data_ptr(), g.h_new.data_ptr(),
                  g.h_rew.data_ptr(), g.h_done.data_ptr(), g.ep_rew.ctypes.data, g.ep_len.ctypes.data]
-        weights = [c1.weight.data_ptr(), c1.bias.data_ptr(), c2.weight.data_ptr(), c2.bias.data_ptr(),
-                   dl.weight.data_ptr(), dl.bias.data_ptr(), hd.weight.data_ptr(), hd.bias.data_ptr()]
-        bufs = [g.s_obs.data_ptr(), int(g.h_new_dev), g.buf_obs.data_ptr(), self._server_h2.data_ptr(),
+        if x3:
+            from ray_memory_management_amd.ops import x3 as X3
+
+            P = m.x3_pairs()
+            S_ = hip.x3_dense_fwd_part_slices(B, 3872, 256)
+            self._server_h2 = X3.Pair.empty((B, 3872), self.device)
+            h2_hi, h2_lo = self._server_h2.hi.data_ptr(), self._server_h2.lo.data_ptr()
+            weights = ([P[n].hi.data_ptr() for n in m._X3_NAMES] + [P[n].lo.data_ptr() for n in m._X3_NAMES])
+        else:
+            S_ = hip.dense_fwd_part_slices(B, 3872, 256)
+            self._server_h2 = torch.empty((B, 3872), dtype=torch.bfloat16, device=self.device)
+            h2_hi, h2_lo = self._server_h2.data_ptr(), 0
+            weights = [c1.weight.data_ptr(), c1.bias.data_ptr(), c2.weight.data_ptr(), c2.bias.data_ptr(),
+                       dl.weight.data_ptr(), dl.bias.data_ptr(), hd.weight.data_ptr(), hd.bias.data_ptr()]
+        self._server_hpart = torch.empty(S_ * B * 256, dtype=torch.float32, device=self.device)
+        bufs = [g.s_obs.data_ptr(), int(g.h_new_dev), g.buf_obs.data_ptr(), h2_hi,
                 self._server_hpart.data_ptr(), g.buf_act.data_ptr(), g.buf_logp.data_ptr(), g.buf_vf.data_ptr(),
                 g.buf_logits.data_ptr(), int(g.h_act_dev), g.ctr_t.data_ptr()]
+        if x3:
+            bufs.append(h2_lo)
         if os.environ.get("RMM_ROLLOUT_SERVER_PROF"):  # per-step phase stamps of workgroup 0 (probe)
             self._server_prof = torch.zeros((self.T, 5), dtype=torch.int64, device=self.device)
             bufs.append(self._server_prof.data_ptr())
@@ -632,7 +724,7 @@ class HybridRolloutWorker(GPURolloutWorker):
         wgs = int(os.environ.get("RMM_ROLLOUT_SERVER_WGS", "128"))
         self._server_cache = dict(group=group, weights=weights, w1s=list(c1.weight.stride()),
                                   w2s=list(c2.weight.stride()), bufs=bufs, B=B, S=S_, A1=A1, seed=int(g.seed),
-                                  workgroups=max(wgs, B))
+                                  workgroups=max(wgs, B), x3=x3)
         return self._server_cache
 
     def _native_loop(self, G, S):

@@ -134,17 +134,51 @@ class LearnerActor:
         flat = L.w_bf16 if L.w_bf16 is not None else L.master
         return {"__rmm_flat_bf16__": flat.detach().clone(), "__rmm_layout__": layout}
 
-    def shared_weights_device(self):
-        """Zero-copy weight sharing with co-located rollout workers (opt-in, RMM_SHARED_WEIGHTS=1):
-        the bf16 compute weights move ONCE into an HBM object of this process's GPU object store
-        and the learner keeps updating them in place there; a rollout worker on the same GPU maps
-        the object (hipIPC) and points its parameters at it, so no weights move per iteration. Safe
-        because the training loop orders every update (ends with a host sync) before the next
-        sample, and every sample (ends with a stream sync) before the next update. The owner's view
-        pins the object (never spilled)."""
+    def shared_weights_kind(self):
+        """Which live weights this learner can share zero-copy: "bf16" (the bf16 compute weights), "x3"
+        (the fp32 learner's split-bf16 pair) or None (CPU / autograd learners: publish copies instead)."""
         L = self.learner
-        if self.device == "cpu" or not getattr(L, "fast", False) or L.w_bf16 is None:
-            return self.get_weights_device()
+        if self.device == "cpu" or not getattr(L, "fast", False):
+            return None
+        if L.w_bf16 is not None:
+            return "bf16"
+        return "x3" if getattr(L, "w_x3", None) is not None else None
+
+    def _layout(self):
+        L = self.learner
+        names = {id(p): n for n, p in L.model.named_parameters()}
+        layout, off = [], 0
+        for p in L.params:
+            layout.append((names[id(p)], off, tuple(p.shape), tuple(p.stride())))
+            off += p.numel()
+        return layout
+
+    def shared_weights_device(self):
+        """Zero-copy weight sharing with co-located rollout workers (default on): the live compute
+        weights (bf16, or the fp32 learner's split pair) move ONCE into HBM objects of this process's GPU
+        object store and the learner keeps updating them in place there; a rollout worker on the same
+        GPU maps the objects (hipIPC) and points its parameters at them, so no weights move per
+        iteration. Safe because the training loop orders every update (ends with a host sync) before
+        the next sample, and every sample (ends with a stream sync) before the next update. The owner's
+        views pin the objects (never spilled). Learners without live weights to share raise: the
+        driver checks shared_weights_kind() first and publishes copies for them."""
+        L = self.learner
+        kind = self.shared_weights_kind()
+        if kind is None:
+            raise RuntimeError("this learner has no live device weights to share; publish get_weights_device()")
+        if kind == "x3":
+            if getattr(self, "_shared", None) is None:
+                import ray_memory_management_amd as rt
+
+                # three objects: the fp32 master (the parameters) and its split pair (what the kernels read)
+                refs = [rt.put(L.master.detach().clone()), rt.put(L.w_x3.hi.detach().clone()),
+                        rt.put(L.w_x3.lo.detach().clone())]
+                views = [rt.get(r) for r in refs]  # owner-side zero-copy views (pin the objects)
+                L.rebind_master(views[0])
+                L.rebind_x3(views[1], views[2])
+                self._shared = (refs, views, self._layout())
+            refs, _, layout = self._shared
+            return {"__rmm_shared_x3__": list(refs), "__rmm_layout__": layout}
         if getattr(self, "_shared", None) is None:
             import os
             import sys
@@ -243,6 +277,12 @@ class LearnerGroup:
 
     def get_weights(self):
         return ray.get(self.weights_ref())
+
+    def shared_kind(self):
+        """Learner 0's shareable live-weight kind ("bf16", "x3" or None), asked once."""
+        if not hasattr(self, "_shared_kind"):
+            self._shared_kind = ray.get(self.learners[0].shared_weights_kind.remote()) if self.learners else None
+        return self._shared_kind
 
     def shared_weights_refs(self) -> List:
         """One shared-weights descriptor per learner (LearnerActor.shared_weights_device)."""

@@ -436,6 +436,83 @@ class VisionNetwork(nn.Module):
                 and self.heads.weight.dtype == torch.bfloat16 and not torch.is_autocast_enabled()
                 and not os.environ.get("RMM_NO_FUSED_TRUNK"))
 
+    # ------------------------------------------------------------ precision-matched (fp32) fused path
+    # The fp32 policy keeps fp32 parameters; its fused kernels (K10x / K13x / K16x, csrc/hip/x3_kernels.hip)
+    # read every weight as a split bf16 pair hi + lo (rllib/ops/x3.py). The owner attaches the pairs:
+    # the PPO learner attaches views of the flat pair its optimizer rewrites after every step, a rollout
+    # worker its own pair buffers (copied weights, refresh_x3) or views of the learner's live pair
+    # (zero-copy shared weights).
+    _X3_NAMES = ("convs.0.weight", "convs.0.bias", "convs.1.weight", "convs.1.bias", "dense_tail.weight",
+                 "dense_tail.bias", "heads.weight", "heads.bias")
+
+    def attach_x3(self, pairs) -> None:
+        """pairs: {parameter name: ops.x3.Pair} for the 8 Nature-CNN parameters (or None to detach)."""
+        if pairs is not None and set(pairs) != set(self._X3_NAMES):
+            raise ValueError(f"attach_x3 needs pairs for {self._X3_NAMES}")
+        self._x3 = pairs
+
+    def refresh_x3(self) -> None:
+        """(Re)split the fp32 parameters into this model's own pair buffers (after a weight copy)."""
+        from ray_memory_management_amd.ops import x3
+
+        params = dict(self.named_parameters())
+        own = getattr(self, "_x3_own", None)
+        if own is None or any(own[n].hi.shape != params[n].shape for n in self._X3_NAMES):
+            own = self._x3_own = {n: x3.split_like(params[n]) for n in self._X3_NAMES}
+        else:
+            for n in self._X3_NAMES:
+                p = params[n].detach()
+                own[n].hi.copy_(p.to(torch.bfloat16))
+                own[n].lo.copy_((p - own[n].hi.float()).to(torch.bfloat16))
+        self._x3 = own
+
+    def x3_pairs(self):
+        return getattr(self, "_x3", None)
+
+    def fused_x3_ok(self, obs) -> bool:
+        """The fp32 policy's fused path applies: Nature-CNN layout, u8 frames, fp32 weights with attached pairs."""
+        return (self.nature and getattr(self, "_x3", None) is not None and obs.is_cuda and obs.dtype == torch.uint8
+                and obs.dim() == 4 and tuple(obs.shape[1:]) == (4, 84, 84) and obs.is_contiguous()
+                and self.heads.weight.dtype == torch.float32 and 3 <= self.heads.out_features <= 16
+                and self.dense_tail.out_features == 256 and self.dense_tail.in_features == 3872
+                and not os.environ.get("RMM_NO_X3"))
+
+    @torch.no_grad()
+    def forward_sample_x3(self, obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now, done=None, push=None) -> bool:
+        """fp32 rollout step: K10x trunk (push mode when given) → K13x split-K → K16x (fp32 head row,
+        Gumbel-max sampling, rollout-row stores, optional step advance). Same contract as forward_sample."""
+        from ray_memory_management_amd._native import require_hip
+        from ray_memory_management_amd.ops import x3
+
+        if not self.fused_x3_ok(obs) or (push is not None and len(push) == 3):
+            return False
+        P = self._x3
+        hip = require_hip()
+        B = obs.shape[0]
+        dev = obs.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        ws = getattr(self, "_x3_ws", None)
+        if ws is None or ws["B"] != B:
+            S = x3.dense_part_slices(B, 3872, 256)
+            ws = self._x3_ws = {"B": B, "h2": x3.Pair.empty((B, 3872), dev), "S": S,
+                                "hpart": torch.empty(S * B * 256, dtype=torch.float32, device=dev)}
+        w1, b1, w2, b2 = (P[n] for n in self._X3_NAMES[:4])
+        if push is not None:
+            nf, rows = push[:2]
+            hip.x3_trunk_fwd_push(obs.data_ptr(), int(nf), rows.data_ptr() if rows is not None else 0,
+                                  t_ptr.data_ptr(), B, w1.ptrs(), list(w1.hi.stride()), b1.ptrs(), w2.ptrs(),
+                                  list(w2.hi.stride()), b2.ptrs(), ws["h2"].ptrs(), stream)
+        else:
+            x3.trunk_fwd(obs, w1, b1, w2, b2, h2=ws["h2"])
+        hip.x3_dense_fwd_part(ws["h2"].ptrs(), P["dense_tail.weight"].ptrs(), B, 3872, 256, ws["hpart"].data_ptr(),
+                              ws["S"], stream)
+        hip.x3_heads_sample(ws["hpart"].data_ptr(), ws["S"], P["dense_tail.bias"].ptrs(), P["heads.weight"].ptrs(),
+                            P["heads.bias"].ptrs(), t_ptr.data_ptr(), ctr.data_ptr(), seed, act.data_ptr(),
+                            logp.data_ptr(), vf.data_ptr(), lout.data_ptr(),
+                            act_now.data_ptr() if hasattr(act_now, "data_ptr") else int(act_now), B,
+                            self.heads.out_features, stream, done=done.data_ptr() if done is not None else 0)
+        return True
+
     def forward_frames(self, obs, idx=None, ctr=None, period: int = 1, rows: int = None):
         """u8 frames (optionally gathered by a minibatch index window) → heads [rows, A+1], with both
         convs in the fused K10 kernel."""
@@ -455,6 +532,8 @@ class VisionNetwork(nn.Module):
         (then only the push runs and False is returned)."""
         from ray_memory_management_amd._native import require_hip
 
+        if self.fused_x3_ok(obs) and not (push is not None and len(push) == 3):
+            return self.forward_sample_x3(obs, t_ptr, ctr, seed, act, logp, vf, lout, act_now, done=done, push=push)
         B = obs.shape[0]
         layer, heads = self.dense_tail, self.heads
         if not (self.fused_trunk_ok(obs) and heads.out_features >= 3 and heads.out_features <= 16

@@ -59,6 +59,17 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def _x3_available() -> bool:
+    """The precision-matched learner's split-bf16 kernels (csrc/hip/x3_kernels.hip) are built in;
+    RMM_NO_X3=1 sends compute_dtype fp32 back through autograd (MIOpen / hipBLASLt), for A/B only."""
+    if os.environ.get("RMM_NO_X3"):
+        return False
+    try:
+        return hasattr(require_hip(), "x3_trunk_fwd")
+    except Exception:
+        return False
+
+
 def _comm_overlap() -> bool:
     """Multi-rank step with the dense-bucket all-reduce forked onto a comm stream beside the trunk
     backward (opt-in: the fork / join costs more than it hides on MI355X)."""
@@ -240,6 +251,15 @@ class PPOLearner:
                 p.data = view
                 self.params.append(p)
                 off += k
+        # fp32 learner on the hand-written kernels: the optimizer keeps a split-bf16 pair (hi + lo) of the
+        # fp32 master next to it (K6 writes both planes), which the x3 kernels read (csrc/hip/x3_device.h)
+        self.x3 = self.fp32 and _x3_available()
+        self.w_x3 = None
+        if self.x3:
+            from ray_memory_management_amd.ops import x3 as X3
+
+            self.w_x3 = X3.split(self.master)
+            self._attach_x3()
         self.m1 = torch.zeros(n, dtype=torch.float32, device=dev)
         self.m2 = torch.zeros(n, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(n, dtype=self.cdt, device=dev)
@@ -278,8 +298,66 @@ class PPOLearner:
         self._manual = self._manual_layout()
 
     def _wptr(self) -> int:
-        """K6's bf16 weight output (0 for the fp32 learner: its parameters are the master)."""
-        return self.w_bf16.data_ptr() if self.w_bf16 is not None else 0
+        """K6's bf16 weight output: the bf16 compute weights, the hi plane of the fp32 learner's split
+        pair, or 0 (fp32 learner without the x3 kernels: its parameters are the master)."""
+        if self.w_bf16 is not None:
+            return self.w_bf16.data_ptr()
+        return self.w_x3.hi.data_ptr() if self.w_x3 is not None else 0
+
+    def _wlo(self) -> int:
+        """K6's lo-plane output (the split pair's residual), 0 unless the fp32 learner runs the x3 kernels."""
+        return self.w_x3.lo.data_ptr() if self.w_x3 is not None else 0
+
+    def _x3_views(self):
+        """{parameter name: Pair view} of the flat split pair, in each parameter's memory layout."""
+        names = {id(p): n for n, p in self.model.named_parameters()}
+        out, off = {}, 0
+        for p in self.params:
+            out[names[id(p)]] = self.w_x3.as_strided(p.size(), p.stride(), off)
+            off += p.numel()
+        return out
+
+    def _attach_x3(self):
+        """Point the model's fused fp32 path (rollout sampling with the learner's own model) at the pair."""
+        if hasattr(self.model, "attach_x3") and getattr(self.model, "nature", False):
+            try:
+                self.model.attach_x3(self._x3_views())
+            except ValueError:
+                pass
+
+    def rebind_master(self, flat: torch.Tensor) -> None:
+        """Move the fp32 master (the fp32 learner's parameters are views of it) to `flat`, same layout,
+        e.g. an HBM object co-located rollout workers alias; K6 keeps updating it in place."""
+        if not self.fast or flat.dtype != torch.float32 or flat.numel() != self.n_params \
+                or flat.device != self.master.device:
+            raise ValueError("rebind_master: flat fp32 buffer of the learner's size on its device expected")
+        torch.cuda.synchronize(self.device)
+        with torch.no_grad():
+            flat.copy_(self.master)
+            if self.fp32:
+                off = 0
+                for p in self.params:
+                    p.data = flat.as_strided(p.size(), p.stride(), off)
+                    off += p.numel()
+        self.master = flat
+        self._graph = self._graphs_split = None
+
+    def rebind_x3(self, hi: torch.Tensor, lo: torch.Tensor) -> None:
+        """Move the fp32 learner's split pair to (hi, lo) (e.g. HBM objects that co-located rollout
+        workers map zero-copy), same layout; captured graphs are dropped (recaptured next update)."""
+        from ray_memory_management_amd.ops import x3 as X3
+
+        if self.w_x3 is None:
+            raise RuntimeError("rebind_x3 needs the fp32 learner on the x3 kernels")
+        for t in (hi, lo):
+            if t.dtype != torch.bfloat16 or t.numel() != self.n_params or t.device != self.w_x3.hi.device:
+                raise ValueError("rebind_x3: flat bf16 planes of the learner's size on its device expected")
+        torch.cuda.synchronize(self.device)
+        hi.copy_(self.w_x3.hi)
+        lo.copy_(self.w_x3.lo)
+        self.w_x3 = X3.Pair(hi, lo)
+        self._attach_x3()
+        self._graph = self._graphs_split = None
 
     def _bucket_order(self, params):
         """Flat-bucket order: for the Nature-CNN layout the trunk (conv) parameters first, then
@@ -304,7 +382,7 @@ class PPOLearner:
         from ray_memory_management_amd.rllib.models import VisionNetwork
 
         m = self.model
-        if self.fp32:  # the hand-written SGD-step kernels (K10 / K12 / K13 / K15) compute in bf16
+        if self.fp32 and not self.x3:  # fp32 without the split-bf16 kernels: autograd (RMM_NO_X3)
             return None
         if not (self.cfg.get("manual_step", True) and isinstance(m, VisionNetwork) and m.nature
                 and m.dense_tail is not None and not os.environ.get("RMM_NO_MANUAL_STEP")):
@@ -321,6 +399,8 @@ class PPOLearner:
         return sum(p.numel() for p in order[:4])
 
     def _manual_ok(self, full) -> bool:
+        if self.x3:
+            return self._manual is not None and self.model.fused_x3_ok(full["obs"])
         return (self._manual is not None and full["obs"].dtype == torch.uint8 and full["mbs"] <= 640
                 and self.model.fused_trunk_ok(full["obs"]) and not os.environ.get("RMM_NO_K12")
                 and not os.environ.get("RMM_NO_K15"))
@@ -329,6 +409,8 @@ class PPOLearner:
         ws = getattr(self, "_mws", None)
         if ws is not None and ws["mbs"] == mbs:
             return ws
+        if self.x3:
+            return self._manual_ws_x3(mbs)
         dev, bf = self.device, torch.bfloat16
         A1 = self.model.heads.out_features
         K = self.model.dense_tail.in_features
@@ -343,8 +425,71 @@ class PPOLearner:
         self._mws = ws
         return ws
 
+    def _manual_ws_x3(self, mbs):
+        """Split-pair activations of the fp32 SGD step (K10x → K13x → K15x → K12x → K10x bwd)."""
+        from ray_memory_management_amd.ops import x3 as X3
+
+        dev = self.device
+        A1 = self.model.heads.out_features
+        K = self.model.dense_tail.in_features
+        S = X3.dense_part_slices(mbs, K, 256)
+        ws = {"mbs": mbs, "h1": X3.Pair.empty((mbs, 441, 16), dev), "h2": X3.Pair.empty((mbs, K), dev),
+              "hid": X3.Pair.empty((mbs, 256), dev), "dz": X3.Pair.empty((mbs, A1), dev),
+              "dpre": X3.Pair.empty((mbs, 256), dev), "dx": X3.Pair.empty((mbs, K), dev),
+              "dpre1": X3.Pair.empty((mbs, 441, 16), dev), "S": S,
+              "hpart": torch.empty(S * mbs * 256, dtype=torch.float32, device=dev),
+              "part": torch.empty(X3.trunk_partial_floats(mbs), dtype=torch.float32, device=dev)}
+        self._mws = ws
+        return ws
+
+    def _x3_fwd_dense_bwd(self, full):
+        """fp32 step, first half: K10x fwd → K13x → K15x (loss stats, dheads, dpre) → K12x (dense + heads
+        gradients, fp32, into the bucket; dx for the trunk backward)."""
+        h = require_hip()
+        m = self.model
+        P = self._x3_views_cached()
+        mbs, period, idx, ctr = full["mbs"], full["period"], full["idx"], self._ctr()
+        ws = self._manual_ws(mbs)
+        st = _stream()
+        K, A1 = m.dense_tail.in_features, m.heads.out_features
+        w1, b1, w2, b2 = (P[n] for n in m._X3_NAMES[:4])
+        wd, bd, wh, bh = (P[n] for n in m._X3_NAMES[4:])
+        h.x3_trunk_fwd(full["obs"].data_ptr(), idx.data_ptr(), ctr.data_ptr(), int(period), int(mbs), w1.ptrs(),
+                       list(w1.hi.stride()), b1.ptrs(), w2.ptrs(), list(w2.hi.stride()), b2.ptrs(), ws["h1"].ptrs(),
+                       ws["h2"].ptrs(), st)
+        h.x3_dense_fwd_part(ws["h2"].ptrs(), wd.ptrs(), mbs, K, 256, ws["hpart"].data_ptr(), ws["S"], st)
+        h.x3_heads_ppo(ws["hpart"].data_ptr(), ws["S"], bd.ptrs(), wh.ptrs(), bh.ptrs(), full["cols"].data_ptr(),
+                       self.coef.data_ptr(), self.acc.data_ptr(), self._one.data_ptr(), mbs, A1, ws["dz"].ptrs(),
+                       ws["dpre"].ptrs(), ws["hid"].ptrs(), st, cidx=idx.data_ptr(), ctr=ctr.data_ptr(),
+                       period=int(period))
+        g = [p._rmm_grad_out for p in self.params]
+        h.x3_dense_heads_bwd(ws["dz"].ptrs(), A1, ws["hid"].ptrs(), ws["h2"].ptrs(), wd.ptrs(), ws["dpre"].ptrs(), mbs,
+                             K, ws["dx"].ptrs(), g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr(), st)
+
+    def _x3_trunk_bwd(self, full):
+        """fp32 step, second half: K10x conv2 backward → conv1 weight gradient → reduce (fp32 trunk grads)."""
+        h = require_hip()
+        m = self.model
+        P = self._x3_views_cached()
+        ws = self._manual_ws(full["mbs"])
+        g = [p._rmm_grad_out for p in self.params]
+        w2 = P[m._X3_NAMES[2]]
+        h.x3_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), self._ctr().data_ptr(), int(full["period"]),
+                       int(full["mbs"]), w2.ptrs(), list(w2.hi.stride()), ws["h1"].ptrs(), ws["h2"].hi.data_ptr(),
+                       ws["dx"].ptrs(), ws["dpre1"].ptrs(), ws["part"].data_ptr(), g[0].data_ptr(),
+                       list(m.convs[0].weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream())
+
+    def _x3_views_cached(self):
+        key = (self.w_x3.hi.data_ptr(), self.w_x3.lo.data_ptr())
+        c = getattr(self, "_x3v", None)
+        if c is None or c[0] != key:
+            c = self._x3v = (key, self._x3_views())
+        return c[1]
+
     def _manual_fwd_dense_bwd(self, full):
         """K10 fwd → K13 → K15 (loss stats + dheads + dpre) → K12: dense+heads grads into the bucket."""
+        if self.x3:
+            return self._x3_fwd_dense_bwd(full)
         h = require_hip()
         m = self.model
         c1, c2, dl, hd = m.convs[0], m.convs[1], m.dense_tail, m.heads
@@ -376,6 +521,8 @@ class PPOLearner:
 
     def _manual_trunk_bwd(self, full):
         """K10 backward: trunk grads (conv1/conv2 weights + biases) into the bucket."""
+        if self.x3:
+            return self._x3_trunk_bwd(full)
         h = require_hip()
         c1, c2 = self.model.convs[0], self.model.convs[1]
         ws = self._manual_ws(full["mbs"])
@@ -427,7 +574,7 @@ class PPOLearner:
         11.04 -> 10.62 / 10.67 ms per iteration on MI355X (profiles/tail_adam_r4.txt). RMM_TAIL_ADAM=0
         restores the separate K6."""
         return (self._manual is not None and self.world == 1 and self.clip_out is None and self._manual % 4 == 0
-                and not self._fused_adam() and not self._split_adam_ok()
+                and not self.x3 and not self._fused_adam() and not self._split_adam_ok()
                 and os.environ.get("RMM_TAIL_ADAM", "1") != "0")
 
     def _tail_adam_args(self):
@@ -464,7 +611,7 @@ class PPOLearner:
         Opt-in (RMM_FUSED_ADAM=1): measured 5 µs per SGD step SLOWER on MI355X (fused loop 12.2 vs
         11.7 ms/iter, profiles/fused_adam_r3.txt) — K12 runs 122 workgroups, so the 26 MB of Adam
         traffic its epilogue adds moves through half the CUs, while K6 spreads it over the whole chip."""
-        return (self._manual is not None and self.world == 1 and self.clip_out is None
+        return (self._manual is not None and self.world == 1 and self.clip_out is None and not self.x3
                 and not self._split_adam_ok() and os.environ.get("RMM_FUSED_ADAM") == "1")
 
     def _fused_adam_args(self, bump: bool):
@@ -491,11 +638,11 @@ class PPOLearner:
         if self._parity and not (self._parity_last and self._par == 0):
             # chained graph: advance into the other copy from one lane (see __init__)
             h.adam_flat(*args, step_ctr=cur.data_ptr() + 8, bump=cur.data_ptr(), nbump=2, scale_ptr=scale_ptr,
-                        bump_next=self._ctrs[1 - self._par].data_ptr())
+                        bump_next=self._ctrs[1 - self._par].data_ptr(), wlo=self._wlo())
             self._par ^= 1
         else:  # in place: the last workgroup advances the counters after every workgroup read them
             h.adam_flat(*args, step_ctr=cur.data_ptr() + 8, bump=cur.data_ptr(), nbump=2,
-                        done=self._bump_done.data_ptr(), scale_ptr=scale_ptr)
+                        done=self._bump_done.data_ptr(), scale_ptr=scale_ptr, wlo=self._wlo())
 
     def _adam_range(self, lo: int, hi: int, stream: int, bump: bool, max_blocks: int = 0):
         """K6 over params [lo, hi) of the flat buckets on `stream`; `bump` advances the device
@@ -514,7 +661,7 @@ class PPOLearner:
         K6's 16-B vector alignment. Opt-in (RMM_SPLIT_ADAM_BLOCKS=<grid cap>): with the full
         977-block grid beside K10 backward the SGD step got 16 µs SLOWER on MI355X (the Adam
         waves delay the LDS-bound trunk workgroups), profiles/split_adam_r3.txt."""
-        return (self._manual is not None and self.clip_out is None and self._manual % 4 == 0
+        return (self._manual is not None and self.clip_out is None and self._manual % 4 == 0 and not self.x3
                 and int(os.environ.get("RMM_SPLIT_ADAM_BLOCKS", "0")) > 0)
 
     def _overlapped_tail(self, full):
@@ -689,9 +836,10 @@ class PPOLearner:
 
     def _capture(self, full):
         self._dbg("capture: start")
+        wx = (self.w_x3.hi, self.w_x3.lo) if self.w_x3 is not None else (None, None)
         saved = (self.master.clone(), self.m1.clone(), self.m2.clone(),
                  self.w_bf16.clone() if self.w_bf16 is not None else None, self.ctr.clone(),
-                 self.acc.clone())
+                 self.acc.clone(), *(t.clone() if t is not None else None for t in wx))
         manual = self._manual_ok(full)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -798,7 +946,7 @@ class PPOLearner:
                 self._fast_step(full, False)
             self._graph = g
         self._dbg("capture: graphs captured")
-        for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc), saved):
+        for dst, src in zip((self.master, self.m1, self.m2, self.w_bf16, self.ctr, self.acc, *wx), saved):
             if dst is not None:
                 dst.copy_(src)  # undo warm-up updates
         self._dbg("capture: state restored")
@@ -1120,6 +1268,10 @@ class PPOLearner:
                     self.master.as_strided(p.size(), p.stride(), off).copy_(src)
                     p.copy_(src)
                     off += p.numel()
+                if self.w_x3 is not None:  # the kernels' split pair follows the master (in place: aliases stay valid)
+                    from ray_memory_management_amd.ops import x3 as X3
+
+                    X3.split(self.master, out=self.w_x3)
             else:
                 self.model.load_state_dict(w)
 

@@ -140,6 +140,37 @@ def test_freed_object_not_recycled_while_reader_holds_view(gpu_ray):
     assert ray.get(o.gpu_objects.remote()) == 0  # deferred frees completed once the views died
 
 
+def test_killed_cross_process_reader_releases_hbm(gpu_ray):
+    """A reader in another process maps an HBM object zero-copy (its view pins the descriptor in the
+    shm store) and is SIGKILLed while holding it: the head releases the dead client's store pins
+    (Store::ReleaseClient), the descriptor goes, and the owner's deferred free recycles the HBM."""
+    import torch
+
+    from ray_memory_management_amd._private import gpu_object_store as gos
+    from ray_memory_management_amd._private.worker import global_worker
+
+    def n_objects():
+        return sum(s["num_objects"] for s in gos.stats(global_worker).values())
+
+    @ray.remote(num_gpus=0.5)
+    class Reader:
+        def hold(self, refs):
+            self.x = ray.get(refs[0])  # zero-copy hipIPC view: pins the descriptor
+            return float(self.x.sum())
+
+    base = n_objects()
+    ref = ray.put(torch.ones(1 << 22, device="cuda"))
+    assert n_objects() == base + 1
+    r = Reader.remote()
+    assert ray.get(r.hold.remote([ref])) == float(1 << 22)
+    ray.kill(r)
+    del ref
+    deadline = time.time() + 20
+    while time.time() < deadline and n_objects() > base:
+        time.sleep(0.1)
+    assert n_objects() == base, gos.stats(global_worker)
+
+
 def test_nested_cuda_tensors_stay_in_hbm(gpu_ray):
     import torch
 

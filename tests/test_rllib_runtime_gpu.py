@@ -438,10 +438,14 @@ def test_hybrid_recapture_mid_life_keeps_fragments(cuda):
         assert torch.equal(fa["_raw"], fb["_raw"]) and torch.equal(fa["_boot"], fb["_boot"])
 
 
-def test_ppo_hybrid_shared_weights(cuda, monkeypatch):
-    """Zero-copy weights (RMM_SHARED_WEIGHTS=1): the learner's bf16 weights move once into an HBM
-    object that the co-located hybrid rollout workers alias over hipIPC; after the learner's next
-    in-place Adam steps the workers' parameters ARE the new weights (no per-iteration publish)."""
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_ppo_hybrid_shared_weights(cuda, monkeypatch, dtype):
+    """Zero-copy weights (RMM_SHARED_WEIGHTS=1): the learner's live weights move once into HBM objects
+    that the co-located hybrid rollout workers alias over hipIPC; after the learner's next in-place
+    Adam steps the workers' parameters ARE the new weights (no per-iteration publish). bf16: the bf16
+    compute weights. fp32 (precision-matched): the fp32 master (the workers' parameters) and its split
+    pair (what their x3 kernels read) — and the weights the workers sample with change every iteration
+    (a one-time snapshot must never be mistaken for a live alias)."""
     import ray_memory_management_amd as ray
     from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
 
@@ -451,48 +455,62 @@ def test_ppo_hybrid_shared_weights(cuda, monkeypatch):
         cfg = (PPOConfig().environment("SyntheticAtariVec-v0", env_config={"episode_len": 50})
                .rollouts(num_rollout_workers=2, num_envs_per_worker=5, rollout_fragment_length=20,
                          postprocess_on_learner=True)
-               .training(train_batch_size=200, sgd_minibatch_size=50, num_sgd_iter=2)
+               .training(train_batch_size=200, sgd_minibatch_size=50, num_sgd_iter=2, compute_dtype=dtype, lr=1e-3)
                .resources(num_learner_workers=1, num_gpus_per_learner_worker=0.5, num_gpus_per_worker=0.25)
                .debugging(seed=0))
         algo = cfg.build()
+        ws = algo.workers.remote_workers()
+        seen = []
         for _ in range(3):
             r = algo.train()
+            if dtype == "fp32":  # what the workers' kernels read: the pair they alias
+                seen.append(ray.get(ws[0].apply.remote(
+                    lambda x: {n: p.float().cpu().numpy() for n, p in x.model.x3_pairs().items()})))
         st = r["info"]["learner"]["default_policy"]["learner_stats"]
         assert np.isfinite(st["total_loss"]) and st["num_sgd_steps"] == 8
         assert algo._shared_weights_ok() and algo._dev_refs is not None
+        assert algo.learner_group.shared_kind() == ("x3" if dtype == "fp32" else "bf16")
         # the next iteration's samples were queued behind the last update (RMM_PREFETCH_SAMPLE default)
         assert algo._prefetched is not None and len(algo._prefetched) == 2
-        ws = algo.workers.remote_workers()
         assert all(ray.get([w.apply.remote(lambda x: getattr(x, "_shared_key", None) is not None) for w in ws]))
         master = algo.learner_group.get_weights()
         for w in ws:  # no set_weights here: the aliased parameters already hold the last update
             got = ray.get(w.get_weights.remote())
             for k, v in master.items():
-                want = torch.from_numpy(np.ascontiguousarray(v)).to(torch.bfloat16).float().numpy()
+                want = np.ascontiguousarray(v)
+                if dtype == "bf16":
+                    want = torch.from_numpy(want).to(torch.bfloat16).float().numpy()
                 np.testing.assert_array_equal(got[k], want)
+        if dtype == "fp32":
+            pair = ray.get(ws[1].apply.remote(lambda x: {n: p.float().cpu().numpy() for n, p in x.model.x3_pairs().items()}))
+            for k, v in master.items():  # hi + lo == the fp32 master to the split's 2^-17
+                np.testing.assert_allclose(pair[k], v, rtol=2.0 ** -16, atol=1e-12)
+            for a, b in zip(seen, seen[1:]):  # weights move every iteration (not a stale snapshot)
+                assert any(not np.array_equal(a[k], b[k]) for k in a)
         algo.stop()
     finally:
         ray.shutdown()
 
 
 @pytest.mark.parametrize("seq", ["0", "1"])
-@pytest.mark.parametrize("n_envs,T", [(6, 12), (50, 20)])
-def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T, seq):
+@pytest.mark.parametrize("n_envs,T,dtype", [(6, 12, "bf16"), (50, 20, "bf16"), (6, 12, "fp32"), (50, 20, "fp32")])
+def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T, seq, dtype):
     """The native loop with direct kernel launches per policy step (RMM_ROLLOUT_DIRECT=1: K10 push →
-    K13s → K16 launched from the loop's thread, no graph) yields the same fragments, bit for bit, and
-    the same finished episodes as the per-step graph launches."""
+    K13s → K16 launched from the loop's thread, no graph; fp32 policy: K10x push → K13x → K16x) yields
+    the same fragments, bit for bit, and the same finished episodes as the per-step graph launches."""
     import torch
 
     from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
 
     cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": n_envs,
-           "rollout_fragment_length": T, "seed": 3}
+           "rollout_fragment_length": T, "seed": 3, "compute_dtype": dtype}
     monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
     monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "1")
     monkeypatch.setenv("RMM_ROLLOUT_SEQ", seq)  # "1": completion through K16's host word, no events
     a = HybridRolloutWorker(config=cfg)
     fa = [a.sample() for _ in range(3)]
     assert getattr(a, "_server_cache", None) is not None  # the direct path's argument cache
+    assert bool(a._server_cache.get("x3")) == (dtype == "fp32")  # fp32: the split-bf16 kernels
     if seq == "1":
         assert int(a._h_seq[0]) == T  # the last step (row T-1) stored T
     monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "0")
