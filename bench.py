@@ -10,7 +10,8 @@ Default mode ``runtime`` (BASELINE config "RLlib PPO, N GPU learner actors + CPU
 synthetic 84x84 frames, sample-batch GPU ingest + GAE HIP scan"):
 
 * ``PPO`` with ``num_learner_workers=N``: N learner ACTORS, one per GPU, each running the fused
-  bf16 learner (HIP graphs, MFMA kernels) and all-reducing gradients over RCCL (xGMI);
+  precision-matched fp32 learner (HIP graphs, hand-written split-bf16 MFMA kernels, fp32 master /
+  gradients / Adam) and all-reducing gradients across GPUs (peer-memory kernel over xGMI, RCCL fallback);
 * CPU rollout-worker ACTORS stepping the synthetic Atari vector env (native env core) on their CPU,
   with the policy on the worker's slice of the learner GPU (RLlib ``num_gpus_per_worker > 0``;
   default ``--rollout hybrid``): the whole fragment loop runs in C++ (csrc/hip/rollout_loop.cc) and
@@ -24,10 +25,12 @@ synthetic 84x84 frames, sample-batch GPU ingest + GAE HIP scan"):
   GAE + advantage standardisation run as one kernel (K17); with N learners the gradient bucket is
   all-reduced by the peer-memory kernel (csrc/hip/peer_allreduce.hip) inside the chained SGD graph.
 
-``--dtype bf16`` (default): bf16 MFMA kernels with fp32 master weights / Adam moments. ``--dtype fp32``:
-the precision-matched learner (fp32 weights, gradients and convolutions, as the reference's fp32
-torch PPO) and an fp32 rollout policy; at N=1 the bf16 run also reports it as
-``runtime_fp32_samples_per_s``.
+``--dtype fp32`` (default, the reference's precision: its torch PPO trains fp32,
+rllib/algorithms/ppo/ppo_torch_policy.py:70): the learner and the rollout policy run the x3 kernels
+(csrc/hip/x3_kernels.hip: every fp32 operand as a hi + lo bf16 pair, three bf16 MFMAs per product,
+fp32 accumulation; fp32 master weights, gradients, loss and Adam) — gfx950 has no TF32 and its fp32 MFMA
+runs at 1/16 of the bf16 rate. ``--dtype bf16``: bf16 operands (8 significant bits) with fp32 master
+weights / Adam moments; at N=1 the fp32 run also reports it as ``runtime_bf16_samples_per_s``.
 
 One timed step = one ``algo.train()`` iteration: sample 5000·N env steps, ingest, 10 epochs of
 500-sample minibatch SGD on every learner, publish weights. Weak scaling (per-GPU batch fixed).
@@ -152,7 +155,8 @@ def _fused_loop(args, world, rank, local_rank, dist_backend):
     n_envs = TRAIN_BATCH // args.fragment
     env = GPUSyntheticAtariVectorEnv(n_envs, dev, num_actions=4, seed=rank)
     learner = PPOLearner(VisionNetwork(4), {"sgd_minibatch_size": args.minibatch, "num_sgd_iter": args.sgd_iters,
-                                            "train_batch_size": TRAIN_BATCH}, device=dev,
+                                            "train_batch_size": TRAIN_BATCH,
+                                            "compute_dtype": getattr(args, "dtype", "fp32")}, device=dev,
                          action_space=env.action_space)
     sampler = GPURolloutSampler(env, learner.model, fragment=args.fragment)
     for _ in range(args.warmup):
@@ -260,9 +264,10 @@ def main():
     ap.add_argument("--no-gpu-rollout", action="store_true",
                     help="skip the extra runtime measurement with GPU rollout actors")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL) or gloo (rehearsal)")
-    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="fp32",
                     help="learner / GPU policy compute precision (fp32 = precision-matched with the reference)")
-    ap.add_argument("--no-fp32", action="store_true", help="skip the extra fp32 runtime measurement (N=1)")
+    ap.add_argument("--no-fp32", action="store_true", help="bf16 headline: skip the extra fp32 runtime measurement")
+    ap.add_argument("--no-bf16", action="store_true", help="fp32 headline: skip the extra bf16 runtime measurement")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every learner on GPU 0 (RCCL ranks get distinct host ids "
                          "and use the socket transport; or --dist-backend gloo)")
@@ -354,10 +359,12 @@ def main():
             modes = [m for m in ("cpu", "hybrid", "gpu") if m != args.rollout]
             if args.dtype == "bf16" and not args.no_fp32:
                 modes.append("fp32")  # precision-matched learner + policy, same runtime path as `value`
+            if args.dtype == "fp32" and not args.no_bf16:
+                modes.append("bf16")  # bf16 operands, same runtime path as `value`
             for mode in modes:
                 a2 = copy.copy(args)
-                if mode == "fp32":
-                    a2.dtype = "fp32"
+                if mode in ("fp32", "bf16"):
+                    a2.dtype = mode
                 else:
                     a2.rollout = mode
                 algo2 = None
@@ -367,7 +374,7 @@ def main():
                     for _ in range(args.steps):
                         algo2.train()
                     e2 = time.perf_counter() - t0
-                    key = "runtime_fp32" if mode == "fp32" else f"runtime_{mode}_rollout"
+                    key = f"runtime_{mode}" if mode in ("fp32", "bf16") else f"runtime_{mode}_rollout"
                     extra[f"{key}_samples_per_s"] = round(TRAIN_BATCH * n_gpus * args.steps / e2, 1)
                     extra[f"{key}_ms_per_step"] = round(e2 / args.steps * 1e3, 3)
                 except Exception as ex:  # noqa: BLE001

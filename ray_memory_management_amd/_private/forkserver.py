@@ -9,9 +9,12 @@ modules once and never touches a GPU; each worker is a fork() of it (copy-on-wri
 milliseconds), which then applies the worker's own environment (GPU visibility, runtime env) before
 anything reads it and runs ``worker_main.main()``.
 
-Protocol (Unix socket, one JSON line per request): {"env": {...}, "log": path} →
-{"pid": child_pid} or {"error": msg}. The template reaps its children (SIGCHLD), so a dead worker
-never lingers as a zombie whose pid still answers kill(pid, 0).
+Protocol (Unix socket, JSON lines): the head sends {"env": {...}, "log": path} (fork a worker) or
+{"kill": pid, "sig": n}; the template answers a fork with {"pid": child_pid} or {"error": msg} and,
+unprompted, reports every child it reaps as {"exit": pid, "code": c} (c = exit status, or -signal as
+in subprocess). The head therefore learns real exit codes (OOM kill -9 vs segfault -11), and every
+signal to a worker is sent by the template, which only signals its own children that it has not
+reaped yet: a recycled pid can never be hit.
 """
 from __future__ import annotations
 
@@ -77,14 +80,19 @@ def serve(path: str):
         except ImportError:
             pass
 
+    children = set()   # forked, not reaped yet: the only pids this process ever signals
+    exited = []        # (pid, code) reaped, not reported yet
+
     def reap(*_):
         while True:
             try:
-                pid, _ = os.waitpid(-1, os.WNOHANG)
+                pid, status = os.waitpid(-1, os.WNOHANG)
             except ChildProcessError:
                 return
             if pid == 0:
                 return
+            children.discard(pid)
+            exited.append((pid, os.waitstatus_to_exitcode(status)))
 
     signal.signal(signal.SIGCHLD, reap)
     listen = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -94,17 +102,28 @@ def serve(path: str):
     listen.settimeout(1.0)
     conn = None
     buf = b""
+
+    def send(obj) -> None:
+        if conn is not None:
+            try:
+                conn.sendall(json.dumps(obj).encode() + b"\n")
+            except OSError:
+                pass
+
     while True:
         if conn is None:
             try:
                 conn, _ = listen.accept()
-                conn.settimeout(1.0)
+                conn.settimeout(0.05)  # exit reports go out within ~50 ms of the reap
             except socket.timeout:
                 if os.getppid() != head_pid:  # the head is gone
                     return
                 continue
             except InterruptedError:
                 continue
+        while exited:
+            pid, code = exited.pop(0)
+            send({"exit": pid, "code": code})
         try:
             data = conn.recv(1 << 20)
         except socket.timeout:
@@ -124,44 +143,47 @@ def serve(path: str):
             line, buf = buf.split(b"\n", 1)
             try:
                 req = json.loads(line)
+                if "kill" in req:
+                    pid = int(req["kill"])
+                    if pid in children:  # still ours and not reaped: the pid cannot have been reused
+                        try:
+                            os.kill(pid, int(req.get("sig", signal.SIGKILL)))
+                        except ProcessLookupError:
+                            pass
+                    continue
                 pid = os.fork()
                 if pid == 0:
                     _child(req["env"], req["log"], listen, conn)
+                children.add(pid)
                 reply = {"pid": pid}
             except Exception as e:  # noqa: BLE001
                 reply = {"error": repr(e)}
-            try:
-                conn.sendall(json.dumps(reply).encode() + b"\n")
-            except OSError:
-                pass
+            send(reply)
 
 
 class ForkedProc:
-    """Popen-like handle of a worker forked by the template (not our child: poll by pid)."""
+    """Popen-like handle of a worker forked by the template. Not our child: its exit code arrives as the
+    template's {"exit": pid, "code": c} report (the real status: -9 for an OOM kill, -11 for a
+    segfault), and signals are sent by the template, which only signals children it has not reaped."""
 
-    def __init__(self, pid: int):
+    def __init__(self, pid: int, client: "ForkClient"):
         self.pid = pid
         self.returncode = None
+        self._client = client
 
     def poll(self):
         if self.returncode is None:
-            try:
-                os.kill(self.pid, 0)
-            except ProcessLookupError:
-                self.returncode = -1
-            except PermissionError:
-                pass
+            self._client.drain()
+            code = self._client.exit_codes.pop(self.pid, None)
+            if code is not None:
+                self.returncode = code
+            elif self._client.lost and not _pid_exists(self.pid):
+                self.returncode = -1  # the template is gone: no exit report will come
         return self.returncode
 
     def wait(self, timeout=None):
-        # the template reaps the process, so there is no zombie for the caller to collect: a short
-        # wait (the head's reap-after-death) is one poll, never a sleep on the head's event loop
-        if timeout is not None and timeout <= 0.1:
-            if self.poll() is None:
-                import subprocess
-
-                raise subprocess.TimeoutExpired(f"pid {self.pid}", timeout)
-            return self.returncode
+        # a short wait (the head's reap-after-death) polls for ~the template's report period; never a
+        # long sleep on the head's event loop
         deadline = None if timeout is None else time.time() + timeout
         while self.poll() is None:
             if deadline is not None and time.time() >= deadline:
@@ -171,17 +193,25 @@ class ForkedProc:
             time.sleep(0.005)
         return self.returncode
 
+    def send_signal(self, sig):
+        if self.returncode is None:
+            self._client.signal(self.pid, sig)
+
     def kill(self):
-        try:
-            os.kill(self.pid, signal.SIGKILL)
-        except ProcessLookupError:
-            pass
+        self.send_signal(signal.SIGKILL)
 
     def terminate(self):
-        try:
-            os.kill(self.pid, signal.SIGTERM)
-        except ProcessLookupError:
-            pass
+        self.send_signal(signal.SIGTERM)
+
+
+def _pid_exists(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        pass
+    return True
 
 
 class ForkClient:
@@ -217,18 +247,63 @@ class ForkClient:
         if self.sock is None:
             raise RuntimeError("fork server did not come up")
 
+        self.exit_codes = {}  # pid -> exit code reported by the template, until its ForkedProc polls it
+        self.lost = False     # the template's connection closed
+
+    def _handle(self, line: bytes):
+        rep = json.loads(line)
+        if "exit" in rep:
+            self.exit_codes[int(rep["exit"])] = int(rep["code"])
+            return None
+        return rep
+
+    def drain(self) -> None:
+        """Read the exit reports that arrived (non-blocking)."""
+        if self.sock is None or self.lost:
+            return
+        try:
+            self.sock.setblocking(False)
+            while True:
+                data = self.sock.recv(1 << 16)
+                if not data:
+                    self.lost = True
+                    break
+                self.buf += data
+        except (BlockingIOError, InterruptedError):
+            pass
+        except OSError:
+            self.lost = True
+        finally:
+            try:
+                self.sock.settimeout(10.0)
+            except OSError:
+                pass
+        while b"\n" in self.buf:
+            line, self.buf = self.buf.split(b"\n", 1)
+            self._handle(line)
+
     def spawn(self, env: dict, log: str) -> ForkedProc:
         self.sock.sendall(json.dumps({"env": env, "log": log}).encode() + b"\n")
-        while b"\n" not in self.buf:
-            data = self.sock.recv(4096)
-            if not data:
-                raise RuntimeError("fork server closed the connection")
-            self.buf += data
-        line, self.buf = self.buf.split(b"\n", 1)
-        rep = json.loads(line)
+        while True:
+            while b"\n" not in self.buf:
+                data = self.sock.recv(4096)
+                if not data:
+                    self.lost = True
+                    raise RuntimeError("fork server closed the connection")
+                self.buf += data
+            line, self.buf = self.buf.split(b"\n", 1)
+            rep = self._handle(line)
+            if rep is not None:
+                break
         if "pid" not in rep:
             raise RuntimeError(f"fork server: {rep.get('error')}")
-        return ForkedProc(int(rep["pid"]))
+        return ForkedProc(int(rep["pid"]), self)
+
+    def signal(self, pid: int, sig: int) -> None:
+        try:
+            self.sock.sendall(json.dumps({"kill": int(pid), "sig": int(sig)}).encode() + b"\n")
+        except OSError:
+            self.lost = True
 
     def close(self):
         try:

@@ -229,6 +229,7 @@ class Head:
         self.gc_auto_interval = float(self.config.get("automatic_gc_min_interval_s", 30.0))
         self.mem_stats = collections.Counter()
         self._pins_pending = {}  # pid -> proc: exited clients whose store pins are released once gone
+        self._death_reports = {}  # pid -> (proc, event fields, time): WORKER_DIED waiting for the exit code
         self.sched = sched_ext().Scheduler()
         self.sched.set_spread_threshold(float(self.config.get("scheduler_spread_threshold", 0.5)))
         self.nodes: Dict[int, dict] = {}
@@ -280,6 +281,13 @@ class Head:
         self.max_workers = int(self.config.get("max_workers", max(64, 4 * int(res.get("CPU", 1)))))
         self.prestart = int(self.config.get("prestart_workers", min(2, int(res.get("CPU", 1)))))
         self.idle_timeout = float(self.config.get("idle_worker_killing_time_threshold_ms", 60000)) / 1000.0
+        # scheduler warnings pushed to drivers (reference node_manager.cc:372 PublishInfeasibleTaskError,
+        # :889 WarnResourceDeadlock with debug_dump_period_milliseconds = 10 s)
+        self.deadlock_period = float(self.config.get("resource_deadlock_check_period_s", 10.0))
+        self._infeasible_warned = set()
+        self._deadlock_warned = 0
+        self._deadlock_next = time.time() + self.deadlock_period
+        self.pushed_errors = collections.deque(maxlen=1000)
         self.memory_monitor = None
         self.autoscaler = None
         if self.config.get("autoscaler"):
@@ -811,6 +819,14 @@ class Head:
         elif c.worker is not None:
             self._worker_died(c.worker)
 
+    def _emit_worker_died(self, fields: dict, code) -> None:
+        sig = -code if isinstance(code, int) and code < 0 else None
+        how = (f"killed by signal {sig}" + (" (SIGKILL: OOM killer or an external kill)" if sig == 9 else
+                                            " (SIGSEGV)" if sig == 11 else "")) if sig else f"exit code {code}"
+        self._event("RAYLET", "ERROR", "WORKER_DIED",
+                    f"Worker pid {fields['pid']} died unexpectedly ({how}) in state {fields.pop('state')}.",
+                    exit_code=code, signal=sig, **fields)
+
     def _release_client_pins(self, pid: int, proc=None) -> None:
         """A client process is gone: release every object-store pin it still held (objects it was
         reading when it was killed, its creator pins) so they can be freed / evicted / spilled again.
@@ -871,13 +887,17 @@ class Head:
             self._release_client_pins(w.pid, w.proc)
         if prev_state != "DEAD":  # not a kill the head asked for (those report their own reason)
             t0 = self.tasks.get(w.task) if w.task is not None else None
+            fields = dict(pid=w.pid, worker_id=self._hex(w.worker_id),
+                          task_id=self._hex(t0.spec["task_id"]) if t0 is not None else None,
+                          job_id=self._hex(t0.spec.get("job_id")) if t0 is not None else None,
+                          actor_id=self._hex(w.actor_id), state=prev_state)
             code = w.proc.poll() if w.proc is not None else None
-            self._event("RAYLET", "ERROR", "WORKER_DIED",
-                        f"Worker pid {w.pid} died unexpectedly (exit code {code}) in state {prev_state}.",
-                        pid=w.pid, worker_id=self._hex(w.worker_id), exit_code=code,
-                        task_id=self._hex(t0.spec["task_id"]) if t0 is not None else None,
-                        job_id=self._hex(t0.spec.get("job_id")) if t0 is not None else None,
-                        actor_id=self._hex(w.actor_id))
+            if code is None and w.proc is not None:
+                # the exit status is not known yet (a fork-server worker's arrives as the template's
+                # reap report): the event waits for it, at most 2 s (housekeeping)
+                self._death_reports[w.pid] = (w.proc, fields, time.time())
+            else:
+                self._emit_worker_died(fields, code)
         if w.task is not None:
             t = self.tasks.get(w.task)
             w.task = None
@@ -1624,6 +1644,12 @@ class Head:
         now = time.time()
         if self.recovery.awaiting:
             self.recovery.expire_awaiting(now)
+        # WORKER_DIED events waiting for the exit status
+        for pid, (proc, fields, t0) in list(self._death_reports.items()):
+            code = proc.poll()
+            if code is not None or now - t0 > 2.0:
+                self._death_reports.pop(pid, None)
+                self._emit_worker_died(fields, code)
         # pins of exited clients whose release had to wait for the process to finish exiting
         for pid, proc in list(self._pins_pending.items()):
             self._release_client_pins(pid, proc)
@@ -1649,6 +1675,11 @@ class Head:
                 self.io_pool.submit(self._io_spill, job)
         self._disk_monitor(now)
         self._maybe_global_gc(now, st)
+        try:
+            self._scheduler_warnings(now)
+        except Exception as e:  # a diagnostic must never take the head down
+            self.mem_stats["scheduler_warning_errors"] += 1
+            print(f"[head] scheduler warning check failed: {e!r}", file=sys.stderr, flush=True)
         # idle worker reaping (keep prestart pool)
         idle_total = sum(len(v) for v in self.idle.values())
         if idle_total > self.prestart:
@@ -1678,6 +1709,93 @@ class Head:
                             pid=victim.pid, task_id=self._hex(t.spec["task_id"]) if t is not None else None,
                             job_id=self._hex(t.spec.get("job_id")) if t is not None else None)
                 self._kill_worker(victim)
+
+    # ------------------------------------------------------------------ scheduler warnings
+    def _push_error(self, job_id, etype: str, msg: str, **fields):
+        """Send a warning to the job's driver (printed there as "(raylet) ..." and kept in
+        worker.pushed_errors), record it in the head's error table and as a cluster event."""
+        self.pushed_errors.append({"type": etype, "message": msg, "job_id": self._hex(job_id), "time": time.time()})
+        self._event("RAYLET", "WARNING", etype.upper(), msg, job_id=self._hex(job_id), **fields)
+        targets = []
+        job = self.jobs.get(job_id) if job_id is not None else None
+        if job is not None and job.get("alive") and job.get("conn") is not None:
+            targets.append(job["conn"])
+        elif job_id is None or job is None:  # unknown job: every connected driver
+            targets = [c for c in self.conns.values() if c.kind == "driver" and c.alive]
+        for c in targets:
+            self._send_nb(c, (P.PUSH_ERROR, etype, msg, job_id))
+
+    def _scheduler_warnings(self, now: float):
+        """Infeasible tasks / actors (no node can ever hold their resources) warn their driver once;
+        a resource deadlock (ready tasks pending for two consecutive check periods while no worker runs an
+        unblocked non-actor task: the resources are held by actors or by tasks blocked on each other)
+        warns once per episode and triggers a global GC (actor handles caught in reference cycles may
+        be holding the resources)."""
+        inf = self.sched.infeasible_tasks()
+        if inf or self._infeasible_warned:
+            cur = set(inf)
+            for key in cur - self._infeasible_warned:
+                tid = self.task_keys.get(key)
+                if tid is None:
+                    continue
+                if isinstance(tid, tuple):  # actor creation
+                    a = self.actors.get(tid[1])
+                    if a is None:
+                        continue
+                    res, job, what = (a.spec.get("_pres") or {}), a.job_id, tid[1]
+                else:
+                    t = self.tasks.get(tid)
+                    if t is None:
+                        continue
+                    res, job, what = t.spec.get("_res", {}), t.spec.get("job_id"), tid
+                    if job is None and t.owner_conn is not None:  # a worker lease: its owner's job
+                        job = getattr(t.owner_conn, "job_id", None)
+                if any("_group_" in k for k in res):  # placement-group bundles warn through the PG
+                    continue
+                req = ", ".join(f"{k}: {v:g}" for k, v in sorted(res.items()) if v)
+                self._push_error(job, "infeasible_task",
+                                 f"The actor or task with ID {self._hex(what)} cannot be scheduled right now. It "
+                                 f"requires {{{req}}} for placement, however the cluster currently cannot provide "
+                                 f"the requested resources (cluster total: {self._fmt_res(self.sched.cluster_total())}). "
+                                 "The required resources may be added as autoscaling takes place or placement groups "
+                                 "are scheduled. Otherwise, consider reducing the resource requirements of the task.",
+                                 task_id=self._hex(what))
+            self._infeasible_warned = cur
+        if now < self._deadlock_next:
+            return
+        self._deadlock_next = now + self.deadlock_period
+        ready = self.sched.num_pending() - len(self.sched.waiting_tasks()) - len(inf)
+        # progress = some worker runs a (non-actor) task and is not blocked in get (reference
+        # worker.h IsAvailableForScheduling); a long task backlog therefore never warns
+        running = any(w.task is not None and not w.blocked and w.actor_id is None for w in self.workers.values())
+        if ready <= 0 or running:
+            self._deadlock_warned = 0
+            return
+        self._deadlock_warned += 1
+        if self._deadlock_warned < 2:
+            return
+        self._global_gc("resource deadlock")
+        if self._deadlock_warned > 2:
+            return
+        ex = next((t for t in self.tasks.values() if t.state == PENDING and t.assign is None), None)
+        job = ex.spec.get("job_id") if ex is not None else None
+        res = ex.spec.get("_res", {}) if ex is not None else {}
+        req = ", ".join(f"{k}: {v:g}" for k, v in sorted(res.items()) if v)
+        self._push_error(job, "resource_deadlock",
+                         f"The actor or task with ID {self._hex(ex.spec['task_id']) if ex is not None else '?'} cannot "
+                         "be scheduled right now. You can ignore this message if this cluster is expected to "
+                         "auto-scale. Otherwise, this is likely due to all cluster resources being claimed by actors "
+                         "or by tasks waiting on each other. To resolve the issue, consider creating fewer actors or "
+                         f"increasing the resources available to this cluster.\nRequired resources for this actor or "
+                         f"task: {{{req}}}\nAvailable resources: {self._fmt_res(self.sched.cluster_available())} In "
+                         f"total there are {ready} pending tasks / actors.", pending=ready)
+
+    @staticmethod
+    def _fmt_res(d) -> str:
+        try:
+            return "{" + ", ".join(f"{k}: {v:g}" for k, v in sorted(dict(d).items()) if v and "_group_" not in k) + "}"
+        except Exception:
+            return str(d)
 
     def _io_spill(self, nbytes):
         try:

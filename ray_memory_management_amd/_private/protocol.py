@@ -62,6 +62,7 @@ REPLY = 105
 FREE_GPU = 106
 TRIGGER_GC = 107
 NODES_CHANGED = 108  # (NODES_CHANGED, multi_node: bool)
+PUSH_ERROR = 109     # (PUSH_ERROR, error_type, message, job_id): a warning for the job's driver
 
 # ---- caller -> actor (direct transport)
 ACTOR_TASK = 201

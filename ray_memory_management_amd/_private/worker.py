@@ -220,6 +220,7 @@ class CoreWorker:
         self.actor_handle_for_self = None
         self.direct = None  # DirectTaskSubmitter (worker leases), created on first eligible task
         self.multi_node = False  # head-pushed: direct submission only on single-node clusters
+        self.pushed_errors = collections.deque(maxlen=100)  # head-pushed warnings (PUSH_ERROR) for this job
         self._reader_t = threading.Thread(target=self._reader, daemon=True, name="rmm-reader")
         self._reader_t.start()
         self._flusher_stop = threading.Event()
@@ -247,6 +248,10 @@ class CoreWorker:
                     self.multi_node = bool(m[1])
                 elif t == P.TRIGGER_GC:
                     threading.Thread(target=_collect_garbage, daemon=True).start()
+                elif t == P.PUSH_ERROR:  # scheduler warning for this job (infeasible task, resource deadlock)
+                    self.pushed_errors.append({"type": m[1], "message": m[2], "time": time.time()})
+                    if self.mode == SCRIPT_MODE:
+                        print(f"(raylet) [{m[1]}] {m[2]}", file=sys.stderr, flush=True)
                 elif t in (P.CANCEL_TASK, P.FREE_GPU):
                     try:  # a failing side-channel handler must never take the reader thread down
                         if t == P.CANCEL_TASK:

@@ -219,9 +219,10 @@ class PPO(Algorithm):
         # the weight publication is queued right behind the update on each learner (actor calls run
         # in order), so it runs while the driver is still collecting the update's stats: no extra
         # driver round trip before the next iteration's set_weights + sample
-        if shared:  # once: the learners move their bf16 weights into HBM objects the workers alias
+        if shared:  # once: the learners move their live weights into HBM objects the workers alias
             if self._dev_refs is None:
                 self._dev_refs = self.learner_group.shared_weights_refs()
+                self._dev_shared = True
         elif dev:  # GPU rollout workers read the learners' bf16 weights from HBM (hipIPC)
             self._dev_refs = self.learner_group.device_weights_refs()
         else:
@@ -246,6 +247,7 @@ class PPO(Algorithm):
     _dev_refs = None
     _prefetched = None  # next iteration's sample refs, queued behind this iteration's update
     _aliased = False    # the rollout workers were sent the learners' shared weights
+    _dev_shared = False  # _dev_refs are live shared-weight descriptors (not per-iteration copies)
 
     def _shared_weights_ok(self) -> bool:
         """Rollout workers alias the learners' live HBM weights (zero-copy, set once) instead of
@@ -309,7 +311,7 @@ class PPO(Algorithm):
         if self.learner_group is not None:
             self.learner_group.set_weights(weights)
             self._weights_ref = self.learner_group.weights_ref()
-            if self._dev_refs is not None and not (self._device_weights_ok() and self._shared_weights_ok()):
+            if self._dev_refs is not None and not self._dev_shared:
                 # copies: the next iteration must not push pre-restore HBM weights. Shared mode keeps its
                 # descriptors: the learners wrote the restored weights into the aliased buffers in place,
                 # and a flat snapshot must never be copied into parameters that alias the learner

@@ -632,7 +632,9 @@ class HybridRolloutWorker(GPURolloutWorker):
         if not (on == "1" if on is not None else bool(self.config.get("rollout_server", False))):
             return None
         k = self._kernel_args(G, S)
-        return None if k is None or k.get("x3") else k
+        if k is None or k.get("x3"):
+            return None
+        return {key: v for key, v in k.items() if key != "x3"}
 
     def _direct_args(self, G, S):
         """Arguments of the native loop with DIRECT kernel launches per policy step (K10 push → K13s →

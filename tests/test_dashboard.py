@@ -176,6 +176,9 @@ def test_event_snapshot_actor_modules(dash):
     assert {"WORKER_DIED", "ACTOR_RESTARTED", "JOB_STARTED"} <= labels, labels
     died = [e for evs in _get(url + "/events")["data"]["events"].values() for e in evs if e["label"] == "WORKER_DIED"]
     assert any(e["custom_fields"]["pid"] == pid and e["severity"] == "ERROR" for e in died), died
+    # the real exit status (the fork-server template reaps the worker and reports it): SIGKILL
+    mine = [e for e in died if e["custom_fields"]["pid"] == pid]
+    assert mine[0]["custom_fields"]["exit_code"] == -9 and mine[0]["custom_fields"]["signal"] == 9, mine
     assert ray.get(a.pid.remote()) != pid  # restarted
 
     snap = _get(url + "/api/snapshot")["data"]["snapshot"]
