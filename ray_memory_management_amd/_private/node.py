@@ -82,7 +82,7 @@ def _pid_alive(pid: int) -> bool:
         return False
 
 class Conn:
-    __slots__ = ("sock", "reader", "kind", "worker", "pid", "lock", "job_id", "alive", "wbuf")
+    __slots__ = ("sock", "reader", "kind", "worker", "pid", "lock", "job_id", "alive", "wbuf", "held")
 
     def __init__(self, sock):
         self.sock = sock
@@ -93,6 +93,7 @@ class Conn:
         self.lock = threading.Lock()
         self.job_id = None
         self.alive = True
+        self.held = {}  # oid -> net references this process holds (its REF_DELTAS summed)
 
     def send(self, msg):
         if not self.alive:
@@ -555,6 +556,13 @@ class Head:
     def _handle(self, c: Conn, m):
         t = m[0]
         if t == P.REF_DELTAS:
+            held = c.held
+            for oid, d in m[1]:
+                n = held.get(oid, 0) + d
+                if n:
+                    held[oid] = n
+                else:
+                    held.pop(oid, None)
             self._ref_deltas(m[1])
         elif t == P.SUBMIT_TASK:
             self._submit_task(c, m[1])
@@ -818,6 +826,20 @@ class Head:
             self._driver_exit(c)
         elif c.worker is not None:
             self._worker_died(c.worker)
+        self._release_conn_refs(c)
+
+    def _release_conn_refs(self, c: Conn) -> None:
+        """A process disconnected (exited, or was killed before it could flush its ref deltas): drop
+        the references it still held, so objects it was borrowing are freed once nobody else holds
+        them. Each process contributes at most +1 per object (its first local ref) and -1 when its
+        last one goes, so c.held is exactly what it still holds. Reference
+        src/ray/core_worker/reference_count.cc: a borrower's refs are released when the owner's
+        WaitForRefRemoved on it fails (the borrower died)."""
+        held, c.held = c.held, {}
+        drop = [(oid, -n) for oid, n in held.items() if n > 0]
+        if drop:
+            self.mem_stats["dead_client_refs_released"] = self.mem_stats.get("dead_client_refs_released", 0) + len(drop)
+            self._ref_deltas(drop)
 
     def _emit_worker_died(self, fields: dict, code) -> None:
         sig = -code if isinstance(code, int) and code < 0 else None

@@ -163,12 +163,16 @@ def test_killed_cross_process_reader_releases_hbm(gpu_ray):
     assert n_objects() == base + 1
     r = Reader.remote()
     assert ray.get(r.hold.remote([ref])) == float(1 << 22)
+    oid = ref.binary()
     ray.kill(r)
     del ref
     deadline = time.time() + 20
     while time.time() < deadline and n_objects() > base:
         time.sleep(0.1)
-    assert n_objects() == base, gos.stats(global_worker)
+    st = global_worker.store
+    assert n_objects() == base, (gos.stats(global_worker), "descriptor state", st.state(oid),
+                                 "deferred", len(getattr(global_worker, "_gpu_deferred_free", ())),
+                                 "pin overflows", st.pin_overflows())
 
 
 def test_nested_cuda_tensors_stay_in_hbm(gpu_ray):

@@ -196,3 +196,39 @@ def test_runtime_killed_actor_holding_a_view_frees_the_object():
         assert store.stats()["bytes_in_use"] == base, store.stats()
     finally:
         ray.shutdown()
+
+
+def test_runtime_killed_borrower_keeping_the_ref_frees_the_object():
+    """A borrower that keeps the ObjectRef itself (not only a view) and is killed before it can flush
+    its ref deltas: the head drops the dead process's references (per-connection ledger) and the
+    object is freed. Reference src/ray/core_worker/reference_count.cc: a dead borrower's refs are
+    released when the owner's WaitForRefRemoved on it fails."""
+    import ray_memory_management_amd as ray
+
+    ray.init(num_cpus=2, object_store_memory=256 << 20)
+    try:
+        from ray_memory_management_amd._private.worker import global_worker
+
+        store = global_worker.store
+
+        @ray.remote
+        class Borrower:
+            def keep(self, refs):
+                self.r = refs[0]  # the ref itself: this process now holds a reference
+                self.x = ray.get(self.r)
+                return int(self.x.nbytes)
+
+        ref = ray.put(np.ones(16 << 20, np.uint8))
+        oid = ref.binary()
+        b = Borrower.remote()
+        assert ray.get(b.keep.remote([ref])) == 16 << 20
+        del ref
+        time.sleep(0.5)
+        assert store.state(oid) == K_SEALED  # still borrowed
+        ray.kill(b)
+        deadline = time.time() + 15
+        while time.time() < deadline and store.state(oid) != -1:
+            time.sleep(0.1)
+        assert store.state(oid) == -1
+    finally:
+        ray.shutdown()
