@@ -141,12 +141,28 @@ def many_pgs(ray, n):
 
 
 def many_running_tasks(ray, n, sleep_s):
-    @ray.remote(num_cpus=0.25)
-    def task():
-        time.sleep(sleep_s)
+    """Reference release/benchmarks/distributed/test_many_tasks.py: n sleeping tasks that must all run
+    at once (one worker process each), rate = n / (wall time - sleep). The reference uses 0.25-CPU
+    tasks on a 2,500-CPU cluster; on one node the tasks are 0-CPU so that n >> CPUs can run together.
+    Peak concurrency comes from the tasks' own start / end times."""
 
+    @ray.remote(num_cpus=0)
+    def task():
+        t0 = time.time()
+        time.sleep(sleep_s)
+        return t0, time.time()
+
+    t0 = time.time()
     refs = [task.remote() for _ in range(n)]
-    assert all(x is None for x in ray.get(refs))
+    spans = ray.get(refs)
+    wall = time.time() - t0
+    edges = sorted([(a, 1) for a, _ in spans] + [(b, -1) for _, b in spans])
+    cur = peak = 0
+    for _, d in edges:
+        cur += d
+        peak = max(peak, cur)
+    last_start = max(a for a, _ in spans) - t0
+    return wall, {"peak_concurrent": peak, "all_started_after_s": round(last_start, 3), "sleep_s": sleep_s}
 
 
 def main():
@@ -158,7 +174,8 @@ def main():
     ap.add_argument("--large-gb", type=float, default=8.0)
     ap.add_argument("--actors", type=int, default=200)
     ap.add_argument("--pgs", type=int, default=1000)
-    ap.add_argument("--tasks", type=int, default=0, help="concurrently running 0.25-CPU sleep tasks (0 = 4x CPUs)")
+    ap.add_argument("--tasks", type=int, default=1000, help="concurrently running 0-CPU sleep tasks")
+    ap.add_argument("--task-sleep", type=float, default=20.0)
     ap.add_argument("--num-cpus", type=int, default=0)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
@@ -167,7 +184,8 @@ def main():
 
     cpus = a.num_cpus or (os.cpu_count() or 8)
     store = int(max(a.large_gb * 1.2, 4.0) * (1 << 30))
-    ray.init(num_cpus=cpus, object_store_memory=store)
+    # one worker process per running task: raise the worker cap above the concurrent-task count
+    ray.init(num_cpus=cpus, object_store_memory=store, _system_config={"max_workers": a.tasks + 64})
     only = set(a.only.split(",")) if a.only else None
     out = {"cpus": cpus, "object_store_bytes": store}
 
@@ -205,9 +223,17 @@ def main():
     run("many_actors", lambda: _t(lambda: many_actors(ray, a.actors)), a.actors, REF_DISTRIBUTED["actors_per_second"],
         "actors_per_s")
     run("many_pgs", lambda: _t(lambda: many_pgs(ray, a.pgs)), a.pgs, REF_DISTRIBUTED["pgs_per_second"], "pgs_per_s")
-    nt = a.tasks or 4 * cpus
-    run("many_running_tasks", lambda: _t(lambda: many_running_tasks(ray, nt, 5.0)) - 5.0, nt,
-        REF_DISTRIBUTED["tasks_per_second_10000"], "tasks_per_s")
+    nt = a.tasks
+    extra = {}
+
+    def running():
+        wall, info = many_running_tasks(ray, nt, a.task_sleep)
+        extra.update(info)
+        return wall - a.task_sleep
+
+    run("many_running_tasks", running, nt, REF_DISTRIBUTED["tasks_per_second_10000"], "tasks_per_s")
+    if "many_running_tasks" in out:
+        out["many_running_tasks"].update(extra)
     ray.shutdown()
     print(json.dumps(out), flush=True)
 

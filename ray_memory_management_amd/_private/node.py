@@ -1907,6 +1907,12 @@ class Head:
                 self._forker.close()
         except OSError:
             pass
+        try:  # explicitly: other references to the store (IO threads) would keep `del` from unlinking
+            from _posixshmem import shm_unlink
+
+            shm_unlink(self.args.store_name)
+        except (ImportError, OSError):
+            pass
         del self.store
 
 
@@ -1921,8 +1927,19 @@ def main():
     args = ap.parse_args()
     os.makedirs(os.path.join(args.session_dir, "logs"), exist_ok=True)
     os.makedirs(os.path.join(args.session_dir, "sockets"), exist_ok=True)
-    signal.signal(signal.SIGTERM, lambda *a: sys.exit(0))
+    signal.signal(signal.SIGTERM, lambda *a: sys.exit(0))  # until the loop runs
     h = Head(args)
+
+    def _term(*_):
+        # `rmm stop`: leave the loop and shut down the normal way (workers told to exit, the GCS
+        # flushed, the store segment unlinked) instead of unwinding out of it
+        h.running = False
+        try:
+            os.write(h.wake_w, b"x")
+        except OSError:
+            pass
+
+    signal.signal(signal.SIGTERM, _term)
     prof_path = os.environ.get("RMM_HEAD_PROFILE")  # control-plane profiling: cProfile of the loop
     prof = None
     if prof_path:

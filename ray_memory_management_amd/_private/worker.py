@@ -927,6 +927,16 @@ def _find_session(address):
         return f.read().strip()
 
 
+def _shm_unlink(name: str) -> None:
+    """Remove this session's store segment name (processes that still map it keep their mapping)."""
+    try:
+        from _posixshmem import shm_unlink
+
+        shm_unlink(name)
+    except (ImportError, OSError):
+        pass
+
+
 def shutdown(_exiting_interpreter: bool = False):
     global global_worker, _head_proc, _local_mode, _client
     tr = sys.modules.get(_TRACING_MOD)
@@ -965,6 +975,7 @@ def shutdown(_exiting_interpreter: bool = False):
             except subprocess.TimeoutExpired:
                 _head_proc.kill()
                 _head_proc.wait()
+                _shm_unlink(w.store_name)  # the head this driver started could not clean up its segment
             _head_proc = None
 
 

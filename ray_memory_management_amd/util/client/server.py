@@ -174,7 +174,24 @@ def main(argv=None):
         with open(tmp, "w") as f:
             json.dump({"port": srv.port, "pid": os.getpid()}, f)
         os.replace(tmp, a.ready_file)
-    srv.serve_forever()
+    srv.start()
+    # exit with the cluster (like the dashboard): when the head process is gone, or this server's
+    # connection to it closed, nothing can be served any more
+    import time
+
+    from ray_memory_management_amd._private import worker as _w
+
+    while True:
+        time.sleep(1.0)
+        w = _w.global_worker
+        if w is None or not w.connected:
+            break
+    srv.stop()
+    for sess in list(srv.sessions):
+        try:
+            sess.sock.close()
+        except (AttributeError, OSError):
+            pass
 
 
 if __name__ == "__main__":
