@@ -220,9 +220,19 @@ def main():
     nb = int(a.large_gb * (1 << 30))
     run("large_object", lambda: _t(lambda: large_object(ray, nb)), nb,
         {"bytes": 107374182400, "seconds": REF_SINGLE_NODE["107374182400_large_object_time"]})
+    def fresh():
+        # the reference runs each distributed benchmark (release/benchmarks/distributed/*) on its own
+        # cluster; here a fresh head, so the single-node tests' cleanup (e.g. the ref-delta backlog of
+        # a million finished tasks) does not run underneath
+        ray.shutdown()
+        ray.init(num_cpus=cpus, object_store_memory=1 << 30, _system_config={"max_workers": a.tasks + 64})
+
+    fresh()
     run("many_actors", lambda: _t(lambda: many_actors(ray, a.actors)), a.actors, REF_DISTRIBUTED["actors_per_second"],
         "actors_per_s")
+    fresh()
     run("many_pgs", lambda: _t(lambda: many_pgs(ray, a.pgs)), a.pgs, REF_DISTRIBUTED["pgs_per_second"], "pgs_per_s")
+    fresh()
     nt = a.tasks
     extra = {}
 

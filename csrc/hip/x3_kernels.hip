@@ -656,12 +656,16 @@ constexpr int H = dense::H;
 // ---- K13x: split-K dense layer hidden_pre = x Wᵀ over split pairs -> fp32 partials part[S][M][N]
 // (no bias / ReLU: the consumer K15x / K16x sums the S slices, adds the bias, applies ReLU in fp32).
 // Unit = FM x FN 16x16 fragments per wave, the workgroup's 4 waves split the slice's k-steps and
-// combine through LDS in a fixed order (deterministic).
-template <int FM, int FN>
+// combine through LDS in a fixed order (deterministic). Each wave has only ~8 k-steps at ~2 waves per
+// SIMD, so a step's loads are issued D steps ahead (a register ring of D stages): the MFMAs of step i
+// overlap the global latency of steps i+1..i+D-1 instead of waiting for it.
+template <int FM, int FN, int D>
 __global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
                                                            float* __restrict__ part) {
   __shared__ f32x4 red[3][FM * FN][64];
-  const int lane = threadIdx.x & 63, kw = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  // the wave index is wave-uniform: in an SGPR the k-step guards below are scalar branches
+  const int lane = threadIdx.x & 63, kw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 15,
+            g = lane >> 4;
   const int nt = N / (16 * FN);
   const int64_t mt = (M + 16 * FM - 1) / (16 * FM);
   const int64_t tiles = mt * nt, total_ = gridDim.x;
@@ -670,27 +674,61 @@ __global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int
   const int64_t sl = id / tiles, rem = id % tiles, tm = rem / nt, tn = rem % nt;
   const int64_t m0 = tm * 16 * FM, n0 = tn * 16 * FN;
   const int64_t steps = K / 32, lo = steps * sl / S, hi = steps * (sl + 1) / S;
-  int64_t xo[FM], wo[FN];
+  const unsigned short *xh[FM], *xl[FM], *wh[FN], *wl[FN];
 #pragma unroll
-  for (int i = 0; i < FM; i++) xo[i] = min(m0 + 16 * i + r, M - 1) * K + 8 * g;
+  for (int i = 0; i < FM; i++) {
+    const int64_t o = min(m0 + 16 * i + r, M - 1) * K + 8 * g + (lo + kw) * 32;
+    xh[i] = x.hi + o, xl[i] = x.lo + o;
+  }
 #pragma unroll
-  for (int j = 0; j < FN; j++) wo[j] = (n0 + 16 * j + r) * K + 8 * g;
+  for (int j = 0; j < FN; j++) {
+    const int64_t o = (n0 + 16 * j + r) * K + 8 * g + (lo + kw) * 32;
+    wh[j] = w.hi + o, wl[j] = w.lo + o;
+  }
+  // this wave's k-steps: lo + kw + 4 t, t < n (step t is 128 t elements past the pointers above)
+  const int n = lo + kw < hi ? int((hi - lo - kw + 3) / 4) : 0;
   Acc acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; i++)
 #pragma unroll
     for (int j = 0; j < FN; j++) acc[i][j] = acc0();
-  for (int64_t k = lo + kw; k < hi; k += 4) {
-    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
-#pragma unroll
-    for (int i = 0; i < FM; i++) ah[i] = ld8(x.hi + xo[i] + k * 32), al[i] = ld8(x.lo + xo[i] + k * 32);
-#pragma unroll
-    for (int j = 0; j < FN; j++) bh[j] = ld8(w.hi + wo[j] + k * 32), bl[j] = ld8(w.lo + wo[j] + k * 32);
-#pragma unroll
-    for (int i = 0; i < FM; i++)
-#pragma unroll
-      for (int j = 0; j < FN; j++) mma3(acc[i][j], ah[i], al[i], bh[j], bl[j]);
+  bf16x8 ah[D][FM], al[D][FM], bh[D][FN], bl[D][FN];
+#define K13X_LOAD(slot, t)                                                                      \
+  {                                                                                             \
+    const int64_t e_ = int64_t(t) * 128;                                                        \
+    _Pragma("unroll") for (int i = 0; i < FM; i++) ah[slot][i] = ld8(xh[i] + e_), al[slot][i] = ld8(xl[i] + e_); \
+    _Pragma("unroll") for (int j = 0; j < FN; j++) bh[slot][j] = ld8(wh[j] + e_), bl[slot][j] = ld8(wl[j] + e_); \
   }
+#define K13X_MMA(slot)                                                                          \
+  _Pragma("unroll") for (int i = 0; i < FM; i++) _Pragma("unroll") for (int j = 0; j < FN; j++)  \
+      mma3(acc[i][j], ah[slot][i], al[slot][i], bh[slot][j], bl[slot][j]);
+  if (n > 0) {
+    // prologue: steps 0..D-1 (clamped: a repeated last step is loaded but never multiplied)
+#pragma unroll
+    for (int d = 0; d < D; d++) K13X_LOAD(d, min(d, n - 1));
+    int t0 = 0;
+    // steady state, no guards: every slot is multiplied and refilled D steps ahead
+    for (; t0 + 2 * D <= n; t0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; d++) {
+        K13X_MMA(d);
+        K13X_LOAD(d, t0 + d + D);
+      }
+    }
+    // tail: steps t0 .. n-1 (fewer than 2D)
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      if (t0 + d < n) {
+        K13X_MMA(d);
+        if (t0 + d + D < n) K13X_LOAD(d, t0 + d + D);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; d++)
+      if (t0 + D + d < n) K13X_MMA(d);
+  }
+#undef K13X_MMA
+#undef K13X_LOAD
   if (kw > 0) {
 #pragma unroll
     for (int i = 0; i < FM; i++)
@@ -1153,9 +1191,9 @@ void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part,
   const int64_t tiles = ((M + 16 * f - 1) / (16 * f)) * (N / (16 * f));
   const dim3 grid(uint32_t(tiles * S)), block(256);
   if (f == 1)
-    hipLaunchKernelGGL((x3::k_dense_fwd_part_x3<1, 1>), grid, block, 0, stream, cp(x), cp(w), M, K, N, S, part);
+    hipLaunchKernelGGL((x3::k_dense_fwd_part_x3<1, 1, 4>), grid, block, 0, stream, cp(x), cp(w), M, K, N, S, part);
   else
-    hipLaunchKernelGGL((x3::k_dense_fwd_part_x3<2, 2>), grid, block, 0, stream, cp(x), cp(w), M, K, N, S, part);
+    hipLaunchKernelGGL((x3::k_dense_fwd_part_x3<2, 2, 4>), grid, block, 0, stream, cp(x), cp(w), M, K, N, S, part);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -15,6 +15,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
+from ray_memory_management_amd.rllib.ppo_learner import bootstrap_value
+
 
 class GPURolloutWorker:
     def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
@@ -65,7 +67,7 @@ class GPURolloutWorker:
         S = self.sampler
         with torch.no_grad():
             S.run_fragment()
-            _, last_v = self.model(S.s_obs)
+            last_v = bootstrap_value(self.model, S.s_obs)
             frag = pack_fragment_device(S.buf_obs, S.buf_logits, S.buf_logp, S.buf_vf, S.buf_rew, S.buf_done,
                                         S.buf_act, last_v)
         self._sample_time += time.perf_counter() - t0
@@ -599,10 +601,10 @@ class HybridRolloutWorker(GPURolloutWorker):
                     if g.device_stack:  # observation after the last env step (pushed next fragment)
                         g.s_new.copy_(g.h_new, non_blocking=True)
                         stack = g.buf_obs[T - 1] if g.band else g.s_obs  # the last step's frame stack
-                        _, last_v = self.model(torch.cat([stack[:, 1:], g.s_new.unsqueeze(1)], dim=1))
+                        last_v = bootstrap_value(self.model, torch.cat([stack[:, 1:], g.s_new.unsqueeze(1)], dim=1))
                     else:
                         g.s_obs.copy_(g.h_obs, non_blocking=True)
-                        _, last_v = self.model(g.s_obs)
+                        last_v = bootstrap_value(self.model, g.s_obs)
                     parts.append((g.buf_obs, g.buf_logits, g.buf_logp, g.buf_vf,
                                   g.h_rew.to(self.device, non_blocking=True),
                                   g.h_done.to(self.device, non_blocking=True), g.buf_act, last_v.reshape(-1)))

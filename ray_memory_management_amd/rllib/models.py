@@ -589,6 +589,30 @@ class VisionNetwork(nn.Module):
         _dbg_sync(f"K16 (Wh {heads.weight.data_ptr():#x} bh {heads.bias.data_ptr():#x})")
         return True
 
+    @torch.no_grad()
+    def forward_value(self, obs):
+        """Value head only ([B] fp32), e.g. the bootstrap value after a rollout fragment. On the fused
+        paths this is one sampling step (K10 → K13 → K16, bf16 or x3) into scratch rows — the value
+        column is what the step stores; otherwise the plain forward (a torch fp32 conv there runs
+        MIOpen's naive kernel on gfx950, ≈0.3 ms for 50 frames)."""
+        if obs.is_cuda and (self.fused_x3_ok(obs) or self.fused_trunk_ok(obs)):
+            B, A = obs.shape[0], self.heads.out_features - 1
+            sc = getattr(self, "_value_scratch", None)
+            if sc is None or sc["B"] != B or sc["dev"] != obs.device:
+                dev = obs.device
+                sc = self._value_scratch = {
+                    "B": B, "dev": dev, "t": torch.zeros(1, dtype=torch.int64, device=dev),
+                    "ctr": torch.zeros(1, dtype=torch.int64, device=dev),
+                    "act": torch.empty((1, B), dtype=torch.int64, device=dev),
+                    "logp": torch.empty((1, B), dtype=torch.float32, device=dev),
+                    "vf": torch.empty((1, B), dtype=torch.float32, device=dev),
+                    "logits": torch.empty((1, B, A), dtype=torch.float32, device=dev),
+                    "act_now": torch.empty(B, dtype=torch.int64, device=dev)}
+            if self.forward_sample(obs, sc["t"], sc["ctr"], 0, sc["act"], sc["logp"], sc["vf"], sc["logits"],
+                                   sc["act_now"]):
+                return sc["vf"][0].clone()
+        return self(obs)[1].float()
+
     def forward_frames_ppo(self, obs, cols, coef, acc, gout, idx=None, ctr=None, period: int = 1,
                            rows: int = None):
         """forward_frames fused with the PPO loss (K10 trunk → K13 → K15); `cols` is the FULL loss-column

@@ -1276,6 +1276,13 @@ class PPOLearner:
                 self.model.load_state_dict(w)
 
 
+def bootstrap_value(model, obs):
+    """Value of the observation after a fragment's last step ([B]): the model's fused value-only
+    forward when it has one, else the plain forward's value column."""
+    fv = getattr(model, "forward_value", None)
+    return fv(obs) if fv is not None else model(obs)[1]
+
+
 class GPURolloutSampler:
     """Samples `fragment` steps from a device-resident vectorised env with on-GPU inference and
     postprocesses with the GAE kernel. Output: a flat SampleBatch of fragment*num_envs rows in HBM.
@@ -1391,7 +1398,7 @@ class GPURolloutSampler:
     @torch.no_grad()
     def sample(self) -> SampleBatch:
         self.run_fragment()
-        _, last_v = self.model(self.s_obs)
+        last_v = bootstrap_value(self.model, self.s_obs)
         adv, ret = ops.gae(self.buf_rew, self.buf_vf, self.buf_done, last_v.float(), self.gamma, self.lam)
         n = self.T * self.B
         return SampleBatch({

@@ -215,3 +215,27 @@ def test_x3_heads_sample_fp32_rows(cuda, B):
     ref_lp = torch.log_softmax(lout[1].double(), -1).gather(1, act[1][:, None])[:, 0]
     torch.testing.assert_close(logp[1].double(), ref_lp, rtol=1e-5, atol=1e-5)
     assert torch.equal(now, act[1]) and int(act[0].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_forward_value_matches_plain_forward(cuda, dtype):
+    """VisionNetwork.forward_value (the rollout's bootstrap value: one fused sampling step into scratch
+    rows) equals the value column of the plain forward, on the x3 (fp32) and bf16 fused paths."""
+    from ray_memory_management_amd.rllib.models import VisionNetwork
+
+    torch.manual_seed(3)
+    m = VisionNetwork(4).to(cuda).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        m.heads.weight.normal_(0, 0.05)  # a value column that is not ~0
+    if dtype == "bf16":
+        m = m.to(torch.bfloat16)
+    else:
+        m.refresh_x3()
+    obs = torch.randint(0, 256, (50, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    assert (m.fused_x3_ok(obs) if dtype == "fp32" else m.fused_trunk_ok(obs))
+    v = m.forward_value(obs)
+    with torch.no_grad():
+        ref = m.float()(obs)[1].double() if dtype == "fp32" else m(obs)[1].double()
+    tol = 2e-4 if dtype == "fp32" else 3e-2
+    assert v.shape == (50,) and v.dtype == torch.float32
+    assert _rel(v, ref) < tol, _rel(v, ref)
