@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--partitions", type=int, default=8, help="output partitions per worker")
     ap.add_argument("--row-bytes", type=int, default=248)
     ap.add_argument("--no-compress", action="store_true")
+    ap.add_argument("--no-prealloc", action="store_true",
+                    help="do not MAP_POPULATE the host store / pre-pin the spill arena")
+    ap.add_argument("--spill-threshold", type=float, default=0.7,
+                    help="HBM store occupancy above which its background thread spills (0 = only on demand)")
     a = ap.parse_args()
 
     import ray_memory_management_amd as ray
@@ -35,7 +39,12 @@ def main():
     ray.init(num_cpus=max(4, 2 * a.workers + 2), num_gpus=a.workers,
              object_store_memory=int(total * 1.25) + (2 << 30),
              _system_config={"gpu_object_store_memory": quota, "prestart_workers": 0,
-                             "gpu_spill_compression": not a.no_compress})
+                             "gpu_spill_compression": not a.no_compress,
+                             "gpu_object_spilling_threshold": a.spill_threshold,
+                             # the host arena the HBM blocks spill into: faulted in at init (reference
+                             # preallocate_plasma_memory) and page-locked by the GPU store in the background
+                             "preallocate_plasma_memory": not a.no_prealloc,
+                             "gpu_spill_prepin_bytes": 0 if a.no_prealloc else int(total * 1.1)})
     try:
         r = run_out_of_core_gpu_shuffle(num_workers=a.workers, total_bytes=total, rounds=a.rounds,
                                         partitions_per_worker=a.partitions, row_bytes=a.row_bytes)

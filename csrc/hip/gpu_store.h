@@ -31,6 +31,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -79,7 +80,7 @@ struct GpuStats {
 class GpuStore {
  public:
   GpuStore(int device, uint64_t capacity, uint64_t slab_bytes, const std::string& shm_name,
-           bool compress_spill, double spill_threshold = 0.0);
+           bool compress_spill, double spill_threshold = 0.0, uint64_t prepin_bytes = 0);
   ~GpuStore();
 
   // Allocate an object and return its device pointer (unsealed, pinned by the creator).
@@ -163,6 +164,18 @@ class GpuStore {
   bool stop_ = false;
   std::condition_variable bg_cv_;
   std::thread bg_;
+  // background page-locking of the host arena's first prepin bytes (spill targets): a spill into
+  // registered memory is one DMA; into fresh pages it first pays the pin (and page faults)
+  std::thread prepin_;
+  std::atomic<bool> prepin_stop_{false};
+  std::atomic<uint64_t> prepin_done_{0};
+  uint64_t prepin_total_ = 0;
+
+ public:
+  // (bytes of the host arena page-locked so far, bytes requested)
+  std::pair<uint64_t, uint64_t> PrepinProgress() const { return {prepin_done_.load(), prepin_total_}; }
+
+ private:
   std::mutex err_mu_;
   std::string last_error_;
   std::string last_stale_;

@@ -67,7 +67,7 @@ std::string GpuStore::HostId(const std::string& id) {
 }
 
 GpuStore::GpuStore(int device, uint64_t capacity, uint64_t slab_bytes, const std::string& shm_name,
-                   bool compress_spill, double spill_threshold)
+                   bool compress_spill, double spill_threshold, uint64_t prepin_bytes)
     : device_(device), capacity_(capacity), slab_bytes_(AlignG(slab_bytes)), compress_(compress_spill),
       spill_threshold_(spill_threshold) {
   RMM_HIP_CHECK(hipSetDevice(device_));
@@ -81,9 +81,20 @@ GpuStore::GpuStore(int device, uint64_t capacity, uint64_t slab_bytes, const std
   }
   st_.capacity = capacity_;
   bg_ = std::thread([this] { BackgroundSpiller(); });
+  if (host_ && prepin_bytes) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(host_->Base());
+    const uint64_t n = std::min<uint64_t>(prepin_bytes, host_->MappedSize());
+    prepin_total_ = n;
+    prepin_ = std::thread([this, base, n] {
+      (void)hipSetDevice(device_);
+      host_prepin(base, n, &prepin_stop_, &prepin_done_);
+    });
+  }
 }
 
 GpuStore::~GpuStore() {
+  prepin_stop_ = true;
+  if (prepin_.joinable()) prepin_.join();
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;

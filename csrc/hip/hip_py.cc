@@ -751,9 +751,10 @@ PYBIND11_MODULE(_hip, m) {
 
   // ---------------------------------------------------------------- GPU object store
   py::class_<GpuStore, std::shared_ptr<GpuStore>>(m, "GpuStore")
-      .def(py::init<int, uint64_t, uint64_t, const std::string&, bool, double>(), py::arg("device"),
+      .def(py::init<int, uint64_t, uint64_t, const std::string&, bool, double, uint64_t>(), py::arg("device"),
            py::arg("capacity"), py::arg("slab_bytes") = 8ull << 30, py::arg("shm_name") = "",
-           py::arg("compress_spill") = true, py::arg("spill_threshold") = 0.0)
+           py::arg("compress_spill") = true, py::arg("spill_threshold") = 0.0, py::arg("prepin_bytes") = 0)
+      .def("prepin_progress", [](GpuStore& s) { return s.PrepinProgress(); })
       .def("seal_descriptor_async", [](GpuStore& s, py::bytes desc_id, uint64_t stream) {
         s.SealDescriptorAsync(std::string(desc_id), S(stream));
       })

@@ -331,6 +331,15 @@ std::vector<uint64_t> h2d_stats() {
   return {g_h2d.direct.load(), g_h2d.staged.load(), g_h2d.chunks_ok.load(), g_h2d.chunks_failed.load()};
 }
 
+void host_prepin(uintptr_t base, uint64_t bytes, const std::atomic<bool>* stop, std::atomic<uint64_t>* done_bytes) {
+  for (uint64_t off = 0; off < bytes; off += kRegChunk) {
+    if (stop && stop->load()) return;
+    const uint64_t len = std::min<uint64_t>(kRegChunk, bytes - off);
+    host_pin_range(reinterpret_cast<const void*>(base + off), len, nullptr);
+    if (done_bytes) done_bytes->fetch_add(len);
+  }
+}
+
 void host_unregister_segment(uintptr_t base) {
   auto& R = Registry();
   std::lock_guard<std::mutex> g(R.mu);

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -317,6 +318,9 @@ void host_unregister_all();
 // Unpin every chunk of a segment and forget it: MUST run before the segment is unmapped (a stale
 // registration would alias whatever is mapped at that address next).
 void host_unregister_segment(uintptr_t base);
+// page-lock [base, base + bytes) of a registered segment chunk by chunk (stops early once *stop is set)
+void host_prepin(uintptr_t base, uint64_t bytes, const std::atomic<bool>* stop,
+                 std::atomic<uint64_t>* done_bytes = nullptr);
 
 }  // namespace hip
 }  // namespace rmm

@@ -85,7 +85,8 @@ static void InitSync(Header* h) {
 }
 
 Store* Store::Create(const std::string& name, uint64_t size, const std::string& spill_dir,
-                     double spill_threshold, uint64_t min_spill_size, bool fallback, double oom_grace_s) {
+                     double spill_threshold, uint64_t min_spill_size, bool fallback, double oom_grace_s,
+                     bool populate) {
   if (spill_dir.size() >= sizeof(Header::spill_dir))
     throw std::runtime_error("spill directory list too long");
   if (size < (8ull << 20)) size = 8ull << 20;
@@ -113,7 +114,9 @@ Store* Store::Create(const std::string& name, uint64_t size, const std::string& 
     shm_unlink(name.c_str());
     throw std::runtime_error("ftruncate failed: " + std::string(strerror(errno)));
   }
-  void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  // populate: fault every page in now (reference preallocate_plasma_memory, plasma/dlmalloc.cc
+  // MAP_POPULATE) so puts and GPU spills into the arena never pay first-touch page faults
+  void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED | (populate ? MAP_POPULATE : 0), fd, 0);
   close(fd);
   if (p == MAP_FAILED) {
     shm_unlink(name.c_str());

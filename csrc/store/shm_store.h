@@ -187,7 +187,7 @@ class Store {
   // Create a new segment (head process) or attach to an existing one.
   static Store* Create(const std::string& name, uint64_t size, const std::string& spill_dir,
                        double spill_threshold, uint64_t min_spill_size, bool fallback,
-                       double oom_grace_s = 2.0);
+                       double oom_grace_s = 2.0, bool populate = false);
   // Memory-pressure controls / counters (see Header).
   void SetDiskFull(bool full);
   bool DiskFull() const { return hdr_->disk_full != 0; }

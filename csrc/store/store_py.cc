@@ -181,15 +181,16 @@ PYBIND11_MODULE(_store, m) {
       .def_static(
           "create_segment",
           [](const std::string& name, uint64_t size, const std::string& spill_dir,
-             double spill_threshold, uint64_t min_spill_size, bool fallback, double oom_grace_s) {
+             double spill_threshold, uint64_t min_spill_size, bool fallback, double oom_grace_s,
+             bool populate) {
             PyStore ps;
             ps.s.reset(Store::Create(name, size, spill_dir, spill_threshold, min_spill_size, fallback,
-                                     oom_grace_s));
+                                     oom_grace_s, populate));
             return ps;
           },
           py::arg("name"), py::arg("size"), py::arg("spill_dir") = "",
           py::arg("spill_threshold") = 0.8, py::arg("min_spill_size") = 100ull << 20,
-          py::arg("fallback") = true, py::arg("oom_grace_s") = 2.0)
+          py::arg("fallback") = true, py::arg("oom_grace_s") = 2.0, py::arg("populate") = false)
       .def_static("attach",
                   [](const std::string& name) {
                     PyStore ps;

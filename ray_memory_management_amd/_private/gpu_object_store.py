@@ -110,8 +110,11 @@ def process_store(worker, device: int):
         cfg = worker.config or {}
         cap = int(cfg.get("gpu_object_store_memory", int(total * float(cfg.get("gpu_object_store_fraction", 0.3)))))
         slab = int(cfg.get("gpu_object_store_slab_bytes", min(cap, 8 << 30)))
+        # gpu_spill_prepin_bytes: page-lock that much of the host arena (the spill target) in the
+        # background, so spills are straight DMAs instead of pin-on-first-use
         s = h.GpuStore(device, cap, slab, worker.store_name, bool(cfg.get("gpu_spill_compression", True)),
-                       float(cfg.get("gpu_object_spilling_threshold", 0.0)))
+                       float(cfg.get("gpu_object_spilling_threshold", 0.0)),
+                       int(cfg.get("gpu_spill_prepin_bytes", 0)))
         stores[device] = s
         try:  # occupancy / spill counters for the dashboard's GPU reporter (internal KV)
             from ray_memory_management_amd.dashboard.gpu_reporter import publish_store_stats

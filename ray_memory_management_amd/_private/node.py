@@ -206,7 +206,10 @@ class Head:
             self.store_name, cap,
             ":".join(self.spill_dirs) if self.config.get("automatic_object_spilling_enabled", True) else "",
             self.spill_threshold, min_spill, bool(self.config.get("object_store_fallback_allocation", True)),
-            float(self.config.get("oom_grace_period_s", 2.0)))
+            float(self.config.get("oom_grace_period_s", 2.0)),
+            # reference ray_config_def.h:150 preallocate_plasma_memory (RAY_preallocate_plasma_memory=1)
+            populate=bool(self.config.get("preallocate_plasma_memory",
+                                          os.environ.get("RAY_preallocate_plasma_memory") == "1")))
         # memory-pressure machinery (reference: local_object_manager.cc IO-worker spilling,
         # local_task_manager.cc:615 PinTaskArgsIfMemoryAvailable, node_manager.cc:2799
         # TriggerGlobalGC, file_system_monitor.cc)

@@ -204,9 +204,28 @@ def run_gpu_shuffle(num_workers: int = 2, rows_per_worker: int = 1 << 20, row_by
 # ================================================================== out-of-core (multi-round) shuffle
 def _payload(keys: torch.Tensor, row_bytes: int) -> torch.Tensor:
     """Row payload derived from its key (so the reduce side can verify every byte after the block
-    was spilled, compressed, restored and moved): byte j of row i = low byte of (key_i * 0x9E3779B1 + j)."""
-    j = torch.arange(row_bytes, device=keys.device, dtype=torch.int64)
-    return ((keys.unsqueeze(1) * 0x9E3779B1 + j.unsqueeze(0)) & 0xFF).to(torch.uint8)
+    was spilled, compressed, restored and moved): byte j of row i = low byte of (key_i * 0x9E3779B1 + j).
+    Only the key's low byte matters for that, so it is computed in uint8 (no [n, row_bytes] int64
+    temporary): ((key & 0xFF) * 0xB1 + j) mod 256."""
+    base = ((keys & 0xFF) * 0xB1 & 0xFF).to(torch.uint8)
+    j = torch.arange(row_bytes, device=keys.device, dtype=torch.int64).to(torch.uint8)
+    return base.unsqueeze(1) + j.unsqueeze(0)  # uint8 addition wraps mod 256
+
+
+def _count_at(keys: torch.Tensor, num_partitions: int, mode: str, gid: int) -> int:
+    """How many keys the partition function sends to partition `gid` (on the GPU: the K11 histogram)."""
+    if keys.numel() == 0:
+        return 0
+    if keys.is_cuda:
+        from ray_memory_management_amd._native import require_hip
+
+        h = require_hip()
+        n = keys.shape[0]
+        cw = torch.zeros((h.partition_groups(n), num_partitions), dtype=torch.int64, device=keys.device)
+        h.partition_hist(keys.data_ptr(), n, num_partitions, MODES[mode], cw.data_ptr(),
+                         torch.cuda.current_stream(keys.device).cuda_stream)
+        return int(cw[:, gid].sum().item())
+    return int((destinations(keys, num_partitions, mode) == gid).sum().item())
 
 
 class OutOfCoreShuffleWorker(ShuffleWorker):
@@ -215,29 +234,48 @@ class OutOfCoreShuffleWorker(ShuffleWorker):
     block in HBM, and in ONE collective round K11 partitions it by destination rank, the all-to-all
     exchanges the pieces over xGMI, and K11 partitions what arrived into this rank's P output
     partitions — the merged map output of every mapper for this round. Each (round, partition)
-    block is ``ray.put`` into the HBM object store; once the store is at its quota it spills the
-    least recently used blocks to host memory (K4-compressed, pinned DMA). The reduce of partition
-    p gathers its blocks (restoring spilled ones) and sorts them by key on the GPU."""
+    block is ``ray.put`` into the HBM object store; the store's background spiller moves the least
+    recently used blocks to host memory (K4-compressed, pinned DMA) while later rounds are partitioned.
+    The reduce of partition p gathers its blocks (restoring spilled ones) and sorts them by key on
+    the GPU; destinations, sort order and every payload byte are verified on the GPU.
+
+    Nothing in a map round waits for the host except the [P] partition counts: the input block is
+    generated on the device, its checksum accumulates on the device, puts are asynchronous."""
 
     def setup(self, partitions: int, row_bytes: int, rows_per_round: int, mode: str = "range"):
         self.P, self.row_bytes, self.rows = int(partitions), int(row_bytes), int(rows_per_round)
         self.mode = mode
         self.blocks = [[] for _ in range(self.P)]
         self.in_rows = 0
-        self.in_key_sum = 0
-        return True
+        self._in_sum = torch.zeros((), dtype=torch.int64, device=self.device)  # wraps mod 2^64
+        prepin_s = 0.0
+        if self.device.type == "cuda":
+            # start-up, like the reference's plasma preallocation: create this process's HBM store now
+            # and let it page-lock its spill arena (gpu_spill_prepin_bytes) before the first round
+            from ray_memory_management_amd._private import gpu_object_store as gos
+            from ray_memory_management_amd._private.worker import global_worker
+
+            g = gos.process_store(global_worker, self.device.index or 0)
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 300:
+                done, total = g.prepin_progress()
+                if done >= total:
+                    break
+                time.sleep(0.01)
+            prepin_s = time.perf_counter() - t0
+        return {"prepin_seconds": prepin_s}
 
     def map_round(self, r: int):
         import ray_memory_management_amd as ray
 
         dev = self.device
         t0 = time.perf_counter()
-        g = torch.Generator(device="cpu").manual_seed(7919 * (r + 1) + self.rank)
+        g = torch.Generator(device=dev).manual_seed(7919 * (r + 1) + self.rank)
         # keys over the whole u64 range: "range" partitioning splits the UNSIGNED key space evenly
-        keys = torch.randint(-(2 ** 63), 2 ** 63 - 1, (self.rows,), generator=g, dtype=torch.int64).to(dev)
+        keys = torch.randint(-(2 ** 63), 2 ** 63 - 1, (self.rows,), generator=g, dtype=torch.int64, device=dev)
         vals = _payload(keys, self.row_bytes)
         self.in_rows += int(keys.numel())
-        self.in_key_sum = (self.in_key_sum + int(keys.sum().item())) % (1 << 61)
+        self._in_sum += keys.sum()
         if self.world > 1:
             from ray_memory_management_amd.util.collective.collective import get_group_handle
 
@@ -248,35 +286,46 @@ class OutOfCoreShuffleWorker(ShuffleWorker):
         k, v, counts = partition(keys, vals, self.world * self.P, self.mode)
         cs = counts.tolist()[self.rank * self.P:(self.rank + 1) * self.P]
         off = 0
-        for p, c in enumerate(cs):
-            self.blocks[p].append(ray.put((k[off:off + c].clone(), v[off:off + c].clone())))
+        for p, c in enumerate(cs):  # put copies the slice into the store (asynchronously)
+            self.blocks[p].append(ray.put((k[off:off + c], v[off:off + c])))
             off += c
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
         return {"round": r, "seconds": time.perf_counter() - t0, "rows": int(k.numel())}
+
+    def finish_map(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return True
 
     def reduce_partition(self, p: int):
         import ray_memory_management_amd as ray
 
         t0 = time.perf_counter()
         parts = ray.get(self.blocks[p])
-        keys = torch.cat([x[0].to(self.device) for x in parts]) if parts else torch.empty(0, dtype=torch.int64)
-        vals = torch.cat([x[1].to(self.device) for x in parts]) if parts else torch.empty(0, dtype=torch.uint8)
+        if parts:
+            keys = torch.cat([x[0] for x in parts]).to(self.device)
+            vals = torch.cat([x[1] for x in parts]).to(self.device)
+        else:
+            keys = torch.empty(0, dtype=torch.int64, device=self.device)
+            vals = torch.empty((0, self.row_bytes), dtype=torch.uint8, device=self.device)
         del parts
         keys, order = torch.sort(keys)
         vals = vals[order]
+        del order
         gid = self.rank * self.P + p
-        dest_ok = bool((destinations(keys, self.world * self.P, self.mode) == gid).all().item()) if keys.numel() else True
-        payload_ok = bool(torch.equal(vals, _payload(keys, self.row_bytes))) if keys.numel() else True
-        sorted_ok = bool((keys[1:] >= keys[:-1]).all().item()) if keys.numel() > 1 else True
-        out = {"partition": gid, "rows": int(keys.numel()), "key_sum": int(keys.sum().item()) % (1 << 61),
+        n = int(keys.numel())
+        dest_ok = _count_at(keys, self.world * self.P, self.mode, gid) == n
+        payload_ok, step = True, 1 << 20  # row chunks bound the reference payload's size
+        for i in range(0, n, step):
+            payload_ok = payload_ok and bool(torch.equal(vals[i:i + step], _payload(keys[i:i + step], self.row_bytes)))
+        sorted_ok = bool((keys[1:] >= keys[:-1]).all().item()) if n > 1 else True
+        out = {"partition": gid, "rows": n, "key_sum": int(keys.sum().item()) % (1 << 61) if n else 0,
                "ok": dest_ok and payload_ok and sorted_ok, "payload_ok": payload_ok,
                "seconds": time.perf_counter() - t0}
         self.blocks[p] = []  # the partition's blocks are freed with their last reference
         return out
 
     def inputs(self):
-        return {"rows": self.in_rows, "key_sum": self.in_key_sum}
+        return {"rows": self.in_rows, "key_sum": int(self._in_sum.item()) % (1 << 61)}
 
     def gpu_store_stats(self):
         from ray_memory_management_amd._private import gpu_object_store as gos
@@ -309,12 +358,13 @@ def run_out_of_core_gpu_shuffle(num_workers: int = 1, total_bytes: int = 16 << 3
         if num_workers > 1:
             col.create_collective_group(workers, num_workers, list(range(num_workers)), backend=backend,
                                         group_name=f"oocshuffle-{time.time_ns()}")
-        ray.get([w.setup.remote(partitions_per_worker, row_bytes, rows_per_round, mode) for w in workers])
+        setup = ray.get([w.setup.remote(partitions_per_worker, row_bytes, rows_per_round, mode) for w in workers])
         t0 = time.perf_counter()
-        map_s = []
-        for r in range(rounds):
-            res = ray.get([w.map_round.remote(r) for w in workers])
-            map_s.append(max(x["seconds"] for x in res))
+        # every round is submitted at once: each actor runs them in order (the collective rounds of
+        # several ranks line up), so the driver is off the per-round critical path
+        refs = [w.map_round.remote(r) for r in range(rounds) for w in workers]
+        ray.get(refs)
+        ray.get([w.finish_map.remote() for w in workers])
         t_map = time.perf_counter() - t0
         st_map = ray.get([w.gpu_store_stats.remote() for w in workers])
         red = []
@@ -339,6 +389,7 @@ def run_out_of_core_gpu_shuffle(num_workers: int = 1, total_bytes: int = 16 << 3
             "rows": in_rows, "bytes": data, "GBps": data / elapsed / 1e9, "seconds": elapsed,
             "map_seconds": t_map, "reduce_seconds": elapsed - t_map, "rounds": rounds,
             "partitions": partitions_per_worker * num_workers, "workers": num_workers,
+            "setup_prepin_seconds": max(s["prepin_seconds"] for s in setup),
             "payload_ok": all(x["payload_ok"] for x in red),
             "partition_rows_min": min((x["rows"] for x in red), default=0),
             "partition_rows_max": max((x["rows"] for x in red), default=0),
