@@ -179,23 +179,27 @@ def _runtime(args, n_gpus):
     from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
 
     budget = _cpu_budget(n_gpus)
+    K = max(1, int(getattr(args, "learners_per_gpu", 1)))
+    n_l = n_gpus * K          # learner actors (K share each GPU, each with its own rollout worker(s))
+    per_l = TRAIN_BATCH // K  # samples per learner per iteration
     if args.rollout in ("cpu", "hybrid"):
-        w_per, envs = _rollout_layout(n_gpus, budget, args.fragment)
+        w_per, envs = _rollout_layout(n_l, budget, args.fragment)
+        envs = max(1, per_l // (args.fragment * w_per))
         if args.rollout == "hybrid" and not args.workers_per_learner:
             # GPU policy: ONE worker x 50 envs per learner GPU measured best on MI355X with the native
             # rollout loop (profiles/native_rollout_r3.txt: 15.4-15.9 ms/iter vs 16.9-17.0 for 2 x 25
             # and 34-35 for 5 x 10): one policy step of all 50 envs per env step, one GPU context
-            w_per, envs = 1, TRAIN_BATCH // args.fragment
+            w_per, envs = 1, per_l // args.fragment
         if args.workers_per_learner:
             w_per = args.workers_per_learner
-            envs = max(1, TRAIN_BATCH // (args.fragment * w_per))
+            envs = max(1, per_l // (args.fragment * w_per))
         # hybrid: --env-threads N gives each rollout worker N CPUs and splits its env steps over them
         # (native rollout loop); 1 by default (measured neutral, profiles/native_rollout_r3.txt)
         cpw = max(1, args.env_threads) if args.rollout != "cpu" else 1
-        n_cpus = max(budget, n_gpus * (w_per * cpw + 1) + 1)
+        n_cpus = max(budget, n_l * (w_per * cpw + 1) + 1)
     else:
-        w_per, envs, cpw = 1, TRAIN_BATCH // args.fragment, 1
-        n_cpus = max(budget, 2 * n_gpus + 1)
+        w_per, envs, cpw = 1, per_l // args.fragment, 1
+        n_cpus = max(budget, 2 * n_l + 1)
     phys = 1 if args.same_device else n_gpus
     # the runtime's processes (head, learner / rollout actors) do not inherit the launcher's torchrun
     # rendezvous variables: they form their own groups (util.collective), and a stray RANK /
@@ -206,7 +210,7 @@ def _runtime(args, n_gpus):
              or k.startswith("TORCHELASTIC_")}
     if saved:
         print(f"[bench] runtime processes start without the launcher's {sorted(saved)}", file=sys.stderr)
-    if args.same_device and args.dist_backend == "nccl":
+    if (args.same_device or K > 1) and args.dist_backend == "nccl":
         # 1-GPU rehearsal of the RCCL learner group: every learner claims its own host id so RCCL
         # accepts several ranks on one device (socket transport over loopback; functional only)
         os.environ["RMM_RCCL_SAME_DEVICE"] = "1"
@@ -216,22 +220,22 @@ def _runtime(args, n_gpus):
         cfg = (PPOConfig()
                .environment("GPUSyntheticAtari-v0" if args.rollout == "gpu" else "SyntheticAtariVec-v0",
                             env_config={"num_actions": 4, "episode_len": 1000})
-               .rollouts(num_rollout_workers=w_per * n_gpus, num_envs_per_worker=envs,
+               .rollouts(num_rollout_workers=w_per * n_l, num_envs_per_worker=envs,
                          rollout_fragment_length=args.fragment, postprocess_on_learner=True, rollout_env_threads=cpw,
                          gpu_rollouts=args.rollout == "gpu")
                .training(train_batch_size=TRAIN_BATCH * n_gpus, sgd_minibatch_size=args.minibatch * n_gpus,
                          num_sgd_iter=args.sgd_iters, lr=5e-5, lambda_=0.95, kl_coeff=0.5, clip_param=0.1,
                          vf_clip_param=10.0, entropy_coeff=0.01, vf_loss_coeff=1.0, gamma=0.99,
                          compute_dtype=getattr(args, "dtype", "bf16"))
-               .resources(num_learner_workers=n_gpus, num_cpus_per_worker=cpw,
-                          num_gpus_per_learner_worker=(0.5 if args.rollout != "cpu" else 1.0) * phys / n_gpus,
+               .resources(num_learner_workers=n_l, num_cpus_per_worker=cpw,
+                          num_gpus_per_learner_worker=(0.5 if args.rollout != "cpu" else 1.0) * phys / n_l,
                           # hybrid: CPU env, policy on the worker's slice of the learner's GPU
-                          num_gpus_per_worker={"gpu": 0.5, "hybrid": 0.5 / w_per}.get(args.rollout, 0) * phys / n_gpus,
+                          num_gpus_per_worker={"gpu": 0.5, "hybrid": 0.5 / w_per}.get(args.rollout, 0) * phys / n_l,
                           learner_collective_backend=args.dist_backend)
                .debugging(seed=0))
         algo = cfg.build()
-        info = {"rollout_workers": w_per * n_gpus, "envs_per_worker": envs, "cpus_per_rollout_worker": cpw,
-                "learner_actors": n_gpus,
+        info = {"rollout_workers": w_per * n_l, "envs_per_worker": envs, "cpus_per_rollout_worker": cpw,
+                "learner_actors": n_l, "learners_per_gpu": K,
                 "cpu_budget": budget, "learners": algo.learner_group.device_info()}
         for _ in range(args.warmup):
             algo.train()
@@ -268,6 +272,9 @@ def main():
                     help="learner / GPU policy compute precision (fp32 = precision-matched with the reference)")
     ap.add_argument("--no-fp32", action="store_true", help="bf16 headline: skip the extra fp32 runtime measurement")
     ap.add_argument("--no-bf16", action="store_true", help="fp32 headline: skip the extra bf16 runtime measurement")
+    ap.add_argument("--learners-per-gpu", type=int, default=1,
+                    help="learner actors (data-parallel ranks, gradients averaged every SGD step) per GPU; the "
+                         "per-GPU batch (5000) and minibatch (500) are split between them")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every learner on GPU 0 (RCCL ranks get distinct host ids "
                          "and use the socket transport; or --dist-backend gloo)")
@@ -410,7 +417,9 @@ def main():
             "data": "synthetic 84x84x4 uint8 frames (vectorised synthetic Atari env), random-init weights",
             "config": {"model": "RLlib PPO VisionNetwork (Atari filters 16/32/256), atari-ppo.yaml hyper-parameters",
                        "global_batch": TRAIN_BATCH * n_gpus, "seq_len": args.fragment,
-                       "parallelism": f"dp{n_gpus}", "sgd_minibatch_size": args.minibatch,
+                       "parallelism": f"dp{n_gpus}" if args.learners_per_gpu <= 1 else
+                       f"dp{n_gpus * args.learners_per_gpu} ({args.learners_per_gpu} learner ranks per GPU)",
+                       "sgd_minibatch_size": args.minibatch,
                        "num_sgd_iter": args.sgd_iters, **mode_info},
             **extra,
             "put_get_GBps": None if put_gbps is None else round(put_gbps, 2),

@@ -275,7 +275,14 @@ class PeerComm(Comm):
         except Exception as e:  # noqa: BLE001
             err = e
         store.set(f"{key}/h{self.rank}", blob)
+        try:  # which physical GPU each rank drives: ranks sharing one only contend when they overlap
+            bus = h.pci_bus_id(self.device.index).encode()
+        except Exception:  # noqa: BLE001
+            bus = f"?{self.rank}".encode()
+        store.set(f"{key}/bus{self.rank}", bus)
         hs = [store.get(f"{key}/h{r}") for r in range(self.world)]
+        #: True when some ranks share a physical GPU (1-GPU rehearsals, several learners per GPU)
+        self.shared_device = len({store.get(f"{key}/bus{r}") for r in range(self.world)}) < self.world
         ok = err is None and all(len(b) > 0 for b in hs)
         if ok:
             try:

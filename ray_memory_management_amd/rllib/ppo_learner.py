@@ -70,11 +70,6 @@ def _x3_available() -> bool:
         return False
 
 
-def _comm_overlap() -> bool:
-    """Multi-rank step with the dense-bucket all-reduce forked onto a comm stream beside the trunk
-    backward (opt-in: the fork / join costs more than it hides on MI355X)."""
-    return os.environ.get("RMM_COMM_OVERLAP") == "1"
-
 
 class _CatPPOLoss(torch.autograd.Function):
     """K5b: the categorical PPO loss head; forward = stats, backward = d/dlogits, d/dvalues."""
@@ -516,7 +511,7 @@ class PPOLearner:
         h.dense_heads_bwd(ws["dz"].data_ptr(), A1, hd.weight.data_ptr(), ws["hidden"].data_ptr(), ws["h2"].data_ptr(),
                           dl.weight.data_ptr(), mbs, K, ws["dx"].data_ptr(), g[4].data_ptr(), g[5].data_ptr(),
                           g[6].data_ptr(), g[7].data_ptr(), ws["dpre"].data_ptr(), st, dpre_ready=True,
-                          adam=self._fused_adam_args(bump=False), defer_finalize=self._split_fin(),
+                          defer_finalize=self._split_fin(),
                           split=self._k12_split(mbs))
 
     def _manual_trunk_bwd(self, full):
@@ -528,7 +523,7 @@ class PPOLearner:
         ws = self._manual_ws(full["mbs"])
         g = [p._rmm_grad_out for p in self.params]
         ctr = self._ctr().data_ptr()
-        adam, tail = (self._tail_adam_args() if self._tail_adam() else (self._fused_adam_args(bump=True), []))
+        adam, tail = self._tail_adam_args() if self._tail_adam() else ([], [])
         fin = []
         if self._split_fin():  # the deferred K12 finalize (+ Adam) runs in the trunk-reduce launch
             part, rs, groups = self._split_plan(int(full["mbs"]))
@@ -574,7 +569,7 @@ class PPOLearner:
         11.04 -> 10.62 / 10.67 ms per iteration on MI355X (profiles/tail_adam_r4.txt). RMM_TAIL_ADAM=0
         restores the separate K6."""
         return (self._manual is not None and self.world == 1 and self.clip_out is None and self._manual % 4 == 0
-                and not self.x3 and not self._fused_adam() and not self._split_adam_ok()
+                and not self.x3
                 and os.environ.get("RMM_TAIL_ADAM", "1") != "0")
 
     def _tail_adam_args(self):
@@ -603,25 +598,6 @@ class PPOLearner:
             self._par ^= 1
         return adam, tail
 
-    def _fused_adam(self) -> bool:
-        """World of one without a global-norm clip: K6 folds into the gradient epilogues — K12 applies
-        Adam to the dense + heads parameters as their gradients become final, the K10 trunk reduce to
-        the trunk parameters, and the trunk reduce's last workgroup advances the step counters. The
-        gradients are rounded to bf16 first, so the update is bit-identical to K12/K10 → K6.
-        Opt-in (RMM_FUSED_ADAM=1): measured 5 µs per SGD step SLOWER on MI355X (fused loop 12.2 vs
-        11.7 ms/iter, profiles/fused_adam_r3.txt) — K12 runs 122 workgroups, so the 26 MB of Adam
-        traffic its epilogue adds moves through half the CUs, while K6 spreads it over the whole chip."""
-        return (self._manual is not None and self.world == 1 and self.clip_out is None and not self.x3
-                and not self._split_adam_ok() and os.environ.get("RMM_FUSED_ADAM") == "1")
-
-    def _fused_adam_args(self, bump: bool):
-        if not self._fused_adam():
-            return []
-        c = self.ctr.data_ptr()
-        return [self.flat_grad.data_ptr(), self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(),
-                self._wptr(), self.hp.data_ptr(), c + 8, c if bump else 0, 2 if bump else 0,
-                self._bump_done.data_ptr() if bump else 0]
-
     def _opt_launch(self):
         """[K6b global-norm clip coefficient →] K6 Adam; K6 also advances both device counters
         {minibatch step, Adam step} from its last workgroup. Graph-capturable."""
@@ -644,40 +620,6 @@ class PPOLearner:
             h.adam_flat(*args, step_ctr=cur.data_ptr() + 8, bump=cur.data_ptr(), nbump=2,
                         done=self._bump_done.data_ptr(), scale_ptr=scale_ptr, wlo=self._wlo())
 
-    def _adam_range(self, lo: int, hi: int, stream: int, bump: bool, max_blocks: int = 0):
-        """K6 over params [lo, hi) of the flat buckets on `stream`; `bump` advances the device
-        counters (exactly one launch per SGD step may)."""
-        h = require_hip()
-        f4, b2 = 4 * lo, 2 * lo
-        h.adam_flat(self.master.data_ptr() + f4, self.m1.data_ptr() + f4, self.m2.data_ptr() + f4,
-                    self.flat_grad.data_ptr() + b2, True, self._wptr() + b2, self.hp.data_ptr(),
-                    1.0 / self.world, hi - lo, stream, step_ctr=self.ctr.data_ptr() + 8,
-                    bump=self.ctr.data_ptr() if bump else 0, nbump=2 if bump else 0,
-                    done=self._bump_done.data_ptr() if bump else 0, max_blocks=max_blocks)
-
-    def _split_adam_ok(self) -> bool:
-        """The dense+heads Adam can run beside the trunk backward: their buffers are disjoint and
-        only a global-norm clip (needs every gradient first) couples them. Bucket offsets must keep
-        K6's 16-B vector alignment. Opt-in (RMM_SPLIT_ADAM_BLOCKS=<grid cap>): with the full
-        977-block grid beside K10 backward the SGD step got 16 µs SLOWER on MI355X (the Adam
-        waves delay the LDS-bound trunk workgroups), profiles/split_adam_r3.txt."""
-        return (self._manual is not None and self.clip_out is None and self._manual % 4 == 0 and not self.x3
-                and int(os.environ.get("RMM_SPLIT_ADAM_BLOCKS", "0")) > 0)
-
-    def _overlapped_tail(self, full):
-        """World of one: after K12 the dense+heads gradients are final, so their Adam (≈99% of the
-        parameters, ~8 µs of memory traffic) runs on a side stream WHILE the trunk backward (256
-        LDS-bound workgroups, one per CU, leaving most wave slots free) runs on the capture stream;
-        the trunk Adam then joins and advances the step counters."""
-        cap = torch.cuda.current_stream(self.device)
-        side = self._side_stream()
-        side.wait_stream(cap)
-        self._adam_range(self._manual, self.n_params, side.cuda_stream, bump=False,
-                         max_blocks=int(os.environ.get("RMM_SPLIT_ADAM_BLOCKS", "0")))
-        self._manual_trunk_bwd(full)
-        cap.wait_stream(side)
-        self._adam_range(0, self._manual, cap.cuda_stream, bump=True)
-
     def _peer_in_graph(self) -> bool:
         """The communicator's collectives are plain kernels with no host step (PeerComm): they can
         sit inside a chained multi-step SGD graph."""
@@ -685,11 +627,16 @@ class PPOLearner:
             and os.environ.get("RMM_PEER_IN_GRAPH", "1") != "0"
 
     def _peer_mode(self) -> str:
-        """How a peer-comm SGD step reduces its bucket (RMM_PEER_MODE):
-        ``one`` (default): one all-reduce of the whole bucket after both backwards;
-        ``split``: the dense+heads bucket right after K12, the trunk bucket after K10 bwd (same stream);
-        ``fork``: the dense+heads all-reduce forked onto the comm stream beside the K10 backward."""
-        return os.environ.get("RMM_PEER_MODE", "one")
+        """How a peer-comm SGD step reduces its bucket (RMM_PEER_MODE overrides):
+        ``fork`` (default when every rank has its own GPU): the dense+heads bucket (≈99% of the bytes,
+        final after K12) is all-reduced on the comm stream WHILE the trunk backward runs on the compute
+        stream; then the small trunk bucket; Adam after both;
+        ``one`` (default when ranks share a GPU, where the overlap only contends for the same CUs):
+        one all-reduce of the whole bucket after both backwards."""
+        m = os.environ.get("RMM_PEER_MODE")
+        if m in ("one", "fork"):
+            return m
+        return "one" if getattr(self.comm, "shared_device", True) else "fork"
 
     def _manual_peer_step(self, full):
         """One multi-rank SGD step with the peer-memory all-reduce (eager or under capture): every
@@ -702,22 +649,14 @@ class PPOLearner:
             cs.wait_stream(cap)
             self.comm.allreduce_on(self.flat_grad[self._manual:], cs)
             self._manual_trunk_bwd(full)
-            self.comm.allreduce_on(self.flat_grad[:self._manual], cap)
+            # the two all-reduces share the peer kernel's per-workgroup epoch counters (and staging
+            # parity): the trunk one may only start once the dense one has finished
             cap.wait_stream(cs)
-        elif mode == "split":
-            self.comm.allreduce(self.flat_grad[self._manual:])
-            self._manual_trunk_bwd(full)
-            self.comm.allreduce(self.flat_grad[:self._manual])
+            self.comm.allreduce_on(self.flat_grad[:self._manual], cap)
         else:
             self._manual_trunk_bwd(full)
             self.comm.allreduce(self.flat_grad)
         self._opt_launch()
-
-    def _side_stream(self):
-        s = getattr(self, "_side", None)
-        if s is None:
-            s = self._side = torch.cuda.Stream(self.device)
-        return s
 
     def _ctr(self):
         """The device counter copy the step being launched / captured reads."""
@@ -789,21 +728,12 @@ class PPOLearner:
             self._manual_peer_step(full)
         elif self._manual_ok(full):
             self._manual_fwd_dense_bwd(full)
-            if self.world > 1 and _comm_overlap():
-                work = self.comm.allreduce_async(self.flat_grad[self._manual:])   # dense+heads bucket
-                self._manual_trunk_bwd(full)                                        # overlaps the RCCL op
-                work2 = self.comm.allreduce_async(self.flat_grad[:self._manual])  # trunk bucket
-                work.wait()
-                work2.wait()
-            elif self.world > 1:
+            if self.world > 1:
                 self._manual_trunk_bwd(full)
                 self.comm.allreduce(self.flat_grad)  # one collective, same stream: no fork / join
-            elif self._split_adam_ok():
-                self._overlapped_tail(full)
-                return
             else:
                 self._manual_trunk_bwd(full)
-                if self._fused_adam() or self._tail_adam():
+                if self._tail_adam():
                     return
             self._opt_launch()
         else:
@@ -851,35 +781,7 @@ class PPOLearner:
         self._graph = self._graphs_split = None
         self._graph_has_comm = False
         self._chain = 1
-        if self.world > 1 and manual and getattr(self.comm, "graph_capturable", False) \
-                and os.environ.get("RMM_RCCL_IN_GRAPH") == "1":
-            # ONE graph per SGD step with the all-reduces inside it: after K12 the graph forks onto
-            # the comm stream (dense+heads bucket, ≈99% of the bytes) while K10 backward runs on
-            # the compute stream, then reduces the small trunk bucket and joins before K6 Adam.
-            # Opt-in: a captured RCCL op over the socket transport (the 1-GPU rehearsal) crashes
-            # hipGraph capture on torch's RCCL 2.26 (profiles/rccl_native_r3.txt), so the default
-            # multi-rank step is the split-graph one below with the same fork/join done eagerly
-            cs = self.comm.stream
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                cap = torch.cuda.current_stream(self.device)
-                self._manual_fwd_dense_bwd(full)
-                cs.wait_stream(cap)
-                self.comm.allreduce_on(self.flat_grad[self._manual:], cs)
-                self._manual_trunk_bwd(full)
-                cs.wait_stream(cap)
-                self.comm.allreduce_on(self.flat_grad[:self._manual], cs)
-                cap.wait_stream(cs)
-                self._opt_launch()
-            self._graph = g
-            self._graph_has_comm = True
-        elif self.world == 1 and manual and self._split_adam_ok():
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._manual_fwd_dense_bwd(full)
-                self._overlapped_tail(full)
-            self._graph = g
-        elif self.world == 1 or self.cfg["allreduce_in_graph"] or self._peer_in_graph():
+        if self.world == 1 or self.cfg["allreduce_in_graph"] or self._peer_in_graph():
             # world of one: `chain` consecutive SGD steps per graph (the device counters index each
             # step's minibatch and Adam step) — consecutive replays of a one-step graph leave ~8 µs
             # idle between them on MI355X (profiles/sgd_chain_r3.txt), a chained graph none.
@@ -888,8 +790,7 @@ class PPOLearner:
             peer = self.world > 1 and self._peer_in_graph()
             chain = self._sgd_chain(int(full["period"])) if (self.world == 1 or peer) else 1
             self._graph_has_comm = self.world > 1
-            self._parity = (manual and chain > 1 and not self._fused_adam()
-                            and os.environ.get("RMM_CTR_PARITY", "1") != "0")
+            self._parity = manual and chain > 1 and os.environ.get("RMM_CTR_PARITY", "1") != "0"
             self._par = 0
             try:
                 g = torch.cuda.CUDAGraph()
@@ -905,7 +806,7 @@ class PPOLearner:
                             self._manual_trunk_bwd(full)
                             if self.world > 1:
                                 self.comm.allreduce(self.flat_grad[:self._manual])
-                            if not (self._fused_adam() or self._tail_adam()):
+                            if not self._tail_adam():
                                 self._opt_launch()
                         else:
                             self._fast_step(full, True)
@@ -916,17 +817,6 @@ class PPOLearner:
                 raise RuntimeError("chained SGD graph must leave the step counters in copy 0")
             self._graph = g
             self._chain = chain
-        elif manual and _comm_overlap():
-            # multi-rank, RMM_COMM_OVERLAP=1: three graphs with the two bucket all-reduces between
-            # them, the dense+heads all-reduce forked onto the comm stream during graph B
-            ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
-                self._manual_fwd_dense_bwd(full)
-            with torch.cuda.graph(gb):
-                self._manual_trunk_bwd(full)
-            with torch.cuda.graph(gc):
-                self._opt_launch()
-            self._graphs_split = (ga, gb, gc)
         elif manual:
             # multi-rank default: forward + both backwards in one graph, ONE all-reduce of the whole
             # flat bucket on the same stream, Adam graph. A fork onto a comm stream and the join
@@ -962,15 +852,6 @@ class PPOLearner:
             ga, _, gc = self._graphs_split
             ga.replay()
             self.comm.allreduce(self.flat_grad)
-            gc.replay()
-        elif self._graphs_split is not None:
-            ga, gb, gc = self._graphs_split
-            ga.replay()
-            work = self.comm.allreduce_async(self.flat_grad[self._manual:])
-            gb.replay()
-            work2 = self.comm.allreduce_async(self.flat_grad[:self._manual])
-            work.wait()
-            work2.wait()
             gc.replay()
         elif self.world > 1 and not self.cfg["allreduce_in_graph"] and not self._graph_has_comm:
             self._graph.replay()

@@ -78,18 +78,15 @@ def test_manual_step_matches_autograd_step(cuda, graphs, monkeypatch):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-def test_fused_adam_epilogues_match_k6(cuda, graphs, monkeypatch):
-    """Adam folded into the K12 / K10-trunk-reduce epilogues (world of one) vs the separate K6 launch:
-    same weights, moments and step counters after two updates (4 minibatches x 2 epochs each)."""
-    monkeypatch.setenv("RMM_K12_SPLIT", "1")  # the fused epilogues need K12 unsplit: same row order both sides
+def test_tail_adam_matches_k6(cuda, graphs, monkeypatch):
+    """Adam folded into the K10 trunk-reduce launch (tail Adam, the world-of-one default) vs the separate
+    K6 launch: same weights, moments and step counters after two updates (4 minibatches x 2 epochs)."""
+    monkeypatch.setenv("RMM_K12_SPLIT", "1")  # same K12 row order both sides
     outs = []
-    for fused in (True, False):
-        if fused:
-            monkeypatch.setenv("RMM_FUSED_ADAM", "1")
-        else:
-            monkeypatch.delenv("RMM_FUSED_ADAM", raising=False)
+    for tail in (True, False):
+        monkeypatch.setenv("RMM_TAIL_ADAM", "1" if tail else "0")
         L = _learner(cuda, use_graphs=graphs, lr=1e-3, weight_decay=0.01)
-        assert L._fused_adam() == fused
+        assert L._tail_adam() == tail
         obs, cols = _tables(cuda)
         torch.manual_seed(5)
         st = L._update_tables(obs, cols, 4)
