@@ -65,6 +65,28 @@ struct AdamTail {
   int64_t K = 0;
 };
 
+// Adam folded into the x3 (fp32 learner) trunk-reduce launch: the flat fp32 buffers (param memory
+// order; the trunk range [0, n_trunk) is reduced in this launch, [n_trunk, n) holds the final dense +
+// heads gradients), the split-pair weight planes, and the step counters (bump_next set = parity
+// counters, else `done` tickets the last workgroup, which advances them in place).
+struct X3Adam {
+  float* master = nullptr;  // null: gradients only (Adam runs as K6 afterwards)
+  float* m1 = nullptr;
+  float* m2 = nullptr;
+  const float* grad = nullptr;
+  void* whi = nullptr;
+  void* wlo = nullptr;
+  int64_t n_trunk = 0;
+  int64_t n = 0;
+  const float* hp = nullptr;
+  const int64_t* step_ctr = nullptr;
+  float grad_scale = 1.f;
+  int64_t* bump = nullptr;
+  int nbump = 0;
+  uint32_t* done = nullptr;
+  int64_t* bump_next = nullptr;
+};
+
 // XCD-aware remap of a linear workgroup id (bijective for any grid size): consecutive
 // logical ids land on the same XCD so neighbouring tiles share an L2.
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {

@@ -671,12 +671,28 @@ PYBIND11_MODULE(_hip, m) {
   m.def("x3_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, XP W2,
                            std::vector<int64_t> w2s, XP h1, uint64_t h2hi, XP dh2, XP dpre1, uint64_t partial,
                            uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
-                           uint64_t stream) {
+                           uint64_t stream, std::vector<uint64_t> adam, float grad_scale) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_bwd: 4 strides per weight");
+    // adam (optional, the tail Adam): [master, m1, m2, grad, whi, wlo, n_trunk, n, hp, step_ctr, bump, nbump,
+    // done, bump_next]
+    X3Adam xa;
+    if (!adam.empty()) {
+      if (adam.size() != 14) throw std::invalid_argument("x3_trunk_bwd: adam needs 14 fields");
+      xa.master = P<float>(adam[0]), xa.m1 = P<float>(adam[1]), xa.m2 = P<float>(adam[2]);
+      xa.grad = P<const float>(adam[3]), xa.whi = P<void>(adam[4]), xa.wlo = P<void>(adam[5]);
+      xa.n_trunk = int64_t(adam[6]), xa.n = int64_t(adam[7]);
+      xa.hp = P<const float>(adam[8]), xa.step_ctr = P<const int64_t>(adam[9]);
+      xa.bump = adam[10] ? P<int64_t>(adam[10]) : nullptr, xa.nbump = int(adam[11]);
+      xa.done = adam[12] ? P<uint32_t>(adam[12]) : nullptr, xa.bump_next = adam[13] ? P<int64_t>(adam[13]) : nullptr;
+      xa.grad_scale = grad_scale;
+    }
     x3_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr,
                  period, B, xin(W2), w2s.data(), xin(h1), P<const void>(h2hi), xin(dh2), xout(dpre1), P<float>(partial),
-                 P<float>(dW1), w1s.data(), P<float>(db1), P<float>(dW2), P<float>(db2), S(stream));
-  });
+                 P<float>(dW1), w1s.data(), P<float>(db1), P<float>(dW2), P<float>(db2), S(stream), xa);
+  }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W2"), py::arg("w2s"),
+     py::arg("h1"), py::arg("h2hi"), py::arg("dh2"), py::arg("dpre1"), py::arg("partial"), py::arg("dW1"),
+     py::arg("w1s"), py::arg("db1"), py::arg("dW2"), py::arg("db2"), py::arg("stream"),
+     py::arg("adam") = std::vector<uint64_t>{}, py::arg("grad_scale") = 1.0f);
   m.def("x3_dense_fwd_part_slices", &x3_dense_fwd_part_slices);
   m.def("x3_dense_fwd_part", [](XP x, XP w, int64_t M, int64_t K, int N, uint64_t part, int nslices, uint64_t stream) {
     x3_dense_fwd_part(xin(x), xin(w), M, K, N, P<float>(part), nslices, S(stream));

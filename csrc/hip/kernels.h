@@ -226,7 +226,8 @@ int x3_conv1_wgrad_groups(int64_t B);
 int64_t x3_trunk_partial_floats(int64_t B);
 void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W2,
                   const int64_t* w2s, X3In h1, const void* h2hi, X3In dh2, X3Out dpre1, float* partial, float* dW1,
-                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream);
+                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream,
+                  const X3Adam& xa = X3Adam{});
 // K13x: split-K dense layer -> fp32 partials part[S][M][N]
 int x3_dense_fwd_part_slices(int64_t M, int64_t K, int N);
 void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part, int S, hipStream_t stream);

@@ -21,6 +21,7 @@
 // C/D col l&15, row 4(l>>4)+i.
 #include <hip/hip_bf16.h>
 
+#include "adam_device.h"
 #include "common.h"
 #include "dense_device.h"
 #include "kernels.h"
@@ -513,6 +514,15 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
 // Sum the two backward launches' per-workgroup partials in a fixed order into fp32 gradients in the
 // parameters' memory order (deterministic). Output index e as conv_kernels.hip: [dW1 4096][dW2 8192][db1 16][db2 32].
 constexpr int PARTX = C1 * 256 + C2 * 256 + C1 + C2;
+// the step counters advance once every workgroup of the launch has read them
+__device__ __forceinline__ void x3_tail_bump(const X3Adam& xa) {
+  if (xa.bump_next) {  // parity counters: the next step reads the other copy
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      for (int k = 0; k < xa.nbump; k++) xa.bump_next[k] = xa.bump[k] + 1;
+    return;
+  }
+  last_block_bump(xa.bump, xa.nbump, xa.done);
+}
 constexpr int RED_SLICES = 8, RED_BATCH = 16;
 __device__ __forceinline__ float* trunk_grad_dst_f32(int e, float* dW1, WStrides w1, float* db1, float* dW2,
                                                      WStrides w2, float* db2) {
@@ -529,8 +539,20 @@ __device__ __forceinline__ float* trunk_grad_dst_f32(int e, float* dW1, WStrides
 }
 __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict__ part1, int G1,
                                                          const float* __restrict__ part2, int G2, float* dW1,
-                                                         WStrides w1, float* db1, float* dW2, WStrides w2, float* db2) {
+                                                         WStrides w1, float* db1, float* dW2, WStrides w2, float* db2,
+                                                         const X3Adam xa, int nred) {
   __shared__ float red[RED_SLICES][64];
+  if (int(blockIdx.x) >= nred) {  // Adam workgroups: K6's vector pass over the dense + heads range
+    const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
+    const int64_t o = xa.n_trunk;
+    const int64_t tid = int64_t(blockIdx.x - nred) * blockDim.x + threadIdx.x;
+    const int64_t nthr = int64_t(gridDim.x - nred) * blockDim.x;
+    adam_span<float, true, 2>(xa.master + o, xa.m1 + o, xa.m2 + o, xa.grad + o,
+                              static_cast<__hip_bfloat16*>(xa.whi) + o, xa.grad_scale, ac, tid, nthr, xa.n - o,
+                              static_cast<__hip_bfloat16*>(xa.wlo) + o);
+    x3_tail_bump(xa);
+    return;
+  }
   const int c = threadIdx.x & 63, slice = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + c;
   // source: dW1 from the conv1 launch (stride PART1), the rest from the conv2 launch: its layout is
@@ -561,8 +583,23 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
-    *trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2) = t;
+    float* dst = trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2);
+    *dst = t;
+    if (xa.master) {  // the trunk gradient is final: Adam on it (same math as K6's scalar pass)
+      const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
+      const int64_t i = dst - xa.grad;
+      float a = xa.m1[i], b = xa.m2[i];
+      const float w = adam_one(xa.master[i], t * xa.grad_scale, a, b, ac);
+      xa.m1[i] = a;
+      xa.m2[i] = b;
+      xa.master[i] = w;
+      unsigned short hi, lo;
+      split(w, hi, lo);
+      static_cast<unsigned short*>(xa.whi)[i] = hi;
+      static_cast<unsigned short*>(xa.wlo)[i] = lo;
+    }
   }
+  if (xa.master) x3_tail_bump(xa);
 }
 
 }  // namespace x3
@@ -621,8 +658,19 @@ int64_t x3_trunk_partial_floats(int64_t B) {
 
 void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W2,
                   const int64_t* w2s, X3In h1, const void* h2hi, X3In dh2, X3Out dpre1, float* partial, float* dW1,
-                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream) {
+                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream, const X3Adam& xa) {
   if (B <= 0) return;
+  if (xa.master) {
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool ok = al(xa.master) && al(xa.m1) && al(xa.m2) && al(xa.grad) && xa.whi && xa.wlo &&
+                    (reinterpret_cast<uintptr_t>(xa.whi) & 7) == 0 && (reinterpret_cast<uintptr_t>(xa.wlo) & 7) == 0 &&
+                    xa.n_trunk % 4 == 0 && xa.n_trunk >= x3::PARTX && xa.n > xa.n_trunk && xa.hp && xa.step_ctr &&
+                    xa.bump && xa.nbump > 0 && (xa.bump_next || xa.done) && dW1 >= xa.grad &&
+                    db2 < xa.grad + xa.n_trunk;
+    if (!ok)
+      throw std::invalid_argument("x3_trunk_bwd: Adam tail needs aligned flat buffers (trunk range first, "
+                                  "n_trunk % 4 == 0), both weight planes, hp, the step counters and a bump target");
+  }
   if (period <= 0) period = 1;
   for (const X3In* p : {&W2, &h1, &dh2})
     if (!p->hi || !p->lo) throw std::invalid_argument("x3_trunk_bwd: W2 / h1 / dh2 need hi and lo planes");
@@ -638,8 +686,10 @@ void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
                      p1);
   RMM_HIP_CHECK(hipGetLastError());
   const int nred = (x3::PARTX + 63) / 64;
-  hipLaunchKernelGGL(x3::k_trunk_reduce_x3, dim3(nred), dim3(512), 0, stream, p1, G1, p2, G2, dW1, wsx(w1s), db1,
-                     dW2, wsx(w2s), db2);
+  // Adam workgroups: two groups of 4 elements per lane (K6's default unroll)
+  const int nadam = xa.master ? int(std::max<int64_t>(1, ((xa.n - xa.n_trunk + 3) / 4 + 1023) / 1024)) : 0;
+  hipLaunchKernelGGL(x3::k_trunk_reduce_x3, dim3(nred + nadam), dim3(512), 0, stream, p1, G1, p2, G2, dW1, wsx(w1s),
+                     db1, dW2, wsx(w2s), db2, xa, nred);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -469,10 +469,27 @@ class PPOLearner:
         ws = self._manual_ws(full["mbs"])
         g = [p._rmm_grad_out for p in self.params]
         w2 = P[m._X3_NAMES[2]]
-        h.x3_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), self._ctr().data_ptr(), int(full["period"]),
+        ctr = self._ctr().data_ptr()  # this step's counter copy (the tail args advance the parity)
+        adam = self._x3_tail_args() if self._tail_adam() else []
+        h.x3_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), ctr, int(full["period"]),
                        int(full["mbs"]), w2.ptrs(), list(w2.hi.stride()), ws["h1"].ptrs(), ws["h2"].hi.data_ptr(),
                        ws["dx"].ptrs(), ws["dpre1"].ptrs(), ws["part"].data_ptr(), g[0].data_ptr(),
-                       list(m.convs[0].weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream())
+                       list(m.convs[0].weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
+                       adam=adam, grad_scale=1.0 / self.world)
+
+    def _x3_tail_args(self):
+        """Tail Adam of the fp32 learner (world of one): K6 folded into the x3 trunk-reduce launch — the
+        reduce workgroups update each trunk parameter as its gradient becomes final, extra workgroups run
+        K6's pass over the dense + heads range; both write the fp32 master, the moments and the split
+        pair (hi / lo planes), and the launch advances the step counters (same rules as K6)."""
+        cur = self._ctr().data_ptr()
+        parity = self._parity and not (self._parity_last and self._par == 0)
+        nxt = self._ctrs[1 - self._par].data_ptr() if parity else 0
+        if parity:
+            self._par ^= 1
+        return [self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(),
+                self.w_x3.hi.data_ptr(), self.w_x3.lo.data_ptr(), self._manual, self.n_params, self.hp.data_ptr(),
+                cur + 8, cur, 2, 0 if parity else self._bump_done.data_ptr(), nxt]
 
     def _x3_views_cached(self):
         key = (self.w_x3.hi.data_ptr(), self.w_x3.lo.data_ptr())
@@ -569,7 +586,6 @@ class PPOLearner:
         11.04 -> 10.62 / 10.67 ms per iteration on MI355X (profiles/tail_adam_r4.txt). RMM_TAIL_ADAM=0
         restores the separate K6."""
         return (self._manual is not None and self.world == 1 and self.clip_out is None and self._manual % 4 == 0
-                and not self.x3
                 and os.environ.get("RMM_TAIL_ADAM", "1") != "0")
 
     def _tail_adam_args(self):

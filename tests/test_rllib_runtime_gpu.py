@@ -100,6 +100,31 @@ def test_tail_adam_matches_k6(cuda, graphs, monkeypatch):
     assert abs(a[5]["total_loss"] - b[5]["total_loss"]) < 1e-5 * max(1.0, abs(a[5]["total_loss"]))
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_x3_tail_adam_matches_k6(cuda, graphs, monkeypatch):
+    """fp32 learner (x3 kernels): Adam folded into the x3 trunk-reduce launch vs the separate K6 launch —
+    identical fp32 master, moments, split-pair planes and step counters after two updates."""
+    outs = []
+    for tail in (True, False):
+        monkeypatch.setenv("RMM_TAIL_ADAM", "1" if tail else "0")
+        L = _learner(cuda, use_graphs=graphs, lr=1e-3, weight_decay=0.01, compute_dtype="fp32")
+        assert L.x3 and L._tail_adam() == tail
+        obs, cols = _tables(cuda)
+        torch.manual_seed(5)
+        st = L._update_tables(obs, cols, 4)
+        torch.manual_seed(6)
+        L._update_tables(obs, cols, 4)
+        outs.append((L.master.clone(), L.m1.clone(), L.m2.clone(), L.w_x3.hi.clone(), L.w_x3.lo.clone(),
+                     L.ctr.clone(), st))
+    a, b = outs
+    assert torch.equal(a[5], b[5])
+    for x, y in zip(a[:5], b[:5]):
+        assert torch.equal(x, y), float((x.float() - y.float()).abs().max())
+    # the split pair is the master's split
+    assert torch.equal(a[3], a[0].to(torch.bfloat16))
+    assert abs(a[6]["total_loss"] - b[6]["total_loss"]) < 1e-5 * max(1.0, abs(a[6]["total_loss"]))
+
+
 def test_grad_clip_coef_matches_torch(cuda):
     from ray_memory_management_amd._native import require_hip
 
