@@ -3,7 +3,8 @@
 // Geometry (rllib/models/utils.py:get_filter_config for 84x84, SAME padding as RLlib SlimConv2d):
 //   frames u8 [B,4,84,84] --conv1 8x8/4 pad 2, 4->16, +b, ReLU--> h1 [B,21,21,16]
 //                          --conv2 4x4/2 pad 2, 16->32, +b, ReLU--> h2 [B,11,11,32] (= NHWC flatten 3872)
-// The 11x11 "valid" third conv is a dense GEMM and stays in hipBLASLt.
+// The 11x11 "valid" third conv is a dense layer (3872 -> 256): the hand-written K13s / K12 kernels in
+// dense_kernels.hip (bf16) and K13x / K12x in x3_kernels.hip (fp32-level) run it, not hipBLASLt.
 //
 // Why fused: per SGD minibatch (500 frames) these two layers are ~3.6+2.0 MFLOP/frame — nothing
 // for MFMA — but MIOpen runs them as 10+ launches (gather/convert, implicit-GEMM fwd, bias/ReLU,
