@@ -29,6 +29,7 @@
 #include "x3_device.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -143,6 +144,23 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   trunk::weight_store(r2l, W2.lo, w2, w2l, W2_PITCH);
   if (push_stack)
     trunk::frame_push_store<NTF>(fr, push_stack + b * FB, push_rows ? push_rows + (push_t[0] * B + b) * FB : nullptr);
+  // every B fragment a wave multiplies is the same for all its tiles and frames: conv1's depends on the
+  // k-step only (N = 16), conv2's on the k-step and the wave's N tile (jobs step by 8 waves, so a wave's
+  // nt = wave & 1 never changes) — read them from LDS once (128 VGPRs) instead of 2 of every 3 (conv1) /
+  // 4 (conv2) LDS reads per MFMA group
+  __syncthreads();  // weights staged
+  bf16x8 w1fh[8], w1fl[8], w2fh[8], w2fl[8];
+  {
+    const int nt = wave & 1;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const int wo1 = r * W1_PITCH + (s * 8 + 2 * g) * 4;
+      w1fh[s] = ld8(&w1h[wo1]), w1fl[s] = ld8(&w1l[wo1]);
+      const int pp = 2 * s + (g >> 1);
+      const int wo2 = (nt * 16 + r) * W2_PITCH + pp * 16 + 8 * (g & 1);
+      w2fh[s] = ld8(&w2h[wo2]), w2fl[s] = ld8(&w2l[wo2]);
+    }
+  }
 
   for (; b < B; b += G) {
     frame_image_store<NTF>(fr, img);
@@ -155,11 +173,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       const int oy = p / H1, ox = p - oy * H1;
       Acc acc = acc0();
 #pragma unroll
-      for (int s = 0; s < 8; s++) {
-        const bf16x8 a = ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]);
-        const int wo = r * W1_PITCH + (s * 8 + 2 * g) * 4;
-        mma2a(acc, a, ld8(&w1h[wo]), ld8(&w1l[wo]));
-      }
+      for (int s = 0; s < 8; s++) mma2a(acc, ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]), w1fh[s], w1fl[s]);
       const f32x4 t = total(acc);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -183,6 +197,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     __syncthreads();
 
     // ---- conv2: 8 M-tiles x 2 N-tiles = 16 jobs over the waves, K = 256 (pixel pp = 2s + (g>>1), ci half g&1)
+    static_assert(NTF / 64 % 2 == 0, "a wave's conv2 N tile (job & 1) must not change");
     for (int job = wave; job < 16; job += NTF / 64) {
       const int mt = job >> 1, nt = job & 1;
       const int q = min(mt * 16 + r, NP2 - 1);
@@ -192,8 +207,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       for (int s = 0; s < 8; s++) {
         const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
         const int ao = ((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1);
-        const int wo = (nt * 16 + r) * W2_PITCH + pp * 16 + 8 * (g & 1);
-        mma3(acc, ld8(&h1h[ao]), ld8(&h1l[ao]), ld8(&w2h[wo]), ld8(&w2l[wo]));
+        mma3(acc, ld8(&h1h[ao]), ld8(&h1l[ao]), w2fh[s], w2fl[s]);
       }
       const f32x4 t = total(acc);
 #pragma unroll
@@ -801,6 +815,129 @@ __global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int
     }
 }
 
+// ---- K13x-L: the same product for the SGD step's M = 500 rows, staged through LDS. The register-direct
+// K13x above is L1-bound there (each 16-B fragment load touches 16 rows x 64 B, and no two waves share an
+// operand: TA stalled by TCP ~45% of the time, profiles/x3_kernels_r5.txt). Here a workgroup owns a
+// 64 x 64 output tile of one K slice; per stage (2 k-steps = 128 B of every row) it loads the A and B
+// tiles of both planes with full-line coalesced 16-B loads (registers for stage s+1 in flight while
+// stage s multiplies), stores them into padded LDS rows (144-B pitch: the 16-row fragment reads are
+// bank-conflict free) and its 4 waves (2 x 2, 32 x 32 each) read their fragments from there: 4x less
+// L1 traffic per MFMA and no half-line requests.
+constexpr int KL_T = 64, KL_PITCH = 72, KL_PLANE = KL_T * KL_PITCH;  // elements
+constexpr int KL_STAGE = 4 * KL_PLANE;  // A hi, A lo, B hi, B lo
+constexpr int KL_D = 4;                 // register-ring depth (stages of global loads in flight)
+__global__ __launch_bounds__(256) void k_dense_fwd_lds_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
+                                                          float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) unsigned short t[2 * KL_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4, wm = wave >> 1, wn = wave & 1;
+  const int nt = N / KL_T;
+  const int64_t mt = (M + KL_T - 1) / KL_T, tiles = mt * nt, total_ = gridDim.x;
+  int64_t id = blockIdx.x;
+  if ((total_ & 7) == 0) id = (id & 7) * (total_ >> 3) + (id >> 3);  // XCD-contiguous runs
+  const int64_t sl = id / tiles, rem = id % tiles, tm = rem / nt, tn = rem % nt;
+  const int64_t m0 = tm * KL_T, n0 = tn * KL_T;
+  const int64_t steps = K / 32, lo = steps * sl / S, hi = steps * (sl + 1) / S;
+  const int nst = int((hi - lo + 1) / 2);  // stages of 2 k-steps (the last may hold one)
+  // loader: 8 x 16 B per thread per stage = {A, B} x {hi, lo} x 2 row halves; thread -> (row, 16-B segment)
+  const int lrow = tid >> 3, lseg = tid & 7;  // rows lrow and lrow + 32
+  const unsigned short* src[8];
+  int64_t kend = hi * 32;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int64_t ar = min(m0 + lrow + 32 * h, M - 1), br = n0 + lrow + 32 * h;
+    src[0 + h] = x.hi + ar * K + lo * 32 + lseg * 8;
+    src[2 + h] = x.lo + ar * K + lo * 32 + lseg * 8;
+    src[4 + h] = w.hi + br * K + lo * 32 + lseg * 8;
+    src[6 + h] = w.lo + br * K + lo * 32 + lseg * 8;
+  }
+  const int64_t kseg = lo * 32 + lseg * 8;  // this thread's k within the stage (+ 64 per stage)
+  // register ring: stage st lives in slot st % KL_D from its issue until it is stashed into LDS one stage
+  // ahead of its use, so KL_D - 1 stages of global loads are in flight behind the MFMAs
+  u16x8 v[KL_D][8];
+  bool okv[KL_D];
+  // loads are unconditional, from an address clamped into the slice (never past a row / the buffer); a
+  // segment past the slice end (the odd last step's second half) is zeroed when it is stashed, so no
+  // load result is consumed before its stash and the loads stay in flight
+#define KL_ISSUE(slot, st_)                                                                             \
+  {                                                                                                     \
+    const int64_t k_ = kseg + int64_t(st_) * 64;                                                        \
+    okv[slot] = k_ < kend;                                                                              \
+    const int64_t o_ = (okv[slot] ? k_ : kend - 8) - kseg;                                              \
+    _Pragma("unroll") for (int q = 0; q < 8; q++) v[slot][q] = *reinterpret_cast<const u16x8*>(src[q] + o_); \
+  }
+#define KL_STASH(slot, buf_)                                                                            \
+  {                                                                                                     \
+    unsigned short* b_ = t + (buf_) * KL_STAGE;                                                         \
+    _Pragma("unroll") for (int q = 0; q < 8; q++)                                                       \
+        *reinterpret_cast<u16x8*>(b_ + (q >> 1) * KL_PLANE + (lrow + 32 * (q & 1)) * KL_PITCH + lseg * 8) = \
+            okv[slot] ? v[slot][q] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};                                     \
+  }
+  Acc acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = acc0();
+#define KL_MMA(st_)                                                                                     \
+  {                                                                                                     \
+    const unsigned short* b = t + ((st_) & 1) * KL_STAGE;                                               \
+    _Pragma("unroll") for (int kk = 0; kk < 2; kk++) {                                                  \
+      bf16x8 ah[2], al[2], bh[2], bl[2];                                                                \
+      _Pragma("unroll") for (int i = 0; i < 2; i++) {                                                   \
+        const int ao = (wm * 32 + 16 * i + r) * KL_PITCH + kk * 32 + 8 * g;                             \
+        ah[i] = ld8(b + ao), al[i] = ld8(b + KL_PLANE + ao);                                            \
+        const int bo = (wn * 32 + 16 * i + r) * KL_PITCH + kk * 32 + 8 * g;                             \
+        bh[i] = ld8(b + 2 * KL_PLANE + bo), bl[i] = ld8(b + 3 * KL_PLANE + bo);                         \
+      }                                                                                                 \
+      _Pragma("unroll") for (int i = 0; i < 2; i++) _Pragma("unroll") for (int j = 0; j < 2; j++)       \
+          mma3(acc[i][j], ah[i], al[i], bh[j], bl[j]);                                                  \
+    }                                                                                                   \
+  }
+  if (nst > 0) {
+    // stage indices are clamped to the last stage: loads and stashes stay unconditional (a clamped
+    // repeat is never multiplied), so the compiler can count the loads in flight instead of draining them
+    const int last = nst - 1;
+#pragma unroll
+    for (int d = 0; d < KL_D; d++) KL_ISSUE(d, min(d, last));
+    KL_STASH(0, 0);
+    KL_ISSUE(0, min(KL_D, last));
+    __syncthreads();
+    int st0 = 0;
+    for (; st0 + KL_D <= nst; st0 += KL_D) {  // steady state: KL_D stages, no guards
+#pragma unroll
+      for (int d = 0; d < KL_D; d++) {
+        const int st = st0 + d;
+        KL_MMA(st);
+        KL_STASH((d + 1) % KL_D, (st + 1) & 1);              // stage st+1 (a clamped repeat past the end)
+        KL_ISSUE((d + 1) % KL_D, min(st + 1 + KL_D, last));  // its slot takes stage st+1+KL_D
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < KL_D - 1; d++) {  // tail: fewer than KL_D stages, all already loaded
+      const int st = st0 + d;
+      if (st < nst) {
+        KL_MMA(st);
+        if (st + 1 < nst) KL_STASH((d + 1) % KL_D, (st + 1) & 1);
+        __syncthreads();
+      }
+    }
+  }
+#undef KL_MMA
+#undef KL_ISSUE
+#undef KL_STASH
+  float* out = part + (sl * M) * N + n0 + wn * 32 + r;
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const f32x4 tt = total(acc[i][j]);
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int64_t row = m0 + wm * 32 + 16 * i + 4 * g + e;
+        if (row < M) out[row * N + 16 * j] = tt[e];
+      }
+    }
+}
+
 // consumer prologue: a lane's 4 hidden values of row rr = ReLU(Σ_s part[s] + b) in fp32 (slice order)
 __device__ __forceinline__ void load_hidden4_x3(const float* __restrict__ hpart, int S, CPair hb, int64_t M,
                                                 int64_t rr, int lane, float (&hv)[4]) {
@@ -1216,6 +1353,16 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd_x3(CPair dz, CPair y, CP
 // ---------------------------------------------------------------- host launchers (dense tail)
 // K13x configurations: M <= 64: 16x16 per wave (FM = FN = 1); larger M: 32x32 (FM = FN = 2)
 static void x3_part_cfg(int64_t M, int64_t K, int N, int* fm, int* S) {
+  if (M > 64 && N % 64 == 0) {  // K13x-L: 64 x 64 tiles, slices for >= 256 workgroups, >= 4 k-steps each
+    const int64_t tiles = ((M + 63) / 64) * (N / 64), steps = K / 32;
+    // 256 workgroups (one per CU): 512 / 1024 measured slower for both K13x-L and its consumer, which sums
+    // the S slices (11.2 / 13.2 / 16.1 us at M = 500, profiles/x3_kernels_r5.txt)
+    int64_t s = (256 + tiles - 1) / tiles;
+    s = std::max<int64_t>(1, std::min<int64_t>({s, 32, std::max<int64_t>(1, steps / 4)}));
+    *fm = 0;
+    *S = int(s);
+    return;
+  }
   const int f = M <= 64 ? 1 : 2;
   const int64_t tiles = ((M + 16 * f - 1) / (16 * f)) * (N / (16 * f));
   const int64_t steps = K / 32;
@@ -1238,6 +1385,13 @@ void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part,
   int f, s_cfg;
   x3_part_cfg(M, K, N, &f, &s_cfg);
   if (S != s_cfg) throw std::invalid_argument("x3_dense_fwd_part: S must be x3_dense_fwd_part_slices(M, K, N)");
+  if (f == 0) {
+    const int64_t tiles = ((M + 63) / 64) * (N / 64);
+    hipLaunchKernelGGL(x3::k_dense_fwd_lds_x3, dim3(uint32_t(tiles * S)), dim3(256), 0, stream, cp(x), cp(w), M, K, N,
+                       S, part);
+    RMM_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int64_t tiles = ((M + 16 * f - 1) / (16 * f)) * (N / (16 * f));
   const dim3 grid(uint32_t(tiles * S)), block(256);
   if (f == 1)

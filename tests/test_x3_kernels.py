@@ -98,12 +98,13 @@ def test_x3_trunk_fwd_bwd_match_fp64(cuda, rows, channels_last):
     assert max(errs.values()) < GRAD_TOL, errs
 
 
-@pytest.mark.parametrize("M", [12, 50, 500, 777])
-def test_x3_dense_fwd_part_matches_fp64(cuda, M):
+@pytest.mark.parametrize("M,K", [(12, 3872), (50, 3872), (500, 3872), (777, 3872), (200, 320), (130, 96)])
+def test_x3_dense_fwd_part_matches_fp64(cuda, M, K):
+    """M <= 64: register-direct K13x; larger M: the LDS-staged K13x-L (odd slice lengths: a half stage)."""
     from ray_memory_management_amd.ops import x3
 
     torch.manual_seed(M)
-    K, N = 3872, 256
+    N = 256
     x = x3.split(torch.relu(torch.randn(M, K, device=cuda)))
     w = x3.split(torch.randn(N, K, device=cuda) * 0.02)
     part, S = x3.dense_fwd_part(x, w)
