@@ -664,7 +664,14 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
   RMM_HIP_CHECK(hipGetLastError());
 }
 
-int x3_conv2_bwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 512))); }
+// conv2 backward: at most one workgroup per CU, frames spread evenly (B = 500: 250 workgroups x 2 frames,
+// the second frame's loads in flight during the first). One frame per workgroup (two per CU) measured 29.9 us
+// vs 22.9 us, and it doubles the partials the reduce reads (11.4 vs 10.1 us); 3 frames each: 28.1 us
+// (profiles/x3_kernels_r5.txt). conv1's weight gradient: 256 (14.8 us; 128: 22.9, 500: 17.7).
+int x3_conv2_bwd_groups(int64_t B) {
+  const int64_t per = std::max<int64_t>(1, (B + 255) / 256);
+  return int(std::max<int64_t>(1, (B + per - 1) / per));
+}
 int x3_conv1_wgrad_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 256))); }
 int64_t x3_trunk_partial_floats(int64_t B) {
   return int64_t(x3_conv2_bwd_groups(B)) * x3::PART2 + int64_t(x3_conv1_wgrad_groups(B)) * x3::PART1;
