@@ -153,12 +153,12 @@ std::vector<double> launch_overhead_probe(int n, hipStream_t stream) {
 }
 
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
-                         int64_t* host_seq_dev) {
+                         int64_t* host_seq_dev, int64_t gate_want) {
   // ctr_t = {rng counter, rollout row}: K10 stores row *t, K16 samples with the counter and advances both
   if (a.x3) {  // fp32 policy: the split-bf16 twins (K10x push -> K13x -> K16x)
     const X3Out h2{a.h2, a.h2lo};
     x3_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, X3In{a.W1, a.W1lo}, a.w1s, X3In{a.b1, a.b1lo},
-                      X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream);
+                      X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream, a.gate, gate_want, a.gate_err);
     x3_dense_fwd_part(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, 256, a.hpart, a.S, stream);
     x3_heads_sample(a.hpart, a.S, X3In{a.bd, a.bdlo}, X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t,
                     a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B, a.A1, stream, k16_done, host_seq_dev);
@@ -203,7 +203,9 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
   std::vector<std::pair<double, int64_t>> completed;
   auto launch = [&](size_t i, int64_t step) {
     if (G[i].direct) {
-      rollout_step_direct(*G[i].direct, G[i].k16_done, G[i].stream, G[i].host_seq_dev);
+      // gated direct launches: step s waits in K10x until the release counter reaches s + 1
+      rollout_step_direct(*G[i].direct, G[i].k16_done, G[i].stream, G[i].host_seq_dev,
+                          G[i].release ? step + 1 : 0);
       if (G[i].host_seq) return;  // completion comes through the host word
     } else {
       RMM_HIP_CHECK(hipGraphLaunch(G[i].exec, G[i].stream));
@@ -218,6 +220,8 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
     for (auto& e : ev) RMM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (size_t i = 0; i < G.size(); i++) {
       if (G[i].host_seq) __atomic_store_n(G[i].host_seq, int64_t(0), __ATOMIC_RELEASE);  // rows restart at 0
+      // the in-kernel gate of direct launches counts from 0 each fragment (nothing is in flight here)
+      if (G[i].direct && G[i].release) __atomic_store_n(G[i].release, int64_t(0), __ATOMIC_RELEASE);
       launch(i, 0);
       if (G[i].release) {
         release(i);                  // step 0's frames are already staged

@@ -40,7 +40,7 @@ struct RolloutGroup {
 std::vector<double> launch_overhead_probe(int n, hipStream_t stream);
 // One policy step of `a` as direct launches on `stream` (the kernels a captured step graph holds).
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
-                         int64_t* host_seq_dev = nullptr);
+                         int64_t* host_seq_dev = nullptr, int64_t gate_want = 0);
 
 // Launch step 0 of every group, then for t < T and each group: wait for its step (poll when
 // `spin`), step its envs (actions → newest frames, rewards, dones at row t) on `threads` CPU threads,

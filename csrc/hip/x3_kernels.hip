@@ -107,7 +107,8 @@ __device__ __forceinline__ void zero_image_border(unsigned short* img) {
 __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, CPair W1, WStrides w1, CPair b1, CPair W2, WStrides w2, CPair b2, Pair h1_out, Pair h2_out,
-    uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t) {
+    uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t,
+    const int64_t* gate, int64_t gate_want, int* gate_err) {
   __shared__ __attribute__((aligned(16))) unsigned short img[FIMG];
   __shared__ __attribute__((aligned(16))) unsigned short h1h[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short h1l[H1P_ELEMS];
@@ -130,6 +131,22 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   trunk::weight_issue(W2.lo, w2, r2l);
   FrameRegs<NTF> fr;
   int64_t b = blockIdx.x;
+  if (gate) {
+    // step gate: this launch was enqueued before the host stepped the envs; wait for the release counter
+    // (mapped pinned memory, bumped after the new frames are written) before reading them. Bounded
+    // (~0.2-0.5 s): a host that died mid-fragment can never leave a wave spinning (*gate_err is set)
+    if (threadIdx.x == 0) {
+      int64_t n = 0;
+      while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gate_want) {
+        if (++n >= 200000) {
+          if (gate_err) *gate_err = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+  }
   if (push_stack)
     trunk::frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
   else
@@ -251,11 +268,15 @@ __device__ __forceinline__ void b1_issue(int64_t bb, CPair h1, const unsigned sh
 
 __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStrides w2, CPair h1,
                                                       const unsigned short* __restrict__ h2hi, CPair dh2,
-                                                      Pair dpre1, float* __restrict__ partial) {
+                                                      Pair dpre1, float* __restrict__ partial,
+                                                      int dbg /* timing probes: bit 1 skips dW2, bit 2 dh1 */) {
   __shared__ __attribute__((aligned(16))) unsigned short h1s[2 * H1P_ELEMS];      // hi plane, lo plane
   __shared__ __attribute__((aligned(16))) unsigned short dp2[2 * D2W * D2W * C2];   // [plane][oy*12+ox][co2]
   __shared__ __attribute__((aligned(16))) unsigned short dp2t[2 * C2 * DP2_PITCH];  // [plane][co2][kperm(q)]
   __shared__ float red[8 * 64];
+  // the frame's dpre1 pair, staged so it leaves in coalesced 16-B stores (scattered 2-B stores measured 7.9 us
+  // of the launch's 23.5; one workgroup per CU leaves the LDS for it)
+  __shared__ __attribute__((aligned(16))) unsigned short dq[2 * NP1 * C1];
   static_assert(2 * C2 * W2_PITCH <= 2 * H1P_ELEMS, "W2 staging aliases the h1 tile");
   unsigned short* h1hs = h1s;
   unsigned short* h1ls = h1s + H1P_ELEMS;
@@ -335,7 +356,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
 
     // ---- P1a: dW2[co2][k = (ky, kx, ci)] += Σ_q dpre2[q][co2] · h1[2oy+ky][2ox+kx][ci]
 #pragma unroll
-    for (int s = 0; s < NP2P / 32; s++) {
+    for (int s = 0; s < ((dbg & 1) ? 0 : NP2P / 32); s++) {
       const int ao0 = r * DP2_PITCH + 32 * s + 8 * g, ao1 = (16 + r) * DP2_PITCH + 32 * s + 8 * g;
       const bf16x8 a0h = ld8(&dp2t[ao0]), a0l = ld8(&dp2t[DTL + ao0]);
       const bf16x8 a1h = ld8(&dp2t[ao1]), a1l = ld8(&dp2t[DTL + ao1]);
@@ -369,7 +390,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
       }
     }
     // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 -> dpre1 (HBM), db1
-    for (int mt = half; mt * 16 < ncls; mt += 2) {
+    for (int mt = half; mt * 16 < ((dbg & 2) ? 0 : ncls); mt += 2) {
       const int m = min(mt * 16 + r, ncls - 1);
       const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
       Acc acc = acc0();
@@ -391,13 +412,22 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
           unsigned short dh, dl;
           split(d, dh, dl);
           db1 += bf2f(dh) + bf2f(dl);
-          const int64_t go = (b * NP1 + y * H1 + x) * C1 + r;
-          dpre1.hi[go] = dh;
-          dpre1.lo[go] = dl;
+          const int lo_ = (y * H1 + x) * C1 + r;
+          dq[lo_] = dh;
+          dq[NP1 * C1 + lo_] = dl;
         }
       }
     }
-    __syncthreads();  // tiles free for the next frame
+    __syncthreads();  // tiles free for the next frame; dq complete
+    {  // dpre1 pair of frame b: 2 x 441 x 16 bf16 -> HBM in 16-B vectors
+      constexpr int NV = NP1 * C1 / 8;  // vectors per plane
+      const int64_t go = b * NP1 * C1;
+      for (int v = threadIdx.x; v < 2 * NV; v += NTB) {
+        const int pl = v >= NV, vv = v - pl * NV;
+        const u16x8 d = *reinterpret_cast<const u16x8*>(&dq[pl * NP1 * C1 + 8 * vv]);
+        *reinterpret_cast<u16x8*>(&(pl ? dpre1.lo : dpre1.hi)[go + 8 * vv]) = d;
+      }
+    }
   }
 
   float* out = partial + int64_t(blockIdx.x) * PART2;
@@ -642,13 +672,13 @@ void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
     throw std::invalid_argument("x3_trunk_fwd: h2 (and h1) need hi and lo planes");
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(x3_trunk_fwd_groups(B))), dim3(x3::NTF), 0, stream, obs, idx,
                      ctr, period, B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), pp(h1), pp(h2), nullptr,
-                     nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
 void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
                        X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
-                       hipStream_t stream) {
+                       hipStream_t stream, const int64_t* gate, int64_t gate_want, int* gate_err) {
   if (B <= 0) return;
   if (stack == nullptr || new_frames == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: stack and new frames");
   if (rows != nullptr && t_ptr == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: rows need the row counter");
@@ -660,7 +690,7 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
   // push mode: one frame per workgroup (each workgroup shifts its own env's stack)
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(B)), dim3(x3::NTF), 0, stream, nullptr, nullptr, nullptr,
                      int64_t(1), B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), x3::Pair{}, pp(h2), stack,
-                     new_frames, rows, t_ptr);
+                     new_frames, rows, t_ptr, gate, gate_want, gate_err);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -700,7 +730,7 @@ void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
   float* p2 = partial;                              // conv2 launch partials [G2][PART2]
   float* p1 = partial + int64_t(G2) * x3::PART2;    // conv1 launch partials [G1][PART1]
   hipLaunchKernelGGL(x3::k_conv2_bwd_x3, dim3(uint32_t(G2)), dim3(x3::NTB), 0, stream, B, cp(W2), wsx(w2s), cp(h1),
-                     static_cast<const unsigned short*>(h2hi), cp(dh2), pp(dpre1), p2);
+                     static_cast<const unsigned short*>(h2hi), cp(dh2), pp(dpre1), p2, 0);
   RMM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(x3::k_conv1_wgrad_x3, dim3(uint32_t(G1)), dim3(x3::NTB), 0, stream, obs, idx, ctr, period, B,
                      x3::CPair{static_cast<const unsigned short*>(dpre1.hi), static_cast<const unsigned short*>(dpre1.lo)},

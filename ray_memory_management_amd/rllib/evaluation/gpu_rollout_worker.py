@@ -564,6 +564,9 @@ class HybridRolloutWorker(GPURolloutWorker):
                 spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
                 self._completed.extend(require_hip().hybrid_rollout_direct(**direct, T=T, threads=max(1, th),
                                                                           spin=spin))
+                if "gate_err" in direct and int(self._gate_err.item()):
+                    self._gate_err.zero_()  # a gated step gave up waiting: it ran on stale frames
+                    raise RuntimeError("rollout step gate timed out during this fragment; fragment discarded")
             elif server is not None:  # K21: the whole fragment in ONE persistent kernel launch
                 from ray_memory_management_amd._native import require_hip
 
@@ -670,6 +673,21 @@ class HybridRolloutWorker(GPURolloutWorker):
                 self._h_seq_dev = int(require_hip().host_device_pointer(self._h_seq.data_ptr()))
             if self._h_seq_dev:
                 out.update(host_seq=self._h_seq.data_ptr(), host_seq_dev=self._h_seq_dev)
+        if k.get("x3") and os.environ.get("RMM_ROLLOUT_DIRECT_GATE", "1") != "0":
+            # in-kernel step gate (fp32 policy): step t+1 is launched before step t's env step and K10x
+            # waits for the host's release counter before reading the new frames, so the three launches
+            # leave the step's critical path
+            if getattr(self, "_h_rel", None) is None:
+                import torch
+
+                from ray_memory_management_amd._native import require_hip
+
+                self._h_rel = torch.zeros(1, dtype=torch.int64).pin_memory()
+                self._h_rel_dev = int(require_hip().host_device_pointer(self._h_rel.data_ptr()))
+                self._gate_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+            if self._h_rel_dev:
+                out.update(release=self._h_rel.data_ptr(), release_dev=self._h_rel_dev,
+                           gate_err=self._gate_err.data_ptr())
         return out
 
     def _kernel_args(self, G, S):
