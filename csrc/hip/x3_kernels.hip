@@ -29,7 +29,6 @@
 #include "x3_device.h"
 
 #include <algorithm>
-#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -1156,7 +1155,8 @@ __device__ __forceinline__ uint4 keep_if(bool ok, uint4 v) {
 }
 constexpr int IMG = MC * DMP;                      // one plane of a 64-row [m][h] chunk image
 constexpr int K12X_COLS = 2 * IMG + 2 * 2 * MC * 16 + 2 * 2 * H * 16;
-constexpr int K12X_HEAD = 4 * IMG + 2 * MC * 16;
+constexpr int HQ = 64, HQP = HQ + 16;              // head role: h-columns per workgroup, image pitch
+constexpr int K12X_HEAD = 4 * MC * HQP + 2 * MC * 16;
 constexpr int K12X_LDS = K12X_COLS > K12X_HEAD ? K12X_COLS : K12X_HEAD;
 static_assert(K12X_LDS * 2 <= 160 * 1024, "K12x LDS");
 
@@ -1168,36 +1168,38 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int q = r >> 2, p = r & 3;
   const int NC = int((M + MC - 1) / MC);
-  uint4 sdh[4], sdl[4], sxh, sxl;
-  auto load = [&](int c) {
+  // two register stages: chunk c + 2's loads are issued while chunk c computes. Loads are unconditional
+  // from clamped rows, masked at the LDS store, so the compiler's vmcnt counting never drains a stage
+  uint4 sdh[2][4], sdl[2][4], sxh[2], sxl[2];
+  auto load = [&](int st, int c) {
     const int64_t m0 = int64_t(c) * MC;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int v = tid + NT * k, row = v >> 5, pc = v & 31;
       const int64_t o = min(m0 + row, M - 1) * H + 8 * pc;
-      sdh[k] = *reinterpret_cast<const uint4*>(&dpre.hi[o]);
-      sdl[k] = *reinterpret_cast<const uint4*>(&dpre.lo[o]);
+      sdh[st][k] = *reinterpret_cast<const uint4*>(&dpre.hi[o]);
+      sdl[st][k] = *reinterpret_cast<const uint4*>(&dpre.lo[o]);
     }
     const int row = (tid >> 2) & (MC - 1), pc = tid & 3;
     const int64_t o = min(m0 + row, M - 1) * K + J0 + 8 * pc;
-    sxh = *reinterpret_cast<const uint4*>(&x.hi[o]);
-    sxl = *reinterpret_cast<const uint4*>(&x.lo[o]);
+    sxh[st] = *reinterpret_cast<const uint4*>(&x.hi[o]);
+    sxl[st] = *reinterpret_cast<const uint4*>(&x.lo[o]);
   };
-  auto store = [&](int c) {
+  auto store = [&](int st, int c) {
     const int64_t m0 = int64_t(c) * MC;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int v = tid + NT * k, row = v >> 5, pc = v & 31;
       const bool ok = m0 + row < M;
-      *reinterpret_cast<uint4*>(&dm[row * DMP + 8 * pc]) = keep_if(ok, sdh[k]);
-      *reinterpret_cast<uint4*>(&dm[IMG + row * DMP + 8 * pc]) = keep_if(ok, sdl[k]);
+      *reinterpret_cast<uint4*>(&dm[row * DMP + 8 * pc]) = keep_if(ok, sdh[st][k]);
+      *reinterpret_cast<uint4*>(&dm[IMG + row * DMP + 8 * pc]) = keep_if(ok, sdl[st][k]);
     }
     if (tid < MC * 4) {
       const int row = tid >> 2, pc = tid & 3;
       const bool ok = m0 + row < M;
       const int o = ((pc >> 1) * MC + row) * 16 + 8 * (pc & 1);
-      *reinterpret_cast<uint4*>(&xs[o]) = keep_if(ok, sxh);
-      *reinterpret_cast<uint4*>(&xs[2 * MC * 16 + o]) = keep_if(ok, sxl);
+      *reinterpret_cast<uint4*>(&xs[o]) = keep_if(ok, sxh[st]);
+      *reinterpret_cast<uint4*>(&xs[2 * MC * 16 + o]) = keep_if(ok, sxl[st]);
     }
   };
   {  // W[:, J] -> ws planes, then the Wᵀ fragments into registers
@@ -1208,7 +1210,8 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
       wvh[k] = *reinterpret_cast<const uint4*>(&w.hi[int64_t(h) * K + J0 + 8 * pc]);
       wvl[k] = *reinterpret_cast<const uint4*>(&w.lo[int64_t(h) * K + J0 + 8 * pc]);
     }
-    load(0);
+    load(0, 0);
+    load(1, min(1, NC - 1));
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int v = tid + NT * k, h = v >> 2, pc = v & 3;
@@ -1219,26 +1222,25 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
   }
   __syncthreads();
   const int mt = wave >> 1, nt = wave & 1;
-  bf16x8 wfh[H / 32], wfl[H / 32];
-#pragma unroll
-  for (int s = 0; s < H / 32; s++) {
-    const unsigned short* p0 = &ws[(nt * H + 32 * s + 8 * g + q) * 16 + 4 * p];
-    wfh[s] = tr8(p0, p0 + 4 * 16);
-    wfl[s] = tr8(p0 + 2 * H * 16, p0 + 2 * H * 16 + 4 * 16);
-  }
+  // Wᵀ fragments are re-read from the resident ws planes per chunk: holding them in registers (64 VGPRs)
+  // with two load stages in flight spilled
   Acc adw[2][2];
 #pragma unroll
   for (int i = 0; i < 2; i++) adw[i][0] = adw[i][1] = acc0();
 
-  for (int c = 0; c < NC; c++) {
-    store(c);
+  auto chunk = [&](int st, int c) {
+    store(st, c);
     __syncthreads();
-    if (c + 1 < NC) load(c + 1);  // in flight during this chunk's MFMAs
+    load(st, min(c + 2, NC - 1));  // in flight during this and the next chunk's MFMAs
     {  // dxᵀ tile: D[j][m] = Σ_h Wᵀ[j][h] dpre[m][h]
       Acc a = acc0();
       const int ro = (16 * mt + r) * DMP + 8 * g;
 #pragma unroll
-      for (int s = 0; s < H / 32; s++) mma3(a, wfh[s], wfl[s], ld8(&dm[ro + 32 * s]), ld8(&dm[IMG + ro + 32 * s]));
+      for (int s = 0; s < H / 32; s++) {
+        const unsigned short* p0 = &ws[(nt * H + 32 * s + 8 * g + q) * 16 + 4 * p];
+        mma3(a, tr8(p0, p0 + 4 * 16), tr8(p0 + 2 * H * 16, p0 + 2 * H * 16 + 4 * 16), ld8(&dm[ro + 32 * s]),
+             ld8(&dm[IMG + ro + 32 * s]));
+      }
       const int64_t row = int64_t(c) * MC + 16 * mt + r;
       if (row < M) {
         const f32x4 t = total(a);
@@ -1265,6 +1267,10 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
       }
     }
     __syncthreads();  // chunk images free
+  };
+  for (int c = 0; c < NC; c += 2) {  // pairs of chunks; an odd NC runs one all-zero chunk past the end
+    chunk(0, c);
+    chunk(1, c + 1);
   }
 #pragma unroll
   for (int hi = 0; hi < 2; hi++)
@@ -1276,100 +1282,106 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
     }
 }
 
+// Head role, one workgroup per 64 h-columns (H / HQ of them; one workgroup for all 256 streamed 1 MB
+// through one CU, ~21 us): dWh[:, Hq], db[Hq] and (hq = 0) dbh over all rows. Wave w takes h-tile w & 3
+// of the 64-row chunk's 32-row half w >> 2; the halves are summed through LDS at the end.
 template <int A1>
 __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t M, float* __restrict__ db,
-                                          float* __restrict__ dwh, float* __restrict__ dbh, unsigned short* lds) {
-  unsigned short* dm = lds;              // [plane][m][DMP]
-  unsigned short* ys = lds + 2 * IMG;    // [plane][m][DMP]
-  unsigned short* zs = lds + 4 * IMG;    // [plane][m][16] (a >= A1 and rows >= M zero)
+                                          float* __restrict__ dwh, float* __restrict__ dbh, unsigned short* lds,
+                                          int hq) {
+  unsigned short* dm = lds;                  // [plane][m][HQP]
+  unsigned short* ys = lds + 2 * MC * HQP;   // [plane][m][HQP]
+  unsigned short* zs = lds + 4 * MC * HQP;   // [plane][m][16] (a >= A1 and rows >= M zero)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-  const int q = r >> 2, p = r & 3;
+  const int q = r >> 2, p = r & 3, ht = wave & 3, ks = wave >> 2;
   const int NC = int((M + MC - 1) / MC);
-  uint4 sdh[4], sdl[4], syh[4], syl[4];
-  unsigned short zh[2], zl[2];
-  auto load = [&](int c) {
-    const int64_t m0 = int64_t(c) * MC;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
-      const int64_t o = min(m0 + row, M - 1) * H + 8 * pc;
-      sdh[k] = *reinterpret_cast<const uint4*>(&dpre.hi[o]);
-      sdl[k] = *reinterpret_cast<const uint4*>(&dpre.lo[o]);
-      syh[k] = *reinterpret_cast<const uint4*>(&y.hi[o]);
-      syl[k] = *reinterpret_cast<const uint4*>(&y.lo[o]);
-    }
+  const int64_t h0 = int64_t(hq) * HQ;
+  // 64 rows x 64 h x 4 planes = 32 KB per chunk: one uint4 per plane per thread; two stages
+  uint4 sd[2][2], sy[2][2];
+  unsigned short zh[2][2], zl[2][2];
+  const int lrow = tid >> 3, lpc = tid & 7;
+  auto load = [&](int st, int c) {
+    const int64_t o = min(int64_t(c) * MC + lrow, M - 1) * H + h0 + 8 * lpc;
+    sd[st][0] = *reinterpret_cast<const uint4*>(&dpre.hi[o]);
+    sd[st][1] = *reinterpret_cast<const uint4*>(&dpre.lo[o]);
+    sy[st][0] = *reinterpret_cast<const uint4*>(&y.hi[o]);
+    sy[st][1] = *reinterpret_cast<const uint4*>(&y.lo[o]);
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int e = tid + NT * k, m = e >> 4, a = e & 15;
-      const int64_t o = min(m0 + m, M - 1) * A1 + min(a, A1 - 1);
-      zh[k] = dz.hi[o];
-      zl[k] = dz.lo[o];
+      const int64_t oz = min(int64_t(c) * MC + m, M - 1) * A1 + min(a, A1 - 1);
+      zh[st][k] = dz.hi[oz];
+      zl[st][k] = dz.lo[oz];
     }
   };
-  auto store = [&](int c) {
+  auto store = [&](int st, int c) {
     const int64_t m0 = int64_t(c) * MC;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int v = tid + NT * k, row = v >> 5, pc = v & 31;
-      const bool ok = m0 + row < M;
-      const int o = row * DMP + 8 * pc;
-      *reinterpret_cast<uint4*>(&dm[o]) = keep_if(ok, sdh[k]);
-      *reinterpret_cast<uint4*>(&dm[IMG + o]) = keep_if(ok, sdl[k]);
-      *reinterpret_cast<uint4*>(&ys[o]) = keep_if(ok, syh[k]);
-      *reinterpret_cast<uint4*>(&ys[IMG + o]) = keep_if(ok, syl[k]);
-    }
+    const bool ok = m0 + lrow < M;
+    const int o = lrow * HQP + 8 * lpc;
+    *reinterpret_cast<uint4*>(&dm[o]) = keep_if(ok, sd[st][0]);
+    *reinterpret_cast<uint4*>(&dm[MC * HQP + o]) = keep_if(ok, sd[st][1]);
+    *reinterpret_cast<uint4*>(&ys[o]) = keep_if(ok, sy[st][0]);
+    *reinterpret_cast<uint4*>(&ys[MC * HQP + o]) = keep_if(ok, sy[st][1]);
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int e = tid + NT * k, m = e >> 4, a = e & 15;
-      const bool ok = m0 + m < M && a < A1;
-      zs[e] = ok ? zh[k] : static_cast<unsigned short>(0);
-      zs[MC * 16 + e] = ok ? zl[k] : static_cast<unsigned short>(0);
+      const bool okz = m0 + m < M && a < A1;
+      zs[e] = okz ? zh[st][k] : static_cast<unsigned short>(0);
+      zs[MC * 16 + e] = okz ? zl[st][k] : static_cast<unsigned short>(0);
     }
   };
   u16x8 onev;
 #pragma unroll
   for (int j = 0; j < 8; j++) onev[j] = (r == 0) ? static_cast<unsigned short>(0x3f80) : static_cast<unsigned short>(0);
   const bf16x8 ones = as_bf(onev);  // as A: row 0 all ones; as B: column 0 all ones
-  Acc awh[2], adb[2], abh = acc0();
-  awh[0] = awh[1] = adb[0] = adb[1] = acc0();
-  load(0);
-  for (int c = 0; c < NC; c++) {
-    store(c);
+  const bool want_bh = hq == 0 && ht == 0;
+  Acc awh = acc0(), adb = acc0(), abh = acc0();
+  load(0, 0);
+  load(1, min(1, NC - 1));
+  auto chunk = [&](int st, int c) {
+    store(st, c);
     __syncthreads();
-    if (c + 1 < NC) load(c + 1);
-#pragma unroll
-    for (int ks = 0; ks < MC / 32; ks++) {
-      const unsigned short* pz = &zs[(32 * ks + 4 * g + q) * 16 + 4 * p];
-      const bf16x8 azh = tr8(pz, pz + 16 * 16), azl = tr8(pz + MC * 16, pz + MC * 16 + 16 * 16);
-#pragma unroll
-      for (int hi = 0; hi < 2; hi++) {
-        const int off = (32 * ks + 4 * g + q) * DMP + 16 * (wave + 8 * hi) + 4 * p;
-        const bf16x8 byh = tr8(&ys[off], &ys[off + 16 * DMP]), byl = tr8(&ys[IMG + off], &ys[IMG + off + 16 * DMP]);
-        const bf16x8 bdh = tr8(&dm[off], &dm[off + 16 * DMP]), bdl = tr8(&dm[IMG + off], &dm[IMG + off + 16 * DMP]);
-        mma3(awh[hi], azh, azl, byh, byl);
-        mma2a(adb[hi], ones, bdh, bdl);
-      }
-      if (wave == 0) {  // dbh: dzᵀ times a ones column (B exact)
-        abh.x = mfma(azl, ones, abh.x);
-        abh.hh = mfma(azh, ones, abh.hh);
-      }
+    load(st, min(c + 2, NC - 1));
+    const unsigned short* pz = &zs[(32 * ks + 4 * g + q) * 16 + 4 * p];
+    const bf16x8 azh = tr8(pz, pz + 16 * 16), azl = tr8(pz + MC * 16, pz + MC * 16 + 16 * 16);
+    const int off = (32 * ks + 4 * g + q) * HQP + 16 * ht + 4 * p;
+    const bf16x8 byh = tr8(&ys[off], &ys[off + 16 * HQP]), byl = tr8(&ys[MC * HQP + off], &ys[MC * HQP + off + 16 * HQP]);
+    const bf16x8 bdh = tr8(&dm[off], &dm[off + 16 * HQP]), bdl = tr8(&dm[MC * HQP + off], &dm[MC * HQP + off + 16 * HQP]);
+    mma3(awh, azh, azl, byh, byl);
+    mma2a(adb, ones, bdh, bdl);
+    if (want_bh) {  // dbh: dzᵀ times a ones column (B exact)
+      abh.x = mfma(azl, ones, abh.x);
+      abh.hh = mfma(azh, ones, abh.hh);
     }
     __syncthreads();
+  };
+  for (int c = 0; c < NC; c += 2) {  // an odd NC runs one all-zero chunk past the end
+    chunk(0, c);
+    chunk(1, c + 1);
   }
+  // sum the two row halves: waves 4..7 park their totals in LDS (the images are free after the last barrier)
+  float* red = reinterpret_cast<float*>(lds);
+  f32x4 tw = total(awh), tb = total(adb), tbh = total(abh);
+  if (ks == 1) {
+    float* o = red + (ht * 64 + lane) * 12;
 #pragma unroll
-  for (int hi = 0; hi < 2; hi++) {
-    const int h = 16 * (wave + 8 * hi) + r;
-    const f32x4 tw = total(awh[hi]), tb = total(adb[hi]);
+    for (int i = 0; i < 4; i++) o[i] = tw[i], o[4 + i] = tb[i], o[8 + i] = tbh[i];
+  }
+  __syncthreads();
+  if (ks == 0) {
+    const float* o = red + (ht * 64 + lane) * 12;
+#pragma unroll
+    for (int i = 0; i < 4; i++) tw[i] += o[i], tb[i] += o[4 + i], tbh[i] += o[8 + i];
+    const int64_t h = h0 + 16 * ht + r;
 #pragma unroll
     for (int i = 0; i < 4; i++)
       if (4 * g + i < A1) dwh[(4 * g + i) * H + h] = tw[i];
     if (g == 0) db[h] = tb[0];
-  }
-  if (wave == 0 && r == 0) {
-    const f32x4 tb = total(abh);
+    if (want_bh && r == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (4 * g + i < A1) dbh[4 * g + i] = tb[i];
+      for (int i = 0; i < 4; i++)
+        if (4 * g + i < A1) dbh[4 * g + i] = tbh[i];
+    }
   }
 }
 
@@ -1379,10 +1391,15 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd_x3(CPair dz, CPair y, CP
                                                            float* __restrict__ db, float* __restrict__ dwh,
                                                            float* __restrict__ dbh) {
   __shared__ __attribute__((aligned(16))) unsigned short lds[K12X_LDS];
-  if (int64_t(blockIdx.x) * JB == K)
-    k12x_head<A1>(dz, y, dpre, M, db, dwh, dbh, lds);
+  // grid: K / JB column workgroups, then H / HQ head workgroups. (A row split of the columns, dW partials
+  // merged in-launch, measured slower: the agent-scope release / acquire of the merge writes back and
+  // invalidates the XCD's L2 under every other workgroup still streaming dpre, 21.8 -> 34.7 us at M = 500,
+  // profiles/x3_kernels_r5.txt)
+  const int NJ = int(K / JB), b = blockIdx.x;
+  if (b >= NJ)
+    k12x_head<A1>(dz, y, dpre, M, db, dwh, dbh, lds, b - NJ);
   else
-    k12x_cols(x, w, dpre, M, K, int64_t(blockIdx.x) * JB, dx, dw, lds);
+    k12x_cols(x, w, dpre, M, K, int64_t(b) * JB, dx, dw, lds);
 }
 
 }  // namespace x3
@@ -1507,7 +1524,7 @@ void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int6
   for (const X3In* p : {&dz, &y, &x, &w, &dpre})
     if (!p->hi || !p->lo) throw std::invalid_argument("x3_dense_heads_bwd: inputs need hi and lo planes");
   if (!dx.hi || !dx.lo || !dw || !db || !dwh || !dbh) throw std::invalid_argument("x3_dense_heads_bwd: outputs");
-  const dim3 grid(uint32_t(K / x3::JB + 1)), block(x3::NT);
+  const dim3 grid(uint32_t(K / x3::JB + x3::H / x3::HQ)), block(x3::NT);
 #define RMM_K12X(N)                                                                                                 \
   case N:                                                                                                           \
     hipLaunchKernelGGL(x3::k_dense_heads_bwd_x3<N>, grid, block, 0, stream, cp(dz), cp(y), cp(x), cp(w), cp(dpre), M, \

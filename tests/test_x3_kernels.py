@@ -130,10 +130,10 @@ def _ppo_ref(heads, cols, coef, A):
     return per.mean(), stats
 
 
-@pytest.mark.parametrize("M,K,A", [(500, 3872, 4), (37, 96, 6), (130, 64, 15), (640, 3872, 2)])
+@pytest.mark.parametrize("M,K,A", [(500, 3872, 4), (37, 96, 6), (130, 64, 15), (640, 3872, 2), (200, 96, 5)])
 def test_x3_dense_heads_ppo_chain_matches_fp64(cuda, M, K, A):
     """K13x -> K15x (hidden, heads, PPO loss stats, dheads, dpre) -> K12x (dx, dW, db, dWh, dbh) vs
-    float64 autograd of the same PPO loss of heads(ReLU(x Wᵀ + b))."""
+    float64 autograd of the same PPO loss of heads(ReLU(x Wᵀ + b)); K12x launched twice, bit-identical."""
     from ray_memory_management_amd._native import require_hip
     from ray_memory_management_amd.ops import x3
 
@@ -162,9 +162,14 @@ def test_x3_dense_heads_ppo_chain_matches_fp64(cuda, M, K, A):
     dx = x3.Pair.empty((M, K), cuda)
     dW, db = torch.empty(256, K, device=cuda), torch.empty(256, device=cuda)
     dWh, dbh = torch.empty(A1, 256, device=cuda), torch.empty(A1, device=cuda)
-    h.x3_dense_heads_bwd(dz.ptrs(), A1, hid.ptrs(), x.ptrs(), W.ptrs(), dpre.ptrs(), M, K, dx.ptrs(), dW.data_ptr(),
-                         db.data_ptr(), dWh.data_ptr(), dbh.data_ptr(), s)
-    torch.cuda.synchronize()
+    outs = []
+    for _ in range(2):
+        h.x3_dense_heads_bwd(dz.ptrs(), A1, hid.ptrs(), x.ptrs(), W.ptrs(), dpre.ptrs(), M, K, dx.ptrs(),
+                             dW.data_ptr(), db.data_ptr(), dWh.data_ptr(), dbh.data_ptr(), s)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (dx.hi, dx.lo, dW, db, dWh, dbh)])
+    for first, second in zip(*outs):
+        assert torch.equal(first, second)
     xr = x.float().double().requires_grad_(True)
     ps = [t.float().double().requires_grad_(True) for t in (W, b, Wh, bh)]
     mask = (hid.float() > 0).double()
