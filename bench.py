@@ -239,6 +239,8 @@ def _runtime(args, n_gpus):
                 "cpu_budget": budget, "learners": algo.learner_group.device_info()}
         for _ in range(args.warmup):
             algo.train()
+        if n_l > 1:  # communicator, peer mode and whether the optimizer step is the ZeRO-1 launch
+            info["learner_comm"] = ray.get([a.comm_info.remote() for a in algo.learner_group.learners])
         dev = bool(getattr(algo, "_device_weights_ok", lambda: False)())
         info["weights_sync"] = ("shared-hbm" if dev and algo._shared_weights_ok() else "hbm-object" if dev
                                 else "host")

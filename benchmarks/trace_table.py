@@ -24,6 +24,7 @@ def main():
             k = r["Kernel_Name"]
             if a.match and a.match not in k:
                 continue
+            k = k.replace("(anonymous namespace)::", "")
             key = (k.split("(")[0].replace("rmm::hip::", "")[:56], r["Grid_Size_X"], r["Workgroup_Size_X"],
                    r["LDS_Block_Size"], r["VGPR_Count"])
             rows[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)

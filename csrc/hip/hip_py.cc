@@ -879,6 +879,23 @@ PYBIND11_MODULE(_hip, m) {
       })
       .def("all_reduce", &PeerAllReduce::AllReduce, py::arg("buf"), py::arg("count"), py::arg("dtype"),
            py::arg("stream"), py::arg("algo") = 0)
+      .def("all_reduce_adam",
+           [](PeerAllReduce& c, uint64_t grad, uint64_t count, int dtype, uint64_t stream, uint64_t master, uint64_t m1,
+              uint64_t m2, uint64_t whi, uint64_t wlo, uint64_t hp, float grad_scale, uint64_t step_ctr, uint64_t bump,
+              int nbump, uint64_t done, uint64_t bump_next) {
+             PeerAllReduce::AdamArgs z{P<float>(master), P<float>(m1), P<float>(m2), reinterpret_cast<void*>(whi),
+                                       reinterpret_cast<void*>(wlo), P<const float>(hp), grad_scale,
+                                       step_ctr ? P<const int64_t>(step_ctr) : nullptr,
+                                       bump ? P<int64_t>(bump) : nullptr, nbump,
+                                       done ? P<uint32_t>(done) : nullptr, bump_next ? P<int64_t>(bump_next) : nullptr};
+             c.AllReduceAdam(grad, count, dtype, stream, z);
+           },
+           py::arg("grad"), py::arg("count"), py::arg("dtype"), py::arg("stream"), py::arg("master"), py::arg("m1"),
+           py::arg("m2"), py::arg("whi"), py::arg("wlo") = 0, py::arg("hp") = 0, py::arg("grad_scale") = 1.0f,
+           py::arg("step_ctr") = 0, py::arg("bump") = 0, py::arg("nbump") = 0, py::arg("done") = 0,
+           py::arg("bump_next") = 0)
+      .def("mask_unowned", &PeerAllReduce::MaskUnowned, py::arg("buf"), py::arg("count"), py::arg("dtype"),
+           py::arg("stream"))
       .def("error", &PeerAllReduce::Error)
       .def("clear_error", &PeerAllReduce::ClearError)
       .def("set_timeout", &PeerAllReduce::set_timeout)

@@ -31,6 +31,30 @@ class PeerAllReduce {
   // in-place sum of `count` elements (dtype 0 = bf16, 1 = fp32) on `stream`; legal inside capture.
   // algo: 0 = auto, 1 = one-shot, 2 = two-shot
   void AllReduce(uint64_t buf, uint64_t count, int dtype, uint64_t stream, int algo);
+  // ZeRO-1 step in ONE launch per `cap / 4` elements: reduce-scatter the gradient (dtype 0 = bf16, 1 =
+  // fp32; fp32 sum in rank order, bf16 gradients rounded once as AllReduce does), K6's Adam on the
+  // chunk this rank owns (master / m1 / m2 and the bf16 weight planes), all-gather of the updated fp32
+  // masters; every rank re-derives the weight planes from the gathered masters with the owner's
+  // rounding, so weights and masters are bit-identical everywhere; m1 / m2 are current on the owner
+  // only (MaskUnowned + AllReduce replicates them). Counters as adam_flat: the step from step_ctr,
+  // `bump` advanced by the last launch (ticket `done`, or parity `bump_next`); bump = null: no advance.
+  struct AdamArgs {
+    float* master;
+    float* m1;
+    float* m2;
+    void* whi;  // bf16 weights (hi plane)
+    void* wlo;  // optional split-pair lo plane
+    const float* hp;
+    float grad_scale;
+    const int64_t* step_ctr;
+    int64_t* bump;
+    int nbump;
+    uint32_t* done;
+    int64_t* bump_next;
+  };
+  void AllReduceAdam(uint64_t grad, uint64_t count, int dtype, uint64_t stream, const AdamArgs& z);
+  // zero the fp32 `buf[0, count)` elements this rank does NOT own under AllReduceAdam(count, dtype)
+  void MaskUnowned(uint64_t buf, uint64_t count, int dtype, uint64_t stream);
   // 0 = healthy; otherwise 1 + the rank whose flag timed out (+ block in the upper bits)
   int64_t Error() const;
   void ClearError();

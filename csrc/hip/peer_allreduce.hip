@@ -33,6 +33,8 @@
 #include "peer_allreduce.h"
 
 #include <cstring>
+
+#include "adam_device.h"
 #include <stdexcept>
 #include <vector>
 
@@ -241,6 +243,189 @@ __global__ void __launch_bounds__(kThreads) k_peer_allreduce(PeerArgs a, void* b
   if (tid == 0) a.epochs[b] = e;
 }
 
+// ---------------------------------------------------------------- ZeRO-1: reduce-scatter + Adam + all-gather
+// The partition is AllReduce's two-shot one: workgroup b owns a 128-B-line slice of the staged
+// gradient vectors, rank r chunk r of it. Red regions hold fp32 masters (4 B per element, so a launch
+// covers at most cap / 4 elements whatever the gradient dtype).
+struct Part {
+  int64_t c0, c1;  // this rank's chunk, in gradient vectors
+  int64_t lo, hi, su, cu;
+};
+template <int N>
+__device__ __forceinline__ Part zero1_part(int64_t n, int nblocks, int b, int rank, int world) {
+  Part p;
+  const int64_t nv = (n + N - 1) / N;
+  const int64_t nu = (nv + kUnitVecs - 1) / kUnitVecs;
+  const int64_t ub = (nu + nblocks - 1) / nblocks;
+  const int64_t u0 = min(nu, int64_t(b) * ub), u1 = min(nu, u0 + ub);
+  p.lo = u0 * kUnitVecs;
+  p.hi = min(nv, u1 * kUnitVecs);
+  p.su = u1 - u0;
+  p.cu = (p.su + world - 1) / world;
+  p.c0 = p.lo + min(p.su, int64_t(rank) * p.cu) * kUnitVecs;
+  p.c1 = min(p.hi, p.lo + min(p.su, int64_t(rank + 1) * p.cu) * kUnitVecs);
+  return p;
+}
+
+struct Zero1Dev {
+  float* master;
+  float* m1;
+  float* m2;
+  __hip_bfloat16* whi;
+  __hip_bfloat16* wlo;
+  const float* hp;
+  float grad_scale;
+  const int64_t* step_ctr;
+  int64_t* bump;
+  int nbump;
+  uint32_t* done;
+  int64_t* bump_next;
+};
+
+// the weight planes of element e from its fp32 master (adam_span's rounding: hi = RNE(w), lo = RNE(w - hi))
+__device__ __forceinline__ void zero1_planes4(const Zero1Dev& z, int64_t e, const float4& w) {
+  *reinterpret_cast<uint2*>(z.whi + e) = make_uint2(bf16x2_rn(w.x, w.y), bf16x2_rn(w.z, w.w));
+  if (z.wlo) *reinterpret_cast<uint2*>(z.wlo + e) = make_uint2(bf16x2_lo(w.x, w.y), bf16x2_lo(w.z, w.w));
+}
+__device__ __forceinline__ void zero1_planes1(const Zero1Dev& z, int64_t e, float w) {
+  z.whi[e] = __float2bfloat16(w);
+  if (z.wlo) z.wlo[e] = __float2bfloat16(w - __bfloat162float(__float2bfloat16(w)));
+}
+
+// <= 128 VGPRs (two workgroups per CU): the peers' same-index workgroups must be able to run at once,
+// and ranks sharing a GPU (or a concurrent kernel) compete for the same slots
+constexpr int kZThreads = 512, kZU = 4;  // kZU vectors in flight per lane in the copy loops
+template <bool BF16>
+__global__ void __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(4)))
+k_peer_zero1(PeerArgs a, const void* grad, int64_t n, Zero1Dev z) {
+  __shared__ uint64_t s_epoch;
+  __shared__ int s_dead;
+  constexpr int N = V<BF16>::N;
+  const int tid = threadIdx.x, b = blockIdx.x;
+  if (tid == 0) {
+    s_epoch = a.epochs[b] + 1;
+    s_dead = __hip_atomic_load(a.err_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  }
+  const AdamCoef c = adam_coef(z.hp, z.step_ctr);  // every workgroup reads the step before any bump
+  int64_t* bump = z.bump;
+  if (z.bump_next) {  // parity counters (k_adam_flat): one lane writes the next copy, no ticket
+    if (b == 0 && tid == 0)
+      for (int k = 0; k < z.nbump; k++) z.bump_next[k] = z.bump[k] + 1;
+    bump = nullptr;
+  }
+  const Part p = zero1_part<N>(n, a.nblocks, b, a.rank, a.world);
+  __syncthreads();
+  if (!s_dead) {
+    const uint64_t e = s_epoch, par = e & 1ull;
+    uint4* mine = reinterpret_cast<uint4*>(const_cast<char*>(a.data[a.rank]) + par * a.cap);
+    for (int64_t v0 = p.lo + tid; v0 < p.hi; v0 += kZThreads * kZU) {  // loads first: kZU in flight
+      uint4 t[kZU];
+#pragma unroll
+      for (int u = 0; u < kZU; u++)
+        if (v0 + u * kZThreads < p.hi) t[u] = load_user<BF16>(grad, v0 + u * kZThreads, n);
+#pragma unroll
+      for (int u = 0; u < kZU; u++)
+        if (v0 + u * kZThreads < p.hi) mine[v0 + u * kZThreads] = t[u];
+    }
+    bool ok = a.world == 1 || block_barrier(a, 0, e);
+    if (ok) {
+      float* red = reinterpret_cast<float*>(const_cast<char*>(a.data[a.rank]) + (2 + par) * a.cap);
+      for (int64_t v = p.c0 + tid; v < p.c1; v += kZThreads) {
+        uint4 x[kPeerMaxRanks];
+#pragma unroll
+        for (int r = 0; r < kPeerMaxRanks; r++)
+          if (r < a.world) x[r] = reinterpret_cast<const uint4*>(a.data[r] + par * a.cap)[v];
+        float acc[N], f[N];
+        V<BF16>::unpack(x[0], acc);
+#pragma unroll
+        for (int r = 1; r < kPeerMaxRanks; r++) {
+          if (r < a.world) {
+            V<BF16>::unpack(x[r], f);
+#pragma unroll
+            for (int i = 0; i < N; i++) acc[i] += f[i];
+          }
+        }
+        if constexpr (BF16) V<BF16>::unpack(V<BF16>::pack(acc), acc);  // the all-reduce's single rounding
+#pragma unroll
+        for (int q = 0; q < N / 4; q++) {
+          const int64_t e0 = v * N + 4 * q;
+          if (e0 + 4 <= n) {
+            float4 w = *reinterpret_cast<const float4*>(z.master + e0);
+            float4 m = *reinterpret_cast<const float4*>(z.m1 + e0);
+            float4 s2 = *reinterpret_cast<const float4*>(z.m2 + e0);
+            w.x = adam_one(w.x, acc[4 * q] * z.grad_scale, m.x, s2.x, c);
+            w.y = adam_one(w.y, acc[4 * q + 1] * z.grad_scale, m.y, s2.y, c);
+            w.z = adam_one(w.z, acc[4 * q + 2] * z.grad_scale, m.z, s2.z, c);
+            w.w = adam_one(w.w, acc[4 * q + 3] * z.grad_scale, m.w, s2.w, c);
+            *reinterpret_cast<float4*>(z.master + e0) = w;
+            *reinterpret_cast<float4*>(z.m1 + e0) = m;
+            *reinterpret_cast<float4*>(z.m2 + e0) = s2;
+            *reinterpret_cast<float4*>(red + e0) = w;
+            zero1_planes4(z, e0, w);
+          } else {
+            for (int i = 0; i < 4; i++) {
+              const int64_t ei = e0 + i;
+              if (ei < n) {
+                float m = z.m1[ei], s2 = z.m2[ei];
+                const float w = adam_one(z.master[ei], acc[4 * q + i] * z.grad_scale, m, s2, c);
+                z.master[ei] = w;
+                z.m1[ei] = m;
+                z.m2[ei] = s2;
+                red[ei] = w;
+                zero1_planes1(z, ei, w);
+              }
+            }
+          }
+        }
+      }
+      ok = a.world == 1 || block_barrier(a, 1, e);
+      if (ok) {  // all-gather the other chunks' fp32 masters; the planes follow with the same rounding
+        for (int cc = 0; cc < a.world; cc++) {
+          if (cc == a.rank) continue;
+          const int64_t g0 = p.lo + min(p.su, int64_t(cc) * p.cu) * kUnitVecs;
+          const int64_t g1 = min(p.hi, p.lo + min(p.su, int64_t(cc + 1) * p.cu) * kUnitVecs);
+          const float* src = reinterpret_cast<const float*>(a.data[cc] + (2 + par) * a.cap);
+          // groups of 4 masters; whole groups (all but possibly the last) kZU at a time, loads first
+          const int64_t q0 = g0 * (N / 4), q1 = min(g1 * (N / 4), n / 4);
+          for (int64_t j0 = q0 + tid; j0 < q1; j0 += kZThreads * kZU) {
+            float4 w[kZU];
+#pragma unroll
+            for (int u = 0; u < kZU; u++)
+              if (j0 + u * kZThreads < q1) w[u] = *reinterpret_cast<const float4*>(src + 4 * (j0 + u * kZThreads));
+#pragma unroll
+            for (int u = 0; u < kZU; u++)
+              if (j0 + u * kZThreads < q1) {
+                const int64_t e0 = 4 * (j0 + u * kZThreads);
+                *reinterpret_cast<float4*>(z.master + e0) = w[u];
+                zero1_planes4(z, e0, w[u]);
+              }
+          }
+          if (tid == 0)  // n % 4 tail inside this chunk
+            for (int64_t e1 = max(4 * q1, g0 * N); e1 < min(g1 * N, n); e1++) {
+              const float w = src[e1];
+              z.master[e1] = w;
+              zero1_planes1(z, e1, w);
+            }
+        }
+      }
+    }
+    if (tid == 0) a.epochs[b] = e;
+  }
+  last_block_bump(bump, z.nbump, z.done);  // every workgroup, dead or not, so the tickets stay whole
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) k_zero1_mask(float* buf, int64_t n, int nblocks, int rank, int world) {
+  for (int b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const Part p = zero1_part<N>(n, nblocks, b, rank, world);
+    for (int64_t v = p.lo + threadIdx.x; v < p.hi; v += blockDim.x) {
+      if (v >= p.c0 && v < p.c1) continue;
+      for (int i = 0; i < N; i++)
+        if (v * N + i < n) buf[v * N + i] = 0.f;
+    }
+  }
+}
+
 }  // namespace
 
 PeerAllReduce::PeerAllReduce(int rank, int world, int device, uint64_t cap_bytes, int nblocks, double timeout_s)
@@ -380,6 +565,66 @@ void PeerAllReduce::AllReduce(uint64_t buf, uint64_t count, int dtype, uint64_t 
     }
     RMM_HIP_CHECK(hipGetLastError());
     launches_++;
+  }
+}
+
+void PeerAllReduce::AllReduceAdam(uint64_t grad, uint64_t count, int dtype, uint64_t stream, const AdamArgs& z) {
+  if (!open_ && world_ > 1) throw std::runtime_error("PeerAllReduce: Open() the peers first");
+  if (dtype != 0 && dtype != 1) throw std::invalid_argument("AllReduceAdam: dtype 0 (bf16) or 1 (fp32)");
+  if (grad % 16 || reinterpret_cast<uintptr_t>(z.master) % 16 || reinterpret_cast<uintptr_t>(z.m1) % 16 ||
+      reinterpret_cast<uintptr_t>(z.m2) % 16 || reinterpret_cast<uintptr_t>(z.whi) % 8 ||
+      reinterpret_cast<uintptr_t>(z.wlo) % 8)
+    throw std::invalid_argument("AllReduceAdam: 16-B aligned gradient / master / moments, 8-B aligned planes");
+  if (!z.master || !z.m1 || !z.m2 || !z.whi || !z.hp) throw std::invalid_argument("AllReduceAdam: buffers");
+  if (z.bump_next && (!z.bump || z.nbump <= 0)) throw std::invalid_argument("AllReduceAdam: bump_next needs bump");
+  if (z.bump && !z.bump_next && !z.done) throw std::invalid_argument("AllReduceAdam: in-place bump needs done");
+  if (count == 0) return;
+  const uint64_t esz = dtype == 0 ? 2 : 4;
+  const uint64_t per = (cap_ / 4) & ~uint64_t(127);  // the red regions hold fp32 masters
+  PeerArgs a{};
+  for (int r = 0; r < world_; r++) {
+    a.data[r] = peer_data_[r];
+    a.sig[r] = peer_sig_[r];
+  }
+  a.epochs = epochs_;
+  a.err_dev = err_dev_;
+  void* dh = nullptr;
+  RMM_HIP_CHECK(hipHostGetDevicePointer(&dh, err_host_, 0));
+  a.err_host = static_cast<int64_t*>(dh);
+  a.cap = cap_;
+  a.timeout_ticks = timeout_ticks_;
+  a.rank = rank_;
+  a.world = world_;
+  a.nblocks = nblocks_;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (uint64_t off = 0; off < count; off += per) {
+    const uint64_t n = count - off < per ? count - off : per;
+    const bool last = off + per >= count;
+    Zero1Dev d{z.master + off, z.m1 + off, z.m2 + off, static_cast<__hip_bfloat16*>(z.whi) + off,
+               z.wlo ? static_cast<__hip_bfloat16*>(z.wlo) + off : nullptr, z.hp, z.grad_scale, z.step_ctr,
+               last ? z.bump : nullptr, z.nbump, z.done, last ? z.bump_next : nullptr};
+    const void* g = reinterpret_cast<const void*>(grad + off * esz);
+    if (dtype == 0)
+      hipLaunchKernelGGL((k_peer_zero1<true>), dim3(nblocks_), dim3(kZThreads), 0, s, a, g, int64_t(n), d);
+    else
+      hipLaunchKernelGGL((k_peer_zero1<false>), dim3(nblocks_), dim3(kZThreads), 0, s, a, g, int64_t(n), d);
+    RMM_HIP_CHECK(hipGetLastError());
+    launches_++;
+  }
+}
+
+void PeerAllReduce::MaskUnowned(uint64_t buf, uint64_t count, int dtype, uint64_t stream) {
+  if (dtype != 0 && dtype != 1) throw std::invalid_argument("MaskUnowned: dtype 0 (bf16) or 1 (fp32)");
+  const uint64_t per = (cap_ / 4) & ~uint64_t(127);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (uint64_t off = 0; off < count && world_ > 1; off += per) {
+    const uint64_t n = count - off < per ? count - off : per;
+    float* p = reinterpret_cast<float*>(buf) + off;
+    if (dtype == 0)
+      hipLaunchKernelGGL(k_zero1_mask<8>, dim3(64), dim3(256), 0, s, p, int64_t(n), nblocks_, rank_, world_);
+    else
+      hipLaunchKernelGGL(k_zero1_mask<4>, dim3(64), dim3(256), 0, s, p, int64_t(n), nblocks_, rank_, world_);
+    RMM_HIP_CHECK(hipGetLastError());
   }
 }
 

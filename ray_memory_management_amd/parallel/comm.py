@@ -239,6 +239,15 @@ def _store_barrier(store, key: str, world: int, timeout_s: float = 300.0) -> Non
         time.sleep(0.002)
 
 
+class _FlatView:
+    """(pointer, element count) of an fp32 device range handed to the native communicator."""
+
+    def __init__(self, ptr: int, count: int, device):
+        if ptr % 16:
+            raise ValueError("PeerComm: 16-B aligned fp32 ranges only")
+        self.ptr, self.count, self.device = ptr, count, device
+
+
 class PeerComm(Comm):
     """MI355X-native intra-node all-reduce (csrc/hip/peer_allreduce.hip): every rank exports a
     staging region once through hipIPC and maps every peer's; one kernel per all-reduce reads the
@@ -246,16 +255,18 @@ class PeerComm(Comm):
     flag barriers (bounded spins that report a dead peer instead of hanging). No host involvement
     per call, so the collective lives INSIDE the learner's chained SGD graph (``in_graph``).
 
-    bf16 / fp32 sums natively; `broadcast` of a float tensor is an all-reduce against zeros from
-    the other ranks (exact); anything else goes to `fallback` (an RcclComm or a torch group) when
-    one is given. Reference parity: rllib/execution/multi_gpu_learner_thread.py:20 (tower gradient
+    bf16 / fp32 sums natively, plus the ZeRO-1 optimizer step (`allreduce_adam_on`); `broadcast` of
+    a device tensor is an all-reduce against zeros from the other ranks, bit-exact for every dtype
+    (bf16 / fp32 directly, anything else as its raw bytes); host tensors and other ops go to
+    `fallback` (an RcclComm or a torch group) when one is given. Reference parity: rllib/execution/multi_gpu_learner_thread.py:20 (tower gradient
     averaging), rllib/execution/train_ops.py:98."""
 
     graph_capturable = True
     in_graph = True
 
     def __init__(self, store, rank: int, world: int, key: str = "rmm-peer", device=None,
-                 cap_bytes: int = 8 << 20, nblocks: int = 0, timeout_s: float = 0.0, fallback: Optional[Comm] = None):
+                 cap_bytes: int = 8 << 20, nblocks: int = 0, timeout_s: float = 0.0, fallback: Optional[Comm] = None,
+                 zero1_blocks: Optional[int] = None):
         from ray_memory_management_amd._native import require_hip
 
         h = require_hip()
@@ -323,10 +334,48 @@ class PeerComm(Comm):
         if bad:
             self._c.close()
             raise PeerUnavailable(f"peer all-reduce self-test failed on ranks {bad}")
+        # the ZeRO-1 optimizer launch (allreduce_adam_on) runs on its OWN communicator: its Adam pass
+        # over 1/W of the bucket wants many more workgroups than the plain all-reduce's barrier fan-in
+        # does (64 -> 256: the fp32 PPO bucket's step on 64 workgroups was latency-bound), and one
+        # communicator must keep one workgroup count (its staging reuse is argued per workgroup slice)
+        if zero1_blocks is None:
+            env = os.environ.get("RMM_PEER_ZERO1_BLOCKS")
+            # ranks sharing one GPU compete for the same workgroup slots, and a rank's workgroup that
+            # waits for a peer's same-index one that cannot be placed waits until the timeout: there,
+            # unless set explicitly, the all-reduce's count
+            zero1_blocks = int(env) if env else (min(256, nblocks) if self.shared_device else 256)
+        self._cz = None
+        if zero1_blocks > 0:
+            zerr, zblob = None, b""
+            try:
+                self._cz = h.PeerAllReduce(self.rank, self.world, self.device.index, int(cap_bytes),
+                                           int(zero1_blocks), float(timeout_s))
+                zblob = self._cz.handles()
+            except Exception as e:  # noqa: BLE001
+                zerr = e
+            store.set(f"{key}/zh{self.rank}", zblob)
+            zhs = [store.get(f"{key}/zh{r}") for r in range(self.world)]
+            zok = zerr is None and all(len(b) > 0 for b in zhs)
+            if zok:
+                try:
+                    self._cz.open(zhs)
+                except Exception:  # noqa: BLE001
+                    zok = False
+            store.set(f"{key}/zok{self.rank}", b"1" if zok else b"0")
+            if any(store.get(f"{key}/zok{r}") != b"1" for r in range(self.world)):
+                if self._cz is not None:
+                    self._cz.close()
+                self._cz = None  # every rank agrees: plain all-reduce -> Adam
+            _store_barrier(store, f"{key}/zready", self.world)
+
+    @property
+    def zero1_ready(self) -> bool:
+        """allreduce_adam_on is available (its communicator opened on every rank)."""
+        return self._cz is not None
 
     @property
     def launches(self) -> int:
-        return int(self._c.launches)
+        return int(self._c.launches) + (int(self._cz.launches) if self._cz is not None else 0)
 
     def allreduce_on(self, t, stream, op="sum"):
         if op != "sum" or t.dtype not in _PEER_DT or not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16:
@@ -335,6 +384,34 @@ class PeerComm(Comm):
                                  f"(got op={op}, dtype={t.dtype})")
             return self.fallback.allreduce(t, op)
         self._c.all_reduce(t.data_ptr(), t.numel(), _PEER_DT[t.dtype], stream.cuda_stream, self.algo)
+
+    def allreduce_adam_on(self, grad, stream, *, master: int, m1: int, m2: int, whi: int, wlo: int = 0, hp: int,
+                          grad_scale: float = 1.0, step_ctr: int = 0, bump: int = 0, nbump: int = 0, done: int = 0,
+                          bump_next: int = 0) -> None:
+        """ZeRO-1 optimizer step in one launch (per `cap / 4` elements): reduce-scatter `grad` (bf16 / fp32,
+        summed in fp32 in rank order), K6's Adam on this rank's chunk of the fp32 master / moments (device
+        pointers to `grad.numel()` elements) writing the bf16 weight plane `whi` (+ split lo plane `wlo`),
+        all-gather of the updated masters. Masters and weights end bit-identical on every rank and equal
+        to all-reduce -> K6; m1 / m2 are current on their owner only (`replicate_moments`). Counters as
+        K6: Adam step from `step_ctr`, `bump` advanced by the last launch (`done` ticket words or parity
+        `bump_next`). Reference: rllib/execution/train_ops.py:98 (the tower-averaged gradient step)."""
+        if grad.dtype not in _PEER_DT or not grad.is_cuda or not grad.is_contiguous():
+            raise ValueError(f"PeerComm.allreduce_adam_on: contiguous bf16/fp32 device gradient (got {grad.dtype})")
+        if self._cz is None:
+            raise RuntimeError("PeerComm: the ZeRO-1 communicator is not open (zero1_blocks=0 or setup failed)")
+        self._cz.all_reduce_adam(grad.data_ptr(), grad.numel(), _PEER_DT[grad.dtype], stream.cuda_stream,
+                                int(master), int(m1), int(m2), int(whi), int(wlo), int(hp), float(grad_scale),
+                                int(step_ctr), int(bump), int(nbump), int(done), int(bump_next))
+
+    def replicate_moments(self, grad_dtype, count: int, *bufs, stream=None) -> None:
+        """Make fp32 buffers (moment pointers) that `allreduce_adam_on(count elements of grad_dtype)` only
+        keeps current on each element's owner identical on every rank: zero the unowned elements, then
+        sum (exact: one non-zero term per element)."""
+        st = stream or torch.cuda.current_stream(self.device)
+        for ptr in bufs:
+            t = _FlatView(int(ptr), int(count), self.device)
+            self._cz.mask_unowned(int(ptr), int(count), _PEER_DT[grad_dtype], st.cuda_stream)
+            self._c.all_reduce(t.ptr, t.count, _PEER_DT[torch.float32], st.cuda_stream, self.algo)
 
     def allreduce(self, t, op="sum"):
         if t.data_ptr() % 16 and op == "sum" and t.dtype in _PEER_DT and t.is_cuda:
@@ -361,10 +438,13 @@ class PeerComm(Comm):
             if buf is not t:
                 t.copy_(buf)
             return
-        if t.is_floating_point() and t.is_cuda:
-            f = t.float()
+        if t.is_cuda:
+            # any other dtype (float64, integers, bool): its raw bytes, one fp32 per byte (0..255 are
+            # exact in fp32 and so is x + 0), so the result is bit-exact whatever the dtype
+            src_t = t.contiguous()
+            f = src_t.view(torch.uint8).float() if src_t.numel() else torch.zeros(0, device=t.device)
             self.broadcast(f, src)
-            t.copy_(f)
+            t.copy_(f.to(torch.uint8).view(t.dtype).view(src_t.shape))
             return
         if self.fallback is None:
             raise ValueError(f"PeerComm.broadcast: unsupported tensor {t.dtype} on {t.device}")
@@ -378,12 +458,14 @@ class PeerComm(Comm):
 
     def check(self):
         """Raise if a flag wait timed out (a peer died or never launched its side)."""
-        e = int(self._c.error())
+        e = int(self._c.error()) or (int(self._cz.error()) if self._cz is not None else 0)
         if e:
             raise RuntimeError(f"PeerComm rank {self.rank}: all-reduce flag wait timed out "
                                f"(peer {(e - 1) & 0xff}, workgroup {((e - 1) >> 8) & 0xffff}, phase {(e - 1) >> 24})")
 
     def close(self):
+        if self._cz is not None:
+            self._cz.close()
         self._c.close()
 
 

@@ -228,7 +228,9 @@ class LearnerActor:
         L = self.learner
         return {"comm": type(L.comm).__name__, "graph_has_comm": bool(L._graph_has_comm),
                 "split_graphs": L._graphs_split is not None, "graphs": bool(L.graphs),
-                "chain": int(getattr(L, "_chain", 1)), "launches": int(getattr(L.comm, "launches", 0))}
+                "chain": int(getattr(L, "_chain", 1)), "launches": int(getattr(L.comm, "launches", 0)),
+                "zero1": bool(getattr(L, "_zero1", lambda: False)()),
+                "peer_mode": L._peer_mode() if hasattr(L, "_peer_mode") and L.world > 1 else None}
 
     def device_info(self):
         import torch

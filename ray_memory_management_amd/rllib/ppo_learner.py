@@ -291,6 +291,8 @@ class PPOLearner:
             self.clip_ws = torch.zeros(require_hip().grad_clip_workspace_floats(), dtype=torch.float32, device=dev)
             self.clip_out = torch.ones(2, dtype=torch.float32, device=dev)
         self._manual = self._manual_layout()
+        #: flat ranges whose Adam ran ZeRO-1 style (moments current on their owner rank only)
+        self._zero1_ranges = set()
 
     def _wptr(self) -> int:
         """K6's bf16 weight output: the bf16 compute weights, the hi plane of the fp32 learner's split
@@ -618,6 +620,8 @@ class PPOLearner:
         """[K6b global-norm clip coefficient →] K6 Adam; K6 also advances both device counters
         {minibatch step, Adam step} from its last workgroup. Graph-capturable."""
         h = require_hip()
+        if self._zero1_ranges:
+            self._zero1_sync()
         scale_ptr = 0
         if self.clip_out is not None:
             h.grad_clip_coef(self.flat_grad.data_ptr(), self.grad_bf16, self.n_params, 1.0 / self.world,
@@ -654,10 +658,60 @@ class PPOLearner:
             return m
         return "one" if getattr(self.comm, "shared_device", True) else "fork"
 
+    def _zero1(self) -> bool:
+        """Multi-rank optimizer step ZeRO-1 style (PeerComm.allreduce_adam_on): each rank reduces its
+        1/W of the fp32 gradient bucket over the peers, applies Adam to it and all-gathers the updated
+        masters, in ONE launch per bucket — instead of an all-reduce of the whole bucket followed by
+        every rank running the same full Adam (K6). Same bits as all-reduce -> K6 (peer self-test).
+        Not with global-norm clipping (the norm needs the whole summed gradient first).
+        RMM_PEER_ZERO1=0 restores all-reduce -> K6."""
+        return (self._manual is not None and self.world > 1 and self.clip_out is None and self._wptr() != 0
+                and getattr(self.comm, "zero1_ready", False) and os.environ.get("RMM_PEER_ZERO1", "1") != "0")
+
+    def _zero1_adam(self, lo: int, hi: int, stream, last: bool):
+        """Fused reduce-scatter + Adam + all-gather over flat elements [lo, hi) on `stream`; the last
+        launch of the step advances the counters (parity copy in a chained graph, else the ticket)."""
+        cur = self._ctr().data_ptr()
+        wlo = self._wlo()
+        kw = dict(master=self.master.data_ptr() + 4 * lo, m1=self.m1.data_ptr() + 4 * lo,
+                  m2=self.m2.data_ptr() + 4 * lo, whi=self._wptr() + 2 * lo, wlo=wlo + 2 * lo if wlo else 0,
+                  hp=self.hp.data_ptr(), grad_scale=1.0 / self.world, step_ctr=cur + 8)
+        if last:
+            kw.update(bump=cur, nbump=2)
+            if self._parity and not (self._parity_last and self._par == 0):
+                kw["bump_next"] = self._ctrs[1 - self._par].data_ptr()
+                self._par ^= 1
+            else:
+                kw["done"] = self._bump_done.data_ptr()
+        self.comm.allreduce_adam_on(self.flat_grad[lo:hi], stream, **kw)
+        self._zero1_ranges.add((lo, hi))
+
+    def _zero1_sync(self):
+        """Before any non-ZeRO Adam: replicate the moments the ZeRO-1 steps kept on their owners."""
+        for lo, hi in sorted(self._zero1_ranges):
+            self.comm.replicate_moments(self.flat_grad.dtype, hi - lo, self.m1.data_ptr() + 4 * lo,
+                                        self.m2.data_ptr() + 4 * lo)
+        self._zero1_ranges.clear()
+
     def _manual_peer_step(self, full):
         """One multi-rank SGD step with the peer-memory all-reduce (eager or under capture): every
         rank issues the same all-reduce sequence, so the device epoch counters stay in step."""
         mode = self._peer_mode()
+        if self._zero1():
+            n, t = self.n_params, self._manual
+            self._manual_fwd_dense_bwd(full)
+            cap = torch.cuda.current_stream(self.device)
+            if mode == "fork":  # the dense + heads Adam (final after K12) overlaps the trunk backward
+                cs = self.comm.stream
+                cs.wait_stream(cap)
+                self._zero1_adam(t, n, cs, last=False)
+                self._manual_trunk_bwd(full)
+                cap.wait_stream(cs)  # one communicator: the two launches may not overlap
+                self._zero1_adam(0, t, cap, last=True)
+            else:
+                self._manual_trunk_bwd(full)
+                self._zero1_adam(0, n, cap, last=True)
+            return
         self._manual_fwd_dense_bwd(full)
         if mode == "fork":
             cap = torch.cuda.current_stream(self.device)
