@@ -1,6 +1,6 @@
 """Microbenchmark of K12 (fused dense-tail backward, csrc/hip/dense_kernels.hip) and K13 (dense
 forward) at the PPO minibatch shape: M = 500 rows, K = 3872 (Nature-CNN flatten), hidden 256,
-A+1 = 5 heads. Prints µs per call as one JSON line. RMM_K12_V1=1 selects the first K12 version.
+A+1 = 5 heads. Prints µs per call as one JSON line.
 Usage: python benchmarks/bench_dense.py [--M 500]"""
 import argparse
 import json
@@ -55,7 +55,7 @@ def main():
                                                          scratch.data_ptr(), st), a.iters), 2),
         "k13_us": round(timeit(lambda: h.dense_relu_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), M, K, 256,
                                                         hid.data_ptr(), st), a.iters), 2),
-        "M": M, "K": K, "A1": A1, "k12_version": 1 if os.environ.get("RMM_K12_V1") == "1" else 2,
+        "M": M, "K": K, "A1": A1, "k12_version": 2,
     }
     print(json.dumps(out), flush=True)
 

@@ -219,7 +219,8 @@ void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
 void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
                        X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
                        hipStream_t stream,
-                       const int64_t* gate = nullptr, int64_t gate_want = 0, int* gate_err = nullptr);
+                       const int64_t* gate = nullptr, int64_t gate_want = 0, int* gate_err = nullptr,
+                       int gate_parts = 1);
 // K10x backward: conv2 launch (dW2, db2, dpre1 -> dpre1 pair, db1) + conv1 weight-grad launch + reduce;
 // fp32 gradients in the parameters' memory order. partial: x3_trunk_partial_floats(B) floats.
 int x3_conv2_bwd_groups(int64_t B);

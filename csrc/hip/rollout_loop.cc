@@ -47,6 +47,23 @@ class EnvThreads {
     seq_.fetch_add(1, std::memory_order_acq_rel);
     for (auto& t : th_) t.join();
   }
+  // env step of group g at row t in `parts` consecutive env ranges on the calling thread, `after(p)`
+  // once range p is written (the gated K10x workgroups of that range may start reading its frames).
+  // With helper threads the ranges are not ordered: one full step, then every after(p).
+  template <typename F>
+  void step_parts(const RolloutGroup& g, uint64_t step, int64_t t, int parts, F&& after) {
+    if (n_ > 0 || parts <= 1) {
+      this->step(g, step, t);
+      for (int p = 0; p < std::max(1, parts); p++) after(p);
+      return;
+    }
+    const int64_t n = g.env.n;
+    for (int p = 0; p < parts; p++) {
+      const int64_t i0 = n * p / parts, i1 = n * (p + 1) / parts;
+      rl::synth_step_range(g.env, step, i0, i1, g.act, g.new_frames, false, g.rew + t * n, g.done + t * n);
+      after(p);
+    }
+  }
   // env step of group g at row t, split over all threads (the caller takes part)
   void step(const RolloutGroup& g, uint64_t step, int64_t t) {
     job_ = Job{&g, step, t};
@@ -153,12 +170,13 @@ std::vector<double> launch_overhead_probe(int n, hipStream_t stream) {
 }
 
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
-                         int64_t* host_seq_dev, int64_t gate_want) {
+                         int64_t* host_seq_dev, int64_t gate_want, int gate_parts) {
   // ctr_t = {rng counter, rollout row}: K10 stores row *t, K16 samples with the counter and advances both
   if (a.x3) {  // fp32 policy: the split-bf16 twins (K10x push -> K13x -> K16x)
     const X3Out h2{a.h2, a.h2lo};
     x3_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, X3In{a.W1, a.W1lo}, a.w1s, X3In{a.b1, a.b1lo},
-                      X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream, a.gate, gate_want, a.gate_err);
+                      X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream, a.gate, gate_want, a.gate_err,
+                      gate_parts);
     x3_dense_fwd_part(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, 256, a.hpart, a.S, stream);
     x3_heads_sample(a.hpart, a.S, X3In{a.bd, a.bdlo}, X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t,
                     a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B, a.A1, stream, k16_done, host_seq_dev);
@@ -204,16 +222,18 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
   auto launch = [&](size_t i, int64_t step) {
     if (G[i].direct) {
       // gated direct launches: step s waits in K10x until the release counter reaches s + 1
+      // step s opens at release count s P + 1 (P = gate_parts; range p of it at s P + 1 + p)
+      const int P = G[i].release ? std::max(1, G[i].gate_parts) : 1;
       rollout_step_direct(*G[i].direct, G[i].k16_done, G[i].stream, G[i].host_seq_dev,
-                          G[i].release ? step + 1 : 0);
+                          G[i].release ? step * P + 1 : 0, P);
       if (G[i].host_seq) return;  // completion comes through the host word
     } else {
       RMM_HIP_CHECK(hipGraphLaunch(G[i].exec, G[i].stream));
     }
     RMM_HIP_CHECK(hipEventRecord(ev[2 * i + (step & 1)], G[i].stream));
   };
-  auto release = [&](size_t i) {  // frames of the next step are written: open its gate
-    __atomic_fetch_add(G[i].release, int64_t(1), __ATOMIC_RELEASE);
+  auto release = [&](size_t i, int64_t k = 1) {  // frames of the next step (range) are written: open its gate
+    __atomic_fetch_add(G[i].release, k, __ATOMIC_RELEASE);
   };
   try {
     EnvThreads pool(std::max(1, std::min(threads, 16)));
@@ -224,7 +244,7 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
       if (G[i].direct && G[i].release) __atomic_store_n(G[i].release, int64_t(0), __ATOMIC_RELEASE);
       launch(i, 0);
       if (G[i].release) {
-        release(i);                  // step 0's frames are already staged
+        release(i, G[i].direct ? std::max(1, G[i].gate_parts) : 1);  // step 0's frames are already staged
         if (T > 1) launch(i, 1);     // step 1 waits on the device for its frames
       }
     }
@@ -239,14 +259,21 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
           wait_event(ev[2 * i + (t & 1)], spin);  // step t's actions are in g.act
         ph[0] += us_since(c0);
         c0 = Clock::now();
-        pool.step(g, g.env.step[0]++, t);
+        const int P = g.release && g.direct ? std::max(1, g.gate_parts) : 1;
+        if (g.release && P > 1) {  // open step t+1 range by range as the envs are stepped
+          pool.step_parts(g, g.env.step[0]++, t, P, [&](int) {
+            if (t + 1 < T) release(i);
+          });
+        } else {
+          pool.step(g, g.env.step[0]++, t);
+        }
         rl::episode_update(g.env.n, g.rew + t * g.env.n, g.done + t * g.env.n, g.ep_rew, g.ep_len, completed);
         ph[1] += us_since(c0);
         c0 = Clock::now();
         if (g.release) {
           // gate: step t+1 is already enqueued (its launch latency hid behind step t); open it, then
           // enqueue step t+2 while step t+1 runs
-          if (t + 1 < T) release(i);
+          if (t + 1 < T && P == 1) release(i);
           if (t + 2 < T) launch(i, t + 2);
         } else if (t + 1 < T) {
           launch(i, t + 1);

@@ -25,6 +25,9 @@ struct RolloutGroup {
   // step gate (optional): the graph starts with a device-side wait until *release passes its
   // sequence number, so step t+1 is launched BEFORE step t's env step and only released after it
   int64_t* release = nullptr;     // pinned host release counter (null: no gate)
+  // the envs are stepped in `gate_parts` ranges with a release after each (the counter advances
+  // gate_parts per step), and each K10x workgroup waits for its own range only
+  int gate_parts = 1;
   // direct launches (optional): the policy step as its three kernel launches (K10 push → K13s →
   // K16 with the step advance) from this thread instead of a graph launch; `exec` is then unused
   const RolloutServerArgs* direct = nullptr;
@@ -40,7 +43,7 @@ struct RolloutGroup {
 std::vector<double> launch_overhead_probe(int n, hipStream_t stream);
 // One policy step of `a` as direct launches on `stream` (the kernels a captured step graph holds).
 void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hipStream_t stream,
-                         int64_t* host_seq_dev = nullptr, int64_t gate_want = 0);
+                         int64_t* host_seq_dev = nullptr, int64_t gate_want = 0, int gate_parts = 1);
 
 // Launch step 0 of every group, then for t < T and each group: wait for its step (poll when
 // `spin`), step its envs (actions → newest frames, rewards, dones at row t) on `threads` CPU threads,

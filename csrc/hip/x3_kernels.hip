@@ -107,7 +107,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, CPair W1, WStrides w1, CPair b1, CPair W2, WStrides w2, CPair b2, Pair h1_out, Pair h2_out,
     uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t,
-    const int64_t* gate, int64_t gate_want, int* gate_err) {
+    const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts) {
   __shared__ __attribute__((aligned(16))) unsigned short img[FIMG];
   __shared__ __attribute__((aligned(16))) unsigned short h1h[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short h1l[H1P_ELEMS];
@@ -132,11 +132,16 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   int64_t b = blockIdx.x;
   if (gate) {
     // step gate: this launch was enqueued before the host stepped the envs; wait for the release counter
-    // (mapped pinned memory, bumped after the new frames are written) before reading them. Bounded
-    // (~0.2-0.5 s): a host that died mid-fragment can never leave a wave spinning (*gate_err is set)
+    // (mapped pinned memory, bumped after the new frames are written) before reading them. With
+    // gate_parts P the host steps the envs in P ranges and bumps the counter after each, so frame b waits
+    // only for its own range: the first ranges' frames cross PCIe and their conv1
+    // runs while the host still steps the rest. Bounded (~0.2-0.5 s): a host that died mid-fragment can
+    // never leave a wave spinning (*gate_err is set)
     if (threadIdx.x == 0) {
+      // range of frame b under the host's split [B p / P, B (p + 1) / P): p = ((b + 1) P - 1) / B
+      const int64_t want = gate_want + (gate_parts > 1 ? ((b + 1) * gate_parts - 1) / B : 0);
       int64_t n = 0;
-      while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gate_want) {
+      while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
         if (++n >= 200000) {
           if (gate_err) *gate_err = 1;
           break;
@@ -671,15 +676,16 @@ void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
     throw std::invalid_argument("x3_trunk_fwd: h2 (and h1) need hi and lo planes");
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(x3_trunk_fwd_groups(B))), dim3(x3::NTF), 0, stream, obs, idx,
                      ctr, period, B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), pp(h1), pp(h2), nullptr,
-                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr);
+                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
 void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
                        X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
-                       hipStream_t stream, const int64_t* gate, int64_t gate_want, int* gate_err) {
+                       hipStream_t stream, const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts) {
   if (B <= 0) return;
   if (stack == nullptr || new_frames == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: stack and new frames");
+  if (gate_parts < 1 || gate_parts > B) throw std::invalid_argument("x3_trunk_fwd_push: 1 <= gate_parts <= B");
   if (rows != nullptr && t_ptr == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: rows need the row counter");
   if ((reinterpret_cast<uintptr_t>(stack) | reinterpret_cast<uintptr_t>(new_frames) | reinterpret_cast<uintptr_t>(rows)) & 3)
     throw std::invalid_argument("x3_trunk_fwd_push: buffers must be 4-byte aligned");
@@ -689,7 +695,7 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
   // push mode: one frame per workgroup (each workgroup shifts its own env's stack)
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(B)), dim3(x3::NTF), 0, stream, nullptr, nullptr, nullptr,
                      int64_t(1), B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), x3::Pair{}, pp(h2), stack,
-                     new_frames, rows, t_ptr, gate, gate_want, gate_err);
+                     new_frames, rows, t_ptr, gate, gate_want, gate_err, gate_parts);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -686,8 +686,12 @@ class HybridRolloutWorker(GPURolloutWorker):
                 self._h_rel_dev = int(require_hip().host_device_pointer(self._h_rel.data_ptr()))
                 self._gate_err = torch.zeros(1, dtype=torch.int32, device=self.device)
             if self._h_rel_dev:
+                # the envs are stepped in `parts` ranges, each released as soon as its frames are written
+                # (K10x workgroup b waits for its own range): the first frames cross PCIe while the rest
+                # are stepped. RMM_ROLLOUT_GATE_PARTS=1: one release after the whole env step
+                parts = int(os.environ.get("RMM_ROLLOUT_GATE_PARTS", "10"))
                 out.update(release=self._h_rel.data_ptr(), release_dev=self._h_rel_dev,
-                           gate_err=self._gate_err.data_ptr())
+                           gate_err=self._gate_err.data_ptr(), gate_parts=max(1, min(parts, int(k["B"]))))
         return out
 
     def _kernel_args(self, G, S):
