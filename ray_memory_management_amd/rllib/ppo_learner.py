@@ -1257,9 +1257,13 @@ class GPURolloutSampler:
         self.buf_rew = torch.empty((T, B), dtype=torch.float32, device=dev)
         self.buf_done = torch.empty((T, B), dtype=torch.float32, device=dev)
         self.act_now = torch.zeros(B, dtype=torch.int64, device=dev)
-        with torch.no_grad():
-            logits, _ = self.model(self.s_obs)
-        self.A = logits.shape[-1]
+        heads = getattr(self.model, "heads", None)
+        if getattr(heads, "out_features", 0) >= 2:  # [A logits | value]: no probe forward (MIOpen's solver
+            self.A = heads.out_features - 1          # search for a torch fp32 conv costs ~2.5 ms at start-up)
+        else:
+            with torch.no_grad():
+                logits, _ = self.model(self.s_obs)
+            self.A = logits.shape[-1]
         self.buf_logits = torch.empty((T, B, self.A), dtype=torch.float32, device=dev)
         # device-side {rng counter, rollout row}; both advance by one per step (one add launch)
         self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)
