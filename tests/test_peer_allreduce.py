@@ -63,13 +63,17 @@ def test_peer_allreduce_three_ranks_two_shot():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("learners", [2, 3])
-def test_ppo_learner_actors_peer_comm_in_graph(ray_start, learners):
+@pytest.mark.parametrize("learners,mode", [(2, None), (3, None), (2, "fork")])
+def test_ppo_learner_actors_peer_comm_in_graph(ray_start, learners, mode, monkeypatch):
     """2 / 3 fused PPO learner actors on one GPU over PeerComm: the optimizer step is the ZeRO-1 launch
     (reduce-scatter + Adam + all-gather; its bits equal all-reduce -> K6 in the peer self-test) INSIDE
-    the chained SGD graph (chain > 1), and the replicas stay bit-identical."""
+    the chained SGD graph (chain > 1), and the replicas stay bit-identical. mode "fork": the layout ranks
+    on separate GPUs take (dense bucket's launch on the comm stream beside the trunk backward, then the
+    trunk bucket's), forced here on one GPU."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if mode:
+        monkeypatch.setenv("RMM_PEER_MODE", mode)
     import ray_memory_management_amd as ray
     from ray_memory_management_amd.rllib.algorithms.ppo import PPOConfig
 
@@ -89,7 +93,7 @@ def test_ppo_learner_actors_peer_comm_in_graph(ray_start, learners):
         assert np.isfinite(st["total_loss"]) and st["num_learners"] == learners
         info = ray.get([a.comm_info.remote() for a in algo.learner_group.learners])
         assert all(i["comm"] == "PeerComm" and i["graph_has_comm"] and i["chain"] > 1 and i["zero1"]
-                   for i in info), info
+                   and i["peer_mode"] == (mode or "one") for i in info), info
         assert len({i["launches"] for i in info}) == 1 and info[0]["launches"] > 0, info
         d = algo.learner_group.weights_digests()
         assert len(set(d)) == 1, d

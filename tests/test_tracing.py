@@ -91,3 +91,112 @@ def test_tracing_off_by_default(span_dir):
     assert ray.get(f.remote()) == 1
     ray.shutdown()
     assert _spans(span_dir) == []
+
+
+class _Collector:
+    """A local OTLP/HTTP endpoint (what Tempo serves on :4318) recording every ExportTraceServiceRequest."""
+
+    def __init__(self):
+        import http.server
+        import threading
+
+        got = self.requests = []
+
+        class H(http.server.BaseHTTPRequestHandler):
+            def do_POST(self):
+                n = int(self.headers.get("Content-Length", 0))
+                got.append((self.path, self.headers.get("Content-Type"), json.loads(self.rfile.read(n))))
+                self.send_response(200)
+                self.end_headers()
+                self.wfile.write(b"{}")
+
+            def log_message(self, *a):
+                pass
+
+        self.srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self.url = f"http://127.0.0.1:{self.srv.server_address[1]}/v1/traces"
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    def spans(self):
+        return [sp for _, _, req in self.requests for rs in req["resourceSpans"] for ss in rs["scopeSpans"]
+                for sp in ss["spans"]]
+
+    def close(self):
+        self.srv.shutdown()
+
+
+def test_tempo_exporter_posts_otlp_json(monkeypatch):
+    """setup_tempo_tracing: spans leave as OTLP/HTTP JSON (trace / span ids in hex, kinds and status as
+    the proto enums, int64 times as strings), batched by a background thread."""
+    from ray_memory_management_amd.util.tracing import setup_tempo_tracing as tempo
+    from ray_memory_management_amd.util.tracing import tracing_helper as th
+
+    col = _Collector()
+    monkeypatch.setenv("RMM_OTLP_ENDPOINT", col.url)
+    monkeypatch.setenv("RMM_OTLP_CONSOLE", "0")
+    try:
+        tempo.setup_tracing()
+        spec = {}
+        th.inject(spec, "f", {"k": 3})
+        with th.execution_span(spec, "f", {"ok": True}):
+            pass
+        tempo._installed.flush()
+        spans = col.spans()
+        assert col.requests[0][0] == "/v1/traces" and col.requests[0][1] == "application/json"
+        res = col.requests[0][2]["resourceSpans"][0]["resource"]["attributes"]
+        assert {"key": "service.name", "value": {"stringValue": "ray_memory_management_amd"}} in res
+        prod = next(s for s in spans if s["kind"] == 4)
+        cons = next(s for s in spans if s["kind"] == 5)
+        assert cons["parentSpanId"] == prod["spanId"] and cons["traceId"] == prod["traceId"]
+        assert len(prod["traceId"]) == 32 and len(prod["spanId"]) == 16
+        assert int(cons["endTimeUnixNano"]) >= int(cons["startTimeUnixNano"]) > 0
+        assert cons["status"] == {"code": 1}
+        assert {"key": "k", "value": {"intValue": "3"}} in prod["attributes"]
+        assert tempo._installed.sent == 2 and tempo._installed.dropped == 0
+    finally:
+        th.set_exporter(None)
+        if tempo._installed is not None:
+            tempo._installed.shutdown()
+        col.close()
+
+
+def test_tempo_exporter_across_processes(monkeypatch):
+    """The tempo hook in a cluster: driver and worker processes post to the collector, and the worker's
+    execution span hangs off the driver's submission span."""
+    col = _Collector()
+    monkeypatch.setenv("RMM_OTLP_ENDPOINT", col.url)
+    monkeypatch.setenv("RMM_OTLP_CONSOLE", "0")
+    monkeypatch.setenv("RMM_OTLP_FLUSH_S", "0.1")
+    try:
+        ray.init(num_cpus=1, _tracing_startup_hook="ray_memory_management_amd.util.tracing.setup_tempo_tracing:"
+                                                   "setup_tracing")
+
+        @ray.remote
+        def g(x):
+            return x * 3
+
+        assert ray.get(g.remote(2)) == 6
+        import time
+
+        deadline = time.time() + 20
+        while time.time() < deadline and not any(s["kind"] == 5 for s in col.spans()):
+            time.sleep(0.1)
+        ray.shutdown()
+        from ray_memory_management_amd.util.tracing import setup_tempo_tracing as tempo
+
+        if tempo._installed is not None:
+            tempo._installed.flush()
+        spans = col.spans()
+        prod = [s for s in spans if s["kind"] == 4 and ".g ray.remote" in s["name"]]
+        cons = [s for s in spans if s["kind"] == 5 and ".g ray.remote_worker" in s["name"]]
+        assert prod and cons, [s["name"] for s in spans]
+        assert cons[0]["parentSpanId"] == prod[0]["spanId"]
+        pids = {a["value"]["intValue"] for _, _, req in col.requests for rs in req["resourceSpans"]
+                for a in rs["resource"]["attributes"] if a["key"] == "process.pid"}
+        assert len(pids) >= 2
+    finally:
+        ray.shutdown()
+        from ray_memory_management_amd.util.tracing import tracing_helper as th
+
+        th.set_exporter(None)
+        col.close()
