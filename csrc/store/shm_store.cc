@@ -1244,6 +1244,7 @@ int Store::AbortCreator(int pid) {
 
 bool Store::Get(const ObjectId& id, int64_t timeout_ms, View* out) {
   int64_t deadline = timeout_ms < 0 ? -1 : NowNs() + timeout_ms * 1000000ll;
+  int64_t restore_deadline = -1;  // a restore that found no room waits like Create does (oom_grace_ns)
   Lock();
   for (;;) {
     int64_t idx = Find(id);
@@ -1272,10 +1273,26 @@ bool Store::Get(const ObjectId& id, int64_t timeout_ms, View* out) {
         return true;
       }
       if (e->state == kSpilled) {
-        if (!RestoreLocked(idx)) {
+        if (RestoreLocked(idx)) continue;
+        // no room right now: other processes' spills in flight, readers' pins and a global GC free
+        // memory shortly (a concurrent map / reduce stage); wait for them like Create before failing
+        const int64_t now = NowNs();
+        if (restore_deadline < 0) {
+          restore_deadline = now + std::max<int64_t>(hdr_->oom_grace_ns, 0);
+          __atomic_add_fetch(&hdr_->gc_requests, 1, __ATOMIC_RELEASE);
+          hdr_->oom_waits_total++;
+        }
+        if (now >= restore_deadline) {
           Unlock();
           throw std::runtime_error("ObjectStoreFullError: cannot restore spilled object");
         }
+        if (deadline >= 0 && now >= deadline) {
+          Unlock();
+          return false;
+        }
+        int64_t until = std::min<int64_t>(restore_deadline, now + 20000000ll);  // re-check every 20 ms
+        if (deadline >= 0) until = std::min(until, deadline);
+        CondWait(until);
         continue;
       }
     }
