@@ -270,7 +270,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     int64_t B, const unsigned short* __restrict__ W2, WStrides w2, const unsigned short* __restrict__ h1,
     const unsigned short* __restrict__ h2, const unsigned short* __restrict__ dh2, float* __restrict__ partial,
     int dbg) {
-  __shared__ __attribute__((aligned(16))) unsigned short st[ST_C * ST_CP];  // space-to-depth frame
+  __shared__ __attribute__((aligned(16))) unsigned short st[ST_ELEMS];  // space-to-depth frame
   __shared__ __attribute__((aligned(16))) unsigned short h1p[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short dp2[D2W * D2W * C2];  // [oy*12+ox][co2]
   __shared__ __attribute__((aligned(16))) unsigned short dp2t[C2 * DP2_PITCH];   // [co2][kperm(q)]
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     bwd_issue(blockIdx.x, idx, obs, h1, h2, dh2, fr, hv1, hv2, gv2);
     h1_issue(blockIdx.x, h1, hv1);
   }
-  if (!(dbg & (32 | 256))) zero_lds(st, ST_C * ST_CP * 2);
+  if (!(dbg & (32 | 256))) zero_lds(st, ST_ELEMS * 2);
   if (!(dbg & 256)) {
     zero_lds(h1p, H1P_ELEMS * 2);
     zero_lds(dp2, D2W * D2W * C2 * 2);
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(NTB) void k_trunk_bwd(
     // share the st operand.
     {
       const int cb = wave & 3, a = wave >> 2;
-      const unsigned short* sa = st + (16 * cb + r) * ST_CP + 8 * g;
+      const unsigned short* sa = st + st_chan(16 * cb + r) + 8 * g;
       const unsigned short* d0 = dp1s + r * DB_CP + (1 - a) * ST_W + 8 * g;
 #pragma unroll
       for (int s = 0; s < ((dbg & 4) ? 0 : KSTEPS1); s++) {

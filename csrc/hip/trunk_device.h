@@ -178,8 +178,12 @@ __device__ __forceinline__ void zero_frame_border(uint8_t* frame) {
 // grid positions, which are CONTIGUOUS per channel here (one 16-B LDS read per MFMA operand
 // instead of 8 strided 2-B gathers). Row pitch ST_W = 24 (3 chunks of 8), 23 rows (row 22 and
 // columns 22, 23 stay zero: K padding), channel pitch 552 el = 276 dwords (8 lanes reading 8
-// channels hit distinct 4-bank groups).
-constexpr int ST_W = 24, ST_CP = 23 * ST_W, ST_C = 64;
+// channels hit distinct 4-bank groups). The four 16-channel blocks (ry = yp & 3) are ST_BP = 32 el
+// apart beyond that: a wave's staging stores span ~3 frame rows, i.e. 3 blocks, whose stride 16 x 276
+// dwords is 0 mod 64 banks — without the pad those rows' stores met on the same banks.
+constexpr int ST_W = 24, ST_CP = 23 * ST_W, ST_C = 64, ST_BP = 32;
+constexpr int ST_ELEMS = ST_C * ST_CP + (ST_C / 16) * ST_BP;
+__device__ __forceinline__ int st_chan(int c) { return c * ST_CP + (c >> 4) * ST_BP; }  // channel c's base
 template <int NT>
 __device__ __forceinline__ void frame_store_s2d(const FrameRegs<NT>& f, unsigned short* st) {
   constexpr int NW = FrameRegs<NT>::NW, PER = FrameRegs<NT>::PER;
@@ -189,7 +193,7 @@ __device__ __forceinline__ void frame_store_s2d(const FrameRegs<NT>& f, unsigned
     if (o < NW) {
       const int y = o / 21, xw = o - y * 21;  // pixels x = 4xw .. 4xw+3 → xp = 4xw+2 .. 4xw+5
       const int yp = y + 2;
-      unsigned short* row = st + (16 * (yp & 3)) * ST_CP + (yp >> 2) * ST_W + xw;
+      unsigned short* row = st + st_chan(16 * (yp & 3)) + (yp >> 2) * ST_W + xw;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int rx = (q + 2) & 3, dX = (q + 2) >> 2;
@@ -218,7 +222,7 @@ __device__ __forceinline__ void load_frame_s2d(const uint8_t* __restrict__ src, 
     if (o < NW) {
       const int y = o / 21, xw = o - y * 21;  // pixels x = 4xw .. 4xw+3 → xp = 4xw+2 .. 4xw+5
       const int yp = y + 2;
-      unsigned short* row = st + (16 * (yp & 3)) * ST_CP + (yp >> 2) * ST_W + xw;
+      unsigned short* row = st + st_chan(16 * (yp & 3)) + (yp >> 2) * ST_W + xw;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int rx = (q + 2) & 3, dX = (q + 2) >> 2;  // compile-time after unrolling

@@ -490,7 +490,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
                                                         const int64_t* __restrict__ idx0,
                                                         const int64_t* __restrict__ ctr, int64_t period, int64_t B,
                                                         CPair dpre1, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) unsigned short st[ST_C * ST_CP];    // space-to-depth frame (exact)
+  __shared__ __attribute__((aligned(16))) unsigned short st[trunk::ST_ELEMS];  // space-to-depth frame (exact)
   __shared__ __attribute__((aligned(16))) unsigned short dp[4 * DB_B];        // [hi b0][hi b1][lo b0][lo b1]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
     }
   };
   if (int64_t(blockIdx.x) < B) issue(blockIdx.x);
-  trunk::zero_lds(st, ST_C * ST_CP * 2);
+  trunk::zero_lds(st, trunk::ST_ELEMS * 2);
   trunk::zero_lds(dp, 4 * DB_B * 2);
   Acc aw[2];
   aw[0] = aw[1] = acc0();
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
     if (b + gridDim.x < B) issue(b + gridDim.x);
     {
       const int cb = wave & 3, a = wave >> 2;
-      const unsigned short* sa = st + (16 * cb + r) * ST_CP + 8 * g;
+      const unsigned short* sa = st + trunk::st_chan(16 * cb + r) + 8 * g;
       const unsigned short* d0 = dp + r * DB_CP + (1 - a) * ST_W + 8 * g;
 #pragma unroll
       for (int s = 0; s < KSTEPS1; s++) {
