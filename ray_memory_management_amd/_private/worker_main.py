@@ -424,6 +424,7 @@ class Executor:
                 result = True
             else:
                 args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
+                t_res = time.time()
                 m = getattr(self.actor, name)
                 if "_trace_ctx" in spec:
                     from ray_memory_management_amd.util.tracing.tracing_helper import execution_span
@@ -434,7 +435,12 @@ class Executor:
                     result = m(*args, **kwargs)
                 if inspect.iscoroutine(result):
                     raise RuntimeError("coroutine returned from a non-async actor path")
+                t_ret = time.time()
             self.store_outputs(ret_ids, spec.get("num_returns", 1), result, contained_map, holds)
+            st = getattr(w, "task_stamps", None)
+            if st is not None and name not in ("__ray_ready__",):
+                # (method, arrived, args resolved, method returned, outputs stored): hand-off probes
+                st.append((name, t0, t_res, t_ret, time.time()))
         except BaseException as e:  # noqa: BLE001
             from ray_memory_management_amd.actor import _ActorExit
 

@@ -526,6 +526,9 @@ class HybridRolloutWorker(GPURolloutWorker):
         from ray_memory_management_amd.rllib.execution.sample_ingest import pack_fragment_device
 
         t0 = time.perf_counter()
+        stamps = getattr(self, "_stamps", None)
+        if stamps is not None:
+            stamps.append(("sample_start", time.time()))
         G, T, st = self.groups, self.T, self.stream
         with torch.no_grad():
             S = self.group_streams
@@ -595,6 +598,8 @@ class HybridRolloutWorker(GPURolloutWorker):
 
                 torch.cuda.synchronize(self.device)
                 print(f"[hybrid-worker pid {os.getpid()}] fragment loop ok", file=sys.stderr, flush=True)
+            t_loop = time.perf_counter()
+            self._loop_time = getattr(self, "_loop_time", 0.0) + (t_loop - t0)
             with torch.cuda.stream(st):
                 for gs in dict.fromkeys(S):
                     if gs is not st:
@@ -623,7 +628,21 @@ class HybridRolloutWorker(GPURolloutWorker):
                     raise RuntimeError("rollout step gate timed out during this fragment (a policy step ran "
                                        "without its frames); fragment discarded")
         self._sample_time += time.perf_counter() - t0
+        if stamps is not None:
+            stamps.append(("sample_end", time.time()))
         return frag
+
+    def phase_stamps(self, on: bool = True):
+        """Wall-clock (start, end) stamps of every sample() from now on (hand-off latency probes); returns
+        and clears the stamps recorded so far."""
+        from ray_memory_management_amd._private import worker as _w
+
+        cw = _w.global_worker
+        out = (getattr(self, "_stamps", None) or []) + [("task",) + t for t in (getattr(cw, "task_stamps", None) or [])]
+        self._stamps = [] if on else None
+        if cw is not None:
+            cw.task_stamps = [] if on else None
+        return out
 
     def _server_args(self, G, S):
         """Arguments of the K21 persistent rollout server (csrc/hip/rollout_server.hip) for this
@@ -837,4 +856,5 @@ class HybridRolloutWorker(GPURolloutWorker):
 
     def timing(self):
         """Accumulated seconds in sample() and set_weights() (phase breakdown probes)."""
-        return {"sample_s": self._sample_time, "set_weights_s": getattr(self, "_set_weights_time", 0.0)}
+        return {"sample_s": self._sample_time, "set_weights_s": getattr(self, "_set_weights_time", 0.0),
+                "loop_s": getattr(self, "_loop_time", 0.0)}

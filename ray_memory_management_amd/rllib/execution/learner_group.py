@@ -86,8 +86,13 @@ class LearnerActor:
 
     def update(self, *fragments) -> Dict:
         t0 = time.perf_counter()
+        stamps = getattr(self, "_stamps", None)
+        if stamps is not None:
+            stamps.append(("update_start", time.time()))
         st = self.learner.update_fragments(list(fragments))  # ends with a device sync (stats to host)
         dt = time.perf_counter() - t0
+        if stamps is not None:
+            stamps.append(("update_end", time.time()))
         self.update_time += dt
         self.updates += 1
         st = dict(st)
@@ -222,6 +227,18 @@ class LearnerActor:
             h.update(k.encode())
             h.update(v.tobytes())
         return h.hexdigest()
+
+    def phase_stamps(self, on: bool = True):
+        """Wall-clock (start, end) stamps of every update from now on (hand-off latency probes); returns
+        and clears the stamps recorded so far."""
+        from ray_memory_management_amd._private import worker as _w
+
+        cw = _w.global_worker
+        out = (getattr(self, "_stamps", None) or []) + [("task",) + t for t in (getattr(cw, "task_stamps", None) or [])]
+        self._stamps = [] if on else None
+        if cw is not None:
+            cw.task_stamps = [] if on else None
+        return out
 
     def comm_info(self):
         """Which communicator carries the gradients and whether the SGD-step graph contains them."""
