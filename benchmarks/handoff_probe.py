@@ -1,7 +1,6 @@
 """Hand-off latencies of the runtime PPO iteration (rollout fragment -> learner update -> next sample) from
 wall-clock stamps in the rollout worker, the learner actor and their task executors:
     python benchmarks/handoff_probe.py [--steps 20] [--dtype fp32]"""
-end -> worker's (prefetched) next sample start, from wall-clock stamps in both processes."""
 import sys, argparse
 sys.path.insert(0, ".")
 import bench
