@@ -667,11 +667,14 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("x3_trunk_fwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, XP W1,
                            std::vector<int64_t> w1s, XP b1, XP W2, std::vector<int64_t> w2s, XP b2, XP h1, XP h2,
-                           uint64_t stream) {
+                           uint64_t stream, uint64_t cols, uint64_t cols_out, int ncols) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_fwd: 4 strides per weight");
     x3_trunk_fwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr,
-                 period, B, xin(W1), w1s.data(), xin(b1), xin(W2), w2s.data(), xin(b2), xout(h1), xout(h2), S(stream));
-  });
+                 period, B, xin(W1), w1s.data(), xin(b1), xin(W2), w2s.data(), xin(b2), xout(h1), xout(h2), S(stream),
+                 cols ? P<const float>(cols) : nullptr, cols_out ? P<float>(cols_out) : nullptr, ncols);
+  }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W1"), py::arg("w1s"),
+     py::arg("b1"), py::arg("W2"), py::arg("w2s"), py::arg("b2"), py::arg("h1"), py::arg("h2"), py::arg("stream"),
+     py::arg("cols") = 0, py::arg("cols_out") = 0, py::arg("ncols") = 0);
   m.def("x3_trunk_fwd_push", [](uint64_t stack, uint64_t nf, uint64_t rows, uint64_t t_ptr, int64_t B, XP W1,
                                 std::vector<int64_t> w1s, XP b1, XP W2, std::vector<int64_t> w2s, XP b2, XP h2,
                                 uint64_t stream) {

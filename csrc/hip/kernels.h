@@ -215,7 +215,7 @@ struct X3Out {
 int x3_trunk_fwd_groups(int64_t B);
 void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W1,
                   const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h1, X3Out h2,
-                  hipStream_t stream);
+                  hipStream_t stream, const float* cols = nullptr, float* cols_out = nullptr, int ncols = 0);
 void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
                        X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
                        hipStream_t stream,

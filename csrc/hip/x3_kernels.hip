@@ -107,7 +107,8 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, CPair W1, WStrides w1, CPair b1, CPair W2, WStrides w2, CPair b2, Pair h1_out, Pair h2_out,
     uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t,
-    const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts) {
+    const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts, const float* __restrict__ cols,
+    float* __restrict__ cols_out, int ncols) {
   __shared__ __attribute__((aligned(16))) unsigned short img[FIMG];
   __shared__ __attribute__((aligned(16))) unsigned short h1h[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short h1l[H1P_ELEMS];
@@ -184,6 +185,10 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   }
 
   for (; b < B; b += G) {
+    // the frame's PPO loss columns, gathered through the same index window, so the loss kernel (K15x)
+    // reads its row directly instead of a step counter -> index -> row chain of dependent loads
+    if (cols_out != nullptr && int(threadIdx.x) < ncols)
+      cols_out[b * ncols + threadIdx.x] = cols[(idx ? idx[b] : b) * ncols + threadIdx.x];
     frame_image_store<NTF>(fr, img);
     __syncthreads();  // image (+ first frame: border / h1 zeros, weights); the previous conv2 is done
     if (b + G < B) trunk::frame_issue<NTF>(obs + (idx ? idx[b + G] : b + G) * FB, fr);  // in flight meanwhile
@@ -667,16 +672,18 @@ int x3_trunk_fwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<in
 
 void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W1,
                   const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h1, X3Out h2,
-                  hipStream_t stream) {
+                  hipStream_t stream, const float* cols, float* cols_out, int ncols) {
   if (B <= 0) return;
   if (period <= 0) period = 1;
   for (const X3In* p : {&W1, &b1, &W2, &b2})
     if (!p->hi || !p->lo) throw std::invalid_argument("x3_trunk_fwd: weights need hi and lo planes");
   if (!h2.hi || !h2.lo || (h1.hi == nullptr) != (h1.lo == nullptr))
     throw std::invalid_argument("x3_trunk_fwd: h2 (and h1) need hi and lo planes");
+  if ((cols == nullptr) != (cols_out == nullptr) || (cols_out && (ncols < 1 || ncols > x3::NTF)))
+    throw std::invalid_argument("x3_trunk_fwd: cols and cols_out together, 1 <= ncols <= 512");
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(x3_trunk_fwd_groups(B))), dim3(x3::NTF), 0, stream, obs, idx,
                      ctr, period, B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), pp(h1), pp(h2), nullptr,
-                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1);
+                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1, cols, cols_out, ncols);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -695,7 +702,7 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
   // push mode: one frame per workgroup (each workgroup shifts its own env's stack)
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(B)), dim3(x3::NTF), 0, stream, nullptr, nullptr, nullptr,
                      int64_t(1), B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), x3::Pair{}, pp(h2), stack,
-                     new_frames, rows, t_ptr, gate, gate_want, gate_err, gate_parts);
+                     new_frames, rows, t_ptr, gate, gate_want, gate_err, gate_parts, nullptr, nullptr, 0);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -435,7 +435,9 @@ class PPOLearner:
               "dpre": X3.Pair.empty((mbs, 256), dev), "dx": X3.Pair.empty((mbs, K), dev),
               "dpre1": X3.Pair.empty((mbs, 441, 16), dev), "S": S,
               "hpart": torch.empty(S * mbs * 256, dtype=torch.float32, device=dev),
-              "part": torch.empty(X3.trunk_partial_floats(mbs), dtype=torch.float32, device=dev)}
+              "part": torch.empty(X3.trunk_partial_floats(mbs), dtype=torch.float32, device=dev),
+              # the minibatch's loss columns, gathered by K10x so K15x reads them without the index chain
+              "colsg": torch.empty((mbs, A1 + 3), dtype=torch.float32, device=dev)}
         self._mws = ws
         return ws
 
@@ -451,14 +453,18 @@ class PPOLearner:
         K, A1 = m.dense_tail.in_features, m.heads.out_features
         w1, b1, w2, b2 = (P[n] for n in m._X3_NAMES[:4])
         wd, bd, wh, bh = (P[n] for n in m._X3_NAMES[4:])
+        cols, colsg = full["cols"], ws["colsg"]
+        gather = cols.dtype == torch.float32 and cols.is_contiguous() and cols.shape[1] == colsg.shape[1] \
+            and not os.environ.get("RMM_NO_COLS_GATHER")
         h.x3_trunk_fwd(full["obs"].data_ptr(), idx.data_ptr(), ctr.data_ptr(), int(period), int(mbs), w1.ptrs(),
                        list(w1.hi.stride()), b1.ptrs(), w2.ptrs(), list(w2.hi.stride()), b2.ptrs(), ws["h1"].ptrs(),
-                       ws["h2"].ptrs(), st)
+                       ws["h2"].ptrs(), st, cols=cols.data_ptr() if gather else 0,
+                       cols_out=colsg.data_ptr() if gather else 0, ncols=colsg.shape[1] if gather else 0)
         h.x3_dense_fwd_part(ws["h2"].ptrs(), wd.ptrs(), mbs, K, 256, ws["hpart"].data_ptr(), ws["S"], st)
-        h.x3_heads_ppo(ws["hpart"].data_ptr(), ws["S"], bd.ptrs(), wh.ptrs(), bh.ptrs(), full["cols"].data_ptr(),
-                       self.coef.data_ptr(), self.acc.data_ptr(), self._one.data_ptr(), mbs, A1, ws["dz"].ptrs(),
-                       ws["dpre"].ptrs(), ws["hid"].ptrs(), st, cidx=idx.data_ptr(), ctr=ctr.data_ptr(),
-                       period=int(period))
+        h.x3_heads_ppo(ws["hpart"].data_ptr(), ws["S"], bd.ptrs(), wh.ptrs(), bh.ptrs(),
+                       (colsg if gather else cols).data_ptr(), self.coef.data_ptr(), self.acc.data_ptr(),
+                       self._one.data_ptr(), mbs, A1, ws["dz"].ptrs(), ws["dpre"].ptrs(), ws["hid"].ptrs(), st,
+                       cidx=0 if gather else idx.data_ptr(), ctr=0 if gather else ctr.data_ptr(), period=int(period))
         g = [p._rmm_grad_out for p in self.params]
         h.x3_dense_heads_bwd(ws["dz"].ptrs(), A1, ws["hid"].ptrs(), ws["h2"].ptrs(), wd.ptrs(), ws["dpre"].ptrs(), mbs,
                              K, ws["dx"].ptrs(), g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr(), st)
