@@ -182,14 +182,20 @@ class SampleIngest:
             bo += n
         if segs:  # K1: every device-side fragment column into the learner tables, one launch
             h.multi_copy(segs, stream)
-        blocks = torch.from_numpy(table.view(np.uint8).reshape(-1)).to(self.device, non_blocking=False)
+        key = table.tobytes()
+        if getattr(self, "_blocks_key", None) != key:  # the fragment layout rarely changes: upload once
+            self._blocks = torch.from_numpy(table.view(np.uint8).reshape(-1)).to(self.device, non_blocking=False)
+            self._blocks_key = key
+        blocks = self._blocks
         self._stats.zero_()
         h.ingest_gae(raw.data_ptr(), boot.data_ptr(), blocks.data_ptr(), len(frags), A, self.gamma, self.lam,
                      cols.data_ptr(), self._stats.data_ptr(), stream)
         if standardize:
             h.standardize_col(cols.data_ptr(), N, A + 4, A + 1, self._stats.data_ptr(), stream)
-        # the host fragments (store views) may be released once the DMAs drained
-        torch.cuda.current_stream(self.device).synchronize()
+        if not on_dev:  # the host fragments (store views) may be released once the DMAs drained
+            torch.cuda.current_stream(self.device).synchronize()
+        # device fragments: their HBM objects stay referenced by the caller (the update call's arguments)
+        # until the update's final stats readback, so the copies need no host wait here
         return obs, cols
 
 
