@@ -27,6 +27,7 @@ Parity: no reference equivalent (the reference serializes CUDA tensors through h
 from __future__ import annotations
 
 import collections
+import math
 import os
 import pickle
 import struct
@@ -144,9 +145,52 @@ def put_tensor(worker, oid: bytes, t) -> None:
     nbytes = t.numel() * t.element_size()
     stream = torch.cuda.current_stream(dev).cuda_stream
     g.put_segments(oid, [(t.data_ptr(), nbytes)] if nbytes else [], _elem_bits(t.dtype), stream)
+    _publish_descriptor(worker, g, oid, dev, {"dtype": t.dtype, "shape": tuple(t.shape),
+                                              "requires_grad": t.requires_grad}, nbytes, stream, sealed=False)
+
+
+class GpuObjectHandle:
+    """A GPU object this process created in place (create_object) and published (publish_created): as a
+    task output or inside one it serializes as a reference to that object, with no copy."""
+
+    __slots__ = ("oid", "shape", "dtype")
+
+    def __init__(self, oid: bytes, shape, dtype):
+        self.oid, self.shape, self.dtype = oid, tuple(shape), dtype
+
+
+def create_object(worker, oid: bytes, shape, dtype, device: int) -> int:
+    """Allocate an unsealed GPU object of `shape` / `dtype` and return its device address: a producer
+    (e.g. the rollout kernels) writes it in place, then publish_created seals and publishes it."""
+    import torch
+
+    nbytes = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
+    return int(process_store(worker, device).create(oid, nbytes, _elem_bits(dtype)))
+
+
+def publish_created(worker, oid: bytes, shape, dtype, device: int, stream) -> GpuObjectHandle:
+    """Seal an object from create_object once `stream`'s work so far is done (its ready event) and publish
+    its descriptor; returns the handle to put in a task's output."""
+    import torch
+
+    g = process_store(worker, device)
+    g.seal(oid, stream)
+    nbytes = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
+    _publish_descriptor(worker, g, oid, device, {"dtype": dtype, "shape": tuple(shape), "requires_grad": False},
+                        nbytes, stream, sealed=True)
+    from ray_memory_management_amd._private import protocol as P
+
+    worker.send((P.GPU_OBJECT, oid))
+    return GpuObjectHandle(oid, shape, dtype)
+
+
+def _publish_descriptor(worker, g, oid: bytes, dev: int, meta_d: dict, nbytes: int, stream, sealed: bool) -> None:
+    """Write the host-store descriptor of GPU object `oid` (location, IPC handle, meta). sealed: the data is
+    complete once `stream` drains (seal now if the caller has synchronised, else on a host callback)."""
+    import torch
+
     slab, off, n = g.locate(oid)  # location is known at allocation time: no wait for the copy
     handle = g.slab_ipc_handle(slab) if slab >= 0 else b""
-    meta_d = {"dtype": t.dtype, "shape": tuple(t.shape), "requires_grad": t.requires_grad}
     meta = pickle.dumps(meta_d, protocol=5)
     hdr = _DESC.pack(store_ext().GPU_DESC_MAGIC, nbytes, slab, off, dev, os.getpid(),
                      handle.ljust(64, b"\0")[:64], pci_bus_id(dev).encode()[:16].ljust(16, b"\0"), len(meta))
@@ -158,7 +202,10 @@ def put_tensor(worker, oid: bytes, t) -> None:
     mv[len(hdr):len(hdr) + len(meta)] = meta
     del mv
     _meta_cache(worker)[oid] = meta_d
-    if (worker.config or {}).get("gpu_async_put", True):
+    if sealed:  # the producer's stream has drained (the caller synchronised): no callback needed
+        worker.store.seal(oid)
+        buf.release()
+    elif (worker.config or {}).get("gpu_async_put", True):
         buf.disown()  # the host callback seals + releases once the copy on `stream` is done
         g.seal_descriptor_async(oid, stream)
     else:

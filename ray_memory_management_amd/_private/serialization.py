@@ -72,6 +72,9 @@ class _Pickler(cloudpickle.CloudPickler):
             if ent is not None:
                 return _rebuild_custom, (ent[1], ent[0](obj))
         mod = t.__module__
+        if t.__name__ == "GpuObjectHandle" and mod.endswith("gpu_object_store"):
+            note_contained(obj.oid)  # already in the GPU store (created in place): a reference, no copy
+            return _rebuild_gpu_object, (obj.oid,)
         if mod == "torch" and t.__name__ in ("Tensor", "Parameter"):
             try:
                 import torch

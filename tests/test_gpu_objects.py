@@ -196,6 +196,49 @@ def test_nested_cuda_tensors_stay_in_hbm(gpu_ray):
     assert ray.get(total.remote(r)) == 256.0
 
 
+def test_object_created_in_place_is_returned_without_copy(gpu_ray):
+    """create_object / publish_created: an actor writes a GPU-store object in place (the hybrid rollout
+    worker's K10x stores its rows this way), returns its handle nested in a value, the driver reads it
+    zero-copy, and dropping the reference frees the HBM."""
+    import torch
+
+    @ray.remote(num_gpus=1)
+    class Producer:
+        def make(self, k):
+            from ray_memory_management_amd._native import require_hip
+            from ray_memory_management_amd._private import gpu_object_store as gos
+            from ray_memory_management_amd._private import ids
+            from ray_memory_management_amd._private.worker import global_worker as w
+
+            src = torch.arange(3 * 1000, device="cuda", dtype=torch.int32).reshape(3, 1000) + k
+            oid = ids.new_put_id()
+            ptr = gos.create_object(w, oid, (3, 1000), torch.int32, 0)
+            s = torch.cuda.current_stream()
+            require_hip().memcpy_async(ptr, src.data_ptr(), src.numel() * 4, s.cuda_stream)
+            s.synchronize()
+            puts = gos.stats(w)
+            h = gos.publish_created(w, oid, (3, 1000), torch.int32, 0, s.cuda_stream)
+            return {"x": h, "k": k, "puts": sum(v["puts"] for v in puts.values())}
+
+        def n_objects(self):
+            from ray_memory_management_amd._private import gpu_object_store as gos
+            from ray_memory_management_amd._private.worker import global_worker as w
+
+            return sum(v["num_objects"] for v in gos.stats(w).values())
+
+    p = Producer.remote()
+    for k in range(3):
+        d = ray.get(p.make.remote(k))
+        assert d["k"] == k and d["x"].is_cuda and d["x"].dtype == torch.int32 and d["x"].shape == (3, 1000)
+        assert torch.equal(d["x"].cpu(), torch.arange(3000, dtype=torch.int32).reshape(3, 1000) + k)
+        assert d["puts"] == k + 1  # one store allocation per call: the handle was not copied again
+        del d
+    deadline = time.time() + 20
+    while time.time() < deadline and ray.get(p.n_objects.remote()) > 0:
+        time.sleep(0.1)
+    assert ray.get(p.n_objects.remote()) == 0
+
+
 def test_cross_gpu_pull_path_with_quota(gpu_ray):
     """Forced peer path (RMM_TEST_FORCE_PEER_COPY): the consumer imports the owner's slab and DMAs
     the object into its own memory under the pull quota instead of aliasing it."""
