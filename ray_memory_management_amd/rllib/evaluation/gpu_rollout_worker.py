@@ -560,136 +560,76 @@ class HybridRolloutWorker(GPURolloutWorker):
             server = self._server_args(G, S)
             direct = None if server is not None else self._direct_args(G, S)
             native = None if (server is not None or direct is not None) else self._native_loop(G, S)
-            inplace = self._inplace_rows(G) if direct is not None else None
-            if inplace is not None:
-                direct["bufs"][2] = inplace[1]  # K10x stores the rows straight into the fragment's object
-            try:
-                frag = self._sample_loops(G, S, T, st, shared, server, direct, native, dbg, t0,
-                                          pack_fragment_device)
-            except BaseException:
-                if inplace is not None:
-                    self._drop_inplace(inplace[0])
-                raise
-            if inplace is not None:
-                from ray_memory_management_amd._private import gpu_object_store as gos
-                from ray_memory_management_amd._private import worker as _w
+            if direct is not None:  # the native loop, launching the step's kernels directly
+                from ray_memory_management_amd._native import require_hip
 
-                g = G[0]
-                frag["obs"] = gos.publish_created(_w.global_worker, inplace[0], (T * g.buf_obs.shape[1],)
-                                                  + tuple(g.buf_obs.shape[2:]), torch.uint8, self.device.index,
-                                                  st.cuda_stream)
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
+                spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
+                self._completed.extend(require_hip().hybrid_rollout_direct(**direct, T=T, threads=max(1, th),
+                                                                          spin=spin))
+                if "gate_err" in direct and int(self._gate_err.item()):
+                    self._gate_err.zero_()  # a gated step gave up waiting: it ran on stale frames
+                    raise RuntimeError("rollout step gate timed out during this fragment; fragment discarded")
+            elif server is not None:  # K21: the whole fragment in ONE persistent kernel launch
+                from ray_memory_management_amd._native import require_hip
+
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
+                try:
+                    self._completed.extend(require_hip().hybrid_rollout_server(**server, T=T, threads=max(1, th)))
+                except RuntimeError:
+                    # a server timeout (e.g. another process held the CUs) aborts this fragment; the
+                    # worker falls back to the per-step graph loop for good
+                    self._server_off = True
+                    raise
+            elif native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
+                from ray_memory_management_amd._native import require_hip
+
+                # rollout_env_threads (default 1) splits each env step over that many CPU threads; measured
+                # neutral for the synthetic env (profiles/native_rollout_r3.txt); RMM_ENV_THREADS overrides
+                th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
+                # blocking event waits by default: a bounded poll was faster on an idle host but gave
+                # outliers when the host's CPUs were shared (profiles/native_rollout_r3.txt)
+                spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
+                self._completed.extend(require_hip().hybrid_rollout(native, T, threads=max(1, th), spin=spin))
+            else:
+                self._python_loop(G, S, T, st, shared)
+            if dbg:
+                import sys
+
+                torch.cuda.synchronize(self.device)
+                print(f"[hybrid-worker pid {os.getpid()}] fragment loop ok", file=sys.stderr, flush=True)
+            t_loop = time.perf_counter()
+            self._loop_time = getattr(self, "_loop_time", 0.0) + (t_loop - t0)
+            with torch.cuda.stream(st):
+                for gs in dict.fromkeys(S):
+                    if gs is not st:
+                        st.wait_stream(gs)
+                parts = []
+                for g in G:
+                    if g.device_stack:  # observation after the last env step (pushed next fragment)
+                        g.s_new.copy_(g.h_new, non_blocking=True)
+                        stack = g.buf_obs[T - 1] if g.band else g.s_obs  # the last step's frame stack
+                        last_v = bootstrap_value(self.model, torch.cat([stack[:, 1:], g.s_new.unsqueeze(1)], dim=1))
+                    else:
+                        g.s_obs.copy_(g.h_obs, non_blocking=True)
+                        last_v = bootstrap_value(self.model, g.s_obs)
+                    parts.append((g.buf_obs, g.buf_logits, g.buf_logp, g.buf_vf,
+                                  g.h_rew.to(self.device, non_blocking=True),
+                                  g.h_done.to(self.device, non_blocking=True), g.buf_act, last_v.reshape(-1)))
+                if len(parts) == 1:
+                    frag = pack_fragment_device(*parts[0])
+                else:  # time-major [T, n]: the groups' env columns side by side
+                    cat = [torch.cat(xs, dim=0 if k == 7 else 1) for k, xs in enumerate(zip(*parts))]
+                    frag = pack_fragment_device(*cat)
+            st.synchronize()
+            for g in G:  # a gated step that timed out ran on stale frames: never hand that fragment out
+                if g.gate and int(g.gate_err.item()):
+                    g.gate_err.zero_()
+                    raise RuntimeError("rollout step gate timed out during this fragment (a policy step ran "
+                                       "without its frames); fragment discarded")
         self._sample_time += time.perf_counter() - t0
         if stamps is not None:
             stamps.append(("sample_end", time.time()))
-        return frag
-
-    def _inplace_rows(self, G):
-        """(oid, device address) of a fresh GPU-store object for this fragment's observation rows, or None.
-        The direct rollout loop writes the rows into it and sample() publishes it as the fragment's "obs",
-        so the task return needs no 141 MB copy into the store nor a host-callback seal (one env group with
-        device frame stacks, not band mode, inside a worker process whose returns go to the GPU store).
-        Opt-in (RMM_FRAG_INPLACE=1): measured no faster end to end, the hand-off gained 0.05 ms but the
-        learner's resolve / the sample loop lost about as much (profiles/handoff_r5.txt)."""
-        from ray_memory_management_amd._private import worker as _w
-
-        cw = _w.global_worker
-        if (os.environ.get("RMM_FRAG_INPLACE", "0") != "1" or len(G) != 1 or not G[0].device_stack or G[0].band
-                or cw is None or cw.mode != _w.WORKER_MODE or cw.current_actor_id is None
-                or not cw.config.get("gpu_object_store", True) or not cw.config.get("gpu_nested_tensors", True)):
-            return None
-        import torch
-
-        from ray_memory_management_amd._private import gpu_object_store as gos
-        from ray_memory_management_amd._private import ids as _ids
-
-        oid = _ids.new_put_id()
-        shape = (self.T * G[0].buf_obs.shape[1],) + tuple(G[0].buf_obs.shape[2:])
-        return oid, gos.create_object(cw, oid, shape, torch.uint8, self.device.index)
-
-    def _drop_inplace(self, oid):
-        import torch
-
-        from ray_memory_management_amd._private import gpu_object_store as gos
-        from ray_memory_management_amd._private import worker as _w
-
-        torch.cuda.synchronize(self.device)  # no kernel may still write the rows
-        g = gos.process_store(_w.global_worker, self.device.index)
-        g.seal(oid, torch.cuda.current_stream(self.device).cuda_stream)
-        g.delete(oid)
-
-    def _sample_loops(self, G, S, T, st, shared, server, direct, native, dbg, t0, pack_fragment_device):
-        """sample()'s T-step loop (direct / server / native / Python) and the fragment packing."""
-        import time
-
-        import torch
-
-        if direct is not None:  # the native loop, launching the step's kernels directly
-            from ray_memory_management_amd._native import require_hip
-
-            th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
-            spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
-            self._completed.extend(require_hip().hybrid_rollout_direct(**direct, T=T, threads=max(1, th),
-                                                                      spin=spin))
-            if "gate_err" in direct and int(self._gate_err.item()):
-                self._gate_err.zero_()  # a gated step gave up waiting: it ran on stale frames
-                raise RuntimeError("rollout step gate timed out during this fragment; fragment discarded")
-        elif server is not None:  # K21: the whole fragment in ONE persistent kernel launch
-            from ray_memory_management_amd._native import require_hip
-
-            th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
-            try:
-                self._completed.extend(require_hip().hybrid_rollout_server(**server, T=T, threads=max(1, th)))
-            except RuntimeError:
-                # a server timeout (e.g. another process held the CUs) aborts this fragment; the
-                # worker falls back to the per-step graph loop for good
-                self._server_off = True
-                raise
-        elif native is not None:  # the whole T-step loop in C++ (csrc/hip/rollout_loop.cc)
-            from ray_memory_management_amd._native import require_hip
-
-            # rollout_env_threads (default 1) splits each env step over that many CPU threads; measured
-            # neutral for the synthetic env (profiles/native_rollout_r3.txt); RMM_ENV_THREADS overrides
-            th = int(os.environ.get("RMM_ENV_THREADS") or self.config.get("rollout_env_threads", 1) or 1)
-            # blocking event waits by default: a bounded poll was faster on an idle host but gave
-            # outliers when the host's CPUs were shared (profiles/native_rollout_r3.txt)
-            spin = os.environ.get("RMM_NATIVE_SPIN", "0") == "1"
-            self._completed.extend(require_hip().hybrid_rollout(native, T, threads=max(1, th), spin=spin))
-        else:
-            self._python_loop(G, S, T, st, shared)
-        if dbg:
-            import sys
-
-            torch.cuda.synchronize(self.device)
-            print(f"[hybrid-worker pid {os.getpid()}] fragment loop ok", file=sys.stderr, flush=True)
-        t_loop = time.perf_counter()
-        self._loop_time = getattr(self, "_loop_time", 0.0) + (t_loop - t0)
-        with torch.cuda.stream(st):
-            for gs in dict.fromkeys(S):
-                if gs is not st:
-                    st.wait_stream(gs)
-            parts = []
-            for g in G:
-                if g.device_stack:  # observation after the last env step (pushed next fragment)
-                    g.s_new.copy_(g.h_new, non_blocking=True)
-                    stack = g.buf_obs[T - 1] if g.band else g.s_obs  # the last step's frame stack
-                    last_v = bootstrap_value(self.model, torch.cat([stack[:, 1:], g.s_new.unsqueeze(1)], dim=1))
-                else:
-                    g.s_obs.copy_(g.h_obs, non_blocking=True)
-                    last_v = bootstrap_value(self.model, g.s_obs)
-                parts.append((g.buf_obs, g.buf_logits, g.buf_logp, g.buf_vf,
-                              g.h_rew.to(self.device, non_blocking=True),
-                              g.h_done.to(self.device, non_blocking=True), g.buf_act, last_v.reshape(-1)))
-            if len(parts) == 1:
-                frag = pack_fragment_device(*parts[0])
-            else:  # time-major [T, n]: the groups' env columns side by side
-                cat = [torch.cat(xs, dim=0 if k == 7 else 1) for k, xs in enumerate(zip(*parts))]
-                frag = pack_fragment_device(*cat)
-        st.synchronize()
-        for g in G:  # a gated step that timed out ran on stale frames: never hand that fragment out
-            if g.gate and int(g.gate_err.item()):
-                g.gate_err.zero_()
-                raise RuntimeError("rollout step gate timed out during this fragment (a policy step ran "
-                                   "without its frames); fragment discarded")
         return frag
 
     def phase_stamps(self, on: bool = True):

@@ -37,6 +37,28 @@ def test_two_learner_actors_stay_identical(ray_start):
         algo.stop()
 
 
+def test_four_learner_actors_stay_identical():
+    """A wider data-parallel group (the 1-node bench runs one learner per GPU, up to 8): four gloo
+    learners, one rollout worker each, stay bit-identical and train on every worker's samples."""
+    import ray_memory_management_amd as ray
+
+    ray.init(num_cpus=8, object_store_memory=256 << 20)
+    try:
+        algo = _cfg(n_learners=4, workers=4).build()
+        try:
+            for _ in range(2):
+                r = algo.train()
+            st = r["info"]["learner"]["default_policy"]["learner_stats"]
+            assert st["num_learners"] == 4 and np.isfinite(st["total_loss"])
+            assert r["num_env_steps_trained"] >= 64
+            d = algo.learner_group.weights_digests()
+            assert len(d) == 4 and len(set(d)) == 1
+        finally:
+            algo.stop()
+    finally:
+        ray.shutdown()
+
+
 def test_learner_actor_checkpoint_roundtrip(ray_start, tmp_path):
     algo = _cfg(n_learners=1, workers=1).build()
     try:
