@@ -40,7 +40,8 @@ template <typename TG, bool VEC, int U>
 __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __restrict__ m1, float* __restrict__ m2,
                                           const TG* __restrict__ grad, __hip_bfloat16* __restrict__ wbf16,
                                           float grad_scale, const AdamCoef& c, int64_t tid, int64_t nthr, int64_t n,
-                                          __hip_bfloat16* __restrict__ wlo = nullptr) {
+                                          __hip_bfloat16* __restrict__ wlo = nullptr,
+                                          const float* __restrict__ grad2 = nullptr) {
   int64_t scalar_from = 0;
   if constexpr (VEC) {
     const int64_t nv = n >> 2;
@@ -53,6 +54,10 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
         if (v < nv) {
           const int64_t i = v << 2;
           adam_load4(grad, i, g[u]);
+          if (grad2) {  // a second partial of the same gradient (K12x row parts), added in a fixed order
+            const float4 q = *reinterpret_cast<const float4*>(grad2 + i);
+            g[u][0] += q.x, g[u][1] += q.y, g[u][2] += q.z, g[u][3] += q.w;
+          }
           w[u] = *reinterpret_cast<const float4*>(master + i);
           a[u] = *reinterpret_cast<const float4*>(m1 + i);
           b[u] = *reinterpret_cast<const float4*>(m2 + i);
@@ -81,7 +86,7 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
   }
   for (int64_t i = scalar_from + tid; i < n; i += nthr) {
     float a = m1[i], b = m2[i];
-    const float w = adam_one(master[i], adam_ld1(grad, i) * grad_scale, a, b, c);
+    const float w = adam_one(master[i], (grad2 ? adam_ld1(grad, i) + grad2[i] : adam_ld1(grad, i)) * grad_scale, a, b, c);
     m1[i] = a;
     m2[i] = b;
     master[i] = w;

@@ -85,6 +85,9 @@ struct X3Adam {
   int nbump = 0;
   uint32_t* done = nullptr;
   int64_t* bump_next = nullptr;
+  // K12x row parts (rs = 2): the second part's dense + heads gradients, element n_trunk + i at grad2[i];
+  // the Adam workgroups use grad[n_trunk + i] + grad2[i]
+  const float* grad2 = nullptr;
 };
 
 // XCD-aware remap of a linear workgroup id (bijective for any grid size): consecutive

@@ -690,10 +690,14 @@ PYBIND11_MODULE(_hip, m) {
                            uint64_t stream, std::vector<uint64_t> adam, float grad_scale) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_bwd: 4 strides per weight");
     // adam (optional, the tail Adam): [master, m1, m2, grad, whi, wlo, n_trunk, n, hp, step_ctr, bump, nbump,
-    // done, bump_next]
+    // done, bump_next(, grad2: the K12x second row part's dense + heads gradients)]
     X3Adam xa;
     if (!adam.empty()) {
-      if (adam.size() != 14) throw std::invalid_argument("x3_trunk_bwd: adam needs 14 fields");
+      if (adam.size() != 14 && adam.size() != 15) throw std::invalid_argument("x3_trunk_bwd: adam needs 14 or 15 fields");
+      if (adam.size() == 15 && adam[14]) {
+        if (adam[14] & 15) throw std::invalid_argument("x3_trunk_bwd: grad2 must be 16-byte aligned");
+        xa.grad2 = P<const float>(adam[14]);
+      }
       xa.master = P<float>(adam[0]), xa.m1 = P<float>(adam[1]), xa.m2 = P<float>(adam[2]);
       xa.grad = P<const float>(adam[3]), xa.whi = P<void>(adam[4]), xa.wlo = P<void>(adam[5]);
       xa.n_trunk = int64_t(adam[6]), xa.n = int64_t(adam[7]);
@@ -733,10 +737,14 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"), py::arg("lout"), py::arg("act_now"), py::arg("B"),
      py::arg("A1"), py::arg("stream"), py::arg("done") = 0, py::arg("host_seq") = 0);
   m.def("x3_dense_heads_bwd", [](XP dz, int A1, XP y, XP x, XP w, XP dpre, int64_t M, int64_t K, XP dx, uint64_t dw,
-                                 uint64_t db, uint64_t dwh, uint64_t dbh, uint64_t stream) {
+                                 uint64_t db, uint64_t dwh, uint64_t dbh, uint64_t stream, int rs, uint64_t dw2,
+                                 uint64_t db2, uint64_t dwh2, uint64_t dbh2) {
     x3_dense_heads_bwd(xin(dz), A1, xin(y), xin(x), xin(w), xin(dpre), M, K, xout(dx), P<float>(dw), P<float>(db),
-                       P<float>(dwh), P<float>(dbh), S(stream));
-  });
+                       P<float>(dwh), P<float>(dbh), S(stream), rs, dw2 ? P<float>(dw2) : nullptr,
+                       db2 ? P<float>(db2) : nullptr, dwh2 ? P<float>(dwh2) : nullptr, dbh2 ? P<float>(dbh2) : nullptr);
+  }, py::arg("dz"), py::arg("A1"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("dpre"), py::arg("M"), py::arg("K"),
+     py::arg("dx"), py::arg("dw"), py::arg("db"), py::arg("dwh"), py::arg("dbh"), py::arg("stream"), py::arg("rs") = 1,
+     py::arg("dw2") = 0, py::arg("db2") = 0, py::arg("dwh2") = 0, py::arg("dbh2") = 0);
 
   // ---------------------------------------------------------------- IPC
   m.def("ipc_open", [](py::bytes handle, int device) {

@@ -241,9 +241,11 @@ void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const fl
 void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const int64_t* t_ptr, const int64_t* ctr,
                      uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B, int A1,
                      hipStream_t stream, unsigned int* done = nullptr, int64_t* host_seq = nullptr);
-// K12x: dx (split pair) and fp32 dW, db, dWh, dbh
+// K12x: dx (split pair) and fp32 dW, db, dWh, dbh. rs = 2: two row parts, the second one's dW / db / dWh / dbh
+// into dw2 / db2 / dwh2 / dbh2 (summed by the tail Adam, X3Adam::grad2)
 void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int64_t M, int64_t K, X3Out dx, float* dw,
-                        float* db, float* dwh, float* dbh, hipStream_t stream);
+                        float* db, float* dwh, float* dbh, hipStream_t stream, int rs = 1, float* dw2 = nullptr,
+                        float* db2 = nullptr, float* dwh2 = nullptr, float* dbh2 = nullptr);
 // fp32 -> split pair (weights after a host-side update, tests)
 void x3_split(const float* src, void* hi, void* lo, int64_t n, hipStream_t stream);
 

@@ -602,7 +602,7 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     const int64_t nthr = int64_t(gridDim.x - nred) * blockDim.x;
     adam_span<float, true, 2>(xa.master + o, xa.m1 + o, xa.m2 + o, xa.grad + o,
                               static_cast<__hip_bfloat16*>(xa.whi) + o, xa.grad_scale, ac, tid, nthr, xa.n - o,
-                              static_cast<__hip_bfloat16*>(xa.wlo) + o);
+                              static_cast<__hip_bfloat16*>(xa.wlo) + o, xa.grad2);
     x3_tail_bump(xa);
     return;
   }
@@ -1174,13 +1174,13 @@ constexpr int K12X_LDS = K12X_COLS > K12X_HEAD ? K12X_COLS : K12X_HEAD;
 static_assert(K12X_LDS * 2 <= 160 * 1024, "K12x LDS");
 
 __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t M, int64_t K, int64_t J0, Pair dx,
-                                          float* __restrict__ dw, unsigned short* lds) {
+                                          float* __restrict__ dw, unsigned short* lds, int c0, int c1) {
   unsigned short* dm = lds;                       // [plane][m][DMP]
   unsigned short* xs = lds + 2 * IMG;             // [plane][jt][m][16]
   unsigned short* ws = xs + 2 * 2 * MC * 16;      // [plane][jt][h][16]  (setup)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int q = r >> 2, p = r & 3;
-  const int NC = int((M + MC - 1) / MC);
+  const int64_t Mend = min(M, int64_t(c1) * MC);  // rows [c0 MC, Mend): this workgroup's row part
   // two register stages: chunk c + 2's loads are issued while chunk c computes. Loads are unconditional
   // from clamped rows, masked at the LDS store, so the compiler's vmcnt counting never drains a stage
   uint4 sdh[2][4], sdl[2][4], sxh[2], sxl[2];
@@ -1203,13 +1203,13 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int v = tid + NT * k, row = v >> 5, pc = v & 31;
-      const bool ok = m0 + row < M;
+      const bool ok = m0 + row < Mend;
       *reinterpret_cast<uint4*>(&dm[row * DMP + 8 * pc]) = keep_if(ok, sdh[st][k]);
       *reinterpret_cast<uint4*>(&dm[IMG + row * DMP + 8 * pc]) = keep_if(ok, sdl[st][k]);
     }
     if (tid < MC * 4) {
       const int row = tid >> 2, pc = tid & 3;
-      const bool ok = m0 + row < M;
+      const bool ok = m0 + row < Mend;
       const int o = ((pc >> 1) * MC + row) * 16 + 8 * (pc & 1);
       *reinterpret_cast<uint4*>(&xs[o]) = keep_if(ok, sxh[st]);
       *reinterpret_cast<uint4*>(&xs[2 * MC * 16 + o]) = keep_if(ok, sxl[st]);
@@ -1223,8 +1223,8 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
       wvh[k] = *reinterpret_cast<const uint4*>(&w.hi[int64_t(h) * K + J0 + 8 * pc]);
       wvl[k] = *reinterpret_cast<const uint4*>(&w.lo[int64_t(h) * K + J0 + 8 * pc]);
     }
-    load(0, 0);
-    load(1, min(1, NC - 1));
+    load(0, c0);
+    load(1, min(c0 + 1, c1 - 1));
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int v = tid + NT * k, h = v >> 2, pc = v & 3;
@@ -1244,7 +1244,7 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
   auto chunk = [&](int st, int c) {
     store(st, c);
     __syncthreads();
-    load(st, min(c + 2, NC - 1));  // in flight during this and the next chunk's MFMAs
+    load(st, min(c + 2, c1 - 1));  // in flight during this and the next chunk's MFMAs
     {  // dxᵀ tile: D[j][m] = Σ_h Wᵀ[j][h] dpre[m][h]
       Acc a = acc0();
       const int ro = (16 * mt + r) * DMP + 8 * g;
@@ -1255,7 +1255,7 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
              ld8(&dm[IMG + ro + 32 * s]));
       }
       const int64_t row = int64_t(c) * MC + 16 * mt + r;
-      if (row < M) {
+      if (row < Mend) {
         const f32x4 t = total(a);
         const float v[4] = {t[0], t[1], t[2], t[3]};
         store4(dx, row * K + J0 + 16 * nt + 4 * g, v);
@@ -1281,7 +1281,7 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
     }
     __syncthreads();  // chunk images free
   };
-  for (int c = 0; c < NC; c += 2) {  // pairs of chunks; an odd NC runs one all-zero chunk past the end
+  for (int c = c0; c < c1; c += 2) {  // pairs of chunks; an odd count runs one all-zero chunk past the end
     chunk(0, c);
     chunk(1, c + 1);
   }
@@ -1301,13 +1301,13 @@ __device__ __forceinline__ void k12x_cols(CPair x, CPair w, CPair dpre, int64_t 
 template <int A1>
 __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t M, float* __restrict__ db,
                                           float* __restrict__ dwh, float* __restrict__ dbh, unsigned short* lds,
-                                          int hq) {
+                                          int hq, int c0, int c1) {
   unsigned short* dm = lds;                  // [plane][m][HQP]
   unsigned short* ys = lds + 2 * MC * HQP;   // [plane][m][HQP]
   unsigned short* zs = lds + 4 * MC * HQP;   // [plane][m][16] (a >= A1 and rows >= M zero)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int q = r >> 2, p = r & 3, ht = wave & 3, ks = wave >> 2;
-  const int NC = int((M + MC - 1) / MC);
+  const int64_t Mend = min(M, int64_t(c1) * MC);
   const int64_t h0 = int64_t(hq) * HQ;
   // 64 rows x 64 h x 4 planes = 32 KB per chunk: one uint4 per plane per thread; two stages
   uint4 sd[2][2], sy[2][2];
@@ -1329,7 +1329,7 @@ __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t
   };
   auto store = [&](int st, int c) {
     const int64_t m0 = int64_t(c) * MC;
-    const bool ok = m0 + lrow < M;
+    const bool ok = m0 + lrow < Mend;
     const int o = lrow * HQP + 8 * lpc;
     *reinterpret_cast<uint4*>(&dm[o]) = keep_if(ok, sd[st][0]);
     *reinterpret_cast<uint4*>(&dm[MC * HQP + o]) = keep_if(ok, sd[st][1]);
@@ -1338,7 +1338,7 @@ __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int e = tid + NT * k, m = e >> 4, a = e & 15;
-      const bool okz = m0 + m < M && a < A1;
+      const bool okz = m0 + m < Mend && a < A1;
       zs[e] = okz ? zh[st][k] : static_cast<unsigned short>(0);
       zs[MC * 16 + e] = okz ? zl[st][k] : static_cast<unsigned short>(0);
     }
@@ -1349,12 +1349,12 @@ __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t
   const bf16x8 ones = as_bf(onev);  // as A: row 0 all ones; as B: column 0 all ones
   const bool want_bh = hq == 0 && ht == 0;
   Acc awh = acc0(), adb = acc0(), abh = acc0();
-  load(0, 0);
-  load(1, min(1, NC - 1));
+  load(0, c0);
+  load(1, min(c0 + 1, c1 - 1));
   auto chunk = [&](int st, int c) {
     store(st, c);
     __syncthreads();
-    load(st, min(c + 2, NC - 1));
+    load(st, min(c + 2, c1 - 1));
     const unsigned short* pz = &zs[(32 * ks + 4 * g + q) * 16 + 4 * p];
     const bf16x8 azh = tr8(pz, pz + 16 * 16), azl = tr8(pz + MC * 16, pz + MC * 16 + 16 * 16);
     const int off = (32 * ks + 4 * g + q) * HQP + 16 * ht + 4 * p;
@@ -1368,7 +1368,7 @@ __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t
     }
     __syncthreads();
   };
-  for (int c = 0; c < NC; c += 2) {  // an odd NC runs one all-zero chunk past the end
+  for (int c = c0; c < c1; c += 2) {  // an odd count runs one all-zero chunk past the end
     chunk(0, c);
     chunk(1, c + 1);
   }
@@ -1398,21 +1398,28 @@ __device__ __forceinline__ void k12x_head(CPair dz, CPair y, CPair dpre, int64_t
   }
 }
 
+// Row parts: with rs = 2 every column / head workgroup exists twice, each over half of the 64-row chunks;
+// part 0 writes dW / db / dWh / dbh in place, part 1 into the second slab (same layout), and the next
+// launch's Adam workgroups add the two (x3 trunk reduce, X3Adam::grad2) — no merge inside this launch (an
+// in-launch merge measured slower: its agent-scope release / acquire writes back and invalidates the XCD's
+// L2 under the workgroups still streaming dpre, 21.8 -> 34.7 us at M = 500, profiles/x3_kernels_r5.txt).
 template <int A1>
 __global__ __launch_bounds__(NT) void k_dense_heads_bwd_x3(CPair dz, CPair y, CPair x, CPair w, CPair dpre, int64_t M,
                                                            int64_t K, Pair dx, float* __restrict__ dw,
                                                            float* __restrict__ db, float* __restrict__ dwh,
-                                                           float* __restrict__ dbh) {
+                                                           float* __restrict__ dbh, int rs, float* __restrict__ dw2,
+                                                           float* __restrict__ db2, float* __restrict__ dwh2,
+                                                           float* __restrict__ dbh2) {
   __shared__ __attribute__((aligned(16))) unsigned short lds[K12X_LDS];
-  // grid: K / JB column workgroups, then H / HQ head workgroups. (A row split of the columns, dW partials
-  // merged in-launch, measured slower: the agent-scope release / acquire of the merge writes back and
-  // invalidates the XCD's L2 under every other workgroup still streaming dpre, 21.8 -> 34.7 us at M = 500,
-  // profiles/x3_kernels_r5.txt)
-  const int NJ = int(K / JB), b = blockIdx.x;
-  if (b >= NJ)
-    k12x_head<A1>(dz, y, dpre, M, db, dwh, dbh, lds, b - NJ);
+  // grid: rs x K / JB column workgroups, then rs x H / HQ head workgroups
+  const int NJ = int(K / JB), b = blockIdx.x, NC = int((M + MC - 1) / MC);
+  const bool head = b >= NJ * rs;
+  const int i = head ? b - NJ * rs : b, per = head ? H / HQ : NJ, part = i / per, j = i - part * per;
+  const int c0 = NC * part / rs, c1 = NC * (part + 1) / rs;
+  if (head)
+    k12x_head<A1>(dz, y, dpre, M, part ? db2 : db, part ? dwh2 : dwh, part ? dbh2 : dbh, lds, j, c0, c1);
   else
-    k12x_cols(x, w, dpre, M, K, int64_t(b) * JB, dx, dw, lds);
+    k12x_cols(x, w, dpre, M, K, int64_t(j) * JB, dx, part ? dw2 : dw, lds, c0, c1);
 }
 
 }  // namespace x3
@@ -1530,18 +1537,22 @@ void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const
 }
 
 void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int64_t M, int64_t K, X3Out dx, float* dw,
-                        float* db, float* dwh, float* dbh, hipStream_t stream) {
+                        float* db, float* dwh, float* dbh, hipStream_t stream, int rs, float* dw2, float* db2,
+                        float* dwh2, float* dbh2) {
   if (M <= 0) return;
   if (K % x3::JB != 0) throw std::invalid_argument("x3_dense_heads_bwd: K must be a multiple of 32");
   if (A1 < 1 || A1 > dense::AMAX) throw std::invalid_argument("x3_dense_heads_bwd: 1 <= A+1 <= 16");
   for (const X3In* p : {&dz, &y, &x, &w, &dpre})
     if (!p->hi || !p->lo) throw std::invalid_argument("x3_dense_heads_bwd: inputs need hi and lo planes");
   if (!dx.hi || !dx.lo || !dw || !db || !dwh || !dbh) throw std::invalid_argument("x3_dense_heads_bwd: outputs");
-  const dim3 grid(uint32_t(K / x3::JB + x3::H / x3::HQ)), block(x3::NT);
+  if (rs != 1 && rs != 2) throw std::invalid_argument("x3_dense_heads_bwd: rs (row parts) is 1 or 2");
+  if (rs == 2 && (!dw2 || !db2 || !dwh2 || !dbh2 || (M + x3::MC - 1) / x3::MC < 2))
+    throw std::invalid_argument("x3_dense_heads_bwd: rs = 2 needs the second slab's outputs and >= 2 row chunks");
+  const dim3 grid(uint32_t(rs * (K / x3::JB + x3::H / x3::HQ))), block(x3::NT);
 #define RMM_K12X(N)                                                                                                 \
   case N:                                                                                                           \
     hipLaunchKernelGGL(x3::k_dense_heads_bwd_x3<N>, grid, block, 0, stream, cp(dz), cp(y), cp(x), cp(w), cp(dpre), M, \
-                       K, pp(dx), dw, db, dwh, dbh);                                                                \
+                       K, pp(dx), dw, db, dwh, dbh, rs, dw2, db2, dwh2, dbh2);                                      \
     break;
   switch (A1) {
     RMM_K12X(1) RMM_K12X(2) RMM_K12X(3) RMM_K12X(4) RMM_K12X(5) RMM_K12X(6) RMM_K12X(7) RMM_K12X(8)

@@ -438,8 +438,19 @@ class PPOLearner:
               "part": torch.empty(X3.trunk_partial_floats(mbs), dtype=torch.float32, device=dev),
               # the minibatch's loss columns, gathered by K10x so K15x reads them without the index chain
               "colsg": torch.empty((mbs, A1 + 3), dtype=torch.float32, device=dev)}
+        if self._manual is not None:  # K12x second row part's dense + heads gradients (see _x3_rows)
+            ws["grad2"] = torch.empty(self.n_params - self._manual, dtype=torch.float32, device=dev)
         self._mws = ws
         return ws
+
+    def _x3_rows(self, mbs) -> int:
+        """K12x row parts: 2 when the tail Adam consumes the dense + heads gradients (world of one, no clip)
+        and the minibatch has >= 4 chunks of 64 rows. Each column / head workgroup then streams half of
+        dpre (its bound); the second part's gradients go to a side slab that the tail Adam adds, so no
+        merge runs inside K12x. RMM_X3_K12_ROWS=1: one part."""
+        if not self._tail_adam() or (mbs + 63) // 64 < 4 or os.environ.get("RMM_X3_K12_ROWS", "2") == "1":
+            return 1
+        return 2
 
     def _x3_fwd_dense_bwd(self, full):
         """fp32 step, first half: K10x fwd → K13x → K15x (loss stats, dheads, dpre) → K12x (dense + heads
@@ -466,8 +477,16 @@ class PPOLearner:
                        self._one.data_ptr(), mbs, A1, ws["dz"].ptrs(), ws["dpre"].ptrs(), ws["hid"].ptrs(), st,
                        cidx=0 if gather else idx.data_ptr(), ctr=0 if gather else ctr.data_ptr(), period=int(period))
         g = [p._rmm_grad_out for p in self.params]
+        rs = self._x3_rows(mbs)
+        side = {}
+        if rs == 2:  # the second row part's outputs at the same offsets of the side slab
+            base, s2 = self.flat_grad.data_ptr() + 4 * self._manual, ws["grad2"].data_ptr()
+            side = dict(dw2=s2 + g[4].data_ptr() - base, db2=s2 + g[5].data_ptr() - base,
+                        dwh2=s2 + g[6].data_ptr() - base, dbh2=s2 + g[7].data_ptr() - base)
+        self._x3_grad2 = ws["grad2"].data_ptr() if rs == 2 else 0
         h.x3_dense_heads_bwd(ws["dz"].ptrs(), A1, ws["hid"].ptrs(), ws["h2"].ptrs(), wd.ptrs(), ws["dpre"].ptrs(), mbs,
-                             K, ws["dx"].ptrs(), g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr(), st)
+                             K, ws["dx"].ptrs(), g[4].data_ptr(), g[5].data_ptr(), g[6].data_ptr(), g[7].data_ptr(), st,
+                             rs=rs, **side)
 
     def _x3_trunk_bwd(self, full):
         """fp32 step, second half: K10x conv2 backward → conv1 weight gradient → reduce (fp32 trunk grads)."""
@@ -497,7 +516,7 @@ class PPOLearner:
             self._par ^= 1
         return [self.master.data_ptr(), self.m1.data_ptr(), self.m2.data_ptr(), self.flat_grad.data_ptr(),
                 self.w_x3.hi.data_ptr(), self.w_x3.lo.data_ptr(), self._manual, self.n_params, self.hp.data_ptr(),
-                cur + 8, cur, 2, 0 if parity else self._bump_done.data_ptr(), nxt]
+                cur + 8, cur, 2, 0 if parity else self._bump_done.data_ptr(), nxt, getattr(self, "_x3_grad2", 0)]
 
     def _x3_views_cached(self):
         key = (self.w_x3.hi.data_ptr(), self.w_x3.lo.data_ptr())

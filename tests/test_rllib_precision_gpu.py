@@ -104,6 +104,8 @@ def test_fp32_fast_learner_matches_torch_fp32_update(cuda):
     fast, ref = lns["fp32"], lns["torch"]
     assert fast.fast and fast.fp32 and fast.w_bf16 is None and not ref.fast
     assert fast.x3 and fast._manual is not None  # the hand-written split-bf16 SGD step, not autograd
+    # world of one, no clip: the tail Adam adds K12x's two row parts (256 rows = 4 chunks)
+    assert fast._x3_rows(256) == (2 if fast._tail_adam() else 1)
     g = torch.Generator(device=cuda).manual_seed(1)
     batch, _ = _batch(ref, 256, g, cuda)
     w0 = {k: v.float().cpu() for k, v in ref.get_weights().items()}

@@ -186,6 +186,48 @@ def test_x3_dense_heads_ppo_chain_matches_fp64(cuda, M, K, A):
     assert max(errs.values()) < GRAD_TOL, errs
 
 
+@pytest.mark.parametrize("M,K,A", [(500, 3872, 4), (130, 64, 15), (257, 96, 5)])
+def test_x3_dense_heads_bwd_row_parts(cuda, M, K, A):
+    """K12x with two row parts (rs = 2): the second part's dW / db / dWh / dbh land in their own slab;
+    part 0 + part 1 match one part to fp32 rounding and float64 autograd, dx is bit-identical (per row)."""
+    from ray_memory_management_amd._native import require_hip
+    from ray_memory_management_amd.ops import x3
+
+    h = require_hip()
+    torch.manual_seed(M + K + A)
+    A1 = A + 1
+    x = x3.split(torch.relu(torch.randn(M, K, device=cuda)))
+    W = x3.split(torch.randn(256, K, device=cuda) * (1.0 / K ** 0.5))
+    dz = x3.split(torch.randn(M, A1, device=cuda) * 0.1)
+    hid = x3.split(torch.relu(torch.randn(M, 256, device=cuda)))
+    dpre = x3.split(torch.randn(M, 256, device=cuda) * 0.1 * (hid.float() > 0))
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run(rs):
+        dx = x3.Pair.empty((M, K), cuda)
+        o = [torch.full((256, K), 7.0, device=cuda), torch.full((256,), 7.0, device=cuda),
+             torch.full((A1, 256), 7.0, device=cuda), torch.full((A1,), 7.0, device=cuda)]
+        o2 = [torch.full_like(t, 7.0) for t in o]
+        side = dict(dw2=o2[0].data_ptr(), db2=o2[1].data_ptr(), dwh2=o2[2].data_ptr(), dbh2=o2[3].data_ptr()) \
+            if rs == 2 else {}
+        h.x3_dense_heads_bwd(dz.ptrs(), A1, hid.ptrs(), x.ptrs(), W.ptrs(), dpre.ptrs(), M, K, dx.ptrs(),
+                             *[t.data_ptr() for t in o], s, rs=rs, **side)
+        torch.cuda.synchronize()
+        return dx, o, o2
+
+    dx1, one, _ = run(1)
+    dx2, p0, p1 = run(2)
+    assert torch.equal(dx1.hi, dx2.hi) and torch.equal(dx1.lo, dx2.lo)
+    xd, dpd, dzd, hd = x.float().double(), dpre.float().double(), dz.float().double(), hid.float().double()
+    ref = [dpd.t() @ xd, dpd.sum(0), dzd.t() @ hd, dzd.sum(0)]
+    for a, b_, u, r in zip(p0, p1, one, ref):
+        assert _rel(a + b_, r) < GRAD_TOL and _rel(u, r) < GRAD_TOL
+        assert _rel(a + b_, u) < 1e-5
+    with pytest.raises(ValueError):  # rs = 2 without the second slab
+        h.x3_dense_heads_bwd(dz.ptrs(), A1, hid.ptrs(), x.ptrs(), W.ptrs(), dpre.ptrs(), M, K, dx1.ptrs(),
+                             *[t.data_ptr() for t in one], s, rs=2)
+
+
 @pytest.mark.parametrize("B", [12, 50, 77])
 def test_x3_heads_sample_fp32_rows(cuda, B):
     """K16x: fp32 head rows (logits / value) vs float64, logp consistent with the logits and the
