@@ -161,23 +161,24 @@ class GpuObjectHandle:
 
 def create_object(worker, oid: bytes, shape, dtype, device: int) -> int:
     """Allocate an unsealed GPU object of `shape` / `dtype` and return its device address: a producer
-    (e.g. the rollout kernels) writes it in place, then publish_created seals and publishes it."""
+    (a kernel writing its output buffer) writes it in place, then publish_created seals and publishes it."""
     import torch
 
     nbytes = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
     return int(process_store(worker, device).create(oid, nbytes, _elem_bits(dtype)))
 
 
-def publish_created(worker, oid: bytes, shape, dtype, device: int, stream) -> GpuObjectHandle:
+def publish_created(worker, oid: bytes, shape, dtype, device: int, stream, synced: bool = False) -> GpuObjectHandle:
     """Seal an object from create_object once `stream`'s work so far is done (its ready event) and publish
-    its descriptor; returns the handle to put in a task's output."""
+    its descriptor; returns the handle to put in a task's output. The host descriptor is sealed by a host
+    callback after that work, or at once when the caller has already synchronised `stream` (synced)."""
     import torch
 
     g = process_store(worker, device)
     g.seal(oid, stream)
     nbytes = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
     _publish_descriptor(worker, g, oid, device, {"dtype": dtype, "shape": tuple(shape), "requires_grad": False},
-                        nbytes, stream, sealed=True)
+                        nbytes, stream, sealed=synced)
     from ray_memory_management_amd._private import protocol as P
 
     worker.send((P.GPU_OBJECT, oid))

@@ -197,9 +197,9 @@ def test_nested_cuda_tensors_stay_in_hbm(gpu_ray):
 
 
 def test_object_created_in_place_is_returned_without_copy(gpu_ray):
-    """create_object / publish_created: an actor writes a GPU-store object in place (the hybrid rollout
-    worker's K10x stores its rows this way), returns its handle nested in a value, the driver reads it
-    zero-copy, and dropping the reference frees the HBM."""
+    """create_object / publish_created: an actor writes a GPU-store object in place (a producer kernel's
+    output buffer), returns its handle nested in a value, the driver reads it zero-copy (descriptor sealed
+    at once after a sync, or by the host callback), and dropping the reference frees the HBM."""
     import torch
 
     @ray.remote(num_gpus=1)
@@ -215,9 +215,11 @@ def test_object_created_in_place_is_returned_without_copy(gpu_ray):
             ptr = gos.create_object(w, oid, (3, 1000), torch.int32, 0)
             s = torch.cuda.current_stream()
             require_hip().memcpy_async(ptr, src.data_ptr(), src.numel() * 4, s.cuda_stream)
-            s.synchronize()
+            if k == 1:  # the descriptor sealed at once (the copy is done) ...
+                s.synchronize()
             puts = gos.stats(w)
-            h = gos.publish_created(w, oid, (3, 1000), torch.int32, 0, s.cuda_stream)
+            # ... or by the host callback after the copy on `s`
+            h = gos.publish_created(w, oid, (3, 1000), torch.int32, 0, s.cuda_stream, synced=k == 1)
             return {"x": h, "k": k, "puts": sum(v["puts"] for v in puts.values())}
 
         def n_objects(self):
