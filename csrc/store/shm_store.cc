@@ -4,13 +4,17 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <signal.h>
+#include <linux/futex.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <cstring>
 #include <stdexcept>
 
@@ -19,7 +23,7 @@ namespace rmm {
 namespace {
 
 constexpr uint64_t kMagic = 0x524d4d53544f5245ull;  // "RMMSTORE"
-constexpr uint64_t kVersion = 6;  // 6: per-client pin records, Entry.io_pid / anon_pins
+constexpr uint64_t kVersion = 7;  // 6: per-client pin records, Entry.io_pid / anon_pins; 7: futex condition word
 constexpr uint64_t kFreeBit = 1;
 constexpr uint64_t kSizeMask = ~uint64_t(kAlign - 1);
 
@@ -76,12 +80,7 @@ static void InitSync(Header* h) {
   pthread_mutexattr_setrobust(&ma, PTHREAD_MUTEX_ROBUST);
   pthread_mutex_init(&h->mu, &ma);
   pthread_mutexattr_destroy(&ma);
-  pthread_condattr_t ca;
-  pthread_condattr_init(&ca);
-  pthread_condattr_setpshared(&ca, PTHREAD_PROCESS_SHARED);
-  pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
-  pthread_cond_init(&h->cv, &ca);
-  pthread_condattr_destroy(&ca);
+  h->cv_seq = 0;
 }
 
 Store* Store::Create(const std::string& name, uint64_t size, const std::string& spill_dir,
@@ -387,12 +386,23 @@ void Store::CondWait(int64_t deadline_ns) {
     // Bounded waits even for "forever" so a lost wakeup can never hang a reader.
     deadline_ns = NowNs() + 200000000ll;
   }
-  timespec ts;
-  ts.tv_sec = deadline_ns / 1000000000ll;
-  ts.tv_nsec = deadline_ns % 1000000000ll;
-  hdr_->lock_pid = 0;
-  int rc = pthread_cond_timedwait(&hdr_->cv, &hdr_->mu, &ts);
-  OnLocked(rc == ETIMEDOUT ? 0 : rc);
+  // the word is read under the lock and every Broadcast bumps it under the lock, so a broadcast between
+  // the unlock and the futex wait makes the wait return at once (EAGAIN): no lost wakeup
+  const uint32_t v = __atomic_load_n(&hdr_->cv_seq, __ATOMIC_ACQUIRE);
+  Unlock();
+  const int64_t rem = deadline_ns - NowNs();
+  if (rem > 0) {
+    timespec rel;
+    rel.tv_sec = rem / 1000000000ll;
+    rel.tv_nsec = rem % 1000000000ll;
+    syscall(SYS_futex, &hdr_->cv_seq, FUTEX_WAIT, v, &rel, nullptr, 0);  // shared (not _PRIVATE): cross-process
+  }
+  Lock();
+}
+
+void Store::Broadcast() {
+  __atomic_add_fetch(&hdr_->cv_seq, 1u, __ATOMIC_RELEASE);
+  syscall(SYS_futex, &hdr_->cv_seq, FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
 }
 
 void Store::Wake() {

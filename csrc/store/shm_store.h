@@ -139,7 +139,11 @@ struct Header {
   uint64_t heap_off;   // absolute offset of heap start inside the segment
   uint64_t heap_size;
   pthread_mutex_t mu;
-  pthread_cond_t cv;
+  // The store's condition is a futex word, not a pthread_cond_t: glibc's process-shared condvar keeps
+  // per-group waiter references, so a waiter SIGKILLed inside pthread_cond_timedwait leaves the next
+  // broadcast waiting for it forever -- while it holds the store mutex, which hangs every process
+  // (found by tests/test_chaos.py). A futex wait holds no state for the kernel to clean up.
+  uint32_t cv_seq;
   uint64_t seal_seq;
   uint64_t ring_head;
   uint64_t next_file_id;
@@ -314,7 +318,7 @@ class Store {
   std::string SpillPath(uint64_t fid) const;
   std::string DirFor(uint64_t fid) const;
   std::string FallbackPath(uint64_t fid) const;
-  void Broadcast() { pthread_cond_broadcast(&hdr_->cv); }
+  void Broadcast();  // under the lock: bump the condition word, wake every waiter
   void CondWait(int64_t deadline_ns);
   // TLSF
   void TlsfInsert(uint64_t blk);

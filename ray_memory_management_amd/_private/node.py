@@ -1943,6 +1943,10 @@ def main():
             pass
 
     signal.signal(signal.SIGTERM, _term)
+    import faulthandler
+
+    # `rmm stack` / debugging a stuck control plane: SIGUSR1 dumps every head thread's stack to its log
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
     prof_path = os.environ.get("RMM_HEAD_PROFILE")  # control-plane profiling: cProfile of the loop
     prof = None
     if prof_path:
