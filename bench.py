@@ -337,6 +337,14 @@ def main():
         if rank == 0:
             import ray_memory_management_amd as ray
 
+            if algo is not None and err is None and len(algo.learner_group.learners) > 1:
+                # after the timed region: data-parallel replicas must hold the same weights bit for bit
+                try:
+                    digests = ray.get([a.weights_digest.remote() for a in algo.learner_group.learners])
+                    info["replicas_identical"] = len(set(digests)) == 1
+                    info["learner_comm"] = ray.get([a.comm_info.remote() for a in algo.learner_group.learners])
+                except Exception as ex:  # noqa: BLE001
+                    info["replicas_check_error"] = repr(ex)[:300]
             if algo is not None:
                 try:
                     algo.stop()

@@ -364,7 +364,7 @@ PYBIND11_MODULE(_hip, m) {
                                     const std::vector<uint64_t>& bufs, int64_t B, int slices, int A1, uint32_t seed,
                                     uint64_t k16_done, int64_t T, int threads, bool spin, uint64_t host_seq,
                                     uint64_t host_seq_dev, uint64_t release, uint64_t release_dev, uint64_t gate_err,
-                                    int gate_parts) {
+                                    int gate_parts, int gate_timeout_ms) {
     // fp32 policy: 16 weights (8 hi planes, then the 8 lo planes) and a 12th buffer (the h2 lo plane)
     const bool x3 = wts.size() == 16;
     if (v.size() < 15 || (wts.size() != 8 && !x3) || bufs.size() < size_t(x3 ? 12 : 11) || w1s.size() != 4 ||
@@ -439,6 +439,8 @@ PYBIND11_MODULE(_hip, m) {
       a.gate_err = P<int>(gate_err);
       if (gate_parts < 1 || gate_parts > B) throw std::invalid_argument("hybrid_rollout_direct: 1 <= gate_parts <= B");
       g.gate_parts = gate_parts;
+      if (gate_timeout_ms < 1) throw std::invalid_argument("hybrid_rollout_direct: gate_timeout_ms >= 1");
+      a.gate_timeout_ms = gate_timeout_ms;
     }
     std::vector<RolloutGroup> G{g};
     py::gil_scoped_release nogil;
@@ -446,7 +448,7 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("group"), py::arg("weights"), py::arg("w1s"), py::arg("w2s"), py::arg("bufs"), py::arg("B"), py::arg("S"),
      py::arg("A1"), py::arg("seed"), py::arg("k16_done"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false,
      py::arg("host_seq") = 0, py::arg("host_seq_dev") = 0, py::arg("release") = 0, py::arg("release_dev") = 0,
-     py::arg("gate_err") = 0, py::arg("gate_parts") = 1);
+     py::arg("gate_err") = 0, py::arg("gate_parts") = 1, py::arg("gate_timeout_ms") = 2000);
   // K21 persistent rollout server over one group: `group` = hybrid_rollout's 15 group fields (exec
   // ignored); weights = [W1, b1, W2, b2, Wd, bd, Wh, bh]; bufs = [stack, nf, rows, h2, hpart, act,
   // logp, vf, lout, act_now, ctr_t]
@@ -882,6 +884,14 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   // ---------------------------------------------------------------- peer-memory all-reduce (xGMI / hipIPC)
+  m.def("peer_occupancy", [](int device) {
+    const PeerOccupancy o = PeerKernelOccupancy(device);
+    py::dict d;
+    d["cus"] = o.cus;
+    d["allreduce_per_cu"] = o.allreduce_per_cu;
+    d["zero1_per_cu"] = o.zero1_per_cu;
+    return d;
+  });
   py::class_<PeerAllReduce, std::shared_ptr<PeerAllReduce>>(m, "PeerAllReduce")
       .def(py::init<int, int, int, uint64_t, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("cap_bytes") = 8ull << 20, py::arg("nblocks") = 64, py::arg("timeout_s") = 30.0)

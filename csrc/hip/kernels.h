@@ -220,7 +220,7 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
                        X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
                        hipStream_t stream,
                        const int64_t* gate = nullptr, int64_t gate_want = 0, int* gate_err = nullptr,
-                       int gate_parts = 1);
+                       int gate_parts = 1, int gate_timeout_ms = 2000);
 // K10x backward: conv2 launch (dW2, db2, dpre1 -> dpre1 pair, db1) + conv1 weight-grad launch + reduce;
 // fp32 gradients in the parameters' memory order. partial: x3_trunk_partial_floats(B) floats.
 int x3_conv2_bwd_groups(int64_t B);
@@ -307,6 +307,7 @@ struct RolloutServerArgs {
   // counter) reaches the step's number before it reads the newest frames; bounded, *gate_err set on timeout
   const int64_t* gate = nullptr;
   int* gate_err = nullptr;
+  int gate_timeout_ms = 2000;  // wall-clock bound of one gate wait (s_memrealtime)
 };
 int rollout_server_launch(const RolloutServerArgs& a, hipStream_t stream);
 

@@ -14,6 +14,17 @@ namespace rmm::hip {
 
 constexpr int kPeerMaxRanks = 16;
 
+// How many workgroups of the peer kernels one CU holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor)
+// and the device's CU count: a launch whose workgroups wait on their peers' same-index workgroups must have
+// ALL of them resident together (with every rank sharing the GPU, and beside concurrent kernels), so the
+// communicators derive their workgroup counts from this instead of a constant.
+struct PeerOccupancy {
+  int cus;
+  int allreduce_per_cu;
+  int zero1_per_cu;
+};
+PeerOccupancy PeerKernelOccupancy(int device);
+
 class PeerAllReduce {
  public:
   // `cap_bytes`: largest payload one kernel reduces (larger calls are split into several launches);

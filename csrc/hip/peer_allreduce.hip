@@ -428,6 +428,20 @@ __global__ void __launch_bounds__(256) k_zero1_mask(float* buf, int64_t n, int n
 
 }  // namespace
 
+PeerOccupancy PeerKernelOccupancy(int device) {
+  int prev = 0;
+  RMM_HIP_CHECK(hipGetDevice(&prev));
+  RMM_HIP_CHECK(hipSetDevice(device));
+  PeerOccupancy o{};
+  RMM_HIP_CHECK(hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, device));
+  RMM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &o.allreduce_per_cu, reinterpret_cast<const void*>(&k_peer_allreduce<false, false>), kThreads, 0));
+  RMM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &o.zero1_per_cu, reinterpret_cast<const void*>(&k_peer_zero1<false>), kZThreads, 0));
+  RMM_HIP_CHECK(hipSetDevice(prev));
+  return o;
+}
+
 PeerAllReduce::PeerAllReduce(int rank, int world, int device, uint64_t cap_bytes, int nblocks, double timeout_s)
     : rank_(rank), world_(world), device_(device), nblocks_(nblocks) {
   if (world < 1 || world > kPeerMaxRanks || rank < 0 || rank >= world)

@@ -176,7 +176,7 @@ void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hip
     const X3Out h2{a.h2, a.h2lo};
     x3_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, X3In{a.W1, a.W1lo}, a.w1s, X3In{a.b1, a.b1lo},
                       X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream, a.gate, gate_want, a.gate_err,
-                      gate_parts);
+                      gate_parts, a.gate_timeout_ms);
     x3_dense_fwd_part(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, 256, a.hpart, a.S, stream);
     x3_heads_sample(a.hpart, a.S, X3In{a.bd, a.bdlo}, X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t,
                     a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B, a.A1, stream, k16_done, host_seq_dev);
@@ -232,7 +232,14 @@ std::vector<std::pair<double, int64_t>> hybrid_rollout(const std::vector<Rollout
     }
     RMM_HIP_CHECK(hipEventRecord(ev[2 * i + (step & 1)], G[i].stream));
   };
+  // test hook: a host that stalls before opening each gate (RMM_TEST_GATE_DELAY_US), to exercise the gate's
+  // timeout and the worker's ungated re-run (tests/test_rllib_runtime_gpu.py)
+  const long delay_us = [] {
+    const char* e = std::getenv("RMM_TEST_GATE_DELAY_US");
+    return e ? std::atol(e) : 0L;
+  }();
   auto release = [&](size_t i, int64_t k = 1) {  // frames of the next step (range) are written: open its gate
+    if (delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
     __atomic_fetch_add(G[i].release, k, __ATOMIC_RELEASE);
   };
   try {

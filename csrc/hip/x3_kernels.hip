@@ -107,8 +107,8 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx0, const int64_t* __restrict__ ctr, int64_t period,
     int64_t B, CPair W1, WStrides w1, CPair b1, CPair W2, WStrides w2, CPair b2, Pair h1_out, Pair h2_out,
     uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t,
-    const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts, const float* __restrict__ cols,
-    float* __restrict__ cols_out, int ncols) {
+    const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts, int gate_timeout_ms,
+    const float* __restrict__ cols, float* __restrict__ cols_out, int ncols) {
   __shared__ __attribute__((aligned(16))) unsigned short img[FIMG];
   __shared__ __attribute__((aligned(16))) unsigned short h1h[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short h1l[H1P_ELEMS];
@@ -136,15 +136,17 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     // (mapped pinned memory, bumped after the new frames are written) before reading them. With
     // gate_parts P the host steps the envs in P ranges and bumps the counter after each, so frame b waits
     // only for its own range: the first ranges' frames cross PCIe and their conv1
-    // runs while the host still steps the rest. Bounded (~0.2-0.5 s): a host that died mid-fragment can
-    // never leave a wave spinning (*gate_err is set)
+    // runs while the host still steps the rest. Bounded by wall clock (gate_timeout_ms on the 100 MHz
+    // real-time counter): a host that died mid-fragment can never leave a wave spinning (*gate_err is
+    // set; the worker then re-runs the fragment ungated instead of using stale frames)
     if (threadIdx.x == 0) {
       // range of frame b under the host's split [B p / P, B (p + 1) / P): p = ((b + 1) P - 1) / B
       const int64_t want = gate_want + (gate_parts > 1 ? ((b + 1) * gate_parts - 1) / B : 0);
-      int64_t n = 0;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t limit = uint64_t(gate_timeout_ms > 0 ? gate_timeout_ms : 2000) * 100000ull;
       while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
-        if (++n >= 200000) {
-          if (gate_err) *gate_err = 1;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
+          if (gate_err) __hip_atomic_store(gate_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -683,13 +685,14 @@ void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
     throw std::invalid_argument("x3_trunk_fwd: cols and cols_out together, 1 <= ncols <= 512");
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(x3_trunk_fwd_groups(B))), dim3(x3::NTF), 0, stream, obs, idx,
                      ctr, period, B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), pp(h1), pp(h2), nullptr,
-                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1, cols, cols_out, ncols);
+                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1, 0, cols, cols_out, ncols);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
 void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows, const int64_t* t_ptr, int64_t B,
                        X3In W1, const int64_t* w1s, X3In b1, X3In W2, const int64_t* w2s, X3In b2, X3Out h2,
-                       hipStream_t stream, const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts) {
+                       hipStream_t stream, const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts,
+                       int gate_timeout_ms) {
   if (B <= 0) return;
   if (stack == nullptr || new_frames == nullptr) throw std::invalid_argument("x3_trunk_fwd_push: stack and new frames");
   if (gate_parts < 1 || gate_parts > B) throw std::invalid_argument("x3_trunk_fwd_push: 1 <= gate_parts <= B");
@@ -702,7 +705,8 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
   // push mode: one frame per workgroup (each workgroup shifts its own env's stack)
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(B)), dim3(x3::NTF), 0, stream, nullptr, nullptr, nullptr,
                      int64_t(1), B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), x3::Pair{}, pp(h2), stack,
-                     new_frames, rows, t_ptr, gate, gate_want, gate_err, gate_parts, nullptr, nullptr, 0);
+                     new_frames, rows, t_ptr, gate, gate_want, gate_err, gate_parts, gate_timeout_ms, nullptr,
+                     nullptr, 0);
   RMM_HIP_CHECK(hipGetLastError());
 }
 

@@ -14,16 +14,19 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
+#include <unordered_map>
 
 namespace rmm {
 
 namespace {
 
 constexpr uint64_t kMagic = 0x524d4d53544f5245ull;  // "RMMSTORE"
-constexpr uint64_t kVersion = 7;  // 6: per-client pin records, Entry.io_pid / anon_pins; 7: futex condition word
+// 6: per-client pin records, Entry.io_pid / anon_pins; 7: futex condition word; 8: integrity counters
+constexpr uint64_t kVersion = 8;
 constexpr uint64_t kFreeBit = 1;
 constexpr uint64_t kSizeMask = ~uint64_t(kAlign - 1);
 
@@ -60,7 +63,25 @@ inline uint64_t HashId(const ObjectId& id) {
 int g_crash_point = 0;
 
 inline void CrashPoint(int p) {
-  if (g_crash_point == p) kill(getpid(), SIGKILL);  // dies holding the store mutex (test hook)
+  // dies holding the store mutex (test hook); point 7 stops instead (a stuck holder for the watchdog)
+  if (g_crash_point == p) kill(getpid(), p == 7 ? SIGSTOP : SIGKILL);
+}
+
+// A process that has exited: no such pid, or a zombie not yet reaped by its parent (its memory and
+// its store mappings are gone already).
+bool ProcessGone(int pid) {
+  if (pid <= 0) return true;
+  if (kill(pid, 0) != 0) return errno == ESRCH;
+  char path[64], buf[512];
+  snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  const char* rp = strrchr(buf, ')');
+  return rp && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X');
 }
 
 inline void MappingInsert(uint64_t size, int* fl, int* sl) {
@@ -215,7 +236,59 @@ void Store::OnLocked(int rc) {
   hdr_->lock_pid = int32_t(getpid());
 }
 
-void Store::Lock() { OnLocked(pthread_mutex_lock(&hdr_->mu)); }
+namespace {
+int64_t g_watchdog_ms = 10000;
+}
+
+void Store::SetLockWatchdogMs(int64_t ms) { g_watchdog_ms = ms; }
+
+// Lock with a watchdog: every critical section is short (file IO and waits run with the lock dropped),
+// so a wait longer than the period means a holder is stuck. Report it (pid, once per holder) and keep
+// waiting -- a dead holder is handled by the robust mutex (EOWNERDEAD), a live one must finish.
+void Store::Lock() {
+  if (g_watchdog_ms <= 0) {
+    OnLocked(pthread_mutex_lock(&hdr_->mu));
+    return;
+  }
+  int rc = pthread_mutex_trylock(&hdr_->mu);
+  if (rc != EBUSY) {
+    OnLocked(rc);
+    return;
+  }
+  int32_t reported = 0;
+  for (;;) {
+    timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    const int64_t ns = int64_t(ts.tv_nsec) + (g_watchdog_ms % 1000) * 1000000ll;
+    ts.tv_sec += time_t(g_watchdog_ms / 1000 + ns / 1000000000ll);
+    ts.tv_nsec = long(ns % 1000000000ll);
+    rc = pthread_mutex_timedlock(&hdr_->mu, &ts);
+    if (rc != ETIMEDOUT) break;
+    const int32_t holder = __atomic_load_n(&hdr_->lock_pid, __ATOMIC_ACQUIRE);
+    if (holder != reported) {
+      reported = holder;
+      __atomic_add_fetch(&hdr_->lock_stalls_total, 1, __ATOMIC_RELEASE);
+      __atomic_store_n(&hdr_->lock_stall_pid, holder, __ATOMIC_RELEASE);
+      fprintf(stderr, "[rmm store] pid %d: store mutex held by pid %d for more than %lld ms\n", int(getpid()),
+              int(holder), (long long)g_watchdog_ms);
+    }
+  }
+  OnLocked(rc);
+}
+
+bool Store::UsedBlock(uint64_t payload_off) const {
+  const uint64_t lo = hdr_->heap_off + kBlockHdr, hi = hdr_->heap_off + hdr_->heap_size - kBlockHdr;
+  if (payload_off < lo || payload_off >= hi || payload_off % kAlign != 0) return false;
+  const Blk* b = reinterpret_cast<const Blk*>(base_ + payload_off - kBlockHdr);
+  const uint64_t sz = b->size & kSizeMask;
+  return !(b->size & kFreeBit) && sz >= kMinBlock && payload_off - kBlockHdr + sz <= hi;
+}
+
+void Store::Heal(const char* why) {
+  __atomic_add_fetch(&hdr_->corruptions_total, 1, __ATOMIC_RELEASE);
+  fprintf(stderr, "[rmm store] pid %d: %s; rebuilding the store metadata\n", int(getpid()), why);
+  Recover(0);
+}
 
 void Store::Unlock() {
   hdr_->lock_pid = 0;
@@ -225,7 +298,13 @@ void Store::Unlock() {
 void Store::Recover(int dead_pid) {
   const uint64_t cap = hdr_->table_cap;
   const uint64_t heap_lo = hdr_->heap_off, heap_hi = hdr_->heap_off + hdr_->heap_size - kBlockHdr;
-  auto alive = [&](int pid) { return pid > 0 && pid != dead_pid && (kill(pid, 0) == 0 || errno == EPERM); };
+  std::unordered_map<int, bool> seen;  // one liveness probe per pid
+  auto alive = [&](int pid) {
+    if (pid <= 0 || pid == dead_pid) return false;
+    auto it = seen.find(pid);
+    if (it != seen.end()) return it->second;
+    return seen[pid] = !ProcessGone(pid);
+  };
   auto resident = [](const Entry& e) {
     return !(e.flags & kFlagFallback) &&
            (e.state == kCreating || e.state == kSealed || e.state == kSpilling || e.state == kRestoring);
@@ -487,6 +566,14 @@ uint64_t Store::HeapAlloc(uint64_t n) {
 }
 
 void Store::HeapFree(uint64_t payload_off) {
+  if (!UsedBlock(payload_off)) {
+    // never merge from a block that is not ours (offset 0 = "no block yet" would address the segment
+    // header): count it and leak nothing else
+    __atomic_add_fetch(&hdr_->corruptions_total, 1, __ATOMIC_RELEASE);
+    fprintf(stderr, "[rmm store] pid %d: refused to free heap offset %llu (not a used block)\n", int(getpid()),
+            (unsigned long long)payload_off);
+    return;
+  }
   uint64_t blk = payload_off - kBlockHdr;
   Blk* b = reinterpret_cast<Blk*>(base_ + blk);
   uint64_t bsize = b->size & kSizeMask;
@@ -573,11 +660,27 @@ uint64_t Store::CheckHeap() {
   }
   if (off != end) ok = false;
   uint64_t listed = 0;
+  const uint64_t max_blocks = hdr_->heap_size / kMinBlock + 1;
   for (int f = 0; f < kFL && ok; f++)
-    for (int s = 0; s < kSL; s++)
-      for (uint64_t b = hdr_->free_heads[f][s]; b != kNil;
-           b = reinterpret_cast<Blk*>(base_ + b)->next_free)
-        listed++;
+    for (int s = 0; s < kSL && ok; s++)
+      for (uint64_t b = hdr_->free_heads[f][s]; b != kNil && ok;
+           b = reinterpret_cast<Blk*>(base_ + b)->next_free) {
+        // a listed block must be a free block inside the heap; the walk is bounded (no cycle can spin)
+        ok = b >= hdr_->heap_off && b < end && (reinterpret_cast<Blk*>(base_ + b)->size & kFreeBit) &&
+             ++listed <= max_blocks;
+      }
+  // LRU list: bounded, consistent links, only evictable entries
+  {
+    uint64_t n = 0;
+    int32_t prev_i = -1;
+    for (int32_t i = hdr_->lru_head; i >= 0 && ok; i = table_[i].lru_next) {
+      ok = uint64_t(i) < hdr_->table_cap && ++n <= hdr_->table_cap && table_[i].in_lru &&
+           table_[i].lru_prev == prev_i && table_[i].state == kSealed && table_[i].pin_count == 0;
+      prev_i = i;
+      if (!ok) break;
+    }
+    if (ok && prev_i != hdr_->lru_tail) ok = false;
+  }
   if (listed != nfree) ok = false;
   if (used_bytes != hdr_->stats.bytes_in_use) ok = false;
   Unlock();
@@ -610,25 +713,35 @@ int64_t Store::Insert(const ObjectId& id) {
     std::vector<Entry> keep;
     keep.reserve(live);
     std::vector<int64_t> lru_order;
-    for (int32_t i = hdr_->lru_head; i >= 0; i = table_[i].lru_next) lru_order.push_back(i);
-    std::vector<ObjectId> lru_ids;
-    for (auto i : lru_order) { ObjectId o; memcpy(o.b, table_[i].id, kIdSize); lru_ids.push_back(o); }
-    for (uint64_t i = 0; i < cap; i++)
-      if (table_[i].state != kEmpty && table_[i].state != kTombstone) keep.push_back(table_[i]);
-    memset(table_, 0, cap * sizeof(Entry));
-    hdr_->table_used = 0;
-    hdr_->lru_head = hdr_->lru_tail = -1;
-    for (auto& e : keep) {
-      ObjectId o;
-      memcpy(o.b, e.id, kIdSize);
-      uint64_t mask = cap - 1, j = HashId(o) & mask;
-      while (table_[j].state != kEmpty) j = (j + 1) & mask;
-      table_[j] = e;
-      table_[j].in_lru = 0;
-      table_[j].lru_prev = table_[j].lru_next = -1;
-      hdr_->table_used++;
+    bool damaged = false;
+    for (int32_t i = hdr_->lru_head; i >= 0;) {
+      damaged = uint64_t(i) >= cap || lru_order.size() >= cap || !table_[i].in_lru;
+      if (damaged) break;
+      lru_order.push_back(i);
+      i = table_[i].lru_next;
     }
-    for (auto& o : lru_ids) LruPush(Find(o));
+    if (damaged) {
+      Heal("LRU list walk exceeded the table during a rehash");  // rebuilds the table without tombstones
+    } else {
+      std::vector<ObjectId> lru_ids;
+      for (auto i : lru_order) { ObjectId o; memcpy(o.b, table_[i].id, kIdSize); lru_ids.push_back(o); }
+      for (uint64_t i = 0; i < cap; i++)
+        if (table_[i].state != kEmpty && table_[i].state != kTombstone) keep.push_back(table_[i]);
+      memset(table_, 0, cap * sizeof(Entry));
+      hdr_->table_used = 0;
+      hdr_->lru_head = hdr_->lru_tail = -1;
+      for (auto& e : keep) {
+        ObjectId o;
+        memcpy(o.b, e.id, kIdSize);
+        uint64_t mask = cap - 1, j = HashId(o) & mask;
+        while (table_[j].state != kEmpty) j = (j + 1) & mask;
+        table_[j] = e;
+        table_[j].in_lru = 0;
+        table_[j].lru_prev = table_[j].lru_next = -1;
+        hdr_->table_used++;
+      }
+      for (auto& o : lru_ids) LruPush(Find(o));
+    }
   }
   uint64_t mask = cap - 1;
   uint64_t i = HashId(id) & mask;
@@ -755,25 +868,25 @@ void Store::PinErase(const uint8_t* id, int32_t pid) {
   hdr_->pins_live--;
 }
 
-// Release one pin of entry idx on behalf of `pid`: its own record first, then an anonymous pin, then
-// (a pin handed to another process, e.g. a view passed along) any record of the same object.
+// Release one pin of entry idx on behalf of `pid`: its own record, else an anonymous pin (a pin taken
+// when the record table was full). A release by a process that holds neither (a late release after
+// ReleaseClient already dropped its pins) is counted and ignored: taking another client's record would
+// let the object be evicted while that client still maps it.
 void Store::PinDrop(int64_t idx, int32_t pid) {
   Entry* e = E(idx);
   if (e->pin_count <= 0) return;
   PinRec* P = Pins();
   int64_t r = PinFind(e->id, pid);
-  if (r < 0 && e->anon_pins > 0) {
+  if (r < 0 && e->anon_pins > (e->io_pid != 0 ? 1 : 0)) {  // never the spill / restore IO pin
     e->anon_pins--;
     e->pin_count--;
     return;
   }
-  if (r < 0)
-    for (uint64_t i = 0; i < kPinCap; i++)
-      if (P[i].state == 1 && memcmp(P[i].id, e->id, kIdSize) == 0) {
-        r = int64_t(i);
-        break;
-      }
-  if (r >= 0 && --P[r].count <= 0) {
+  if (r < 0) {
+    hdr_->unmatched_releases_total++;
+    return;
+  }
+  if (--P[r].count <= 0) {
     P[r].state = 2;
     P[r].count = 0;
     hdr_->pins_live--;
@@ -927,7 +1040,14 @@ void Store::FreeEntryStorage(int64_t idx) {
     FallbackUnlink(e->fallback_id);
     e->flags &= ~kFlagFallback;
   } else if (e->state == kSealed || e->state == kCreating || e->state == kSpilling) {
-    HeapFree(e->offset);
+    // a create still waiting for memory (or mapping its fallback file with the lock dropped) owns no
+    // heap block: offset 0 means "none", it is not a block to free
+    if (e->offset != 0) HeapFree(e->offset);
+    e->offset = 0;
+    if (e->state == kCreating && e->fallback_id != 0) {
+      unlink(FallbackPath(e->fallback_id).c_str());  // a fallback file reserved by a creator that died mapping it
+      e->fallback_id = 0;
+    }
   }
   if (e->flags & kFlagHasSpillCopy) {
     DropSpillRef(e->spill_file);
@@ -947,7 +1067,16 @@ uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
   std::vector<ObjectId> batch;
   uint64_t batch_bytes = 0;
   uint64_t target = std::max<uint64_t>(bytes, hdr_->min_spill_size);
+  const uint64_t cap = hdr_->table_cap;
+  uint64_t steps = 0;
+  bool damaged = false;
   for (int32_t i = hdr_->lru_head; i >= 0 && (freed < bytes || batch_bytes < target);) {
+    // the LRU list links at most every slot once: a longer walk, an out-of-range link or a listed entry
+    // that is not marked in_lru means the metadata is damaged -- never follow it under the mutex
+    if (uint64_t(i) >= cap || ++steps > cap || !table_[i].in_lru) {
+      damaged = true;
+      break;
+    }
     Entry* e = &table_[i];
     int32_t nxt = e->lru_next;
     if (e->state == kSealed && e->pin_count == 0 && !(e->flags & kFlagFallback)) {
@@ -969,6 +1098,16 @@ uint64_t Store::SpillLocked(uint64_t bytes, std::vector<int64_t>* /*unused*/) {
       }
     }
     i = nxt;
+  }
+  if (damaged) {
+    for (auto& o : batch) {  // undo this walk's claims, then rebuild from the entries
+      const int64_t idx = Find(o);
+      if (idx < 0) continue;
+      E(idx)->state = kSealed;
+      IoUnpin(idx);
+    }
+    Heal("LRU list walk exceeded the table (cycle or bad link)");
+    return freed;
   }
   if (batch.empty()) return freed;
   uint64_t fid = hdr_->next_file_id++;
@@ -1067,6 +1206,11 @@ bool Store::RestoreLocked(int64_t idx) {
     if (off == kNil && f == 0) break;
   }
   idx = Find(id);
+  if (idx < 0) {  // dropped by a rebuild while a spill had the lock released
+    if (off != kNil) HeapFree(off);
+    Broadcast();
+    return false;
+  }
   e = E(idx);
   if (off == kNil) {
     e->state = kSpilled;
@@ -1091,6 +1235,11 @@ bool Store::RestoreLocked(int64_t idx) {
   if (fd >= 0) close(fd);
   Lock();
   idx = Find(id);
+  if (idx < 0) {
+    HeapFree(off);
+    Broadcast();
+    return false;
+  }
   e = E(idx);
   IoUnpin(idx);
   if (!ok) {
@@ -1166,7 +1315,17 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
     CondWait(std::min<int64_t>(wait_deadline, now + 20000000ll));  // re-check every 20 ms (or on a broadcast)
     off = HeapAlloc(len);
   }
-  idx = Find(id);
+  // the lock was dropped (spill IO, grace wait): the pending entry may have been aborted meanwhile
+  auto still_mine = [&]() {
+    idx = Find(id);
+    return idx >= 0 && E(idx)->state == kCreating && E(idx)->creator_pid == int32_t(getpid());
+  };
+  if (!still_mine()) {
+    if (off != kNil) HeapFree(off);
+    Broadcast();
+    Unlock();
+    throw std::runtime_error("ObjectStoreFullError: the pending create was aborted while waiting for memory");
+  }
   e = E(idx);
   uint8_t* ptr = nullptr;
   if (off != kNil) {
@@ -1174,16 +1333,24 @@ uint8_t* Store::CreateObject(const ObjectId& id, uint64_t data_size, uint64_t me
     ptr = base_ + off;
   } else if (hdr_->fallback_enabled && !hdr_->disk_full) {
     uint64_t fid = hdr_->next_file_id++;
+    e->fallback_id = fid;  // reserved: an abort while the file is mapped unlinks it (FreeEntryStorage)
     Unlock();
     ptr = FallbackMap(fid, len, true);
     Lock();
-    idx = Find(id);
+    if (!still_mine()) {
+      FallbackUnlink(fid);
+      Broadcast();
+      Unlock();
+      throw std::runtime_error("ObjectStoreFullError: the pending create was aborted while mapping its fallback file");
+    }
     e = E(idx);
     if (ptr) {
       e->flags |= kFlagFallback;
-      e->fallback_id = fid;
       hdr_->stats.fallback_bytes_current += len;
       hdr_->stats.fallback_allocs_total++;
+    } else {
+      e->fallback_id = 0;
+      unlink(FallbackPath(fid).c_str());
     }
   }
   if (!ptr) {
@@ -1224,7 +1391,11 @@ void Store::Seal(const ObjectId& id) {
 void Store::Abort(const ObjectId& id) {
   Lock();
   int64_t idx = Find(id);
-  if (idx >= 0 && E(idx)->state == kCreating) {
+  // another process may abort a create only once its creator is gone: a live creator may be writing
+  // into the block right now (it aborts its own creates itself)
+  const int32_t creator = idx >= 0 ? E(idx)->creator_pid : 0;
+  const bool creator_gone = creator == int32_t(getpid()) || ProcessGone(creator);
+  if (idx >= 0 && E(idx)->state == kCreating && creator_gone) {
     PinErase(E(idx)->id, E(idx)->creator_pid);
     FreeEntryStorage(idx);
     RemoveEntry(idx);
@@ -1430,6 +1601,7 @@ bool Store::Delete(const ObjectId& id) {
 
 bool Store::Contains(const ObjectId& id) {
   Lock();
+  CrashPoint(7);
   int64_t idx = Find(id);
   bool r = false;
   if (idx >= 0) {

@@ -183,6 +183,14 @@ struct Header {
   uint64_t io_now;                   // entries holding a spill / restore IO pin (ReleaseClient skips its scan at 0)
   uint64_t clients_released_total;   // ReleaseClient calls that found something to release
   uint64_t client_pins_released_total;
+  // integrity: a release by a process holding no pin of the object (never taken from another client's
+  // record), metadata found inconsistent by a bounded walk or a heap-free check (the store rebuilt itself
+  // with Recover instead of spinning under the mutex), lock waits that exceeded the watchdog period
+  uint64_t unmatched_releases_total;
+  uint64_t corruptions_total;
+  uint64_t lock_stalls_total;
+  int32_t lock_stall_pid;            // the holder the watchdog last reported
+  int32_t pad2;
   Stats stats;
 };
 
@@ -258,6 +266,15 @@ class Store {
   // Pins currently recorded for `pid` (tests / memory summary).
   int64_t PinsHeldBy(int pid);
   uint64_t PinOverflows() const { return hdr_->pin_overflow_total; }
+  uint64_t UnmatchedReleases() const { return hdr_->unmatched_releases_total; }
+  uint64_t Corruptions() const { return __atomic_load_n(&hdr_->corruptions_total, __ATOMIC_ACQUIRE); }
+  uint64_t LockStalls() const { return __atomic_load_n(&hdr_->lock_stalls_total, __ATOMIC_ACQUIRE); }
+  int LockPid() const { return __atomic_load_n(&hdr_->lock_pid, __ATOMIC_ACQUIRE); }
+  // Watchdog period of the store mutex: a lock wait longer than this logs the holder's pid (once per
+  // holder) and counts a stall. Process-local; 0 disables.
+  static void SetLockWatchdogMs(int64_t ms);
+  // Entries in kCreating (tests: a creator blocked in the create grace wait)
+  uint64_t CreatingNow() const { return hdr_->creating_now; }
   // Sealed-notification ring: returns new cursor; sets overflow when the consumer fell behind.
   uint64_t PollSealed(uint64_t cursor, std::vector<ObjectId>* out, bool* overflow);
   uint64_t SealSeq();
@@ -276,7 +293,8 @@ class Store {
   // Test hook: SIGKILL this process at crash point `p` (1 = mid heap split, 2 = mid heap merge,
   // 3 = mid table insert, 4 = mid LRU unlink), i.e. while holding the store mutex in the middle
   // of a multi-word metadata update; 5 = mid restore IO, 6 = mid spill IO (lock released, the
-  // entries carry this process's IO pin). 0 disables. Process-local.
+  // entries carry this process's IO pin); 7 = SIGSTOP inside Contains (a holder that never returns:
+  // the lock watchdog reports it). 0 disables. Process-local.
   static void SetCrashPointForTest(int p);
 
  private:
@@ -288,6 +306,11 @@ class Store {
   // Rebuild allocator, object table, LRU list, spill-file refcounts and derived statistics from
   // the entries that validate, after `dead_pid` died holding the lock (mutex already consistent).
   void Recover(int dead_pid);
+  // A bounded walk or a block check found the metadata inconsistent: count it, log it and rebuild
+  // (Recover) under the lock instead of following the damage.
+  void Heal(const char* why);
+  // payload offset of a used heap block (in range, aligned, not marked free)
+  bool UsedBlock(uint64_t payload_off) const;
   int64_t Find(const ObjectId& id);
   int64_t Insert(const ObjectId& id);
   void RemoveEntry(int64_t idx);

@@ -123,7 +123,14 @@ struct Pinned {
   bool writable;
   bool released = false;
   ~Pinned() {
-    if (!released && store) store->Release(id);
+    if (released || !store) return;
+    // the store mutex may be contended (or, in a bug, stuck): never wait for it holding the GIL
+    if (PyGILState_Check() && !_Py_IsFinalizing()) {
+      py::gil_scoped_release nogil;
+      store->Release(id);
+    } else {
+      store->Release(id);
+    }
   }
 };
 
@@ -170,6 +177,7 @@ PYBIND11_MODULE(_store, m) {
       .def("release", [](Pinned& p) {
         if (!p.released) {
           p.released = true;
+          py::gil_scoped_release nogil;
           p.store->Release(p.id);
         }
       })
@@ -218,8 +226,16 @@ PYBIND11_MODULE(_store, m) {
            },
            py::arg("oid"), py::arg("data_size"), py::arg("meta_size") = 0, py::arg("tag") = 0,
            py::arg("error") = false)
-      .def("seal", [](PyStore& self, py::bytes oid) { self.s->Seal(ToId(oid)); })
-      .def("abort", [](PyStore& self, py::bytes oid) { self.s->Abort(ToId(oid)); })
+      .def("seal", [](PyStore& self, py::bytes oid) {
+        ObjectId id = ToId(oid);
+        py::gil_scoped_release nogil;
+        self.s->Seal(id);
+      })
+      .def("abort", [](PyStore& self, py::bytes oid) {
+        ObjectId id = ToId(oid);
+        py::gil_scoped_release nogil;
+        self.s->Abort(id);
+      })
       // Serialize-and-seal: pickle payload + out-of-band buffers in one shot.
       // Layout: [magic u64][nbuf u64][pickle_len u64][buf_len u64 * nbuf] pad64
       //         [pickle] pad64 [buf0] pad64 [buf1] ...
@@ -335,7 +351,11 @@ PYBIND11_MODULE(_store, m) {
             return r;
           },
           py::arg("oids"), py::arg("num_required"), py::arg("timeout_ms") = -1)
-      .def("release", [](PyStore& self, py::bytes oid) { self.s->Release(ToId(oid)); })
+      .def("release", [](PyStore& self, py::bytes oid) {
+        ObjectId id = ToId(oid);
+        py::gil_scoped_release nogil;
+        self.s->Release(id);
+      })
       .def("delete",
            [](PyStore& self, std::vector<py::bytes> oids) {
              std::vector<ObjectId> ids;
@@ -345,12 +365,21 @@ PYBIND11_MODULE(_store, m) {
              for (auto& i : ids) n += self.s->Delete(i) ? 1 : 0;
              return n;
            })
-      .def("contains", [](PyStore& self, py::bytes oid) { return self.s->Contains(ToId(oid)); })
-      .def("state", [](PyStore& self, py::bytes oid) { return self.s->State(ToId(oid)); })
+      .def("contains", [](PyStore& self, py::bytes oid) {
+        ObjectId id = ToId(oid);
+        py::gil_scoped_release nogil;
+        return self.s->Contains(id);
+      })
+      .def("state", [](PyStore& self, py::bytes oid) {
+        ObjectId id = ToId(oid);
+        py::gil_scoped_release nogil;
+        return self.s->State(id);
+      })
       .def("sizes", [](PyStore& self, const std::vector<py::bytes>& oids) {
         std::vector<ObjectId> ids;
         ids.reserve(oids.size());
         for (auto& o : oids) ids.push_back(ToId(o));
+        py::gil_scoped_release nogil;
         return self.s->Sizes(ids);
       })
       .def("spill",
@@ -358,18 +387,28 @@ PYBIND11_MODULE(_store, m) {
              py::gil_scoped_release nogil;
              return self.s->SpillBytes(bytes);
            })
-      .def("abort_creator", [](PyStore& self, int pid) { return self.s->AbortCreator(pid); })
+      .def("abort_creator", [](PyStore& self, int pid) {
+        py::gil_scoped_release nogil;
+        return self.s->AbortCreator(pid);
+      })
       .def("release_client", [](PyStore& self, int pid) {
         py::gil_scoped_release nogil;
         return self.s->ReleaseClient(pid);
       })
-      .def("pins_held_by", [](PyStore& self, int pid) { return self.s->PinsHeldBy(pid); })
+      .def("pins_held_by", [](PyStore& self, int pid) {
+        py::gil_scoped_release nogil;
+        return self.s->PinsHeldBy(pid);
+      })
       .def("pin_overflows", [](PyStore& self) { return self.s->PinOverflows(); })
       .def("poll_sealed",
            [](PyStore& self, uint64_t cursor) {
              std::vector<ObjectId> out;
              bool overflow = false;
-             uint64_t c = self.s->PollSealed(cursor, &out, &overflow);
+             uint64_t c;
+             {
+               py::gil_scoped_release nogil;
+               c = self.s->PollSealed(cursor, &out, &overflow);
+             }
              py::list l;
              for (auto& o : out) l.append(py::bytes(reinterpret_cast<const char*>(o.b), kIdSize));
              return py::make_tuple(c, l, overflow);
@@ -380,13 +419,29 @@ PYBIND11_MODULE(_store, m) {
              py::gil_scoped_release nogil;
              return self.s->WaitSealSeq(seq, timeout_ms);
            })
-      .def("wake", [](PyStore& self) { self.s->Wake(); })
-      .def("stats", [](PyStore& self) { return StatsDict(self.s->GetStats(), self.s->Capacity()); })
+      .def("wake", [](PyStore& self) {
+        py::gil_scoped_release nogil;
+        self.s->Wake();
+      })
+      .def("stats", [](PyStore& self) {
+        Stats st;
+        {
+          py::gil_scoped_release nogil;
+          st = self.s->GetStats();
+        }
+        return StatsDict(st, self.s->Capacity());
+      })
       .def("capacity", [](PyStore& self) { return self.s->Capacity(); })
-      .def("set_disk_full", [](PyStore& self, bool full) { self.s->SetDiskFull(full); })
+      .def("set_disk_full", [](PyStore& self, bool full) {
+        py::gil_scoped_release nogil;
+        self.s->SetDiskFull(full);
+      })
       .def("disk_full", [](PyStore& self) { return self.s->DiskFull(); })
       .def("gc_requests", [](PyStore& self) { return self.s->GcRequests(); })
-      .def("set_oom_grace", [](PyStore& self, double s) { self.s->SetOomGrace(s); })
+      .def("set_oom_grace", [](PyStore& self, double s) {
+        py::gil_scoped_release nogil;
+        self.s->SetOomGrace(s);
+      })
       .def("spill_dirs", [](PyStore& self) { return self.s->SpillDirs(); })
       .def("oom_stats", [](PyStore& self) {
         py::dict d;
@@ -398,14 +453,35 @@ PYBIND11_MODULE(_store, m) {
       })
       .def("base_address", [](PyStore& self) { return reinterpret_cast<uintptr_t>(self.s->Base()); })
       .def("mapped_size", [](PyStore& self) { return self.s->MappedSize(); })
-      .def("check_heap", [](PyStore& self) { return self.s->CheckHeap(); })
+      .def("check_heap", [](PyStore& self) {
+        py::gil_scoped_release nogil;
+        return self.s->CheckHeap();
+      })
       .def("recoveries", [](PyStore& self) { return self.s->Recoveries(); })
+      .def("integrity", [](PyStore& self) {
+        py::dict d;
+        d["corruptions_total"] = self.s->Corruptions();
+        d["lock_stalls_total"] = self.s->LockStalls();
+        d["unmatched_releases_total"] = self.s->UnmatchedReleases();
+        d["pin_overflow_total"] = self.s->PinOverflows();
+        d["recoveries_total"] = self.s->Recoveries();
+        d["lock_pid"] = self.s->LockPid();
+        d["creating_now"] = self.s->CreatingNow();
+        return d;
+      })
+      .def("creating_now", [](PyStore& self) { return self.s->CreatingNow(); })
+      .def_static("set_lock_watchdog_ms", &rmm::Store::SetLockWatchdogMs)
       .def("recovered_dropped", [](PyStore& self) { return self.s->RecoveredDropped(); })
       .def_static("set_crash_point_for_test", &rmm::Store::SetCrashPointForTest)
       .def("list_objects", [](PyStore& self) {
         py::list out;
         static const char* names[] = {"EMPTY", "CREATING", "SEALED", "SPILLING", "SPILLED", "RESTORING", "TOMBSTONE"};
-        for (auto& pr : self.s->ListObjects()) {
+        std::vector<std::pair<ObjectId, Entry>> objs;
+        {
+          py::gil_scoped_release nogil;
+          objs = self.s->ListObjects();
+        }
+        for (auto& pr : objs) {
           py::dict d;
           d["object_id"] = py::bytes(reinterpret_cast<const char*>(pr.first.b), kIdSize);
           d["state"] = names[pr.second.state < 7 ? pr.second.state : 0];

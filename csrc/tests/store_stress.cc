@@ -170,13 +170,27 @@ int main(int argc, char** argv) {
     int status = 0;
     waitpid(pid, &status, 0);
     const uint64_t rec = s->Recoveries();
-    if (!(WIFSIGNALED(status) && WTERMSIG(status) == SIGKILL)) crash_bad++;
+    if (point == 2 && WIFEXITED(status) && WEXITSTATUS(status) == 3) {
+      // the merge point needs `a` to sit right before `b`; the stress phase's leftovers decide the
+      // layout, so when they were not neighbours the crash point is not reached (nothing to recover)
+      std::printf("crash point 2: a and b not neighbours in this layout (skipped)\n");
+      for (ObjectId x : {a, b, c, d}) s->Delete(x);
+      continue;
+    }
+    if (!(WIFSIGNALED(status) && WTERMSIG(status) == SIGKILL)) {
+      crash_bad++;
+      std::printf("crash point %d: child not killed (status %d)\n", point, status);
+    }
     (void)s->Contains(c);  // first lock after the kill: EOWNERDEAD -> Recover
-    if (s->Recoveries() != rec + 1) crash_bad++;
+    if (s->Recoveries() != rec + 1) {
+      crash_bad++;
+      std::printf("crash point %d: no recovery\n", point);
+    }
     try {
       s->CheckHeap();
     } catch (const std::runtime_error&) {
       crash_bad++;
+      std::printf("crash point %d: heap check failed\n", point);
     }
     Store::View v;
     if (s->Get(c, 0, &v)) {
@@ -273,6 +287,70 @@ int main(int argc, char** argv) {
   }
   std::printf("client-death phase: bad=%ld\n", client_bad);
   g_bad += client_bad;
+
+  // ---- dead waiting creator: a create blocked in the grace wait (entry kCreating, no heap block yet)
+  // is SIGKILLed; AbortCreator must free nothing (round 5: it freed heap offset 0 and corrupted the
+  // segment header), the heap check passes and other creates proceed
+  long waiter_bad = 0;
+  {
+    s->SetOomGrace(30.0);
+    s->SpillBytes(1ull << 40);  // the stress phase's leftovers go to disk: only pinned bytes stay
+    std::vector<ObjectId> held;
+    for (int k = 0; k < 64; k++) {  // fill the arena with objects this process keeps pinned
+      ObjectId x = Id(30000 + k);
+      bool ex = false;
+      uint8_t* p = nullptr;
+      try {
+        p = s->CreateObject(x, 1u << 20, 0, 0, 0, &ex);
+      } catch (const std::runtime_error&) {
+        break;
+      }
+      if (!p) break;
+      std::memset(p, 0x6c, 1u << 20);
+      s->Seal(x);  // the creator pin stays: nothing can spill
+      held.push_back(x);
+      if (s->GetStats().bytes_in_use + (2u << 20) > s->Capacity()) break;
+    }
+    const uint64_t free_before = s->CheckHeap();
+    const uint64_t waits0 = s->OomWaits();
+    pid_t pid = fork();
+    if (pid == 0) {
+      Store* cs = Store::Attach(name);
+      bool ex = false;
+      try {
+        (void)cs->CreateObject(Id(39999), 8u << 20, 0, 0, 0, &ex);
+      } catch (const std::runtime_error&) {
+      }
+      _exit(3);
+    }
+    for (int t = 0; t < 3000 && !(s->CreatingNow() == 1 && s->OomWaits() > waits0); t++) usleep(10000);
+    if (s->CreatingNow() != 1 || s->OomWaits() <= waits0) waiter_bad++;
+    kill(pid, SIGKILL);
+    int status = 0;
+    waitpid(pid, &status, 0);
+    if (s->AbortCreator(pid) != 1) waiter_bad++;
+    try {
+      if (s->CheckHeap() != free_before) waiter_bad++;
+    } catch (const std::runtime_error&) {
+      waiter_bad++;
+    }
+    if (s->Corruptions() != 0 || s->CreatingNow() != 0) waiter_bad++;
+    for (ObjectId x : held) {
+      s->Release(x);
+      s->Delete(x);
+    }
+    s->SetOomGrace(0.05);
+    bool ex = false;
+    uint8_t* p = s->CreateObject(Id(39998), 8u << 20, 0, 0, 0, &ex);
+    if (!p) waiter_bad++;
+    else {
+      s->Seal(Id(39998));
+      s->Release(Id(39998));
+      s->Delete(Id(39998));
+    }
+  }
+  std::printf("dead-waiting-creator phase: bad=%ld\n", waiter_bad);
+  g_bad += waiter_bad;
 
   uint64_t free_before = s->CheckHeap();
   for (int k = 0; k < kKeys; k++) s->Delete(Id(k));

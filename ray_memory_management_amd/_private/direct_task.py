@@ -127,6 +127,12 @@ class DirectTaskSubmitter:
         os.write(self.wake_w, b"x")
 
     def _io_loop(self):
+        try:
+            self._io_loop_body()
+        except exc.LocalRayletDiedError:
+            self.running = False  # the head is gone (shutdown): nothing left to submit to
+
+    def _io_loop_body(self):
         while self.running:
             try:
                 events = self.sel.select(timeout=self.lease_idle_s if self.idle_leases else 1.0)
@@ -380,6 +386,7 @@ class DirectTaskSubmitter:
 
     def _on_conn_lost(self, conn: _WorkerConn):
         drop = []
+        crashed = []  # (spec, keep) of tasks out of retries: they fail once the head says why the worker died
         with self.lock:
             if self.conns.get(conn.addr) is conn:
                 del self.conns[conn.addr]
@@ -405,10 +412,27 @@ class DirectTaskSubmitter:
                             ks.queue.appendleft([spec, keep, attempt + 1])
                             self.queued[tid] = sk
                         else:
-                            self.w._store_errors(spec["return_ids"], exc.WorkerCrashedError())
-                            drop.append(keep)
+                            crashed.append((spec, keep))
                 self._pump(sk, ks)
         del drop
+        if crashed:
+            self._fail_crashed(conn.addr, crashed)
+
+    def _fail_crashed(self, addr, crashed):
+        """Tasks whose leased worker died with no retries left: WorkerCrashedError, or OutOfMemoryError with
+        the exit detail when the head's memory monitor killed that worker (reference node_manager.cc:2962
+        DestroyWorker with the "System memory low ..." detail). The head records the detail before it kills,
+        so asking after the connection dropped always finds it."""
+
+        def done(reply):
+            err = exc.OutOfMemoryError(reply) if isinstance(reply, str) and reply else exc.WorkerCrashedError()
+            for spec, _keep in crashed:
+                self.w._store_errors(spec["return_ids"], err)
+
+        try:
+            self.w.request_async(lambda rid: (P.EXIT_DETAIL, rid, addr), done)
+        except Exception:  # noqa: BLE001 - the head is gone: plain crash errors
+            done(None)
 
     # ------------------------------------------------------------------ bookkeeping
     def _record(self, spec, status, lease: _Lease, attempt, t0, t1):

@@ -151,10 +151,18 @@ def serve(path: str):
                         except ProcessLookupError:
                             pass
                     continue
-                pid = os.fork()
-                if pid == 0:
-                    _child(req["env"], req["log"], listen, conn)
-                children.add(pid)
+                # SIGCHLD stays blocked across fork + add: a child that exits at once is reaped only after
+                # it is in `children`, so a reaped pid can never be left there (and later signalled after
+                # the kernel reused it)
+                signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGCHLD})
+                try:
+                    pid = os.fork()
+                    if pid == 0:
+                        signal.pthread_sigmask(signal.SIG_UNBLOCK, {signal.SIGCHLD})
+                        _child(req["env"], req["log"], listen, conn)
+                    children.add(pid)
+                finally:
+                    signal.pthread_sigmask(signal.SIG_UNBLOCK, {signal.SIGCHLD})
                 reply = {"pid": pid}
             except Exception as e:  # noqa: BLE001
                 reply = {"error": repr(e)}

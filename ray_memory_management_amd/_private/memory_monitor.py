@@ -1,11 +1,27 @@
-"""Node memory monitor. Parity: reference python/ray/_private/memory_monitor.py and the raylet's
-memory-pressure worker killing (src/ray/raylet/worker_killing_policy.cc in later versions):
-when node memory usage crosses `memory_usage_threshold`, the most recently started retriable
-task worker is killed (its task is retried), which is the reference's policy."""
+"""Node memory monitor and the memory-pressure worker-killing policy.
+
+Parity:
+* reference python/ray/_private/memory_monitor.py (node usage from /proc/meminfo, cgroup limits);
+* src/ray/common/memory_monitor.cc (a periodic usage check against `memory_usage_threshold_fraction`
+  every `memory_monitor_interval_ms`, 0 disables);
+* src/ray/raylet/node_manager.cc:2902-3001 CreateMemoryUsageRefreshCallback /
+  WorkersWithLatestSubmittedTasks: above the threshold, the registered worker whose task was assigned
+  most recently is killed -- task or actor, retriable or not -- with a "System memory low at node with IP
+  ..." exit detail, and no new victim is picked until that one is dead (one eviction in flight, since a
+  kill can take seconds to return memory).
+
+The policy itself runs in the head (`Head._memory_pressure`); this module holds the usage source and
+the victim choice so both are unit-testable. The usage source is injectable: `_system_config=
+{"memory_monitor_test_usage_file": path}` reads "used total" (bytes) or a single fraction from a file, so
+tests drive memory pressure deterministically without exhausting the machine's RAM;
+`{"memory_monitor_test_usage_dir": path}` sums per-process "allocations" of live pids (a killed worker's
+share disappears with it, as real memory does).
+"""
 from __future__ import annotations
 
 import os
 import time
+from typing import Callable, Optional, Tuple
 
 
 def _read_meminfo():
@@ -40,41 +56,139 @@ def get_used_and_total():
     return total - avail, total
 
 
+def file_usage_source(path: str) -> Callable[[], Tuple[int, int]]:
+    """Usage from a file: "used total" in bytes, or one fraction in [0, 1] (of the real total). A missing
+    or unreadable file falls back to the real node usage."""
+
+    def read():
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+        except OSError:
+            return get_used_and_total()
+        try:
+            if len(parts) >= 2:
+                return int(float(parts[0])), int(float(parts[1]))
+            if len(parts) == 1:
+                _, total = get_used_and_total()
+                return int(float(parts[0]) * total), total
+        except ValueError:
+            pass
+        return get_used_and_total()
+
+    return read
+
+
+def dir_usage_source(path: str, total: int = 16 << 30) -> Callable[[], Tuple[int, int]]:
+    """Simulated node memory for tests: every process "allocates" by writing a byte count into
+    `<path>/<its pid>`; usage is the sum over processes still alive, so a killed worker's memory is
+    returned to the node exactly as a real kill returns it. `<path>/total` overrides the capacity."""
+
+    def read():
+        used, cap = 0, total
+        try:
+            names = os.listdir(path)
+        except OSError:
+            return 0, cap
+        for n in names:
+            try:
+                with open(os.path.join(path, n)) as f:
+                    v = int(float(f.read().strip() or 0))
+            except (OSError, ValueError):
+                continue
+            if n == "total":
+                cap = v
+            elif n.isdigit() and pid_alive(int(n)):
+                used += v
+        return used, cap
+
+    return read
+
+
+def format_eviction_message(ip: str, used: int, total: int, threshold: float, name: str, kind: str,
+                            ident: str) -> str:
+    """The exit detail of a worker killed for memory (reference node_manager.cc:2932-2945)."""
+    gb = 1024 ** 3
+    frac = used / total if total else 0.0
+    return (f"System memory low at node with IP {ip}. Used memory ({used / gb:.2f}GB) / total capacity "
+            f"({total / gb:.2f}GB) ({frac:.6f}) exceeds threshold {threshold}, killing latest task with name "
+            f"{name} and {kind} ID {ident} to avoid running out of memory.\n"
+            "This may indicate a memory leak in a task or actor, or that too many tasks are running in parallel.")
+
+
 class MemoryMonitor:
-    def __init__(self, threshold: float = 0.95, min_interval: float = 0.25):
-        self.threshold = threshold
-        self.min_interval = min_interval
+    """Periodic usage check (`interval_s`) against `threshold`, plus the single in-flight eviction target."""
+
+    def __init__(self, threshold: float = 0.95, interval_s: float = 0.25,
+                 usage_fn: Optional[Callable[[], Tuple[int, int]]] = None):
+        self.threshold = float(threshold)
+        self.interval_s = max(float(interval_s), 0.0)
+        self.usage_fn = usage_fn or get_used_and_total
         self.last = 0.0
         self.last_used = 0
         self.last_total = 0
+        self.above = False
         self.kills = 0
+        self.task_evictions = 0
+        self.actor_evictions = 0
+        self.target = None          # the worker being evicted (one at a time)
+        self.target_since = 0.0
+        self.last_wait_log = 0.0
 
     def snapshot(self):
-        used, total = get_used_and_total()
-        return {"used": used, "total": total, "threshold": self.threshold, "kills": self.kills}
+        used, total = self.usage_fn()
+        return {"used": used, "total": total, "threshold": self.threshold, "kills": self.kills,
+                "task_evictions": self.task_evictions, "actor_evictions": self.actor_evictions,
+                "interval_ms": self.interval_s * 1000.0,
+                "eviction_in_flight": self.target is not None}
 
-    def over_threshold(self) -> bool:
-        now = time.time()
-        if now - self.last < self.min_interval:
-            return False
+    def refresh(self, now: Optional[float] = None) -> Optional[bool]:
+        """Re-read usage if the interval elapsed: True / False above the threshold, None when not due."""
+        now = time.time() if now is None else now
+        if now - self.last < self.interval_s:
+            return None
         self.last = now
-        used, total = get_used_and_total()
+        used, total = self.usage_fn()
         self.last_used, self.last_total = used, total
-        return total > 0 and used / total > self.threshold
+        self.above = total > 0 and used / total > self.threshold
+        return self.above
 
-    def pick_victim(self, head):
-        if self.threshold >= 1.0 or not self.over_threshold():
-            return None
-        cands = []
-        for w in head.workers.values():
-            if w.task is None or w.state != "BUSY":
-                continue
-            t = head.tasks.get(w.task)
-            if t is None or t.retries_left == 0:
-                continue
-            cands.append((t.start_time or 0, w))
-        if not cands:
-            return None
-        cands.sort(key=lambda x: x[0])
+    # kept for callers of the round-5 API
+    def over_threshold(self) -> bool:
+        return bool(self.refresh())
+
+    @staticmethod
+    def pick_victim(workers):
+        """The worker whose task (or actor) was assigned most recently (WorkersWithLatestSubmittedTasks).
+        `workers` yields (assigned_time, worker) for every worker with an assigned task or actor."""
+        best = None
+        for t, w in workers:
+            if best is None or t > best[0]:
+                best = (t, w)
+        return None if best is None else best[1]
+
+    def record_kill(self, is_actor: bool, target, now: Optional[float] = None):
         self.kills += 1
-        return cands[-1][1]
+        if is_actor:
+            self.actor_evictions += 1
+        else:
+            self.task_evictions += 1
+        self.target = target
+        self.target_since = time.time() if now is None else now
+
+
+def pid_alive(pid: Optional[int]) -> bool:
+    if not pid:
+        return False
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            st = f.read()
+        return st[st.rindex(")") + 2] not in "ZX"
+    except (OSError, ValueError, IndexError):
+        return True

@@ -107,7 +107,7 @@ class Conn:
 class WorkerRec:
     __slots__ = ("worker_id", "pid", "proc", "conn", "node", "env_key", "state", "task", "actor_id",
                  "fns", "gpu_key", "blocked", "start_time", "tasks_run", "lease", "idle_since", "calls",
-                 "direct_addr")
+                 "direct_addr", "assigned_time", "exit_detail")
 
     def __init__(self, worker_id, proc, node, env_key, gpu_key):
         self.worker_id = worker_id
@@ -128,6 +128,8 @@ class WorkerRec:
         self.idle_since = time.time()
         self.calls = collections.Counter()
         self.direct_addr = None  # the worker's direct-task socket (leased task submission)
+        self.assigned_time = 0.0  # when its current task / lease / actor was assigned (memory-pressure victim order)
+        self.exit_detail = None   # why the head killed it (e.g. the memory monitor's "System memory low ...")
 
 
 class TaskRec:
@@ -309,11 +311,19 @@ class Head:
         self.gcs_restored = {"kv_namespaces": 0, "actors": 0, "jobs": 0}
         self.watcher = threading.Thread(target=self._seal_watcher, daemon=True)
         self.watcher.start()
-        if self.config.get("memory_monitor_refresh_ms", 250) > 0:
-            from ray_memory_management_amd._private.memory_monitor import MemoryMonitor
+        # memory-pressure worker killing (reference keys memory_usage_threshold_fraction /
+        # memory_monitor_interval_ms, 0 disables; the round-5 keys are accepted as aliases)
+        self.exit_details = collections.OrderedDict()  # worker id / direct addr / actor id -> exit detail
+        self.dead_workers = collections.deque(maxlen=1000)  # state API rows of exited workers
+        mm_ms = self.config.get("memory_monitor_interval_ms", self.config.get("memory_monitor_refresh_ms", 250))
+        if float(mm_ms) > 0:
+            from ray_memory_management_amd._private import memory_monitor as _mm
 
-            self.memory_monitor = MemoryMonitor(
-                threshold=float(self.config.get("memory_usage_threshold", 0.95)))
+            thr = self.config.get("memory_usage_threshold_fraction", self.config.get("memory_usage_threshold", 0.95))
+            src, sdir = self.config.get("memory_monitor_test_usage_file"), self.config.get("memory_monitor_test_usage_dir")
+            usage = _mm.file_usage_source(src) if src else _mm.dir_usage_source(sdir) if sdir else None
+            self.memory_monitor = _mm.MemoryMonitor(threshold=float(thr), interval_s=float(mm_ms) / 1000.0,
+                                                    usage_fn=usage)
 
     def _spill_dirs(self):
         """Spill directories: `spill_dir` (str or list) or the reference's object_spilling_config
@@ -575,6 +585,8 @@ class Head:
             self._lease_request(c, m[1], m[2])
         elif t == P.LEASE_RETURN:
             self._lease_return(m[1], m[2])
+        elif t == P.EXIT_DETAIL:  # why a worker / actor died, if the head killed it (owner-side errors)
+            self._reply(c, m[1], self.exit_details.get(m[2]))
         elif t == P.FN_EXPORT:
             self.fn_table[m[1]] = m[2]
         elif t == P.TASK_DONE:
@@ -704,6 +716,7 @@ class Head:
                 self._kill_worker(w)
                 return
             w.state = "ACTOR"
+            w.assigned_time = time.time()
             self._send_nb(c, (P.CREATE_ACTOR_INSTANCE, a.spec, self.fn_table.get(a.spec["class_id"]),
                               {"gpu_ids": a.assign[1] if a.assign else [], "node_id": a.node,
                                "restart": a.num_restarts}))
@@ -893,6 +906,9 @@ class Head:
         prev_state = w.state
         w.state = "GONE"
         self.workers.pop(w.worker_id, None)
+        self.dead_workers.append({"worker_id": w.worker_id.hex(), "pid": w.pid, "state": "DEAD", "node_id": w.node,
+                                  "actor_id": w.actor_id.hex() if w.actor_id else None, "tasks_run": w.tasks_run,
+                                  "exit_detail": w.exit_detail})
         for lst in self.idle.values():
             if w in lst:
                 lst.remove(w)
@@ -941,7 +957,9 @@ class Head:
                     t.state = PENDING
                     self._enqueue(t)
                 else:
-                    self._fail_task(t, exc.WorkerCrashedError(), FAILED)
+                    err = exc.OutOfMemoryError(w.exit_detail) if t.error == "oom" and w.exit_detail \
+                        else exc.WorkerCrashedError()
+                    self._fail_task(t, err, FAILED)
         if w.actor_id is not None:
             a = self.actors.get(w.actor_id)
             if a is not None and a.worker is w:
@@ -1213,7 +1231,7 @@ class Head:
             w.task = spec["task_id"]
             t.worker = w
             t.state = RUNNING
-            t.start_time = time.time()
+            t.start_time = w.assigned_time = time.time()
             self.lease_stats["granted"] += 1
             multi = self._multi_node()
             self._reply(t.owner_conn, spec["_lease"], ("granted", spec["task_id"], w.direct_addr, w.worker_id,
@@ -1232,7 +1250,7 @@ class Head:
         w.task = spec["task_id"]
         t.worker = w
         t.state = RUNNING
-        t.start_time = time.time()
+        t.start_time = w.assigned_time = time.time()
         self._send_nb(w.conn, (P.EXECUTE, spec, blob, {"gpu_ids": gpu_ids, "attempt": t.attempt,
                                                        "node_id": node}))
         return True
@@ -1582,12 +1600,16 @@ class Head:
         if what == "cluster_resources":
             return self.sched.cluster_total()
         if what == "available_resources":
-            return self.sched.cluster_available()
+            # object_store_memory is reported as the store's free bytes (reference: the raylet reports
+            # plasma usage against the resource, python/ray/tests/test_memory_scheduling.py:46)
+            return self._store_adjusted(self.sched.cluster_available())
         if what == "nodes":
             out = []
             for nid, n in self.nodes.items():
                 out.append({"NodeID": nid, "Alive": n["alive"], "Resources": self.sched.total(nid) if n["alive"] else {},
-                            "Available": self.sched.available(nid) if n["alive"] else {}, "IsHead": n["is_head"],
+                            "Available": (self._store_adjusted(self.sched.available(nid)) if n["is_head"]
+                                          else self.sched.available(nid)) if n["alive"] else {},
+                            "IsHead": n["is_head"],
                             "NodeManagerAddress": "127.0.0.1", "ObjectStoreSocketName": self.store_name,
                             "alive": n["alive"]})
             return out
@@ -1620,8 +1642,9 @@ class Head:
                                                           if t.spec.get("_lease") is not None and t.state == RUNNING)}
         if what == "workers":
             return [{"worker_id": w.worker_id.hex(), "pid": w.pid, "state": w.state, "node_id": w.node,
-                     "actor_id": w.actor_id.hex() if w.actor_id else None, "tasks_run": w.tasks_run}
-                    for w in self.workers.values()]
+                     "actor_id": w.actor_id.hex() if w.actor_id else None, "tasks_run": w.tasks_run,
+                     "exit_detail": w.exit_detail}
+                    for w in self.workers.values()] + list(self.dead_workers)
         if what == "objects":
             objs = self.store.list_objects()
             for o in objs:
@@ -1663,6 +1686,16 @@ class Head:
                     "pinned_arg_tasks": self.pinned_arg_tasks, "spills_in_flight": self.spills_in_flight,
                     "spill_dirs": self.spill_dirs, **self.store.oom_stats()}
         raise ValueError(f"unknown state query {what}")
+
+    def _store_adjusted(self, avail: dict) -> dict:
+        if "object_store_memory" in avail:
+            try:
+                used = self.store.stats()["bytes_in_use"]
+            except Exception:  # noqa: BLE001
+                used = 0
+            avail = dict(avail)
+            avail["object_store_memory"] = max(0.0, float(avail["object_store_memory"]) - float(used))
+        return avail
 
     # ------------------------------------------------------------------ housekeeping
     def _housekeeping(self):
@@ -1719,21 +1752,74 @@ class Head:
                         idle_total -= 1
         if self.autoscaler is not None:
             self.autoscaler.tick()
-        # memory monitor: kill the newest retriable task worker when the node is nearly OOM
         if self.memory_monitor is not None:
-            victim = self.memory_monitor.pick_victim(self)
-            if victim is not None:
-                t = self.tasks.get(victim.task) if victim.task else None
-                if t is not None:
-                    t.error = "oom"
-                mm = self.memory_monitor
-                self._event("RAYLET", "ERROR", "OUT_OF_MEMORY",
-                            f"Killed worker pid {victim.pid} to relieve memory pressure (used "
-                            f"{getattr(mm, 'last_used', None)} of {getattr(mm, 'last_total', None)} bytes, "
-                            f"threshold {mm.threshold}).",
-                            pid=victim.pid, task_id=self._hex(t.spec["task_id"]) if t is not None else None,
-                            job_id=self._hex(t.spec.get("job_id")) if t is not None else None)
-                self._kill_worker(victim)
+            self._memory_pressure(now)
+
+    # ------------------------------------------------------------------ memory-pressure worker killing
+    def _memory_pressure(self, now: float):
+        """Reference node_manager.cc:2902-3001: above `memory_usage_threshold_fraction`, kill the worker whose
+        task / lease / actor was assigned most recently -- retriable or not, task or actor -- and pick no new
+        victim until that one is dead. Its task is retried by its owner while retries are left (head path:
+        here; leased workers: the owner's direct submitter), else fails with OutOfMemoryError (a
+        WorkerCrashedError) carrying the exit detail; an actor without restarts dies with it as the death
+        cause (RayActorError)."""
+        from ray_memory_management_amd._private import memory_monitor as _mm
+
+        mm = self.memory_monitor
+        if mm.target is not None:
+            tw = mm.target
+            gone = tw.state == "GONE" or (tw.proc.poll() is not None if tw.proc is not None else not _mm.pid_alive(tw.pid))
+            if gone:
+                mm.target = None
+        above = mm.refresh(now)
+        if not above:
+            return
+        if mm.target is not None:  # one eviction in flight: wait for it to return memory
+            if now - mm.last_wait_log > 1.0:
+                mm.last_wait_log = now
+                self.mem_stats["memory_manager_eviction_waits"] += 1
+            return
+        cands = []
+        for w in self.workers.values():
+            if w.state in ("DEAD", "GONE", "STARTING") or w.conn is None:
+                continue
+            if w.task is None and w.actor_id is None:
+                continue
+            cands.append((w.assigned_time, w))
+        victim = mm.pick_victim(cands)
+        if victim is None:
+            return
+        t = self.tasks.get(victim.task) if victim.task is not None else None
+        is_actor = victim.actor_id is not None
+        a = self.actors.get(victim.actor_id) if is_actor else None
+        if is_actor:
+            name = (a.spec.get("class_name") if a is not None else None) or "actor"
+            kind, ident = "actor", victim.actor_id.hex()
+        elif t is not None and t.spec.get("_lease") is not None:
+            name, kind, ident = "leased worker (direct tasks)", "task", self._hex(t.spec["task_id"])
+        else:
+            name = (t.spec.get("name") if t is not None else None) or "task"
+            kind, ident = "task", self._hex(t.spec["task_id"]) if t is not None else "?"
+        detail = _mm.format_eviction_message("127.0.0.1", mm.last_used, mm.last_total, mm.threshold, name, kind, ident)
+        victim.exit_detail = detail
+        ed = self.exit_details
+        for key in (victim.worker_id, victim.direct_addr, victim.actor_id):
+            if key is not None:
+                ed[key] = detail
+        while len(ed) > 10000:
+            ed.popitem(last=False)
+        if t is not None:
+            t.error = "oom"
+        if a is not None and a.restarts_left == 0:
+            a.death_cause = detail
+        mm.record_kill(is_actor, victim, now)
+        self.mem_stats["memory_manager_actor_eviction_total" if is_actor else "memory_manager_task_eviction_total"] += 1
+        self._event("RAYLET", "ERROR", "OUT_OF_MEMORY", detail, pid=victim.pid, worker_id=self._hex(victim.worker_id),
+                    task_id=self._hex(t.spec["task_id"]) if t is not None else None,
+                    actor_id=self._hex(victim.actor_id),
+                    job_id=self._hex(t.spec.get("job_id")) if t is not None else None)
+        print(f"[head] {detail}", file=sys.stderr, flush=True)
+        self._kill_worker(victim)
 
     # ------------------------------------------------------------------ scheduler warnings
     def _push_error(self, job_id, etype: str, msg: str, **fields):

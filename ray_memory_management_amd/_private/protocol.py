@@ -52,6 +52,7 @@ LEASE_REQUEST = 33   # owner asks for a worker lease (direct task submission)
 LEASE_RETURN = 34    # owner hands a lease back (optionally: kill the worker)
 DIRECT_DONE = 35     # batched completion records of directly submitted tasks (lineage + state)
 FN_EXPORT = 36       # function blob for the head's table (first direct submission of a function)
+EXIT_DETAIL = 37     # (EXIT_DETAIL, rid, worker id | direct addr | actor id) -> why the head killed it, or None
 
 # ---- head -> worker
 EXECUTE = 101

@@ -81,8 +81,15 @@ class RayTaskError(RayError):
 
 
 class WorkerCrashedError(RayError):
+    def __init__(self, message: str = None):
+        self.message = message
+        super().__init__(*([message] if message else []))
+
     def __str__(self):
-        return "The worker died unexpectedly while executing this task."
+        return self.message or "The worker died unexpectedly while executing this task."
+
+    def __reduce__(self):
+        return (type(self), (self.message,))
 
 
 class RayActorError(RayError):
@@ -158,8 +165,13 @@ class OutOfDiskError(RayError):
     pass
 
 
-class OutOfMemoryError(RayError):
-    pass
+class OutOfMemoryError(WorkerCrashedError):
+    """The worker running the task was killed by the node's memory monitor (reference node_manager.cc:2902
+    memory-pressure eviction). A WorkerCrashedError, as the reference of this era raises for it; the message
+    is the eviction's exit detail ("System memory low at node with IP ...")."""
+
+    def __str__(self):
+        return self.message or "The worker was killed because the node ran low on memory."
 
 
 class NodeDiedError(RayError):

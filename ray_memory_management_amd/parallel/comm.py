@@ -248,6 +248,24 @@ class _FlatView:
         self.ptr, self.count, self.device = ptr, count, device
 
 
+def zero1_blocks_for(h, device: int, ranks_on_device: int = 1, cap: int = 256, concurrent_per_cu: int = 1) -> int:
+    """Workgroups of the ZeRO-1 launch, from the kernel's occupancy instead of a constant.
+
+    Every workgroup of `k_peer_zero1` waits (bounded) on its peers' same-index workgroups, so ALL the
+    workgroups of every rank driving the GPU must be resident at once, next to the kernels the learner
+    runs concurrently on its compute stream (fork mode: the trunk backward, one 512-thread workgroup per
+    CU): per rank ((zero1 workgroups per CU - concurrent_per_cu) x CUs) / ranks on the device, capped at
+    `cap` (256 measured best for the fp32 PPO bucket on one GPU per rank: the Adam pass over 1/W of the
+    bucket is latency-bound at 64), rounded down to a multiple of 8, at least 8."""
+    try:
+        occ = h.peer_occupancy(int(device))
+        slots = max(0, int(occ["zero1_per_cu"]) - int(concurrent_per_cu)) * int(occ["cus"])
+    except Exception:  # noqa: BLE001 - no query: the conservative all-reduce count
+        return 64
+    n = min(int(cap), slots // max(1, int(ranks_on_device)))
+    return max(8, n - n % 8)
+
+
 class PeerComm(Comm):
     """MI355X-native intra-node all-reduce (csrc/hip/peer_allreduce.hip): every rank exports a
     staging region once through hipIPC and maps every peer's; one kernel per all-reduce reads the
@@ -338,12 +356,13 @@ class PeerComm(Comm):
         # over 1/W of the bucket wants many more workgroups than the plain all-reduce's barrier fan-in
         # does (64 -> 256: the fp32 PPO bucket's step on 64 workgroups was latency-bound), and one
         # communicator must keep one workgroup count (its staging reuse is argued per workgroup slice)
+        buses = [store.get(f"{key}/bus{r}") for r in range(self.world)]
+        #: ranks driving this rank's physical GPU (1 = one process per GPU)
+        self.ranks_on_device = max(1, buses.count(buses[self.rank]))
         if zero1_blocks is None:
             env = os.environ.get("RMM_PEER_ZERO1_BLOCKS")
-            # ranks sharing one GPU compete for the same workgroup slots, and a rank's workgroup that
-            # waits for a peer's same-index one that cannot be placed waits until the timeout: there,
-            # unless set explicitly, the all-reduce's count
-            zero1_blocks = int(env) if env else (min(256, nblocks) if self.shared_device else 256)
+            zero1_blocks = int(env) if env else zero1_blocks_for(h, self.device.index, self.ranks_on_device)
+        self.zero1_blocks = int(zero1_blocks)
         self._cz = None
         if zero1_blocks > 0:
             zerr, zblob = None, b""
@@ -407,6 +426,8 @@ class PeerComm(Comm):
         """Make fp32 buffers (moment pointers) that `allreduce_adam_on(count elements of grad_dtype)` only
         keeps current on each element's owner identical on every rank: zero the unowned elements, then
         sum (exact: one non-zero term per element)."""
+        if self._cz is None:
+            raise RuntimeError("PeerComm: the ZeRO-1 communicator is not open (zero1_blocks=0 or setup failed)")
         st = stream or torch.cuda.current_stream(self.device)
         for ptr in bufs:
             t = _FlatView(int(ptr), int(count), self.device)
@@ -441,10 +462,10 @@ class PeerComm(Comm):
         if t.is_cuda:
             # any other dtype (float64, integers, bool): its raw bytes, one fp32 per byte (0..255 are
             # exact in fp32 and so is x + 0), so the result is bit-exact whatever the dtype
-            src_t = t.contiguous()
+            src_t = t.contiguous().reshape(-1)  # 1-d first: a 0-dim tensor of a wide dtype cannot view as bytes
             f = src_t.view(torch.uint8).float() if src_t.numel() else torch.zeros(0, device=t.device)
             self.broadcast(f, src)
-            t.copy_(f.to(torch.uint8).view(t.dtype).view(src_t.shape))
+            t.copy_(f.to(torch.uint8).view(t.dtype).view(t.shape))
             return
         if self.fallback is None:
             raise ValueError(f"PeerComm.broadcast: unsupported tensor {t.dtype} on {t.device}")

@@ -283,9 +283,12 @@ def _rank_main(rank, world, path, out_dir, bench_iters, sweep=False):
     i64 = torch.randint(-2**62, 2**62, (33,), generator=g, dtype=torch.int64).to(d)
     bi = i64.clone() if rank == 0 else torch.zeros_like(i64)
     comm.broadcast(bi, src=0)
+    s0 = torch.tensor(-(2**61) - 7, dtype=torch.int64, device=d)  # 0-dim, 8-byte dtype
+    b0 = s0.clone() if rank == 0 else torch.zeros_like(s0)
+    comm.broadcast(b0, src=0)
     torch.cuda.synchronize()
-    res["cases"]["broadcast_bytes_f64_i64"] = {"ok": bool(torch.equal(b64, src64)) and bool(torch.equal(bi, i64)),
-                                               "n": 810}
+    res["cases"]["broadcast_bytes_f64_i64"] = {"ok": bool(torch.equal(b64, src64)) and bool(torch.equal(bi, i64))
+                                               and b0.dim() == 0 and bool(torch.equal(b0, s0)), "n": 818}
 
     # graph capture: 3 all-reduces inside one graph, replayed with fresh inputs
     n = 65536 + 3

@@ -18,6 +18,10 @@ import numpy as np
 from ray_memory_management_amd.rllib.ppo_learner import bootstrap_value
 
 
+class _GateTimeout(RuntimeError):
+    """A gated policy step gave up waiting for its frames (the fragment is re-sampled ungated)."""
+
+
 class GPURolloutWorker:
     def __init__(self, env_creator=None, config: Optional[Dict] = None, worker_index: int = 0,
                  num_workers: int = 0, policy_config: Optional[Dict] = None, seed: Optional[int] = None):
@@ -57,6 +61,20 @@ class GPURolloutWorker:
         return {}
 
     def sample(self, *_after):  # _after: refs the runtime resolves first (prefetched samples)
+        """One fragment. A step-gate timeout (the host stalled longer than `rollout_gate_timeout_ms`
+        between a launch and its release, so a gated policy step read stale frames) never fails the
+        iteration: that fragment is discarded and re-sampled once on the ungated path."""
+        try:
+            return self._sample_once()
+        except _GateTimeout:
+            self.gate_timeouts = getattr(self, "gate_timeouts", 0) + 1
+            self._gate_bypass = True
+            try:
+                return self._sample_once()
+            finally:
+                self._gate_bypass = False
+
+    def _sample_once(self):
         import time
 
         import torch
@@ -569,7 +587,7 @@ class HybridRolloutWorker(GPURolloutWorker):
                                                                           spin=spin))
                 if "gate_err" in direct and int(self._gate_err.item()):
                     self._gate_err.zero_()  # a gated step gave up waiting: it ran on stale frames
-                    raise RuntimeError("rollout step gate timed out during this fragment; fragment discarded")
+                    raise _GateTimeout("rollout step gate timed out during this fragment; fragment discarded")
             elif server is not None:  # K21: the whole fragment in ONE persistent kernel launch
                 from ray_memory_management_amd._native import require_hip
 
@@ -692,7 +710,7 @@ class HybridRolloutWorker(GPURolloutWorker):
                 self._h_seq_dev = int(require_hip().host_device_pointer(self._h_seq.data_ptr()))
             if self._h_seq_dev:
                 out.update(host_seq=self._h_seq.data_ptr(), host_seq_dev=self._h_seq_dev)
-        if k.get("x3") and os.environ.get("RMM_ROLLOUT_DIRECT_GATE", "1") != "0":
+        if k.get("x3") and os.environ.get("RMM_ROLLOUT_DIRECT_GATE", "1") != "0" and not getattr(self, "_gate_bypass", False):
             # in-kernel step gate (fp32 policy): step t+1 is launched before step t's env step and K10x
             # waits for the host's release counter before reading the new frames, so the three launches
             # leave the step's critical path
@@ -709,8 +727,10 @@ class HybridRolloutWorker(GPURolloutWorker):
                 # (K10x workgroup b waits for its own range): the first frames cross PCIe while the rest
                 # are stepped. RMM_ROLLOUT_GATE_PARTS=1: one release after the whole env step
                 parts = int(os.environ.get("RMM_ROLLOUT_GATE_PARTS", "10"))
+                tmo = int(os.environ.get("RMM_ROLLOUT_GATE_TIMEOUT_MS") or self.config.get("rollout_gate_timeout_ms", 2000))
                 out.update(release=self._h_rel.data_ptr(), release_dev=self._h_rel_dev,
-                           gate_err=self._gate_err.data_ptr(), gate_parts=max(1, min(parts, int(k["B"]))))
+                           gate_err=self._gate_err.data_ptr(), gate_parts=max(1, min(parts, int(k["B"]))),
+                           gate_timeout_ms=max(1, tmo))
         return out
 
     def _kernel_args(self, G, S):

@@ -247,6 +247,8 @@ class LearnerActor:
                 "split_graphs": L._graphs_split is not None, "graphs": bool(L.graphs),
                 "chain": int(getattr(L, "_chain", 1)), "launches": int(getattr(L.comm, "launches", 0)),
                 "zero1": bool(getattr(L, "_zero1", lambda: False)()),
+                "zero1_blocks": getattr(L.comm, "zero1_blocks", None),
+                "ranks_on_device": getattr(L.comm, "ranks_on_device", None),
                 "peer_mode": L._peer_mode() if hasattr(L, "_peer_mode") and L.world > 1 else None}
 
     def device_info(self):

@@ -179,14 +179,15 @@ def test_chaos_readers_killed_while_holding_views(chaos_cluster):
     assert _wait_bytes(base) == base, object_store_stats()
 
 
-@pytest.mark.skipif(os.environ.get("RMM_CHAOS_SOAK") != "1",
-                    reason="soak test: about 1 run in 10 leaves the head unresponsive (its state queries block) "
-                           "when workers die while creates wait on spills; root cause not yet found, run with "
-                           "RMM_CHAOS_SOAK=1")
 def test_chaos_under_spilling():
     """Workers killed while the store is over capacity (creates wait on spills, gets restore spilled
     objects): every object reads back intact, and once the refs are gone neither store memory nor spill
-    files are left behind (reference test_chaos.py runs its workloads with object spilling on)."""
+    files are left behind (reference test_chaos.py runs its workloads with object spilling on).
+
+    Round 5 kept this opt-in: about one run in ten hung the node. A creator killed while its create
+    waited for memory was aborted by freeing heap offset 0, which corrupted the segment header and left
+    a cycle in the LRU list (fixed in csrc/store/shm_store.cc FreeEntryStorage; deterministic test in
+    tests/test_store_dead_creator.py). The store's integrity counters must stay at zero."""
     ray.init(num_cpus=4, object_store_memory=64 << 20)
     try:
         base = _store_bytes()
@@ -218,5 +219,9 @@ def test_chaos_under_spilling():
         while time.time() < deadline and object_store_stats()["spilled_bytes_current"]:
             time.sleep(0.1)
         assert object_store_stats()["spilled_bytes_current"] == 0, object_store_stats()
+        from ray_memory_management_amd._private.worker import global_worker
+
+        integ = global_worker.store.integrity()
+        assert integ["corruptions_total"] == 0 and integ["lock_stalls_total"] == 0, integ
     finally:
         ray.shutdown()

@@ -62,6 +62,11 @@ def test_state_lists_and_filters(dash):
     assert all(x["state"] == "DEAD" for x in _get(url + "/api/v0/actors?" + q)["result"])
     objs = _get(url + "/api/v0/objects")["result"]
     assert any(o["object_id"] == ref.hex() for o in objs)
+    # directly submitted tasks reach the head's task table with the owner's batched completion records
+    # (flushed every 10 ms): eventually consistent, as the reference's state API is
+    deadline = time.time() + 10
+    while _get(url + "/api/v0/tasks/summarize")["cluster"]["total_tasks"] < 3 and time.time() < deadline:
+        time.sleep(0.05)
     assert _get(url + "/api/v0/tasks/summarize")["cluster"]["total_tasks"] >= 3
     assert _get(url + "/api/v0/tasks?limit=1")["total"] == 1
     ray.kill(a)

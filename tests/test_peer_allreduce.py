@@ -63,7 +63,7 @@ def test_peer_allreduce_three_ranks_two_shot():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("learners,mode", [(2, None), (3, None), (2, "fork")])
+@pytest.mark.parametrize("learners,mode", [(2, None), (3, None), (2, "fork"), (4, "fork")])
 def test_ppo_learner_actors_peer_comm_in_graph(ray_start, learners, mode, monkeypatch):
     """2 / 3 fused PPO learner actors on one GPU over PeerComm: the optimizer step is the ZeRO-1 launch
     (reduce-scatter + Adam + all-gather; its bits equal all-reduce -> K6 in the peer self-test) INSIDE
@@ -95,6 +95,15 @@ def test_ppo_learner_actors_peer_comm_in_graph(ray_start, learners, mode, monkey
         assert all(i["comm"] == "PeerComm" and i["graph_has_comm"] and i["chain"] > 1 and i["zero1"]
                    and i["peer_mode"] == (mode or "one") for i in info), info
         assert len({i["launches"] for i in info}) == 1 and info[0]["launches"] > 0, info
+        # ZeRO-1 workgroups derived from the kernel's occupancy: every rank's workgroups resident together
+        # beside one concurrent workgroup per CU (the trunk backward in fork mode)
+        from ray_memory_management_amd._native import require_hip
+        from ray_memory_management_amd.parallel.comm import zero1_blocks_for
+
+        want = zero1_blocks_for(require_hip(), 0, learners)
+        occ = require_hip().peer_occupancy(0)
+        assert all(i["ranks_on_device"] == learners and i["zero1_blocks"] == want for i in info), (info, want)
+        assert learners * want <= (occ["zero1_per_cu"] - 1) * occ["cus"], (occ, want)
         d = algo.learner_group.weights_digests()
         assert len(set(d)) == 1, d
     finally:

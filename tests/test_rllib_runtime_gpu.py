@@ -543,3 +543,29 @@ def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T, 
         for k in ("obs", "_raw", "_boot"):
             assert torch.equal(x[k], y[k]), k
     assert len(a._completed) > 0 and a._completed == b._completed
+
+
+def test_gate_timeout_resamples_the_fragment_ungated(cuda, monkeypatch):
+    """A host that stalls longer than the step gate's bound between a launch and its release
+    (RMM_TEST_GATE_DELAY_US in the native loop, gate bound 1 ms) makes the gated policy steps give up
+    and read stale frames: sample() discards that fragment and re-samples it on the ungated path instead
+    of failing the iteration; once the host keeps up again the gated path is used with no timeout."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": 6,
+           "rollout_fragment_length": 8, "seed": 3, "compute_dtype": "fp32", "rollout_gate_timeout_ms": 1}
+    monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "1")
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT_GATE", "1")
+    monkeypatch.setenv("RMM_TEST_GATE_DELAY_US", "20000")
+    a = HybridRolloutWorker(config=cfg)
+    fa = a.sample()
+    assert getattr(a, "gate_timeouts", 0) == 1
+    monkeypatch.delenv("RMM_TEST_GATE_DELAY_US")
+    a.config["rollout_gate_timeout_ms"] = 2000
+    fb = a.sample()
+    assert getattr(a, "gate_timeouts", 0) == 1
+    for f in (fa, fb):
+        assert f["obs"].shape[:2] == (8, 6) and torch.isfinite(f["_raw"].float()).all()
