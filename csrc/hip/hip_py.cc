@@ -165,6 +165,26 @@ py::object make_dlpack(uint64_t ptr, std::vector<int64_t> shape, int code, int b
 
 }  // namespace
 
+// adam (the x3 tail Adam): [master, m1, m2, grad, whi, wlo, n_trunk, n, hp, step_ctr, bump, nbump, done, bump_next
+// (, grad2: the K12x second row part's dense + heads gradients)]; empty = no Adam
+X3Adam x3_adam_args(const std::vector<uint64_t>& adam, float grad_scale, const char* who) {
+  X3Adam xa;
+  if (adam.empty()) return xa;
+  if (adam.size() != 14 && adam.size() != 15) throw std::invalid_argument(std::string(who) + ": adam needs 14 or 15 fields");
+  if (adam.size() == 15 && adam[14]) {
+    if (adam[14] & 15) throw std::invalid_argument(std::string(who) + ": grad2 must be 16-byte aligned");
+    xa.grad2 = P<const float>(adam[14]);
+  }
+  xa.master = P<float>(adam[0]), xa.m1 = P<float>(adam[1]), xa.m2 = P<float>(adam[2]);
+  xa.grad = P<const float>(adam[3]), xa.whi = P<void>(adam[4]), xa.wlo = P<void>(adam[5]);
+  xa.n_trunk = int64_t(adam[6]), xa.n = int64_t(adam[7]);
+  xa.hp = P<const float>(adam[8]), xa.step_ctr = P<const int64_t>(adam[9]);
+  xa.bump = adam[10] ? P<int64_t>(adam[10]) : nullptr, xa.nbump = int(adam[11]);
+  xa.done = adam[12] ? P<uint32_t>(adam[12]) : nullptr, xa.bump_next = adam[13] ? P<int64_t>(adam[13]) : nullptr;
+  xa.grad_scale = grad_scale;
+  return xa;
+}
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "CDNA4 (gfx950) kernels + HBM GPU object store";
 
@@ -364,9 +384,11 @@ PYBIND11_MODULE(_hip, m) {
                                     const std::vector<uint64_t>& bufs, int64_t B, int slices, int A1, uint32_t seed,
                                     uint64_t k16_done, int64_t T, int threads, bool spin, uint64_t host_seq,
                                     uint64_t host_seq_dev, uint64_t release, uint64_t release_dev, uint64_t gate_err,
-                                    int gate_parts, int gate_timeout_ms) {
+                                    int gate_parts, int gate_timeout_ms, bool fused_heads) {
     // fp32 policy: 16 weights (8 hi planes, then the 8 lo planes) and a 12th buffer (the h2 lo plane)
     const bool x3 = wts.size() == 16;
+    if (fused_heads && (!x3 || B > 64))
+      throw std::invalid_argument("hybrid_rollout_direct: fused K13x + K16x needs the fp32 policy and B <= 64");
     if (v.size() < 15 || (wts.size() != 8 && !x3) || bufs.size() < size_t(x3 ? 12 : 11) || w1s.size() != 4 ||
         w2s.size() != 4 || !k16_done)
       throw std::invalid_argument("hybrid_rollout_direct: 15 group fields, 8 (16) weights, 11 (12) buffers, 4+4 strides, done");
@@ -423,6 +445,7 @@ PYBIND11_MODULE(_hip, m) {
       a.bhlo = P<const void>(wts[15]);
       a.h2lo = P<void>(bufs[11]);
     }
+    a.fused_heads = fused_heads;
     g.direct = &a;
     g.k16_done = P<unsigned int>(k16_done);
     if ((host_seq == 0) != (host_seq_dev == 0))
@@ -448,7 +471,8 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("group"), py::arg("weights"), py::arg("w1s"), py::arg("w2s"), py::arg("bufs"), py::arg("B"), py::arg("S"),
      py::arg("A1"), py::arg("seed"), py::arg("k16_done"), py::arg("T"), py::arg("threads") = 1, py::arg("spin") = false,
      py::arg("host_seq") = 0, py::arg("host_seq_dev") = 0, py::arg("release") = 0, py::arg("release_dev") = 0,
-     py::arg("gate_err") = 0, py::arg("gate_parts") = 1, py::arg("gate_timeout_ms") = 2000);
+     py::arg("gate_err") = 0, py::arg("gate_parts") = 1, py::arg("gate_timeout_ms") = 2000,
+     py::arg("fused_heads") = false);
   // K21 persistent rollout server over one group: `group` = hybrid_rollout's 15 group fields (exec
   // ignored); weights = [W1, b1, W2, b2, Wd, bd, Wh, bh]; bufs = [stack, nf, rows, h2, hpart, act,
   // logp, vf, lout, act_now, ctr_t]
@@ -689,32 +713,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("x3_trunk_bwd", [](uint64_t obs, uint64_t idx, uint64_t ctr, int64_t period, int64_t B, XP W2,
                            std::vector<int64_t> w2s, XP h1, uint64_t h2hi, XP dh2, XP dpre1, uint64_t partial,
                            uint64_t dW1, std::vector<int64_t> w1s, uint64_t db1, uint64_t dW2, uint64_t db2,
-                           uint64_t stream, std::vector<uint64_t> adam, float grad_scale) {
+                           uint64_t stream, std::vector<uint64_t> adam, float grad_scale, bool dense_separate) {
     if (w1s.size() != 4 || w2s.size() != 4) throw std::invalid_argument("x3_trunk_bwd: 4 strides per weight");
-    // adam (optional, the tail Adam): [master, m1, m2, grad, whi, wlo, n_trunk, n, hp, step_ctr, bump, nbump,
-    // done, bump_next(, grad2: the K12x second row part's dense + heads gradients)]
-    X3Adam xa;
-    if (!adam.empty()) {
-      if (adam.size() != 14 && adam.size() != 15) throw std::invalid_argument("x3_trunk_bwd: adam needs 14 or 15 fields");
-      if (adam.size() == 15 && adam[14]) {
-        if (adam[14] & 15) throw std::invalid_argument("x3_trunk_bwd: grad2 must be 16-byte aligned");
-        xa.grad2 = P<const float>(adam[14]);
-      }
-      xa.master = P<float>(adam[0]), xa.m1 = P<float>(adam[1]), xa.m2 = P<float>(adam[2]);
-      xa.grad = P<const float>(adam[3]), xa.whi = P<void>(adam[4]), xa.wlo = P<void>(adam[5]);
-      xa.n_trunk = int64_t(adam[6]), xa.n = int64_t(adam[7]);
-      xa.hp = P<const float>(adam[8]), xa.step_ctr = P<const int64_t>(adam[9]);
-      xa.bump = adam[10] ? P<int64_t>(adam[10]) : nullptr, xa.nbump = int(adam[11]);
-      xa.done = adam[12] ? P<uint32_t>(adam[12]) : nullptr, xa.bump_next = adam[13] ? P<int64_t>(adam[13]) : nullptr;
-      xa.grad_scale = grad_scale;
-    }
+    const X3Adam xa = x3_adam_args(adam, grad_scale, "x3_trunk_bwd");
     x3_trunk_bwd(P<const uint8_t>(obs), idx ? P<const int64_t>(idx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr,
                  period, B, xin(W2), w2s.data(), xin(h1), P<const void>(h2hi), xin(dh2), xout(dpre1), P<float>(partial),
-                 P<float>(dW1), w1s.data(), P<float>(db1), P<float>(dW2), P<float>(db2), S(stream), xa);
+                 P<float>(dW1), w1s.data(), P<float>(db1), P<float>(dW2), P<float>(db2), S(stream), xa, dense_separate);
   }, py::arg("obs"), py::arg("idx"), py::arg("ctr"), py::arg("period"), py::arg("B"), py::arg("W2"), py::arg("w2s"),
      py::arg("h1"), py::arg("h2hi"), py::arg("dh2"), py::arg("dpre1"), py::arg("partial"), py::arg("dW1"),
      py::arg("w1s"), py::arg("db1"), py::arg("dW2"), py::arg("db2"), py::arg("stream"),
-     py::arg("adam") = std::vector<uint64_t>{}, py::arg("grad_scale") = 1.0f);
+     py::arg("adam") = std::vector<uint64_t>{}, py::arg("grad_scale") = 1.0f, py::arg("dense_separate") = false);
+  // the tail Adam's dense + heads range alone (same adam fields; the counters are not advanced here)
+  m.def("x3_dense_adam", [](std::vector<uint64_t> adam, float grad_scale, uint64_t stream) {
+    x3_dense_adam(x3_adam_args(adam, grad_scale, "x3_dense_adam"), S(stream));
+  }, py::arg("adam"), py::arg("grad_scale"), py::arg("stream"));
   m.def("x3_dense_fwd_part_slices", &x3_dense_fwd_part_slices);
   m.def("x3_dense_fwd_part", [](XP x, XP w, int64_t M, int64_t K, int N, uint64_t part, int nslices, uint64_t stream) {
     x3_dense_fwd_part(xin(x), xin(w), M, K, N, P<float>(part), nslices, S(stream));
@@ -738,6 +750,17 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("hpart"), py::arg("S"), py::arg("hb"), py::arg("wh"), py::arg("bh"), py::arg("t_ptr"), py::arg("ctr"),
      py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"), py::arg("lout"), py::arg("act_now"), py::arg("B"),
      py::arg("A1"), py::arg("stream"), py::arg("done") = 0, py::arg("host_seq") = 0);
+  m.def("x3_dense_heads_sample", [](XP x, XP w, int64_t M, int64_t K, uint64_t part, int nslices, XP hb, XP wh, XP bh,
+                                    uint64_t t_ptr, uint64_t ctr, uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf,
+                                    uint64_t lout, uint64_t act_now, int A1, uint64_t stream, uint64_t done,
+                                    uint64_t host_seq) {
+    x3_dense_heads_sample(xin(x), xin(w), M, K, P<float>(part), nslices, xin(hb), xin(wh), xin(bh),
+                          P<const int64_t>(t_ptr), P<const int64_t>(ctr), seed, P<int64_t>(act), P<float>(logp),
+                          P<float>(vf), P<float>(lout), P<int64_t>(act_now), A1, S(stream), P<unsigned int>(done),
+                          host_seq ? P<int64_t>(host_seq) : nullptr);
+  }, py::arg("x"), py::arg("w"), py::arg("M"), py::arg("K"), py::arg("part"), py::arg("S"), py::arg("hb"), py::arg("wh"),
+     py::arg("bh"), py::arg("t_ptr"), py::arg("ctr"), py::arg("seed"), py::arg("act"), py::arg("logp"), py::arg("vf"),
+     py::arg("lout"), py::arg("act_now"), py::arg("A1"), py::arg("stream"), py::arg("done"), py::arg("host_seq") = 0);
   m.def("x3_dense_heads_bwd", [](XP dz, int A1, XP y, XP x, XP w, XP dpre, int64_t M, int64_t K, XP dx, uint64_t dw,
                                  uint64_t db, uint64_t dwh, uint64_t dbh, uint64_t stream, int rs, uint64_t dw2,
                                  uint64_t db2, uint64_t dwh2, uint64_t dbh2) {

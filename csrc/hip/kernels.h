@@ -229,7 +229,11 @@ int64_t x3_trunk_partial_floats(int64_t B);
 void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W2,
                   const int64_t* w2s, X3In h1, const void* h2hi, X3In dh2, X3Out dpre1, float* partial, float* dW1,
                   const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream,
-                  const X3Adam& xa = X3Adam{});
+                  const X3Adam& xa = X3Adam{}, bool dense_separate = false);
+// the tail Adam's dense + heads range as its own launch (dense_separate above): forked beside the trunk
+// backward; the trunk-reduce launch of the same step still advances the (parity) counters
+int x3_dense_adam_groups(const X3Adam& xa);
+void x3_dense_adam(const X3Adam& xa, hipStream_t stream);
 // K13x: split-K dense layer -> fp32 partials part[S][M][N]
 int x3_dense_fwd_part_slices(int64_t M, int64_t K, int N);
 void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part, int S, hipStream_t stream);
@@ -241,6 +245,13 @@ void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const fl
 void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const int64_t* t_ptr, const int64_t* ctr,
                      uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B, int A1,
                      hipStream_t stream, unsigned int* done = nullptr, int64_t* host_seq = nullptr);
+// K13x + K16x in one launch (rollout, M <= 64): split-K partials, per-row-tile tickets, the finisher of a
+// row tile runs the heads + sampling of its 16 rows, the last one advances the step. done: 1 + ceil(M/16)
+// zero-initialised words (zero again when the launch ends)
+void x3_dense_heads_sample(X3In x, X3In w, int64_t M, int64_t K, float* part, int S, X3In hb, X3In wh, X3In bh,
+                           const int64_t* t_ptr, const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf,
+                           float* lout, int64_t* act_now, int A1, hipStream_t stream, unsigned int* done,
+                           int64_t* host_seq = nullptr);
 // K12x: dx (split pair) and fp32 dW, db, dWh, dbh. rs = 2: two row parts, the second one's dW / db / dWh / dbh
 // into dw2 / db2 / dwh2 / dbh2 (summed by the tail Adam, X3Adam::grad2)
 void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int64_t M, int64_t K, X3Out dx, float* dw,
@@ -308,6 +319,9 @@ struct RolloutServerArgs {
   const int64_t* gate = nullptr;
   int* gate_err = nullptr;
   int gate_timeout_ms = 2000;  // wall-clock bound of one gate wait (s_memrealtime)
+  // fp32 direct launches: K13x + K16x as ONE launch (x3_dense_heads_sample; k16_done then holds
+  // 1 + ceil(B / 16) ticket words)
+  bool fused_heads = false;
 };
 int rollout_server_launch(const RolloutServerArgs& a, hipStream_t stream);
 

@@ -177,9 +177,15 @@ void rollout_step_direct(const RolloutServerArgs& a, unsigned int* k16_done, hip
     x3_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, X3In{a.W1, a.W1lo}, a.w1s, X3In{a.b1, a.b1lo},
                       X3In{a.W2, a.W2lo}, a.w2s, X3In{a.b2, a.b2lo}, h2, stream, a.gate, gate_want, a.gate_err,
                       gate_parts, a.gate_timeout_ms);
-    x3_dense_fwd_part(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, 256, a.hpart, a.S, stream);
-    x3_heads_sample(a.hpart, a.S, X3In{a.bd, a.bdlo}, X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t,
-                    a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B, a.A1, stream, k16_done, host_seq_dev);
+    if (a.fused_heads) {
+      x3_dense_heads_sample(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, a.hpart, a.S, X3In{a.bd, a.bdlo},
+                            X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t, a.seed, a.act, a.logp, a.vf,
+                            a.lout, a.act_now, a.A1, stream, k16_done, host_seq_dev);
+    } else {
+      x3_dense_fwd_part(X3In{a.h2, a.h2lo}, X3In{a.Wd, a.Wdlo}, a.B, 3872, 256, a.hpart, a.S, stream);
+      x3_heads_sample(a.hpart, a.S, X3In{a.bd, a.bdlo}, X3In{a.Wh, a.Whlo}, X3In{a.bh, a.bhlo}, a.ctr_t + 1, a.ctr_t,
+                      a.seed, a.act, a.logp, a.vf, a.lout, a.act_now, a.B, a.A1, stream, k16_done, host_seq_dev);
+    }
     return;
   }
   nature_trunk_fwd_push(a.stack, a.nf, a.rows, a.ctr_t + 1, a.B, a.W1, a.w1s, a.b1, a.W2, a.w2s, a.b2, a.h2, stream);

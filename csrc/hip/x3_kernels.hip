@@ -657,6 +657,18 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
   if (xa.master) x3_tail_bump(xa);
 }
 
+// The dense + heads range's Adam as its own launch (no counter advance: the trunk-reduce launch of the same
+// step advances the parity counters). The learner forks it onto a side stream right after K12x, so it
+// runs beside the trunk backward (conv2 bwd + conv1 wgrad, one workgroup per CU) instead of after it.
+__global__ __launch_bounds__(512) void k_dense_adam_x3(const X3Adam xa) {
+  const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
+  const int64_t o = xa.n_trunk;
+  const int64_t tid = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t nthr = int64_t(gridDim.x) * blockDim.x;
+  adam_span<float, true, 2>(xa.master + o, xa.m1 + o, xa.m2 + o, xa.grad + o, static_cast<__hip_bfloat16*>(xa.whi) + o,
+                            xa.grad_scale, ac, tid, nthr, xa.n - o, static_cast<__hip_bfloat16*>(xa.wlo) + o, xa.grad2);
+}
+
 }  // namespace x3
 
 // ---------------------------------------------------------------- host launchers (K10x)
@@ -723,10 +735,25 @@ int64_t x3_trunk_partial_floats(int64_t B) {
   return int64_t(x3_conv2_bwd_groups(B)) * x3::PART2 + int64_t(x3_conv1_wgrad_groups(B)) * x3::PART1;
 }
 
+int x3_dense_adam_groups(const X3Adam& xa) {
+  return int(std::max<int64_t>(1, ((xa.n - xa.n_trunk + 3) / 4 + 1023) / 1024));
+}
+
+void x3_dense_adam(const X3Adam& xa, hipStream_t stream) {
+  if (!xa.master || !xa.m1 || !xa.m2 || !xa.grad || !xa.whi || !xa.wlo || !xa.hp || !xa.step_ctr || xa.n <= xa.n_trunk ||
+      xa.n_trunk % 4 != 0)
+    throw std::invalid_argument("x3_dense_adam: flat buffers, both weight planes, hp and the step counter");
+  hipLaunchKernelGGL(x3::k_dense_adam_x3, dim3(uint32_t(x3_dense_adam_groups(xa))), dim3(512), 0, stream, xa);
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
 void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, int64_t period, int64_t B, X3In W2,
                   const int64_t* w2s, X3In h1, const void* h2hi, X3In dh2, X3Out dpre1, float* partial, float* dW1,
-                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream, const X3Adam& xa) {
+                  const int64_t* w1s, float* db1, float* dW2, float* db2, hipStream_t stream, const X3Adam& xa,
+                  bool dense_separate) {
   if (B <= 0) return;
+  if (dense_separate && (!xa.master || !xa.bump_next))
+    throw std::invalid_argument("x3_trunk_bwd: a separate dense Adam needs the tail Adam with parity counters");
   if (xa.master) {
     auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool ok = al(xa.master) && al(xa.m1) && al(xa.m2) && al(xa.grad) && xa.whi && xa.wlo &&
@@ -754,7 +781,7 @@ void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
   RMM_HIP_CHECK(hipGetLastError());
   const int nred = (x3::PARTX + 63) / 64;
   // Adam workgroups: two groups of 4 elements per lane (K6's default unroll)
-  const int nadam = xa.master ? int(std::max<int64_t>(1, ((xa.n - xa.n_trunk + 3) / 4 + 1023) / 1024)) : 0;
+  const int nadam = xa.master && !dense_separate ? x3_dense_adam_groups(xa) : 0;
   hipLaunchKernelGGL(x3::k_trunk_reduce_x3, dim3(nred + nadam), dim3(512), 0, stream, p1, G1, p2, G2, dW1, wsx(w1s),
                      db1, dW2, wsx(w2s), db2, xa, nred);
   RMM_HIP_CHECK(hipGetLastError());
@@ -777,9 +804,9 @@ constexpr int H = dense::H;
 // SIMD, so a step's loads are issued D steps ahead (a register ring of D stages): the MFMAs of step i
 // overlap the global latency of steps i+1..i+D-1 instead of waiting for it.
 template <int FM, int FN, int D>
-__global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
-                                                           float* __restrict__ part) {
-  __shared__ f32x4 red[3][FM * FN][64];
+__device__ __forceinline__ void dense_part_tile_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
+                                                   float* __restrict__ part, f32x4 (&red)[3][FM * FN][64],
+                                                   int64_t* tm_out) {
   // the wave index is wave-uniform: in an SGPR the k-step guards below are scalar branches
   const int lane = threadIdx.x & 63, kw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 15,
             g = lane >> 4;
@@ -789,6 +816,7 @@ __global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int
   int64_t id = blockIdx.x;
   if ((total_ & 7) == 0) id = (id & 7) * (total_ >> 3) + (id >> 3);  // XCD-contiguous runs
   const int64_t sl = id / tiles, rem = id % tiles, tm = rem / nt, tn = rem % nt;
+  *tm_out = tm;
   const int64_t m0 = tm * 16 * FM, n0 = tn * 16 * FN;
   const int64_t steps = K / 32, lo = steps * sl / S, hi = steps * (sl + 1) / S;
   const unsigned short *xh[FM], *xl[FM], *wh[FN], *wl[FN];
@@ -866,6 +894,13 @@ __global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int
         if (row < M) out[row * N + 16 * j] = t[e];
       }
     }
+}
+template <int FM, int FN, int D>
+__global__ __launch_bounds__(256) void k_dense_fwd_part_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
+                                                           float* __restrict__ part) {
+  __shared__ f32x4 red[3][FM * FN][64];
+  int64_t tm;
+  dense_part_tile_x3<FM, FN, D>(x, w, M, K, N, S, part, red, &tm);
 }
 
 // ---- K13x-L: the same product for the SGD step's M = 500 rows, staged through LDS. The register-direct
@@ -1108,6 +1143,66 @@ __global__ __launch_bounds__(256) void k_heads_sample_x3(const float* __restrict
     }
     __syncthreads();
     if (last && threadIdx.x == 0) {
+      int64_t* tw = const_cast<int64_t*>(t_ptr);
+      int64_t* cw = const_cast<int64_t*>(ctr);
+      *tw += 1;
+      if (cw != tw) *cw += 1;
+      atomicExch(done, 0u);
+      if (host_seq) __hip_atomic_store(host_seq, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+// ---- K13x + K16x in ONE launch (rollout step, M <= 16 * 63 rows): every workgroup computes its split-K
+// partial tile exactly as K13x (FM = FN = 1, D = 4) and takes a ticket on its 16-row tile; the workgroup
+// that completes a row tile (the last of its N/16 x S contributors) sums the partials, adds bias + ReLU
+// and runs K16x's heads + Gumbel-max sampling for those 16 rows (one wave per 4 rows); the last row tile's
+// finisher advances the step counters and publishes the host word. The kernel boundary between K13x and
+// K16x (their launch gap and K16x's fill) is gone; the sums and the sampling are bit-identical.
+// tickets: done[0] = row tiles finished this step, done[1 + tm] = contributors of row tile tm (reset by
+// the tile's finisher, so every counter is 0 again when the launch ends).
+template <int A1>
+__global__ __launch_bounds__(256) void k_dense_heads_sample_x3(CPair x, CPair w, int64_t M, int64_t K, int S,
+                                                               float* __restrict__ part, CPair hb, CPair wh, CPair bh,
+                                                               const int64_t* t_ptr, const int64_t* ctr, uint32_t seed,
+                                                               int64_t* __restrict__ act, float* __restrict__ logp,
+                                                               float* __restrict__ vf, float* __restrict__ lout,
+                                                               int64_t* __restrict__ act_now,
+                                                               unsigned int* __restrict__ done, int64_t* host_seq) {
+  __shared__ f32x4 red[3][1][64];
+  __shared__ __attribute__((aligned(16))) float whs[A1 * H];
+  __shared__ float bhs[A1];
+  __shared__ unsigned int s_last;
+  int64_t tm;
+  dense_part_tile_x3<1, 1, 4>(x, w, M, K, H, S, part, red, &tm);
+  const unsigned int contributors = unsigned(H / 16) * unsigned(S);
+  __threadfence();  // this workgroup's partial tile before its ticket
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&done[1 + tm], 1u) == contributors - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // every contributor's partial tile of row tile tm
+  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
+  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int64_t b = 16 * tm + wv + 4 * q;
+    if (b < M) {
+      float hv[4];
+      load_hidden4_x3(part, S, hb, M, b, lane, hv);
+      dense::heads_sample_row_pre<A1, false>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, M, b, lane);
+    }
+  }
+  if (host_seq) __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    done[1 + tm] = 0u;
+    __threadfence();
+    const unsigned int ntm = unsigned((M + 15) / 16);
+    if (atomicAdd(done, 1u) == ntm - 1) {
       int64_t* tw = const_cast<int64_t*>(t_ptr);
       int64_t* cw = const_cast<int64_t*>(ctr);
       *tw += 1;
@@ -1537,6 +1632,36 @@ void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const
     RMM_K16X(10) RMM_K16X(11) RMM_K16X(12) RMM_K16X(13) RMM_K16X(14) RMM_K16X(15) RMM_K16X(16)
   }
 #undef RMM_K16X
+  RMM_HIP_CHECK(hipGetLastError());
+}
+
+void x3_dense_heads_sample(X3In x, X3In w, int64_t M, int64_t K, float* part, int S, X3In hb, X3In wh, X3In bh,
+                           const int64_t* t_ptr, const int64_t* ctr, uint32_t seed, int64_t* act, float* logp, float* vf,
+                           float* lout, int64_t* act_now, int A1, hipStream_t stream, unsigned int* done,
+                           int64_t* host_seq) {
+  if (M <= 0) return;
+  int f, s_cfg;
+  x3_part_cfg(M, K, dense::H, &f, &s_cfg);
+  if (f != 1 || S != s_cfg) throw std::invalid_argument("x3_dense_heads_sample: M <= 64 and S = x3_dense_fwd_part_slices");
+  if (K % 32 != 0) throw std::invalid_argument("x3_dense_heads_sample: K % 32 == 0");
+  if (!done || !part) throw std::invalid_argument("x3_dense_heads_sample: ticket words (1 + ceil(M / 16)) and partials");
+  if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("x3_dense_heads_sample: 2 <= A <= 15 actions");
+  check_pair(x, "x3_dense_heads_sample x");
+  check_pair(w, "x3_dense_heads_sample w");
+  if (!hb.hi || !hb.lo || !wh.hi || !wh.lo || !bh.hi || !bh.lo)
+    throw std::invalid_argument("x3_dense_heads_sample: split head weights required");
+  const int64_t tiles = ((M + 15) / 16) * (dense::H / 16);
+  const dim3 grid(uint32_t(tiles * S)), block(256);
+#define RMM_K1316X(N)                                                                                              \
+  case N:                                                                                                          \
+    hipLaunchKernelGGL(x3::k_dense_heads_sample_x3<N>, grid, block, 0, stream, cp(x), cp(w), M, K, S, part, cp(hb), \
+                       cp(wh), cp(bh), t_ptr, ctr, seed, act, logp, vf, lout, act_now, done, host_seq);           \
+    break;
+  switch (A1) {
+    RMM_K1316X(3) RMM_K1316X(4) RMM_K1316X(5) RMM_K1316X(6) RMM_K1316X(7) RMM_K1316X(8) RMM_K1316X(9)
+    RMM_K1316X(10) RMM_K1316X(11) RMM_K1316X(12) RMM_K1316X(13) RMM_K1316X(14) RMM_K1316X(15) RMM_K1316X(16)
+  }
+#undef RMM_K1316X
   RMM_HIP_CHECK(hipGetLastError());
 }
 

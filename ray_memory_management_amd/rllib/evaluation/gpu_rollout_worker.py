@@ -61,20 +61,6 @@ class GPURolloutWorker:
         return {}
 
     def sample(self, *_after):  # _after: refs the runtime resolves first (prefetched samples)
-        """One fragment. A step-gate timeout (the host stalled longer than `rollout_gate_timeout_ms`
-        between a launch and its release, so a gated policy step read stale frames) never fails the
-        iteration: that fragment is discarded and re-sampled once on the ungated path."""
-        try:
-            return self._sample_once()
-        except _GateTimeout:
-            self.gate_timeouts = getattr(self, "gate_timeouts", 0) + 1
-            self._gate_bypass = True
-            try:
-                return self._sample_once()
-            finally:
-                self._gate_bypass = False
-
-    def _sample_once(self):
         import time
 
         import torch
@@ -265,8 +251,9 @@ class _EnvGroup:
         self.act_now = torch.zeros(n, dtype=torch.int64, device=dev)
         self.ctr_t = torch.zeros(2, dtype=torch.int64, device=dev)  # {rng counter, rollout row}
         # K16's completion counter (K16 advances the step counters itself); RMM_NO_K16_ADVANCE=1 → add kernel
+        # (word 0; the fused K13x + K16x launch also uses one ticket word per 16-row tile after it)
         self.k16_done = (None if os.environ.get("RMM_NO_K16_ADVANCE")
-                         else torch.zeros(1, dtype=torch.int32, device=dev))
+                         else torch.zeros(64, dtype=torch.int32, device=dev))
         self.fused = hasattr(model, "forward_sample") and getattr(
             getattr(model, "heads", None), "out_features", -1) == A + 1
         # device frame stacks (K19): upload only each env's newest frame, shift the stack in HBM
@@ -537,6 +524,20 @@ class HybridRolloutWorker(GPURolloutWorker):
         self._sample_time = 0.0
 
     def sample(self, *_after):  # _after: refs the runtime resolves first (prefetched samples)
+        """One fragment. A step-gate timeout (the host stalled longer than `rollout_gate_timeout_ms`
+        between a launch and its release, so a gated policy step read stale frames) never fails the
+        iteration: that fragment is discarded and re-sampled once on the ungated path."""
+        try:
+            return self._sample_once()
+        except _GateTimeout:
+            self.gate_timeouts = getattr(self, "gate_timeouts", 0) + 1
+            self._gate_bypass = True
+            try:
+                return self._sample_once()
+            finally:
+                self._gate_bypass = False
+
+    def _sample_once(self):
         import time
 
         import torch
@@ -697,6 +698,9 @@ class HybridRolloutWorker(GPURolloutWorker):
         out = dict(group=k["group"], weights=k["weights"], w1s=k["w1s"], w2s=k["w2s"],
                    bufs=k["bufs"][:12] if k.get("x3") else k["bufs"][:11],
                    B=k["B"], S=k["S"], A1=k["A1"], seed=k["seed"], k16_done=G[0].k16_done.data_ptr())
+        if k.get("x3") and int(k["B"]) <= 64 and G[0].k16_done.numel() >= 1 + (int(k["B"]) + 15) // 16 and \
+                os.environ.get("RMM_ROLLOUT_FUSED_HEADS", "0") == "1":
+            out["fused_heads"] = True  # K13x + K16x in one launch (x3_dense_heads_sample)
         if os.environ.get("RMM_ROLLOUT_SEQ", "1") != "0":
             # completion word: K16 stores row + 1 into mapped pinned memory, the loop polls it (no event
             # record / interrupt wake-up): 44-47 -> 41-42 µs per 50-env step, runtime bench +2%

@@ -498,11 +498,23 @@ class PPOLearner:
         w2 = P[m._X3_NAMES[2]]
         ctr = self._ctr().data_ptr()  # this step's counter copy (the tail args advance the parity)
         adam = self._x3_tail_args() if self._tail_adam() else []
+        # the dense + heads Adam is final after K12x: fork it onto a side stream beside the trunk backward
+        # (parity counters only: the reduce launch advances them into the other copy, never under its reads)
+        fork = bool(adam) and adam[13] != 0 and os.environ.get("RMM_X3_DENSE_ADAM_FORK", "0") == "1"
+        if fork:
+            cur = torch.cuda.current_stream(self.device)
+            side = getattr(self, "_adam_stream", None)
+            if side is None:
+                side = self._adam_stream = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            h.x3_dense_adam(adam, 1.0 / self.world, side.cuda_stream)
         h.x3_trunk_bwd(full["obs"].data_ptr(), full["idx"].data_ptr(), ctr, int(full["period"]),
                        int(full["mbs"]), w2.ptrs(), list(w2.hi.stride()), ws["h1"].ptrs(), ws["h2"].hi.data_ptr(),
                        ws["dx"].ptrs(), ws["dpre1"].ptrs(), ws["part"].data_ptr(), g[0].data_ptr(),
                        list(m.convs[0].weight.stride()), g[1].data_ptr(), g[2].data_ptr(), g[3].data_ptr(), _stream(),
-                       adam=adam, grad_scale=1.0 / self.world)
+                       adam=adam, grad_scale=1.0 / self.world, dense_separate=fork)
+        if fork:
+            cur.wait_stream(side)
 
     def _x3_tail_args(self):
         """Tail Adam of the fp32 learner (world of one): K6 folded into the x3 trunk-reduce launch — the

@@ -125,6 +125,31 @@ def test_x3_tail_adam_matches_k6(cuda, graphs, monkeypatch):
     assert abs(a[6]["total_loss"] - b[6]["total_loss"]) < 1e-5 * max(1.0, abs(a[6]["total_loss"]))
 
 
+def test_x3_dense_adam_fork_matches_folded(cuda, monkeypatch):
+    """fp32 learner with graphs (parity counters): the dense + heads Adam forked onto a side stream beside
+    the trunk backward (RMM_X3_DENSE_ADAM_FORK=1) gives bit-identical masters, moments, weight planes and
+    counters to the Adam folded into the trunk-reduce launch."""
+    outs = []
+    monkeypatch.setenv("RMM_TAIL_ADAM", "1")
+    for fork in ("0", "1"):
+        monkeypatch.setenv("RMM_X3_DENSE_ADAM_FORK", fork)
+        L = _learner(cuda, use_graphs=True, lr=1e-3, weight_decay=0.01, compute_dtype="fp32")
+        assert L.x3 and L._tail_adam()
+        obs, cols = _tables(cuda)
+        torch.manual_seed(5)
+        st = L._update_tables(obs, cols, 4)
+        torch.manual_seed(6)
+        L._update_tables(obs, cols, 4)
+        if fork == "1":
+            assert getattr(L, "_adam_stream", None) is not None  # the fork was taken
+        outs.append((L.master.clone(), L.m1.clone(), L.m2.clone(), L.w_x3.hi.clone(), L.w_x3.lo.clone(),
+                     L.ctr.clone(), st))
+    a, b = outs
+    assert torch.equal(a[5], b[5])
+    for x, y in zip(a[:5], b[:5]):
+        assert torch.equal(x, y), float((x.float() - y.float()).abs().max())
+
+
 def test_grad_clip_coef_matches_torch(cuda):
     from ray_memory_management_amd._native import require_hip
 
@@ -545,6 +570,31 @@ def test_rollout_direct_launch_matches_graph_loop(cuda, monkeypatch, n_envs, T, 
     assert len(a._completed) > 0 and a._completed == b._completed
 
 
+@pytest.mark.parametrize("n_envs", [6, 50])
+def test_rollout_fused_heads_matches_two_launches(cuda, monkeypatch, n_envs):
+    """fp32 direct rollout launches with K13x + K16x fused into one launch (RMM_ROLLOUT_FUSED_HEADS=1):
+    fragments and finished episodes bit-identical to the two-launch step."""
+    import torch
+
+    from ray_memory_management_amd.rllib.evaluation.gpu_rollout_worker import HybridRolloutWorker
+
+    cfg = {"env": "SyntheticAtariVec-v0", "env_config": {"episode_len": 9}, "num_envs_per_worker": n_envs,
+           "rollout_fragment_length": 20, "seed": 3, "compute_dtype": "fp32"}
+    monkeypatch.delenv("RMM_NO_NATIVE_ROLLOUT", raising=False)
+    monkeypatch.setenv("RMM_ROLLOUT_DIRECT", "1")
+    frags = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("RMM_ROLLOUT_FUSED_HEADS", fused)
+        w = HybridRolloutWorker(config=cfg)
+        frags.append(([w.sample() for _ in range(3)], list(w._completed)))
+        assert bool(w._direct_args(w.groups, w.group_streams).get("fused_heads")) == (fused == "1")
+    (fa, ca), (fb, cb) = frags
+    for x, y in zip(fa, fb):
+        for k in ("obs", "_raw", "_boot"):
+            assert torch.equal(x[k], y[k]), k
+    assert len(ca) > 0 and ca == cb
+
+
 def test_gate_timeout_resamples_the_fragment_ungated(cuda, monkeypatch):
     """A host that stalls longer than the step gate's bound between a launch and its release
     (RMM_TEST_GATE_DELAY_US in the native loop, gate bound 1 ms) makes the gated policy steps give up
@@ -568,4 +618,4 @@ def test_gate_timeout_resamples_the_fragment_ungated(cuda, monkeypatch):
     fb = a.sample()
     assert getattr(a, "gate_timeouts", 0) == 1
     for f in (fa, fb):
-        assert f["obs"].shape[:2] == (8, 6) and torch.isfinite(f["_raw"].float()).all()
+        assert f["obs"].shape[0] == 8 * 6 and torch.isfinite(f["_raw"].float()).all()

@@ -265,6 +265,51 @@ def test_x3_heads_sample_fp32_rows(cuda, B):
     assert torch.equal(now, act[1]) and int(act[0].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("B", [12, 50, 64])
+def test_x3_dense_heads_sample_fused_matches_two_launches(cuda, B):
+    """K13x + K16x in one launch (per-row-tile tickets, the tile finisher samples its rows) vs the K13x and
+    K16x launches: identical actions, log-probs, values and logits (same partial sums, same row math), the
+    step counters advanced once per launch, every ticket word back at 0 (three launches in a row)."""
+    from ray_memory_management_amd._native import require_hip
+    from ray_memory_management_amd.ops import x3
+
+    h = require_hip()
+    torch.manual_seed(B)
+    A, T, K = 4, 3, 3872
+    A1 = A + 1
+    x = x3.split(torch.relu(torch.randn(B, K, device=cuda)))
+    W = x3.split(torch.randn(256, K, device=cuda) * 0.02)
+    b = x3.split(torch.randn(256, device=cuda) * 0.1)
+    Wh = x3.split(torch.randn(A1, 256, device=cuda) * 0.5)
+    bh = x3.split(torch.randn(A1, device=cuda) * 0.1)
+    S = h.x3_dense_fwd_part_slices(B, K, 256)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for fused in (False, True):
+        part = torch.zeros(S, B, 256, device=cuda)
+        t = torch.tensor([0], device=cuda)
+        ctr = torch.tensor([777], device=cuda)
+        done = torch.zeros(64, dtype=torch.int32, device=cuda)
+        act = torch.zeros(T, B, dtype=torch.int64, device=cuda)
+        logp, vf = torch.zeros(T, B, device=cuda), torch.zeros(T, B, device=cuda)
+        lout, now = torch.zeros(T, B, A, device=cuda), torch.zeros(B, dtype=torch.int64, device=cuda)
+        for _ in range(T):
+            if fused:
+                h.x3_dense_heads_sample(x.ptrs(), W.ptrs(), B, K, part.data_ptr(), S, b.ptrs(), Wh.ptrs(), bh.ptrs(),
+                                        t.data_ptr(), ctr.data_ptr(), 7, act.data_ptr(), logp.data_ptr(), vf.data_ptr(),
+                                        lout.data_ptr(), now.data_ptr(), A1, st, done.data_ptr())
+            else:
+                h.x3_dense_fwd_part(x.ptrs(), W.ptrs(), B, K, 256, part.data_ptr(), S, st)
+                h.x3_heads_sample(part.data_ptr(), S, b.ptrs(), Wh.ptrs(), bh.ptrs(), t.data_ptr(), ctr.data_ptr(), 7,
+                                  act.data_ptr(), logp.data_ptr(), vf.data_ptr(), lout.data_ptr(), now.data_ptr(), B,
+                                  A1, st, done=done.data_ptr())
+        torch.cuda.synchronize()
+        assert int(t) == T and int(ctr) == 777 + T and int(done.abs().sum()) == 0
+        outs.append((act.clone(), logp.clone(), vf.clone(), lout.clone(), now.clone()))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_forward_value_matches_plain_forward(cuda, dtype):
     """VisionNetwork.forward_value (the rollout's bootstrap value: one fused sampling step into scratch
