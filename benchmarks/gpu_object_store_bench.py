@@ -130,14 +130,23 @@ def bench_spill(gb, shm_name):
     del w
     for name, x in (("randn", torch.randn(n, device="cuda", dtype=torch.bfloat16)),
                     ("smooth", torch.linspace(-1, 1, n, device="cuda").to(torch.bfloat16))):
-        oid = os.urandom(20)
-        g.put_segments(oid, [(x.data_ptr(), n * 2)], 16, s)
-        _sync()
-        st0 = g.stats()
-        t0 = time.perf_counter()
-        assert g.spill_object(oid) > 0, g.last_error()
-        ts = time.perf_counter() - t0
-        st1 = g.stats()
+        # three spills of the same tensor: the first one may land on arena pages no spill has touched yet
+        # and pays their first hipHostRegister (64 MB chunks); the steady-state rate is the best of the
+        # three, the first one is reported separately
+        reps = []
+        for rep in range(3):
+            oid = os.urandom(20)
+            g.put_segments(oid, [(x.data_ptr(), n * 2)], 16, s)
+            _sync()
+            st0 = g.stats()
+            t0 = time.perf_counter()
+            assert g.spill_object(oid) > 0, g.last_error()
+            reps.append(time.perf_counter() - t0)
+            st1 = g.stats()
+            if rep < 2:
+                g.delete(oid)
+        ts = min(reps)
+        out[f"spill_GBps_{name}_first_touch"] = round(n * 2 / reps[0] / 1e9, 2)
         host_bytes = st1["spilled_host_bytes_total"] - st0["spilled_host_bytes_total"]
         out_t = torch.empty_like(x)
         t0 = time.perf_counter()

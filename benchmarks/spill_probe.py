@@ -50,7 +50,11 @@ def main():
         torch.cuda.synchronize()
         g.spill_object(wid)
         g.delete(wid)
-        for name, x in data.items():
+        for mode, name, x in [(m, nm, t) for m in ("0", "1") for nm, t in data.items()]:
+            # RMM_SPILL_DEVICE_PLACE=1: chunks written by a copy kernel at a device-resident offset
+            os.environ["RMM_SPILL_DEVICE_PLACE"] = mode
+            name = name + ("_devplace" if mode == "1" else "")
+            placed0 = g.stats().get("spills_device_placed", 0)
             ts = []
             ratio = None
             for _ in range(a.reps):
@@ -70,6 +74,7 @@ def main():
             out[f"spill_GBps_{name}"] = round(n * 2 / min(ts) / 1e9, 2)
             out[f"spill_ms_{name}"] = [round(t * 1e3, 2) for t in ts]
             out[f"ratio_{name}"] = round(ratio, 3)
+            out[f"device_placed_{name}"] = g.stats().get("spills_device_placed", 0) - placed0
         # raw line rate into pinned host memory (same size)
         host = torch.empty(n * 2, dtype=torch.uint8).pin_memory()
         src = data["noise"].view(torch.uint8)

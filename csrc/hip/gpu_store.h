@@ -75,6 +75,7 @@ struct GpuStats {
   uint64_t spilled_objects, spilled_bytes_total, spilled_host_bytes_total, restored_bytes_total;
   uint64_t puts, gets;
   uint64_t spill_ns_total, restore_ns_total, proactive_spills, deferred_deletes;
+  uint64_t spills_device_placed;  // spills whose chunks a copy kernel placed (no per-chunk host round trip)
 };
 
 class GpuStore {
@@ -157,6 +158,7 @@ class GpuStore {
   void* work_ = nullptr;
   uint64_t scratch_bytes_ = 0;
   uint64_t work_bytes_ = 0;
+  uint64_t* spill_meta_ = nullptr;  // device: [host offset cursor, per-chunk compressed sizes...] (device-placed spill)
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   GpuStats st_{};
   int spills_in_flight_ = 0;

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -19,7 +20,9 @@ namespace hip {
 namespace {
 constexpr uint64_t kAlignG = 256;
 constexpr uint64_t kSpillChunk = 64ull << 20;  // input bytes per compression chunk
-constexpr uint64_t kSpillMagic = 0x4c4c495053555047ull;  // "GPUSPILL"
+constexpr uint64_t kSpillMagic = 0x4c4c495053555047ull;   // "GPUSPILL": chunks packed back to back
+constexpr uint64_t kSpillMagic2 = 0x324c495053555047ull;  // "GPUSPIL2": device-placed, each chunk 64-byte aligned
+constexpr uint64_t kSpillMaxDeviceChunks = 4096;          // device-placed spills up to 256 GiB
 constexpr uint32_t kTagGpuSpill = 0x47505553u;           // "GPUS"
 inline uint64_t AlignG(uint64_t v) { return (v + kAlignG - 1) & ~(kAlignG - 1); }
 
@@ -112,6 +115,7 @@ GpuStore::~GpuStore() {
   for (auto p : scratch_)
     if (p) (void)hipFree(p);
   if (work_) (void)hipFree(work_);
+  if (spill_meta_) (void)hipFree(spill_meta_);
   for (auto e : ev_)
     if (e) (void)hipEventDestroy(e);
   if (host_) host_unregister_segment(reinterpret_cast<uintptr_t>(host_->Base()));
@@ -448,6 +452,14 @@ void GpuStore::ClearStaleError(const char* where) {
   }
 }
 
+namespace {
+// device-placed spill chunks (SpillTransfer): RMM_SPILL_DEVICE_PLACE=1 / 0 overrides the default
+bool SpillDevicePlace() {
+  const char* e = std::getenv("RMM_SPILL_DEVICE_PLACE");
+  return e ? std::atoi(e) != 0 : false;
+}
+}  // namespace
+
 bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t nbytes, int elem_bits,
                              hipEvent_t ready, uint64_t* host_bytes, bool* compressed) {
   RMM_HIP_CHECK(hipSetDevice(device_));
@@ -478,6 +490,63 @@ bool GpuStore::SpillTransfer(const std::string& id, const uint8_t* src, uint64_t
   host_pin_range(dst, hdr + nbytes);
   if (use_c) EnsureScratch();
   if (ready) RMM_HIP_CHECK(hipStreamWaitEvent(side_, ready, 0));
+  // Device-placed chunks (RMM_SPILL_DEVICE_PLACE=1): the compressed size of chunk c never comes back to the host
+  // before chunk c is written; a copy kernel writes it at a device-resident cursor into the arena's device
+  // mapping, so compression of chunk c+1 and the PCIe write of chunk c run back to back without host round trips.
+  uint8_t* dst_dev = nullptr;
+  if (use_c && nchunks <= kSpillMaxDeviceChunks && SpillDevicePlace()) {
+    void* d0 = nullptr;
+    void* d1 = nullptr;
+    const uint64_t span = hdr + nbytes;
+    bool ok = hipHostGetDevicePointer(&d0, dst, 0) == hipSuccess &&
+              hipHostGetDevicePointer(&d1, dst + span - 1, 0) == hipSuccess &&
+              static_cast<uint8_t*>(d1) - static_cast<uint8_t*>(d0) == int64_t(span - 1);
+    for (uint64_t o = (64ull << 20); ok && o < span; o += (64ull << 20)) {  // contiguous across registrations
+      void* dm = nullptr;
+      ok = hipHostGetDevicePointer(&dm, dst + o, 0) == hipSuccess && static_cast<uint8_t*>(dm) - static_cast<uint8_t*>(d0) == int64_t(o);
+    }
+    (void)hipGetLastError();
+    if (ok && (reinterpret_cast<uintptr_t>(src) & 15) == 0) dst_dev = static_cast<uint8_t*>(d0);
+  }
+  if (dst_dev) {
+    if (!spill_meta_) RMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&spill_meta_), 8 * (1 + kSpillMaxDeviceChunks)));
+    RMM_HIP_CHECK(hipMemsetAsync(spill_meta_, 0, 8 * (1 + nchunks), side2_));
+    const uint64_t eb = uint64_t(elem_bits / 8);
+    for (uint64_t c = 0; c < nchunks; c++) {
+      const uint64_t len = std::min(kSpillChunk, nbytes - c * kSpillChunk);
+      const uint8_t* sc = src + c * kSpillChunk;
+      const int b = int(c & 1);
+      const bool try_c = len % eb == 0;
+      if (try_c) {
+        if (c >= 2) RMM_HIP_CHECK(hipStreamWaitEvent(side_, ev_[b], 0));  // the commit that last read scratch[b]
+        compress(sc, len / eb, elem_bits, scratch_[b], static_cast<uint8_t*>(work_) + uint64_t(b) * work_bytes_, side_,
+                 /*readback=*/false);
+      }
+      RMM_HIP_CHECK(hipEventRecord(ev_[2], side_));  // orders after `ready` and this chunk's compression
+      RMM_HIP_CHECK(hipStreamWaitEvent(side2_, ev_[2], 0));
+      spill_commit(scratch_[b], sc, len, try_c, dst_dev + hdr, spill_meta_, spill_meta_ + 1 + c, side2_);
+      RMM_HIP_CHECK(hipEventRecord(ev_[b], side2_));
+    }
+    std::vector<uint64_t> meta(1 + nchunks, 0);
+    RMM_HIP_CHECK(hipMemcpyAsync(meta.data(), spill_meta_, 8 * (1 + nchunks), hipMemcpyDeviceToHost, side2_));
+    RMM_HIP_CHECK(hipStreamSynchronize(side2_));
+    RMM_HIP_CHECK(hipStreamSynchronize(side_));
+    uint64_t* h = reinterpret_cast<uint64_t*>(dst);
+    for (uint64_t c = 0; c < nchunks; c++) h[4 + c] = meta[1 + c];
+    h[1] = nbytes;
+    h[2] = uint64_t(elem_bits);
+    h[3] = nchunks;
+    h[0] = kSpillMagic2;  // header last
+    const uint64_t doff = hdr + meta[0];
+    host_->ShrinkCreating(hid, doff);
+    host_->Seal(hid);
+    host_->Release(hid);
+    guard.done = true;
+    *host_bytes = doff;
+    *compressed = true;
+    st_.spills_device_placed++;
+    return true;
+  }
   std::vector<uint64_t> csize(nchunks, 0);
   uint64_t doff = hdr;
   hipEvent_t* done = ev_;  // done[b]: the D2H that last read scratch[b]
@@ -655,7 +724,7 @@ uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uin
   Store::View v;
   if (!host_->Get(hid, 0, &v)) return 0;
   const uint64_t* h = reinterpret_cast<const uint64_t*>(v.data);
-  if (h[0] != kSpillMagic || h[1] != nbytes) {
+  if ((h[0] != kSpillMagic && h[0] != kSpillMagic2) || h[1] != nbytes) {
     host_->Release(hid);
     return 0;
   }
@@ -667,6 +736,7 @@ uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uin
   for (uint64_t c = 0; c < nchunks; c++) any_c |= h[4 + c] != 0;
   if (any_c) EnsureScratch();
   uint64_t soff = hdr;
+  const uint64_t amask = h[0] == kSpillMagic2 ? 63 : 0;  // device-placed chunks start 64-byte aligned
   hipEvent_t* done = ev_;  // done[b]: the decompression that last read scratch[b]
   for (uint64_t c = 0; c < nchunks; c++) {
     const uint64_t len = std::min(kSpillChunk, nbytes - c * kSpillChunk);
@@ -681,10 +751,10 @@ uint64_t GpuStore::RestoreTransfer(const std::string& host_id, uint8_t* dst, uin
       decompress(scratch_[b], dst + c * kSpillChunk, len / eb, bits,
                  static_cast<uint8_t*>(work_) + uint64_t(b) * work_bytes_, side_);
       RMM_HIP_CHECK(hipEventRecord(done[b], side_));
-      soff += cs;
+      soff += (cs + amask) & ~amask;
     } else {
       dma_host_segment(const_cast<uint8_t*>(v.data) + soff, dst + c * kSpillChunk, len, true, side2_);
-      soff += len;
+      soff += (len + amask) & ~amask;
     }
   }
   RMM_HIP_CHECK(hipStreamSynchronize(side2_));

@@ -890,6 +890,7 @@ PYBIND11_MODULE(_hip, m) {
         d["restore_s_total"] = double(st.restore_ns_total) * 1e-9;
         d["proactive_spills"] = st.proactive_spills;
         d["deferred_deletes"] = st.deferred_deletes;
+        d["spills_device_placed"] = st.spills_device_placed;
         return d;
       });
 

@@ -45,9 +45,15 @@ uint64_t compress_bound(uint64_t n_elems, int elem_bits);
 // Workspace bytes needed by compress/decompress.
 uint64_t compress_workspace(uint64_t n_elems);
 // Compress `n_elems` elements at `src` into `dst` (device, >= compress_bound bytes).
-// Synchronises the stream once to read back the total; returns compressed byte count.
+// Synchronises the stream once to read back the total; returns compressed byte count. readback = false:
+// no synchronisation, returns 0 (the size stays in the stream's header on the device).
 uint64_t compress(const void* src, uint64_t n_elems, int elem_bits, void* dst, void* workspace,
-                  hipStream_t stream);
+                  hipStream_t stream, bool readback = true);
+// Device-placed spill chunk: a copy kernel writes chunk bytes into the host arena's device mapping at
+// host_dev + *base_dev (compressed from `scratch` when try_compressed and it saves >= len / 16, else `raw`),
+// then *csize_dev = compressed bytes or 0 and *base_dev advances by the bytes rounded up to 64.
+void spill_commit(const void* scratch, const void* raw, uint64_t len, bool try_compressed, void* host_dev,
+                  uint64_t* base_dev, uint64_t* csize_dev, hipStream_t stream);
 // Inverse of compress(); `src` is the device copy of the compressed stream.
 void decompress(const void* src, void* dst, uint64_t n_elems, int elem_bits, void* workspace,
                 hipStream_t stream);

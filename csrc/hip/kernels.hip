@@ -692,7 +692,8 @@ uint64_t compress_workspace(uint64_t n_elems) {
   return ((nb + 1) * 8 + 255) / 256 * 256 + (nparts + 1) * 8 + 256;
 }
 
-uint64_t compress(const void* src, uint64_t n, int elem_bits, void* dst, void* workspace, hipStream_t stream) {
+uint64_t compress(const void* src, uint64_t n, int elem_bits, void* dst, void* workspace, hipStream_t stream,
+                  bool readback) {
   if (elem_bits != 16 && elem_bits != 32) throw std::invalid_argument("compress: elem_bits must be 16 or 32");
   uint64_t nb = (n + kCBlock - 1) / kCBlock;
   uint8_t* d = static_cast<uint8_t*>(dst);
@@ -720,10 +721,62 @@ uint64_t compress(const void* src, uint64_t n, int elem_bits, void* dst, void* w
   }
   hipLaunchKernelGGL(k_write_header, dim3(1), dim3(1), 0, stream, d, uint32_t(elem_bits), n, nb, offs + nb);
   RMM_HIP_CHECK(hipGetLastError());
+  if (!readback) return 0;  // the size stays on the device (CHeader::payload_bytes)
   uint64_t total = 0;
   RMM_HIP_CHECK(hipMemcpyAsync(&total, offs + nb, sizeof(total), hipMemcpyDeviceToHost, stream));
   RMM_HIP_CHECK(hipStreamSynchronize(stream));
   return c_payload_off(nb) + total;
+}
+
+// ---- device-placed spill (GpuStore::SpillTransfer): chunk c of a spill is written by a copy kernel straight into
+// the registered host arena at a device-resident offset, so the host never waits for a chunk's compressed size.
+// The chunk goes compressed when its stream (header + sizes + payload, read from the compress() output on the
+// device) saves at least len / 16, else raw; every chunk starts 64-byte aligned.
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t spill_chunk_bytes(const uint8_t* scratch, uint64_t len, bool try_c, bool* comp) {
+  uint64_t t = len;
+  *comp = false;
+  if (try_c) {
+    const CHeader* h = reinterpret_cast<const CHeader*>(scratch);
+    t = c_payload_off(h->n_blocks) + h->payload_bytes;
+    *comp = t < len - len / 16;
+  }
+  return *comp ? t : len;
+}
+
+__global__ __launch_bounds__(256) void k_spill_commit(const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ raw,
+                                                      uint64_t len, int try_c, uint8_t* host, const uint64_t* base) {
+  bool comp;
+  const uint64_t n = spill_chunk_bytes(scratch, len, try_c != 0, &comp);
+  const uint8_t* src = comp ? scratch : raw;
+  uint8_t* dst = host + *base;  // 64-byte aligned
+  const uint64_t nv = n / 16;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nv; i += stride)
+    __builtin_nontemporal_store(reinterpret_cast<const u32x4v*>(src)[i], reinterpret_cast<u32x4v*>(dst) + i);
+  if (blockIdx.x == 0 && threadIdx.x < n % 16) dst[nv * 16 + threadIdx.x] = src[nv * 16 + threadIdx.x];
+}
+
+__global__ void k_spill_advance(const uint8_t* __restrict__ scratch, uint64_t len, int try_c, uint64_t* base,
+                                uint64_t* csize) {
+  bool comp;
+  const uint64_t n = spill_chunk_bytes(scratch, len, try_c != 0, &comp);
+  *csize = comp ? n : 0;
+  *base += (n + 63) & ~uint64_t(63);
+}
+
+void spill_commit(const void* scratch, const void* raw, uint64_t len, bool try_compressed, void* host_dev,
+                  uint64_t* base_dev, uint64_t* csize_dev, hipStream_t stream) {
+  if ((reinterpret_cast<uintptr_t>(raw) | reinterpret_cast<uintptr_t>(scratch) | reinterpret_cast<uintptr_t>(host_dev)) & 15)
+    throw std::invalid_argument("spill_commit: 16-byte aligned source, scratch and host mapping");
+  const uint32_t grid = uint32_t(std::min<uint64_t>(1024, std::max<uint64_t>(1, (len / 16 + 255) / 256)));
+  hipLaunchKernelGGL(k_spill_commit, dim3(grid), dim3(256), 0, stream, static_cast<const uint8_t*>(scratch),
+                     static_cast<const uint8_t*>(raw), len, int(try_compressed), static_cast<uint8_t*>(host_dev),
+                     base_dev);
+  hipLaunchKernelGGL(k_spill_advance, dim3(1), dim3(1), 0, stream, static_cast<const uint8_t*>(scratch), len,
+                     int(try_compressed), base_dev, csize_dev);
+  RMM_HIP_CHECK(hipGetLastError());
 }
 
 void decompress(const void* src, void* dst, uint64_t n, int elem_bits, void* workspace, hipStream_t stream) {

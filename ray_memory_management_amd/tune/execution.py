@@ -113,7 +113,8 @@ class TrialRunner:
                  max_concurrent_trials: Optional[int] = None, time_budget_s: Optional[float] = None,
                  checkpoint_freq: int = 0, checkpoint_at_end: bool = False, max_failures: int = 0,
                  fail_fast: bool = False, callbacks=None, resources=None, num_to_keep: Optional[int] = None,
-                 verbose: int = 0, reuse_actors: bool = False, progress_reporter=None, sync_config=None):
+                 verbose: int = 0, reuse_actors: bool = False, progress_reporter=None, sync_config=None,
+                 server_port: Optional[int] = None):
         self.trainable_cls = trainable_cls
         self.trainable_name = getattr(trainable_cls, "__name__", "trainable")
         self.search_alg = search_alg
@@ -148,10 +149,61 @@ class TrialRunner:
         self._actor_cls = ray.remote(_TrialActor)
         self._stop_all = False
         os.makedirs(local_dir, exist_ok=True)
+        # HTTP control server (reference trial_runner.py:380 TuneServer): its requests are applied by step()
+        self._server = self._server_reqs = None
+        self.server_port = None
+        if server_port is not None:
+            from ray_memory_management_amd.tune.web_server import ServerRequests, TuneServer
+
+            self._server_reqs = ServerRequests()
+            self._server = TuneServer(self, server_port)
+            self.server_port = self._server.port
 
     # ------------------------------------------------------------------ public
     def get_trials(self) -> List[Trial]:
         return self._trials
+
+    def get_trial(self, trial_id: str) -> Optional[Trial]:
+        return next((t for t in list(self._trials) if t.trial_id == trial_id), None)
+
+    # ---- TuneServer requests (called from the server thread; applied by the runner loop)
+    def request_stop_trial(self, trial: Trial):
+        self._server_reqs.q.put(("stop", trial))
+
+    def request_stop_experiment(self):
+        self._server_reqs.stop_experiment.set()
+
+    def request_add_trials(self, name: str, spec: Dict) -> List[Trial]:
+        """New trials from an experiment spec ({"config": {...}, "num_samples": n}): one per variant, added
+        to the experiment by the runner loop."""
+        from ray_memory_management_amd.tune.search.variant_generator import generate_variants
+
+        if not isinstance(spec, dict):
+            raise TypeError("spec must be a dict")
+        config = spec.get("config", {k: v for k, v in spec.items() if k not in ("num_samples", "run")})
+        trials = []
+        for _ in range(int(spec.get("num_samples", 1))):
+            for cfg in generate_variants(config):
+                trials.append(Trial(self.trainable_name, cfg, uuid.uuid4().hex[:8], self.local_dir, self.pgf,
+                                    self.max_failures, experiment_tag=f"{name}_{len(trials)}"))
+        self._server_reqs.q.put(("add", trials))
+        return trials
+
+    def _apply_server_requests(self):
+        if self._server_reqs is None:
+            return
+        if self._server_reqs.stop_experiment.is_set():
+            self._stop_all = True
+        while True:
+            try:
+                kind, arg = self._server_reqs.q.get_nowait()
+            except Exception:  # queue.Empty
+                break
+            if kind == "stop":
+                self.stop_trial(arg)
+            elif kind == "add":
+                for t in arg:
+                    self.add_trial(t)
 
     def add_trial(self, trial: Trial):
         self._trials.append(trial)
@@ -189,6 +241,8 @@ class TrialRunner:
         if self.syncer is not None:
             self.syncer.sync_up(force=True)
         self._cb("on_experiment_end", trials=self._trials)
+        if self._server is not None:
+            self._server.shutdown()
         return self._trials
 
     def is_finished(self) -> bool:
@@ -216,10 +270,14 @@ class TrialRunner:
                                  experiment_tag=f"{len(self._trials)}"))
 
     def step(self):
+        self._apply_server_requests()
         if self.time_budget_s and time.time() - self._start > self.time_budget_s:
             self._stop_all = True
         if self.stopper.stop_all():
             self._stop_all = True
+        if self._stop_all:  # time budget, stopper, TuneServer stop_experiment: running trials stop now
+            for t in [t for t in self._trials if t.status == Trial.RUNNING]:
+                self.stop_trial(t)
         if not self._stop_all:
             self._create_trials()
             while True:

@@ -166,7 +166,8 @@ def run(run_or_experiment, *, name: Optional[str] = None, metric: Optional[str] 
                          time_budget_s=time_budget_s, checkpoint_freq=checkpoint_freq,
                          checkpoint_at_end=checkpoint_at_end, max_failures=max_failures, fail_fast=fail_fast,
                          callbacks=callbacks, resources=resources_per_trial, num_to_keep=keep_checkpoints_num,
-                         verbose=verbose, progress_reporter=progress_reporter, sync_config=sync_config)
+                         verbose=verbose, progress_reporter=progress_reporter, sync_config=sync_config,
+                         server_port=server_port)
     if restore:
         ck = None
         from ray_memory_management_amd.air.checkpoint import Checkpoint
