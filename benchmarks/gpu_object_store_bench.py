@@ -186,10 +186,13 @@ def main():
     try:
         res = {"bench": "gpu_object_store"}
         res.update(bench_put_get(sizes, a.iters))
+        print("[gos] put/get done", file=sys.stderr, flush=True)
         res.update(bench_xproc(a.xproc_gb, a.iters))
+        print("[gos] cross-process get done", file=sys.stderr, flush=True)
         from ray_memory_management_amd._private.worker import global_worker
 
         res.update(bench_spill(a.spill_gb, global_worker.store_name))
+        print("[gos] spill done", file=sys.stderr, flush=True)
     finally:
         ray.shutdown()
     print(json.dumps(res), flush=True)

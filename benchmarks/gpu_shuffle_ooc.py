@@ -50,6 +50,10 @@ def main():
                                         partitions_per_worker=a.partitions, row_bytes=a.row_bytes)
     finally:
         ray.shutdown()
+    # the arena pre-pin (setup_prepin_seconds) is a one-time actor setup cost, like plasma's preallocation;
+    # the rate with it counted in the timed region is reported next to the shuffle rate
+    if r.get("setup_prepin_seconds") is not None and r.get("seconds"):
+        r["GBps_including_prepin"] = r["bytes"] / 1e9 / (r["seconds"] + r["setup_prepin_seconds"])
     r.update(metric="out-of-core GPU shuffle throughput", unit="GB/s", quota_bytes=quota,
              data_over_quota=round(r["bytes"] / (quota * a.workers), 2),
              data="synthetic random int64 keys + key-derived uint8 payload")

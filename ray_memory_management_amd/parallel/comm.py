@@ -386,6 +386,45 @@ class PeerComm(Comm):
                     self._cz.close()
                 self._cz = None  # every rank agrees: plain all-reduce -> Adam
             _store_barrier(store, f"{key}/zready", self.world)
+            if self._cz is not None:
+                self._zero1_selftest(store, key, timeout_s)
+
+    def _zero1_selftest(self, store, key: str, timeout_s: float) -> None:
+        """One small ZeRO-1 launch before the learner relies on it (as the all-reduce self-test above): every
+        rank's gradient is rank + 1, so after the first Adam step every master element is -lr (Adam's first
+        step is lr x sign), on every rank, bit for bit. Any failure (a flag timeout, a wrong or diverging
+        master) closes the ZeRO-1 communicator on ALL ranks together; the learner then runs all-reduce -> K6."""
+        import hashlib
+
+        n = 8192 * self.world
+        ok = True
+        digest = b""
+        try:
+            self._cz.set_timeout(5.0)
+            d = self.device
+            g = torch.full((n,), float(self.rank + 1), dtype=torch.float32, device=d)
+            master, m1, m2 = (torch.zeros(n, dtype=torch.float32, device=d) for _ in range(3))
+            whi, wlo = torch.zeros(n, dtype=torch.bfloat16, device=d), torch.zeros(n, dtype=torch.bfloat16, device=d)
+            hp = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0], dtype=torch.float32, device=d)
+            st = torch.cuda.current_stream(d)
+            self.allreduce_adam_on(g, st, master=master.data_ptr(), m1=m1.data_ptr(), m2=m2.data_ptr(),
+                                   whi=whi.data_ptr(), wlo=wlo.data_ptr(), hp=hp.data_ptr(), grad_scale=1.0 / self.world)
+            st.synchronize()
+            ok = int(self._cz.error()) == 0 and bool((master - (-1e-3)).abs().max().item() < 1e-6)
+            digest = hashlib.sha256(master.cpu().numpy().tobytes()).hexdigest().encode()
+        except Exception:  # noqa: BLE001
+            ok = False
+        finally:
+            try:
+                self._cz.set_timeout(float(timeout_s))
+            except Exception:  # noqa: BLE001
+                pass
+        store.set(f"{key}/ztest{self.rank}", digest if ok else b"bad")
+        got = [store.get(f"{key}/ztest{r}") for r in range(self.world)]
+        if any(x == b"bad" for x in got) or len(set(got)) != 1:
+            self._cz.close()
+            self._cz = None
+            self.zero1_selftest_failed = True
 
     @property
     def zero1_ready(self) -> bool:
