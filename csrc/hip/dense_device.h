@@ -136,13 +136,18 @@ __device__ __forceinline__ void load_hidden4(const unsigned short* __restrict__ 
   if (hpart == nullptr) {
     bits = *reinterpret_cast<const uint2*>(&hid[rr * H + 4 * lane]);
   } else {
+    const uint2 bb = *reinterpret_cast<const uint2*>(&hb[4 * lane]);
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* p = hpart + rr * H + 4 * lane;
-    for (int s = 0; s < S; s++) {
-      const float4 v = *reinterpret_cast<const float4*>(p + int64_t(s) * M * H);
-      a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
+    // slices loaded 8 at a time before any is summed (a load -> add loop waits out each round trip)
+    for (int s0 = 0; s0 < S; s0 += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = *reinterpret_cast<const float4*>(p + int64_t(min(s0 + j, S - 1)) * M * H);
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (s0 + j < S) a.x += v[j].x, a.y += v[j].y, a.z += v[j].z, a.w += v[j].w;
     }
-    const uint2 bb = *reinterpret_cast<const uint2*>(&hb[4 * lane]);
     const unsigned short o0 = f2bf(fmaxf(a.x + __uint_as_float(bb.x << 16), 0.f));
     const unsigned short o1 = f2bf(fmaxf(a.y + __uint_as_float(bb.x & 0xffff0000u), 0.f));
     const unsigned short o2 = f2bf(fmaxf(a.z + __uint_as_float(bb.y << 16), 0.f));

@@ -1026,20 +1026,59 @@ __global__ __launch_bounds__(256) void k_dense_fwd_lds_x3(CPair x, CPair w, int6
     }
 }
 
-// consumer prologue: a lane's 4 hidden values of row rr = ReLU(Σ_s part[s] + b) in fp32 (slice order)
+// consumer prologue: a lane's 4 hidden values of row rr = ReLU(Σ_s part[s] + b) in fp32 (slice order).
+// The slices' loads are issued in batches of 8 before any is waited for: a runtime-bounded loop of
+// load -> add compiled to one load and one `s_waitcnt vmcnt(0)` per slice, i.e. S serial round trips to
+// the partials (written by another launch, so L2 misses) — most of K15x's / K16x's time.
+constexpr int HID_BATCH = 8;
 __device__ __forceinline__ void load_hidden4_x3(const float* __restrict__ hpart, int S, CPair hb, int64_t M,
                                                 int64_t rr, int lane, float (&hv)[4]) {
+  unsigned short bh4[4], bl4[4];  // bias pair first: in flight with the slices
+#pragma unroll
+  for (int k = 0; k < 4; k++) bh4[k] = hb.hi[4 * lane + k], bl4[k] = hb.lo[4 * lane + k];
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* p = hpart + rr * H + 4 * lane;
-  for (int s = 0; s < S; s++) {
-    const float4 v = *reinterpret_cast<const float4*>(p + int64_t(s) * M * H);
-    a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
+  for (int s0 = 0; s0 < S; s0 += HID_BATCH) {
+    float4 v[HID_BATCH];
+#pragma unroll
+    for (int j = 0; j < HID_BATCH; j++)  // clamped: every load is valid, only the first S - s0 are summed
+      v[j] = *reinterpret_cast<const float4*>(p + int64_t(min(s0 + j, S - 1)) * M * H);
+#pragma unroll
+    for (int j = 0; j < HID_BATCH; j++)
+      if (s0 + j < S) a.x += v[j].x, a.y += v[j].y, a.z += v[j].z, a.w += v[j].w;
   }
-  hv[0] = fmaxf(a.x + join(hb, 4 * lane), 0.f);
-  hv[1] = fmaxf(a.y + join(hb, 4 * lane + 1), 0.f);
-  hv[2] = fmaxf(a.z + join(hb, 4 * lane + 2), 0.f);
-  hv[3] = fmaxf(a.w + join(hb, 4 * lane + 3), 0.f);
+  hv[0] = fmaxf(a.x + join(bh4[0], bl4[0]), 0.f);
+  hv[1] = fmaxf(a.y + join(bh4[1], bl4[1]), 0.f);
+  hv[2] = fmaxf(a.z + join(bh4[2], bl4[2]), 0.f);
+  hv[3] = fmaxf(a.w + join(bh4[3], bl4[3]), 0.f);
 }
+
+// the heads' split weights joined into fp32 LDS images (whs [A1][H], bhs [A1]) by a workgroup of exactly NT
+// threads, in two halves: issue() puts every global load in flight (the kernels issue it before their other
+// loads), store() joins them into LDS. The strided loop it replaces waited for each pass in turn.
+template <int A1, int NT>
+struct HeadsStage {
+  static constexpr int PER = (A1 * H + NT - 1) / NT;
+  unsigned short vh[PER], vl[PER], bhh = 0, bhl = 0;
+  __device__ __forceinline__ void issue(CPair wh, CPair bh) {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int e = min(int(threadIdx.x) + NT * k, A1 * H - 1);
+      vh[k] = wh.hi[e];
+      vl[k] = wh.lo[e];
+    }
+    const int eb = min(int(threadIdx.x), A1 - 1);  // unconditional (clamped): a guarded load is waited for at once
+    bhh = bh.hi[eb], bhl = bh.lo[eb];
+  }
+  __device__ __forceinline__ void store(float* whs, float* bhs) const {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int e = int(threadIdx.x) + NT * k;
+      if (e < A1 * H) whs[e] = join(vh[k], vl[k]);
+    }
+    if (threadIdx.x < A1) bhs[threadIdx.x] = join(bhh, bhl);
+  }
+};
 
 // ---- K15x: heads + PPO loss statistics + dheads + dpre, one wave per row, all fp32 math
 // (dense_kernels.hip K15 with fp32 heads / gradients). Outputs as split pairs: dz [M, A1], dpre [M, 256]
@@ -1064,10 +1103,11 @@ __global__ __launch_bounds__(256) void k_heads_ppo_x3(const float* __restrict__ 
   float cv[A + 4];
 #pragma unroll
   for (int j = 0; j < A + 4; j++) cv[j] = crow[j];
+  HeadsStage<A1, 256> hs;  // launched with 256 threads; its loads in flight with the row's
+  hs.issue(wh, bh);
   float hv[4];
   load_hidden4_x3(hpart, S, hb, M, rr, lane, hv);
-  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
-  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  hs.store(whs, bhs);
   __syncthreads();
   const float gs = gout[0] / float(M);
   if (valid) store4(hid, row * H + 4 * lane, hv);
@@ -1125,12 +1165,13 @@ __global__ __launch_bounds__(256) void k_heads_sample_x3(const float* __restrict
   __shared__ float bhs[A1];
   const int lane = threadIdx.x & 63;
   const int64_t b = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  float hv[4] = {0.f, 0.f, 0.f, 0.f};
-  if (b < B) load_hidden4_x3(hpart, S, hb, B, b, lane, hv);
+  HeadsStage<A1, 256> hs;  // launched with 256 threads
+  hs.issue(wh, bh);
   const int64_t t = *t_ptr;
   const uint32_t c = uint32_t(*ctr);
-  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
-  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  float hv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (b < B) load_hidden4_x3(hpart, S, hb, B, b, lane, hv);
+  hs.store(whs, bhs);
   __syncthreads();
   if (b < B) dense::heads_sample_row_pre<A1, false>(hv, whs, bhs, t, c, seed, act, logp, vf, lout, act_now, B, b, lane);
   if (done) {
@@ -1181,8 +1222,11 @@ __global__ __launch_bounds__(256) void k_dense_heads_sample_x3(CPair x, CPair w,
   __syncthreads();
   if (!s_last) return;
   __threadfence();  // every contributor's partial tile of row tile tm
-  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
-  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
+  {
+    HeadsStage<A1, 256> hs;
+    hs.issue(wh, bh);
+    hs.store(whs, bhs);
+  }
   const int64_t t = *t_ptr;
   const uint32_t c = uint32_t(*ctr);
   __syncthreads();
@@ -1224,14 +1268,15 @@ __global__ __launch_bounds__(1024) void k_heads_sample1_x3(const float* __restri
   constexpr int kWaves = 16;
   const int lane = threadIdx.x & 63;
   const int64_t b0 = threadIdx.x >> 6;
+  HeadsStage<A1, 1024> hs;  // launched with 1024 threads
+  hs.issue(wh, bh);
+  const int64_t t = *t_ptr;
+  const uint32_t c = uint32_t(*ctr);
   float hv[R][4];
 #pragma unroll
   for (int q = 0; q < R; q++)
     if (b0 + q * kWaves < B) load_hidden4_x3(hpart, S, hb, B, b0 + q * kWaves, lane, hv[q]);
-  for (int e = threadIdx.x; e < A1 * H; e += blockDim.x) whs[e] = join(wh, e);
-  if (threadIdx.x < A1) bhs[threadIdx.x] = join(bh, threadIdx.x);
-  const int64_t t = *t_ptr;
-  const uint32_t c = uint32_t(*ctr);
+  hs.store(whs, bhs);
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < R; q++)
