@@ -688,6 +688,7 @@ PYBIND11_MODULE(_hip, m) {
 
   // ---------------------------------------------------------------- split-bf16 (fp32-level) kernels
   // a split pair crosses as (hi_ptr, lo_ptr); (0, 0) = absent
+  m.def("x3_probe_set", [](uint64_t ts) { x3_probe_set(reinterpret_cast<uint64_t*>(ts)); }, py::arg("ts"));
   m.def("x3_split", [](uint64_t src, uint64_t hi, uint64_t lo, int64_t n, uint64_t stream) {
     x3_split(P<const float>(src), P<void>(hi), P<void>(lo), n, S(stream));
   });
@@ -733,13 +734,14 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("x3_heads_ppo", [](uint64_t hpart, int nslices, XP hb, XP wh, XP bh, uint64_t cols, uint64_t coef, uint64_t acc,
                            uint64_t gout, int64_t M, int A1, XP dz, XP dpre, XP hid, uint64_t stream, uint64_t cidx,
-                           uint64_t ctr, int64_t period) {
+                           uint64_t ctr, int64_t period, bool acc_slab) {
     x3_heads_ppo(P<const float>(hpart), nslices, xin(hb), xin(wh), xin(bh), P<const float>(cols), P<const float>(coef),
                  P<float>(acc), P<const float>(gout), M, A1, xout(dz), xout(dpre), xout(hid), S(stream),
-                 cidx ? P<const int64_t>(cidx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr, period);
+                 cidx ? P<const int64_t>(cidx) : nullptr, ctr ? P<const int64_t>(ctr) : nullptr, period, acc_slab);
   }, py::arg("hpart"), py::arg("S"), py::arg("hb"), py::arg("wh"), py::arg("bh"), py::arg("cols"), py::arg("coef"),
      py::arg("acc"), py::arg("gout"), py::arg("M"), py::arg("A1"), py::arg("dz"), py::arg("dpre"), py::arg("hid"),
-     py::arg("stream"), py::arg("cidx") = 0, py::arg("ctr") = 0, py::arg("period") = 1);
+     py::arg("stream"), py::arg("cidx") = 0, py::arg("ctr") = 0, py::arg("period") = 1, py::arg("acc_slab") = false);
+  m.def("x3_heads_ppo_groups", &x3_heads_ppo_groups, py::arg("M"));
   m.def("x3_heads_sample", [](uint64_t hpart, int nslices, XP hb, XP wh, XP bh, uint64_t t_ptr, uint64_t ctr,
                               uint32_t seed, uint64_t act, uint64_t logp, uint64_t vf, uint64_t lout, uint64_t act_now,
                               int64_t B, int A1, uint64_t stream, uint64_t done, uint64_t host_seq) {

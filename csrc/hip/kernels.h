@@ -243,10 +243,14 @@ void x3_dense_adam(const X3Adam& xa, hipStream_t stream);
 // K13x: split-K dense layer -> fp32 partials part[S][M][N]
 int x3_dense_fwd_part_slices(int64_t M, int64_t K, int N);
 void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part, int S, hipStream_t stream);
-// K15x: hidden = ReLU(Σ partials + hb) (fp32), heads, PPO loss stats into acc, dz / dpre / hid split pairs
+// K15x: hidden = ReLU(Σ partials + hb) (fp32), heads, PPO loss stats into acc, dz / dpre / hid split pairs.
+// acc_slab: acc is a per-workgroup slab [x3_heads_ppo_groups(M)][8] (each workgroup adds its 6 sums into its
+// own row, no atomics; the caller sums the rows) instead of 6 floats every workgroup adds to atomically
+int x3_heads_ppo_groups(int64_t M);
 void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const float* cols, const float* coef, float* acc,
                   const float* gout, int64_t M, int A1, X3Out dz, X3Out dpre, X3Out hid, hipStream_t stream,
-                  const int64_t* cidx = nullptr, const int64_t* ctr = nullptr, int64_t period = 1);
+                  const int64_t* cidx = nullptr, const int64_t* ctr = nullptr, int64_t period = 1,
+                  bool acc_slab = false);
 // K16x: fp32 head row + Gumbel-max sampling + rollout-row stores (+ the step advance with `done`)
 void x3_heads_sample(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const int64_t* t_ptr, const int64_t* ctr,
                      uint32_t seed, int64_t* act, float* logp, float* vf, float* lout, int64_t* act_now, int64_t B, int A1,
@@ -265,6 +269,8 @@ void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int6
                         float* db2 = nullptr, float* dwh2 = nullptr, float* dbh2 = nullptr);
 // fp32 -> split pair (weights after a host-side update, tests)
 void x3_split(const float* src, void* hi, void* lo, int64_t n, hipStream_t stream);
+// phase probe of the x3 SGD-step kernels: a device buffer of 7 x 1024 x 16 uint64 (nullptr: off)
+void x3_probe_set(uint64_t* ts);
 
 // K17: learner-side sample-batch ingest (see ingest_kernels.hip). raw [rows, A+5] fp32 =
 // [logits(A) | logp | vf | reward | done | action], blocks = one entry per rollout fragment

@@ -335,6 +335,21 @@ k_peer_zero1(PeerArgs a, const void* grad, int64_t n, Zero1Dev z) {
 #pragma unroll
         for (int r = 0; r < kPeerMaxRanks; r++)
           if (r < a.world) x[r] = reinterpret_cast<const uint4*>(a.data[r] + par * a.cap)[v];
+        // this slot's master / moments loaded with the peers' slices, before the sum waits for them (loaded
+        // after it, they cost a second round trip per slot); clamped to the last whole quad, used only when
+        // the quad is whole
+        constexpr int NQ = N / 4;
+        float4 wq[NQ], mq[NQ], sq[NQ];
+        if (n >= 4) {
+          const int64_t lastq = ((n >> 2) - 1) << 2;
+#pragma unroll
+          for (int q = 0; q < NQ; q++) {
+            const int64_t el = min(v * N + 4 * q, lastq);
+            wq[q] = *reinterpret_cast<const float4*>(z.master + el);
+            mq[q] = *reinterpret_cast<const float4*>(z.m1 + el);
+            sq[q] = *reinterpret_cast<const float4*>(z.m2 + el);
+          }
+        }
         float acc[N], f[N];
         V<BF16>::unpack(x[0], acc);
 #pragma unroll
@@ -350,9 +365,7 @@ k_peer_zero1(PeerArgs a, const void* grad, int64_t n, Zero1Dev z) {
         for (int q = 0; q < N / 4; q++) {
           const int64_t e0 = v * N + 4 * q;
           if (e0 + 4 <= n) {
-            float4 w = *reinterpret_cast<const float4*>(z.master + e0);
-            float4 m = *reinterpret_cast<const float4*>(z.m1 + e0);
-            float4 s2 = *reinterpret_cast<const float4*>(z.m2 + e0);
+            float4 w = wq[q], m = mq[q], s2 = sq[q];
             w.x = adam_one(w.x, acc[4 * q] * z.grad_scale, m.x, s2.x, c);
             w.y = adam_one(w.y, acc[4 * q + 1] * z.grad_scale, m.y, s2.y, c);
             w.z = adam_one(w.z, acc[4 * q + 2] * z.grad_scale, m.z, s2.z, c);

@@ -54,6 +54,18 @@ using trunk::W2_PITCH;
 using trunk::WeightRegs;
 using trunk::WStrides;
 
+// ---------------------------------------------------------------- phase probe (opt-in, x3_probe_set)
+// When a buffer is set, thread 0 of every workgroup stores the 100 MHz real-time counter at the kernels'
+// phase boundaries: ts[(kernel * 1024 + workgroup) * 16 + slot] (benchmarks/x3_phase_probe.py reads it).
+// Unset (the default) a probe site costs one scalar-pointer test.
+__device__ uint64_t* g_x3_ts = nullptr;
+enum : int { TS_FWD = 0, TS_C2B = 1, TS_C1W = 2, TS_K12 = 3, TS_RED = 4, TS_K13L = 5, TS_K15 = 6 };
+__device__ __forceinline__ void x3_ts(int k, int slot) {
+  uint64_t* p = g_x3_ts;
+  if (p != nullptr && threadIdx.x == 0 && blockIdx.x < 1024 && slot < 16)
+    p[(int64_t(k) * 1024 + blockIdx.x) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 // ================================================================ K10x forward
 constexpr int NTF = 512;  // 8 waves (1024 threads cap a lane at 128 VGPRs: the W1 / W2 pair fragments spilled)
 constexpr int FIMG = P0 * P0 * C0;  // the whole padded HWC frame as bf16 (exact for 0..255)
@@ -121,6 +133,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   const int64_t G = gridDim.x;
   const int64_t* idx = trunk::window(idx0, ctr, period, B);
   constexpr int64_t FB = C0 * H0 * H0;
+  x3_ts(TS_FWD, 0);
 
   // prologue: weight loads (L2), then the first frame's HBM loads, then zeroing and staging
   WeightRegs<NTF, C1, C0, 8> r1h, r1l;
@@ -173,6 +186,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   // nt = wave & 1 never changes) — read them from LDS once (128 VGPRs) instead of 2 of every 3 (conv1) /
   // 4 (conv2) LDS reads per MFMA group
   __syncthreads();  // weights staged
+  x3_ts(TS_FWD, 1);
   bf16x8 w1fh[8], w1fl[8], w2fh[8], w2fl[8];
   {
     const int nt = wave & 1;
@@ -193,6 +207,8 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       cols_out[b * ncols + threadIdx.x] = cols[(idx ? idx[b] : b) * ncols + threadIdx.x];
     frame_image_store<NTF>(fr, img);
     __syncthreads();  // image (+ first frame: border / h1 zeros, weights); the previous conv2 is done
+    const int fi = int((b - blockIdx.x) / G);
+    x3_ts(TS_FWD, 2 + 3 * fi);
     if (b + G < B) trunk::frame_issue<NTF>(obs + (idx ? idx[b + G] : b + G) * FB, fr);  // in flight meanwhile
 
     // ---- conv1: M = 441 positions (28 tiles) x N = 16 x K = 256 (k = ky, kx, ci); frame exact -> 2 MFMAs
@@ -223,6 +239,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       }
     }
     __syncthreads();
+    x3_ts(TS_FWD, 3 + 3 * fi);
 
     // ---- conv2: 8 M-tiles x 2 N-tiles = 16 jobs over the waves, K = 256 (pixel pp = 2s + (g>>1), ci half g&1)
     static_assert(NTF / 64 % 2 == 0, "a wave's conv2 N tile (job & 1) must not change");
@@ -244,7 +261,9 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
         if (qq < NP2) store1(h2_out, (b * NP2 + qq) * C2 + nt * 16 + r, fmaxf(t[i] + bias2[nt], 0.f));
       }
     }
+    x3_ts(TS_FWD, 4 + 3 * fi);
   }
+  x3_ts(TS_FWD, 15);
 }
 
 // ================================================================ K10x backward, launch 1: conv2
@@ -296,6 +315,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   constexpr int DPL = D2W * D2W * C2, DTL = C2 * DP2_PITCH;
+  x3_ts(TS_C2B, 0);
 
   WeightRegs<NTB, C2, C1, 4> wrh, wrl;
   trunk::weight_issue(W2.hi, w2, wrh);
@@ -332,8 +352,10 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
   for (int i = 0; i < 2; i++) aw2[0][i] = aw2[1][i] = acc0();
   float db1 = 0.f, db2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   __syncthreads();
+  x3_ts(TS_C2B, 1);
 
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    const int fi = int((b - blockIdx.x) / gridDim.x);
     // ---- P0: h1 -> padded tile planes, dpre2 (both layouts, both planes) + db2
 #pragma unroll
     for (int k = 0; k < B1_PH1; k++) {
@@ -363,6 +385,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
       *reinterpret_cast<u16x8*>(&dp2[DPL + (oy * D2W + ox) * C2 + c0]) = ol;
     }
     __syncthreads();
+    x3_ts(TS_C2B, 2 + 4 * fi);
     if (b + gridDim.x < B) b1_issue(b + gridDim.x, h1, h2hi, dh2, R);  // next frame: in flight through P1
 
     // ---- P1a: dW2[co2][k = (ky, kx, ci)] += Σ_q dpre2[q][co2] · h1[2oy+ky][2ox+kx][ci]
@@ -400,6 +423,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
         mma3(aw2[1][i], a1h, a1l, as_bf(bh), as_bf(bl));
       }
     }
+    x3_ts(TS_C2B, 3 + 4 * fi);
     // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 -> dpre1 (HBM), db1
     for (int mt = half; mt * 16 < ((dbg & 2) ? 0 : ncls); mt += 2) {
       const int m = min(mt * 16 + r, ncls - 1);
@@ -430,6 +454,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
       }
     }
     __syncthreads();  // tiles free for the next frame; dq complete
+    x3_ts(TS_C2B, 4 + 4 * fi);
     {  // dpre1 pair of frame b: 2 x 441 x 16 bf16 -> HBM in 16-B vectors
       constexpr int NV = NP1 * C1 / 8;  // vectors per plane
       const int64_t go = b * NP1 * C1;
@@ -439,6 +464,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
         *reinterpret_cast<u16x8*>(&(pl ? dpre1.lo : dpre1.hi)[go + 8 * vv]) = d;
       }
     }
+    x3_ts(TS_C2B, 5 + 4 * fi);
   }
 
   float* out = partial + int64_t(blockIdx.x) * PART2;
@@ -480,6 +506,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
     for (int w = 0; w < 8; w++) s += red[w * 16 + threadIdx.x];
     out[C2 * 256 + C2 + threadIdx.x] = s;
   }
+  x3_ts(TS_C2B, 15);
 }
 
 // ================================================================ K10x backward, launch 2: conv1 dW1
@@ -514,6 +541,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
       vl[k] = *reinterpret_cast<const u16x8*>(&dpre1.lo[o]);
     }
   };
+  x3_ts(TS_C1W, 0);
   if (int64_t(blockIdx.x) < B) issue(blockIdx.x);
   trunk::zero_lds(st, trunk::ST_ELEMS * 2);
   trunk::zero_lds(dp, 4 * DB_B * 2);
@@ -540,6 +568,8 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
       }
     }
     __syncthreads();
+    const int fi = int((b - blockIdx.x) / gridDim.x);
+    x3_ts(TS_C1W, 1 + 2 * fi);
     if (b + gridDim.x < B) issue(b + gridDim.x);
     {
       const int cb = wave & 3, a = wave >> 2;
@@ -553,6 +583,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
       }
     }
     __syncthreads();
+    x3_ts(TS_C1W, 2 + 2 * fi);
   }
   // tile b holds D[m = 4g+e][co = r], channel c = 16cb + m -> ry = cb, rx = g, ci = e; ky = 4a+ry, kx = 4b+rx
   float* out = partial + int64_t(blockIdx.x) * PART1;
@@ -563,6 +594,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
 #pragma unroll
     for (int e = 0; e < 4; e++) out[r * 256 + ky * 32 + kx * 4 + e] = t[e] * (1.0f / 255.0f);
   }
+  x3_ts(TS_C1W, 15);
 }
 
 // ================================================================ K10x reduce
@@ -578,7 +610,7 @@ __device__ __forceinline__ void x3_tail_bump(const X3Adam& xa) {
   }
   last_block_bump(xa.bump, xa.nbump, xa.done);
 }
-constexpr int RED_SLICES = 8, RED_BATCH = 16;
+constexpr int RED_SLICES = 8, RED_BATCH = 32;  // G <= 256 partials: one batch of loads per thread
 __device__ __forceinline__ float* trunk_grad_dst_f32(int e, float* dW1, WStrides w1, float* db1, float* dW2,
                                                      WStrides w2, float* db2) {
   if (e < C1 * 256) {
@@ -597,6 +629,7 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
                                                          WStrides w1, float* db1, float* dW2, WStrides w2, float* db2,
                                                          const X3Adam xa, int nred) {
   __shared__ float red[RED_SLICES][64];
+  x3_ts(TS_RED, 0);
   if (int(blockIdx.x) >= nred) {  // Adam workgroups: K6's vector pass over the dense + heads range
     const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
     const int64_t o = xa.n_trunk;
@@ -605,6 +638,7 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     adam_span<float, true, 2>(xa.master + o, xa.m1 + o, xa.m2 + o, xa.grad + o,
                               static_cast<__hip_bfloat16*>(xa.whi) + o, xa.grad_scale, ac, tid, nthr, xa.n - o,
                               static_cast<__hip_bfloat16*>(xa.wlo) + o, xa.grad2);
+    x3_ts(TS_RED, 15);
     x3_tail_bump(xa);
     return;
   }
@@ -621,6 +655,13 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     const int o = f < C2 * 256 ? f : (f < C2 * 256 + C1 ? C2 * 256 + C2 + (f - C2 * 256) : C2 * 256 + (f - C2 * 256 - C1));
     src = part2 + o, G = G2, stride = PART2;
   }
+  // the element's Adam state is loaded FIRST, with the partials behind it: every load of the workgroup is in
+  // flight at once (loaded after the partial sum, it was a second serial round trip before the update)
+  const bool upd = slice == 0 && e < PARTX && xa.master != nullptr;
+  float* dst = e < PARTX ? trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2) : nullptr;
+  const int64_t ai = upd ? dst - xa.grad : 0;
+  float am1 = 0.f, am2 = 0.f, aw = 0.f;
+  if (upd) am1 = xa.m1[ai], am2 = xa.m2[ai], aw = xa.master[ai];
   float s = 0.f;
   if (src) {
     for (int g0 = slice; g0 < G; g0 += RED_SLICES * RED_BATCH) {
@@ -638,22 +679,20 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
-    float* dst = trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2);
     *dst = t;
-    if (xa.master) {  // the trunk gradient is final: Adam on it (same math as K6's scalar pass)
+    if (upd) {  // the trunk gradient is final: Adam on it (same math as K6's scalar pass)
       const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
-      const int64_t i = dst - xa.grad;
-      float a = xa.m1[i], b = xa.m2[i];
-      const float w = adam_one(xa.master[i], t * xa.grad_scale, a, b, ac);
-      xa.m1[i] = a;
-      xa.m2[i] = b;
-      xa.master[i] = w;
+      const float w = adam_one(aw, t * xa.grad_scale, am1, am2, ac);
+      xa.m1[ai] = am1;
+      xa.m2[ai] = am2;
+      xa.master[ai] = w;
       unsigned short hi, lo;
       split(w, hi, lo);
-      static_cast<unsigned short*>(xa.whi)[i] = hi;
-      static_cast<unsigned short*>(xa.wlo)[i] = lo;
+      static_cast<unsigned short*>(xa.whi)[ai] = hi;
+      static_cast<unsigned short*>(xa.wlo)[ai] = lo;
     }
   }
+  x3_ts(TS_RED, 15);
   if (xa.master) x3_tail_bump(xa);
 }
 
@@ -680,6 +719,10 @@ static x3::Pair pp(const X3Out& p) { return x3::Pair{static_cast<unsigned short*
 
 static void check_pair(const X3In& p, const char* what) {
   if ((p.hi == nullptr) != (p.lo == nullptr)) throw std::invalid_argument(std::string(what) + ": hi and lo planes");
+}
+
+void x3_probe_set(uint64_t* ts) {
+  RMM_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(x3::g_x3_ts), &ts, sizeof(ts)));
 }
 
 int x3_trunk_fwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 256))); }
@@ -917,6 +960,7 @@ constexpr int KL_D = 4;                 // register-ring depth (stages of global
 __global__ __launch_bounds__(256) void k_dense_fwd_lds_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
                                                           float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) unsigned short t[2 * KL_STAGE];
+  x3_ts(TS_K13L, 0);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4, wm = wave >> 1, wn = wave & 1;
   const int nt = N / KL_T;
@@ -1024,6 +1068,7 @@ __global__ __launch_bounds__(256) void k_dense_fwd_lds_x3(CPair x, CPair w, int6
         if (row < M) out[row * N + 16 * j] = tt[e];
       }
     }
+  x3_ts(TS_K13L, 15);
 }
 
 // consumer prologue: a lane's 4 hidden values of row rr = ReLU(Σ_s part[s] + b) in fp32 (slice order).
@@ -1089,8 +1134,12 @@ __global__ __launch_bounds__(256) void k_heads_ppo_x3(const float* __restrict__ 
                                                       const float* __restrict__ coef, float* __restrict__ acc,
                                                       const float* __restrict__ gout, int64_t M, Pair dz, Pair dpre,
                                                       Pair hid, const int64_t* __restrict__ cidx,
-                                                      const int64_t* __restrict__ ctr, int64_t period) {
+                                                      const int64_t* __restrict__ ctr, int64_t period, int acc_slab) {
   constexpr int A = A1 - 1;
+  x3_ts(TS_K15, 0);
+  // slab mode: this workgroup's running sums, loaded now (in flight with everything else), rewritten at the end
+  float* srow = acc + int64_t(blockIdx.x) * 8;
+  const float sold = (acc && acc_slab && threadIdx.x < 6) ? srow[threadIdx.x] : 0.f;
   __shared__ __attribute__((aligned(16))) float whs[A1 * H];
   __shared__ float bhs[A1];
   __shared__ float red[6][4];
@@ -1146,11 +1195,17 @@ __global__ __launch_bounds__(256) void k_heads_ppo_x3(const float* __restrict__ 
   if (lane == 0)
     for (int k = 0; k < 6; k++) red[k][wave] = s[k];
   __syncthreads();
-  if (threadIdx.x < 6) {
+  if (acc && threadIdx.x < 6) {
     float t = 0.f;
     for (int k = 0; k < int(blockDim.x >> 6); k++) t += red[threadIdx.x][k];
-    atomicAdd(&acc[threadIdx.x], t);
+    // 125 workgroups' atomics on the same 6 words serialise at the device-coherent atomic unit (~1.3 us of
+    // the launch at M = 500); the slab gives each workgroup its own row
+    if (acc_slab)
+      srow[threadIdx.x] = sold + t;
+    else
+      atomicAdd(&acc[threadIdx.x], t);
   }
+  x3_ts(TS_K15, 15);
 }
 
 // ---- K16x: heads + Gumbel-max sampling + rollout-row stores (+ step advance), fp32 head row
@@ -1560,10 +1615,12 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd_x3(CPair dz, CPair y, CP
   const bool head = b >= NJ * rs;
   const int i = head ? b - NJ * rs : b, per = head ? H / HQ : NJ, part = i / per, j = i - part * per;
   const int c0 = NC * part / rs, c1 = NC * (part + 1) / rs;
+  x3_ts(TS_K12, 0);
   if (head)
     k12x_head<A1>(dz, y, dpre, M, part ? db2 : db, part ? dwh2 : dwh, part ? dbh2 : dbh, lds, j, c0, c1);
   else
     k12x_cols(x, w, dpre, M, K, int64_t(j) * JB, dx, part ? dw2 : dw, lds, c0, c1);
+  x3_ts(TS_K12, 15);
 }
 
 }  // namespace x3
@@ -1619,20 +1676,21 @@ void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part,
   RMM_HIP_CHECK(hipGetLastError());
 }
 
+int x3_heads_ppo_groups(int64_t M) { return int((M + 3) / 4); }
 void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const float* cols, const float* coef, float* acc,
                   const float* gout, int64_t M, int A1, X3Out dz, X3Out dpre, X3Out hid, hipStream_t stream,
-                  const int64_t* cidx, const int64_t* ctr, int64_t period) {
+                  const int64_t* cidx, const int64_t* ctr, int64_t period, bool acc_slab) {
   if (M <= 0) return;
   if (period < 1) period = 1;
   if (A1 < 3 || A1 > dense::AMAX) throw std::invalid_argument("x3_heads_ppo: 2 <= A <= 15 actions");
   if (!hpart || S < 1 || !hb.hi || !hb.lo || !wh.hi || !wh.lo || !bh.hi || !bh.lo || !dz.hi || !dz.lo || !dpre.hi ||
       !dpre.lo || !hid.hi || !hid.lo)
     throw std::invalid_argument("x3_heads_ppo: partials, split weights and split outputs required");
-  const dim3 grid(uint32_t((M + 3) / 4)), block(256);
+  const dim3 grid(uint32_t(x3_heads_ppo_groups(M))), block(256);
 #define RMM_K15X(N)                                                                                               \
   case N:                                                                                                         \
     hipLaunchKernelGGL(x3::k_heads_ppo_x3<N>, grid, block, 0, stream, hpart, S, cp(hb), cp(wh), cp(bh), cols, coef, \
-                       acc, gout, M, pp(dz), pp(dpre), pp(hid), cidx, ctr, period);                              \
+                       acc, gout, M, pp(dz), pp(dpre), pp(hid), cidx, ctr, period, int(acc_slab));               \
     break;
   switch (A1) {
     RMM_K15X(3) RMM_K15X(4) RMM_K15X(5) RMM_K15X(6) RMM_K15X(7) RMM_K15X(8) RMM_K15X(9)

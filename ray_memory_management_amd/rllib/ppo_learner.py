@@ -437,11 +437,27 @@ class PPOLearner:
               "hpart": torch.empty(S * mbs * 256, dtype=torch.float32, device=dev),
               "part": torch.empty(X3.trunk_partial_floats(mbs), dtype=torch.float32, device=dev),
               # the minibatch's loss columns, gathered by K10x so K15x reads them without the index chain
-              "colsg": torch.empty((mbs, A1 + 3), dtype=torch.float32, device=dev)}
+              "colsg": torch.empty((mbs, A1 + 3), dtype=torch.float32, device=dev),
+              # K15x's loss statistics, one row of running sums per workgroup (no same-word atomics), folded
+              # into `acc` once per update (_fold_k15_stats)
+              "k15s": torch.zeros((require_hip().x3_heads_ppo_groups(mbs), 8), dtype=torch.float32, device=dev)}
         if self._manual is not None:  # K12x second row part's dense + heads gradients (see _x3_rows)
             ws["grad2"] = torch.empty(self.n_params - self._manual, dtype=torch.float32, device=dev)
         self._mws = ws
         return ws
+
+    def _zero_k15_stats(self):
+        ws = getattr(self, "_mws", None)
+        if ws is not None and "k15s" in ws:
+            ws["k15s"].zero_()
+
+    def _fold_k15_stats(self):
+        """Add K15x's per-workgroup loss-statistics rows into `acc` (a fixed-order sum: deterministic, unlike
+        the same-word atomics it replaces) and clear them."""
+        ws = getattr(self, "_mws", None)
+        if ws is not None and "k15s" in ws:
+            self.acc.add_(ws["k15s"][:, :6].sum(0))
+            ws["k15s"].zero_()
 
     def _x3_rows(self, mbs) -> int:
         """K12x row parts: 2 when the tail Adam consumes the dense + heads gradients (world of one, no clip)
@@ -473,9 +489,10 @@ class PPOLearner:
                        cols_out=colsg.data_ptr() if gather else 0, ncols=colsg.shape[1] if gather else 0)
         h.x3_dense_fwd_part(ws["h2"].ptrs(), wd.ptrs(), mbs, K, 256, ws["hpart"].data_ptr(), ws["S"], st)
         h.x3_heads_ppo(ws["hpart"].data_ptr(), ws["S"], bd.ptrs(), wh.ptrs(), bh.ptrs(),
-                       (colsg if gather else cols).data_ptr(), self.coef.data_ptr(), self.acc.data_ptr(),
+                       (colsg if gather else cols).data_ptr(), self.coef.data_ptr(), ws["k15s"].data_ptr(),
                        self._one.data_ptr(), mbs, A1, ws["dz"].ptrs(), ws["dpre"].ptrs(), ws["hid"].ptrs(), st,
-                       cidx=0 if gather else idx.data_ptr(), ctr=0 if gather else ctr.data_ptr(), period=int(period))
+                       cidx=0 if gather else idx.data_ptr(), ctr=0 if gather else ctr.data_ptr(), period=int(period),
+                       acc_slab=True)
         g = [p._rmm_grad_out for p in self.params]
         rs = self._x3_rows(mbs)
         side = {}
@@ -1047,6 +1064,7 @@ class PPOLearner:
         else:
             full = packed
         self.ctr[0:1].zero_()
+        self._zero_k15_stats()  # after any capture: its warm-up steps wrote the slab too
         steps, total = 0, c["num_sgd_iter"] * nmb
         chain = getattr(self, "_chain", 1) if self.graphs and self._graph is not None else 1
         if total % chain:  # not expected: the chain divides the period it was captured for
@@ -1058,6 +1076,7 @@ class PPOLearner:
                 self._step_eager(full)
             steps += chain
         self._dbg(f"update: {steps} SGD steps")
+        self._fold_k15_stats()
         if self.world > 1:  # KL adaptation and stats from the global batch, identical on every rank
             self.comm.allreduce(self.acc)
             self.acc.mul_(1.0 / self.world)

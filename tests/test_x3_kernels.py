@@ -184,6 +184,17 @@ def test_x3_dense_heads_ppo_chain_matches_fp64(cuda, M, K, A):
     errs = {n: _rel(a, r.grad) for n, a, r in zip(("dx", "dW", "db", "dWh", "dbh"),
                                                    (dx.float(), dW, db, dWh, dbh), [xr] + ps)}
     assert max(errs.values()) < GRAD_TOL, errs
+    # slab mode (the learner's): each workgroup adds its sums into its own row, no atomics; two launches
+    # accumulate, the rows sum to twice the atomic total; outputs unchanged
+    slab = torch.zeros(h.x3_heads_ppo_groups(M), 8, device=cuda)
+    dz0 = dz.hi.clone()
+    for _ in range(2):
+        h.x3_heads_ppo(part.data_ptr(), S, b.ptrs(), Wh.ptrs(), bh.ptrs(), cols.data_ptr(), coef.data_ptr(),
+                       slab.data_ptr(), one.data_ptr(), M, A1, dz.ptrs(), dpre.ptrs(), hid.ptrs(), s, acc_slab=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dz.hi, dz0)
+    torch.testing.assert_close(slab[:, :6].sum(0), 2 * acc, rtol=1e-5, atol=1e-5)
+    assert not slab[:, 6:].any()
 
 
 @pytest.mark.parametrize("M,K,A", [(500, 3872, 4), (130, 64, 15), (257, 96, 5)])
