@@ -263,6 +263,11 @@ def zero1_blocks_for(h, device: int, ranks_on_device: int = 1, cap: int = 256, c
     except Exception:  # noqa: BLE001 - no query: the conservative all-reduce count
         return 64
     n = min(int(cap), slots // max(1, int(ranks_on_device)))
+    if int(ranks_on_device) >= 8:
+        # 8 ranks on one device (1-GPU rehearsals): 32 spinning workgroups per rank kept a slot busy on every
+        # CU and a lagging rank's trunk kernels (one ~150 KB-LDS workgroup per CU) could not run; 8 completes
+        # (profiles/multirank_r6.txt)
+        n = 8
     return max(8, n - n % 8)
 
 
@@ -291,9 +296,20 @@ class PeerComm(Comm):
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self.world, self.rank = int(world), int(rank)
         timeout_s = timeout_s or float(os.environ.get("RMM_PEER_TIMEOUT_S", "60"))
+        try:  # which physical GPU each rank drives: ranks sharing one only contend when they overlap
+            bus = h.pci_bus_id(self.device.index).encode()
+        except Exception:  # noqa: BLE001
+            bus = f"?{self.rank}".encode()
+        store.set(f"{key}/bus{self.rank}", bus)
+        buses = [store.get(f"{key}/bus{r}") for r in range(self.world)]
+        #: True when some ranks share a physical GPU (1-GPU rehearsals, several learners per GPU)
+        self.shared_device = len(set(buses)) < self.world
+        #: ranks driving this rank's physical GPU (1 = one process per GPU)
+        self.ranks_on_device = max(1, buses.count(buses[self.rank]))
         # one workgroup per CU would saturate the links long before the payload does; 64 keeps the
         # barrier fan-in small (64 x W flags) and still leaves most of the chip to the trunk kernels
-        nblocks = nblocks or int(os.environ.get("RMM_PEER_BLOCKS", "64"))
+        # (8 when 8 ranks share the device: see zero1_blocks_for)
+        nblocks = nblocks or int(os.environ.get("RMM_PEER_BLOCKS", "64" if self.ranks_on_device < 8 else "8"))
         # every rank reaches every store key even when its own setup fails, so the ranks agree on
         # the outcome (all PeerComm, or all raise PeerUnavailable and fall back) instead of hanging
         err, blob, self._c = None, b"", None
@@ -304,14 +320,7 @@ class PeerComm(Comm):
         except Exception as e:  # noqa: BLE001
             err = e
         store.set(f"{key}/h{self.rank}", blob)
-        try:  # which physical GPU each rank drives: ranks sharing one only contend when they overlap
-            bus = h.pci_bus_id(self.device.index).encode()
-        except Exception:  # noqa: BLE001
-            bus = f"?{self.rank}".encode()
-        store.set(f"{key}/bus{self.rank}", bus)
         hs = [store.get(f"{key}/h{r}") for r in range(self.world)]
-        #: True when some ranks share a physical GPU (1-GPU rehearsals, several learners per GPU)
-        self.shared_device = len({store.get(f"{key}/bus{r}") for r in range(self.world)}) < self.world
         ok = err is None and all(len(b) > 0 for b in hs)
         if ok:
             try:
@@ -356,9 +365,6 @@ class PeerComm(Comm):
         # over 1/W of the bucket wants many more workgroups than the plain all-reduce's barrier fan-in
         # does (64 -> 256: the fp32 PPO bucket's step on 64 workgroups was latency-bound), and one
         # communicator must keep one workgroup count (its staging reuse is argued per workgroup slice)
-        buses = [store.get(f"{key}/bus{r}") for r in range(self.world)]
-        #: ranks driving this rank's physical GPU (1 = one process per GPU)
-        self.ranks_on_device = max(1, buses.count(buses[self.rank]))
         if zero1_blocks is None:
             env = os.environ.get("RMM_PEER_ZERO1_BLOCKS")
             zero1_blocks = int(env) if env else zero1_blocks_for(h, self.device.index, self.ranks_on_device)
