@@ -1,0 +1,8 @@
+# round-6: h1 (K10x fwd) and dpre1 (conv2 bwd) stored write-through from LDS: tests, phase probe, fused trace, bench
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_x3_kernels.py tests/test_rllib_precision_gpu.py tests/test_rllib_runtime_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_wt.log 2>&1 || exit $?
+timeout -k 10 200 python -u benchmarks/x3_phase_probe.py > gpurun_out/x3_phase_probe_wt.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_wt -o wt -- python3 -u bench.py --mode fused --steps 10 --warmup 2 --no-putget > gpurun_out/prof_wt.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --no-putget > gpurun_out/bench_wt.log 2>&1 || exit $?
