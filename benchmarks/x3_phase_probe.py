@@ -40,6 +40,9 @@ def main():
 
     h = require_hip()
     dev = torch.device("cuda", 0)
+    # the probe buffer is a kernel argument: set it before the learner captures its SGD graphs
+    ts = torch.zeros(7 * 1024 * 16, dtype=torch.int64, device=dev)
+    h.x3_probe_set(ts.data_ptr())
     torch.manual_seed(0)
     L = PPOLearner(VisionNetwork(4), {"sgd_minibatch_size": a.mbs, "num_sgd_iter": 10, "train_batch_size": 5000,
                                       "compute_dtype": "fp32"}, device=dev)
@@ -48,13 +51,9 @@ def main():
     obs = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=g).to(dev)
     cols = torch.cat([torch.randn(N, A, generator=g), torch.randn(N, 1, generator=g) - 1.4,
                       torch.randn(N, 2, generator=g), torch.randint(0, A, (N, 1), generator=g).float()], 1).to(dev)
-    for _ in range(2):
-        L._update_tables(obs, cols, A)
-    torch.cuda.synchronize()
-    ts = torch.zeros(7 * 1024 * 16, dtype=torch.int64, device=dev)
-    h.x3_probe_set(ts.data_ptr())
     try:
-        L._update_tables(obs, cols, A)
+        for _ in range(3):  # every update rewrites the rows: the last one's last SGD step is read
+            L._update_tables(obs, cols, A)
         torch.cuda.synchronize()
     finally:
         h.x3_probe_set(0)

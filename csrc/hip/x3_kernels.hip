@@ -55,15 +55,16 @@ using trunk::WeightRegs;
 using trunk::WStrides;
 
 // ---------------------------------------------------------------- phase probe (opt-in, x3_probe_set)
-// When a buffer is set, thread 0 of every workgroup stores the 100 MHz real-time counter at the kernels'
-// phase boundaries: ts[(kernel * 1024 + workgroup) * 16 + slot] (benchmarks/x3_phase_probe.py reads it).
-// Unset (the default) a probe site costs one scalar-pointer test.
-__device__ uint64_t* g_x3_ts = nullptr;
+// When a buffer is set (before the learner captures its SGD graphs: the pointer is a kernel argument), thread 0
+// of every workgroup stores the 100 MHz real-time counter at the kernels' phase boundaries:
+// ts[(kernel * 1024 + workgroup) * 16 + slot] (benchmarks/x3_phase_probe.py reads it). A null argument costs
+// one scalar test per site (a device-global pointer instead cost a load whose wait drained every memory op
+// in flight at each site).
+uint64_t* g_x3_probe = nullptr;  // host side: the buffer the launchers pass
 enum : int { TS_FWD = 0, TS_C2B = 1, TS_C1W = 2, TS_K12 = 3, TS_RED = 4, TS_K13L = 5, TS_K15 = 6 };
-__device__ __forceinline__ void x3_ts(int k, int slot) {
-  uint64_t* p = g_x3_ts;
-  if (p != nullptr && threadIdx.x == 0 && blockIdx.x < 1024 && slot < 16)
-    p[(int64_t(k) * 1024 + blockIdx.x) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+__device__ __forceinline__ void x3_ts(uint64_t* ts, int k, int slot) {
+  if (ts != nullptr && threadIdx.x == 0 && blockIdx.x < 1024 && slot < 16)
+    ts[(int64_t(k) * 1024 + blockIdx.x) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ================================================================ K10x forward
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     int64_t B, CPair W1, WStrides w1, CPair b1, CPair W2, WStrides w2, CPair b2, Pair h1_out, Pair h2_out,
     uint8_t* push_stack, const uint8_t* __restrict__ push_new, uint8_t* push_rows, const int64_t* __restrict__ push_t,
     const int64_t* gate, int64_t gate_want, int* gate_err, int gate_parts, int gate_timeout_ms,
-    const float* __restrict__ cols, float* __restrict__ cols_out, int ncols) {
+    const float* __restrict__ cols, float* __restrict__ cols_out, int ncols, uint64_t* __restrict__ ts) {
   __shared__ __attribute__((aligned(16))) unsigned short img[FIMG];
   __shared__ __attribute__((aligned(16))) unsigned short h1h[H1P_ELEMS];
   __shared__ __attribute__((aligned(16))) unsigned short h1l[H1P_ELEMS];
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   const int64_t G = gridDim.x;
   const int64_t* idx = trunk::window(idx0, ctr, period, B);
   constexpr int64_t FB = C0 * H0 * H0;
-  x3_ts(TS_FWD, 0);
+  x3_ts(ts, TS_FWD, 0);
 
   // prologue: weight loads (L2), then the first frame's HBM loads, then zeroing and staging
   WeightRegs<NTF, C1, C0, 8> r1h, r1l;
@@ -167,10 +168,17 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     }
     __syncthreads();
   }
+  // source rows are loaded one frame AHEAD and the loss-column gather one frame ahead too: a load issued
+  // after a frame's h1 / h2 stores is waited for with vmcnt, which also drains those stores (vmcnt counts
+  // stores on gfx950), and the next frame's loads could not leave until it had
+  const bool gcols = cols_out != nullptr && int(threadIdx.x) < ncols;
+  int64_t src = idx ? idx[b] : b;
   if (push_stack)
     trunk::frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
   else
-    trunk::frame_issue<NTF>(obs + (idx ? idx[b] : b) * FB, fr);
+    trunk::frame_issue<NTF>(obs + src * FB, fr);
+  float cval = gcols ? cols[src * ncols + threadIdx.x] : 0.f;
+  src = b + G < B ? (idx ? idx[b + G] : b + G) : 0;  // the next frame's source row
   const float bias1 = join(b1, r), bias2[2] = {join(b2, r), join(b2, 16 + r)};
   zero_image_border(img);
   trunk::zero_lds(h1h, H1P_ELEMS * 2);
@@ -186,7 +194,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   // nt = wave & 1 never changes) — read them from LDS once (128 VGPRs) instead of 2 of every 3 (conv1) /
   // 4 (conv2) LDS reads per MFMA group
   __syncthreads();  // weights staged
-  x3_ts(TS_FWD, 1);
+  x3_ts(ts, TS_FWD, 1);
   bf16x8 w1fh[8], w1fl[8], w2fh[8], w2fl[8];
   {
     const int nt = wave & 1;
@@ -203,21 +211,28 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   for (; b < B; b += G) {
     // the frame's PPO loss columns, gathered through the same index window, so the loss kernel (K15x)
     // reads its row directly instead of a step counter -> index -> row chain of dependent loads
-    if (cols_out != nullptr && int(threadIdx.x) < ncols)
-      cols_out[b * ncols + threadIdx.x] = cols[(idx ? idx[b] : b) * ncols + threadIdx.x];
+    if (gcols) cols_out[b * ncols + threadIdx.x] = cval;
     frame_image_store<NTF>(fr, img);
     __syncthreads();  // image (+ first frame: border / h1 zeros, weights); the previous conv2 is done
     const int fi = int((b - blockIdx.x) / G);
-    x3_ts(TS_FWD, 2 + 3 * fi);
-    if (b + G < B) trunk::frame_issue<NTF>(obs + (idx ? idx[b + G] : b + G) * FB, fr);  // in flight meanwhile
+    x3_ts(ts, TS_FWD, 2 + 3 * fi);
+    if (b + G < B) {  // next frame in flight meanwhile; the one after's source row issued before any store
+      trunk::frame_issue<NTF>(obs + src * FB, fr);
+      if (gcols) cval = cols[src * ncols + threadIdx.x];
+      src = b + 2 * G < B ? (idx ? idx[b + 2 * G] : b + 2 * G) : 0;
+    }
 
     // ---- conv1: M = 441 positions (28 tiles) x N = 16 x K = 256 (k = ky, kx, ci); frame exact -> 2 MFMAs
     for (int mt = wave; mt < 28; mt += NTF / 64) {
       const int p = min(mt * 16 + r, NP1 - 1);
       const int oy = p / H1, ox = p - oy * H1;
       Acc acc = acc0();
+      bf16x8 av[8];  // the tile's 8 fragment reads before its MFMAs: one LDS wait instead of four
 #pragma unroll
-      for (int s = 0; s < 8; s++) mma2a(acc, ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]), w1fh[s], w1fl[s]);
+      for (int s = 0; s < 8; s++) av[s] = ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 8; s++) mma2a(acc, av[s], w1fh[s], w1fl[s]);
       const f32x4 t = total(acc);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -239,7 +254,7 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       }
     }
     __syncthreads();
-    x3_ts(TS_FWD, 3 + 3 * fi);
+    x3_ts(ts, TS_FWD, 3 + 3 * fi);
 
     // ---- conv2: 8 M-tiles x 2 N-tiles = 16 jobs over the waves, K = 256 (pixel pp = 2s + (g>>1), ci half g&1)
     static_assert(NTF / 64 % 2 == 0, "a wave's conv2 N tile (job & 1) must not change");
@@ -249,10 +264,17 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       const int oy = q / H2, ox = q - oy * H2;
       Acc acc = acc0();
 #pragma unroll
-      for (int s = 0; s < 8; s++) {
-        const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
-        const int ao = ((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1);
-        mma3(acc, ld8(&h1h[ao]), ld8(&h1l[ao]), w2fh[s], w2fl[s]);
+      for (int s0 = 0; s0 < 8; s0 += 4) {  // 4 k-steps' fragment reads (8) before their MFMAs
+        bf16x8 ah[4], al[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int pp = 2 * (s0 + j) + (g >> 1), ky = pp >> 2, kx = pp & 3;
+          const int ao = ((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1);
+          ah[j] = ld8(&h1h[ao]), al[j] = ld8(&h1l[ao]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) mma3(acc, ah[j], al[j], w2fh[s0 + j], w2fl[s0 + j]);
       }
       const f32x4 t = total(acc);
 #pragma unroll
@@ -261,9 +283,9 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
         if (qq < NP2) store1(h2_out, (b * NP2 + qq) * C2 + nt * 16 + r, fmaxf(t[i] + bias2[nt], 0.f));
       }
     }
-    x3_ts(TS_FWD, 4 + 3 * fi);
+    x3_ts(ts, TS_FWD, 4 + 3 * fi);
   }
-  x3_ts(TS_FWD, 15);
+  x3_ts(ts, TS_FWD, 15);
 }
 
 // ================================================================ K10x backward, launch 1: conv2
@@ -299,7 +321,8 @@ __device__ __forceinline__ void b1_issue(int64_t bb, CPair h1, const unsigned sh
 __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStrides w2, CPair h1,
                                                       const unsigned short* __restrict__ h2hi, CPair dh2,
                                                       Pair dpre1, float* __restrict__ partial,
-                                                      int dbg /* timing probes: bit 1 skips dW2, bit 2 dh1 */) {
+                                                      int dbg /* timing probes: bit 1 skips dW2, bit 2 dh1 */,
+                                                      uint64_t* __restrict__ ts) {
   __shared__ __attribute__((aligned(16))) unsigned short h1s[2 * H1P_ELEMS];      // hi plane, lo plane
   __shared__ __attribute__((aligned(16))) unsigned short dp2[2 * D2W * D2W * C2];   // [plane][oy*12+ox][co2]
   __shared__ __attribute__((aligned(16))) unsigned short dp2t[2 * C2 * DP2_PITCH];  // [plane][co2][kperm(q)]
@@ -315,7 +338,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   constexpr int DPL = D2W * D2W * C2, DTL = C2 * DP2_PITCH;
-  x3_ts(TS_C2B, 0);
+  x3_ts(ts, TS_C2B, 0);
 
   WeightRegs<NTB, C2, C1, 4> wrh, wrl;
   trunk::weight_issue(W2.hi, w2, wrh);
@@ -352,7 +375,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
   for (int i = 0; i < 2; i++) aw2[0][i] = aw2[1][i] = acc0();
   float db1 = 0.f, db2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   __syncthreads();
-  x3_ts(TS_C2B, 1);
+  x3_ts(ts, TS_C2B, 1);
 
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
     const int fi = int((b - blockIdx.x) / gridDim.x);
@@ -385,7 +408,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
       *reinterpret_cast<u16x8*>(&dp2[DPL + (oy * D2W + ox) * C2 + c0]) = ol;
     }
     __syncthreads();
-    x3_ts(TS_C2B, 2 + 4 * fi);
+    x3_ts(ts, TS_C2B, 2 + 4 * fi);
     if (b + gridDim.x < B) b1_issue(b + gridDim.x, h1, h2hi, dh2, R);  // next frame: in flight through P1
 
     // ---- P1a: dW2[co2][k = (ky, kx, ci)] += Σ_q dpre2[q][co2] · h1[2oy+ky][2ox+kx][ci]
@@ -423,38 +446,65 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
         mma3(aw2[1][i], a1h, a1l, as_bf(bh), as_bf(bl));
       }
     }
-    x3_ts(TS_C2B, 3 + 4 * fi);
+    x3_ts(ts, TS_C2B, 3 + 4 * fi);
     // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 -> dpre1 (HBM), db1
-    for (int mt = half; mt * 16 < ((dbg & 2) ? 0 : ncls); mt += 2) {
-      const int m = min(mt * 16 + r, ncls - 1);
-      const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
-      Acc acc = acc0();
+    // Every LDS read of a pass (the tiles' A fragments and their ReLU-mask words) is issued before the first
+    // MFMA, so the pass waits out ONE LDS round trip; with the reads interleaved the loop waited ~8 round trips
+    // per 16-row tile (3.4 us per frame, profiles/x3_phases_r6.txt). P1B_U tiles (mt, mt + 2, ..) per pass;
+    // same tile order, so db1 sums in the same order.
+    constexpr int P1B_U = 1;
+    for (int mt0 = half; mt0 * 16 < ((dbg & 2) ? 0 : ncls); mt0 += 2 * P1B_U) {
+      bf16x8 ah[P1B_U][4], al[P1B_U][4];
+      unsigned short hm[P1B_U][4];
+      int qo[P1B_U][4];
 #pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
-        const int o = (oy * D2W + ox) * C2 + 8 * g;
-        mma3(acc, ld8(&dp2[o]), ld8(&dp2[DPL + o]), wth[t], wtl[t]);
-      }
-      const f32x4 tt = total(acc);
+      for (int u = 0; u < P1B_U; u++) {
+        const int mt = mt0 + 2 * u;  // a tile past the class is computed on clamped rows and never stored
+        const int m = min(mt * 16 + r, ncls - 1);
+        const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int mm = mt * 16 + 4 * g + i;
-        if (mm < ncls) {
-          const int aa = int((uint32_t(mm) * cdiv) >> 16), cc = mm - aa * ncol;
+        for (int t = 0; t < 4; t++) {
+          const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
+          const int o = (oy * D2W + ox) * C2 + 8 * g;
+          ah[u][t] = ld8(&dp2[o]);
+          al[u][t] = ld8(&dp2[DPL + o]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int mm = mt * 16 + 4 * g + i, mc = min(mm, ncls - 1);
+          const int aa = int((uint32_t(mc) * cdiv) >> 16), cc = mc - aa * ncol;
           const int y = 2 * aa + py, x = 2 * cc + px;
-          const unsigned short hv = h1hs[((y + 2) * P1 + (x + 2)) * C1 + r];
-          const float d = (hv != 0 && !(hv & 0x8000)) ? tt[i] : 0.f;
-          unsigned short dh, dl;
-          split(d, dh, dl);
-          db1 += bf2f(dh) + bf2f(dl);
-          const int lo_ = (y * H1 + x) * C1 + r;
-          dq[lo_] = dh;
-          dq[NP1 * C1 + lo_] = dl;
+          hm[u][i] = h1hs[((y + 2) * P1 + (x + 2)) * C1 + r];
+          qo[u][i] = mm < ncls ? (y * H1 + x) * C1 + r : -1;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep every read above in front of the MFMAs
+      Acc acc[P1B_U];
+#pragma unroll
+      for (int u = 0; u < P1B_U; u++) acc[u] = acc0();
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < P1B_U; u++) mma3(acc[u], ah[u][t], al[u][t], wth[t], wtl[t]);
+#pragma unroll
+      for (int u = 0; u < P1B_U; u++) {
+        const f32x4 tt = total(acc[u]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          if (qo[u][i] >= 0) {
+            const unsigned short hv = hm[u][i];
+            const float d = (hv != 0 && !(hv & 0x8000)) ? tt[i] : 0.f;
+            unsigned short dh, dl;
+            split(d, dh, dl);
+            db1 += bf2f(dh) + bf2f(dl);
+            dq[qo[u][i]] = dh;
+            dq[NP1 * C1 + qo[u][i]] = dl;
+          }
         }
       }
     }
     __syncthreads();  // tiles free for the next frame; dq complete
-    x3_ts(TS_C2B, 4 + 4 * fi);
+    x3_ts(ts, TS_C2B, 4 + 4 * fi);
     {  // dpre1 pair of frame b: 2 x 441 x 16 bf16 -> HBM in 16-B vectors
       constexpr int NV = NP1 * C1 / 8;  // vectors per plane
       const int64_t go = b * NP1 * C1;
@@ -464,7 +514,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
         *reinterpret_cast<u16x8*>(&(pl ? dpre1.lo : dpre1.hi)[go + 8 * vv]) = d;
       }
     }
-    x3_ts(TS_C2B, 5 + 4 * fi);
+    x3_ts(ts, TS_C2B, 5 + 4 * fi);
   }
 
   float* out = partial + int64_t(blockIdx.x) * PART2;
@@ -506,7 +556,7 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
     for (int w = 0; w < 8; w++) s += red[w * 16 + threadIdx.x];
     out[C2 * 256 + C2 + threadIdx.x] = s;
   }
-  x3_ts(TS_C2B, 15);
+  x3_ts(ts, TS_C2B, 15);
 }
 
 // ================================================================ K10x backward, launch 2: conv1 dW1
@@ -523,7 +573,8 @@ constexpr int B2_N = NP1 * 2, B2_PER = (B2_N + NTB - 1) / NTB;  // 882 x 16 B pe
 __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restrict__ obs,
                                                         const int64_t* __restrict__ idx0,
                                                         const int64_t* __restrict__ ctr, int64_t period, int64_t B,
-                                                        CPair dpre1, float* __restrict__ partial) {
+                                                        CPair dpre1, float* __restrict__ partial,
+                                                        uint64_t* __restrict__ ts) {
   __shared__ __attribute__((aligned(16))) unsigned short st[trunk::ST_ELEMS];  // space-to-depth frame (exact)
   __shared__ __attribute__((aligned(16))) unsigned short dp[4 * DB_B];        // [hi b0][hi b1][lo b0][lo b1]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -531,8 +582,13 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
   const int64_t* idx = trunk::window(idx0, ctr, period, B);
   FrameRegs<NTB> fr;
   u16x8 vh[B2_PER], vl[B2_PER];
+  // frame bb's source row src; the NEXT frame's row is loaded here too, before anything waits: resolving it
+  // when that frame is issued cost a round trip with the wave idle before its MFMAs
+  int64_t src = int64_t(blockIdx.x) < B ? (idx ? idx[blockIdx.x] : blockIdx.x) : 0;
   auto issue = [&](int64_t bb) {
-    trunk::frame_issue<NTB>(obs + (idx ? idx[bb] : bb) * (C0 * H0 * H0), fr);
+    trunk::frame_issue<NTB>(obs + src * (C0 * H0 * H0), fr);
+    const int64_t nb = bb + gridDim.x;
+    src = nb < B ? (idx ? idx[nb] : nb) : 0;
 #pragma unroll
     for (int k = 0; k < B2_PER; k++) {
       const int v = min(int(threadIdx.x) + NTB * k, B2_N - 1);
@@ -541,7 +597,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
       vl[k] = *reinterpret_cast<const u16x8*>(&dpre1.lo[o]);
     }
   };
-  x3_ts(TS_C1W, 0);
+  x3_ts(ts, TS_C1W, 0);
   if (int64_t(blockIdx.x) < B) issue(blockIdx.x);
   trunk::zero_lds(st, trunk::ST_ELEMS * 2);
   trunk::zero_lds(dp, 4 * DB_B * 2);
@@ -569,21 +625,37 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
     }
     __syncthreads();
     const int fi = int((b - blockIdx.x) / gridDim.x);
-    x3_ts(TS_C1W, 1 + 2 * fi);
+    x3_ts(ts, TS_C1W, 1 + 2 * fi);
     if (b + gridDim.x < B) issue(b + gridDim.x);
     {
       const int cb = wave & 3, a = wave >> 2;
       const unsigned short* sa = st + trunk::st_chan(16 * cb + r) + 8 * g;
       const unsigned short* d0 = dp + r * DB_CP + (1 - a) * ST_W + 8 * g;
+      // KB k-steps per batch: the batch's 5 KB fragment reads are issued before its MFMAs (one LDS wait per
+      // batch; the scheduler had put a full wait in front of every k-step's pair of MFMAs)
+      constexpr int KB = 4;
 #pragma unroll
-      for (int s = 0; s < KSTEPS1; s++) {
-        const bf16x8 av = ld8(sa + 32 * s);
-        mma2a(aw[0], av, ld8(d0 + 32 * s), ld8(d0 + 2 * DB_B + 32 * s));
-        mma2a(aw[1], av, ld8(d0 + DB_B + 32 * s), ld8(d0 + 3 * DB_B + 32 * s));
+      for (int s0 = 0; s0 < KSTEPS1; s0 += KB) {
+        bf16x8 av[KB], f[KB][4];
+#pragma unroll
+        for (int j = 0; j < KB; j++) {
+          const int s = min(s0 + j, KSTEPS1 - 1);
+          av[j] = ld8(sa + 32 * s);
+          f[j][0] = ld8(d0 + 32 * s), f[j][1] = ld8(d0 + 2 * DB_B + 32 * s);
+          f[j][2] = ld8(d0 + DB_B + 32 * s), f[j][3] = ld8(d0 + 3 * DB_B + 32 * s);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < KB; j++) {
+          if (s0 + j < KSTEPS1) {
+            mma2a(aw[0], av[j], f[j][0], f[j][1]);
+            mma2a(aw[1], av[j], f[j][2], f[j][3]);
+          }
+        }
       }
     }
     __syncthreads();
-    x3_ts(TS_C1W, 2 + 2 * fi);
+    x3_ts(ts, TS_C1W, 2 + 2 * fi);
   }
   // tile b holds D[m = 4g+e][co = r], channel c = 16cb + m -> ry = cb, rx = g, ci = e; ky = 4a+ry, kx = 4b+rx
   float* out = partial + int64_t(blockIdx.x) * PART1;
@@ -594,7 +666,7 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
 #pragma unroll
     for (int e = 0; e < 4; e++) out[r * 256 + ky * 32 + kx * 4 + e] = t[e] * (1.0f / 255.0f);
   }
-  x3_ts(TS_C1W, 15);
+  x3_ts(ts, TS_C1W, 15);
 }
 
 // ================================================================ K10x reduce
@@ -627,9 +699,9 @@ __device__ __forceinline__ float* trunk_grad_dst_f32(int e, float* dW1, WStrides
 __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict__ part1, int G1,
                                                          const float* __restrict__ part2, int G2, float* dW1,
                                                          WStrides w1, float* db1, float* dW2, WStrides w2, float* db2,
-                                                         const X3Adam xa, int nred) {
+                                                         const X3Adam xa, int nred, uint64_t* __restrict__ ts) {
   __shared__ float red[RED_SLICES][64];
-  x3_ts(TS_RED, 0);
+  x3_ts(ts, TS_RED, 0);
   if (int(blockIdx.x) >= nred) {  // Adam workgroups: K6's vector pass over the dense + heads range
     const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
     const int64_t o = xa.n_trunk;
@@ -638,7 +710,7 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     adam_span<float, true, 2>(xa.master + o, xa.m1 + o, xa.m2 + o, xa.grad + o,
                               static_cast<__hip_bfloat16*>(xa.whi) + o, xa.grad_scale, ac, tid, nthr, xa.n - o,
                               static_cast<__hip_bfloat16*>(xa.wlo) + o, xa.grad2);
-    x3_ts(TS_RED, 15);
+    x3_ts(ts, TS_RED, 15);
     x3_tail_bump(xa);
     return;
   }
@@ -692,7 +764,7 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
       static_cast<unsigned short*>(xa.wlo)[ai] = lo;
     }
   }
-  x3_ts(TS_RED, 15);
+  x3_ts(ts, TS_RED, 15);
   if (xa.master) x3_tail_bump(xa);
 }
 
@@ -721,9 +793,7 @@ static void check_pair(const X3In& p, const char* what) {
   if ((p.hi == nullptr) != (p.lo == nullptr)) throw std::invalid_argument(std::string(what) + ": hi and lo planes");
 }
 
-void x3_probe_set(uint64_t* ts) {
-  RMM_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(x3::g_x3_ts), &ts, sizeof(ts)));
-}
+void x3_probe_set(uint64_t* ts) { x3::g_x3_probe = ts; }
 
 int x3_trunk_fwd_groups(int64_t B) { return int(std::max<int64_t>(1, std::min<int64_t>(B, 256))); }
 
@@ -740,7 +810,7 @@ void x3_trunk_fwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
     throw std::invalid_argument("x3_trunk_fwd: cols and cols_out together, 1 <= ncols <= 512");
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(x3_trunk_fwd_groups(B))), dim3(x3::NTF), 0, stream, obs, idx,
                      ctr, period, B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), pp(h1), pp(h2), nullptr,
-                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1, 0, cols, cols_out, ncols);
+                     nullptr, nullptr, nullptr, nullptr, int64_t(0), nullptr, 1, 0, cols, cols_out, ncols, x3::g_x3_probe);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -761,7 +831,7 @@ void x3_trunk_fwd_push(uint8_t* stack, const uint8_t* new_frames, uint8_t* rows,
   hipLaunchKernelGGL(x3::k_trunk_fwd_x3, dim3(uint32_t(B)), dim3(x3::NTF), 0, stream, nullptr, nullptr, nullptr,
                      int64_t(1), B, cp(W1), wsx(w1s), cp(b1), cp(W2), wsx(w2s), cp(b2), x3::Pair{}, pp(h2), stack,
                      new_frames, rows, t_ptr, gate, gate_want, gate_err, gate_parts, gate_timeout_ms, nullptr,
-                     nullptr, 0);
+                     nullptr, 0, nullptr);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -816,17 +886,17 @@ void x3_trunk_bwd(const uint8_t* obs, const int64_t* idx, const int64_t* ctr, in
   float* p2 = partial;                              // conv2 launch partials [G2][PART2]
   float* p1 = partial + int64_t(G2) * x3::PART2;    // conv1 launch partials [G1][PART1]
   hipLaunchKernelGGL(x3::k_conv2_bwd_x3, dim3(uint32_t(G2)), dim3(x3::NTB), 0, stream, B, cp(W2), wsx(w2s), cp(h1),
-                     static_cast<const unsigned short*>(h2hi), cp(dh2), pp(dpre1), p2, 0);
+                     static_cast<const unsigned short*>(h2hi), cp(dh2), pp(dpre1), p2, 0, x3::g_x3_probe);
   RMM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(x3::k_conv1_wgrad_x3, dim3(uint32_t(G1)), dim3(x3::NTB), 0, stream, obs, idx, ctr, period, B,
                      x3::CPair{static_cast<const unsigned short*>(dpre1.hi), static_cast<const unsigned short*>(dpre1.lo)},
-                     p1);
+                     p1, x3::g_x3_probe);
   RMM_HIP_CHECK(hipGetLastError());
   const int nred = (x3::PARTX + 63) / 64;
   // Adam workgroups: two groups of 4 elements per lane (K6's default unroll)
   const int nadam = xa.master && !dense_separate ? x3_dense_adam_groups(xa) : 0;
   hipLaunchKernelGGL(x3::k_trunk_reduce_x3, dim3(nred + nadam), dim3(512), 0, stream, p1, G1, p2, G2, dW1, wsx(w1s),
-                     db1, dW2, wsx(w2s), db2, xa, nred);
+                     db1, dW2, wsx(w2s), db2, xa, nred, x3::g_x3_probe);
   RMM_HIP_CHECK(hipGetLastError());
 }
 
@@ -958,9 +1028,9 @@ constexpr int KL_T = 64, KL_PITCH = 72, KL_PLANE = KL_T * KL_PITCH;  // elements
 constexpr int KL_STAGE = 4 * KL_PLANE;  // A hi, A lo, B hi, B lo
 constexpr int KL_D = 4;                 // register-ring depth (stages of global loads in flight)
 __global__ __launch_bounds__(256) void k_dense_fwd_lds_x3(CPair x, CPair w, int64_t M, int64_t K, int N, int S,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, uint64_t* __restrict__ ts) {
   __shared__ __attribute__((aligned(16))) unsigned short t[2 * KL_STAGE];
-  x3_ts(TS_K13L, 0);
+  x3_ts(ts, TS_K13L, 0);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4, wm = wave >> 1, wn = wave & 1;
   const int nt = N / KL_T;
@@ -1068,7 +1138,7 @@ __global__ __launch_bounds__(256) void k_dense_fwd_lds_x3(CPair x, CPair w, int6
         if (row < M) out[row * N + 16 * j] = tt[e];
       }
     }
-  x3_ts(TS_K13L, 15);
+  x3_ts(ts, TS_K13L, 15);
 }
 
 // consumer prologue: a lane's 4 hidden values of row rr = ReLU(Σ_s part[s] + b) in fp32 (slice order).
@@ -1134,9 +1204,10 @@ __global__ __launch_bounds__(256) void k_heads_ppo_x3(const float* __restrict__ 
                                                       const float* __restrict__ coef, float* __restrict__ acc,
                                                       const float* __restrict__ gout, int64_t M, Pair dz, Pair dpre,
                                                       Pair hid, const int64_t* __restrict__ cidx,
-                                                      const int64_t* __restrict__ ctr, int64_t period, int acc_slab) {
+                                                      const int64_t* __restrict__ ctr, int64_t period, int acc_slab,
+                                                      uint64_t* __restrict__ ts) {
   constexpr int A = A1 - 1;
-  x3_ts(TS_K15, 0);
+  x3_ts(ts, TS_K15, 0);
   // slab mode: this workgroup's running sums, loaded now (in flight with everything else), rewritten at the end
   float* srow = acc + int64_t(blockIdx.x) * 8;
   const float sold = (acc && acc_slab && threadIdx.x < 6) ? srow[threadIdx.x] : 0.f;
@@ -1205,7 +1276,7 @@ __global__ __launch_bounds__(256) void k_heads_ppo_x3(const float* __restrict__ 
     else
       atomicAdd(&acc[threadIdx.x], t);
   }
-  x3_ts(TS_K15, 15);
+  x3_ts(ts, TS_K15, 15);
 }
 
 // ---- K16x: heads + Gumbel-max sampling + rollout-row stores (+ step advance), fp32 head row
@@ -1608,19 +1679,19 @@ __global__ __launch_bounds__(NT) void k_dense_heads_bwd_x3(CPair dz, CPair y, CP
                                                            float* __restrict__ db, float* __restrict__ dwh,
                                                            float* __restrict__ dbh, int rs, float* __restrict__ dw2,
                                                            float* __restrict__ db2, float* __restrict__ dwh2,
-                                                           float* __restrict__ dbh2) {
+                                                           float* __restrict__ dbh2, uint64_t* __restrict__ ts) {
   __shared__ __attribute__((aligned(16))) unsigned short lds[K12X_LDS];
   // grid: rs x K / JB column workgroups, then rs x H / HQ head workgroups
   const int NJ = int(K / JB), b = blockIdx.x, NC = int((M + MC - 1) / MC);
   const bool head = b >= NJ * rs;
   const int i = head ? b - NJ * rs : b, per = head ? H / HQ : NJ, part = i / per, j = i - part * per;
   const int c0 = NC * part / rs, c1 = NC * (part + 1) / rs;
-  x3_ts(TS_K12, 0);
+  x3_ts(ts, TS_K12, 0);
   if (head)
     k12x_head<A1>(dz, y, dpre, M, part ? db2 : db, part ? dwh2 : dwh, part ? dbh2 : dbh, lds, j, c0, c1);
   else
     k12x_cols(x, w, dpre, M, K, int64_t(j) * JB, dx, part ? dw2 : dw, lds, c0, c1);
-  x3_ts(TS_K12, 15);
+  x3_ts(ts, TS_K12, 15);
 }
 
 }  // namespace x3
@@ -1663,7 +1734,7 @@ void x3_dense_fwd_part(X3In x, X3In w, int64_t M, int64_t K, int N, float* part,
   if (f == 0) {
     const int64_t tiles = ((M + 63) / 64) * (N / 64);
     hipLaunchKernelGGL(x3::k_dense_fwd_lds_x3, dim3(uint32_t(tiles * S)), dim3(256), 0, stream, cp(x), cp(w), M, K, N,
-                       S, part);
+                       S, part, x3::g_x3_probe);
     RMM_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -1690,7 +1761,7 @@ void x3_heads_ppo(const float* hpart, int S, X3In hb, X3In wh, X3In bh, const fl
 #define RMM_K15X(N)                                                                                               \
   case N:                                                                                                         \
     hipLaunchKernelGGL(x3::k_heads_ppo_x3<N>, grid, block, 0, stream, hpart, S, cp(hb), cp(wh), cp(bh), cols, coef, \
-                       acc, gout, M, pp(dz), pp(dpre), pp(hid), cidx, ctr, period, int(acc_slab));               \
+                       acc, gout, M, pp(dz), pp(dpre), pp(hid), cidx, ctr, period, int(acc_slab), x3::g_x3_probe); \
     break;
   switch (A1) {
     RMM_K15X(3) RMM_K15X(4) RMM_K15X(5) RMM_K15X(6) RMM_K15X(7) RMM_K15X(8) RMM_K15X(9)
@@ -1784,7 +1855,7 @@ void x3_dense_heads_bwd(X3In dz, int A1, X3In y, X3In x, X3In w, X3In dpre, int6
 #define RMM_K12X(N)                                                                                                 \
   case N:                                                                                                           \
     hipLaunchKernelGGL(x3::k_dense_heads_bwd_x3<N>, grid, block, 0, stream, cp(dz), cp(y), cp(x), cp(w), cp(dpre), M, \
-                       K, pp(dx), dw, db, dwh, dbh, rs, dw2, db2, dwh2, dbh2);                                      \
+                       K, pp(dx), dw, db, dwh, dbh, rs, dw2, db2, dwh2, dbh2, x3::g_x3_probe);                       \
     break;
   switch (A1) {
     RMM_K12X(1) RMM_K12X(2) RMM_K12X(3) RMM_K12X(4) RMM_K12X(5) RMM_K12X(6) RMM_K12X(7) RMM_K12X(8)
