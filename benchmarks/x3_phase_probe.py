@@ -6,6 +6,10 @@ LAST SGD step: each kernel's span (first workgroup start -> last workgroup end),
 kernel, the workgroup start skew, and the mean time from a workgroup's start to each probed phase boundary.
 Timestamps are the 100 MHz real-time counter (10 ns).
 
+The probe sites compile to nothing in the default build (their cost showed up in the kernels): build the
+extension with them first, and rebuild without them afterwards:
+    RMM_X3_PROBE=1 python build_native.py --force --only _hip
+
 usage: python benchmarks/x3_phase_probe.py [--mbs 500]
 """
 from __future__ import annotations

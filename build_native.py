@@ -69,7 +69,9 @@ def extensions():
     exts.append(
         _ext("_hip", ["csrc/hip/kernels.hip", "csrc/hip/rl_kernels.hip", "csrc/hip/conv_kernels.hip", "csrc/hip/dense_kernels.hip", "csrc/hip/x3_kernels.hip", "csrc/hip/shuffle_kernels.hip", "csrc/hip/ingest_kernels.hip", "csrc/hip/vtrace_kernels.hip", "csrc/hip/gpu_store.hip", "csrc/hip/peer_allreduce.hip", "csrc/hip/rollout_server.hip", "csrc/hip/rccl_comm.cc", "csrc/hip/rollout_loop.cc", "csrc/hip/hip_py.cc",
               "csrc/store/shm_store.cc"], HIPCC,
-             common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"],
+             common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"]
+             # RMM_X3_PROBE=1: the x3 kernels' phase timestamps (benchmarks/x3_phase_probe.py; build with --force)
+             + (["-DRMM_X3_PROBE"] if os.environ.get("RMM_X3_PROBE") == "1" else []),
              hip_ld, ["csrc/hip/kernels.h", "csrc/hip/gpu_store.h", "csrc/hip/rccl_comm.h", "csrc/hip/peer_allreduce.h", "csrc/hip/common.h", "csrc/store/shm_store.h",
                      "csrc/hip/rollout_loop.h", "csrc/rl/synth_env.h", "csrc/hip/trunk_device.h",
                      "csrc/hip/dense_device.h", "csrc/hip/adam_device.h", "csrc/hip/x3_device.h"]))

@@ -47,18 +47,17 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
     const int64_t nv = n >> 2;
     for (int64_t v0 = tid; v0 < nv; v0 += nthr * U) {
       float g[U][4];
-      float4 w[U], a[U], b[U], q[U];
-      // every load of the U groups is issued before any is used: an add of grad2 inside the load loop
-      // made each group wait out its gradient loads before its master / moment loads were even issued
-      // (4 serial round trips per thread instead of 1)
+      float4 w[U], a[U], b[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const int64_t v = v0 + u * nthr;
         if (v < nv) {
           const int64_t i = v << 2;
           adam_load4(grad, i, g[u]);
-          // a second partial of the same gradient (K12x row parts), added below in a fixed order
-          if (grad2) q[u] = *reinterpret_cast<const float4*>(grad2 + i);
+          if (grad2) {  // a second partial of the same gradient (K12x row parts), added in a fixed order
+            const float4 q = *reinterpret_cast<const float4*>(grad2 + i);
+            g[u][0] += q.x, g[u][1] += q.y, g[u][2] += q.z, g[u][3] += q.w;
+          }
           w[u] = *reinterpret_cast<const float4*>(master + i);
           a[u] = *reinterpret_cast<const float4*>(m1 + i);
           b[u] = *reinterpret_cast<const float4*>(m2 + i);
@@ -69,7 +68,6 @@ __device__ __forceinline__ void adam_span(float* __restrict__ master, float* __r
         const int64_t v = v0 + u * nthr;
         if (v < nv) {
           const int64_t i = v << 2;
-          if (grad2) g[u][0] += q[u].x, g[u][1] += q[u].y, g[u][2] += q[u].z, g[u][3] += q[u].w;
           w[u].x = adam_one(w[u].x, g[u][0] * grad_scale, a[u].x, b[u].x, c);
           w[u].y = adam_one(w[u].y, g[u][1] * grad_scale, a[u].y, b[u].y, c);
           w[u].z = adam_one(w[u].z, g[u][2] * grad_scale, a[u].z, b[u].z, c);
@@ -124,14 +122,9 @@ __device__ __forceinline__ void adam_span_split(float* __restrict__ master, floa
       if (v < nv) {
         const int64_t i = v << 2;
         float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int h0 = 0; h0 < rs; h0 += 4) {  // members loaded 4 at a time before any is summed (in order)
-          float4 p[4];
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            p[j] = *reinterpret_cast<const float4*>(part + k12_part_index(i, K, rs, min(h0 + j, rs - 1)));
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            if (h0 + j < rs) t.x += p[j].x, t.y += p[j].y, t.z += p[j].z, t.w += p[j].w;
+        for (int h = 0; h < rs; h++) {
+          const float4 p = *reinterpret_cast<const float4*>(part + k12_part_index(i, K, rs, h));
+          t.x += p.x, t.y += p.y, t.z += p.z, t.w += p.w;
         }
         g[u][0] = __uint_as_float(uint32_t(bf16_bits_rn(t.x)) << 16);
         g[u][1] = __uint_as_float(uint32_t(bf16_bits_rn(t.y)) << 16);

@@ -57,14 +57,17 @@ using trunk::WStrides;
 // ---------------------------------------------------------------- phase probe (opt-in, x3_probe_set)
 // When a buffer is set (before the learner captures its SGD graphs: the pointer is a kernel argument), thread 0
 // of every workgroup stores the 100 MHz real-time counter at the kernels' phase boundaries:
-// ts[(kernel * 1024 + workgroup) * 16 + slot] (benchmarks/x3_phase_probe.py reads it). A null argument costs
-// one scalar test per site (a device-global pointer instead cost a load whose wait drained every memory op
-// in flight at each site).
+// ts[(kernel * 1024 + workgroup) * 16 + slot] (benchmarks/x3_phase_probe.py reads it). The sites compile to
+// nothing unless the extension is built with RMM_X3_PROBE=1 (build_native.py): even a null-pointer test per
+// site measured +0.3 us on kernels that had only two (same-box A/B), and a device-global pointer cost a load
+// whose wait drained every memory op in flight at each site.
 uint64_t* g_x3_probe = nullptr;  // host side: the buffer the launchers pass
 enum : int { TS_FWD = 0, TS_C2B = 1, TS_C1W = 2, TS_K12 = 3, TS_RED = 4, TS_K13L = 5, TS_K15 = 6 };
 __device__ __forceinline__ void x3_ts(uint64_t* ts, int k, int slot) {
+#ifdef RMM_X3_PROBE
   if (ts != nullptr && threadIdx.x == 0 && blockIdx.x < 1024 && slot < 16)
     ts[(int64_t(k) * 1024 + blockIdx.x) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ================================================================ K10x forward
@@ -168,17 +171,10 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
     }
     __syncthreads();
   }
-  // source rows are loaded one frame AHEAD and the loss-column gather one frame ahead too: a load issued
-  // after a frame's h1 / h2 stores is waited for with vmcnt, which also drains those stores (vmcnt counts
-  // stores on gfx950), and the next frame's loads could not leave until it had
-  const bool gcols = cols_out != nullptr && int(threadIdx.x) < ncols;
-  int64_t src = idx ? idx[b] : b;
   if (push_stack)
     trunk::frame_issue_push<NTF>(push_stack + b * FB, push_new + b * (H0 * H0), fr);
   else
-    trunk::frame_issue<NTF>(obs + src * FB, fr);
-  float cval = gcols ? cols[src * ncols + threadIdx.x] : 0.f;
-  src = b + G < B ? (idx ? idx[b + G] : b + G) : 0;  // the next frame's source row
+    trunk::frame_issue<NTF>(obs + (idx ? idx[b] : b) * FB, fr);
   const float bias1 = join(b1, r), bias2[2] = {join(b2, r), join(b2, 16 + r)};
   zero_image_border(img);
   trunk::zero_lds(h1h, H1P_ELEMS * 2);
@@ -211,28 +207,21 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
   for (; b < B; b += G) {
     // the frame's PPO loss columns, gathered through the same index window, so the loss kernel (K15x)
     // reads its row directly instead of a step counter -> index -> row chain of dependent loads
-    if (gcols) cols_out[b * ncols + threadIdx.x] = cval;
+    if (cols_out != nullptr && int(threadIdx.x) < ncols)
+      cols_out[b * ncols + threadIdx.x] = cols[(idx ? idx[b] : b) * ncols + threadIdx.x];
     frame_image_store<NTF>(fr, img);
     __syncthreads();  // image (+ first frame: border / h1 zeros, weights); the previous conv2 is done
     const int fi = int((b - blockIdx.x) / G);
     x3_ts(ts, TS_FWD, 2 + 3 * fi);
-    if (b + G < B) {  // next frame in flight meanwhile; the one after's source row issued before any store
-      trunk::frame_issue<NTF>(obs + src * FB, fr);
-      if (gcols) cval = cols[src * ncols + threadIdx.x];
-      src = b + 2 * G < B ? (idx ? idx[b + 2 * G] : b + 2 * G) : 0;
-    }
+    if (b + G < B) trunk::frame_issue<NTF>(obs + (idx ? idx[b + G] : b + G) * FB, fr);  // in flight meanwhile
 
     // ---- conv1: M = 441 positions (28 tiles) x N = 16 x K = 256 (k = ky, kx, ci); frame exact -> 2 MFMAs
     for (int mt = wave; mt < 28; mt += NTF / 64) {
       const int p = min(mt * 16 + r, NP1 - 1);
       const int oy = p / H1, ox = p - oy * H1;
       Acc acc = acc0();
-      bf16x8 av[8];  // the tile's 8 fragment reads before its MFMAs: one LDS wait instead of four
 #pragma unroll
-      for (int s = 0; s < 8; s++) av[s] = ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < 8; s++) mma2a(acc, av[s], w1fh[s], w1fl[s]);
+      for (int s = 0; s < 8; s++) mma2a(acc, ld8(&img[((4 * oy + s) * P0 + 4 * ox + 2 * g) * C0]), w1fh[s], w1fl[s]);
       const f32x4 t = total(acc);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -264,17 +253,10 @@ __global__ __launch_bounds__(NTF) void k_trunk_fwd_x3(
       const int oy = q / H2, ox = q - oy * H2;
       Acc acc = acc0();
 #pragma unroll
-      for (int s0 = 0; s0 < 8; s0 += 4) {  // 4 k-steps' fragment reads (8) before their MFMAs
-        bf16x8 ah[4], al[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int pp = 2 * (s0 + j) + (g >> 1), ky = pp >> 2, kx = pp & 3;
-          const int ao = ((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1);
-          ah[j] = ld8(&h1h[ao]), al[j] = ld8(&h1l[ao]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; j++) mma3(acc, ah[j], al[j], w2fh[s0 + j], w2fl[s0 + j]);
+      for (int s = 0; s < 8; s++) {
+        const int pp = 2 * s + (g >> 1), ky = pp >> 2, kx = pp & 3;
+        const int ao = ((2 * oy + ky) * P1 + (2 * ox + kx)) * C1 + 8 * (g & 1);
+        mma3(acc, ld8(&h1h[ao]), ld8(&h1l[ao]), w2fh[s], w2fl[s]);
       }
       const f32x4 t = total(acc);
 #pragma unroll
@@ -448,58 +430,31 @@ __global__ __launch_bounds__(NTB) void k_conv2_bwd_x3(int64_t B, CPair W2, WStri
     }
     x3_ts(ts, TS_C2B, 3 + 4 * fi);
     // ---- P1b: dh1 for this wave's parity class, masked by h1 > 0 -> dpre1 (HBM), db1
-    // Every LDS read of a pass (the tiles' A fragments and their ReLU-mask words) is issued before the first
-    // MFMA, so the pass waits out ONE LDS round trip; with the reads interleaved the loop waited ~8 round trips
-    // per 16-row tile (3.4 us per frame, profiles/x3_phases_r6.txt). P1B_U tiles (mt, mt + 2, ..) per pass;
-    // same tile order, so db1 sums in the same order.
-    constexpr int P1B_U = 1;
-    for (int mt0 = half; mt0 * 16 < ((dbg & 2) ? 0 : ncls); mt0 += 2 * P1B_U) {
-      bf16x8 ah[P1B_U][4], al[P1B_U][4];
-      unsigned short hm[P1B_U][4];
-      int qo[P1B_U][4];
+    for (int mt = half; mt * 16 < ((dbg & 2) ? 0 : ncls); mt += 2) {
+      const int m = min(mt * 16 + r, ncls - 1);
+      const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
+      Acc acc = acc0();
 #pragma unroll
-      for (int u = 0; u < P1B_U; u++) {
-        const int mt = mt0 + 2 * u;  // a tile past the class is computed on clamped rows and never stored
-        const int m = min(mt * 16 + r, ncls - 1);
-        const int a = int((uint32_t(m) * cdiv) >> 16), c = m - a * ncol;
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
-          const int o = (oy * D2W + ox) * C2 + 8 * g;
-          ah[u][t] = ld8(&dp2[o]);
-          al[u][t] = ld8(&dp2[DPL + o]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int mm = mt * 16 + 4 * g + i, mc = min(mm, ncls - 1);
-          const int aa = int((uint32_t(mc) * cdiv) >> 16), cc = mc - aa * ncol;
-          const int y = 2 * aa + py, x = 2 * cc + px;
-          hm[u][i] = h1hs[((y + 2) * P1 + (x + 2)) * C1 + r];
-          qo[u][i] = mm < ncls ? (y * H1 + x) * C1 + r : -1;
-        }
+      for (int t = 0; t < 4; t++) {
+        const int oy = a + 1 - (t >> 1), ox = c + 1 - (t & 1);
+        const int o = (oy * D2W + ox) * C2 + 8 * g;
+        mma3(acc, ld8(&dp2[o]), ld8(&dp2[DPL + o]), wth[t], wtl[t]);
       }
-      __builtin_amdgcn_sched_barrier(0);  // keep every read above in front of the MFMAs
-      Acc acc[P1B_U];
+      const f32x4 tt = total(acc);
 #pragma unroll
-      for (int u = 0; u < P1B_U; u++) acc[u] = acc0();
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int u = 0; u < P1B_U; u++) mma3(acc[u], ah[u][t], al[u][t], wth[t], wtl[t]);
-#pragma unroll
-      for (int u = 0; u < P1B_U; u++) {
-        const f32x4 tt = total(acc[u]);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          if (qo[u][i] >= 0) {
-            const unsigned short hv = hm[u][i];
-            const float d = (hv != 0 && !(hv & 0x8000)) ? tt[i] : 0.f;
-            unsigned short dh, dl;
-            split(d, dh, dl);
-            db1 += bf2f(dh) + bf2f(dl);
-            dq[qo[u][i]] = dh;
-            dq[NP1 * C1 + qo[u][i]] = dl;
-          }
+      for (int i = 0; i < 4; i++) {
+        const int mm = mt * 16 + 4 * g + i;
+        if (mm < ncls) {
+          const int aa = int((uint32_t(mm) * cdiv) >> 16), cc = mm - aa * ncol;
+          const int y = 2 * aa + py, x = 2 * cc + px;
+          const unsigned short hv = h1hs[((y + 2) * P1 + (x + 2)) * C1 + r];
+          const float d = (hv != 0 && !(hv & 0x8000)) ? tt[i] : 0.f;
+          unsigned short dh, dl;
+          split(d, dh, dl);
+          db1 += bf2f(dh) + bf2f(dl);
+          const int lo_ = (y * H1 + x) * C1 + r;
+          dq[lo_] = dh;
+          dq[NP1 * C1 + lo_] = dl;
         }
       }
     }
@@ -582,13 +537,8 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
   const int64_t* idx = trunk::window(idx0, ctr, period, B);
   FrameRegs<NTB> fr;
   u16x8 vh[B2_PER], vl[B2_PER];
-  // frame bb's source row src; the NEXT frame's row is loaded here too, before anything waits: resolving it
-  // when that frame is issued cost a round trip with the wave idle before its MFMAs
-  int64_t src = int64_t(blockIdx.x) < B ? (idx ? idx[blockIdx.x] : blockIdx.x) : 0;
   auto issue = [&](int64_t bb) {
-    trunk::frame_issue<NTB>(obs + src * (C0 * H0 * H0), fr);
-    const int64_t nb = bb + gridDim.x;
-    src = nb < B ? (idx ? idx[nb] : nb) : 0;
+    trunk::frame_issue<NTB>(obs + (idx ? idx[bb] : bb) * (C0 * H0 * H0), fr);
 #pragma unroll
     for (int k = 0; k < B2_PER; k++) {
       const int v = min(int(threadIdx.x) + NTB * k, B2_N - 1);
@@ -631,27 +581,11 @@ __global__ __launch_bounds__(NTB) void k_conv1_wgrad_x3(const uint8_t* __restric
       const int cb = wave & 3, a = wave >> 2;
       const unsigned short* sa = st + trunk::st_chan(16 * cb + r) + 8 * g;
       const unsigned short* d0 = dp + r * DB_CP + (1 - a) * ST_W + 8 * g;
-      // KB k-steps per batch: the batch's 5 KB fragment reads are issued before its MFMAs (one LDS wait per
-      // batch; the scheduler had put a full wait in front of every k-step's pair of MFMAs)
-      constexpr int KB = 4;
 #pragma unroll
-      for (int s0 = 0; s0 < KSTEPS1; s0 += KB) {
-        bf16x8 av[KB], f[KB][4];
-#pragma unroll
-        for (int j = 0; j < KB; j++) {
-          const int s = min(s0 + j, KSTEPS1 - 1);
-          av[j] = ld8(sa + 32 * s);
-          f[j][0] = ld8(d0 + 32 * s), f[j][1] = ld8(d0 + 2 * DB_B + 32 * s);
-          f[j][2] = ld8(d0 + DB_B + 32 * s), f[j][3] = ld8(d0 + 3 * DB_B + 32 * s);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < KB; j++) {
-          if (s0 + j < KSTEPS1) {
-            mma2a(aw[0], av[j], f[j][0], f[j][1]);
-            mma2a(aw[1], av[j], f[j][2], f[j][3]);
-          }
-        }
+      for (int s = 0; s < KSTEPS1; s++) {
+        const bf16x8 av = ld8(sa + 32 * s);
+        mma2a(aw[0], av, ld8(d0 + 32 * s), ld8(d0 + 2 * DB_B + 32 * s));
+        mma2a(aw[1], av, ld8(d0 + DB_B + 32 * s), ld8(d0 + 3 * DB_B + 32 * s));
       }
     }
     __syncthreads();
@@ -682,7 +616,7 @@ __device__ __forceinline__ void x3_tail_bump(const X3Adam& xa) {
   }
   last_block_bump(xa.bump, xa.nbump, xa.done);
 }
-constexpr int RED_SLICES = 8, RED_BATCH = 32;  // G <= 256 partials: one batch of loads per thread
+constexpr int RED_SLICES = 8, RED_BATCH = 16;
 __device__ __forceinline__ float* trunk_grad_dst_f32(int e, float* dW1, WStrides w1, float* db1, float* dW2,
                                                      WStrides w2, float* db2) {
   if (e < C1 * 256) {
@@ -727,13 +661,6 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     const int o = f < C2 * 256 ? f : (f < C2 * 256 + C1 ? C2 * 256 + C2 + (f - C2 * 256) : C2 * 256 + (f - C2 * 256 - C1));
     src = part2 + o, G = G2, stride = PART2;
   }
-  // the element's Adam state is loaded FIRST, with the partials behind it: every load of the workgroup is in
-  // flight at once (loaded after the partial sum, it was a second serial round trip before the update)
-  const bool upd = slice == 0 && e < PARTX && xa.master != nullptr;
-  float* dst = e < PARTX ? trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2) : nullptr;
-  const int64_t ai = upd ? dst - xa.grad : 0;
-  float am1 = 0.f, am2 = 0.f, aw = 0.f;
-  if (upd) am1 = xa.m1[ai], am2 = xa.m2[ai], aw = xa.master[ai];
   float s = 0.f;
   if (src) {
     for (int g0 = slice; g0 < G; g0 += RED_SLICES * RED_BATCH) {
@@ -751,17 +678,20 @@ __global__ __launch_bounds__(512) void k_trunk_reduce_x3(const float* __restrict
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < RED_SLICES; k++) t += red[k][c];
+    float* dst = trunk_grad_dst_f32(e, dW1, w1, db1, dW2, w2, db2);
     *dst = t;
-    if (upd) {  // the trunk gradient is final: Adam on it (same math as K6's scalar pass)
+    if (xa.master) {  // the trunk gradient is final: Adam on it (same math as K6's scalar pass)
       const AdamCoef ac = adam_coef(xa.hp, xa.step_ctr);
-      const float w = adam_one(aw, t * xa.grad_scale, am1, am2, ac);
-      xa.m1[ai] = am1;
-      xa.m2[ai] = am2;
-      xa.master[ai] = w;
+      const int64_t i = dst - xa.grad;
+      float a = xa.m1[i], b = xa.m2[i];
+      const float w = adam_one(xa.master[i], t * xa.grad_scale, a, b, ac);
+      xa.m1[i] = a;
+      xa.m2[i] = b;
+      xa.master[i] = w;
       unsigned short hi, lo;
       split(w, hi, lo);
-      static_cast<unsigned short*>(xa.whi)[ai] = hi;
-      static_cast<unsigned short*>(xa.wlo)[ai] = lo;
+      static_cast<unsigned short*>(xa.whi)[i] = hi;
+      static_cast<unsigned short*>(xa.wlo)[i] = lo;
     }
   }
   x3_ts(ts, TS_RED, 15);
