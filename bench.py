@@ -173,6 +173,17 @@ def _fused_loop(args, world, rank, local_rank, dist_backend):
     return time.perf_counter() - t0, stats
 
 
+def _worker_timing(algo):
+    """Seconds the first rollout worker has spent in sample() so far (None if it does not report it)."""
+    try:
+        import ray_memory_management_amd as ray
+
+        ws = algo.workers.remote_workers()
+        return float(ray.get(ws[0].timing.remote())["sample_s"]) if ws else None
+    except Exception:  # noqa: BLE001 - a worker class without timing()
+        return None
+
+
 def _runtime(args, n_gpus):
     """PPO through the runtime (rank 0 only). Returns (elapsed_s for K iterations, info)."""
     import ray_memory_management_amd as ray
@@ -312,15 +323,22 @@ def main():
                 algo, info = _runtime(args, n_gpus)
             except BaseException as e:  # noqa: BLE001 - report after releasing the other ranks
                 err = e
+        tw0 = _worker_timing(algo) if rank == 0 and err is None else None
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         stats = {}
+        iter_ms = []
         if rank == 0 and err is None:
             try:
                 for _ in range(args.steps):
+                    ti = time.perf_counter()
                     r = algo.train()  # learners end every update with a device sync
+                    iter_ms.append(round((time.perf_counter() - ti) * 1e3, 3))
                 stats = r["info"]["learner"]["default_policy"]["learner_stats"]
+                # per-iteration wall times (inside the timed region, one perf_counter each): the spread
+                # between iterations, reported next to the aggregate
+                info["iter_ms"] = iter_ms
                 # next iteration's samples queued behind the last update (RMM_PREFETCH_SAMPLE, shared weights)
                 info["sample_prefetch"] = getattr(algo, "_prefetched", None) is not None
             except BaseException as e:  # noqa: BLE001
@@ -328,6 +346,10 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        if tw0 is not None and err is None:  # after the timed region: mean sample() time per iteration
+            tw1 = _worker_timing(algo)
+            if tw1 is not None:
+                info["worker_sample_ms"] = round((tw1 - tw0) / max(1, args.steps) * 1e3, 3)
         if world > 1:
             import torch
 
