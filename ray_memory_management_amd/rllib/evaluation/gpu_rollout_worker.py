@@ -42,6 +42,9 @@ class GPURolloutWorker:
         s = (int(base_seed or 0) * 1000 + worker_index) & 0x7FFFFFFF
         self.device = torch.device("cuda:0")
         torch.cuda.set_device(0)
+        from ray_memory_management_amd._private.numa import pin_to_gpu
+
+        self.cpu_affinity = pin_to_gpu(0)  # the launching thread on the GPU's socket
         n = int(self.config.get("num_envs_per_worker", 1))
         self.env = GPUSyntheticAtariVectorEnv(n, self.device, num_actions=int(ec.get("num_actions", 4)),
                                               episode_len=int(ec.get("episode_len", 1000)), seed=s)
@@ -483,6 +486,11 @@ class HybridRolloutWorker(GPURolloutWorker):
         dbl = self.config.get("rollout_double_buffer", "auto")
         if os.environ.get("RMM_ROLLOUT_DOUBLE_BUFFER") is not None:  # A/B override
             dbl = os.environ["RMM_ROLLOUT_DOUBLE_BUFFER"] != "0"
+        from ray_memory_management_amd._private.numa import pin_to_gpu
+
+        # the env loop thread, the native envs' memory and the pinned frame / completion buffers (all
+        # allocated below) on the GPU's socket
+        self.cpu_affinity = pin_to_gpu(0)
         first = make_vector_env(self.config.get("env"), n, {**ec, "seed": s * 7})
         if dbl == "auto":
             dbl = getattr(first, "_native", None) is None or os.environ.get("RMM_NO_NATIVE_ROLLOUT") is not None

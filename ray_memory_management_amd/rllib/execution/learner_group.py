@@ -51,6 +51,9 @@ class LearnerActor:
 
             require_hip()  # the fused learner needs the HIP kernels: fail loudly if they are missing
             torch.cuda.set_device(idx)
+            from ray_memory_management_amd._private.numa import pin_to_gpu
+
+            self.cpu_affinity = pin_to_gpu(idx)  # CPUs local to this GPU (before any buffer is allocated)
         if world > 1 and backend == "nccl" and self.device != "cpu" and not os.environ.get("RMM_TORCH_PG_COMM"):
             # framework-owned RCCL communicator (parallel/comm.py:RcclComm): collectives enqueued on
             # the learner's own stream, capturable in graphs (torch's ProcessGroupNCCL watchdog
@@ -260,6 +263,8 @@ class LearnerActor:
         if self.device != "cpu":
             info["pci_bus_id"] = getattr(torch.cuda.get_device_properties(self.device), "pci_bus_id", None)
             info["visible_devices"] = torch.cuda.device_count()
+            aff = getattr(self, "cpu_affinity", None)  # NUMA-local pin (None: left to the OS)
+            info["cpus"] = f"{len(aff)} GPU-local" if aff else "os"
         return info
 
 

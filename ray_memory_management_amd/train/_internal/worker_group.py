@@ -49,6 +49,9 @@ class TrainWorker:
                     import torch
 
                     torch.cuda.set_device(int(dev))
+                    from ray_memory_management_amd._private.numa import pin_to_gpu
+
+                    pin_to_gpu(int(dev))  # this worker (and its data-loader children) on the GPU's socket
 
                 nparams = len(inspect.signature(train_fn).parameters)
                 out = train_fn(config) if nparams >= 1 else train_fn()
