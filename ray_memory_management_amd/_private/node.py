@@ -891,14 +891,27 @@ class Head:
             self.gcs_dirty = True
             self._event("JOBS", "INFO", "JOB_FINISHED", f"Driver pid {job.get('pid')} exited.",
                         job_id=self._hex(c.job_id), pid=job.get("pid"))
-        # kill non-detached actors of this job
+        # kill non-detached actors of this job, except those owned (directly or through other actors) by a
+        # detached actor: in the reference an actor fate-shares with its owner, and a detached owner outlives
+        # the job (e.g. Serve replicas and proxies created by its detached controller)
         for a in list(self.actors.values()):
-            if a.job_id == c.job_id and not a.detached and a.state != ACTOR_DEAD:
+            if a.job_id == c.job_id and not a.detached and a.state != ACTOR_DEAD and not self._owned_by_detached(a):
                 a.restarts_left = 0
                 self._kill_actor(a.actor_id, True, "The driver exited.")
         # release the driver's references
         if c is self.driver_conn and not self.args.persistent:
             self.running = False
+
+    def _owned_by_detached(self, a) -> bool:
+        for _ in range(64):  # owner chain: creating connection -> its worker's actor -> that actor's owner
+            w = getattr(a.owner_conn, "worker", None)
+            aid = getattr(w, "actor_id", None) if w is not None else None
+            a = self.actors.get(aid) if aid is not None else None
+            if a is None or a.state == ACTOR_DEAD:
+                return False
+            if a.detached:
+                return True
+        return False
 
     def _worker_died(self, w: WorkerRec):
         if w.state == "GONE":

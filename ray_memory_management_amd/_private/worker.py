@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import atexit
 import collections
+import contextvars
 import ctypes
 import hashlib
 import json
@@ -54,6 +55,29 @@ class _Pending:
         self.cb = cb
 
 
+# id of the actor task running in this thread / asyncio task (actors run calls on several threads or
+# coroutines at once, so one worker attribute would be wrong): read by RuntimeContext.get_task_id
+actor_task_id: "contextvars.ContextVar[Optional[bytes]]" = contextvars.ContextVar("rmm_actor_task_id", default=None)
+
+
+class _ActorCallPin:
+    """A reference to an actor (its scope key) held by one submitted call's keep-alive list until the call
+    is done; used for actor handles nested inside a call's inline arguments. Released by __del__ when the
+    call's in-flight / queued entry is dropped, whichever path drops it."""
+
+    __slots__ = ("worker", "key")
+
+    def __init__(self, worker, key: bytes):
+        self.worker, self.key = worker, key
+        worker.add_local_ref(key)
+
+    def __del__(self):
+        try:
+            self.worker.remove_local_ref(self.key)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
 class ActorConn:
     """Direct caller→actor connection with in-flight tracking (direct actor transport).
 
@@ -75,6 +99,19 @@ class ActorConn:
         self.epoch = -1
         self.connected = threading.Event()
         self.connecting = False
+        # While any call is queued or in flight the caller holds one reference to the actor, so dropping the
+        # last handle right after a call, as in ``ray.get(Actor.remote().method.remote())``, terminates the
+        # actor only once that call has run (reference python/ray/tests/test_actor.py:797
+        # test_actor_method_deletion). One ref per busy period, not per call: the submit path stays cheap.
+        self.pinned = False
+        from ray_memory_management_amd.actor import _actor_ref_key
+
+        self.scope_key = _actor_ref_key(actor_id)
+
+    def _unpin_if_idle_locked(self):
+        if self.pinned and not self.inflight and not self.queued:
+            self.pinned = False
+            self.worker.remove_local_ref(self.scope_key)
 
     def _connect(self):
         """Blocking: the head's WAIT_ACTOR answer -> a connected socket, or None (dead_error set)."""
@@ -135,6 +172,7 @@ class ActorConn:
             if s is None:
                 for spec, keep, tries in items:
                     self.worker._store_errors(spec["return_ids"], self.dead_error)
+                self._unpin_if_idle_locked()
                 return
             self.sock = s
             self.connected.set()
@@ -156,6 +194,9 @@ class ActorConn:
             if self.dead_error is not None:
                 self.worker._store_errors(spec["return_ids"], self.dead_error)
                 return
+            if not self.pinned:
+                self.pinned = True
+                self.worker.add_local_ref(self.scope_key)
             if self.sock is None or self.queued:
                 self.queued.append((spec, keep_alive, 0))
                 self._start_connect_locked()
@@ -170,6 +211,8 @@ class ActorConn:
                     with self.lock:
                         for sq in m[2]:
                             self.inflight.pop(sq, None)
+                        if not self.inflight:
+                            self._unpin_if_idle_locked()
         except (ConnectionError, OSError, EOFError):
             pass
         self._on_disconnect(s)
@@ -194,6 +237,8 @@ class ActorConn:
                 self.queued[:0] = retry
             if self.queued:
                 self._start_connect_locked()
+            else:
+                self._unpin_if_idle_locked()
 
     def _fail_inflight(self, failed):
         """In-flight calls of an actor whose process died: RayActorError, with the head's exit detail when
@@ -232,7 +277,7 @@ class CoreWorker:
         self.store = store_ext().ObjectStore.attach(store_name)
         self.worker_id = worker_id or os.urandom(16)
         self.job_id = job_id or os.urandom(4)
-        self.namespace = namespace
+        self._namespace = namespace
         self.node_id = node_id
         self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         self.sock.connect(head_socket)
@@ -603,6 +648,35 @@ class CoreWorker:
         self.exported.add(fid)
         return blob
 
+    @property
+    def namespace(self):
+        """The namespace of the job the current task belongs to (reference: a worker runs in its job's
+        namespace, so named-actor lookups inside tasks and actors resolve like the driver's). Workers
+        resolve it lazily from the head's job table."""
+        ns = self._namespace
+        if ns is None and self.mode != SCRIPT_MODE:
+            ns = self._namespace = self._job_namespace(self.job_id)
+        return ns
+
+    @namespace.setter
+    def namespace(self, ns):
+        self._namespace = ns
+
+    def enter_job(self, job_id):
+        """A task / actor of job `job_id` is about to run here: nested submissions belong to that job."""
+        if job_id is not None and job_id != self.job_id:
+            self.job_id = job_id
+            self._namespace = None
+
+    def _job_namespace(self, job_id):
+        try:
+            for j in self.request(lambda rid: (P.STATE, rid, "jobs", None)):
+                if j.get("job_id") == job_id:
+                    return j.get("namespace")
+        except Exception:  # noqa: BLE001 - head unreachable: no namespace
+            pass
+        return None
+
     def prepare_args(self, args, kwargs):
         """Returns (encoded_args, encoded_kwargs, arg_refs, keep_alive)."""
         arg_refs: List[bytes] = []
@@ -666,7 +740,8 @@ class CoreWorker:
         self.send((P.SUBMIT_TASK, spec))
         return refs
 
-    def submit_actor_task(self, actor_id: bytes, spec: dict, keep, max_task_retries: int) -> List[ObjectRef]:
+    def submit_actor_task(self, actor_id: bytes, spec: dict, keep, max_task_retries: int,
+                          arg_refs=None) -> List[ObjectRef]:
         task_id = _ids.new_task_id()
         spec["task_id"] = task_id
         nr = spec.get("num_returns", 1)
@@ -681,6 +756,10 @@ class CoreWorker:
         conn = self.actor_conns.get(actor_id)
         if conn is None:
             conn = self.actor_conns.setdefault(actor_id, ActorConn(self, actor_id, max_task_retries))
+        if arg_refs:  # refs and actor handles nested inside inline args stay alive until the call is done
+            have = {k.binary() for k in keep if isinstance(k, ObjectRef)}
+            keep = list(keep) + [_ActorCallPin(self, r) if r[:1] == b"\xaa" and r[-3:] == b"\xaa\xaa\xaa"
+                                 else ObjectRef(r) for r in arg_refs if r not in have]
         # flush ref deltas first so the actor never sees a ref the head does not know about
         self.send(None)
         conn.submit(spec, keep)
@@ -1127,6 +1206,11 @@ def wait(object_refs, *, num_returns: int = 1, timeout: Optional[float] = None, 
         raise ValueError("Invalid number of objects to return %d." % num_returns)
     if num_returns > len(object_refs):
         raise ValueError("num_returns cannot be greater than the number of objects provided.")
+    if timeout is not None and timeout < 0:
+        raise ValueError(f"The 'timeout' argument must be nonnegative. Received {timeout}")
+    for r in object_refs:
+        if not isinstance(r, ObjectRef):
+            raise TypeError(f"wait() expected a list of ray.ObjectRef, got list containing {type(r)}")
     return _require_worker().wait(object_refs, num_returns, timeout, fetch_local)
 
 
@@ -1156,6 +1240,12 @@ def cancel(object_ref: ObjectRef, *, force: bool = False, recursive: bool = True
     if _local_mode:
         return
     w = _require_worker()
+    tid = object_ref.binary()[:16]
+    for conn in list(w.actor_conns.values()):  # a call still queued / in flight to an actor
+        with conn.lock:
+            specs = [e[0] for e in conn.inflight.values()] + [e[0] for e in conn.queued]
+        if any(sp.get("task_id") == tid for sp in specs):
+            raise TypeError("ray.cancel() only supported for non-actor object refs.")
     if w.direct is not None and w.direct.cancel(object_ref.binary()[:16], force):
         return
     w.send((P.CANCEL, object_ref.binary()[:16], force, recursive))

@@ -247,6 +247,8 @@ class Executor:
                 raise RuntimeError("function blob missing")
             fn = cloudpickle.loads(blob)
             self.fns[fid] = fn
+        w.enter_job(spec.get("job_id"))
+        w.assigned_resources = spec.get("resources")
         w.current_task_id = spec["task_id"]
         w.current_task_name = spec.get("name")
         w.gpu_ids = list(info.get("gpu_ids") or [])
@@ -334,6 +336,9 @@ class Executor:
         w = self.w
         self.actor_spec = spec
         w.current_actor_id = spec["actor_id"]
+        w.enter_job(spec.get("job_id"))
+        w.actor_restart_count = int(info.get("restart") or 0)
+        w.assigned_resources = spec.get("resources")
         w.gpu_ids = list(info.get("gpu_ids") or [])
         for k, v in ((spec.get("runtime_env") or {}).get("env_vars") or {}).items():
             os.environ[str(k)] = str(v)
@@ -423,6 +428,7 @@ class Executor:
             if name == "__ray_ready__":
                 result = True
             else:
+                _w.actor_task_id.set(spec["task_id"])
                 args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
                 t_res = time.time()
                 m = getattr(self.actor, name)
@@ -478,6 +484,7 @@ class Executor:
                     self._ack(s, lock, spec["seq"])
                     os._exit(0)
                 else:
+                    _w.actor_task_id.set(spec["task_id"])
                     loop = asyncio.get_running_loop()
                     args, kwargs = await loop.run_in_executor(None, self.resolve_all, spec["args"], spec["kwargs"])
                     m = getattr(self.actor, name)

@@ -111,7 +111,7 @@ class ActorHandle:
         ea, ek, arg_refs, keep = w.prepare_args(args, kwargs)
         spec = {"method": method_name, "args": ea, "kwargs": ek, "num_returns": num_returns,
                 "concurrency_group": concurrency_group, "name": f"{self._class_name}.{method_name}"}
-        refs = w.submit_actor_task(self._actor_id, spec, keep, self._max_task_retries)
+        refs = w.submit_actor_task(self._actor_id, spec, keep, self._max_task_retries, arg_refs)
         if num_returns == 0:
             return None
         if num_returns == 1 or num_returns == "dynamic":

@@ -6,44 +6,8 @@ from typing import List, Optional
 
 from ray_memory_management_amd._private import protocol as P
 from ray_memory_management_amd._private import worker as _w
-
-
-def free(object_refs: list, local_only: bool = False):
-    """Eagerly delete objects from the store (reference ray.internal.free)."""
-    w = _w._require_worker()
-    w.store.delete([r.binary() for r in object_refs])
-
-
-def memory_summary(address=None, stats_only: bool = False, units: str = "MB", num_entries: int = 50) -> str:
-    """`ray memory` equivalent: object store usage, spilling stats and the largest objects."""
-    div = {"B": 1, "KB": 1 << 10, "MB": 1 << 20, "GB": 1 << 30}[units]
-    st = _w._state("store_stats")
-    lines = ["======== Object store statistics ========",
-             f"Object store: {st['bytes_in_use'] / div:.2f} / {st['capacity'] / div:.2f} {units} used, "
-             f"{st['num_objects']} objects",
-             f"Spilled: {st['bytes_spilled_total'] / div:.2f} {units} in {st['objects_spilled_total']} objects "
-             f"(currently {st['spilled_objects_current']} spilled, {st['spilled_bytes_current'] / div:.2f} {units})",
-             f"Restored: {st['bytes_restored_total'] / div:.2f} {units} in {st['objects_restored_total']} objects",
-             f"Fallback allocations: {st['fallback_allocs_total']} ({st['fallback_bytes_current'] / div:.2f} {units} live)"]
-    if not stats_only:
-        objs = sorted(_w._state("objects"), key=lambda o: -o["size"])[:num_entries]
-        lines.append("======== Objects (largest first) ========")
-        lines.append(f"{'object_id':42s} {'size':>12s} {'state':>10s} {'pins':>5s} {'refs':>5s}")
-        for o in objs:
-            lines.append(f"{o['object_id']:42s} {o['size'] / div:12.3f} {o['state']:>10s} {o['pin_count']:5d} "
-                         f"{o['reference_count']:5d}")
-    return "\n".join(lines)
-
-
-def global_gc():
-    """Trigger a garbage collection in every worker and driver of the cluster (reference
-    python/ray/_private/internal_api.py global_gc → raylet TriggerGlobalGC)."""
-    import gc
-
-    gc.collect()
-    w = _w.global_worker
-    if w is not None:
-        w.send((P.GLOBAL_GC,))
+from ray_memory_management_amd._private.internal_api import (free, get_store_stats, global_gc,  # noqa: F401
+                                                              memory_summary)
 
 
 def memory_pressure_stats() -> dict:

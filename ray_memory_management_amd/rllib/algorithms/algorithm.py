@@ -147,7 +147,7 @@ class Algorithm(Trainable):
                                  {"default_policy": {"learner_stats": results}}), **dict(self._counters)},
         }
         if c.evaluation_interval and (self.iteration + 1) % c.evaluation_interval == 0:
-            out["evaluation"] = self.evaluate()
+            out.update(self.evaluate())
         if self.callbacks is not None and hasattr(self.callbacks, "on_train_result"):
             self.callbacks.on_train_result(algorithm=self, result=out)
         return out
@@ -201,9 +201,11 @@ class Algorithm(Trainable):
         c = self.algo_config
         rewards, lens = RolloutWorker.evaluate_episodes(self.get_policy(), self._env_creator, c.env, c.env_config,
                                                         int(c.evaluation_duration), seed=c.seed)
-        return {"episode_reward_mean": float(np.mean(rewards)), "episode_reward_max": float(np.max(rewards)),
-                "episode_reward_min": float(np.min(rewards)), "episode_len_mean": float(np.mean(lens)),
-                "episodes_this_iter": len(rewards)}
+        # reference rllib/algorithms/algorithm.py evaluate(): metrics under the "evaluation" key
+        return {"evaluation": {"episode_reward_mean": float(np.mean(rewards)),
+                               "episode_reward_max": float(np.max(rewards)),
+                               "episode_reward_min": float(np.min(rewards)), "episode_len_mean": float(np.mean(lens)),
+                               "episodes_this_iter": len(rewards)}}
 
     def get_policy(self, policy_id: str = "default_policy"):
         if getattr(self, "_multi_agent", False):

@@ -222,8 +222,8 @@ class DT(Algorithm):
                 S.append(np.asarray(o, np.float32))
                 R.append(R[-1] - r)
             rets.append(ret)
-        return {"episode_reward_mean": float(np.mean(rets)), "episode_reward_max": float(np.max(rets)),
-                "episodes_this_iter": episodes}
+        return {"evaluation": {"episode_reward_mean": float(np.mean(rets)), "episode_reward_max": float(np.max(rets)),
+                               "episodes_this_iter": episodes}}
 
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}

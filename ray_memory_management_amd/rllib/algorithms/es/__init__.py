@@ -328,7 +328,7 @@ class ES(Trainable):
         self.policy.set_flat(self.theta)
         rs = [rollout(self.policy, self.eval_env, self.filter, self.algo_config.timestep_limit, False, False)[0]
               for _ in range(episodes)]
-        return {"episode_reward_mean": float(np.mean(rs))}
+        return {"evaluation": {"episode_reward_mean": float(np.mean(rs))}}
 
     def get_weights(self):
         return {"theta": self.theta.copy(), "filter": self.filter.get_state()}

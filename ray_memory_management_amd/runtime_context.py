@@ -27,13 +27,18 @@ class RuntimeContext:
     def get_node_id(self):
         return self.worker.node_id
 
+    def _task_id_bytes(self):
+        if self.worker.current_actor_id is not None:
+            return _w.actor_task_id.get()
+        return self.worker.current_task_id
+
     @property
     def task_id(self):
-        t = self.worker.current_task_id
+        t = self._task_id_bytes()
         return TaskID(t) if t else None
 
     def get_task_id(self):
-        t = self.worker.current_task_id
+        t = self._task_id_bytes()
         return t.hex() if t else None
 
     @property
@@ -72,8 +77,16 @@ class RuntimeContext:
         pg = self.worker.placement_group_capture
         return pg.id if pg else None
 
+    def get_placement_group_id(self):
+        pg = self.worker.placement_group_capture
+        return pg.id.hex() if pg else None
+
     def get_assigned_resources(self):
-        return {"GPU": len(self.worker.gpu_ids)} if self.worker.gpu_ids else {}
+        """Resources reserved for the running task / actor (its scheduling request), e.g. {"CPU": 1.0}."""
+        res = dict(getattr(self.worker, "assigned_resources", None) or {})
+        if self.worker.gpu_ids and "GPU" not in res:
+            res["GPU"] = float(len(self.worker.gpu_ids))
+        return res
 
     @property
     def gcs_address(self):

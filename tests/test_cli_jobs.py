@@ -36,7 +36,7 @@ def test_cli_status_memory_list_timeline(head, tmp_path):
     r = _cli("status", "--address", head)
     assert r.returncode == 0 and "CPU" in r.stdout, r.stderr
     r = _cli("memory", "--address", head, "--stats-only")
-    assert r.returncode == 0 and "Object store" in r.stdout, r.stderr
+    assert r.returncode == 0 and "Plasma memory usage" in r.stdout, r.stderr
     r = _cli("list", "nodes", "--address", head, "--format", "json")
     assert r.returncode == 0 and len(json.loads(r.stdout)) >= 1, r.stderr
     out = tmp_path / "tl.json"

@@ -108,6 +108,14 @@ def test_named_actor_and_namespace(ray_start):
         ray.get_actor("dd")
     assert ray.get(ray.get_actor("dd", namespace="other").get.remote()) == 1
 
+    # tasks and actors run in their job's namespace (reference test_namespace.py): a named actor of the
+    # driver's namespace resolves from inside a task, and the task reports the driver's namespace
+    @ray.remote
+    def lookup():
+        return ray.get_runtime_context().namespace, ray.get(ray.get_actor("ctr").get.remote())
+
+    assert ray.get(lookup.remote()) == (ray.get_runtime_context().namespace, 4)
+
 
 def test_actor_creation_error(ray_start):
     @ray.remote
@@ -218,6 +226,47 @@ def test_actor_out_of_scope_is_killed(ray_start):
     assert not alive
 
 
+def test_actor_method_on_temporary_handle(ray_start):
+    """Reference python/ray/tests/test_actor.py:797 test_actor_method_deletion: a call submitted right before
+    the last handle is dropped still runs; the actor is terminated after it (pending calls keep it in scope)."""
+    assert ray.get(Counter.remote().inc.remote()) == 1
+    pid = ray.get(Counter.remote().pid.remote())
+    deadline = time.time() + 10
+    alive = True
+    while time.time() < deadline:
+        try:
+            os.kill(pid, 0)
+        except OSError:
+            alive = False
+            break
+        time.sleep(0.1)
+    assert not alive
+    # several calls in flight on a dropped handle all complete, in order
+    c = Counter.remote()
+    refs = [c.inc.remote() for _ in range(5)]
+    del c
+    assert ray.get(refs) == [1, 2, 3, 4, 5]
+
+
+def test_actor_call_keeps_nested_args_alive(ray_start):
+    """A handle or ObjectRef passed (inline, possibly nested) to an actor method stays alive until the call
+    ran, even when the caller dropped its own (reference test_actor.py test_use_actor_within_actor /
+    test_reference_counting.py borrowed-ref cases)."""
+
+    @ray.remote
+    class Caller:
+        def call(self, h):
+            return ray.get(h.inc.remote(7))
+
+        def deref(self, lst):
+            return ray.get(lst[0])
+
+    assert ray.get(Caller.remote().call.remote(Counter.remote(1))) == 8
+    c = Caller.remote()
+    r = c.deref.remote([ray.put(41)])
+    assert ray.get(r) == 41
+
+
 def test_detached_actor_listed(ray_start):
     c = Counter.options(name="det", lifetime="detached").remote()
     ray.get(c.inc.remote())
@@ -264,3 +313,60 @@ def test_actor_gpu_assignment():
         assert len(ray.get(frac.remote(), timeout=20)) == 1
     finally:
         ray.shutdown()
+
+
+def test_runtime_context_in_actor_and_task(ray_start):
+    """Reference python/ray/tests/test_runtime_context.py: actor-task ids, was_current_actor_reconstructed after
+    a restart, assigned resources of a task, placement-group id outside a group."""
+
+    @ray.remote(max_restarts=1)
+    class R:
+        def info(self):
+            ctx = ray.get_runtime_context()
+            return ctx.get_actor_id(), ctx.get_task_id(), ctx.was_current_actor_reconstructed
+
+        def die(self):
+            os._exit(1)
+
+    r = R.remote()
+    aid, t1, rec = ray.get(r.info.remote())
+    _, t2, _ = ray.get(r.info.remote())
+    assert aid is not None and t1 is not None and t1 != t2 and rec is False
+    r.die.remote()
+    deadline = time.time() + 20
+    while time.time() < deadline:
+        try:
+            assert ray.get(r.info.remote(), timeout=10)[2] is True
+            break
+        except ray.exceptions.RayActorError:
+            time.sleep(0.2)
+    else:
+        raise AssertionError("actor did not restart")
+
+    @ray.remote(num_cpus=2)
+    def t():
+        ctx = ray.get_runtime_context()
+        return ctx.get_assigned_resources(), ctx.get_placement_group_id()
+
+    assert ray.get(t.remote()) == ({"CPU": 2.0}, None)
+
+
+def test_cancel_rejects_actor_task_and_wait_validates(ray_start):
+    """Reference _private/worker.py cancel ("TypeError ... also raised for actor tasks") and wait's argument
+    checks (nonnegative timeout, list of ObjectRefs)."""
+
+    @ray.remote
+    class Slow:
+        def nap(self):
+            time.sleep(1.0)
+            return 1
+
+    s = Slow.remote()
+    r = s.nap.remote()
+    with pytest.raises(TypeError):
+        ray.cancel(r)
+    assert ray.get(r) == 1
+    with pytest.raises(ValueError):
+        ray.wait([r], timeout=-1)
+    with pytest.raises(TypeError):
+        ray.wait([r, "x"], num_returns=1)

@@ -60,7 +60,7 @@ def test_ppo_learns_cartpole(ray_shared):
     w1 = algo2.get_weights()
     assert all(np.allclose(w0[k].numpy(), w1[k].numpy()) for k in w0)
     assert algo2.iteration == 10
-    ev = algo2.evaluate()
+    ev = algo2.evaluate()["evaluation"]
     assert ev["episodes_this_iter"] == 10 and ev["episode_reward_mean"] > 20
     algo.stop()
     algo2.stop()

@@ -94,7 +94,7 @@ def test_es_ars_learn_cartpole(ray_shared, name):
     best = 0.0
     for _ in range(25):
         algo.train()
-        best = max(best, algo.evaluate(3)["episode_reward_mean"])
+        best = max(best, algo.evaluate(3)["evaluation"]["episode_reward_mean"])
         if best >= 150:
             break
     assert best >= 150, (name, best)

@@ -148,7 +148,7 @@ def test_learns_continuous_target(ray_shared, algo):
     best = -1e9
     for _ in range(12):
         algo_.train()
-        ev = algo_.evaluate()["episode_reward_mean"]
+        ev = algo_.evaluate()["evaluation"]["episode_reward_mean"]
         best = max(best, ev)
         if best > -0.8:
             break
@@ -199,7 +199,7 @@ def test_apex_dqn_replay_shards_and_per_worker_epsilon(ray_shared):
     best, r = 0.0, None
     for _ in range(40):
         r = algo.train()
-        best = max(best, algo.evaluate()["episode_reward_mean"])
+        best = max(best, algo.evaluate()["evaluation"]["episode_reward_mean"])
         if best > 100:
             break
     assert best > 100, best
@@ -225,7 +225,7 @@ def test_apex_ddpg_runs_on_continuous_target(ray_shared):
     best = -1e9
     for _ in range(25):
         algo.train()
-        best = max(best, algo.evaluate()["episode_reward_mean"])
+        best = max(best, algo.evaluate()["evaluation"]["episode_reward_mean"])
         if best > -1.0:
             break
     assert best > -1.0, best
@@ -270,7 +270,7 @@ def test_offline_continuous_from_random_data(ray_shared, tmp_path, algo):
     for i in range(80):
         r = a.train()
         if i % 10 == 9:
-            best = max(best, a.evaluate()["episode_reward_mean"])
+            best = max(best, a.evaluate()["evaluation"]["episode_reward_mean"])
             if best > -1.5:
                 break
     st = r["info"]["learner"]["default_policy"]["learner_stats"]

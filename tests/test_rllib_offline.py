@@ -114,7 +114,7 @@ def test_offline_algorithms_learn_from_expert(ray_shared, tmp_path, algo):
     assert np.isfinite(st["policy_loss"])
     if algo == "MARWIL":
         assert st["vf_loss"] > 0
-    ev = a.evaluate()
+    ev = a.evaluate()["evaluation"]
     assert ev["episode_reward_mean"] > 100, ev
     a.stop()
 
@@ -140,7 +140,7 @@ def test_decision_transformer_from_expert_episodes(ray_shared, tmp_path):
         r = a.train()
         losses.append(r["info"]["learner"]["default_policy"]["learner_stats"]["loss"])
     assert np.mean(losses[-20:]) < 0.5 * np.mean(losses[:5]), (losses[:5], losses[-20:])
-    ev = a.evaluate(episodes=3)
+    ev = a.evaluate(episodes=3)["evaluation"]
     assert ev["episode_reward_mean"] > 150, ev
     a.stop()
 
