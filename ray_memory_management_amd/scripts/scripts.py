@@ -163,6 +163,148 @@ def cmd_list(a):
     return 0
 
 
+def cmd_get(a):
+    """`ray get <resource> <id>` (reference scripts.py ray_get): one state record as JSON."""
+    _connect(a.address)
+    from ray_memory_management_amd.util import state
+
+    fn = {"actors": state.get_actor, "tasks": state.get_task, "objects": state.get_objects,
+          "nodes": state.get_node, "workers": state.get_worker, "jobs": state.get_job,
+          "placement-groups": state.get_placement_group}[a.resource]
+    row = fn(a.id)
+    if not row:
+        print(f"{a.resource[:-1]} {a.id} not found", file=sys.stderr)
+        return 1
+    print(json.dumps(row, indent=1, default=str))
+    return 0
+
+
+def cmd_logs(a):
+    """`ray logs` (reference scripts.py:1961): without a target, list the session's log files by category;
+    with a file name / --actor-id / --task-id / --pid, print its last --tail lines (--follow keeps going)."""
+    _connect(a.address)
+    from ray_memory_management_amd.util import state
+
+    if not (a.glob and any(c in a.glob for c in "*?[")) and (a.glob or a.actor_id or a.task_id or a.pid):
+        for line in state.get_log(filename=a.glob, actor_id=a.actor_id, task_id=a.task_id, pid=a.pid,
+                                  follow=a.follow, tail=a.tail):
+            print(line, flush=a.follow)
+        return 0
+    for cat, files in sorted(state.list_logs(glob_filter=a.glob).items()):
+        print(f"{cat}:")
+        for f in files:
+            print(f"  {f}")
+    return 0
+
+
+def cmd_global_gc(a):
+    """`ray global-gc` (reference scripts.py): gc.collect() in every worker and driver."""
+    _connect(a.address)
+    from ray_memory_management_amd._private.internal_api import global_gc
+
+    global_gc()
+    print("Triggered gc.collect() on all workers.")
+    return 0
+
+
+def cmd_local_dump(a):
+    """`ray local-dump` (reference scripts.py:2165, trimmed to what exists here): tar.gz of the session's
+    logs, session.json and a state snapshot (actors / tasks / workers / nodes / memory summary)."""
+    import io
+    import tarfile
+
+    sess = _session(a.address)
+    out = a.output or os.path.join(tempfile.gettempdir(), f"rmm-local-dump-{int(time.time())}.tar.gz")
+    with tarfile.open(out, "w:gz") as tar:
+        logs = os.path.join(sess, "logs")
+        if os.path.isdir(logs):
+            tar.add(logs, arcname="logs")
+        sj = os.path.join(sess, "session.json")
+        if os.path.exists(sj):
+            tar.add(sj, arcname="session.json")
+        try:
+            _connect(a.address)
+            from ray_memory_management_amd._private.internal_api import memory_summary
+            from ray_memory_management_amd.util import state
+
+            snap = {"actors": state.list_actors(), "tasks": state.list_tasks(limit=2000),
+                    "workers": state.list_workers(), "nodes": state.list_nodes(),
+                    "memory_summary": memory_summary(stats_only=True)}
+            data = json.dumps(snap, indent=1, default=str).encode()
+            ti = tarfile.TarInfo("state.json")
+            ti.size, ti.mtime = len(data), int(time.time())
+            tar.addfile(ti, io.BytesIO(data))
+        except Exception as e:  # noqa: BLE001 - a dead head still leaves its logs worth dumping
+            print(f"state snapshot skipped: {e}", file=sys.stderr)
+    print(out)
+    return 0
+
+
+def cmd_debug(a):
+    """`ray debug` (reference scripts.py:202): list the active remote-pdb breakpoints registered in the
+    cluster KV and attach to one (stdin/stdout relayed over its TCP socket)."""
+    import socket
+
+    _connect(a.address)
+    from ray_memory_management_amd.util import rpdb
+
+    bps = rpdb.list_breakpoints()
+    if not bps:
+        print("No active breakpoints.")
+        return 0
+    for i, b in enumerate(bps):
+        print(f"{i}: pid {b['pid']} at {b['host']}:{b['port']} ({b['uuid']})")
+    if a.list:
+        return 0
+    idx = a.index if a.index is not None else int(input("Enter breakpoint index or press enter to refresh: "))
+    b = bps[idx]
+    with socket.create_connection((b["host"], int(b["port"]))) as c:
+        f = c.makefile("rw", buffering=1)
+        import select
+
+        while True:
+            r, _, _ = select.select([c, sys.stdin], [], [])
+            if c in r:
+                data = c.recv(65536)
+                if not data:
+                    return 0
+                sys.stdout.write(data.decode(errors="replace"))
+                sys.stdout.flush()
+            if sys.stdin in r:
+                line = sys.stdin.readline()
+                if not line:
+                    return 0
+                f.write(line)
+                f.flush()
+
+
+def _usage_stats_file():
+    return os.path.join(os.path.expanduser("~"), ".rmm", "config.json")
+
+
+def cmd_usage_stats(a):
+    """`ray enable-usage-stats / disable-usage-stats`: recorded in ~/.rmm/config.json. Nothing is ever sent
+    (no telemetry exists here); the flag is kept so scripts written for the reference run unchanged."""
+    p = _usage_stats_file()
+    os.makedirs(os.path.dirname(p), exist_ok=True)
+    cfg = {}
+    if os.path.exists(p):
+        try:
+            cfg = json.load(open(p))
+        except ValueError:
+            cfg = {}
+    cfg["usage_stats"] = a.cmd == "enable-usage-stats"
+    json.dump(cfg, open(p, "w"))
+    print(f"Usage stats collection is {'enabled' if cfg['usage_stats'] else 'disabled'} (nothing is reported).")
+    return 0
+
+
+def cmd_serve(a):
+    from ray_memory_management_amd.serve import scripts as serve_scripts
+
+    return int(serve_scripts.main(a.serve_args) or 0)
+
+
 def cmd_summary(a):
     _connect(a.address)
     from ray_memory_management_amd.util import state
@@ -283,6 +425,39 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--limit", type=int, default=100)
     s.add_argument("--format", default="table", choices=["table", "json"])
     s.set_defaults(fn=cmd_list)
+    s = sub.add_parser("get", help="one state record by id")
+    s.add_argument("resource", choices=["actors", "tasks", "objects", "nodes", "workers", "jobs",
+                                        "placement-groups"])
+    s.add_argument("id")
+    s.add_argument("--address", default=None)
+    s.set_defaults(fn=cmd_get)
+    s = sub.add_parser("logs", help="list the session's log files, or print one")
+    s.add_argument("glob", nargs="?", default=None, help="file name, or a glob filter for the listing")
+    s.add_argument("--actor-id", default=None)
+    s.add_argument("--task-id", default=None)
+    s.add_argument("--pid", type=int, default=None)
+    s.add_argument("--tail", type=int, default=1000)
+    s.add_argument("-f", "--follow", action="store_true")
+    s.add_argument("--address", default=None)
+    s.set_defaults(fn=cmd_logs)
+    s = sub.add_parser("global-gc", help="gc.collect() in every worker and driver")
+    s.add_argument("--address", default=None)
+    s.set_defaults(fn=cmd_global_gc)
+    s = sub.add_parser("local-dump", help="tar.gz of the session's logs and a state snapshot")
+    s.add_argument("--address", default=None)
+    s.add_argument("--output", default=None)
+    s.set_defaults(fn=cmd_local_dump)
+    s = sub.add_parser("debug", help="list / attach to remote-pdb breakpoints")
+    s.add_argument("--address", default=None)
+    s.add_argument("--list", action="store_true")
+    s.add_argument("--index", type=int, default=None)
+    s.set_defaults(fn=cmd_debug)
+    for name in ("enable-usage-stats", "disable-usage-stats"):
+        s = sub.add_parser(name)
+        s.set_defaults(fn=cmd_usage_stats)
+    s = sub.add_parser("serve", help="serve deploy / run / status / shutdown")
+    s.add_argument("serve_args", nargs=argparse.REMAINDER)
+    s.set_defaults(fn=cmd_serve)
     s = sub.add_parser("summary")
     s.add_argument("resource", choices=["tasks", "actors", "objects"])
     s.add_argument("--address", default=None)

@@ -42,6 +42,30 @@ def test_cli_status_memory_list_timeline(head, tmp_path):
     out = tmp_path / "tl.json"
     r = _cli("timeline", "--address", head, "--output", str(out))
     assert r.returncode == 0 and out.exists(), r.stderr
+    # reference CLI commands beyond list: get / logs / global-gc / local-dump / debug / usage stats
+    nid = str(json.loads(_cli("list", "nodes", "--address", head, "--format", "json").stdout)[0]["NodeID"])
+    r = _cli("get", "nodes", nid, "--address", head)
+    assert r.returncode == 0 and json.loads(r.stdout), r.stdout + r.stderr
+    r = _cli("get", "actors", "ffff", "--address", head)
+    assert r.returncode == 1
+    r = _cli("logs", "--address", head)
+    assert r.returncode == 0 and ":" in r.stdout, r.stderr
+    first = [ln.strip() for ln in r.stdout.splitlines() if ln.startswith("  ")][0]
+    r = _cli("logs", first, "--tail", "5", "--address", head)
+    assert r.returncode == 0 and len(r.stdout.splitlines()) <= 5, r.stderr
+    r = _cli("global-gc", "--address", head)
+    assert r.returncode == 0 and "gc.collect" in r.stdout, r.stderr
+    dump = tmp_path / "dump.tar.gz"
+    r = _cli("local-dump", "--address", head, "--output", str(dump))
+    assert r.returncode == 0 and dump.exists(), r.stderr
+    import tarfile
+
+    with tarfile.open(dump) as t:
+        assert "state.json" in t.getnames()
+    r = _cli("debug", "--list", "--address", head)
+    assert r.returncode == 0 and "No active breakpoints" in r.stdout, r.stderr
+    r = _cli("disable-usage-stats", env={"HOME": str(tmp_path)})
+    assert r.returncode == 0 and json.load(open(tmp_path / ".rmm" / "config.json")) == {"usage_stats": False}
 
 
 def test_job_submission_lifecycle(head, tmp_path):
