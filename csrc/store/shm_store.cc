@@ -972,6 +972,14 @@ void Store::SetDiskFull(bool full) {
   Unlock();
 }
 
+void Store::SetSpillEnabled(bool on) {
+  // spilling needs a directory: a store created without one keeps it off (fallback files are separate)
+  Lock();
+  hdr_->spill_enabled = (on && hdr_->spill_dir[0] != 0) ? 1 : 0;
+  Broadcast();
+  Unlock();
+}
+
 void Store::SetOomGrace(double seconds) {
   Lock();
   hdr_->oom_grace_ns = int64_t(seconds * 1e9);

@@ -202,6 +202,8 @@ class Store {
                        double oom_grace_s = 2.0, bool populate = false);
   // Memory-pressure controls / counters (see Header).
   void SetDiskFull(bool full);
+  // automatic_object_spilling_enabled: off keeps the directories for fallback files only
+  void SetSpillEnabled(bool on);
   bool DiskFull() const { return hdr_->disk_full != 0; }
   uint64_t GcRequests() const { return __atomic_load_n(&hdr_->gc_requests, __ATOMIC_ACQUIRE); }
   uint64_t OomWaits() const { return hdr_->oom_waits_total; }

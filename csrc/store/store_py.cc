@@ -437,6 +437,10 @@ PYBIND11_MODULE(_store, m) {
         self.s->SetDiskFull(full);
       })
       .def("disk_full", [](PyStore& self) { return self.s->DiskFull(); })
+      .def("set_spill_enabled", [](PyStore& self, bool on) {
+        py::gil_scoped_release nogil;
+        self.s->SetSpillEnabled(on);
+      })
       .def("gc_requests", [](PyStore& self) { return self.s->GcRequests(); })
       .def("set_oom_grace", [](PyStore& self, double s) {
         py::gil_scoped_release nogil;

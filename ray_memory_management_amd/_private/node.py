@@ -206,12 +206,16 @@ class Head:
         self.spill_threshold = float(self.config.get("object_spilling_threshold", 0.8))
         self.store = store_ext().ObjectStore.create_segment(
             self.store_name, cap,
-            ":".join(self.spill_dirs) if self.config.get("automatic_object_spilling_enabled", True) else "",
+            ":".join(self.spill_dirs),
             self.spill_threshold, min_spill, bool(self.config.get("object_store_fallback_allocation", True)),
             float(self.config.get("oom_grace_period_s", 2.0)),
             # reference ray_config_def.h:150 preallocate_plasma_memory (RAY_preallocate_plasma_memory=1)
             populate=bool(self.config.get("preallocate_plasma_memory",
                                           os.environ.get("RAY_preallocate_plasma_memory") == "1")))
+        if not self.config.get("automatic_object_spilling_enabled", True):
+            # reference: spilling off, but a full store still falls back to file-backed allocation
+            # (plasma_allocator.cc fallback mmap) after the grace period
+            self.store.set_spill_enabled(False)
         # memory-pressure machinery (reference: local_object_manager.cc IO-worker spilling,
         # local_task_manager.cc:615 PinTaskArgsIfMemoryAvailable, node_manager.cc:2799
         # TriggerGlobalGC, file_system_monitor.cc)
@@ -2009,6 +2013,18 @@ class Head:
                 self._forker.close()
         except OSError:
             pass
+        # spill / fallback files die with the store (reference: the raylet deletes an owner's spilled
+        # objects when it exits, test_object_spilling_2.py:366 test_file_deleted_when_driver_exits)
+        for d in self.spill_dirs:
+            try:
+                for f in os.listdir(d):
+                    if (f.startswith("rmm-spill-") or f.startswith("rmm-fallback-")) and f.endswith(".bin"):
+                        try:
+                            os.unlink(os.path.join(d, f))
+                        except OSError:
+                            pass
+            except OSError:
+                pass
         try:  # explicitly: other references to the store (IO threads) would keep `del` from unlinking
             from _posixshmem import shm_unlink
 
