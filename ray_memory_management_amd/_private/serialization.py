@@ -160,10 +160,14 @@ def serialize(value: Any) -> Tuple[bytes, List[pickle.PickleBuffer], List[bytes]
     return data, out, contained
 
 
-def note_contained(oid: bytes):
+def note_contained(oid: bytes) -> bool:
+    """Record a reference met while pickling; False when no runtime serialization is in progress (the
+    reference is being pickled out of band, e.g. cloudpickle.dumps of a ref or of a function capturing one)."""
     c = getattr(_tls, "contained", None)
     if c is not None:
         c.append(oid)
+        return True
+    return False
 
 
 def deserialize(data, buffers) -> Any:

@@ -461,6 +461,28 @@ class CoreWorker:
             if self._eager_gpu_free:
                 self._run_eager_frees()
 
+    def pending_borrows(self) -> bool:
+        """True when this process took references (0 -> 1) the head has not been told about yet."""
+        with self.ref_lock:
+            self._drain_removes()
+            return any(v > 0 for v in self.deltas.values())
+
+    def flush_refs_sync(self):
+        """Make the head apply this process's new references before returning. An actor calls it before it
+        acknowledges a call to its caller: the ack lets the caller drop the refs it kept for the call, and the
+        head must see the actor's borrow of those refs first (both reach the head over different
+        connections)."""
+        if self.pending_borrows():
+            self.request(lambda rid: (P.STATE, rid, "session_dir", None))
+
+    def pin_out_of_band(self, oid: bytes):
+        """One permanent local reference per object pickled out of band (dropped with this process)."""
+        pins = self.__dict__.setdefault("_oob_pins", set())
+        if oid in pins:
+            return
+        pins.add(oid)
+        self.add_local_ref(oid)
+
     def note_escaped(self, oid: bytes):
         """The ref is being serialized or handed to a task: another process may now borrow it."""
         self._gpu_unescaped.discard(oid)

@@ -468,6 +468,7 @@ class Executor:
         t1 = time.time()
         w.record_event({"cat": "actor_task", "name": spec.get("name", name), "ph": "X", "pid": "actors",
                         "tid": f"actor {self.pid}", "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6})
+        w.flush_refs_sync()  # borrows taken by this call reach the head before the caller may drop its refs
         self._ack(s, lock, spec["seq"])
         del holds
 
@@ -503,6 +504,8 @@ class Executor:
             if contained_map:
                 for outer, inners in contained_map.items():
                     self.w.send((P.CONTAINED, outer, inners))
+            if self.w.pending_borrows():  # see run_actor_task
+                await asyncio.get_running_loop().run_in_executor(None, self.w.flush_refs_sync)
             self._ack(s, lock, spec["seq"])
 
     def actor_loop(self):

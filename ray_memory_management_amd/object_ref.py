@@ -73,11 +73,22 @@ class ObjectRef:
                     pass
 
     def __reduce__(self):
-        ser.note_contained(self._id)
+        in_band = ser.note_contained(self._id)
         w = _worker
         if w is not None:
             w.note_escaped(self._id)
+            if not in_band:
+                # pickled out of band (cloudpickle.dumps(ref), a remote function / actor class capturing it):
+                # nothing tracks the copy, so the object stays pinned for this process's lifetime (reference
+                # test_reference_counting.py:259,276 out-of-band / captured refs)
+                w.pin_out_of_band(self._id)
         return (_rebuild_ref, (self._id,))
+
+    def __copy__(self):
+        return ObjectRef(self._id)
+
+    def __deepcopy__(self, memo):
+        return ObjectRef(self._id)
 
     # ---- futures / asyncio integration (reference: ObjectRef.future(), __await__)
     def future(self) -> concurrent.futures.Future:
