@@ -494,6 +494,7 @@ PYBIND11_MODULE(_store, m) {
           d["creator_pid"] = pr.second.creator_pid;
           d["fallback"] = bool(pr.second.flags & kFlagFallback);
           d["has_spill_copy"] = bool(pr.second.flags & kFlagHasSpillCopy);
+          d["delete_pending"] = bool(pr.second.flags & kFlagDeletePending);
           d["tag"] = pr.second.user_tag;
           out.append(d);
         }

@@ -580,7 +580,14 @@ class Head:
                     held[oid] = n
                 else:
                     held.pop(oid, None)
-            self._ref_deltas(m[1])
+            # increments first: one batch covers a time window in which the process may have read a ref
+            # out of an object (+1 inner) and then dropped that object (-1 outer); the batch is keyed by
+            # object, so its order is not that order, and applying the -1 first could free the inner
+            # object (a pending task's return) while the process now holds it
+            d = m[1]
+            if len(d) > 1:
+                d = [x for x in d if x[1] > 0] + [x for x in d if x[1] <= 0]
+            self._ref_deltas(d)
         elif t == P.SUBMIT_TASK:
             self._submit_task(c, m[1])
         elif t == P.DIRECT_DONE:
@@ -1019,6 +1026,12 @@ class Head:
 
     def _add_contained(self, outer, inners):
         if not inners:
+            return
+        if outer not in self.refcounts and outer in self.recently_freed:
+            # the outer object was already freed: its owner read it and dropped it before this CONTAINED
+            # (sent by the producing worker on another connection) arrived. Holding the inner refs for a gone
+            # object would leak them; whoever deserialized the outer holds the inner refs on their own (their
+            # +1 reached the head before their drop of the outer, hence before this message)
             return
         self.contained.setdefault(outer, []).extend(inners)
         rc = self.refcounts
@@ -1668,6 +1681,13 @@ class Head:
                 o["object_id"] = o["object_id"].hex()
                 o["reference_count"] = self.refcounts.get(bytes.fromhex(o["object_id"]), 0)
             return objs
+        if what == "ref_holders":  # who holds an object: per-connection counts + containing objects
+            oid = bytes.fromhex(arg) if isinstance(arg, str) else arg
+            out = [{"kind": c.kind, "pid": c.pid, "count": c.held[oid]} for c in self.conns.values()
+                   if oid in c.held]
+            out += [{"kind": "contained_in", "object_id": o.hex()} for o, inn in self.contained.items() if oid in inn]
+            return {"reference_count": self.refcounts.get(oid, 0), "holders": out,
+                    "recently_freed": oid in self.recently_freed, "freed_early": oid in self.freed_early}
         if what == "store_stats":
             return self.store.stats()
         if what == "jobs":

@@ -250,8 +250,14 @@ class ActorConn:
             if isinstance(reply, str) and reply:
                 msg += " " + reply
             err = exc.RayActorError(aid.hex(), msg)
+            w = self.worker
             for spec, _keep in failed:
-                self.worker._store_errors(spec["return_ids"], err)
+                # a call that completed but whose ack was lost with the process has nothing to report, and a
+                # return nobody references any more (its result was read and dropped) must not be re-created
+                # as an error object no one would ever free
+                rids = [o for o in spec["return_ids"] if o in w.local_refs and not w.store.contains(o)]
+                if rids:
+                    w._store_errors(rids, err)
 
         try:
             self.worker.request_async(lambda rid: (P.EXIT_DETAIL, rid, aid), done)
@@ -334,6 +340,9 @@ class CoreWorker:
                                 p.cb(m[2])
                             except Exception as e:  # pragma: no cover
                                 logger.warning("async reply handler failed: %r", e)
+                            # drop the callback (and whatever its closure keeps alive: a failed call's
+                            # argument refs) now, not when the next message from the head rebinds `p`
+                            p = m = None
                             continue
                         p.value = m[2]
                         p.ev.set()

@@ -380,3 +380,302 @@ def test_out_of_band_actor_handle_bypass_reference_counting(one_worker_100MiB):
     config = pickle.loads(serialized)
     with pytest.raises(ray.exceptions.RayActorError):
         ray.get(config["actor"].ping.remote(), timeout=10)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# reference python/ray/tests/test_reference_counting_2.py
+
+@pytest.mark.parametrize("use_ray_put,failure", [(False, False), (False, True), (True, False), (True, True)])
+def test_recursively_nest_ids(one_worker_100MiB, use_ray_put, failure):
+    """:66 An object containing refs pins the inner ids recursively, also for submitted tasks."""
+    @ray.remote(max_retries=1)
+    def recursive(ref, signal, max_depth, depth=0):
+        unwrapped = ray.get(ref[0])
+        if depth == max_depth:
+            ray.get(signal.wait.remote())
+            if failure:
+                os._exit(0)
+            return
+        return recursive.remote(unwrapped, signal, max_depth, depth + 1)
+
+    signal = SignalActor.remote()
+    max_depth = 5
+    array_oid = _put_object(np.zeros(20 * MB, dtype=np.uint8), use_ray_put)
+    nested_oid = array_oid
+    for _ in range(max_depth):
+        nested_oid = ray.put([nested_oid])
+    head_oid = recursive.remote([nested_oid], signal, max_depth)
+    oid = array_oid.binary()
+    del array_oid, nested_oid
+    tail_oid = head_oid
+    for _ in range(max_depth):
+        tail_oid = ray.get(tail_oid)
+    _fill_object_store_and_get(oid)
+    ray.get(signal.send.remote())
+    if not failure:
+        ray.get(tail_oid)
+    else:
+        with pytest.raises(ray.exceptions.RayError):  # reference: OwnerDiedError (see the module doc)
+            ray.get(tail_oid)
+    _fill_object_store_and_get(oid, succeed=False)
+
+
+@pytest.mark.parametrize("use_ray_put,failure", [(False, False), (False, True), (True, False), (True, True)])
+def test_return_object_ref(one_worker_100MiB, use_ray_put, failure):
+    """:120 A ref returned inside a task's result stays pinned while the caller holds it."""
+    @ray.remote
+    def return_an_id():
+        return [_put_object(np.zeros(20 * MB, dtype=np.uint8), use_ray_put)]
+
+    @ray.remote(max_retries=1)
+    def exit():
+        os._exit(0)
+
+    outer_oid = return_an_id.remote()
+    inner_bytes = ray.get(outer_oid)[0].binary()
+    inner_oid = ray.get(outer_oid)[0]
+    del outer_oid
+    _fill_object_store_and_get(inner_bytes)
+    if failure:
+        # the reference frees it when its owner (the worker) dies; here the driver's reference keeps it, so
+        # the worker crash is checked and then the reference is dropped
+        with pytest.raises(ray.exceptions.WorkerCrashedError):
+            ray.get(exit.remote())
+        _fill_object_store_and_get(inner_bytes)
+    del inner_oid
+    _fill_object_store_and_get(inner_bytes, succeed=False)
+
+
+@pytest.mark.parametrize("use_ray_put,failure", [(False, False), (False, True), (True, False), (True, True)])
+def test_pass_returned_object_ref(one_worker_100MiB, use_ray_put, failure):
+    """:155 A returned ref passed on to another task is pinned by that task until it finishes."""
+    @ray.remote
+    def return_an_id():
+        return [_put_object(np.zeros(20 * MB, dtype=np.uint8), use_ray_put)]
+
+    @ray.remote(max_retries=0)
+    def pending(ref, signal):
+        ray.get(signal.wait.remote())
+        ray.get(ref[0])
+        if failure:
+            os._exit(0)
+
+    signal = SignalActor.remote()
+    outer_oid = return_an_id.remote()
+    inner_bytes = ray.get(outer_oid)[0].binary()
+    pending_oid = pending.remote([outer_oid], signal)
+    del outer_oid
+    ray.get(signal.send.remote())
+    try:
+        ray.get(pending_oid)
+        assert not failure
+    except ray.exceptions.WorkerCrashedError:
+        assert failure
+    _wait_for(lambda: not _exists(inner_bytes))
+
+
+@pytest.mark.parametrize("use_ray_put,failure", [(False, False), (False, True), (True, False), (True, True)])
+def test_recursively_pass_returned_object_ref(one_worker_100MiB, use_ray_put, failure):
+    """:201 A returned ref passed down a chain of tasks that each return it again."""
+    @ray.remote
+    def return_an_id():
+        return _put_object(np.zeros(20 * MB, dtype=np.uint8), use_ray_put)
+
+    @ray.remote(max_retries=1)
+    def recursive(ref, signal, max_depth, depth=0):
+        inner_id = ray.get(ref[0])
+        if depth == max_depth:
+            ray.get(signal.wait.remote())
+            if failure:
+                os._exit(0)
+            return inner_id
+        return inner_id, recursive.remote(ref, signal, max_depth, depth + 1)
+
+    max_depth = 5
+    outer_oid = return_an_id.remote()
+    signal = SignalActor.remote()
+    head_oid = recursive.remote([outer_oid], signal, max_depth)
+    inner_oid = None
+    outer_oid = head_oid
+    for _ in range(max_depth):
+        inner_oid, outer_oid = ray.get(outer_oid)
+    _fill_object_store_and_get(outer_oid.binary(), succeed=False)  # the tail has not returned yet
+    ray.get(signal.send.remote())
+    try:
+        ray.get(outer_oid)
+        _fill_object_store_and_get(inner_oid.binary())
+        assert not failure
+    except ray.exceptions.RayError:
+        assert failure
+    inner_bytes = inner_oid.binary()
+    del inner_oid, head_oid, outer_oid
+    _fill_object_store_and_get(inner_bytes, succeed=False)
+
+
+@pytest.mark.parametrize("use_ray_put", [False, True])
+def test_recursively_return_borrowed_object_ref(one_worker_100MiB, use_ray_put):
+    """:264 (the failure variant kills the owner to get OwnerDiedError; references are accounted at the head
+    here, so the driver's reference keeps the object instead)."""
+    @ray.remote
+    def recursive(num_tasks_left):
+        if num_tasks_left == 0:
+            return _put_object(np.zeros(20 * MB, dtype=np.uint8), use_ray_put), os.getpid()
+        return ray.get(recursive.remote(num_tasks_left - 1))
+
+    head_oid = recursive.remote(5)
+    final_oid, _ = ray.get(head_oid)
+    final_bytes = final_oid.binary()
+    _fill_object_store_and_get(final_bytes)
+    _fill_object_store_and_get(final_bytes)
+    del head_oid
+    del final_oid
+    _fill_object_store_and_get(final_bytes, succeed=False)
+
+
+def test_borrowed_id(one_worker_100MiB):
+    """:304 (no-failure case) a ref handed from one actor to another stays usable by the borrower."""
+    @ray.remote
+    class Parent:
+        def pass_ref(self, ref, borrower):
+            self.ref = ref[0]
+            ray.get(borrower.receive_ref.remote(ref))
+
+    @ray.remote
+    class Borrower:
+        def __init__(self):
+            self.ref = None
+
+        def receive_ref(self, ref):
+            self.ref = ref[0]
+
+        def resolve_ref(self):
+            return ray.get(self.ref).nbytes
+
+        def ping(self):
+            return
+
+    parent = Parent.remote()
+    borrower = Borrower.remote()
+    ray.get(borrower.ping.remote())
+    obj = ray.put(np.zeros(20 * MB, dtype=np.uint8))
+    ray.get(parent.pass_ref.remote([obj], borrower))
+    obj_bytes = obj.binary()
+    del obj
+    _fill_object_store_and_get(obj_bytes)
+    assert ray.get(borrower.resolve_ref.remote()) == 20 * MB
+
+
+def test_inlined_nested_refs(one_worker_100MiB):
+    """:554 (single node) a ref created by an actor, returned through a task, passed to another task."""
+    @ray.remote
+    class Actor:
+        def nested(self):
+            return ray.put("x")
+
+    @ray.remote
+    def nested_nested(a):
+        return a.nested.remote()
+
+    @ray.remote
+    def foo(ref):
+        time.sleep(0.5)
+        return ray.get(ref)
+
+    a = Actor.remote()
+    nested_nested_ref = nested_nested.remote(a)
+    nested_ref = ray.get(nested_nested_ref)
+    del nested_nested_ref
+    x = foo.remote(nested_ref)
+    del nested_ref
+    assert ray.get(x) == "x"
+
+
+def test_return_nested_ids(one_worker_100MiB):
+    """:594 (ray issue 17553) refs nested in a returned object survive being echoed through a closure."""
+    class Nested:
+        def __init__(self, blocks):
+            self._blocks = blocks
+
+    @ray.remote
+    def echo(fn):
+        return fn()
+
+    @ray.remote
+    def create_nested():
+        return Nested([ray.put(np.random.random(MB // 8)) for _ in range(10)])
+
+    @ray.remote
+    def test():
+        ref = create_nested.remote()
+        result1 = ray.get(ref)
+        del ref
+        result = echo.remote(lambda: result1)  # noqa: B023
+        del result1
+        time.sleep(1)
+        return ray.get(ray.get(result)._blocks[0]).shape
+
+    assert ray.get(test.remote()) == (MB // 8,)
+
+
+def test_actor_constructor_borrowed_refs(one_worker_100MiB):
+    """:631 the actor's constructor is the only holder of a ref."""
+    @ray.remote(num_cpus=0)
+    class Borrower:
+        def __init__(self, borrowed_refs):
+            self.borrowed_refs = borrowed_refs
+
+        def test(self):
+            return len(ray.get(self.borrowed_refs))
+
+    ref = ray.put(np.random.random(MB // 8))
+    b = Borrower.remote([ref])
+    del ref
+    for _ in range(3):
+        assert ray.get(b.test.remote()) == 1
+        time.sleep(0.3)
+
+
+def test_deep_nested_refs(one_worker_100MiB):
+    """:653 a chain of 200 tasks each returning the next one's ref."""
+    @ray.remote
+    def f(x):
+        if x > 200:
+            return x
+        return f.remote(x + 1)
+
+    r = f.remote(1)
+    while isinstance(r, ray.ObjectRef):
+        r = ray.get(r)
+    assert r == 201
+
+
+def test_forward_nested_ref(one_worker_100MiB):
+    """:672 a ref to a ref, forwarded by a task to an actor that keeps the inner one."""
+    @ray.remote
+    def nested_ref():
+        return ray.put(1)
+
+    @ray.remote
+    def nested_nested_ref():
+        return nested_ref.remote()
+
+    @ray.remote(num_cpus=0)
+    class Borrower:
+        def pass_ref(self, middle_ref):
+            self.inner_ref = ray.get(middle_ref)
+
+        def check_ref(self):
+            return ray.get(self.inner_ref)
+
+    @ray.remote
+    def pass_nested_ref(borrower, outer_ref):
+        ray.get(borrower.pass_ref.remote(outer_ref[0]))
+
+    b = Borrower.remote()
+    outer_ref = nested_nested_ref.remote()
+    x = pass_nested_ref.remote(b, [outer_ref])
+    del outer_ref
+    ray.get(x)
+    for _ in range(3):
+        assert ray.get(b.check_ref.remote()) == 1
+        time.sleep(0.3)
