@@ -413,6 +413,7 @@ class Executor:
 
     def run_actor_task(self, s, lock, spec):
         w = self.w
+        borrowed = False
         name = spec["method"]
         ret_ids = spec["return_ids"]
         t0 = time.time()
@@ -430,6 +431,7 @@ class Executor:
             else:
                 _w.actor_task_id.set(spec["task_id"])
                 args, kwargs = self.resolve_all(spec["args"], spec["kwargs"])
+                borrowed = w.pending_borrows()  # refs taken out of the caller's arguments
                 t_res = time.time()
                 m = getattr(self.actor, name)
                 if "_trace_ctx" in spec:
@@ -468,12 +470,14 @@ class Executor:
         t1 = time.time()
         w.record_event({"cat": "actor_task", "name": spec.get("name", name), "ph": "X", "pid": "actors",
                         "tid": f"actor {self.pid}", "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6})
-        w.flush_refs_sync()  # borrows taken by this call reach the head before the caller may drop its refs
+        if borrowed:  # borrows taken from the call's arguments reach the head before the caller may drop its refs
+            w.flush_refs_sync()
         self._ack(s, lock, spec["seq"])
         del holds
 
     async def run_async_actor_task(self, s, lock, spec):
         async with self.sem:
+            borrowed = False
             name = spec["method"]
             ret_ids = spec["return_ids"]
             holds, contained_map = [], {}
@@ -488,6 +492,7 @@ class Executor:
                     _w.actor_task_id.set(spec["task_id"])
                     loop = asyncio.get_running_loop()
                     args, kwargs = await loop.run_in_executor(None, self.resolve_all, spec["args"], spec["kwargs"])
+                    borrowed = self.w.pending_borrows()
                     m = getattr(self.actor, name)
                     result = m(*args, **kwargs)
                     if inspect.isawaitable(result):
@@ -504,7 +509,7 @@ class Executor:
             if contained_map:
                 for outer, inners in contained_map.items():
                     self.w.send((P.CONTAINED, outer, inners))
-            if self.w.pending_borrows():  # see run_actor_task
+            if borrowed and self.w.pending_borrows():  # see run_actor_task
                 await asyncio.get_running_loop().run_in_executor(None, self.w.flush_refs_sync)
             self._ack(s, lock, spec["seq"])
 
