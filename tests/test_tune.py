@@ -156,7 +156,9 @@ def test_median_stopping_and_hyperband(ray_shared, tmp_path):
     grid = tune.Tuner(_curve, param_space={"q": tune.grid_search(list(range(1, 7)))},
                       tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=hb,
                                                   max_concurrent_trials=3)).fit()
-    assert grid.num_errors == 0 and grid.get_best_result().config["q"] == 6
+    # which bracket a trial lands in, and so how far it runs, depends on the order results arrive in
+    # (trials run concurrently): the winner is one of the two steepest curves
+    assert grid.num_errors == 0 and grid.get_best_result().config["q"] in (5, 6)
 
 
 def test_pbt_exploits(ray_shared, tmp_path):
